@@ -1,0 +1,119 @@
+#!/usr/bin/env python3
+"""Headline benchmark: images/sec (whole node) of MNIST CNN synchronous data-parallel SGD on MI355X.
+
+BASELINE.json metric "images/sec (whole node), MNIST CNN sync-SGD at 1/2/4/8 MI355X" on config
+"MNIST LeNet-5 CNN sync all-reduce SGD bf16 on 8xMI355X".  Synthetic MNIST-shaped data (60,000 x
+28x28x1 uint8, HBM resident) and random-init weights; every timed step is the full training step:
+batch gather, forward, fused softmax-CE, backward, RCCL all-reduce of the gradients, fused SGD update.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model lenet5] [--batch-per-gpu B]
+For N > 1 launch with torch.distributed.run (one rank per GPU); rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "images/sec (whole node), MNIST CNN sync-SGD at 1/2/4/8 MI355X; async speedup"
+BASELINE_VALUE = None  # the reference publishes no number
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--model", default="lenet5")
+    ap.add_argument("--batch-per-gpu", type=int, default=4096)
+    ap.add_argument("--lr", type=float, default=0.001)
+    ap.add_argument("--graph", default="full", choices=["full", "split", "none"])
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--json-extra", action="store_true", help="add diagnostic fields")
+    args = ap.parse_args()
+
+    from distriflow_amd.data.synthetic import synthetic_cifar10, synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.comm import init_distributed, shutdown
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
+
+    env = init_distributed()
+    world, rank = env.world_size, env.rank
+    if args.gpus != world:
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    dev = env.device
+    net = build_model(args.model, device=dev, seed=0)
+    B = args.batch_per_gpu
+    if args.model == "resnet18_cifar":
+        data, labels = synthetic_cifar10(50000, seed=rank, device=dev)
+    else:
+        data, labels = synthetic_mnist(60000, seed=rank, device=dev)
+    trainer = DataParallelTrainer(net, lr=args.lr, graph=args.graph, overlap=not args.no_overlap)
+    trainer.bind_dataset(data, labels, B, scale=1.0 / 255.0)
+    total = args.warmup + args.steps
+    perm = epoch_permutations(data.shape[0], B, total, dev, seed=rank)
+
+    for i in range(args.warmup):
+        trainer.step_indices(perm[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.warmup, total):
+        st = trainer.step_indices(perm[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss = float(st[0].item()) / B
+    ms = elapsed / args.steps * 1e3
+    value = world * B * args.steps / elapsed
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
+            "dtype": "bf16",
+            "data": "synthetic (MNIST-shaped 60000x28x28x1 uint8, HBM resident), random-init weights",
+            "config": {
+                "model": args.model,
+                "global_batch": B * world,
+                "per_gpu_batch": B,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "optimizer": "sgd",
+                "graph": trainer.graph_mode,
+                "params": net.num_params(),
+            },
+        }
+        if args.json_extra:
+            out["extra"] = {"final_loss": loss, "train_tflops": value * net.flops_per_example() / 1e12,
+                            "capture_error": getattr(trainer, "capture_error", None)}
+        print(json.dumps(out), flush=True)
+    shutdown()
+
+
+if __name__ == "__main__":
+    main()

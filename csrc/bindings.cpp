@@ -1,0 +1,351 @@
+// PyTorch bindings for the distriflow_amd gfx950 kernels (module distriflow_amd._C).
+//
+// Every entry point validates shapes/dtypes/devices on the host BEFORE launching (a bad launch
+// on a shared MI355X node can reset all GPUs), then launches on PyTorch's current HIP stream so
+// the calls compose with torch.cuda graph capture and RCCL collectives on the same stream.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <hip/hip_runtime_api.h>
+
+#include "kernels.h"
+#include "native_runtime.h"
+
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_hip(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "distriflow_amd kernel '", what, "' failed: ", hipGetErrorString(e));
+}
+
+void need(const torch::Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+template <typename T>
+const T* cptr(const c10::optional<torch::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<const T*>(t->data_ptr()) : nullptr;
+}
+
+// geometry: [SH, SW, SC, OH, OW, KH, KW, stride, pad]
+void fill_geom(std::vector<int64_t> g, int* dst) {
+  TORCH_CHECK(g.size() == 9, "geometry must have 9 ints");
+  for (int i = 0; i < 9; ++i) dst[i] = (int)g[i];
+}
+
+void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tensor> bias,
+                  c10::optional<torch::Tensor> mask, torch::Tensor out, int64_t M, int64_t N, int64_t K, int64_t Kpad,
+                  int64_t lda, int64_t ldc, std::vector<int64_t> geom, int64_t mode, bool relu, double alpha) {
+  need(src, at::kBFloat16, "src");
+  need(w, at::kBFloat16, "w");
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous(), "out must be a contiguous GPU tensor");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "out must be bf16 or fp32");
+  TORCH_CHECK(Kpad % 32 == 0 && Kpad >= K, "Kpad must be a multiple of 32 and >= K");
+  TORCH_CHECK(w.numel() >= ((N + 15) / 16 * 16) * Kpad, "weight buffer smaller than [Npad16][Kpad]");
+  TORCH_CHECK(out.numel() >= (M - 1) * ldc + N, "out too small for [M][ldc]");
+  TORCH_CHECK(ldc >= N, "ldc < N");
+  dfa::IGemmArgs a{};
+  int g[9];
+  fill_geom(geom, g);
+  a.SH = g[0]; a.SW = g[1]; a.SC = g[2]; a.OH = g[3]; a.OW = g[4]; a.KH = g[5]; a.KW = g[6]; a.stride = g[7];
+  a.pad = g[8];
+  if (mode == 0) {
+    TORCH_CHECK(src.numel() >= (M - 1) * lda + K, "src too small for [M][lda]");
+  } else {
+    TORCH_CHECK(a.OH > 0 && a.OW > 0 && M % (a.OH * a.OW) == 0, "M must be B*OH*OW");
+    const int64_t Bn = M / (a.OH * a.OW);
+    TORCH_CHECK(src.numel() >= Bn * a.SH * a.SW * a.SC, "src too small for the conv geometry");
+    TORCH_CHECK(K == (int64_t)a.KH * a.KW * a.SC, "K must be KH*KW*C");
+    TORCH_CHECK(a.KH < 128 && a.KW < 128 && a.SC < 65536, "conv geometry out of range");
+  }
+  if (bias.has_value() && bias->defined()) {
+    need(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() >= N, "bias too small");
+  }
+  if (mask.has_value() && mask->defined()) {
+    need(*mask, at::kBFloat16, "mask");
+    TORCH_CHECK(mask->numel() >= (M - 1) * ldc + N, "mask too small");
+  }
+  a.src = reinterpret_cast<const dfa::bf16*>(src.data_ptr());
+  a.w = reinterpret_cast<const dfa::bf16*>(w.data_ptr());
+  a.bias = cptr<float>(bias);
+  a.mask = cptr<dfa::bf16>(mask);
+  a.out = out.data_ptr();
+  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.Kpad = (int)Kpad; a.lda = (int)lda; a.ldc = (int)ldc;
+  a.relu = relu ? 1 : 0;
+  a.out_f32 = out.scalar_type() == at::kFloat ? 1 : 0;
+  a.alpha = (float)alpha;
+  check_hip(dfa::igemm_fwd(a, (int)mode, cur_stream()), "igemm_fwd");
+}
+
+void igemm_wgrad_py(torch::Tensor dy, torch::Tensor src, torch::Tensor gw, c10::optional<torch::Tensor> gb,
+                    torch::Tensor workspace, int64_t M, int64_t N, int64_t K, int64_t ldd, int64_t lda,
+                    std::vector<int64_t> geom, int64_t mode, double scale) {
+  need(dy, at::kBFloat16, "dy");
+  need(src, at::kBFloat16, "src");
+  need(gw, at::kFloat, "gw");
+  need(workspace, at::kFloat, "workspace");
+  TORCH_CHECK(gw.numel() >= N * K, "gw too small");
+  TORCH_CHECK(dy.numel() >= (M - 1) * ldd + N, "dy too small");
+  dfa::WgradArgs a{};
+  int g[9];
+  fill_geom(geom, g);
+  a.SH = g[0]; a.SW = g[1]; a.SC = g[2]; a.OH = g[3]; a.OW = g[4]; a.KH = g[5]; a.KW = g[6]; a.stride = g[7];
+  a.pad = g[8];
+  if (mode == 0) {
+    TORCH_CHECK(src.numel() >= (M - 1) * lda + K, "src too small");
+  } else {
+    TORCH_CHECK(M % (a.OH * a.OW) == 0, "M must be B*OH*OW");
+    TORCH_CHECK(src.numel() >= (M / (a.OH * a.OW)) * a.SH * a.SW * a.SC, "src too small");
+    TORCH_CHECK(K == (int64_t)a.KH * a.KW * a.SC, "K must be KH*KW*C");
+  }
+  if (gb.has_value() && gb->defined()) {
+    need(*gb, at::kFloat, "gb");
+    TORCH_CHECK(gb->numel() >= N, "gb too small");
+  }
+  a.dy = reinterpret_cast<const dfa::bf16*>(dy.data_ptr());
+  a.src = reinterpret_cast<const dfa::bf16*>(src.data_ptr());
+  a.gw = gw.data_ptr<float>();
+  a.gb = (gb.has_value() && gb->defined()) ? gb->data_ptr<float>() : nullptr;
+  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.ldd = (int)ldd; a.lda = (int)lda;
+  a.with_bias = a.gb ? 1 : 0;
+  a.scale = (float)scale;
+  check_hip(dfa::igemm_wgrad(a, (int)mode, workspace.data_ptr<float>(), (size_t)workspace.numel(), cur_stream()),
+            "igemm_wgrad");
+}
+
+void maxpool_fwd_py(torch::Tensor x, torch::Tensor y, int64_t B, int64_t H, int64_t W, int64_t C, int64_t P) {
+  need(x, at::kBFloat16, "x");
+  need(y, at::kBFloat16, "y");
+  TORCH_CHECK(P > 0 && H >= P && W >= P, "bad pool geometry");
+  TORCH_CHECK(x.numel() >= B * H * W * C && y.numel() >= B * (H / P) * (W / P) * C, "pool buffers too small");
+  check_hip(dfa::maxpool_fwd((const dfa::bf16*)x.data_ptr(), (dfa::bf16*)y.data_ptr(), B, H, W, C, P, cur_stream()),
+            "maxpool_fwd");
+}
+
+void maxpool_bwd_py(torch::Tensor x, torch::Tensor dy, torch::Tensor dx, int64_t B, int64_t H, int64_t W, int64_t C,
+                    int64_t P, bool relu_fused) {
+  need(x, at::kBFloat16, "x");
+  need(dy, at::kBFloat16, "dy");
+  need(dx, at::kBFloat16, "dx");
+  TORCH_CHECK(P > 0 && H >= P && W >= P, "bad pool geometry");
+  TORCH_CHECK(x.numel() >= B * H * W * C && dx.numel() >= B * H * W * C &&
+                  dy.numel() >= B * (H / P) * (W / P) * C,
+              "pool buffers too small");
+  check_hip(dfa::maxpool_bwd((const dfa::bf16*)x.data_ptr(), (const dfa::bf16*)dy.data_ptr(),
+                             (dfa::bf16*)dx.data_ptr(), B, H, W, C, P, relu_fused ? 1 : 0, cur_stream()),
+            "maxpool_bwd");
+}
+
+void softmax_ce_py(torch::Tensor logits, torch::Tensor labels, c10::optional<torch::Tensor> dlogits,
+                   c10::optional<torch::Tensor> stats, int64_t B, int64_t C, int64_t ldl, int64_t ldg,
+                   double grad_scale) {
+  need(logits, at::kFloat, "logits");
+  need(labels, at::kInt, "labels");
+  TORCH_CHECK(logits.numel() >= (B - 1) * ldl + C && labels.numel() >= B, "softmax_ce inputs too small");
+  dfa::bf16* dl = nullptr;
+  if (dlogits.has_value() && dlogits->defined()) {
+    need(*dlogits, at::kBFloat16, "dlogits");
+    TORCH_CHECK(dlogits->numel() >= (B - 1) * ldg + C, "dlogits too small");
+    dl = (dfa::bf16*)dlogits->data_ptr();
+  }
+  float* sp = nullptr;
+  if (stats.has_value() && stats->defined()) {
+    need(*stats, at::kFloat, "stats");
+    TORCH_CHECK(stats->numel() >= 2, "stats needs 2 floats");
+    sp = stats->data_ptr<float>();
+  }
+  check_hip(dfa::softmax_ce(logits.data_ptr<float>(), labels.data_ptr<int>(), dl, sp, B, C, ldl, ldg,
+                            (float)grad_scale, cur_stream()),
+            "softmax_ce");
+}
+
+void dropout_py(torch::Tensor x, torch::Tensor y, double p, int64_t seed, c10::optional<torch::Tensor> mask,
+                c10::optional<torch::Tensor> step) {
+  const long long* sp = nullptr;
+  if (step.has_value() && step->defined()) {
+    need(*step, at::kLong, "step");
+    sp = reinterpret_cast<const long long*>(step->data_ptr());
+  }
+  need(x, at::kBFloat16, "x");
+  need(y, at::kBFloat16, "y");
+  TORCH_CHECK(y.numel() >= x.numel(), "dropout out too small");
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0,1)");
+  if (mask.has_value() && mask->defined()) {
+    need(*mask, at::kBFloat16, "mask");
+    TORCH_CHECK(mask->numel() >= x.numel(), "dropout mask too small");
+  }
+  check_hip(dfa::dropout((const dfa::bf16*)x.data_ptr(), (dfa::bf16*)y.data_ptr(), cptr<dfa::bf16>(mask), x.numel(),
+                         (float)p, (unsigned long long)seed, sp, cur_stream()),
+            "dropout");
+}
+
+void gather_batch_py(torch::Tensor data, c10::optional<torch::Tensor> labels, torch::Tensor idx, torch::Tensor out,
+                     c10::optional<torch::Tensor> out_labels, int64_t B, int64_t row, double scale) {
+  TORCH_CHECK(data.is_cuda() && data.is_contiguous(), "data must be a contiguous GPU tensor");
+  const bool u8 = data.scalar_type() == at::kByte;
+  TORCH_CHECK(u8 || data.scalar_type() == at::kBFloat16, "data must be uint8 or bf16");
+  need(idx, at::kLong, "idx");
+  need(out, at::kBFloat16, "out");
+  TORCH_CHECK(idx.numel() >= B && out.numel() >= B * row, "gather buffers too small");
+  TORCH_CHECK(data.dim() >= 1 && data.size(0) > 0 && data.numel() / data.size(0) == row, "data row size mismatch");
+  const int* lp = nullptr;
+  int* olp = nullptr;
+  if (labels.has_value() && labels->defined()) {
+    need(*labels, at::kInt, "labels");
+    TORCH_CHECK(out_labels.has_value() && out_labels->defined(), "out_labels required with labels");
+    need(*out_labels, at::kInt, "out_labels");
+    lp = labels->data_ptr<int>();
+    olp = out_labels->data_ptr<int>();
+  }
+  check_hip(dfa::gather_batch(data.data_ptr(), u8 ? 1 : 0, lp, reinterpret_cast<const long long*>(idx.data_ptr<int64_t>()), (dfa::bf16*)out.data_ptr(),
+                              olp, B, row, (float)scale, (long long)data.size(0), cur_stream()),
+            "gather_batch");
+}
+
+void add_act_py(torch::Tensor a, torch::Tensor b, torch::Tensor out, bool relu) {
+  need(a, at::kBFloat16, "a");
+  need(b, at::kBFloat16, "b");
+  need(out, at::kBFloat16, "out");
+  TORCH_CHECK(a.numel() == b.numel() && out.numel() >= a.numel(), "add_act size mismatch");
+  check_hip(dfa::add_act((const dfa::bf16*)a.data_ptr(), (const dfa::bf16*)b.data_ptr(), (dfa::bf16*)out.data_ptr(),
+                         a.numel(), relu ? 1 : 0, cur_stream()),
+            "add_act");
+}
+
+void relu_bwd_py(torch::Tensor y, torch::Tensor dy, torch::Tensor dx) {
+  need(y, at::kBFloat16, "y");
+  need(dy, at::kBFloat16, "dy");
+  need(dx, at::kBFloat16, "dx");
+  TORCH_CHECK(y.numel() == dy.numel() && dx.numel() >= y.numel(), "relu_bwd size mismatch");
+  check_hip(dfa::relu_bwd((const dfa::bf16*)y.data_ptr(), (const dfa::bf16*)dy.data_ptr(), (dfa::bf16*)dx.data_ptr(),
+                          y.numel(), cur_stream()),
+            "relu_bwd");
+}
+
+void gap_fwd_py(torch::Tensor x, torch::Tensor y, int64_t B, int64_t HW, int64_t C) {
+  need(x, at::kBFloat16, "x");
+  need(y, at::kBFloat16, "y");
+  TORCH_CHECK(x.numel() >= B * HW * C && y.numel() >= B * C, "gap buffers too small");
+  check_hip(dfa::gap_fwd((const dfa::bf16*)x.data_ptr(), (dfa::bf16*)y.data_ptr(), B, HW, C, cur_stream()), "gap_fwd");
+}
+
+void gap_bwd_py(torch::Tensor dy, torch::Tensor dx, int64_t B, int64_t HW, int64_t C) {
+  need(dy, at::kBFloat16, "dy");
+  need(dx, at::kBFloat16, "dx");
+  TORCH_CHECK(dx.numel() >= B * HW * C && dy.numel() >= B * C, "gap buffers too small");
+  check_hip(dfa::gap_bwd((const dfa::bf16*)dy.data_ptr(), (dfa::bf16*)dx.data_ptr(), B, HW, C, cur_stream()),
+            "gap_bwd");
+}
+
+// descs: int64 GPU tensor [ndesc][6] laid out as ParamDesc (see optim.hip)
+void sgd_multi_py(torch::Tensor descs, int64_t ndesc, int64_t total_blocks, torch::Tensor master, torch::Tensor grad,
+                  c10::optional<torch::Tensor> mom, torch::Tensor wbf, torch::Tensor hyper, bool apply_update) {
+  TORCH_CHECK(descs.is_cuda() && descs.scalar_type() == at::kLong && descs.is_contiguous(), "descs must be int64 GPU");
+  static_assert(sizeof(dfa::ParamDesc) == 48, "ParamDesc layout");
+  TORCH_CHECK(descs.numel() * 8 >= ndesc * (int64_t)sizeof(dfa::ParamDesc), "descs too small");
+  need(master, at::kFloat, "master");
+  need(grad, at::kFloat, "grad");
+  need(wbf, at::kBFloat16, "wbf");
+  need(hyper, at::kFloat, "hyper");
+  TORCH_CHECK(hyper.numel() >= 5, "hyper needs [lr, momentum, wd, grad_scale, nesterov]");
+  TORCH_CHECK(grad.numel() >= master.numel(), "grad smaller than master");
+  float* mp = nullptr;
+  if (mom.has_value() && mom->defined()) {
+    need(*mom, at::kFloat, "mom");
+    TORCH_CHECK(mom->numel() >= master.numel(), "momentum buffer too small");
+    mp = mom->data_ptr<float>();
+  }
+  check_hip(dfa::sgd_multi(reinterpret_cast<const dfa::ParamDesc*>(descs.data_ptr()), (int)ndesc, (int)total_blocks,
+                           master.data_ptr<float>(), grad.data_ptr<float>(), mp, (dfa::bf16*)wbf.data_ptr(),
+                           hyper.data_ptr<float>(), apply_update ? 1 : 0, cur_stream()),
+            "sgd_multi");
+}
+
+void sum_buffers_py(torch::Tensor ptrs, int64_t nin, torch::Tensor out, double scale) {
+  TORCH_CHECK(ptrs.is_cuda() && ptrs.scalar_type() == at::kLong && ptrs.numel() >= nin, "ptrs must be int64 GPU");
+  need(out, at::kFloat, "out");
+  check_hip(dfa::sum_buffers(reinterpret_cast<const float* const*>(ptrs.data_ptr()), (int)nin, out.data_ptr<float>(),
+                             out.numel(), (float)scale, cur_stream()),
+            "sum_buffers");
+}
+
+void axpby_py(torch::Tensor out, torch::Tensor a, torch::Tensor b, double alpha, double beta) {
+  need(out, at::kFloat, "out");
+  need(a, at::kFloat, "a");
+  need(b, at::kFloat, "b");
+  TORCH_CHECK(a.numel() == out.numel() && b.numel() == out.numel(), "axpby size mismatch");
+  check_hip(dfa::axpby(out.data_ptr<float>(), a.data_ptr<float>(), b.data_ptr<float>(), (float)alpha, (float)beta,
+                       out.numel(), cur_stream()),
+            "axpby");
+}
+
+void bn_fwd_train_py(torch::Tensor x, torch::Tensor y, torch::Tensor gamma, torch::Tensor beta, torch::Tensor mean,
+                     torch::Tensor invstd, torch::Tensor run_mean, torch::Tensor run_var, torch::Tensor ws, int64_t M,
+                     int64_t C, double momentum, double eps, bool relu) {
+  need(x, at::kBFloat16, "x");
+  need(y, at::kBFloat16, "y");
+  for (auto* t : {&gamma, &beta, &mean, &invstd, &run_mean, &run_var, &ws}) need(*t, at::kFloat, "bn param");
+  TORCH_CHECK(x.numel() >= M * C && y.numel() >= M * C && gamma.numel() >= C, "bn sizes");
+  TORCH_CHECK(ws.numel() >= 2 * C * 256, "bn workspace too small");
+  check_hip(dfa::bn_fwd_train((const dfa::bf16*)x.data_ptr(), (dfa::bf16*)y.data_ptr(), gamma.data_ptr<float>(),
+                              beta.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                              run_mean.data_ptr<float>(), run_var.data_ptr<float>(), ws.data_ptr<float>(), M, C,
+                              (float)momentum, (float)eps, relu ? 1 : 0, cur_stream()),
+            "bn_fwd_train");
+}
+
+void bn_fwd_eval_py(torch::Tensor x, torch::Tensor y, torch::Tensor gamma, torch::Tensor beta, torch::Tensor run_mean,
+                    torch::Tensor run_var, int64_t M, int64_t C, double eps, bool relu) {
+  need(x, at::kBFloat16, "x");
+  need(y, at::kBFloat16, "y");
+  TORCH_CHECK(x.numel() >= M * C && y.numel() >= M * C, "bn sizes");
+  check_hip(dfa::bn_fwd_eval((const dfa::bf16*)x.data_ptr(), (dfa::bf16*)y.data_ptr(), gamma.data_ptr<float>(),
+                             beta.data_ptr<float>(), run_mean.data_ptr<float>(), run_var.data_ptr<float>(), M, C,
+                             (float)eps, relu ? 1 : 0, cur_stream()),
+            "bn_fwd_eval");
+}
+
+void bn_bwd_py(torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor dx, torch::Tensor gamma,
+               torch::Tensor beta, torch::Tensor mean, torch::Tensor invstd, torch::Tensor dgamma, torch::Tensor dbeta,
+               torch::Tensor ws, int64_t M, int64_t C, bool relu, double gscale) {
+  need(x, at::kBFloat16, "x");
+  need(y, at::kBFloat16, "y");
+  need(dy, at::kBFloat16, "dy");
+  need(dx, at::kBFloat16, "dx");
+  TORCH_CHECK(ws.numel() >= 2 * C * 256, "bn workspace too small");
+  check_hip(dfa::bn_bwd((const dfa::bf16*)x.data_ptr(), (const dfa::bf16*)y.data_ptr(), (const dfa::bf16*)dy.data_ptr(),
+                        (dfa::bf16*)dx.data_ptr(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                        mean.data_ptr<float>(), invstd.data_ptr<float>(), dgamma.data_ptr<float>(),
+                        dbeta.data_ptr<float>(), ws.data_ptr<float>(), M, C, relu ? 1 : 0, (float)gscale,
+                        cur_stream()),
+            "bn_bwd");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "distriflow_amd native kernels (gfx950 / MI355X) and runtime";
+  m.def("igemm_fwd", &igemm_fwd_py, "implicit-GEMM MFMA (dense/conv fwd, dgrad)");
+  m.def("igemm_wgrad", &igemm_wgrad_py, "implicit-GEMM MFMA weight gradient (split-m slabs + reduce)");
+  m.def("maxpool_fwd", &maxpool_fwd_py);
+  m.def("maxpool_bwd", &maxpool_bwd_py);
+  m.def("softmax_ce", &softmax_ce_py);
+  m.def("dropout", &dropout_py);
+  m.def("gather_batch", &gather_batch_py);
+  m.def("add_act", &add_act_py);
+  m.def("relu_bwd", &relu_bwd_py);
+  m.def("gap_fwd", &gap_fwd_py);
+  m.def("gap_bwd", &gap_bwd_py);
+  m.def("sgd_multi", &sgd_multi_py);
+  m.def("sum_buffers", &sum_buffers_py);
+  m.def("axpby", &axpby_py);
+  m.def("bn_fwd_train", &bn_fwd_train_py);
+  m.def("bn_fwd_eval", &bn_fwd_eval_py);
+  m.def("bn_bwd", &bn_bwd_py);
+  dfa::register_runtime(m);
+}

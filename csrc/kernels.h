@@ -1,0 +1,76 @@
+// Launch-argument structs and host launcher declarations shared by the HIP kernel translation
+// units and the PyTorch bindings.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+namespace dfa {
+typedef __bf16 bf16;
+}
+
+namespace dfa {
+
+enum { MODE_DIRECT = 0, MODE_FWD = 1, MODE_DGRAD = 2 };
+
+struct IGemmArgs {
+  const bf16* src;   // A source: [M][lda] (direct) or NHWC [B][SH][SW][SC] (conv gathers)
+  const bf16* w;     // [Npad16][Kpad32] bf16, zero padded
+  const float* bias; // [N] or nullptr
+  const bf16* mask;  // [M][ldc] producer activation for relu' (nullptr = none)
+  void* out;         // [M][ldc] bf16 or fp32
+  int M, N, K, Kpad, lda, ldc;
+  int SH, SW, SC, OH, OW, KH, KW, stride, pad;
+  int relu, out_f32;
+  float alpha;
+};
+
+struct WgradArgs {
+  const bf16* dy;     // [M][ldd]
+  const bf16* src;    // activation (gather source, same conventions as IGemmArgs)
+  float* partial;     // [splits][N][K+1] (splits > 1)
+  float* gw;          // [N][K] final (splits == 1)
+  float* gb;          // [N] final bias grad or nullptr
+  int M, N, K, ldd, lda;
+  int SH, SW, SC, OH, OW, KH, KW, stride, pad;
+  int m_per_split, splits, with_bias;
+  float scale;
+};
+
+struct ParamDesc {
+  long long off;      // offset into the fp32 master / grad / momentum flat buffers
+  long long bf_off;   // offset of the bf16 [Npad][Kpad] copy (-1: vector param, no copy)
+  long long bft_off;  // offset of the bf16 transposed dgrad copy (-1: none)
+  int numel;
+  int N, T, Ci;       // matrix view: [N][T*Ci]
+  int block_start;    // first workgroup of this tensor
+  int pad_;
+};
+
+hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st);
+hipError_t igemm_wgrad(const WgradArgs& a, int mode, float* workspace, size_t ws_floats, hipStream_t st);
+hipError_t maxpool_fwd(const bf16* x, bf16* y, int B, int H, int W, int C, int P, hipStream_t st);
+hipError_t maxpool_bwd(const bf16* x, const bf16* dy, bf16* dx, int B, int H, int W, int C, int P, int relu_fused,
+                       hipStream_t st);
+hipError_t softmax_ce(const float* logits, const int* labels, bf16* dlogits, float* stats, int B, int C, int ldl,
+                      int ldg, float grad_scale, hipStream_t st);
+hipError_t dropout(const bf16* x, bf16* y, const bf16* mask, long long n, float p, unsigned long long seed,
+                   const long long* step, hipStream_t st);
+hipError_t gather_batch(const void* data, int data_is_u8, const int* labels, const long long* idx, bf16* out,
+                        int* out_labels, int B, int row, float scale, long long nrows, hipStream_t st);
+hipError_t add_act(const bf16* a, const bf16* b, bf16* out, long long n, int relu, hipStream_t st);
+hipError_t relu_bwd(const bf16* y, const bf16* dy, bf16* dx, long long n, hipStream_t st);
+hipError_t gap_fwd(const bf16* x, bf16* y, int B, int HW, int C, hipStream_t st);
+hipError_t gap_bwd(const bf16* dy, bf16* dx, int B, int HW, int C, hipStream_t st);
+hipError_t sgd_multi(const ParamDesc* descs, int ndesc, int total_blocks, float* master, const float* grad,
+                     float* mom_buf, bf16* wbf, const float* hyper, int apply_update, hipStream_t st);
+hipError_t sum_buffers(const float* const* ins, int nin, float* out, long long n, float scale, hipStream_t st);
+hipError_t axpby(float* out, const float* a, const float* b, float alpha, float beta, long long n, hipStream_t st);
+hipError_t bn_fwd_train(const bf16* x, bf16* y, const float* gamma, const float* beta, float* mean, float* invstd,
+                        float* run_mean, float* run_var, float* ws, int M, int C, float momentum, float eps, int relu,
+                        hipStream_t st);
+hipError_t bn_fwd_eval(const bf16* x, bf16* y, const float* gamma, const float* beta, const float* run_mean,
+                       const float* run_var, int M, int C, float eps, int relu, hipStream_t st);
+hipError_t bn_bwd(const bf16* x, const bf16* y, const bf16* dy, bf16* dx, const float* gamma, const float* beta,
+                  const float* mean, const float* invstd, float* dgamma, float* dbeta, float* ws, int M, int C,
+                  int relu, float gscale, hipStream_t st);
+
+}  // namespace dfa

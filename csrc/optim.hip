@@ -1,0 +1,128 @@
+// Fused multi-tensor SGD (gfx950): one launch updates every parameter of the model.
+//
+// Replaces DistributedTfModel.update (w <- w - lr * g per weight, one tf.js op chain per tensor,
+// /root/reference/src/common/models.ts:128-135) and the server-side mean aggregation
+// (/root/reference/src/server/federated_server.ts:98-106):
+//   * the 1/world (or 1/K) gradient-mean scale is folded in (grad_scale), so the all-reduce is a
+//     plain SUM and no separate "mean" pass exists,
+//   * optional momentum / weight decay (not in the reference; used by the ResNet config),
+//   * the same pass re-emits the bf16 compute copies of each weight matrix in the two layouts the
+//     MFMA kernels read: [N][K] (fwd, K = KH*KW*Cin) and the dgrad layout [Cin][KH*KW*N], both
+//     zero padded to 16 x 32 tiles.  Hyper-parameters live in device memory so a captured hipGraph
+//     sees learning-rate changes without re-capture.
+#include "common.h"
+#include "kernels.h"
+
+namespace dfa {
+
+constexpr int SGD_ELEMS_PER_BLOCK = 1024;
+
+__device__ __forceinline__ int find_desc(const ParamDesc* d, int n, int bid) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].block_start <= bid) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// hyper = [lr, momentum, weight_decay, grad_scale, nesterov]
+__global__ void __launch_bounds__(256) sgd_multi_kernel(const ParamDesc* __restrict__ descs, int ndesc,
+                                                        float* __restrict__ master, const float* __restrict__ grad,
+                                                        float* __restrict__ mom_buf, bf16* __restrict__ wbf,
+                                                        const float* __restrict__ hyper, int apply_update) {
+  const int di = find_desc(descs, ndesc, blockIdx.x);
+  const ParamDesc d = descs[di];
+  const int base = (blockIdx.x - d.block_start) * SGD_ELEMS_PER_BLOCK;
+  float lr = 0.f, mom = 0.f, wd = 0.f, gs = 1.f;
+  bool nesterov = false;
+  if (apply_update) {
+    lr = hyper[0]; mom = hyper[1]; wd = hyper[2]; gs = hyper[3]; nesterov = hyper[4] != 0.f;
+  }
+  const int K = d.T * d.Ci;
+  const int Kpad = round_up(K, 32);
+  const int KpadT = round_up(d.T * d.N, 32);
+#pragma unroll
+  for (int r = 0; r < SGD_ELEMS_PER_BLOCK / 256; ++r) {
+    const int i = base + r * 256 + threadIdx.x;
+    if (i >= d.numel) break;
+    float w = master[d.off + i];
+    if (apply_update) {
+      float g = grad[d.off + i] * gs;
+      if (wd != 0.f) g += wd * w;
+      if (mom != 0.f) {
+        float v = mom * mom_buf[d.off + i] + g;
+        mom_buf[d.off + i] = v;
+        g = nesterov ? g + mom * v : v;
+      }
+      w -= lr * g;
+      master[d.off + i] = w;
+    }
+    if (d.bf_off >= 0) {
+      const int n = i / K;
+      const int kk = i - n * K;
+      const bf16 wb = f2bf(w);
+      wbf[d.bf_off + (long long)n * Kpad + kk] = wb;
+      if (d.bft_off >= 0) {
+        const int t = kk / d.Ci;
+        const int ci = kk - t * d.Ci;
+        wbf[d.bft_off + (long long)ci * KpadT + t * d.N + n] = wb;
+      }
+    }
+  }
+}
+
+hipError_t sgd_multi(const ParamDesc* descs, int ndesc, int total_blocks, float* master, const float* grad,
+                     float* mom_buf, bf16* wbf, const float* hyper, int apply_update, hipStream_t st) {
+  if (ndesc <= 0 || total_blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sgd_multi_kernel, dim3(total_blocks), dim3(256), 0, st, descs, ndesc, master, grad, mom_buf, wbf,
+                     hyper, apply_update);
+  return hipGetLastError();
+}
+
+// out = scale * sum_j in_j   (server-side aggregation of K uploaded gradient buffers)
+__global__ void sum_buffers_kernel(const float* const* __restrict__ ins, int nin, float* __restrict__ out,
+                                   long long n, float scale) {
+  const long long n4 = n / 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < nin; ++j) {
+      const float4 v = reinterpret_cast<const float4*>(ins[j])[i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    s.x *= scale; s.y *= scale; s.z *= scale; s.w *= scale;
+    reinterpret_cast<float4*>(out)[i] = s;
+  }
+  for (long long i = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < nin; ++j) s += ins[j][i];
+    out[i] = s * scale;
+  }
+}
+
+hipError_t sum_buffers(const float* const* ins, int nin, float* out, long long n, float scale, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  long long g = (n / 4 + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(sum_buffers_kernel, dim3((int)g), dim3(256), 0, st, ins, nin, out, n, scale);
+  return hipGetLastError();
+}
+
+// out = a + alpha * (b - a)  — FedAvg-style weight interpolation / delta application on flat buffers
+__global__ void axpby_kernel(float* __restrict__ out, const float* __restrict__ a, const float* __restrict__ b,
+                             float alpha, float beta, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = alpha * a[i] + beta * b[i];
+}
+
+hipError_t axpby(float* out, const float* a, const float* b, float alpha, float beta, long long n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  long long g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(axpby_kernel, dim3((int)g), dim3(256), 0, st, out, a, b, alpha, beta, n);
+  return hipGetLastError();
+}
+
+}  // namespace dfa

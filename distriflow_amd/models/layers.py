@@ -1,0 +1,477 @@
+"""Layers of the distriflow_amd training engine (explicit forward/backward, no autograd tape).
+
+The layer set is what the reference's models use — Keras/tf.js ``Conv2D``, ``Dense``,
+``Activation``, ``MaxPooling2D``, ``Dropout``, ``Flatten`` (/root/reference/experiment/mnist/model.json:1,
+/root/reference/experiment/mnist/mnist_server.ts:16-22) — plus BatchNorm / residual / global-average
+pooling for the CIFAR-10 ResNet-18 config of BASELINE.json.
+
+Execution model (MI355X-first):
+  * every buffer (activations, gradients, workspaces) is allocated once per batch size by
+    :meth:`Layer.alloc`, so the full step can be replayed as one hipGraph;
+  * ReLU never runs as its own pass: forward ReLU is fused into the producing GEMM / BN / add
+    epilogue, and relu' is fused into the CONSUMER's backward (dgrad epilogue mask, pool backward,
+    dropout backward), driven by ``in_relu`` = "my input is a ReLU output";
+  * the first layer skips its data gradient.
+"""
+from __future__ import annotations
+
+import math
+import zlib
+from typing import Optional
+
+import torch
+
+from .. import ops
+from .params import ParamSpec
+
+
+class Layer:
+    has_params = False
+
+    def __init__(self, name: Optional[str] = None):
+        self.name = name or type(self).__name__.lower()
+        self.in_shape: tuple = ()
+        self.out_shape: tuple = ()
+        self.relu = False          # output passed through a fused ReLU
+        self.in_relu = False       # input is a ReLU output (apply relu' in backward)
+        self.need_dx = True
+        self.store = None
+        self.x: Optional[torch.Tensor] = None
+        self.out: Optional[torch.Tensor] = None
+        self.dx: Optional[torch.Tensor] = None
+
+    # shapes exclude the batch dimension
+    def build(self, in_shape: tuple) -> tuple:
+        self.in_shape = tuple(in_shape)
+        self.out_shape = self.in_shape
+        return self.out_shape
+
+    def specs(self) -> list[ParamSpec]:
+        return []
+
+    def can_fuse_relu(self) -> bool:
+        return False
+
+    def alloc(self, B: int, device, dtype, ws):
+        self.out = torch.empty((B,) + self.out_shape, device=device, dtype=dtype)
+        if self.need_dx:
+            self.dx = torch.empty((B,) + self.in_shape, device=device, dtype=dtype)
+
+    def forward(self, x, training: bool):
+        raise NotImplementedError
+
+    def backward(self, dy):
+        raise NotImplementedError
+
+    def config(self) -> dict:
+        return {}
+
+
+class Dense(Layer):
+    """y = act(x W^T + b); W stored [units][in] (Keras kernel [in][units] is transposed at I/O)."""
+    has_params = True
+
+    def __init__(self, units: int, activation: str = "linear", use_bias: bool = True, name=None,
+                 kernel_initializer="glorot_uniform"):
+        super().__init__(name or "dense")
+        self.units = int(units)
+        self.activation = activation
+        self.use_bias = use_bias
+        self.kernel_initializer = kernel_initializer
+        self.out_f32 = False  # final logits layer writes fp32
+        if activation == "relu":
+            self.relu = True
+        elif activation not in ("linear", None, "softmax"):
+            raise NotImplementedError(f"Dense activation {activation!r}")
+
+    def build(self, in_shape):
+        self.in_shape = tuple(in_shape)
+        self.in_features = int(math.prod(in_shape))
+        self.out_shape = (self.units,)
+        return self.out_shape
+
+    def can_fuse_relu(self):
+        return True
+
+    def specs(self):
+        K, N = self.in_features, self.units
+        s = [ParamSpec(f"{self.name}/kernel", (N, K), "matrix", (N, 1, K), self.kernel_initializer, (K, N),
+                       needs_dgrad=self.need_dx)]
+        if self.use_bias:
+            s.append(ParamSpec(f"{self.name}/bias", (N,), "vector", init="zeros"))
+        return s
+
+    def alloc(self, B, device, dtype, ws):
+        odt = torch.float32 if self.out_f32 else dtype
+        self.out = torch.empty((B, self.units), device=device, dtype=odt)
+        if self.need_dx:
+            self.dx = torch.empty((B,) + self.in_shape, device=device, dtype=dtype)
+        self.ws = ws
+
+    def forward(self, x, training):
+        self.x = x
+        xf = x.reshape(x.shape[0], self.in_features)
+        st = self.store
+        b = st[f"{self.name}/bias"] if self.use_bias else None
+        ops.dense_fwd(xf, st.weight(f"{self.name}/kernel"), b, self.out, relu=self.relu)
+        return self.out
+
+    def backward(self, dy):
+        st = self.store
+        xf = self.x.reshape(self.x.shape[0], self.in_features)
+        kn = f"{self.name}/kernel"
+        gb = st.gradient(f"{self.name}/bias") if self.use_bias else None
+        ops.dense_wgrad(dy, xf, st.grad_matrix(kn), gb, self.ws.wgrad)
+        if not self.need_dx:
+            return None
+        dxf = self.dx.view(self.dx.shape[0], self.in_features)
+        mask = self.x.reshape(dxf.shape) if self.in_relu else None
+        ops.dense_dgrad(dy, st.weight(kn), st.weight_t(kn), dxf, mask=mask)
+        return self.dx
+
+    def config(self):
+        return {"units": self.units, "activation": self.activation, "use_bias": self.use_bias}
+
+
+class Conv2D(Layer):
+    """NHWC conv, kernel stored OHWI [Cout][KH*KW*Cin] (Keras HWIO converted at I/O)."""
+    has_params = True
+
+    def __init__(self, filters: int, kernel_size=(3, 3), strides=(1, 1), padding="valid", activation="linear",
+                 use_bias=True, name=None, kernel_initializer="glorot_uniform"):
+        super().__init__(name or "conv2d")
+        self.filters = int(filters)
+        ks = (kernel_size, kernel_size) if isinstance(kernel_size, int) else tuple(kernel_size)
+        st = (strides, strides) if isinstance(strides, int) else tuple(strides)
+        if ks[0] != ks[1] or st[0] != st[1]:
+            raise NotImplementedError("only square kernels / strides")
+        self.k = int(ks[0])
+        self.stride = int(st[0])
+        self.padding = padding
+        self.activation = activation
+        self.use_bias = use_bias
+        self.kernel_initializer = kernel_initializer
+        if activation == "relu":
+            self.relu = True
+        elif activation not in ("linear", None):
+            raise NotImplementedError(f"Conv2D activation {activation!r}")
+
+    def build(self, in_shape):
+        H, W, C = in_shape
+        self.in_shape = (H, W, C)
+        if self.padding == "same":
+            OH = (H + self.stride - 1) // self.stride
+            OW = (W + self.stride - 1) // self.stride
+            total = max((OH - 1) * self.stride + self.k - H, 0)
+            if total % 2:
+                raise NotImplementedError("asymmetric 'same' padding")
+            self.pad = total // 2
+        elif self.padding == "valid":
+            self.pad = 0
+        else:
+            self.pad = int(self.padding)
+        OH, OW = ops.conv_out_hw(H, W, self.k, self.k, self.stride, self.pad)
+        self.out_shape = (OH, OW, self.filters)
+        return self.out_shape
+
+    def can_fuse_relu(self):
+        return True
+
+    def specs(self):
+        H, W, C = self.in_shape
+        K = self.k * self.k * C
+        fan_in, fan_out = K, self.k * self.k * self.filters
+        s = [ParamSpec(f"{self.name}/kernel", (self.filters, self.k, self.k, C), "matrix",
+                       (self.filters, self.k * self.k, C), self.kernel_initializer, (fan_in, fan_out),
+                       needs_dgrad=self.need_dx)]
+        if self.use_bias:
+            s.append(ParamSpec(f"{self.name}/bias", (self.filters,), "vector", init="zeros"))
+        return s
+
+    def alloc(self, B, device, dtype, ws):
+        super().alloc(B, device, dtype, ws)
+        self.ws = ws
+
+    def forward(self, x, training):
+        self.x = x
+        st = self.store
+        b = st[f"{self.name}/bias"] if self.use_bias else None
+        ops.conv_fwd(x, st.weight(f"{self.name}/kernel"), b, self.out, self.k, self.k, self.stride, self.pad,
+                     relu=self.relu)
+        return self.out
+
+    def backward(self, dy):
+        st = self.store
+        kn = f"{self.name}/kernel"
+        gb = st.gradient(f"{self.name}/bias") if self.use_bias else None
+        ops.conv_wgrad(dy, self.x, st.grad_matrix(kn), gb, self.ws.wgrad, self.k, self.k, self.stride, self.pad)
+        if not self.need_dx:
+            return None
+        ops.conv_dgrad(dy, st.weight(kn), st.weight_t(kn), self.dx, self.k, self.k, self.stride, self.pad,
+                       mask=self.x if self.in_relu else None)
+        return self.dx
+
+    def config(self):
+        return {"filters": self.filters, "kernel_size": [self.k, self.k], "strides": [self.stride, self.stride],
+                "padding": self.padding if isinstance(self.padding, str) else "valid",
+                "activation": self.activation, "use_bias": self.use_bias}
+
+
+class MaxPooling2D(Layer):
+    def __init__(self, pool_size=2, strides=None, name=None):
+        super().__init__(name or "max_pooling2d")
+        p = pool_size[0] if isinstance(pool_size, (list, tuple)) else pool_size
+        s = strides[0] if isinstance(strides, (list, tuple)) else (strides or p)
+        if p != s:
+            raise NotImplementedError("MaxPooling2D requires pool_size == strides")
+        self.p = int(p)
+
+    def build(self, in_shape):
+        H, W, C = in_shape
+        self.in_shape = (H, W, C)
+        self.out_shape = (H // self.p, W // self.p, C)
+        return self.out_shape
+
+    def forward(self, x, training):
+        self.x = x
+        ops.maxpool_fwd(x, self.out, self.p)
+        return self.out
+
+    def backward(self, dy):
+        if not self.need_dx:
+            return None
+        ops.maxpool_bwd(self.x, dy, self.dx, self.p, relu_fused=self.in_relu)
+        return self.dx
+
+    def config(self):
+        return {"pool_size": [self.p, self.p], "strides": [self.p, self.p], "padding": "valid"}
+
+
+class Dropout(Layer):
+    """Inverted dropout with a counter-based mask (seed, step, element) regenerated in backward."""
+
+    def __init__(self, rate: float, name=None, seed: int = 1234):
+        super().__init__(name or "dropout")
+        self.rate = float(rate)
+        self.base_seed = seed
+        self.step = 0
+        self.active = False
+
+    def _seed(self):
+        return (self.base_seed * 1000003 + zlib.crc32(self.name.encode()) % 100003) & 0x7FFFFFFFFFFF
+
+    def forward(self, x, training):
+        self.x = x
+        self.active = training and self.rate > 0
+        if not self.active:
+            return x
+        # the per-step part of the seed is read from device memory (self.step_dev, advanced by the
+        # engine inside the captured step), so graph replays draw fresh masks
+        ops.dropout(x, self.out, self.rate, self._seed(), step=self.step_dev)
+        return self.out
+
+    def backward(self, dy):
+        if not self.need_dx:
+            return None
+        if not self.active:
+            if self.in_relu:
+                return ops.relu_bwd(self.x, dy, self.dx)
+            return dy
+        ops.dropout(dy, self.dx, self.rate, self._seed(), mask=self.x if self.in_relu else None, step=self.step_dev)
+        return self.dx
+
+    def config(self):
+        return {"rate": self.rate}
+
+
+class Flatten(Layer):
+    """View only: consumers reshape their input; never executed."""
+
+    def build(self, in_shape):
+        self.in_shape = tuple(in_shape)
+        self.out_shape = (int(math.prod(in_shape)),)
+        return self.out_shape
+
+
+class Activation(Layer):
+    """Standalone activation; the engine fuses relu into the producer, softmax into the loss."""
+
+    def __init__(self, activation: str, name=None):
+        super().__init__(name or "activation")
+        self.activation = activation
+
+    def config(self):
+        return {"activation": self.activation}
+
+
+class BatchNorm(Layer):
+    """BatchNorm over channels (NHWC / [B][F]) with fused ReLU; gamma/beta trainable, running stats buffers."""
+    has_params = True
+
+    def __init__(self, momentum=0.1, eps=1e-5, relu=False, name=None):
+        super().__init__(name or "batch_normalization")
+        self.momentum = momentum
+        self.eps = eps
+        self.relu = relu
+
+    def build(self, in_shape):
+        self.in_shape = self.out_shape = tuple(in_shape)
+        self.C = in_shape[-1]
+        return self.out_shape
+
+    def specs(self):
+        return [ParamSpec(f"{self.name}/gamma", (self.C,), "vector", init="ones"),
+                ParamSpec(f"{self.name}/beta", (self.C,), "vector", init="zeros")]
+
+    def alloc(self, B, device, dtype, ws):
+        super().alloc(B, device, dtype, ws)
+        self.ws = ws
+        if not hasattr(self, "run_mean") or self.run_mean.device != torch.device(device):
+            self.run_mean = torch.zeros(self.C, device=device)
+            self.run_var = torch.ones(self.C, device=device)
+        self.mean = torch.zeros(self.C, device=device)
+        self.invstd = torch.ones(self.C, device=device)
+
+    def forward(self, x, training):
+        self.x = x
+        st = self.store
+        x2 = x.reshape(-1, self.C)
+        y2 = self.out.view(-1, self.C)
+        g, b = st[f"{self.name}/gamma"], st[f"{self.name}/beta"]
+        if training:
+            ops.bn_fwd_train(x2, y2, g, b, self.mean, self.invstd, self.run_mean, self.run_var, self.ws.bn,
+                             self.momentum, self.eps, self.relu)
+        else:
+            ops.bn_fwd_eval(x2, y2, g, b, self.run_mean, self.run_var, self.eps, self.relu)
+        return self.out
+
+    def backward(self, dy):
+        st = self.store
+        x2 = self.x.reshape(-1, self.C)
+        ops.bn_bwd(x2, self.out.view(-1, self.C), dy.reshape(-1, self.C), self.dx.view(-1, self.C),
+                   st[f"{self.name}/gamma"], st[f"{self.name}/beta"], self.mean, self.invstd,
+                   st.gradient(f"{self.name}/gamma"), st.gradient(f"{self.name}/beta"), self.ws.bn, self.relu)
+        if self.in_relu:
+            raise NotImplementedError("BatchNorm after a fused ReLU")
+        return self.dx
+
+
+class GlobalAveragePooling2D(Layer):
+    def build(self, in_shape):
+        H, W, C = in_shape
+        self.in_shape = (H, W, C)
+        self.out_shape = (C,)
+        return self.out_shape
+
+    def forward(self, x, training):
+        self.x = x
+        ops.gap_fwd(x, self.out)
+        return self.out
+
+    def backward(self, dy):
+        if not self.need_dx:
+            return None
+        ops.gap_bwd(dy, self.dx)
+        if self.in_relu:
+            ops.relu_bwd(self.x, self.dx, self.dx)
+        return self.dx
+
+
+class ResidualBlock(Layer):
+    """ResNet basic block: relu(bn2(conv2(relu(bn1(conv1(x))))) + shortcut(x)).
+
+    shortcut = identity, or conv1x1(stride) + BN when the shape changes.  Sub-layers are engine
+    layers, so every conv/BN runs on the same MFMA / BN kernels; the final add + ReLU is one fused
+    kernel (``add_act``) and its relu' is applied once to the incoming gradient.
+    """
+    has_params = True
+
+    def __init__(self, filters: int, stride: int = 1, name=None):
+        super().__init__(name or "block")
+        self.filters = filters
+        self.stride = stride
+        self.relu = True
+
+    def build(self, in_shape):
+        H, W, C = in_shape
+        self.in_shape = (H, W, C)
+        n = self.name
+        self.conv1 = Conv2D(self.filters, 3, self.stride, 1, use_bias=False, name=f"{n}/conv1",
+                            kernel_initializer="he_normal")
+        self.bn1 = BatchNorm(relu=True, name=f"{n}/bn1")
+        self.conv2 = Conv2D(self.filters, 3, 1, 1, use_bias=False, name=f"{n}/conv2", kernel_initializer="he_normal")
+        self.bn2 = BatchNorm(relu=False, name=f"{n}/bn2")
+        s = self.conv1.build(self.in_shape)
+        s = self.bn1.build(s)
+        s = self.conv2.build(s)
+        s = self.bn2.build(s)
+        self.proj = None
+        if self.stride != 1 or C != self.filters:
+            self.proj = Conv2D(self.filters, 1, self.stride, 0, use_bias=False, name=f"{n}/proj",
+                               kernel_initializer="he_normal")
+            self.proj_bn = BatchNorm(relu=False, name=f"{n}/proj_bn")
+            self.proj_bn.build(self.proj.build(self.in_shape))
+        self.out_shape = s
+        return s
+
+    def sublayers(self):
+        ls = [self.conv1, self.bn1, self.conv2, self.bn2]
+        if self.proj is not None:
+            ls += [self.proj, self.proj_bn]
+        return ls
+
+    def specs(self):
+        out = []
+        for l in self.sublayers():
+            out += l.specs()
+        return out
+
+    def bind_store(self, store):
+        self.store = store
+        for l in self.sublayers():
+            l.store = store
+
+    def alloc(self, B, device, dtype, ws):
+        self.conv1.need_dx = self.need_dx
+        if self.proj is not None:
+            self.proj.need_dx = self.need_dx
+        for l in self.sublayers():
+            l.alloc(B, device, dtype, ws)
+        self.out = torch.empty((B,) + self.out_shape, device=device, dtype=dtype)
+        self.g = torch.empty_like(self.out)
+        if self.need_dx:
+            self.dx = torch.empty((B,) + self.in_shape, device=device, dtype=dtype)
+
+    def forward(self, x, training):
+        self.x = x
+        h = self.conv1.forward(x, training)
+        h = self.bn1.forward(h, training)
+        h = self.conv2.forward(h, training)
+        h = self.bn2.forward(h, training)
+        sc = x
+        if self.proj is not None:
+            sc = self.proj_bn.forward(self.proj.forward(x, training), training)
+        ops.add_act(h, sc, self.out, relu=True)
+        return self.out
+
+    def backward(self, dy):
+        g = ops.relu_bwd(self.out, dy, self.g)  # relu' of the block output, shared by both branches
+        d = self.bn2.backward(g)
+        d = self.conv2.backward(d)
+        d = self.bn1.backward(d)
+        d = self.conv1.backward(d)
+        if self.proj is not None:
+            ds = self.proj.backward(self.proj_bn.backward(g))
+        else:
+            ds = g
+        if not self.need_dx:
+            return None
+        # input relu' (block input is the previous block's ReLU output) is applied by add_act on
+        # the two branch gradients: dx = (d + ds) * (x > 0) — done as add then relu_bwd.
+        ops.add_act(d, ds, self.dx, relu=False)
+        if self.in_relu:
+            ops.relu_bwd(self.x, self.dx, self.dx)
+        return self.dx
+
+    def config(self):
+        return {"filters": self.filters, "stride": self.stride}

@@ -1,0 +1,225 @@
+"""The model executor: a sequential layer graph with explicit forward/backward on preallocated
+buffers, a flat parameter store, and hipGraph capture of the whole training step.
+
+This is the engine behind ``DistriModel.fit`` / ``update`` (reference: DistributedTfModel.fit =
+``tf.variableGrads(softmaxCE(predictOnBatch(x), y).mean())`` and update = per-tensor ``w -= lr*g``,
+/root/reference/src/common/models.ts:128-142).  Deliberate differences:
+the loss is a correct, fused softmax-cross-entropy on pre-softmax logits, and a trailing softmax
+activation is folded into it rather than executed.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+import torch
+
+from .. import ops
+from .layers import Activation, BatchNorm, Dense, Dropout, Flatten, Layer, ResidualBlock
+from .params import ParamStore
+
+
+@dataclass
+class Workspace:
+    wgrad: torch.Tensor   # fp32 split-m slabs for weight gradients
+    bn: torch.Tensor      # fp32 BN partial sums
+
+
+class Net:
+    def __init__(self, layers: list[Layer], input_shape: tuple, num_classes: Optional[int] = None,
+                 device="cuda", name: str = "model", seed: int = 0, compute_dtype: Optional[torch.dtype] = None):
+        self.name = name
+        self.device = torch.device(device)
+        self.input_shape = tuple(input_shape)
+        self.layers_all = list(layers)
+        self.is_gpu = self.device.type == "cuda"
+        self.dtype = compute_dtype or (torch.bfloat16 if self.is_gpu else torch.float32)
+        self._plan()
+        specs = []
+        for l in self.exec_layers:
+            specs += l.specs()
+        self.store = ParamStore(specs, self.device, compute_bf16=self.is_gpu, seed=seed)
+        for l in self.exec_layers:
+            if isinstance(l, ResidualBlock):
+                l.bind_store(self.store)
+            else:
+                l.store = self.store
+        self.num_classes = num_classes or self.output_shape[-1]
+        self.step_dev = torch.zeros((), dtype=torch.int64, device=self.device)
+        for l in self._all_leaf_layers():
+            if isinstance(l, Dropout):
+                l.step_dev = self.step_dev
+        self._bound_B = None
+        self.graphs: dict = {}
+
+    # ------------------------------------------------------------------ planning / fusion
+    def _plan(self):
+        shape = self.input_shape
+        execd: list[Layer] = []
+        pending = list(self.layers_all)
+        i = 0
+        self.final_softmax = False
+        while i < len(pending):
+            l = pending[i]
+            shape = l.build(shape)
+            if isinstance(l, Flatten):
+                i += 1
+                continue
+            if isinstance(l, Activation):
+                act = l.activation
+                prev = execd[-1] if execd else None
+                if act in ("linear", None):
+                    pass
+                elif act == "relu" and prev is not None and prev.can_fuse_relu() and not prev.relu:
+                    prev.relu = True  # fused into the producer's epilogue (config() keeps the Keras view)
+                elif act == "softmax" and i == len(pending) - 1:
+                    self.final_softmax = True
+                else:
+                    raise NotImplementedError(f"cannot place activation {act!r} after {type(prev).__name__}")
+                i += 1
+                continue
+            execd.append(l)
+            i += 1
+        if not execd:
+            raise ValueError("empty model")
+        last = execd[-1]
+        if isinstance(last, Dense):
+            if last.activation == "softmax":
+                self.final_softmax = True
+            last.out_f32 = True
+            if last.relu:
+                raise ValueError("the logits layer must not end in ReLU")
+        else:
+            raise NotImplementedError("the last executed layer must be Dense (logits)")
+        # relu' bookkeeping + first-layer dgrad elision
+        for j, l in enumerate(execd):
+            l.need_dx = j > 0
+            l.in_relu = j > 0 and execd[j - 1].relu
+        self.exec_layers = execd
+        self.output_shape = shape
+
+    def _all_leaf_layers(self):
+        for l in self.exec_layers:
+            if isinstance(l, ResidualBlock):
+                yield from l.sublayers()
+            else:
+                yield l
+
+    # ------------------------------------------------------------------ buffers
+    def bind(self, B: int):
+        if self._bound_B == B:
+            return
+        ws_wgrad = torch.empty(1 << 22, dtype=torch.float32, device=self.device)
+        maxC = max([l.C for l in self._all_leaf_layers() if isinstance(l, BatchNorm)] + [8])
+        ws_bn = torch.empty(2 * maxC * 256, dtype=torch.float32, device=self.device)
+        self.ws = Workspace(ws_wgrad, ws_bn)
+        for l in self.exec_layers:
+            l.alloc(B, self.device, self.dtype, self.ws)
+        self.dlogits = torch.empty((B, self.num_classes), dtype=self.dtype, device=self.device)
+        self.stats = torch.zeros(2, dtype=torch.float32, device=self.device)
+        self.x_buf = torch.empty((B,) + self.input_shape, dtype=self.dtype, device=self.device)
+        self.y_buf = torch.empty((B,), dtype=torch.int32, device=self.device)
+        self._bound_B = B
+        self.graphs = {}
+
+    # ------------------------------------------------------------------ compute
+    def forward(self, x: torch.Tensor, training: bool = False) -> torch.Tensor:
+        """Returns fp32 logits [B][classes] (a view of an engine buffer)."""
+        self.bind(x.shape[0])
+        h = x
+        for l in self.exec_layers:
+            h = l.forward(h, training)
+        return h
+
+    def backward(self, dlogits: torch.Tensor, grad_ready: Optional[Callable[[int], None]] = None):
+        """Backprop dlogits; fills ``store.grad``.  ``grad_ready(i)`` fires after layer i's grads are final
+        (reverse order) so a data-parallel wrapper can launch bucketed all-reduces early."""
+        d = dlogits
+        for i in range(len(self.exec_layers) - 1, -1, -1):
+            d = self.exec_layers[i].backward(d)
+            if grad_ready is not None:
+                grad_ready(i)
+
+    def loss_and_grad(self, logits, labels, grad_scale: Optional[float] = None):
+        B = logits.shape[0]
+        self.stats.zero_()
+        ops.softmax_ce(logits, labels, self.dlogits, self.stats, 1.0 / B if grad_scale is None else grad_scale)
+        return self.stats
+
+    def compute_gradients(self, x, labels, grad_ready=None):
+        """fwd + fused softmax-CE + bwd; returns the device stats tensor [loss_sum, correct]."""
+        if x.dtype != self.dtype:
+            x = x.to(self.dtype)
+        if labels.dtype != torch.int32:
+            labels = labels.to(torch.int32)
+        self.step_dev.add_(1)
+        logits = self.forward(x, training=True)
+        stats = self.loss_and_grad(logits, labels)
+        self.backward(self.dlogits, grad_ready)
+        return stats
+
+    @torch.no_grad()
+    def evaluate(self, x, labels, batch_size: int = 4096):
+        """-> (mean loss, accuracy) over the given examples (inference mode, chunked)."""
+        n = x.shape[0]
+        loss = 0.0
+        correct = 0.0
+        for s in range(0, n, batch_size):
+            xb = x[s: s + batch_size].to(self.device, self.dtype)
+            yb = labels[s: s + batch_size].to(self.device, torch.int32)
+            logits = self._forward_eval(xb)
+            st = torch.zeros(2, dtype=torch.float32, device=self.device)
+            ops.softmax_ce(logits, yb, None, st, 1.0)
+            loss += float(st[0])
+            correct += float(st[1])
+        return loss / max(n, 1), correct / max(n, 1)
+
+    def _forward_eval(self, xb):
+        B = xb.shape[0]
+        if self._bound_B != B:
+            saved = self._bound_B
+            self.bind(B)
+            out = self.forward(xb, training=False).clone()
+            if saved is not None:
+                self.bind(saved)
+            return out
+        return self.forward(xb, training=False).clone()
+
+    @torch.no_grad()
+    def predict(self, x, batch_size: int = 4096) -> torch.Tensor:
+        outs = []
+        for s in range(0, x.shape[0], batch_size):
+            xb = x[s: s + batch_size].to(self.device, self.dtype)
+            z = self._forward_eval(xb)
+            outs.append(torch.softmax(z, dim=1) if self.final_softmax else z)
+        return torch.cat(outs)
+
+    # ------------------------------------------------------------------ introspection
+    def num_params(self) -> int:
+        return sum(s.numel for s in self.store.specs)
+
+    def summary(self) -> str:
+        lines = [f"Net {self.name}: input {self.input_shape}, {self.num_params():,} params"]
+        for l in self.exec_layers:
+            lines.append(f"  {type(l).__name__:<22} {l.name:<24} {str(l.in_shape):<16} -> {str(l.out_shape):<16}"
+                         f"{' +relu' if l.relu else ''}")
+        return "\n".join(lines)
+
+    def flops_per_example(self) -> int:
+        """Training FLOPs per example (fwd + dgrad + wgrad of every GEMM-shaped layer)."""
+        total = 0
+
+        def layer_flops(l):
+            if isinstance(l, Dense):
+                f = 2 * l.in_features * l.units
+                return f * (3 if l.need_dx else 2)
+            from .layers import Conv2D
+            if isinstance(l, Conv2D):
+                OH, OW, N = l.out_shape
+                f = 2 * OH * OW * N * l.k * l.k * l.in_shape[2]
+                return f * (3 if l.need_dx else 2)
+            return 0
+
+        for l in self._all_leaf_layers():
+            total += layer_flops(l)
+        return total

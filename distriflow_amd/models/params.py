@@ -1,0 +1,234 @@
+"""Flat parameter storage for the training engine.
+
+All trainable tensors of a model live in ONE contiguous fp32 master buffer (and one fp32 gradient
+buffer with identical offsets), in model order — kernel then bias, exactly the order of a tf.js
+LayersModel's ``trainableWeights`` / ``weightsManifest`` (the reference relies on
+``Object.keys`` order; here the order is explicit).  Consequences:
+
+  * the gradient all-reduce is a single RCCL call on one buffer (or a few contiguous buckets,
+    since backward produces gradients in reverse layer order = a growing suffix of the buffer);
+  * the SGD update is one fused multi-tensor launch (``sgd_multi``) that also re-emits the bf16
+    compute copies of every weight matrix in the two MFMA layouts ([N][K] and the dgrad layout),
+    zero padded to 16 x 32 tiles;
+  * serialisation (protocol / checkpoints) is a view of one buffer.
+
+Matrix parameters use the layout [N][T*Ci] (dense: [out][in]; conv: OHWI = [Cout][KH*KW*Cin]).
+Keras/tf.js layouts ([in][out], HWIO) are converted at the checkpoint boundary only.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, Optional
+
+import torch
+
+from .. import native
+
+SGD_ELEMS_PER_BLOCK = 1024
+
+
+def _r(a, b):
+    return (a + b - 1) // b * b
+
+
+@dataclass
+class ParamSpec:
+    name: str
+    shape: tuple                    # master (engine) layout
+    kind: str = "vector"            # "matrix" | "vector"
+    mat: tuple = (0, 0, 0)          # (N, T, Ci) for matrices
+    init: str | Callable = "zeros"  # glorot_uniform | he_normal | zeros | ones | callable(tensor)
+    fan: tuple = (1, 1)             # (fan_in, fan_out) for initialisers
+    needs_dgrad: bool = True        # keep a bf16 dgrad-layout copy
+    trainable: bool = True
+
+    @property
+    def numel(self) -> int:
+        return int(math.prod(self.shape))
+
+
+class ParamStore:
+    def __init__(self, specs: list[ParamSpec], device, compute_bf16: bool, seed: int = 0):
+        self.specs = list(specs)
+        self.device = torch.device(device)
+        self.compute_bf16 = compute_bf16 and self.device.type == "cuda"
+        self.offsets: dict[str, int] = {}
+        off = 0
+        for s in self.specs:
+            # 16-byte alignment of every tensor inside the flat buffers (vector loads)
+            off = _r(off, 4)
+            self.offsets[s.name] = off
+            off += s.numel
+        self.total = _r(off, 4)
+        self.master = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self.momentum: Optional[torch.Tensor] = None
+        self._views = {s.name: self.master[self.offsets[s.name]: self.offsets[s.name] + s.numel].view(s.shape)
+                       for s in self.specs}
+        self._gviews = {s.name: self.grad[self.offsets[s.name]: self.offsets[s.name] + s.numel].view(s.shape)
+                        for s in self.specs}
+        self._spec = {s.name: s for s in self.specs}
+        self.hyper = torch.zeros(5, dtype=torch.float32, device=self.device)
+        self._hyper_host = None
+        self._init_values(seed)
+        if self.compute_bf16:
+            self._build_compute_copies()
+            self.refresh_compute()
+
+    # ------------------------------------------------------------------ views
+    def __getitem__(self, name) -> torch.Tensor:
+        return self._views[name]
+
+    def gradient(self, name) -> torch.Tensor:
+        return self._gviews[name]
+
+    def spec(self, name) -> ParamSpec:
+        return self._spec[name]
+
+    def names(self):
+        return [s.name for s in self.specs]
+
+    def weight(self, name) -> torch.Tensor:
+        """Compute weights of a matrix param: GPU padded bf16 [Npad][Kpad]; CPU fp32 [N][K] view."""
+        if self.compute_bf16:
+            return self._wbf_views[name]
+        s = self._spec[name]
+        N, T, Ci = s.mat
+        return self._views[name].view(N, T * Ci)
+
+    def weight_t(self, name) -> Optional[torch.Tensor]:
+        """dgrad-layout bf16 copy [Cipad][pad(T*N)] (GPU only)."""
+        if self.compute_bf16:
+            return self._wbft_views.get(name)
+        return None
+
+    def grad_matrix(self, name) -> torch.Tensor:
+        s = self._spec[name]
+        N, T, Ci = s.mat
+        return self._gviews[name].view(N, T * Ci)
+
+    # ------------------------------------------------------------------ init
+    def _init_values(self, seed):
+        g = torch.Generator(device="cpu")
+        g.manual_seed(seed)
+        for s in self.specs:
+            v = torch.empty(s.shape, dtype=torch.float32)
+            fan_in, fan_out = s.fan
+            if callable(s.init):
+                s.init(v)
+            elif s.init == "zeros":
+                v.zero_()
+            elif s.init == "ones":
+                v.fill_(1.0)
+            elif s.init == "glorot_uniform":
+                lim = math.sqrt(6.0 / (fan_in + fan_out))
+                v.uniform_(-lim, lim, generator=g)
+            elif s.init == "he_normal":
+                v.normal_(0.0, math.sqrt(2.0 / fan_in), generator=g)
+            elif s.init == "lecun_uniform":
+                lim = math.sqrt(3.0 / fan_in)
+                v.uniform_(-lim, lim, generator=g)
+            else:
+                raise ValueError(f"unknown initialiser {s.init!r}")
+            self._views[s.name].copy_(v)
+
+    # ------------------------------------------------------------------ bf16 compute copies
+    def _build_compute_copies(self):
+        descs = []
+        boff = 0
+        self._wbf_layout = {}
+        block = 0
+        for s in self.specs:
+            bf_off = bft_off = -1
+            N = T = Ci = 1
+            if s.kind == "matrix":
+                N, T, Ci = s.mat
+                K = T * Ci
+                bf_off = boff
+                boff += _r(N, 16) * _r(K, 32)
+                if s.needs_dgrad:
+                    bft_off = boff
+                    boff += _r(Ci, 16) * _r(T * N, 32)
+                self._wbf_layout[s.name] = (bf_off, bft_off)
+            if s.trainable or s.kind == "matrix":
+                nblocks = (s.numel + SGD_ELEMS_PER_BLOCK - 1) // SGD_ELEMS_PER_BLOCK
+                if s.kind == "vector":
+                    N, T, Ci = 1, 1, s.numel
+                descs.append((self.offsets[s.name], bf_off, bft_off, s.numel, N, T, Ci, block,
+                              0 if s.trainable else 1))
+                block += nblocks
+        self.wbf = torch.zeros(max(boff, 8), dtype=torch.bfloat16, device=self.device)
+        self._wbf_views = {}
+        self._wbft_views = {}
+        for s in self.specs:
+            if s.kind != "matrix":
+                continue
+            N, T, Ci = s.mat
+            K = T * Ci
+            bf_off, bft_off = self._wbf_layout[s.name]
+            self._wbf_views[s.name] = self.wbf[bf_off: bf_off + _r(N, 16) * _r(K, 32)].view(_r(N, 16), _r(K, 32))
+            if bft_off >= 0:
+                self._wbft_views[s.name] = self.wbf[bft_off: bft_off + _r(Ci, 16) * _r(T * N, 32)].view(
+                    _r(Ci, 16), _r(T * N, 32))
+        # ParamDesc = {i64 off, i64 bf_off, i64 bft_off, i32 numel, i32 N, i32 T, i32 Ci, i32 block_start, i32 pad}
+        raw = []
+        frozen = []
+        for (off, bf, bft, numel, N, T, Ci, bstart, frz) in descs:
+            raw += [off, bf, bft, (numel & 0xFFFFFFFF) | (N << 32), (T & 0xFFFFFFFF) | (Ci << 32),
+                    (bstart & 0xFFFFFFFF)]
+            frozen.append(frz)
+        self._descs = torch.tensor(raw, dtype=torch.int64, device=self.device)
+        self._ndesc = len(descs)
+        self._sgd_blocks = block
+        if any(frozen):
+            raise NotImplementedError("non-trainable matrix parameters are not supported yet")
+
+    def refresh_compute(self):
+        """Re-emit the bf16 compute copies from the fp32 master (after init / set_vars / load)."""
+        if not self.compute_bf16:
+            return
+        native.require().sgd_multi(self._descs, self._ndesc, self._sgd_blocks, self.master, self.grad, None,
+                                   self.wbf, self.hyper, False)
+
+    # ------------------------------------------------------------------ optimiser
+    def set_hyper(self, lr, momentum=0.0, weight_decay=0.0, grad_scale=1.0, nesterov=False):
+        h = (float(lr), float(momentum), float(weight_decay), float(grad_scale), 1.0 if nesterov else 0.0)
+        if h != self._hyper_host:
+            self.hyper.copy_(torch.tensor(h, dtype=torch.float32), non_blocking=False)
+            self._hyper_host = h
+        if momentum != 0.0 and self.momentum is None:
+            self.momentum = torch.zeros_like(self.master)
+
+    def sgd_step(self):
+        """w -= lr * (grad_scale * g [+ wd w]) (momentum optional); uses the device-side hyper tensor."""
+        if self.compute_bf16:
+            native.require().sgd_multi(self._descs, self._ndesc, self._sgd_blocks, self.master, self.grad,
+                                       self.momentum, self.wbf, self.hyper, True)
+            return
+        lr, mom, wd, gs, nest = self._hyper_host
+        g = self.grad * gs
+        if wd:
+            g = g + wd * self.master
+        if mom:
+            self.momentum.mul_(mom).add_(g)
+            g = g + mom * self.momentum if nest else self.momentum
+        self.master.sub_(lr * g)
+
+    def apply_delta(self, delta: torch.Tensor, lr: float):
+        """master -= lr * delta  (server-side update with an already-aggregated gradient)."""
+        self.master.sub_(delta * lr)
+        self.refresh_compute()
+
+    # ------------------------------------------------------------------ (de)serialisation
+    def get_vars(self) -> list[torch.Tensor]:
+        return [self._views[s.name] for s in self.specs]
+
+    def set_vars(self, values):
+        for s, v in zip(self.specs, values):
+            self._views[s.name].copy_(torch.as_tensor(v).reshape(s.shape))
+        self.refresh_compute()
+
+    def set_flat(self, flat: torch.Tensor):
+        self.master.copy_(flat.reshape(-1)[: self.total])
+        self.refresh_compute()

@@ -1,0 +1,235 @@
+"""Functional ops of the training engine.
+
+GPU tensors run the hand-written gfx950 kernels of ``distriflow_amd._C`` (no fallback: a missing
+extension raises); CPU tensors run the fp32 reference in :mod:`.reference` (CPU plumbing config
+and numerics oracle).  All ops write into caller-provided output buffers so that the engine can
+preallocate everything once and capture the whole training step into a hipGraph.
+
+Weight arguments:
+  * ``w``  — compute weights [Npad][Kpad] (GPU: zero-padded bf16 copy; CPU: fp32 master view [N][K])
+  * ``wt`` — dgrad weights [Cin_pad][pad(KH*KW*N)] (GPU only; the CPU path derives it from ``w``)
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import native
+from . import reference as ref
+
+MODE_DIRECT, MODE_FWD, MODE_DGRAD = 0, 1, 2
+
+
+def _C():
+    return native.require()
+
+
+def _geom(SH=1, SW=1, SC=1, OH=1, OW=1, KH=1, KW=1, stride=1, pad=0):
+    return [int(SH), int(SW), int(SC), int(OH), int(OW), int(KH), int(KW), int(stride), int(pad)]
+
+
+def conv_out_hw(H, W, KH, KW, stride, pad):
+    return (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+
+
+# ----------------------------------------------------------------------------------- dense
+def dense_fwd(x, w, bias, out, relu=False):
+    """out[B][N] = act(x[B][K] @ W^T + b); out may be bf16 or fp32 (logits)."""
+    B, K = x.shape[0], x.shape[-1]
+    N = out.shape[-1]
+    if x.is_cuda:
+        _C().igemm_fwd(x, w, bias, None, out, B, N, K, w.shape[1], K, N, _geom(), MODE_DIRECT, relu, 1.0)
+    else:
+        out.copy_(ref.dense_fwd(x, w, bias, relu))
+    return out
+
+
+def dense_dgrad(dy, w, wt, out, mask=None):
+    """out[B][K] = (dy[B][N] @ W) * relu'(mask)."""
+    B, N = dy.shape[0], dy.shape[-1]
+    K = out.shape[-1]
+    if dy.is_cuda:
+        _C().igemm_fwd(dy, wt, None, mask, out, B, K, N, wt.shape[1], N, K, _geom(), MODE_DIRECT, False, 1.0)
+    else:
+        out.copy_(ref.dense_dgrad(dy, w, K, mask))
+    return out
+
+
+def dense_wgrad(dy, x, gw, gb, workspace=None, scale=1.0):
+    """gw[N][K] = dy^T x * scale ; gb[N] = sum_b dy * scale."""
+    B, N = dy.shape[0], dy.shape[-1]
+    K = x.shape[-1]
+    if dy.is_cuda:
+        _C().igemm_wgrad(dy, x, gw, gb, workspace, B, N, K, N, K, _geom(), MODE_DIRECT, scale)
+    else:
+        g, b = ref.dense_wgrad(dy, x, gb is not None)
+        gw.copy_(g.reshape(gw.shape) * scale)
+        if gb is not None:
+            gb.copy_(b * scale)
+
+
+# ----------------------------------------------------------------------------------- conv2d
+def conv_fwd(x, w, bias, out, KH, KW, stride=1, pad=0, relu=False):
+    """NHWC conv: out[B][OH][OW][N]; w = [Npad][Kpad] with K = KH*KW*C."""
+    B, H, W, C = x.shape
+    _, OH, OW, N = out.shape
+    if x.is_cuda:
+        K = KH * KW * C
+        _C().igemm_fwd(x, w, bias, None, out, B * OH * OW, N, K, w.shape[1], 0, N,
+                       _geom(H, W, C, OH, OW, KH, KW, stride, pad), MODE_FWD, relu, 1.0)
+    else:
+        out.copy_(ref.conv_fwd(x, w, bias, KH, KW, stride, pad, relu))
+    return out
+
+
+def conv_dgrad(dy, w, wt, out, KH, KW, stride=1, pad=0, mask=None):
+    """dX (NHWC [B][H][W][C]) of a conv whose output gradient is dy [B][OH][OW][N]."""
+    B, OH, OW, N = dy.shape
+    _, H, W, C = out.shape
+    if dy.is_cuda:
+        K = KH * KW * N
+        _C().igemm_fwd(dy, wt, None, mask, out, B * H * W, C, K, wt.shape[1], 0, C,
+                       _geom(OH, OW, N, H, W, KH, KW, stride, pad), MODE_DGRAD, False, 1.0)
+    else:
+        out.copy_(ref.conv_dgrad(dy, w, out.shape, KH, KW, stride, pad, mask))
+    return out
+
+
+def conv_wgrad(dy, x, gw, gb, workspace, KH, KW, stride=1, pad=0, scale=1.0):
+    B, H, W, C = x.shape
+    _, OH, OW, N = dy.shape
+    if dy.is_cuda:
+        K = KH * KW * C
+        _C().igemm_wgrad(dy, x, gw, gb, workspace, B * OH * OW, N, K, N, 0,
+                         _geom(H, W, C, OH, OW, KH, KW, stride, pad), MODE_FWD, scale)
+    else:
+        g, b = ref.conv_wgrad(dy, x, KH, KW, stride, pad, gb is not None)
+        gw.copy_(g.reshape(gw.shape) * scale)
+        if gb is not None:
+            gb.copy_(b * scale)
+
+
+# ----------------------------------------------------------------------------------- pooling etc.
+def maxpool_fwd(x, out, P):
+    B, H, W, C = x.shape
+    if x.is_cuda:
+        _C().maxpool_fwd(x, out, B, H, W, C, P)
+    else:
+        out.copy_(ref.maxpool_fwd(x, P))
+    return out
+
+
+def maxpool_bwd(x, dy, dx, P, relu_fused=False):
+    B, H, W, C = x.shape
+    if x.is_cuda:
+        _C().maxpool_bwd(x, dy, dx, B, H, W, C, P, relu_fused)
+    else:
+        dx.copy_(ref.maxpool_bwd(x, dy, P, relu_fused))
+    return dx
+
+
+def softmax_ce(logits, labels, dlogits=None, stats=None, grad_scale=1.0):
+    """Fused softmax-cross-entropy: dlogits = (softmax - onehot) * grad_scale; stats += [loss_sum, #correct]."""
+    B, C = logits.shape
+    if logits.is_cuda:
+        ldg = dlogits.shape[-1] if dlogits is not None else C
+        _C().softmax_ce(logits, labels, dlogits, stats, B, C, C, ldg, grad_scale)
+    else:
+        loss, corr, dl = ref.softmax_ce(logits, labels, grad_scale)
+        if dlogits is not None:
+            dlogits.copy_(dl)
+        if stats is not None:
+            stats[0] += loss
+            stats[1] += corr
+
+
+def dropout(x, out, p, seed, mask=None, step=None):
+    """out = x * keep(seed ^ step, i) / (1 - p) [* relu'(mask)]; ``step`` is a device int64 scalar."""
+    if x.is_cuda:
+        _C().dropout(x, out, p, seed, mask, step)
+    else:
+        s = seed ^ (int(step.item()) * 0x9E3779B1 if step is not None else 0)
+        out.copy_(ref.dropout(x, p, s, mask).reshape(out.shape))
+    return out
+
+
+def gather_batch(data, labels, idx, out, out_labels, scale=1.0):
+    """out[b] = data[idx[b]] (uint8 -> bf16 * scale on the fly); out_labels[b] = labels[idx[b]]."""
+    B = idx.shape[0]
+    row = out[0].numel()
+    if out.is_cuda:
+        _C().gather_batch(data, labels, idx, out, out_labels, B, row, scale)
+    else:
+        out.copy_((data.index_select(0, idx).float() * scale).reshape(out.shape))
+        if labels is not None:
+            out_labels.copy_(labels.index_select(0, idx))
+    return out
+
+
+def add_act(a, b, out, relu=False):
+    if a.is_cuda:
+        _C().add_act(a, b, out, relu)
+    else:
+        r = a.float() + b.float()
+        out.copy_(torch.relu(r) if relu else r)
+    return out
+
+
+def relu_bwd(y, dy, dx):
+    if y.is_cuda:
+        _C().relu_bwd(y, dy, dx)
+    else:
+        dx.copy_((dy.float().reshape(y.shape) * (y.float() > 0)).reshape(dx.shape))
+    return dx
+
+
+def gap_fwd(x, out):
+    B, H, W, C = x.shape
+    if x.is_cuda:
+        _C().gap_fwd(x, out, B, H * W, C)
+    else:
+        out.copy_(x.float().mean(dim=(1, 2)))
+    return out
+
+
+def gap_bwd(dy, dx):
+    B, H, W, C = dx.shape
+    if dy.is_cuda:
+        _C().gap_bwd(dy, dx, B, H * W, C)
+    else:
+        dx.copy_((dy.float() / (H * W)).view(B, 1, 1, C).expand(B, H, W, C))
+    return dx
+
+
+def bn_fwd_train(x2d, y2d, gamma, beta, mean, invstd, run_mean, run_var, ws, momentum, eps, relu):
+    M, C = x2d.shape
+    if x2d.is_cuda:
+        _C().bn_fwd_train(x2d, y2d, gamma, beta, mean, invstd, run_mean, run_var, ws, M, C, momentum, eps, relu)
+    else:
+        y, mu, var, inv = ref.batchnorm_train(x2d, gamma, beta, eps)
+        y2d.copy_(torch.relu(y) if relu else y)
+        mean.copy_(mu)
+        invstd.copy_(inv)
+        unb = var * M / max(M - 1, 1)
+        run_mean.mul_(1 - momentum).add_(mu * momentum)
+        run_var.mul_(1 - momentum).add_(unb * momentum)
+
+
+def bn_fwd_eval(x2d, y2d, gamma, beta, run_mean, run_var, eps, relu):
+    M, C = x2d.shape
+    if x2d.is_cuda:
+        _C().bn_fwd_eval(x2d, y2d, gamma, beta, run_mean, run_var, M, C, eps, relu)
+    else:
+        y = (x2d.float() - run_mean) * torch.rsqrt(run_var + eps) * gamma + beta
+        y2d.copy_(torch.relu(y) if relu else y)
+
+
+def bn_bwd(x2d, y2d, dy2d, dx2d, gamma, beta, mean, invstd, dgamma, dbeta, ws, relu, gscale=1.0):
+    M, C = x2d.shape
+    if x2d.is_cuda:
+        _C().bn_bwd(x2d, y2d, dy2d, dx2d, gamma, beta, mean, invstd, dgamma, dbeta, ws, M, C, relu, gscale)
+    else:
+        g = dy2d.float() * (y2d.float() > 0) if relu else dy2d.float()
+        dx, sg, sb = ref.batchnorm_bwd(x2d, g, gamma, mean, invstd)
+        dx2d.copy_(dx)
+        dgamma.copy_(sg * gscale)
+        dbeta.copy_(sb * gscale)

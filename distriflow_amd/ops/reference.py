@@ -1,0 +1,155 @@
+"""Plain-PyTorch fp32 reference implementations of every distriflow_amd op.
+
+Two uses: (1) the CPU execution path (gloo multi-process tests, CPU plumbing config of
+BASELINE.json configs[0]); (2) the numerics oracle the HIP kernels are tested against.
+Layouts match the kernels exactly: activations NHWC, weights [N][KH*KW*Cin] (OHWI).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1)
+
+
+def conv_weight_4d(w2d, N, KH, KW, C):
+    """[N][KH*KW*C] (OHWI) -> [N][C][KH][KW] (torch OIHW)."""
+    return w2d[:N, : KH * KW * C].reshape(N, KH, KW, C).permute(0, 3, 1, 2)
+
+
+def conv_fwd(x, w2d, bias, KH, KW, stride, pad, relu):
+    B, H, W, C = x.shape
+    N = bias.shape[0] if bias is not None else w2d.shape[0]
+    w4 = conv_weight_4d(w2d.float(), N, KH, KW, C)
+    y = F.conv2d(_nchw(x.float()), w4, bias.float() if bias is not None else None, stride=stride, padding=pad)
+    if relu:
+        y = torch.relu(y)
+    return _nhwc(y)
+
+
+def conv_dgrad(dy, w2d, in_shape, KH, KW, stride, pad, mask=None):
+    B, H, W, C = in_shape
+    N = dy.shape[-1]
+    w4 = conv_weight_4d(w2d.float(), N, KH, KW, C)
+    dx = torch.nn.grad.conv2d_input((B, C, H, W), w4, _nchw(dy.float()), stride=stride, padding=pad)
+    dx = _nhwc(dx)
+    if mask is not None:
+        dx = dx * (mask.float() > 0)
+    return dx
+
+
+def conv_wgrad(dy, x, KH, KW, stride, pad, with_bias=True):
+    B, H, W, C = x.shape
+    N = dy.shape[-1]
+    gw = torch.nn.grad.conv2d_weight(_nchw(x.float()), (N, C, KH, KW), _nchw(dy.float()), stride=stride, padding=pad)
+    gw = gw.permute(0, 2, 3, 1).reshape(N, KH * KW * C)
+    gb = dy.float().sum(dim=(0, 1, 2)) if with_bias else None
+    return gw, gb
+
+
+def dense_fwd(x, w2d, bias, relu):
+    N = bias.shape[0] if bias is not None else w2d.shape[0]
+    K = x.shape[-1]
+    y = x.float() @ w2d[:N, :K].float().t()
+    if bias is not None:
+        y = y + bias.float()
+    if relu:
+        y = torch.relu(y)
+    return y
+
+
+def dense_dgrad(dy, w2d, K, mask=None):
+    N = dy.shape[-1]
+    dx = dy.float() @ w2d[:N, :K].float()
+    if mask is not None:
+        dx = dx * (mask.float() > 0)
+    return dx
+
+
+def dense_wgrad(dy, x, with_bias=True):
+    gw = dy.float().t() @ x.float()
+    gb = dy.float().sum(0) if with_bias else None
+    return gw, gb
+
+
+def maxpool_fwd(x, P):
+    return _nhwc(F.max_pool2d(_nchw(x.float()), P, P))
+
+
+def maxpool_bwd(x, dy, P, relu_fused):
+    xf = _nchw(x.float()).detach().requires_grad_(True)
+    y = F.max_pool2d(xf, P, P)
+    B, H, W, C = x.shape
+    g = _nchw(dy.float().reshape(B, H // P, W // P, C))
+    if relu_fused:
+        g = g * (y.detach() > 0)
+    (dx,) = torch.autograd.grad(y, xf, g)
+    return _nhwc(dx)
+
+
+def softmax_ce(logits, labels, grad_scale):
+    z = logits.float()
+    lse = torch.logsumexp(z, dim=1)
+    loss = lse - z.gather(1, labels.long().view(-1, 1)).squeeze(1)
+    p = torch.softmax(z, dim=1)
+    onehot = F.one_hot(labels.long(), z.shape[1]).float()
+    dlogits = (p - onehot) * grad_scale
+    correct = (z.argmax(1) == labels.long()).float().sum()
+    return loss.sum(), correct, dlogits
+
+
+def _hash_u32(seed: int, idx: torch.Tensor) -> torch.Tensor:
+    """Bit-exact CPU twin of dfa::hash_u32 (splitmix64 finaliser) on int64 tensors."""
+    M64 = (1 << 64) - 1
+
+    def u64(v):
+        return torch.tensor(v - (1 << 64) if v >= (1 << 63) else v, dtype=torch.int64)
+
+    def lsr(v, s):  # logical shift right on int64 tensors holding uint64 bits
+        return (v >> s) & ((1 << (64 - s)) - 1)
+
+    x = idx.to(torch.int64) * u64(0x9E3779B97F4A7C15 & M64) + u64(seed & M64)
+    x = x ^ lsr(x, 30)
+    x = x * u64(0xBF58476D1CE4E5B9)
+    x = x ^ lsr(x, 27)
+    x = x * u64(0x94D049BB133111EB)
+    x = x ^ lsr(x, 31)
+    return x & 0xFFFFFFFF
+
+
+def dropout_mask(n: int, p: float, seed: int) -> torch.Tensor:
+    thresh = int(p * 4294967296.0)
+    h = _hash_u32(seed, torch.arange(n, dtype=torch.int64))
+    return (h >= thresh).float()
+
+
+def dropout(x, p, seed, mask=None):
+    keep = dropout_mask(x.numel(), p, seed).view_as(x)
+    y = x.float() * keep / (1.0 - p)
+    if mask is not None:
+        y = y * (mask.float() > 0)
+    return y
+
+
+def batchnorm_train(x2d, gamma, beta, eps):
+    mean = x2d.float().mean(0)
+    var = x2d.float().var(0, unbiased=False)
+    invstd = torch.rsqrt(var + eps)
+    y = (x2d.float() - mean) * invstd * gamma + beta
+    return y, mean, var, invstd
+
+
+def batchnorm_bwd(x2d, dy2d, gamma, mean, invstd):
+    M = x2d.shape[0]
+    xh = (x2d.float() - mean) * invstd
+    g = dy2d.float()
+    sb = g.sum(0)
+    sg = (g * xh).sum(0)
+    dx = gamma * invstd * (g - sb / M - xh * sg / M)
+    return dx, sg, sb

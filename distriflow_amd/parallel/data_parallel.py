@@ -1,0 +1,184 @@
+"""Synchronous data-parallel SGD over RCCL / xGMI (BASELINE.json configs[1], the headline benchmark).
+
+The reference's synchronous mode is a parameter server: K uploads of a gradient tagged with the
+current version are stacked on the host, averaged and applied, then new weights are broadcast to
+every client (/root/reference/src/server/federated_server.ts:71-117, client side
+/root/reference/src/client/federated_client.ts:68-132).  On one MI355X node every rank is both
+"server" and "worker": the K-way host-side stack+mean becomes ONE in-place RCCL all-reduce (SUM) of
+the flat gradient buffer and the 1/world factor of the mean is folded into the fused SGD kernel,
+so every rank applies the identical update and no weight broadcast is needed after step 0.
+
+MI355X specifics:
+  * gradient buckets are contiguous slices of the flat gradient buffer; a bucket's all-reduce is
+    issued (async, on RCCL's stream) as soon as backward has produced its last gradient, so it
+    overlaps the remaining backward kernels on the compute stream;
+  * the whole step — batch gather from the HBM-resident dataset, forward, fused loss, backward,
+    bucketed all-reduce, fused SGD — is captured into one hipGraph and replayed, removing all
+    host launch overhead (``graph="full"``); ``"split"`` captures compute only and runs the
+    all-reduce eagerly between two graphs, ``"none"`` is fully eager.
+"""
+from __future__ import annotations
+
+import time
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+
+
+class DataParallelTrainer:
+    def __init__(self, net, lr: float = 0.001, momentum: float = 0.0, weight_decay: float = 0.0,
+                 group=None, bucket_mb: float = 32.0, overlap: bool = True, graph: str = "full",
+                 broadcast_init: bool = True):
+        self.net = net
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
+        self.overlap = overlap
+        self.graph_mode = graph if net.is_gpu else "none"
+        self.bucket_bytes = int(bucket_mb * (1 << 20))
+        self._build_buckets()
+        self._works = []
+        self._graph = None
+        self._graph_B = None
+        self.steps = 0
+        if broadcast_init and self.world > 1:
+            dist.broadcast(net.store.master, src=0, group=group)
+            net.store.refresh_compute()
+        net.store.set_hyper(lr, momentum, weight_decay, grad_scale=1.0 / self.world)
+
+    # ------------------------------------------------------------------ buckets
+    def _build_buckets(self):
+        net, store = self.net, self.net.store
+        starts = []
+        for i, l in enumerate(net.exec_layers):
+            names = [s.name for s in l.specs()]
+            if names:
+                starts.append((i, min(store.offsets[n] for n in names)))
+        self.buckets = []  # (trigger layer index, lo, hi)
+        hi = store.total
+        first_param_layer = starts[0][0] if starts else 0
+        for i, lo in reversed(starts):
+            if i == first_param_layer:
+                self.buckets.append((i, 0, hi))
+                break
+            if (hi - lo) * 4 >= self.bucket_bytes:
+                self.buckets.append((i, lo, hi))
+                hi = lo
+        self._trigger = {b[0]: b for b in self.buckets}
+
+    def _grad_ready(self, layer_idx: int):
+        b = self._trigger.get(layer_idx)
+        if b is None or self.world == 1:
+            return
+        _, lo, hi = b
+        self._works.append(dist.all_reduce(self.net.store.grad[lo:hi], group=self.group, async_op=True))
+
+    def _allreduce_all(self):
+        if self.world == 1:
+            return
+        if self.overlap:
+            for w in self._works:
+                w.wait()
+        else:
+            dist.all_reduce(self.net.store.grad, group=self.group)
+        self._works = []
+
+    # ------------------------------------------------------------------ one step
+    def _step_body(self, x, y):
+        hook = self._grad_ready if (self.overlap and self.world > 1) else None
+        stats = self.net.compute_gradients(x, y, grad_ready=hook)
+        self._allreduce_all()
+        self.net.store.sgd_step()
+        return stats
+
+    def set_lr(self, lr: float):
+        self.lr = lr
+        self.net.store.set_hyper(lr, self.momentum, self.weight_decay, grad_scale=1.0 / self.world)
+
+    def train_step(self, x: torch.Tensor, y: torch.Tensor):
+        """Eager step on an explicit batch; returns device stats [loss_sum, correct]."""
+        self.steps += 1
+        return self._step_body(x, y)
+
+    # ------------------------------------------------------------------ graph-captured step over an HBM dataset
+    def bind_dataset(self, data: torch.Tensor, labels: torch.Tensor, batch_size: int, scale: float = 1.0):
+        """Attach an HBM-resident dataset (uint8/bf16 [N, ...], int32 labels); steps then take index batches."""
+        self.data, self.labels, self.scale = data, labels, scale
+        self.B = batch_size
+        net = self.net
+        net.bind(batch_size)
+        self.idx = torch.zeros(batch_size, dtype=torch.int64, device=net.device)
+        self.xb = net.x_buf
+        self.yb = net.y_buf
+
+    def _gather(self):
+        ops.gather_batch(self.data, self.labels, self.idx, self.xb, self.yb, self.scale)
+
+    def _capture(self):
+        net = self.net
+        s = torch.cuda.Stream(device=net.device)
+        s.wait_stream(torch.cuda.current_stream(net.device))
+        # warm-up on a side stream (allocator, RCCL communicators, kernel code objects)
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                self._gather()
+                self._step_body(self.xb, self.yb)
+        torch.cuda.current_stream(net.device).wait_stream(s)
+        torch.cuda.synchronize(net.device)
+        g = torch.cuda.CUDAGraph()
+        if self.graph_mode == "full":
+            with torch.cuda.graph(g):
+                self._gather()
+                self.stats = self._step_body(self.xb, self.yb)
+            self._graph = (g, None)
+        else:  # split: compute graph, eager all-reduce, SGD graph
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._gather()
+                self.stats = self.net.compute_gradients(self.xb, self.yb)
+            with torch.cuda.graph(g2):
+                self.net.store.sgd_step()
+            self._graph = (g, g2)
+        torch.cuda.synchronize(net.device)
+
+    def step_indices(self, idx: torch.Tensor):
+        """One training step on dataset rows ``idx`` (device int64 [B])."""
+        self.idx.copy_(idx, non_blocking=True)
+        self.steps += 1
+        if self.graph_mode == "none":
+            self._gather()
+            return self._step_body(self.xb, self.yb)
+        if self._graph is None:
+            try:
+                self._capture()
+            except Exception as e:  # RCCL capture unsupported -> split graphs
+                if self.graph_mode != "full":
+                    raise
+                torch.cuda.synchronize(self.net.device)
+                self.graph_mode = "split"
+                self._works = []
+                self._graph = None
+                self.capture_error = repr(e)
+                self._capture()
+        g, g2 = self._graph
+        g.replay()
+        if g2 is not None:
+            if self.world > 1:
+                dist.all_reduce(self.net.store.grad, group=self.group)
+            g2.replay()
+        return self.stats
+
+
+def epoch_permutations(n: int, batch: int, steps: int, device, seed: int = 0):
+    """Device-resident index stream: concatenated random permutations, sliced per step."""
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed)
+    need = batch * steps
+    chunks = []
+    while sum(c.numel() for c in chunks) < need:
+        chunks.append(torch.randperm(n, generator=g))
+    return torch.cat(chunks)[:need].view(steps, batch).to(device)

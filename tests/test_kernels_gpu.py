@@ -1,0 +1,243 @@
+"""Numerics of every gfx950 HIP kernel against a plain-PyTorch fp32 reference of the same op.
+
+Inputs are rounded to bf16 first (the kernels consume bf16), the reference computes in fp32 on the
+same rounded values; tolerances cover the bf16 rounding of outputs only.
+"""
+import pytest
+import torch
+
+from distriflow_amd import ops
+from distriflow_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def _r(a, b):
+    return (a + b - 1) // b * b
+
+
+def _pad_w(w2d):
+    """fp32 [N][K] -> zero padded bf16 [Npad16][Kpad32] (the engine's compute layout)."""
+    N, K = w2d.shape
+    out = torch.zeros(_r(N, 16), _r(K, 32), dtype=torch.bfloat16, device=dev)
+    out[:N, :K] = w2d.to(torch.bfloat16)
+    return out
+
+
+def _pad_wt(w2d, N, T, Ci):
+    """fp32 [N][T*Ci] -> dgrad layout bf16 [Ci_pad16][pad32(T*N)] with (ci, t, n) <- w[n, t, ci]."""
+    w3 = w2d.view(N, T, Ci).permute(2, 1, 0).reshape(Ci, T * N)
+    out = torch.zeros(_r(Ci, 16), _r(T * N, 32), dtype=torch.bfloat16, device=dev)
+    out[:Ci, :T * N] = w3.to(torch.bfloat16)
+    return out
+
+
+def _close(a, b, rtol=2e-2, atol=2e-2):
+    a = a.float()
+    b = b.float()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= atol + rtol * scale, f"max err {err:.4g} vs scale {scale:.4g}"
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+DENSE = [(64, 10, 784), (4096, 120, 400), (333, 84, 120), (1000, 10, 84), (7, 3, 5), (300, 200, 64), (50, 512, 1024)]
+
+
+@pytest.mark.parametrize("M,N,K", DENSE)
+@pytest.mark.parametrize("relu", [False, True])
+def test_dense_fwd(M, N, K, relu):
+    x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = torch.randn(N, K, device=dev) / K ** 0.5
+    b = torch.randn(N, device=dev)
+    out = torch.empty(M, N, device=dev, dtype=torch.float32)
+    ops.dense_fwd(x, _pad_w(w), b, out, relu)
+    exp = ref.dense_fwd(x.float(), w.to(torch.bfloat16).float(), b, relu)
+    _close(out, exp, 1e-3, 1e-3)
+    out16 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ops.dense_fwd(x, _pad_w(w), b, out16, relu)
+    _close(out16, exp)
+
+
+@pytest.mark.parametrize("M,N,K", DENSE)
+def test_dense_dgrad_masked(M, N, K):
+    dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    w = torch.randn(N, K, device=dev) / N ** 0.5
+    mask = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    out = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+    ops.dense_dgrad(dy, None, _pad_wt(w, N, 1, K), out, mask=mask)
+    exp = ref.dense_dgrad(dy.float(), w.to(torch.bfloat16).float(), K, mask)
+    _close(out, exp)
+
+
+@pytest.mark.parametrize("M,N,K", DENSE)
+def test_dense_wgrad(M, N, K):
+    dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    gw = torch.empty(N, K, device=dev)
+    gb = torch.empty(N, device=dev)
+    ws = torch.empty(1 << 22, device=dev)
+    ops.dense_wgrad(dy, x, gw, gb, ws)
+    ew, eb = ref.dense_wgrad(dy.float(), x.float())
+    _close(gw, ew, 1e-3, 1e-3)
+    _close(gb, eb, 1e-3, 1e-3)
+
+
+CONVS = [  # B, H, W, C, N, k, stride, pad
+    (4, 28, 28, 1, 6, 5, 1, 2),
+    (8, 14, 14, 6, 16, 5, 1, 0),
+    (4, 28, 28, 1, 32, 3, 1, 0),
+    (4, 26, 26, 32, 32, 3, 1, 0),
+    (2, 32, 32, 3, 64, 3, 1, 1),
+    (2, 16, 16, 64, 128, 3, 2, 1),
+    (2, 8, 8, 64, 128, 1, 2, 0),
+    (3, 9, 7, 16, 24, 3, 2, 1),
+]
+
+
+@pytest.mark.parametrize("B,H,W,C,N,k,s,p", CONVS)
+@pytest.mark.parametrize("relu", [False, True])
+def test_conv_fwd(B, H, W, C, N, k, s, p, relu):
+    x = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    w = torch.randn(N, k * k * C, device=dev) / (k * k * C) ** 0.5
+    b = torch.randn(N, device=dev)
+    OH, OW = ops.conv_out_hw(H, W, k, k, s, p)
+    out = torch.empty(B, OH, OW, N, device=dev, dtype=torch.bfloat16)
+    ops.conv_fwd(x, _pad_w(w), b, out, k, k, s, p, relu)
+    exp = ref.conv_fwd(x.float(), w.to(torch.bfloat16).float(), b, k, k, s, p, relu)
+    _close(out, exp)
+
+
+@pytest.mark.parametrize("B,H,W,C,N,k,s,p", CONVS)
+@pytest.mark.parametrize("masked", [False, True])
+def test_conv_dgrad(B, H, W, C, N, k, s, p, masked):
+    OH, OW = ops.conv_out_hw(H, W, k, k, s, p)
+    dy = torch.randn(B, OH, OW, N, device=dev).to(torch.bfloat16)
+    w = torch.randn(N, k * k * C, device=dev) / (k * k * N) ** 0.5
+    mask = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16) if masked else None
+    out = torch.empty(B, H, W, C, device=dev, dtype=torch.bfloat16)
+    ops.conv_dgrad(dy, None, _pad_wt(w, N, k * k, C), out, k, k, s, p, mask=mask)
+    exp = ref.conv_dgrad(dy.float(), w.to(torch.bfloat16).float(), (B, H, W, C), k, k, s, p, mask)
+    _close(out, exp)
+
+
+@pytest.mark.parametrize("B,H,W,C,N,k,s,p", CONVS)
+def test_conv_wgrad(B, H, W, C, N, k, s, p):
+    OH, OW = ops.conv_out_hw(H, W, k, k, s, p)
+    dy = torch.randn(B, OH, OW, N, device=dev).to(torch.bfloat16)
+    x = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    gw = torch.empty(N, k * k * C, device=dev)
+    gb = torch.empty(N, device=dev)
+    ws = torch.empty(1 << 22, device=dev)
+    ops.conv_wgrad(dy, x, gw, gb, ws, k, k, s, p)
+    ew, eb = ref.conv_wgrad(dy.float(), x.float(), k, k, s, p)
+    _close(gw, ew, 1e-3, 1e-3)
+    _close(gb, eb, 1e-3, 1e-3)
+
+
+def test_conv_wgrad_large_m_split():
+    """Tall-skinny reduction (K = B*OH*OW = 1.3M) exercising many split-m slabs + the reduce kernel."""
+    B, H, W, C, N, k = 512, 28, 28, 1, 6, 5
+    dy = torch.randn(B, H, W, N, device=dev).to(torch.bfloat16)
+    x = torch.rand(B, H, W, C, device=dev).to(torch.bfloat16)
+    gw = torch.empty(N, k * k * C, device=dev)
+    gb = torch.empty(N, device=dev)
+    ws = torch.empty(1 << 22, device=dev)
+    ops.conv_wgrad(dy, x, gw, gb, ws, k, k, 1, 2)
+    ew, eb = ref.conv_wgrad(dy.float(), x.float(), k, k, 1, 2)
+    _close(gw, ew, 1e-3, 1e-2)
+    _close(gb, eb, 1e-3, 1e-2)
+
+
+POOLS = [(4, 28, 28, 6, 2), (4, 24, 24, 32, 2), (2, 10, 10, 16, 2), (2, 5, 5, 3, 2), (2, 9, 9, 8, 3)]
+
+
+@pytest.mark.parametrize("B,H,W,C,P", POOLS)
+def test_maxpool(B, H, W, C, P):
+    # distinct values so the arg-max is unique (tie-breaking is implementation defined)
+    x = (torch.randperm(B * H * W * C, device=dev).float() / (B * H * W * C) - 0.3).view(B, H, W, C)
+    x = x.to(torch.bfloat16)
+    # bf16 rounding can create ties; re-draw until unique within windows is overkill: use few values
+    y = torch.empty(B, H // P, W // P, C, device=dev, dtype=torch.bfloat16)
+    ops.maxpool_fwd(x, y, P)
+    _close(y, ref.maxpool_fwd(x.float(), P), 0, 0)
+    dy = torch.randn(B, H // P, W // P, C, device=dev).to(torch.bfloat16)
+    for relu in (False, True):
+        dx = torch.empty(B, H, W, C, device=dev, dtype=torch.bfloat16)
+        ops.maxpool_bwd(x, dy, dx, P, relu)
+        exp = ref.maxpool_bwd(x.float(), dy.float(), P, relu)
+        # compare sums per window (robust to ties created by bf16 rounding)
+        _close(dx.float().sum(), exp.sum(), 1e-2, 1e-2)
+        assert ((dx.float() != 0).sum() <= (exp != 0).sum() + 8)
+
+
+@pytest.mark.parametrize("B,C", [(4096, 10), (100, 5), (64, 100), (3, 1000)])
+def test_softmax_ce(B, C):
+    z = torch.randn(B, C, device=dev) * 3
+    y = torch.randint(0, C, (B,), device=dev, dtype=torch.int32)
+    dl = torch.empty(B, C, device=dev, dtype=torch.bfloat16)
+    st = torch.zeros(2, device=dev)
+    ops.softmax_ce(z, y, dl, st, 1.0 / B)
+    el, ec, ed = ref.softmax_ce(z, y, 1.0 / B)
+    _close(dl, ed, 1e-2, 1e-4)
+    assert abs(st[0].item() - el.item()) <= 1e-3 * abs(el.item()) + 1e-3
+    assert st[1].item() == ec.item()
+
+
+def test_dropout_matches_cpu_hash():
+    x = torch.randn(3, 1001, device=dev).to(torch.bfloat16)
+    y = torch.empty_like(x)
+    step = torch.tensor(5, dtype=torch.int64, device=dev)
+    ops.dropout(x, y, 0.25, 12345, step=step)
+    seed = 12345 ^ (5 * 0x9E3779B1)
+    exp = ref.dropout(x.cpu().float(), 0.25, seed)
+    _close(y.cpu(), exp, 1e-2, 1e-2)
+    keep = (y != 0).float().mean().item()
+    assert 0.7 < keep < 0.8
+
+
+def test_gather_batch_u8():
+    data = torch.randint(0, 256, (1000, 28, 28, 1), dtype=torch.uint8, device=dev)
+    labels = torch.randint(0, 10, (1000,), dtype=torch.int32, device=dev)
+    idx = torch.randperm(1000, device=dev)[:257]
+    out = torch.empty(257, 28, 28, 1, dtype=torch.bfloat16, device=dev)
+    ol = torch.empty(257, dtype=torch.int32, device=dev)
+    ops.gather_batch(data, labels, idx, out, ol, 1.0 / 255)
+    _close(out, data[idx].float() / 255, 1e-2, 1e-3)
+    assert torch.equal(ol, labels[idx])
+
+
+@pytest.mark.parametrize("M,C,relu", [(4096, 64, True), (1000, 128, False), (512, 6, True)])
+def test_batchnorm(M, C, relu):
+    x = (torch.randn(M, C, device=dev) * 2 + 0.5).to(torch.bfloat16)
+    g = torch.rand(C, device=dev) + 0.5
+    b = torch.randn(C, device=dev)
+    y = torch.empty_like(x)
+    mean = torch.empty(C, device=dev)
+    inv = torch.empty(C, device=dev)
+    rm = torch.zeros(C, device=dev)
+    rv = torch.ones(C, device=dev)
+    ws = torch.empty(2 * C * 256, device=dev)
+    ops.bn_fwd_train(x, y, g, b, mean, inv, rm, rv, ws, 0.1, 1e-5, relu)
+    ey, emu, evar, einv = ref.batchnorm_train(x.float(), g, b, 1e-5)
+    if relu:
+        ey = torch.relu(ey)
+    _close(y, ey)
+    _close(mean, emu, 1e-4, 1e-4)
+    _close(inv, einv, 1e-3, 1e-3)
+    dy = torch.randn(M, C, device=dev).to(torch.bfloat16)
+    dx = torch.empty_like(x)
+    dg = torch.empty(C, device=dev)
+    db = torch.empty(C, device=dev)
+    ops.bn_bwd(x, y, dy, dx, g, b, mean, inv, dg, db, ws, relu)
+    gin = dy.float() * (y.float() > 0) if relu else dy.float()
+    edx, esg, esb = ref.batchnorm_bwd(x.float(), gin, g, emu, einv)
+    _close(dx, edx, 3e-2, 3e-2)
+    _close(dg, esg, 1e-2, 1e-2)
+    _close(db, esb, 1e-3, 1e-3)
