@@ -326,6 +326,126 @@ void bn_bwd_py(torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor
             "bn_bwd");
 }
 
+// geometry: [B, H, W, C, KH, KW, pad, N]
+struct CPIn {
+  const void* x = nullptr;
+  int u8 = 0;
+  const long long* idx = nullptr;
+  long long nrows = 0;
+};
+
+CPIn cp_input(const torch::Tensor& x, const c10::optional<torch::Tensor>& idx, int64_t B, int64_t HWC) {
+  CPIn r;
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "x must be a contiguous GPU tensor");
+  if (idx.has_value() && idx->defined()) {
+    need(*idx, at::kLong, "idx");
+    TORCH_CHECK(idx->numel() >= B, "idx shorter than the batch");
+    TORCH_CHECK(x.scalar_type() == at::kByte || x.scalar_type() == at::kBFloat16, "dataset must be u8 or bf16");
+    TORCH_CHECK(x.dim() >= 1 && x.size(0) > 0 && x.numel() / x.size(0) == HWC, "dataset row size mismatch");
+    TORCH_CHECK(x.scalar_type() == at::kByte, "indexed input must be a uint8 dataset");
+    r.u8 = 1;
+    r.idx = reinterpret_cast<const long long*>(idx->data_ptr<int64_t>());
+    r.nrows = x.size(0);
+  } else {
+    TORCH_CHECK(x.scalar_type() == at::kBFloat16, "x must be bf16");
+    TORCH_CHECK(x.numel() >= B * HWC, "x too small");
+  }
+  r.x = x.data_ptr();
+  return r;
+}
+
+void convpool_fwd_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double scale, torch::Tensor w,
+                     c10::optional<torch::Tensor> bias, torch::Tensor p, c10::optional<torch::Tensor> code,
+                     std::vector<int64_t> geom) {
+  TORCH_CHECK(geom.size() == 8, "geom = [B,H,W,C,KH,KW,pad,N]");
+  const int B = geom[0], H = geom[1], W = geom[2], C = geom[3], KH = geom[4], KW = geom[5], pad = geom[6], N = geom[7];
+  TORCH_CHECK(dfa::convpool_supported(H, W, C, KH, KW, pad, N), "convpool: unsupported geometry");
+  CPIn in = cp_input(x, idx, B, (int64_t)H * W * C);
+  need(w, at::kBFloat16, "w");
+  const int K = KH * KW * C, Kpad = (K + 31) / 32 * 32;
+  TORCH_CHECK(w.numel() >= (int64_t)((N + 15) / 16 * 16) * Kpad && w.size(-1) == Kpad, "w must be [Npad16][Kpad32]");
+  const int OH = H + 2 * pad - KH + 1, OW = W + 2 * pad - KW + 1;
+  const int64_t pn = (int64_t)B * (OH / 2) * (OW / 2) * N;
+  need(p, at::kBFloat16, "p");
+  TORCH_CHECK(p.numel() >= pn, "p too small");
+  uint8_t* cp = nullptr;
+  if (code.has_value() && code->defined()) {
+    need(*code, at::kByte, "code");
+    TORCH_CHECK(code->numel() >= pn, "code too small");
+    cp = code->data_ptr<uint8_t>();
+  }
+  if (bias.has_value() && bias->defined()) {
+    need(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() >= N, "bias too small");
+  }
+  check_hip(dfa::convpool_fwd(in.x, in.u8, in.idx, in.nrows, (float)scale, B, H, W, C, KH, KW, pad, N,
+                              (const dfa::bf16*)w.data_ptr(), cptr<float>(bias), (dfa::bf16*)p.data_ptr(), cp,
+                              cur_stream()),
+            "convpool_fwd");
+}
+
+void convpool_wgrad_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double scale, torch::Tensor dp,
+                       torch::Tensor code, torch::Tensor gw, c10::optional<torch::Tensor> gb, torch::Tensor ws,
+                       std::vector<int64_t> geom) {
+  TORCH_CHECK(geom.size() == 8, "geom = [B,H,W,C,KH,KW,pad,N]");
+  const int B = geom[0], H = geom[1], W = geom[2], C = geom[3], KH = geom[4], KW = geom[5], pad = geom[6], N = geom[7];
+  TORCH_CHECK(dfa::convpool_supported(H, W, C, KH, KW, pad, N), "convpool: unsupported geometry");
+  CPIn in = cp_input(x, idx, B, (int64_t)H * W * C);
+  const int OH = H + 2 * pad - KH + 1, OW = W + 2 * pad - KW + 1;
+  const int64_t pn = (int64_t)B * (OH / 2) * (OW / 2) * N;
+  need(dp, at::kBFloat16, "dp");
+  need(code, at::kByte, "code");
+  TORCH_CHECK(dp.numel() >= pn && code.numel() >= pn, "dp/code too small");
+  need(gw, at::kFloat, "gw");
+  TORCH_CHECK(gw.numel() >= (int64_t)N * KH * KW * C, "gw too small");
+  float* gbp = nullptr;
+  if (gb.has_value() && gb->defined()) {
+    need(*gb, at::kFloat, "gb");
+    TORCH_CHECK(gb->numel() >= N, "gb too small");
+    gbp = gb->data_ptr<float>();
+  }
+  need(ws, at::kFloat, "workspace");
+  check_hip(dfa::convpool_wgrad(in.x, in.u8, in.idx, in.nrows, (float)scale, B, H, W, C, KH, KW, pad, N,
+                                (const dfa::bf16*)dp.data_ptr(), code.data_ptr<uint8_t>(), gw.data_ptr<float>(), gbp,
+                                ws.data_ptr<float>(), (size_t)ws.numel(), cur_stream()),
+            "convpool_wgrad");
+}
+
+void convpool_dgrad_py(torch::Tensor dp, torch::Tensor code, torch::Tensor wt, torch::Tensor dx,
+                       std::vector<int64_t> geom) {
+  TORCH_CHECK(geom.size() == 8, "geom = [B,H,W,C,KH,KW,pad,N]");
+  const int B = geom[0], H = geom[1], W = geom[2], C = geom[3], KH = geom[4], KW = geom[5], pad = geom[6], N = geom[7];
+  TORCH_CHECK(dfa::convpool_supported(H, W, C, KH, KW, pad, N), "convpool: unsupported geometry");
+  const int OH = H + 2 * pad - KH + 1, OW = W + 2 * pad - KW + 1;
+  const int64_t pn = (int64_t)B * (OH / 2) * (OW / 2) * N;
+  need(dp, at::kBFloat16, "dp");
+  need(code, at::kByte, "code");
+  TORCH_CHECK(dp.numel() >= pn && code.numel() >= pn, "dp/code too small");
+  need(wt, at::kBFloat16, "wt");
+  const int K2pad = (KH * KW * N + 31) / 32 * 32;
+  TORCH_CHECK(wt.size(-1) == K2pad && wt.numel() >= (int64_t)((C + 15) / 16 * 16) * K2pad, "wt must be [Cpad16][K2pad]");
+  need(dx, at::kBFloat16, "dx");
+  TORCH_CHECK(dx.numel() >= (int64_t)B * H * W * C, "dx too small");
+  check_hip(dfa::convpool_dgrad((const dfa::bf16*)dp.data_ptr(), code.data_ptr<uint8_t>(),
+                                (const dfa::bf16*)wt.data_ptr(), (dfa::bf16*)dx.data_ptr(), B, H, W, C, KH, KW, pad,
+                                N, cur_stream()),
+            "convpool_dgrad");
+}
+
+void gather_labels_py(torch::Tensor labels, torch::Tensor idx, torch::Tensor out) {
+  need(labels, at::kInt, "labels");
+  need(idx, at::kLong, "idx");
+  need(out, at::kInt, "out");
+  TORCH_CHECK(out.numel() >= idx.numel() && labels.numel() > 0, "gather_labels sizes");
+  check_hip(dfa::gather_labels(labels.data_ptr<int>(), reinterpret_cast<const long long*>(idx.data_ptr<int64_t>()),
+                               out.data_ptr<int>(), (int)idx.numel(), labels.numel(), cur_stream()),
+            "gather_labels");
+}
+
+bool convpool_supported_py(int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t pad, int64_t N) {
+  return dfa::convpool_supported(H, W, C, KH, KW, pad, N);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -347,5 +467,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd_train", &bn_fwd_train_py);
   m.def("bn_fwd_eval", &bn_fwd_eval_py);
   m.def("bn_bwd", &bn_bwd_py);
+  m.def("convpool_fwd", &convpool_fwd_py, "fused conv+bias+relu+maxpool2x2 (pooled map + argmax codes)");
+  m.def("convpool_wgrad", &convpool_wgrad_py, "weight gradient through the fused conv+pool");
+  m.def("convpool_dgrad", &convpool_dgrad_py, "data gradient through the fused conv+pool");
+  m.def("convpool_supported", &convpool_supported_py);
+  m.def("gather_labels", &gather_labels_py);
   dfa::register_runtime(m);
 }

@@ -555,13 +555,7 @@ static hipError_t launch_wgrad_cfg(WgradArgs a, float* workspace, size_t ws_floa
   hipLaunchKernelGGL((igemm_wgrad_kernel<BN, BKO, WN, WK, MODE, DVEC, XVEC>), dim3(tiles * splits), dim3(256), 0,
                      st, a);
   DFA_HIP_CHECK(hipGetLastError());
-  if (splits > 1) {
-    const int total = a.N * Kt;
-    const int blocks = min(cdiv(total, 256), 1024);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, workspace, a.gw, a.gb, a.N, a.K,
-                       Kt, splits, a.scale);
-    DFA_HIP_CHECK(hipGetLastError());
-  }
+  if (splits > 1) DFA_HIP_CHECK(slab_reduce(workspace, a.gw, a.gb, a.N, a.K, Kt, splits, a.scale, st));
   return hipSuccess;
 }
 

@@ -2,6 +2,8 @@
 // units and the PyTorch bindings.
 #pragma once
 #include <hip/hip_runtime_api.h>
+#include <stddef.h>
+#include <stdint.h>
 
 namespace dfa {
 typedef __bf16 bf16;
@@ -56,6 +58,7 @@ hipError_t dropout(const bf16* x, bf16* y, const bf16* mask, long long n, float 
                    const long long* step, hipStream_t st);
 hipError_t gather_batch(const void* data, int data_is_u8, const int* labels, const long long* idx, bf16* out,
                         int* out_labels, int B, int row, float scale, long long nrows, hipStream_t st);
+hipError_t gather_labels(const int* labels, const long long* idx, int* out, int B, long long nrows, hipStream_t st);
 hipError_t add_act(const bf16* a, const bf16* b, bf16* out, long long n, int relu, hipStream_t st);
 hipError_t relu_bwd(const bf16* y, const bf16* dy, bf16* dx, long long n, hipStream_t st);
 hipError_t gap_fwd(const bf16* x, bf16* y, int B, int HW, int C, hipStream_t st);
@@ -72,5 +75,18 @@ hipError_t bn_fwd_eval(const bf16* x, bf16* y, const float* gamma, const float* 
 hipError_t bn_bwd(const bf16* x, const bf16* y, const bf16* dy, bf16* dx, const float* gamma, const float* beta,
                   const float* mean, const float* invstd, float* dgamma, float* dbeta, float* ws, int M, int C,
                   int relu, float gscale, hipStream_t st);
+
+// fused Conv2D(+bias+ReLU)+MaxPool2x2 for small channel counts (convpool.hip)
+bool convpool_supported(int H, int W, int C, int KH, int KW, int pad, int N);
+hipError_t convpool_fwd(const void* x, int x_u8, const long long* idx, long long nrows, float scale, int B, int H,
+                        int W, int C, int KH, int KW, int pad, int N, const bf16* w, const float* bias, bf16* p,
+                        uint8_t* code, hipStream_t st);
+hipError_t convpool_wgrad(const void* x, int x_u8, const long long* idx, long long nrows, float scale, int B, int H,
+                          int W, int C, int KH, int KW, int pad, int N, const bf16* dp, const uint8_t* code,
+                          float* gw, float* gb, float* workspace, size_t ws_floats, hipStream_t st);
+hipError_t convpool_dgrad(const bf16* dp, const uint8_t* code, const bf16* wt, bf16* dx, int B, int H, int W, int C,
+                          int KH, int KW, int pad, int N, hipStream_t st);
+hipError_t slab_reduce(const float* partial, float* gw, float* gb, int N, int K, int Kt, int S, float scale,
+                       hipStream_t st);
 
 }  // namespace dfa

@@ -334,6 +334,12 @@ hipError_t gather_batch(const void* data, int data_is_u8, const int* labels, con
   return hipSuccess;
 }
 
+hipError_t gather_labels(const int* labels, const long long* idx, int* out, int B, long long nrows, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_labels_kernel, dim3(cdiv(B, 256)), dim3(256), 0, st, labels, idx, out, B, nrows);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------
 // Elementwise: out = a + b (+ optional relu), and relu backward dx = dy * (y > 0).
 __global__ void add_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b, bf16* __restrict__ out, long long n8,

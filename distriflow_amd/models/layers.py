@@ -475,3 +475,52 @@ class ResidualBlock(Layer):
 
     def config(self):
         return {"filters": self.filters, "stride": self.stride}
+
+
+class FusedConvPool(Layer):
+    """Conv2D(stride 1, +bias, ReLU) immediately followed by MaxPooling2D(2): one fused kernel each for
+    forward, weight gradient and data gradient (csrc/convpool.hip).  Only the pooled map and a 1-byte
+    argmax/relu' code are materialised; the parameters keep the Conv2D's names (checkpoint-compatible).
+    relu' of this layer's output is applied inside its own backward (code bit 2), so consumers see
+    ``relu = False``."""
+    has_params = True
+
+    def __init__(self, conv: "Conv2D", pool: "MaxPooling2D"):
+        super().__init__(conv.name)
+        self.conv, self.pool = conv, pool
+        self.k, self.pad = conv.k, conv.pad
+        self.use_bias = conv.use_bias
+        self.in_shape = conv.in_shape
+        self.out_shape = pool.out_shape
+        self.relu = False
+
+    def specs(self):
+        self.conv.need_dx = self.need_dx
+        return self.conv.specs()
+
+    def alloc(self, B, device, dtype, ws):
+        self.out = torch.empty((B,) + self.out_shape, device=device, dtype=dtype)
+        self.code = torch.empty((B,) + self.out_shape, device=device, dtype=torch.uint8)
+        if self.need_dx:
+            self.dx = torch.empty((B,) + self.in_shape, device=device, dtype=dtype)
+        self.ws = ws
+
+    def forward(self, x, training):
+        self.x = x
+        st = self.store
+        b = st[f"{self.name}/bias"] if self.use_bias else None
+        ops.convpool_fwd(x, st.weight(f"{self.name}/kernel"), b, self.out, self.code, self.k, self.k, self.pad)
+        return self.out
+
+    def backward(self, dy):
+        st = self.store
+        kn = f"{self.name}/kernel"
+        gb = st.gradient(f"{self.name}/bias") if self.use_bias else None
+        dp = dy.reshape(self.out.shape)
+        ops.convpool_wgrad(self.x, dp, self.code, st.grad_matrix(kn), gb, self.ws.wgrad, self.k, self.k, self.pad)
+        if not self.need_dx:
+            return None
+        ops.convpool_dgrad(dp, self.code, st.weight(kn), st.weight_t(kn), self.dx, self.k, self.k, self.pad)
+        if self.in_relu:
+            ops.relu_bwd(self.x, self.dx, self.dx)
+        return self.dx

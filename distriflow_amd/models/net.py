@@ -15,7 +15,8 @@ from typing import Callable, Optional
 import torch
 
 from .. import ops
-from .layers import Activation, BatchNorm, Dense, Dropout, Flatten, Layer, ResidualBlock
+from .layers import (Activation, BatchNorm, Conv2D, Dense, Dropout, Flatten, FusedConvPool, Layer, MaxPooling2D,
+                     ResidualBlock)
 from .params import ParamStore
 
 
@@ -27,13 +28,15 @@ class Workspace:
 
 class Net:
     def __init__(self, layers: list[Layer], input_shape: tuple, num_classes: Optional[int] = None,
-                 device="cuda", name: str = "model", seed: int = 0, compute_dtype: Optional[torch.dtype] = None):
+                 device="cuda", name: str = "model", seed: int = 0, compute_dtype: Optional[torch.dtype] = None,
+                 fuse: bool = True):
         self.name = name
         self.device = torch.device(device)
         self.input_shape = tuple(input_shape)
         self.layers_all = list(layers)
         self.is_gpu = self.device.type == "cuda"
         self.dtype = compute_dtype or (torch.bfloat16 if self.is_gpu else torch.float32)
+        self.fuse = fuse
         self._plan()
         specs = []
         for l in self.exec_layers:
@@ -82,6 +85,8 @@ class Net:
             i += 1
         if not execd:
             raise ValueError("empty model")
+        if self.fuse:
+            execd = self._fuse_conv_pool(execd)
         last = execd[-1]
         if isinstance(last, Dense):
             if last.activation == "softmax":
@@ -97,6 +102,24 @@ class Net:
             l.in_relu = j > 0 and execd[j - 1].relu
         self.exec_layers = execd
         self.output_shape = shape
+
+    @staticmethod
+    def _fuse_conv_pool(execd):
+        out = []
+        i = 0
+        while i < len(execd):
+            l = execd[i]
+            nxt = execd[i + 1] if i + 1 < len(execd) else None
+            if (isinstance(l, Conv2D) and isinstance(nxt, MaxPooling2D) and l.relu and l.stride == 1 and nxt.p == 2
+                    and l.out_shape[0] % 2 == 0 and l.out_shape[1] % 2 == 0
+                    and ops.convpool_supported(l.in_shape[0], l.in_shape[1], l.in_shape[2], l.k, l.k, l.pad,
+                                               l.filters)):
+                out.append(FusedConvPool(l, nxt))
+                i += 2
+                continue
+            out.append(l)
+            i += 1
+        return out
 
     def _all_leaf_layers(self):
         for l in self.exec_layers:
@@ -123,9 +146,12 @@ class Net:
         self.graphs = {}
 
     # ------------------------------------------------------------------ compute
-    def forward(self, x: torch.Tensor, training: bool = False) -> torch.Tensor:
-        """Returns fp32 logits [B][classes] (a view of an engine buffer)."""
+    def forward(self, x, training: bool = False) -> torch.Tensor:
+        """Returns fp32 logits [B][classes] (a view of an engine buffer).  ``x`` is a tensor or an
+        :class:`ops.GatherRef` (rows of the HBM dataset; fused into the first layer when it can)."""
         self.bind(x.shape[0])
+        if isinstance(x, ops.GatherRef) and not isinstance(self.exec_layers[0], FusedConvPool):
+            x = x.materialise(self.x_buf)
         h = x
         for l in self.exec_layers:
             h = l.forward(h, training)
@@ -148,7 +174,7 @@ class Net:
 
     def compute_gradients(self, x, labels, grad_ready=None):
         """fwd + fused softmax-CE + bwd; returns the device stats tensor [loss_sum, correct]."""
-        if x.dtype != self.dtype:
+        if not isinstance(x, ops.GatherRef) and x.dtype != self.dtype:
             x = x.to(self.dtype)
         if labels.dtype != torch.int32:
             labels = labels.to(torch.int32)
@@ -213,7 +239,11 @@ class Net:
             if isinstance(l, Dense):
                 f = 2 * l.in_features * l.units
                 return f * (3 if l.need_dx else 2)
-            from .layers import Conv2D
+            if isinstance(l, FusedConvPool):
+                c = l.conv
+                OH, OW, N = c.out_shape
+                f = 2 * OH * OW * N * c.k * c.k * c.in_shape[2]
+                return f * (3 if l.need_dx else 2)
             if isinstance(l, Conv2D):
                 OH, OW, N = l.out_shape
                 f = 2 * OH * OW * N * l.k * l.k * l.in_shape[2]

@@ -233,3 +233,81 @@ def bn_bwd(x2d, y2d, dy2d, dx2d, gamma, beta, mean, invstd, dgamma, dbeta, ws, r
         dx2d.copy_(dx)
         dgamma.copy_(sg * gscale)
         dbeta.copy_(sb * gscale)
+
+
+# ----------------------------------------------------------------------------------- fused conv+pool
+class GatherRef:
+    """A batch that has not been materialised: rows ``idx`` of an HBM-resident uint8 dataset, scaled.
+    The first layer reads it directly (fused gather + cast); other consumers call :meth:`materialise`."""
+
+    def __init__(self, data, idx, scale, shape):
+        self.data, self.idx, self.scale = data, idx, scale
+        self.shape = (idx.shape[0],) + tuple(shape)
+        self.device = data.device
+        self.is_cuda = data.is_cuda
+
+    def materialise(self, out):
+        return gather_batch(self.data, None, self.idx, out, None, self.scale)
+
+
+def convpool_supported(H, W, C, KH, KW, pad, N) -> bool:
+    m = native.get(build_if_missing=False)
+    if m is None:
+        return False
+    return bool(m.convpool_supported(H, W, C, KH, KW, pad, N))
+
+
+def _cp_in(x):
+    if isinstance(x, GatherRef):
+        return x.data, x.idx, x.scale
+    return x, None, 1.0
+
+
+def convpool_fwd(x, w, bias, out, code, KH, KW, pad):
+    """Fused conv(stride 1) + bias + ReLU + maxpool 2x2 -> pooled map ``out`` and argmax ``code``."""
+    B, H, W, C = x.shape
+    N = out.shape[-1]
+    if x.is_cuda:
+        src, idx, scale = _cp_in(x)
+        _C().convpool_fwd(src, idx, scale, w, bias, out, code, [B, H, W, C, KH, KW, pad, N])
+    else:
+        if isinstance(x, GatherRef):
+            x = (x.data.index_select(0, x.idx).float() * x.scale).reshape(x.shape)
+        p, c = ref.convpool_fwd(x, w, bias, KH, KW, pad)
+        out.copy_(p)
+        if code is not None:
+            code.copy_(c)
+    return out
+
+
+def convpool_wgrad(x, dp, code, gw, gb, workspace, KH, KW, pad):
+    B, H, W, C = x.shape
+    N = code.shape[-1]
+    if code.is_cuda:
+        src, idx, scale = _cp_in(x)
+        _C().convpool_wgrad(src, idx, scale, dp, code, gw, gb, workspace, [B, H, W, C, KH, KW, pad, N])
+    else:
+        if isinstance(x, GatherRef):
+            x = (x.data.index_select(0, x.idx).float() * x.scale).reshape(x.shape)
+        g, b = ref.convpool_wgrad(x, dp, code, KH, KW, pad)
+        gw.copy_(g.reshape(gw.shape))
+        if gb is not None:
+            gb.copy_(b)
+
+
+def convpool_dgrad(dp, code, w, wt, dx, KH, KW, pad):
+    B, H, W, C = dx.shape
+    N = code.shape[-1]
+    if code.is_cuda:
+        _C().convpool_dgrad(dp, code, wt, dx, [B, H, W, C, KH, KW, pad, N])
+    else:
+        dx.copy_(ref.convpool_dgrad(dp, code, w, dx.shape, KH, KW, pad))
+    return dx
+
+
+def gather_labels(labels, idx, out):
+    if out.is_cuda:
+        _C().gather_labels(labels, idx, out)
+    else:
+        out.copy_(labels.index_select(0, idx))
+    return out

@@ -153,3 +153,40 @@ def batchnorm_bwd(x2d, dy2d, gamma, mean, invstd):
     sg = (g * xh).sum(0)
     dx = gamma * invstd * (g - sb / M - xh * sg / M)
     return dx, sg, sb
+
+
+# ---------------------------------------------------------------- fused conv + relu + maxpool2x2
+def convpool_fwd(x, w2d, bias, KH, KW, pad):
+    """-> (pooled relu output [B,PH,PW,N], code uint8 = argmax(dy*2+dx) | 4*(max>0))."""
+    y = conv_fwd(x, w2d, bias, KH, KW, 1, pad, relu=False)  # [B,OH,OW,N] pre-activation
+    B, OH, OW, N = y.shape
+    win = y.reshape(B, OH // 2, 2, OW // 2, 2, N).permute(0, 1, 3, 5, 2, 4).reshape(B, OH // 2, OW // 2, N, 4)
+    m, am = win.max(dim=-1)  # first maximal index on ties
+    code = (am | ((m > 0).to(am.dtype) << 2)).to(torch.uint8)
+    return torch.relu(m), code
+
+
+def convpool_unpool(dp, code, OH, OW):
+    """Regenerate the full-resolution conv gradient from the pooled gradient and the codes."""
+    B, PH, PW, N = code.shape
+    dp = dp.float().reshape(B, PH, PW, N)
+    c = code.long()
+    sel = torch.nn.functional.one_hot(c & 3, 4).float() * ((c & 4) > 0).float().unsqueeze(-1)  # [B,PH,PW,N,4]
+    full = (sel * dp.unsqueeze(-1)).reshape(B, PH, PW, N, 2, 2).permute(0, 1, 4, 2, 5, 3).reshape(B, 2 * PH, 2 * PW, N)
+    out = torch.zeros(B, OH, OW, N, dtype=full.dtype)
+    out[:, : 2 * PH, : 2 * PW] = full
+    return out
+
+
+def convpool_wgrad(x, dp, code, KH, KW, pad):
+    B, H, W, C = x.shape
+    OH, OW = H + 2 * pad - KH + 1, W + 2 * pad - KW + 1
+    dconv = convpool_unpool(dp, code, OH, OW)
+    return conv_wgrad(dconv, x, KH, KW, 1, pad, True)
+
+
+def convpool_dgrad(dp, code, w2d, in_shape, KH, KW, pad):
+    B, H, W, C = in_shape
+    OH, OW = H + 2 * pad - KH + 1, W + 2 * pad - KW + 1
+    dconv = convpool_unpool(dp, code, OH, OW)
+    return conv_dgrad(dconv, w2d, in_shape, KH, KW, 1, pad, None)

@@ -112,11 +112,18 @@ class DataParallelTrainer:
         net = self.net
         net.bind(batch_size)
         self.idx = torch.zeros(batch_size, dtype=torch.int64, device=net.device)
-        self.xb = net.x_buf
         self.yb = net.y_buf
+        if data.dtype == torch.uint8:
+            # the first layer reads dataset rows through the index vector (fused gather + cast)
+            self.xb = ops.GatherRef(data, self.idx, scale, net.input_shape)
+        else:
+            self.xb = net.x_buf
 
     def _gather(self):
-        ops.gather_batch(self.data, self.labels, self.idx, self.xb, self.yb, self.scale)
+        if isinstance(self.xb, ops.GatherRef):
+            ops.gather_labels(self.labels, self.idx, self.yb)
+        else:
+            ops.gather_batch(self.data, self.labels, self.idx, self.xb, self.yb, self.scale)
 
     def _capture(self):
         net = self.net

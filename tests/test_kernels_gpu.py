@@ -241,3 +241,58 @@ def test_batchnorm(M, C, relu):
     _close(dx, edx, 3e-2, 3e-2)
     _close(dg, esg, 1e-2, 1e-2)
     _close(db, esb, 1e-3, 1e-3)
+
+
+CONVPOOL = [  # B, H, W, C, N, k, pad
+    (16, 28, 28, 1, 6, 5, 2),    # LeNet conv1 ('same')
+    (16, 14, 14, 6, 16, 5, 0),   # LeNet conv2
+    (5, 12, 12, 3, 20, 3, 1),    # odd batch, N > 16, partial window tiles
+    (3, 10, 10, 16, 8, 3, 0),
+]
+
+
+@pytest.mark.parametrize("B,H,W,C,N,k,p", CONVPOOL)
+def test_convpool_fwd_wgrad_dgrad(B, H, W, C, N, k, p):
+    from distriflow_amd import ops as O
+
+    x = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, k * k * C, device=dev) / (k * k * C) ** 0.5).to(torch.bfloat16).float()
+    b = torch.randn(N, device=dev) * 0.1
+    OH, OW = H + 2 * p - k + 1, W + 2 * p - k + 1
+    out = torch.empty(B, OH // 2, OW // 2, N, device=dev, dtype=torch.bfloat16)
+    code = torch.empty(B, OH // 2, OW // 2, N, device=dev, dtype=torch.uint8)
+    O.convpool_fwd(x, _pad_w(w), b, out, code, k, k, p)
+    ep, ec = ref.convpool_fwd(x.float().cpu(), w.cpu(), b.cpu(), k, k, p)
+    _close(out.cpu(), ep)
+    agree = (code.cpu() == ec).float().mean().item()
+    assert agree > 0.97, agree  # near-ties may resolve differently under bf16 vs fp32 accumulation order
+    # backward uses the kernel's own codes so both sides see the same routing
+    dp = torch.randn(B, OH // 2, OW // 2, N, device=dev).to(torch.bfloat16)
+    gw = torch.empty(N, k * k * C, device=dev)
+    gb = torch.empty(N, device=dev)
+    ws = torch.empty(1 << 22, device=dev)
+    O.convpool_wgrad(x, dp, code, gw, gb, ws, k, k, p)
+    ew, eb = ref.convpool_wgrad(x.float().cpu(), dp.float().cpu(), code.cpu(), k, k, p)
+    _close(gw.cpu(), ew, 1e-3, 1e-3)
+    _close(gb.cpu(), eb, 1e-3, 1e-3)
+    if C <= 16:
+        dx = torch.empty(B, H, W, C, device=dev, dtype=torch.bfloat16)
+        O.convpool_dgrad(dp, code, None, _pad_wt(w, N, k * k, C), dx, k, k, p)
+        edx = ref.convpool_dgrad(dp.float().cpu(), code.cpu(), w.cpu(), (B, H, W, C), k, k, p)
+        _close(dx.cpu(), edx)
+
+
+def test_convpool_fused_gather_u8():
+    from distriflow_amd import ops as O
+
+    data = torch.randint(0, 256, (300, 28, 28, 1), dtype=torch.uint8, device=dev)
+    idx = torch.randperm(300, device=dev)[:64]
+    w = (torch.randn(6, 25, device=dev) / 5).to(torch.bfloat16).float()
+    b = torch.zeros(6, device=dev)
+    out = torch.empty(64, 14, 14, 6, device=dev, dtype=torch.bfloat16)
+    code = torch.empty(64, 14, 14, 6, device=dev, dtype=torch.uint8)
+    O.convpool_fwd(O.GatherRef(data, idx, 1 / 255, (28, 28, 1)), _pad_w(w), b, out, code, 5, 5, 2)
+    xb = (data[idx].float() / 255).to(torch.bfloat16)
+    out2 = torch.empty_like(out)
+    O.convpool_fwd(xb, _pad_w(w), b, out2, None, 5, 5, 2)
+    assert torch.equal(out, out2)
