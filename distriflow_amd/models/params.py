@@ -207,7 +207,11 @@ class ParamStore:
                                        self.momentum, self.wbf, self.hyper, True)
             return
         lr, mom, wd, gs, nest = self._hyper_host
-        g = self.grad * gs
+        if not hasattr(self, "_valid"):
+            self._valid = torch.zeros(self.total, dtype=torch.bool, device=self.device)
+            for s in self.specs:
+                self._valid[self.offsets[s.name]: self.offsets[s.name] + s.numel] = True
+        g = torch.where(self._valid, self.grad * gs, torch.zeros((), device=self.device))
         if wd:
             g = g + wd * self.master
         if mom:

@@ -1,0 +1,79 @@
+"""DistriDataset FCFS semantics (reference dataset.ts) on the native dispenser."""
+import torch
+
+from distriflow_amd.data.dataset import DistriDataset, batch_to_data_msg
+from distriflow_amd.data.mnist import load_mnist, one_hot, write_idx
+from distriflow_amd.data.synthetic import non_iid_shards, synthetic_mnist
+
+
+def _ds(n=100, bs=32, epochs=2, small=False, shuffle=False):
+    x = torch.arange(n, dtype=torch.float32).view(n, 1)
+    y = torch.arange(n)
+    return DistriDataset(x, y, {"batchSize": bs, "epochs": epochs, "smallLastBatch": small}, shuffle=shuffle)
+
+
+def test_sequential_dispatch_and_epochs():
+    d = _ds(96, 32, 2)
+    assert d.batches == 3
+    seen = []
+    while True:
+        b, done = d.next()
+        if done:
+            break
+        seen.append((b.epoch, b.batch))
+        assert b.x.shape[0] == 32 and float(b.x[0]) == b.batch * 32
+        d.complete_batch(b.batch)
+    assert seen == [(0, 0), (0, 1), (0, 2), (1, 0), (1, 1), (1, 2)]
+
+
+def test_redispatch_of_unacknowledged_batches():
+    d = _ds(96, 32, 1)
+    got = [d.next()[0].batch for _ in range(3)]
+    assert got == [0, 1, 2]
+    d.complete_batch(0)
+    d.complete_batch(2)
+    b, _ = d.next()           # cursor ran off the end: batch 1 (never completed) is re-dispatched
+    assert b.batch == 1
+    d.complete_batch(1)
+    assert d.next() == (None, True)
+
+
+def test_small_last_batch_and_drop():
+    assert _ds(100, 32, 1, small=False).batches == 3
+    d = _ds(100, 32, 1, small=True)
+    assert d.batches == 4
+    for _ in range(3):
+        d.next()
+    b, _ = d.next()
+    assert b.batch == 3 and b.x.shape[0] == 4
+
+
+def test_preprocess_and_state_roundtrip():
+    d = _ds(64, 16, 3, shuffle=True)
+    d.add_preprocess_callback(lambda b: (setattr(b, "x", b.x * 2) or b))
+    b, _ = d.next()
+    assert torch.equal(b.x, d.x.index_select(0, b.indices) * 2)
+    d.complete_batch(b.batch)
+    st = d.state()
+    e = _ds(64, 16, 3, shuffle=True)
+    e.load_state(st)
+    assert e.epoch == d.epoch and e.remaining == d.remaining
+    assert e.next()[0].batch == d.next()[0].batch
+    msg = batch_to_data_msg(b)
+    assert msg.x.shape == list(b.x.shape)
+
+
+def test_idx_round_trip(tmp_path):
+    x, y = synthetic_mnist(50)
+    write_idx(str(tmp_path / "train-images-idx3-ubyte"), str(tmp_path / "train-labels-idx1-ubyte"), x, y)
+    x2, y2 = load_mnist(str(tmp_path), "train")
+    assert torch.equal(x2, x) and torch.equal(y2, y)
+    assert one_hot(y2[:3]).shape == (3, 10)
+
+
+def test_non_iid_shards_cover_each_example_once():
+    _, y = synthetic_mnist(1000)
+    shards = non_iid_shards(y, 8, 2)
+    allidx = torch.cat(shards).sort().values
+    assert torch.equal(allidx, torch.arange(1000))
+    assert all(len(torch.unique(y[s])) <= 4 for s in shards)
