@@ -310,7 +310,8 @@ class AsynchronousSGDServer(AbstractServer):
         self.updating = False
 
     def all_done(self) -> bool:
-        return bool(self.clients) and set(self.clients) <= self.finished_clients
+        """Dataset exhausted and every connected worker has been told DONE (or has left)."""
+        return self.num_updates > 0 and self.dataset.done and set(self.clients) <= self.finished_clients
 
 
 class FedAvgServer(AbstractServer):

@@ -1,0 +1,60 @@
+"""Parameter-server roles with the GPU engine (HIP kernels) on one MI355X: server and workers share the
+device through the in-process transport (multi-rank RCCL needs >1 GPU; the gloo tests cover the
+torch.distributed transport)."""
+import threading
+
+import pytest
+import torch
+
+from distriflow_amd.data.dataset import DistriDataset
+from distriflow_amd.data.synthetic import synthetic_mnist
+from distriflow_amd.models.distri_model import ClientModel, InMemoryServerModel
+from distriflow_amd.parallel.server import AsynchronousSGDServer, FederatedServer
+from distriflow_amd.parallel.transport import LocalHub
+from distriflow_amd.parallel.worker import AsynchronousSGDClient, FederatedClient
+
+pytestmark = pytest.mark.gpu
+
+
+def test_async_sgd_on_gpu_learns():
+    x, y = synthetic_mnist(4096, seed=3, device="cuda")
+    hub = LocalHub(3)
+    ds = DistriDataset(x, y, {"batchSize": 256, "epochs": 3})
+    smodel = InMemoryServerModel("lenet5", {"learningRate": 0.05}, device="cuda")
+    server = AsynchronousSGDServer(hub.endpoint(0), smodel, ds,
+                                   {"modelDir": False, "serverHyperparams": {"maximumStaleness": 2}})
+    server.setup()
+    x_eval = x[:1024].float() / 255
+    loss0 = smodel.evaluate(x_eval, y[:1024])
+    th = threading.Thread(target=server.serve, kwargs={"until": server.all_done, "timeout": 120}, daemon=True)
+    th.start()
+    ws = [AsynchronousSGDClient(hub.endpoint(r, [0]), ClientModel("lenet5", device="cuda"), {"clientId": f"g{r}"},
+                                data=x, labels=y, data_scale=1 / 255) for r in (1, 2)]
+    ts = [threading.Thread(target=lambda w=w: (w.setup(), w.run(timeout=120)), daemon=True) for w in ws]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(150)
+    th.join(20)
+    assert ds.done
+    loss1 = smodel.evaluate(x_eval, y[:1024])
+    assert loss1[1] > loss0[1] or loss1[0] < loss0[0]
+
+
+def test_fedsgd_on_gpu():
+    x, y = synthetic_mnist(1024, seed=4, device="cuda")
+    hub = LocalHub(2)
+    smodel = InMemoryServerModel("mlp_mnist", {"learningRate": 0.1}, device="cuda")
+    server = FederatedServer(hub.endpoint(0), smodel, {"modelDir": False, "serverHyperparams": {"minUpdatesPerVersion": 2},
+                                                       "clientHyperparams": {"examplesPerUpdate": 64}})
+    server.setup()
+    th = threading.Thread(target=server.serve, kwargs={"timeout": 60}, daemon=True)
+    th.start()
+    c = FederatedClient(hub.endpoint(1), ClientModel("mlp_mnist", device="cuda"))
+    c.setup()
+    c.distributed_update(x.float() / 255, y)
+    c.poll(0.5)
+    assert server.version_id >= 4
+    torch.testing.assert_close(c.model.get_flat(), smodel.get_flat())
+    server.stop()
+    th.join(5)
