@@ -362,8 +362,11 @@ void convpool_fwd_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double s
   TORCH_CHECK(dfa::convpool_supported(H, W, C, KH, KW, pad, N), "convpool: unsupported geometry");
   CPIn in = cp_input(x, idx, B, (int64_t)H * W * C);
   need(w, at::kBFloat16, "w");
-  const int K = KH * KW * C, Kpad = (K + 31) / 32 * 32;
-  TORCH_CHECK(w.numel() >= (int64_t)((N + 15) / 16 * 16) * Kpad && w.size(-1) == Kpad, "w must be [Npad16][Kpad32]");
+  // row-segment layout [Npad16][Kpad2] (ParamSpec.row_pad / row_cp, convpool_fwd_layout)
+  int Cp = 0, Kpad2 = 0;
+  dfa::convpool_fwd_layout(H, W, C, KH, KW, pad, N, &Cp, &Kpad2);
+  TORCH_CHECK(w.numel() >= (int64_t)((N + 15) / 16 * 16) * Kpad2 && w.size(-1) == Kpad2,
+              "w must be the row-segment layout [Npad16][", Kpad2, "] (channel stride ", Cp, ")");
   const int OH = H + 2 * pad - KH + 1, OW = W + 2 * pad - KW + 1;
   const int64_t pn = (int64_t)B * (OH / 2) * (OW / 2) * N;
   need(p, at::kBFloat16, "p");
@@ -442,6 +445,109 @@ void gather_labels_py(torch::Tensor labels, torch::Tensor idx, torch::Tensor out
             "gather_labels");
 }
 
+// Fused dense head: per layer l tensors (w, wt?, b?, gw, gb?, hT?, dzT) and dims (K, N).
+void head_train_py(std::vector<torch::Tensor> w, std::vector<c10::optional<torch::Tensor>> wt,
+                   std::vector<c10::optional<torch::Tensor>> b, std::vector<torch::Tensor> gw,
+                   std::vector<c10::optional<torch::Tensor>> gb, std::vector<c10::optional<torch::Tensor>> hT,
+                   std::vector<torch::Tensor> dzT, std::vector<int64_t> K, std::vector<int64_t> N, torch::Tensor x,
+                   bool x_relu, torch::Tensor xT, c10::optional<torch::Tensor> dx,
+                   c10::optional<torch::Tensor> logits, torch::Tensor labels, c10::optional<torch::Tensor> idx,
+                   double grad_scale, torch::Tensor loss_part, torch::Tensor stats) {
+  const int nl = (int)w.size();
+  TORCH_CHECK(nl >= 1 && nl <= dfa::kHeadMaxLayers, "head: 1..", dfa::kHeadMaxLayers, " layers");
+  TORCH_CHECK((int)wt.size() == nl && (int)b.size() == nl && (int)gw.size() == nl && (int)gb.size() == nl &&
+                  (int)hT.size() == nl && (int)dzT.size() == nl && (int)K.size() == nl && (int)N.size() == nl,
+              "head: per-layer lists must have equal length");
+  need(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() >= 2, "x must be [B, ...]");
+  const int64_t B = x.size(0);
+  const int64_t ldt = (B + 31) / 32 * 32;
+  TORCH_CHECK(x.numel() == B * K[0], "x must have B*K0 elements");
+  TORCH_CHECK(K[0] % 8 == 0 && K[0] <= 1024, "head: K0 must be a multiple of 8 and <= 1024");
+  TORCH_CHECK(N[nl - 1] <= 16, "head: at most 16 classes");
+  dfa::HeadArgs a{};
+  a.nl = nl;
+  a.B = (int)B;
+  a.ldt = (int)ldt;
+  a.x_relu = x_relu ? 1 : 0;
+  for (int l = 0; l < nl; ++l) {
+    dfa::HeadLayer& L = a.L[l];
+    L.K = (int)K[l];
+    L.N = (int)N[l];
+    TORCH_CHECK(L.N <= 256 || l == 0, "head: hidden widths must be <= 256");
+    TORCH_CHECK(l == 0 || K[l] == N[l - 1], "head: layer ", l, " input width must equal layer ", l - 1, " width");
+    L.Kpad = (L.K + 31) / 32 * 32;
+    L.ldwt = (L.N + 31) / 32 * 32;
+    need(w[l], at::kBFloat16, "w");
+    TORCH_CHECK(w[l].numel() >= (int64_t)((L.N + 15) / 16 * 16) * L.Kpad && w[l].size(-1) == L.Kpad,
+                "head: w must be [Npad16][Kpad32]");
+    L.w = reinterpret_cast<const dfa::bf16*>(w[l].data_ptr());
+    const bool need_wt = l > 0 || (dx.has_value() && dx->defined());
+    if (need_wt) {
+      TORCH_CHECK(wt[l].has_value() && wt[l]->defined(), "head: dgrad-layout weights required for layer ", l);
+      need(*wt[l], at::kBFloat16, "wt");
+      TORCH_CHECK(wt[l]->size(-1) == L.ldwt && wt[l]->numel() >= (int64_t)((L.K + 15) / 16 * 16) * L.ldwt,
+                  "head: wt must be [Kpad16][pad32(N)]");
+      L.wt = reinterpret_cast<const dfa::bf16*>(wt[l]->data_ptr());
+    }
+    if (b[l].has_value() && b[l]->defined()) {
+      need(*b[l], at::kFloat, "b");
+      TORCH_CHECK(b[l]->numel() >= L.N, "head: bias too small");
+      L.b = b[l]->data_ptr<float>();
+    }
+    need(gw[l], at::kFloat, "gw");
+    TORCH_CHECK(gw[l].numel() >= (int64_t)L.N * L.K, "head: gw too small");
+    L.gw = gw[l].data_ptr<float>();
+    if (gb[l].has_value() && gb[l]->defined()) {
+      need(*gb[l], at::kFloat, "gb");
+      TORCH_CHECK(gb[l]->numel() >= L.N, "head: gb too small");
+      L.gb = gb[l]->data_ptr<float>();
+    }
+    if (l < nl - 1) {
+      TORCH_CHECK(hT[l].has_value() && hT[l]->defined(), "head: hT required for hidden layers");
+      need(*hT[l], at::kBFloat16, "hT");
+      TORCH_CHECK(hT[l]->numel() >= (int64_t)L.N * ldt, "head: hT must be [N][round32(B)]");
+      L.hT = reinterpret_cast<dfa::bf16*>(hT[l]->data_ptr());
+    }
+    need(dzT[l], at::kBFloat16, "dzT");
+    TORCH_CHECK(dzT[l].numel() >= (int64_t)L.N * ldt, "head: dzT must be [N][round32(B)]");
+    L.dzT = reinterpret_cast<dfa::bf16*>(dzT[l].data_ptr());
+  }
+  a.x = reinterpret_cast<const dfa::bf16*>(x.data_ptr());
+  need(xT, at::kBFloat16, "xT");
+  TORCH_CHECK(xT.numel() >= K[0] * ldt, "head: xT must be [K0][round32(B)]");
+  a.xT = reinterpret_cast<dfa::bf16*>(xT.data_ptr());
+  if (dx.has_value() && dx->defined()) {
+    need(*dx, at::kBFloat16, "dx");
+    TORCH_CHECK(dx->numel() >= B * K[0], "head: dx too small");
+    a.dx = reinterpret_cast<dfa::bf16*>(dx->data_ptr());
+  }
+  if (logits.has_value() && logits->defined()) {
+    need(*logits, at::kFloat, "logits");
+    TORCH_CHECK(logits->numel() >= B * N[nl - 1], "head: logits too small");
+    a.logits = logits->data_ptr<float>();
+  }
+  need(labels, at::kInt, "labels");
+  a.labels = labels.data_ptr<int>();
+  a.nrows = labels.numel();
+  if (idx.has_value() && idx->defined()) {
+    need(*idx, at::kLong, "idx");
+    TORCH_CHECK(idx->numel() >= B, "head: idx too small");
+    a.idx = reinterpret_cast<const long long*>(idx->data_ptr());
+  } else {
+    TORCH_CHECK(labels.numel() >= B, "head: labels too small");
+  }
+  a.grad_scale = (float)grad_scale;
+  need(loss_part, at::kFloat, "loss_part");
+  TORCH_CHECK(loss_part.numel() >= 2 * ((B + 15) / 16), "head: loss_part must hold 2 floats per 16 rows");
+  a.loss_part = loss_part.data_ptr<float>();
+  need(stats, at::kFloat, "stats");
+  TORCH_CHECK(stats.numel() >= 2, "head: stats must hold 2 floats");
+  a.stats = stats.data_ptr<float>();
+  TORCH_CHECK(dfa::head_train_lds(a) <= 160 * 1024, "head: LDS footprint too large");
+  check_hip(dfa::head_train(a, cur_stream()), "head_train");
+}
+
 bool convpool_supported_py(int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t pad, int64_t N) {
   return dfa::convpool_supported(H, W, C, KH, KW, pad, N);
 }
@@ -470,7 +576,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("convpool_fwd", &convpool_fwd_py, "fused conv+bias+relu+maxpool2x2 (pooled map + argmax codes)");
   m.def("convpool_wgrad", &convpool_wgrad_py, "weight gradient through the fused conv+pool");
   m.def("convpool_dgrad", &convpool_dgrad_py, "data gradient through the fused conv+pool");
+  m.def("convpool_set_debug", &dfa::convpool_set_debug, "profiling aid: skip kernel phases (bit mask)");
+  m.def("convpool_fwd_layout", [](int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t pad, int64_t N) {
+    int Cp = 0, Kpad2 = 0;
+    dfa::convpool_fwd_layout(H, W, C, KH, KW, pad, N, &Cp, &Kpad2);
+    return std::make_tuple(Cp, Kpad2);
+  }, "forward weight layout of the fused conv+pool kernel: (channel stride Cp, row length Kpad2)");
   m.def("convpool_supported", &convpool_supported_py);
+  m.def("head_train", &head_train_py, "fused dense head: forward + softmax-CE + backward (2 launches)");
   m.def("gather_labels", &gather_labels_py);
   dfa::register_runtime(m);
 }

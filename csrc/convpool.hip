@@ -29,13 +29,27 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <array>
+#include <map>
+#include <mutex>
+#include <numeric>
+
 namespace dfa {
 
 struct CPGeom {
   int B, H, W, C, KH, KW, pad, N, OH, OW, PH, PW, K, Kpad;
   int Hp, Wp, img_elems;  // padded input image in LDS
   int imgs;               // images per workgroup
+  // forward row-segment layout: k = ky*RLp + (kx*C + c); every 8-slot k group is 8 CONSECUTIVE
+  // elements of one padded image row, read with one 16-byte LDS load from one of S shifted copies
+  int Cp;                  // LDS channel stride of the forward image (>= C, zero-filled channels)
+  int RLp, chunks, Kpad2;  // RLp = round8(KW*Cp), chunks = RLp/8, Kpad2 = round32(KH*RLp)
+  int G, S, RowP, ystr, xs_img;  // G = gcd(C,8): copy ci is shifted by ci*G elements, S = 8/G copies
+  int dbg;                        // profiling aid: bit0 skip staging, bit1 skip shift build, bit2 skip MFMA, bit3 skip stores
 };
+
+static int g_cp_debug = 0;
+void convpool_set_debug(int mask) { g_cp_debug = mask; }
 
 __device__ __forceinline__ long long cp_clamp(long long r, long long n) { return r < 0 ? 0 : (r >= n ? n - 1 : r); }
 
@@ -50,7 +64,8 @@ __device__ __forceinline__ void lds_zero(bf16* p, int elems) {
 // dataset rows gathered through idx.  One thread per image row segment keeps the divisions out of
 // the element loop.
 __device__ __forceinline__ void stage_images(bf16* xs, const CPGeom& g, const void* x, int x_u8, const long long* idx,
-                                             long long nrows, float scale, int b0, int nimg) {
+                                             long long nrows, float scale, int b0, int nimg, int img_stride,
+                                             int row_stride, int cp) {
   const int WC = g.W * g.C;
   const int HWC = g.H * WC;
   const int rows = nimg * g.H;
@@ -63,14 +78,87 @@ __device__ __forceinline__ void stage_images(bf16* xs, const CPGeom& g, const vo
   for (int r = r0; r < rows; r += rpb) {
     const int i = r / g.H;
     const int y = r - i * g.H;
-    bf16* dst = xs + i * g.img_elems + ((y + g.pad) * g.Wp + g.pad) * g.C;
-    if (x_u8) {
-      const uint8_t* src = reinterpret_cast<const uint8_t*>(x) + cp_clamp(idx[b0 + i], nrows) * HWC + y * WC;
-      for (int c = c0; c < WC; c += tpr) dst[c] = f2bf((float)src[c] * scale);
-    } else {
-      const bf16* src = reinterpret_cast<const bf16*>(x) + ((long long)(b0 + i) * HWC + y * WC);
-      for (int c = c0; c < WC; c += tpr) dst[c] = src[c];
+    bf16* dst = xs + i * img_stride + (y + g.pad) * row_stride + g.pad * cp;
+    for (int c = c0; c < WC; c += tpr) {
+      const int d = cp == g.C ? c : (c / g.C) * cp + c % g.C;
+      if (x_u8) {
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(x) + cp_clamp(idx[b0 + i], nrows) * HWC + y * WC;
+        dst[d] = f2bf((float)src[c] * scale);
+      } else {
+        const bf16* src = reinterpret_cast<const bf16*>(x) + ((long long)(b0 + i) * HWC + y * WC);
+        dst[d] = src[c];
+      }
     }
+  }
+}
+
+// ---- Register-staged copies.  A plain "for (e = tid; e < n; e += 256) lds[..] = global[..]" loop
+// is a chain of dependent global-load latencies (one round trip per iteration).  Instead every thread
+// owns up to CHM fixed chunks of 4 consecutive elements (positions relative to the group start are
+// the same for every group, so the index math is done once per workgroup), issues ALL loads of a group
+// back to back, then stores.  Requires W*C % 4 == 0 and 4-element-aligned sources (host checks).
+template <int CHM>
+struct ImgPlan {
+  int img[CHM];    // image slot within the group, or a large sentinel
+  int soff[CHM];   // element offset inside the source image
+  int doff[CHM];   // element offset inside the LDS image slot
+  int split[CHM];  // elements of the chunk before the next pixel (a chunk spans at most 2 pixels)
+};
+
+template <int CHM>
+__device__ __forceinline__ void make_img_plan(ImgPlan<CHM>& pl, const CPGeom& g, int row_stride, int cp) {
+  const int WC = g.W * g.C, cpr = WC / 4, cpi = g.H * cpr;
+#pragma unroll
+  for (int j = 0; j < CHM; ++j) {
+    const int c = threadIdx.x + 256 * j;
+    const int i = c / cpi, r = c - (c / cpi) * cpi;
+    const int y = r / cpr, x4 = 4 * (r - (r / cpr) * cpr);
+    const int px = x4 / g.C, ch = x4 - px * g.C;
+    pl.img[j] = c < g.imgs * cpi ? i : (1 << 20);
+    pl.soff[j] = y * WC + x4;
+    pl.doff[j] = (y + g.pad) * row_stride + (g.pad + px) * cp + ch;
+    pl.split[j] = cp == g.C ? 4 : g.C - ch;
+  }
+}
+
+template <int CHM>
+__device__ __forceinline__ void stage_plan(bf16* xs, int img_stride, const ImgPlan<CHM>& pl, const CPGeom& g,
+                                           const void* x, int x_u8, const long long* idx, long long nrows,
+                                           float scale, int b0, int nimg, int cp) {
+  const long long HWC = (long long)g.H * g.W * g.C;
+  const int gap = cp - g.C;
+  if (x_u8) {
+    uint32_t v[CHM];
+#pragma unroll
+    for (int j = 0; j < CHM; ++j)
+      if (pl.img[j] < nimg) {
+        const long long r = cp_clamp(idx[b0 + pl.img[j]], nrows);
+        v[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(x) + r * HWC + pl.soff[j]);
+      }
+#pragma unroll
+    for (int j = 0; j < CHM; ++j)
+      if (pl.img[j] < nimg) {
+        bf16* d = xs + pl.img[j] * img_stride + pl.doff[j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          d[k + (((pl.split[j] - k - 1) >> 31) & gap)] = f2bf((float)((v[j] >> (8 * k)) & 255u) * scale);
+      }
+  } else {
+    uint2 v[CHM];
+#pragma unroll
+    for (int j = 0; j < CHM; ++j)
+      if (pl.img[j] < nimg)
+        v[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(x) + (b0 + pl.img[j]) * HWC + pl.soff[j]);
+#pragma unroll
+    for (int j = 0; j < CHM; ++j)
+      if (pl.img[j] < nimg) {
+        uint16_t* d = reinterpret_cast<uint16_t*>(xs + pl.img[j] * img_stride + pl.doff[j]);
+        const int sp = pl.split[j];
+        d[0] = (uint16_t)(v[j].x & 0xffffu);
+        d[1 + (((sp - 2) >> 31) & gap)] = (uint16_t)(v[j].x >> 16);
+        d[2 + (((sp - 3) >> 31) & gap)] = (uint16_t)(v[j].y & 0xffffu);
+        d[3 + (((sp - 4) >> 31) & gap)] = (uint16_t)(v[j].y >> 16);
+      }
   }
 }
 
@@ -89,36 +177,63 @@ __device__ __forceinline__ int window_pixel_off(const CPGeom& g, int wg, int j, 
 }
 
 // ------------------------------------------------------------------------------------------------
-template <int NT, int NKMAX>
-__global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, const void* x, int x_u8, const long long* idx,
-                                                           long long nrows, float scale, const bf16* __restrict__ w,
-                                                           const float* __restrict__ bias, bf16* __restrict__ p,
-                                                           uint8_t* __restrict__ code) {
+// Forward.  LDS image layout per row y: S copies of the padded row, copy ci shifted left by sh = ci*G
+// elements (copy[i] = row[i + sh]).  The 8 k-slots (kx*C + c = 8j..8j+7 of kernel row ky) of output
+// pixel (oy, ox) are row[oy+ky][ox*C + 8j + e], e < 8 = copy_sh[(ox*C - sh) + 8j + e] with
+// sh = (ox*C) & 7: 16-byte aligned, so each A fragment is ONE ds_read_b128 at
+// pixel_base(tile, row) + koff(ky, j) — both table lookups.
+//
+// Latency, not issue, bounds these small convolutions, so every wave keeps U tiles in flight: all
+// U*NK fragment loads are issued back to back (no data-dependent branches between them: NK is the
+// exact k-step count or zero-padded), then the U*NK MFMAs, then the U epilogues.
+template <int NK>
+struct FwdU {
+  static constexpr int value = NK <= 2 ? 4 : (NK <= 5 ? 2 : 1);
+};
+
+template <int NT, int NK, int CHM>
+__global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, const void* x, int x_u8,
+                                                           const long long* idx, long long nrows, float scale,
+                                                           const bf16* __restrict__ w, const float* __restrict__ bias,
+                                                           bf16* __restrict__ p, uint8_t* __restrict__ code) {
+  constexpr int U = FwdU<NK>::value;
+  constexpr int BT = 8;  // shifted-copy build tasks per thread held in registers
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int npool = g.PH * g.PW;
   const int tpi = (npool + 3) / 4;  // MFMA tiles (4 windows) per image
-  int* ttab = reinterpret_cast<int*>(smem);                                          // [tpi*16]
-  int* klut = ttab + round_up(tpi * 16, 4);                                          // [Kpad]
-  bf16* xs = reinterpret_cast<bf16*>(smem + round_up((round_up(tpi * 16, 4) + g.Kpad) * 4, 16));
+  const int gtiles = g.imgs * tpi;  // tiles per group
+  int* ttab = reinterpret_cast<int*>(smem);                      // [gtiles*16] LDS offset of each tile row
+  int2* wtab = reinterpret_cast<int2*>(ttab + gtiles * 16);      // [gtiles] (first pooled index, valid windows)
+  bf16* xs = reinterpret_cast<bf16*>(smem + round_up(gtiles * 16 * 4 + gtiles * 8, 16));  // [imgs][Hp][S][RowP]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (g.dbg & 16) return;
 
-  // ---- once per workgroup: address tables, zero-bordered image slots, register-resident weights
-  for (int e = tid; e < tpi * 16; e += 256) {
-    const int row = e & 15;
-    ttab[e] = window_pixel_off(g, (e >> 4) * 4 + (row >> 2), row & 3, g.Wp, g.C);
+  // ---- once per workgroup: tables, zero-bordered image slots, register-resident weights
+  for (int e = tid; e < gtiles * 16; e += 256) {
+    const int T = e >> 4, row = e & 15;
+    const int i = T / tpi, tw = T - (T / tpi) * tpi;
+    const int wg = tw * 4 + (row >> 2), j = row & 3;
+    int v = i * g.xs_img;
+    if (wg < npool) {
+      const int py = wg / g.PW, px = wg - py * g.PW;
+      const int oy = 2 * py + (j >> 1), ox = 2 * px + (j & 1);
+      const int t0 = ox * g.Cp, sh = t0 & 7;
+      v += oy * g.ystr + (sh / g.G) * g.RowP + (t0 - sh);
+    }
+    ttab[e] = v;
+    if (row == 0) wtab[T] = make_int2(i * npool + tw * 4, npool - tw * 4);
   }
-  for (int k = tid; k < g.Kpad; k += 256) klut[k] = im2col_off(g, k);
-  lds_zero(xs, g.imgs * g.img_elems);
-  const int nk = g.Kpad / 32;
+  lds_zero(xs, g.imgs * g.xs_img);
+  const int nk = g.Kpad2 / 32;
   const int Npad = round_up(g.N, 16);
-  bf16x8 bfr[NKMAX][NT];
+  bf16x8 bfr[NK][NT];
 #pragma unroll
-  for (int s = 0; s < NKMAX; ++s)
+  for (int s = 0; s < NK; ++s)
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int n = 16 * t + (lane & 15);
       if (s < nk && n < Npad)
-        bfr[s][t] = *reinterpret_cast<const bf16x8*>(w + (long long)n * g.Kpad + 32 * s + 8 * (lane >> 4));
+        bfr[s][t] = *reinterpret_cast<const bf16x8*>(w + (long long)n * g.Kpad2 + 32 * s + 8 * (lane >> 4));
       else
 #pragma unroll
         for (int e = 0; e < 8; ++e) bfr[s][t][e] = (bf16)0.f;
@@ -129,53 +244,131 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, const void*
     const int n = 16 * t + (lane & 15);
     bv[t] = (bias && n < g.N) ? bias[n] : 0.f;
   }
+  int koff[NK];
+#pragma unroll
+  for (int s = 0; s < NK; ++s) {
+    const int q = 4 * s + (lane >> 4);  // 8-slot group of this lane in k-step s
+    int v = 0;
+    if (s < nk && q < g.KH * g.chunks) {
+      const int ky = q / g.chunks;
+      v = ky * g.ystr + 8 * (q - ky * g.chunks);
+    }
+    koff[s] = v;
+  }
+  // shifted-copy build plan: task = (image, interior row, copy ci >= 1, 16-byte chunk); all offsets
+  // are fixed per thread, so the per-group build is loads + stores only
+  const int WC = g.Wp * g.Cp;
+  const int cpr = g.RowP / 8;
+  const int per_img = g.H * (g.S - 1) * cpr;
+  int bsrc[BT], bdst[BT], blim[BT];
+#pragma unroll
+  for (int j = 0; j < BT; ++j) {
+    const int e = tid + 256 * j;
+    const int i = e / max(per_img, 1);
+    int r = e - i * per_img;
+    const int y = r / max((g.S - 1) * cpr, 1);
+    r -= y * ((g.S - 1) * cpr);
+    const int ci = 1 + r / cpr, c8 = 8 * (r - (r / cpr) * cpr), sh = ci * g.G;
+    const int row = i * g.xs_img + (y + g.pad) * g.ystr;
+    bsrc[j] = row + c8 + sh;
+    bdst[j] = row + ci * g.RowP + c8;
+    // chunks whose source starts past the row stay zero from lds_zero (never written); the others
+    // read 8 elements unguarded (copy 0 has >= 8 zero elements of slack after the row)
+    blim[j] = per_img > 0 && i < g.imgs && c8 + sh < WC ? e : (1 << 30);
+  }
   __syncthreads();
-  int koff[NKMAX][8];
-#pragma unroll
-  for (int s = 0; s < NKMAX; ++s)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) koff[s][e] = (s < nk) ? klut[32 * s + 8 * (lane >> 4) + e] : 0;
 
   const int wl = lane >> 4;  // window of this lane's accumulator rows
+  if (g.dbg & 32) {
+    if (bv[0] == 12345.f && koff[0] == 7 && blim[0] == 3) p[0] = bfr[0][0][0];
+    return;
+  }
+  ImgPlan<CHM> plan;
+  make_img_plan(plan, g, g.ystr, g.Cp);
   // ---- persistent loop over groups of images
   for (int b0 = blockIdx.x * g.imgs; b0 < g.B; b0 += gridDim.x * g.imgs) {
     const int nimg = min(g.imgs, g.B - b0);
-    stage_images(xs, g, x, x_u8, idx, nrows, scale, b0, nimg);
+    if (g.dbg & 1) {
+    } else if (vec) {  // -> copy 0 of each row
+      stage_plan(xs, g.xs_img, plan, g, x, x_u8, idx, nrows, scale, b0, nimg, g.Cp);
+    } else {
+      stage_images(xs, g, x, x_u8, idx, nrows, scale, b0, nimg, g.xs_img, g.ystr, g.Cp);
+    }
     __syncthreads();
-    for (int i = 0; i < nimg; ++i) {
-      const bf16* xi = xs + i * g.img_elems;
-      bf16* pi = p + (long long)(b0 + i) * npool * g.N;
-      uint8_t* ci = code ? code + (long long)(b0 + i) * npool * g.N : nullptr;
-      for (int tw = wid; tw < tpi; tw += 4) {
-        const bf16* xb = xi + ttab[tw * 16 + (lane & 15)];
-        f32x4 acc[NT];
+    if (g.S > 1 && !(g.dbg & 2)) {  // shifted copies of the interior rows (border rows stay zero in every copy)
+      const int lim_img = nimg * per_img;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < BT; ++j) {
+        if (blim[j] < lim_img) {
+          bf16x8 v;
 #pragma unroll
-        for (int s = 0; s < NKMAX; ++s) {
-          if (s < nk) {
-            bf16x8 a;
+          for (int k = 0; k < 8; ++k) v[k] = xs[bsrc[j] + k];
+          *reinterpret_cast<bf16x8*>(xs + bdst[j]) = v;
+        }
+      }
+      for (int e = tid + 256 * BT; e < lim_img; e += 256) {  // beyond the register plan
+        const int i = e / per_img;
+        int r = e - i * per_img;
+        const int y = r / ((g.S - 1) * cpr);
+        r -= y * ((g.S - 1) * cpr);
+        const int ci = 1 + r / cpr, c8 = 8 * (r - (r / cpr) * cpr), sh = ci * g.G;
+        const bf16* src = xs + i * g.xs_img + (y + g.pad) * g.ystr;
+        if (c8 + sh >= WC) continue;
+        bf16x8 v;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) a[e] = xb[koff[s][e]];
+        for (int k = 0; k < 8; ++k) v[k] = src[c8 + k + sh];
+        *reinterpret_cast<bf16x8*>(xs + i * g.xs_img + (y + g.pad) * g.ystr + ci * g.RowP + c8) = v;
+      }
+      __syncthreads();
+    }
+    const int ntiles = nimg * tpi;
+    bf16* pg = p + (long long)b0 * npool * g.N;
+    uint8_t* cg = code ? code + (long long)b0 * npool * g.N : nullptr;
+    for (int T0 = wid * U; T0 < ntiles; T0 += 4 * U) {
+      int offs[U];
 #pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x32(a, bfr[s][t], acc[t]);
+      for (int u = 0; u < U; ++u) offs[u] = ttab[min(T0 + u, ntiles - 1) * 16 + (lane & 15)];
+      bf16x8 a[U][NK];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int s = 0; s < NK; ++s) a[u][s] = *reinterpret_cast<const bf16x8*>(xs + offs[u] + koff[s]);
+      f32x4 acc[U][NT];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          acc[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (g.dbg & 4) {
+#pragma unroll
+            for (int s = 0; s < NK; ++s) acc[u][t][s & 3] += (float)a[u][s][0];
+          } else {
+#pragma unroll
+            for (int s = 0; s < NK; ++s) acc[u][t] = mfma16x16x32(a[u][s], bfr[s][t], acc[u][t]);
           }
         }
-        const int wo = tw * 4 + wl;
-        if (wo < npool) {
 #pragma unroll
-          for (int t = 0; t < NT; ++t) {
-            const int n = 16 * t + (lane & 15);
-            if (n < g.N) {
-              float m = acc[t][0];
-              int am = 0;
+      for (int u = 0; u < U; ++u) {
+        if (T0 + u >= ntiles) break;
+        const int2 wt = wtab[T0 + u];
+        if (g.dbg & 8) {
+          if (acc[u][0][0] == 12345.f) pg[0] = (bf16)0.f;
+          continue;
+        }
+        if (wl >= wt.y) continue;
+        const int o = (wt.x + wl) * g.N;
 #pragma unroll
-              for (int r = 1; r < 4; ++r)
-                if (acc[t][r] > m) { m = acc[t][r]; am = r; }
-              m += bv[t];
-              pi[wo * g.N + n] = f2bf(fmaxf(m, 0.f));
-              if (ci) ci[wo * g.N + n] = (uint8_t)(am | (m > 0.f ? 4 : 0));
-            }
+        for (int t = 0; t < NT; ++t) {
+          const int n = 16 * t + (lane & 15);
+          if (n < g.N) {
+            float m = acc[u][t][0];
+            int am = 0;
+#pragma unroll
+            for (int r = 1; r < 4; ++r)
+              if (acc[u][t][r] > m) { m = acc[u][t][r]; am = r; }
+            m += bv[t];
+            pg[o + n] = f2bf(fmaxf(m, 0.f));
+            if (cg) cg[o + n] = (uint8_t)(am | (m > 0.f ? 4 : 0));
           }
         }
       }
@@ -186,112 +379,149 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, const void*
 
 // ------------------------------------------------------------------------------------------------
 // Weight gradient through the pool: partial[block][n][k] (k < K), partial[block][n][K] = bias grad.
-template <int NT, int KTMAX>
-__global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, const void* x, int x_u8, const long long* idx,
-                                                             long long nrows, float scale,
+// The bias gradient is column K of the same MFMA product (B = 1 there): sum over pixels of dConv.
+// Reduction slots: a 32-pixel chunk = 8 pool windows x 4 pixels; each wave keeps U chunks in flight.
+template <int KT>
+struct WgU {
+  static constexpr int value = KT <= 2 ? 4 : (KT <= 5 ? 2 : 1);
+};
+
+template <int NT, int KTMAX, int CHM>
+__global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, int vec, const void* x, int x_u8,
+                                                             const long long* idx, long long nrows, float scale,
                                                              const bf16* __restrict__ dp,
                                                              const uint8_t* __restrict__ code,
                                                              float* __restrict__ partial) {
+  constexpr int U = WgU<KTMAX>::value;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int Kt = g.K + 1;
-  const int KT = (g.K + 15) / 16;  // k-tiles of the weight part
+  const int KT = (Kt + 15) / 16;  // k-tiles incl. the bias column
   const int npool = g.PH * g.PW;
+  const int wn = npool * g.N;       // pooled elements per image
   const int cpi = (npool + 7) / 8;  // 32-pixel chunks (8 windows) per image
-  int* ctab = reinterpret_cast<int*>(smem);                                     // [cpi*32] pixel offsets
-  int* klut = ctab + cpi * 32;                                                  // [KT*16]
-  float* bsum = reinterpret_cast<float*>(smem + round_up((cpi * 32 + KT * 16) * 4, 16));  // [32]
-  bf16* xs = reinterpret_cast<bf16*>(reinterpret_cast<char*>(bsum) + 128);      // [imgs][img_elems]
+  const int gch = g.imgs * cpi;     // chunks per group
+  int* ctab = reinterpret_cast<int*>(smem);                                     // [gch*32] pixel offsets
+  int2* wtab = reinterpret_cast<int2*>(ctab + gch * 32);                        // [gch]
+  int* klut = reinterpret_cast<int*>(wtab + gch);                               // [KT*16]
+  bf16* xs = reinterpret_cast<bf16*>(smem + round_up((gch * 34 + KT * 16) * 4, 16));  // [imgs][img_elems]
   char* after_x = reinterpret_cast<char*>(xs) + round_up(g.imgs * g.img_elems * 2, 16);
   bf16* dps = reinterpret_cast<bf16*>(after_x);                                 // [imgs][npool][N]
-  uint8_t* cds = reinterpret_cast<uint8_t*>(after_x + round_up(g.imgs * npool * g.N * 2, 16));
+  uint8_t* cds = reinterpret_cast<uint8_t*>(after_x + round_up(g.imgs * wn * 2, 16));
   float* red = reinterpret_cast<float*>(smem);  // aliases all of the above after the main loop
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int e = tid; e < cpi * 32; e += 256) {
-    const int m = e & 31;  // m = 4*window_in_chunk + pixel
-    ctab[e] = window_pixel_off(g, (e >> 5) * 8 + (m >> 2), m & 3, g.Wp, g.C);
+  for (int e = tid; e < gch * 32; e += 256) {
+    const int c = e >> 5, m = e & 31;  // m = 4*window_in_chunk + pixel
+    const int i = c / cpi, cw = c - (c / cpi) * cpi;
+    ctab[e] = i * g.img_elems + window_pixel_off(g, cw * 8 + (m >> 2), m & 3, g.Wp, g.C);
+    if (m == 0) wtab[c] = make_int2(i * wn + cw * 8 * g.N, npool - cw * 8);
   }
   for (int k = tid; k < KT * 16; k += 256) klut[k] = im2col_off(g, k);
-  if (tid < 32) bsum[tid] = 0.f;
   lds_zero(xs, g.imgs * g.img_elems);
   __syncthreads();
   int qoff[KTMAX];
 #pragma unroll
   for (int q = 0; q < KTMAX; ++q) qoff[q] = (q < KT) ? klut[16 * q + (lane & 15)] : 0;
+  const bool bias_col = 16 * (KT - 1) + (lane & 15) == g.K;  // this lane's column in the last tile
 
   f32x4 acc[NT][KTMAX];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int q = 0; q < KTMAX; ++q) acc[t][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // the dp/code load loop strides by a multiple of N, so each thread always sees channel tid % N
-  // and accumulates that channel's bias gradient in a register
-  float bpart = 0.f;
-  const int lstride = 256 - 256 % g.N;
 
+  ImgPlan<CHM> plan;
+  make_img_plan(plan, g, g.Wp * g.C, g.C);
   const int h = lane >> 4;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
   for (int b0 = blockIdx.x * g.imgs; b0 < g.B; b0 += gridDim.x * g.imgs) {
     const int nimg = min(g.imgs, g.B - b0);
-    {
-      const int n = nimg * npool * g.N;
-      const long long o0 = (long long)b0 * npool * g.N;
-      if (tid < lstride) {
-        for (int e = tid; e < n; e += lstride) {
-          const bf16 dv = dp[o0 + e];
-          const int cd = code[o0 + e];
-          dps[e] = dv;
-          cds[e] = cd;
-          if (cd & 4) bpart += (float)dv;
+    const long long o0 = (long long)b0 * wn;
+    if (vec) {
+      // pooled gradient + codes: 4-element chunks, all loads first (wn % 4 == 0 on this path)
+      constexpr int DCH = 2 * CHM;
+      const int nch = nimg * wn / 4;
+      uint2 dv[DCH];
+      uint32_t cv[DCH];
+#pragma unroll
+      for (int j = 0; j < DCH; ++j) {
+        const int c = tid + 256 * j;
+        if (c < nch) {
+          dv[j] = *reinterpret_cast<const uint2*>(dp + o0 + 4 * c);
+          cv[j] = *reinterpret_cast<const uint32_t*>(code + o0 + 4 * c);
         }
       }
-    }
-    stage_images(xs, g, x, x_u8, idx, nrows, scale, b0, nimg);
-    __syncthreads();
-    for (int i = 0; i < nimg; ++i) {
-      const bf16* xi = xs + i * g.img_elems;
-      const int pbase_i = i * npool * g.N;
-      for (int cw = wid; cw < cpi; cw += 4) {
-        // reduction slots m = 8h + e of this lane -> windows w0, w0+1 (4 pixels each)
-        const int w0 = cw * 8 + 2 * h;
-        int pofs[8];
+      stage_plan(xs, g.img_elems, plan, g, x, x_u8, idx, nrows, scale, b0, nimg, g.C);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) pofs[e] = ctab[cw * 32 + 8 * h + e];
-        bf16x8 afr[NT];
+      for (int j = 0; j < DCH; ++j) {
+        const int c = tid + 256 * j;
+        if (c < nch) {
+          *reinterpret_cast<uint2*>(dps + 4 * c) = dv[j];
+          *reinterpret_cast<uint32_t*>(cds + 4 * c) = cv[j];
+        }
+      }
+      for (int c = tid + 256 * DCH; c < nch; c += 256) {  // beyond the register plan (large groups)
+        *reinterpret_cast<uint2*>(dps + 4 * c) = *reinterpret_cast<const uint2*>(dp + o0 + 4 * c);
+        *reinterpret_cast<uint32_t*>(cds + 4 * c) = *reinterpret_cast<const uint32_t*>(code + o0 + 4 * c);
+      }
+    } else {
+      for (int e = tid; e < nimg * wn; e += 256) {
+        dps[e] = dp[o0 + e];
+        cds[e] = code[o0 + e];
+      }
+      stage_images(xs, g, x, x_u8, idx, nrows, scale, b0, nimg, g.img_elems, g.Wp * g.C, g.C);
+    }
+    __syncthreads();
+    const int nchunks = nimg * cpi;
+    for (int C0 = wid * U; C0 < nchunks; C0 += 4 * U) {
+      int pofs[U][8];
+      int2 wt[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int c = min(C0 + u, nchunks - 1);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pofs[u][e] = ctab[c * 32 + 8 * h + e];
+        wt[u] = wtab[c];
+        if (C0 + u >= nchunks) wt[u].y = 0;  // tail: no valid windows
+      }
+      // A = dConv^T: lane row n, slots = 2 windows x 4 pixels, regenerated from (dPooled, code)
+      bf16x8 afr[U][NT];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const int n = 16 * t + (lane & 15);
 #pragma unroll
           for (int ww = 0; ww < 2; ++ww) {
-            int cd = 0;
-            bf16 dv = (bf16)0.f;
-            if (n < g.N && w0 + ww < npool) {
-              const int o = pbase_i + (w0 + ww) * g.N + n;
-              cd = cds[o];
-              dv = dps[o];
-            }
+            const bool ok = n < g.N && 2 * h + ww < wt[u].y;
+            const int o = ok ? wt[u].x + (2 * h + ww) * g.N + n : 0;
+            const int cd = ok ? (int)cds[o] : 0;
+            const bf16 dv = dps[o];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) afr[t][4 * ww + j] = ((cd & 4) && (cd & 3) == j) ? dv : (bf16)0.f;
+            for (int j = 0; j < 4; ++j) afr[u][t][4 * ww + j] = ((cd & 4) && (cd & 3) == j) ? dv : (bf16)0.f;
           }
         }
+      bf16x8 bfr[U][KTMAX];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int q = 0; q < KTMAX; ++q)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bfr[u][q][e] = xs[pofs[u][e] + qoff[q]];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int q = 0; q < KTMAX; ++q) {
-          if (q < KT) {
-            bf16x8 b;
+          const bf16x8 b = (q == KT - 1 && bias_col) ? ones : bfr[u][q];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) b[e] = xi[pofs[e] + qoff[q]];
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t][q] = mfma16x16x32(afr[t], b, acc[t][q]);
-          }
+          for (int t = 0; t < NT; ++t) acc[t][q] = mfma16x16x32(afr[u][t], b, acc[t][q]);
         }
-      }
     }
     __syncthreads();  // slots are restaged by the next group
   }
-  // bias gradient: per-thread partials of channel tid % N -> LDS
-  if (tid < lstride) atomicAdd(&bsum[tid % g.N], bpart);
-  __syncthreads();
-  const float bias_v = tid < g.N ? bsum[tid] : 0.f;
-  __syncthreads();  // everything staged is dead now; reuse LDS for the cross-wave reduction
+  // cross-wave reduction (LDS reused) -> per-block slab [N][K+1]
   const int RW = KT * 16;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
@@ -308,14 +538,13 @@ __global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, const voi
     }
   __syncthreads();
   float* out = partial + (long long)blockIdx.x * g.N * Kt;
-  for (int e = tid; e < g.N * g.K; e += 256) {
-    const int n = e / g.K, k = e - (e / g.K) * g.K;
+  for (int e = tid; e < g.N * Kt; e += 256) {
+    const int n = e / Kt, k = e - (e / Kt) * Kt;
     float s = 0.f;
 #pragma unroll
     for (int ww = 0; ww < 4; ++ww) s += red[(ww * NT * 16 + n) * RW + k];
-    out[n * Kt + k] = s;
+    out[e] = s;
   }
-  if (tid < g.N) out[tid * Kt + g.K] = bias_v;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -323,33 +552,40 @@ __global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, const voi
 struct CPDgrad {
   int Hq, Wq, q_elems, P;  // padded dConv image in LDS, P = KH-1-pad
   int K2, K2pad;           // K2 = KH*KW*N
+  int Nq;                  // LDS pixel stride (>= N): 16-byte reads of 8 consecutive pixels hit distinct banks
 };
 
-template <int NT, int NKMAX, bool VEC>
+template <int NT, int NKMAX, bool VEC, int CHM>
 __global__ void __launch_bounds__(256) convpool_dgrad_kernel(CPGeom g, CPDgrad d, const bf16* __restrict__ dp,
                                                              const uint8_t* __restrict__ code,
                                                              const bf16* __restrict__ wt, bf16* __restrict__ dx) {
+  constexpr int U = NKMAX <= 4 ? 4 : (NKMAX <= 8 ? 2 : 1);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int HW = g.H * g.W;
   const int tpi = (HW + 15) / 16;
-  int* ttab = reinterpret_cast<int*>(smem);  // [tpi*16] input pixel -> qs offset
-  int* klut = ttab + tpi * 16;               // [K2pad]
-  bf16* qs = reinterpret_cast<bf16*>(smem + round_up((tpi * 16 + d.K2pad) * 4, 16));  // [imgs][Hq][Wq][N]
+  const int gtiles = g.imgs * tpi;
+  int* ttab = reinterpret_cast<int*>(smem);             // [gtiles*16] input pixel -> qs offset
+  int2* otab = reinterpret_cast<int2*>(ttab + gtiles * 16);  // [gtiles] (first output pixel, valid pixels)
+  int* klut = reinterpret_cast<int*>(otab + gtiles);    // [K2pad]
+  bf16* qs = reinterpret_cast<bf16*>(smem + round_up((gtiles * 18 + d.K2pad) * 4, 16));  // [imgs][Hq][Wq][N]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int npool = g.PH * g.PW;
-  for (int e = tid; e < tpi * 16; e += 256) {
-    int v = 0;
-    if (e < HW) {
-      const int iy = e / g.W, ix = e - (e / g.W) * g.W;
-      v = (iy * d.Wq + ix) * g.N;
+  for (int e = tid; e < gtiles * 16; e += 256) {
+    const int T = e >> 4, i = T / tpi, tw = T - (T / tpi) * tpi;
+    const int px = tw * 16 + (e & 15);
+    int v = i * d.q_elems;
+    if (px < HW) {
+      const int iy = px / g.W, ix = px - (px / g.W) * g.W;
+      v += (iy * d.Wq + ix) * d.Nq;
     }
     ttab[e] = v;
+    if ((e & 15) == 0) otab[T] = make_int2(i * HW + tw * 16, HW - tw * 16);
   }
   for (int k = tid; k < d.K2pad; k += 256) {
     int v = 0;
     if (k < d.K2) {
       const int n = k % g.N, t = k / g.N, ky = t / g.KW, kx = t - ky * g.KW;
-      v = ((g.KH - 1 - ky) * d.Wq + (g.KW - 1 - kx)) * g.N + n;
+      v = ((g.KH - 1 - ky) * d.Wq + (g.KW - 1 - kx)) * d.Nq + n;
     }
     klut[k] = v;
   }
@@ -377,68 +613,131 @@ __global__ void __launch_bounds__(256) convpool_dgrad_kernel(CPGeom g, CPDgrad d
     for (int e = 0; e < EO; ++e) koff[s][e] = (s < nk) ? klut[32 * s + 8 * (lane >> 4) + e] : 0;
 
   const int wn = npool * g.N;
+  // scatter plan (CHM > 0, wn % 4 == 0): this thread's fixed 4-element chunks of a group's pooled
+  // gradient and the LDS position of each element's window origin; codes stay in registers so the
+  // same positions are cleared again after the group
+  constexpr int PC = CHM > 0 ? CHM : 1;
+  int sbase[PC][4];
+  if (CHM > 0) {
+#pragma unroll
+    for (int j = 0; j < PC; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = 4 * (tid + 256 * j) + k;
+        const int i = e / wn, r = e - (e / wn) * wn;
+        const int wg = r / g.N, c = r - (r / g.N) * g.N;
+        const int py = wg / g.PW, px = wg - (wg / g.PW) * g.PW;
+        sbase[j][k] = i * d.q_elems + ((2 * py + d.P) * d.Wq + 2 * px + d.P) * d.Nq + c;
+      }
+  }
+  const int rowq = d.Wq * d.Nq;
+  uint32_t cv[PC];
   for (int b0 = blockIdx.x * g.imgs; b0 < g.B; b0 += gridDim.x * g.imgs) {
     const int nimg = min(g.imgs, g.B - b0);
     const long long o0 = (long long)b0 * wn;
     const int ntot = nimg * wn;
-    // scatter the routed pooled gradient into the zero full-resolution dConv image
-    for (int e = tid; e < ntot; e += 256) {
-      const int cd = code[o0 + e];
-      if (cd & 4) {
-        const int i = e / wn;
-        const int r = e - i * wn;
-        const int wg = r / g.N, c = r - (r / g.N) * g.N;
-        const int py = wg / g.PW, px = wg - (wg / g.PW) * g.PW;
-        const int oy = 2 * py + ((cd & 3) >> 1), ox = 2 * px + (cd & 1);
-        qs[i * d.q_elems + ((oy + d.P) * d.Wq + ox + d.P) * g.N + c] = dp[o0 + e];
+    if (CHM > 0) {
+      const int nch = ntot / 4;
+      uint2 dv[PC];
+#pragma unroll
+      for (int j = 0; j < PC; ++j) {
+        const int c = tid + 256 * j;
+        cv[j] = 0;
+        if (c < nch) {
+          cv[j] = *reinterpret_cast<const uint32_t*>(code + o0 + 4 * c);
+          dv[j] = *reinterpret_cast<const uint2*>(dp + o0 + 4 * c);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < PC; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t cd = (cv[j] >> (8 * k)) & 255u;
+          if (cd & 4) {
+            const uint32_t bits = (k < 2 ? dv[j].x : dv[j].y) >> (16 * (k & 1));
+            reinterpret_cast<uint16_t*>(qs)[sbase[j][k] + ((cd >> 1) & 1) * rowq + (cd & 1) * d.Nq] =
+                (uint16_t)(bits & 0xffffu);
+          }
+        }
+    } else {
+      // scatter the routed pooled gradient into the zero full-resolution dConv image
+      for (int e = tid; e < ntot; e += 256) {
+        const int cd = code[o0 + e];
+        if (cd & 4) {
+          const int i = e / wn;
+          const int r = e - i * wn;
+          const int wg = r / g.N, c = r - (r / g.N) * g.N;
+          const int py = wg / g.PW, px = wg - (wg / g.PW) * g.PW;
+          const int oy = 2 * py + ((cd & 3) >> 1), ox = 2 * px + (cd & 1);
+          qs[i * d.q_elems + ((oy + d.P) * d.Wq + ox + d.P) * d.Nq + c] = dp[o0 + e];
+        }
       }
     }
     __syncthreads();
-    for (int i = 0; i < nimg; ++i) {
-      const bf16* qi = qs + i * d.q_elems;
-      bf16* xo = dx + (long long)(b0 + i) * HW * g.C;
-      for (int tw = wid; tw < tpi; tw += 4) {
-        const bf16* qb = qi + ttab[tw * 16 + (lane & 15)];
-        f32x4 acc[NT];
+    const int ntiles = nimg * tpi;
+    bf16* xg = dx + (long long)b0 * HW * g.C;
+    for (int T0 = wid * U; T0 < ntiles; T0 += 4 * U) {
+      int offs[U];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int u = 0; u < U; ++u) offs[u] = ttab[min(T0 + u, ntiles - 1) * 16 + (lane & 15)];
+      bf16x8 a[U][NKMAX];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int s = 0; s < NKMAX; ++s) {
-          if (s < nk) {
-            bf16x8 a;
-            if (VEC) {
-              a = *reinterpret_cast<const bf16x8*>(qb + koff[s][0]);
-            } else {
+          if (VEC) {
+            a[u][s] = *reinterpret_cast<const bf16x8*>(qs + offs[u] + koff[s][0]);
+          } else {
 #pragma unroll
-              for (int e = 0; e < 8; ++e) a[e] = qb[koff[s][VEC ? 0 : e]];
-            }
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x32(a, bfr[s][t], acc[t]);
+            for (int e = 0; e < 8; ++e) a[u][s][e] = qs[offs[u] + koff[s][VEC ? 0 : e]];
           }
         }
+      f32x4 acc[U][NT];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          acc[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < NKMAX; ++s) acc[u][t] = mfma16x16x32(a[u][s], bfr[s][t], acc[u][t]);
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (T0 + u >= ntiles) break;
+        const int2 ot = otab[T0 + u];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const int c = 16 * t + (lane & 15);
           if (c >= g.C) continue;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int mm = tw * 16 + 4 * (lane >> 4) + r;
-            if (mm < HW) xo[mm * g.C + c] = f2bf(acc[t][r]);
+            const int mm = 4 * (lane >> 4) + r;
+            if (mm < ot.y) xg[(long long)(ot.x + mm) * g.C + c] = f2bf(acc[u][t][r]);
           }
         }
       }
     }
     __syncthreads();
     // restore the zero image: clear exactly the positions scattered above
-    for (int e = tid; e < ntot; e += 256) {
-      const int cd = code[o0 + e];
-      if (cd & 4) {
-        const int i = e / wn;
-        const int r = e - i * wn;
-        const int wg = r / g.N, c = r - (r / g.N) * g.N;
-        const int py = wg / g.PW, px = wg - (wg / g.PW) * g.PW;
-        const int oy = 2 * py + ((cd & 3) >> 1), ox = 2 * px + (cd & 1);
-        qs[i * d.q_elems + ((oy + d.P) * d.Wq + ox + d.P) * g.N + c] = (bf16)0.f;
+    if (CHM > 0) {
+#pragma unroll
+      for (int j = 0; j < PC; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t cd = (cv[j] >> (8 * k)) & 255u;
+          if (cd & 4) qs[sbase[j][k] + ((cd >> 1) & 1) * rowq + (cd & 1) * d.Nq] = (bf16)0.f;
+        }
+    } else {
+      for (int e = tid; e < ntot; e += 256) {
+        const int cd = code[o0 + e];
+        if (cd & 4) {
+          const int i = e / wn;
+          const int r = e - i * wn;
+          const int wg = r / g.N, c = r - (r / g.N) * g.N;
+          const int py = wg / g.PW, px = wg - (wg / g.PW) * g.PW;
+          const int oy = 2 * py + ((cd & 3) >> 1), ox = 2 * px + (cd & 1);
+          qs[i * d.q_elems + ((oy + d.P) * d.Wq + ox + d.P) * d.Nq + c] = (bf16)0.f;
+        }
       }
     }
     __syncthreads();
@@ -509,8 +808,92 @@ hipError_t slab_reduce(const float* partial, float* gw, float* gb, int N, int K,
 
 // ------------------------------------------------------------------------------------------------
 // host side
+// ---- forward LDS layout choice.  Every A fragment is one ds_read_b128; 8 lanes (8 MFMA rows = two
+// pool windows) issue together, so their 16-byte chunks should fall in distinct 128-byte bank
+// windows.  The channel stride Cp (>= C), the row-copy length RowP and a per-row pad are chosen by
+// simulating that bank mapping over all tiles of the image, scored by k-steps x conflict degree
+// (x a small charge per shifted copy, which must be built per group).
+struct FwdLayout {
+  int Cp, RowP, ypad;
+};
+
+static void set_fwd_layout(CPGeom& g, int Cp, int RowP, int ypad) {
+  g.Cp = Cp;
+  g.RLp = round_up(g.KW * Cp, 8);
+  g.chunks = g.RLp / 8;
+  g.Kpad2 = round_up(g.KH * g.RLp, 32);
+  g.G = std::gcd(Cp, 8);
+  g.S = 8 / g.G;
+  // furthest element a fragment read touches in a row copy: floor8((OW-1)*Cp) + RLp - 1
+  const int maxel = ((g.OW - 1) * Cp) / 8 * 8 + g.RLp;
+  // + 8: zero slack after the row so shifted-copy builds read whole 8-element windows unguarded
+  const int minrow = round_up(max(g.Wp * Cp + 8, maxel), 8);
+  g.RowP = max(RowP, minrow);
+  g.ystr = g.S * g.RowP + ypad;
+  g.xs_img = g.Hp * g.ystr;
+}
+
+static double fwd_conflicts(const CPGeom& g) {
+  const int npool = g.PH * g.PW, tpi = cdiv(npool, 4);
+  double tot = 0.0;
+  int cnt = 0;
+  for (int tw = 0; tw < tpi; ++tw) {
+    int slot[16];
+    for (int row = 0; row < 16; ++row) {
+      const int wg = tw * 4 + (row >> 2), j = row & 3;
+      int off = 0;
+      if (wg < npool) {
+        const int py = wg / g.PW, px = wg % g.PW;
+        const int oy = 2 * py + (j >> 1), ox = 2 * px + (j & 1);
+        const int t0 = ox * g.Cp, sh = t0 & 7;
+        off = oy * g.ystr + (sh / g.G) * g.RowP + (t0 - sh);
+      }
+      slot[row] = (off / 8) & 7;  // 16-byte chunk within a 128-byte window
+    }
+    for (int g0 = 0; g0 < 16; g0 += 8) {
+      int m = 1;
+      for (int a = 0; a < 8; ++a) {
+        int c = 0;
+        for (int b = 0; b < 8; ++b) c += slot[g0 + a] == slot[g0 + b];
+        m = max(m, c);
+      }
+      tot += m;
+      ++cnt;
+    }
+  }
+  return cnt ? tot / cnt : 1.0;
+}
+
+static const FwdLayout& choose_fwd_layout(const CPGeom& g0) {
+  static std::mutex mu;
+  static std::map<std::array<int, 6>, FwdLayout> cache;
+  const std::array<int, 6> key{g0.H, g0.W, g0.C, g0.KH, g0.KW, g0.pad};
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  FwdLayout best{g0.C, 0, 0};
+  double best_score = 1e30;
+  for (int Cp : {g0.C, round_up(g0.C, 2), round_up(g0.C, 4), round_up(g0.C, 8)}) {
+    CPGeom g = g0;
+    set_fwd_layout(g, Cp, 0, 0);
+    if (g.Kpad2 / 32 > 16) continue;
+    const int minrow = g.RowP;
+    for (int rp = minrow; rp < minrow + 64; rp += 8)
+      for (int yp = 0; yp < 64; yp += 8) {
+        set_fwd_layout(g, Cp, rp, yp);
+        const double score = (g.Kpad2 / 32) * fwd_conflicts(g) * (1.0 + 0.1 * (g.S - 1)) * (1.0 + 0.002 * g.xs_img / 64);
+        if (score < best_score - 1e-9) {
+          best_score = score;
+          best = FwdLayout{Cp, rp, yp};
+        }
+      }
+  }
+  return cache.emplace(key, best).first->second;
+}
+
 static CPGeom make_geom(int B, int H, int W, int C, int KH, int KW, int pad, int N) {
   CPGeom g{};
+  g.dbg = g_cp_debug;
   g.B = B; g.H = H; g.W = W; g.C = C; g.KH = KH; g.KW = KW; g.pad = pad; g.N = N;
   g.OH = H + 2 * pad - KH + 1;
   g.OW = W + 2 * pad - KW + 1;
@@ -521,22 +904,34 @@ static CPGeom make_geom(int B, int H, int W, int C, int KH, int KW, int pad, int
   g.Hp = H + 2 * pad;
   g.Wp = W + 2 * pad;
   g.img_elems = round_up(g.Hp * g.Wp * C + 8, 8);  // +8: slack for the finite "padding column" reads
+  set_fwd_layout(g, C, 0, 0);
+  const FwdLayout& L = choose_fwd_layout(g);
+  set_fwd_layout(g, L.Cp, L.RowP, L.ypad);
   return g;
 }
 
 static const size_t kLdsBudget = 64 * 1024;  // keeps >= 2 workgroups per CU (160 KiB LDS)
+constexpr int kStageChunks = 4;              // register-staged 4-element chunks per thread and group
+
+void convpool_fwd_layout(int H, int W, int C, int KH, int KW, int pad, int N, int* Cp, int* Kpad2) {
+  CPGeom g = make_geom(1, H, W, C, KH, KW, pad, N);
+  *Cp = g.Cp;
+  *Kpad2 = g.Kpad2;
+}
 
 bool convpool_supported(int H, int W, int C, int KH, int KW, int pad, int N) {
   CPGeom g = make_geom(1, H, W, C, KH, KW, pad, N);
   if (g.OH <= 0 || g.OW <= 0 || (g.OH & 1) || (g.OW & 1)) return false;
   if (C > 16 || N > 32 || KH > 7 || KW > 7) return false;
-  if (g.Kpad / 32 > 16) return false;                     // fwd weight fragments in registers
-  if ((g.K + 15) / 16 > 12) return false;                 // wgrad accumulators
+  if (g.Kpad2 / 32 > 16) return false;                    // fwd weight fragments in registers
+  if ((g.K + 16) / 16 > 13) return false;                 // wgrad accumulators (incl. bias column)
   if (round_up(KH * KW * N, 32) / 32 > 16) return false;  // dgrad weight fragments
   const int P = KH - 1 - pad;
   if (P < 0) return false;
-  const size_t q_elems = (size_t)(g.OH + 2 * P) * (g.OW + 2 * P) * N;
+  const int Nq = N % 8 == 0 ? ((N / 8) % 2 == 1 ? N : N + 8) : N;
+  const size_t q_elems = (size_t)(g.OH + 2 * P) * (g.OW + 2 * P) * Nq;
   if ((size_t)g.img_elems * 2 > kLdsBudget / 2 || q_elems * 2 > kLdsBudget / 2) return false;
+  if ((size_t)g.xs_img * 2 > kLdsBudget / 2) return false;
   return true;
 }
 
@@ -552,22 +947,59 @@ static int num_cus() {
 
 // Persistent grid: `wg_per_cu` workgroups per CU, each looping over groups of `imgs` images; the
 // per-workgroup setup (tables, weights in registers) is paid once per workgroup, not per group.
-static int pick_imgs(int B, size_t fixed, size_t per_img, int wg_per_cu, int* grid) {
-  const size_t budget = (160 * 1024) / wg_per_cu;
-  int fit = (int)max((size_t)1, (budget > fixed ? budget - fixed : 0) / per_img);
-  fit = min(fit, 32);
-  const int wg = num_cus() * wg_per_cu;
-  int imgs = min(fit, max(1, cdiv(B, wg)));
-  *grid = min(wg, cdiv(B, imgs));
-  return imgs;
+// Persistent-grid sizing from the kernel's real occupancy: blocks/CU allowed by its registers picks
+// the LDS budget per block (-> images per group), then the grid is exactly the resident block count
+// at that LDS size, so every block starts in the first (and only) dispatch round.
+static int blocks_per_cu(const void* kern, size_t lds) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, size_t>, int> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto key = std::make_pair(kern, lds);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, lds) != hipSuccess || nb < 1) nb = 1;
+  cache[key] = nb;
+  return nb;
 }
 
-template <int NT, int NKMAX>
-static void launch_cp_fwd(const CPGeom& g, int grid, size_t lds, const void* x, int x_u8, const long long* idx,
-                          long long nrows, float scale, const bf16* w, const float* bias, bf16* p, uint8_t* code,
-                          hipStream_t st) {
-  hipLaunchKernelGGL((convpool_fwd_kernel<NT, NKMAX>), dim3(grid), dim3(256), lds, st, g, x, x_u8, idx, nrows, scale,
-                     w, bias, p, code);
+struct Sizing {
+  int imgs, grid;
+  size_t lds;
+};
+
+static Sizing size_persistent(const void* kern, int B, size_t fixed, size_t per_img, size_t min_lds, int cap) {
+  const int wpc = min(8, blocks_per_cu(kern, 0));
+  const size_t budget = (160 * 1024) / wpc;
+  int fit = (int)max((size_t)1, (budget > fixed ? budget - fixed : 0) / per_img);
+  fit = max(1, min(fit, min(cap, 32)));
+  Sizing z{};
+  z.imgs = min(fit, max(1, cdiv(B, num_cus() * wpc)));
+  z.lds = max(fixed + (size_t)z.imgs * per_img, min_lds);
+  const int nb = blocks_per_cu(kern, z.lds);
+  z.grid = min(num_cus() * nb, cdiv(B, z.imgs));
+  return z;
+}
+
+template <int NT, int NK>
+static hipError_t launch_cp_fwd(CPGeom g, bool vec, const void* x, int x_u8, const long long* idx, long long nrows,
+                                float scale, const bf16* w, const float* bias, bf16* p, uint8_t* code,
+                                hipStream_t st) {
+  auto kern = convpool_fwd_kernel<NT, NK, kStageChunks>;
+  const int tpi = cdiv(g.PH * g.PW, 4);
+  const Sizing z = size_persistent(reinterpret_cast<const void*>(kern), g.B, 32,
+                                   (size_t)tpi * (16 * 4 + 8) + (size_t)g.xs_img * 2, 0,
+                                   kStageChunks * 256 * 4 / (g.H * g.W * g.C));
+  g.imgs = z.imgs;
+  hipLaunchKernelGGL(kern, dim3(z.grid), dim3(256), z.lds, st, g, (int)vec, x, x_u8, idx, nrows, scale, w, bias, p,
+                     code);
+  return hipGetLastError();
+}
+
+// 4-element vector staging applies when image rows are whole 4-element chunks and the source is aligned
+static bool stage_vec_ok(const CPGeom& g, const void* x, int x_u8) {
+  return (g.W * g.C) % 4 == 0 && g.H * g.W * g.C <= kStageChunks * 1024 && (g.Cp == g.C || g.C >= 2) &&
+         (reinterpret_cast<uintptr_t>(x) % (x_u8 ? 4 : 8)) == 0;
 }
 
 hipError_t convpool_fwd(const void* x, int x_u8, const long long* idx, long long nrows, float scale, int B, int H,
@@ -575,33 +1007,53 @@ hipError_t convpool_fwd(const void* x, int x_u8, const long long* idx, long long
                         uint8_t* code, hipStream_t st) {
   if (!convpool_supported(H, W, C, KH, KW, pad, N)) return hipErrorInvalidValue;
   CPGeom g = make_geom(B, H, W, C, KH, KW, pad, N);
-  const int tpi = cdiv(g.PH * g.PW, 4);
-  const size_t fixed = round_up((round_up(tpi * 16, 4) + g.Kpad) * 4, 16);
-  int grid = 0;
-  g.imgs = pick_imgs(B, fixed, (size_t)g.img_elems * 2, 4, &grid);
-  const size_t lds = fixed + (size_t)g.imgs * g.img_elems * 2;
-  const int nk = g.Kpad / 32;
+  const bool vec = stage_vec_ok(g, x, x_u8);
+  const int nk = g.Kpad2 / 32;
   const int nt = cdiv(N, 16);
+#define CP_FWD(NT_, NK_) return launch_cp_fwd<NT_, NK_>(g, vec, x, x_u8, idx, nrows, scale, w, bias, p, code, st)
   if (nt == 1) {
-    if (nk <= 1) launch_cp_fwd<1, 1>(g, grid, lds, x, x_u8, idx, nrows, scale, w, bias, p, code, st);
-    else if (nk <= 2) launch_cp_fwd<1, 2>(g, grid, lds, x, x_u8, idx, nrows, scale, w, bias, p, code, st);
-    else if (nk <= 5) launch_cp_fwd<1, 5>(g, grid, lds, x, x_u8, idx, nrows, scale, w, bias, p, code, st);
-    else if (nk <= 8) launch_cp_fwd<1, 8>(g, grid, lds, x, x_u8, idx, nrows, scale, w, bias, p, code, st);
-    else launch_cp_fwd<1, 16>(g, grid, lds, x, x_u8, idx, nrows, scale, w, bias, p, code, st);
-  } else {
-    if (nk <= 2) launch_cp_fwd<2, 2>(g, grid, lds, x, x_u8, idx, nrows, scale, w, bias, p, code, st);
-    else if (nk <= 8) launch_cp_fwd<2, 8>(g, grid, lds, x, x_u8, idx, nrows, scale, w, bias, p, code, st);
-    else launch_cp_fwd<2, 16>(g, grid, lds, x, x_u8, idx, nrows, scale, w, bias, p, code, st);
+    if (nk <= 1) CP_FWD(1, 1);
+    if (nk <= 2) CP_FWD(1, 2);
+    if (nk <= 3) CP_FWD(1, 3);
+    if (nk <= 4) CP_FWD(1, 4);
+    if (nk <= 5) CP_FWD(1, 5);
+    if (nk <= 6) CP_FWD(1, 6);
+    if (nk <= 7) CP_FWD(1, 7);
+    if (nk <= 8) CP_FWD(1, 8);
+    if (nk <= 10) CP_FWD(1, 10);
+    if (nk <= 13) CP_FWD(1, 13);
+    CP_FWD(1, 16);
   }
-  return hipGetLastError();
+  if (nk <= 2) CP_FWD(2, 2);
+  if (nk <= 4) CP_FWD(2, 4);
+  if (nk <= 5) CP_FWD(2, 5);
+  if (nk <= 7) CP_FWD(2, 7);
+  if (nk <= 8) CP_FWD(2, 8);
+  if (nk <= 13) CP_FWD(2, 13);
+  CP_FWD(2, 16);
+#undef CP_FWD
 }
 
 template <int NT, int KTMAX>
-static void launch_cp_wgrad(const CPGeom& g, size_t lds, int grid, const void* x, int x_u8, const long long* idx,
-                            long long nrows, float scale, const bf16* dp, const uint8_t* code, float* partial,
-                            hipStream_t st) {
-  hipLaunchKernelGGL((convpool_wgrad_kernel<NT, KTMAX>), dim3(grid), dim3(256), lds, st, g, x, x_u8, idx, nrows,
-                     scale, dp, code, partial);
+static hipError_t launch_cp_wgrad(CPGeom g, bool vec, const void* x, int x_u8, const long long* idx, long long nrows,
+                                  float scale, const bf16* dp, const uint8_t* code, float* gw, float* gb,
+                                  float* workspace, size_t ws_floats, hipStream_t st) {
+  auto kern = convpool_wgrad_kernel<NT, KTMAX, kStageChunks>;
+  const int Kt = g.K + 1;
+  const int KT = cdiv(Kt, 16);
+  const int npool = g.PH * g.PW;
+  const int cpi = cdiv(npool, 8);
+  const size_t red_bytes = (size_t)4 * NT * 16 * KT * 16 * 4;
+  Sizing z = size_persistent(reinterpret_cast<const void*>(kern), g.B, (size_t)KT * 64 + 64,
+                             (size_t)cpi * 136 + (size_t)g.img_elems * 2 + (size_t)npool * g.N * 3 + 48, red_bytes,
+                             kStageChunks * 256 * 4 / (g.H * g.W * g.C));
+  while ((size_t)z.grid * g.N * Kt > ws_floats && z.grid > 1) z.grid /= 2;
+  if ((size_t)z.grid * g.N * Kt > ws_floats || z.lds > 160 * 1024) return hipErrorInvalidValue;
+  g.imgs = z.imgs;
+  hipLaunchKernelGGL(kern, dim3(z.grid), dim3(256), z.lds, st, g, (int)vec, x, x_u8, idx, nrows, scale, dp, code,
+                     workspace);
+  DFA_HIP_CHECK(hipGetLastError());
+  return slab_reduce(workspace, gw, gb, g.N, g.K, Kt, z.grid, 1.f, st);
 }
 
 hipError_t convpool_wgrad(const void* x, int x_u8, const long long* idx, long long nrows, float scale, int B, int H,
@@ -609,40 +1061,35 @@ hipError_t convpool_wgrad(const void* x, int x_u8, const long long* idx, long lo
                           float* gw, float* gb, float* workspace, size_t ws_floats, hipStream_t st) {
   if (!convpool_supported(H, W, C, KH, KW, pad, N)) return hipErrorInvalidValue;
   CPGeom g = make_geom(B, H, W, C, KH, KW, pad, N);
-  const int Kt = g.K + 1;
-  const int KT = cdiv(g.K, 16);
+  const int KT = cdiv(g.K + 1, 16);
   const int NT = cdiv(N, 16);
   const int npool = g.PH * g.PW;
-  const int cpi = cdiv(npool, 8);
-  const size_t fixed = round_up((cpi * 32 + KT * 16) * 4, 16) + 128;
-  const size_t per_img = (size_t)g.img_elems * 2 + (size_t)npool * N * 3 + 32;
-  int grid = 0;
-  g.imgs = pick_imgs(B, fixed, per_img, 2, &grid);
-  while ((size_t)grid * N * Kt > ws_floats && grid > 1) grid /= 2;
-  if ((size_t)grid * N * Kt > ws_floats) return hipErrorInvalidValue;
-  size_t lds = fixed + round_up(g.imgs * g.img_elems * 2, 16) + round_up(g.imgs * npool * N * 2, 16) +
-               round_up(g.imgs * npool * N, 16);
-  const size_t red_bytes = (size_t)4 * NT * 16 * KT * 16 * 4;
-  if (lds < red_bytes) lds = red_bytes;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const bool vec = stage_vec_ok(g, x, x_u8) && (npool * N) % 4 == 0 &&
+                   reinterpret_cast<uintptr_t>(dp) % 8 == 0 && reinterpret_cast<uintptr_t>(code) % 4 == 0;
+#define CP_WG(NT_, KT_) return launch_cp_wgrad<NT_, KT_>(g, vec, x, x_u8, idx, nrows, scale, dp, code, gw, gb, workspace, ws_floats, st)
   if (NT == 1) {
-    if (KT <= 2) launch_cp_wgrad<1, 2>(g, lds, grid, x, x_u8, idx, nrows, scale, dp, code, workspace, st);
-    else if (KT <= 4) launch_cp_wgrad<1, 4>(g, lds, grid, x, x_u8, idx, nrows, scale, dp, code, workspace, st);
-    else if (KT <= 10) launch_cp_wgrad<1, 10>(g, lds, grid, x, x_u8, idx, nrows, scale, dp, code, workspace, st);
-    else launch_cp_wgrad<1, 12>(g, lds, grid, x, x_u8, idx, nrows, scale, dp, code, workspace, st);
-  } else {
-    if (KT <= 2) launch_cp_wgrad<2, 2>(g, lds, grid, x, x_u8, idx, nrows, scale, dp, code, workspace, st);
-    else if (KT <= 4) launch_cp_wgrad<2, 4>(g, lds, grid, x, x_u8, idx, nrows, scale, dp, code, workspace, st);
-    else launch_cp_wgrad<2, 12>(g, lds, grid, x, x_u8, idx, nrows, scale, dp, code, workspace, st);
+    if (KT <= 2) CP_WG(1, 2);
+    if (KT <= 4) CP_WG(1, 4);
+    if (KT <= 10) CP_WG(1, 10);
+    CP_WG(1, 13);
   }
-  DFA_HIP_CHECK(hipGetLastError());
-  return slab_reduce(workspace, gw, gb, N, g.K, Kt, grid, 1.f, st);
+  if (KT <= 2) CP_WG(2, 2);
+  if (KT <= 4) CP_WG(2, 4);
+  CP_WG(2, 13);
+#undef CP_WG
 }
 
 template <int NT, int NKMAX, bool VEC>
-static void launch_cp_dgrad(const CPGeom& g, const CPDgrad& d, int grid, size_t lds, const bf16* dp,
-                            const uint8_t* code, const bf16* wt, bf16* dx, hipStream_t st) {
-  hipLaunchKernelGGL((convpool_dgrad_kernel<NT, NKMAX, VEC>), dim3(grid), dim3(256), lds, st, g, d, dp, code, wt, dx);
+static hipError_t launch_cp_dgrad(CPGeom g, const CPDgrad& d, bool plan, const bf16* dp, const uint8_t* code,
+                                  const bf16* wt, bf16* dx, hipStream_t st) {
+  auto kern = plan ? convpool_dgrad_kernel<NT, NKMAX, VEC, kStageChunks> : convpool_dgrad_kernel<NT, NKMAX, VEC, 0>;
+  const int tpi = cdiv(g.H * g.W, 16);
+  const int wn = g.PH * g.PW * g.N;
+  const Sizing z = size_persistent(reinterpret_cast<const void*>(kern), g.B, (size_t)d.K2pad * 4 + 32,
+                                   (size_t)tpi * 72 + (size_t)d.q_elems * 2, 0, plan ? kStageChunks * 256 * 4 / wn : 32);
+  g.imgs = z.imgs;
+  hipLaunchKernelGGL(kern, dim3(z.grid), dim3(256), z.lds, st, g, d, dp, code, wt, dx);
+  return hipGetLastError();
 }
 
 hipError_t convpool_dgrad(const bf16* dp, const uint8_t* code, const bf16* wt, bf16* dx, int B, int H, int W, int C,
@@ -653,27 +1100,29 @@ hipError_t convpool_dgrad(const bf16* dp, const uint8_t* code, const bf16* wt, b
   d.P = KH - 1 - pad;
   d.Hq = g.OH + 2 * d.P;
   d.Wq = g.OW + 2 * d.P;
-  d.q_elems = round_up(d.Hq * d.Wq * N + 8, 8);
+  // pixel stride: a multiple of 8 elements with an odd number of 16-byte chunks, so 8 consecutive
+  // pixels start in 8 different 16-byte bank groups
+  d.Nq = N % 8 == 0 ? ((N / 8) % 2 == 1 ? N : N + 8) : N;
+  d.q_elems = round_up(d.Hq * d.Wq * d.Nq + 8, 8);
   d.K2 = KH * KW * N;
   d.K2pad = round_up(d.K2, 32);
-  const int tpi = cdiv(H * W, 16);
-  const size_t fixed = round_up((tpi * 16 + d.K2pad) * 4, 16);
-  int grid = 0;
-  g.imgs = pick_imgs(B, fixed, (size_t)d.q_elems * 2, 4, &grid);
-  const size_t lds = fixed + (size_t)g.imgs * d.q_elems * 2;
+  const int wn = g.PH * g.PW * N;
+  const bool plan = wn % 4 == 0 && wn <= kStageChunks * 1024 && reinterpret_cast<uintptr_t>(dp) % 8 == 0 &&
+                    reinterpret_cast<uintptr_t>(code) % 4 == 0;
   const int nk = d.K2pad / 32;
-  const int nt = cdiv(C, 16);
-  const bool vec = N % 8 == 0;
-  if (nt != 1) return hipErrorInvalidValue;
-  if (vec) {
-    if (nk <= 8) launch_cp_dgrad<1, 8, true>(g, d, grid, lds, dp, code, wt, dx, st);
-    else if (nk <= 13) launch_cp_dgrad<1, 13, true>(g, d, grid, lds, dp, code, wt, dx, st);
-    else launch_cp_dgrad<1, 16, true>(g, d, grid, lds, dp, code, wt, dx, st);
-  } else {
-    if (nk <= 8) launch_cp_dgrad<1, 8, false>(g, d, grid, lds, dp, code, wt, dx, st);
-    else launch_cp_dgrad<1, 16, false>(g, d, grid, lds, dp, code, wt, dx, st);
+  if (cdiv(C, 16) != 1) return hipErrorInvalidValue;
+  if (N % 8 == 0) {
+    if (nk <= 2) return launch_cp_dgrad<1, 2, true>(g, d, plan, dp, code, wt, dx, st);
+    if (nk <= 4) return launch_cp_dgrad<1, 4, true>(g, d, plan, dp, code, wt, dx, st);
+    if (nk <= 5) return launch_cp_dgrad<1, 5, true>(g, d, plan, dp, code, wt, dx, st);
+    if (nk <= 8) return launch_cp_dgrad<1, 8, true>(g, d, plan, dp, code, wt, dx, st);
+    if (nk <= 10) return launch_cp_dgrad<1, 10, true>(g, d, plan, dp, code, wt, dx, st);
+    if (nk <= 13) return launch_cp_dgrad<1, 13, true>(g, d, plan, dp, code, wt, dx, st);
+    return launch_cp_dgrad<1, 16, true>(g, d, plan, dp, code, wt, dx, st);
   }
-  return hipGetLastError();
+  if (nk <= 4) return launch_cp_dgrad<1, 4, false>(g, d, plan, dp, code, wt, dx, st);
+  if (nk <= 8) return launch_cp_dgrad<1, 8, false>(g, d, plan, dp, code, wt, dx, st);
+  return launch_cp_dgrad<1, 16, false>(g, d, plan, dp, code, wt, dx, st);
 }
 
 }  // namespace dfa

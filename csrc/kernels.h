@@ -77,6 +77,39 @@ hipError_t bn_bwd(const bf16* x, const bf16* y, const bf16* dy, bf16* dx, const 
                   int relu, float gscale, hipStream_t st);
 
 // fused Conv2D(+bias+ReLU)+MaxPool2x2 for small channel counts (convpool.hip)
+// ---- fused dense head (csrc/mlphead.hip)
+constexpr int kHeadMaxLayers = 4;
+struct HeadLayer {
+  const bf16* w;    // [Npad16][Kpad] compute copy
+  const bf16* wt;   // dgrad layout [Kpad16][ldwt] (may be null for layer 0 when dX is not needed)
+  const float* b;   // bias (nullable)
+  float* gw;        // grad [N][K] fp32
+  float* gb;        // bias grad (nullable)
+  bf16* hT;         // H^T [N][ldt] (hidden layers)
+  bf16* dzT;        // dZ^T [N][ldt]
+  int K, N, Kpad, ldwt, tiles, pad_;
+};
+struct HeadArgs {
+  HeadLayer L[kHeadMaxLayers];
+  int nl, B, ldt, x_relu;
+  const bf16* x;        // [B][K0] input activations
+  bf16* xT;             // X^T [K0][ldt]
+  bf16* dx;             // [B][K0] (nullable)
+  float* logits;        // [B][C] fp32 (nullable)
+  const int* labels;    // labels (indexed through idx when idx != null)
+  const long long* idx;
+  long long nrows;
+  float grad_scale;     // d(loss)/d(logit) scale, 1/B for the mean
+  float* loss_part;     // [nblocks][2]
+  float* stats;         // [2] = (loss sum, correct)
+  int nblocks, wg_tiles;
+};
+size_t head_train_lds(const HeadArgs& a);
+hipError_t head_train(HeadArgs a, hipStream_t st);
+
+void convpool_set_debug(int mask);
+// forward weight layout: [Npad16][Kpad2], column ky*round8(KW*Cp) + kx*Cp + c (zero for c >= C)
+void convpool_fwd_layout(int H, int W, int C, int KH, int KW, int pad, int N, int* Cp, int* Kpad2);
 bool convpool_supported(int H, int W, int C, int KH, int KW, int pad, int N);
 hipError_t convpool_fwd(const void* x, int x_u8, const long long* idx, long long nrows, float scale, int B, int H,
                         int W, int C, int KH, int KW, int pad, int N, const bf16* w, const float* bias, bf16* p,

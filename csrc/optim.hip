@@ -8,7 +8,7 @@
 //   * optional momentum / weight decay (not in the reference; used by the ResNet config),
 //   * the same pass re-emits the bf16 compute copies of each weight matrix in the two layouts the
 //     MFMA kernels read: [N][K] (fwd, K = KH*KW*Cin) and the dgrad layout [Cin][KH*KW*N], both
-//     zero padded to 16 x 32 tiles.  Hyper-parameters live in device memory so a captured hipGraph
+//     zero padded to 16 x 32 tiles (or the row-segment layout of the fused conv+pool forward).  Hyper-parameters live in device memory so a captured hipGraph
 //     sees learning-rate changes without re-capture.
 #include "common.h"
 #include "kernels.h"
@@ -40,7 +40,12 @@ __global__ void __launch_bounds__(256) sgd_multi_kernel(const ParamDesc* __restr
     lr = hyper[0]; mom = hyper[1]; wd = hyper[2]; gs = hyper[3]; nesterov = hyper[4] != 0.f;
   }
   const int K = d.T * d.Ci;
-  const int Kpad = round_up(K, 32);
+  // d.pad_ = KW | Cp << 16 (KW > 0): the primary copy uses the row-segment layout of the fused
+  // conv+pool forward, [Npad16][round32(KH * round8(KW*Cp))], column ky*round8(KW*Cp) + kx*Cp + ci
+  const int rKW = d.pad_ & 0xffff;
+  const int rCp = (d.pad_ >> 16) > 0 ? (d.pad_ >> 16) : d.Ci;
+  const int RLp = rKW > 0 ? round_up(rKW * rCp, 8) : K;
+  const int Kpad = round_up(rKW > 0 ? (d.T / rKW) * RLp : K, 32);
   const int KpadT = round_up(d.T * d.N, 32);
 #pragma unroll
   for (int r = 0; r < SGD_ELEMS_PER_BLOCK / 256; ++r) {
@@ -62,7 +67,13 @@ __global__ void __launch_bounds__(256) sgd_multi_kernel(const ParamDesc* __restr
       const int n = i / K;
       const int kk = i - n * K;
       const bf16 wb = f2bf(w);
-      wbf[d.bf_off + (long long)n * Kpad + kk] = wb;
+      int col = kk;
+      if (rKW > 0) {
+        const int t = kk / d.Ci, ci = kk - (kk / d.Ci) * d.Ci;
+        const int ky = t / rKW, kx = t - (t / rKW) * rKW;
+        col = ky * RLp + kx * rCp + ci;
+      }
+      wbf[d.bf_off + (long long)n * Kpad + col] = wb;
       if (d.bft_off >= 0) {
         const int t = kk / d.Ci;
         const int ci = kk - t * d.Ci;

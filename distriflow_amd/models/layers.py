@@ -496,7 +496,12 @@ class FusedConvPool(Layer):
 
     def specs(self):
         self.conv.need_dx = self.need_dx
-        return self.conv.specs()
+        sp = self.conv.specs()
+        # the forward reads the row-segment weight layout chosen by the kernel (csrc/convpool.hip)
+        H, W, C = self.in_shape
+        sp[0].row_pad = self.k
+        sp[0].row_cp = ops.convpool_fwd_layout(H, W, C, self.k, self.k, self.pad, self.conv.filters)[0]
+        return sp
 
     def alloc(self, B, device, dtype, ws):
         self.out = torch.empty((B,) + self.out_shape, device=device, dtype=dtype)

@@ -49,9 +49,11 @@ class Net:
                 l.store = self.store
         self.num_classes = num_classes or self.output_shape[-1]
         self.step_dev = torch.zeros((), dtype=torch.int64, device=self.device)
+        self.has_dropout = False
         for l in self._all_leaf_layers():
             if isinstance(l, Dropout):
                 l.step_dev = self.step_dev
+                self.has_dropout = True
         self._bound_B = None
         self.graphs: dict = {}
 
@@ -102,6 +104,25 @@ class Net:
             l.in_relu = j > 0 and execd[j - 1].relu
         self.exec_layers = execd
         self.output_shape = shape
+        self.head_start = self._plan_head(execd) if self.fuse else None
+
+    def _plan_head(self, execd):
+        """Index of the first layer of the trailing Dense chain trained by the fused head kernels
+        (csrc/mlphead.hip), or None.  Conditions: <= 4 Dense layers, ReLU on all but the logits layer,
+        <= 16 classes, hidden widths <= 256, input width a multiple of 8 and <= 1024."""
+        if not self.is_gpu or not ops.head_supported():
+            return None
+        j = len(execd)
+        while j > 0 and isinstance(execd[j - 1], Dense) and len(execd) - j < 4:
+            j -= 1
+        head = execd[j:]
+        if not head or head[-1].units > 16 or head[-1].relu:
+            return None
+        if any(not l.relu for l in head[:-1]) or any(l.units > 256 for l in head[:-1]):
+            return None
+        if head[0].in_features % 8 or head[0].in_features > 1024:
+            return None
+        return j
 
     @staticmethod
     def _fuse_conv_pool(execd):
@@ -142,6 +163,14 @@ class Net:
         self.stats = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.x_buf = torch.empty((B,) + self.input_shape, dtype=self.dtype, device=self.device)
         self.y_buf = torch.empty((B,), dtype=torch.int32, device=self.device)
+        if self.head_start is not None:
+            ldt = (B + 31) // 32 * 32  # transposed activation / gradient buffers, zero tail columns
+            head = self.exec_layers[self.head_start:]
+            z = lambda *shape: torch.zeros(shape, dtype=self.dtype, device=self.device)  # noqa: E731
+            self.head_xT = z(head[0].in_features, ldt)
+            self.head_hT = [z(l.units, ldt) for l in head[:-1]] + [None]
+            self.head_dzT = [z(l.units, ldt) for l in head]
+            self.head_loss_part = torch.zeros(2 * ((B + 15) // 16), dtype=torch.float32, device=self.device)
         self._bound_B = B
         self.graphs = {}
 
@@ -173,16 +202,60 @@ class Net:
         return self.stats
 
     def compute_gradients(self, x, labels, grad_ready=None):
-        """fwd + fused softmax-CE + bwd; returns the device stats tensor [loss_sum, correct]."""
+        """fwd + fused softmax-CE + bwd; returns the device stats tensor [loss_sum, correct].
+        ``labels``: int tensor [B], or an :class:`ops.LabelRef` (dataset labels + batch indices)."""
         if not isinstance(x, ops.GatherRef) and x.dtype != self.dtype:
             x = x.to(self.dtype)
+        if self.has_dropout:
+            self.step_dev.add_(1)
+        if self.head_start is not None:
+            return self._compute_gradients_head(x, labels, grad_ready)
+        if isinstance(labels, ops.LabelRef):
+            labels = labels.materialise(self.y_buf)
         if labels.dtype != torch.int32:
             labels = labels.to(torch.int32)
-        self.step_dev.add_(1)
         logits = self.forward(x, training=True)
         stats = self.loss_and_grad(logits, labels)
         self.backward(self.dlogits, grad_ready)
         return stats
+
+    def _compute_gradients_head(self, x, labels, grad_ready):
+        """Body layers one by one, then the fused dense head (2 launches: forward + CE + backward data
+        chain, then all head weight gradients), then the body's backward from the head's dX."""
+        self.bind(x.shape[0])
+        if isinstance(x, ops.GatherRef) and not isinstance(self.exec_layers[0], FusedConvPool):
+            x = x.materialise(self.x_buf)
+        h = x
+        for l in self.exec_layers[: self.head_start]:
+            h = l.forward(h, True)
+        head = self.exec_layers[self.head_start:]
+        if isinstance(labels, ops.LabelRef):
+            lab, idx = labels.labels, labels.idx
+        else:
+            lab, idx = (labels if labels.dtype == torch.int32 else labels.to(torch.int32)), None
+        st = self.store
+        first = head[0]
+        ops.head_train(
+            w=[st.weight(f"{l.name}/kernel") for l in head],
+            wt=[st.weight_t(f"{l.name}/kernel") for l in head],
+            b=[st[f"{l.name}/bias"] if l.use_bias else None for l in head],
+            gw=[st.grad_matrix(f"{l.name}/kernel") for l in head],
+            gb=[st.gradient(f"{l.name}/bias") if l.use_bias else None for l in head],
+            hT=self.head_hT, dzT=self.head_dzT, K=[l.in_features for l in head], N=[l.units for l in head],
+            x=h, x_relu=first.in_relu, xT=self.head_xT, dx=first.dx if first.need_dx else None,
+            logits=head[-1].out, labels=lab, idx=idx, grad_scale=1.0 / x.shape[0],
+            loss_part=self.head_loss_part, stats=self.stats)
+        for l in head:  # keep the per-layer views coherent for evaluate()/introspection
+            l.x = None
+        if grad_ready is not None:
+            for i in range(len(self.exec_layers) - 1, self.head_start - 1, -1):
+                grad_ready(i)
+        d = first.dx if first.need_dx else None
+        for i in range(self.head_start - 1, -1, -1):
+            d = self.exec_layers[i].backward(d)
+            if grad_ready is not None:
+                grad_ready(i)
+        return self.stats
 
     @torch.no_grad()
     def evaluate(self, x, labels, batch_size: int = 4096):

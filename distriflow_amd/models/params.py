@@ -32,6 +32,16 @@ def _r(a, b):
     return (a + b - 1) // b * b
 
 
+def primary_kpad(spec: "ParamSpec") -> int:
+    """Row length of the primary bf16 copy: round32(K), or for the row-segment layout
+    (csrc/optim.hip, csrc/convpool.hip) round32(KH * round8(KW*Cp))."""
+    N, T, Ci = spec.mat
+    if spec.row_pad:
+        cp = spec.row_cp or Ci
+        return _r((T // spec.row_pad) * _r(spec.row_pad * cp, 8), 32)
+    return _r(T * Ci, 32)
+
+
 @dataclass
 class ParamSpec:
     name: str
@@ -41,6 +51,8 @@ class ParamSpec:
     init: str | Callable = "zeros"  # glorot_uniform | he_normal | zeros | ones | callable(tensor)
     fan: tuple = (1, 1)             # (fan_in, fan_out) for initialisers
     needs_dgrad: bool = True        # keep a bf16 dgrad-layout copy
+    row_pad: int = 0                # KW > 0: primary bf16 copy in the fused conv+pool row-segment layout
+    row_cp: int = 0                 #   ... with LDS channel stride Cp (>= Ci; 0 = Ci)
     trainable: bool = True
 
     @property
@@ -144,9 +156,8 @@ class ParamStore:
             N = T = Ci = 1
             if s.kind == "matrix":
                 N, T, Ci = s.mat
-                K = T * Ci
                 bf_off = boff
-                boff += _r(N, 16) * _r(K, 32)
+                boff += _r(N, 16) * primary_kpad(s)
                 if s.needs_dgrad:
                     bft_off = boff
                     boff += _r(Ci, 16) * _r(T * N, 32)
@@ -156,7 +167,8 @@ class ParamStore:
                 if s.kind == "vector":
                     N, T, Ci = 1, 1, s.numel
                 descs.append((self.offsets[s.name], bf_off, bft_off, s.numel, N, T, Ci, block,
-                              0 if s.trainable else 1))
+                              0 if s.trainable else 1,
+                              (s.row_pad | (s.row_cp << 16)) if s.kind == "matrix" else 0))
                 block += nblocks
         self.wbf = torch.zeros(max(boff, 8), dtype=torch.bfloat16, device=self.device)
         self._wbf_views = {}
@@ -167,16 +179,17 @@ class ParamStore:
             N, T, Ci = s.mat
             K = T * Ci
             bf_off, bft_off = self._wbf_layout[s.name]
-            self._wbf_views[s.name] = self.wbf[bf_off: bf_off + _r(N, 16) * _r(K, 32)].view(_r(N, 16), _r(K, 32))
+            kp = primary_kpad(s)
+            self._wbf_views[s.name] = self.wbf[bf_off: bf_off + _r(N, 16) * kp].view(_r(N, 16), kp)
             if bft_off >= 0:
                 self._wbft_views[s.name] = self.wbf[bft_off: bft_off + _r(Ci, 16) * _r(T * N, 32)].view(
                     _r(Ci, 16), _r(T * N, 32))
         # ParamDesc = {i64 off, i64 bf_off, i64 bft_off, i32 numel, i32 N, i32 T, i32 Ci, i32 block_start, i32 pad}
         raw = []
         frozen = []
-        for (off, bf, bft, numel, N, T, Ci, bstart, frz) in descs:
+        for (off, bf, bft, numel, N, T, Ci, bstart, frz, rpad) in descs:
             raw += [off, bf, bft, (numel & 0xFFFFFFFF) | (N << 32), (T & 0xFFFFFFFF) | (Ci << 32),
-                    (bstart & 0xFFFFFFFF)]
+                    (bstart & 0xFFFFFFFF) | (rpad << 32)]
             frozen.append(frz)
         self._descs = torch.tensor(raw, dtype=torch.int64, device=self.device)
         self._ndesc = len(descs)

@@ -250,11 +250,42 @@ class GatherRef:
         return gather_batch(self.data, None, self.idx, out, None, self.scale)
 
 
+class LabelRef:
+    """Labels of a batch that has not been gathered: ``labels[idx]`` (consumers that can read through
+    the index vector — the fused head — never materialise it)."""
+
+    def __init__(self, labels, idx):
+        self.labels, self.idx = labels, idx
+        self.shape = (idx.shape[0],)
+
+    def materialise(self, out):
+        return gather_labels(self.labels, self.idx, out)
+
+
+def head_supported() -> bool:
+    m = native.get(build_if_missing=False)
+    return m is not None and hasattr(m, "head_train")
+
+
+def head_train(w, wt, b, gw, gb, hT, dzT, K, N, x, x_relu, xT, dx, logits, labels, idx, grad_scale, loss_part,
+               stats):
+    """Fused dense head on GPU (csrc/mlphead.hip): forward + softmax-CE + backward of a Dense chain.
+    Writes gw/gb (per-layer gradients, batch-mean scaled via grad_scale), dx, logits, stats."""
+    _C().head_train(list(w), list(wt), list(b), list(gw), list(gb), list(hT), list(dzT), list(K), list(N),
+                    x.reshape(x.shape[0], -1) if x.is_contiguous() else x.contiguous().reshape(x.shape[0], -1),
+                    bool(x_relu), xT, dx, logits, labels, idx, float(grad_scale), loss_part, stats)
+
+
 def convpool_supported(H, W, C, KH, KW, pad, N) -> bool:
     m = native.get(build_if_missing=False)
     if m is None:
         return False
     return bool(m.convpool_supported(H, W, C, KH, KW, pad, N))
+
+
+def convpool_fwd_layout(H, W, C, KH, KW, pad, N):
+    """(channel stride Cp, row length Kpad2) of the fused conv+pool forward weight layout."""
+    return tuple(_C().convpool_fwd_layout(H, W, C, KH, KW, pad, N))
 
 
 def _cp_in(x):

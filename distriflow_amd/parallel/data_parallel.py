@@ -121,7 +121,11 @@ class DataParallelTrainer:
 
     def _gather(self):
         if isinstance(self.xb, ops.GatherRef):
-            ops.gather_labels(self.labels, self.idx, self.yb)
+            if self.net.head_start is not None:
+                # the fused head reads labels through the index vector: no gather launch
+                self.yb = ops.LabelRef(self.labels, self.idx)
+            else:
+                ops.gather_labels(self.labels, self.idx, self.yb)
         else:
             ops.gather_batch(self.data, self.labels, self.idx, self.xb, self.yb, self.scale)
 

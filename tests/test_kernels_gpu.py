@@ -26,6 +26,21 @@ def _pad_w(w2d):
     return out
 
 
+def _rowpad_w(w2d, KH, KW, C, H, W, pad):
+    """fp32 [N][KH*KW*C] -> fused conv+pool forward layout bf16 [Npad16][Kpad2], column
+    ky*round8(KW*Cp) + kx*Cp + c with the kernel's chosen channel stride Cp."""
+    from distriflow_amd import ops as O
+    N = w2d.shape[0]
+    Cp, kp = O.convpool_fwd_layout(H, W, C, KH, KW, pad, N)
+    RLp = _r(KW * Cp, 8)
+    out = torch.zeros(_r(N, 16), kp, dtype=torch.bfloat16, device=dev)
+    w4 = w2d.view(N, KH, KW, C).to(torch.bfloat16)
+    for ky in range(KH):
+        for kx in range(KW):
+            out[:N, ky * RLp + kx * Cp: ky * RLp + kx * Cp + C] = w4[:, ky, kx]
+    return out
+
+
 def _pad_wt(w2d, N, T, Ci):
     """fp32 [N][T*Ci] -> dgrad layout bf16 [Ci_pad16][pad32(T*N)] with (ci, t, n) <- w[n, t, ci]."""
     w3 = w2d.view(N, T, Ci).permute(2, 1, 0).reshape(Ci, T * N)
@@ -261,7 +276,7 @@ def test_convpool_fwd_wgrad_dgrad(B, H, W, C, N, k, p):
     OH, OW = H + 2 * p - k + 1, W + 2 * p - k + 1
     out = torch.empty(B, OH // 2, OW // 2, N, device=dev, dtype=torch.bfloat16)
     code = torch.empty(B, OH // 2, OW // 2, N, device=dev, dtype=torch.uint8)
-    O.convpool_fwd(x, _pad_w(w), b, out, code, k, k, p)
+    O.convpool_fwd(x, _rowpad_w(w, k, k, C, H, W, p), b, out, code, k, k, p)
     ep, ec = ref.convpool_fwd(x.float().cpu(), w.cpu(), b.cpu(), k, k, p)
     _close(out.cpu(), ep)
     agree = (code.cpu() == ec).float().mean().item()
@@ -291,8 +306,63 @@ def test_convpool_fused_gather_u8():
     b = torch.zeros(6, device=dev)
     out = torch.empty(64, 14, 14, 6, device=dev, dtype=torch.bfloat16)
     code = torch.empty(64, 14, 14, 6, device=dev, dtype=torch.uint8)
-    O.convpool_fwd(O.GatherRef(data, idx, 1 / 255, (28, 28, 1)), _pad_w(w), b, out, code, 5, 5, 2)
+    O.convpool_fwd(O.GatherRef(data, idx, 1 / 255, (28, 28, 1)), _rowpad_w(w, 5, 5, 1, 28, 28, 2), b, out, code, 5, 5, 2)
     xb = (data[idx].float() / 255).to(torch.bfloat16)
     out2 = torch.empty_like(out)
-    O.convpool_fwd(xb, _pad_w(w), b, out2, None, 5, 5, 2)
+    O.convpool_fwd(xb, _rowpad_w(w, 5, 5, 1, 28, 28, 2), b, out2, None, 5, 5, 2)
     assert torch.equal(out, out2)
+
+
+@pytest.mark.parametrize("B,dims,with_idx,x_relu", [
+    (50, (64, 48, 32, 10), False, False),    # odd batch: partial row block + zero tail columns
+    (256, (400, 120, 84, 10), True, True),   # LeNet-5 head, labels through an index vector, relu' on X
+    (96, (784, 10), False, False),           # single-layer (softmax regression) head
+])
+def test_fused_head_matches_autograd(B, dims, with_idx, x_relu):
+    from distriflow_amd import ops as O
+
+    torch.manual_seed(0)
+    nl = len(dims) - 1
+    x = torch.randn(B, dims[0], device=dev)
+    if x_relu:
+        x = x.clamp_min(0)
+    x = x.to(torch.bfloat16)
+    ws = [(torch.randn(dims[i + 1], dims[i], device=dev) / dims[i] ** 0.5).to(torch.bfloat16).float()
+          for i in range(nl)]
+    bs = [torch.randn(dims[i + 1], device=dev) * 0.1 for i in range(nl)]
+    nrows = 3 * B
+    all_labels = torch.randint(0, dims[-1], (nrows,), device=dev, dtype=torch.int32)
+    idx = torch.randperm(nrows, device=dev)[:B] if with_idx else None
+    y = all_labels[idx] if with_idx else all_labels[:B]
+    ldt = (B + 31) // 32 * 32
+    gw = [torch.empty(dims[i + 1], dims[i], device=dev) for i in range(nl)]
+    gb = [torch.empty(dims[i + 1], device=dev) for i in range(nl)]
+    hT = [torch.zeros(dims[i + 1], ldt, device=dev, dtype=torch.bfloat16) for i in range(nl - 1)] + [None]
+    dzT = [torch.zeros(dims[i + 1], ldt, device=dev, dtype=torch.bfloat16) for i in range(nl)]
+    xT = torch.zeros(dims[0], ldt, device=dev, dtype=torch.bfloat16)
+    dx = torch.empty(B, dims[0], device=dev, dtype=torch.bfloat16)
+    logits = torch.empty(B, dims[-1], device=dev)
+    loss_part = torch.zeros(2 * ((B + 15) // 16), device=dev)
+    stats = torch.zeros(2, device=dev)
+    O.head_train([_pad_w(w) for w in ws], [_pad_wt(w, w.shape[0], 1, w.shape[1]) for w in ws], bs, gw, gb, hT, dzT,
+                 list(dims[:-1]), list(dims[1:]), x, x_relu, xT, dx, logits,
+                 all_labels if with_idx else y, idx, 1.0 / B, loss_part, stats)
+    # fp32 reference
+    xr = x.float().requires_grad_(True)
+    wr = [w.clone().requires_grad_(True) for w in ws]
+    br = [b.clone().requires_grad_(True) for b in bs]
+    h = xr
+    for i in range(nl):
+        h = h @ wr[i].t() + br[i]
+        if i < nl - 1:
+            h = torch.relu(h)
+    loss = torch.nn.functional.cross_entropy(h, y.long(), reduction="sum")
+    (loss / B).backward()
+    _close(logits, h.detach(), 3e-2, 3e-2)
+    for i in range(nl):
+        _close(gw[i], wr[i].grad, 3e-2, 3e-2)
+        _close(gb[i], br[i].grad, 3e-2, 3e-2)
+    edx = xr.grad * (x.float() > 0) if x_relu else xr.grad
+    _close(dx, edx, 3e-2, 3e-2)
+    torch.testing.assert_close(stats[0], loss.detach(), rtol=2e-2, atol=2e-2 * B)
+    assert abs(stats[1].item() - (h.argmax(1) == y.long()).sum().item()) <= 2
