@@ -452,8 +452,9 @@ void head_train_py(std::vector<torch::Tensor> w, std::vector<c10::optional<torch
                    std::vector<torch::Tensor> dzT, std::vector<int64_t> K, std::vector<int64_t> N, torch::Tensor x,
                    bool x_relu, torch::Tensor xT, c10::optional<torch::Tensor> dx,
                    c10::optional<torch::Tensor> logits, torch::Tensor labels, c10::optional<torch::Tensor> idx,
-                   double grad_scale, torch::Tensor loss_part, torch::Tensor stats) {
+                   double grad_scale, torch::Tensor loss_part, torch::Tensor stats, int64_t phases) {
   const int nl = (int)w.size();
+  TORCH_CHECK(phases >= 1 && phases <= 3, "head: phases must be 1, 2 or 3");
   TORCH_CHECK(nl >= 1 && nl <= dfa::kHeadMaxLayers, "head: 1..", dfa::kHeadMaxLayers, " layers");
   TORCH_CHECK((int)wt.size() == nl && (int)b.size() == nl && (int)gw.size() == nl && (int)gb.size() == nl &&
                   (int)hT.size() == nl && (int)dzT.size() == nl && (int)K.size() == nl && (int)N.size() == nl,
@@ -545,7 +546,7 @@ void head_train_py(std::vector<torch::Tensor> w, std::vector<c10::optional<torch
   TORCH_CHECK(stats.numel() >= 2, "head: stats must hold 2 floats");
   a.stats = stats.data_ptr<float>();
   TORCH_CHECK(dfa::head_train_lds(a) <= 160 * 1024, "head: LDS footprint too large");
-  check_hip(dfa::head_train(a, cur_stream()), "head_train");
+  check_hip(dfa::head_train(a, (int)phases, cur_stream()), "head_train");
 }
 
 bool convpool_supported_py(int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t pad, int64_t N) {
@@ -577,6 +578,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("convpool_wgrad", &convpool_wgrad_py, "weight gradient through the fused conv+pool");
   m.def("convpool_dgrad", &convpool_dgrad_py, "data gradient through the fused conv+pool");
   m.def("convpool_set_debug", &dfa::convpool_set_debug, "profiling aid: skip kernel phases (bit mask)");
+  m.def("convpool_set_stamps", [](c10::optional<torch::Tensor> buf) {
+    if (buf.has_value() && buf->defined()) {
+      TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == at::kLong && buf->numel() >= 4096 * 32,
+                  "stamp buffer: int64 GPU tensor of >= 4096*32 elements");
+      dfa::convpool_set_stamps(buf->data_ptr());
+    } else {
+      dfa::convpool_set_stamps(nullptr);
+    }
+  }, "profiling aid: per-block phase stamps of the convpool kernels");
   m.def("convpool_fwd_layout", [](int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t pad, int64_t N) {
     int Cp = 0, Kpad2 = 0;
     dfa::convpool_fwd_layout(H, W, C, KH, KW, pad, N, &Cp, &Kpad2);

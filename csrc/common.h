@@ -42,6 +42,17 @@ __device__ __forceinline__ float wave_max(float v) {
 __host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
 __host__ __device__ __forceinline__ int round_up(int a, int b) { return cdiv(a, b) * b; }
 
+// Division of small non-negative ints (a < 2^20, d >= 1) for index tables: 3 VALU instead of the
+// ~25-instruction integer division sequence.  (a + 0.5) / d stays >= 0.5/d away from any integer,
+// which exceeds the combined v_rcp_f32 + rounding error in that range, so truncation is exact.
+struct FDiv {
+  int d;
+  float inv;
+  __device__ __forceinline__ explicit FDiv(int dd) : d(dd), inv(__builtin_amdgcn_rcpf((float)dd)) {}
+  __device__ __forceinline__ int div(int a) const { return (int)(((float)a + 0.5f) * inv); }
+  __device__ __forceinline__ int mod(int a, int q) const { return a - q * d; }
+};
+
 // Bijective XCD-aware remap of a 1-D block id: consecutive logical tiles land on the same XCD
 // (blocks b and b+8 share an XCD under round-robin dispatch) so neighbouring tiles share L2.
 __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {

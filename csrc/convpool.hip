@@ -45,11 +45,26 @@ struct CPGeom {
   int Cp;                  // LDS channel stride of the forward image (>= C, zero-filled channels)
   int RLp, chunks, Kpad2;  // RLp = round8(KW*Cp), chunks = RLp/8, Kpad2 = round32(KH*RLp)
   int G, S, RowP, ystr, xs_img;  // G = gcd(C,8): copy ci is shifted by ci*G elements, S = 8/G copies
-  int dbg;                        // profiling aid: bit0 skip staging, bit1 skip shift build, bit2 skip MFMA, bit3 skip stores
+  int dbg;                        // profiling aid: bit0 skip staging, bit1 skip shift build, 16/32 early exits
+  unsigned long long* stamps;     // profiling aid: per-block s_memtime stamps [grid][32] (nullptr = off)
 };
 
 static int g_cp_debug = 0;
+static unsigned long long* g_cp_stamps = nullptr;
 void convpool_set_debug(int mask) { g_cp_debug = mask; }
+void convpool_set_stamps(void* buf) { g_cp_stamps = reinterpret_cast<unsigned long long*>(buf); }
+
+// Diagnostic phase stamps (cdna_hip_programming.md §7 "In-kernel stamps"): read SHARES, not lengths.
+#define CP_STAMP(slot)                                                                    \
+  do {                                                                                    \
+    if (g.stamps) {                                                                       \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      unsigned long long t_;                                                              \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      if (threadIdx.x == 0 && (slot) < 32) g.stamps[blockIdx.x * 32 + (slot)] = t_;     \
+    }                                                                                     \
+  } while (0)
 
 __device__ __forceinline__ long long cp_clamp(long long r, long long n) { return r < 0 ? 0 : (r >= n ? n - 1 : r); }
 
@@ -206,6 +221,7 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
   int2* wtab = reinterpret_cast<int2*>(ttab + gtiles * 16);      // [gtiles] (first pooled index, valid windows)
   bf16* xs = reinterpret_cast<bf16*>(smem + round_up(gtiles * 16 * 4 + gtiles * 8, 16));  // [imgs][Hp][S][RowP]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  CP_STAMP(0);
   if (g.dbg & 16) return;
 
   // ---- once per workgroup: tables, zero-bordered image slots, register-resident weights
@@ -285,8 +301,10 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
   }
   ImgPlan<CHM> plan;
   make_img_plan(plan, g, g.ystr, g.Cp);
+  CP_STAMP(1);
+  int grp = 0;
   // ---- persistent loop over groups of images
-  for (int b0 = blockIdx.x * g.imgs; b0 < g.B; b0 += gridDim.x * g.imgs) {
+  for (int b0 = blockIdx.x * g.imgs; b0 < g.B; b0 += gridDim.x * g.imgs, ++grp) {
     const int nimg = min(g.imgs, g.B - b0);
     if (g.dbg & 1) {
     } else if (vec) {  // -> copy 0 of each row
@@ -295,6 +313,7 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
       stage_images(xs, g, x, x_u8, idx, nrows, scale, b0, nimg, g.xs_img, g.ystr, g.Cp);
     }
     __syncthreads();
+    CP_STAMP(2 + 3 * grp);
     if (g.S > 1 && !(g.dbg & 2)) {  // shifted copies of the interior rows (border rows stay zero in every copy)
       const int lim_img = nimg * per_img;
 #pragma unroll
@@ -321,6 +340,7 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
       }
       __syncthreads();
     }
+    CP_STAMP(3 + 3 * grp);
     const int ntiles = nimg * tpi;
     bf16* pg = p + (long long)b0 * npool * g.N;
     uint8_t* cg = code ? code + (long long)b0 * npool * g.N : nullptr;
@@ -339,22 +359,13 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           acc[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (g.dbg & 4) {
 #pragma unroll
-            for (int s = 0; s < NK; ++s) acc[u][t][s & 3] += (float)a[u][s][0];
-          } else {
-#pragma unroll
-            for (int s = 0; s < NK; ++s) acc[u][t] = mfma16x16x32(a[u][s], bfr[s][t], acc[u][t]);
-          }
+          for (int s = 0; s < NK; ++s) acc[u][t] = mfma16x16x32(a[u][s], bfr[s][t], acc[u][t]);
         }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (T0 + u >= ntiles) break;
         const int2 wt = wtab[T0 + u];
-        if (g.dbg & 8) {
-          if (acc[u][0][0] == 12345.f) pg[0] = (bf16)0.f;
-          continue;
-        }
         if (wl >= wt.y) continue;
         const int o = (wt.x + wl) * g.N;
 #pragma unroll
@@ -373,21 +384,38 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
         }
       }
     }
+    CP_STAMP(4 + 3 * grp);
     __syncthreads();  // image slots are restaged by the next group
   }
+  CP_STAMP(31);
 }
 
 // ------------------------------------------------------------------------------------------------
 // Weight gradient through the pool: partial[block][n][k] (k < K), partial[block][n][K] = bias grad.
-// The bias gradient is column K of the same MFMA product (B = 1 there): sum over pixels of dConv.
-// Reduction slots: a 32-pixel chunk = 8 pool windows x 4 pixels; each wave keeps U chunks in flight.
+//   dW[n][k] = sum_pixels dConv[pixel][n] * im2col(X)[pixel][k]      (bias: column K of ones)
+// Reduction slots of one lane are 8 CONSECUTIVE conv-output pixels of one row, so both MFMA operands
+// are single aligned 16-byte LDS reads:
+//   A = dConv^T: channel-planar LDS image [N][OHc][DWc], scattered from (dPooled, code) once per
+//       group (the full-resolution gradient never reaches HBM);
+//   B = im2col(X): channel-planar LDS image with KW x-shifted copies of every row,
+//       [C][Hq][KW][RowQ], copy s = row shifted left by s, so column k = (ky, kx, c) of pixels
+//       ox0..ox0+7 is copy kx of row oy+ky at ox0 (ox0 a multiple of 8).
+// A chunk = (4/G) output rows x 8G columns (one row / 8 columns per 16-lane group).
+struct CPWg {
+  int G, R;                          // lane-group split: chunk = R = 4/G rows x 8G cols
+  int OHc, OWc, cpr, cpc, cpi;       // chunk-aligned output extent, chunk rows/cols, chunks per image
+  int Hq, RowQ, ystr, cstr, xs_img;  // X image [C][Hq][KW][RowQ] (+pads)
+  int DWc, dcs, dc_img;              // dConv image [N+1][OHc][DWc] (+pad; plane N stays zero), dc_img = (N+1)*dcs
+  int build_per_img;                 // shifted-copy build tasks per image
+};
+
 template <int KT>
 struct WgU {
   static constexpr int value = KT <= 2 ? 4 : (KT <= 5 ? 2 : 1);
 };
 
 template <int NT, int KTMAX, int CHM>
-__global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, int vec, const void* x, int x_u8,
+__global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, CPWg q, int vec, const void* x, int x_u8,
                                                              const long long* idx, long long nrows, float scale,
                                                              const bf16* __restrict__ dp,
                                                              const uint8_t* __restrict__ code,
@@ -397,142 +425,264 @@ __global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, int vec, 
   const int Kt = g.K + 1;
   const int KT = (Kt + 15) / 16;  // k-tiles incl. the bias column
   const int npool = g.PH * g.PW;
-  const int wn = npool * g.N;       // pooled elements per image
-  const int cpi = (npool + 7) / 8;  // 32-pixel chunks (8 windows) per image
-  const int gch = g.imgs * cpi;     // chunks per group
-  int* ctab = reinterpret_cast<int*>(smem);                                     // [gch*32] pixel offsets
-  int2* wtab = reinterpret_cast<int2*>(ctab + gch * 32);                        // [gch]
-  int* klut = reinterpret_cast<int*>(wtab + gch);                               // [KT*16]
-  bf16* xs = reinterpret_cast<bf16*>(smem + round_up((gch * 34 + KT * 16) * 4, 16));  // [imgs][img_elems]
-  char* after_x = reinterpret_cast<char*>(xs) + round_up(g.imgs * g.img_elems * 2, 16);
-  bf16* dps = reinterpret_cast<bf16*>(after_x);                                 // [imgs][npool][N]
-  uint8_t* cds = reinterpret_cast<uint8_t*>(after_x + round_up(g.imgs * wn * 2, 16));
+  const int wn = npool * g.N;      // pooled elements per image
+  const int gch = g.imgs * q.cpi;  // chunks per group
+  int2* ctab = reinterpret_cast<int2*>(smem);                                   // [gch] (X base, dConv base)
+  bf16* xs = reinterpret_cast<bf16*>(smem + round_up(gch * 8, 16));             // [imgs][xs_img]
+  bf16* dc = xs + g.imgs * q.xs_img;                                            // [imgs][dc_img]
   float* red = reinterpret_cast<float*>(smem);  // aliases all of the above after the main loop
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int e = tid; e < gch * 32; e += 256) {
-    const int c = e >> 5, m = e & 31;  // m = 4*window_in_chunk + pixel
-    const int i = c / cpi, cw = c - (c / cpi) * cpi;
-    ctab[e] = i * g.img_elems + window_pixel_off(g, cw * 8 + (m >> 2), m & 3, g.Wp, g.C);
-    if (m == 0) wtab[c] = make_int2(i * wn + cw * 8 * g.N, npool - cw * 8);
+  CP_STAMP(0);
+  const FDiv dcpi(q.cpi), dcpc(q.cpc);
+  for (int c = tid; c < gch; c += 256) {
+    const int i = dcpi.div(c), r = c - i * q.cpi;
+    const int rc = dcpc.div(r), cc = r - rc * q.cpc;
+    ctab[c] = make_int2(i * q.xs_img + rc * q.R * q.ystr + cc * 8 * q.G,
+                        i * q.dc_img + rc * q.R * q.DWc + cc * 8 * q.G);
   }
-  for (int k = tid; k < KT * 16; k += 256) klut[k] = im2col_off(g, k);
-  lds_zero(xs, g.imgs * g.img_elems);
-  __syncthreads();
-  int qoff[KTMAX];
+  lds_zero(xs, g.imgs * (q.xs_img + q.dc_img));
+  // per-lane constants: 16-lane group h -> (row hr, 8-column block hx) inside a chunk
+  const int h = lane >> 4, hr = h / q.G, hx = h - hr * q.G;
+  const int xlane = hr * q.ystr + hx * 8;
+  const int dlane = hr * q.DWc + hx * 8;
+  int aoff[NT];  // channel plane of this lane's A row (rows >= N read the image's zero plane N)
 #pragma unroll
-  for (int q = 0; q < KTMAX; ++q) qoff[q] = (q < KT) ? klut[16 * q + (lane & 15)] : 0;
-  const bool bias_col = 16 * (KT - 1) + (lane & 15) == g.K;  // this lane's column in the last tile
+  for (int t = 0; t < NT; ++t) aoff[t] = min(16 * t + (lane & 15), g.N) * q.dcs + dlane;
+  int koff[KTMAX];  // B column k = (ky*KW + kx)*C + c -> copy kx of channel c, row +ky
+  bool bias_col = false, zero_col = false;
+  const FDiv dC(g.C), dKW(g.KW);
+#pragma unroll
+  for (int t = 0; t < KTMAX; ++t) {
+    const int k = 16 * t + (lane & 15);
+    int v = 0;
+    if (t < KT && k < g.K) {
+      const int tt = dC.div(k), c = k - tt * g.C, ky = dKW.div(tt), kx = tt - ky * g.KW;
+      v = c * q.cstr + ky * q.ystr + kx * q.RowQ;
+    }
+    koff[t] = v;
+    if (t == KT - 1) {
+      bias_col = k == g.K;
+      zero_col = k > g.K;
+    }
+  }
+  // X staging plan: NHWC source chunk of 4 elements -> channel-planar copy-0 positions.  dst of
+  // element k = sbase + k*cstr (channel steps), minus (C*cstr - 1) once the chunk crosses into the
+  // next pixel (k >= split); C == 1 chunks are 4 consecutive pixels.
+  const int WC = g.W * g.C, cprw = WC / 4, cpimg = g.H * cprw;
+  int sdst[CHM], ssplit[CHM], simg[CHM], ssrc[CHM];
+  const FDiv dcpimg(cpimg), dcprw(cprw);
+#pragma unroll
+  for (int j = 0; j < CHM; ++j) {
+    const int c = tid + 256 * j;
+    const int i = dcpimg.div(c), r = c - i * cpimg;
+    const int y = dcprw.div(r), e0 = 4 * (r - y * cprw);
+    const int px = dC.div(e0), ch = e0 - px * g.C;
+    simg[j] = c < g.imgs * cpimg ? i : (1 << 20);
+    ssrc[j] = y * WC + e0;
+    sdst[j] = i * q.xs_img + ch * q.cstr + (y + g.pad) * q.ystr + px + g.pad;
+    ssplit[j] = g.C - ch;
+  }
+  const int cstep = g.C == 1 ? 1 : q.cstr;
+  const int cwrap = g.C == 1 ? 0 : g.C * q.cstr - 1;
+  // dConv scatter plan: 4-element chunks of a group's pooled gradient (wn % 4 == 0), offsets of
+  // the windows' top-left pixel packed as 16-bit pairs (the dConv images of a group are < 64K elems)
+  constexpr int PC = CHM;
+  uint32_t sbase[PC][2];
+  const FDiv dwn(wn), dN(g.N), dPW(g.PW);
+#pragma unroll
+  for (int j = 0; j < PC; ++j)
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int e = 4 * (tid + 256 * j) + 2 * k2 + hh;
+        const int i = dwn.div(e), r = e - i * wn;
+        const int wg = dN.div(r), n = r - wg * g.N;
+        const int py = dPW.div(wg), px = wg - py * g.PW;
+        // elements past the group's images point at image 0's zero plane (their writes are zeros)
+        const uint32_t off = i < g.imgs ? (uint32_t)(i * q.dc_img + n * q.dcs + 2 * py * q.DWc + 2 * px)
+                                        : (uint32_t)(g.N * q.dcs);
+        v |= (off & 0xffffu) << (16 * hh);
+      }
+      sbase[j][k2] = v;
+    }
+  uint32_t cvr[PC];
+  __syncthreads();
 
   f32x4 acc[NT][KTMAX];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int q = 0; q < KTMAX; ++q) acc[t][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  ImgPlan<CHM> plan;
-  make_img_plan(plan, g, g.Wp * g.C, g.C);
-  const int h = lane >> 4;
-  bf16x8 ones;
+    for (int u = 0; u < KTMAX; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones, zeros;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
-  for (int b0 = blockIdx.x * g.imgs; b0 < g.B; b0 += gridDim.x * g.imgs) {
+  for (int e = 0; e < 8; ++e) {
+    ones[e] = (bf16)1.f;
+    zeros[e] = (bf16)0.f;
+  }
+  CP_STAMP(1);
+  int grp = 0;
+  for (int b0 = blockIdx.x * g.imgs; b0 < g.B; b0 += gridDim.x * g.imgs, ++grp) {
     const int nimg = min(g.imgs, g.B - b0);
     const long long o0 = (long long)b0 * wn;
-    if (vec) {
-      // pooled gradient + codes: 4-element chunks, all loads first (wn % 4 == 0 on this path)
-      constexpr int DCH = 2 * CHM;
-      const int nch = nimg * wn / 4;
-      uint2 dv[DCH];
-      uint32_t cv[DCH];
+    const int nch = nimg * wn / 4;
+    const long long HWC = (long long)g.H * WC;
+    // ---- issue every global load of the group first: pooled grads + codes, image chunks
+    uint2 dv[PC];  // (nch <= PC*256: imgs is capped by the host)
 #pragma unroll
-      for (int j = 0; j < DCH; ++j) {
-        const int c = tid + 256 * j;
-        if (c < nch) {
-          dv[j] = *reinterpret_cast<const uint2*>(dp + o0 + 4 * c);
-          cv[j] = *reinterpret_cast<const uint32_t*>(code + o0 + 4 * c);
-        }
+    for (int j = 0; j < PC; ++j) {
+      const int c = tid + 256 * j;
+      cvr[j] = 0;
+      if (c < nch) {
+        cvr[j] = *reinterpret_cast<const uint32_t*>(code + o0 + 4 * c);
+        dv[j] = *reinterpret_cast<const uint2*>(dp + o0 + 4 * c);
       }
-      stage_plan(xs, g.img_elems, plan, g, x, x_u8, idx, nrows, scale, b0, nimg, g.C);
-#pragma unroll
-      for (int j = 0; j < DCH; ++j) {
-        const int c = tid + 256 * j;
-        if (c < nch) {
-          *reinterpret_cast<uint2*>(dps + 4 * c) = dv[j];
-          *reinterpret_cast<uint32_t*>(cds + 4 * c) = cv[j];
-        }
-      }
-      for (int c = tid + 256 * DCH; c < nch; c += 256) {  // beyond the register plan (large groups)
-        *reinterpret_cast<uint2*>(dps + 4 * c) = *reinterpret_cast<const uint2*>(dp + o0 + 4 * c);
-        *reinterpret_cast<uint32_t*>(cds + 4 * c) = *reinterpret_cast<const uint32_t*>(code + o0 + 4 * c);
-      }
-    } else {
-      for (int e = tid; e < nimg * wn; e += 256) {
-        dps[e] = dp[o0 + e];
-        cds[e] = code[o0 + e];
-      }
-      stage_images(xs, g, x, x_u8, idx, nrows, scale, b0, nimg, g.img_elems, g.Wp * g.C, g.C);
     }
-    __syncthreads();
-    const int nchunks = nimg * cpi;
-    for (int C0 = wid * U; C0 < nchunks; C0 += 4 * U) {
-      int pofs[U][8];
-      int2 wt[U];
+    if (vec) {
+      uint32_t xv[CHM];
+      uint2 xb[CHM];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int c = min(C0 + u, nchunks - 1);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) pofs[u][e] = ctab[c * 32 + 8 * h + e];
-        wt[u] = wtab[c];
-        if (C0 + u >= nchunks) wt[u].y = 0;  // tail: no valid windows
-      }
-      // A = dConv^T: lane row n, slots = 2 windows x 4 pixels, regenerated from (dPooled, code)
-      bf16x8 afr[U][NT];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const int n = 16 * t + (lane & 15);
-#pragma unroll
-          for (int ww = 0; ww < 2; ++ww) {
-            const bool ok = n < g.N && 2 * h + ww < wt[u].y;
-            const int o = ok ? wt[u].x + (2 * h + ww) * g.N + n : 0;
-            const int cd = ok ? (int)cds[o] : 0;
-            const bf16 dv = dps[o];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) afr[u][t][4 * ww + j] = ((cd & 4) && (cd & 3) == j) ? dv : (bf16)0.f;
+      for (int j = 0; j < CHM; ++j)
+        if (simg[j] < nimg) {
+          if (x_u8) {
+            const long long r = cp_clamp(idx[b0 + simg[j]], nrows);
+            xv[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(x) + r * HWC + ssrc[j]);
+          } else {
+            xb[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(x) + (b0 + simg[j]) * HWC + ssrc[j]);
           }
         }
-      bf16x8 bfr[U][KTMAX];
+#pragma unroll
+      for (int j = 0; j < CHM; ++j)
+        if (simg[j] < nimg) {
+          uint16_t* xs16 = reinterpret_cast<uint16_t*>(xs);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int d = sdst[j] + k * cstep - (((ssplit[j] - k - 1) >> 31) & cwrap);
+            if (x_u8)
+              xs[d] = f2bf((float)((xv[j] >> (8 * k)) & 255u) * scale);
+            else
+              xs16[d] = (uint16_t)(((k < 2 ? xb[j].x : xb[j].y) >> (16 * (k & 1))) & 0xffffu);
+          }
+        }
+    } else {
+      // generic element path (unaligned sources)
+      for (int e = tid; e < nimg * (int)HWC; e += 256) {
+        const int i = e / (int)HWC, r = e - i * (int)HWC;
+        const int y = r / WC, rr = r - y * WC, px = rr / g.C, ch = rr - px * g.C;
+        float v;
+        if (x_u8) {
+          const long long row = cp_clamp(idx[b0 + i], nrows);
+          v = (float)reinterpret_cast<const uint8_t*>(x)[row * HWC + r] * scale;
+        } else {
+          v = (float)reinterpret_cast<const bf16*>(x)[(long long)(b0 + i) * HWC + r];
+        }
+        xs[i * q.xs_img + ch * q.cstr + (y + g.pad) * q.ystr + px + g.pad] = f2bf(v);
+      }
+    }
+    // ---- scatter the routed pooled gradient into the zero dConv image.  Branch-free: an element
+    // whose window max was <= 0 (code bit 2 clear) writes 0 to its own window's pixel.
+#pragma unroll
+    for (int j = 0; j < PC; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t cd = (cvr[j] >> (8 * k)) & 255u;
+        const uint32_t bits = ((k < 2 ? dv[j].x : dv[j].y) >> (16 * (k & 1))) & (0u - ((cd >> 2) & 1u));
+        const uint32_t base = (sbase[j][k >> 1] >> (16 * (k & 1))) & 0xffffu;
+        reinterpret_cast<uint16_t*>(dc)[base + ((cd >> 1) & 1) * q.DWc + (cd & 1)] = (uint16_t)(bits & 0xffffu);
+      }
+    __syncthreads();
+    // ---- shifted copies of the staged rows (copy s = row shifted left by s elements)
+    {
+      auto build_chunk = [&](int src) {
+        const uint4 lo = *reinterpret_cast<const uint4*>(xs + src);
+        const uint4 hi = *reinterpret_cast<const uint4*>(xs + src + 8);
+        const uint32_t d[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+        for (int sc = 1; sc < 8; ++sc) {
+          if (sc < g.KW) {
+            uint4 o;
+            uint32_t* op = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+              const int w0 = m + sc / 2;
+              op[m] = (sc & 1) ? __builtin_amdgcn_alignbyte(d[w0 + 1], d[w0], 2) : d[w0];
+            }
+            *reinterpret_cast<uint4*>(xs + src + sc * q.RowQ) = o;
+          }
+        }
+      };
+      // task = (image, channel, interior row, 8-column chunk c8): reads row[c8, c8+16) and writes
+      // chunk c8 of every copy s = 1..KW-1
+      const int lim = nimg * q.build_per_img;
+      const int per_row = q.RowQ / 8, per_ch = g.H * per_row;
+      const FDiv dimg(max(q.build_per_img, 1)), dch(per_ch), drow(per_row);
+#pragma unroll 1
+      for (int e = tid; e < lim; e += 256) {
+        const int i = dimg.div(e);
+        int r = e - i * q.build_per_img;
+        const int ch = dch.div(r);
+        r -= ch * per_ch;
+        const int y = drow.div(r), c8 = 8 * (r - y * per_row);
+        if (c8 < g.Wp) build_chunk(i * q.xs_img + ch * q.cstr + (y + g.pad) * q.ystr + c8);
+      }
+    }
+    __syncthreads();
+    CP_STAMP(2 + 2 * grp);
+    // ---- MFMA: U chunks per wave iteration, every LDS read issued before the MFMAs
+    const int nchunks = nimg * q.cpi;
+    for (int C0 = wid * U; C0 < nchunks; C0 += 4 * U) {
+      int2 cb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) cb[u] = ctab[min(C0 + u, nchunks - 1)];
+      bf16x8 af[U][NT], bfv[U][KTMAX];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool live = C0 + u < nchunks;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(dc + cb[u].y + aoff[t]);
+          af[u][t] = live ? v : zeros;
+        }
+#pragma unroll
+        for (int t = 0; t < KTMAX; ++t) bfv[u][t] = *reinterpret_cast<const bf16x8*>(xs + cb[u].x + xlane + koff[t]);
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int q = 0; q < KTMAX; ++q)
+        for (int t = 0; t < KTMAX; ++t) {
+          bf16x8 bb = bfv[u][t];
+          if (t == KT - 1) bb = bias_col ? ones : (zero_col ? zeros : bb);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) bfr[u][q][e] = xs[pofs[u][e] + qoff[q]];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int q = 0; q < KTMAX; ++q) {
-          const bf16x8 b = (q == KT - 1 && bias_col) ? ones : bfr[u][q];
-#pragma unroll
-          for (int t = 0; t < NT; ++t) acc[t][q] = mfma16x16x32(afr[u][t], b, acc[t][q]);
+          for (int n = 0; n < NT; ++n) acc[n][t] = mfma16x16x32(af[u][n], bb, acc[n][t]);
         }
     }
-    __syncthreads();  // slots are restaged by the next group
+    __syncthreads();
+    // ---- restore the zero dConv image (same positions as the scatter)
+#pragma unroll
+    for (int j = 0; j < PC; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t cd = (cvr[j] >> (8 * k)) & 255u;
+        dc[((sbase[j][k >> 1] >> (16 * (k & 1))) & 0xffffu) + ((cd >> 1) & 1) * q.DWc + (cd & 1)] = (bf16)0.f;
+      }
+    __syncthreads();  // clean dConv image before the next group's scatter
+    CP_STAMP(3 + 2 * grp);
   }
-  // cross-wave reduction (LDS reused) -> per-block slab [N][K+1]
+  CP_STAMP(30);
+  __syncthreads();  // everything staged is dead now; reuse LDS for the cross-wave reduction
   const int RW = KT * 16;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int q = 0; q < KTMAX; ++q) {
-      if (q < KT) {
+    for (int u = 0; u < KTMAX; ++u) {
+      if (u < KT) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = 16 * t + 4 * (lane >> 4) + r;
-          const int k = 16 * q + (lane & 15);
-          red[(wid * NT * 16 + n) * RW + k] = acc[t][q][r];
+          const int k = 16 * u + (lane & 15);
+          red[(wid * NT * 16 + n) * RW + k] = acc[t][u][r];
         }
       }
     }
@@ -540,11 +690,12 @@ __global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, int vec, 
   float* out = partial + (long long)blockIdx.x * g.N * Kt;
   for (int e = tid; e < g.N * Kt; e += 256) {
     const int n = e / Kt, k = e - (e / Kt) * Kt;
-    float s = 0.f;
+    float sum = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < 4; ++ww) s += red[(ww * NT * 16 + n) * RW + k];
-    out[e] = s;
+    for (int ww = 0; ww < 4; ++ww) sum += red[(ww * NT * 16 + n) * RW + k];
+    out[e] = sum;
   }
+  CP_STAMP(31);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -569,6 +720,7 @@ __global__ void __launch_bounds__(256) convpool_dgrad_kernel(CPGeom g, CPDgrad d
   int* klut = reinterpret_cast<int*>(otab + gtiles);    // [K2pad]
   bf16* qs = reinterpret_cast<bf16*>(smem + round_up((gtiles * 18 + d.K2pad) * 4, 16));  // [imgs][Hq][Wq][N]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  CP_STAMP(0);
   const int npool = g.PH * g.PW;
   for (int e = tid; e < gtiles * 16; e += 256) {
     const int T = e >> 4, i = T / tpi, tw = T - (T / tpi) * tpi;
@@ -632,7 +784,9 @@ __global__ void __launch_bounds__(256) convpool_dgrad_kernel(CPGeom g, CPDgrad d
   }
   const int rowq = d.Wq * d.Nq;
   uint32_t cv[PC];
-  for (int b0 = blockIdx.x * g.imgs; b0 < g.B; b0 += gridDim.x * g.imgs) {
+  CP_STAMP(1);
+  int grp = 0;
+  for (int b0 = blockIdx.x * g.imgs; b0 < g.B; b0 += gridDim.x * g.imgs, ++grp) {
     const int nimg = min(g.imgs, g.B - b0);
     const long long o0 = (long long)b0 * wn;
     const int ntot = nimg * wn;
@@ -674,6 +828,7 @@ __global__ void __launch_bounds__(256) convpool_dgrad_kernel(CPGeom g, CPDgrad d
       }
     }
     __syncthreads();
+    CP_STAMP(2 + 3 * grp);
     const int ntiles = nimg * tpi;
     bf16* xg = dx + (long long)b0 * HW * g.C;
     for (int T0 = wid * U; T0 < ntiles; T0 += 4 * U) {
@@ -718,6 +873,7 @@ __global__ void __launch_bounds__(256) convpool_dgrad_kernel(CPGeom g, CPDgrad d
       }
     }
     __syncthreads();
+    CP_STAMP(3 + 3 * grp);
     // restore the zero image: clear exactly the positions scattered above
     if (CHM > 0) {
 #pragma unroll
@@ -741,7 +897,9 @@ __global__ void __launch_bounds__(256) convpool_dgrad_kernel(CPGeom g, CPDgrad d
       }
     }
     __syncthreads();
+    CP_STAMP(4 + 3 * grp);
   }
+  CP_STAMP(31);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -894,6 +1052,7 @@ static const FwdLayout& choose_fwd_layout(const CPGeom& g0) {
 static CPGeom make_geom(int B, int H, int W, int C, int KH, int KW, int pad, int N) {
   CPGeom g{};
   g.dbg = g_cp_debug;
+  g.stamps = g_cp_stamps;
   g.B = B; g.H = H; g.W = W; g.C = C; g.KH = KH; g.KW = KW; g.pad = pad; g.N = N;
   g.OH = H + 2 * pad - KH + 1;
   g.OW = W + 2 * pad - KW + 1;
@@ -922,6 +1081,8 @@ void convpool_fwd_layout(int H, int W, int C, int KH, int KW, int pad, int N, in
 bool convpool_supported(int H, int W, int C, int KH, int KW, int pad, int N) {
   CPGeom g = make_geom(1, H, W, C, KH, KW, pad, N);
   if (g.OH <= 0 || g.OW <= 0 || (g.OH & 1) || (g.OW & 1)) return false;
+  if ((g.PH * g.PW * N) % 4 != 0) return false;  // 4-element pooled-gradient chunks (wgrad scatter plan)
+  if (g.PH * g.PW * N > kStageChunks * 1024) return false;  // one image's pooled gradient fits the plan
   if (C > 16 || N > 32 || KH > 7 || KW > 7) return false;
   if (g.Kpad2 / 32 > 16) return false;                    // fwd weight fragments in registers
   if ((g.K + 16) / 16 > 13) return false;                 // wgrad accumulators (incl. bias column)
@@ -1034,23 +1195,58 @@ hipError_t convpool_fwd(const void* x, int x_u8, const long long* idx, long long
 #undef CP_FWD
 }
 
+static CPWg make_wg(const CPGeom& g) {
+  CPWg q{};
+  // lane-group split G (chunk = 4/G rows x 8G columns) minimising the padded pixel count
+  int best = 1 << 30;
+  for (int G : {1, 2, 4}) {
+    const int R = 4 / G;
+    const int n = cdiv(g.OH, R) * cdiv(g.OW, 8 * G);
+    if (n < best) {
+      best = n;
+      q.G = G;
+    }
+  }
+  q.R = 4 / q.G;
+  q.OHc = round_up(g.OH, q.R);
+  q.OWc = round_up(g.OW, 8 * q.G);
+  q.cpr = q.OHc / q.R;
+  q.cpc = q.OWc / (8 * q.G);
+  q.cpi = q.cpr * q.cpc;
+  // X copies: rows oy+ky < OHc+KH-1; reads ox0..ox0+7 < OWc; build slack: copy 0 keeps >= 8 zero
+  // elements after the padded row.  Odd 16-byte counts spread copies / rows / channels over banks.
+  auto odd16 = [](int elems) { return ((elems / 8) % 2 == 0) ? elems + 8 : elems; };
+  q.Hq = max(q.OHc + g.KH - 1, g.Hp);
+  q.RowQ = odd16(round_up(max(q.OWc, g.Wp + 8), 8));
+  q.ystr = odd16(g.KW * q.RowQ);
+  q.cstr = odd16(q.Hq * q.ystr);
+  q.xs_img = g.C * q.cstr;
+  q.DWc = odd16(q.OWc);
+  q.dcs = odd16(q.OHc * q.DWc);
+  q.dc_img = (g.N + 1) * q.dcs;
+  q.build_per_img = g.KW > 1 ? g.C * g.H * (q.RowQ / 8) : 0;
+  return q;
+}
+
 template <int NT, int KTMAX>
 static hipError_t launch_cp_wgrad(CPGeom g, bool vec, const void* x, int x_u8, const long long* idx, long long nrows,
                                   float scale, const bf16* dp, const uint8_t* code, float* gw, float* gb,
                                   float* workspace, size_t ws_floats, hipStream_t st) {
   auto kern = convpool_wgrad_kernel<NT, KTMAX, kStageChunks>;
+  const CPWg q = make_wg(g);
   const int Kt = g.K + 1;
   const int KT = cdiv(Kt, 16);
-  const int npool = g.PH * g.PW;
-  const int cpi = cdiv(npool, 8);
+  const int wn = g.PH * g.PW * g.N;
   const size_t red_bytes = (size_t)4 * NT * 16 * KT * 16 * 4;
-  Sizing z = size_persistent(reinterpret_cast<const void*>(kern), g.B, (size_t)KT * 64 + 64,
-                             (size_t)cpi * 136 + (size_t)g.img_elems * 2 + (size_t)npool * g.N * 3 + 48, red_bytes,
-                             kStageChunks * 256 * 4 / (g.H * g.W * g.C));
+  // caps: register staging plans (image chunks, 2x pooled chunks per thread)
+  int cap = min(kStageChunks * 256 * 4 / (g.H * g.W * g.C), kStageChunks * 256 * 4 / wn);
+  cap = min(cap, 65535 / q.dc_img);  // scatter offsets are packed as 16 bits
+  Sizing z = size_persistent(reinterpret_cast<const void*>(kern), g.B, 64,
+                             (size_t)q.cpi * 8 + ((size_t)q.xs_img + q.dc_img) * 2 + 16, red_bytes, max(cap, 1));
   while ((size_t)z.grid * g.N * Kt > ws_floats && z.grid > 1) z.grid /= 2;
   if ((size_t)z.grid * g.N * Kt > ws_floats || z.lds > 160 * 1024) return hipErrorInvalidValue;
   g.imgs = z.imgs;
-  hipLaunchKernelGGL(kern, dim3(z.grid), dim3(256), z.lds, st, g, (int)vec, x, x_u8, idx, nrows, scale, dp, code,
+  hipLaunchKernelGGL(kern, dim3(z.grid), dim3(256), z.lds, st, g, q, (int)vec, x, x_u8, idx, nrows, scale, dp, code,
                      workspace);
   DFA_HIP_CHECK(hipGetLastError());
   return slab_reduce(workspace, gw, gb, g.N, g.K, Kt, z.grid, 1.f, st);
@@ -1064,8 +1260,10 @@ hipError_t convpool_wgrad(const void* x, int x_u8, const long long* idx, long lo
   const int KT = cdiv(g.K + 1, 16);
   const int NT = cdiv(N, 16);
   const int npool = g.PH * g.PW;
-  const bool vec = stage_vec_ok(g, x, x_u8) && (npool * N) % 4 == 0 &&
-                   reinterpret_cast<uintptr_t>(dp) % 8 == 0 && reinterpret_cast<uintptr_t>(code) % 4 == 0;
+  if (reinterpret_cast<uintptr_t>(dp) % 8 != 0 || reinterpret_cast<uintptr_t>(code) % 4 != 0)
+    return hipErrorInvalidValue;  // pooled gradient / codes are read as 4-element chunks
+  (void)npool;
+  const bool vec = stage_vec_ok(g, x, x_u8);
 #define CP_WG(NT_, KT_) return launch_cp_wgrad<NT_, KT_>(g, vec, x, x_u8, idx, nrows, scale, dp, code, gw, gb, workspace, ws_floats, st)
   if (NT == 1) {
     if (KT <= 2) CP_WG(1, 2);

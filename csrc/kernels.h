@@ -105,9 +105,10 @@ struct HeadArgs {
   int nblocks, wg_tiles;
 };
 size_t head_train_lds(const HeadArgs& a);
-hipError_t head_train(HeadArgs a, hipStream_t st);
+hipError_t head_train(HeadArgs a, int phases, hipStream_t st);  // phases: 1 fwd/CE/bwd-data, 2 wgrad
 
 void convpool_set_debug(int mask);
+void convpool_set_stamps(void* buf);  // [grid][32] uint64 s_memtime stamps, nullptr = off
 // forward weight layout: [Npad16][Kpad2], column ky*round8(KW*Cp) + kx*Cp + c (zero for c >= C)
 void convpool_fwd_layout(int H, int W, int C, int KH, int KW, int pad, int N, int* Cp, int* Kpad2);
 bool convpool_supported(int H, int W, int C, int KH, int KW, int pad, int N);

@@ -343,19 +343,26 @@ size_t head_train_lds(const HeadArgs& a) {
   return bytes + HR * 16 * 4;
 }
 
-hipError_t head_train(HeadArgs a, hipStream_t st) {
-  if (a.nl < 1 || a.nl > kHeadMaxLayers || a.L[a.nl - 1].N > 16) return hipErrorInvalidValue;
+static void head_prepare(HeadArgs& a) {
   a.nblocks = cdiv(a.B, HR);
   a.wg_tiles = 0;
   for (int l = 0; l < a.nl; ++l) {
     a.L[l].tiles = cdiv(a.L[l].N, 16) * cdiv(a.L[l].K + 1, 16);
     a.wg_tiles += a.L[l].tiles;
   }
-  const size_t lds = head_train_lds(a);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(head_train_kernel, dim3(a.nblocks), dim3(256), lds, st, a);
-  DFA_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(head_wgrad_kernel, dim3(a.wg_tiles + 1), dim3(256), 0, st, a);
+}
+
+// phase bit 1: forward + CE + backward data chain; bit 2: weight gradients + loss reduction
+hipError_t head_train(HeadArgs a, int phases, hipStream_t st) {
+  if (a.nl < 1 || a.nl > kHeadMaxLayers || a.L[a.nl - 1].N > 16) return hipErrorInvalidValue;
+  head_prepare(a);
+  if (phases & 1) {
+    const size_t lds = head_train_lds(a);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(head_train_kernel, dim3(a.nblocks), dim3(256), lds, st, a);
+    DFA_HIP_CHECK(hipGetLastError());
+  }
+  if (phases & 2) hipLaunchKernelGGL(head_wgrad_kernel, dim3(a.wg_tiles + 1), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

@@ -63,6 +63,17 @@ class Layer:
     def backward(self, dy):
         raise NotImplementedError
 
+    # Layers that can separate their weight gradient from their data gradient set split_backward;
+    # the engine then runs backward_weights on a side stream, concurrently with the data-gradient
+    # chain of the layers below (backward == backward_weights + backward_data).
+    split_backward = False
+
+    def backward_weights(self, dy):
+        raise NotImplementedError
+
+    def backward_data(self, dy):
+        raise NotImplementedError
+
     def config(self) -> dict:
         return {}
 
@@ -503,12 +514,15 @@ class FusedConvPool(Layer):
         sp[0].row_cp = ops.convpool_fwd_layout(H, W, C, self.k, self.k, self.pad, self.conv.filters)[0]
         return sp
 
+    split_backward = True
+
     def alloc(self, B, device, dtype, ws):
         self.out = torch.empty((B,) + self.out_shape, device=device, dtype=dtype)
         self.code = torch.empty((B,) + self.out_shape, device=device, dtype=torch.uint8)
         if self.need_dx:
             self.dx = torch.empty((B,) + self.in_shape, device=device, dtype=dtype)
-        self.ws = ws
+        # private split-m slab workspace: this layer's weight gradient may run concurrently with others
+        self.ws_wgrad = torch.empty(1 << 22, dtype=torch.float32, device=device) if device.type == "cuda" else ws.wgrad
 
     def forward(self, x, training):
         self.x = x
@@ -517,15 +531,24 @@ class FusedConvPool(Layer):
         ops.convpool_fwd(x, st.weight(f"{self.name}/kernel"), b, self.out, self.code, self.k, self.k, self.pad)
         return self.out
 
-    def backward(self, dy):
+    def backward_weights(self, dy):
         st = self.store
         kn = f"{self.name}/kernel"
         gb = st.gradient(f"{self.name}/bias") if self.use_bias else None
-        dp = dy.reshape(self.out.shape)
-        ops.convpool_wgrad(self.x, dp, self.code, st.grad_matrix(kn), gb, self.ws.wgrad, self.k, self.k, self.pad)
+        ops.convpool_wgrad(self.x, dy.reshape(self.out.shape), self.code, st.grad_matrix(kn), gb, self.ws_wgrad,
+                           self.k, self.k, self.pad)
+
+    def backward_data(self, dy):
         if not self.need_dx:
             return None
-        ops.convpool_dgrad(dp, self.code, st.weight(kn), st.weight_t(kn), self.dx, self.k, self.k, self.pad)
+        st = self.store
+        kn = f"{self.name}/kernel"
+        ops.convpool_dgrad(dy.reshape(self.out.shape), self.code, st.weight(kn), st.weight_t(kn), self.dx, self.k,
+                           self.k, self.pad)
         if self.in_relu:
             ops.relu_bwd(self.x, self.dx, self.dx)
         return self.dx
+
+    def backward(self, dy):
+        self.backward_weights(dy)
+        return self.backward_data(dy)

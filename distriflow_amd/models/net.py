@@ -56,6 +56,9 @@ class Net:
                 self.has_dropout = True
         self._bound_B = None
         self.graphs: dict = {}
+        # side streams for weight gradients that run concurrently with the data-gradient chain
+        self.concurrent_backward = False  # measured: cross-stream joins cost more than the overlap wins (LeNet-5)
+        self._side = [torch.cuda.Stream(device=self.device) for _ in range(3)] if self.is_gpu else []
 
     # ------------------------------------------------------------------ planning / fusion
     def _plan(self):
@@ -235,7 +238,7 @@ class Net:
             lab, idx = (labels if labels.dtype == torch.int32 else labels.to(torch.int32)), None
         st = self.store
         first = head[0]
-        ops.head_train(
+        args = dict(
             w=[st.weight(f"{l.name}/kernel") for l in head],
             wt=[st.weight_t(f"{l.name}/kernel") for l in head],
             b=[st[f"{l.name}/bias"] if l.use_bias else None for l in head],
@@ -245,15 +248,46 @@ class Net:
             x=h, x_relu=first.in_relu, xT=self.head_xT, dx=first.dx if first.need_dx else None,
             logits=head[-1].out, labels=lab, idx=idx, grad_scale=1.0 / x.shape[0],
             loss_part=self.head_loss_part, stats=self.stats)
-        for l in head:  # keep the per-layer views coherent for evaluate()/introspection
-            l.x = None
-        if grad_ready is not None:
-            for i in range(len(self.exec_layers) - 1, self.head_start - 1, -1):
-                grad_ready(i)
-        d = first.dx if first.need_dx else None
-        for i in range(self.head_start - 1, -1, -1):
-            d = self.exec_layers[i].backward(d)
+        head_ids = range(len(self.exec_layers) - 1, self.head_start - 1, -1)
+        if not self.concurrent_backward:
+            ops.head_train(**args, phases=3)
             if grad_ready is not None:
+                for i in head_ids:
+                    grad_ready(i)
+            d = first.dx if first.need_dx else None
+            for i in range(self.head_start - 1, -1, -1):
+                d = self.exec_layers[i].backward(d)
+                if grad_ready is not None:
+                    grad_ready(i)
+            return self.stats
+        # critical path on the main stream: head fwd/CE/bwd-data -> each body layer's data gradient;
+        # weight gradients fork onto side streams as soon as their input gradient exists.  Gradient
+        # hooks (bucketed all-reduce) fire after the join: a bucket spans layers whose gradients
+        # complete on different streams.
+        main = torch.cuda.current_stream(self.device)
+        ops.head_train(**args, phases=1)
+        ev = main.record_event()
+        side = self._side
+        side[0].wait_event(ev)
+        with torch.cuda.stream(side[0]):
+            ops.head_train(**args, phases=2)
+        d = first.dx if first.need_dx else None
+        k = 1
+        for i in range(self.head_start - 1, -1, -1):
+            l = self.exec_layers[i]
+            if l.split_backward:
+                s = side[k]
+                k = 1 + (k % (len(side) - 1))
+                s.wait_event(main.record_event())
+                with torch.cuda.stream(s):
+                    l.backward_weights(d)
+                d = l.backward_data(d)
+            else:
+                d = l.backward(d)
+        for s in side:
+            main.wait_stream(s)
+        if grad_ready is not None:
+            for i in range(len(self.exec_layers) - 1, -1, -1):
                 grad_ready(i)
         return self.stats
 

@@ -268,12 +268,14 @@ def head_supported() -> bool:
 
 
 def head_train(w, wt, b, gw, gb, hT, dzT, K, N, x, x_relu, xT, dx, logits, labels, idx, grad_scale, loss_part,
-               stats):
+               stats, phases=3):
     """Fused dense head on GPU (csrc/mlphead.hip): forward + softmax-CE + backward of a Dense chain.
-    Writes gw/gb (per-layer gradients, batch-mean scaled via grad_scale), dx, logits, stats."""
+    phases bit 1: forward, loss, backward data chain (dx, logits, H^T/dZ^T); bit 2: weight/bias
+    gradients gw/gb (batch-mean scaled via grad_scale) and stats.  Each phase is one launch on the
+    current stream, so the two can be placed on different streams."""
     _C().head_train(list(w), list(wt), list(b), list(gw), list(gb), list(hT), list(dzT), list(K), list(N),
                     x.reshape(x.shape[0], -1) if x.is_contiguous() else x.contiguous().reshape(x.shape[0], -1),
-                    bool(x_relu), xT, dx, logits, labels, idx, float(grad_scale), loss_part, stats)
+                    bool(x_relu), xT, dx, logits, labels, idx, float(grad_scale), loss_part, stats, int(phases))
 
 
 def convpool_supported(H, W, C, KH, KW, pad, N) -> bool:

@@ -346,7 +346,7 @@ def test_fused_head_matches_autograd(B, dims, with_idx, x_relu):
     stats = torch.zeros(2, device=dev)
     O.head_train([_pad_w(w) for w in ws], [_pad_wt(w, w.shape[0], 1, w.shape[1]) for w in ws], bs, gw, gb, hT, dzT,
                  list(dims[:-1]), list(dims[1:]), x, x_relu, xT, dx, logits,
-                 all_labels if with_idx else y, idx, 1.0 / B, loss_part, stats)
+                 all_labels if with_idx else y, idx, 1.0 / B, loss_part, stats, phases=3)
     # fp32 reference
     xr = x.float().requires_grad_(True)
     wr = [w.clone().requires_grad_(True) for w in ws]
