@@ -123,12 +123,13 @@ struct ImgPlan {
 template <int CHM>
 __device__ __forceinline__ void make_img_plan(ImgPlan<CHM>& pl, const CPGeom& g, int row_stride, int cp) {
   const int WC = g.W * g.C, cpr = WC / 4, cpi = g.H * cpr;
+  const FDiv dcpi(cpi), dcpr(cpr), dC(g.C);
 #pragma unroll
   for (int j = 0; j < CHM; ++j) {
     const int c = threadIdx.x + 256 * j;
-    const int i = c / cpi, r = c - (c / cpi) * cpi;
-    const int y = r / cpr, x4 = 4 * (r - (r / cpr) * cpr);
-    const int px = x4 / g.C, ch = x4 - px * g.C;
+    const int i = dcpi.div(c), r = c - i * cpi;
+    const int y = dcpr.div(r), x4 = 4 * (r - y * cpr);
+    const int px = dC.div(x4), ch = x4 - px * g.C;
     pl.img[j] = c < g.imgs * cpi ? i : (1 << 20);
     pl.soff[j] = y * WC + x4;
     pl.doff[j] = (y + g.pad) * row_stride + (g.pad + px) * cp + ch;
@@ -142,14 +143,17 @@ __device__ __forceinline__ void stage_plan(bf16* xs, int img_stride, const ImgPl
                                            float scale, int b0, int nimg, int cp) {
   const long long HWC = (long long)g.H * g.W * g.C;
   const int gap = cp - g.C;
+  // loads are unconditional (clamped image slot): a load under a branch makes hipcc wait vmcnt(0)
+  // right after it, serialising the group's loads
   if (x_u8) {
+    long long r[CHM];
+#pragma unroll
+    for (int j = 0; j < CHM; ++j) r[j] = idx[b0 + min(pl.img[j], nimg - 1)];
     uint32_t v[CHM];
 #pragma unroll
     for (int j = 0; j < CHM; ++j)
-      if (pl.img[j] < nimg) {
-        const long long r = cp_clamp(idx[b0 + pl.img[j]], nrows);
-        v[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(x) + r * HWC + pl.soff[j]);
-      }
+      v[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(x) + cp_clamp(r[j], nrows) * HWC +
+                                                pl.soff[j]);
 #pragma unroll
     for (int j = 0; j < CHM; ++j)
       if (pl.img[j] < nimg) {
@@ -162,8 +166,8 @@ __device__ __forceinline__ void stage_plan(bf16* xs, int img_stride, const ImgPl
     uint2 v[CHM];
 #pragma unroll
     for (int j = 0; j < CHM; ++j)
-      if (pl.img[j] < nimg)
-        v[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(x) + (b0 + pl.img[j]) * HWC + pl.soff[j]);
+      v[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(x) + (b0 + min(pl.img[j], nimg - 1)) * HWC +
+                                             pl.soff[j]);
 #pragma unroll
     for (int j = 0; j < CHM; ++j)
       if (pl.img[j] < nimg) {
@@ -225,16 +229,17 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
   if (g.dbg & 16) return;
 
   // ---- once per workgroup: tables, zero-bordered image slots, register-resident weights
+  const FDiv dtpi(tpi), dPW(g.PW), dG(g.G);
   for (int e = tid; e < gtiles * 16; e += 256) {
     const int T = e >> 4, row = e & 15;
-    const int i = T / tpi, tw = T - (T / tpi) * tpi;
+    const int i = dtpi.div(T), tw = T - i * tpi;
     const int wg = tw * 4 + (row >> 2), j = row & 3;
     int v = i * g.xs_img;
     if (wg < npool) {
-      const int py = wg / g.PW, px = wg - py * g.PW;
+      const int py = dPW.div(wg), px = wg - py * g.PW;
       const int oy = 2 * py + (j >> 1), ox = 2 * px + (j & 1);
       const int t0 = ox * g.Cp, sh = t0 & 7;
-      v += oy * g.ystr + (sh / g.G) * g.RowP + (t0 - sh);
+      v += oy * g.ystr + dG.div(sh) * g.RowP + (t0 - sh);
     }
     ttab[e] = v;
     if (row == 0) wtab[T] = make_int2(i * npool + tw * 4, npool - tw * 4);
@@ -261,12 +266,13 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
     bv[t] = (bias && n < g.N) ? bias[n] : 0.f;
   }
   int koff[NK];
+  const FDiv dchunks(g.chunks);
 #pragma unroll
   for (int s = 0; s < NK; ++s) {
     const int q = 4 * s + (lane >> 4);  // 8-slot group of this lane in k-step s
     int v = 0;
     if (s < nk && q < g.KH * g.chunks) {
-      const int ky = q / g.chunks;
+      const int ky = dchunks.div(q);
       v = ky * g.ystr + 8 * (q - ky * g.chunks);
     }
     koff[s] = v;
@@ -277,14 +283,16 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
   const int cpr = g.RowP / 8;
   const int per_img = g.H * (g.S - 1) * cpr;
   int bsrc[BT], bdst[BT], blim[BT];
+  const FDiv dpimg(max(per_img, 1)), dprow(max((g.S - 1) * cpr, 1)), dcpr(cpr);
 #pragma unroll
   for (int j = 0; j < BT; ++j) {
     const int e = tid + 256 * j;
-    const int i = e / max(per_img, 1);
+    const int i = dpimg.div(e);
     int r = e - i * per_img;
-    const int y = r / max((g.S - 1) * cpr, 1);
+    const int y = dprow.div(r);
     r -= y * ((g.S - 1) * cpr);
-    const int ci = 1 + r / cpr, c8 = 8 * (r - (r / cpr) * cpr), sh = ci * g.G;
+    const int q8 = dcpr.div(r);
+    const int ci = 1 + q8, c8 = 8 * (r - q8 * cpr), sh = ci * g.G;
     const int row = i * g.xs_img + (y + g.pad) * g.ystr;
     bsrc[j] = row + c8 + sh;
     bdst[j] = row + ci * g.RowP + c8;
@@ -523,36 +531,62 @@ __global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, CPWg q, i
     zeros[e] = (bf16)0.f;
   }
   CP_STAMP(1);
-  int grp = 0;
-  for (int b0 = blockIdx.x * g.imgs; b0 < g.B; b0 += gridDim.x * g.imgs, ++grp) {
-    const int nimg = min(g.imgs, g.B - b0);
-    const long long o0 = (long long)b0 * wn;
-    const int nch = nimg * wn / 4;
-    const long long HWC = (long long)g.H * WC;
-    // ---- issue every global load of the group first: pooled grads + codes, image chunks
-    uint2 dv[PC];  // (nch <= PC*256: imgs is capped by the host)
+  // ---- software pipeline over groups: group g+1's global loads are issued right after group g's
+  // data has been written to LDS, so their latency overlaps g's copy build and MFMA phase.  The
+  // dataset row indices run one more group ahead (index -> row is a dependent load).
+  const long long HWC = (long long)g.H * WC;
+  const int gstride = gridDim.x * g.imgs;
+  uint32_t cvn[PC];
+  uint2 dvn[PC], xbn[CHM];
+  uint32_t xvn[CHM];
+  long long rown[CHM];
+  // All loads below are UNconditional (clamped addresses): a load under a branch makes hipcc wait
+  // vmcnt(0) right after it, serialising the whole group's loads.  Validity is applied at use.
+  auto load_rows = [&](int b0n) {  // raw dataset row index per staging chunk of group b0n
+    const int bl = min(b0n, g.B - 1);
+    const int nl = min(g.imgs, g.B - bl);
+#pragma unroll
+    for (int j = 0; j < CHM; ++j) rown[j] = x_u8 ? idx[bl + min(simg[j], nl - 1)] : 0;
+  };
+  auto issue_loads = [&](int b0n) {
+    const int nimg_n = min(g.imgs, g.B - b0n);
+    const long long o0n = (long long)b0n * wn;
+    const int nch_n = nimg_n * wn / 4;
 #pragma unroll
     for (int j = 0; j < PC; ++j) {
-      const int c = tid + 256 * j;
-      cvr[j] = 0;
-      if (c < nch) {
-        cvr[j] = *reinterpret_cast<const uint32_t*>(code + o0 + 4 * c);
-        dv[j] = *reinterpret_cast<const uint2*>(dp + o0 + 4 * c);
-      }
+      const int c = min(tid + 256 * j, nch_n - 1);
+      cvn[j] = *reinterpret_cast<const uint32_t*>(code + o0n + 4 * c);
+      dvn[j] = *reinterpret_cast<const uint2*>(dp + o0n + 4 * c);
     }
     if (vec) {
-      uint32_t xv[CHM];
-      uint2 xb[CHM];
 #pragma unroll
-      for (int j = 0; j < CHM; ++j)
-        if (simg[j] < nimg) {
-          if (x_u8) {
-            const long long r = cp_clamp(idx[b0 + simg[j]], nrows);
-            xv[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(x) + r * HWC + ssrc[j]);
-          } else {
-            xb[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(x) + (b0 + simg[j]) * HWC + ssrc[j]);
-          }
-        }
+      for (int j = 0; j < CHM; ++j) {
+        const int im = min(simg[j], nimg_n - 1);
+        if (x_u8)
+          xvn[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(x) +
+                                                       cp_clamp(rown[j], nrows) * HWC + ssrc[j]);
+        else
+          xbn[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(x) + (b0n + im) * HWC + ssrc[j]);
+      }
+    }
+  };
+  int grp = 0;
+  {
+    const int b0s = blockIdx.x * g.imgs;
+    load_rows(b0s);
+    if (b0s < g.B) issue_loads(b0s);
+    load_rows(b0s + gstride);
+  }
+  for (int b0 = blockIdx.x * g.imgs; b0 < g.B; b0 += gstride, ++grp) {
+    const int nimg = min(g.imgs, g.B - b0);
+    const int nch = nimg * wn / 4;
+    uint2 dv[PC];
+#pragma unroll
+    for (int j = 0; j < PC; ++j) {  // chunks past the group carry no gradient (code 0)
+      cvr[j] = tid + 256 * j < nch ? cvn[j] : 0u;
+      dv[j] = dvn[j];
+    }
+    if (vec) {
 #pragma unroll
       for (int j = 0; j < CHM; ++j)
         if (simg[j] < nimg) {
@@ -561,9 +595,9 @@ __global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, CPWg q, i
           for (int k = 0; k < 4; ++k) {
             const int d = sdst[j] + k * cstep - (((ssplit[j] - k - 1) >> 31) & cwrap);
             if (x_u8)
-              xs[d] = f2bf((float)((xv[j] >> (8 * k)) & 255u) * scale);
+              xs[d] = f2bf((float)((xvn[j] >> (8 * k)) & 255u) * scale);
             else
-              xs16[d] = (uint16_t)(((k < 2 ? xb[j].x : xb[j].y) >> (16 * (k & 1))) & 0xffffu);
+              xs16[d] = (uint16_t)(((k < 2 ? xbn[j].x : xbn[j].y) >> (16 * (k & 1))) & 0xffffu);
           }
         }
     } else {
@@ -592,6 +626,9 @@ __global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, CPWg q, i
         const uint32_t base = (sbase[j][k >> 1] >> (16 * (k & 1))) & 0xffffu;
         reinterpret_cast<uint16_t*>(dc)[base + ((cd >> 1) & 1) * q.DWc + (cd & 1)] = (uint16_t)(bits & 0xffffu);
       }
+    // ---- prefetch: next group's loads (rows already known), then the row indices one further
+    if (b0 + gstride < g.B) issue_loads(b0 + gstride);
+    load_rows(b0 + 2 * gstride);
     __syncthreads();
     // ---- shifted copies of the staged rows (copy s = row shifted left by s elements)
     {
@@ -722,21 +759,23 @@ __global__ void __launch_bounds__(256) convpool_dgrad_kernel(CPGeom g, CPDgrad d
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   CP_STAMP(0);
   const int npool = g.PH * g.PW;
+  const FDiv dtpi(tpi), dW(g.W);
   for (int e = tid; e < gtiles * 16; e += 256) {
-    const int T = e >> 4, i = T / tpi, tw = T - (T / tpi) * tpi;
+    const int T = e >> 4, i = dtpi.div(T), tw = T - i * tpi;
     const int px = tw * 16 + (e & 15);
     int v = i * d.q_elems;
     if (px < HW) {
-      const int iy = px / g.W, ix = px - (px / g.W) * g.W;
+      const int iy = dW.div(px), ix = px - iy * g.W;
       v += (iy * d.Wq + ix) * d.Nq;
     }
     ttab[e] = v;
     if ((e & 15) == 0) otab[T] = make_int2(i * HW + tw * 16, HW - tw * 16);
   }
+  const FDiv dNk(g.N), dKWk(g.KW);
   for (int k = tid; k < d.K2pad; k += 256) {
     int v = 0;
     if (k < d.K2) {
-      const int n = k % g.N, t = k / g.N, ky = t / g.KW, kx = t - ky * g.KW;
+      const int t = dNk.div(k), n = k - t * g.N, ky = dKWk.div(t), kx = t - ky * g.KW;
       v = ((g.KH - 1 - ky) * d.Wq + (g.KW - 1 - kx)) * d.Nq + n;
     }
     klut[k] = v;
@@ -771,14 +810,15 @@ __global__ void __launch_bounds__(256) convpool_dgrad_kernel(CPGeom g, CPDgrad d
   constexpr int PC = CHM > 0 ? CHM : 1;
   int sbase[PC][4];
   if (CHM > 0) {
+    const FDiv dwn(wn), dN(g.N), dPW(g.PW);
 #pragma unroll
     for (int j = 0; j < PC; ++j)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int e = 4 * (tid + 256 * j) + k;
-        const int i = e / wn, r = e - (e / wn) * wn;
-        const int wg = r / g.N, c = r - (r / g.N) * g.N;
-        const int py = wg / g.PW, px = wg - (wg / g.PW) * g.PW;
+        const int i = dwn.div(e), r = e - i * wn;
+        const int wg = dN.div(r), c = r - wg * g.N;
+        const int py = dPW.div(wg), px = wg - py * g.PW;
         sbase[j][k] = i * d.q_elems + ((2 * py + d.P) * d.Wq + 2 * px + d.P) * d.Nq + c;
       }
   }
@@ -794,14 +834,14 @@ __global__ void __launch_bounds__(256) convpool_dgrad_kernel(CPGeom g, CPDgrad d
       const int nch = ntot / 4;
       uint2 dv[PC];
 #pragma unroll
-      for (int j = 0; j < PC; ++j) {
-        const int c = tid + 256 * j;
-        cv[j] = 0;
-        if (c < nch) {
-          cv[j] = *reinterpret_cast<const uint32_t*>(code + o0 + 4 * c);
-          dv[j] = *reinterpret_cast<const uint2*>(dp + o0 + 4 * c);
-        }
+      for (int j = 0; j < PC; ++j) {  // unconditional (clamped) loads; validity applied at use
+        const int c = min(tid + 256 * j, nch - 1);
+        cv[j] = *reinterpret_cast<const uint32_t*>(code + o0 + 4 * c);
+        dv[j] = *reinterpret_cast<const uint2*>(dp + o0 + 4 * c);
       }
+#pragma unroll
+      for (int j = 0; j < PC; ++j)
+        if (tid + 256 * j >= nch) cv[j] = 0;
 #pragma unroll
       for (int j = 0; j < PC; ++j)
 #pragma unroll
