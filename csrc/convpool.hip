@@ -626,10 +626,13 @@ __global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, CPWg q, i
         const uint32_t base = (sbase[j][k >> 1] >> (16 * (k & 1))) & 0xffffu;
         reinterpret_cast<uint16_t*>(dc)[base + ((cd >> 1) & 1) * q.DWc + (cd & 1)] = (uint16_t)(bits & 0xffffu);
       }
+    if (grp == 1) CP_STAMP(20);
     // ---- prefetch: next group's loads (rows already known), then the row indices one further
     if (b0 + gstride < g.B) issue_loads(b0 + gstride);
     load_rows(b0 + 2 * gstride);
+    if (grp == 1) CP_STAMP(21);
     __syncthreads();
+    if (grp == 1) CP_STAMP(22);
     // ---- shifted copies of the staged rows (copy s = row shifted left by s elements)
     {
       auto build_chunk = [&](int src) {
@@ -665,6 +668,7 @@ __global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, CPWg q, i
         if (c8 < g.Wp) build_chunk(i * q.xs_img + ch * q.cstr + (y + g.pad) * q.ystr + c8);
       }
     }
+    if (grp == 1) CP_STAMP(23);
     __syncthreads();
     CP_STAMP(2 + 2 * grp);
     // ---- MFMA: U chunks per wave iteration, every LDS read issued before the MFMAs

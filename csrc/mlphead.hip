@@ -22,6 +22,7 @@
 namespace dfa {
 
 constexpr int HR = 16;  // batch rows per workgroup of the train kernel
+constexpr int HW = 16;  // waves per workgroup (both kernels): tiles of a layer spread over 16 waves
 
 __device__ __forceinline__ bf16x8 ld16(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
@@ -35,7 +36,7 @@ __device__ __forceinline__ void head_gemm_fwd(const bf16* A, int lda, const bf16
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int ks = Kpad / 32;
   const int ntiles = (N + 15) / 16;
-  for (int t = wid; t < ntiles; t += 4) {
+  for (int t = wid; t < ntiles; t += HW) {
     const int n = 16 * t + (lane & 15);
     const bf16* wrow = W + (long long)n * Kpad + 8 * (lane >> 4);
     const bf16* arow = A + (lane & 15) * lda + 8 * (lane >> 4);
@@ -78,7 +79,7 @@ __device__ __forceinline__ void head_gemm_bwd(const bf16* dZ, int ldz, const bf1
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int ks = ldwt / 32;
   const int ktiles = (K + 15) / 16;
-  for (int t = wid; t < ktiles; t += 4) {
+  for (int t = wid; t < ktiles; t += HW) {
     const int j = 16 * t + (lane & 15);
     const bf16* wrow = Wt + (long long)j * ldwt + 8 * (lane >> 4);
     const bf16* zrow = dZ + (lane & 15) * ldz + 8 * (lane >> 4);
@@ -110,7 +111,7 @@ __device__ __forceinline__ void head_gemm_bwd(const bf16* dZ, int ldz, const bf1
   }
 }
 
-__global__ void __launch_bounds__(256) head_train_kernel(HeadArgs a) {
+__global__ void __launch_bounds__(1024) head_train_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * HR;
@@ -138,7 +139,7 @@ __global__ void __launch_bounds__(256) head_train_kernel(HeadArgs a) {
   // ---- stage X rows (zero padded to Kpad; rows past B are zero)
   const int D0 = a.L[0].K;
   const int Kp0 = a.L[0].Kpad;
-  for (int e = tid; e < HR * (Kp0 / 8); e += 256) {
+  for (int e = tid; e < HR * (Kp0 / 8); e += 64 * HW) {
     const int r = e / (Kp0 / 8), c8 = 8 * (e - r * (Kp0 / 8));
     bf16x8 v;
     if (r < rows && c8 + 8 <= D0 && (D0 & 7) == 0) {
@@ -148,21 +149,33 @@ __global__ void __launch_bounds__(256) head_train_kernel(HeadArgs a) {
       for (int k = 0; k < 8; ++k) v[k] = (r < rows && c8 + k < D0) ? a.x[(long long)(r0 + r) * D0 + c8 + k] : (bf16)0.f;
     }
     *reinterpret_cast<bf16x8*>(xs + r * ldx + c8) = v;
-    if (a.xT) {  // X^T [D0][ldt] for the weight gradient of layer 0
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (r < rows && c8 + k < D0) a.xT[(long long)(c8 + k) * a.ldt + r0 + r] = v[k];
-    }
   }
   // zero the H / dZ buffers (their padding columns are read as K padding by the next GEMM)
 #pragma unroll
   for (int l = 0; l < kHeadMaxLayers; ++l)
     if (l < a.nl)
-      for (int e = tid; e < HR * ld[l]; e += 256) {
+      for (int e = tid; e < HR * ld[l]; e += 64 * HW) {
         hs[l][e] = (bf16)0.f;
         dzs[l][e] = (bf16)0.f;
       }
   __syncthreads();
+  // X^T [D0][ldt] for the weight gradient of layer 0: one feature's 16 rows = 32 contiguous bytes
+  if (a.xT)
+    for (int c = tid; c < D0; c += 64 * HW) {
+      bf16x8 lo, hi;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        lo[r] = xs[r * ldx + c];
+        hi[r] = xs[(r + 8) * ldx + c];
+      }
+      bf16* dst = a.xT + (long long)c * a.ldt + r0;
+      if (rows == HR) {
+        *reinterpret_cast<bf16x8*>(dst) = lo;
+        *reinterpret_cast<bf16x8*>(dst + 8) = hi;
+      } else {
+        for (int r = 0; r < rows; ++r) dst[r] = r < 8 ? lo[r] : hi[r - 8];
+      }
+    }
 
   // ---- forward chain (layer loops unrolled: per-layer arrays stay in registers)
 #pragma unroll
@@ -252,19 +265,23 @@ __global__ void __launch_bounds__(256) head_train_kernel(HeadArgs a) {
 
 // ------------------------------------------------------------------------------------------------
 // dW_l[n][k] = sum_b dZ_l^T[n][b] * H_{l-1}^T[k][b]  (k < K),  db_l[n] = sum_b dZ_l^T[n][b]  (k == K)
-__global__ void __launch_bounds__(256) head_wgrad_kernel(HeadArgs a) {
-  __shared__ float red[4][16][17];
+__global__ void __launch_bounds__(1024) head_wgrad_kernel(HeadArgs a) {
+  __shared__ float red[HW][16][17];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int tile = blockIdx.x;
-  if (tile == a.wg_tiles) {  // loss partials -> stats (fixed order)
-    if (threadIdx.x == 0) {
+  if (tile == a.wg_tiles) {  // loss partials -> stats: one wave, fixed-order (deterministic) tree
+    if (wid == 0) {
       float l = 0.f, c = 0.f;
-      for (int i = 0; i < a.nblocks; ++i) {
+      for (int i = lane; i < a.nblocks; i += 64) {
         l += a.loss_part[2 * i];
         c += a.loss_part[2 * i + 1];
       }
-      a.stats[0] = l;
-      a.stats[1] = c;
+      l = wave_sum(l);
+      c = wave_sum(c);
+      if (lane == 0) {
+        a.stats[0] = l;
+        a.stats[1] = c;
+      }
     }
     return;
   }
@@ -285,8 +302,8 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(HeadArgs a) {
     }
   const int ktiles = (L.K + 1 + 15) / 16;
   const int tn = tile / ktiles, tk = tile - tn * ktiles;
-  const int n = 16 * tn + (lane & 15);      // A row (output channel)
-  const int k = 16 * tk + (lane & 15);      // B column (input feature / bias)
+  const int n = 16 * tn + (lane & 15);  // A row (output channel)
+  const int k = 16 * tk + (lane & 15);  // B column (input feature / bias)
   const bf16* arow = L.dzT + (long long)min(n, L.N - 1) * a.ldt + 8 * (lane >> 4);
   const bf16* brow = hprev + (long long)min(k, L.K - 1) * a.ldt + 8 * (lane >> 4);
   const bool a_ok = n < L.N, b_ones = k == L.K, b_ok = k < L.K;
@@ -296,43 +313,45 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(HeadArgs a) {
     ones[e] = (bf16)1.f;
     zeros[e] = (bf16)0.f;
   }
-  const int steps = a.ldt / 32;  // batch k-steps (ldt = round32(B), tail columns are zero)
-  const int per = (steps + 3) / 4;
+  // batch k-steps (ldt = round32(B), tail columns zero) split over the 16 waves; within a wave 8
+  // k-steps (16 16-byte loads) are in flight at once
+  const int steps = a.ldt / 32;
+  const int per = (steps + HW - 1) / HW;
   const int s0 = wid * per, s1 = min(steps, s0 + per);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  int s = s0;
-  for (; s + 4 <= s1; s += 4) {
-    bf16x8 av[4], bv[4];
+  for (int s = s0; s < s1; s += 8) {
+    bf16x8 av[8], bv[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      av[u] = ld16(arow + 32 * (s + u));
-      bv[u] = ld16(brow + 32 * (s + u));
+    for (int u = 0; u < 8; ++u) {
+      const int ss = min(s + u, s1 - 1);
+      av[u] = ld16(arow + 32 * ss);
+      bv[u] = ld16(brow + 32 * ss);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const bf16x8 aa = a_ok ? av[u] : zeros;
+    for (int u = 0; u < 8; ++u) {
+      const bool live = s + u < s1;
+      const bf16x8 aa = (a_ok && live) ? av[u] : zeros;
       const bf16x8 bb = b_ok ? bv[u] : (b_ones ? ones : zeros);
       acc = mfma16x16x32(aa, bb, acc);
     }
-  }
-  for (; s < s1; ++s) {
-    const bf16x8 aa = a_ok ? ld16(arow + 32 * s) : zeros;
-    const bf16x8 bb = b_ok ? ld16(brow + 32 * s) : (b_ones ? ones : zeros);
-    acc = mfma16x16x32(aa, bb, acc);
   }
   // acc[r] = C[row = 4*(lane>>4)+r (n)][col = lane&15 (k)]
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[wid][4 * (lane >> 4) + r][lane & 15] = acc[r];
   __syncthreads();
   const int t = threadIdx.x;
-  const int rn = t >> 4, ck = t & 15;
-  const float v = (red[0][rn][ck] + red[1][rn][ck]) + (red[2][rn][ck] + red[3][rn][ck]);
-  const int on = 16 * tn + rn, ok = 16 * tk + ck;
-  if (on < L.N) {
-    if (ok < L.K)
-      L.gw[(long long)on * L.K + ok] = v;
-    else if (ok == L.K && L.gb)
-      L.gb[on] = v;
+  if (t < 256) {
+    const int rn = t >> 4, ck = t & 15;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < HW; ++w) v += red[w][rn][ck];
+    const int on = 16 * tn + rn, ok = 16 * tk + ck;
+    if (on < L.N) {
+      if (ok < L.K)
+        L.gw[(long long)on * L.K + ok] = v;
+      else if (ok == L.K && L.gb)
+        L.gb[on] = v;
+    }
   }
 }
 
@@ -359,10 +378,10 @@ hipError_t head_train(HeadArgs a, int phases, hipStream_t st) {
   if (phases & 1) {
     const size_t lds = head_train_lds(a);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(head_train_kernel, dim3(a.nblocks), dim3(256), lds, st, a);
+    hipLaunchKernelGGL(head_train_kernel, dim3(a.nblocks), dim3(64 * HW), lds, st, a);
     DFA_HIP_CHECK(hipGetLastError());
   }
-  if (phases & 2) hipLaunchKernelGGL(head_wgrad_kernel, dim3(a.wg_tiles + 1), dim3(256), 0, st, a);
+  if (phases & 2) hipLaunchKernelGGL(head_wgrad_kernel, dim3(a.wg_tiles + 1), dim3(64 * HW), 0, st, a);
   return hipGetLastError();
 }
 

@@ -45,6 +45,11 @@ def report(name, st, grid, kind):
             print(f"   group {g}: stage {a:.0f}  compute {b:.0f}   ({m.sum()} blocks)")
             g += 1
         print(f"   reduction {np.median(st[:, 31] - st[:, 30]):.0f}")
+        m = st[:, 23] > 0
+        if m.any():
+            d = lambda a, b: np.median(st[m, b] - st[m, a])  # noqa: E731
+            print(f"   group1 detail: writes {d(3, 20):.0f}  issue-loads {d(20, 21):.0f}  sync {d(21, 22):.0f}  "
+                  f"build {d(22, 23):.0f}  sync {d(23, 4):.0f}")
     else:
         g = 0
         while 4 + 3 * g < 31 and (st[:, 4 + 3 * g] > 0).any():
