@@ -35,7 +35,9 @@ def main():
     ap.add_argument("--model", default="lenet5")
     ap.add_argument("--batch-per-gpu", type=int, default=4096)
     ap.add_argument("--lr", type=float, default=0.001)
-    ap.add_argument("--graph", default="full", choices=["full", "split", "none"])
+    ap.add_argument("--graph", default=None, choices=["full", "split", "none"],
+                    help="hipGraph mode; default: full on 1 GPU, split (captured compute + SGD, eager RCCL "
+                         "all-reduce between them) on several")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--json-extra", action="store_true", help="add diagnostic fields")
     args = ap.parse_args()
@@ -51,30 +53,35 @@ def main():
         if rank == 0:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
     dev = env.device
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
     net = build_model(args.model, device=dev, seed=0)
     B = args.batch_per_gpu
     if args.model == "resnet18_cifar":
         data, labels = synthetic_cifar10(50000, seed=rank, device=dev)
     else:
         data, labels = synthetic_mnist(60000, seed=rank, device=dev)
-    trainer = DataParallelTrainer(net, lr=args.lr, graph=args.graph, overlap=not args.no_overlap)
+    graph = args.graph or ("full" if world == 1 else "split")
+    trainer = DataParallelTrainer(net, lr=args.lr, graph=graph, overlap=not args.no_overlap)
     trainer.bind_dataset(data, labels, B, scale=1.0 / 255.0)
     total = args.warmup + args.steps
     perm = epoch_permutations(data.shape[0], B, total, dev, seed=rank)
 
     for i in range(args.warmup):
         trainer.step_indices(perm[i])
-    torch.cuda.synchronize(dev)
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for i in range(args.warmup, total):
         st = trainer.step_indices(perm[i])
-    torch.cuda.synchronize(dev)
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -95,7 +102,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
-            "dtype": "bf16",
+            "dtype": "bf16" if dev.type == "cuda" else "fp32",
             "data": "synthetic (MNIST-shaped 60000x28x28x1 uint8, HBM resident), random-init weights",
             "config": {
                 "model": args.model,

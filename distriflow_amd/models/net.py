@@ -308,15 +308,22 @@ class Net:
         return loss / max(n, 1), correct / max(n, 1)
 
     def _forward_eval(self, xb):
+        """Logits for any batch size WITHOUT rebinding: a bound engine (whose buffers a captured
+        hipGraph may reference) runs the batch in chunks of its bound size, padding the tail."""
         B = xb.shape[0]
-        if self._bound_B != B:
-            saved = self._bound_B
+        if self._bound_B is None:
             self.bind(B)
-            out = self.forward(xb, training=False).clone()
-            if saved is not None:
-                self.bind(saved)
-            return out
-        return self.forward(xb, training=False).clone()
+        bb = self._bound_B
+        if B == bb:
+            return self.forward(xb, training=False).clone()
+        outs = []
+        for s in range(0, B, bb):
+            chunk = xb[s: s + bb]
+            n = chunk.shape[0]
+            if n < bb:
+                chunk = torch.cat([chunk, chunk.new_zeros((bb - n,) + tuple(chunk.shape[1:]))])
+            outs.append(self.forward(chunk, training=False)[:n].clone())
+        return torch.cat(outs)
 
     @torch.no_grad()
     def predict(self, x, batch_size: int = 4096) -> torch.Tensor:

@@ -164,17 +164,22 @@ class DataParallelTrainer:
             self._gather()
             return self._step_body(self.xb, self.yb)
         if self._graph is None:
-            try:
-                self._capture()
-            except Exception as e:  # RCCL capture unsupported -> split graphs
-                if self.graph_mode != "full":
-                    raise
-                torch.cuda.synchronize(self.net.device)
-                self.graph_mode = "split"
-                self._works = []
-                self._graph = None
-                self.capture_error = repr(e)
-                self._capture()
+            # capture fallback chain full -> split -> none (eager); every failure is recorded
+            while True:
+                try:
+                    self._capture()
+                    break
+                except Exception as e:  # e.g. collective capture unsupported by this RCCL/driver
+                    torch.cuda.synchronize(self.net.device)
+                    self.capture_error = repr(e)
+                    self._works = []
+                    self._graph = None
+                    if self.graph_mode == "full":
+                        self.graph_mode = "split"
+                    else:
+                        self.graph_mode = "none"
+                        self._gather()
+                        return self._step_body(self.xb, self.yb)
         g, g2 = self._graph
         g.replay()
         if g2 is not None:

@@ -123,3 +123,24 @@ def test_graph_captured_training_reduces_loss():
         if i % 20 == 0 or i == 119:
             losses.append(float(st[0]) / 256)
     assert losses[-1] < 0.5 * losses[0], losses
+
+
+@pytest.mark.parametrize("name,graph,lr", [("lenet5", "full", 0.05), ("mlp_mnist", "split", 0.05)])
+def test_training_reaches_heldout_accuracy(name, graph, lr):
+    """End-to-end: fused kernels + fused head + SGD learn the synthetic MNIST task (held-out split)."""
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
+
+    net = build_model(name, device="cuda", seed=0)
+    data, labels = synthetic_mnist(12288, seed=3, device="cuda")
+    train_x, train_y = data[:8192], labels[:8192]
+    test_x, test_y = data[8192:], labels[8192:]
+    tr = DataParallelTrainer(net, lr=lr, graph=graph)
+    tr.bind_dataset(train_x, train_y, 256, scale=1 / 255)
+    perm = epoch_permutations(8192, 256, 300, "cuda")
+    for i in range(300):
+        tr.step_indices(perm[i])
+    torch.cuda.synchronize()
+    assert tr.graph_mode == graph
+    loss, acc = net.evaluate(test_x.float() / 255, test_y)
+    assert acc > 0.9, (loss, acc)
