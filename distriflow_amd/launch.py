@@ -1,0 +1,524 @@
+"""Command-line launcher: ``python -m distriflow_amd.launch [--nproc N] MODE [options]``.
+
+The reference has no CLI — its experiments are two hand-written TypeScript mains
+(/root/reference/experiment/mnist/mnist_server.ts:16-37, mnist_client.ts:15-31; SURVEY §5.6 asks
+for ``python -m distriflow.launch``).  One process per GPU, torchrun-compatible environment
+(RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT); with ``--nproc N`` this module is its
+own launcher (children are spawned before anything touches the GPU) and, with ``--max-restarts``,
+restarts a failed job from its last checkpoint (``--resume``), which is the all-reduce mode's
+answer to a lost rank.
+
+Modes
+  sync    synchronous data parallelism: RCCL all-reduce SGD (DataParallelTrainer), tf.js
+          checkpoints + resume record per epoch (``--save-dir``)
+  async   asynchronous parameter server (rank 0) with bounded staleness; workers hold the dataset
+          in HBM and receive batch ids (``--ship-data`` sends tensors instead, as the reference)
+  fedsgd  the reference's FederatedServer / FederatedClient (count barrier + version gating)
+  fedavg  federated averaging over non-IID label shards
+
+With WORLD_SIZE == 1 the parameter-server modes run in one process: server + ``--workers``
+worker threads over the in-process transport (same GPU).
+
+Fault injection (tests / drills): ``--fault-kill-rank R --fault-kill-step S`` makes rank R exit
+abruptly at its step S; ``--fault-delay-rank R --fault-delay-ms D`` slows rank R's every step.
+Metrics: ``--metrics FILE`` appends rank-tagged JSONL records (also ``DISTRIFLOW_METRICS``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import threading
+import time
+from typing import Optional
+
+
+# ------------------------------------------------------------------------------------------ CLI
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="python -m distriflow_amd.launch", description=__doc__.split("\n")[0])
+    ap.add_argument("--nproc", type=int, default=1, help="spawn N local ranks (one per GPU)")
+    ap.add_argument("--max-restarts", type=int, default=0, help="restart the job from its checkpoint on failure")
+    ap.add_argument("--master-port", type=int, default=0)
+    sub = ap.add_subparsers(dest="mode", required=True)
+
+    def common(p):
+        p.add_argument("--model", default="lenet5", help="mlp_mnist | lenet5 | keras_cnn | resnet18_cifar")
+        p.add_argument("--data", default="synthetic", help="synthetic | mnist:<dir with IDX files>")
+        p.add_argument("--num-examples", type=int, default=60000)
+        p.add_argument("--batch", type=int, default=256, help="per-rank batch (sync) / microbatch (PS modes)")
+        p.add_argument("--lr", type=float, default=0.05)
+        p.add_argument("--epochs", type=int, default=1)
+        p.add_argument("--seed", type=int, default=0)
+        p.add_argument("--device", default="auto", help="auto | cuda | cpu")
+        p.add_argument("--metrics", default=None, help="JSONL metrics file")
+        p.add_argument("--verbose", action="store_true")
+        p.add_argument("--fault-kill-rank", type=int, default=-1)
+        p.add_argument("--fault-kill-step", type=int, default=-1)
+        p.add_argument("--fault-delay-rank", type=int, default=-1)
+        p.add_argument("--fault-delay-ms", type=float, default=0.0)
+
+    p = sub.add_parser("sync", help="synchronous all-reduce data parallelism")
+    common(p)
+    p.add_argument("--momentum", type=float, default=0.0)
+    p.add_argument("--graph", default=None, choices=["full", "split", "none"])
+    p.add_argument("--save-dir", default=None)
+    p.add_argument("--resume", action="store_true")
+    p.add_argument("--steps", type=int, default=0, help="stop after this many steps (0 = full epochs)")
+
+    p = sub.add_parser("async", help="asynchronous parameter server, bounded staleness")
+    common(p)
+    p.add_argument("--workers", type=int, default=2, help="worker threads when running in one process")
+    p.add_argument("--max-staleness", type=int, default=-1)
+    p.add_argument("--ship-data", action="store_true")
+
+    p = sub.add_parser("fedsgd", help="FederatedServer / FederatedClient (reference sync PS)")
+    common(p)
+    p.add_argument("--workers", type=int, default=2)
+    p.add_argument("--min-updates", type=int, default=2)
+    p.add_argument("--updates-per-worker", type=int, default=20)
+
+    p = sub.add_parser("fedavg", help="federated averaging over non-IID shards")
+    common(p)
+    p.add_argument("--workers", type=int, default=2)
+    p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--local-steps", type=int, default=20)
+    p.add_argument("--classes-per-client", type=int, default=2)
+    return ap
+
+
+# ------------------------------------------------------------------------------------------ spawner
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawn(argv: list, nproc: int, max_restarts: int, port: int) -> int:
+    """Run ``nproc`` ranks of this module; on a failure stop the others (their exact PIDs) and
+    restart everything with ``--resume`` up to ``max_restarts`` times."""
+    child_argv = [a for a in argv]
+    attempt = 0
+    while True:
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port or _free_port()), WORLD_SIZE=str(nproc))
+        procs = []
+        for r in range(nproc):
+            e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+            procs.append(subprocess.Popen([sys.executable, "-m", "distriflow_amd.launch"] + child_argv, env=e))
+        failed = None
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(i, c) for i, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                failed = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                return 0
+            time.sleep(0.2)
+        for p in procs:  # stop the survivors of a failed job
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        deadline = time.time() + 20
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        print(f"[launch] rank {failed[0]} exited with {failed[1]} (attempt {attempt})", file=sys.stderr, flush=True)
+        if attempt >= max_restarts:
+            return failed[1] or 1
+        attempt += 1
+        # a restarted job resumes from its checkpoint and runs without the injected fault
+        child_argv = [a for a in child_argv if a != "--resume"]
+        child_argv = _strip_opt(child_argv, "--fault-kill-rank") + ["--resume"] if "sync" in child_argv else child_argv
+        child_argv = _strip_opt(child_argv, "--fault-kill-step")
+
+
+def _strip_opt(argv: list, name: str) -> list:
+    out, skip = [], False
+    for a in argv:
+        if skip:
+            skip = False
+            continue
+        if a == name:
+            skip = True
+            continue
+        if a.startswith(name + "="):
+            continue
+        out.append(a)
+    return out
+
+
+# ------------------------------------------------------------------------------------------ helpers
+class Faults:
+    def __init__(self, args, rank: int):
+        self.kill = args.fault_kill_rank == rank and args.fault_kill_step >= 0
+        self.kill_step = args.fault_kill_step
+        self.delay = (args.fault_delay_ms / 1e3) if args.fault_delay_rank == rank else 0.0
+
+    def step(self, i: int):
+        if self.delay:
+            time.sleep(self.delay)
+        if self.kill and i >= self.kill_step:
+            print(f"[fault] rank {os.environ.get('RANK', '0')} killed at step {i}", file=sys.stderr, flush=True)
+            os._exit(17)
+
+
+def _device(args):
+    import torch
+
+    if args.device == "auto":
+        return "cuda" if torch.cuda.is_available() else "cpu"
+    return args.device
+
+
+def _load_data(args, device, seed=0):
+    from .data.synthetic import synthetic_cifar10, synthetic_mnist
+
+    if args.data.startswith("mnist:"):
+        from .data.mnist import load_mnist
+
+        x, y = load_mnist(args.data.split(":", 1)[1], "train")
+        return x.to(device), y.to(device)
+    if args.model == "resnet18_cifar":
+        return synthetic_cifar10(args.num_examples, seed=seed, device=device)
+    return synthetic_mnist(args.num_examples, seed=seed, device=device)
+
+
+def _logger(args, role):
+    from .utils.logging import Logger
+
+    return Logger(role, verbose=args.verbose, metrics_file=args.metrics)
+
+
+# ------------------------------------------------------------------------------------------ sync
+def run_sync(args) -> dict:
+    import torch
+    import torch.distributed as dist
+
+    from .checkpoint.store import VersionedStore
+    from .checkpoint.tfjs import load_layers_model_weights, save_layers_model
+    from .models.zoo import build_model
+    from .parallel.comm import init_distributed, shutdown
+    from .parallel.data_parallel import DataParallelTrainer, epoch_permutations
+
+    env = init_distributed(device=_device(args))
+    rank, world, dev = env.rank, env.world_size, env.device
+    log = _logger(args, f"Distributed Worker {rank}")
+    faults = Faults(args, rank)
+    net = build_model(args.model, device=dev, seed=args.seed)
+    x, y = _load_data(args, dev)
+    n = x.shape[0]
+    B = args.batch
+    steps_per_epoch = n // (B * world)
+    start_epoch = 0
+    store = VersionedStore(args.save_dir) if args.save_dir else None
+    if store is not None:
+        store.setup()
+        if args.resume and store.last() is not None:
+            load_layers_model_weights(net, os.path.join(store.path(store.last()), "model.json"))
+            rec = store.read_resume() or {}
+            start_epoch = int(rec.get("epoch", -1)) + 1
+            log.log(f"resumed from version {store.last()} at epoch {start_epoch}")
+    graph = args.graph or ("full" if world == 1 else "split")
+    tr = DataParallelTrainer(net, lr=args.lr, momentum=args.momentum, graph=graph if dev.type == "cuda" else "none")
+    scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
+    tr.bind_dataset(x, y, B, scale=scale)
+    step = 0
+    t0 = time.perf_counter()
+    seen = 0
+    last_loss = float("nan")
+    for epoch in range(start_epoch, args.epochs):
+        perm = epoch_permutations(n, B * world, steps_per_epoch, dev, seed=args.seed + epoch)
+        for i in range(steps_per_epoch):
+            faults.step(step)
+            st = tr.step_indices(perm[i, rank * B:(rank + 1) * B])
+            step += 1
+            seen += B * world
+            if args.steps and step >= args.steps:
+                break
+        last_loss = float(st[0]) / B
+        el = time.perf_counter() - t0
+        log.metric(event="epoch", epoch=epoch, step=step, loss=last_loss, images_per_s=seen / el)
+        log.log(f"epoch {epoch}: loss {last_loss:.4f}, {seen / el:.0f} images/s")
+        if store is not None and rank == 0:
+            v = store.new_version()
+            save_layers_model(net, store.path(v))
+            store.mark_current(v)
+            store.write_resume({"epoch": epoch, "step": step, "version": v})
+        if world > 1:
+            dist.barrier()
+        if args.steps and step >= args.steps:
+            break
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    out = {"mode": "sync", "world": world, "steps": step, "images_per_s": seen / max(el, 1e-9), "loss": last_loss,
+           "graph": tr.graph_mode}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    shutdown()
+    return out
+
+
+# ------------------------------------------------------------------------------------------ parameter-server modes
+def _ps_setup(args):
+    from .parallel.comm import init_distributed
+
+    env = init_distributed(device=_device(args))
+    return env
+
+
+def run_async(args) -> dict:
+    import torch
+
+    from .data.dataset import DistriDataset
+    from .models.distri_model import ClientModel, InMemoryServerModel
+    from .parallel.server import AsynchronousSGDServer
+    from .parallel.transport import LocalHub, make_star_transports
+    from .parallel.worker import AsynchronousSGDClient
+
+    env = _ps_setup(args)
+    dev = env.device
+    x, y = _load_data(args, dev)
+    scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
+    srv_cfg = {"modelDir": False, "verbose": args.verbose,
+               "serverHyperparams": {"maximumStaleness": args.max_staleness}}
+    compile_cfg = {"learningRate": args.lr}
+
+    def make_server(tp):
+        ds = DistriDataset(x, y, {"batchSize": args.batch, "epochs": args.epochs}, shuffle=True, seed=args.seed)
+        model = InMemoryServerModel(args.model, compile_cfg, device=dev)
+        return AsynchronousSGDServer(tp, model, ds, srv_cfg, ship_data=args.ship_data), ds
+
+    def make_worker(tp, r):
+        cm = ClientModel(args.model, compile_cfg, device=dev)
+        return AsynchronousSGDClient(tp, cm, {"clientId": f"async-{r}", "verbose": args.verbose},
+                                     data=None if args.ship_data else x, labels=None if args.ship_data else y,
+                                     data_scale=scale)
+
+    log = _logger(args, "Distributed Server")
+    t0 = time.perf_counter()
+    if env.world_size == 1:
+        hub = LocalHub(1 + args.workers)
+        srv, ds = make_server(hub.endpoint(0))
+        srv.setup()
+        workers = [make_worker(hub.endpoint(r, [0]), r) for r in range(1, 1 + args.workers)]
+        faults = [Faults(args, r) for r in range(1, 1 + args.workers)]
+        for w, f in zip(workers, faults):
+            if f.delay:
+                w.on_upload(lambda msg, f=f: time.sleep(f.delay))
+        ths = [threading.Thread(target=lambda w=w: (w.setup(), w.run(timeout=3600)), daemon=True) for w in workers]
+        for t in ths:
+            t.start()
+        srv.serve(until=srv.all_done, timeout=3600)
+        for t in ths:
+            t.join(timeout=30)
+        result = srv
+    else:
+        tp = make_star_transports(0)
+        if env.rank == 0:
+            srv, ds = make_server(tp)
+            srv.setup()
+            srv.serve(until=lambda: srv.all_done() and srv.num_clients == 0, timeout=3600)
+            result = srv
+        else:
+            w = make_worker(tp, env.rank)
+            faults = Faults(args, env.rank)
+            if faults.delay or faults.kill:
+                cnt = [0]
+
+                def _hook(msg, f=faults, c=cnt):
+                    f.step(c[0])
+                    c[0] += 1
+
+                w.on_upload(_hook)
+            w.setup()
+            w.run(timeout=3600)
+            w.dispose()
+            result = None
+        tp.close()
+    el = time.perf_counter() - t0
+    out = None
+    if result is not None:
+        images = result.num_updates * args.batch
+        out = {"mode": "async", "world": env.world_size, "workers": args.workers if env.world_size == 1 else
+               env.world_size - 1, "updates": result.num_updates, "rejected": result.rejected,
+               "staleness_hist": list(result.gate.histogram()), "images_per_s": images / max(el, 1e-9),
+               "max_staleness": args.max_staleness}
+        log.metric(event="async_done", **{k: v for k, v in out.items() if k != "staleness_hist"})
+        print(json.dumps(out), flush=True)
+    from .parallel.comm import shutdown
+
+    shutdown()
+    return out or {}
+
+
+def run_fedsgd(args) -> dict:
+    import torch
+
+    from .models.distri_model import ClientModel, InMemoryServerModel
+    from .parallel.server import FederatedServer
+    from .parallel.transport import LocalHub, make_star_transports
+    from .parallel.worker import FederatedClient
+
+    env = _ps_setup(args)
+    dev = env.device
+    x, y = _load_data(args, dev)
+    xf = x.float() / 255.0 if x.dtype == torch.uint8 else x
+    epu = args.batch
+    cfg = {"modelDir": False, "verbose": args.verbose, "serverHyperparams": {"minUpdatesPerVersion": args.min_updates},
+           "clientHyperparams": {"examplesPerUpdate": epu}}
+    compile_cfg = {"learningRate": args.lr}
+
+    def feed(c, r, nworkers):
+        shard = torch.arange(r - 1, x.shape[0], nworkers, device=x.device)[: epu * args.updates_per_worker]
+        f = Faults(args, r)
+        for i in range(0, shard.numel(), epu):
+            f.step(i // epu)
+            idx = shard[i: i + epu]
+            c.distributed_update(xf.index_select(0, idx), y.index_select(0, idx))
+
+    t0 = time.perf_counter()
+    out = None
+    if env.world_size == 1:
+        hub = LocalHub(1 + args.workers)
+        srv = FederatedServer(hub.endpoint(0), InMemoryServerModel(args.model, compile_cfg, device=dev), cfg)
+        srv.setup()
+        th = threading.Thread(target=srv.serve, kwargs={"timeout": 3600}, daemon=True)
+        th.start()
+        clients = [FederatedClient(hub.endpoint(r, [0]), ClientModel(args.model, compile_cfg, device=dev),
+                                   {"clientId": f"fed-{r}"}) for r in range(1, 1 + args.workers)]
+        ths = []
+        for r, c in enumerate(clients, 1):
+            def go(c=c, r=r):
+                c.setup()
+                feed(c, r, args.workers)
+            ths.append(threading.Thread(target=go, daemon=True))
+            ths[-1].start()
+        for t in ths:
+            t.join()
+        time.sleep(0.2)
+        srv.stop()
+        out = {"mode": "fedsgd", "versions": srv.version_id,
+               "uploads": sum(c.num_updates() for c in clients)}
+    else:
+        tp = make_star_transports(0)
+        if env.rank == 0:
+            srv = FederatedServer(tp, InMemoryServerModel(args.model, compile_cfg, device=dev), cfg)
+            srv.setup()
+            srv.serve(until=lambda: srv.num_clients == 0 and srv.version_id > 0, timeout=3600)
+            out = {"mode": "fedsgd", "versions": srv.version_id}
+        else:
+            c = FederatedClient(tp, ClientModel(args.model, compile_cfg, device=dev), {"clientId": f"fed-{env.rank}"})
+            c.setup()
+            feed(c, env.rank, env.world_size - 1)
+            c.poll(0.5)
+            c.dispose()
+        tp.close()
+    el = time.perf_counter() - t0
+    if out is not None:
+        out["seconds"] = el
+        print(json.dumps(out), flush=True)
+    from .parallel.comm import shutdown
+
+    shutdown()
+    return out or {}
+
+
+def run_fedavg(args) -> dict:
+    import torch
+
+    from .data.synthetic import non_iid_shards
+    from .models.distri_model import ClientModel, InMemoryServerModel
+    from .parallel.server import FedAvgServer
+    from .parallel.transport import LocalHub, make_star_transports
+    from .parallel.worker import FedAvgClient
+
+    env = _ps_setup(args)
+    dev = env.device
+    x, y = _load_data(args, dev)
+    scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
+    nclients = args.workers if env.world_size == 1 else env.world_size - 1
+    shards = non_iid_shards(y, nclients, args.classes_per_client, seed=args.seed)
+    compile_cfg = {"learningRate": args.lr}
+    test_x = x[: min(4096, x.shape[0])]
+    test_y = y[: test_x.shape[0]]
+
+    def make_client(tp, r):
+        idx = shards[r - 1].to(x.device)
+        return FedAvgClient(tp, ClientModel(args.model, compile_cfg, device=dev), x.index_select(0, idx),
+                            y.index_select(0, idx), {"clientId": f"avg-{r}"}, batch_size=args.batch,
+                            local_steps=args.local_steps, data_scale=scale, seed=args.seed + r)
+
+    t0 = time.perf_counter()
+    out = None
+    if env.world_size == 1:
+        hub = LocalHub(1 + nclients)
+        model = InMemoryServerModel(args.model, compile_cfg, device=dev)
+        srv = FedAvgServer(hub.endpoint(0), model, {"modelDir": False}, rounds=args.rounds)
+        srv.setup()
+        clients = [make_client(hub.endpoint(r, [0]), r) for r in range(1, 1 + nclients)]
+        ths = [threading.Thread(target=lambda c=c: (c.setup(), c.run(timeout=3600)), daemon=True) for c in clients]
+        for t in ths:
+            t.start()
+        while len(srv.clients) < nclients:
+            srv.step(0.05)
+        srv.start_round()
+        srv.serve(until=srv.finished, timeout=3600)
+        srv.stop()
+    else:
+        tp = make_star_transports(0)
+        if env.rank == 0:
+            model = InMemoryServerModel(args.model, compile_cfg, device=dev)
+            srv = FedAvgServer(tp, model, {"modelDir": False}, rounds=args.rounds)
+            srv.setup()
+            while len(srv.clients) < nclients:
+                srv.step(0.05)
+            srv.start_round()
+            srv.serve(until=srv.finished, timeout=3600)
+            srv.stop()
+        else:
+            c = make_client(tp, env.rank)
+            c.setup()
+            c.run(timeout=3600)
+            c.dispose()
+            srv = None
+        tp.close()
+    el = time.perf_counter() - t0
+    if env.rank == 0:
+        loss, acc = model.evaluate(test_x.float() * scale, test_y)
+        out = {"mode": "fedavg", "clients": nclients, "rounds": srv.round, "rounds_per_s": srv.round / max(el, 1e-9),
+               "test_loss": loss, "test_accuracy": acc}
+        print(json.dumps(out), flush=True)
+    from .parallel.comm import shutdown
+
+    shutdown()
+    return out or {}
+
+
+MODES = {"sync": run_sync, "async": run_async, "fedsgd": run_fedsgd, "fedavg": run_fedavg}
+
+
+def main(argv: Optional[list] = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = build_parser().parse_args(argv)
+    if args.nproc > 1 and "WORLD_SIZE" not in os.environ:
+        child = _strip_opt(_strip_opt(_strip_opt(argv, "--nproc"), "--max-restarts"), "--master-port")
+        return _spawn(child, args.nproc, args.max_restarts, args.master_port)
+    MODES[args.mode](args)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,63 @@
+"""The ``python -m distriflow_amd.launch`` CLI: every mode end to end on CPU, plus the
+fault drill of SURVEY §5.3 — a rank killed mid-run, the job restarted from its checkpoint."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, timeout=600):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, "-m", "distriflow_amd.launch"] + args, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    return p
+
+
+def _last_json(out: str) -> dict:
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert lines, out
+    return json.loads(lines[-1])
+
+
+@pytest.mark.timeout(600)
+def test_ps_modes_single_process():
+    from distriflow_amd.launch import main
+
+    # in-process: server + worker threads over the local transport
+    for argv in (["async", "--model", "mlp_mnist", "--num-examples", "1024", "--batch", "64", "--workers", "2",
+                  "--max-staleness", "1", "--device", "cpu"],
+                 ["fedavg", "--model", "mlp_mnist", "--num-examples", "2048", "--batch", "64", "--workers", "3",
+                  "--rounds", "2", "--local-steps", "5", "--device", "cpu"],
+                 ["fedsgd", "--model", "mlp_mnist", "--num-examples", "1024", "--batch", "32", "--workers", "2",
+                  "--updates-per-worker", "4", "--device", "cpu"]):
+        assert main(argv) == 0
+
+
+@pytest.mark.timeout(900)
+def test_sync_fault_kill_and_resume(tmp_path):
+    d = str(tmp_path / "ckpt")
+    p = _run(["--nproc", "2", "--max-restarts", "1", "sync", "--model", "mlp_mnist", "--num-examples", "2048",
+              "--batch", "64", "--epochs", "3", "--device", "cpu", "--save-dir", d,
+              "--fault-kill-rank", "1", "--fault-kill-step", "20"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "[fault] rank 1 killed" in p.stderr
+    assert "exited with 17" in p.stderr
+    res = _last_json(p.stdout)
+    assert res["mode"] == "sync" and res["world"] == 2
+    rec = json.load(open(os.path.join(d, "resume.json")))
+    assert rec["epoch"] == 2
+    assert os.path.exists(os.path.join(d, "current", "model.json"))
+
+
+@pytest.mark.timeout(900)
+def test_async_parameter_server_three_ranks():
+    p = _run(["--nproc", "3", "async", "--model", "mlp_mnist", "--num-examples", "1024", "--batch", "64",
+              "--max-staleness", "2", "--device", "cpu"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = _last_json(p.stdout)
+    assert res["world"] == 3 and res["updates"] >= 16
