@@ -35,9 +35,9 @@ def main():
     ap.add_argument("--model", default="lenet5")
     ap.add_argument("--batch-per-gpu", type=int, default=4096)
     ap.add_argument("--lr", type=float, default=0.001)
-    ap.add_argument("--graph", default=None, choices=["full", "split", "none"],
-                    help="hipGraph mode; default: full on 1 GPU, split (captured compute + SGD, eager RCCL "
-                         "all-reduce between them) on several")
+    ap.add_argument("--graph", default="full", choices=["full", "split", "none"],
+                    help="hipGraph mode: full = whole step incl. bucketed RCCL all-reduces (falls back to split "
+                         "= captured compute + SGD with an eager all-reduce between, then none, if capture fails)")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--json-extra", action="store_true", help="add diagnostic fields")
     args = ap.parse_args()
@@ -63,21 +63,22 @@ def main():
         data, labels = synthetic_cifar10(50000, seed=rank, device=dev)
     else:
         data, labels = synthetic_mnist(60000, seed=rank, device=dev)
-    graph = args.graph or ("full" if world == 1 else "split")
-    trainer = DataParallelTrainer(net, lr=args.lr, graph=graph, overlap=not args.no_overlap)
+    trainer = DataParallelTrainer(net, lr=args.lr, graph=args.graph, overlap=not args.no_overlap)
     trainer.bind_dataset(data, labels, B, scale=1.0 / 255.0)
     total = args.warmup + args.steps
     perm = epoch_permutations(data.shape[0], B, total, dev, seed=rank)
 
+    # device-resident batch schedule: each step's optimizer launch stages the next step's indices
+    trainer.bind_index_stream(perm)
     for i in range(args.warmup):
-        trainer.step_indices(perm[i])
+        trainer.step()
     sync()
     if world > 1:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
     for i in range(args.warmup, total):
-        st = trainer.step_indices(perm[i])
+        st = trainer.step()
     sync()
     if world > 1:
         dist.barrier()

@@ -244,7 +244,9 @@ void gap_bwd_py(torch::Tensor dy, torch::Tensor dx, int64_t B, int64_t HW, int64
 
 // descs: int64 GPU tensor [ndesc][6] laid out as ParamDesc (see optim.hip)
 void sgd_multi_py(torch::Tensor descs, int64_t ndesc, int64_t total_blocks, torch::Tensor master, torch::Tensor grad,
-                  c10::optional<torch::Tensor> mom, torch::Tensor wbf, torch::Tensor hyper, bool apply_update) {
+                  c10::optional<torch::Tensor> mom, torch::Tensor wbf, torch::Tensor hyper, bool apply_update,
+                  c10::optional<torch::Tensor> idx_stream, c10::optional<torch::Tensor> idx_cursor,
+                  c10::optional<torch::Tensor> idx_dst) {
   TORCH_CHECK(descs.is_cuda() && descs.scalar_type() == at::kLong && descs.is_contiguous(), "descs must be int64 GPU");
   static_assert(sizeof(dfa::ParamDesc) == 48, "ParamDesc layout");
   TORCH_CHECK(descs.numel() * 8 >= ndesc * (int64_t)sizeof(dfa::ParamDesc), "descs too small");
@@ -260,9 +262,23 @@ void sgd_multi_py(torch::Tensor descs, int64_t ndesc, int64_t total_blocks, torc
     TORCH_CHECK(mom->numel() >= master.numel(), "momentum buffer too small");
     mp = mom->data_ptr<float>();
   }
+  dfa::IndexStream is{};
+  if (idx_stream.has_value() && idx_stream->defined()) {
+    TORCH_CHECK(idx_cursor.has_value() && idx_dst.has_value(), "index stream needs cursor and dst");
+    need(*idx_stream, at::kLong, "idx_stream");
+    need(*idx_cursor, at::kLong, "idx_cursor");
+    need(*idx_dst, at::kLong, "idx_dst");
+    TORCH_CHECK(idx_stream->dim() == 2 && idx_stream->size(1) == idx_dst->numel() && idx_cursor->numel() >= 1,
+                "idx_stream must be [nsteps][B] with B = idx_dst.numel()");
+    is.src = reinterpret_cast<const long long*>(idx_stream->data_ptr());
+    is.cursor = reinterpret_cast<long long*>(idx_cursor->data_ptr());
+    is.dst = reinterpret_cast<long long*>(idx_dst->data_ptr());
+    is.B = (int)idx_dst->numel();
+    is.nsteps = (int)idx_stream->size(0);
+  }
   check_hip(dfa::sgd_multi(reinterpret_cast<const dfa::ParamDesc*>(descs.data_ptr()), (int)ndesc, (int)total_blocks,
                            master.data_ptr<float>(), grad.data_ptr<float>(), mp, (dfa::bf16*)wbf.data_ptr(),
-                           hyper.data_ptr<float>(), apply_update ? 1 : 0, cur_stream()),
+                           hyper.data_ptr<float>(), apply_update ? 1 : 0, cur_stream(), is.src ? &is : nullptr),
             "sgd_multi");
 }
 
@@ -568,7 +584,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("relu_bwd", &relu_bwd_py);
   m.def("gap_fwd", &gap_fwd_py);
   m.def("gap_bwd", &gap_bwd_py);
-  m.def("sgd_multi", &sgd_multi_py);
+  m.def("sgd_multi", &sgd_multi_py, py::arg("descs"), py::arg("ndesc"), py::arg("total_blocks"), py::arg("master"),
+        py::arg("grad"), py::arg("mom"), py::arg("wbf"), py::arg("hyper"), py::arg("apply_update"),
+        py::arg("idx_stream") = py::none(), py::arg("idx_cursor") = py::none(), py::arg("idx_dst") = py::none());
   m.def("sum_buffers", &sum_buffers_py);
   m.def("axpby", &axpby_py);
   m.def("bn_fwd_train", &bn_fwd_train_py);

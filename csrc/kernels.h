@@ -63,8 +63,15 @@ hipError_t add_act(const bf16* a, const bf16* b, bf16* out, long long n, int rel
 hipError_t relu_bwd(const bf16* y, const bf16* dy, bf16* dx, long long n, hipStream_t st);
 hipError_t gap_fwd(const bf16* x, bf16* y, int B, int HW, int C, hipStream_t st);
 hipError_t gap_bwd(const bf16* dy, bf16* dx, int B, int HW, int C, hipStream_t st);
+struct IndexStream {  // next-batch staging folded into the optimizer launch (csrc/optim.hip)
+  const long long* src;  // [nsteps][B] batch indices
+  long long* cursor;     // device step cursor
+  long long* dst;        // [B] static index buffer read by the step
+  int B, nsteps;
+};
 hipError_t sgd_multi(const ParamDesc* descs, int ndesc, int total_blocks, float* master, const float* grad,
-                     float* mom_buf, bf16* wbf, const float* hyper, int apply_update, hipStream_t st);
+                     float* mom_buf, bf16* wbf, const float* hyper, int apply_update, hipStream_t st,
+                     const IndexStream* is = nullptr);
 hipError_t sum_buffers(const float* const* ins, int nin, float* out, long long n, float scale, hipStream_t st);
 hipError_t axpby(float* out, const float* a, const float* b, float alpha, float beta, long long n, hipStream_t st);
 hipError_t bn_fwd_train(const bf16* x, bf16* y, const float* gamma, const float* beta, float* mean, float* invstd,

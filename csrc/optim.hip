@@ -27,13 +27,13 @@ __device__ __forceinline__ int find_desc(const ParamDesc* d, int n, int bid) {
 }
 
 // hyper = [lr, momentum, weight_decay, grad_scale, nesterov]
-__global__ void __launch_bounds__(256) sgd_multi_kernel(const ParamDesc* __restrict__ descs, int ndesc,
-                                                        float* __restrict__ master, const float* __restrict__ grad,
-                                                        float* __restrict__ mom_buf, bf16* __restrict__ wbf,
-                                                        const float* __restrict__ hyper, int apply_update) {
-  const int di = find_desc(descs, ndesc, blockIdx.x);
+__device__ __forceinline__ void sgd_multi_body(const ParamDesc* __restrict__ descs, int ndesc,
+                                               float* __restrict__ master, const float* __restrict__ grad,
+                                               float* __restrict__ mom_buf, bf16* __restrict__ wbf,
+                                               const float* __restrict__ hyper, int apply_update, int bid) {
+  const int di = find_desc(descs, ndesc, bid);
   const ParamDesc d = descs[di];
-  const int base = (blockIdx.x - d.block_start) * SGD_ELEMS_PER_BLOCK;
+  const int base = (bid - d.block_start) * SGD_ELEMS_PER_BLOCK;
   float lr = 0.f, mom = 0.f, wd = 0.f, gs = 1.f;
   bool nesterov = false;
   if (apply_update) {
@@ -83,8 +83,47 @@ __global__ void __launch_bounds__(256) sgd_multi_kernel(const ParamDesc* __restr
   }
 }
 
+__global__ void __launch_bounds__(256) sgd_multi_kernel(const ParamDesc* __restrict__ descs, int ndesc,
+                                                        float* __restrict__ master, const float* __restrict__ grad,
+                                                        float* __restrict__ mom_buf, bf16* __restrict__ wbf,
+                                                        const float* __restrict__ hyper, int apply_update) {
+  sgd_multi_body(descs, ndesc, master, grad, mom_buf, wbf, hyper, apply_update, blockIdx.x);
+}
+
+// Device-resident index stream: the optimizer is the last kernel of a training step, so one extra
+// workgroup of the same launch stages the NEXT step's batch indices (src[(cursor+1) % nsteps]) into
+// the static index buffer the step's first kernels read, then advances the cursor.  A replayed step
+// graph then needs no host-side copy (and no extra launch) to move to the next batch.
+__global__ void __launch_bounds__(256) sgd_multi_stream_kernel(const ParamDesc* __restrict__ descs, int ndesc,
+                                                               float* __restrict__ master,
+                                                               const float* __restrict__ grad,
+                                                               float* __restrict__ mom_buf, bf16* __restrict__ wbf,
+                                                               const float* __restrict__ hyper, int apply_update,
+                                                               int total_blocks, IndexStream is) {
+  if ((int)blockIdx.x < total_blocks) {
+    sgd_multi_body(descs, ndesc, master, grad, mom_buf, wbf, hyper, apply_update, blockIdx.x);
+    return;
+  }
+  // the single index-stream workgroup: the only reader/writer of the cursor
+  __shared__ long long next;
+  if (threadIdx.x == 0) {
+    const long long c = *is.cursor;
+    next = (c + 1) % is.nsteps;
+  }
+  __syncthreads();
+  const long long* src = is.src + next * is.B;
+  for (int i = threadIdx.x; i < is.B; i += blockDim.x) is.dst[i] = src[i];
+  if (threadIdx.x == 0) *is.cursor = next;
+}
+
 hipError_t sgd_multi(const ParamDesc* descs, int ndesc, int total_blocks, float* master, const float* grad,
-                     float* mom_buf, bf16* wbf, const float* hyper, int apply_update, hipStream_t st) {
+                     float* mom_buf, bf16* wbf, const float* hyper, int apply_update, hipStream_t st,
+                     const IndexStream* is) {
+  if (is != nullptr && is->src != nullptr) {
+    hipLaunchKernelGGL(sgd_multi_stream_kernel, dim3(max(total_blocks, 0) + 1), dim3(256), 0, st, descs, ndesc,
+                       master, grad, mom_buf, wbf, hyper, apply_update, max(total_blocks, 0), *is);
+    return hipGetLastError();
+  }
   if (ndesc <= 0 || total_blocks <= 0) return hipSuccess;
   hipLaunchKernelGGL(sgd_multi_kernel, dim3(total_blocks), dim3(256), 0, st, descs, ndesc, master, grad, mom_buf, wbf,
                      hyper, apply_update);

@@ -230,7 +230,7 @@ def run_sync(args) -> dict:
             rec = store.read_resume() or {}
             start_epoch = int(rec.get("epoch", -1)) + 1
             log.log(f"resumed from version {store.last()} at epoch {start_epoch}")
-    graph = args.graph or ("full" if world == 1 else "split")
+    graph = args.graph or "full"
     tr = DataParallelTrainer(net, lr=args.lr, momentum=args.momentum, graph=graph if dev.type == "cuda" else "none")
     scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
     tr.bind_dataset(x, y, B, scale=scale)

@@ -334,6 +334,26 @@ class Net:
             outs.append(torch.softmax(z, dim=1) if self.final_softmax else z)
         return torch.cat(outs)
 
+    # ------------------------------------------------------------------ mutable state
+    def state_tensors(self) -> list:
+        """Every tensor a training step mutates besides gradients/activations: master weights,
+        optimizer state, BN running statistics, the dropout step counter."""
+        out = [self.store.master, self.step_dev]
+        if self.store.momentum is not None:
+            out.append(self.store.momentum)
+        for l in self._all_leaf_layers():
+            if isinstance(l, BatchNorm) and hasattr(l, "run_mean"):
+                out += [l.run_mean, l.run_var]
+        return out
+
+    def snapshot_state(self) -> list:
+        return [t.clone() for t in self.state_tensors()]
+
+    def restore_state(self, snap: list):
+        for t, v in zip(self.state_tensors(), snap):
+            t.copy_(v)
+        self.store.refresh_compute()
+
     # ------------------------------------------------------------------ introspection
     def num_params(self) -> int:
         return sum(s.numel for s in self.store.specs)

@@ -213,12 +213,20 @@ class ParamStore:
         if momentum != 0.0 and self.momentum is None:
             self.momentum = torch.zeros_like(self.master)
 
-    def sgd_step(self):
-        """w -= lr * (grad_scale * g [+ wd w]) (momentum optional); uses the device-side hyper tensor."""
+    def sgd_step(self, index_stream=None):
+        """w -= lr * (grad_scale * g [+ wd w]) (momentum optional); uses the device-side hyper tensor.
+        ``index_stream = (stream [nsteps][B], cursor [1], dst [B])`` (GPU): the same launch stages the
+        next step's batch indices into ``dst`` and advances ``cursor`` (csrc/optim.hip)."""
         if self.compute_bf16:
+            src, cur, dst = index_stream if index_stream is not None else (None, None, None)
             native.require().sgd_multi(self._descs, self._ndesc, self._sgd_blocks, self.master, self.grad,
-                                       self.momentum, self.wbf, self.hyper, True)
+                                       self.momentum, self.wbf, self.hyper, True, src, cur, dst)
             return
+        if index_stream is not None:
+            src, cur, dst = index_stream
+            nxt = (int(cur[0]) + 1) % src.shape[0]
+            dst.copy_(src[nxt])
+            cur.fill_(nxt)
         lr, mom, wd, gs, nest = self._hyper_host
         if not hasattr(self, "_valid"):
             self._valid = torch.zeros(self.total, dtype=torch.bool, device=self.device)

@@ -30,7 +30,7 @@ from .. import ops
 
 class DataParallelTrainer:
     def __init__(self, net, lr: float = 0.001, momentum: float = 0.0, weight_decay: float = 0.0,
-                 group=None, bucket_mb: float = 32.0, overlap: bool = True, graph: str = "full",
+                 group=None, bucket_mb: Optional[float] = None, overlap: bool = True, graph: str = "full",
                  broadcast_init: bool = True):
         self.net = net
         self.group = group
@@ -39,11 +39,18 @@ class DataParallelTrainer:
         self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
         self.overlap = overlap
         self.graph_mode = graph if net.is_gpu else "none"
-        self.bucket_bytes = int(bucket_mb * (1 << 20))
+        # bucket size: small models still get >= 2 buckets (the head's gradient all-reduce then overlaps
+        # the convolution backward); large ones use up to 32 MB (few, large RCCL calls over xGMI)
+        total_bytes = net.store.total * 4
+        if bucket_mb is None:
+            self.bucket_bytes = int(min(32 << 20, max(64 << 10, total_bytes // 4)))
+        else:
+            self.bucket_bytes = int(bucket_mb * (1 << 20))
         self._build_buckets()
         self._works = []
         self._graph = None
         self._graph_B = None
+        self._index_stream = None
         self.steps = 0
         if broadcast_init and self.world > 1:
             dist.broadcast(net.store.master, src=0, group=group)
@@ -92,7 +99,7 @@ class DataParallelTrainer:
         hook = self._grad_ready if (self.overlap and self.world > 1) else None
         stats = self.net.compute_gradients(x, y, grad_ready=hook)
         self._allreduce_all()
-        self.net.store.sgd_step()
+        self.net.store.sgd_step(self._index_stream)
         return stats
 
     def set_lr(self, lr: float):
@@ -133,12 +140,21 @@ class DataParallelTrainer:
         net = self.net
         s = torch.cuda.Stream(device=net.device)
         s.wait_stream(torch.cuda.current_stream(net.device))
-        # warm-up on a side stream (allocator, RCCL communicators, kernel code objects)
+        # warm-up on a side stream (allocator, RCCL communicators, kernel code objects); the warm-up
+        # steps are not training steps: the engine state is restored before capture
+        snap = net.snapshot_state()
+        cursor = self._index_stream[1].clone() if self._index_stream is not None else None
+        idx0 = self.idx.clone()
         with torch.cuda.stream(s):
             for _ in range(3):
                 self._gather()
                 self._step_body(self.xb, self.yb)
         torch.cuda.current_stream(net.device).wait_stream(s)
+        torch.cuda.synchronize(net.device)
+        net.restore_state(snap)
+        self.idx.copy_(idx0)
+        if cursor is not None:
+            self._index_stream[1].copy_(cursor)
         torch.cuda.synchronize(net.device)
         g = torch.cuda.CUDAGraph()
         if self.graph_mode == "full":
@@ -152,34 +168,72 @@ class DataParallelTrainer:
                 self._gather()
                 self.stats = self.net.compute_gradients(self.xb, self.yb)
             with torch.cuda.graph(g2):
-                self.net.store.sgd_step()
+                self.net.store.sgd_step(self._index_stream)
             self._graph = (g, g2)
         torch.cuda.synchronize(net.device)
 
+    def bind_index_stream(self, stream: torch.Tensor):
+        """Device-resident batch schedule ``stream`` [nsteps][B] (int64, this rank's rows): the step's
+        optimizer launch stages the next step's indices itself (csrc/optim.hip), so :meth:`step`
+        is a bare graph replay.  Wraps around after ``nsteps`` steps."""
+        if stream.shape[1] != self.B:
+            raise ValueError(f"index stream rows must have {self.B} indices")
+        stream = stream.to(self.idx.device, torch.int64).contiguous()
+        cursor = torch.zeros(1, dtype=torch.int64, device=self.idx.device)
+        self.idx.copy_(stream[0])
+        if self._index_stream is None or self._index_stream[0].shape != stream.shape:
+            self._graph = None  # the captured optimizer launch references the stream buffers
+        self._index_stream = (stream, cursor, self.idx)
+
+    def step(self):
+        """One training step on the next batch of the bound index stream."""
+        if self._index_stream is None:
+            raise RuntimeError("bind_index_stream() first")
+        self.steps += 1
+        if self.graph_mode == "none":
+            self._gather()
+            return self._step_body(self.xb, self.yb)
+        if self._graph is None:
+            self._capture_with_fallback()
+            if self._graph is None:
+                return self._last_eager
+        return self._replay()
+
     def step_indices(self, idx: torch.Tensor):
         """One training step on dataset rows ``idx`` (device int64 [B])."""
+        if self._index_stream is not None:
+            raise RuntimeError("an index stream is bound: use step()")
         self.idx.copy_(idx, non_blocking=True)
         self.steps += 1
         if self.graph_mode == "none":
             self._gather()
             return self._step_body(self.xb, self.yb)
         if self._graph is None:
-            # capture fallback chain full -> split -> none (eager); every failure is recorded
-            while True:
-                try:
-                    self._capture()
-                    break
-                except Exception as e:  # e.g. collective capture unsupported by this RCCL/driver
-                    torch.cuda.synchronize(self.net.device)
-                    self.capture_error = repr(e)
-                    self._works = []
-                    self._graph = None
-                    if self.graph_mode == "full":
-                        self.graph_mode = "split"
-                    else:
-                        self.graph_mode = "none"
-                        self._gather()
-                        return self._step_body(self.xb, self.yb)
+            self._capture_with_fallback()
+            if self._graph is None:
+                return self._last_eager
+        return self._replay()
+
+    def _capture_with_fallback(self):
+        """Capture fallback chain full -> split -> none (eager); every failure is recorded."""
+        while True:
+            try:
+                self._capture()
+                return
+            except Exception as e:  # e.g. collective capture unsupported by this RCCL/driver
+                torch.cuda.synchronize(self.net.device)
+                self.capture_error = repr(e)
+                self._works = []
+                self._graph = None
+                if self.graph_mode == "full":
+                    self.graph_mode = "split"
+                else:
+                    self.graph_mode = "none"
+                    self._gather()
+                    self._last_eager = self._step_body(self.xb, self.yb)
+                    return
+
+    def _replay(self):
         g, g2 = self._graph
         g.replay()
         if g2 is not None:

@@ -128,3 +128,26 @@ def test_training_converges_on_synthetic_mnist():
     for i in range(1, 60):
         st = tr.step_indices(perm[i])
     assert float(st[0]) / 64 < 0.5 * first
+
+
+def test_index_stream_cpu_eager():
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
+
+    data, labels = synthetic_mnist(512, seed=2)
+    perm = epoch_permutations(512, 32, 3, "cpu", seed=4)
+    outs = []
+    for mode in ("explicit", "stream"):
+        net = build_model("mlp_mnist", device="cpu", seed=0)
+        tr = DataParallelTrainer(net, lr=0.1, graph="none")
+        tr.bind_dataset(data, labels, 32, scale=1 / 255)
+        if mode == "explicit":
+            for i in range(3):
+                tr.step_indices(perm[i])
+        else:
+            tr.bind_index_stream(perm)
+            for _ in range(3):
+                tr.step()
+        outs.append(net.store.master.clone())
+    assert torch.equal(outs[0], outs[1])

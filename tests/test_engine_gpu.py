@@ -144,3 +144,28 @@ def test_training_reaches_heldout_accuracy(name, graph, lr):
     assert tr.graph_mode == graph
     loss, acc = net.evaluate(test_x.float() / 255, test_y)
     assert acc > 0.9, (loss, acc)
+
+
+def test_index_stream_matches_explicit_indices():
+    """bind_index_stream + step() (next batch staged by the optimizer launch) == step_indices(perm[i]),
+    and graph capture's warm-up steps leave no trace in the trained weights."""
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
+
+    data, labels = synthetic_mnist(4096, device="cuda")
+    perm = epoch_permutations(4096, 256, 6, "cuda", seed=1)
+    outs = []
+    for mode in ("explicit", "stream"):
+        net = build_model("lenet5", device="cuda", seed=0)
+        tr = DataParallelTrainer(net, lr=0.05, graph="full")
+        tr.bind_dataset(data, labels, 256, scale=1 / 255)
+        if mode == "explicit":
+            for i in range(6):
+                tr.step_indices(perm[i])
+        else:
+            tr.bind_index_stream(perm)
+            for _ in range(6):
+                tr.step()
+        torch.cuda.synchronize()
+        outs.append(net.store.master.clone())
+    assert torch.equal(outs[0], outs[1])
