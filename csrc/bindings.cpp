@@ -379,8 +379,8 @@ void convpool_fwd_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double s
   CPIn in = cp_input(x, idx, B, (int64_t)H * W * C);
   need(w, at::kBFloat16, "w");
   // row-segment layout [Npad16][Kpad2] (ParamSpec.row_pad / row_cp, convpool_fwd_layout)
-  int Cp = 0, Kpad2 = 0;
-  dfa::convpool_fwd_layout(H, W, C, KH, KW, pad, N, &Cp, &Kpad2);
+  int Cp = 0, Kpad2 = 0, pair = 0;
+  dfa::convpool_fwd_layout(H, W, C, KH, KW, pad, N, &Cp, &Kpad2, &pair);
   TORCH_CHECK(w.numel() >= (int64_t)((N + 15) / 16 * 16) * Kpad2 && w.size(-1) == Kpad2,
               "w must be the row-segment layout [Npad16][", Kpad2, "] (channel stride ", Cp, ")");
   const int OH = H + 2 * pad - KH + 1, OW = W + 2 * pad - KW + 1;
@@ -606,10 +606,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     }
   }, "profiling aid: per-block phase stamps of the convpool kernels");
   m.def("convpool_fwd_layout", [](int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t pad, int64_t N) {
-    int Cp = 0, Kpad2 = 0;
-    dfa::convpool_fwd_layout(H, W, C, KH, KW, pad, N, &Cp, &Kpad2);
-    return std::make_tuple(Cp, Kpad2);
-  }, "forward weight layout of the fused conv+pool kernel: (channel stride Cp, row length Kpad2)");
+    int Cp = 0, Kpad2 = 0, pair = 0;
+    dfa::convpool_fwd_layout(H, W, C, KH, KW, pad, N, &Cp, &Kpad2, &pair);
+    return std::make_tuple(Cp, Kpad2, pair);
+  }, "forward weight layout of the fused conv+pool kernel: (channel stride Cp, row length Kpad2, pair)");
   m.def("convpool_supported", &convpool_supported_py);
   m.def("head_train", &head_train_py, "fused dense head: forward + softmax-CE + backward (2 launches)");
   m.def("gather_labels", &gather_labels_py);

@@ -45,6 +45,8 @@ struct CPGeom {
   int Cp;                  // LDS channel stride of the forward image (>= C, zero-filled channels)
   int RLp, chunks, Kpad2;  // RLp = round8(KW*Cp), chunks = RLp/8, Kpad2 = round32(KH*RLp)
   int G, S, RowP, ystr, xs_img;  // G = gcd(C,8): copy ci is shifted by ci*G elements, S = 8/G copies
+  int pair;                       // forward pair mode (N <= 8): cols 8-15 = pixel x+1 via shifted weights
+  int wRLp, wKpad2;               // GLOBAL weight layout (row-segment, KW columns): round8(KW*Cp), row length
   int dbg;                        // profiling aid: bit0 skip staging, bit1 skip shift build, 16/32 early exits
   unsigned long long* stamps;     // profiling aid: per-block s_memtime stamps [grid][32] (nullptr = off)
 };
@@ -210,7 +212,11 @@ struct FwdU {
   static constexpr int value = NK <= 2 ? 4 : (NK <= 5 ? 2 : 1);
 };
 
-template <int NT, int NK, int CHM>
+// PAIR (N <= 8): columns 0-7 = channels at pixel (oy, 2px), columns 8-15 = the same channels at
+// (oy, 2px+1), through weights shifted by one kernel column; 16 rows = 8 windows x 2 rows, so one
+// MFMA tile covers 8 pool windows and only even-x pixels are read.  The two halves of each window
+// meet with one DPP row rotation by 8 lanes.
+template <int NT, int NK, int CHM, bool PAIR>
 __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, const void* x, int x_u8,
                                                            const long long* idx, long long nrows, float scale,
                                                            const bf16* __restrict__ w, const float* __restrict__ bias,
@@ -219,7 +225,8 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
   constexpr int BT = 8;  // shifted-copy build tasks per thread held in registers
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int npool = g.PH * g.PW;
-  const int tpi = (npool + 3) / 4;  // MFMA tiles (4 windows) per image
+  constexpr int WPT = PAIR ? 8 : 4;           // pool windows per MFMA tile
+  const int tpi = (npool + WPT - 1) / WPT;    // MFMA tiles per image
   const int gtiles = g.imgs * tpi;  // tiles per group
   int* ttab = reinterpret_cast<int*>(smem);                      // [gtiles*16] LDS offset of each tile row
   int2* wtab = reinterpret_cast<int2*>(ttab + gtiles * 16);      // [gtiles] (first pooled index, valid windows)
@@ -233,16 +240,18 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
   for (int e = tid; e < gtiles * 16; e += 256) {
     const int T = e >> 4, row = e & 15;
     const int i = dtpi.div(T), tw = T - i * tpi;
-    const int wg = tw * 4 + (row >> 2), j = row & 3;
+    // plain: row = 4 windows x (dy, dx);  pair: row = 8 windows x dy at even x
+    const int wg = PAIR ? tw * 8 + 2 * (row >> 2) + ((row & 3) >> 1) : tw * 4 + (row >> 2);
+    const int dy = PAIR ? (row & 1) : ((row & 3) >> 1), dx = PAIR ? 0 : (row & 1);
     int v = i * g.xs_img;
     if (wg < npool) {
       const int py = dPW.div(wg), px = wg - py * g.PW;
-      const int oy = 2 * py + (j >> 1), ox = 2 * px + (j & 1);
+      const int oy = 2 * py + dy, ox = 2 * px + dx;
       const int t0 = ox * g.Cp, sh = t0 & 7;
       v += oy * g.ystr + dG.div(sh) * g.RowP + (t0 - sh);
     }
     ttab[e] = v;
-    if (row == 0) wtab[T] = make_int2(i * npool + tw * 4, npool - tw * 4);
+    if (row == 0) wtab[T] = make_int2(i * npool + tw * WPT, npool - tw * WPT);
   }
   lds_zero(xs, g.imgs * g.xs_img);
   const int nk = g.Kpad2 / 32;
@@ -254,7 +263,7 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
     for (int t = 0; t < NT; ++t) {
       const int n = 16 * t + (lane & 15);
       if (s < nk && n < Npad)
-        bfr[s][t] = *reinterpret_cast<const bf16x8*>(w + (long long)n * g.Kpad2 + 32 * s + 8 * (lane >> 4));
+        bfr[s][t] = *reinterpret_cast<const bf16x8*>(w + (long long)n * g.wKpad2 + 32 * s + 8 * (lane >> 4));
       else
 #pragma unroll
         for (int e = 0; e < 8; ++e) bfr[s][t][e] = (bf16)0.f;
@@ -262,7 +271,7 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
   float bv[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int n = 16 * t + (lane & 15);
+    const int n = PAIR ? (lane & 7) : 16 * t + (lane & 15);
     bv[t] = (bias && n < g.N) ? bias[n] : 0.f;
   }
   int koff[NK];
@@ -302,7 +311,6 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
   }
   __syncthreads();
 
-  const int wl = lane >> 4;  // window of this lane's accumulator rows
   if (g.dbg & 32) {
     if (bv[0] == 12345.f && koff[0] == 7 && blim[0] == 3) p[0] = bfr[0][0][0];
     return;
@@ -374,6 +382,35 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
       for (int u = 0; u < U; ++u) {
         if (T0 + u >= ntiles) break;
         const int2 wt = wtab[T0 + u];
+        if (PAIR) {
+          // lane (row group gq, column n): acc rows = windows 2gq, 2gq+1 x dy, at dx = set = n >> 3.
+          // Each lane finishes window 2gq+set: own dx half + the partner's (lane ^ 8) half.
+          const int n = lane & 15, set = n >> 3, ch = n & 7, gq = lane >> 4;
+          const f32x4 a4 = acc[u][0];
+          const float m0 = fmaxf(a4[0], a4[1]), m1 = fmaxf(a4[2], a4[3]);
+          const int d0 = a4[1] > a4[0] ? 1 : 0, d1 = a4[3] > a4[2] ? 1 : 0;
+          // send the half the partner needs (its window 2gq + (1-set)), receive ours
+          const float sendm = set ? m0 : m1;
+          const int sendd = set ? d0 : d1;
+          const float pm = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sendm), 0x128, 0xf, 0xf, false));
+          const int pd = __builtin_amdgcn_mov_dpp(sendd, 0x128, 0xf, 0xf, false);
+          const float mo = set ? m1 : m0;
+          const int dd = set ? d1 : d0;
+          // window max over (dy, dx); ties resolve to the lower (dy*2 + dx) like the plain kernel
+          const int jo = dd * 2 + set, jp = pd * 2 + (1 - set);
+          const bool take_p = pm > mo || (pm == mo && jp < jo);
+          float m = take_p ? pm : mo;
+          const int am = take_p ? jp : jo;
+          const int wloc = 2 * gq + set;
+          if (ch < g.N && wloc < wt.y) {
+            m += bv[0];
+            const int o = (wt.x + wloc) * g.N + ch;
+            pg[o] = f2bf(fmaxf(m, 0.f));
+            if (cg) cg[o] = (uint8_t)(am | (m > 0.f ? 4 : 0));
+          }
+          continue;
+        }
+        const int wl = lane >> 4;  // window of this lane's accumulator rows
         if (wl >= wt.y) continue;
         const int o = (wt.x + wl) * g.N;
 #pragma unroll
@@ -1035,41 +1072,97 @@ static void set_fwd_layout(CPGeom& g, int Cp, int RowP, int ypad) {
   g.xs_img = g.Hp * g.ystr;
 }
 
-static double fwd_conflicts(const CPGeom& g) {
-  const int npool = g.PH * g.PW, tpi = cdiv(npool, 4);
+// Pixel (padded-image origin) of MFMA row m of forward tile tw; false when the row is padding.
+//  plain: rows = 4 windows x 4 pixels;  pair: rows = 8 windows x 2 dy at even x (odd x in cols 8-15)
+static bool fwd_row_pixel(const CPGeom& g, bool pair, int tw, int m, int* oy, int* ox) {
+  const int npool = g.PH * g.PW;
+  int wg, dy, dx;
+  if (pair) {
+    wg = tw * 8 + 2 * (m >> 2) + ((m & 3) >> 1);
+    dy = m & 1;
+    dx = 0;
+  } else {
+    wg = tw * 4 + (m >> 2);
+    dy = (m & 3) >> 1;
+    dx = m & 1;
+  }
+  if (wg >= npool) return false;
+  *oy = 2 * (wg / g.PW) + dy;
+  *ox = 2 * (wg % g.PW) + dx;
+  return true;
+}
+
+// Mean LDS cycles per A-fragment ds_read_b128 (1.0 = conflict free), from the ISA's lane grouping:
+// 4 groups of 16 lanes {0-3,12-15,20-27} {4-11,16-19,28-31} {32-35,44-47,52-59} {36-43,48-51,60-63},
+// bank = (addr/4) mod 64; each extra distinct 16-byte address on a busy slot adds a cycle.
+static double fwd_conflicts(const CPGeom& g, bool pair) {
+  static const int grp[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                 {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                                 {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                                 {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+  const int npool = g.PH * g.PW, wpt = pair ? 8 : 4, tpi = cdiv(npool, wpt);
+  const int nk = g.Kpad2 / 32;
   double tot = 0.0;
   int cnt = 0;
   for (int tw = 0; tw < tpi; ++tw) {
-    int slot[16];
-    for (int row = 0; row < 16; ++row) {
-      const int wg = tw * 4 + (row >> 2), j = row & 3;
-      int off = 0;
-      if (wg < npool) {
-        const int py = wg / g.PW, px = wg % g.PW;
-        const int oy = 2 * py + (j >> 1), ox = 2 * px + (j & 1);
+    int base[16];
+    for (int m = 0; m < 16; ++m) {
+      int oy, ox;
+      base[m] = 0;
+      if (fwd_row_pixel(g, pair, tw, m, &oy, &ox)) {
         const int t0 = ox * g.Cp, sh = t0 & 7;
-        off = oy * g.ystr + (sh / g.G) * g.RowP + (t0 - sh);
+        base[m] = oy * g.ystr + (sh / g.G) * g.RowP + (t0 - sh);
       }
-      slot[row] = (off / 8) & 7;  // 16-byte chunk within a 128-byte window
     }
-    for (int g0 = 0; g0 < 16; g0 += 8) {
-      int m = 1;
-      for (int a = 0; a < 8; ++a) {
-        int c = 0;
-        for (int b = 0; b < 8; ++b) c += slot[g0 + a] == slot[g0 + b];
-        m = max(m, c);
+    for (int sk = 0; sk < nk; ++sk) {
+      for (int q = 0; q < 4; ++q) {
+        int addr[16];
+        for (int i = 0; i < 16; ++i) {
+          const int l = grp[q][i], kq = 4 * sk + (l >> 4);
+          int koff = 0;
+          if (kq < g.KH * g.chunks) koff = (kq / g.chunks) * g.ystr + 8 * (kq % g.chunks);
+          addr[i] = base[l & 15] + koff;  // element offset (16-byte aligned)
+        }
+        int worst = 1;
+        for (int i = 0; i < 16; ++i) {
+          int distinct = 0;
+          for (int j = 0; j < 16; ++j) {
+            if (((addr[j] / 8) & 15) != ((addr[i] / 8) & 15)) continue;
+            bool seen = false;
+            for (int k2 = 0; k2 < j; ++k2)
+              if (addr[k2] == addr[j]) seen = true;
+            if (!seen) ++distinct;
+          }
+          worst = max(worst, distinct);
+        }
+        tot += worst;
+        ++cnt;
       }
-      tot += m;
-      ++cnt;
     }
   }
   return cnt ? tot / cnt : 1.0;
 }
 
-static const FwdLayout& choose_fwd_layout(const CPGeom& g0) {
+// pair mode (N <= 8): row segments cover KW+1 columns, only even-x pixels are read
+static void set_fwd_pair_layout(CPGeom& g) {
+  g.pair = 1;
+  g.RLp = round_up((g.KW + 1) * g.Cp, 8);
+  g.chunks = g.RLp / 8;
+  g.Kpad2 = round_up(g.KH * g.RLp, 32);
+  g.G = std::gcd(2 * g.Cp, 8);
+  g.S = 8 / g.G;
+  const int maxel = ((g.OW - 2) * g.Cp) / 8 * 8 + g.RLp;
+  const int minrow = round_up(max(g.Wp * g.Cp + 8, maxel), 8);
+  const int ypad = g.ystr - g.S * g.RowP;  // keep the row pad chosen for this layout
+  g.RowP = max(g.RowP, minrow);
+  g.ystr = g.S * g.RowP + max(ypad, 0);
+  g.xs_img = g.Hp * g.ystr;
+}
+
+static const FwdLayout& choose_fwd_layout(const CPGeom& g0, bool pair) {
   static std::mutex mu;
-  static std::map<std::array<int, 6>, FwdLayout> cache;
-  const std::array<int, 6> key{g0.H, g0.W, g0.C, g0.KH, g0.KW, g0.pad};
+  static std::map<std::array<int, 7>, FwdLayout> cache;
+  const std::array<int, 7> key{g0.H, g0.W, g0.C, g0.KH, g0.KW, g0.pad, pair ? 1 : 0};
   std::lock_guard<std::mutex> lock(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
@@ -1078,12 +1171,15 @@ static const FwdLayout& choose_fwd_layout(const CPGeom& g0) {
   for (int Cp : {g0.C, round_up(g0.C, 2), round_up(g0.C, 4), round_up(g0.C, 8)}) {
     CPGeom g = g0;
     set_fwd_layout(g, Cp, 0, 0);
+    if (pair) set_fwd_pair_layout(g);
     if (g.Kpad2 / 32 > 16) continue;
     const int minrow = g.RowP;
     for (int rp = minrow; rp < minrow + 64; rp += 8)
       for (int yp = 0; yp < 64; yp += 8) {
         set_fwd_layout(g, Cp, rp, yp);
-        const double score = (g.Kpad2 / 32) * fwd_conflicts(g) * (1.0 + 0.1 * (g.S - 1)) * (1.0 + 0.002 * g.xs_img / 64);
+        if (pair) set_fwd_pair_layout(g);
+        const double score =
+            (g.Kpad2 / 32) * fwd_conflicts(g, pair) * (1.0 + 0.1 * (g.S - 1)) * (1.0 + 0.002 * g.xs_img / 64);
         if (score < best_score - 1e-9) {
           best_score = score;
           best = FwdLayout{Cp, rp, yp};
@@ -1108,18 +1204,23 @@ static CPGeom make_geom(int B, int H, int W, int C, int KH, int KW, int pad, int
   g.Wp = W + 2 * pad;
   g.img_elems = round_up(g.Hp * g.Wp * C + 8, 8);  // +8: slack for the finite "padding column" reads
   set_fwd_layout(g, C, 0, 0);
-  const FwdLayout& L = choose_fwd_layout(g);
+  const bool pair = N <= 8 && g.OW >= 2;
+  const FwdLayout& L = choose_fwd_layout(g, pair);
   set_fwd_layout(g, L.Cp, L.RowP, L.ypad);
+  if (pair) set_fwd_pair_layout(g);
+  g.wRLp = g.RLp;  // the compute copy is emitted by the optimizer in exactly the kernel's layout
+  g.wKpad2 = g.Kpad2;
   return g;
 }
 
 static const size_t kLdsBudget = 64 * 1024;  // keeps >= 2 workgroups per CU (160 KiB LDS)
 constexpr int kStageChunks = 4;              // register-staged 4-element chunks per thread and group
 
-void convpool_fwd_layout(int H, int W, int C, int KH, int KW, int pad, int N, int* Cp, int* Kpad2) {
+void convpool_fwd_layout(int H, int W, int C, int KH, int KW, int pad, int N, int* Cp, int* Kpad2, int* pair) {
   CPGeom g = make_geom(1, H, W, C, KH, KW, pad, N);
   *Cp = g.Cp;
-  *Kpad2 = g.Kpad2;
+  *Kpad2 = g.wKpad2;
+  *pair = g.pair;
 }
 
 bool convpool_supported(int H, int W, int C, int KH, int KW, int pad, int N) {
@@ -1128,7 +1229,7 @@ bool convpool_supported(int H, int W, int C, int KH, int KW, int pad, int N) {
   if ((g.PH * g.PW * N) % 4 != 0) return false;  // 4-element pooled-gradient chunks (wgrad scatter plan)
   if (g.PH * g.PW * N > kStageChunks * 1024) return false;  // one image's pooled gradient fits the plan
   if (C > 16 || N > 32 || KH > 7 || KW > 7) return false;
-  if (g.Kpad2 / 32 > 16) return false;                    // fwd weight fragments in registers
+  if (g.Kpad2 / 32 > 16 || g.wKpad2 / 32 > 16) return false;  // fwd weight fragments in registers
   if ((g.K + 16) / 16 > 13) return false;                 // wgrad accumulators (incl. bias column)
   if (round_up(KH * KW * N, 32) / 32 > 16) return false;  // dgrad weight fragments
   const int P = KH - 1 - pad;
@@ -1186,12 +1287,12 @@ static Sizing size_persistent(const void* kern, int B, size_t fixed, size_t per_
   return z;
 }
 
-template <int NT, int NK>
+template <int NT, int NK, bool PAIR = false>
 static hipError_t launch_cp_fwd(CPGeom g, bool vec, const void* x, int x_u8, const long long* idx, long long nrows,
                                 float scale, const bf16* w, const float* bias, bf16* p, uint8_t* code,
                                 hipStream_t st) {
-  auto kern = convpool_fwd_kernel<NT, NK, kStageChunks>;
-  const int tpi = cdiv(g.PH * g.PW, 4);
+  auto kern = convpool_fwd_kernel<NT, NK, kStageChunks, PAIR>;
+  const int tpi = cdiv(g.PH * g.PW, PAIR ? 8 : 4);
   const Sizing z = size_persistent(reinterpret_cast<const void*>(kern), g.B, 32,
                                    (size_t)tpi * (16 * 4 + 8) + (size_t)g.xs_img * 2, 0,
                                    kStageChunks * 256 * 4 / (g.H * g.W * g.C));
@@ -1216,6 +1317,17 @@ hipError_t convpool_fwd(const void* x, int x_u8, const long long* idx, long long
   const int nk = g.Kpad2 / 32;
   const int nt = cdiv(N, 16);
 #define CP_FWD(NT_, NK_) return launch_cp_fwd<NT_, NK_>(g, vec, x, x_u8, idx, nrows, scale, w, bias, p, code, st)
+#define CP_FWDP(NK_) return launch_cp_fwd<1, NK_, true>(g, vec, x, x_u8, idx, nrows, scale, w, bias, p, code, st)
+  if (g.pair) {
+    if (nk <= 1) CP_FWDP(1);
+    if (nk <= 2) CP_FWDP(2);
+    if (nk <= 3) CP_FWDP(3);
+    if (nk <= 4) CP_FWDP(4);
+    if (nk <= 5) CP_FWDP(5);
+    if (nk <= 7) CP_FWDP(7);
+    if (nk <= 10) CP_FWDP(10);
+    CP_FWDP(16);
+  }
   if (nt == 1) {
     if (nk <= 1) CP_FWD(1, 1);
     if (nk <= 2) CP_FWD(1, 2);
@@ -1237,6 +1349,7 @@ hipError_t convpool_fwd(const void* x, int x_u8, const long long* idx, long long
   if (nk <= 13) CP_FWD(2, 13);
   CP_FWD(2, 16);
 #undef CP_FWD
+#undef CP_FWDP
 }
 
 static CPWg make_wg(const CPGeom& g) {

@@ -42,9 +42,12 @@ __device__ __forceinline__ void sgd_multi_body(const ParamDesc* __restrict__ des
   const int K = d.T * d.Ci;
   // d.pad_ = KW | Cp << 16 (KW > 0): the primary copy uses the row-segment layout of the fused
   // conv+pool forward, [Npad16][round32(KH * round8(KW*Cp))], column ky*round8(KW*Cp) + kx*Cp + ci
+  // d.pad_ = KW | Cp << 16 | pair << 30: pair layout (N <= 8) = 16 rows, rows 8+n hold channel n
+  // shifted right by one kernel column (the fused conv+pool forward computes pixels x and x+1)
   const int rKW = d.pad_ & 0xffff;
-  const int rCp = (d.pad_ >> 16) > 0 ? (d.pad_ >> 16) : d.Ci;
-  const int RLp = rKW > 0 ? round_up(rKW * rCp, 8) : K;
+  const int rCp = ((d.pad_ >> 16) & 0x3fff) > 0 ? ((d.pad_ >> 16) & 0x3fff) : d.Ci;
+  const bool rpair = (d.pad_ >> 30) & 1;
+  const int RLp = rKW > 0 ? round_up((rKW + (rpair ? 1 : 0)) * rCp, 8) : K;
   const int Kpad = round_up(rKW > 0 ? (d.T / rKW) * RLp : K, 32);
   const int KpadT = round_up(d.T * d.N, 32);
 #pragma unroll
@@ -74,6 +77,7 @@ __device__ __forceinline__ void sgd_multi_body(const ParamDesc* __restrict__ des
         col = ky * RLp + kx * rCp + ci;
       }
       wbf[d.bf_off + (long long)n * Kpad + col] = wb;
+      if (rpair) wbf[d.bf_off + (long long)(n + 8) * Kpad + col + rCp] = wb;
       if (d.bft_off >= 0) {
         const int t = kk / d.Ci;
         const int ci = kk - t * d.Ci;

@@ -510,8 +510,8 @@ class FusedConvPool(Layer):
         sp = self.conv.specs()
         # the forward reads the row-segment weight layout chosen by the kernel (csrc/convpool.hip)
         H, W, C = self.in_shape
-        sp[0].row_pad = self.k
-        sp[0].row_cp = ops.convpool_fwd_layout(H, W, C, self.k, self.k, self.pad, self.conv.filters)[0]
+        cp, _, pair = ops.convpool_fwd_layout(H, W, C, self.k, self.k, self.pad, self.conv.filters)
+        sp[0].row_pad, sp[0].row_cp, sp[0].row_pair = self.k, cp, bool(pair)
         return sp
 
     split_backward = True

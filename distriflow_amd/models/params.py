@@ -38,7 +38,7 @@ def primary_kpad(spec: "ParamSpec") -> int:
     N, T, Ci = spec.mat
     if spec.row_pad:
         cp = spec.row_cp or Ci
-        return _r((T // spec.row_pad) * _r(spec.row_pad * cp, 8), 32)
+        return _r((T // spec.row_pad) * _r((spec.row_pad + (1 if spec.row_pair else 0)) * cp, 8), 32)
     return _r(T * Ci, 32)
 
 
@@ -53,6 +53,7 @@ class ParamSpec:
     needs_dgrad: bool = True        # keep a bf16 dgrad-layout copy
     row_pad: int = 0                # KW > 0: primary bf16 copy in the fused conv+pool row-segment layout
     row_cp: int = 0                 #   ... with LDS channel stride Cp (>= Ci; 0 = Ci)
+    row_pair: bool = False          #   ... pair layout: rows 8+n = row n shifted by one kernel column
     trainable: bool = True
 
     @property
@@ -168,7 +169,8 @@ class ParamStore:
                     N, T, Ci = 1, 1, s.numel
                 descs.append((self.offsets[s.name], bf_off, bft_off, s.numel, N, T, Ci, block,
                               0 if s.trainable else 1,
-                              (s.row_pad | (s.row_cp << 16)) if s.kind == "matrix" else 0))
+                              (s.row_pad | (s.row_cp << 16) | ((1 << 30) if s.row_pair else 0))
+                              if s.kind == "matrix" else 0))
                 block += nblocks
         self.wbf = torch.zeros(max(boff, 8), dtype=torch.bfloat16, device=self.device)
         self._wbf_views = {}

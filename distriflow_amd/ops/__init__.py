@@ -286,7 +286,7 @@ def convpool_supported(H, W, C, KH, KW, pad, N) -> bool:
 
 
 def convpool_fwd_layout(H, W, C, KH, KW, pad, N):
-    """(channel stride Cp, row length Kpad2) of the fused conv+pool forward weight layout."""
+    """(channel stride Cp, row length Kpad2, pair) of the fused conv+pool forward weight layout."""
     return tuple(_C().convpool_fwd_layout(H, W, C, KH, KW, pad, N))
 
 

@@ -68,17 +68,18 @@ def test_sgd_step_and_bf16_copies():
         N, T, Ci = spec.mat
         w = st[spec.name].reshape(N, T * Ci)
         wb = st.weight(spec.name)
-        if spec.row_pad:  # fused conv+pool row-segment layout
+        if spec.row_pad:  # fused conv+pool row-segment layout (+ shifted rows 8+n in pair mode)
             KW = spec.row_pad
             KH, Cp = T // KW, spec.row_cp or Ci
-            RLp = (KW * Cp + 7) // 8 * 8
-            exp = torch.zeros(N, wb.shape[1], dtype=torch.bfloat16, device=w.device)
+            RLp = ((KW + (1 if spec.row_pair else 0)) * Cp + 7) // 8 * 8
+            exp = torch.zeros(wb.shape[0], wb.shape[1], dtype=torch.bfloat16, device=w.device)
             w4 = w.view(N, KH, KW, Ci).to(torch.bfloat16)
             for ky in range(KH):
                 for kx in range(KW):
-                    exp[:, ky * RLp + kx * Cp: ky * RLp + kx * Cp + Ci] = w4[:, ky, kx]
-            assert torch.equal(wb[:N], exp)
-            assert wb[N:].abs().sum() == 0
+                    exp[:N, ky * RLp + kx * Cp: ky * RLp + kx * Cp + Ci] = w4[:, ky, kx]
+                    if spec.row_pair:
+                        exp[8:8 + N, ky * RLp + (kx + 1) * Cp: ky * RLp + (kx + 1) * Cp + Ci] = w4[:, ky, kx]
+            assert torch.equal(wb, exp)
         else:
             assert torch.equal(wb[:N, :T * Ci], w.to(torch.bfloat16))
             assert wb[N:].abs().sum() == 0 and wb[:, T * Ci:].abs().sum() == 0

@@ -27,17 +27,20 @@ def _pad_w(w2d):
 
 
 def _rowpad_w(w2d, KH, KW, C, H, W, pad):
-    """fp32 [N][KH*KW*C] -> fused conv+pool forward layout bf16 [Npad16][Kpad2], column
-    ky*round8(KW*Cp) + kx*Cp + c with the kernel's chosen channel stride Cp."""
+    """fp32 [N][KH*KW*C] -> fused conv+pool forward layout bf16 [Npad16][Kpad2]: column
+    ky*RLp + kx*Cp + c with the kernel's channel stride Cp; pair layout (N <= 8) additionally holds
+    in rows 8+n the kernel of channel n shifted right by one column (RLp = round8((KW+1)*Cp))."""
     from distriflow_amd import ops as O
     N = w2d.shape[0]
-    Cp, kp = O.convpool_fwd_layout(H, W, C, KH, KW, pad, N)
-    RLp = _r(KW * Cp, 8)
+    Cp, kp, pair = O.convpool_fwd_layout(H, W, C, KH, KW, pad, N)
+    RLp = _r((KW + (1 if pair else 0)) * Cp, 8)
     out = torch.zeros(_r(N, 16), kp, dtype=torch.bfloat16, device=dev)
     w4 = w2d.view(N, KH, KW, C).to(torch.bfloat16)
     for ky in range(KH):
         for kx in range(KW):
             out[:N, ky * RLp + kx * Cp: ky * RLp + kx * Cp + C] = w4[:, ky, kx]
+            if pair:
+                out[8:8 + N, ky * RLp + (kx + 1) * Cp: ky * RLp + (kx + 1) * Cp + C] = w4[:, ky, kx]
     return out
 
 
