@@ -441,8 +441,11 @@ void convpool_dgrad_py(torch::Tensor dp, torch::Tensor code, torch::Tensor wt, t
   need(code, at::kByte, "code");
   TORCH_CHECK(dp.numel() >= pn && code.numel() >= pn, "dp/code too small");
   need(wt, at::kBFloat16, "wt");
-  const int K2pad = (KH * KW * N + 31) / 32 * 32;
-  TORCH_CHECK(wt.size(-1) == K2pad && wt.numel() >= (int64_t)((C + 15) / 16 * 16) * K2pad, "wt must be [Cpad16][K2pad]");
+  int pair = 0, K2pad = 0;
+  dfa::convpool_dgrad_layout(H, W, C, KH, KW, pad, N, &pair, &K2pad);
+  const int rows = pair ? 16 : (C + 15) / 16 * 16;
+  TORCH_CHECK(wt.size(-1) == K2pad && wt.numel() >= (int64_t)rows * K2pad, "wt must be the dgrad layout [", rows,
+              "][", K2pad, "] (pair ", pair, ")");
   need(dx, at::kBFloat16, "dx");
   TORCH_CHECK(dx.numel() >= (int64_t)B * H * W * C, "dx too small");
   check_hip(dfa::convpool_dgrad((const dfa::bf16*)dp.data_ptr(), code.data_ptr<uint8_t>(),
@@ -610,6 +613,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     dfa::convpool_fwd_layout(H, W, C, KH, KW, pad, N, &Cp, &Kpad2, &pair);
     return std::make_tuple(Cp, Kpad2, pair);
   }, "forward weight layout of the fused conv+pool kernel: (channel stride Cp, row length Kpad2, pair)");
+  m.def("convpool_dgrad_layout", [](int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t pad, int64_t N) {
+    int pair = 0, K2pad = 0;
+    dfa::convpool_dgrad_layout(H, W, C, KH, KW, pad, N, &pair, &K2pad);
+    return std::make_tuple(pair, K2pad);
+  }, "data-gradient weight layout of the fused conv+pool kernel: (pair, row length K2pad)");
   m.def("convpool_supported", &convpool_supported_py);
   m.def("head_train", &head_train_py, "fused dense head: forward + softmax-CE + backward (2 launches)");
   m.def("gather_labels", &gather_labels_py);

@@ -780,18 +780,49 @@ __global__ void __launch_bounds__(256) convpool_wgrad_kernel(CPGeom g, CPWg q, i
 // Data gradient through the pool: dx[b][iy][ix][c] = sum_{ky,kx,n} dConv[iy+pad-ky][ix+pad-kx][n] W[n][ky][kx][c]
 struct CPDgrad {
   int Hq, Wq, q_elems, P;  // padded dConv image in LDS, P = KH-1-pad
-  int K2, K2pad;           // K2 = KH*KW*N
+  int K2, K2pad;           // K2 = KH*KW*N  (pair: KH*(KW+1)*N)
   int Nq;                  // LDS pixel stride (>= N): 16-byte reads of 8 consecutive pixels hit distinct banks
+  int pair;                // C <= 8, W even: MFMA rows = pixel pairs, columns 8-15 = pixel x+1 (shifted weights)
 };
 
-template <int NT, int NKMAX, bool VEC, int CHM>
+// dgrad weight layouts (emitted by the optimizer, csrc/optim.hip):
+//  plain: [Cpad16][round32(KH*KW*N)],   element (c, (ky*KW+kx)*N + n) = W[n][ky][kx][c]
+//  pair:  [16][round32(KH*(KW+1)*N)],  patch tap (a, b) = (row, col) of the flipped kernel window:
+//         row c   : col (a*(KW+1) + b)*N + n = W[n][KH-1-a][KW-1-b][c]    (b < KW)
+//         row 8+c : col (a*(KW+1) + b)*N + n = W[n][KH-1-a][KW-b][c]      (b >= 1)
+static CPGeom make_geom(int B, int H, int W, int C, int KH, int KW, int pad, int N);
+
+static CPDgrad make_dgrad(const CPGeom& g) {
+  CPDgrad d{};
+  d.P = g.KH - 1 - g.pad;
+  d.Hq = g.OH + 2 * d.P;
+  d.Wq = g.OW + 2 * d.P;
+  // pixel stride: a multiple of 8 elements with an odd number of 16-byte chunks, so 8 consecutive
+  // pixels start in 8 different 16-byte bank groups
+  d.Nq = g.N % 8 == 0 ? ((g.N / 8) % 2 == 1 ? g.N : g.N + 8) : g.N;
+  d.q_elems = round_up(d.Hq * d.Wq * d.Nq + 8, 8);
+  d.pair = (g.C <= 8 && g.W % 2 == 0 && g.N % 8 == 0) ? 1 : 0;
+  d.K2 = g.KH * (g.KW + d.pair) * g.N;
+  d.K2pad = round_up(d.K2, 32);
+  return d;
+}
+
+void convpool_dgrad_layout(int H, int W, int C, int KH, int KW, int pad, int N, int* pair, int* K2pad) {
+  CPGeom g = make_geom(1, H, W, C, KH, KW, pad, N);
+  const CPDgrad d = make_dgrad(g);
+  *pair = d.pair;
+  *K2pad = d.K2pad;
+}
+
+template <int NT, int NKMAX, bool VEC, int CHM, bool PAIR>
 __global__ void __launch_bounds__(256) convpool_dgrad_kernel(CPGeom g, CPDgrad d, const bf16* __restrict__ dp,
                                                              const uint8_t* __restrict__ code,
                                                              const bf16* __restrict__ wt, bf16* __restrict__ dx) {
   constexpr int U = NKMAX <= 4 ? 4 : (NKMAX <= 8 ? 2 : 1);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int HW = g.H * g.W;
-  const int tpi = (HW + 15) / 16;
+  const int nrow = PAIR ? HW / 2 : HW;  // MFMA rows per image: pixels, or pixel pairs (x even, x+1)
+  const int tpi = (nrow + 15) / 16;
   const int gtiles = g.imgs * tpi;
   int* ttab = reinterpret_cast<int*>(smem);             // [gtiles*16] input pixel -> qs offset
   int2* otab = reinterpret_cast<int2*>(ttab + gtiles * 16);  // [gtiles] (first output pixel, valid pixels)
@@ -800,24 +831,25 @@ __global__ void __launch_bounds__(256) convpool_dgrad_kernel(CPGeom g, CPDgrad d
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   CP_STAMP(0);
   const int npool = g.PH * g.PW;
-  const FDiv dtpi(tpi), dW(g.W);
+  const FDiv dtpi(tpi), dW(PAIR ? g.W / 2 : g.W);
   for (int e = tid; e < gtiles * 16; e += 256) {
     const int T = e >> 4, i = dtpi.div(T), tw = T - i * tpi;
     const int px = tw * 16 + (e & 15);
     int v = i * d.q_elems;
-    if (px < HW) {
-      const int iy = dW.div(px), ix = px - iy * g.W;
+    if (px < nrow) {
+      const int iy = dW.div(px), ix = (px - iy * (PAIR ? g.W / 2 : g.W)) * (PAIR ? 2 : 1);
       v += (iy * d.Wq + ix) * d.Nq;
     }
     ttab[e] = v;
-    if ((e & 15) == 0) otab[T] = make_int2(i * HW + tw * 16, HW - tw * 16);
+    if ((e & 15) == 0) otab[T] = make_int2(i * nrow + tw * 16, nrow - tw * 16);
   }
-  const FDiv dNk(g.N), dKWk(g.KW);
+  const FDiv dNk(g.N), dKWk(PAIR ? g.KW + 1 : g.KW);
   for (int k = tid; k < d.K2pad; k += 256) {
     int v = 0;
     if (k < d.K2) {
-      const int t = dNk.div(k), n = k - t * g.N, ky = dKWk.div(t), kx = t - ky * g.KW;
-      v = ((g.KH - 1 - ky) * d.Wq + (g.KW - 1 - kx)) * d.Nq + n;
+      const int t = dNk.div(k), n = k - t * g.N, ky = dKWk.div(t), kx = t - ky * (PAIR ? g.KW + 1 : g.KW);
+      // pair: k = (patch row a, patch col b, n) in patch order (the flip lives in the weights)
+      v = PAIR ? (ky * d.Wq + kx) * d.Nq + n : ((g.KH - 1 - ky) * d.Wq + (g.KW - 1 - kx)) * d.Nq + n;
     }
     klut[k] = v;
   }
@@ -941,6 +973,17 @@ __global__ void __launch_bounds__(256) convpool_dgrad_kernel(CPGeom g, CPDgrad d
       for (int u = 0; u < U; ++u) {
         if (T0 + u >= ntiles) break;
         const int2 ot = otab[T0 + u];
+        if (PAIR) {  // column n: pixel 2*pair + (n >> 3), channel n & 7
+          const int c = lane & 7, set = (lane >> 3) & 1;
+          if (c < g.C) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int mm = 4 * (lane >> 4) + r;
+              if (mm < ot.y) xg[(long long)(2 * (ot.x + mm) + set) * g.C + c] = f2bf(acc[u][0][r]);
+            }
+          }
+          continue;
+        }
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const int c = 16 * t + (lane & 15);
@@ -1231,7 +1274,11 @@ bool convpool_supported(int H, int W, int C, int KH, int KW, int pad, int N) {
   if (C > 16 || N > 32 || KH > 7 || KW > 7) return false;
   if (g.Kpad2 / 32 > 16 || g.wKpad2 / 32 > 16) return false;  // fwd weight fragments in registers
   if ((g.K + 16) / 16 > 13) return false;                 // wgrad accumulators (incl. bias column)
-  if (round_up(KH * KW * N, 32) / 32 > 16) return false;  // dgrad weight fragments
+  if (KH != KW) return false;  // dConv padding P = KH-1-pad is shared by both axes
+  {
+    const CPDgrad d = make_dgrad(g);
+    if (d.K2pad / 32 > (d.pair ? 18 : 16)) return false;  // dgrad weight fragments in registers
+  }
   const int P = KH - 1 - pad;
   if (P < 0) return false;
   const int Nq = N % 8 == 0 ? ((N / 8) % 2 == 1 ? N : N + 8) : N;
@@ -1434,11 +1481,12 @@ hipError_t convpool_wgrad(const void* x, int x_u8, const long long* idx, long lo
 #undef CP_WG
 }
 
-template <int NT, int NKMAX, bool VEC>
+template <int NT, int NKMAX, bool VEC, bool PAIR = false>
 static hipError_t launch_cp_dgrad(CPGeom g, const CPDgrad& d, bool plan, const bf16* dp, const uint8_t* code,
                                   const bf16* wt, bf16* dx, hipStream_t st) {
-  auto kern = plan ? convpool_dgrad_kernel<NT, NKMAX, VEC, kStageChunks> : convpool_dgrad_kernel<NT, NKMAX, VEC, 0>;
-  const int tpi = cdiv(g.H * g.W, 16);
+  auto kern = plan ? convpool_dgrad_kernel<NT, NKMAX, VEC, kStageChunks, PAIR>
+                   : convpool_dgrad_kernel<NT, NKMAX, VEC, 0, PAIR>;
+  const int tpi = cdiv(PAIR ? g.H * g.W / 2 : g.H * g.W, 16);
   const int wn = g.PH * g.PW * g.N;
   const Sizing z = size_persistent(reinterpret_cast<const void*>(kern), g.B, (size_t)d.K2pad * 4 + 32,
                                    (size_t)tpi * 72 + (size_t)d.q_elems * 2, 0, plan ? kStageChunks * 256 * 4 / wn : 32);
@@ -1451,21 +1499,19 @@ hipError_t convpool_dgrad(const bf16* dp, const uint8_t* code, const bf16* wt, b
                           int KH, int KW, int pad, int N, hipStream_t st) {
   if (!convpool_supported(H, W, C, KH, KW, pad, N)) return hipErrorInvalidValue;
   CPGeom g = make_geom(B, H, W, C, KH, KW, pad, N);
-  CPDgrad d{};
-  d.P = KH - 1 - pad;
-  d.Hq = g.OH + 2 * d.P;
-  d.Wq = g.OW + 2 * d.P;
-  // pixel stride: a multiple of 8 elements with an odd number of 16-byte chunks, so 8 consecutive
-  // pixels start in 8 different 16-byte bank groups
-  d.Nq = N % 8 == 0 ? ((N / 8) % 2 == 1 ? N : N + 8) : N;
-  d.q_elems = round_up(d.Hq * d.Wq * d.Nq + 8, 8);
-  d.K2 = KH * KW * N;
-  d.K2pad = round_up(d.K2, 32);
+  const CPDgrad d = make_dgrad(g);
   const int wn = g.PH * g.PW * N;
   const bool plan = wn % 4 == 0 && wn <= kStageChunks * 1024 && reinterpret_cast<uintptr_t>(dp) % 8 == 0 &&
                     reinterpret_cast<uintptr_t>(code) % 4 == 0;
   const int nk = d.K2pad / 32;
   if (cdiv(C, 16) != 1) return hipErrorInvalidValue;
+  if (d.pair) {
+    if (nk <= 4) return launch_cp_dgrad<1, 4, true, true>(g, d, plan, dp, code, wt, dx, st);
+    if (nk <= 8) return launch_cp_dgrad<1, 8, true, true>(g, d, plan, dp, code, wt, dx, st);
+    if (nk <= 12) return launch_cp_dgrad<1, 12, true, true>(g, d, plan, dp, code, wt, dx, st);
+    if (nk <= 15) return launch_cp_dgrad<1, 15, true, true>(g, d, plan, dp, code, wt, dx, st);
+    return launch_cp_dgrad<1, 18, true, true>(g, d, plan, dp, code, wt, dx, st);
+  }
   if (N % 8 == 0) {
     if (nk <= 2) return launch_cp_dgrad<1, 2, true>(g, d, plan, dp, code, wt, dx, st);
     if (nk <= 4) return launch_cp_dgrad<1, 4, true>(g, d, plan, dp, code, wt, dx, st);

@@ -119,6 +119,7 @@ void convpool_set_stamps(void* buf);  // [grid][32] uint64 s_memtime stamps, nul
 // forward weight layout: [Npad16][Kpad2], column ky*RLp + kx*Cp + c (zero for c >= C) with
 // RLp = round8(KW*Cp); pair layout (N <= 8): RLp = round8((KW+1)*Cp) and rows 8+n = row n shifted by Cp
 void convpool_fwd_layout(int H, int W, int C, int KH, int KW, int pad, int N, int* Cp, int* Kpad2, int* pair);
+void convpool_dgrad_layout(int H, int W, int C, int KH, int KW, int pad, int N, int* pair, int* K2pad);
 bool convpool_supported(int H, int W, int C, int KH, int KW, int pad, int N);
 hipError_t convpool_fwd(const void* x, int x_u8, const long long* idx, long long nrows, float scale, int B, int H,
                         int W, int C, int KH, int KW, int pad, int N, const bf16* w, const float* bias, bf16* p,

@@ -45,11 +45,15 @@ __device__ __forceinline__ void sgd_multi_body(const ParamDesc* __restrict__ des
   // d.pad_ = KW | Cp << 16 | pair << 30: pair layout (N <= 8) = 16 rows, rows 8+n hold channel n
   // shifted right by one kernel column (the fused conv+pool forward computes pixels x and x+1)
   const int rKW = d.pad_ & 0xffff;
-  const int rCp = ((d.pad_ >> 16) & 0x3fff) > 0 ? ((d.pad_ >> 16) & 0x3fff) : d.Ci;
+  // d.pad_ bit 29: the dgrad copy uses the conv+pool dgrad pair layout (csrc/convpool.hip make_dgrad),
+  // [16][round32(KH*(KW+1)*N)]: row ci col (a*(KW+1) + KW-1-kx)*N + n and row 8+ci col (a*(KW+1) + KW-kx)*N + n,
+  // a = KH-1-ky (the kernel flip of the transposed convolution)
+  const int rCp = ((d.pad_ >> 16) & 0x1fff) > 0 ? ((d.pad_ >> 16) & 0x1fff) : d.Ci;
   const bool rpair = (d.pad_ >> 30) & 1;
+  const bool tpair = rKW > 0 && ((d.pad_ >> 29) & 1);
   const int RLp = rKW > 0 ? round_up((rKW + (rpair ? 1 : 0)) * rCp, 8) : K;
   const int Kpad = round_up(rKW > 0 ? (d.T / rKW) * RLp : K, 32);
-  const int KpadT = round_up(d.T * d.N, 32);
+  const int KpadT = round_up(tpair ? (d.T / rKW) * (rKW + 1) * d.N : d.T * d.N, 32);
 #pragma unroll
   for (int r = 0; r < SGD_ELEMS_PER_BLOCK / 256; ++r) {
     const int i = base + r * 256 + threadIdx.x;
@@ -81,7 +85,14 @@ __device__ __forceinline__ void sgd_multi_body(const ParamDesc* __restrict__ des
       if (d.bft_off >= 0) {
         const int t = kk / d.Ci;
         const int ci = kk - t * d.Ci;
-        wbf[d.bft_off + (long long)ci * KpadT + t * d.N + n] = wb;
+        if (tpair) {
+          const int ky = t / rKW, kx = t - ky * rKW;
+          const int c0 = ((d.T / rKW - 1 - ky) * (rKW + 1) + rKW - 1 - kx) * d.N + n;
+          wbf[d.bft_off + (long long)ci * KpadT + c0] = wb;
+          wbf[d.bft_off + (long long)(ci + 8) * KpadT + c0 + d.N] = wb;
+        } else {
+          wbf[d.bft_off + (long long)ci * KpadT + t * d.N + n] = wb;
+        }
       }
     }
   }

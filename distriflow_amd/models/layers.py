@@ -512,6 +512,8 @@ class FusedConvPool(Layer):
         H, W, C = self.in_shape
         cp, _, pair = ops.convpool_fwd_layout(H, W, C, self.k, self.k, self.pad, self.conv.filters)
         sp[0].row_pad, sp[0].row_cp, sp[0].row_pair = self.k, cp, bool(pair)
+        if self.need_dx:
+            sp[0].t_pair = bool(ops.convpool_dgrad_layout(H, W, C, self.k, self.k, self.pad, self.conv.filters)[0])
         return sp
 
     split_backward = True

@@ -42,6 +42,16 @@ def primary_kpad(spec: "ParamSpec") -> int:
     return _r(T * Ci, 32)
 
 
+def dgrad_shape(spec: "ParamSpec") -> tuple:
+    """Shape of the bf16 dgrad copy: [round16(Ci)][round32(T*N)], or for the pair layout of the fused
+    conv+pool data gradient (csrc/convpool.hip make_dgrad) [16][round32(KH*(KW+1)*N)]."""
+    N, T, Ci = spec.mat
+    if spec.t_pair:
+        kw = spec.row_pad
+        return 16, _r((T // kw) * (kw + 1) * N, 32)
+    return _r(Ci, 16), _r(T * N, 32)
+
+
 @dataclass
 class ParamSpec:
     name: str
@@ -54,6 +64,7 @@ class ParamSpec:
     row_pad: int = 0                # KW > 0: primary bf16 copy in the fused conv+pool row-segment layout
     row_cp: int = 0                 #   ... with LDS channel stride Cp (>= Ci; 0 = Ci)
     row_pair: bool = False          #   ... pair layout: rows 8+n = row n shifted by one kernel column
+    t_pair: bool = False            # dgrad copy in the conv+pool dgrad pair layout (needs row_pad, Ci <= 8)
     trainable: bool = True
 
     @property
@@ -111,7 +122,7 @@ class ParamStore:
         return self._views[name].view(N, T * Ci)
 
     def weight_t(self, name) -> Optional[torch.Tensor]:
-        """dgrad-layout bf16 copy [Cipad][pad(T*N)] (GPU only)."""
+        """dgrad-layout bf16 copy (GPU only): [Cipad][pad(T*N)] or the pair layout (dgrad_shape)."""
         if self.compute_bf16:
             return self._wbft_views.get(name)
         return None
@@ -161,7 +172,7 @@ class ParamStore:
                 boff += _r(N, 16) * primary_kpad(s)
                 if s.needs_dgrad:
                     bft_off = boff
-                    boff += _r(Ci, 16) * _r(T * N, 32)
+                    boff += math.prod(dgrad_shape(s))
                 self._wbf_layout[s.name] = (bf_off, bft_off)
             if s.trainable or s.kind == "matrix":
                 nblocks = (s.numel + SGD_ELEMS_PER_BLOCK - 1) // SGD_ELEMS_PER_BLOCK
@@ -169,7 +180,8 @@ class ParamStore:
                     N, T, Ci = 1, 1, s.numel
                 descs.append((self.offsets[s.name], bf_off, bft_off, s.numel, N, T, Ci, block,
                               0 if s.trainable else 1,
-                              (s.row_pad | (s.row_cp << 16) | ((1 << 30) if s.row_pair else 0))
+                              (s.row_pad | (s.row_cp << 16) | ((1 << 30) if s.row_pair else 0)
+                               | ((1 << 29) if s.t_pair else 0))
                               if s.kind == "matrix" else 0))
                 block += nblocks
         self.wbf = torch.zeros(max(boff, 8), dtype=torch.bfloat16, device=self.device)
@@ -184,8 +196,8 @@ class ParamStore:
             kp = primary_kpad(s)
             self._wbf_views[s.name] = self.wbf[bf_off: bf_off + _r(N, 16) * kp].view(_r(N, 16), kp)
             if bft_off >= 0:
-                self._wbft_views[s.name] = self.wbf[bft_off: bft_off + _r(Ci, 16) * _r(T * N, 32)].view(
-                    _r(Ci, 16), _r(T * N, 32))
+                shp = dgrad_shape(s)
+                self._wbft_views[s.name] = self.wbf[bft_off: bft_off + math.prod(shp)].view(*shp)
         # ParamDesc = {i64 off, i64 bf_off, i64 bft_off, i32 numel, i32 N, i32 T, i32 Ci, i32 block_start, i32 pad}
         raw = []
         frozen = []

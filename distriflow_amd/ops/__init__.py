@@ -290,6 +290,11 @@ def convpool_fwd_layout(H, W, C, KH, KW, pad, N):
     return tuple(_C().convpool_fwd_layout(H, W, C, KH, KW, pad, N))
 
 
+def convpool_dgrad_layout(H, W, C, KH, KW, pad, N):
+    """(pair, row length K2pad) of the fused conv+pool data-gradient weight layout."""
+    return tuple(_C().convpool_dgrad_layout(H, W, C, KH, KW, pad, N))
+
+
 def _cp_in(x):
     if isinstance(x, GatherRef):
         return x.data, x.idx, x.scale

@@ -71,7 +71,7 @@ def main():
         tw = timeit(lambda: ops.convpool_wgrad(x, dp, code, gw, gb, ws, k, k, pad))
         print(f"{name} fwd(us) " + " ".join(res) + f" | wgrad+reduce {tw:.1f}", flush=True)
         if name == "conv2":
-            wt = torch.randn(16, 416, device=dev).to(torch.bfloat16) * 0.1
+            wt = torch.randn(16, ops.convpool_dgrad_layout(14, 14, 6, k, k, pad, 16)[1], device=dev).to(torch.bfloat16) * 0.1
             dx = torch.empty(B, 14, 14, 6, device=dev, dtype=torch.bfloat16)
             td = timeit(lambda: ops.convpool_dgrad(dp, code, None, wt, dx, k, k, pad))
             print(f"{name} dgrad {td:.1f}", flush=True)

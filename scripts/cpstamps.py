@@ -92,7 +92,7 @@ def main():
             elif kind == "wgrad":
                 ops.convpool_wgrad(x, dp, code, gw, gb, ws, k, k, pad)
             else:
-                wt = torch.randn(16, 416, device=dev).to(torch.bfloat16) * 0.1
+                wt = torch.randn(16, ops.convpool_dgrad_layout(14, 14, 6, k, k, pad, 16)[1], device=dev).to(torch.bfloat16) * 0.1
                 dx = torch.empty(B, 14, 14, 6, device=dev, dtype=torch.bfloat16)
                 ops.convpool_dgrad(dp, code, None, wt, dx, k, k, pad)
             torch.cuda.synchronize()

@@ -84,7 +84,20 @@ def test_sgd_step_and_bf16_copies():
             assert torch.equal(wb[:N, :T * Ci], w.to(torch.bfloat16))
             assert wb[N:].abs().sum() == 0 and wb[:, T * Ci:].abs().sum() == 0
         wt = st.weight_t(spec.name)
-        if wt is not None:
+        if wt is not None and spec.t_pair:  # conv+pool dgrad pair layout (csrc/convpool.hip make_dgrad)
+            KW = spec.row_pad
+            KH = T // KW
+            exp = torch.zeros_like(wt)
+            w4 = w.view(N, KH, KW, Ci).to(torch.bfloat16)
+            for a in range(KH):
+                for b in range(KW + 1):
+                    col = (a * (KW + 1) + b) * N
+                    if b < KW:
+                        exp[:Ci, col:col + N] = w4[:, KH - 1 - a, KW - 1 - b, :].t()
+                    if b >= 1:
+                        exp[8:8 + Ci, col:col + N] = w4[:, KH - 1 - a, KW - b, :].t()
+            assert torch.equal(wt, exp)
+        elif wt is not None:
             exp = w.view(N, T, Ci).permute(2, 1, 0).reshape(Ci, T * N).to(torch.bfloat16)
             assert torch.equal(wt[:Ci, :T * N], exp)
 

@@ -52,6 +52,27 @@ def _pad_wt(w2d, N, T, Ci):
     return out
 
 
+def _cp_wt(w2d, KH, KW, C, H, W, pad):
+    """fp32 [N][KH*KW*C] -> fused conv+pool dgrad layout: the plain [Cpad16][K2pad] layout, or the pair
+    layout [16][round32(KH*(KW+1)*N)] (row c: tap (a, b) = W[n][KH-1-a][KW-1-b][c]; row 8+c: the
+    same shifted by one column, W[n][KH-1-a][KW-b][c])."""
+    from distriflow_amd import ops as O
+    N = w2d.shape[0]
+    pair, k2p = O.convpool_dgrad_layout(H, W, C, KH, KW, pad, N)
+    if not pair:
+        return _pad_wt(w2d, N, KH * KW, C)
+    out = torch.zeros(16, k2p, dtype=torch.bfloat16, device=dev)
+    w4 = w2d.view(N, KH, KW, C).to(torch.bfloat16)
+    for a in range(KH):
+        for b in range(KW + 1):
+            col = (a * (KW + 1) + b) * N
+            if b < KW:
+                out[:C, col:col + N] = w4[:, KH - 1 - a, KW - 1 - b, :].t()
+            if b >= 1:
+                out[8:8 + C, col:col + N] = w4[:, KH - 1 - a, KW - b, :].t()
+    return out
+
+
 def _close(a, b, rtol=2e-2, atol=2e-2):
     a = a.float()
     b = b.float()
@@ -266,6 +287,8 @@ CONVPOOL = [  # B, H, W, C, N, k, pad
     (16, 14, 14, 6, 16, 5, 0),   # LeNet conv2
     (5, 12, 12, 3, 20, 3, 1),    # odd batch, N > 16, partial window tiles
     (3, 10, 10, 16, 8, 3, 0),
+    (7, 12, 12, 4, 8, 3, 0),     # dgrad pair mode with N = 8 (odd 16-byte pixel stride), partial tiles
+    (6, 10, 10, 8, 16, 5, 2),    # dgrad pair mode, C = 8 fills both column halves
 ]
 
 
@@ -295,7 +318,7 @@ def test_convpool_fwd_wgrad_dgrad(B, H, W, C, N, k, p):
     _close(gb.cpu(), eb, 1e-3, 1e-3)
     if C <= 16:
         dx = torch.empty(B, H, W, C, device=dev, dtype=torch.bfloat16)
-        O.convpool_dgrad(dp, code, None, _pad_wt(w, N, k * k, C), dx, k, k, p)
+        O.convpool_dgrad(dp, code, None, _cp_wt(w, k, k, C, H, W, p), dx, k, k, p)
         edx = ref.convpool_dgrad(dp.float().cpu(), code.cpu(), w.cpu(), (B, H, W, C), k, k, p)
         _close(dx.cpu(), edx)
 
