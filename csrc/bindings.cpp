@@ -246,8 +246,15 @@ void gap_bwd_py(torch::Tensor dy, torch::Tensor dx, int64_t B, int64_t HW, int64
 void sgd_multi_py(torch::Tensor descs, int64_t ndesc, int64_t total_blocks, torch::Tensor master, torch::Tensor grad,
                   c10::optional<torch::Tensor> mom, torch::Tensor wbf, torch::Tensor hyper, bool apply_update,
                   c10::optional<torch::Tensor> idx_stream, c10::optional<torch::Tensor> idx_cursor,
-                  c10::optional<torch::Tensor> idx_dst) {
+                  c10::optional<torch::Tensor> idx_dst, c10::optional<torch::Tensor> descs_host) {
   TORCH_CHECK(descs.is_cuda() && descs.scalar_type() == at::kLong && descs.is_contiguous(), "descs must be int64 GPU");
+  const dfa::ParamDesc* hd = nullptr;
+  if (descs_host.has_value() && descs_host->defined()) {  // same table, host copy: passed in the kernel arguments
+    TORCH_CHECK(!descs_host->is_cuda() && descs_host->scalar_type() == at::kLong && descs_host->is_contiguous() &&
+                    descs_host->numel() == descs.numel(),
+                "descs_host must be the int64 CPU copy of descs");
+    hd = reinterpret_cast<const dfa::ParamDesc*>(descs_host->data_ptr());
+  }
   static_assert(sizeof(dfa::ParamDesc) == 48, "ParamDesc layout");
   TORCH_CHECK(descs.numel() * 8 >= ndesc * (int64_t)sizeof(dfa::ParamDesc), "descs too small");
   need(master, at::kFloat, "master");
@@ -278,7 +285,7 @@ void sgd_multi_py(torch::Tensor descs, int64_t ndesc, int64_t total_blocks, torc
   }
   check_hip(dfa::sgd_multi(reinterpret_cast<const dfa::ParamDesc*>(descs.data_ptr()), (int)ndesc, (int)total_blocks,
                            master.data_ptr<float>(), grad.data_ptr<float>(), mp, (dfa::bf16*)wbf.data_ptr(),
-                           hyper.data_ptr<float>(), apply_update ? 1 : 0, cur_stream(), is.src ? &is : nullptr),
+                           hyper.data_ptr<float>(), apply_update ? 1 : 0, cur_stream(), is.src ? &is : nullptr, hd),
             "sgd_multi");
 }
 
@@ -589,7 +596,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gap_bwd", &gap_bwd_py);
   m.def("sgd_multi", &sgd_multi_py, py::arg("descs"), py::arg("ndesc"), py::arg("total_blocks"), py::arg("master"),
         py::arg("grad"), py::arg("mom"), py::arg("wbf"), py::arg("hyper"), py::arg("apply_update"),
-        py::arg("idx_stream") = py::none(), py::arg("idx_cursor") = py::none(), py::arg("idx_dst") = py::none());
+        py::arg("idx_stream") = py::none(), py::arg("idx_cursor") = py::none(), py::arg("idx_dst") = py::none(),
+        py::arg("descs_host") = py::none());
   m.def("sum_buffers", &sum_buffers_py);
   m.def("axpby", &axpby_py);
   m.def("bn_fwd_train", &bn_fwd_train_py);
@@ -604,8 +612,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == at::kLong && buf->numel() >= 4096 * 32,
                   "stamp buffer: int64 GPU tensor of >= 4096*32 elements");
       dfa::convpool_set_stamps(buf->data_ptr());
+      dfa::head_set_stamps(buf->data_ptr());
     } else {
       dfa::convpool_set_stamps(nullptr);
+      dfa::head_set_stamps(nullptr);
     }
   }, "profiling aid: per-block phase stamps of the convpool kernels");
   m.def("convpool_fwd_layout", [](int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t pad, int64_t N) {

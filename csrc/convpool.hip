@@ -1038,24 +1038,34 @@ __device__ __forceinline__ void slab_store(float* gw, float* gb, int o, int K, i
     gb[n] = v;
 }
 
-__global__ void __launch_bounds__(256) slab_reduce_wave_kernel(const float* __restrict__ partial,
-                                                               float* __restrict__ gw, float* __restrict__ gb, int N,
-                                                               int K, int Kt, int S, float scale) {
+// Many slabs: a 1024-thread block owns 64 consecutive outputs (one per lane, so every slab row is a
+// coalesced 256-byte read) and its 16 waves split the slabs, 8 loads in flight per lane; the 16 wave
+// partials are combined in LDS in a fixed order.
+__global__ void __launch_bounds__(1024) slab_reduce_wave_kernel(const float* __restrict__ partial,
+                                                                float* __restrict__ gw, float* __restrict__ gb, int N,
+                                                                int K, int Kt, int S, float scale) {
+  __shared__ float red[16][64];
   const int total = N * Kt;
-  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (o >= total) return;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int p = lane;
-  for (; p + 192 < S; p += 256) {
-    a0 += partial[(long long)p * total + o];
-    a1 += partial[(long long)(p + 64) * total + o];
-    a2 += partial[(long long)(p + 128) * total + o];
-    a3 += partial[(long long)(p + 192) * total + o];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int o = blockIdx.x * 64 + lane;
+  const int oc = min(o, total - 1);
+  float a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = 0.f;
+  int p = wv;
+  for (; p + 7 * 16 < S; p += 8 * 16) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += partial[(long long)(p + 16 * j) * total + oc];
   }
-  for (; p < S; p += 64) a0 += partial[(long long)p * total + o];
-  const float v = wave_sum((a0 + a1) + (a2 + a3));
-  if (lane == 0) slab_store(gw, gb, o, K, Kt, v * scale);
+  for (; p < S; p += 16) a[0] += partial[(long long)p * total + oc];
+  red[wv][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (wv == 0 && o < total) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) v += red[w][lane];
+    slab_store(gw, gb, o, K, Kt, v * scale);
+  }
 }
 
 __global__ void __launch_bounds__(256) slab_reduce_thread_kernel(const float* __restrict__ partial,
@@ -1079,9 +1089,9 @@ __global__ void __launch_bounds__(256) slab_reduce_thread_kernel(const float* __
 hipError_t slab_reduce(const float* partial, float* gw, float* gb, int N, int K, int Kt, int S, float scale,
                        hipStream_t st) {
   const int total = N * Kt;
-  if (S >= 32 && (long long)total * 64 <= (1ll << 24))
-    hipLaunchKernelGGL(slab_reduce_wave_kernel, dim3(cdiv(total, 4)), dim3(256), 0, st, partial, gw, gb, N, K, Kt, S,
-                       scale);
+  if (S >= 64 && total <= (1 << 16))
+    hipLaunchKernelGGL(slab_reduce_wave_kernel, dim3(cdiv(total, 64)), dim3(1024), 0, st, partial, gw, gb, N, K, Kt,
+                       S, scale);
   else
     hipLaunchKernelGGL(slab_reduce_thread_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, partial, gw, gb, N, K, Kt,
                        S, scale);

@@ -47,6 +47,13 @@ struct ParamDesc {
   int pad_;
 };
 
+// Small models: the descriptor table travels in the kernel arguments (scalar-cache reads instead of a
+// dependent chain of global loads for the per-workgroup descriptor search).
+constexpr int kInlineDescs = 32;
+struct ParamDescTable {
+  ParamDesc d[kInlineDescs];
+};
+
 hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st);
 hipError_t igemm_wgrad(const WgradArgs& a, int mode, float* workspace, size_t ws_floats, hipStream_t st);
 hipError_t maxpool_fwd(const bf16* x, bf16* y, int B, int H, int W, int C, int P, hipStream_t st);
@@ -71,7 +78,7 @@ struct IndexStream {  // next-batch staging folded into the optimizer launch (cs
 };
 hipError_t sgd_multi(const ParamDesc* descs, int ndesc, int total_blocks, float* master, const float* grad,
                      float* mom_buf, bf16* wbf, const float* hyper, int apply_update, hipStream_t st,
-                     const IndexStream* is = nullptr);
+                     const IndexStream* is = nullptr, const ParamDesc* host_descs = nullptr);
 hipError_t sum_buffers(const float* const* ins, int nin, float* out, long long n, float scale, hipStream_t st);
 hipError_t axpby(float* out, const float* a, const float* b, float alpha, float beta, long long n, hipStream_t st);
 hipError_t bn_fwd_train(const bf16* x, bf16* y, const float* gamma, const float* beta, float* mean, float* invstd,
@@ -109,6 +116,7 @@ struct HeadArgs {
   float grad_scale;     // d(loss)/d(logit) scale, 1/B for the mean
   float* loss_part;     // [nblocks][2]
   float* stats;         // [2] = (loss sum, correct)
+  unsigned long long* stamps;  // profiling aid (head_set_stamps): per-block phase clocks, or null
   int nblocks, wg_tiles;
 };
 size_t head_train_lds(const HeadArgs& a);
@@ -119,6 +127,7 @@ void convpool_set_stamps(void* buf);  // [grid][32] uint64 s_memtime stamps, nul
 // forward weight layout: [Npad16][Kpad2], column ky*RLp + kx*Cp + c (zero for c >= C) with
 // RLp = round8(KW*Cp); pair layout (N <= 8): RLp = round8((KW+1)*Cp) and rows 8+n = row n shifted by Cp
 void convpool_fwd_layout(int H, int W, int C, int KH, int KW, int pad, int N, int* Cp, int* Kpad2, int* pair);
+void head_set_stamps(void* buf);
 void convpool_dgrad_layout(int H, int W, int C, int KH, int KW, int pad, int N, int* pair, int* K2pad);
 bool convpool_supported(int H, int W, int C, int KH, int KW, int pad, int N);
 hipError_t convpool_fwd(const void* x, int x_u8, const long long* idx, long long nrows, float scale, int B, int H,

@@ -21,6 +21,21 @@
 
 namespace dfa {
 
+static unsigned long long* g_head_stamps = nullptr;
+void head_set_stamps(void* buf) { g_head_stamps = reinterpret_cast<unsigned long long*>(buf); }
+
+// per-block phase clocks (diagnostic; scripts/headstamps.py)
+#define HD_STAMP(slot)                                                            \
+  do {                                                                            \
+    if (a.stamps) {                                                               \
+      __builtin_amdgcn_sched_barrier(0);                                          \
+      unsigned long long t_;                                                      \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+      __builtin_amdgcn_sched_barrier(0);                                          \
+      if (threadIdx.x == 0) a.stamps[blockIdx.x * 32 + (slot)] = t_;              \
+    }                                                                             \
+  } while (0)
+
 constexpr int HR = 16;  // batch rows per workgroup of the train kernel
 constexpr int HW = 16;  // waves per workgroup (both kernels): tiles of a layer spread over 16 waves
 
@@ -135,6 +150,7 @@ __global__ void __launch_bounds__(1024) head_train_kernel(HeadArgs a) {
     }
   }
   float* lg = reinterpret_cast<float*>(p);  // [16][16]
+  HD_STAMP(0);
 
   // ---- stage X rows (zero padded to Kpad; rows past B are zero)
   const int D0 = a.L[0].K;
@@ -159,6 +175,7 @@ __global__ void __launch_bounds__(1024) head_train_kernel(HeadArgs a) {
         dzs[l][e] = (bf16)0.f;
       }
   __syncthreads();
+  HD_STAMP(1);
   // X^T [D0][ldt] for the weight gradient of layer 0: one feature's 16 rows = 32 contiguous bytes
   if (a.xT)
     for (int c = tid; c < D0; c += 64 * HW) {
@@ -188,6 +205,7 @@ __global__ void __launch_bounds__(1024) head_train_kernel(HeadArgs a) {
       head_gemm_fwd<13>(A, lda, L.w, L.Kpad, L.b, L.N, last ? 0 : 1, hs[l], ld[l], last ? lg : nullptr,
                         last ? nullptr : L.hT, a.ldt, r0, rows);
       __syncthreads();
+      HD_STAMP(2 + l);
     }
   }
 
@@ -243,6 +261,7 @@ __global__ void __launch_bounds__(1024) head_train_kernel(HeadArgs a) {
     }
   }
   __syncthreads();
+  HD_STAMP(6);
 
   // ---- backward data chain: dZ_{l-1} = (dZ_l W_l) * relu'(H_{l-1}); l = 0 produces dX
 #pragma unroll
@@ -259,8 +278,10 @@ __global__ void __launch_bounds__(1024) head_train_kernel(HeadArgs a) {
                          a.ldt, r0, rows);
       }
       __syncthreads();
+      HD_STAMP(7 + l);
     }
   }
+  HD_STAMP(31);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -373,6 +394,7 @@ static void head_prepare(HeadArgs& a) {
 
 // phase bit 1: forward + CE + backward data chain; bit 2: weight gradients + loss reduction
 hipError_t head_train(HeadArgs a, int phases, hipStream_t st) {
+  a.stamps = g_head_stamps;
   if (a.nl < 1 || a.nl > kHeadMaxLayers || a.L[a.nl - 1].N > 16) return hipErrorInvalidValue;
   head_prepare(a);
   if (phases & 1) {

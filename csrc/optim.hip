@@ -17,7 +17,8 @@ namespace dfa {
 
 constexpr int SGD_ELEMS_PER_BLOCK = 1024;
 
-__device__ __forceinline__ int find_desc(const ParamDesc* d, int n, int bid) {
+template <typename DT>
+__device__ __forceinline__ int find_desc(const DT& d, int n, int bid) {
   int lo = 0, hi = n - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -27,7 +28,8 @@ __device__ __forceinline__ int find_desc(const ParamDesc* d, int n, int bid) {
 }
 
 // hyper = [lr, momentum, weight_decay, grad_scale, nesterov]
-__device__ __forceinline__ void sgd_multi_body(const ParamDesc* __restrict__ descs, int ndesc,
+template <typename DT>
+__device__ __forceinline__ void sgd_multi_body(const DT& descs, int ndesc,
                                                float* __restrict__ master, const float* __restrict__ grad,
                                                float* __restrict__ mom_buf, bf16* __restrict__ wbf,
                                                const float* __restrict__ hyper, int apply_update, int bid) {
@@ -98,28 +100,11 @@ __device__ __forceinline__ void sgd_multi_body(const ParamDesc* __restrict__ des
   }
 }
 
-__global__ void __launch_bounds__(256) sgd_multi_kernel(const ParamDesc* __restrict__ descs, int ndesc,
-                                                        float* __restrict__ master, const float* __restrict__ grad,
-                                                        float* __restrict__ mom_buf, bf16* __restrict__ wbf,
-                                                        const float* __restrict__ hyper, int apply_update) {
-  sgd_multi_body(descs, ndesc, master, grad, mom_buf, wbf, hyper, apply_update, blockIdx.x);
-}
-
 // Device-resident index stream: the optimizer is the last kernel of a training step, so one extra
 // workgroup of the same launch stages the NEXT step's batch indices (src[(cursor+1) % nsteps]) into
 // the static index buffer the step's first kernels read, then advances the cursor.  A replayed step
 // graph then needs no host-side copy (and no extra launch) to move to the next batch.
-__global__ void __launch_bounds__(256) sgd_multi_stream_kernel(const ParamDesc* __restrict__ descs, int ndesc,
-                                                               float* __restrict__ master,
-                                                               const float* __restrict__ grad,
-                                                               float* __restrict__ mom_buf, bf16* __restrict__ wbf,
-                                                               const float* __restrict__ hyper, int apply_update,
-                                                               int total_blocks, IndexStream is) {
-  if ((int)blockIdx.x < total_blocks) {
-    sgd_multi_body(descs, ndesc, master, grad, mom_buf, wbf, hyper, apply_update, blockIdx.x);
-    return;
-  }
-  // the single index-stream workgroup: the only reader/writer of the cursor
+__device__ __forceinline__ void index_stream_body(const IndexStream& is) {
   __shared__ long long next;
   if (threadIdx.x == 0) {
     const long long c = *is.cursor;
@@ -127,21 +112,60 @@ __global__ void __launch_bounds__(256) sgd_multi_stream_kernel(const ParamDesc* 
   }
   __syncthreads();
   const long long* src = is.src + next * is.B;
-  for (int i = threadIdx.x; i < is.B; i += blockDim.x) is.dst[i] = src[i];
+  // all loads of a thread are issued before its stores (one memory round trip for B <= 8192)
+  constexpr int R = 16;
+  long long v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = threadIdx.x + 256 * r;
+    v[r] = src[min(i, is.B - 1)];
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = threadIdx.x + 256 * r;
+    if (i < is.B) is.dst[i] = v[r];
+  }
+  for (int i = threadIdx.x + 256 * R; i < is.B; i += 256) is.dst[i] = src[i];
   if (threadIdx.x == 0) *is.cursor = next;
+}
+
+template <bool INL>
+__global__ void __launch_bounds__(256) sgd_multi_stream_kernel(const ParamDesc* __restrict__ descs,
+                                                               const ParamDescTable tab, int ndesc,
+                                                               float* __restrict__ master,
+                                                               const float* __restrict__ grad,
+                                                               float* __restrict__ mom_buf, bf16* __restrict__ wbf,
+                                                               const float* __restrict__ hyper, int apply_update,
+                                                               int total_blocks, IndexStream is) {
+  if ((int)blockIdx.x < total_blocks) {
+    if (INL)
+      sgd_multi_body(tab.d, ndesc, master, grad, mom_buf, wbf, hyper, apply_update, blockIdx.x);
+    else
+      sgd_multi_body(descs, ndesc, master, grad, mom_buf, wbf, hyper, apply_update, blockIdx.x);
+    return;
+  }
+  if (is.src != nullptr) index_stream_body(is);  // the single index-stream workgroup
 }
 
 hipError_t sgd_multi(const ParamDesc* descs, int ndesc, int total_blocks, float* master, const float* grad,
                      float* mom_buf, bf16* wbf, const float* hyper, int apply_update, hipStream_t st,
-                     const IndexStream* is) {
-  if (is != nullptr && is->src != nullptr) {
-    hipLaunchKernelGGL(sgd_multi_stream_kernel, dim3(max(total_blocks, 0) + 1), dim3(256), 0, st, descs, ndesc,
-                       master, grad, mom_buf, wbf, hyper, apply_update, max(total_blocks, 0), *is);
-    return hipGetLastError();
+                     const IndexStream* is, const ParamDesc* host_descs) {
+  const bool stream = is != nullptr && is->src != nullptr;
+  total_blocks = max(total_blocks, 0);
+  if ((ndesc <= 0 || total_blocks <= 0) && !stream) return hipSuccess;
+  IndexStream isv{};
+  if (stream) isv = *is;
+  const int grid = total_blocks + (stream ? 1 : 0);
+  if (host_descs != nullptr && ndesc <= kInlineDescs) {
+    ParamDescTable tab{};
+    for (int i = 0; i < ndesc; ++i) tab.d[i] = host_descs[i];
+    hipLaunchKernelGGL(sgd_multi_stream_kernel<true>, dim3(grid), dim3(256), 0, st, descs, tab, ndesc, master, grad,
+                       mom_buf, wbf, hyper, apply_update, total_blocks, isv);
+  } else {
+    ParamDescTable tab{};
+    hipLaunchKernelGGL(sgd_multi_stream_kernel<false>, dim3(grid), dim3(256), 0, st, descs, tab, ndesc, master,
+                       grad, mom_buf, wbf, hyper, apply_update, total_blocks, isv);
   }
-  if (ndesc <= 0 || total_blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(sgd_multi_kernel, dim3(total_blocks), dim3(256), 0, st, descs, ndesc, master, grad, mom_buf, wbf,
-                     hyper, apply_update);
   return hipGetLastError();
 }
 

@@ -205,7 +205,8 @@ class ParamStore:
             raw += [off, bf, bft, (numel & 0xFFFFFFFF) | (N << 32), (T & 0xFFFFFFFF) | (Ci << 32),
                     (bstart & 0xFFFFFFFF) | (rpad << 32)]
             frozen.append(frz)
-        self._descs = torch.tensor(raw, dtype=torch.int64, device=self.device)
+        self._descs_host = torch.tensor(raw, dtype=torch.int64)
+        self._descs = self._descs_host.to(self.device)
         self._ndesc = len(descs)
         self._sgd_blocks = block
         if any(frozen):
@@ -216,7 +217,7 @@ class ParamStore:
         if not self.compute_bf16:
             return
         native.require().sgd_multi(self._descs, self._ndesc, self._sgd_blocks, self.master, self.grad, None,
-                                   self.wbf, self.hyper, False)
+                                   self.wbf, self.hyper, False, descs_host=self._descs_host)
 
     # ------------------------------------------------------------------ optimiser
     def set_hyper(self, lr, momentum=0.0, weight_decay=0.0, grad_scale=1.0, nesterov=False):
@@ -234,7 +235,8 @@ class ParamStore:
         if self.compute_bf16:
             src, cur, dst = index_stream if index_stream is not None else (None, None, None)
             native.require().sgd_multi(self._descs, self._ndesc, self._sgd_blocks, self.master, self.grad,
-                                       self.momentum, self.wbf, self.hyper, True, src, cur, dst)
+                                       self.momentum, self.wbf, self.hyper, True, src, cur, dst,
+                                       self._descs_host)
             return
         if index_stream is not None:
             src, cur, dst = index_stream
