@@ -39,7 +39,8 @@ void fill_geom(std::vector<int64_t> g, int* dst) {
 
 void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tensor> bias,
                   c10::optional<torch::Tensor> mask, torch::Tensor out, int64_t M, int64_t N, int64_t K, int64_t Kpad,
-                  int64_t lda, int64_t ldc, std::vector<int64_t> geom, int64_t mode, bool relu, double alpha) {
+                  int64_t lda, int64_t ldc, std::vector<int64_t> geom, int64_t mode, bool relu, double alpha,
+                  c10::optional<torch::Tensor> res, c10::optional<torch::Tensor> resmask) {
   need(src, at::kBFloat16, "src");
   need(w, at::kBFloat16, "w");
   TORCH_CHECK(out.is_cuda() && out.is_contiguous(), "out must be a contiguous GPU tensor");
@@ -70,10 +71,20 @@ void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tenso
     need(*mask, at::kBFloat16, "mask");
     TORCH_CHECK(mask->numel() >= (M - 1) * ldc + N, "mask too small");
   }
+  for (auto* t : {&res, &resmask}) {
+    if (t->has_value() && (*t)->defined()) {
+      need(**t, at::kBFloat16, "residual");
+      TORCH_CHECK((*t)->numel() >= (M - 1) * ldc + N, "residual too small");
+    }
+  }
+  TORCH_CHECK(!(resmask.has_value() && resmask->defined()) || (res.has_value() && res->defined()),
+              "resmask without res");
   a.src = reinterpret_cast<const dfa::bf16*>(src.data_ptr());
   a.w = reinterpret_cast<const dfa::bf16*>(w.data_ptr());
   a.bias = cptr<float>(bias);
   a.mask = cptr<dfa::bf16>(mask);
+  a.res = cptr<dfa::bf16>(res);
+  a.resmask = cptr<dfa::bf16>(resmask);
   a.out = out.data_ptr();
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.Kpad = (int)Kpad; a.lda = (int)lda; a.ldc = (int)ldc;
   a.relu = relu ? 1 : 0;
@@ -307,46 +318,124 @@ void axpby_py(torch::Tensor out, torch::Tensor a, torch::Tensor b, double alpha,
             "axpby");
 }
 
-void bn_fwd_train_py(torch::Tensor x, torch::Tensor y, torch::Tensor gamma, torch::Tensor beta, torch::Tensor mean,
-                     torch::Tensor invstd, torch::Tensor run_mean, torch::Tensor run_var, torch::Tensor ws, int64_t M,
-                     int64_t C, double momentum, double eps, bool relu) {
-  need(x, at::kBFloat16, "x");
-  need(y, at::kBFloat16, "y");
-  for (auto* t : {&gamma, &beta, &mean, &invstd, &run_mean, &run_var, &ws}) need(*t, at::kFloat, "bn param");
-  TORCH_CHECK(x.numel() >= M * C && y.numel() >= M * C && gamma.numel() >= C, "bn sizes");
-  TORCH_CHECK(ws.numel() >= 2 * C * 256, "bn workspace too small");
-  check_hip(dfa::bn_fwd_train((const dfa::bf16*)x.data_ptr(), (dfa::bf16*)y.data_ptr(), gamma.data_ptr<float>(),
-                              beta.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                              run_mean.data_ptr<float>(), run_var.data_ptr<float>(), ws.data_ptr<float>(), M, C,
-                              (float)momentum, (float)eps, relu ? 1 : 0, cur_stream()),
-            "bn_fwd_train");
+void bn_check_vec(const torch::Tensor& t, int64_t n, const char* name) {
+  need(t, at::kFloat, name);
+  TORCH_CHECK(t.numel() >= n, name, " too small");
 }
 
-void bn_fwd_eval_py(torch::Tensor x, torch::Tensor y, torch::Tensor gamma, torch::Tensor beta, torch::Tensor run_mean,
-                    torch::Tensor run_var, int64_t M, int64_t C, double eps, bool relu) {
-  need(x, at::kBFloat16, "x");
-  need(y, at::kBFloat16, "y");
-  TORCH_CHECK(x.numel() >= M * C && y.numel() >= M * C, "bn sizes");
-  check_hip(dfa::bn_fwd_eval((const dfa::bf16*)x.data_ptr(), (dfa::bf16*)y.data_ptr(), gamma.data_ptr<float>(),
-                             beta.data_ptr<float>(), run_mean.data_ptr<float>(), run_var.data_ptr<float>(), M, C,
-                             (float)eps, relu ? 1 : 0, cur_stream()),
-            "bn_fwd_eval");
+void bn_check_act(const torch::Tensor& t, int64_t n, const char* name) {
+  need(t, at::kBFloat16, name);
+  TORCH_CHECK(t.numel() >= n, name, " too small");
 }
 
-void bn_bwd_py(torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor dx, torch::Tensor gamma,
-               torch::Tensor beta, torch::Tensor mean, torch::Tensor invstd, torch::Tensor dgamma, torch::Tensor dbeta,
-               torch::Tensor ws, int64_t M, int64_t C, bool relu, double gscale) {
-  need(x, at::kBFloat16, "x");
-  need(y, at::kBFloat16, "y");
-  need(dy, at::kBFloat16, "dy");
-  need(dx, at::kBFloat16, "dx");
-  TORCH_CHECK(ws.numel() >= 2 * C * 256, "bn workspace too small");
-  check_hip(dfa::bn_bwd((const dfa::bf16*)x.data_ptr(), (const dfa::bf16*)y.data_ptr(), (const dfa::bf16*)dy.data_ptr(),
-                        (dfa::bf16*)dx.data_ptr(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
-                        mean.data_ptr<float>(), invstd.data_ptr<float>(), dgamma.data_ptr<float>(),
-                        dbeta.data_ptr<float>(), ws.data_ptr<float>(), M, C, relu ? 1 : 0, (float)gscale,
-                        cur_stream()),
-            "bn_bwd");
+void bn_check_stats_ws(const torch::Tensor& ws, const torch::Tensor& counter, int64_t M, int64_t C) {
+  TORCH_CHECK(C > 0 && C <= 1024 && M > 0, "bn: need 0 < C <= 1024 and M > 0");
+  TORCH_CHECK(C % 8 == 0 || C <= 256, "bn: C must be a multiple of 8 or <= 256");
+  bn_check_vec(ws, dfa::bn_stats_ws_floats((int)M, (int)C), "bn workspace");
+  need(counter, at::kInt, "bn counter");
+  TORCH_CHECK(counter.numel() >= dfa::bn_stats_counters((int)M, (int)C), "bn counter: need ",
+              dfa::bn_stats_counters((int)M, (int)C), " int32 tickets");
+}
+
+// forward statistics: batch mean / invstd (+ running statistics) in one launch
+void bn_stats_fwd_py(torch::Tensor x, torch::Tensor mean, torch::Tensor invstd, c10::optional<torch::Tensor> run_mean,
+                     c10::optional<torch::Tensor> run_var, torch::Tensor ws, torch::Tensor counter, int64_t M,
+                     int64_t C, double momentum, double eps) {
+  bn_check_act(x, M * C, "x");
+  bn_check_vec(mean, C, "mean");
+  bn_check_vec(invstd, C, "invstd");
+  const bool run = run_mean.has_value() && run_mean->defined();
+  if (run) {
+    bn_check_vec(*run_mean, C, "run_mean");
+    TORCH_CHECK(run_var.has_value() && run_var->defined(), "run_var required with run_mean");
+    bn_check_vec(*run_var, C, "run_var");
+  }
+  bn_check_stats_ws(ws, counter, M, C);
+  dfa::BnStatsArgs a{};
+  a.x = (const dfa::bf16*)x.data_ptr();
+  a.mean_out = mean.data_ptr<float>();
+  a.invstd_out = invstd.data_ptr<float>();
+  a.run_mean = run ? run_mean->data_ptr<float>() : nullptr;
+  a.run_var = run ? run_var->data_ptr<float>() : nullptr;
+  a.ws = ws.data_ptr<float>();
+  a.counter = reinterpret_cast<unsigned*>(counter.data_ptr<int>());
+  a.M = (int)M; a.C = (int)C; a.momentum = (float)momentum; a.eps = (float)eps;
+  check_hip(dfa::bn_stats(a, 0, cur_stream()), "bn_stats_fwd");
+}
+
+// backward statistics: dgamma/dbeta + dx coefficients coef[3][C]; g = dy * (mask > 0) when mask is given
+void bn_stats_bwd_py(torch::Tensor x, c10::optional<torch::Tensor> mask, torch::Tensor dy, torch::Tensor gamma,
+                     torch::Tensor mean, torch::Tensor invstd, torch::Tensor dgamma, torch::Tensor dbeta,
+                     torch::Tensor coef, torch::Tensor ws, torch::Tensor counter, int64_t M, int64_t C, double gscale) {
+  bn_check_act(x, M * C, "x");
+  bn_check_act(dy, M * C, "dy");
+  if (mask.has_value() && mask->defined()) bn_check_act(*mask, M * C, "mask");
+  bn_check_vec(gamma, C, "gamma");
+  bn_check_vec(mean, C, "mean");
+  bn_check_vec(invstd, C, "invstd");
+  bn_check_vec(dgamma, C, "dgamma");
+  bn_check_vec(dbeta, C, "dbeta");
+  bn_check_vec(coef, 3 * C, "coef");
+  bn_check_stats_ws(ws, counter, M, C);
+  dfa::BnStatsArgs a{};
+  a.x = (const dfa::bf16*)x.data_ptr();
+  a.mask = cptr<dfa::bf16>(mask);
+  a.dy = (const dfa::bf16*)dy.data_ptr();
+  a.gamma = gamma.data_ptr<float>();
+  a.mean = mean.data_ptr<float>();
+  a.invstd = invstd.data_ptr<float>();
+  a.dgamma = dgamma.data_ptr<float>();
+  a.dbeta = dbeta.data_ptr<float>();
+  a.coef = coef.data_ptr<float>();
+  a.ws = ws.data_ptr<float>();
+  a.counter = reinterpret_cast<unsigned*>(counter.data_ptr<int>());
+  a.M = (int)M; a.C = (int)C; a.gscale = (float)gscale;
+  check_hip(dfa::bn_stats(a, 1, cur_stream()), "bn_stats_bwd");
+}
+
+// y = act(bn(x) [+ r | + bn_r(r)]); eval: mean/invstd are the running mean / variance
+void bn_apply_py(torch::Tensor x, torch::Tensor y, torch::Tensor gamma, torch::Tensor beta, torch::Tensor mean,
+                 torch::Tensor invstd, c10::optional<torch::Tensor> r, c10::optional<torch::Tensor> rgamma,
+                 c10::optional<torch::Tensor> rbeta, c10::optional<torch::Tensor> rmean,
+                 c10::optional<torch::Tensor> rinvstd, int64_t M, int64_t C, bool relu, bool eval, double eps) {
+  bn_check_act(x, M * C, "x");
+  bn_check_act(y, M * C, "y");
+  for (auto* t : {&gamma, &beta, &mean, &invstd}) bn_check_vec(*t, C, "bn vector");
+  dfa::BnApplyArgs a{};
+  a.x = (const dfa::bf16*)x.data_ptr();
+  a.y = (dfa::bf16*)y.data_ptr();
+  a.gamma = gamma.data_ptr<float>();
+  a.beta = beta.data_ptr<float>();
+  a.mean = mean.data_ptr<float>();
+  a.invstd = invstd.data_ptr<float>();
+  if (r.has_value() && r->defined()) {
+    bn_check_act(*r, M * C, "residual");
+    a.r = (const dfa::bf16*)r->data_ptr();
+    if (rgamma.has_value() && rgamma->defined()) {
+      for (auto* t : {&rgamma, &rbeta, &rmean, &rinvstd}) {
+        TORCH_CHECK(t->has_value() && (*t)->defined(), "residual BN needs gamma, beta, mean, invstd");
+        bn_check_vec(**t, C, "residual bn vector");
+      }
+      a.rgamma = rgamma->data_ptr<float>();
+      a.rbeta = rbeta->data_ptr<float>();
+      a.rmean = rmean->data_ptr<float>();
+      a.rinvstd = rinvstd->data_ptr<float>();
+    }
+  }
+  a.M = (int)M; a.C = (int)C; a.relu = relu ? 1 : 0; a.eval = eval ? 1 : 0; a.eps = (float)eps;
+  check_hip(dfa::bn_apply(a, cur_stream()), "bn_apply");
+}
+
+void bn_dx_py(torch::Tensor x, c10::optional<torch::Tensor> mask, torch::Tensor dy, torch::Tensor dx,
+              torch::Tensor coef, int64_t M, int64_t C) {
+  bn_check_act(x, M * C, "x");
+  bn_check_act(dy, M * C, "dy");
+  bn_check_act(dx, M * C, "dx");
+  if (mask.has_value() && mask->defined()) bn_check_act(*mask, M * C, "mask");
+  bn_check_vec(coef, 3 * C, "coef");
+  check_hip(dfa::bn_dx((const dfa::bf16*)x.data_ptr(), cptr<dfa::bf16>(mask), (const dfa::bf16*)dy.data_ptr(),
+                       (dfa::bf16*)dx.data_ptr(), coef.data_ptr<float>(), (int)M, (int)C, cur_stream()),
+            "bn_dx");
 }
 
 // geometry: [B, H, W, C, KH, KW, pad, N]
@@ -583,7 +672,10 @@ bool convpool_supported_py(int64_t H, int64_t W, int64_t C, int64_t KH, int64_t 
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "distriflow_amd native kernels (gfx950 / MI355X) and runtime";
-  m.def("igemm_fwd", &igemm_fwd_py, "implicit-GEMM MFMA (dense/conv fwd, dgrad)");
+  m.def("igemm_fwd", &igemm_fwd_py, "implicit-GEMM MFMA (dense/conv fwd, dgrad)", py::arg("src"), py::arg("w"),
+        py::arg("bias"), py::arg("mask"), py::arg("out"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("Kpad"),
+        py::arg("lda"), py::arg("ldc"), py::arg("geom"), py::arg("mode"), py::arg("relu"), py::arg("alpha"),
+        py::arg("res") = py::none(), py::arg("resmask") = py::none());
   m.def("igemm_wgrad", &igemm_wgrad_py, "implicit-GEMM MFMA weight gradient (split-m slabs + reduce)");
   m.def("maxpool_fwd", &maxpool_fwd_py);
   m.def("maxpool_bwd", &maxpool_bwd_py);
@@ -600,9 +692,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("descs_host") = py::none());
   m.def("sum_buffers", &sum_buffers_py);
   m.def("axpby", &axpby_py);
-  m.def("bn_fwd_train", &bn_fwd_train_py);
-  m.def("bn_fwd_eval", &bn_fwd_eval_py);
-  m.def("bn_bwd", &bn_bwd_py);
+  m.def("bn_stats_fwd", &bn_stats_fwd_py, "BN forward statistics (partials + last-workgroup finalize, one launch)");
+  m.def("bn_stats_bwd", &bn_stats_bwd_py, "BN backward statistics: dgamma, dbeta and dx coefficients");
+  m.def("bn_apply", &bn_apply_py, "BN normalize (+ residual join, + ReLU)");
+  m.def("bn_dx", &bn_dx_py, "BN input gradient dx = k1*g + k2*x + k3");
+  m.def("bn_stats_grid", &dfa::bn_stats_grid, "partial-slab count of a BN statistics launch");
   m.def("convpool_fwd", &convpool_fwd_py, "fused conv+bias+relu+maxpool2x2 (pooled map + argmax codes)");
   m.def("convpool_wgrad", &convpool_wgrad_py, "weight gradient through the fused conv+pool");
   m.def("convpool_dgrad", &convpool_dgrad_py, "data gradient through the fused conv+pool");

@@ -1,17 +1,31 @@
 // BatchNorm (NHWC, per-channel over M = B*H*W rows) for the CIFAR-10 ResNet-18 config
 // (BASELINE.json configs[3]; not present in the reference).
 //
-// Train forward = 3 launches: per-block partial sums (fp32, 16-byte vector loads) ->
-// single-block finalize in fp64 (mean, invstd, running-stat update) -> normalize(+ReLU).
-// Backward = 3 launches: partial (sum g, sum g*xhat) with relu' fused -> finalize (writes dgamma,
-// dbeta straight into the flat gradient buffer) -> dx.  Partial slabs keep the reduction
-// deterministic (no float atomics).
+// Two launches per direction:
+//   stats  : every workgroup reduces a row range into an fp32 partial slab [2][C]; the slabs are
+//            then combined inside the same launch by last-arriver hand-offs (agent-scope release,
+//            ticket counter, agent-scope acquire): the last of every 16 workgroups sums its
+//            group's slabs, and the last group reducer sums the (<= 16) group slabs in fp64 and
+//            finalises — forward: mean, invstd and the running statistics; backward: dgamma/dbeta
+//            straight into the flat gradient buffer plus the per-channel coefficients of
+//            dx = k1*g + k2*x + k3.  Every sum runs in a fixed order: deterministic, no atomics on
+//            data.  Two levels keep each reducer at one round trip of independent loads.
+//   apply  : a streaming pass with 16-byte loads whose channel chunk is constant per thread (the
+//            grid stride is a multiple of C/8), so the per-channel affine coefficients live in
+//            registers.  The forward apply optionally fuses the residual join of a ResNet block,
+//            y = relu(bn(x) + r) or relu(bn(x) + bn_r(r)) (projection shortcut), and the backward
+//            apply fuses relu' of a mask tensor into g = dy * (mask > 0).
 #include "common.h"
 #include "kernels.h"
 
 namespace dfa {
 
 constexpr int BN_MAX_G = 255;
+constexpr int BN_GROUP = 16;
+
+static bool bn_vec(int C) { return C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0; }
+
+static int bn_rows_per_pass(int C, bool vec) { return 256 / (vec ? C / 8 : C); }
 
 static int bn_grid(int M, int rpp) {
   int g = cdiv(M, rpp * 16);
@@ -20,14 +34,36 @@ static int bn_grid(int M, int rpp) {
   return g;
 }
 
-// mode 0: s += x, q += x*x ; mode 1: g = dy*relu'(y), xh = (x-mean)*invstd ; s += g, q += g*xh
+// Publish this workgroup's global stores and draw a ticket from `counter`; returns true (in every
+// thread) in the last of `n` arrivers, which has then acquired the others' stores and re-armed the
+// counter to 0 for the next launch.
+__device__ __forceinline__ bool bn_last_arriver(unsigned* counter, unsigned n, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned tk = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = (tk == n - 1) ? 1 : 0;
+    if (*flag) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// MODE 0: s += x, q += x*x.   MODE 1: g = dy * relu'(mask), xh = (x - mean) * invstd; s += g, q += g*xh.
 template <int MODE, bool VEC>
-__global__ void __launch_bounds__(256) bn_partial_kernel(const bf16* __restrict__ x, const bf16* __restrict__ y,
-                                                         const bf16* __restrict__ dy, const float* __restrict__ mean,
-                                                         const float* __restrict__ invstd, float* __restrict__ ws,
-                                                         int M, int C, int relu) {
-  __shared__ float ls[2048], lq[2048];
+__global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
+  __shared__ __attribute__((aligned(16))) float lsq[4096];
+  __shared__ int last;
+  float* ls = lsq;
+  float* lq = lsq + 2048;
   constexpr int W = VEC ? 8 : 1;
+  const int C = a.C, M = a.M;
   const int cpr = C / W;
   const int rpp = 256 / cpr;
   const int t = threadIdx.x;
@@ -35,26 +71,38 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const bf16* __restrict_
   float s[W], q[W], mu[W], is[W];
 #pragma unroll
   for (int j = 0; j < W; ++j) {
-    s[j] = 0.f; q[j] = 0.f;
-    if (MODE == 1) { mu[j] = mean[chunk * W + j]; is[j] = invstd[chunk * W + j]; }
+    s[j] = 0.f;
+    q[j] = 0.f;
+    mu[j] = 0.f;
+    is[j] = 1.f;
+    if (MODE == 1 && rsub < rpp) {
+      mu[j] = a.mean[chunk * W + j];
+      is[j] = a.invstd[chunk * W + j];
+    }
   }
   if (rsub < rpp) {
+#pragma unroll 4
     for (long long r = (long long)blockIdx.x * rpp + rsub; r < M; r += (long long)gridDim.x * rpp) {
       const long long o = r * C + chunk * W;
       float xv[W], gv[W];
       if (VEC) {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + o);
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(a.x + o);
 #pragma unroll
         for (int j = 0; j < W; ++j) xv[j] = (float)v[j];
         if (MODE == 1) {
-          const bf16x8 g = *reinterpret_cast<const bf16x8*>(dy + o);
-          const bf16x8 yy = *reinterpret_cast<const bf16x8*>(y + o);
+          const bf16x8 g = *reinterpret_cast<const bf16x8*>(a.dy + o);
+          if (a.mask) {
+            const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.mask + o);
 #pragma unroll
-          for (int j = 0; j < W; ++j) gv[j] = (relu && !((float)yy[j] > 0.f)) ? 0.f : (float)g[j];
+            for (int j = 0; j < W; ++j) gv[j] = ((float)mk[j] > 0.f) ? (float)g[j] : 0.f;
+          } else {
+#pragma unroll
+            for (int j = 0; j < W; ++j) gv[j] = (float)g[j];
+          }
         }
       } else {
-        xv[0] = (float)x[o];
-        if (MODE == 1) gv[0] = (relu && !((float)y[o] > 0.f)) ? 0.f : (float)dy[o];
+        xv[0] = (float)a.x[o];
+        if (MODE == 1) gv[0] = (a.mask && !((float)a.mask[o] > 0.f)) ? 0.f : (float)a.dy[o];
       }
 #pragma unroll
       for (int j = 0; j < W; ++j) {
@@ -75,194 +123,235 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const bf16* __restrict_
     }
   }
   __syncthreads();
+  const int G = gridDim.x;
+  const int ncol = 2 * C;
+  float* slab = a.ws + (long long)blockIdx.x * ncol;
   for (int c = t; c < C; c += 256) {
-    float a = 0.f, b = 0.f;
-    for (int r = 0; r < rpp; ++r) { a += ls[r * C + c]; b += lq[r * C + c]; }
-    ws[(long long)blockIdx.x * 2 * C + c] = a;
-    ws[(long long)blockIdx.x * 2 * C + C + c] = b;
-  }
-}
-
-__global__ void bn_fwd_finalize_kernel(const float* __restrict__ ws, int G, int M, int C, float momentum, float eps,
-                                       float* __restrict__ mean, float* __restrict__ invstd,
-                                       float* __restrict__ run_mean, float* __restrict__ run_var) {
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    double s = 0.0, q = 0.0;
-    for (int g = 0; g < G; ++g) { s += ws[(long long)g * 2 * C + c]; q += ws[(long long)g * 2 * C + C + c]; }
-    const double mu = s / M;
-    double var = q / M - mu * mu;
-    if (var < 0.0) var = 0.0;
-    mean[c] = (float)mu;
-    invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
-    if (run_mean) {
-      const double unb = M > 1 ? var * M / (M - 1) : var;
-      run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mu);
-      run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
+    float u = 0.f, v = 0.f;
+    for (int r = 0; r < rpp; ++r) {
+      u += ls[r * C + c];
+      v += lq[r * C + c];
     }
+    slab[c] = u;
+    slab[C + c] = v;
   }
-}
 
-__global__ void bn_bwd_finalize_kernel(float* __restrict__ ws, int G, int C, float gscale, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta) {
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    double s = 0.0, q = 0.0;
-    for (int g = 0; g < G; ++g) { s += ws[(long long)g * 2 * C + c]; q += ws[(long long)g * 2 * C + C + c]; }
-    ws[(long long)G * 2 * C + c] = (float)s;       // raw sums for the dx pass
-    ws[(long long)G * 2 * C + C + c] = (float)q;
-    dbeta[c] = (float)s * gscale;
-    dgamma[c] = (float)q * gscale;
-  }
-}
-
-// mode 0 (train/eval fwd): y = (x - a) * b * gamma + beta (+relu), with (a, b) = (mean, invstd)
-template <bool VEC>
-__global__ void bn_apply_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, const float* __restrict__ gamma,
-                                const float* __restrict__ beta, const float* __restrict__ mean,
-                                const float* __restrict__ invstd, int eval_var, float eps, long long M, int C,
-                                int relu) {
-  constexpr int W = VEC ? 8 : 1;
-  const long long total = M * C / W;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c0 = (int)((i * W) % C);
-    float xv[W];
-    if (VEC) {
-      const bf16x8 v = reinterpret_cast<const bf16x8*>(x)[i];
+  // ---- level 1: the last of each group of 16 workgroups sums the group's slabs
+  const int grp = blockIdx.x / BN_GROUP;
+  const int gbeg = grp * BN_GROUP, gn = min(BN_GROUP, G - gbeg);
+  const int ngrp = cdiv(G, BN_GROUP);
+  float* gslab = a.ws + (long long)G * ncol;  // [ngrp][2C]
+  if (!bn_last_arriver(a.counter + 1 + grp, (unsigned)gn, &last)) return;
+  for (int col = t; col < ncol; col += 256) {
+    float v[BN_GROUP];
 #pragma unroll
-      for (int j = 0; j < W; ++j) xv[j] = (float)v[j];
-    } else {
-      xv[0] = (float)x[i];
+    for (int j = 0; j < BN_GROUP; ++j) v[j] = a.ws[(long long)(gbeg + min(j, gn - 1)) * ncol + col];  // all loads issued
+    float u = 0.f;
+#pragma unroll
+    for (int j = 0; j < BN_GROUP; ++j) u += j < gn ? v[j] : 0.f;
+    gslab[(long long)grp * ncol + col] = u;
+  }
+
+  // ---- level 2: the last group reducer sums the group slabs in fp64 and finalises
+  if (!bn_last_arriver(a.counter, (unsigned)ngrp, &last)) return;
+  for (int c = t; c < C; c += 256) {
+    float su[BN_GROUP], qu[BN_GROUP];
+#pragma unroll
+    for (int j = 0; j < BN_GROUP; ++j) {
+      const long long base = (long long)min(j, ngrp - 1) * ncol;
+      su[j] = gslab[base + c];
+      qu[j] = gslab[base + C + c];
     }
-    bf16x8 o;
+    double sv = 0.0, qv = 0.0;
 #pragma unroll
-    for (int j = 0; j < W; ++j) {
-      const int c = c0 + j;
-      const float is = eval_var ? rsqrtf(invstd[c] + eps) : invstd[c];
-      float v = (xv[j] - mean[c]) * is * gamma[c] + beta[c];
-      if (relu) v = fmaxf(v, 0.f);
-      o[j] = f2bf(v);
+    for (int j = 0; j < BN_GROUP; ++j) {
+      if (j < ngrp) {
+        sv += (double)su[j];
+        qv += (double)qu[j];
+      }
     }
-    if (VEC)
-      reinterpret_cast<bf16x8*>(y)[i] = o;
-    else
-      y[i] = o[0];
-  }
-}
-
-template <bool VEC>
-__global__ void bn_dx_kernel(const bf16* __restrict__ x, const bf16* __restrict__ y, const bf16* __restrict__ dy,
-                             bf16* __restrict__ dx, const float* __restrict__ gamma, const float* __restrict__ mean,
-                             const float* __restrict__ invstd, const float* __restrict__ sums, long long M, int C,
-                             int relu) {
-  constexpr int W = VEC ? 8 : 1;
-  const long long total = M * C / W;
-  const float invM = 1.f / (float)M;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c0 = (int)((i * W) % C);
-    float xv[W], gv[W];
-    if (VEC) {
-      const bf16x8 v = reinterpret_cast<const bf16x8*>(x)[i];
-      const bf16x8 g = reinterpret_cast<const bf16x8*>(dy)[i];
-      const bf16x8 yy = reinterpret_cast<const bf16x8*>(y)[i];
-#pragma unroll
-      for (int j = 0; j < W; ++j) {
-        xv[j] = (float)v[j];
-        gv[j] = (relu && !((float)yy[j] > 0.f)) ? 0.f : (float)g[j];
+    if (MODE == 0) {
+      const double m = sv / M;
+      double var = qv / M - m * m;
+      if (var < 0.0) var = 0.0;
+      a.mean_out[c] = (float)m;
+      a.invstd_out[c] = (float)(1.0 / sqrt(var + (double)a.eps));
+      if (a.run_mean) {
+        const double unb = M > 1 ? var * M / (M - 1) : var;
+        a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * m);
+        a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
       }
     } else {
-      xv[0] = (float)x[i];
-      gv[0] = (relu && !((float)y[i] > 0.f)) ? 0.f : (float)dy[i];
+      a.dbeta[c] = (float)sv * a.gscale;
+      a.dgamma[c] = (float)qv * a.gscale;
+      const double isd = a.invstd[c], gam = a.gamma[c], m = a.mean[c];
+      const double k1 = gam * isd;
+      a.coef[c] = (float)k1;
+      a.coef[C + c] = (float)(-k1 * isd * qv / M);
+      a.coef[2 * C + c] = (float)(k1 * (m * isd * qv / M - sv / M));
     }
-    bf16x8 o;
+  }
+}
+
+__device__ __forceinline__ void bn_affine(const BnApplyArgs& a, const float* g, const float* b, const float* m,
+                                          const float* v, int c, float& sa, float& sb) {
+  const float is = a.eval ? rsqrtf(v[c] + a.eps) : v[c];
+  sa = g[c] * is;
+  sb = b[c] - m[c] * sa;
+}
+
+// Forward apply: y = act(x*sa + sb [+ r | + r*ra + rb]), (sa, sb) = (gamma*invstd, beta - mean*gamma*invstd);
+// eval mode derives invstd from the running variance.
+template <int RES, bool VEC>
+__global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
+  const int C = a.C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  if (VEC) {
+    const long long total = (long long)a.M * C / 8;
+    const int c0 = (int)(threadIdx.x % (C / 8)) * 8;  // constant: 256 and the grid stride are multiples of C/8
+    float sa[8], sb[8], ra[8], rb[8];
 #pragma unroll
-    for (int j = 0; j < W; ++j) {
-      const int c = c0 + j;
-      const float is = invstd[c];
-      const float xh = (xv[j] - mean[c]) * is;
-      const float v = gamma[c] * is * (gv[j] - sums[c] * invM - xh * sums[C + c] * invM);
-      o[j] = f2bf(v);
+    for (int j = 0; j < 8; ++j) {
+      bn_affine(a, a.gamma, a.beta, a.mean, a.invstd, c0 + j, sa[j], sb[j]);
+      ra[j] = 1.f;
+      rb[j] = 0.f;
+      if (RES == 2) bn_affine(a, a.rgamma, a.rbeta, a.rmean, a.rinvstd, c0 + j, ra[j], rb[j]);
     }
-    if (VEC)
+#pragma unroll 2
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += stride) {
+      const bf16x8 xv = reinterpret_cast<const bf16x8*>(a.x)[i];
+      bf16x8 rv;
+      if (RES) rv = reinterpret_cast<const bf16x8*>(a.r)[i];
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = (float)xv[j] * sa[j] + sb[j];
+        if (RES) v += (float)rv[j] * ra[j] + rb[j];
+        if (a.relu) v = fmaxf(v, 0.f);
+        o[j] = f2bf(v);
+      }
+      reinterpret_cast<bf16x8*>(a.y)[i] = o;
+    }
+  } else {
+    const long long total = (long long)a.M * C;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += stride) {
+      const int c = (int)(i % C);
+      float sa, sb, ra = 1.f, rb = 0.f;
+      bn_affine(a, a.gamma, a.beta, a.mean, a.invstd, c, sa, sb);
+      if (RES == 2) bn_affine(a, a.rgamma, a.rbeta, a.rmean, a.rinvstd, c, ra, rb);
+      float v = (float)a.x[i] * sa + sb;
+      if (RES) v += (float)a.r[i] * ra + rb;
+      if (a.relu) v = fmaxf(v, 0.f);
+      a.y[i] = f2bf(v);
+    }
+  }
+}
+
+// Backward apply: dx = k1*g + k2*x + k3 with g = dy * relu'(mask).
+template <bool VEC>
+__global__ void __launch_bounds__(256) bn_dx_kernel(const bf16* __restrict__ x, const bf16* __restrict__ mask,
+                                                    const bf16* __restrict__ dy, bf16* __restrict__ dx,
+                                                    const float* __restrict__ coef, long long M, int C) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  if (VEC) {
+    const long long total = M * C / 8;
+    const int c0 = (int)(threadIdx.x % (C / 8)) * 8;
+    float k1[8], k2[8], k3[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      k1[j] = coef[c0 + j];
+      k2[j] = coef[C + c0 + j];
+      k3[j] = coef[2 * C + c0 + j];
+    }
+#pragma unroll 2
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += stride) {
+      const bf16x8 xv = reinterpret_cast<const bf16x8*>(x)[i];
+      const bf16x8 gv = reinterpret_cast<const bf16x8*>(dy)[i];
+      bf16x8 mv;
+      if (mask) mv = reinterpret_cast<const bf16x8*>(mask)[i];
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float g = (mask && !((float)mv[j] > 0.f)) ? 0.f : (float)gv[j];
+        o[j] = f2bf(k1[j] * g + k2[j] * (float)xv[j] + k3[j]);
+      }
       reinterpret_cast<bf16x8*>(dx)[i] = o;
-    else
-      dx[i] = o[0];
+    }
+  } else {
+    const long long total = M * C;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += stride) {
+      const int c = (int)(i % C);
+      const float g = (mask && !((float)mask[i] > 0.f)) ? 0.f : (float)dy[i];
+      dx[i] = f2bf(coef[c] * g + coef[C + c] * (float)x[i] + coef[2 * C + c]);
+    }
   }
 }
 
 static int ew_grid(long long n) {
   long long g = (n + 255) / 256;
-  if (g > 8192) g = 8192;
+  if (g > 4096) g = 4096;
   if (g < 1) g = 1;
   return (int)g;
 }
 
-hipError_t bn_fwd_train(const bf16* x, bf16* y, const float* gamma, const float* beta, float* mean, float* invstd,
-                        float* run_mean, float* run_var, float* ws, int M, int C, float momentum, float eps, int relu,
-                        hipStream_t st) {
-  if (C > 2048 || M <= 0) return hipErrorInvalidValue;
-  const bool vec = C % 8 == 0 && C / 8 <= 256;
-  if (!vec && C > 256) return hipErrorInvalidValue;
-  const int rpp = 256 / (vec ? C / 8 : C);
-  const int G = bn_grid(M, rpp);
-  if (vec)
-    hipLaunchKernelGGL((bn_partial_kernel<0, true>), dim3(G), dim3(256), 0, st, x, nullptr, nullptr, nullptr, nullptr,
-                       ws, M, C, 0);
-  else
-    hipLaunchKernelGGL((bn_partial_kernel<0, false>), dim3(G), dim3(256), 0, st, x, nullptr, nullptr, nullptr, nullptr,
-                       ws, M, C, 0);
-  DFA_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(1), dim3(256), 0, st, ws, G, M, C, momentum, eps, mean, invstd,
-                     run_mean, run_var);
-  DFA_HIP_CHECK(hipGetLastError());
-  const long long n = (long long)M * C / (vec ? 8 : 1);
-  if (vec)
-    hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(ew_grid(n)), dim3(256), 0, st, x, y, gamma, beta, mean, invstd, 0,
-                       eps, (long long)M, C, relu);
-  else
-    hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(ew_grid(n)), dim3(256), 0, st, x, y, gamma, beta, mean, invstd, 0,
-                       eps, (long long)M, C, relu);
+int bn_stats_grid(int M, int C) { return bn_grid(M, bn_rows_per_pass(C, bn_vec(C))); }
+
+long long bn_stats_ws_floats(int M, int C) {
+  const int G = bn_stats_grid(M, C);
+  return (long long)(G + cdiv(G, BN_GROUP)) * 2 * C;
+}
+
+int bn_stats_counters(int M, int C) { return 1 + cdiv(bn_stats_grid(M, C), BN_GROUP); }
+
+hipError_t bn_stats(const BnStatsArgs& a, int mode, hipStream_t st) {
+  if (a.C > 1024 || a.C <= 0 || a.M <= 0) return hipErrorInvalidValue;
+  const bool vec = bn_vec(a.C);
+  if (!vec && a.C > 256) return hipErrorInvalidValue;
+  const int G = bn_grid(a.M, bn_rows_per_pass(a.C, vec));
+  if (mode == 0) {
+    if (vec)
+      hipLaunchKernelGGL((bn_stats_kernel<0, true>), dim3(G), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((bn_stats_kernel<0, false>), dim3(G), dim3(256), 0, st, a);
+  } else {
+    if (vec)
+      hipLaunchKernelGGL((bn_stats_kernel<1, true>), dim3(G), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((bn_stats_kernel<1, false>), dim3(G), dim3(256), 0, st, a);
+  }
   return hipGetLastError();
 }
 
-hipError_t bn_fwd_eval(const bf16* x, bf16* y, const float* gamma, const float* beta, const float* run_mean,
-                       const float* run_var, int M, int C, float eps, int relu, hipStream_t st) {
-  const bool vec = C % 8 == 0;
-  const long long n = (long long)M * C / (vec ? 8 : 1);
-  if (vec)
-    hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(ew_grid(n)), dim3(256), 0, st, x, y, gamma, beta, run_mean, run_var,
-                       1, eps, (long long)M, C, relu);
-  else
-    hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(ew_grid(n)), dim3(256), 0, st, x, y, gamma, beta, run_mean,
-                       run_var, 1, eps, (long long)M, C, relu);
+hipError_t bn_apply(const BnApplyArgs& a, hipStream_t st) {
+  const bool vec = bn_vec(a.C);
+  const long long n = (long long)a.M * a.C / (vec ? 8 : 1);
+  const int grid = ew_grid(n);
+  const int res = a.r == nullptr ? 0 : (a.rgamma == nullptr ? 1 : 2);
+#define DFA_BN_APPLY(R)                                                              \
+  if (vec)                                                                           \
+    hipLaunchKernelGGL((bn_apply_kernel<R, true>), dim3(grid), dim3(256), 0, st, a); \
+  else                                                                               \
+    hipLaunchKernelGGL((bn_apply_kernel<R, false>), dim3(grid), dim3(256), 0, st, a);
+  if (res == 0) {
+    DFA_BN_APPLY(0)
+  } else if (res == 1) {
+    DFA_BN_APPLY(1)
+  } else {
+    DFA_BN_APPLY(2)
+  }
+#undef DFA_BN_APPLY
   return hipGetLastError();
 }
 
-hipError_t bn_bwd(const bf16* x, const bf16* y, const bf16* dy, bf16* dx, const float* gamma, const float* beta,
-                  const float* mean, const float* invstd, float* dgamma, float* dbeta, float* ws, int M, int C,
-                  int relu, float gscale, hipStream_t st) {
-  (void)beta;
-  if (C > 2048 || M <= 0) return hipErrorInvalidValue;
-  const bool vec = C % 8 == 0 && C / 8 <= 256;
-  if (!vec && C > 256) return hipErrorInvalidValue;
-  const int rpp = 256 / (vec ? C / 8 : C);
-  const int G = bn_grid(M, rpp);
-  if (vec)
-    hipLaunchKernelGGL((bn_partial_kernel<1, true>), dim3(G), dim3(256), 0, st, x, y, dy, mean, invstd, ws, M, C, relu);
-  else
-    hipLaunchKernelGGL((bn_partial_kernel<1, false>), dim3(G), dim3(256), 0, st, x, y, dy, mean, invstd, ws, M, C,
-                       relu);
-  DFA_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(256), 0, st, ws, G, C, gscale, dgamma, dbeta);
-  DFA_HIP_CHECK(hipGetLastError());
-  const float* sums = ws + (long long)G * 2 * C;
+hipError_t bn_dx(const bf16* x, const bf16* mask, const bf16* dy, bf16* dx, const float* coef, int M, int C,
+                 hipStream_t st) {
+  const bool vec = bn_vec(C);
   const long long n = (long long)M * C / (vec ? 8 : 1);
   if (vec)
-    hipLaunchKernelGGL(bn_dx_kernel<true>, dim3(ew_grid(n)), dim3(256), 0, st, x, y, dy, dx, gamma, mean, invstd, sums,
-                       (long long)M, C, relu);
+    hipLaunchKernelGGL(bn_dx_kernel<true>, dim3(ew_grid(n)), dim3(256), 0, st, x, mask, dy, dx, coef, (long long)M, C);
   else
-    hipLaunchKernelGGL(bn_dx_kernel<false>, dim3(ew_grid(n)), dim3(256), 0, st, x, y, dy, dx, gamma, mean, invstd,
-                       sums, (long long)M, C, relu);
+    hipLaunchKernelGGL(bn_dx_kernel<false>, dim3(ew_grid(n)), dim3(256), 0, st, x, mask, dy, dx, coef, (long long)M,
+                       C);
   return hipGetLastError();
 }
 

@@ -268,8 +268,12 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(IGemmArgs a) {
         const int row = m0 + wm * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
         if (row >= a.M) continue;
         float v = acc[i][j][r] * a.alpha + bv;
-        if (a.relu) v = fmaxf(v, 0.f);
         const long long o = (long long)row * a.ldc + col;
+        if (a.res) {
+          const float rv = (float)a.res[o];
+          if (!a.resmask || (float)a.resmask[o] > 0.f) v += rv;
+        }
+        if (a.relu) v = fmaxf(v, 0.f);
         if (a.mask && !((float)a.mask[o] > 0.f)) v = 0.f;
         if (a.out_f32)
           reinterpret_cast<float*>(a.out)[o] = v;
@@ -581,6 +585,7 @@ hipError_t igemm_wgrad(const WgradArgs& a, int mode, float* workspace, size_t ws
     const bool xvec = ((uintptr_t)a.src & 15) == 0 && a.lda % 8 == 0;
     return launch_wgrad_x<MODE_DIRECT>(a, dvec, xvec, workspace, ws_floats, st);
   }
+  if (wgrad_tr_supported(a, mode)) return wgrad_tr(a, workspace, ws_floats, st);
   const bool xvec = ((uintptr_t)a.src & 15) == 0 && a.SC % 8 == 0;
   return launch_wgrad_x<MODE_FWD>(a, dvec, xvec, workspace, ws_floats, st);
 }

@@ -18,6 +18,8 @@ struct IGemmArgs {
   const bf16* w;     // [Npad16][Kpad32] bf16, zero padded
   const float* bias; // [N] or nullptr
   const bf16* mask;  // [M][ldc] producer activation for relu' (nullptr = none)
+  const bf16* res;     // [M][ldc] residual added before relu / mask (nullptr = none): ResNet shortcut gradient
+  const bf16* resmask; // [M][ldc] res counts only where resmask > 0 (nullptr = everywhere)
   void* out;         // [M][ldc] bf16 or fp32
   int M, N, K, Kpad, lda, ldc;
   int SH, SW, SC, OH, OW, KH, KW, stride, pad;
@@ -56,6 +58,9 @@ struct ParamDescTable {
 
 hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st);
 hipError_t igemm_wgrad(const WgradArgs& a, int mode, float* workspace, size_t ws_floats, hipStream_t st);
+// conv weight gradient with transposed LDS reads (csrc/wgrad_tr.hip): conv, C % 8 == 0, no bias
+bool wgrad_tr_supported(const WgradArgs& a, int mode);
+hipError_t wgrad_tr(const WgradArgs& a, float* workspace, size_t ws_floats, hipStream_t st);
 hipError_t maxpool_fwd(const bf16* x, bf16* y, int B, int H, int W, int C, int P, hipStream_t st);
 hipError_t maxpool_bwd(const bf16* x, const bf16* dy, bf16* dx, int B, int H, int W, int C, int P, int relu_fused,
                        hipStream_t st);
@@ -81,14 +86,42 @@ hipError_t sgd_multi(const ParamDesc* descs, int ndesc, int total_blocks, float*
                      const IndexStream* is = nullptr, const ParamDesc* host_descs = nullptr);
 hipError_t sum_buffers(const float* const* ins, int nin, float* out, long long n, float scale, hipStream_t st);
 hipError_t axpby(float* out, const float* a, const float* b, float alpha, float beta, long long n, hipStream_t st);
-hipError_t bn_fwd_train(const bf16* x, bf16* y, const float* gamma, const float* beta, float* mean, float* invstd,
-                        float* run_mean, float* run_var, float* ws, int M, int C, float momentum, float eps, int relu,
-                        hipStream_t st);
-hipError_t bn_fwd_eval(const bf16* x, bf16* y, const float* gamma, const float* beta, const float* run_mean,
-                       const float* run_var, int M, int C, float eps, int relu, hipStream_t st);
-hipError_t bn_bwd(const bf16* x, const bf16* y, const bf16* dy, bf16* dx, const float* gamma, const float* beta,
-                  const float* mean, const float* invstd, float* dgamma, float* dbeta, float* ws, int M, int C,
-                  int relu, float gscale, hipStream_t st);
+// ---- BatchNorm (csrc/bn.hip)
+struct BnStatsArgs {
+  const bf16* x;         // [M][C] BN input
+  const bf16* mask;      // backward: g = dy * (mask > 0) (nullable)
+  const bf16* dy;        // backward: incoming gradient
+  const float* gamma;    // backward
+  const float* mean;     // backward: saved batch statistics
+  const float* invstd;
+  float* mean_out;       // forward outputs
+  float* invstd_out;
+  float* run_mean;       // forward: running statistics (nullable)
+  float* run_var;
+  float* dgamma;         // backward outputs (flat gradient buffer slices)
+  float* dbeta;
+  float* coef;           // backward: [3][C] dx = k1*g + k2*x + k3
+  float* ws;             // [G][2][C] partial slabs
+  unsigned* counter;     // last-arriver ticket, 0 between launches
+  int M, C;
+  float momentum, eps, gscale;
+};
+struct BnApplyArgs {
+  const bf16* x;
+  bf16* y;
+  const float *gamma, *beta, *mean, *invstd;      // eval: invstd holds the running variance
+  const bf16* r;                                  // residual (nullable)
+  const float *rgamma, *rbeta, *rmean, *rinvstd;  // BN of the residual (nullable: plain residual)
+  int M, C, relu, eval;
+  float eps;
+};
+int bn_stats_grid(int M, int C);
+long long bn_stats_ws_floats(int M, int C);  // slabs + group slabs
+int bn_stats_counters(int M, int C);         // ticket counters: 1 global + 1 per group of 16 workgroups
+hipError_t bn_stats(const BnStatsArgs& a, int mode, hipStream_t st);  // mode 0 forward, 1 backward
+hipError_t bn_apply(const BnApplyArgs& a, hipStream_t st);
+hipError_t bn_dx(const bf16* x, const bf16* mask, const bf16* dy, bf16* dx, const float* coef, int M, int C,
+                 hipStream_t st);
 
 // fused Conv2D(+bias+ReLU)+MaxPool2x2 for small channel counts (convpool.hip)
 // ---- fused dense head (csrc/mlphead.hip)

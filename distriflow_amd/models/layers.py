@@ -211,15 +211,18 @@ class Conv2D(Layer):
                      relu=self.relu)
         return self.out
 
-    def backward(self, dy):
+    def backward(self, dy, residual=None, residual_mask=None, dx_mask=None):
+        """``residual`` / ``residual_mask`` / ``dx_mask``: the ResNet block join fused into the dgrad
+        epilogue, dx = (conv^T dy + residual * [residual_mask > 0]) * [dx_mask > 0]."""
         st = self.store
         kn = f"{self.name}/kernel"
         gb = st.gradient(f"{self.name}/bias") if self.use_bias else None
         ops.conv_wgrad(dy, self.x, st.grad_matrix(kn), gb, self.ws.wgrad, self.k, self.k, self.stride, self.pad)
         if not self.need_dx:
             return None
+        mask = dx_mask if dx_mask is not None else (self.x if self.in_relu else None)
         ops.conv_dgrad(dy, st.weight(kn), st.weight_t(kn), self.dx, self.k, self.k, self.stride, self.pad,
-                       mask=self.x if self.in_relu else None)
+                       mask=mask, residual=residual, residual_mask=residual_mask)
         return self.dx
 
     def config(self):
@@ -342,26 +345,44 @@ class BatchNorm(Layer):
             self.run_var = torch.ones(self.C, device=device)
         self.mean = torch.zeros(self.C, device=device)
         self.invstd = torch.ones(self.C, device=device)
+        self.coef = torch.zeros(3 * self.C, device=device)               # dx = k1*g + k2*x + k3
+        # last-arriver ticket counters of the statistics launches (forward row 0, backward row 1)
+        self.counter = torch.zeros(2, ops.BN_COUNTERS, dtype=torch.int32, device=device)
+
+    def stats(self, x):
+        """Training-mode batch statistics of ``x`` (and the running statistics); writes no output."""
+        self.x = x
+        ops.bn_stats_fwd(x.reshape(-1, self.C), self.mean, self.invstd, self.run_mean, self.run_var, self.ws.bn,
+                         self.counter[0], self.momentum, self.eps)
+
+    def affine(self, training):
+        st = self.store
+        g, b = st[f"{self.name}/gamma"], st[f"{self.name}/beta"]
+        return (g, b, self.mean, self.invstd) if training else (g, b, self.run_mean, self.run_var)
+
+    def apply(self, x, out, training, residual=None, residual_bn=None, relu=None):
+        """out = act(bn(x) [+ residual | + residual_bn(residual)]) in one streaming pass."""
+        g, b, m, v = self.affine(training)
+        rbn = residual_bn.affine(training) if residual_bn is not None else None
+        ops.bn_apply(x.reshape(-1, self.C), out.view(-1, self.C), g, b, m, v, self.relu if relu is None else relu,
+                     residual.reshape(-1, self.C) if residual is not None else None, rbn, not training, self.eps)
+        return out
 
     def forward(self, x, training):
         self.x = x
-        st = self.store
-        x2 = x.reshape(-1, self.C)
-        y2 = self.out.view(-1, self.C)
-        g, b = st[f"{self.name}/gamma"], st[f"{self.name}/beta"]
         if training:
-            ops.bn_fwd_train(x2, y2, g, b, self.mean, self.invstd, self.run_mean, self.run_var, self.ws.bn,
-                             self.momentum, self.eps, self.relu)
-        else:
-            ops.bn_fwd_eval(x2, y2, g, b, self.run_mean, self.run_var, self.eps, self.relu)
-        return self.out
+            self.stats(x)
+        return self.apply(x, self.out, training)
 
-    def backward(self, dy):
+    def backward(self, dy, mask=None):
+        """``mask``: relu' source applied to dy (default: this layer's own output when it ends in ReLU)."""
         st = self.store
-        x2 = self.x.reshape(-1, self.C)
-        ops.bn_bwd(x2, self.out.view(-1, self.C), dy.reshape(-1, self.C), self.dx.view(-1, self.C),
-                   st[f"{self.name}/gamma"], st[f"{self.name}/beta"], self.mean, self.invstd,
-                   st.gradient(f"{self.name}/gamma"), st.gradient(f"{self.name}/beta"), self.ws.bn, self.relu)
+        if mask is None and self.relu:
+            mask = self.out
+        ops.bn_bwd(self.x.reshape(-1, self.C), mask.reshape(-1, self.C) if mask is not None else None,
+                   dy.reshape(-1, self.C), self.dx.view(-1, self.C), st[f"{self.name}/gamma"], self.mean, self.invstd,
+                   st.gradient(f"{self.name}/gamma"), st.gradient(f"{self.name}/beta"), self.ws.bn, self.coef,
+                   self.counter[1])
         if self.in_relu:
             raise NotImplementedError("BatchNorm after a fused ReLU")
         return self.dx
@@ -449,39 +470,46 @@ class ResidualBlock(Layer):
         for l in self.sublayers():
             l.alloc(B, device, dtype, ws)
         self.out = torch.empty((B,) + self.out_shape, device=device, dtype=dtype)
-        self.g = torch.empty_like(self.out)
-        if self.need_dx:
-            self.dx = torch.empty((B,) + self.in_shape, device=device, dtype=dtype)
+        # conv1's data gradient IS the block's: its dgrad epilogue adds the shortcut gradient and relu'(x)
+        self.dx = self.conv1.dx if self.need_dx else None
 
     def forward(self, x, training):
         self.x = x
         h = self.conv1.forward(x, training)
         h = self.bn1.forward(h, training)
         h = self.conv2.forward(h, training)
-        h = self.bn2.forward(h, training)
-        sc = x
+        self.bn2.x = h
+        if training:
+            self.bn2.stats(h)
+        r, rbn = x, None
         if self.proj is not None:
-            sc = self.proj_bn.forward(self.proj.forward(x, training), training)
-        ops.add_act(h, sc, self.out, relu=True)
+            p = self.proj.forward(x, training)
+            self.proj_bn.x = p
+            if training:
+                self.proj_bn.stats(p)
+            r, rbn = p, self.proj_bn
+        # one streaming pass: out = relu(bn2(h) + shortcut), shortcut = x or proj_bn(proj(x))
+        self.bn2.apply(h, self.out, training, residual=r, residual_bn=rbn, relu=True)
         return self.out
 
     def backward(self, dy):
-        g = ops.relu_bwd(self.out, dy, self.g)  # relu' of the block output, shared by both branches
-        d = self.bn2.backward(g)
+        # relu' of the block output is applied inside both BN backward passes (mask = block output)
+        d = self.bn2.backward(dy, mask=self.out)
         d = self.conv2.backward(d)
         d = self.bn1.backward(d)
-        d = self.conv1.backward(d)
+        ds = None
         if self.proj is not None:
-            ds = self.proj.backward(self.proj_bn.backward(g))
-        else:
-            ds = g
+            ds = self.proj.backward(self.proj_bn.backward(dy, mask=self.out))
         if not self.need_dx:
+            self.conv1.backward(d)
             return None
-        # input relu' (block input is the previous block's ReLU output) is applied by add_act on
-        # the two branch gradients: dx = (d + ds) * (x > 0) — done as add then relu_bwd.
-        ops.add_act(d, ds, self.dx, relu=False)
-        if self.in_relu:
-            ops.relu_bwd(self.x, self.dx, self.dx)
+        # conv1's dgrad epilogue joins the branches: dx = (conv1^T d + shortcut grad) * relu'(x), where the
+        # shortcut gradient is proj^T(...) or the identity path's dy * relu'(out)
+        if self.proj is not None:
+            res, res_mask = ds, None
+        else:
+            res, res_mask = dy, self.out
+        self.conv1.backward(d, residual=res, residual_mask=res_mask, dx_mask=self.x if self.in_relu else None)
         return self.dx
 
     def config(self):

@@ -156,9 +156,12 @@ class Net:
     def bind(self, B: int):
         if self._bound_B == B:
             return
-        ws_wgrad = torch.empty(1 << 22, dtype=torch.float32, device=self.device)
+        # split-m weight-gradient slabs: room for 4 slabs of the largest conv kernel (>= 16 MB)
+        nk = max([l.filters * l.k * l.k * l.in_shape[2] for l in self._all_leaf_layers() if isinstance(l, Conv2D)]
+                 + [0])
+        ws_wgrad = torch.empty(max(1 << 22, 4 * nk), dtype=torch.float32, device=self.device)
         maxC = max([l.C for l in self._all_leaf_layers() if isinstance(l, BatchNorm)] + [8])
-        ws_bn = torch.empty(2 * maxC * 256, dtype=torch.float32, device=self.device)
+        ws_bn = torch.empty(ops.bn_workspace_floats(maxC), dtype=torch.float32, device=self.device)
         self.ws = Workspace(ws_wgrad, ws_bn)
         for l in self.exec_layers:
             l.alloc(B, self.device, self.dtype, self.ws)

@@ -81,16 +81,26 @@ def conv_fwd(x, w, bias, out, KH, KW, stride=1, pad=0, relu=False):
     return out
 
 
-def conv_dgrad(dy, w, wt, out, KH, KW, stride=1, pad=0, mask=None):
-    """dX (NHWC [B][H][W][C]) of a conv whose output gradient is dy [B][OH][OW][N]."""
+def conv_dgrad(dy, w, wt, out, KH, KW, stride=1, pad=0, mask=None, residual=None, residual_mask=None):
+    """dX (NHWC [B][H][W][C]) of a conv whose output gradient is dy [B][OH][OW][N].
+
+    Epilogue (ResNet block join): dX = (conv^T dy + residual * [residual_mask > 0]) * [mask > 0]."""
     B, OH, OW, N = dy.shape
     _, H, W, C = out.shape
     if dy.is_cuda:
         K = KH * KW * N
         _C().igemm_fwd(dy, wt, None, mask, out, B * H * W, C, K, wt.shape[1], 0, C,
-                       _geom(OH, OW, N, H, W, KH, KW, stride, pad), MODE_DGRAD, False, 1.0)
+                       _geom(OH, OW, N, H, W, KH, KW, stride, pad), MODE_DGRAD, False, 1.0, residual, residual_mask)
     else:
-        out.copy_(ref.conv_dgrad(dy, w, out.shape, KH, KW, stride, pad, mask))
+        dx = ref.conv_dgrad(dy, w, out.shape, KH, KW, stride, pad, None)
+        if residual is not None:
+            r = residual.float().reshape(dx.shape)
+            if residual_mask is not None:
+                r = r * (residual_mask.float().reshape(dx.shape) > 0)
+            dx = dx + r
+        if mask is not None:
+            dx = dx * (mask.float().reshape(dx.shape) > 0)
+        out.copy_(dx)
     return out
 
 
@@ -200,39 +210,68 @@ def gap_bwd(dy, dx):
     return dx
 
 
-def bn_fwd_train(x2d, y2d, gamma, beta, mean, invstd, run_mean, run_var, ws, momentum, eps, relu):
+BN_COUNTERS = 17  # ticket counters of one BN statistics launch: 1 global + 1 per group of 16 (<= 255) workgroups
+
+
+def bn_workspace_floats(C: int) -> int:
+    """fp32 workspace of a BN statistics launch of any M: <= 255 partial slabs + <= 16 group slabs of [2][C]."""
+    return (255 + 16) * 2 * C
+
+
+def bn_stats_fwd(x2d, mean, invstd, run_mean, run_var, ws, counter, momentum=0.1, eps=1e-5):
+    """Training batch statistics of x2d [M][C] -> mean, invstd; running statistics updated in place.
+    GPU: one launch (csrc/bn.hip; ``counter`` = int32 last-arriver ticket, zero between launches)."""
     M, C = x2d.shape
     if x2d.is_cuda:
-        _C().bn_fwd_train(x2d, y2d, gamma, beta, mean, invstd, run_mean, run_var, ws, M, C, momentum, eps, relu)
+        _C().bn_stats_fwd(x2d, mean, invstd, run_mean, run_var, ws, counter, M, C, momentum, eps)
     else:
-        y, mu, var, inv = ref.batchnorm_train(x2d, gamma, beta, eps)
-        y2d.copy_(torch.relu(y) if relu else y)
+        mu = x2d.float().mean(0)
+        var = x2d.float().var(0, unbiased=False)
         mean.copy_(mu)
-        invstd.copy_(inv)
-        unb = var * M / max(M - 1, 1)
-        run_mean.mul_(1 - momentum).add_(mu * momentum)
-        run_var.mul_(1 - momentum).add_(unb * momentum)
+        invstd.copy_(torch.rsqrt(var + eps))
+        if run_mean is not None:
+            unb = var * M / max(M - 1, 1)
+            run_mean.mul_(1 - momentum).add_(mu * momentum)
+            run_var.mul_(1 - momentum).add_(unb * momentum)
 
 
-def bn_fwd_eval(x2d, y2d, gamma, beta, run_mean, run_var, eps, relu):
+def bn_apply(x2d, y2d, gamma, beta, mean, invstd, relu=False, residual=None, residual_bn=None, eval_mode=False,
+             eps=1e-5):
+    """y = act(bn(x) [+ r | + bn_r(r)]): ``residual_bn`` = (gamma, beta, mean, invstd) of the residual's BN
+    (ResNet projection shortcut).  ``eval_mode``: mean / invstd are the running mean / variance."""
     M, C = x2d.shape
     if x2d.is_cuda:
-        _C().bn_fwd_eval(x2d, y2d, gamma, beta, run_mean, run_var, M, C, eps, relu)
+        rg = rb = rm = ri = None
+        if residual_bn is not None:
+            rg, rb, rm, ri = residual_bn
+        _C().bn_apply(x2d, y2d, gamma, beta, mean, invstd, residual, rg, rb, rm, ri, M, C, relu, eval_mode, eps)
     else:
-        y = (x2d.float() - run_mean) * torch.rsqrt(run_var + eps) * gamma + beta
+        def aff(x, g, b, m, v):
+            inv = torch.rsqrt(v + eps) if eval_mode else v
+            return (x.float() - m) * inv * g + b
+
+        y = aff(x2d, gamma, beta, mean, invstd)
+        if residual is not None:
+            r = residual.reshape(M, C)
+            y = y + (aff(r, *residual_bn) if residual_bn is not None else r.float())
         y2d.copy_(torch.relu(y) if relu else y)
+    return y2d
 
 
-def bn_bwd(x2d, y2d, dy2d, dx2d, gamma, beta, mean, invstd, dgamma, dbeta, ws, relu, gscale=1.0):
+def bn_bwd(x2d, mask2d, dy2d, dx2d, gamma, mean, invstd, dgamma, dbeta, ws, coef, counter, gscale=1.0):
+    """Backward of y = bn(x): dx, dgamma, dbeta (scaled by gscale) from dy; g = dy * (mask > 0) when a
+    mask (relu' source) is given.  GPU: statistics launch (which also writes the dx coefficients) + dx pass."""
     M, C = x2d.shape
     if x2d.is_cuda:
-        _C().bn_bwd(x2d, y2d, dy2d, dx2d, gamma, beta, mean, invstd, dgamma, dbeta, ws, M, C, relu, gscale)
+        _C().bn_stats_bwd(x2d, mask2d, dy2d, gamma, mean, invstd, dgamma, dbeta, coef, ws, counter, M, C, gscale)
+        _C().bn_dx(x2d, mask2d, dy2d, dx2d, coef, M, C)
     else:
-        g = dy2d.float() * (y2d.float() > 0) if relu else dy2d.float()
+        g = dy2d.float() * (mask2d.float() > 0) if mask2d is not None else dy2d.float()
         dx, sg, sb = ref.batchnorm_bwd(x2d, g, gamma, mean, invstd)
         dx2d.copy_(dx)
         dgamma.copy_(sg * gscale)
         dbeta.copy_(sb * gscale)
+    return dx2d
 
 
 # ----------------------------------------------------------------------------------- fused conv+pool

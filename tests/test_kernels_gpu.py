@@ -180,6 +180,28 @@ def test_conv_wgrad(B, H, W, C, N, k, s, p):
     _close(gb, eb, 1e-3, 1e-3)
 
 
+WGRAD_TR = [  # B, H, W, C, N, k, stride, pad: ResNet-18 CIFAR shapes on the transposed-read kernel
+    (8, 32, 32, 64, 64, 3, 1, 1),
+    (8, 32, 32, 64, 128, 3, 2, 1),
+    (8, 16, 16, 128, 128, 3, 1, 1),
+    (8, 16, 16, 64, 128, 1, 2, 0),
+    (16, 4, 4, 512, 512, 3, 1, 1),
+    (3, 9, 7, 16, 24, 3, 2, 1),       # odd sizes: m / n / k tails
+]
+
+
+@pytest.mark.parametrize("B,H,W,C,N,k,s,p", WGRAD_TR)
+def test_conv_wgrad_transposed_reads(B, H, W, C, N, k, s, p):
+    OH, OW = ops.conv_out_hw(H, W, k, k, s, p)
+    dy = torch.randn(B, OH, OW, N, device=dev).to(torch.bfloat16)
+    x = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    gw = torch.full((N, k * k * C), float("nan"), device=dev)
+    ws = torch.empty(1 << 24, device=dev)
+    ops.conv_wgrad(dy, x, gw, None, ws, k, k, s, p, scale=0.5)
+    ew, _ = ref.conv_wgrad(dy.float(), x.float(), k, k, s, p, with_bias=False)
+    _close(gw, 0.5 * ew, 1e-3, 1e-3)
+
+
 def test_conv_wgrad_large_m_split():
     """Tall-skinny reduction (K = B*OH*OW = 1.3M) exercising many split-m slabs + the reduce kernel."""
     B, H, W, C, N, k = 512, 28, 28, 1, 6, 5
@@ -252,7 +274,8 @@ def test_gather_batch_u8():
     assert torch.equal(ol, labels[idx])
 
 
-@pytest.mark.parametrize("M,C,relu", [(4096, 64, True), (1000, 128, False), (512, 6, True)])
+@pytest.mark.parametrize("M,C,relu", [(4096, 64, True), (1000, 128, False), (512, 6, True), (65536, 512, False),
+                                      (262144, 64, True), (300, 1024, False)])
 def test_batchnorm(M, C, relu):
     x = (torch.randn(M, C, device=dev) * 2 + 0.5).to(torch.bfloat16)
     g = torch.rand(C, device=dev) + 0.5
@@ -262,24 +285,68 @@ def test_batchnorm(M, C, relu):
     inv = torch.empty(C, device=dev)
     rm = torch.zeros(C, device=dev)
     rv = torch.ones(C, device=dev)
-    ws = torch.empty(2 * C * 256, device=dev)
-    ops.bn_fwd_train(x, y, g, b, mean, inv, rm, rv, ws, 0.1, 1e-5, relu)
+    ws = torch.empty(ops.bn_workspace_floats(C), device=dev)
+    cnt = torch.zeros(2, ops.BN_COUNTERS, dtype=torch.int32, device=dev)
+    coef = torch.empty(3 * C, device=dev)
+    for _ in range(2):  # the last workgroups re-arm the ticket counters: a second launch must agree
+        ops.bn_stats_fwd(x, mean, inv, rm, rv, ws, cnt[0], 0.1, 1e-5)
+    ops.bn_apply(x, y, g, b, mean, inv, relu=relu)
     ey, emu, evar, einv = ref.batchnorm_train(x.float(), g, b, 1e-5)
     if relu:
         ey = torch.relu(ey)
     _close(y, ey)
     _close(mean, emu, 1e-4, 1e-4)
     _close(inv, einv, 1e-3, 1e-3)
+    unb = evar * M / (M - 1)
+    _close(rm, 0.19 * emu, 1e-4, 1e-4)          # two momentum-0.1 updates from 0
+    _close(rv, 0.81 + 0.19 * unb, 1e-3, 1e-3)   # ... and from 1
+    assert int(cnt[0].abs().sum()) == 0
     dy = torch.randn(M, C, device=dev).to(torch.bfloat16)
     dx = torch.empty_like(x)
     dg = torch.empty(C, device=dev)
     db = torch.empty(C, device=dev)
-    ops.bn_bwd(x, y, dy, dx, g, b, mean, inv, dg, db, ws, relu)
+    ops.bn_bwd(x, y if relu else None, dy, dx, g, mean, inv, dg, db, ws, coef, cnt[1])
+    assert int(cnt[1].abs().sum()) == 0
     gin = dy.float() * (y.float() > 0) if relu else dy.float()
     edx, esg, esb = ref.batchnorm_bwd(x.float(), gin, g, emu, einv)
     _close(dx, edx, 3e-2, 3e-2)
     _close(dg, esg, 1e-2, 1e-2)
     _close(db, esb, 1e-3, 1e-3)
+    # eval mode normalizes with the running statistics
+    ops.bn_apply(x, y, g, b, rm, rv, relu=relu, eval_mode=True)
+    ee = (x.float() - rm) * torch.rsqrt(rv + 1e-5) * g + b
+    _close(y, torch.relu(ee) if relu else ee)
+
+
+@pytest.mark.parametrize("proj", [False, True])
+def test_bn_apply_residual_join(proj):
+    M, C = 2048, 128
+    x = torch.randn(M, C, device=dev).to(torch.bfloat16)
+    r = torch.randn(M, C, device=dev).to(torch.bfloat16)
+    g, b = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
+    m, inv = torch.randn(C, device=dev), torch.rand(C, device=dev) + 0.5
+    rbn = (torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev), torch.randn(C, device=dev),
+           torch.rand(C, device=dev) + 0.5) if proj else None
+    y = torch.empty_like(x)
+    ops.bn_apply(x, y, g, b, m, inv, relu=True, residual=r, residual_bn=rbn)
+    e = (x.float() - m) * inv * g + b
+    e = e + (((r.float() - rbn[2]) * rbn[3] * rbn[0] + rbn[1]) if proj else r.float())
+    _close(y, torch.relu(e))
+
+
+def test_conv_dgrad_residual_epilogue():
+    """ResNet block join in the dgrad epilogue: dx = (conv^T dy + res * [resmask > 0]) * [mask > 0]."""
+    B, H, W, C, N, k = 4, 16, 16, 64, 64, 3
+    dy = torch.randn(B, H, W, N, device=dev).to(torch.bfloat16)
+    w = torch.randn(N, k * k * C, device=dev) / (k * k * N) ** 0.5
+    res = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    rmask = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    mask = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    out = torch.empty(B, H, W, C, device=dev, dtype=torch.bfloat16)
+    ops.conv_dgrad(dy, None, _pad_wt(w, N, k * k, C), out, k, k, 1, 1, mask=mask, residual=res, residual_mask=rmask)
+    exp = ref.conv_dgrad(dy.float(), w.to(torch.bfloat16).float(), (B, H, W, C), k, k, 1, 1, None)
+    exp = (exp + res.float() * (rmask.float() > 0)) * (mask.float() > 0)
+    _close(out, exp)
 
 
 CONVPOOL = [  # B, H, W, C, N, k, pad
