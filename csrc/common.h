@@ -53,6 +53,23 @@ struct FDiv {
   __device__ __forceinline__ int mod(int a, int q) const { return a - q * d; }
 };
 
+// Unsigned division by a launch constant: q = n / d for 0 <= n < 2^31 as (mulhi(n, mul) + n) >> shr,
+// with the magic number computed on the host (pixel decomposition of implicit-GEMM rows).
+struct FastDiv {
+  unsigned mul, shr;
+};
+
+inline FastDiv make_fastdiv(unsigned d) {
+  unsigned l = 0;
+  while ((1u << l) < d) ++l;
+  FastDiv f;
+  f.mul = (unsigned)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+  f.shr = l;
+  return f;
+}
+
+__device__ __forceinline__ unsigned fdiv(unsigned n, FastDiv f) { return (__umulhi(n, f.mul) + n) >> f.shr; }
+
 // Bijective XCD-aware remap of a 1-D block id: consecutive logical tiles land on the same XCD
 // (blocks b and b+8 share an XCD under round-robin dispatch) so neighbouring tiles share L2.
 __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {

@@ -532,6 +532,7 @@ static hipError_t launch_fwd_mode(const IGemmArgs& a, hipStream_t st) {
 
 hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0) return hipSuccess;
+  if (igemm64_supported(a, mode)) return igemm64(a, mode, st);
   const bool aligned = ((uintptr_t)a.src & 15) == 0;
   if (mode == MODE_DIRECT) {
     const bool vec = aligned && a.lda % 8 == 0 && a.K % 8 == 0;

@@ -1,0 +1,236 @@
+// Implicit-GEMM forward / data-gradient MFMA kernel with 64-deep k steps (gfx950), for the
+// vectorizable cases of igemm_fwd: dense layers with K % 8 == 0 and NHWC conv / transposed-conv
+// gathers with C % 8 == 0 (every ResNet-18 conv but the 3-channel stem).  SURVEY §2.4 O2/O3/O8:
+// the reference's tf.js matMul / conv2d forward and the data gradients of its autodiff.
+//
+//   C[m][n] = epi( sum_k A[m][k] * W[n][k] ),  A = rows of the activation (dense), the im2col row
+//   of an output pixel (conv forward) or the transposed-conv gather of dY (data gradient).
+//
+//   * 4 waves (2 x 2) on a 128x128 / 128x64 / 64x128 tile; v_mfma_f32_16x16x32_bf16; each 64-deep
+//     step is two 32-deep halves, so a wave issues 2*TM*TN MFMAs per barrier (32 on 128x128)
+//   * register-staged double buffer: the 16-byte global loads of step k+1 are issued before the
+//     MFMAs of step k and stored to the other LDS buffer after them; one barrier per step
+//   * LDS rows of 64 bf16 (128 B) with the 16-byte chunk swizzle c ^ ((row >> 1) & 7): the 16 rows
+//     one ds_read_b128 lane group reads sit on 16 distinct 16-byte bank slots
+//   * a thread's 16-byte chunk column is fixed (c = tid & 7), so ONE (kh, kw, ci) state per thread
+//     advances per step; the per-row pixel state is computed once with multiply-high division
+//   * every load comes from a clamped address and is masked afterwards (no load under a branch)
+//   * epilogue as igemm.hip: alpha, bias, residual join (res * [resmask > 0]), ReLU, relu'(mask)
+#include "common.h"
+#include "kernels.h"
+
+namespace dfa {
+
+namespace {
+
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3); }
+
+template <int BM, int BN, int MODE>
+__global__ void __launch_bounds__(256) igemm64_kernel(IGemmArgs a, FastDiv d_ow, FastDiv d_ohw) {
+  constexpr int WM = 2, WN = 2;
+  constexpr int TM = BM / (WM * 16), TN = BN / (WN * 16);
+  constexpr int AP = BM / 32, BP = BN / 32;  // 16-byte chunks per thread and step (8 chunks per 64-deep row)
+  static_assert(TM >= 1 && TN >= 1 && AP >= 1 && BP >= 1, "tile shape");
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * (BM + BN) * 64];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntn = cdiv(a.N, BN), ntm = cdiv(a.M, BM);
+  const int logical = xcd_remap(blockIdx.x, ntn * ntm);
+  const int tile_n = logical % ntn, tile_m = logical / ntn;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int c = tid & 7, r0 = tid >> 3;  // chunk column; rows r0 + 32 i
+
+  // per-row source state (fixed over the k loop)
+  long long rbase[AP];
+  int rh[AP], rw[AP];
+  bool rval[AP];
+#pragma unroll
+  for (int i = 0; i < AP; ++i) {
+    const int m = m0 + r0 + 32 * i;
+    rval[i] = m < a.M;
+    const unsigned mm = (unsigned)min(m, a.M - 1);
+    if (MODE == MODE_DIRECT) {
+      rbase[i] = (long long)mm * a.lda;
+      rh[i] = rw[i] = 0;
+    } else {
+      const unsigned b = fdiv(mm, d_ohw);
+      const unsigned rem = mm - b * (unsigned)(a.OH * a.OW);
+      const unsigned oh = fdiv(rem, d_ow);
+      const int ow = (int)(rem - oh * (unsigned)a.OW);
+      rbase[i] = (long long)b * a.SH * a.SW * a.SC;
+      if (MODE == MODE_FWD) {
+        rh[i] = (int)oh * a.stride - a.pad;
+        rw[i] = ow * a.stride - a.pad;
+      } else {
+        rh[i] = (int)oh + a.pad;
+        rw[i] = ow + a.pad;
+      }
+    }
+  }
+  // this thread's k chunk: k = kt * 64 + 8c  ->  (kh, kw, ci) for the gathers
+  int kk = 8 * c, kh = 0, kw = 0, ci = kk;
+  if (MODE != MODE_DIRECT) {
+    ci = kk % a.SC;
+    const int t = kk / a.SC;
+    kh = t / a.KW;
+    kw = t - kh * a.KW;
+  }
+  const int npad = round_up(a.N, 16);
+
+  u32x4_t ra[AP], rb[BP];
+  auto gload = [&]() {
+    const bool kv = kk < a.K;
+#pragma unroll
+    for (int i = 0; i < AP; ++i) {
+      bool v = rval[i] && kv;
+      long long off;
+      if (MODE == MODE_DIRECT) {
+        off = rbase[i] + kk;
+      } else if (MODE == MODE_FWD) {
+        const int sh = rh[i] + kh, sw = rw[i] + kw;
+        v = v && (unsigned)sh < (unsigned)a.SH && (unsigned)sw < (unsigned)a.SW;
+        off = rbase[i] + ((long long)sh * a.SW + sw) * a.SC + ci;
+      } else {  // dX(ih, iw) <- dY((ih + pad - kh) / s, (iw + pad - kw) / s)
+        int th = rh[i] - kh, tw = rw[i] - kw;
+        v = v && th >= 0 && tw >= 0;
+        if (a.stride > 1) {
+          v = v && (th % a.stride) == 0 && (tw % a.stride) == 0;
+          th /= a.stride;
+          tw /= a.stride;
+        }
+        v = v && th < a.SH && tw < a.SW;
+        off = rbase[i] + ((long long)th * a.SW + tw) * a.SC + ci;
+      }
+      const u32x4_t t = *reinterpret_cast<const u32x4_t*>(a.src + (v ? off : 0));
+      ra[i] = t & (v ? 0xffffffffu : 0u);
+    }
+#pragma unroll
+    for (int i = 0; i < BP; ++i) {
+      const int n = n0 + r0 + 32 * i;
+      const bool v = n < npad && kk < a.Kpad;
+      const u32x4_t t = *reinterpret_cast<const u32x4_t*>(a.w + (v ? (long long)n * a.Kpad + kk : 0));
+      rb[i] = t & (v ? 0xffffffffu : 0u);
+    }
+  };
+  auto advance = [&]() {
+    kk += 64;
+    if (MODE != MODE_DIRECT) {
+      ci += 64;
+      while (ci >= a.SC) {
+        ci -= a.SC;
+        if (++kw == a.KW) {
+          kw = 0;
+          ++kh;
+        }
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+    bf16* as = lds + buf * (BM + BN) * 64;
+    bf16* bs = as + BM * 64;
+#pragma unroll
+    for (int i = 0; i < AP; ++i) *reinterpret_cast<u32x4_t*>(as + swz(r0 + 32 * i, c)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BP; ++i) *reinterpret_cast<u32x4_t*>(bs + swz(r0 + 32 * i, c)) = rb[i];
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = cdiv(a.K, 64);
+  gload();
+  sstore(0);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      advance();
+      gload();
+    }
+    const bf16* as = lds + cur * (BM + BN) * 64;
+    const bf16* bs = as + BM * 64;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(as + swz(wm * TM * 16 + i * 16 + fr, h * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(bs + swz(wn * TN * 16 + j * 16 + fr, h * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fa[i], fb[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: C/D layout of the 16x16 MFMA: col (n) = lane & 15, row (m) = 4 * (lane >> 4) + r
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * TN * 16 + j * 16 + fr;
+      if (col >= a.N) continue;
+      const float bv = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * TM * 16 + i * 16 + fq * 4 + r;
+        if (row >= a.M) continue;
+        float v = acc[i][j][r] * a.alpha + bv;
+        const long long o = (long long)row * a.ldc + col;
+        if (a.res) {
+          const float rv = (float)a.res[o];
+          if (!a.resmask || (float)a.resmask[o] > 0.f) v += rv;
+        }
+        if (a.relu) v = fmaxf(v, 0.f);
+        if (a.mask && !((float)a.mask[o] > 0.f)) v = 0.f;
+        if (a.out_f32)
+          reinterpret_cast<float*>(a.out)[o] = v;
+        else
+          reinterpret_cast<bf16*>(a.out)[o] = f2bf(v);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int MODE>
+hipError_t launch64(const IGemmArgs& a, hipStream_t st) {
+  const FastDiv d_ow = make_fastdiv((unsigned)max(a.OW, 1)), d_ohw = make_fastdiv((unsigned)max(a.OH * a.OW, 1));
+  const int blocks = cdiv(a.M, BM) * cdiv(a.N, BN);
+  hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE>), dim3(blocks), dim3(256), 0, st, a, d_ow, d_ohw);
+  return hipGetLastError();
+}
+
+template <int MODE>
+hipError_t launch64_mode(const IGemmArgs& a, hipStream_t st) {
+  if (a.N <= 64) return launch64<128, 64, MODE>(a, st);
+  // 128x128 while that still gives >= 2 workgroups per CU, else 64x128
+  if ((long long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 512) return launch64<128, 128, MODE>(a, st);
+  return launch64<64, 128, MODE>(a, st);
+}
+
+}  // namespace
+
+bool igemm64_supported(const IGemmArgs& a, int mode) {
+  if (((uintptr_t)a.src & 15) || ((uintptr_t)a.w & 15) || a.Kpad % 8 || a.M <= 0 || a.N <= 0) return false;
+  if (mode == MODE_DIRECT) return a.lda % 8 == 0 && a.K % 8 == 0;
+  return a.SC % 8 == 0 && a.OH > 0 && a.OW > 0;
+}
+
+hipError_t igemm64(const IGemmArgs& a, int mode, hipStream_t st) {
+  if (mode == MODE_DIRECT) return launch64_mode<MODE_DIRECT>(a, st);
+  if (mode == MODE_FWD) return launch64_mode<MODE_FWD>(a, st);
+  return launch64_mode<MODE_DGRAD>(a, st);
+}
+
+}  // namespace dfa

@@ -57,6 +57,9 @@ struct ParamDescTable {
 };
 
 hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st);
+// 64-deep-step variant for the vectorizable cases (csrc/igemm64.hip); igemm_fwd dispatches to it
+bool igemm64_supported(const IGemmArgs& a, int mode);
+hipError_t igemm64(const IGemmArgs& a, int mode, hipStream_t st);
 hipError_t igemm_wgrad(const WgradArgs& a, int mode, float* workspace, size_t ws_floats, hipStream_t st);
 // conv weight gradient with transposed LDS reads (csrc/wgrad_tr.hip): conv, C % 8 == 0, no bias
 bool wgrad_tr_supported(const WgradArgs& a, int mode);

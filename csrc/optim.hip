@@ -42,24 +42,7 @@ __device__ __forceinline__ void sgd_multi_body(const DT& descs, int ndesc,
     lr = hyper[0]; mom = hyper[1]; wd = hyper[2]; gs = hyper[3]; nesterov = hyper[4] != 0.f;
   }
   const int K = d.T * d.Ci;
-  // d.pad_ = KW | Cp << 16 (KW > 0): the primary copy uses the row-segment layout of the fused
-  // conv+pool forward, [Npad16][round32(KH * round8(KW*Cp))], column ky*round8(KW*Cp) + kx*Cp + ci
-  // d.pad_ = KW | Cp << 16 | pair << 30: pair layout (N <= 8) = 16 rows, rows 8+n hold channel n
-  // shifted right by one kernel column (the fused conv+pool forward computes pixels x and x+1)
-  const int rKW = d.pad_ & 0xffff;
-  // d.pad_ bit 29: the dgrad copy uses the conv+pool dgrad pair layout (csrc/convpool.hip make_dgrad),
-  // [16][round32(KH*(KW+1)*N)]: row ci col (a*(KW+1) + KW-1-kx)*N + n and row 8+ci col (a*(KW+1) + KW-kx)*N + n,
-  // a = KH-1-ky (the kernel flip of the transposed convolution)
-  const int rCp = ((d.pad_ >> 16) & 0x1fff) > 0 ? ((d.pad_ >> 16) & 0x1fff) : d.Ci;
-  const bool rpair = (d.pad_ >> 30) & 1;
-  const bool tpair = rKW > 0 && ((d.pad_ >> 29) & 1);
-  const int RLp = rKW > 0 ? round_up((rKW + (rpair ? 1 : 0)) * rCp, 8) : K;
-  const int Kpad = round_up(rKW > 0 ? (d.T / rKW) * RLp : K, 32);
-  const int KpadT = round_up(tpair ? (d.T / rKW) * (rKW + 1) * d.N : d.T * d.N, 32);
-#pragma unroll
-  for (int r = 0; r < SGD_ELEMS_PER_BLOCK / 256; ++r) {
-    const int i = base + r * 256 + threadIdx.x;
-    if (i >= d.numel) break;
+  auto update = [&](int i) -> float {
     float w = master[d.off + i];
     if (apply_update) {
       float g = grad[d.off + i] * gs;
@@ -72,6 +55,59 @@ __device__ __forceinline__ void sgd_multi_body(const DT& descs, int ndesc,
       w -= lr * g;
       master[d.off + i] = w;
     }
+    return w;
+  };
+  // d.pad_ bit 28: tile mode for a plain [N][K] matrix with a plain dgrad copy [Ci][T*N]: the workgroup
+  // owns a 32 (n) x 32 (k) tile; the update and the primary copy run along k (coalesced), and the
+  // dgrad copy is written through an LDS transpose as 64-byte runs along n (instead of 2-byte
+  // scatters one KpadT row apart)
+  if ((d.pad_ >> 28) & 1) {
+    __shared__ bf16 tt[32][34];
+    const int ntk = cdiv(K, 32);
+    const int tl = bid - d.block_start;
+    const int n0 = (tl / ntk) * 32, k0 = (tl % ntk) * 32;
+    const int Kp = round_up(K, 32);
+    const int KpT = round_up(d.T * d.N, 32);
+    const int cc = threadIdx.x & 31, r0 = threadIdx.x >> 5;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int n = n0 + r0 + 8 * rr, k = k0 + cc;
+      if (n < d.N && k < K) {
+        const bf16 wb = f2bf(update(n * K + k));
+        wbf[d.bf_off + (long long)n * Kp + k] = wb;
+        tt[cc][r0 + 8 * rr] = wb;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int k = k0 + r0 + 8 * rr, n = n0 + cc;
+      if (n < d.N && k < K) {
+        const int t = k / d.Ci, ci = k - t * d.Ci;
+        wbf[d.bft_off + (long long)ci * KpT + t * d.N + n] = tt[r0 + 8 * rr][cc];
+      }
+    }
+    return;
+  }
+  // d.pad_ = KW | Cp << 16 (KW > 0): the primary copy uses the row-segment layout of the fused
+  // conv+pool forward, [Npad16][round32(KH * round8(KW*Cp))], column ky*round8(KW*Cp) + kx*Cp + ci
+  // d.pad_ = KW | Cp << 16 | pair << 30: pair layout (N <= 8) = 16 rows, rows 8+n hold channel n
+  // shifted right by one kernel column (the fused conv+pool forward computes pixels x and x+1)
+  const int rKW = d.pad_ & 0xffff;
+  // d.pad_ bit 29: the dgrad copy uses the conv+pool dgrad pair layout (csrc/convpool.hip make_dgrad),
+  // [16][round32(KH*(KW+1)*N)]: row ci col (a*(KW+1) + KW-1-kx)*N + n and row 8+ci col (a*(KW+1) + KW-kx)*N + n,
+  // a = KH-1-ky (the kernel flip of the transposed convolution)
+  const int rCp = ((d.pad_ >> 16) & 0xfff) > 0 ? ((d.pad_ >> 16) & 0xfff) : d.Ci;
+  const bool rpair = (d.pad_ >> 30) & 1;
+  const bool tpair = rKW > 0 && ((d.pad_ >> 29) & 1);
+  const int RLp = rKW > 0 ? round_up((rKW + (rpair ? 1 : 0)) * rCp, 8) : K;
+  const int Kpad = round_up(rKW > 0 ? (d.T / rKW) * RLp : K, 32);
+  const int KpadT = round_up(tpair ? (d.T / rKW) * (rKW + 1) * d.N : d.T * d.N, 32);
+#pragma unroll
+  for (int r = 0; r < SGD_ELEMS_PER_BLOCK / 256; ++r) {
+    const int i = base + r * 256 + threadIdx.x;
+    if (i >= d.numel) break;
+    const float w = update(i);
     if (d.bf_off >= 0) {
       const int n = i / K;
       const int kk = i - n * K;

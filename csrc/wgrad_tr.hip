@@ -30,21 +30,6 @@ namespace {
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4_vs __attribute__((__vector_size__(8)));
 
-struct FastDiv {  // q = n / d for 0 <= n < 2^31: (mulhi(n, mul) + n) >> shr
-  unsigned mul, shr;
-};
-
-FastDiv make_fastdiv(unsigned d) {
-  unsigned l = 0;
-  while ((1u << l) < d) ++l;
-  FastDiv f;
-  f.mul = (unsigned)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
-  f.shr = l;
-  return f;
-}
-
-__device__ __forceinline__ unsigned fdiv(unsigned n, FastDiv f) { return (__umulhi(n, f.mul) + n) >> f.shr; }
-
 __device__ __forceinline__ bf16x4 tr_read(const bf16* p) {
   auto* lp = (__attribute__((address_space(3))) bf16*)(const_cast<bf16*>(p));
   const bf16x4_vs v =

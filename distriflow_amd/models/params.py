@@ -178,10 +178,16 @@ class ParamStore:
                 nblocks = (s.numel + SGD_ELEMS_PER_BLOCK - 1) // SGD_ELEMS_PER_BLOCK
                 if s.kind == "vector":
                     N, T, Ci = 1, 1, s.numel
+                # tile mode (csrc/optim.hip, pad bit 28): plain layouts with a dgrad copy get 32x32 tiles
+                # whose transposed copy is written through LDS
+                tile = s.kind == "matrix" and s.needs_dgrad and not s.row_pad and not s.t_pair
+                if tile:
+                    nblocks = ((N + 31) // 32) * ((T * Ci + 31) // 32)
+                assert s.row_cp < (1 << 12), "row-segment channel stride must fit 12 bits"
                 descs.append((self.offsets[s.name], bf_off, bft_off, s.numel, N, T, Ci, block,
                               0 if s.trainable else 1,
                               (s.row_pad | (s.row_cp << 16) | ((1 << 30) if s.row_pair else 0)
-                               | ((1 << 29) if s.t_pair else 0))
+                               | ((1 << 29) if s.t_pair else 0) | ((1 << 28) if tile else 0))
                               if s.kind == "matrix" else 0))
                 block += nblocks
         self.wbf = torch.zeros(max(boff, 8), dtype=torch.bfloat16, device=self.device)

@@ -50,8 +50,10 @@ def test_model_gradients_match_cpu(name, B, min_cos):
     assert not bad, bad
 
 
-def test_sgd_step_and_bf16_copies():
-    g = build_model("lenet5", device="cuda", seed=1)
+@pytest.mark.parametrize("name", ["lenet5", "keras_cnn", "resnet18_cifar"])
+def test_sgd_step_and_bf16_copies(name):
+    """fp32 update + the bf16 compute copies (row-segment, pair, tile-mode transposed layouts)."""
+    g = build_model(name, device="cuda", seed=1)
     st = g.store
     st.grad.normal_()
     before = st.master.clone()
