@@ -39,6 +39,8 @@ def main():
                     help="hipGraph mode: full = whole step incl. bucketed RCCL all-reduces (falls back to split "
                          "= captured compute + SGD with an eager all-reduce between, then none, if capture fails)")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--allreduce", default="auto", choices=["auto", "p2p", "rccl"],
+                    help="gradient all-reduce: one-shot xGMI kernel for small buckets (auto/p2p) or RCCL only")
     ap.add_argument("--json-extra", action="store_true", help="add diagnostic fields")
     args = ap.parse_args()
 
@@ -63,7 +65,8 @@ def main():
         data, labels = synthetic_cifar10(50000, seed=rank, device=dev)
     else:
         data, labels = synthetic_mnist(60000, seed=rank, device=dev)
-    trainer = DataParallelTrainer(net, lr=args.lr, graph=args.graph, overlap=not args.no_overlap)
+    trainer = DataParallelTrainer(net, lr=args.lr, graph=args.graph, overlap=not args.no_overlap,
+                                  allreduce=args.allreduce)
     trainer.bind_dataset(data, labels, B, scale=1.0 / 255.0)
     total = args.warmup + args.steps
     perm = epoch_permutations(data.shape[0], B, total, dev, seed=rank)
@@ -84,6 +87,7 @@ def main():
         dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    trainer.check_comm()  # sticky peer-timeout flag of the one-shot all-reduce (never set on a healthy run)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -104,7 +108,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
             "dtype": "bf16" if dev.type == "cuda" else "fp32",
-            "data": "synthetic (MNIST-shaped 60000x28x28x1 uint8, HBM resident), random-init weights",
+            "data": ("synthetic (CIFAR-10-shaped 50000x32x32x3 uint8" if args.model == "resnet18_cifar" else
+                     "synthetic (MNIST-shaped 60000x28x28x1 uint8") + ", HBM resident), random-init weights",
             "config": {
                 "model": args.model,
                 "global_batch": B * world,
@@ -113,6 +118,7 @@ def main():
                 "parallelism": f"dp{world}",
                 "optimizer": "sgd",
                 "graph": trainer.graph_mode,
+                "allreduce": trainer.allreduce_path if world > 1 else None,
                 "params": net.num_params(),
             },
         }

@@ -668,6 +668,100 @@ bool convpool_supported_py(int64_t H, int64_t W, int64_t C, int64_t KH, int64_t 
   return dfa::convpool_supported(H, W, C, KH, KW, pad, N);
 }
 
+// One-shot xGMI all-reduce communicator (csrc/allreduce_p2p.hip): owns this rank's IPC-exported
+// flag+staging buffer and the peer mappings.  Handles are exchanged by the Python side over the
+// process group (parallel/p2p.py); every launch goes onto PyTorch's current stream (graph capturable).
+class P2PComm {
+ public:
+  P2PComm(int64_t rank, int64_t world, int64_t max_floats, double timeout_s) : rank_((int)rank), world_((int)world) {
+    TORCH_CHECK(world >= 1 && world <= dfa::kP2PMaxRanks, "p2p: world must be in [1, 8]");
+    TORCH_CHECK(rank >= 0 && rank < world, "p2p: bad rank");
+    TORCH_CHECK(max_floats > 0 && max_floats <= (int64_t(1) << 28), "p2p: max_floats out of range");
+    check_hip(hipGetDevice(&dev_), "p2p getDevice");
+    max_blocks_ = (int)((max_floats + dfa::kP2PChunk - 1) / dfa::kP2PChunk);
+    half_ = (int64_t)max_blocks_ * dfa::kP2PChunk;
+    flag_bytes_ = ((int64_t)max_blocks_ * dfa::kP2PMaxRanks * 4 + 4095) / 4096 * 4096;
+    bytes_ = flag_bytes_ + 2 * half_ * 4;
+    void* p = nullptr;
+    hipError_t e = hipExtMallocWithFlags(&p, (size_t)bytes_, hipDeviceMallocUncached);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      check_hip(hipExtMallocWithFlags(&p, (size_t)bytes_, hipDeviceMallocFinegrained), "p2p alloc");
+    }
+    local_ = (char*)p;
+    check_hip(hipMemset(local_, 0, (size_t)bytes_), "p2p memset");
+    check_hip(hipMalloc((void**)&epochs_, (size_t)max_blocks_ * 4), "p2p epochs alloc");
+    check_hip(hipMemset(epochs_, 0, (size_t)max_blocks_ * 4), "p2p epochs memset");
+    check_hip(hipMalloc((void**)&err_, 4), "p2p err alloc");
+    check_hip(hipMemset(err_, 0, 4), "p2p err memset");
+    check_hip(hipDeviceSynchronize(), "p2p init sync");
+    timeout_ticks_ = (int64_t)(timeout_s * 1e8);  // wall_clock64 runs at 100 MHz
+    for (auto& b : bases_) b = nullptr;
+    bases_[rank_] = local_;
+  }
+  ~P2PComm() {
+    for (int r = 0; r < world_; ++r)
+      if (r != rank_ && bases_[r]) (void)hipIpcCloseMemHandle(bases_[r]);
+    if (local_) (void)hipFree(local_);
+    if (epochs_) (void)hipFree(epochs_);
+    if (err_) (void)hipFree(err_);
+  }
+  py::bytes handle() const {
+    hipIpcMemHandle_t h;
+    check_hip(hipIpcGetMemHandle(&h, local_), "hipIpcGetMemHandle");
+    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  }
+  void open(const std::vector<std::string>& handles) {
+    TORCH_CHECK((int)handles.size() == world_, "p2p: need one handle per rank");
+    for (int r = 0; r < world_; ++r) {
+      if (r == rank_) continue;
+      TORCH_CHECK(handles[r].size() == sizeof(hipIpcMemHandle_t), "p2p: bad handle size");
+      hipIpcMemHandle_t h;
+      memcpy(&h, handles[r].data(), sizeof(h));
+      void* p = nullptr;
+      check_hip(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+      bases_[r] = (char*)p;
+    }
+    opened_ = true;
+  }
+  void allreduce(torch::Tensor t, double scale) {
+    need(t, at::kFloat, "p2p tensor");
+    TORCH_CHECK(opened_ || world_ == 1, "p2p: open() the peer handles first");
+    TORCH_CHECK(t.get_device() == dev_, "p2p: tensor on the wrong device");
+    TORCH_CHECK(t.numel() <= half_, "p2p: tensor larger than the staging buffer");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "p2p: tensor must be 16-byte aligned");
+    dfa::P2PArgs a{};
+    for (int r = 0; r < dfa::kP2PMaxRanks; ++r) a.bases[r] = bases_[r];
+    a.data = t.data_ptr<float>();
+    a.n = t.numel();
+    a.epochs = epochs_;
+    a.err = err_;
+    a.flag_bytes = flag_bytes_;
+    a.half_floats = half_;
+    a.timeout_ticks = timeout_ticks_;
+    a.rank = rank_;
+    a.world = world_;
+    a.max_blocks = max_blocks_;
+    a.scale = (float)scale;
+    check_hip(dfa::p2p_allreduce(a, cur_stream()), "p2p_allreduce");
+  }
+  int64_t error() const {
+    int v = 0;
+    check_hip(hipMemcpy(&v, err_, 4, hipMemcpyDeviceToHost), "p2p error readback");
+    return v;
+  }
+  int64_t max_floats() const { return half_; }
+
+ private:
+  int rank_, world_, dev_ = 0, max_blocks_ = 0;
+  int64_t half_ = 0, flag_bytes_ = 0, bytes_ = 0, timeout_ticks_ = 0;
+  char* local_ = nullptr;
+  char* bases_[dfa::kP2PMaxRanks];
+  unsigned* epochs_ = nullptr;
+  int* err_ = nullptr;
+  bool opened_ = false;
+};
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -725,5 +819,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("convpool_supported", &convpool_supported_py);
   m.def("head_train", &head_train_py, "fused dense head: forward + softmax-CE + backward (2 launches)");
   m.def("gather_labels", &gather_labels_py);
+  py::class_<P2PComm>(m, "P2PComm", "one-shot xGMI all-reduce over IPC-mapped peer buffers")
+      .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("world"), py::arg("max_floats"),
+           py::arg("timeout_s") = 2.0)
+      .def("handle", &P2PComm::handle)
+      .def("open", &P2PComm::open)
+      .def("allreduce", &P2PComm::allreduce, py::arg("t"), py::arg("scale") = 1.0)
+      .def("error", &P2PComm::error)
+      .def_property_readonly("max_floats", &P2PComm::max_floats);
   dfa::register_runtime(m);
 }

@@ -177,4 +177,22 @@ hipError_t convpool_dgrad(const bf16* dp, const uint8_t* code, const bf16* wt, b
 hipError_t slab_reduce(const float* partial, float* gw, float* gb, int N, int K, int Kt, int S, float scale,
                        hipStream_t st);
 
+
+// One-shot xGMI all-reduce (csrc/allreduce_p2p.hip).  Each rank's IPC buffer: flags
+// [max_blocks][kP2PMaxRanks] u32 (flag_bytes, 4 KB aligned) followed by two staging halves of
+// half_floats fp32 each.  Workgroup b always owns elements [b*kP2PChunk, (b+1)*kP2PChunk).
+constexpr int kP2PMaxRanks = 8;
+constexpr int kP2PChunk = 2048;
+struct P2PArgs {
+  char* bases[kP2PMaxRanks];  // bases[r] = rank r's buffer mapped into this process (bases[rank] local)
+  float* data;                // in/out fp32 [n] (this rank's gradient, replaced by the sum * scale)
+  long long n;
+  unsigned* epochs;           // [max_blocks] per-block call counters (local)
+  int* err;                   // sticky error word (local): bit 0 = a peer flag timed out
+  long long flag_bytes, half_floats, timeout_ticks;  // timeout in wall_clock64 ticks (100 MHz)
+  int rank, world, max_blocks;
+  float scale;
+};
+hipError_t p2p_allreduce(const P2PArgs& a, hipStream_t st);
+
 }  // namespace dfa

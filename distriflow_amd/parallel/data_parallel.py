@@ -31,7 +31,7 @@ from .. import ops
 class DataParallelTrainer:
     def __init__(self, net, lr: float = 0.001, momentum: float = 0.0, weight_decay: float = 0.0,
                  group=None, bucket_mb: Optional[float] = None, overlap: bool = True, graph: str = "full",
-                 broadcast_init: bool = True):
+                 broadcast_init: bool = True, allreduce: str = "auto", p2p_max_mb: float = 4.0):
         self.net = net
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -47,6 +47,7 @@ class DataParallelTrainer:
         else:
             self.bucket_bytes = int(bucket_mb * (1 << 20))
         self._build_buckets()
+        self._setup_p2p(allreduce, int(p2p_max_mb * (1 << 20)))
         self._works = []
         self._graph = None
         self._graph_B = None
@@ -77,12 +78,54 @@ class DataParallelTrainer:
                 hi = lo
         self._trigger = {b[0]: b for b in self.buckets}
 
+    def _setup_p2p(self, mode: str, limit_bytes: int):
+        """Pick the transport per bucket: the one-shot xGMI kernel (parallel/p2p.py) for buckets up to
+        ``limit_bytes``, RCCL above.  ``mode``: auto (p2p when usable) | p2p (required) | rccl."""
+        self.p2p = None
+        self.p2p_limit = limit_bytes
+        self.p2p_reason = "single rank" if self.world == 1 else ("cpu" if not self.net.is_gpu else "")
+        if mode not in ("auto", "p2p", "rccl"):
+            raise ValueError(f"allreduce must be auto|p2p|rccl, got {mode!r}")
+        if self.world == 1 or not self.net.is_gpu or mode == "rccl":
+            self.p2p_reason = self.p2p_reason or "disabled"
+            return
+        sizes = [(hi - lo) * 4 for _, lo, hi in self.buckets] + [self.net.store.total * 4]
+        small = [s for s in sizes if s <= limit_bytes]
+        if not small:
+            self.p2p_reason = "all buckets above the p2p limit"
+            return
+        from .p2p import make_p2p
+
+        self.p2p = make_p2p(self.group, max_bytes=max(small))
+        if self.p2p is None:
+            self.p2p_reason = "unavailable (self-test or IPC failed, or DISTRIFLOW_ALLREDUCE=rccl)"
+            if mode == "p2p":
+                raise RuntimeError("allreduce='p2p' requested but the one-shot path is unusable")
+        else:
+            self._comm_stream = torch.cuda.Stream(device=self.net.device)
+            self._p2p_pending = False
+
+    def _reduce(self, t: torch.Tensor, async_op: bool):
+        if self.p2p is not None and t.numel() * 4 <= self.p2p_limit:
+            if async_op:  # side stream: overlaps the rest of backward, joined in _allreduce_all
+                cur = torch.cuda.current_stream(self.net.device)
+                self._comm_stream.wait_stream(cur)
+                with torch.cuda.stream(self._comm_stream):
+                    self.p2p.all_reduce(t)
+                self._p2p_pending = True
+            else:
+                self.p2p.all_reduce(t)
+            return
+        w = dist.all_reduce(t, group=self.group, async_op=async_op)
+        if async_op:
+            self._works.append(w)
+
     def _grad_ready(self, layer_idx: int):
         b = self._trigger.get(layer_idx)
         if b is None or self.world == 1:
             return
         _, lo, hi = b
-        self._works.append(dist.all_reduce(self.net.store.grad[lo:hi], group=self.group, async_op=True))
+        self._reduce(self.net.store.grad[lo:hi], async_op=True)
 
     def _allreduce_all(self):
         if self.world == 1:
@@ -90,9 +133,22 @@ class DataParallelTrainer:
         if self.overlap:
             for w in self._works:
                 w.wait()
+            if self.p2p is not None and self._p2p_pending:
+                torch.cuda.current_stream(self.net.device).wait_stream(self._comm_stream)
+                self._p2p_pending = False
         else:
-            dist.all_reduce(self.net.store.grad, group=self.group)
+            self._reduce(self.net.store.grad, async_op=False)
         self._works = []
+
+    def check_comm(self):
+        """Raise if the one-shot all-reduce recorded a peer timeout (call outside the timed loop)."""
+        if self.p2p is not None:
+            self.p2p.check()
+
+    @property
+    def allreduce_path(self) -> str:
+        return "p2p+rccl" if self.p2p is not None and any(
+            (hi - lo) * 4 > self.p2p_limit for _, lo, hi in self.buckets) else ("p2p" if self.p2p else "rccl")
 
     # ------------------------------------------------------------------ one step
     def _step_body(self, x, y):
@@ -238,7 +294,7 @@ class DataParallelTrainer:
         g.replay()
         if g2 is not None:
             if self.world > 1:
-                dist.all_reduce(self.net.store.grad, group=self.group)
+                self._reduce(self.net.store.grad, async_op=False)
             g2.replay()
         return self.stats
 
