@@ -41,6 +41,10 @@ def main():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--allreduce", default="auto", choices=["auto", "p2p", "rccl"],
                     help="gradient all-reduce: one-shot xGMI kernel for small buckets (auto/p2p) or RCCL only")
+    ap.add_argument("--mode", default="sync", choices=["sync", "async"],
+                    help="sync = all-reduce data parallel (headline); async = device-resident bounded-staleness "
+                         "parameter server on rank 0 (parallel/async_ps.py)")
+    ap.add_argument("--max-staleness", type=int, default=4)
     ap.add_argument("--json-extra", action="store_true", help="add diagnostic fields")
     args = ap.parse_args()
 
@@ -65,14 +69,20 @@ def main():
         data, labels = synthetic_cifar10(50000, seed=rank, device=dev)
     else:
         data, labels = synthetic_mnist(60000, seed=rank, device=dev)
-    trainer = DataParallelTrainer(net, lr=args.lr, graph=args.graph, overlap=not args.no_overlap,
-                                  allreduce=args.allreduce)
-    trainer.bind_dataset(data, labels, B, scale=1.0 / 255.0)
     total = args.warmup + args.steps
-    perm = epoch_permutations(data.shape[0], B, total, dev, seed=rank)
+    if args.mode == "async":
+        from distriflow_amd.parallel.async_ps import AsyncPSTrainer
 
-    # device-resident batch schedule: each step's optimizer launch stages the next step's indices
-    trainer.bind_index_stream(perm)
+        trainer = AsyncPSTrainer(net, lr=args.lr, max_staleness=args.max_staleness, graph=args.graph)
+        trainer.bind_dataset(data, labels, B, scale=1.0 / 255.0)
+        # one global FCFS microbatch table; ranks claim ids from the shared counter
+        trainer.bind_schedule(epoch_permutations(data.shape[0], B, max(total, data.shape[0] // B), dev, seed=0))
+    else:
+        trainer = DataParallelTrainer(net, lr=args.lr, graph=args.graph, overlap=not args.no_overlap,
+                                      allreduce=args.allreduce)
+        trainer.bind_dataset(data, labels, B, scale=1.0 / 255.0)
+        # device-resident batch schedule: each step's optimizer launch stages the next step's indices
+        trainer.bind_index_stream(epoch_permutations(data.shape[0], B, total, dev, seed=rank))
     for i in range(args.warmup):
         trainer.step()
     sync()
@@ -115,13 +125,15 @@ def main():
                 "global_batch": B * world,
                 "per_gpu_batch": B,
                 "seq_len": None,
-                "parallelism": f"dp{world}",
+                "parallelism": f"dp{world}" if args.mode == "sync" else f"async-ps{world}",
                 "optimizer": "sgd",
                 "graph": trainer.graph_mode,
                 "allreduce": trainer.allreduce_path if world > 1 else None,
                 "params": net.num_params(),
             },
         }
+        if args.mode == "async":
+            out["async"] = dict(trainer.ps_stats(), max_staleness_bound=args.max_staleness)
         if args.json_extra:
             out["extra"] = {"final_loss": loss, "train_tflops": value * net.flops_per_example() / 1e12,
                             "capture_error": getattr(trainer, "capture_error", None)}

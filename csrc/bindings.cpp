@@ -762,6 +762,123 @@ class P2PComm {
   bool opened_ = false;
 };
 
+// Device-resident async parameter server (csrc/async_ps.hip): the server rank owns the shared
+// seqlock / batch counter / fp32 master buffer (IPC exported); every rank maps it.
+class PSComm {
+ public:
+  PSComm(int64_t rank, int64_t server_rank, int64_t n, double timeout_s)
+      : rank_((int)rank), server_((int)server_rank), n_(n) {
+    TORCH_CHECK(n > 0 && n % 4 == 0, "ps: n must be a positive multiple of 4");
+    check_hip(hipGetDevice(&dev_), "ps getDevice");
+    if (rank_ == server_) {
+      void* p = nullptr;
+      const size_t bytes = 256 + (size_t)n * 4;
+      hipError_t e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        check_hip(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained), "ps alloc");
+      }
+      shared_ = (char*)p;
+      check_hip(hipMemset(shared_, 0, bytes), "ps memset");
+    }
+    check_hip(hipMalloc((void**)&local_, 256), "ps local alloc");
+    check_hip(hipMemset(local_, 0, 256), "ps local memset");
+    check_hip(hipDeviceSynchronize(), "ps init sync");
+    timeout_ticks_ = (int64_t)(timeout_s * 1e8);
+  }
+  ~PSComm() {
+    if (shared_ && rank_ != server_) (void)hipIpcCloseMemHandle(shared_);
+    if (shared_ && rank_ == server_) (void)hipFree(shared_);
+    if (local_) (void)hipFree(local_);
+  }
+  py::bytes handle() const {
+    TORCH_CHECK(rank_ == server_, "ps: only the server rank exports the shared buffer");
+    hipIpcMemHandle_t h;
+    check_hip(hipIpcGetMemHandle(&h, shared_), "hipIpcGetMemHandle");
+    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  }
+  void open(const std::string& handle) {
+    if (rank_ == server_) return;
+    TORCH_CHECK(handle.size() == sizeof(hipIpcMemHandle_t), "ps: bad handle size");
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle.data(), sizeof(h));
+    void* p = nullptr;
+    check_hip(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    shared_ = (char*)p;
+  }
+  // server only: seed the shared master (before any worker pulls)
+  void init_master(torch::Tensor w) {
+    TORCH_CHECK(rank_ == server_ && shared_, "ps: init_master on the server rank");
+    need(w, at::kFloat, "ps master");
+    TORCH_CHECK(w.numel() == n_, "ps: master size mismatch");
+    check_hip(hipMemcpy(shared_ + 256, w.data_ptr(), (size_t)n_ * 4, hipMemcpyDeviceToDevice), "ps init copy");
+    check_hip(hipDeviceSynchronize(), "ps init sync");
+  }
+  void fetch_pull(torch::Tensor w, c10::optional<torch::Tensor> perm, c10::optional<torch::Tensor> idx) {
+    dfa::PSArgs a = args();
+    need(w, at::kFloat, "ps local master");
+    TORCH_CHECK(w.numel() == n_ && w.get_device() == dev_, "ps: local master mismatch");
+    a.w = w.data_ptr<float>();
+    if (perm.has_value() && perm->defined()) {
+      need(*perm, at::kLong, "ps perm");
+      TORCH_CHECK(idx.has_value() && idx->defined(), "ps: idx required with perm");
+      need(*idx, at::kLong, "ps idx");
+      TORCH_CHECK(perm->dim() == 2 && perm->size(1) == idx->numel(), "ps: perm must be [nbatches][B]");
+      a.perm = reinterpret_cast<const long long*>(perm->data_ptr());
+      a.idx = reinterpret_cast<long long*>(idx->data_ptr());
+      a.nbatches = perm->size(0);
+      a.B = (int)idx->numel();
+    }
+    check_hip(dfa::ps_fetch_pull(a, cur_stream()), "ps_fetch_pull");
+  }
+  void apply(torch::Tensor g, double lr, int64_t max_stale) {
+    dfa::PSArgs a = args();
+    need(g, at::kFloat, "ps grad");
+    TORCH_CHECK(g.numel() == n_ && g.get_device() == dev_, "ps: gradient mismatch");
+    a.g = g.data_ptr<float>();
+    a.lr = (float)lr;
+    a.max_stale = (int)max_stale;
+    check_hip(dfa::ps_apply(a, cur_stream()), "ps_apply");
+  }
+  // [accepted, rejected, sum staleness, max staleness, torn retries, err, version, batches claimed]
+  std::vector<int64_t> stats() const {
+    unsigned long long h[8] = {0};
+    check_hip(hipMemcpy(h, local_ + 64, 48, hipMemcpyDeviceToHost), "ps stats");
+    unsigned seq = 0;
+    unsigned long long ctr = 0;
+    check_hip(hipMemcpy(&seq, shared_, 4, hipMemcpyDeviceToHost), "ps seq");
+    check_hip(hipMemcpy(&ctr, shared_ + 16, 8, hipMemcpyDeviceToHost), "ps ctr");
+    return {(int64_t)h[0], (int64_t)h[1], (int64_t)h[2], (int64_t)h[3], (int64_t)h[4], (int64_t)h[5],
+            (int64_t)(seq >> 1), (int64_t)ctr};
+  }
+  void copy_master(torch::Tensor dst) const {
+    need(dst, at::kFloat, "ps dst");
+    TORCH_CHECK(dst.numel() == n_, "ps: dst size mismatch");
+    check_hip(hipMemcpyAsync(dst.data_ptr(), shared_ + 256, (size_t)n_ * 4, hipMemcpyDeviceToDevice, cur_stream()),
+              "ps copy_master");
+  }
+
+ private:
+  dfa::PSArgs args() const {
+    TORCH_CHECK(shared_ != nullptr, "ps: open() the server handle first");
+    dfa::PSArgs a{};
+    a.seq = reinterpret_cast<unsigned*>(shared_);
+    a.batch_ctr = reinterpret_cast<unsigned long long*>(shared_ + 16);
+    a.ps_w = reinterpret_cast<float*>(shared_ + 256);
+    a.n = n_;
+    a.vpulled = reinterpret_cast<unsigned*>(local_);
+    a.bid_out = reinterpret_cast<long long*>(local_ + 8);
+    a.stats = reinterpret_cast<unsigned long long*>(local_ + 64);
+    a.timeout_ticks = timeout_ticks_;
+    a.max_stale = -1;
+    return a;
+  }
+  int rank_, server_, dev_ = 0;
+  int64_t n_, timeout_ticks_ = 0;
+  char* shared_ = nullptr;
+  char* local_ = nullptr;
+};
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -827,5 +944,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("allreduce", &P2PComm::allreduce, py::arg("t"), py::arg("scale") = 1.0)
       .def("error", &P2PComm::error)
       .def_property_readonly("max_floats", &P2PComm::max_floats);
+  py::class_<PSComm>(m, "PSComm", "device-resident bounded-staleness parameter server over IPC/xGMI")
+      .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("server_rank"), py::arg("n"),
+           py::arg("timeout_s") = 30.0)
+      .def("handle", &PSComm::handle)
+      .def("open", &PSComm::open)
+      .def("init_master", &PSComm::init_master)
+      .def("fetch_pull", &PSComm::fetch_pull, py::arg("w"), py::arg("perm") = py::none(), py::arg("idx") = py::none())
+      .def("apply", &PSComm::apply, py::arg("g"), py::arg("lr"), py::arg("max_stale"))
+      .def("stats", &PSComm::stats)
+      .def("copy_master", &PSComm::copy_master);
   dfa::register_runtime(m);
 }

@@ -195,4 +195,26 @@ struct P2PArgs {
 };
 hipError_t p2p_allreduce(const P2PArgs& a, hipStream_t st);
 
+
+// Device-resident async parameter server (csrc/async_ps.hip).  seq / batch_ctr / ps_w live in the
+// server rank's IPC buffer (mapped into every rank); everything else is local.
+struct PSArgs {
+  unsigned* seq;                // seqlock word: odd = writer active, version = seq / 2
+  unsigned long long* batch_ctr;  // FCFS microbatch counter
+  float* ps_w;                  // shared fp32 master [n]
+  float* w;                     // local fp32 master [n] (pull destination)
+  const float* g;               // local fp32 gradient [n]
+  long long n;
+  unsigned* vpulled;            // local: version of the last pulled snapshot
+  unsigned long long* stats;    // local [8]: accepted, rejected, sum staleness, max staleness, torn retries, err
+  const long long* perm;        // [nbatches][B] example ids (nullptr: no index staging)
+  long long* idx;               // [B] staged ids of the claimed microbatch
+  long long* bid_out;           // local: id of the claimed microbatch
+  long long nbatches, timeout_ticks;
+  int B, max_stale;
+  float lr;
+};
+hipError_t ps_fetch_pull(const PSArgs& a, hipStream_t st);
+hipError_t ps_apply(const PSArgs& a, hipStream_t st);
+
 }  // namespace dfa

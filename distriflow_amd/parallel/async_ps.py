@@ -1,0 +1,120 @@
+"""Asynchronous SGD against a device-resident, bounded-staleness parameter server (BASELINE.json configs[2]).
+
+Reference: ``AsynchronousSGDServer`` keeps the model, dispenses microbatches first-come-first-serve
+and applies every uploaded gradient on arrival; ``AsynchronousSGDClient`` downloads weights plus a
+batch, computes a gradient and uploads it
+(/root/reference/src/server/asynchronousSGD_server.ts:45-108,
+/root/reference/src/client/asynchronousSGD_client.ts:16-84).  The README's ``maximumStaleness``
+(/root/reference/README.md:27) is the intended bound and is enforced here.
+
+This is the throughput path.  The message-level roles (``parallel/server.py``/``worker.py``) keep
+the reference's protocol and callbacks.  On one MI355X node the server state is a single IPC-exported
+buffer in the server rank's HBM: a seqlock version word, the FCFS microbatch counter and the fp32
+master weights.  Every rank maps it over xGMI (csrc/async_ps.hip).  A worker step is a bare hipGraph
+replay of four device stages, with no host round trip:
+
+  1. ``ps_fetch_pull``: claim the next microbatch id (remote atomic), stage its example indices, and
+     copy a consistent weight snapshot together with its version;
+  2. re-emit the bf16 compute copies;
+  3. forward, loss and backward (the same fused kernels as the synchronous trainer);
+  4. ``ps_apply``: under the writer lock, reject the gradient if ``version_now - version_pulled >
+     max_staleness``, otherwise ``w -= lr * g`` on the shared master and publish ``version + 1``.
+
+Ranks never wait for each other except for the short writer lock.  A slow rank only makes its own
+gradients staler, which the bound then rejects.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import native
+from .data_parallel import DataParallelTrainer
+
+
+class AsyncPSTrainer(DataParallelTrainer):
+    def __init__(self, net, lr: float = 0.001, max_staleness: int = 4, group=None, server_rank: int = 0,
+                 graph: str = "full", timeout_s: float = 30.0):
+        if not net.is_gpu:
+            raise RuntimeError("AsyncPSTrainer is the GPU path; use AsynchronousSGDServer/Client on CPU")
+        super().__init__(net, lr=lr, group=group, overlap=False, graph="full" if graph == "split" else graph,
+                         broadcast_init=True, allreduce="rccl")
+        self.max_staleness = int(max_staleness)
+        self.server_rank = server_rank
+        self.ps = native.require().PSComm(self.rank, server_rank, net.store.total, timeout_s)
+        objs = [self.ps.handle() if self.rank == server_rank else b""]
+        if self.world > 1:
+            dist.broadcast_object_list(objs, src=server_rank, group=group)
+        self.ps.open(objs[0])
+        if self.rank == server_rank:
+            self.ps.init_master(net.store.master)
+        if self.world > 1:
+            dist.barrier(group=group)
+        self._perm = None
+
+    # ------------------------------------------------------------------ schedule
+    def bind_schedule(self, perm: torch.Tensor):
+        """Global FCFS microbatch table ``perm`` [nbatches][B] (identical on every rank): microbatch id
+        ``b`` (claimed from the shared counter) trains on rows ``perm[b % nbatches]``."""
+        if perm.dim() != 2 or perm.shape[1] != self.B:
+            raise ValueError(f"schedule must be [nbatches][{self.B}]")
+        self._perm = perm.to(self.idx.device, torch.int64).contiguous()
+        self._graph = None
+
+    # ------------------------------------------------------------------ one step
+    def _gather(self):
+        self.ps.fetch_pull(self.net.store.master, self._perm, self.idx)
+        self.net.store.refresh_compute()
+        super()._gather()
+
+    def _step_body(self, x, y):
+        stats = self.net.compute_gradients(x, y)
+        self.ps.apply(self.net.store.grad, self.lr, self.max_staleness)
+        return stats
+
+    def _capture_with_fallback(self):
+        try:
+            self._capture()
+        except Exception as e:
+            torch.cuda.synchronize(self.net.device)
+            self.capture_error = repr(e)
+            self._graph = None
+            self.graph_mode = "none"
+            self._gather()
+            self._last_eager = self._step_body(self.xb, self.yb)
+
+    def step(self):
+        if self._perm is None:
+            raise RuntimeError("bind_schedule() first")
+        self.steps += 1
+        if self.graph_mode == "none":
+            self._gather()
+            return self._step_body(self.xb, self.yb)
+        if self._graph is None:
+            self._capture_with_fallback()
+            if self._graph is None:
+                return self._last_eager
+        return self._replay()
+
+    # ------------------------------------------------------------------ state
+    def ps_stats(self) -> dict:
+        acc, rej, ssum, smax, torn, err, version, claimed = self.ps.stats()
+        return {"accepted": acc, "rejected": rej, "mean_staleness": ssum / acc if acc else 0.0,
+                "max_staleness": smax, "torn_retries": torn, "error": err, "version": version,
+                "batches_claimed": claimed}
+
+    def check_comm(self):
+        err = self.ps.stats()[5]
+        if err:
+            raise RuntimeError(f"async PS: device wait timed out (error bits {err:#x})")
+
+    def pull_master(self, dst: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Copy the shared master into ``dst`` (default: this rank's store, compute copies refreshed)."""
+        if dst is None:
+            self.ps.copy_master(self.net.store.master)
+            self.net.store.refresh_compute()
+            return self.net.store.master
+        self.ps.copy_master(dst)
+        return dst

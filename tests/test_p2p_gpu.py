@@ -119,15 +119,17 @@ def _trainer_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.timeout(180)
-def test_p2p_allreduce_two_procs_one_gpu():
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world", [2, 8])
+def test_p2p_allreduce_procs_sharing_one_gpu(world):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_primitive_worker, args=(2, _port(), d), nprocs=2, join=True)
-        r = [torch.load(os.path.join(d, f"r{i}.pt"), weights_only=True) for i in range(2)]
-    assert r[0]["ok"] and r[1]["ok"], (r[0]["reason"], r[1]["reason"])
+        mp.spawn(_primitive_worker, args=(world, _port(), d), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"r{i}.pt"), weights_only=True) for i in range(world)]
+    assert all(x["ok"] for x in r), [x["reason"] for x in r]
     for x in r:
-        assert x["eager_err"] < 1e-5 and x["graph_err"] < 1e-5 and x["dev_error"] == 0
-    assert torch.equal(r[0]["eager_bits"], r[1]["eager_bits"])  # rank-order sums: bit-identical replicas
+        assert x["eager_err"] < 1e-4 and x["graph_err"] < 1e-4 and x["dev_error"] == 0
+    for x in r[1:]:
+        assert torch.equal(r[0]["eager_bits"], x["eager_bits"])  # rank-order sums: bit-identical replicas
 
 
 @pytest.mark.timeout(120)
