@@ -45,6 +45,9 @@ def main():
                     help="sync = all-reduce data parallel (headline); async = device-resident bounded-staleness "
                          "parameter server on rank 0 (parallel/async_ps.py)")
     ap.add_argument("--max-staleness", type=int, default=4)
+    ap.add_argument("--async-steps", type=int, default=None,
+                    help="after the sync measurement, also time this many steps of the async parameter-server "
+                         "engine and report the async speedup (default: --steps; 0 disables)")
     ap.add_argument("--json-extra", action="store_true", help="add diagnostic fields")
     args = ap.parse_args()
 
@@ -70,41 +73,65 @@ def main():
     else:
         data, labels = synthetic_mnist(60000, seed=rank, device=dev)
     total = args.warmup + args.steps
-    if args.mode == "async":
-        from distriflow_amd.parallel.async_ps import AsyncPSTrainer
 
-        trainer = AsyncPSTrainer(net, lr=args.lr, max_staleness=args.max_staleness, graph=args.graph)
-        trainer.bind_dataset(data, labels, B, scale=1.0 / 255.0)
-        # one global FCFS microbatch table; ranks claim ids from the shared counter
-        trainer.bind_schedule(epoch_permutations(data.shape[0], B, max(total, data.shape[0] // B), dev, seed=0))
-    else:
-        trainer = DataParallelTrainer(net, lr=args.lr, graph=args.graph, overlap=not args.no_overlap,
-                                      allreduce=args.allreduce)
-        trainer.bind_dataset(data, labels, B, scale=1.0 / 255.0)
-        # device-resident batch schedule: each step's optimizer launch stages the next step's indices
-        trainer.bind_index_stream(epoch_permutations(data.shape[0], B, total, dev, seed=rank))
-    for i in range(args.warmup):
-        trainer.step()
-    sync()
-    if world > 1:
-        dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    for i in range(args.warmup, total):
-        st = trainer.step()
-    sync()
-    if world > 1:
-        dist.barrier()
-    sync()
-    elapsed = time.perf_counter() - t0
-    trainer.check_comm()  # sticky peer-timeout flag of the one-shot all-reduce (never set on a healthy run)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def make_trainer(mode, net):
+        if mode == "async":
+            from distriflow_amd.parallel.async_ps import AsyncPSTrainer
+
+            tr = AsyncPSTrainer(net, lr=args.lr, max_staleness=args.max_staleness, graph=args.graph)
+            tr.bind_dataset(data, labels, B, scale=1.0 / 255.0)
+            # one global FCFS microbatch table; ranks claim ids from the shared counter
+            tr.bind_schedule(epoch_permutations(data.shape[0], B, max(total, data.shape[0] // B), dev, seed=0))
+        else:
+            tr = DataParallelTrainer(net, lr=args.lr, graph=args.graph, overlap=not args.no_overlap,
+                                     allreduce=args.allreduce)
+            tr.bind_dataset(data, labels, B, scale=1.0 / 255.0)
+            # device-resident batch schedule: each step's optimizer launch stages the next step's indices
+            tr.bind_index_stream(epoch_permutations(data.shape[0], B, total, dev, seed=rank))
+        return tr
+
+    def timed(tr, steps):
+        """W untimed warm-up steps, then ``steps`` timed ones between barrier + device syncs; max over ranks."""
+        for _ in range(args.warmup):
+            tr.step()
+        sync()
+        if world > 1:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            st = tr.step()
+        sync()
+        if world > 1:
+            dist.barrier()
+        sync()
+        el = time.perf_counter() - t0
+        tr.check_comm()  # sticky device timeout flags (never set on a healthy run)
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, st
+
+    trainer = make_trainer(args.mode, net)
+    elapsed, st = timed(trainer, args.steps)
     loss = float(st[0].item()) / B
     ms = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
+    async_rec = None
+    async_steps = args.steps if args.async_steps is None else args.async_steps
+    if args.mode == "sync" and async_steps > 0 and dev.type == "cuda":
+        # BASELINE metric "...; async speedup": same model / batch / rank count through the async engine
+        try:
+            anet = build_model(args.model, device=dev, seed=0)
+            atr = make_trainer("async", anet)
+            ael, _ = timed(atr, async_steps)
+            aval = world * B * async_steps / ael
+            async_rec = dict(images_per_s=round(aval, 1), ms_per_step=round(ael / async_steps * 1e3, 4),
+                             steps=async_steps, speedup_vs_sync=round(aval / value, 4),
+                             max_staleness_bound=args.max_staleness, **atr.ps_stats())
+        except Exception as e:  # reported, never fatal to the headline number
+            async_rec = {"error": repr(e)[:300]}
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -134,6 +161,8 @@ def main():
         }
         if args.mode == "async":
             out["async"] = dict(trainer.ps_stats(), max_staleness_bound=args.max_staleness)
+        elif async_rec is not None:
+            out["async"] = async_rec
         if args.json_extra:
             out["extra"] = {"final_loss": loss, "train_tflops": value * net.flops_per_example() / 1e12,
                             "capture_error": getattr(trainer, "capture_error", None)}

@@ -43,16 +43,36 @@ class AsyncPSTrainer(DataParallelTrainer):
                          broadcast_init=True, allreduce="rccl")
         self.max_staleness = int(max_staleness)
         self.server_rank = server_rank
-        self.ps = native.require().PSComm(self.rank, server_rank, net.store.total, timeout_s)
-        objs = [self.ps.handle() if self.rank == server_rank else b""]
+        # collective setup: every rank learns whether every other rank managed its part (no rank is left
+        # waiting in a barrier that a failed peer never reaches)
+        err, handle = None, b""
+        try:
+            self.ps = native.require().PSComm(self.rank, server_rank, net.store.total, timeout_s)
+            if self.rank == server_rank:
+                handle = self.ps.handle()
+        except Exception as e:
+            err = e
+        self._agree(err, "allocation/export")
+        objs = [handle]
         if self.world > 1:
             dist.broadcast_object_list(objs, src=server_rank, group=group)
-        self.ps.open(objs[0])
-        if self.rank == server_rank:
-            self.ps.init_master(net.store.master)
-        if self.world > 1:
-            dist.barrier(group=group)
+        try:
+            self.ps.open(objs[0])
+            if self.rank == server_rank:
+                self.ps.init_master(net.store.master)
+        except Exception as e:
+            err = e
+        self._agree(err, "IPC open")
         self._perm = None
+
+    def _agree(self, err, what):
+        ok = err is None
+        if self.world > 1:
+            from .p2p import _agree
+
+            ok = _agree(ok, self.group, self.net.device)
+        if not ok:
+            raise RuntimeError(f"async PS setup failed ({what}) on {'this' if err else 'another'} rank: {err!r}")
 
     # ------------------------------------------------------------------ schedule
     def bind_schedule(self, perm: torch.Tensor):
