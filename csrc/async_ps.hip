@@ -16,8 +16,9 @@
 //   ps_apply       take the writer lock (seq odd), check staleness = version_now - version_pulled
 //                  against the bound, apply w -= lr * g to the shared master, publish version + 1.
 // Every wait is bounded by a wall-clock timeout that sets a sticky error word instead of spinning
-// forever.  Both kernels run as one 1024-thread workgroup: the MNIST-sized payloads (247 KB for LeNet-5,
-// 2.4 MB for the Keras CNN) are latency bound, and a single workgroup makes the seqlock check exact.
+// forever.  Both kernels spread the weights over up to 64 workgroups (one workgroup moves only
+// ~60 GB/s of uncached / remote traffic; a single-workgroup version spent ~11 us per kernel on
+// LeNet-5's 247 KB).  The last-arriving workgroup finishes the protocol (seqlock check, unlock).
 //
 // Shared buffer layout (rank 0): [0] u32 seq (version = seq / 2), [16] u64 batch counter,
 // [256] fp32 master[n].
@@ -27,36 +28,125 @@
 namespace dfa {
 namespace {
 
-constexpr int kPSThreads = 1024;
-constexpr int kPSUnroll = 8;  // float4 loads in flight per thread per round
+constexpr int kPSBlock = 256;
+constexpr int kPSUnroll = 4;  // float4 loads in flight per thread per round
+// local scratch words (PSArgs::scratch, u32 index)
+constexpr int kPSPullDone = 0, kPSApplyDone = 1, kPSEpoch = 2, kPSDecision = 3, kPSLockedSeq = 4, kPSSlots = 64;
 
 __device__ __forceinline__ unsigned ld_acq(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(kPSThreads) void ps_fetch_pull_kernel(PSArgs a) {
-  const int t = threadIdx.x;
-  __shared__ long long s_bid;
+// Multi-workgroup seqlock snapshot.  Every workgroup copies its slice between two reads of the version
+// word and records the (even) version it saw; the last workgroup to finish checks that all slices saw
+// the same version.  A writer in between (rare: a worker holds the lock for a few microseconds per step)
+// makes the last workgroup redo the whole copy alone under the seqlock loop.
+__device__ void copy_slice(const float* __restrict__ src, float* __restrict__ dst, long long lo, long long hi,
+                           int t, int nt) {
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
+  f32x4* d4 = reinterpret_cast<f32x4*>(dst);
+  const long long lo4 = lo >> 2, hi4 = hi >> 2;  // lo, hi multiples of 4
+  for (long long base = lo4 + t; base < hi4; base += (long long)nt * kPSUnroll) {
+    f32x4 v[kPSUnroll];
+#pragma unroll
+    for (int u = 0; u < kPSUnroll; ++u) {
+      const long long i = base + (long long)u * nt;
+      if (i < hi4) v[u] = s4[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kPSUnroll; ++u) {
+      const long long i = base + (long long)u * nt;
+      if (i < hi4) d4[i] = v[u];
+    }
+  }
+}
+
+__global__ __launch_bounds__(kPSBlock) void ps_fetch_pull_kernel(PSArgs a) {
+  const int t = threadIdx.x, b = blockIdx.x, G = gridDim.x;
   __shared__ unsigned s_seq;
-  __shared__ int s_state;  // 0 = copy, 1 = done, 2 = error
-  // 1. FCFS microbatch id + its example indices
-  if (t == 0) {
-    s_bid = (long long)__hip_atomic_fetch_add(a.batch_ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    *a.bid_out = s_bid;
+  __shared__ int s_state;  // 0 = copy, 1 = consistent, 2 = error
+  __shared__ int s_last;
+  if (b == 0) {
+    // FCFS microbatch id (remote atomic on the server's counter) + its example indices
+    __shared__ long long s_bid;
+    if (t == 0) {
+      s_bid = (long long)__hip_atomic_fetch_add(a.batch_ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      *a.bid_out = s_bid;
+    }
+    __syncthreads();
+    if (a.perm != nullptr) {
+      // 16-byte copies, all loads of a thread in flight before its stores (B is even, rows 16B aligned)
+      typedef long long i64x2 __attribute__((ext_vector_type(2)));
+      const i64x2* src = reinterpret_cast<const i64x2*>(a.perm + (s_bid % a.nbatches) * a.B);
+      i64x2* dst = reinterpret_cast<i64x2*>(a.idx);
+      const int nv = a.B >> 1;
+      for (int base = t; base < nv; base += kPSBlock * 8) {
+        i64x2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (base + u * kPSBlock < nv) v[u] = src[base + u * kPSBlock];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (base + u * kPSBlock < nv) dst[base + u * kPSBlock] = v[u];
+      }
+    }
   }
-  __syncthreads();
-  if (a.perm != nullptr) {
-    const long long row = s_bid % a.nbatches;
-    for (int i = t; i < a.B; i += kPSThreads) a.idx[i] = a.perm[row * a.B + i];
-  }
-  // 2. seqlock snapshot of the shared master
+  const long long per = ((a.n + 4LL * G - 1) / (4LL * G)) * 4;  // slice length, multiple of 4
+  const long long lo = b * per, hi = lo + per < a.n ? lo + per : a.n;
   const unsigned long long t0 = wall_clock64();
-  const long long n4 = a.n >> 2;
-  for (int attempt = 0;; ++attempt) {
+  for (;;) {
     if (t == 0) {
       unsigned s = ld_acq(a.seq);
-      while (s & 1u) {  // a writer holds the lock
-        if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) break;
+      while ((s & 1u) && wall_clock64() - t0 <= (unsigned long long)a.timeout_ticks) {
+        __builtin_amdgcn_s_sleep(2);
+        s = ld_acq(a.seq);
+      }
+      s_seq = s;
+      s_state = (s & 1u) ? 2 : 0;
+    }
+    __syncthreads();
+    if (s_state == 2) break;
+    if (lo < hi) copy_slice(a.ps_w, a.w, lo, hi, t, kPSBlock);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // slice loads complete before the re-check
+    __syncthreads();
+    if (t == 0) {
+      if (ld_acq(a.seq) == s_seq) s_state = 1;
+      else if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) s_state = 2;
+    }
+    __syncthreads();
+    if (s_state != 0) break;
+    __syncthreads();  // every thread has read s_state before thread 0 rewrites it
+  }
+  // publish this slice's version (or an odd "failed" marker) and elect the last workgroup
+  if (t == 0) {
+    a.scratch[kPSSlots + b] = s_state == 1 ? s_seq : 1u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned prev = __hip_atomic_fetch_add(a.scratch + kPSPullDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == (unsigned)G - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (t == 0) {
+    const unsigned v0 = __hip_atomic_load(a.scratch + kPSSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int same = !(v0 & 1u);
+    for (int i = 1; i < G && same; ++i)
+      same = __hip_atomic_load(a.scratch + kPSSlots + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v0;
+    s_state = same ? 1 : 0;
+    s_seq = v0;
+    a.scratch[kPSPullDone] = 0;  // reset for the next launch (kernel boundary orders it)
+  }
+  __syncthreads();
+  if (s_state == 1) {
+    if (t == 0) *a.vpulled = s_seq >> 1;
+    return;
+  }
+  // torn snapshot across slices: redo the whole copy in this workgroup
+  if (t == 0) a.stats[4] += 1;
+  for (;;) {
+    if (t == 0) {
+      unsigned s = ld_acq(a.seq);
+      while ((s & 1u) && wall_clock64() - t0 <= (unsigned long long)a.timeout_ticks) {
         __builtin_amdgcn_s_sleep(2);
         s = ld_acq(a.seq);
       }
@@ -65,121 +155,144 @@ __global__ __launch_bounds__(kPSThreads) void ps_fetch_pull_kernel(PSArgs a) {
     }
     __syncthreads();
     if (s_state == 2) {
-      if (t == 0) atomicOr(reinterpret_cast<unsigned long long*>(a.stats) + 5, 1ull);
+      if (t == 0) atomicOr(a.stats + 5, 1ull);
       return;
     }
-    const f32x4* src = reinterpret_cast<const f32x4*>(a.ps_w);
-    f32x4* dst = reinterpret_cast<f32x4*>(a.w);
-    for (long long base = t; base < n4; base += (long long)kPSThreads * kPSUnroll) {
-      f32x4 v[kPSUnroll];
-#pragma unroll
-      for (int u = 0; u < kPSUnroll; ++u) {
-        const long long i = base + (long long)u * kPSThreads;
-        if (i < n4) v[u] = src[i];
-      }
-#pragma unroll
-      for (int u = 0; u < kPSUnroll; ++u) {
-        const long long i = base + (long long)u * kPSThreads;
-        if (i < n4) dst[i] = v[u];
-      }
-    }
-    for (long long i = (n4 << 2) + t; i < a.n; i += kPSThreads) a.w[i] = a.ps_w[i];
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // data loads complete before the re-check
+    copy_slice(a.ps_w, a.w, 0, a.n, t, kPSBlock);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     __syncthreads();
     if (t == 0) {
-      const unsigned s2 = ld_acq(a.seq);
-      if (s2 == s_seq) {
+      if (ld_acq(a.seq) == s_seq) {
         s_state = 1;
         *a.vpulled = s_seq >> 1;
-      } else {
-        a.stats[4] += 1;  // torn snapshot: retry
-        if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) {
-          atomicOr(reinterpret_cast<unsigned long long*>(a.stats) + 5, 2ull);
-          s_state = 1;
-          *a.vpulled = s_seq >> 1;
-        }
+      } else if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) {
+        atomicOr(a.stats + 5, 2ull);
+        s_state = 1;
+        *a.vpulled = s_seq >> 1;
       }
     }
     __syncthreads();
     if (s_state == 1) return;
-    __syncthreads();  // every thread has read s_state before thread 0 rewrites it
+    __syncthreads();
   }
 }
 
-__global__ __launch_bounds__(kPSThreads) void ps_apply_kernel(PSArgs a) {
-  const int t = threadIdx.x;
+// Multi-workgroup locked apply.  Workgroup 0 takes the writer lock and decides (staleness check); the
+// others wait for that decision on a local word tagged with this launch's epoch, apply their slice, and
+// the last workgroup to finish publishes version + 1 (releases the lock).  The grid is small (<= 64
+// workgroups), so all of it is resident and the decision wait cannot starve workgroup 0.
+__global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
+  const int t = threadIdx.x, b = blockIdx.x, G = gridDim.x;
+  __shared__ unsigned s_dec;  // 1 = apply, 2 = stale (rejected), 3 = error
   __shared__ unsigned s_seq;
-  __shared__ int s_go;  // 1 = apply, 0 = stale (rejected), -1 = lock timeout
+  __shared__ int s_last;
   if (t == 0) {
+    const unsigned ep = __hip_atomic_load(a.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const unsigned long long t0 = wall_clock64();
-    int go = -1;
-    for (;;) {
-      unsigned s = ld_acq(a.seq);
-      if (!(s & 1u)) {
-        unsigned expected = s;
-        if (__hip_atomic_compare_exchange_strong(a.seq, &expected, s + 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_SYSTEM)) {
-          s_seq = s;
-          const unsigned stale = (s >> 1) - *a.vpulled;
-          go = ((int)stale <= a.max_stale || a.max_stale < 0) ? 1 : 0;
-          if (go) {
-            a.stats[0] += 1;
-            a.stats[2] += stale;
-            if (stale > a.stats[3]) a.stats[3] = stale;
-          } else {
-            a.stats[1] += 1;
-            __hip_atomic_store(a.seq, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // unlock, no new version
+    if (b == 0) {
+      unsigned dec = 3, s = 0;
+      for (;;) {
+        s = ld_acq(a.seq);
+        if (!(s & 1u)) {
+          unsigned expected = s;
+          if (__hip_atomic_compare_exchange_strong(a.seq, &expected, s + 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_SYSTEM)) {
+            const unsigned stale = (s >> 1) - *a.vpulled;
+            if ((int)stale <= a.max_stale || a.max_stale < 0) {
+              dec = 1;
+              a.stats[0] += 1;
+              a.stats[2] += stale;
+              if (stale > a.stats[3]) a.stats[3] = stale;
+            } else {
+              dec = 2;
+              a.stats[1] += 1;
+              __hip_atomic_store(a.seq, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // unlock, no new version
+            }
+            break;
           }
+        }
+        if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) {
+          atomicOr(a.stats + 5, 4ull);
           break;
         }
+        __builtin_amdgcn_s_sleep(1);
       }
-      if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) {
-        atomicOr(reinterpret_cast<unsigned long long*>(a.stats) + 5, 4ull);
-        break;
+      a.scratch[kPSLockedSeq] = s;
+      __hip_atomic_store(a.scratch + kPSDecision, (ep << 2) | dec, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      s_dec = dec;
+    } else {
+      unsigned d = 0;
+      for (;;) {
+        d = __hip_atomic_load(a.scratch + kPSDecision, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if ((d >> 2) == ep) break;
+        if (wall_clock64() - t0 > 2ull * (unsigned long long)a.timeout_ticks) {
+          atomicOr(a.stats + 5, 8ull);
+          d = 3;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
-      __builtin_amdgcn_s_sleep(1);
+      s_dec = d & 3u;
     }
-    s_go = go;
+    s_seq = a.scratch[kPSLockedSeq];
   }
   __syncthreads();
-  if (s_go != 1) return;
-  const float lr = a.lr;
-  const long long n4 = a.n >> 2;
-  f32x4* w = reinterpret_cast<f32x4*>(a.ps_w);
-  const f32x4* g = reinterpret_cast<const f32x4*>(a.g);
-  for (long long base = t; base < n4; base += (long long)kPSThreads * kPSUnroll) {
-    f32x4 v[kPSUnroll], gv[kPSUnroll];
+  if (s_dec == 1) {
+    const long long per = ((a.n + 4LL * G - 1) / (4LL * G)) * 4;
+    const long long lo = b * per, hi = lo + per < a.n ? lo + per : a.n;
+    const float lr = a.lr;
+    f32x4* w = reinterpret_cast<f32x4*>(a.ps_w);
+    const f32x4* g = reinterpret_cast<const f32x4*>(a.g);
+    for (long long base = (lo >> 2) + t; base < (hi >> 2); base += (long long)kPSBlock * kPSUnroll) {
+      f32x4 v[kPSUnroll], gv[kPSUnroll];
 #pragma unroll
-    for (int u = 0; u < kPSUnroll; ++u) {
-      const long long i = base + (long long)u * kPSThreads;
-      if (i < n4) {
-        v[u] = w[i];
-        gv[u] = g[i];
+      for (int u = 0; u < kPSUnroll; ++u) {
+        const long long i = base + (long long)u * kPSBlock;
+        if (i < (hi >> 2)) {
+          v[u] = w[i];
+          gv[u] = g[i];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kPSUnroll; ++u) {
+        const long long i = base + (long long)u * kPSBlock;
+        if (i < (hi >> 2)) w[i] = v[u] - lr * gv[u];
       }
     }
-#pragma unroll
-    for (int u = 0; u < kPSUnroll; ++u) {
-      const long long i = base + (long long)u * kPSThreads;
-      if (i < n4) w[i] = v[u] - lr * gv[u];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this slice's weight stores visible system-wide
+  }
+  __syncthreads();
+  if (t == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(a.scratch + kPSApplyDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == (unsigned)G - 1;
+    if (s_last) {
+      a.scratch[kPSApplyDone] = 0;
+      a.scratch[kPSEpoch] += 1u;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // every slice's release happened before the unlock
+      if (s_dec == 1) __hip_atomic_store(a.seq, s_seq + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
-  for (long long i = (n4 << 2) + t; i < a.n; i += kPSThreads) a.ps_w[i] = a.ps_w[i] - lr * a.g[i];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // all weight stores visible before the new version
-  __syncthreads();
-  if (t == 0) __hip_atomic_store(a.seq, s_seq + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace
 
+// ~16 KB of weights per workgroup, at most kPSMaxGrid workgroups (all resident: the apply kernel's
+// decision wait relies on it)
+static int ps_grid(long long n) {
+  long long g = (n + 4095) / 4096;
+  return (int)(g < 1 ? 1 : (g > kPSMaxGrid ? kPSMaxGrid : g));
+}
+
 hipError_t ps_fetch_pull(const PSArgs& a, hipStream_t st) {
-  if (a.n <= 0 || (a.perm != nullptr && (a.B <= 0 || a.nbatches <= 0))) return hipErrorInvalidValue;
-  ps_fetch_pull_kernel<<<1, kPSThreads, 0, st>>>(a);
+  if (a.n <= 0 || (a.n & 3) || (a.perm != nullptr && (a.B <= 0 || (a.B & 1) || a.nbatches <= 0)))
+    return hipErrorInvalidValue;
+  ps_fetch_pull_kernel<<<ps_grid(a.n), kPSBlock, 0, st>>>(a);
   return hipGetLastError();
 }
 
 hipError_t ps_apply(const PSArgs& a, hipStream_t st) {
-  if (a.n <= 0) return hipErrorInvalidValue;
-  ps_apply_kernel<<<1, kPSThreads, 0, st>>>(a);
+  if (a.n <= 0 || (a.n & 3)) return hipErrorInvalidValue;
+  ps_apply_kernel<<<ps_grid(a.n), kPSBlock, 0, st>>>(a);
   return hipGetLastError();
 }
 

@@ -781,8 +781,8 @@ class PSComm {
       shared_ = (char*)p;
       check_hip(hipMemset(shared_, 0, bytes), "ps memset");
     }
-    check_hip(hipMalloc((void**)&local_, 256), "ps local alloc");
-    check_hip(hipMemset(local_, 0, 256), "ps local memset");
+    check_hip(hipMalloc((void**)&local_, 4096), "ps local alloc");
+    check_hip(hipMemset(local_, 0, 4096), "ps local memset");
     check_hip(hipDeviceSynchronize(), "ps init sync");
     timeout_ticks_ = (int64_t)(timeout_s * 1e8);
   }
@@ -824,6 +824,7 @@ class PSComm {
       TORCH_CHECK(idx.has_value() && idx->defined(), "ps: idx required with perm");
       need(*idx, at::kLong, "ps idx");
       TORCH_CHECK(perm->dim() == 2 && perm->size(1) == idx->numel(), "ps: perm must be [nbatches][B]");
+      TORCH_CHECK(idx->numel() % 2 == 0, "ps: batch size must be even");
       a.perm = reinterpret_cast<const long long*>(perm->data_ptr());
       a.idx = reinterpret_cast<long long*>(idx->data_ptr());
       a.nbatches = perm->size(0);
@@ -869,6 +870,7 @@ class PSComm {
     a.vpulled = reinterpret_cast<unsigned*>(local_);
     a.bid_out = reinterpret_cast<long long*>(local_ + 8);
     a.stats = reinterpret_cast<unsigned long long*>(local_ + 64);
+    a.scratch = reinterpret_cast<unsigned*>(local_ + 1024);
     a.timeout_ticks = timeout_ticks_;
     a.max_stale = -1;
     return a;

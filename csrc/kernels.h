@@ -207,6 +207,7 @@ struct PSArgs {
   long long n;
   unsigned* vpulled;            // local: version of the last pulled snapshot
   unsigned long long* stats;    // local [8]: accepted, rejected, sum staleness, max staleness, torn retries, err
+  unsigned* scratch;            // local [64 + kPSMaxGrid] zero-initialised protocol words (async_ps.hip)
   const long long* perm;        // [nbatches][B] example ids (nullptr: no index staging)
   long long* idx;               // [B] staged ids of the claimed microbatch
   long long* bid_out;           // local: id of the claimed microbatch
@@ -214,6 +215,7 @@ struct PSArgs {
   int B, max_stale;
   float lr;
 };
+constexpr int kPSMaxGrid = 64;
 hipError_t ps_fetch_pull(const PSArgs& a, hipStream_t st);
 hipError_t ps_apply(const PSArgs& a, hipStream_t st);
 
