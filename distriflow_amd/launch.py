@@ -74,6 +74,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--workers", type=int, default=2, help="worker threads when running in one process")
     p.add_argument("--max-staleness", type=int, default=-1)
     p.add_argument("--ship-data", action="store_true")
+    p.add_argument("--engine", default="auto", choices=["auto", "device", "roles"],
+                   help="device = GPU-resident parameter server (parallel/async_ps.py, every rank a worker); "
+                        "roles = message-level AsynchronousSGDServer/Client (reference protocol); "
+                        "auto = device on GPUs, roles on CPU")
 
     p = sub.add_parser("fedsgd", help="FederatedServer / FederatedClient (reference sync PS)")
     common(p)
@@ -279,8 +283,62 @@ def _ps_setup(args):
     return env
 
 
+def run_async_device(args) -> dict:
+    """Async SGD on the device-resident bounded-staleness parameter server: rank 0's HBM holds the
+    master weights and the FCFS microbatch counter; every rank (one per GPU) is a worker that replays its
+    own captured step.  The epochs' microbatches are split evenly over the ranks."""
+    import torch
+    import torch.distributed as dist
+
+    from .models.zoo import build_model
+    from .parallel.async_ps import AsyncPSTrainer
+    from .parallel.comm import init_distributed, shutdown
+    from .parallel.data_parallel import epoch_permutations
+
+    env = init_distributed(device=_device(args))
+    rank, world, dev = env.rank, env.world_size, env.device
+    log = _logger(args, f"Distributed Worker {rank}")
+    x, y = _load_data(args, dev)
+    n, B = x.shape[0], args.batch
+    nb = n // B
+    net = build_model(args.model, device=dev, seed=args.seed)
+    tr = AsyncPSTrainer(net, lr=args.lr, max_staleness=args.max_staleness, graph="full")
+    tr.bind_dataset(x, y, B, scale=1.0 / 255.0 if x.dtype == torch.uint8 else 1.0)
+    tr.bind_schedule(epoch_permutations(n, B, nb * args.epochs, dev, seed=args.seed))
+    steps = max(1, (nb * args.epochs) // world)
+    faults = Faults(args, rank)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        faults.step(i)
+        st = tr.step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    tr.check_comm()
+    out = {}
+    if rank == 0:
+        tr.pull_master()
+        loss, acc = net.evaluate(x[:4096].float() * (1.0 / 255.0 if x.dtype == torch.uint8 else 1.0), y[:4096])
+        out = dict(mode="async", engine="device", world=world, steps_per_rank=steps,
+                   images_per_s=world * steps * B / max(el, 1e-9), last_loss=float(st[0]) / B,
+                   eval_loss=float(loss), eval_accuracy=float(acc), max_staleness=args.max_staleness, **tr.ps_stats())
+        log.metric(event="async_done", **out)
+        print(json.dumps(out), flush=True)
+    shutdown()
+    return out
+
+
 def run_async(args) -> dict:
     import torch
+
+    engine = args.engine
+    if engine == "auto":
+        engine = "device" if _device(args) == "cuda" else "roles"
+    if engine == "device":
+        return run_async_device(args)
 
     from .data.dataset import DistriDataset
     from .models.distri_model import ClientModel, InMemoryServerModel

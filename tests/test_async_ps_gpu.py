@@ -97,3 +97,22 @@ def test_async_ps_multi_worker(world, max_stale):
     assert sum(x["accepted"] for x in r) >= steps  # progress
     l0 = r[0]["losses"]
     assert sum(l0[-5:]) < sum(l0[:5])
+
+
+@pytest.mark.timeout(180)
+def test_launcher_async_device_engine():
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, "-m", "distriflow_amd.launch", "async", "--model", "lenet5", "--num-examples",
+                        "16384", "--batch", "512", "--epochs", "3", "--max-staleness", "2"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=170)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["engine"] == "device" and out["error"] == 0
+    assert out["accepted"] + out["rejected"] == out["steps_per_rank"] + 3  # + graph warm-up steps
+    assert out["eval_accuracy"] > 0.5
