@@ -20,7 +20,7 @@
 
 namespace dfa {
 
-constexpr int BN_MAX_G = 255;
+constexpr int BN_MAX_G = 255;  // more workgroups cost more than they add: every one pays a release fence (L2 writeback)
 constexpr int BN_GROUP = 16;
 
 static bool bn_vec(int C) { return C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0; }
@@ -81,38 +81,57 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
     }
   }
   if (rsub < rpp) {
-#pragma unroll 4
-    for (long long r = (long long)blockIdx.x * rpp + rsub; r < M; r += (long long)gridDim.x * rpp) {
-      const long long o = r * C + chunk * W;
-      float xv[W], gv[W];
+    // U rows per thread per round, every load of the round issued before the first use: a streaming
+    // reduction needs ~16-32 KB in flight per CU to cover HBM latency
+    constexpr int U = MODE == 0 ? 8 : 4;
+    const long long step = (long long)gridDim.x * rpp;
+    long long r = (long long)blockIdx.x * rpp + rsub;
+    for (; r < M; r += U * step) {
+      float xv[U][W], gv[U][W];
       if (VEC) {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(a.x + o);
+        bf16x8 vx[U], vg[U], vm[U];
 #pragma unroll
-        for (int j = 0; j < W; ++j) xv[j] = (float)v[j];
-        if (MODE == 1) {
-          const bf16x8 g = *reinterpret_cast<const bf16x8*>(a.dy + o);
-          if (a.mask) {
-            const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.mask + o);
+        for (int u = 0; u < U; ++u) {
+          const long long rr = r + u * step;
+          const long long o = (rr < M ? rr : r) * C + chunk * W;  // clamped, masked below
+          vx[u] = *reinterpret_cast<const bf16x8*>(a.x + o);
+          if (MODE == 1) {
+            vg[u] = *reinterpret_cast<const bf16x8*>(a.dy + o);
+            if (a.mask) vm[u] = *reinterpret_cast<const bf16x8*>(a.mask + o);
+          }
+        }
 #pragma unroll
-            for (int j = 0; j < W; ++j) gv[j] = ((float)mk[j] > 0.f) ? (float)g[j] : 0.f;
-          } else {
+        for (int u = 0; u < U; ++u) {
+          const bool ok = r + u * step < M;
 #pragma unroll
-            for (int j = 0; j < W; ++j) gv[j] = (float)g[j];
+          for (int j = 0; j < W; ++j) {
+            xv[u][j] = ok ? (float)vx[u][j] : 0.f;
+            if (MODE == 1) gv[u][j] = (ok && (!a.mask || (float)vm[u][j] > 0.f)) ? (float)vg[u][j] : 0.f;
           }
         }
       } else {
-        xv[0] = (float)a.x[o];
-        if (MODE == 1) gv[0] = (a.mask && !((float)a.mask[o] > 0.f)) ? 0.f : (float)a.dy[o];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long rr = r + u * step;
+          const bool ok = rr < M;
+          const long long o = (ok ? rr : r) * C + chunk;
+          xv[u][0] = ok ? (float)a.x[o] : 0.f;
+          if (MODE == 1) gv[u][0] = (!ok || (a.mask && !((float)a.mask[o] > 0.f))) ? 0.f : (float)a.dy[o];
+        }
       }
 #pragma unroll
-      for (int j = 0; j < W; ++j) {
-        if (MODE == 0) {
-          s[j] += xv[j];
-          q[j] += xv[j] * xv[j];
-        } else {
-          const float xh = (xv[j] - mu[j]) * is[j];
-          s[j] += gv[j];
-          q[j] += gv[j] * xh;
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          if (MODE == 0) {
+            s[j] += xv[u][j];
+            q[j] += xv[u][j] * xv[u][j];
+          } else {
+            // rows past M contribute g = 0 (and their xh is multiplied by 0)
+            const float xh = (xv[u][j] - mu[j]) * is[j];
+            s[j] += gv[u][j];
+            q[j] += gv[u][j] * xh;
+          }
         }
       }
     }
@@ -155,19 +174,21 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
   // ---- level 2: the last group reducer sums the group slabs in fp64 and finalises
   if (!bn_last_arriver(a.counter, (unsigned)ngrp, &last)) return;
   for (int c = t; c < C; c += 256) {
-    float su[BN_GROUP], qu[BN_GROUP];
-#pragma unroll
-    for (int j = 0; j < BN_GROUP; ++j) {
-      const long long base = (long long)min(j, ngrp - 1) * ncol;
-      su[j] = gslab[base + c];
-      qu[j] = gslab[base + C + c];
-    }
     double sv = 0.0, qv = 0.0;
+    for (int g0 = 0; g0 < ngrp; g0 += BN_GROUP) {
+      float su[BN_GROUP], qu[BN_GROUP];
 #pragma unroll
-    for (int j = 0; j < BN_GROUP; ++j) {
-      if (j < ngrp) {
-        sv += (double)su[j];
-        qv += (double)qu[j];
+      for (int j = 0; j < BN_GROUP; ++j) {
+        const long long base = (long long)min(g0 + j, ngrp - 1) * ncol;
+        su[j] = gslab[base + c];
+        qu[j] = gslab[base + C + c];
+      }
+#pragma unroll
+      for (int j = 0; j < BN_GROUP; ++j) {
+        if (g0 + j < ngrp) {
+          sv += (double)su[j];
+          qv += (double)qu[j];
+        }
       }
     }
     if (MODE == 0) {

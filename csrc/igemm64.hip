@@ -15,7 +15,8 @@
 //   * a thread's 16-byte chunk column is fixed (c = tid & 7), so ONE (kh, kw, ci) state per thread
 //     advances per step; the per-row pixel state is computed once with multiply-high division
 //   * every load comes from a clamped address and is masked afterwards (no load under a branch)
-//   * epilogue as igemm.hip: alpha, bias, residual join (res * [resmask > 0]), ReLU, relu'(mask)
+//   * epilogue as igemm.hip: alpha, bias, residual join (res * [resmask > 0]), ReLU, relu'(mask), with
+//     the weights as the MFMA A operand so each lane stores 4 adjacent output channels at once
 #include "common.h"
 #include "kernels.h"
 
@@ -168,36 +169,73 @@ __global__ void __launch_bounds__(256) igemm64_kernel(IGemmArgs a, FastDiv d_ow,
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fa[i], fb[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);  // D[n][m]
     }
     if (kt + 1 < nk) sstore(cur ^ 1);
     __syncthreads();
   }
 
-  // epilogue: C/D layout of the 16x16 MFMA: col (n) = lane & 15, row (m) = 4 * (lane >> 4) + r
+  // epilogue.  The weights are the MFMA's A operand, so the 16x16 C/D layout puts 4 consecutive output
+  // COLUMNS (n = 4 * (lane >> 4) + r) of one output row (m = lane & 15) in a lane: every lane moves
+  // one 8-byte bf16x4 (16-byte f32x4) store and 8-byte residual / mask loads instead of four 2-byte ones.
+  const bool vec = (a.ldc & 3) == 0 && ((uintptr_t)a.out & 15) == 0 &&
+                   (((uintptr_t)a.res | (uintptr_t)a.resmask | (uintptr_t)a.mask) & 7) == 0;
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    const int row = m0 + wm * TM * 16 + i * 16 + fr;
+    if (row >= a.M) continue;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wn * TN * 16 + j * 16 + fr;
-      if (col >= a.N) continue;
-      const float bv = a.bias ? a.bias[col] : 0.f;
+      const int col0 = n0 + wn * TN * 16 + j * 16 + fq * 4;
+      if (col0 >= a.N) continue;
+      const long long o = (long long)row * a.ldc + col0;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * a.alpha + ((a.bias && col0 + r < a.N) ? a.bias[col0 + r] : 0.f);
+      if (vec && col0 + 3 < a.N) {
+        if (a.res) {
+          const bf16x4_t rv = *reinterpret_cast<const bf16x4_t*>(a.res + o);
+          bf16x4_t rm;
+          if (a.resmask) rm = *reinterpret_cast<const bf16x4_t*>(a.resmask + o);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (!a.resmask || (float)rm[r] > 0.f) v[r] += (float)rv[r];
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (a.mask) {
+          const bf16x4_t mk = *reinterpret_cast<const bf16x4_t*>(a.mask + o);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (!((float)mk[r] > 0.f)) v[r] = 0.f;
+        }
+        if (a.out_f32) {
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+          bf16x4_t ov;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ov[r] = f2bf(v[r]);
+          *reinterpret_cast<bf16x4_t*>(reinterpret_cast<bf16*>(a.out) + o) = ov;
+        }
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * TM * 16 + i * 16 + fq * 4 + r;
-        if (row >= a.M) continue;
-        float v = acc[i][j][r] * a.alpha + bv;
-        const long long o = (long long)row * a.ldc + col;
+        if (col0 + r >= a.N) continue;
+        float x = v[r];
         if (a.res) {
-          const float rv = (float)a.res[o];
-          if (!a.resmask || (float)a.resmask[o] > 0.f) v += rv;
+          const float rv = (float)a.res[o + r];
+          if (!a.resmask || (float)a.resmask[o + r] > 0.f) x += rv;
         }
-        if (a.relu) v = fmaxf(v, 0.f);
-        if (a.mask && !((float)a.mask[o] > 0.f)) v = 0.f;
+        if (a.relu) x = fmaxf(x, 0.f);
+        if (a.mask && !((float)a.mask[o + r] > 0.f)) x = 0.f;
         if (a.out_f32)
-          reinterpret_cast<float*>(a.out)[o] = v;
+          reinterpret_cast<float*>(a.out)[o + r] = x;
         else
-          reinterpret_cast<bf16*>(a.out)[o] = f2bf(v);
+          reinterpret_cast<bf16*>(a.out)[o + r] = f2bf(x);
       }
     }
   }
