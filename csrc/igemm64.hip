@@ -8,13 +8,15 @@
 //
 //   * 4 waves (2 x 2) on a 128x128 / 128x64 / 64x128 tile; v_mfma_f32_16x16x32_bf16; each 64-deep
 //     step is two 32-deep halves, so a wave issues 2*TM*TN MFMAs per barrier (32 on 128x128)
-//   * register-staged double buffer: the 16-byte global loads of step k+1 are issued before the
-//     MFMAs of step k and stored to the other LDS buffer after them; one barrier per step
+//   * register-staged prefetch D steps deep (D register sets) into a double-buffered LDS tile: the
+//     16-byte global loads of step k+D are issued right after step k's barrier and stored to LDS after
+//     the MFMAs of step k+D-1; one barrier per step
 //   * LDS rows of 64 bf16 (128 B) with the 16-byte chunk swizzle c ^ ((row >> 1) & 7): the 16 rows
 //     one ds_read_b128 lane group reads sit on 16 distinct 16-byte bank slots
 //   * a thread's 16-byte chunk column is fixed (c = tid & 7), so ONE (kh, kw, ci) state per thread
 //     advances per step; the per-row pixel state is computed once with multiply-high division
-//   * every load comes from a clamped address and is masked afterwards (no load under a branch)
+//   * a masked-out load reads a 16-byte zero constant (address select: no load under a branch and no
+//     data masking that would force a wait right after the load)
 //   * epilogue as igemm.hip: alpha, bias, residual join (res * [resmask > 0]), ReLU, relu'(mask), with
 //     the weights as the MFMA A operand so each lane stores 4 adjacent output channels at once
 #include "common.h"
@@ -26,10 +28,32 @@ namespace {
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
+#ifndef IGEMM64_STAGES
+#define IGEMM64_STAGES 2
+#endif
+constexpr int kIgemm64Stages = IGEMM64_STAGES;  // register prefetch depth (steps in flight)
+
+__device__ u32x4_t kZero16 = {0u, 0u, 0u, 0u};  // source of every masked-out 16-byte chunk
+
+// Operand loads are issued from inline asm: hipcc's waitcnt pass then does not see them and cannot
+// insert its conservative loop-carried `s_waitcnt vmcnt` (it waited for the newest loads before every
+// LDS store, collapsing any prefetch depth to one step).  The k loop counts them by hand: the stage
+// stored at step k has exactly (D-1) newer stages in flight in the steady state.
+__device__ __forceinline__ u32x4_t gload16(const void* p) {
+  u32x4_t r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
-template <int BM, int BN, int MODE>
-__global__ void __launch_bounds__(256) igemm64_kernel(IGemmArgs a, FastDiv d_ow, FastDiv d_ohw) {
+// occupancy the LDS footprint allows (2 x (BM + BN) x 128 B per workgroup): 3 workgroups of 48 KB or
+// 2 of 64 KB per CU; the register budget is capped to match (one workgroup = one wave per SIMD)
+template <int BM, int BN>
+constexpr int igemm64_occ() { return (BM + BN) * 256 > 60 * 1024 ? 2 : 3; }
+
+template <int BM, int BN, int MODE, int D>
+__global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(IGemmArgs a, FastDiv d_ow, FastDiv d_ohw) {
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / (WM * 16), TN = BN / (WN * 16);
   constexpr int AP = BM / 32, BP = BN / 32;  // 16-byte chunks per thread and step (8 chunks per 64-deep row)
@@ -81,8 +105,11 @@ __global__ void __launch_bounds__(256) igemm64_kernel(IGemmArgs a, FastDiv d_ow,
   }
   const int npad = round_up(a.N, 16);
 
-  u32x4_t ra[AP], rb[BP];
-  auto gload = [&]() {
+  // D register stages of prefetched global loads: the loads of step k are issued D iterations before
+  // step k is stored to LDS, so ~D * (MFMA time of one step) of memory latency is covered even with a
+  // single wave per SIMD (the small-M layers launch one workgroup per CU)
+  u32x4_t ra[D][AP], rb[D][BP];
+  auto gload = [&](int st) {
     const bool kv = kk < a.K;
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
@@ -105,15 +132,15 @@ __global__ void __launch_bounds__(256) igemm64_kernel(IGemmArgs a, FastDiv d_ow,
         v = v && th < a.SH && tw < a.SW;
         off = rbase[i] + ((long long)th * a.SW + tw) * a.SC + ci;
       }
-      const u32x4_t t = *reinterpret_cast<const u32x4_t*>(a.src + (v ? off : 0));
-      ra[i] = t & (v ? 0xffffffffu : 0u);
+      // a masked-out chunk reads 16 zero bytes instead (address select, not a data mask: the loaded value
+      // is not touched until its LDS store D steps later, so no wait is forced right after the load)
+      ra[st][i] = gload16(v ? (const void*)(a.src + off) : (const void*)&kZero16);
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
       const int n = n0 + r0 + 32 * i;
       const bool v = n < npad && kk < a.Kpad;
-      const u32x4_t t = *reinterpret_cast<const u32x4_t*>(a.w + (v ? (long long)n * a.Kpad + kk : 0));
-      rb[i] = t & (v ? 0xffffffffu : 0u);
+      rb[st][i] = gload16(v ? (const void*)(a.w + (long long)n * a.Kpad + kk) : (const void*)&kZero16);
     }
   };
   auto advance = [&]() {
@@ -129,13 +156,13 @@ __global__ void __launch_bounds__(256) igemm64_kernel(IGemmArgs a, FastDiv d_ow,
       }
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, int st) {
     bf16* as = lds + buf * (BM + BN) * 64;
     bf16* bs = as + BM * 64;
 #pragma unroll
-    for (int i = 0; i < AP; ++i) *reinterpret_cast<u32x4_t*>(as + swz(r0 + 32 * i, c)) = ra[i];
+    for (int i = 0; i < AP; ++i) *reinterpret_cast<u32x4_t*>(as + swz(r0 + 32 * i, c)) = ra[st][i];
 #pragma unroll
-    for (int i = 0; i < BP; ++i) *reinterpret_cast<u32x4_t*>(bs + swz(r0 + 32 * i, c)) = rb[i];
+    for (int i = 0; i < BP; ++i) *reinterpret_cast<u32x4_t*>(bs + swz(r0 + 32 * i, c)) = rb[st][i];
   };
 
   f32x4 acc[TM][TN];
@@ -145,34 +172,56 @@ __global__ void __launch_bounds__(256) igemm64_kernel(IGemmArgs a, FastDiv d_ow,
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = cdiv(a.K, 64);
-  gload();
-  sstore(0);
+  // prologue: step 0 -> LDS[0]; steps 1..D in flight (register stage of step s = s % D)
+  gload(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  sstore(0, 0);
+#pragma unroll
+  for (int s = 1; s <= D; ++s) {
+    if (s < nk) {
+      advance();
+      gload(s % D);
+    }
+  }
   __syncthreads();
   const int fr = lane & 15, fq = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      advance();
-      gload();
+  for (int kb = 0; kb < nk; kb += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int kt = kb + u;
+      if (kt < nk) {
+        const int cur = kt & 1;
+        const bf16* as = lds + cur * (BM + BN) * 64;
+        const bf16* bs = as + BM * 64;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          bf16x8 fa[TM], fb[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            fa[i] = *reinterpret_cast<const bf16x8*>(as + swz(wm * TM * 16 + i * 16 + fr, h * 4 + fq));
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            fb[j] = *reinterpret_cast<const bf16x8*>(bs + swz(wn * TN * 16 + j * 16 + fr, h * 4 + fq));
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);  // D[n][m]
+        }
+        const int nst = (u + 1) % D;  // register stage holding step kt + 1
+        if (kt + 1 < nk) {
+          if (kt + D < nk)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"((AP + BP) * (D - 1)) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          sstore(cur ^ 1, nst);
+        }
+        __syncthreads();
+        if (kt + 1 + D < nk) {  // refill the freed stage with step kt + 1 + D
+          advance();
+          gload(nst);
+        }
+      }
     }
-    const bf16* as = lds + cur * (BM + BN) * 64;
-    const bf16* bs = as + BM * 64;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      bf16x8 fa[TM], fb[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        fa[i] = *reinterpret_cast<const bf16x8*>(as + swz(wm * TM * 16 + i * 16 + fr, h * 4 + fq));
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        fb[j] = *reinterpret_cast<const bf16x8*>(bs + swz(wn * TN * 16 + j * 16 + fr, h * 4 + fq));
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);  // D[n][m]
-    }
-    if (kt + 1 < nk) sstore(cur ^ 1);
-    __syncthreads();
   }
 
   // epilogue.  The weights are the MFMA's A operand, so the 16x16 C/D layout puts 4 consecutive output
@@ -245,7 +294,8 @@ template <int BM, int BN, int MODE>
 hipError_t launch64(const IGemmArgs& a, hipStream_t st) {
   const FastDiv d_ow = make_fastdiv((unsigned)max(a.OW, 1)), d_ohw = make_fastdiv((unsigned)max(a.OH * a.OW, 1));
   const int blocks = cdiv(a.M, BM) * cdiv(a.N, BN);
-  hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE>), dim3(blocks), dim3(256), 0, st, a, d_ow, d_ohw);
+  constexpr int D = kIgemm64Stages;
+  hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE, D>), dim3(blocks), dim3(256), 0, st, a, d_ow, d_ohw);
   return hipGetLastError();
 }
 
