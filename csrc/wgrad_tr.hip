@@ -8,8 +8,8 @@
 // ds_read_b64_tr_b16, which transpose a 4-row x 16-column block per 16-lane group inside the LDS
 // read.  (igemm.hip's generic wgrad transposes with eight 2-byte LDS stores per chunk.)
 //
-//   * workgroup = BN x BK output tile, 4 waves as WN x WK, m-steps of 64 rows, two LDS buffers:
-//     the global loads of step s+1 are in flight during the MFMAs of step s, one barrier per step
+//   * workgroup = BN x BK output tile, 4 waves as WN x WK, m-steps of 64 rows, two LDS buffers and a
+//     2-step register prefetch (inline-asm loads, hand-counted vmcnt), one barrier per step
 //   * m is split over workgroups (split-m); slab_reduce sums the slabs in a fixed order
 //   * LDS row stride = 8 x odd dwords (mod 64): the 8 rows one 32-lane half reads with a
 //     transposed read sit on 8 disjoint 8-bank groups (conflict-free), and 8 lanes storing the 8
@@ -19,7 +19,7 @@
 //     makes the row blocks of one transposed read contiguous
 //   * a thread's k chunk (kh, kw, ci) is fixed for the whole launch; per step only the pixel
 //     decomposition (multiply-high division by OW and OH*OW) is recomputed; out-of-image taps and
-//     tails load from a clamped address and are zeroed with a mask (no load under a branch)
+//     tails read a 16-byte zero constant instead (address select: no load under a branch)
 #include "common.h"
 #include "kernels.h"
 
@@ -39,8 +39,22 @@ __device__ __forceinline__ bf16x4 tr_read(const bf16* p) {
 
 constexpr int tr_stride(int cols) { return cols + (((cols / 16) % 2) ? 0 : 16); }
 
+__device__ u32x4_t kZeroTr16 = {0u, 0u, 0u, 0u};  // source of every masked-out 16-byte chunk
+
+// Operand loads from inline asm with hand-counted waits (see igemm64.hip: hipcc's loop-carried
+// vmcnt waits otherwise collapse the register prefetch to one step).
+__device__ __forceinline__ u32x4_t gload16_tr(const void* p) {
+  u32x4_t r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+
+constexpr int kWgradStages = 2;  // register prefetch depth (m-steps in flight)
+
+// two workgroups per CU fit the LDS (57-74 KB each): cap registers at two waves per SIMD
 template <int BN, int BK, int WN, int WK>
-__global__ void __launch_bounds__(256) wgrad_tr_kernel(WgradArgs a, FastDiv d_ow, FastDiv d_ohw) {
+__global__ void __launch_bounds__(256, 2) wgrad_tr_kernel(WgradArgs a, FastDiv d_ow, FastDiv d_ohw) {
+  constexpr int D = kWgradStages;
   constexpr int BM = 64;
   constexpr int SN = tr_stride(BN), SK = tr_stride(BK);
   constexpr int TN = BN / (WN * 16), TK = BK / (WK * 16);
@@ -76,15 +90,13 @@ __global__ void __launch_bounds__(256) wgrad_tr_kernel(WgradArgs a, FastDiv d_ow
   }
   const unsigned ohw = (unsigned)(a.OH * a.OW);
 
-  u32x4_t rd[DP], rx[XP];
-  auto gload = [&](int m0) {
+  u32x4_t rd[D][DP], rx[D][XP];
+  auto gload = [&](int st, int m0) {
 #pragma unroll
     for (int i = 0; i < DP; ++i) {
       const int m = m0 + dr + i * DR;
       const bool v = nval && m < me;
-      const long long off = v ? (long long)m * a.ldd + nn : 0;
-      const u32x4_t t = *reinterpret_cast<const u32x4_t*>(a.dy + off);
-      rd[i] = t & (v ? 0xffffffffu : 0u);
+      rd[st][i] = gload16_tr(v ? (const void*)(a.dy + (long long)m * a.ldd + nn) : (const void*)&kZeroTr16);
     }
 #pragma unroll
     for (int i = 0; i < XP; ++i) {
@@ -97,18 +109,17 @@ __global__ void __launch_bounds__(256) wgrad_tr_kernel(WgradArgs a, FastDiv d_ow
       const int ih = (int)oh * a.stride - a.pad + kh;
       const int iw = ow * a.stride - a.pad + kw;
       const bool v = kval && m < me && (unsigned)ih < (unsigned)a.SH && (unsigned)iw < (unsigned)a.SW;
-      const long long off = v ? (((long long)b * a.SH + ih) * a.SW + iw) * a.SC + ci : 0;
-      const u32x4_t t = *reinterpret_cast<const u32x4_t*>(a.src + off);
-      rx[i] = t & (v ? 0xffffffffu : 0u);
+      rx[st][i] = gload16_tr(v ? (const void*)(a.src + (((long long)b * a.SH + ih) * a.SW + iw) * a.SC + ci)
+                               : (const void*)&kZeroTr16);
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, int st) {
     bf16* ds = lds + buf * BM * SN;
     bf16* xs = lds + 2 * BM * SN + buf * BM * SK;
 #pragma unroll
-    for (int i = 0; i < DP; ++i) *reinterpret_cast<u32x4_t*>(ds + (dr + i * DR) * SN + dc * 8) = rd[i];
+    for (int i = 0; i < DP; ++i) *reinterpret_cast<u32x4_t*>(ds + (dr + i * DR) * SN + dc * 8) = rd[st][i];
 #pragma unroll
-    for (int i = 0; i < XP; ++i) *reinterpret_cast<u32x4_t*>(xs + (xr + i * XR) * SK + xc * 8) = rx[i];
+    for (int i = 0; i < XP; ++i) *reinterpret_cast<u32x4_t*>(xs + (xr + i * XR) * SK + xc * 8) = rx[st][i];
   };
 
   f32x4 acc[TN][TK];
@@ -122,38 +133,56 @@ __global__ void __launch_bounds__(256) wgrad_tr_kernel(WgradArgs a, FastDiv d_ow
   const int dro = (4 * g + q) * SN + 4 * p + wn * (BN / WN);
   const int xro = (4 * g + q) * SK + 4 * p + wk * (BK / WK);
   const int nsteps = me > mb ? cdiv(me - mb, BM) : 0;
+  // prologue: step 0 -> LDS[0]; steps 1..D in flight (register stage of step s = s % D)
   if (nsteps > 0) {
-    gload(mb);
-    sstore(0);
+    gload(0, mb);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sstore(0, 0);
+#pragma unroll
+    for (int s = 1; s <= D; ++s)
+      if (s < nsteps) gload(s % D, mb + s * BM);
   }
   __syncthreads();
-  for (int s = 0; s < nsteps; ++s) {
-    const int cur = s & 1;
-    if (s + 1 < nsteps) gload(mb + (s + 1) * BM);
-    const bf16* ds = lds + cur * BM * SN + dro;
-    const bf16* xs = lds + 2 * BM * SN + cur * BM * SK + xro;
+  for (int sb = 0; sb < nsteps; sb += D) {
 #pragma unroll
-    for (int sub = 0; sub < BM / 32; ++sub) {
-      bf16x8 fa[TN], fb[TK];
+    for (int u = 0; u < D; ++u) {
+      const int s = sb + u;
+      if (s < nsteps) {
+        const int cur = s & 1;
+        const bf16* ds = lds + cur * BM * SN + dro;
+        const bf16* xs = lds + 2 * BM * SN + cur * BM * SK + xro;
 #pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        const bf16x4 lo = tr_read(ds + sub * 32 * SN + i * 16);
-        const bf16x4 hi = tr_read(ds + (sub * 32 + 16) * SN + i * 16);
-        fa[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        for (int sub = 0; sub < BM / 32; ++sub) {
+          bf16x8 fa[TN], fb[TK];
+#pragma unroll
+          for (int i = 0; i < TN; ++i) {
+            const bf16x4 lo = tr_read(ds + sub * 32 * SN + i * 16);
+            const bf16x4 hi = tr_read(ds + (sub * 32 + 16) * SN + i * 16);
+            fa[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+#pragma unroll
+          for (int j = 0; j < TK; ++j) {
+            const bf16x4 lo = tr_read(xs + sub * 32 * SK + j * 16);
+            const bf16x4 hi = tr_read(xs + (sub * 32 + 16) * SK + j * 16);
+            fb[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+#pragma unroll
+          for (int i = 0; i < TN; ++i)
+#pragma unroll
+            for (int j = 0; j < TK; ++j) acc[i][j] = mfma16x16x32(fa[i], fb[j], acc[i][j]);
+        }
+        const int nst = (u + 1) % D;  // register stage holding step s + 1
+        if (s + 1 < nsteps) {
+          if (s + D < nsteps)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"((DP + XP) * (D - 1)) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          sstore(cur ^ 1, nst);
+        }
+        __syncthreads();
+        if (s + 1 + D < nsteps) gload(nst, mb + (s + 1 + D) * BM);
       }
-#pragma unroll
-      for (int j = 0; j < TK; ++j) {
-        const bf16x4 lo = tr_read(xs + sub * 32 * SK + j * 16);
-        const bf16x4 hi = tr_read(xs + (sub * 32 + 16) * SK + j * 16);
-        fb[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TK; ++j) acc[i][j] = mfma16x16x32(fa[i], fb[j], acc[i][j]);
     }
-    if (s + 1 < nsteps) sstore(cur ^ 1);
-    __syncthreads();
   }
 
   // C/D layout of the 16x16 MFMA: column (k) = lane & 15, row (n) = 4 * (lane >> 4) + r
