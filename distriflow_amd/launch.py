@@ -324,7 +324,8 @@ def run_async_device(args) -> dict:
         loss, acc = net.evaluate(x[:4096].float() * (1.0 / 255.0 if x.dtype == torch.uint8 else 1.0), y[:4096])
         out = dict(mode="async", engine="device", world=world, steps_per_rank=steps,
                    images_per_s=world * steps * B / max(el, 1e-9), last_loss=float(st[0]) / B,
-                   eval_loss=float(loss), eval_accuracy=float(acc), max_staleness=args.max_staleness, **tr.ps_stats())
+                   eval_loss=float(loss), eval_accuracy=float(acc), max_staleness_bound=args.max_staleness,
+                   **tr.ps_stats())
         log.metric(event="async_done", **out)
         print(json.dumps(out), flush=True)
     shutdown()

@@ -210,12 +210,12 @@ def gap_bwd(dy, dx):
     return dx
 
 
-BN_COUNTERS = 17  # ticket counters of one BN statistics launch: 1 global + 1 per group of 16 (<= 255) workgroups
+BN_COUNTERS = 65  # ticket counters of one BN statistics launch: 1 global + 1 per group of 16 (<= 1024) workgroups
 
 
 def bn_workspace_floats(C: int) -> int:
-    """fp32 workspace of a BN statistics launch of any M: <= 255 partial slabs + <= 16 group slabs of [2][C]."""
-    return (255 + 16) * 2 * C
+    """fp32 workspace of a BN statistics launch of any M: <= 1024 partial slabs + <= 64 group slabs of [2][C]."""
+    return (1024 + 64) * 2 * C
 
 
 def bn_stats_fwd(x2d, mean, invstd, run_mean, run_var, ws, counter, momentum=0.1, eps=1e-5):
