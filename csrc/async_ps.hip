@@ -10,18 +10,20 @@
 // rank maps over xGMI.  There is no server thread and no message loop.  A worker's whole step is
 // device work that it replays from its own hipGraph at its own pace:
 //   ps_fetch_pull  claim the next microbatch id with a remote atomic (the FCFS dispenser), stage its
-//                  example indices, and copy the current weights out under a seqlock (a consistent
-//                  snapshot plus the version it belongs to);
+//                  example indices, and copy the current weights out (a consistent snapshot plus the
+//                  version it belongs to).  The master is triple buffered (version v in buffer v % 3):
+//                  readers never wait for the writer lock and a snapshot is torn only if three new
+//                  versions are published while it is being copied;
 //   (forward / backward kernels of the model)
 //   ps_apply       take the writer lock (seq odd), check staleness = version_now - version_pulled
-//                  against the bound, apply w -= lr * g to the shared master, publish version + 1.
+//                  against the bound, write w[v+1] = w[v] - lr * g into the next buffer, publish v + 1.
 // Every wait is bounded by a wall-clock timeout that sets a sticky error word instead of spinning
 // forever.  Both kernels spread the weights over up to 64 workgroups (one workgroup moves only
 // ~60 GB/s of uncached / remote traffic; a single-workgroup version spent ~11 us per kernel on
 // LeNet-5's 247 KB).  The last-arriving workgroup finishes the protocol (seqlock check, unlock).
 //
-// Shared buffer layout (rank 0): [0] u32 seq (version = seq / 2), [16] u64 batch counter,
-// [256] fp32 master[n].
+// Shared buffer layout (rank 0): [0] u32 seq (version = seq / 2, odd = writer active), [16] u64 batch
+// counter, [256] fp32 master[3][nstride].
 #include "common.h"
 #include "kernels.h"
 
@@ -37,10 +39,10 @@ __device__ __forceinline__ unsigned ld_acq(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Multi-workgroup seqlock snapshot.  Every workgroup copies its slice between two reads of the version
-// word and records the (even) version it saw; the last workgroup to finish checks that all slices saw
-// the same version.  A writer in between (rare: a worker holds the lock for a few microseconds per step)
-// makes the last workgroup redo the whole copy alone under the seqlock loop.
+// Multi-workgroup snapshot.  Every workgroup copies its slice of the committed version's buffer between
+// two reads of the version word and records the version; the last workgroup to finish checks that all
+// slices copied the same version.  A version published in between (a worker commits every few
+// microseconds at 8 ranks) makes the last workgroup redo the whole copy of one version alone.
 __device__ void copy_slice(const float* __restrict__ src, float* __restrict__ dst, long long lo, long long hi,
                            int t, int nt) {
   const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
@@ -94,32 +96,31 @@ __global__ __launch_bounds__(kPSBlock) void ps_fetch_pull_kernel(PSArgs a) {
   const long long per = ((a.n + 4LL * G - 1) / (4LL * G)) * 4;  // slice length, multiple of 4
   const long long lo = b * per, hi = lo + per < a.n ? lo + per : a.n;
   const unsigned long long t0 = wall_clock64();
+  // Version v lives in buffer v % 3; the writer of v + 1 writes buffer (v + 1) % 3, so a copy of
+  // version v stays valid until a writer of v + 3 starts, i.e. while seq <= 2v + 4.  A reader never
+  // waits for the writer lock.
   for (;;) {
     if (t == 0) {
-      unsigned s = ld_acq(a.seq);
-      while ((s & 1u) && wall_clock64() - t0 <= (unsigned long long)a.timeout_ticks) {
-        __builtin_amdgcn_s_sleep(2);
-        s = ld_acq(a.seq);
-      }
-      s_seq = s;
-      s_state = (s & 1u) ? 2 : 0;
+      const unsigned s = ld_acq(a.seq);
+      s_seq = s >> 1;  // committed version
     }
     __syncthreads();
-    if (s_state == 2) break;
-    if (lo < hi) copy_slice(a.ps_w, a.w, lo, hi, t, kPSBlock);
+    const unsigned v = s_seq;
+    if (lo < hi) copy_slice(a.ps_w + (long long)(v % 3u) * a.nstride, a.w, lo, hi, t, kPSBlock);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // slice loads complete before the re-check
     __syncthreads();
     if (t == 0) {
-      if (ld_acq(a.seq) == s_seq) s_state = 1;
+      if (ld_acq(a.seq) <= 2u * v + 4u) s_state = 1;
       else if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) s_state = 2;
+      else s_state = 0;
     }
     __syncthreads();
     if (s_state != 0) break;
-    __syncthreads();  // every thread has read s_state before thread 0 rewrites it
+    __syncthreads();  // every thread has read s_state / s_seq before thread 0 rewrites them
   }
-  // publish this slice's version (or an odd "failed" marker) and elect the last workgroup
+  // publish this slice's version (or a "failed" marker) and elect the last workgroup
   if (t == 0) {
-    a.scratch[kPSSlots + b] = s_state == 1 ? s_seq : 1u;
+    a.scratch[kPSSlots + b] = s_state == 1 ? s_seq : 0xffffffffu;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const unsigned prev = __hip_atomic_fetch_add(a.scratch + kPSPullDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     s_last = prev == (unsigned)G - 1;
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(kPSBlock) void ps_fetch_pull_kernel(PSArgs a) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (t == 0) {
     const unsigned v0 = __hip_atomic_load(a.scratch + kPSSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int same = !(v0 & 1u);
+    int same = v0 != 0xffffffffu;
     for (int i = 1; i < G && same; ++i)
       same = __hip_atomic_load(a.scratch + kPSSlots + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v0;
     s_state = same ? 1 : 0;
@@ -138,37 +139,27 @@ __global__ __launch_bounds__(kPSBlock) void ps_fetch_pull_kernel(PSArgs a) {
   }
   __syncthreads();
   if (s_state == 1) {
-    if (t == 0) *a.vpulled = s_seq >> 1;
+    if (t == 0) *a.vpulled = s_seq;
     return;
   }
-  // torn snapshot across slices: redo the whole copy in this workgroup
+  // slices of different versions: redo the whole copy of one version in this workgroup
   if (t == 0) a.stats[4] += 1;
   for (;;) {
-    if (t == 0) {
-      unsigned s = ld_acq(a.seq);
-      while ((s & 1u) && wall_clock64() - t0 <= (unsigned long long)a.timeout_ticks) {
-        __builtin_amdgcn_s_sleep(2);
-        s = ld_acq(a.seq);
-      }
-      s_seq = s;
-      s_state = (s & 1u) ? 2 : 0;
-    }
+    if (t == 0) s_seq = ld_acq(a.seq) >> 1;
     __syncthreads();
-    if (s_state == 2) {
-      if (t == 0) atomicOr(a.stats + 5, 1ull);
-      return;
-    }
-    copy_slice(a.ps_w, a.w, 0, a.n, t, kPSBlock);
+    const unsigned v = s_seq;
+    copy_slice(a.ps_w + (long long)(v % 3u) * a.nstride, a.w, 0, a.n, t, kPSBlock);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     __syncthreads();
     if (t == 0) {
-      if (ld_acq(a.seq) == s_seq) {
+      s_state = 0;
+      if (ld_acq(a.seq) <= 2u * v + 4u) {
         s_state = 1;
-        *a.vpulled = s_seq >> 1;
+        *a.vpulled = v;
       } else if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) {
         atomicOr(a.stats + 5, 2ull);
         s_state = 1;
-        *a.vpulled = s_seq >> 1;
+        *a.vpulled = v;
       }
     }
     __syncthreads();
@@ -241,7 +232,9 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
     const long long per = ((a.n + 4LL * G - 1) / (4LL * G)) * 4;
     const long long lo = b * per, hi = lo + per < a.n ? lo + per : a.n;
     const float lr = a.lr;
-    f32x4* w = reinterpret_cast<f32x4*>(a.ps_w);
+    const unsigned v = s_seq >> 1;  // version being replaced: buffer v % 3 -> buffer (v + 1) % 3
+    const f32x4* w = reinterpret_cast<const f32x4*>(a.ps_w + (long long)(v % 3u) * a.nstride);
+    f32x4* wn = reinterpret_cast<f32x4*>(a.ps_w + (long long)((v + 1u) % 3u) * a.nstride);
     const f32x4* g = reinterpret_cast<const f32x4*>(a.g);
     for (long long base = (lo >> 2) + t; base < (hi >> 2); base += (long long)kPSBlock * kPSUnroll) {
       f32x4 v[kPSUnroll], gv[kPSUnroll];
@@ -256,7 +249,7 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
 #pragma unroll
       for (int u = 0; u < kPSUnroll; ++u) {
         const long long i = base + (long long)u * kPSBlock;
-        if (i < (hi >> 2)) w[i] = v[u] - lr * gv[u];
+        if (i < (hi >> 2)) wn[i] = v[u] - lr * gv[u];
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this slice's weight stores visible system-wide

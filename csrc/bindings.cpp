@@ -772,7 +772,7 @@ class PSComm {
     check_hip(hipGetDevice(&dev_), "ps getDevice");
     if (rank_ == server_) {
       void* p = nullptr;
-      const size_t bytes = 256 + (size_t)n * 4;
+      const size_t bytes = 256 + 3 * (size_t)nstride() * 4;
       hipError_t e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
       if (e != hipSuccess) {
         (void)hipGetLastError();
@@ -806,7 +806,8 @@ class PSComm {
     check_hip(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
     shared_ = (char*)p;
   }
-  // server only: seed the shared master (before any worker pulls)
+  int64_t nstride() const { return (n_ + 63) / 64 * 64; }
+  // server only: seed the shared master (before any worker pulls): version 0 lives in buffer 0
   void init_master(torch::Tensor w) {
     TORCH_CHECK(rank_ == server_ && shared_, "ps: init_master on the server rank");
     need(w, at::kFloat, "ps master");
@@ -852,10 +853,15 @@ class PSComm {
     return {(int64_t)h[0], (int64_t)h[1], (int64_t)h[2], (int64_t)h[3], (int64_t)h[4], (int64_t)h[5],
             (int64_t)(seq >> 1), (int64_t)ctr};
   }
+  // copy of the committed version (call while no worker is stepping)
   void copy_master(torch::Tensor dst) const {
     need(dst, at::kFloat, "ps dst");
     TORCH_CHECK(dst.numel() == n_, "ps: dst size mismatch");
-    check_hip(hipMemcpyAsync(dst.data_ptr(), shared_ + 256, (size_t)n_ * 4, hipMemcpyDeviceToDevice, cur_stream()),
+    check_hip(hipDeviceSynchronize(), "ps copy_master sync");
+    unsigned seq = 0;
+    check_hip(hipMemcpy(&seq, shared_, 4, hipMemcpyDeviceToHost), "ps seq");
+    const size_t off = 256 + (size_t)((seq >> 1) % 3u) * nstride() * 4;
+    check_hip(hipMemcpyAsync(dst.data_ptr(), shared_ + off, (size_t)n_ * 4, hipMemcpyDeviceToDevice, cur_stream()),
               "ps copy_master");
   }
 
@@ -867,6 +873,7 @@ class PSComm {
     a.batch_ctr = reinterpret_cast<unsigned long long*>(shared_ + 16);
     a.ps_w = reinterpret_cast<float*>(shared_ + 256);
     a.n = n_;
+    a.nstride = nstride();
     a.vpulled = reinterpret_cast<unsigned*>(local_);
     a.bid_out = reinterpret_cast<long long*>(local_ + 8);
     a.stats = reinterpret_cast<unsigned long long*>(local_ + 64);

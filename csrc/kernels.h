@@ -201,7 +201,7 @@ hipError_t p2p_allreduce(const P2PArgs& a, hipStream_t st);
 struct PSArgs {
   unsigned* seq;                // seqlock word: odd = writer active, version = seq / 2
   unsigned long long* batch_ctr;  // FCFS microbatch counter
-  float* ps_w;                  // shared fp32 master [n]
+  float* ps_w;                  // shared fp32 master, triple buffered [3][nstride] (version v in buffer v % 3)
   float* w;                     // local fp32 master [n] (pull destination)
   const float* g;               // local fp32 gradient [n]
   long long n;
@@ -211,7 +211,7 @@ struct PSArgs {
   const long long* perm;        // [nbatches][B] example ids (nullptr: no index staging)
   long long* idx;               // [B] staged ids of the claimed microbatch
   long long* bid_out;           // local: id of the claimed microbatch
-  long long nbatches, timeout_ticks;
+  long long nbatches, timeout_ticks, nstride;
   int B, max_stale;
   float lr;
 };
