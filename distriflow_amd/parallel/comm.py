@@ -46,8 +46,13 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, de
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_gpu = (device or ("cuda" if torch.cuda.is_available() else "cpu")).startswith("cuda")
+    # DISTRIFLOW_BACKEND=gloo on a GPU box: rehearsal mode, several ranks may share a GPU (rank r on
+    # GPU r % device_count) with gloo as the control plane; RCCL refuses two ranks on one device
+    backend = backend or os.environ.get("DISTRIFLOW_BACKEND") or None
     if backend is None:
         backend = "nccl" if use_gpu else "gloo"
+    if use_gpu and backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     dev = torch.device(f"cuda:{local}") if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(dev)
