@@ -19,8 +19,42 @@ from . import reference as ref
 MODE_DIRECT, MODE_FWD, MODE_DGRAD = 0, 1, 2
 
 
+class _DebugSync:
+    """``DISTRIFLOW_DEBUG_SYNC=1``: every kernel entry point is followed by a device
+    synchronize outside graph capture, so an asynchronous fault or a race between streams is reported
+    at the op that caused it (combine with ``AMD_SERIALIZE_KERNEL=3`` set before the first HIP call)."""
+
+    def __init__(self, mod):
+        self._mod = mod
+
+    def __getattr__(self, name):
+        fn = getattr(self._mod, name)
+        if not callable(fn) or isinstance(fn, type):
+            return fn
+
+        def wrapped(*args, **kw):
+            out = fn(*args, **kw)
+            if torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+                try:
+                    torch.cuda.synchronize()
+                except RuntimeError as e:
+                    raise RuntimeError(f"distriflow_amd kernel '{name}' failed: {e}") from e
+            return out
+
+        return wrapped
+
+
+_DEBUG = None
+
+
 def _C():
-    return native.require()
+    global _DEBUG
+    mod = native.require()
+    if _DEBUG is None:
+        import os
+
+        _DEBUG = os.environ.get("DISTRIFLOW_DEBUG_SYNC", "0") == "1"
+    return _DebugSync(mod) if _DEBUG else mod
 
 
 def _geom(SH=1, SW=1, SC=1, OH=1, OW=1, KH=1, KW=1, stride=1, pad=0):
