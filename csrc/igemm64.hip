@@ -47,10 +47,10 @@ __device__ __forceinline__ u32x4_t gload16(const void* p) {
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
-// occupancy the LDS footprint allows (2 x (BM + BN) x 128 B per workgroup): 3 workgroups of 48 KB or
-// 2 of 64 KB per CU; the register budget is capped to match (one workgroup = one wave per SIMD)
+// occupancy the LDS footprint allows (2 x (BM + BN) x 128 B per workgroup): 4 workgroups of 40 KB, 3 of
+// 48 KB or 2 of 64 KB per CU; the register budget is capped to match (one workgroup = one wave per SIMD)
 template <int BM, int BN>
-constexpr int igemm64_occ() { return (BM + BN) * 256 > 60 * 1024 ? 2 : 3; }
+constexpr int igemm64_occ() { return (160 * 1024) / ((BM + BN) * 256) > 4 ? 4 : (160 * 1024) / ((BM + BN) * 256); }
 
 template <int BM, int BN, int MODE, int D>
 __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(IGemmArgs a, FastDiv d_ow, FastDiv d_ohw) {
@@ -301,6 +301,7 @@ hipError_t launch64(const IGemmArgs& a, hipStream_t st) {
 
 template <int MODE>
 hipError_t launch64_mode(const IGemmArgs& a, hipStream_t st) {
+  if (a.N <= 32) return launch64<128, 32, MODE>(a, st);  // Keras CNN conv2 (32 channels): no half-empty tiles
   if (a.N <= 64) return launch64<128, 64, MODE>(a, st);
   // 128x128 while that still gives >= 2 workgroups per CU, else 64x128
   if ((long long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 512) return launch64<128, 128, MODE>(a, st);

@@ -11,6 +11,7 @@
 //   * workgroup = BN x BK output tile, 4 waves as WN x WK, m-steps of 64 rows, two LDS buffers and a
 //     2-step register prefetch (inline-asm loads, hand-counted vmcnt), one barrier per step
 //   * m is split over workgroups (split-m); slab_reduce sums the slabs in a fixed order
+//   * a conv bias gradient is one more k chunk whose first element reads 1.0 (column K of G)
 //   * LDS row stride = 8 x odd dwords (mod 64): the 8 rows one 32-lane half reads with a
 //     transposed read sit on 8 disjoint 8-bank groups (conflict-free), and 8 lanes storing the 8
 //     consecutive 16-byte chunks of a row cover the 32 store banks once
@@ -40,6 +41,8 @@ __device__ __forceinline__ bf16x4 tr_read(const bf16* p) {
 constexpr int tr_stride(int cols) { return cols + (((cols / 16) % 2) ? 0 : 16); }
 
 __device__ u32x4_t kZeroTr16 = {0u, 0u, 0u, 0u};  // source of every masked-out 16-byte chunk
+// bias gradient = column of ones appended to X at k = K (bf16 1.0 = 0x3F80 in element 0 of the chunk)
+__device__ u32x4_t kOneTr16 = {0x3F80u, 0u, 0u, 0u};
 
 // Operand loads from inline asm with hand-counted waits (see igemm64.hip: hipcc's loop-carried
 // vmcnt waits otherwise collapse the register prefetch to one step).
@@ -51,9 +54,16 @@ __device__ __forceinline__ u32x4_t gload16_tr(const void* p) {
 
 constexpr int kWgradStages = 2;  // register prefetch depth (m-steps in flight)
 
-// two workgroups per CU fit the LDS (57-74 KB each): cap registers at two waves per SIMD
+// workgroups per CU the LDS allows (2 x 64 rows x (SN + SK) bf16 each): register cap to match
+template <int BN, int BK>
+constexpr int wgrad_tr_occ() {
+  return (160 * 1024) / (2 * 64 * (tr_stride(BN) + tr_stride(BK)) * 2) > 4
+             ? 4
+             : (160 * 1024) / (2 * 64 * (tr_stride(BN) + tr_stride(BK)) * 2);
+}
+
 template <int BN, int BK, int WN, int WK>
-__global__ void __launch_bounds__(256, 2) wgrad_tr_kernel(WgradArgs a, FastDiv d_ow, FastDiv d_ohw) {
+__global__ void __launch_bounds__(256, (wgrad_tr_occ<BN, BK>())) wgrad_tr_kernel(WgradArgs a, FastDiv d_ow, FastDiv d_ohw) {
   constexpr int D = kWgradStages;
   constexpr int BM = 64;
   constexpr int SN = tr_stride(BN), SK = tr_stride(BK);
@@ -66,7 +76,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_tr_kernel(WgradArgs a, FastDiv d
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wn = wid / WK, wk = wid % WK;
-  const int ntk = cdiv(a.K, BK);
+  const int Kt = a.K + (a.with_bias ? 1 : 0);   // output columns (bias gradient = column K)
+  const int ntk = cdiv(a.K + (a.with_bias ? 8 : 0), BK);
   const int ntiles = cdiv(a.N, BN) * ntk;
   // tile fastest: the workgroups an XCD runs together share one m range (the same dY / X rows)
   const int logical = xcd_remap(blockIdx.x, ntiles * a.splits);
@@ -81,6 +92,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_tr_kernel(WgradArgs a, FastDiv d
   const int xc = tid % XC, xr = tid / XC;
   const int kk = k0 + xc * 8;
   const bool kval = kk < a.K;
+  const bool kbias = a.with_bias && kk == a.K;
   int kh = 0, kw = 0, ci = 0;
   if (kval) {
     ci = kk % a.SC;
@@ -110,7 +122,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_tr_kernel(WgradArgs a, FastDiv d
       const int iw = ow * a.stride - a.pad + kw;
       const bool v = kval && m < me && (unsigned)ih < (unsigned)a.SH && (unsigned)iw < (unsigned)a.SW;
       rx[st][i] = gload16_tr(v ? (const void*)(a.src + (((long long)b * a.SH + ih) * a.SW + iw) * a.SC + ci)
-                               : (const void*)&kZeroTr16);
+                               : (kbias && m < me) ? (const void*)&kOneTr16 : (const void*)&kZeroTr16);
     }
   };
   auto sstore = [&](int buf, int st) {
@@ -192,15 +204,17 @@ __global__ void __launch_bounds__(256, 2) wgrad_tr_kernel(WgradArgs a, FastDiv d
 #pragma unroll
     for (int j = 0; j < TK; ++j) {
       const int k = k0 + wk * (BK / WK) + j * 16 + li;
-      if (k >= a.K) continue;
+      if (k >= Kt) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + wn * (BN / WN) + i * 16 + 4 * g + r;
         if (n >= a.N) continue;
         if (a.splits > 1)
-          a.partial[((long long)split * a.N + n) * a.K + k] = acc[i][j][r];
-        else
+          a.partial[((long long)split * a.N + n) * Kt + k] = acc[i][j][r];
+        else if (k < a.K)
           a.gw[(long long)n * a.K + k] = acc[i][j][r] * a.scale;
+        else
+          a.gb[n] = acc[i][j][r] * a.scale;
       }
     }
   }
@@ -208,12 +222,13 @@ __global__ void __launch_bounds__(256, 2) wgrad_tr_kernel(WgradArgs a, FastDiv d
 
 template <int BN, int BK, int WN, int WK>
 hipError_t launch_wgrad_tr(WgradArgs a, float* ws, size_t ws_floats, hipStream_t st) {
-  const int tiles = cdiv(a.N, BN) * cdiv(a.K, BK);
+  const int Kt = a.K + (a.with_bias ? 1 : 0);
+  const int tiles = cdiv(a.N, BN) * cdiv(a.K + (a.with_bias ? 8 : 0), BK);
   // about two workgroups per CU (73.7 KB of LDS each), each reducing >= 256 rows
   int splits = cdiv(512, tiles);
   splits = min(splits, cdiv(a.M, 256));
   splits = max(splits, 1);
-  while (splits > 1 && (size_t)splits * a.N * a.K > ws_floats) --splits;
+  while (splits > 1 && (size_t)splits * a.N * Kt > ws_floats) --splits;
   a.m_per_split = round_up(cdiv(a.M, splits), 64);
   splits = cdiv(a.M, a.m_per_split);
   a.splits = splits;
@@ -221,19 +236,20 @@ hipError_t launch_wgrad_tr(WgradArgs a, float* ws, size_t ws_floats, hipStream_t
   const FastDiv d_ow = make_fastdiv((unsigned)a.OW), d_ohw = make_fastdiv((unsigned)(a.OH * a.OW));
   hipLaunchKernelGGL((wgrad_tr_kernel<BN, BK, WN, WK>), dim3(tiles * splits), dim3(256), 0, st, a, d_ow, d_ohw);
   DFA_HIP_CHECK(hipGetLastError());
-  if (splits > 1) DFA_HIP_CHECK(slab_reduce(ws, a.gw, nullptr, a.N, a.K, a.K, splits, a.scale, st));
+  if (splits > 1) DFA_HIP_CHECK(slab_reduce(ws, a.gw, a.with_bias ? a.gb : nullptr, a.N, a.K, Kt, splits, a.scale, st));
   return hipSuccess;
 }
 
 }  // namespace
 
 bool wgrad_tr_supported(const WgradArgs& a, int mode) {
-  return mode == MODE_FWD && !a.with_bias && a.SC % 8 == 0 && a.N % 8 == 0 && a.ldd % 8 == 0 && a.M > 0 &&
+  return mode == MODE_FWD && (!a.with_bias || a.gb != nullptr) && a.SC % 8 == 0 && a.N % 8 == 0 && a.ldd % 8 == 0 && a.M > 0 &&
          a.OH > 0 && a.OW > 0 && ((uintptr_t)a.dy & 15) == 0 && ((uintptr_t)a.src & 15) == 0;
 }
 
 hipError_t wgrad_tr(const WgradArgs& a, float* ws, size_t ws_floats, hipStream_t st) {
   if (a.N >= 128) return launch_wgrad_tr<128, 128, 2, 2>(a, ws, ws_floats, st);
+  if (a.N <= 32) return launch_wgrad_tr<32, 128, 1, 4>(a, ws, ws_floats, st);  // Keras CNN conv2: no empty rows
   return launch_wgrad_tr<64, 128, 2, 2>(a, ws, ws_floats, st);
 }
 

@@ -202,6 +202,23 @@ def test_conv_wgrad_transposed_reads(B, H, W, C, N, k, s, p):
     _close(gw, 0.5 * ew, 1e-3, 1e-3)
 
 
+@pytest.mark.parametrize("B,H,W,C,N,k,s,p", [(64, 26, 26, 32, 32, 3, 1, 0), (8, 16, 16, 64, 128, 3, 2, 1),
+                                              (3, 9, 7, 16, 24, 3, 2, 1)])
+def test_conv_wgrad_transposed_reads_with_bias(B, H, W, C, N, k, s, p):
+    """Conv bias gradient on the transposed-read kernel: an extra k chunk of ones (column K), split-m
+    slabs included (the Keras CNN conv2 shape)."""
+    OH, OW = ops.conv_out_hw(H, W, k, k, s, p)
+    dy = torch.randn(B, OH, OW, N, device=dev).to(torch.bfloat16)
+    x = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    gw = torch.full((N, k * k * C), float("nan"), device=dev)
+    gb = torch.full((N,), float("nan"), device=dev)
+    ws = torch.empty(1 << 24, device=dev)
+    ops.conv_wgrad(dy, x, gw, gb, ws, k, k, s, p, scale=0.5)
+    ew, eb = ref.conv_wgrad(dy.float(), x.float(), k, k, s, p)
+    _close(gw, 0.5 * ew, 1e-3, 1e-3)
+    _close(gb, 0.5 * eb, 1e-3, 1e-3)
+
+
 def test_conv_wgrad_large_m_split():
     """Tall-skinny reduction (K = B*OH*OW = 1.3M) exercising many split-m slabs + the reduce kernel."""
     B, H, W, C, N, k = 512, 28, 28, 1, 6, 5
