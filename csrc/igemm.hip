@@ -533,6 +533,7 @@ static hipError_t launch_fwd_mode(const IGemmArgs& a, hipStream_t st) {
 hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0) return hipSuccess;
   if (igemm64_supported(a, mode)) return igemm64(a, mode, st);
+  if (smallc_fwd_supported(a, mode)) return smallc_fwd(a, st);
   const bool aligned = ((uintptr_t)a.src & 15) == 0;
   if (mode == MODE_DIRECT) {
     const bool vec = aligned && a.lda % 8 == 0 && a.K % 8 == 0;
@@ -587,6 +588,7 @@ hipError_t igemm_wgrad(const WgradArgs& a, int mode, float* workspace, size_t ws
     return launch_wgrad_x<MODE_DIRECT>(a, dvec, xvec, workspace, ws_floats, st);
   }
   if (wgrad_tr_supported(a, mode)) return wgrad_tr(a, workspace, ws_floats, st);
+  if (smallc_wgrad_supported(a, mode)) return smallc_wgrad(a, workspace, ws_floats, st);
   const bool xvec = ((uintptr_t)a.src & 15) == 0 && a.SC % 8 == 0;
   return launch_wgrad_x<MODE_FWD>(a, dvec, xvec, workspace, ws_floats, st);
 }

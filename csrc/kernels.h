@@ -219,4 +219,11 @@ constexpr int kPSMaxGrid = 64;
 hipError_t ps_fetch_pull(const PSArgs& a, hipStream_t st);
 hipError_t ps_apply(const PSArgs& a, hipStream_t st);
 
+
+// Direct convolution for C_in <= 4 (csrc/smallc.hip); igemm_fwd / igemm_wgrad dispatch to it.
+bool smallc_fwd_supported(const IGemmArgs& a, int mode);
+hipError_t smallc_fwd(const IGemmArgs& a, hipStream_t st);
+bool smallc_wgrad_supported(const WgradArgs& a, int mode);
+hipError_t smallc_wgrad(const WgradArgs& a, float* ws, size_t ws_floats, hipStream_t st);
+
 }  // namespace dfa
