@@ -227,12 +227,14 @@ class FederatedClient(AbstractWorker):
         self.y = torch.empty((0,), dtype=torch.int64, device=dev)
 
     def distributed_update(self, x: torch.Tensor, y: torch.Tensor):
-        x = x.to(self.x.device, self.x.dtype).reshape((-1,) + tuple(self.x.shape[1:]))
+        from ..utils.tensors import add_rows, slice_with_empty
+
         y = y.to(self.y.device)
-        if y.dim() > 1:
-            y = y.argmax(dim=1)
-        self.x = torch.cat([self.x, x])
-        self.y = torch.cat([self.y, y.long().reshape(-1)])
+        single = tuple(x.shape) == tuple(self.x.shape[1:])  # one example (reference addRows accepts both)
+        if y.dim() > 1 or (single and y.numel() > 1):  # one-hot labels -> class ids
+            y = y.argmax(dim=-1)
+        self.x = add_rows(self.x, x.to(self.x.device, self.x.dtype), self.x.shape[1:])
+        self.y = add_rows(self.y, y.long().reshape(-1), ())
         per = int(self.hyperparam("examplesPerUpdate"))
         while self.x.shape[0] >= per:
             self.poll(0.0)
@@ -243,7 +245,7 @@ class FederatedClient(AbstractWorker):
             grad = self.time("Fit model", lambda: self.model.fit_flat(xt, yt))
             self._upload(grad, vid, metrics=metrics, num_examples=per)
             self.version_update_counts[version] = self.version_update_counts.get(version, 0) + 1
-            self.x, self.y = self.x[per:], self.y[per:]
+            self.x, self.y = slice_with_empty(self.x, per), slice_with_empty(self.y, per)
         self.poll(0.0)
 
     DistributedUpdate = distributed_update

@@ -61,3 +61,26 @@ def test_header_round_trip():
     assert d["metrics"] == [0.5, 0.25] and d["num_examples"] == 32
     assert d["payloads"] == [(torch.float32, 10), (torch.int64, 3)]
     assert P.payload_json(P.json_payload({"a": [1, 2]})) == {"a": [1, 2]}
+
+
+def test_client_buffer_utils():
+    """Reference src/client/utils.ts:22-47 (concat/slice with empty tensors, addRows single or batch)."""
+    import pytest as _pytest
+
+    from distriflow_amd.utils.tensors import add_rows, concat_with_empty, slice_with_empty, wait_for
+
+    e = torch.empty(0, 2, 2)
+    one = torch.ones(2, 2)
+    b = add_rows(e, one, (2, 2))
+    assert b.shape == (1, 2, 2)
+    b = add_rows(b, torch.zeros(3, 2, 2), (2, 2))
+    assert b.shape == (4, 2, 2) and b[0].sum() == 4
+    with _pytest.raises(ValueError):
+        add_rows(b, torch.zeros(3, 3), (2, 2))
+    assert concat_with_empty(e, b).shape == (4, 2, 2) and concat_with_empty(b, e).shape == (4, 2, 2)
+    assert slice_with_empty(b, 3).shape == (1, 2, 2) and slice_with_empty(b, 9).shape == (0, 2, 2)
+    assert slice_with_empty(b, 1, 2).shape == (2, 2, 2)
+    hits = iter([None, None, 7])
+    assert wait_for(lambda: next(hits), timeout=1.0) == 7
+    with _pytest.raises(TimeoutError):
+        wait_for(lambda: None, timeout=0.01)
