@@ -499,9 +499,9 @@ void convpool_fwd_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double s
             "convpool_fwd");
 }
 
-void convpool_wgrad_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double scale, torch::Tensor dp,
-                       torch::Tensor code, torch::Tensor gw, c10::optional<torch::Tensor> gb, torch::Tensor ws,
-                       std::vector<int64_t> geom) {
+int64_t convpool_wgrad_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double scale, torch::Tensor dp,
+                          torch::Tensor code, torch::Tensor gw, c10::optional<torch::Tensor> gb, torch::Tensor ws,
+                          std::vector<int64_t> geom, bool defer) {
   TORCH_CHECK(geom.size() == 8, "geom = [B,H,W,C,KH,KW,pad,N]");
   const int B = geom[0], H = geom[1], W = geom[2], C = geom[3], KH = geom[4], KW = geom[5], pad = geom[6], N = geom[7];
   TORCH_CHECK(dfa::convpool_supported(H, W, C, KH, KW, pad, N), "convpool: unsupported geometry");
@@ -520,10 +520,43 @@ void convpool_wgrad_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double
     gbp = gb->data_ptr<float>();
   }
   need(ws, at::kFloat, "workspace");
+  int slabs = 0;
   check_hip(dfa::convpool_wgrad(in.x, in.u8, in.idx, in.nrows, (float)scale, B, H, W, C, KH, KW, pad, N,
                                 (const dfa::bf16*)dp.data_ptr(), code.data_ptr<uint8_t>(), gw.data_ptr<float>(), gbp,
-                                ws.data_ptr<float>(), (size_t)ws.numel(), cur_stream()),
+                                ws.data_ptr<float>(), (size_t)ws.numel(), cur_stream(), defer ? &slabs : nullptr),
             "convpool_wgrad");
+  return slabs;  // > 0: the slab reduction was deferred (run it with slab_reduce_multi)
+}
+
+// One launch for several deferred slab reductions: segs = [(partial, gw, gb|None, N, K, Kt, S, scale), ...]
+void slab_reduce_multi_py(std::vector<py::tuple> segs) {
+  TORCH_CHECK(!segs.empty() && (int)segs.size() <= dfa::kMaxSlabSegs, "slab_reduce_multi: 1..8 segments");
+  dfa::SlabSegs ss{};
+  ss.n = (int)segs.size();
+  for (size_t i = 0; i < segs.size(); ++i) {
+    const py::tuple& t = segs[i];
+    TORCH_CHECK(t.size() == 8, "segment = (partial, gw, gb, N, K, Kt, S, scale)");
+    auto partial = t[0].cast<torch::Tensor>();
+    auto gw = t[1].cast<torch::Tensor>();
+    const int N = t[3].cast<int>(), K = t[4].cast<int>(), Kt = t[5].cast<int>(), S = t[6].cast<int>();
+    need(partial, at::kFloat, "partial");
+    need(gw, at::kFloat, "gw");
+    TORCH_CHECK(N > 0 && K > 0 && Kt >= K && S > 0, "slab_reduce_multi: bad segment sizes");
+    TORCH_CHECK(partial.numel() >= (int64_t)S * N * Kt && gw.numel() >= (int64_t)N * K, "slab_reduce_multi: buffers too small");
+    dfa::SlabSeg& sg = ss.s[i];
+    sg.partial = partial.data_ptr<float>();
+    sg.gw = gw.data_ptr<float>();
+    sg.gb = nullptr;
+    if (!t[2].is_none()) {
+      auto gb = t[2].cast<torch::Tensor>();
+      need(gb, at::kFloat, "gb");
+      TORCH_CHECK(gb.numel() >= N, "gb too small");
+      sg.gb = gb.data_ptr<float>();
+    }
+    sg.N = N; sg.K = K; sg.Kt = Kt; sg.S = S;
+    sg.scale = t[7].cast<float>();
+  }
+  check_hip(dfa::slab_reduce_multi(ss, cur_stream()), "slab_reduce_multi");
 }
 
 void convpool_dgrad_py(torch::Tensor dp, torch::Tensor code, torch::Tensor wt, torch::Tensor dx,
@@ -918,7 +951,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_dx", &bn_dx_py, "BN input gradient dx = k1*g + k2*x + k3");
   m.def("bn_stats_grid", &dfa::bn_stats_grid, "partial-slab count of a BN statistics launch");
   m.def("convpool_fwd", &convpool_fwd_py, "fused conv+bias+relu+maxpool2x2 (pooled map + argmax codes)");
-  m.def("convpool_wgrad", &convpool_wgrad_py, "weight gradient through the fused conv+pool");
+  m.def("convpool_wgrad", &convpool_wgrad_py, "weight gradient through the fused conv+pool", py::arg("x"),
+        py::arg("idx"), py::arg("scale"), py::arg("dp"), py::arg("code"), py::arg("gw"), py::arg("gb"), py::arg("ws"),
+        py::arg("geom"), py::arg("defer") = false);
+  m.def("slab_reduce_multi", &slab_reduce_multi_py, "several deferred split-m slab reductions in one launch");
   m.def("convpool_dgrad", &convpool_dgrad_py, "data gradient through the fused conv+pool");
   m.def("convpool_set_debug", &dfa::convpool_set_debug, "profiling aid: skip kernel phases (bit mask)");
   m.def("convpool_set_stamps", [](c10::optional<torch::Tensor> buf) {

@@ -1086,6 +1086,50 @@ __global__ void __launch_bounds__(256) slab_reduce_thread_kernel(const float* __
   slab_store(gw, gb, o, K, Kt, ((a0 + a1) + (a2 + a3)) * scale);
 }
 
+// Several layers' slab reductions in ONE launch (deferred convpool weight gradients): workgroup b
+// serves segment i for b in [block0_i, block0_{i+1}); same per-output fixed summation order as
+// slab_reduce_wave_kernel, so the result is bit-identical to separate launches.
+__global__ void __launch_bounds__(1024) slab_reduce_multi_kernel(SlabSegs segs) {
+  __shared__ float red[16][64];
+  int si = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxSlabSegs; ++i)
+    if (i < segs.n && (int)blockIdx.x >= segs.s[i].block0) si = i;
+  const SlabSeg sg = segs.s[si];
+  const int total = sg.N * sg.Kt;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int o = ((int)blockIdx.x - sg.block0) * 64 + lane;
+  const int oc = min(o, total - 1);
+  float a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = 0.f;
+  int p = wv;
+  for (; p + 7 * 16 < sg.S; p += 8 * 16) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += sg.partial[(long long)(p + 16 * j) * total + oc];
+  }
+  for (; p < sg.S; p += 16) a[0] += sg.partial[(long long)p * total + oc];
+  red[wv][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (wv == 0 && o < total) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) v += red[w][lane];
+    slab_store(sg.gw, sg.gb, o, sg.K, sg.Kt, v * sg.scale);
+  }
+}
+
+hipError_t slab_reduce_multi(SlabSegs segs, hipStream_t st) {
+  if (segs.n <= 0 || segs.n > kMaxSlabSegs) return hipErrorInvalidValue;
+  int blocks = 0;
+  for (int i = 0; i < segs.n; ++i) {
+    segs.s[i].block0 = blocks;
+    blocks += cdiv(segs.s[i].N * segs.s[i].Kt, 64);
+  }
+  hipLaunchKernelGGL(slab_reduce_multi_kernel, dim3(blocks), dim3(1024), 0, st, segs);
+  return hipGetLastError();
+}
+
 hipError_t slab_reduce(const float* partial, float* gw, float* gb, int N, int K, int Kt, int S, float scale,
                        hipStream_t st) {
   const int total = N * Kt;
@@ -1445,7 +1489,7 @@ static CPWg make_wg(const CPGeom& g) {
 template <int NT, int KTMAX>
 static hipError_t launch_cp_wgrad(CPGeom g, bool vec, const void* x, int x_u8, const long long* idx, long long nrows,
                                   float scale, const bf16* dp, const uint8_t* code, float* gw, float* gb,
-                                  float* workspace, size_t ws_floats, hipStream_t st) {
+                                  float* workspace, size_t ws_floats, hipStream_t st, int* deferred) {
   auto kern = convpool_wgrad_kernel<NT, KTMAX, kStageChunks>;
   const CPWg q = make_wg(g);
   const int Kt = g.K + 1;
@@ -1463,12 +1507,16 @@ static hipError_t launch_cp_wgrad(CPGeom g, bool vec, const void* x, int x_u8, c
   hipLaunchKernelGGL(kern, dim3(z.grid), dim3(256), z.lds, st, g, q, (int)vec, x, x_u8, idx, nrows, scale, dp, code,
                      workspace);
   DFA_HIP_CHECK(hipGetLastError());
+  if (deferred) {  // the caller batches this slab reduction with others (slab_reduce_multi)
+    *deferred = z.grid;
+    return hipSuccess;
+  }
   return slab_reduce(workspace, gw, gb, g.N, g.K, Kt, z.grid, 1.f, st);
 }
 
 hipError_t convpool_wgrad(const void* x, int x_u8, const long long* idx, long long nrows, float scale, int B, int H,
                           int W, int C, int KH, int KW, int pad, int N, const bf16* dp, const uint8_t* code,
-                          float* gw, float* gb, float* workspace, size_t ws_floats, hipStream_t st) {
+                          float* gw, float* gb, float* workspace, size_t ws_floats, hipStream_t st, int* deferred) {
   if (!convpool_supported(H, W, C, KH, KW, pad, N)) return hipErrorInvalidValue;
   CPGeom g = make_geom(B, H, W, C, KH, KW, pad, N);
   const int KT = cdiv(g.K + 1, 16);
@@ -1478,7 +1526,8 @@ hipError_t convpool_wgrad(const void* x, int x_u8, const long long* idx, long lo
     return hipErrorInvalidValue;  // pooled gradient / codes are read as 4-element chunks
   (void)npool;
   const bool vec = stage_vec_ok(g, x, x_u8);
-#define CP_WG(NT_, KT_) return launch_cp_wgrad<NT_, KT_>(g, vec, x, x_u8, idx, nrows, scale, dp, code, gw, gb, workspace, ws_floats, st)
+#define CP_WG(NT_, KT_) \
+  return launch_cp_wgrad<NT_, KT_>(g, vec, x, x_u8, idx, nrows, scale, dp, code, gw, gb, workspace, ws_floats, st, deferred)
   if (NT == 1) {
     if (KT <= 2) CP_WG(1, 2);
     if (KT <= 4) CP_WG(1, 4);

@@ -171,11 +171,24 @@ hipError_t convpool_fwd(const void* x, int x_u8, const long long* idx, long long
                         uint8_t* code, hipStream_t st);
 hipError_t convpool_wgrad(const void* x, int x_u8, const long long* idx, long long nrows, float scale, int B, int H,
                           int W, int C, int KH, int KW, int pad, int N, const bf16* dp, const uint8_t* code,
-                          float* gw, float* gb, float* workspace, size_t ws_floats, hipStream_t st);
+                          float* gw, float* gb, float* workspace, size_t ws_floats, hipStream_t st, int* deferred = nullptr);
 hipError_t convpool_dgrad(const bf16* dp, const uint8_t* code, const bf16* wt, bf16* dx, int B, int H, int W, int C,
                           int KH, int KW, int pad, int N, hipStream_t st);
 hipError_t slab_reduce(const float* partial, float* gw, float* gb, int N, int K, int Kt, int S, float scale,
                        hipStream_t st);
+constexpr int kMaxSlabSegs = 8;
+struct SlabSeg {
+  const float* partial;  // [S][N][Kt]
+  float* gw;             // [N][K]
+  float* gb;             // [N] (column K) or nullptr
+  int N, K, Kt, S, block0;
+  float scale;
+};
+struct SlabSegs {
+  SlabSeg s[kMaxSlabSegs];
+  int n;
+};
+hipError_t slab_reduce_multi(SlabSegs segs, hipStream_t st);
 
 
 // One-shot xGMI all-reduce (csrc/allreduce_p2p.hip).  Each rank's IPC buffer: flags

@@ -561,12 +561,12 @@ class FusedConvPool(Layer):
         ops.convpool_fwd(x, st.weight(f"{self.name}/kernel"), b, self.out, self.code, self.k, self.k, self.pad)
         return self.out
 
-    def backward_weights(self, dy):
+    def backward_weights(self, dy, defer=None):
         st = self.store
         kn = f"{self.name}/kernel"
         gb = st.gradient(f"{self.name}/bias") if self.use_bias else None
         ops.convpool_wgrad(self.x, dy.reshape(self.out.shape), self.code, st.grad_matrix(kn), gb, self.ws_wgrad,
-                           self.k, self.k, self.pad)
+                           self.k, self.k, self.pad, defer=defer)
 
     def backward_data(self, dy):
         if not self.need_dx:
@@ -579,6 +579,6 @@ class FusedConvPool(Layer):
             ops.relu_bwd(self.x, self.dx, self.dx)
         return self.dx
 
-    def backward(self, dy):
-        self.backward_weights(dy)
+    def backward(self, dy, defer=None):
+        self.backward_weights(dy, defer)
         return self.backward_data(dy)

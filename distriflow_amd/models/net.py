@@ -258,10 +258,27 @@ class Net:
                 for i in head_ids:
                     grad_ready(i)
             d = first.dx if first.need_dx else None
+            # fused conv+pool weight gradients defer their split-m slab reductions; consecutive ones are
+            # flushed in ONE launch right before the next gradient hook needs them (or at the end)
+            pending, waiting = [], []
             for i in range(self.head_start - 1, -1, -1):
-                d = self.exec_layers[i].backward(d)
+                l = self.exec_layers[i]
+                if isinstance(l, FusedConvPool) and self.is_gpu:
+                    d = l.backward(d, defer=pending)
+                    waiting.append(i)
+                    continue
+                if pending:
+                    ops.flush_slab_reductions(pending)
+                d = l.backward(d)
                 if grad_ready is not None:
-                    grad_ready(i)
+                    for j in waiting + [i]:
+                        grad_ready(j)
+                waiting = []
+            if pending:
+                ops.flush_slab_reductions(pending)
+            if grad_ready is not None:
+                for j in waiting:
+                    grad_ready(j)
             return self.stats
         # critical path on the main stream: head fwd/CE/bwd-data -> each body layer's data gradient;
         # weight gradients fork onto side streams as soon as their input gradient exists.  Gradient

@@ -391,12 +391,18 @@ def convpool_fwd(x, w, bias, out, code, KH, KW, pad):
     return out
 
 
-def convpool_wgrad(x, dp, code, gw, gb, workspace, KH, KW, pad):
+def convpool_wgrad(x, dp, code, gw, gb, workspace, KH, KW, pad, defer: list | None = None):
+    """``defer``: a list to which the GPU path appends its split-m slab reduction instead of launching
+    it; run them all with :func:`flush_slab_reductions` (one launch, bit-identical results)."""
     B, H, W, C = x.shape
     N = code.shape[-1]
     if code.is_cuda:
         src, idx, scale = _cp_in(x)
-        _C().convpool_wgrad(src, idx, scale, dp, code, gw, gb, workspace, [B, H, W, C, KH, KW, pad, N])
+        S = _C().convpool_wgrad(src, idx, scale, dp, code, gw, gb, workspace, [B, H, W, C, KH, KW, pad, N],
+                                defer is not None)
+        if defer is not None and S > 0:
+            K = KH * KW * C
+            defer.append((workspace, gw.reshape(-1), gb, N, K, K + 1, int(S), 1.0))
     else:
         if isinstance(x, GatherRef):
             x = (x.data.index_select(0, x.idx).float() * x.scale).reshape(x.shape)
@@ -404,6 +410,13 @@ def convpool_wgrad(x, dp, code, gw, gb, workspace, KH, KW, pad):
         gw.copy_(g.reshape(gw.shape))
         if gb is not None:
             gb.copy_(b)
+
+
+def flush_slab_reductions(pending: list):
+    """One launch for the deferred slab reductions in ``pending`` (emptied)."""
+    for i in range(0, len(pending), 8):
+        _C().slab_reduce_multi(pending[i:i + 8])
+    pending.clear()
 
 
 def convpool_dgrad(dp, code, w, wt, dx, KH, KW, pad):
