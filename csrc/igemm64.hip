@@ -68,8 +68,11 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int c = tid & 7, r0 = tid >> 3;  // chunk column; rows r0 + 32 i
 
-  // per-row source state (fixed over the k loop)
+  // per-row source state (fixed over the k loop).  rptr folds the row's pixel offset into a pointer
+  // so a k step only adds one 32-bit offset per load (the im2col address math was the VALU hot spot:
+  // ~9 VALU per MFMA in the PMC counters)
   long long rbase[AP];
+  const bf16* rptr[AP];
   int rh[AP], rw[AP];
   bool rval[AP];
 #pragma unroll
@@ -94,6 +97,16 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
         rw[i] = ow + a.pad;
       }
     }
+    rptr[i] = a.src + rbase[i] + ((long long)rh[i] * a.SW + rw[i]) * a.SC;
+  }
+  const bf16* wptr[BP];
+  bool wval[BP];
+  const int npad_ = round_up(a.N, 16);
+#pragma unroll
+  for (int i = 0; i < BP; ++i) {
+    const int n = n0 + r0 + 32 * i;
+    wval[i] = n < npad_;
+    wptr[i] = a.w + (long long)(wval[i] ? n : 0) * a.Kpad;
   }
   // this thread's k chunk: k = kt * 64 + 8c  ->  (kh, kw, ci) for the gathers
   int kk = 8 * c, kh = 0, kw = 0, ci = kk;
@@ -111,36 +124,38 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
   u32x4_t ra[D][AP], rb[D][BP];
   auto gload = [&](int st) {
     const bool kv = kk < a.K;
+    // k-step offset of this thread's chunk relative to the row pointer (same for every row)
+    const int koff = (MODE == MODE_FWD) ? (kh * a.SW + kw) * a.SC + ci : ci - (kh * a.SW + kw) * a.SC;
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
       bool v = rval[i] && kv;
-      long long off;
+      const bf16* p;
       if (MODE == MODE_DIRECT) {
-        off = rbase[i] + kk;
+        p = a.src + rbase[i] + kk;
       } else if (MODE == MODE_FWD) {
         const int sh = rh[i] + kh, sw = rw[i] + kw;
         v = v && (unsigned)sh < (unsigned)a.SH && (unsigned)sw < (unsigned)a.SW;
-        off = rbase[i] + ((long long)sh * a.SW + sw) * a.SC + ci;
+        p = rptr[i] + koff;
+      } else if (a.stride == 1) {  // dX(ih, iw) <- dY(ih + pad - kh, iw + pad - kw)
+        const int th = rh[i] - kh, tw = rw[i] - kw;
+        v = v && (unsigned)th < (unsigned)a.SH && (unsigned)tw < (unsigned)a.SW;
+        p = rptr[i] + koff;
       } else {  // dX(ih, iw) <- dY((ih + pad - kh) / s, (iw + pad - kw) / s)
         int th = rh[i] - kh, tw = rw[i] - kw;
-        v = v && th >= 0 && tw >= 0;
-        if (a.stride > 1) {
-          v = v && (th % a.stride) == 0 && (tw % a.stride) == 0;
-          th /= a.stride;
-          tw /= a.stride;
-        }
+        v = v && th >= 0 && tw >= 0 && (th % a.stride) == 0 && (tw % a.stride) == 0;
+        th /= a.stride;
+        tw /= a.stride;
         v = v && th < a.SH && tw < a.SW;
-        off = rbase[i] + ((long long)th * a.SW + tw) * a.SC + ci;
+        p = a.src + rbase[i] + ((long long)th * a.SW + tw) * a.SC + ci;
       }
       // a masked-out chunk reads 16 zero bytes instead (address select, not a data mask: the loaded value
       // is not touched until its LDS store D steps later, so no wait is forced right after the load)
-      ra[st][i] = gload16(v ? (const void*)(a.src + off) : (const void*)&kZero16);
+      ra[st][i] = gload16(v ? (const void*)p : (const void*)&kZero16);
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
-      const int n = n0 + r0 + 32 * i;
-      const bool v = n < npad && kk < a.Kpad;
-      rb[st][i] = gload16(v ? (const void*)(a.w + (long long)n * a.Kpad + kk) : (const void*)&kZero16);
+      const bool v = wval[i] && kk < a.Kpad;
+      rb[st][i] = gload16(v ? (const void*)(wptr[i] + kk) : (const void*)&kZero16);
     }
   };
   auto advance = [&]() {
@@ -302,6 +317,8 @@ hipError_t launch64(const IGemmArgs& a, hipStream_t st) {
 template <int MODE>
 hipError_t launch64_mode(const IGemmArgs& a, hipStream_t st) {
   if (a.N <= 32) return launch64<128, 32, MODE>(a, st);  // Keras CNN conv2 (32 channels): no half-empty tiles
+  // (a 256 x 64 tile with 4 x 1 waves of 64 x 64 measured 9-16% slower on ResNet layer 1: 8 waves per
+  // CU instead of 12)
   if (a.N <= 64) return launch64<128, 64, MODE>(a, st);
   // 128x128 while that still gives >= 2 workgroups per CU, else 64x128
   if ((long long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 512) return launch64<128, 128, MODE>(a, st);
