@@ -784,6 +784,7 @@ class P2PComm {
     return v;
   }
   int64_t max_floats() const { return half_; }
+  void set_timeout(double timeout_s) { timeout_ticks_ = (int64_t)(timeout_s * 1e8); }
 
  private:
   int rank_, world_, dev_ = 0, max_blocks_ = 0;
@@ -988,6 +989,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("open", &P2PComm::open)
       .def("allreduce", &P2PComm::allreduce, py::arg("t"), py::arg("scale") = 1.0)
       .def("error", &P2PComm::error)
+      .def("set_timeout", &P2PComm::set_timeout)
       .def_property_readonly("max_floats", &P2PComm::max_floats);
   py::class_<PSComm>(m, "PSComm", "device-resident bounded-staleness parameter server over IPC/xGMI")
       .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("server_rank"), py::arg("n"),

@@ -73,9 +73,14 @@ class P2PAllReduce:
             self.reason = why or "a peer could not map the buffers"
             return
         self.comm = comm
-        if self_test and not self._self_test():
-            self.comm = None
-            self.reason = self.reason or "self-test mismatch"
+        if self_test:
+            # a broken peer path shows up as a flag timeout: fail the self-test within seconds, not minutes
+            comm.set_timeout(min(timeout_s, 5.0))
+            passed = self._self_test()
+            comm.set_timeout(timeout_s)
+            if not passed:
+                self.comm = None
+                self.reason = self.reason or "self-test mismatch"
 
     @property
     def ok(self) -> bool:
