@@ -49,6 +49,9 @@ def main():
                     help="after the sync measurement, also time this many steps of the async parameter-server "
                          "engine and report the async speedup (default: --steps; 0 disables)")
     ap.add_argument("--json-extra", action="store_true", help="add diagnostic fields")
+    ap.add_argument("--phases", type=int, default=0,
+                    help="after timing, run this many EAGER steps with hipEvent phase timers and report the "
+                         "data/compute/comm/update breakdown (diagnostic, not part of the timed number)")
     args = ap.parse_args()
 
     from distriflow_amd.data.synthetic import synthetic_cifar10, synthetic_mnist
@@ -118,6 +121,9 @@ def main():
     loss = float(st[0].item()) / B
     ms = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
+    phases = None
+    if args.phases > 0 and args.mode == "sync" and dev.type == "cuda":
+        phases = {k: round(v, 4) for k, v in trainer.timed_eager_steps(args.phases).items()}
     async_rec = None
     async_steps = args.steps if args.async_steps is None else args.async_steps
     if args.mode == "sync" and async_steps > 0 and dev.type == "cuda":
@@ -163,6 +169,8 @@ def main():
             out["async"] = dict(trainer.ps_stats(), max_staleness_bound=args.max_staleness)
         elif async_rec is not None:
             out["async"] = async_rec
+        if phases is not None:
+            out["phases_ms_eager"] = phases
         if args.json_extra:
             out["extra"] = {"final_loss": loss, "train_tflops": value * net.flops_per_example() / 1e12,
                             "capture_error": getattr(trainer, "capture_error", None)}

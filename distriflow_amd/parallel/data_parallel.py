@@ -151,12 +151,45 @@ class DataParallelTrainer:
             (hi - lo) * 4 > self.p2p_limit for _, lo, hi in self.buckets) else ("p2p" if self.p2p else "rccl")
 
     # ------------------------------------------------------------------ one step
+    phase_timer = None  # utils.logging.PhaseTimer: per-phase GPU time of eager steps
+
     def _step_body(self, x, y):
         hook = self._grad_ready if (self.overlap and self.world > 1) else None
+        pt = self.phase_timer
+        if pt is not None and torch.cuda.is_current_stream_capturing():
+            pt = None
+        if pt is not None:
+            pt.start("compute")  # forward + loss + backward (the fused head runs all three)
         stats = self.net.compute_gradients(x, y, grad_ready=hook)
+        if pt is not None:
+            pt.stop("compute")
+            pt.start("comm")  # waits for the overlapped bucket all-reduces
         self._allreduce_all()
+        if pt is not None:
+            pt.stop("comm")
+            pt.start("update")
         self.net.store.sgd_step(self._index_stream)
+        if pt is not None:
+            pt.stop("update")
         return stats
+
+    def timed_eager_steps(self, n: int) -> dict:
+        """Per-phase GPU milliseconds per step over ``n`` eager (uncaptured) steps on the bound index
+        stream: data (batch gather), compute, comm, update.  Diagnostic: eager launches add host gaps."""
+        from ..utils.logging import PhaseTimer
+
+        pt = PhaseTimer()
+        self.phase_timer = pt
+        try:
+            for _ in range(n):
+                pt.start("data")
+                self._gather()
+                pt.stop("data")
+                self._step_body(self.xb, self.yb)
+            out = {k: v / n for k, v in pt.summary().items()}
+        finally:
+            self.phase_timer = None
+        return out
 
     def set_lr(self, lr: float):
         self.lr = lr
