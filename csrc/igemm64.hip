@@ -101,11 +101,11 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
   }
   const bf16* wptr[BP];
   bool wval[BP];
-  const int npad_ = round_up(a.N, 16);
+  const int npad = round_up(a.N, 16);
 #pragma unroll
   for (int i = 0; i < BP; ++i) {
     const int n = n0 + r0 + 32 * i;
-    wval[i] = n < npad_;
+    wval[i] = n < npad;
     wptr[i] = a.w + (long long)(wval[i] ? n : 0) * a.Kpad;
   }
   // this thread's k chunk: k = kt * 64 + 8c  ->  (kh, kw, ci) for the gathers
@@ -116,7 +116,6 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
     kh = t / a.KW;
     kw = t - kh * a.KW;
   }
-  const int npad = round_up(a.N, 16);
 
   // D register stages of prefetched global loads: the loads of step k are issued D iterations before
   // step k is stored to LDS, so ~D * (MFMA time of one step) of memory latency is covered even with a
