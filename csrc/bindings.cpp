@@ -90,6 +90,14 @@ void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tenso
   a.relu = relu ? 1 : 0;
   a.out_f32 = out.scalar_type() == at::kFloat ? 1 : 0;
   a.alpha = (float)alpha;
+  // split-K partials for the under-filled (small-M, long-K) shapes: PyTorch's caching allocator is
+  // stream ordered and graph-capture aware, so the scratch is safe to drop right after the launch
+  torch::Tensor splitk;
+  const long long skf = dfa::igemm64_splitk_floats(a, (int)mode);
+  if (skf > 0) {
+    splitk = torch::empty({skf}, out.options().dtype(at::kFloat));
+    a.splitk_ws = splitk.data_ptr<float>();
+  }
   check_hip(dfa::igemm_fwd(a, (int)mode, cur_stream()), "igemm_fwd");
 }
 

@@ -52,7 +52,7 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chu
 template <int BM, int BN>
 constexpr int igemm64_occ() { return (160 * 1024) / ((BM + BN) * 256) > 4 ? 4 : (160 * 1024) / ((BM + BN) * 256); }
 
-template <int BM, int BN, int MODE, int D>
+template <int BM, int BN, int MODE, int D, bool SPLIT>
 __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(IGemmArgs a, FastDiv d_ow, FastDiv d_ohw) {
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / (WM * 16), TN = BN / (WN * 16);
@@ -63,8 +63,16 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int ntn = cdiv(a.N, BN), ntm = cdiv(a.M, BM);
-  const int logical = xcd_remap(blockIdx.x, ntn * ntm);
+  const int nsplit = SPLIT ? a.splits : 1;
+  const int logical0 = xcd_remap(blockIdx.x, ntn * ntm * nsplit);
+  const int split = SPLIT ? logical0 / (ntn * ntm) : 0;
+  const int logical = SPLIT ? logical0 - split * (ntn * ntm) : logical0;
   const int tile_n = logical % ntn, tile_m = logical / ntn;
+  // k steps of this split: [kt_begin, kt_end)
+  const int nk_all = cdiv(a.K, 64);
+  const int kper = SPLIT ? cdiv(nk_all, nsplit) : nk_all;
+  const int kt_begin = split * kper;
+  const int kt_end = min(nk_all, kt_begin + kper);
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int c = tid & 7, r0 = tid >> 3;  // chunk column; rows r0 + 32 i
 
@@ -109,7 +117,7 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
     wptr[i] = a.w + (long long)(wval[i] ? n : 0) * a.Kpad;
   }
   // this thread's k chunk: k = kt * 64 + 8c  ->  (kh, kw, ci) for the gathers
-  int kk = 8 * c, kh = 0, kw = 0, ci = kk;
+  int kk = kt_begin * 64 + 8 * c, kh = 0, kw = 0, ci = kk;
   if (MODE != MODE_DIRECT) {
     ci = kk % a.SC;
     const int t = kk / a.SC;
@@ -185,7 +193,7 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = cdiv(a.K, 64);
+  const int nk = max(kt_end - kt_begin, 0);  // k steps of this workgroup (a whole K without split-K)
   // prologue: step 0 -> LDS[0]; steps 1..D in flight (register stage of step s = s % D)
   gload(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -236,6 +244,23 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
         }
       }
     }
+  }
+
+  if (SPLIT) {
+    // raw fp32 partials [split][M][N]; the reduce kernel applies the epilogue
+    float* ws = a.splitk_ws + (long long)split * a.M * a.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = m0 + wm * TM * 16 + i * 16 + fr;
+      if (row >= a.M) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col0 = n0 + wn * TN * 16 + j * 16 + fq * 4;
+        if (col0 >= a.N) continue;  // N % 4 == 0 on this path
+        *reinterpret_cast<f32x4*>(ws + (long long)row * a.N + col0) = acc[i][j];
+      }
+    }
+    return;
   }
 
   // epilogue.  The weights are the MFMA's A operand, so the 16x16 C/D layout puts 4 consecutive output
@@ -304,12 +329,78 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
   }
 }
 
+// split-K combine: out = epi(sum_s ws[s]) in a fixed split order (deterministic), 4 columns per thread
+__global__ void __launch_bounds__(256) igemm64_splitk_epilogue_kernel(IGemmArgs a) {
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+  const long long total4 = (long long)a.M * (a.N >> 2);
+  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < total4; q += (long long)gridDim.x * 256) {
+    const long long row = q / (a.N >> 2);
+    const int col0 = (int)(q - row * (a.N >> 2)) * 4;
+    f32x4 sacc = *reinterpret_cast<const f32x4*>(a.splitk_ws + row * a.N + col0);
+    for (int s = 1; s < a.splits; ++s)
+      sacc += *reinterpret_cast<const f32x4*>(a.splitk_ws + ((long long)s * a.M + row) * a.N + col0);
+    const long long o = row * a.ldc + col0;
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = sacc[r] * a.alpha + (a.bias ? a.bias[col0 + r] : 0.f);
+    if (a.res) {
+      const bf16x4_t rv = *reinterpret_cast<const bf16x4_t*>(a.res + o);
+      bf16x4_t rm;
+      if (a.resmask) rm = *reinterpret_cast<const bf16x4_t*>(a.resmask + o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (!a.resmask || (float)rm[r] > 0.f) v[r] += (float)rv[r];
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+    }
+    if (a.mask) {
+      const bf16x4_t mk = *reinterpret_cast<const bf16x4_t*>(a.mask + o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (!((float)mk[r] > 0.f)) v[r] = 0.f;
+    }
+    if (a.out_f32) {
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
+    } else {
+      bf16x4_t ov;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ov[r] = f2bf(v[r]);
+      *reinterpret_cast<bf16x4_t*>(reinterpret_cast<bf16*>(a.out) + o) = ov;
+    }
+  }
+}
+
+// Split-K for under-filled launches: fewer than ~2 workgroups per CU and a long K (ResNet-18 layers 3-4:
+// M = B*8*8 or B*4*4 with K up to 4608) leave one wave per SIMD waiting on every step
+template <int BM, int BN>
+static int splitk_for(const IGemmArgs& a) {
+  const long long tiles = (long long)cdiv(a.M, BM) * cdiv(a.N, BN);
+  const int nk = cdiv(a.K, 64);
+  if (a.N % 4 || a.ldc % 4 || tiles >= 512 || nk < 32) return 1;
+  if (((uintptr_t)a.out & 15) || (((uintptr_t)a.res | (uintptr_t)a.resmask | (uintptr_t)a.mask) & 7)) return 1;
+  int s = 1;
+  while (s < 4 && tiles * s * 2 <= 1024 && nk / (s * 2) >= 16) s *= 2;
+  return s;
+}
+
 template <int BM, int BN, int MODE>
-hipError_t launch64(const IGemmArgs& a, hipStream_t st) {
+hipError_t launch64(IGemmArgs a, hipStream_t st) {
   const FastDiv d_ow = make_fastdiv((unsigned)max(a.OW, 1)), d_ohw = make_fastdiv((unsigned)max(a.OH * a.OW, 1));
   const int blocks = cdiv(a.M, BM) * cdiv(a.N, BN);
   constexpr int D = kIgemm64Stages;
-  hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE, D>), dim3(blocks), dim3(256), 0, st, a, d_ow, d_ohw);
+  const int s = a.splitk_ws ? splitk_for<BM, BN>(a) : 1;
+  if (s > 1) {
+    a.splits = s;
+    hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE, D, true>), dim3(blocks * s), dim3(256), 0, st, a, d_ow, d_ohw);
+    DFA_HIP_CHECK(hipGetLastError());
+    const long long total4 = (long long)a.M * (a.N / 4);
+    const int grid = (int)min((total4 + 255) / 256, 4096LL);
+    hipLaunchKernelGGL(igemm64_splitk_epilogue_kernel, dim3(grid), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE, D, false>), dim3(blocks), dim3(256), 0, st, a, d_ow, d_ohw);
   return hipGetLastError();
 }
 
@@ -325,6 +416,13 @@ hipError_t launch64_mode(const IGemmArgs& a, hipStream_t st) {
 }
 
 }  // namespace
+
+long long igemm64_splitk_floats(const IGemmArgs& a, int mode) {
+  if (!igemm64_supported(a, mode) || a.N <= 64) return 0;
+  if ((long long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 512) return 0;  // 128 x 128 tiles: already filled
+  const int s = splitk_for<64, 128>(a);
+  return s > 1 ? (long long)s * a.M * a.N : 0;
+}
 
 bool igemm64_supported(const IGemmArgs& a, int mode) {
   if (((uintptr_t)a.src & 15) || ((uintptr_t)a.w & 15) || a.Kpad % 8 || a.M <= 0 || a.N <= 0) return false;

@@ -25,6 +25,8 @@ struct IGemmArgs {
   int SH, SW, SC, OH, OW, KH, KW, stride, pad;
   int relu, out_f32;
   float alpha;
+  float* splitk_ws;  // igemm64 split-K partials [splits][M][N] (nullptr: no split)
+  int splits;
 };
 
 struct WgradArgs {
@@ -60,6 +62,9 @@ hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st);
 // 64-deep-step variant for the vectorizable cases (csrc/igemm64.hip); igemm_fwd dispatches to it
 bool igemm64_supported(const IGemmArgs& a, int mode);
 hipError_t igemm64(const IGemmArgs& a, int mode, hipStream_t st);
+// fp32 floats of split-K workspace igemm64 wants for this problem (0: no split); the caller allocates
+// them and passes the buffer in IGemmArgs::splitk_ws
+long long igemm64_splitk_floats(const IGemmArgs& a, int mode);
 hipError_t igemm_wgrad(const WgradArgs& a, int mode, float* workspace, size_t ws_floats, hipStream_t st);
 // conv weight gradient with transposed LDS reads (csrc/wgrad_tr.hip): conv, C % 8 == 0, no bias
 bool wgrad_tr_supported(const WgradArgs& a, int mode);

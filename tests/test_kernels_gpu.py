@@ -366,6 +366,28 @@ def test_conv_dgrad_residual_epilogue():
     _close(out, exp)
 
 
+@pytest.mark.parametrize("B,H,W,C,N", [(16, 4, 4, 512, 512), (8, 8, 8, 256, 256), (3, 4, 4, 256, 512)])
+def test_conv_splitk_fwd_and_dgrad(B, H, W, C, N):
+    """ResNet-18 layer 3/4 shapes: small M, K up to 4608 -> igemm64 split-K (fp32 partials + a fixed-order
+    combine that applies the epilogue), forward with bias + ReLU and data gradient with the full join."""
+    k = 3
+    x = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    w = torch.randn(N, k * k * C, device=dev) / (k * k * C) ** 0.5
+    b = torch.randn(N, device=dev)
+    out = torch.empty(B, H, W, N, device=dev, dtype=torch.bfloat16)
+    ops.conv_fwd(x, _pad_w(w), b, out, k, k, 1, 1, True)
+    _close(out, ref.conv_fwd(x.float(), w.to(torch.bfloat16).float(), b, k, k, 1, 1, True))
+    dy = torch.randn(B, H, W, N, device=dev).to(torch.bfloat16)
+    res = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    rmask = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    mask = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    dx = torch.empty(B, H, W, C, device=dev, dtype=torch.bfloat16)
+    ops.conv_dgrad(dy, None, _pad_wt(w, N, k * k, C), dx, k, k, 1, 1, mask=mask, residual=res, residual_mask=rmask)
+    exp = ref.conv_dgrad(dy.float(), w.to(torch.bfloat16).float(), (B, H, W, C), k, k, 1, 1, None)
+    exp = (exp + res.float() * (rmask.float() > 0)) * (mask.float() > 0)
+    _close(dx, exp)
+
+
 CONVPOOL = [  # B, H, W, C, N, k, pad
     (16, 28, 28, 1, 6, 5, 2),    # LeNet conv1 ('same')
     (16, 14, 14, 6, 16, 5, 0),   # LeNet conv2
