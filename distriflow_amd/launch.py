@@ -91,6 +91,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--local-steps", type=int, default=20)
     p.add_argument("--classes-per-client", type=int, default=2)
+    p.add_argument("--engine", default="auto", choices=["auto", "device", "roles"],
+                   help="device = every rank a client, graph-captured local steps, collective weight average "
+                        "(parallel/fedavg.py); roles = FedAvgServer/FedAvgClient messages; auto = device on GPUs")
     return ap
 
 
@@ -495,8 +498,61 @@ def run_fedsgd(args) -> dict:
     return out or {}
 
 
+def run_fedavg_device(args) -> dict:
+    """FedAvg with every rank a client on its own non-IID shard: captured local SGD steps, then an
+    in-place average of the flat master (one-shot xGMI all-reduce / RCCL) each round."""
+    import torch
+
+    from .data.synthetic import non_iid_shards
+    from .models.zoo import build_model
+    from .parallel.comm import init_distributed, shutdown
+    from .parallel.fedavg import FedAvgTrainer
+
+    env = init_distributed(device=_device(args))
+    rank, world, dev = env.rank, env.world_size, env.device
+    x, y = _load_data(args, dev)
+    scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
+    shard = non_iid_shards(y, world, args.classes_per_client, seed=args.seed)[rank].to(dev)
+    B = args.batch
+    total = args.rounds * args.local_steps
+    g = torch.Generator(device="cpu").manual_seed(args.seed + 1000 * rank)
+    chunks, need = [], total * B
+    while sum(c.numel() for c in chunks) < need:
+        chunks.append(shard[torch.randperm(shard.numel(), generator=g).to(dev)])
+    stream = torch.cat(chunks)[:need].view(total, B)
+    net = build_model(args.model, device=dev, seed=args.seed)
+    tr = FedAvgTrainer(net, lr=args.lr, local_steps=args.local_steps,
+                       graph="full" if dev.type == "cuda" else "none")
+    tr.bind_dataset(x, y, B, scale=scale)
+    tr.bind_index_stream(stream)
+    t0 = time.perf_counter()
+    for _ in range(args.rounds):
+        tr.run_round()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    tr.check_comm()
+    out = {}
+    if rank == 0:
+        n = min(4096, x.shape[0])
+        loss, acc = net.evaluate(x[:n].float() * scale, y[:n])
+        out = {"mode": "fedavg", "engine": "device", "clients": world, "rounds": tr.rounds,
+               "local_steps": args.local_steps, "rounds_per_s": tr.rounds / max(el, 1e-9),
+               "images_per_s": world * total * B / max(el, 1e-9), "test_loss": float(loss),
+               "test_accuracy": float(acc), "allreduce": tr.allreduce_path if world > 1 else None}
+        print(json.dumps(out), flush=True)
+    shutdown()
+    return out
+
+
 def run_fedavg(args) -> dict:
     import torch
+
+    engine = args.engine
+    if engine == "auto":
+        engine = "device" if _device(args) == "cuda" else "roles"
+    if engine == "device":
+        return run_fedavg_device(args)
 
     from .data.synthetic import non_iid_shards
     from .models.distri_model import ClientModel, InMemoryServerModel

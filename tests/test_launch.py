@@ -61,3 +61,26 @@ def test_async_parameter_server_three_ranks():
     assert p.returncode == 0, p.stderr[-3000:]
     res = _last_json(p.stdout)
     assert res["world"] == 3 and res["updates"] >= 16
+
+
+@pytest.mark.timeout(300)
+def test_fedavg_device_engine_two_ranks_cpu():
+    """FedAvgTrainer (parallel/fedavg.py): every rank a client on a non-IID shard, collective averaging."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "distriflow_amd.launch",
+                        "fedavg", "--engine", "device", "--device", "cpu", "--model", "mlp_mnist",
+                        "--num-examples", "4096", "--batch", "64", "--rounds", "4", "--local-steps", "10",
+                        "--lr", "0.1"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = _last_json(p.stdout)
+    assert out["engine"] == "device" and out["clients"] == 2 and out["rounds"] == 4
+    assert out["test_accuracy"] > 0.3

@@ -122,3 +122,29 @@ def test_parameter_server_over_gloo(mode):
         assert res[0]["done"]
         assert res[0]["updates"] == sum(r["uploads"] for r in res[1:]) >= 8
         assert len(res[0]["hist"]) <= 3
+
+
+def _fedavg_worker(rank, world, port, out_dir):
+    _init(rank, world, port)
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.fedavg import FedAvgTrainer
+
+    net = build_model("mlp_mnist", "cpu", seed=0)
+    tr = FedAvgTrainer(net, lr=0.1, local_steps=3, graph="none")
+    # after the initial broadcast every rank diverges: perturb rank-specifically, then average
+    before = net.store.master.clone()
+    net.store.master.add_(float(rank + 1))
+    tr.average()
+    torch.save({"before": before, "after": net.store.master.clone()}, os.path.join(out_dir, f"f{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_fedavg_average_is_the_mean_of_ranks():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_fedavg_worker, args=(2, _port(), d), nprocs=2, join=True)
+        r = [torch.load(os.path.join(d, f"f{i}.pt"), weights_only=True) for i in range(2)]
+    assert torch.equal(r[0]["before"], r[1]["before"])  # broadcast init
+    torch.testing.assert_close(r[0]["after"], r[0]["before"] + 1.5)  # mean of +1 and +2
+    assert torch.equal(r[0]["after"], r[1]["after"])
