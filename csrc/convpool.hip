@@ -26,6 +26,8 @@
 // point at a real LDS element instead of being masked (the matching weight rows are zero padding
 // and activations are finite, so they contribute exactly 0), weights / offsets / bias live in
 // registers for the whole workgroup.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -1375,13 +1377,22 @@ struct Sizing {
   size_t lds;
 };
 
+// Tuning overrides (measurement only): DISTRIFLOW_CP_WPC caps workgroups per CU, DISTRIFLOW_CP_MINIMGS
+// raises the images per group (fewer, longer-lived workgroups amortise the per-workgroup setup).
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
 static Sizing size_persistent(const void* kern, int B, size_t fixed, size_t per_img, size_t min_lds, int cap) {
-  const int wpc = min(8, blocks_per_cu(kern, 0));
+  static const int wpc_cap = max(1, env_int("DISTRIFLOW_CP_WPC", 8));
+  static const int min_imgs = max(1, env_int("DISTRIFLOW_CP_MINIMGS", 1));
+  const int wpc = min(wpc_cap, blocks_per_cu(kern, 0));
   const size_t budget = (160 * 1024) / wpc;
   int fit = (int)max((size_t)1, (budget > fixed ? budget - fixed : 0) / per_img);
   fit = max(1, min(fit, min(cap, 32)));
   Sizing z{};
-  z.imgs = min(fit, max(1, cdiv(B, num_cus() * wpc)));
+  z.imgs = min(fit, max(min_imgs, cdiv(B, num_cus() * wpc)));
   z.lds = max(fixed + (size_t)z.imgs * per_img, min_lds);
   const int nb = blocks_per_cu(kern, z.lds);
   z.grid = min(num_cus() * nb, cdiv(B, z.imgs));
