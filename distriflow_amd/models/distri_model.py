@@ -87,7 +87,69 @@ class DistriModel(ABC):
             off += n
         self.update(grads)
 
+    # ---- README DistriModel fields: modelID + savedGradient (/root/reference/README.md:24-29) ----
+    # The reference advertises ``modelID: UUID`` and ``savedGradient: tf.grads (aggregated gradients
+    # local)`` but never implements them.  Here the saved gradient is a flat fp32
+    # accumulator on the model's device: ``accumulate(x, y)`` / ``save_gradient(g)`` add into it,
+    # ``apply_saved_gradient()`` applies the mean (or sum) with one ``update_flat`` and clears it.
+    @property
+    def model_id(self) -> str:
+        mid = self.__dict__.get("_model_id")
+        if mid is None:
+            import uuid
+
+            mid = self.__dict__["_model_id"] = str(uuid.uuid4())
+        return mid
+
+    @property
+    def saved_gradient(self) -> Optional[torch.Tensor]:
+        return self.__dict__.get("_saved_grad")
+
+    @property
+    def saved_count(self) -> int:
+        return self.__dict__.get("_saved_count", 0)
+
+    def save_gradient(self, grads) -> None:
+        """Add one gradient (flat tensor or per-variable list) into the local saved gradient."""
+        flat = grads if isinstance(grads, torch.Tensor) else torch.cat([g.reshape(-1).float() for g in grads])
+        acc = self.saved_gradient
+        if acc is None:
+            self.__dict__["_saved_grad"] = flat.detach().float().clone()
+        else:
+            if acc.numel() != flat.numel():
+                raise ValueError(f"saved gradient has {acc.numel()} elements, got {flat.numel()}")
+            acc.add_(flat.to(acc.device, torch.float32))
+        self.__dict__["_saved_count"] = self.saved_count + 1
+
+    def accumulate(self, x, y) -> torch.Tensor:
+        """``fit`` one microbatch and add its gradient into the saved gradient (copies out of the live
+        engine buffer, which the next ``fit`` overwrites)."""
+        self.save_gradient(self.fit_flat(x, y))
+        return self.saved_gradient
+
+    def clear_saved_gradient(self) -> None:
+        self.__dict__["_saved_grad"] = None
+        self.__dict__["_saved_count"] = 0
+
+    def apply_saved_gradient(self, mean: bool = True) -> int:
+        """Apply the saved gradient (averaged over the saved microbatches when ``mean``) and clear it.
+        Returns how many microbatches it held (0: nothing applied)."""
+        n, acc = self.saved_count, self.saved_gradient
+        if n == 0 or acc is None:
+            return 0
+        self.update_flat(acc, 1.0 / n if mean else 1.0)
+        self.clear_saved_gradient()
+        return n
+
     # reference camelCase aliases
+    @property
+    def modelID(self):
+        return self.model_id
+
+    @property
+    def savedGradient(self):
+        return self.saved_gradient
+
     def getVars(self):
         return self.get_vars()
 
