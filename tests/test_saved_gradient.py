@@ -2,6 +2,7 @@
 gradient accumulation over microbatches, applied as one averaged update."""
 import uuid
 
+import pytest
 import torch
 
 from distriflow_amd.models.distri_model import DynamicModel, EngineModel
@@ -49,3 +50,26 @@ def test_saved_gradient_on_dynamic_model_list_grads():
     m.save_gradient([3 * torch.ones(3)])
     assert m.apply_saved_gradient(mean=True) == 2
     torch.testing.assert_close(m.get_vars()[0], torch.full((3,), -1.0))
+
+
+@pytest.mark.gpu
+def test_saved_gradient_engine_gpu():
+    """Same identity on the HIP engine (bf16 compute, fp32 gradients): two accumulated half batches,
+    averaged, equal the full-batch gradient up to bf16 rounding of the per-microbatch sums."""
+    from distriflow_amd import native
+
+    native.require()
+    torch.manual_seed(0)
+    x = torch.rand(256, 28, 28, 1, device="cuda").to(torch.bfloat16)
+    y = torch.randint(0, 10, (256,), device="cuda")
+    a = EngineModel(build_model("lenet5", device="cuda:0", seed=0), {"learningRate": 0.05})
+    b = EngineModel(build_model("lenet5", device="cuda:0", seed=0), {"learningRate": 0.05})
+    a.fetch_initial(), b.fetch_initial()
+    a.accumulate(x[:128], y[:128])
+    a.accumulate(x[128:], y[128:])
+    full = b.fit_flat(x, y).clone()
+    assert a.saved_gradient.is_cuda and a.saved_count == 2
+    torch.testing.assert_close(a.saved_gradient / 2, full, rtol=2e-2, atol=2e-4)
+    a.apply_saved_gradient()
+    b.update_flat(full)
+    torch.testing.assert_close(a.get_flat(), b.get_flat(), rtol=1e-3, atol=1e-5)
