@@ -7,13 +7,19 @@ BASELINE.json metric "images/sec (whole node), MNIST CNN sync-SGD at 1/2/4/8 MI3
 batch gather, forward, fused softmax-CE, backward, RCCL all-reduce of the gradients, fused SGD update.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model lenet5] [--batch-per-gpu B]
-For N > 1 launch with torch.distributed.run (one rank per GPU); rank 0 prints one JSON line.
+For N > 1 either launch with torch.distributed.run (one rank per GPU), or run it plainly: with
+WORLD_SIZE unset, ``--gpus N`` makes this process a launcher that starts N fresh rank processes
+(before anything touches the GPU) and exits with the first failing child's code.  Rank 0 prints
+one JSON line; ``world`` / ``backend`` in it come from the live process group.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -25,6 +31,43 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "images/sec (whole node), MNIST CNN sync-SGD at 1/2/4/8 MI355X; async speedup"
 BASELINE_VALUE = None  # the reference publishes no number
+
+
+def _spawn_ranks(n: int) -> int:
+    """Launcher mode (``--gpus N`` without torchrun): N child processes of this script with
+    torchrun-style env.  Runs before any HIP call in this process, and never execs.  On the first
+    child failure the survivors are stopped (their exact PIDs) and that exit code is returned."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                              env=dict(env, RANK=str(r), LOCAL_RANK=str(r))) for r in range(n)]
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0] if bad[0] > 0 else 128 - bad[0]
+            break
+        if all(c == 0 for c in codes):
+            return 0
+        time.sleep(0.1)
+    for p in procs:
+        if p.poll() is None:
+            p.send_signal(signal.SIGTERM)
+    deadline = time.time() + 30
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.1, deadline - time.time()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    print(f"bench: a rank exited with {rc}; job stopped", file=sys.stderr, flush=True)
+    return rc
 
 
 def main():
@@ -53,6 +96,10 @@ def main():
                     help="after timing, run this many EAGER steps with hipEvent phase timers and report the "
                          "data/compute/comm/update breakdown (diagnostic, not part of the timed number)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(args.gpus))
 
     from distriflow_amd.data.synthetic import synthetic_cifar10, synthetic_mnist
     from distriflow_amd.models.zoo import build_model
@@ -61,9 +108,12 @@ def main():
 
     env = init_distributed()
     world, rank = env.world_size, env.rank
-    if args.gpus != world:
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    live_world = dist.get_world_size() if dist.is_initialized() else 1
+    live_backend = dist.get_backend() if dist.is_initialized() else "none"
+    if args.gpus != world or live_world != world:
+        print(f"bench: --gpus {args.gpus} but the process group has {live_world} ranks "
+              f"(WORLD_SIZE={world}); refusing to report a mislabelled number", file=sys.stderr, flush=True)
+        sys.exit(3)
     dev = env.device
 
     def sync():
@@ -144,6 +194,8 @@ def main():
             "value": round(value, 1),
             "unit": "images/s",
             "n_gpus": world,
+            "world": live_world,
+            "backend": live_backend,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
