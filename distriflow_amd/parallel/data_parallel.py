@@ -304,23 +304,36 @@ class DataParallelTrainer:
         return self._replay()
 
     def _capture_with_fallback(self):
-        """Capture fallback chain full -> split -> none (eager); every failure is recorded."""
+        """Capture fallback chain full -> split -> none (eager); every failure is recorded.
+
+        The ranks agree on every attempt (MIN of a success flag, outside any capture): if capture
+        fails on one rank only, all of them fall back together, so no rank replays a graph whose
+        collectives / one-shot epochs its peers never issue."""
         while True:
+            ok = True
             try:
                 self._capture()
-                return
             except Exception as e:  # e.g. collective capture unsupported by this RCCL/driver
                 torch.cuda.synchronize(self.net.device)
                 self.capture_error = repr(e)
-                self._works = []
-                self._graph = None
-                if self.graph_mode == "full":
-                    self.graph_mode = "split"
-                else:
-                    self.graph_mode = "none"
-                    self._gather()
-                    self._last_eager = self._step_body(self.xb, self.yb)
-                    return
+                ok = False
+            if self.world > 1:
+                flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.net.device)
+                dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+                if ok and int(flag.item()) == 0:
+                    self.capture_error = "a peer rank failed to capture"
+                ok = bool(flag.item())
+            if ok:
+                return
+            self._works = []
+            self._graph = None
+            if self.graph_mode == "full":
+                self.graph_mode = "split"
+            else:
+                self.graph_mode = "none"
+                self._gather()
+                self._last_eager = self._step_body(self.xb, self.yb)
+                return
 
     def _replay(self):
         g, g2 = self._graph

@@ -99,6 +99,8 @@ class AbstractServer:
         meta = {"version": self.model.version, "hyperparams": self.client_hyperparams}
         if data is not None:
             meta["data"] = {"batch": data.batch, "epoch": data.epoch, "start": data.start, "size": data.size}
+            if data.indices is not None:
+                meta["data"]["indices"] = [int(i) for i in data.indices]
         tensors = [self.model.get_flat()]
         if data is not None and data.x is not None:
             tensors += [data.x, data.y]
@@ -256,6 +258,7 @@ class AsynchronousSGDServer(AbstractServer):
         self.gate = native.require().StalenessGate(int(self.server_hyperparams["maximumStaleness"]))
         self.rejected = 0
         self.finished_clients = set()
+        self.admitted_batches: list = []  # (epoch, batch) of every applied gradient, in order
 
     def _dispense(self) -> Optional[DataMsg]:
         from ..data.dataset import batch_to_data_msg
@@ -269,7 +272,9 @@ class AsynchronousSGDServer(AbstractServer):
         if r is None:
             return None
         b, epoch, start, size = r
-        return DataMsg(b, epoch, None, None, start, size)
+        # a shuffled dataset's batch is its permuted example ids, not the row range [start, start+size)
+        idx = self.dataset.example_indices(b).tolist() if self.dataset.shuffle else None
+        return DataMsg(b, epoch, None, None, start, size, idx)
 
     def _send_work(self, dst: int):
         data = self._dispense()
@@ -293,9 +298,13 @@ class AsynchronousSGDServer(AbstractServer):
         self.log(f"new update from {msg.client_id}")
         self.num_updates += 1
         self.perform_upload_callbacks(msg)
-        if m.batch >= 0:
-            self.dataset.complete_batch(m.batch, m.epoch if m.epoch >= 0 else None)
         if self.gate.admit(int(m.version_id), int(self.version_id)):
+            # a microbatch counts as done only once its gradient is applied: a rejected (too stale)
+            # gradient leaves the batch incomplete, so the dispenser hands it out again
+            # (at-least-once, /root/reference/src/server/dataset.ts:47-67)
+            if m.batch >= 0:
+                self.dataset.complete_batch(m.batch, m.epoch if m.epoch >= 0 else None)
+            self.admitted_batches.append((int(m.epoch), int(m.batch)))
             self.update_model(m.tensors[0])
         else:
             self.rejected += 1

@@ -279,11 +279,15 @@ class AsynchronousSGDClient(AbstractWorker):
             return x.reshape((-1,) + shape), y
         if self.data is None:
             raise RuntimeError("download carries no data and this worker holds no dataset")
-        s, n = int(d["start"]), int(d["size"])
-        x = self.data[s: s + n]
+        if d.get("indices") is not None:  # shuffled epoch: gather the permuted rows on the device
+            idx = torch.tensor(d["indices"], dtype=torch.int64, device=self.data.device)
+            x, y = self.data.index_select(0, idx), self.labels.index_select(0, idx.to(self.labels.device))
+        else:
+            s, n = int(d["start"]), int(d["size"])
+            x, y = self.data[s: s + n], self.labels[s: s + n]
         if x.dtype == torch.uint8:
             x = x.float() * self.data_scale
-        return x, self.labels[s: s + n]
+        return x, y
 
     def distributed_update(self):
         m = self.msg

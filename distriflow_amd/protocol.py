@@ -148,6 +148,7 @@ class DataMsg:
     y: Any = None
     start: int = 0  # row range of the batch in the (worker-resident) dataset
     size: int = 0
+    indices: Any = None  # example ids of a shuffled batch (list of int) when only ids travel
 
 
 @dataclass

@@ -63,15 +63,18 @@ def test_transmits_updates(fed):
 
 def test_triggers_download_after_enough_uploads(fed):
     server, client, cm = fed
-    seen = []
+    seen, server_versions = [], []
     client.on_new_version(lambda old, new: seen.append((old, new)))
+    server.on_new_version(lambda old, new: server_versions.append(new))
     cm.vars[0].copy_(torch.full((2, 2), 2.0))
     client.distributed_update(torch.zeros(1, 1), torch.zeros(1))
     client.distributed_update(torch.zeros(3, 1), torch.zeros(3))
     wait_for(lambda: (client.poll(0.01) or True) and len(seen) > 0)
     old, new = seen[0]
-    assert old == "initial" and new != "initial" and new == server.model.version
-    # 4 uploads, barrier 2: the uploads computed on the stale version after the bump are dropped
+    # the client may already have uploaded the last two examples on the bumped version, in which case
+    # the server bumps twice; the first new version the client sees is the server's first bump
+    assert old == "initial" and new != "initial" and new == server_versions[0]
+    # 4 uploads, barrier 2: uploads computed on a stale version after a bump are dropped
     assert client.num_updates() == 4
 
 
@@ -128,3 +131,40 @@ def test_fedavg_rounds_non_iid():
     assert server.round == 3 and server.version_id == 3
     assert all(c.rounds_done == 3 for c in clients)
     assert not torch.equal(v0, smodel.get_flat())
+
+
+def test_async_sgd_rejected_batches_are_redispatched():
+    """maximumStaleness 0 with 3 racing workers rejects many gradients; every (epoch, batch) must still
+    end with exactly one ADMITTED gradient (at-least-once dispatch, /root/reference/src/server/
+    dataset.ts:47-67), and a shuffled dataset's workers train on the permuted example ids."""
+    x, y = synthetic_mnist(384, seed=3)
+    hub = LocalHub(4)
+    ds = DistriDataset(x, y, {"batchSize": 32, "epochs": 2}, shuffle=True, seed=5)
+    smodel = InMemoryServerModel("mlp_mnist", {"learningRate": 0.05}, device="cpu")
+    server = AsynchronousSGDServer(hub.endpoint(0), smodel, ds,
+                                   {"modelDir": False, "serverHyperparams": {"maximumStaleness": 0}})
+    seen_idx = []
+    server.setup()
+    th = threading.Thread(target=server.serve, kwargs={"until": server.all_done, "timeout": 90}, daemon=True)
+    th.start()
+    workers = [AsynchronousSGDClient(hub.endpoint(r, [0]), ClientModel("mlp_mnist", device="cpu"),
+                                     {"clientId": f"w{r}"}, data=x, labels=y, data_scale=1 / 255) for r in (1, 2, 3)]
+    orig = workers[0]._batch_tensors
+
+    def spy(m):
+        seen_idx.append(list((m.meta.get("data") or {}).get("indices") or []))
+        return orig(m)
+    workers[0]._batch_tensors = spy
+    threads = [threading.Thread(target=lambda w=w: (w.setup(), w.run(timeout=90)), daemon=True) for w in workers]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(90)
+    th.join(10)
+    assert ds.done
+    admitted = server.admitted_batches
+    assert sorted(admitted) == sorted((e, b) for e in range(2) for b in range(ds.batches))
+    assert server.gate.rejected > 0  # the race really produced stale gradients
+    assert server.gate.accepted == len(admitted)
+    assert seen_idx and all(len(i) == 32 for i in seen_idx)
+    assert any(i != list(range(i[0], i[0] + 32)) for i in seen_idx)  # permuted, not row ranges
