@@ -814,7 +814,7 @@ class PSComm {
     check_hip(hipGetDevice(&dev_), "ps getDevice");
     if (rank_ == server_) {
       void* p = nullptr;
-      const size_t bytes = 256 + 3 * (size_t)nstride() * 4;
+      const size_t bytes = sched_off() + 2 * (size_t)dfa::kPSMaxBatches * 4;
       hipError_t e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
       if (e != hipSuccess) {
         (void)hipGetLastError();
@@ -857,6 +857,30 @@ class PSComm {
     check_hip(hipMemcpy(shared_ + 256, w.data_ptr(), (size_t)n_ * 4, hipMemcpyDeviceToDevice), "ps init copy");
     check_hip(hipDeviceSynchronize(), "ps init sync");
   }
+  // Epoch-scoped at-least-once dispatch over `nbatches` microbatch ids, `max_epochs` dataset epochs
+  // (0 = unbounded).  Called with the same values on every rank before the first step.
+  void set_schedule(int64_t nbatches, int64_t max_epochs) {
+    TORCH_CHECK(nbatches > 0 && nbatches <= dfa::kPSMaxBatches, "ps: nbatches out of range");
+    TORCH_CHECK(max_epochs >= 0, "ps: max_epochs must be >= 0");
+    nbatches_ = nbatches;
+    max_epochs_ = (int)max_epochs;
+  }
+  // [epoch, completed in epoch, completed, redispatched, skipped, duplicates, finished]
+  std::vector<int64_t> schedule_stats() const {
+    unsigned e[2] = {0, 0};
+    unsigned long long c[4] = {0, 0, 0, 0};
+    check_hip(hipMemcpy(e, shared_ + 32, 8, hipMemcpyDeviceToHost), "ps sched");
+    check_hip(hipMemcpy(c, shared_ + 48, 32, hipMemcpyDeviceToHost), "ps sched ctr");
+    const bool fin = max_epochs_ > 0 && (int64_t)e[0] >= max_epochs_;
+    return {(int64_t)e[0], (int64_t)e[1], (int64_t)c[0], (int64_t)c[1], (int64_t)c[2], (int64_t)c[3], fin ? 1 : 0};
+  }
+  // done_epoch[0:nbatches]: e + 1 of the last epoch in which each batch was applied
+  std::vector<int64_t> done_epochs() const {
+    std::vector<unsigned> v((size_t)nbatches_);
+    if (nbatches_ > 0)
+      check_hip(hipMemcpy(v.data(), shared_ + sched_off(), (size_t)nbatches_ * 4, hipMemcpyDeviceToHost), "ps done");
+    return std::vector<int64_t>(v.begin(), v.end());
+  }
   void fetch_pull(torch::Tensor w, c10::optional<torch::Tensor> perm, c10::optional<torch::Tensor> idx) {
     dfa::PSArgs a = args();
     need(w, at::kFloat, "ps local master");
@@ -868,6 +892,7 @@ class PSComm {
       need(*idx, at::kLong, "ps idx");
       TORCH_CHECK(perm->dim() == 2 && perm->size(1) == idx->numel(), "ps: perm must be [nbatches][B]");
       TORCH_CHECK(idx->numel() % 2 == 0, "ps: batch size must be even");
+      TORCH_CHECK(nbatches_ == 0 || perm->size(0) == nbatches_, "ps: perm rows != scheduled nbatches");
       a.perm = reinterpret_cast<const long long*>(perm->data_ptr());
       a.idx = reinterpret_cast<long long*>(idx->data_ptr());
       a.nbatches = perm->size(0);
@@ -887,13 +912,13 @@ class PSComm {
   // [accepted, rejected, sum staleness, max staleness, torn retries, err, version, batches claimed]
   std::vector<int64_t> stats() const {
     unsigned long long h[8] = {0};
-    check_hip(hipMemcpy(h, local_ + 64, 48, hipMemcpyDeviceToHost), "ps stats");
+    check_hip(hipMemcpy(h, local_ + 64, 64, hipMemcpyDeviceToHost), "ps stats");
     unsigned seq = 0;
     unsigned long long ctr = 0;
     check_hip(hipMemcpy(&seq, shared_, 4, hipMemcpyDeviceToHost), "ps seq");
     check_hip(hipMemcpy(&ctr, shared_ + 16, 8, hipMemcpyDeviceToHost), "ps ctr");
     return {(int64_t)h[0], (int64_t)h[1], (int64_t)h[2], (int64_t)h[3], (int64_t)h[4], (int64_t)h[5],
-            (int64_t)(seq >> 1), (int64_t)ctr};
+            (int64_t)(seq >> 1), (int64_t)ctr, (int64_t)h[6]};
   }
   // copy of the committed version (call while no worker is stepping)
   void copy_master(torch::Tensor dst) const {
@@ -922,10 +947,20 @@ class PSComm {
     a.scratch = reinterpret_cast<unsigned*>(local_ + 1024);
     a.timeout_ticks = timeout_ticks_;
     a.max_stale = -1;
+    if (nbatches_ > 0) {
+      a.sched = reinterpret_cast<unsigned*>(shared_ + 32);
+      a.sched_ctr = reinterpret_cast<unsigned long long*>(shared_ + 48);
+      a.done_epoch = reinterpret_cast<unsigned*>(shared_ + sched_off());
+      a.claimed_epoch = a.done_epoch + dfa::kPSMaxBatches;
+      a.nbatches = nbatches_;
+      a.max_epochs = max_epochs_;
+    }
     return a;
   }
+  size_t sched_off() const { return 256 + 3 * (size_t)nstride() * 4; }
   int rank_, server_, dev_ = 0;
-  int64_t n_, timeout_ticks_ = 0;
+  int max_epochs_ = 0;
+  int64_t n_, timeout_ticks_ = 0, nbatches_ = 0;
   char* shared_ = nullptr;
   char* local_ = nullptr;
 };
@@ -1008,6 +1043,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("fetch_pull", &PSComm::fetch_pull, py::arg("w"), py::arg("perm") = py::none(), py::arg("idx") = py::none())
       .def("apply", &PSComm::apply, py::arg("g"), py::arg("lr"), py::arg("max_stale"))
       .def("stats", &PSComm::stats)
+      .def("set_schedule", &PSComm::set_schedule, py::arg("nbatches"), py::arg("max_epochs") = 0)
+      .def("schedule_stats", &PSComm::schedule_stats)
+      .def("done_epochs", &PSComm::done_epochs)
       .def("copy_master", &PSComm::copy_master);
   dfa::register_runtime(m);
 }

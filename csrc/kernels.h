@@ -228,12 +228,21 @@ struct PSArgs {
   unsigned* scratch;            // local [64 + kPSMaxGrid] zero-initialised protocol words (async_ps.hip)
   const long long* perm;        // [nbatches][B] example ids (nullptr: no index staging)
   long long* idx;               // [B] staged ids of the claimed microbatch
-  long long* bid_out;           // local: id of the claimed microbatch
+  long long* bid_out;           // local: claimed microbatch (epoch << 32 | batch), -1 = dataset finished
+  // epoch-scoped completion accounting (shared, nullptr = legacy unbounded counter): sched[0] dataset
+  // epoch, sched[1] batches completed in it; sched_ctr[0..3] completed, redispatched, skipped,
+  // duplicate; done_epoch[b] = e + 1 once batch b is applied in epoch e; claimed_epoch[b] likewise
+  // for its first dispatch
+  unsigned* sched;
+  unsigned long long* sched_ctr;
+  unsigned* done_epoch;
+  unsigned* claimed_epoch;
   long long nbatches, timeout_ticks, nstride;
-  int B, max_stale;
+  int B, max_stale, max_epochs;  // max_epochs 0 = unbounded
   float lr;
 };
 constexpr int kPSMaxGrid = 64;
+constexpr long long kPSMaxBatches = 1 << 20;  // capacity of the shared completion arrays
 hipError_t ps_fetch_pull(const PSArgs& a, hipStream_t st);
 hipError_t ps_apply(const PSArgs& a, hipStream_t st);
 

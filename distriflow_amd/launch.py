@@ -307,13 +307,21 @@ def run_async_device(args) -> dict:
     net = build_model(args.model, device=dev, seed=args.seed)
     tr = AsyncPSTrainer(net, lr=args.lr, max_staleness=args.max_staleness, graph="full")
     tr.bind_dataset(x, y, B, scale=1.0 / 255.0 if x.dtype == torch.uint8 else 1.0)
-    tr.bind_schedule(epoch_permutations(n, B, nb * args.epochs, dev, seed=args.seed))
-    steps = max(1, (nb * args.epochs) // world)
+    # one table row per microbatch id of an epoch; at-least-once dispatch per epoch on the device
+    tr.bind_schedule(epoch_permutations(n, B, nb, dev, seed=args.seed), epochs=args.epochs)
     faults = Faults(args, rank)
+    cap = 4 * nb * args.epochs + 64  # a healthy run ends long before: every claim is a real step
     t0 = time.perf_counter()
-    for i in range(steps):
-        faults.step(i)
-        st = tr.step()
+    steps = 0
+    while True:
+        for _ in range(8):
+            faults.step(steps)
+            st = tr.step()
+            steps += 1
+        if tr.finished():
+            break
+        if steps >= cap:
+            raise RuntimeError(f"async PS did not finish {args.epochs} epochs in {steps} steps: {tr.ps_stats()}")
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     if world > 1:

@@ -75,12 +75,18 @@ class AsyncPSTrainer(DataParallelTrainer):
             raise RuntimeError(f"async PS setup failed ({what}) on {'this' if err else 'another'} rank: {err!r}")
 
     # ------------------------------------------------------------------ schedule
-    def bind_schedule(self, perm: torch.Tensor):
+    def bind_schedule(self, perm: torch.Tensor, epochs: int = 0):
         """Global FCFS microbatch table ``perm`` [nbatches][B] (identical on every rank): microbatch id
-        ``b`` (claimed from the shared counter) trains on rows ``perm[b % nbatches]``."""
+        ``b`` trains on rows ``perm[b]``.  Dispatch is at-least-once per dataset epoch, as the
+        reference's DistributedDataset (/root/reference/src/server/dataset.ts:47-67): a batch is
+        complete only when a gradient for it is admitted, rejected (too stale) batches are handed out
+        again on the cursor's next lap, and an epoch ends when all ``nbatches`` are complete.  After
+        ``epochs`` epochs (0 = unbounded) steps become no-ops and :meth:`finished` turns true."""
         if perm.dim() != 2 or perm.shape[1] != self.B:
             raise ValueError(f"schedule must be [nbatches][{self.B}]")
         self._perm = perm.to(self.idx.device, torch.int64).contiguous()
+        self.epochs = int(epochs)
+        self.ps.set_schedule(int(perm.shape[0]), self.epochs)
         self._graph = None
 
     # ------------------------------------------------------------------ one step
@@ -120,10 +126,21 @@ class AsyncPSTrainer(DataParallelTrainer):
 
     # ------------------------------------------------------------------ state
     def ps_stats(self) -> dict:
-        acc, rej, ssum, smax, torn, err, version, claimed = self.ps.stats()
+        acc, rej, ssum, smax, torn, err, version, cursor, noops = self.ps.stats()
+        epoch, in_epoch, completed, redisp, skipped, dups, fin = self.ps.schedule_stats()
         return {"accepted": acc, "rejected": rej, "mean_staleness": ssum / acc if acc else 0.0,
                 "max_staleness": smax, "torn_retries": torn, "error": err, "version": version,
-                "batches_claimed": claimed}
+                "cursor": cursor, "noop_steps": noops, "epoch": epoch, "completed_in_epoch": in_epoch,
+                "completed": completed, "redispatched": redisp, "skipped": skipped, "duplicates": dups,
+                "finished": bool(fin)}
+
+    def finished(self) -> bool:
+        """Every batch of every configured epoch has an admitted gradient (host read; syncs)."""
+        return bool(self.ps.schedule_stats()[6])
+
+    def done_epochs(self) -> list:
+        """Per batch id: 1 + the last epoch in which its gradient was applied (0 = never)."""
+        return list(self.ps.done_epochs())
 
     def check_comm(self):
         err = self.ps.stats()[5]

@@ -90,8 +90,9 @@ def test_async_ps_multi_worker(world, max_stale):
     total = sum(x["accepted"] + x["rejected"] for x in r)
     warm = 3 if r[0]["graph"] == "full" else 0  # graph capture warms up with real steps
     assert total == world * (steps + warm)
-    assert r[0]["batches_claimed"] == total  # one FCFS claim per worker step
     assert r[0]["version"] == sum(x["accepted"] for x in r)  # one published version per accepted gradient
+    # every admitted gradient either completes its batch or is a duplicate of a re-dispatched one
+    assert r[0]["completed"] + r[0]["duplicates"] == sum(x["accepted"] for x in r)
     assert all(x["error"] == 0 and x["finite"] for x in r)
     assert all(x["max_staleness"] <= max_stale for x in r)
     assert sum(x["accepted"] for x in r) >= steps  # progress
@@ -114,5 +115,58 @@ def test_launcher_async_device_engine():
     assert p.returncode == 0, p.stderr[-2000:]
     out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert out["engine"] == "device" and out["error"] == 0
-    assert out["accepted"] + out["rejected"] == out["steps_per_rank"] + 3  # + graph warm-up steps
+    # + graph warm-up steps; steps after the last epoch finished are no-ops
+    assert out["accepted"] + out["rejected"] + out["noop_steps"] == out["steps_per_rank"] + 3
+    assert out["finished"] and out["epoch"] == 3 and out["completed"] == 3 * (16384 // 512)
     assert out["eval_accuracy"] > 0.5
+
+
+def _epoch_worker(rank, world, port, out_dir, epochs, nb):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.async_ps import AsyncPSTrainer
+    from distriflow_amd.parallel.data_parallel import epoch_permutations
+
+    dev = torch.device("cuda", 0)
+    data, labels = synthetic_mnist(nb * 128, seed=3, device=dev)
+    net = build_model("lenet5", device=dev, seed=rank)
+    tr = AsyncPSTrainer(net, lr=0.05, max_staleness=0, graph="full", timeout_s=20.0)
+    tr.bind_dataset(data, labels, 128, scale=1.0 / 255.0)
+    tr.bind_schedule(epoch_permutations(nb * 128, 128, nb, dev, seed=0), epochs=epochs)
+    steps = 0
+    while not tr.finished() and steps < 20 * nb * epochs:
+        for _ in range(4):
+            tr.step()
+            steps += 1
+    torch.cuda.synchronize()
+    dist.barrier()
+    res = tr.ps_stats()
+    res.update(steps=steps, done=tr.done_epochs())
+    torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_async_ps_every_batch_applied_once_per_epoch():
+    """4 workers at maximumStaleness 0 (many rejections): every batch id of every epoch ends with one
+    admitted gradient, rejected batches are re-dispatched, and the run ends after the configured
+    epochs (reference DistributedDataset, /root/reference/src/server/dataset.ts:47-67)."""
+    world, epochs, nb = 4, 2, 16
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_epoch_worker, args=(world, _port(), d, epochs, nb), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"r{i}.pt"), weights_only=True) for i in range(world)]
+    s = r[0]
+    assert s["finished"] and s["epoch"] == epochs and s["error"] == 0
+    assert s["done"] == [epochs] * nb  # each batch completed in the last epoch (and so in every one)
+    assert s["completed"] == epochs * nb
+    acc = sum(x["accepted"] for x in r)
+    rej = sum(x["rejected"] for x in r)
+    assert acc == s["completed"] + s["duplicates"]
+    assert rej == 0 or s["redispatched"] > 0
+    assert all(x["steps"] < 20 * nb * epochs for x in r)
