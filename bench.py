@@ -106,7 +106,7 @@ def main():
     from distriflow_amd.parallel.comm import init_distributed, shutdown
     from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
 
-    env = init_distributed()
+    env = init_distributed(watchdog=True)  # a lost rank ends the job promptly (parallel/watchdog.py)
     world, rank = env.world_size, env.rank
     live_world = dist.get_world_size() if dist.is_initialized() else 1
     live_backend = dist.get_backend() if dist.is_initialized() else "none"

@@ -71,6 +71,7 @@ __global__ __launch_bounds__(kThreads) void p2p_allreduce_kernel(P2PArgs a) {
     while ((int)(__hip_atomic_load(mf, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
       if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) {
         atomicOr(a.err, 1);
+        if (a.herr) __hip_atomic_store(a.herr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         s_bad = 1;
         break;
       }

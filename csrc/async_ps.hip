@@ -229,6 +229,7 @@ __global__ __launch_bounds__(kPSBlock) void ps_fetch_pull_kernel(PSArgs a) {
         *a.vpulled = v;
       } else if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) {
         atomicOr(a.stats + 5, 2ull);
+        if (a.herr) __hip_atomic_store(a.herr, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         s_state = 1;
         *a.vpulled = v;
       }
@@ -302,6 +303,7 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
         }
         if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) {
           atomicOr(a.stats + 5, 4ull);
+        if (a.herr) __hip_atomic_store(a.herr, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -316,6 +318,7 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
         if ((d >> 2) == ep) break;
         if (wall_clock64() - t0 > 2ull * (unsigned long long)a.timeout_ticks) {
           atomicOr(a.stats + 5, 8ull);
+        if (a.herr) __hip_atomic_store(a.herr, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           d = 3;
           break;
         }

@@ -709,6 +709,29 @@ bool convpool_supported_py(int64_t H, int64_t W, int64_t C, int64_t KH, int64_t 
   return dfa::convpool_supported(H, W, C, KH, KW, pad, N);
 }
 
+// A word of host-mapped, coherent pinned memory that kernels write with system-scope stores: the
+// host watchdog (parallel/watchdog.py) polls it with a plain load, so a peer timeout seen on the
+// device is noticed even while the GPU is busy or hung and without queueing any HIP call.
+class HostFlag {
+ public:
+  HostFlag() {
+    check_hip(hipHostMalloc((void**)&host_, 64, hipHostMallocMapped | hipHostMallocCoherent), "host flag alloc");
+    memset(host_, 0, 64);
+    check_hip(hipHostGetDevicePointer((void**)&dev_, host_, 0), "host flag device pointer");
+  }
+  ~HostFlag() {
+    if (host_) (void)hipHostFree(host_);
+  }
+  HostFlag(const HostFlag&) = delete;
+  HostFlag& operator=(const HostFlag&) = delete;
+  int* device() const { return dev_; }
+  int64_t read() const { return *reinterpret_cast<volatile int*>(host_); }
+
+ private:
+  int* host_ = nullptr;
+  int* dev_ = nullptr;
+};
+
 // One-shot xGMI all-reduce communicator (csrc/allreduce_p2p.hip): owns this rank's IPC-exported
 // flag+staging buffer and the peer mappings.  Handles are exchanged by the Python side over the
 // process group (parallel/p2p.py); every launch goes onto PyTorch's current stream (graph capturable).
@@ -777,6 +800,7 @@ class P2PComm {
     a.n = t.numel();
     a.epochs = epochs_;
     a.err = err_;
+    a.herr = herr_.device();
     a.flag_bytes = flag_bytes_;
     a.half_floats = half_;
     a.timeout_ticks = timeout_ticks_;
@@ -791,6 +815,7 @@ class P2PComm {
     check_hip(hipMemcpy(&v, err_, 4, hipMemcpyDeviceToHost), "p2p error readback");
     return v;
   }
+  int64_t host_error() const { return herr_.read(); }  // no HIP call: safe from a watchdog thread
   int64_t max_floats() const { return half_; }
   void set_timeout(double timeout_s) { timeout_ticks_ = (int64_t)(timeout_s * 1e8); }
 
@@ -801,6 +826,7 @@ class P2PComm {
   char* bases_[dfa::kP2PMaxRanks];
   unsigned* epochs_ = nullptr;
   int* err_ = nullptr;
+  HostFlag herr_;
   bool opened_ = false;
 };
 
@@ -857,6 +883,7 @@ class PSComm {
     check_hip(hipMemcpy(shared_ + 256, w.data_ptr(), (size_t)n_ * 4, hipMemcpyDeviceToDevice), "ps init copy");
     check_hip(hipDeviceSynchronize(), "ps init sync");
   }
+  int64_t host_error() const { return herr_.read(); }  // no HIP call: safe from a watchdog thread
   // Epoch-scoped at-least-once dispatch over `nbatches` microbatch ids, `max_epochs` dataset epochs
   // (0 = unbounded).  Called with the same values on every rank before the first step.
   void set_schedule(int64_t nbatches, int64_t max_epochs) {
@@ -947,6 +974,7 @@ class PSComm {
     a.scratch = reinterpret_cast<unsigned*>(local_ + 1024);
     a.timeout_ticks = timeout_ticks_;
     a.max_stale = -1;
+    a.herr = reinterpret_cast<unsigned*>(herr_.device());
     if (nbatches_ > 0) {
       a.sched = reinterpret_cast<unsigned*>(shared_ + 32);
       a.sched_ctr = reinterpret_cast<unsigned long long*>(shared_ + 48);
@@ -958,6 +986,7 @@ class PSComm {
     return a;
   }
   size_t sched_off() const { return 256 + 3 * (size_t)nstride() * 4; }
+  HostFlag herr_;
   int rank_, server_, dev_ = 0;
   int max_epochs_ = 0;
   int64_t n_, timeout_ticks_ = 0, nbatches_ = 0;
@@ -1032,6 +1061,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("open", &P2PComm::open)
       .def("allreduce", &P2PComm::allreduce, py::arg("t"), py::arg("scale") = 1.0)
       .def("error", &P2PComm::error)
+      .def("host_error", &P2PComm::host_error)
       .def("set_timeout", &P2PComm::set_timeout)
       .def_property_readonly("max_floats", &P2PComm::max_floats);
   py::class_<PSComm>(m, "PSComm", "device-resident bounded-staleness parameter server over IPC/xGMI")
@@ -1043,6 +1073,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("fetch_pull", &PSComm::fetch_pull, py::arg("w"), py::arg("perm") = py::none(), py::arg("idx") = py::none())
       .def("apply", &PSComm::apply, py::arg("g"), py::arg("lr"), py::arg("max_stale"))
       .def("stats", &PSComm::stats)
+      .def("host_error", &PSComm::host_error)
       .def("set_schedule", &PSComm::set_schedule, py::arg("nbatches"), py::arg("max_epochs") = 0)
       .def("schedule_stats", &PSComm::schedule_stats)
       .def("done_epochs", &PSComm::done_epochs)

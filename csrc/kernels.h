@@ -207,6 +207,7 @@ struct P2PArgs {
   long long n;
   unsigned* epochs;           // [max_blocks] per-block call counters (local)
   int* err;                   // sticky error word (local): bit 0 = a peer flag timed out
+  int* herr;                  // host-mapped mirror of err (read by the host watchdog without a HIP call)
   long long flag_bytes, half_floats, timeout_ticks;  // timeout in wall_clock64 ticks (100 MHz)
   int rank, world, max_blocks;
   float scale;
@@ -224,7 +225,9 @@ struct PSArgs {
   const float* g;               // local fp32 gradient [n]
   long long n;
   unsigned* vpulled;            // local: version of the last pulled snapshot
-  unsigned long long* stats;    // local [8]: accepted, rejected, sum staleness, max staleness, torn retries, err
+  unsigned long long* stats;    // local [8]: accepted, rejected, sum staleness, max staleness, torn retries, err,
+                                //            no-op steps after the schedule finished
+  unsigned* herr;               // host-mapped mirror of the error bits (host watchdog, no HIP call)
   unsigned* scratch;            // local [64 + kPSMaxGrid] zero-initialised protocol words (async_ps.hip)
   const long long* perm;        // [nbatches][B] example ids (nullptr: no index staging)
   long long* idx;               // [B] staged ids of the claimed microbatch

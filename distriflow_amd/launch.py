@@ -174,6 +174,9 @@ class Faults:
         self.delay = (args.fault_delay_ms / 1e3) if args.fault_delay_rank == rank else 0.0
 
     def step(self, i: int):
+        from .parallel.watchdog import beat
+
+        beat(i)
         if self.delay:
             time.sleep(self.delay)
         if self.kill and i >= self.kill_step:
@@ -219,7 +222,7 @@ def run_sync(args) -> dict:
     from .parallel.comm import init_distributed, shutdown
     from .parallel.data_parallel import DataParallelTrainer, epoch_permutations
 
-    env = init_distributed(device=_device(args))
+    env = init_distributed(device=_device(args), watchdog=True)
     rank, world, dev = env.rank, env.world_size, env.device
     log = _logger(args, f"Distributed Worker {rank}")
     faults = Faults(args, rank)
@@ -282,7 +285,7 @@ def run_sync(args) -> dict:
 def _ps_setup(args):
     from .parallel.comm import init_distributed
 
-    env = init_distributed(device=_device(args))
+    env = init_distributed(device=_device(args), watchdog=True)
     return env
 
 
@@ -298,7 +301,7 @@ def run_async_device(args) -> dict:
     from .parallel.comm import init_distributed, shutdown
     from .parallel.data_parallel import epoch_permutations
 
-    env = init_distributed(device=_device(args))
+    env = init_distributed(device=_device(args), watchdog=True)
     rank, world, dev = env.rank, env.world_size, env.device
     log = _logger(args, f"Distributed Worker {rank}")
     x, y = _load_data(args, dev)
@@ -516,7 +519,7 @@ def run_fedavg_device(args) -> dict:
     from .parallel.comm import init_distributed, shutdown
     from .parallel.fedavg import FedAvgTrainer
 
-    env = init_distributed(device=_device(args))
+    env = init_distributed(device=_device(args), watchdog=True)
     rank, world, dev = env.rank, env.world_size, env.device
     x, y = _load_data(args, dev)
     scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0

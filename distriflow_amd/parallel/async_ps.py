@@ -64,6 +64,9 @@ class AsyncPSTrainer(DataParallelTrainer):
             err = e
         self._agree(err, "IPC open")
         self._perm = None
+        from .watchdog import register_probe
+
+        register_probe("async_ps", self.ps.host_error)
 
     def _agree(self, err, what):
         ok = err is None

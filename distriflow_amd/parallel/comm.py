@@ -36,10 +36,13 @@ class DistEnv:
 _ENV: Optional[DistEnv] = None
 
 
-def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, device: Optional[str] = None) -> DistEnv:
+def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, device: Optional[str] = None,
+                     watchdog: bool = False) -> DistEnv:
     """Initialise from torchrun-style env vars (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT).
 
     backend: "nccl" (RCCL over xGMI, GPUs), "gloo" (CPU), or None = nccl if GPUs are visible else gloo.
+    watchdog: start the dead-peer watchdog (parallel/watchdog.py) once the group is up, so a lost
+    rank ends the job within ``DISTRIFLOW_DEAD_AFTER_S`` (30 s) instead of the collective timeout.
     """
     global _ENV
     rank = int(os.environ.get("RANK", "0"))
@@ -65,6 +68,10 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, de
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     _ENV = DistEnv(rank, world, local, backend if world > 1 else "none", dev)
+    if watchdog and world > 1:
+        from .watchdog import start_watchdog
+
+        start_watchdog(rank, world)
     return _ENV
 
 
@@ -74,6 +81,11 @@ def env() -> DistEnv:
 
 def shutdown():
     global _ENV
+    from .watchdog import active
+
+    wd = active()
+    if wd is not None:
+        wd.stop()  # normal completion: peers stop watching this rank
     if dist.is_initialized():
         try:
             dist.barrier()

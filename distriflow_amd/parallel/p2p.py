@@ -81,6 +81,10 @@ class P2PAllReduce:
             if not passed:
                 self.comm = None
                 self.reason = self.reason or "self-test mismatch"
+        if self.comm is not None:
+            from .watchdog import register_probe
+
+            register_probe(f"p2p_allreduce@{id(self):x}", self.comm.host_error)
 
     @property
     def ok(self) -> bool:

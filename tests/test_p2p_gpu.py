@@ -86,9 +86,19 @@ def _timeout_worker(rank, world, port, out_dir):
     if p.ok and rank == 0:
         x = torch.ones(4096, device="cuda:0")
         p.all_reduce(x)  # rank 1 never joins
+        # the host-mapped mirror shows the timeout while the kernel may still be running, with no HIP
+        # call (this is what the watchdog thread polls)
+        import time
+
+        t0 = time.time()
+        while p.comm.host_error() == 0 and time.time() - t0 < 10.0:
+            time.sleep(0.01)
+        host_flag = p.comm.host_error()
         torch.cuda.synchronize()
         flag = p.comm.error()
-    torch.save({"ok": p.ok, "flag": flag}, os.path.join(out_dir, f"t{rank}.pt"))
+    else:
+        host_flag = None
+    torch.save({"ok": p.ok, "flag": flag, "host_flag": host_flag}, os.path.join(out_dir, f"t{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -138,7 +148,7 @@ def test_p2p_peer_timeout_sets_error_instead_of_hanging():
         mp.spawn(_timeout_worker, args=(2, _port(), d), nprocs=2, join=True)
         t0 = torch.load(os.path.join(d, "t0.pt"), weights_only=True)
     assert t0["ok"]
-    assert t0["flag"] == 1
+    assert t0["flag"] == 1 and t0["host_flag"] == 1
 
 
 @pytest.mark.timeout(240)
