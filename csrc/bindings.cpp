@@ -705,6 +705,117 @@ void head_train_py(std::vector<torch::Tensor> w, std::vector<c10::optional<torch
   check_hip(dfa::head_train(a, (int)phases, cur_stream()), "head_train");
 }
 
+// Whole-network LeNet-5 training step (csrc/lenet_fused.hip): fills the gradients of all ten
+// parameters and stats = [loss sum, correct].  x: uint8 dataset [nrows][28][28][1] read through idx,
+// or a bf16 batch [B][28][28][1].
+void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double scale, torch::Tensor labels,
+                    std::vector<torch::Tensor> conv, std::vector<torch::Tensor> dense_w,
+                    std::vector<torch::Tensor> dense_wt, std::vector<torch::Tensor> dense_b,
+                    std::vector<torch::Tensor> conv_grads, std::vector<torch::Tensor> dense_gw,
+                    std::vector<torch::Tensor> dense_gb, std::vector<torch::Tensor> hT, std::vector<torch::Tensor> dzT,
+                    torch::Tensor conv_part, torch::Tensor loss_part, torch::Tensor stats, int64_t B,
+                    double grad_scale) {
+  TORCH_CHECK(conv.size() == 4 && conv_grads.size() == 4, "lenet: conv = [w1, b1, w2, b2]");
+  TORCH_CHECK(dense_w.size() == 3 && dense_wt.size() == 3 && dense_b.size() == 3 && dense_gw.size() == 3 &&
+                  dense_gb.size() == 3 && hT.size() == 3 && dzT.size() == 3,
+              "lenet: three dense layers");
+  TORCH_CHECK(B > 0 && B < (1 << 30), "lenet: bad batch");
+  dfa::LeNetArgs a{};
+  const int64_t ldt = (B + 31) / 32 * 32;
+  if (x.scalar_type() == at::kByte) {
+    TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.numel() % 784 == 0, "lenet: uint8 dataset [N][28][28][1]");
+    a.x_u8 = x.data_ptr<uint8_t>();
+    a.nrows = x.numel() / 784;
+    TORCH_CHECK(idx.has_value() && idx->defined(), "lenet: a uint8 dataset needs batch indices");
+  } else {
+    need(x, at::kBFloat16, "lenet x");
+    TORCH_CHECK(x.numel() == B * 784, "lenet: x must be [B][28][28][1]");
+    a.x_bf = reinterpret_cast<const dfa::bf16*>(x.data_ptr());
+    a.nrows = B;
+  }
+  if (idx.has_value() && idx->defined()) {
+    need(*idx, at::kLong, "lenet idx");
+    TORCH_CHECK(idx->numel() == B, "lenet: idx must have B entries");
+    a.idx = reinterpret_cast<const long long*>(idx->data_ptr());
+    if (a.x_u8 == nullptr) a.nrows = labels.numel();
+  }
+  need(labels, at::kInt, "lenet labels");
+  TORCH_CHECK(labels.numel() >= (a.idx ? 1 : B), "lenet: labels too small");
+  if (a.idx) a.nrows = std::min<int64_t>(a.nrows, labels.numel());
+  a.labels = labels.data_ptr<int>();
+  a.scale = (float)scale;
+  const int64_t conv_n[4] = {150, 6, 2400, 16};
+  for (int k = 0; k < 4; ++k) {
+    need(conv[k], at::kFloat, "lenet conv param");
+    need(conv_grads[k], at::kFloat, "lenet conv grad");
+    TORCH_CHECK(conv[k].numel() == conv_n[k] && conv_grads[k].numel() == conv_n[k], "lenet: conv param size");
+  }
+  a.w1 = conv[0].data_ptr<float>();
+  a.b1 = conv[1].data_ptr<float>();
+  a.w2 = conv[2].data_ptr<float>();
+  a.b2 = conv[3].data_ptr<float>();
+  const int64_t wsz[3][2] = {{128, 416}, {96, 128}, {16, 96}}, wtsz[3][2] = {{400, 128}, {128, 96}, {96, 32}};
+  const int64_t NK[3][2] = {{120, 400}, {84, 120}, {10, 84}};
+  const dfa::bf16* dw[3];
+  const dfa::bf16* dwt[3];
+  const float* db[3];
+  for (int l = 0; l < 3; ++l) {
+    need(dense_w[l], at::kBFloat16, "lenet dense w");
+    need(dense_wt[l], at::kBFloat16, "lenet dense wt");
+    need(dense_b[l], at::kFloat, "lenet dense b");
+    TORCH_CHECK(dense_w[l].dim() == 2 && dense_w[l].size(0) == wsz[l][0] && dense_w[l].size(1) == wsz[l][1],
+                "lenet: dense ", l, " weights must be [", wsz[l][0], "][", wsz[l][1], "]");
+    TORCH_CHECK(dense_wt[l].dim() == 2 && dense_wt[l].size(0) == wtsz[l][0] && dense_wt[l].size(1) == wtsz[l][1],
+                "lenet: dense ", l, " dgrad weights must be [", wtsz[l][0], "][", wtsz[l][1], "]");
+    TORCH_CHECK(dense_b[l].numel() == NK[l][0], "lenet: dense bias size");
+    need(dense_gw[l], at::kFloat, "lenet dense gw");
+    need(dense_gb[l], at::kFloat, "lenet dense gb");
+    TORCH_CHECK(dense_gw[l].numel() == NK[l][0] * NK[l][1] && dense_gb[l].numel() == NK[l][0],
+                "lenet: dense grad size");
+    need(hT[l], at::kBFloat16, "lenet hT");
+    need(dzT[l], at::kBFloat16, "lenet dzT");
+    TORCH_CHECK(hT[l].dim() == 2 && hT[l].size(0) == NK[l][1] && hT[l].size(1) == ldt, "lenet: hT shape");
+    TORCH_CHECK(dzT[l].dim() == 2 && dzT[l].size(0) == NK[l][0] && dzT[l].size(1) == ldt, "lenet: dzT shape");
+    dw[l] = reinterpret_cast<const dfa::bf16*>(dense_w[l].data_ptr());
+    dwt[l] = reinterpret_cast<const dfa::bf16*>(dense_wt[l].data_ptr());
+    db[l] = dense_b[l].data_ptr<float>();
+  }
+  a.d1w = dw[0]; a.d2w = dw[1]; a.d3w = dw[2];
+  a.d1wt = dwt[0]; a.d2wt = dwt[1]; a.d3wt = dwt[2];
+  a.d1b = db[0]; a.d2b = db[1]; a.d3b = db[2];
+  const int nblk = dfa::lenet_blocks((int)B);
+  need(conv_part, at::kFloat, "lenet conv_part");
+  need(loss_part, at::kFloat, "lenet loss_part");
+  need(stats, at::kFloat, "lenet stats");
+  TORCH_CHECK(conv_part.numel() >= (int64_t)dfa::kLeNetConvParams * nblk, "lenet: conv_part too small");
+  TORCH_CHECK(loss_part.numel() >= 2 * nblk && stats.numel() >= 2, "lenet: loss buffers too small");
+  a.conv_part = conv_part.data_ptr<float>();
+  a.loss_part = loss_part.data_ptr<float>();
+  auto bp = [](torch::Tensor& t) { return reinterpret_cast<dfa::bf16*>(t.data_ptr()); };
+  a.h0T = bp(hT[0]); a.h1T = bp(hT[1]); a.h2T = bp(hT[2]);
+  a.dz1T = bp(dzT[0]); a.dz2T = bp(dzT[1]); a.dz3T = bp(dzT[2]);
+  a.B = (int)B;
+  a.ldt = (int)ldt;
+  a.grad_scale = (float)grad_scale;
+  dfa::LeNetRedArgs r{};
+  r.conv_part = a.conv_part;
+  r.loss_part = a.loss_part;
+  r.stats = stats.data_ptr<float>();
+  r.g_w1 = conv_grads[0].data_ptr<float>();
+  r.g_b1 = conv_grads[1].data_ptr<float>();
+  r.g_w2 = conv_grads[2].data_ptr<float>();
+  r.g_b2 = conv_grads[3].data_ptr<float>();
+  for (int l = 0; l < 3; ++l) {
+    r.L[l].dzT = reinterpret_cast<const dfa::bf16*>(dzT[l].data_ptr());
+    r.L[l].hT = reinterpret_cast<const dfa::bf16*>(hT[l].data_ptr());
+    r.L[l].gw = dense_gw[l].data_ptr<float>();
+    r.L[l].gb = dense_gb[l].data_ptr<float>();
+    r.L[l].N = (int)NK[l][0];
+    r.L[l].K = (int)NK[l][1];
+  }
+  check_hip(dfa::lenet_train(a, r, cur_stream()), "lenet_train");
+}
+
 bool convpool_supported_py(int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t pad, int64_t N) {
   return dfa::convpool_supported(H, W, C, KH, KW, pad, N);
 }
@@ -1036,9 +1147,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                   "stamp buffer: int64 GPU tensor of >= 4096*32 elements");
       dfa::convpool_set_stamps(buf->data_ptr());
       dfa::head_set_stamps(buf->data_ptr());
+      dfa::lenet_set_stamps(buf->data_ptr());
     } else {
       dfa::convpool_set_stamps(nullptr);
       dfa::head_set_stamps(nullptr);
+      dfa::lenet_set_stamps(nullptr);
     }
   }, "profiling aid: per-block phase stamps of the convpool kernels");
   m.def("convpool_fwd_layout", [](int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t pad, int64_t N) {
@@ -1053,6 +1166,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, "data-gradient weight layout of the fused conv+pool kernel: (pair, row length K2pad)");
   m.def("convpool_supported", &convpool_supported_py);
   m.def("head_train", &head_train_py, "fused dense head: forward + softmax-CE + backward (2 launches)");
+  m.def("lenet_train", &lenet_train_py, "whole-network LeNet-5 training step (fwd + CE + bwd, 2 launches)");
+  m.def("lenet_blocks", [](int64_t B) { return dfa::lenet_blocks((int)B); });
   m.def("gather_labels", &gather_labels_py);
   py::class_<P2PComm>(m, "P2PComm", "one-shot xGMI all-reduce over IPC-mapped peer buffers")
       .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("world"), py::arg("max_floats"),

@@ -250,6 +250,49 @@ hipError_t ps_fetch_pull(const PSArgs& a, hipStream_t st);
 hipError_t ps_apply(const PSArgs& a, hipStream_t st);
 
 
+// Whole-network LeNet-5 training step (csrc/lenet_fused.hip): conv5x5x6 'same' + pool, conv5x5x16 +
+// pool, dense 400-120-84-10, softmax-CE, full backward.  Conv weights are read from the fp32 master,
+// dense weights from the bf16 compute copies ([Npad16][Kpad32] and the dgrad layout).
+constexpr int kLeNetPW1 = 0, kLeNetPB1 = 150, kLeNetPW2 = 156, kLeNetPB2 = 2556, kLeNetConvParams = 2572;
+struct LeNetArgs {
+  const unsigned char* x_u8;  // [nrows][784] uint8 dataset read through idx (or null)
+  const bf16* x_bf;           // [B][784] bf16 batch (when x_u8 is null)
+  const long long* idx;       // [B] dataset rows (or null: row r of the batch)
+  long long nrows;
+  float scale;                // uint8 -> value scale
+  const int* labels;          // read through idx like the images
+  const float *w1, *b1, *w2, *b2;  // fp32 master: conv1 [6][25], [6]; conv2 [16][150], [16]
+  const bf16 *d1w, *d1wt, *d2w, *d2wt, *d3w, *d3wt;  // [128][416] [400][128] [96][128] [128][96] [16][96] [96][32]
+  const float *d1b, *d2b, *d3b;
+  float* conv_part;           // [kLeNetConvParams][nblocks] per-workgroup conv gradient partials
+  float* loss_part;           // [nblocks][2]
+  bf16 *h0T, *h1T, *h2T;      // [400|120|84][ldt] transposed dense inputs
+  bf16 *dz1T, *dz2T, *dz3T;   // [120|84|10][ldt] transposed dense output gradients
+  float* logits;              // [B][10] (nullable)
+  unsigned long long* stamps; // diagnostic phase clocks [grid][16] (lenet_set_stamps), or null
+  int B, ldt;
+  float grad_scale;
+};
+struct LeNetDense {
+  const bf16* dzT;
+  const bf16* hT;
+  float* gw;  // [N][K]
+  float* gb;  // [N]
+  int N, K, tiles;
+};
+struct LeNetRedArgs {
+  const float* conv_part;
+  const float* loss_part;
+  float* stats;  // [2] loss sum, correct
+  float *g_w1, *g_b1, *g_w2, *g_b2;
+  LeNetDense L[3];
+  int nblk, ldt, nconv_blocks, dense_tiles;
+};
+size_t lenet_train_lds();
+int lenet_blocks(int B);
+hipError_t lenet_train(const LeNetArgs& a, LeNetRedArgs r, hipStream_t st);
+void lenet_set_stamps(void* buf);
+
 // Direct convolution for C_in <= 4 (csrc/smallc.hip); igemm_fwd / igemm_wgrad dispatch to it.
 bool smallc_fwd_supported(const IGemmArgs& a, int mode);
 hipError_t smallc_fwd(const IGemmArgs& a, hipStream_t st);

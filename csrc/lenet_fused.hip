@@ -1,0 +1,789 @@
+// Whole-network LeNet-5 training step in two launches (gfx950 / MI355X).
+//
+// The reference trains its MNIST CNNs with one tf.js op per layer and per direction
+// (DistributedTfModel.fit, /root/reference/src/common/models.ts:137-142).  The
+// per-layer design of this repo (convpool.hip + mlphead.hip: 9 launches per step) left LeNet-5 at
+// 0.174 ms per 4096-image step, ~60 us of it fixed per-launch cost and the rest VALU-bound im2col.
+// LeNet-5 is small enough that a workgroup can keep EVERYTHING of its images on chip, so here:
+//
+//   lenet_train_kernel   one workgroup = 8 images, 4 waves, 77 KB of LDS (two workgroups per CU):
+//     conv1 5x5 'same' + bias + ReLU + 2x2 max-pool   MFMA with a banded (Toeplitz) weight operand:
+//                          A = 32 consecutive input pixels of a row (one aligned ds_read_b128),
+//                          B = W[ky][k - j][c] for output column j, so no im2col at all
+//     conv2 5x5 + bias + ReLU + pool                  implicit GEMM, output rows in pool-window order
+//                          (a lane's 4 accumulator rows are one 2x2 window: the pool is in-lane)
+//     dense 400-120-84-10 + softmax-CE + backward     MFMA, weights streamed from L2
+//     conv2 weight gradient                           ds_read_b64_tr_b16 transposed reads of both
+//                          operands from their natural NHWC images; bias = a column of ones
+//     conv2 data gradient                             pair-banded MFMA (two output columns per row)
+//     conv1 weight gradient                           per image: unpooled gradient (channel-major)
+//                          x kx-shifted copies of the input, bias = a column of ones
+//   and writes per-workgroup conv gradient partials plus transposed dense activations/gradients;
+//   lenet_reduce_kernel  deterministic reductions: conv partials (one wave per parameter over all
+//                        workgroups), dense weight gradients over the batch (MFMA, K = batch), loss.
+#include "common.h"
+#include "kernels.h"
+
+namespace dfa {
+namespace {
+
+constexpr int IMG = 8;     // images per workgroup
+constexpr int NT = 256;    // threads per workgroup
+// LDS carve (bytes), every offset 16-byte aligned
+constexpr int XS_ELEMS = IMG * 1024 + 32;           // [8][32][32] padded input (+ tail pad)
+constexpr int OFF_XS = 0;
+constexpr int OFF_P1 = OFF_XS + XS_ELEMS * 2;       // [8][196][8] bf16 pool1 output, later its gradient
+constexpr int OFF_C1 = OFF_P1 + IMG * 196 * 16;     // [8][196] u32 pool1 codes (3 bits per channel)
+constexpr int OFF_K = OFF_C1 + IMG * 196 * 4;       // 64 B zeros, 32 B ones (bf16)
+constexpr int OFF_FT = OFF_K + 128;                 // conv2 dgrad table [98][2][16] u8
+constexpr int OFF_W = OFF_FT + 98 * 2 * 16;         // f32 staging: w1 [150], b1 [6], b2 [16]
+constexpr int OFF_U = OFF_W + 704;                  // phase-dependent union
+constexpr int LD0 = 424, LD1 = 136, LD2 = 104, LD3 = 40;  // dense row strides (elements)
+constexpr int OFF_H0 = OFF_U;
+constexpr int OFF_H1 = OFF_H0 + IMG * LD0 * 2;
+constexpr int OFF_H2 = OFF_H1 + IMG * LD1 * 2;
+constexpr int OFF_Z3 = OFF_H2 + IMG * LD2 * 2;
+constexpr int OFF_Z2 = OFF_Z3 + IMG * LD3 * 2;
+constexpr int OFF_Z1 = OFF_Z2 + IMG * LD2 * 2;
+constexpr int OFF_ZR = OFF_Z1 + IMG * LD1 * 2;      // zero row [LD0] (A rows 8..15 of every dense GEMM)
+constexpr int OFF_LG = OFF_ZR + LD0 * 2;            // [8][16] f32 logits
+constexpr int OFF_C2 = OFF_LG + IMG * 16 * 4;       // [8][25][16] u8 pool2 codes
+constexpr int U_DENSE = OFF_C2 + IMG * 25 * 16 - OFF_U;
+constexpr int OFF_DC2 = OFF_U;                      // [800][16] bf16 conv2 output gradient
+constexpr int U_DC2 = 800 * 16 * 2;
+constexpr int OFF_DC1 = OFF_U;                      // [6][28][32] bf16 conv1 output gradient (one image)
+constexpr int OFF_XK = OFF_DC1 + 6 * 28 * 32 * 2;   // [4][32][32] bf16 input shifted by kx = 1..4 (+pad)
+constexpr int U_G = 6 * 28 * 32 * 2 + (4 * 1024 + 32) * 2;
+constexpr int OFF_RED = OFF_U;                      // [4][16][32] f32 cross-wave conv1 wgrad sums
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int LDS_BYTES = OFF_U + cmax(cmax(U_DENSE, U_DC2), cmax(U_G, 4 * 16 * 32 * 4));
+static_assert(OFF_U % 16 == 0 && OFF_H1 % 16 == 0 && OFF_ZR % 16 == 0 && OFF_C2 % 16 == 0 && OFF_XK % 16 == 0,
+              "LDS carve must stay 16-byte aligned");
+static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
+
+typedef __bf16 bf16x4_vs __attribute__((__vector_size__(8)));
+
+// diagnostic per-phase clocks (scripts/lenetstamps.py): [grid][16] s_memtime after each phase's barrier
+#define LN_STAMP(slot)                                                            \
+  do {                                                                            \
+    if (stamps) {                                                                 \
+      __builtin_amdgcn_sched_barrier(0);                                          \
+      unsigned long long t_;                                                      \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+      __builtin_amdgcn_sched_barrier(0);                                          \
+      if (threadIdx.x == 0) stamps[blockIdx.x * 16 + (slot)] = t_;                \
+    }                                                                             \
+  } while (0)
+
+__device__ __forceinline__ bf16x4 tr_read(const bf16* p) {
+  auto* lp = (__attribute__((address_space(3))) bf16*)(const_cast<bf16*>(p));
+  const bf16x4_vs v =
+      __builtin_amdgcn_ds_read_tr16_b64_v4bf16(reinterpret_cast<__attribute__((address_space(3))) bf16x4_vs*>(lp));
+  return __builtin_bit_cast(bf16x4, v);
+}
+__device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    r[e] = a[e];
+    r[e + 4] = b[e];
+  }
+  return r;
+}
+__device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ void st8(bf16* p, const bf16x8& v) { *reinterpret_cast<bf16x8*>(p) = v; }
+__device__ __forceinline__ bf16x8 zero8() {
+  bf16x8 z;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) z[e] = (bf16)0.f;
+  return z;
+}
+
+// 2x2 max-pool of one window (elements in (dy, dx) row-major order) + ReLU; code = argmax position
+// (first maximum), 4 = inactive (no gradient flows: pooled value <= 0).
+__device__ __forceinline__ void pool4(float a00, float a01, float a10, float a11, float& best, unsigned& code) {
+  best = a00;
+  code = 0;
+  if (a01 > best) { best = a01; code = 1; }
+  if (a10 > best) { best = a10; code = 2; }
+  if (a11 > best) { best = a11; code = 3; }
+  if (!(best > 0.f)) { best = 0.f; code = 4; }
+}
+
+// Z[8 rows][N] = A[8][Kpad] W^T (+bias, ReLU); A rows 8..15 of the MFMA tile read the zero row.
+template <int KS>
+__device__ __forceinline__ void dense_fwd(const bf16* A, int lda, const bf16* zr, const bf16* __restrict__ W,
+                                          const float* __restrict__ bias, int N, bool relu, bf16* out, int ldo,
+                                          float* out32, bf16* __restrict__ hT, int ldt, int r0, int rows) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
+  const int ntiles = (N + 15) / 16;
+  const bf16* arow = (i < IMG ? A + i * lda : zr) + 8 * g;
+  for (int t = w; t < ntiles; t += NT / 64) {
+    const int n = 16 * t + i;
+    const bf16* wrow = W + (long long)n * (32 * KS) + 8 * g;
+    bf16x8 b[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) b[s] = ld8(wrow + 32 * s);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) acc = mfma16x16x32(ld8(arow + 32 * s), b[s], acc);
+    if (g >= 2) continue;  // output rows 8..15 are padding
+    const float bv = (bias != nullptr && n < N) ? bias[n] : 0.f;
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r] = acc[r] + bv;
+      if (relu) v[r] = fmaxf(v[r], 0.f);
+      if (n >= N) v[r] = 0.f;
+      const int row = 4 * g + r;
+      if (out) out[row * ldo + n] = f2bf(v[r]);
+      if (out32) out32[row * 16 + (n & 15)] = v[r];
+    }
+    if (hT != nullptr && n < N) {
+      bf16* dst = hT + (long long)n * ldt + r0 + 4 * g;
+      if (4 * g + 4 <= rows) {
+        bf16x4 pk;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pk[r] = f2bf(v[r]);
+        *reinterpret_cast<bf16x4*>(dst) = pk;
+      } else {
+        for (int r = 0; r < 4; ++r)
+          if (4 * g + r < rows) dst[r] = f2bf(v[r]);
+      }
+    }
+  }
+}
+
+// dA[8][K] = dZ[8][32*KS] Wt^T, masked by (mask > 0); also dZ^T rows for the weight gradient.
+template <int KS>
+__device__ __forceinline__ void dense_bwd(const bf16* dZ, int ldz, const bf16* zr, const bf16* __restrict__ Wt, int K,
+                                          const bf16* mask, int ldm, bf16* out, int ldo, bf16* __restrict__ gT,
+                                          int ldt, int r0, int rows) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
+  const int ktiles = (K + 15) / 16;
+  const bf16* zrow = (i < IMG ? dZ + i * ldz : zr) + 8 * g;
+  for (int t = w; t < ktiles; t += NT / 64) {
+    const int j = 16 * t + i;
+    const bf16* wrow = Wt + (long long)j * (32 * KS) + 8 * g;
+    bf16x8 b[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) b[s] = ld8(wrow + 32 * s);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) acc = mfma16x16x32(ld8(zrow + 32 * s), b[s], acc);
+    if (g >= 2) continue;
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * g + r;
+      v[r] = acc[r];
+      if (mask != nullptr && !((float)mask[row * ldm + j] > 0.f)) v[r] = 0.f;
+      if (j >= K) v[r] = 0.f;
+      out[row * ldo + j] = f2bf(v[r]);
+    }
+    if (gT != nullptr && j < K) {
+      bf16* dst = gT + (long long)j * ldt + r0 + 4 * g;
+      if (4 * g + 4 <= rows) {
+        bf16x4 pk;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pk[r] = f2bf(v[r]);
+        *reinterpret_cast<bf16x4*>(dst) = pk;
+      } else {
+        for (int r = 0; r < 4; ++r)
+          if (4 * g + r < rows) dst[r] = f2bf(v[r]);
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* Xs = reinterpret_cast<bf16*>(smem + OFF_XS);
+  bf16* P1 = reinterpret_cast<bf16*>(smem + OFF_P1);
+  unsigned* C1 = reinterpret_cast<unsigned*>(smem + OFF_C1);
+  bf16* KZ = reinterpret_cast<bf16*>(smem + OFF_K);       // 32 zeros
+  bf16* KO = KZ + 32;                                       // 16 ones
+  unsigned char* FT = reinterpret_cast<unsigned char*>(smem + OFF_FT);
+  float* WS = reinterpret_cast<float*>(smem + OFF_W);       // w1[150] b1[6] b2[16]
+  bf16* H0 = reinterpret_cast<bf16*>(smem + OFF_H0);
+  bf16* H1 = reinterpret_cast<bf16*>(smem + OFF_H1);
+  bf16* H2 = reinterpret_cast<bf16*>(smem + OFF_H2);
+  bf16* Z3 = reinterpret_cast<bf16*>(smem + OFF_Z3);
+  bf16* Z2 = reinterpret_cast<bf16*>(smem + OFF_Z2);
+  bf16* Z1 = reinterpret_cast<bf16*>(smem + OFF_Z1);
+  bf16* ZR = reinterpret_cast<bf16*>(smem + OFF_ZR);
+  float* LG = reinterpret_cast<float*>(smem + OFF_LG);
+  unsigned char* C2 = reinterpret_cast<unsigned char*>(smem + OFF_C2);
+  bf16* DC2 = reinterpret_cast<bf16*>(smem + OFF_DC2);
+  bf16* DC1 = reinterpret_cast<bf16*>(smem + OFF_DC1);
+  bf16* XK = reinterpret_cast<bf16*>(smem + OFF_XK);
+  float* RED = reinterpret_cast<float*>(smem + OFF_RED);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15, g = lane >> 4;
+  const int r0 = blockIdx.x * IMG;
+  const int rows = min(IMG, a.B - r0);
+  const long long nb = gridDim.x;
+  float* part = a.conv_part + blockIdx.x;  // transposed partials: parameter p at part[p * nb]
+  unsigned long long* const stamps = a.stamps;
+  LN_STAMP(0);
+
+  // ---------------------------------------------------------------- phase 0: zero fills, staging
+  const bf16x8 z8 = zero8();
+  for (int e = tid; e < XS_ELEMS / 8; e += NT) st8(Xs + 8 * e, z8);
+  for (int e = tid; e < (LDS_BYTES - OFF_U) / 16; e += NT) st8(reinterpret_cast<bf16*>(smem + OFF_U) + 8 * e, z8);
+  if (tid < 4) st8(KZ + 8 * tid, z8);
+  if (tid < 2) {
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)1.f;
+    st8(KO + 8 * tid, o);
+  }
+  if (tid < 150) WS[tid] = a.w1[tid];
+  if (tid < 6) WS[150 + tid] = a.b1[tid];
+  if (tid < 16) WS[156 + tid] = a.b2[tid];
+  // conv2 dgrad table: (y, X2) x half x step -> window-major conv2 output index or 255 (zero row)
+  for (int e = tid; e < 98 * 2 * 16; e += NT) {
+    const int s = e & 15, hf = (e >> 4) & 1, yx = e >> 5;
+    const int y = yx / 7, X2 = yx - 7 * (yx / 7);
+    const int P = 2 * s + hf;
+    unsigned char v = 255;
+    if (P < 30) {
+      const int ky = P / 6, u = P - 6 * (P / 6);
+      const int oy = y - ky, ox = 2 * X2 + 1 - u;
+      if (oy >= 0 && oy < 10 && ox >= 0 && ox < 10)
+        v = (unsigned char)((((oy >> 1) * 5 + (ox >> 1)) << 2) + ((oy & 1) << 1) + (ox & 1));
+    }
+    FT[e] = v;
+  }
+  __syncthreads();
+  // input rows -> bf16, 2-pixel zero border ('same' padding)
+  if (tid < IMG * 28) {
+    const int img = tid / 28, y = tid - 28 * (tid / 28);
+    if (img < rows) {
+      long long src = a.idx ? a.idx[r0 + img] : (long long)(r0 + img);
+      src = src < 0 ? 0 : (src >= a.nrows ? a.nrows - 1 : src);
+      unsigned* dst = reinterpret_cast<unsigned*>(Xs + img * 1024 + (y + 2) * 32 + 2);
+      if (a.x_u8 != nullptr) {
+        const unsigned* p = reinterpret_cast<const unsigned*>(a.x_u8 + src * 784 + y * 28);
+        unsigned v[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) v[k] = p[k];
+#pragma unroll
+        for (int k = 0; k < 7; ++k)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const float f0 = (float)((v[k] >> (16 * h)) & 255u) * a.scale;
+            const float f1 = (float)((v[k] >> (16 * h + 8)) & 255u) * a.scale;
+            const unsigned lo = __builtin_bit_cast(unsigned short, f2bf(f0));
+            const unsigned hi = __builtin_bit_cast(unsigned short, f2bf(f1));
+            dst[2 * k + h] = lo | (hi << 16);
+          }
+      } else {
+        const uint2* p = reinterpret_cast<const uint2*>(a.x_bf + src * 784 + y * 28);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+          const uint2 v = p[k];
+          dst[2 * k] = v.x;
+          dst[2 * k + 1] = v.y;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  LN_STAMP(1);
+
+  // ---------------------------------------------------------------- phase A: conv1 + ReLU + pool
+  {
+    bf16x8 bc[5][6];  // banded B: [ky][channel], column j = output x offset
+#pragma unroll
+    for (int ky = 0; ky < 5; ++ky)
+#pragma unroll
+      for (int c = 0; c < 6; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int kx = 8 * g + e - i;
+          bc[ky][c][e] = f2bf((kx >= 0 && kx < 5) ? WS[c * 25 + ky * 5 + kx] : 0.f);
+        }
+    float b1[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) b1[c] = WS[150 + c];
+    for (int u = w; u < 28; u += NT / 64) {
+      const int mt = u >> 1, x0 = (u & 1) * 16;
+      const int m = 16 * mt + i;
+      const int img = m / 28, y = m - 28 * (m / 28);
+      const bf16* abase = Xs + img * 1024 + y * 32 + x0 + 8 * g;
+      f32x4 acc[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) acc[c] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ky = 0; ky < 5; ++ky) {
+        const bf16x8 av = ld8(abase + ky * 32);
+#pragma unroll
+        for (int c = 0; c < 6; ++c) acc[c] = mfma16x16x32(av, bc[ky][c], acc[c]);
+      }
+      // lane: rows 16mt + 4g + r = (image, y0 + r), column x = x0 + i; partner lane i^1 = column x+1
+      const int m0 = 16 * mt + 4 * g;
+      const int imgo = m0 / 28, y0 = m0 - 28 * (m0 / 28);
+      const int x = x0 + i;
+      bf16x8 o[2];
+      unsigned cw[2] = {0u, 0u};
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        float v[4], p[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[c][r] + b1[c];
+          p[r] = __shfl_xor(v[r], 1, 64);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float best;
+          unsigned code;
+          pool4(v[2 * h], p[2 * h], v[2 * h + 1], p[2 * h + 1], best, code);
+          o[h][c] = f2bf(best);
+          cw[h] |= code << (3 * c);
+        }
+      }
+      if (!(i & 1) && x < 28) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          o[h][6] = (bf16)0.f;
+          o[h][7] = (bf16)0.f;
+          const int pidx = (imgo * 14 + (y0 >> 1) + h) * 14 + (x >> 1);
+          st8(P1 + pidx * 8, o[h]);
+          C1[pidx] = cw[h];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  LN_STAMP(2);
+
+  // ---------------------------------------------------------------- phase B: conv2 + ReLU + pool
+  {
+    bf16x8 bw[7];
+    int toff[7];
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const int tap = 4 * s + g;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        bw[s][e] = f2bf((tap < 25 && e < 6) ? a.w2[i * 150 + tap * 6 + e] : 0.f);
+      toff[s] = tap < 25 ? ((tap / 5) * 14 + (tap - 5 * (tap / 5))) * 8 : 0;
+    }
+    const float b2 = WS[156 + i];
+    for (int mt = w; mt < 50; mt += NT / 64) {
+      const int m = 16 * mt + i;
+      const int img = m / 100, q = m - 100 * (m / 100);
+      const int win = q >> 2, d = q & 3;
+      const int py = win / 5, px = win - 5 * (win / 5);
+      const bf16* abase = P1 + ((img * 14 + 2 * py + (d >> 1)) * 14 + 2 * px + (d & 1)) * 8;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 7; ++s) acc = mfma16x16x32(ld8(abase + toff[s]), bw[s], acc);
+      const int m0 = 16 * mt + 4 * g;
+      const int img0 = m0 / 100, win0 = (m0 - 100 * (m0 / 100)) >> 2;
+      float best;
+      unsigned code;
+      pool4(acc[0] + b2, acc[1] + b2, acc[2] + b2, acc[3] + b2, best, code);
+      H0[img0 * LD0 + win0 * 16 + i] = f2bf(best);
+      C2[(img0 * 25 + win0) * 16 + i] = (unsigned char)code;
+    }
+  }
+  __syncthreads();
+  LN_STAMP(3);
+
+  // ---------------------------------------------------------------- phase C: dense head, CE, backward
+  // H0^T for the dense-1 weight gradient (before H0 is overwritten by its gradient)
+  for (int k = tid; k < 400; k += NT) {
+    bf16* dst = a.h0T + (long long)k * a.ldt + r0;
+    if (rows == IMG) {
+      bf16x8 v;
+#pragma unroll
+      for (int r = 0; r < IMG; ++r) v[r] = H0[r * LD0 + k];
+      st8(dst, v);
+    } else {
+      for (int r = 0; r < rows; ++r) dst[r] = H0[r * LD0 + k];
+    }
+  }
+  dense_fwd<13>(H0, LD0, ZR, a.d1w, a.d1b, 120, true, H1, LD1, nullptr, a.h1T, a.ldt, r0, rows);
+  __syncthreads();
+  dense_fwd<4>(H1, LD1, ZR, a.d2w, a.d2b, 84, true, H2, LD2, nullptr, a.h2T, a.ldt, r0, rows);
+  __syncthreads();
+  dense_fwd<3>(H2, LD2, ZR, a.d3w, a.d3b, 10, false, nullptr, 0, LG, nullptr, a.ldt, r0, rows);
+  __syncthreads();
+  LN_STAMP(4);
+  if (tid < IMG) {
+    const int r = tid;
+    float lsum = 0.f, corr = 0.f;
+    if (r < rows) {
+      const long long src = a.idx ? a.idx[r0 + r] : (long long)(r0 + r);
+      int y = a.labels[src < 0 ? 0 : (src >= a.nrows ? a.nrows - 1 : src)];
+      y = y < 0 ? 0 : (y > 9 ? 9 : y);
+      float mx = -INFINITY;
+      int am = 0;
+      for (int c = 0; c < 10; ++c) {
+        const float z = LG[r * 16 + c];
+        if (a.logits) a.logits[(long long)(r0 + r) * 10 + c] = z;
+        if (z > mx) { mx = z; am = c; }
+      }
+      float pr[10], s = 0.f;
+      for (int c = 0; c < 10; ++c) {
+        pr[c] = __expf(LG[r * 16 + c] - mx);
+        s += pr[c];
+      }
+      const float inv = 1.f / s;
+      lsum = -(LG[r * 16 + y] - mx - __logf(s));
+      corr = am == y ? 1.f : 0.f;
+      for (int c = 0; c < 10; ++c) {
+        const float gv = (pr[c] * inv - (c == y ? 1.f : 0.f)) * a.grad_scale;
+        Z3[r * LD3 + c] = f2bf(gv);
+        a.dz3T[(long long)c * a.ldt + r0 + r] = f2bf(gv);
+      }
+    }
+#pragma unroll
+    for (int o = 4; o > 0; o >>= 1) {
+      lsum += __shfl_xor(lsum, o, 8);
+      corr += __shfl_xor(corr, o, 8);
+    }
+    if (tid == 0) {
+      a.loss_part[2 * blockIdx.x] = lsum;
+      a.loss_part[2 * blockIdx.x + 1] = corr;
+    }
+  }
+  __syncthreads();
+  LN_STAMP(5);
+  dense_bwd<1>(Z3, LD3, ZR, a.d3wt, 84, H2, LD2, Z2, LD2, a.dz2T, a.ldt, r0, rows);
+  __syncthreads();
+  dense_bwd<3>(Z2, LD2, ZR, a.d2wt, 120, H1, LD1, Z1, LD1, a.dz1T, a.ldt, r0, rows);
+  __syncthreads();
+  dense_bwd<4>(Z1, LD1, ZR, a.d1wt, 400, H0, LD0, H0, LD0, nullptr, 0, r0, rows);  // in place: dP2
+  __syncthreads();
+  LN_STAMP(6);
+
+  // ---------------------------------------------------------------- phase D: unpool dP2 -> dC2
+  {
+    bf16x8 dp[2];
+    unsigned long long cd[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int it = tid + k * NT;
+      if (it < IMG * 50) {
+        const int img = it / 50, rem = it - 50 * (it / 50), win = rem >> 1, nh = rem & 1;
+        dp[k] = ld8(H0 + img * LD0 + win * 16 + 8 * nh);
+        cd[k] = *reinterpret_cast<const unsigned long long*>(C2 + (img * 25 + win) * 16 + 8 * nh);
+      }
+    }
+    __syncthreads();  // dC2 overlays H0 / codes2
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int it = tid + k * NT;
+      if (it < IMG * 50) {
+        const int img = it / 50, rem = it - 50 * (it / 50), win = rem >> 1, nh = rem & 1;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          bf16x8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = ((cd[k] >> (8 * e)) & 255u) == (unsigned)d ? dp[k][e] : (bf16)0.f;
+          st8(DC2 + ((img * 100 + win * 4 + d) * 16 + 8 * nh), o);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  LN_STAMP(7);
+
+  // ---------------------------------------------------------------- phase E: conv2 weight gradient
+  {
+    const int q = (lane & 15) >> 2, p = lane & 3;
+    f32x4 acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < 25; ++s) {
+      bf16x4 ta[2];
+      const bf16* pix[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int m = 32 * s + 8 * g + 4 * h + q;
+        ta[h] = tr_read(DC2 + m * 16 + 4 * p);
+        const int img = m / 100, qq = m - 100 * (m / 100), win = qq >> 2, d = qq & 3;
+        const int py = win / 5, px = win - 5 * (win / 5);
+        pix[h] = P1 + ((img * 14 + 2 * py + (d >> 1)) * 14 + 2 * px + (d & 1)) * 8 + 4 * (p & 1);
+      }
+      const bf16x8 av = cat8(ta[0], ta[1]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int T = w + 4 * k;
+        if (T <= 12) {
+          const int tap = 2 * T + (p >> 1);
+          const int toff = ((tap / 5) * 14 + (tap - 5 * (tap / 5))) * 8;
+          bf16x4 tb[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) tb[h] = tr_read(tap < 25 ? pix[h] + toff : KO);
+          acc[k] = mfma16x16x32(av, cat8(tb[0], tb[1]), acc[k]);
+        }
+      }
+    }
+    // D[row = output channel 4g + r][col i = (tap 2T + (i >> 3), channel i & 7)]
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int T = w + 4 * k;
+      if (T <= 12) {
+        const int tap = 2 * T + (i >> 3), c = i & 7;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = 4 * g + r;
+          if (tap < 25 && c < 6) part[(long long)(kLeNetPW2 + n * 150 + tap * 6 + c) * nb] = acc[k][r];
+          else if (tap == 25 && c == 0) part[(long long)(kLeNetPB2 + n) * nb] = acc[k][r];
+        }
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- phase F: conv2 data gradient
+  {
+    bf16x8 bd[15];  // pair-banded B: column (b = i >> 3: output column 2X2 + b, channel c = i & 7)
+    const int bcol = i >> 3, c = i & 7;
+#pragma unroll
+    for (int s = 0; s < 15; ++s) {
+      const int P = 2 * s + (g >> 1);
+      const int ky = P / 6, u = P - 6 * (P / 6);
+      const int kx = u - 1 + bcol;
+      const bool ok = kx >= 0 && kx < 5 && c < 6;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int n = 8 * (g & 1) + e;
+        bd[s][e] = f2bf(ok ? a.w2[n * 150 + (ky * 5 + kx) * 6 + c] : 0.f);
+      }
+    }
+    __syncthreads();  // phase E finished reading P1: it now receives dP1
+  LN_STAMP(8);
+    for (int mt = w; mt < 49; mt += NT / 64) {
+      const int m = 16 * mt + i;
+      const int img = m / 98, rem = m - 98 * (m / 98);
+      const unsigned char* tb = FT + (rem * 2 + (g >> 1)) * 16;
+      const bf16* dbase = DC2 + img * 1600 + 8 * (g & 1);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 15; ++s) {
+        const unsigned t = tb[s];
+        acc = mfma16x16x32(ld8(t == 255u ? KZ : dbase + t * 16), bd[s], acc);
+      }
+      if (c < 6) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int mm = 16 * mt + 4 * g + r;
+          const int im = mm / 98, rm = mm - 98 * (mm / 98);
+          const int y = rm / 7, X2 = rm - 7 * (rm / 7);
+          P1[((im * 14 + y) * 14 + 2 * X2 + bcol) * 8 + c] = f2bf(acc[r]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  LN_STAMP(9);
+
+  // ---------------------------------------------------------------- phase G: conv1 weight gradient
+  {
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const bool a_ok = i < 6;
+    const int tap0 = i, tap1 = 16 + i;
+    for (int img = 0; img < IMG; ++img) {
+      // unpooled channel-major gradient dC1[c][y][x] (x >= 28 zero) of this image
+      for (int it = tid; it < 6 * 14 * 4; it += NT) {
+        const int c = it / 56, rem = it - 56 * (it / 56), py = rem >> 2, xc = rem & 3;
+        bf16x8 o0 = zero8(), o1 = zero8();
+#pragma unroll
+        for (int wd = 0; wd < 4; ++wd) {
+          const int px = 4 * xc + wd;
+          if (px < 14) {
+            const int pidx = (img * 14 + py) * 14 + px;
+            const unsigned code = (C1[pidx] >> (3 * c)) & 7u;
+            const bf16 v = P1[pidx * 8 + c];
+            o0[2 * wd] = code == 0 ? v : (bf16)0.f;
+            o0[2 * wd + 1] = code == 1 ? v : (bf16)0.f;
+            o1[2 * wd] = code == 2 ? v : (bf16)0.f;
+            o1[2 * wd + 1] = code == 3 ? v : (bf16)0.f;
+          }
+        }
+        st8(DC1 + (c * 28 + 2 * py) * 32 + 8 * xc, o0);
+        st8(DC1 + (c * 28 + 2 * py + 1) * 32 + 8 * xc, o1);
+      }
+      // input rows shifted left by kx = 1..4 (aligned B-operand reads)
+      for (int it = tid; it < 4 * 32 * 4; it += NT) {
+        const int kk = it >> 7, rem = it & 127, yp = rem >> 2, xc = rem & 3;
+        const bf16* srow = Xs + img * 1024 + yp * 32 + 8 * xc;
+        const bf16x8 lo = ld8(srow), hi = ld8(srow + 8);
+        bf16 tmp[16];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          tmp[e] = lo[e];
+          tmp[e + 8] = hi[e];
+        }
+        bf16x8 o;
+        const int kx = kk + 1;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = tmp[e + kx];
+        st8(XK + (kk * 32 + yp) * 32 + 8 * xc, o);
+      }
+      __syncthreads();
+      for (int y = w; y < 28; y += NT / 64) {
+        const bf16x8 av = ld8(a_ok ? DC1 + (i * 28 + y) * 32 + 8 * g : KZ);
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+          const int tap = T ? tap1 : tap0;
+          const bf16* bp;
+          if (tap < 25) {
+            const int ky = tap / 5, kx = tap - 5 * (tap / 5);
+            bp = (kx == 0 ? Xs + img * 1024 : XK + (kx - 1) * 1024) + (y + ky) * 32 + 8 * g;
+          } else {
+            bp = tap == 25 ? KO : KZ;
+          }
+          acc[T] = mfma16x16x32(av, ld8(bp), acc[T]);
+        }
+      }
+      __syncthreads();
+    }
+    // cross-wave sum: D[row = channel 4g + r][col = tap 16T + i]
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) RED[(w * 16 + 4 * g + r) * 32 + 16 * T + i] = acc[T][r];
+    __syncthreads();
+    for (int e = tid; e < 6 * 32; e += NT) {
+      const int c = e >> 5, col = e & 31;
+      const float v = RED[(0 * 16 + c) * 32 + col] + RED[(1 * 16 + c) * 32 + col] + RED[(2 * 16 + c) * 32 + col] +
+                      RED[(3 * 16 + c) * 32 + col];
+      if (col < 25) part[(long long)(kLeNetPW1 + c * 25 + col) * nb] = v;
+      else if (col == 25) part[(long long)(kLeNetPB1 + c) * nb] = v;
+    }
+  }
+  LN_STAMP(10);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Reductions: blocks [0, nconv) one wave per conv parameter (sum over the workgroup partials,
+// fixed order), then one block per 16x16 tile of a dense weight gradient (K = batch, 16 waves split
+// it, LDS combine), then one block for the loss partials.  Deterministic.
+constexpr int RT = 1024;
+
+__global__ void __launch_bounds__(RT) lenet_reduce_kernel(LeNetRedArgs a) {
+  __shared__ float red[16][16][17];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int blk = blockIdx.x;
+  if (blk < a.nconv_blocks) {
+    const int p = blk * (RT / 64) + wid;
+    if (p >= kLeNetConvParams) return;
+    const float* src = a.conv_part + (long long)p * a.nblk;
+    float s = 0.f;
+    for (int k = lane; k < a.nblk; k += 64) s += src[k];
+    s = wave_sum(s);
+    if (lane == 0) {
+      float* dst = p < kLeNetPB1 ? a.g_w1 + p
+                   : p < kLeNetPW2 ? a.g_b1 + (p - kLeNetPB1)
+                   : p < kLeNetPB2 ? a.g_w2 + (p - kLeNetPW2)
+                                   : a.g_b2 + (p - kLeNetPB2);
+      *dst = s;
+    }
+    return;
+  }
+  blk -= a.nconv_blocks;
+  if (blk == a.dense_tiles) {  // loss partials -> stats
+    if (wid == 0) {
+      float l = 0.f, c = 0.f;
+      for (int k = lane; k < a.nblk; k += 64) {
+        l += a.loss_part[2 * k];
+        c += a.loss_part[2 * k + 1];
+      }
+      l = wave_sum(l);
+      c = wave_sum(c);
+      if (lane == 0) {
+        a.stats[0] = l;
+        a.stats[1] = c;
+      }
+    }
+    return;
+  }
+  // dense weight-gradient tile: layer l, tile (tn, tk); dW[n][k] = sum_b dZ^T[n][b] H^T[k][b], k == K: bias
+  int l = 0, tile = blk;
+  if (tile >= a.L[0].tiles) {
+    tile -= a.L[0].tiles;
+    l = 1;
+    if (tile >= a.L[1].tiles) {
+      tile -= a.L[1].tiles;
+      l = 2;
+    }
+  }
+  const LeNetDense L = a.L[l];
+  const int ktiles = (L.K + 1 + 15) / 16;
+  const int tn = tile / ktiles, tk = tile - tn * ktiles;
+  const int n = 16 * tn + (lane & 15), k = 16 * tk + (lane & 15);
+  const bf16* arow = L.dzT + (long long)min(n, L.N - 1) * a.ldt + 8 * (lane >> 4);
+  const bf16* brow = L.hT + (long long)min(k, L.K - 1) * a.ldt + 8 * (lane >> 4);
+  const bool a_ok = n < L.N, b_ones = k == L.K, b_ok = k < L.K;
+  bf16x8 ones, zeros = zero8();
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
+  const int steps = a.ldt / 32;
+  const int per = (steps + 15) / 16;
+  const int s0 = wid * per, s1 = min(steps, s0 + per);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int s = s0; s < s1; s += 8) {
+    bf16x8 av[8], bv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int ss = min(s + u, s1 - 1);
+      av[u] = ld8(arow + 32 * ss);
+      bv[u] = ld8(brow + 32 * ss);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool live = s + u < s1;
+      acc = mfma16x16x32((a_ok && live) ? av[u] : zeros, b_ok ? bv[u] : (b_ones ? ones : zeros), acc);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wid][4 * (lane >> 4) + r][lane & 15] = acc[r];
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < 256) {
+    const int rn = t >> 4, ck = t & 15;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 16; ++ww) v += red[ww][rn][ck];
+    const int on = 16 * tn + rn, ok = 16 * tk + ck;
+    if (on < L.N) {
+      if (ok < L.K) L.gw[(long long)on * L.K + ok] = v;
+      else if (ok == L.K) L.gb[on] = v;
+    }
+  }
+}
+
+}  // namespace
+
+size_t lenet_train_lds() { return LDS_BYTES; }
+int lenet_blocks(int B) { return (B + IMG - 1) / IMG; }
+
+static unsigned long long* g_lenet_stamps_host = nullptr;
+void lenet_set_stamps(void* buf) { g_lenet_stamps_host = reinterpret_cast<unsigned long long*>(buf); }
+
+hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
+  LeNetArgs a = a_in;
+  a.stamps = g_lenet_stamps_host;
+  if (a.B <= 0 || a.ldt % 32 || a.ldt < a.B) return hipErrorInvalidValue;
+  const int nblk = (a.B + IMG - 1) / IMG;
+  hipLaunchKernelGGL(lenet_train_kernel, dim3(nblk), dim3(NT), LDS_BYTES, st, a);
+  DFA_HIP_CHECK(hipGetLastError());
+  r.nblk = nblk;
+  r.ldt = a.ldt;
+  r.nconv_blocks = (kLeNetConvParams + RT / 64 - 1) / (RT / 64);
+  r.dense_tiles = 0;
+  for (int l = 0; l < 3; ++l) {
+    r.L[l].tiles = ((r.L[l].N + 15) / 16) * ((r.L[l].K + 1 + 15) / 16);
+    r.dense_tiles += r.L[l].tiles;
+  }
+  hipLaunchKernelGGL(lenet_reduce_kernel, dim3(r.nconv_blocks + r.dense_tiles + 1), dim3(RT), 0, st, r);
+  return hipGetLastError();
+}
+
+}  // namespace dfa

@@ -108,6 +108,29 @@ class Net:
         self.exec_layers = execd
         self.output_shape = shape
         self.head_start = self._plan_head(execd) if self.fuse else None
+        self.lenet_fused = self._plan_lenet(execd) if self.fuse else False
+
+    def _plan_lenet(self, execd) -> bool:
+        """True when the executed graph is exactly LeNet-5 (conv5x5x6 'same' + relu + pool, conv5x5x16 +
+        relu + pool, dense 120 relu, 84 relu, 10) on the GPU: the whole training step then runs as
+        two launches (csrc/lenet_fused.hip).  ``DISTRIFLOW_LENET_FUSED=0`` keeps the per-layer kernels."""
+        import os
+
+        if not self.is_gpu or os.environ.get("DISTRIFLOW_LENET_FUSED", "1") == "0" or not ops.lenet_supported():
+            return False
+        if self.input_shape != (28, 28, 1) or len(execd) != 5:
+            return False
+        c1, c2, d1, d2, d3 = execd
+        if not (isinstance(c1, FusedConvPool) and isinstance(c2, FusedConvPool)):
+            return False
+        convs_ok = all(c.conv.use_bias and c.conv.k == 5 and c.conv.stride == 1 for c in (c1, c2))
+        convs_ok = convs_ok and c1.conv.filters == 6 and c1.conv.pad == 2 and c1.in_shape == (28, 28, 1)
+        convs_ok = convs_ok and c2.conv.filters == 16 and c2.conv.pad == 0 and c2.in_shape == (14, 14, 6)
+        dense = (d1, d2, d3)
+        if not convs_ok or not all(isinstance(d, Dense) and d.use_bias for d in dense):
+            return False
+        return ((d1.in_features, d1.units, d2.units, d3.units) == (400, 120, 84, 10) and d1.relu and d2.relu
+                and not d3.relu)
 
     def _plan_head(self, execd):
         """Index of the first layer of the trailing Dense chain trained by the fused head kernels
@@ -177,6 +200,10 @@ class Net:
             self.head_hT = [z(l.units, ldt) for l in head[:-1]] + [None]
             self.head_dzT = [z(l.units, ldt) for l in head]
             self.head_loss_part = torch.zeros(2 * ((B + 15) // 16), dtype=torch.float32, device=self.device)
+        if self.lenet_fused:
+            nblk = ops.lenet_blocks(B)
+            self.lenet_conv_part = torch.empty(2572 * nblk, dtype=torch.float32, device=self.device)
+            self.lenet_loss_part = torch.zeros(2 * nblk, dtype=torch.float32, device=self.device)
         self._bound_B = B
         self.graphs = {}
 
@@ -214,6 +241,8 @@ class Net:
             x = x.to(self.dtype)
         if self.has_dropout:
             self.step_dev.add_(1)
+        if self.lenet_fused:
+            return self._compute_gradients_lenet(x, labels, grad_ready)
         if self.head_start is not None:
             return self._compute_gradients_head(x, labels, grad_ready)
         if isinstance(labels, ops.LabelRef):
@@ -224,6 +253,27 @@ class Net:
         stats = self.loss_and_grad(logits, labels)
         self.backward(self.dlogits, grad_ready)
         return stats
+
+    def _compute_gradients_lenet(self, x, labels, grad_ready):
+        """The whole LeNet-5 step in two launches (csrc/lenet_fused.hip); every gradient is final when
+        they end, so all gradient hooks fire afterwards (one bucket's all-reduce)."""
+        B = x.shape[0]
+        self.bind(B)
+        st = self.store
+        c1, c2, d1, d2, d3 = self.exec_layers
+        conv = [st[f"{c1.name}/kernel"], st[f"{c1.name}/bias"], st[f"{c2.name}/kernel"], st[f"{c2.name}/bias"]]
+        cgrads = [st.gradient(f"{c1.name}/kernel"), st.gradient(f"{c1.name}/bias"),
+                  st.gradient(f"{c2.name}/kernel"), st.gradient(f"{c2.name}/bias")]
+        dense = (d1, d2, d3)
+        ops.lenet_train(x, labels, conv, [st.weight(f"{d.name}/kernel") for d in dense],
+                        [st.weight_t(f"{d.name}/kernel") for d in dense], [st[f"{d.name}/bias"] for d in dense],
+                        cgrads, [st.grad_matrix(f"{d.name}/kernel") for d in dense],
+                        [st.gradient(f"{d.name}/bias") for d in dense], [self.head_xT] + self.head_hT[:2],
+                        self.head_dzT, self.lenet_conv_part, self.lenet_loss_part, self.stats, 1.0 / B)
+        if grad_ready is not None:
+            for i in range(len(self.exec_layers) - 1, -1, -1):
+                grad_ready(i)
+        return self.stats
 
     def _compute_gradients_head(self, x, labels, grad_ready):
         """Body layers one by one, then the fused dense head (2 launches: forward + CE + backward data

@@ -351,6 +351,36 @@ def head_train(w, wt, b, gw, gb, hT, dzT, K, N, x, x_relu, xT, dx, logits, label
                     bool(x_relu), xT, dx, logits, labels, idx, float(grad_scale), loss_part, stats, int(phases))
 
 
+def lenet_supported() -> bool:
+    m = native.get(build_if_missing=False)
+    return m is not None and hasattr(m, "lenet_train")
+
+
+def lenet_blocks(B: int) -> int:
+    return int(_C().lenet_blocks(int(B)))
+
+
+def lenet_train(x, labels, conv, dense_w, dense_wt, dense_b, conv_grads, dense_gw, dense_gb, hT, dzT, conv_part,
+                loss_part, stats, grad_scale):
+    """Whole-network LeNet-5 training step on GPU (csrc/lenet_fused.hip, 2 launches): fills every
+    gradient and ``stats`` = [loss sum, correct].  ``x``: bf16 batch [B,28,28,1] or a :class:`GatherRef`
+    over a uint8 dataset; ``labels``: int32 [B] or a :class:`LabelRef` through the same indices."""
+    if isinstance(x, GatherRef):
+        src, idx, scale = x.data, x.idx, x.scale
+    else:
+        src, idx, scale = x.contiguous(), None, 1.0
+    if isinstance(labels, LabelRef):
+        lab, lidx = labels.labels, labels.idx
+        if idx is None:
+            idx = lidx
+    else:
+        lab = labels if labels.dtype == torch.int32 else labels.to(torch.int32)
+    B = x.shape[0]
+    _C().lenet_train(src, idx, float(scale), lab, list(conv), list(dense_w), list(dense_wt), list(dense_b),
+                     list(conv_grads), list(dense_gw), list(dense_gb), list(hT), list(dzT), conv_part, loss_part,
+                     stats, int(B), float(grad_scale))
+
+
 def convpool_supported(H, W, C, KH, KW, pad, N) -> bool:
     m = native.get(build_if_missing=False)
     if m is None:

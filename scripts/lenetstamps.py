@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Phase breakdown of the whole-network LeNet-5 training kernel (csrc/lenet_fused.hip) from in-kernel
+s_memtime stamps (thread 0 of every workgroup, after each phase's barrier), B=4096, plus the wall time
+of both launches with and without stamping.  Slots: 0 start, 1 staged, 2 conv1, 3 conv2, 4 dense
+forward, 5 CE, 6 dense backward, 7 unpool, 8 conv2 wgrad (+dgrad weights), 9 conv2 dgrad, 10 conv1 wgrad."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from distriflow_amd import native, ops  # noqa: E402
+from distriflow_amd.data.synthetic import synthetic_mnist  # noqa: E402
+from distriflow_amd.models.zoo import build_model  # noqa: E402
+
+NAMES = ["stage", "conv1", "conv2", "dense fwd", "CE", "dense bwd", "unpool", "conv2 wgrad", "conv2 dgrad",
+         "conv1 wgrad"]
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    m = native.require()
+    net = build_model("lenet5", device="cuda", seed=0)
+    assert net.lenet_fused
+    data, labels = synthetic_mnist(60000, seed=1, device="cuda")
+    idx = torch.randperm(60000, device="cuda")[:B]
+    x, y = ops.GatherRef(data, idx, 1 / 255.0, (28, 28, 1)), ops.LabelRef(labels, idx)
+
+    def wall(n=50):
+        for _ in range(3):
+            net.compute_gradients(x, y)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            net.compute_gradients(x, y)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / n * 1e3
+
+    base = wall()
+    nblk = ops.lenet_blocks(B)
+    buf = torch.zeros(max(nblk * 16, 4096 * 32), dtype=torch.int64, device="cuda")
+    m.convpool_set_stamps(buf)
+    stamped = wall(5)
+    m.convpool_set_stamps(None)
+    st = buf[: nblk * 16].view(nblk, 16).cpu().numpy().astype(np.int64)
+    d = np.diff(st[:, :11], axis=1)
+    print(f"B={B}: {nblk} workgroups; both launches {base:.1f} us/step (stamped {stamped:.1f})")
+    tot = st[:, 10] - st[:, 0]
+    print(f"kernel-1 workgroup lifetime: median {np.median(tot):.0f} cycles, max {tot.max():.0f}; "
+          f"start spread {st[:, 0].max() - st[:, 0].min():.0f}")
+    for k, name in enumerate(NAMES):
+        col = d[:, k]
+        print(f"  {name:<12} median {np.median(col):8.0f}  p90 {np.percentile(col, 90):8.0f}  "
+              f"share {np.median(col) / np.median(tot) * 100:5.1f}%")
+
+
+if __name__ == "__main__":
+    main()
