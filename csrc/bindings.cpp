@@ -713,8 +713,8 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
                     std::vector<torch::Tensor> dense_wt, std::vector<torch::Tensor> dense_b,
                     std::vector<torch::Tensor> conv_grads, std::vector<torch::Tensor> dense_gw,
                     std::vector<torch::Tensor> dense_gb, std::vector<torch::Tensor> hT, std::vector<torch::Tensor> dzT,
-                    torch::Tensor conv_part, torch::Tensor loss_part, torch::Tensor stats, int64_t B,
-                    double grad_scale) {
+                    torch::Tensor conv_part, torch::Tensor loss_part, torch::Tensor stats, torch::Tensor frag,
+                    torch::Tensor ftab, torch::Tensor pxtab, int64_t B, double grad_scale) {
   TORCH_CHECK(conv.size() == 4 && conv_grads.size() == 4, "lenet: conv = [w1, b1, w2, b2]");
   TORCH_CHECK(dense_w.size() == 3 && dense_wt.size() == 3 && dense_b.size() == 3 && dense_gw.size() == 3 &&
                   dense_gb.size() == 3 && hT.size() == 3 && dzT.size() == 3,
@@ -794,6 +794,13 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
   auto bp = [](torch::Tensor& t) { return reinterpret_cast<dfa::bf16*>(t.data_ptr()); };
   a.h0T = bp(hT[0]); a.h1T = bp(hT[1]); a.h2T = bp(hT[2]);
   a.dz1T = bp(dzT[0]); a.dz2T = bp(dzT[1]); a.dz3T = bp(dzT[2]);
+  TORCH_CHECK(frag.is_cuda() && frag.is_contiguous() && (size_t)frag.nbytes() >= dfa::lenet_frag_bytes(),
+              "lenet: fragment buffer too small");
+  TORCH_CHECK(ftab.is_cuda() && ftab.scalar_type() == at::kByte && ftab.numel() == 98 * 2 * 16, "lenet: ftab");
+  TORCH_CHECK(pxtab.is_cuda() && pxtab.scalar_type() == at::kShort && pxtab.numel() == 800, "lenet: pxtab");
+  a.frag = frag.data_ptr();
+  a.ftab = ftab.data_ptr<uint8_t>();
+  a.pxtab = reinterpret_cast<const unsigned short*>(pxtab.data_ptr());
   a.B = (int)B;
   a.ldt = (int)ldt;
   a.grad_scale = (float)grad_scale;
@@ -1168,6 +1175,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("head_train", &head_train_py, "fused dense head: forward + softmax-CE + backward (2 launches)");
   m.def("lenet_train", &lenet_train_py, "whole-network LeNet-5 training step (fwd + CE + bwd, 2 launches)");
   m.def("lenet_blocks", [](int64_t B) { return dfa::lenet_blocks((int)B); });
+  m.def("lenet_frag_bytes", []() { return (int64_t)dfa::lenet_frag_bytes(); });
   m.def("gather_labels", &gather_labels_py);
   py::class_<P2PComm>(m, "P2PComm", "one-shot xGMI all-reduce over IPC-mapped peer buffers")
       .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("world"), py::arg("max_floats"),

@@ -269,6 +269,9 @@ struct LeNetArgs {
   bf16 *h0T, *h1T, *h2T;      // [400|120|84][ldt] transposed dense inputs
   bf16 *dz1T, *dz2T, *dz3T;   // [120|84|10][ldt] transposed dense output gradients
   float* logits;              // [B][10] (nullable)
+  const void* frag;           // [37][64] x 8 bf16 conv weight fragments of this step (written by the prep launch)
+  const unsigned char* ftab;  // [98][2][16] conv2 dgrad gather table (lenet_tables)
+  const unsigned short* pxtab;  // [800] conv2 output row -> pool1 pixel (lenet_tables)
   unsigned long long* stamps; // diagnostic phase clocks [grid][16] (lenet_set_stamps), or null
   int B, ldt;
   float grad_scale;
@@ -292,6 +295,7 @@ size_t lenet_train_lds();
 int lenet_blocks(int B);
 hipError_t lenet_train(const LeNetArgs& a, LeNetRedArgs r, hipStream_t st);
 void lenet_set_stamps(void* buf);
+size_t lenet_frag_bytes();
 
 // Direct convolution for C_in <= 4 (csrc/smallc.hip); igemm_fwd / igemm_wgrad dispatch to it.
 bool smallc_fwd_supported(const IGemmArgs& a, int mode);

@@ -1,4 +1,4 @@
-// Whole-network LeNet-5 training step in two launches (gfx950 / MI355X).
+// Whole-network LeNet-5 training step in three launches (gfx950 / MI355X).
 //
 // The reference trains its MNIST CNNs with one tf.js op per layer and per direction
 // (DistributedTfModel.fit, /root/reference/src/common/models.ts:137-142).  The
@@ -6,18 +6,21 @@
 // 0.174 ms per 4096-image step, ~60 us of it fixed per-launch cost and the rest VALU-bound im2col.
 // LeNet-5 is small enough that a workgroup can keep EVERYTHING of its images on chip, so here:
 //
-//   lenet_train_kernel   one workgroup = 8 images, 4 waves, 77 KB of LDS (two workgroups per CU):
+//   lenet_prep_kernel    the conv weights of this step as ready-made MFMA B fragments (banded conv1,
+//                        conv2 forward, pair-banded conv2 data gradient): 37 x 1 KB, read by every
+//                        workgroup with one 16-byte load per lane and fragment
+//   lenet_train_kernel   one workgroup = 8 images, 4 waves, ~78 KB of LDS (two workgroups per CU):
 //     conv1 5x5 'same' + bias + ReLU + 2x2 max-pool   MFMA with a banded (Toeplitz) weight operand:
-//                          A = 32 consecutive input pixels of a row (one aligned ds_read_b128),
-//                          B = W[ky][k - j][c] for output column j, so no im2col at all
+//                          A = 32 consecutive input pixels of a row (one aligned ds_read_b128; odd
+//                          output columns read a copy of the image shifted by one pixel), so the
+//                          4 accumulator rows of a lane are one 2x2 pool window: the pool is in-lane
 //     conv2 5x5 + bias + ReLU + pool                  implicit GEMM, output rows in pool-window order
-//                          (a lane's 4 accumulator rows are one 2x2 window: the pool is in-lane)
 //     dense 400-120-84-10 + softmax-CE + backward     MFMA, weights streamed from L2
 //     conv2 weight gradient                           ds_read_b64_tr_b16 transposed reads of both
 //                          operands from their natural NHWC images; bias = a column of ones
 //     conv2 data gradient                             pair-banded MFMA (two output columns per row)
-//     conv1 weight gradient                           per image: unpooled gradient (channel-major)
-//                          x kx-shifted copies of the input, bias = a column of ones
+//     conv1 weight gradient                           A fragments unpooled in registers from the pool
+//                          gradient + argmax codes, B = 4 dword reads of the (shifted) input image
 //   and writes per-workgroup conv gradient partials plus transposed dense activations/gradients;
 //   lenet_reduce_kernel  deterministic reductions: conv partials (one wave per parameter over all
 //                        workgroups), dense weight gradients over the batch (MFMA, K = batch), loss.
@@ -29,15 +32,19 @@ namespace {
 
 constexpr int IMG = 8;     // images per workgroup
 constexpr int NT = 256;    // threads per workgroup
+constexpr int NFRAG = 37;  // prep fragments: conv1 banded [5 ky][3 channel pairs], conv2 fwd [7], dgrad [15]
+constexpr int FR_C1 = 0, FR_C2 = 15, FR_DG = 22;
 // LDS carve (bytes), every offset 16-byte aligned
 constexpr int XS_ELEMS = IMG * 1024 + 32;           // [8][32][32] padded input (+ tail pad)
 constexpr int OFF_XS = 0;
 constexpr int OFF_P1 = OFF_XS + XS_ELEMS * 2;       // [8][196][8] bf16 pool1 output, later its gradient
 constexpr int OFF_C1 = OFF_P1 + IMG * 196 * 16;     // [8][196] u32 pool1 codes (3 bits per channel)
 constexpr int OFF_K = OFF_C1 + IMG * 196 * 4;       // 64 B zeros, 32 B ones (bf16)
-constexpr int OFF_FT = OFF_K + 128;                 // conv2 dgrad table [98][2][16] u8
-constexpr int OFF_W = OFF_FT + 98 * 2 * 16;         // f32 staging: w1 [150], b1 [6], b2 [16]
-constexpr int OFF_U = OFF_W + 704;                  // phase-dependent union
+constexpr int OFF_FT = OFF_K + 128;                 // conv2 dgrad table [98][2][16] u8 (host-built)
+constexpr int OFF_PX = OFF_FT + 98 * 2 * 16;        // conv2 output row -> P1 pixel [800] u16 (host-built)
+constexpr int OFF_W = OFF_PX + 800 * 2;             // f32: b1 [6], b2 [16]
+constexpr int OFF_U = OFF_W + 128;                  // phase-dependent union
+constexpr int OFF_XS1 = OFF_U;                      // phases A and G: input shifted left by one pixel
 constexpr int LD0 = 424, LD1 = 136, LD2 = 104, LD3 = 40;  // dense row strides (elements)
 constexpr int OFF_H0 = OFF_U;
 constexpr int OFF_H1 = OFF_H0 + IMG * LD0 * 2;
@@ -51,13 +58,12 @@ constexpr int OFF_C2 = OFF_LG + IMG * 16 * 4;       // [8][25][16] u8 pool2 code
 constexpr int U_DENSE = OFF_C2 + IMG * 25 * 16 - OFF_U;
 constexpr int OFF_DC2 = OFF_U;                      // [800][16] bf16 conv2 output gradient
 constexpr int U_DC2 = 800 * 16 * 2;
-constexpr int OFF_DC1 = OFF_U;                      // [6][28][32] bf16 conv1 output gradient (one image)
-constexpr int OFF_XK = OFF_DC1 + 6 * 28 * 32 * 2;   // [4][32][32] bf16 input shifted by kx = 1..4 (+pad)
-constexpr int U_G = 6 * 28 * 32 * 2 + (4 * 1024 + 32) * 2;
-constexpr int OFF_RED = OFF_U;                      // [4][16][32] f32 cross-wave conv1 wgrad sums
+constexpr int OFF_RED = OFF_U + XS_ELEMS * 2;       // [4][16][32] f32 cross-wave conv1 wgrad sums
+constexpr int U_G = XS_ELEMS * 2 + 4 * 16 * 32 * 4;
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int LDS_BYTES = OFF_U + cmax(cmax(U_DENSE, U_DC2), cmax(U_G, 4 * 16 * 32 * 4));
-static_assert(OFF_U % 16 == 0 && OFF_H1 % 16 == 0 && OFF_ZR % 16 == 0 && OFF_C2 % 16 == 0 && OFF_XK % 16 == 0,
+constexpr int LDS_BYTES = OFF_U + cmax(cmax(U_DENSE, U_DC2), U_G);
+static_assert(OFF_U % 16 == 0 && OFF_H1 % 16 == 0 && OFF_ZR % 16 == 0 && OFF_C2 % 16 == 0 && OFF_RED % 16 == 0 &&
+                  OFF_PX % 16 == 0 && OFF_W % 16 == 0,
               "LDS carve must stay 16-byte aligned");
 static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
 
@@ -97,6 +103,20 @@ __device__ __forceinline__ bf16x8 zero8() {
 #pragma unroll
   for (int e = 0; e < 8; ++e) z[e] = (bf16)0.f;
   return z;
+}
+
+// Xs1[e] = Xs[e + 1]: the padded images shifted left by one pixel (dword-aligned funnel shift)
+__device__ __forceinline__ void build_shift1(const bf16* Xs, bf16* Xs1) {
+  for (int t = threadIdx.x; t < XS_ELEMS / 8 - 1; t += NT) {
+    const uint4 lo = *reinterpret_cast<const uint4*>(Xs + 8 * t);
+    const unsigned nx = *reinterpret_cast<const unsigned*>(Xs + 8 * t + 8);
+    uint4 o;
+    o.x = __builtin_amdgcn_alignbyte(lo.y, lo.x, 2);
+    o.y = __builtin_amdgcn_alignbyte(lo.z, lo.y, 2);
+    o.z = __builtin_amdgcn_alignbyte(lo.w, lo.z, 2);
+    o.w = __builtin_amdgcn_alignbyte(nx, lo.w, 2);
+    *reinterpret_cast<uint4*>(Xs1 + 8 * t) = o;
+  }
 }
 
 // 2x2 max-pool of one window (elements in (dy, dx) row-major order) + ReLU; code = argmax position
@@ -199,12 +219,14 @@ __device__ __forceinline__ void dense_bwd(const bf16* dZ, int ldz, const bf16* z
 __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* Xs = reinterpret_cast<bf16*>(smem + OFF_XS);
+  bf16* Xs1 = reinterpret_cast<bf16*>(smem + OFF_XS1);
   bf16* P1 = reinterpret_cast<bf16*>(smem + OFF_P1);
   unsigned* C1 = reinterpret_cast<unsigned*>(smem + OFF_C1);
   bf16* KZ = reinterpret_cast<bf16*>(smem + OFF_K);       // 32 zeros
   bf16* KO = KZ + 32;                                       // 16 ones
   unsigned char* FT = reinterpret_cast<unsigned char*>(smem + OFF_FT);
-  float* WS = reinterpret_cast<float*>(smem + OFF_W);       // w1[150] b1[6] b2[16]
+  unsigned short* PX = reinterpret_cast<unsigned short*>(smem + OFF_PX);
+  float* WS = reinterpret_cast<float*>(smem + OFF_W);       // b1[6] b2[16]
   bf16* H0 = reinterpret_cast<bf16*>(smem + OFF_H0);
   bf16* H1 = reinterpret_cast<bf16*>(smem + OFF_H1);
   bf16* H2 = reinterpret_cast<bf16*>(smem + OFF_H2);
@@ -215,21 +237,24 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
   float* LG = reinterpret_cast<float*>(smem + OFF_LG);
   unsigned char* C2 = reinterpret_cast<unsigned char*>(smem + OFF_C2);
   bf16* DC2 = reinterpret_cast<bf16*>(smem + OFF_DC2);
-  bf16* DC1 = reinterpret_cast<bf16*>(smem + OFF_DC1);
-  bf16* XK = reinterpret_cast<bf16*>(smem + OFF_XK);
   float* RED = reinterpret_cast<float*>(smem + OFF_RED);
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15, g = lane >> 4;
   const int r0 = blockIdx.x * IMG;
   const int rows = min(IMG, a.B - r0);
   const long long nb = gridDim.x;
+  const bf16x8* __restrict__ frag = reinterpret_cast<const bf16x8*>(a.frag);
   float* part = a.conv_part + blockIdx.x;  // transposed partials: parameter p at part[p * nb]
   unsigned long long* const stamps = a.stamps;
   LN_STAMP(0);
 
   // ---------------------------------------------------------------- phase 0: zero fills, staging
+  // conv1 B fragments of this step (lenet_prep_kernel): in flight while the images load
+  bf16x8 bc[15];
+#pragma unroll
+  for (int f = 0; f < 15; ++f) bc[f] = frag[(FR_C1 + f) * 64 + lane];
   const bf16x8 z8 = zero8();
-  for (int e = tid; e < XS_ELEMS / 8; e += NT) st8(Xs + 8 * e, z8);
+  for (int e = tid; e < (OFF_K - OFF_XS) / 16; e += NT) st8(Xs + 8 * e, z8);  // Xs, P1 (pad channels), C1
   for (int e = tid; e < (LDS_BYTES - OFF_U) / 16; e += NT) st8(reinterpret_cast<bf16*>(smem + OFF_U) + 8 * e, z8);
   if (tid < 4) st8(KZ + 8 * tid, z8);
   if (tid < 2) {
@@ -238,23 +263,10 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
     for (int e = 0; e < 8; ++e) o[e] = (bf16)1.f;
     st8(KO + 8 * tid, o);
   }
-  if (tid < 150) WS[tid] = a.w1[tid];
-  if (tid < 6) WS[150 + tid] = a.b1[tid];
-  if (tid < 16) WS[156 + tid] = a.b2[tid];
-  // conv2 dgrad table: (y, X2) x half x step -> window-major conv2 output index or 255 (zero row)
-  for (int e = tid; e < 98 * 2 * 16; e += NT) {
-    const int s = e & 15, hf = (e >> 4) & 1, yx = e >> 5;
-    const int y = yx / 7, X2 = yx - 7 * (yx / 7);
-    const int P = 2 * s + hf;
-    unsigned char v = 255;
-    if (P < 30) {
-      const int ky = P / 6, u = P - 6 * (P / 6);
-      const int oy = y - ky, ox = 2 * X2 + 1 - u;
-      if (oy >= 0 && oy < 10 && ox >= 0 && ox < 10)
-        v = (unsigned char)((((oy >> 1) * 5 + (ox >> 1)) << 2) + ((oy & 1) << 1) + (ox & 1));
-    }
-    FT[e] = v;
-  }
+  if (tid < 6) WS[tid] = a.b1[tid];
+  if (tid < 16) WS[6 + tid] = a.b2[tid];
+  if (tid < 98 * 2) reinterpret_cast<uint4*>(FT)[tid] = reinterpret_cast<const uint4*>(a.ftab)[tid];
+  if (tid < 100) reinterpret_cast<uint4*>(PX)[tid] = reinterpret_cast<const uint4*>(a.pxtab)[tid];
   __syncthreads();
   // input rows -> bf16, 2-pixel zero border ('same' padding)
   if (tid < IMG * 28) {
@@ -290,70 +302,45 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
     }
   }
   __syncthreads();
+  build_shift1(Xs, Xs1);
+  __syncthreads();
   LN_STAMP(1);
 
   // ---------------------------------------------------------------- phase A: conv1 + ReLU + pool
+  // rows m = (image, y, parity): A = row y of the image (parity 1: shifted by one pixel) from column
+  // x0; column j of channel-pair tile T = output x = x0 + 2 (j & 7) + parity, channel 2T + (j >> 3).
+  // A lane's 4 accumulator rows (y, y+1) x (parity 0, 1) are one 2x2 pool window.
   {
-    bf16x8 bc[5][6];  // banded B: [ky][channel], column j = output x offset
-#pragma unroll
-    for (int ky = 0; ky < 5; ++ky)
-#pragma unroll
-      for (int c = 0; c < 6; ++c)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int kx = 8 * g + e - i;
-          bc[ky][c][e] = f2bf((kx >= 0 && kx < 5) ? WS[c * 25 + ky * 5 + kx] : 0.f);
-        }
-    float b1[6];
-#pragma unroll
-    for (int c = 0; c < 6; ++c) b1[c] = WS[150 + c];
-    for (int u = w; u < 28; u += NT / 64) {
+    const float b1c[3] = {WS[(i >> 3)], WS[2 + (i >> 3)], WS[4 + (i >> 3)]};
+    for (int u = w; u < 56; u += NT / 64) {
       const int mt = u >> 1, x0 = (u & 1) * 16;
       const int m = 16 * mt + i;
-      const int img = m / 28, y = m - 28 * (m / 28);
-      const bf16* abase = Xs + img * 1024 + y * 32 + x0 + 8 * g;
-      f32x4 acc[6];
+      const int img = m / 56, rem = m - 56 * (m / 56);
+      const bf16* abase = ((rem & 1) ? Xs1 : Xs) + img * 1024 + (rem >> 1) * 32 + x0 + 8 * g;
+      f32x4 acc[3];
 #pragma unroll
-      for (int c = 0; c < 6; ++c) acc[c] = {0.f, 0.f, 0.f, 0.f};
+      for (int T = 0; T < 3; ++T) acc[T] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ky = 0; ky < 5; ++ky) {
         const bf16x8 av = ld8(abase + ky * 32);
 #pragma unroll
-        for (int c = 0; c < 6; ++c) acc[c] = mfma16x16x32(av, bc[ky][c], acc[c]);
+        for (int T = 0; T < 3; ++T) acc[T] = mfma16x16x32(av, bc[ky * 3 + T], acc[T]);
       }
-      // lane: rows 16mt + 4g + r = (image, y0 + r), column x = x0 + i; partner lane i^1 = column x+1
       const int m0 = 16 * mt + 4 * g;
-      const int imgo = m0 / 28, y0 = m0 - 28 * (m0 / 28);
-      const int x = x0 + i;
-      bf16x8 o[2];
-      unsigned cw[2] = {0u, 0u};
+      const int imgo = m0 / 56, py = (m0 - 56 * (m0 / 56)) >> 2;
+      const int px = (x0 >> 1) + (i & 7);
+      unsigned cw = 0;
 #pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        float v[4], p[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = acc[c][r] + b1[c];
-          p[r] = __shfl_xor(v[r], 1, 64);
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          float best;
-          unsigned code;
-          pool4(v[2 * h], p[2 * h], v[2 * h + 1], p[2 * h + 1], best, code);
-          o[h][c] = f2bf(best);
-          cw[h] |= code << (3 * c);
-        }
+      for (int T = 0; T < 3; ++T) {
+        float best;
+        unsigned code;
+        pool4(acc[T][0] + b1c[T], acc[T][1] + b1c[T], acc[T][2] + b1c[T], acc[T][3] + b1c[T], best, code);
+        const int c = 2 * T + (i >> 3);
+        if (px < 14) P1[((imgo * 14 + py) * 14 + px) * 8 + c] = f2bf(best);
+        cw |= code << (3 * c);
       }
-      if (!(i & 1) && x < 28) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          o[h][6] = (bf16)0.f;
-          o[h][7] = (bf16)0.f;
-          const int pidx = (imgo * 14 + (y0 >> 1) + h) * 14 + (x >> 1);
-          st8(P1 + pidx * 8, o[h]);
-          C1[pidx] = cw[h];
-        }
-      }
+      cw |= __shfl_xor(cw, 8, 64);
+      if (i < 8 && px < 14) C1[(imgo * 14 + py) * 14 + px] = cw;
     }
   }
   __syncthreads();
@@ -362,22 +349,17 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
   // ---------------------------------------------------------------- phase B: conv2 + ReLU + pool
   {
     bf16x8 bw[7];
+#pragma unroll
+    for (int s = 0; s < 7; ++s) bw[s] = frag[(FR_C2 + s) * 64 + lane];
     int toff[7];
 #pragma unroll
     for (int s = 0; s < 7; ++s) {
       const int tap = 4 * s + g;
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        bw[s][e] = f2bf((tap < 25 && e < 6) ? a.w2[i * 150 + tap * 6 + e] : 0.f);
       toff[s] = tap < 25 ? ((tap / 5) * 14 + (tap - 5 * (tap / 5))) * 8 : 0;
     }
-    const float b2 = WS[156 + i];
+    const float b2 = WS[6 + i];
     for (int mt = w; mt < 50; mt += NT / 64) {
-      const int m = 16 * mt + i;
-      const int img = m / 100, q = m - 100 * (m / 100);
-      const int win = q >> 2, d = q & 3;
-      const int py = win / 5, px = win - 5 * (win / 5);
-      const bf16* abase = P1 + ((img * 14 + 2 * py + (d >> 1)) * 14 + 2 * px + (d & 1)) * 8;
+      const bf16* abase = P1 + (int)PX[16 * mt + i] * 8;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 7; ++s) acc = mfma16x16x32(ld8(abase + toff[s]), bw[s], acc);
@@ -494,41 +476,45 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
   LN_STAMP(7);
 
   // ---------------------------------------------------------------- phase E: conv2 weight gradient
+  // dW2[n][(tap, c)] = sum_m dC2[m][n] im2col(P1)[m][(tap, c)]: both operands by transposed reads;
+  // wave w owns the 16-column tiles T = w + 4k (taps 2T, 2T + 1); tap 25 is the bias column of ones.
+  bf16x8 bd[15];  // conv2 data-gradient fragments for phase F, in flight during this phase
+#pragma unroll
+  for (int s = 0; s < 15; ++s) bd[s] = frag[(FR_DG + s) * 64 + lane];
   {
     const int q = (lane & 15) >> 2, p = lane & 3;
+    int toff[4];
+    bool ones[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int tap = 2 * (w + 4 * k) + (p >> 1);
+      ones[k] = tap >= 25;
+      toff[k] = tap < 25 ? ((tap / 5) * 14 + (tap - 5 * (tap / 5))) * 8 + 4 * (p & 1) : 0;
+    }
+    const int ntile = w == 0 ? 4 : 3;
     f32x4 acc[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) acc[k] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 5
     for (int s = 0; s < 25; ++s) {
-      bf16x4 ta[2];
-      const bf16* pix[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int m = 32 * s + 8 * g + 4 * h + q;
-        ta[h] = tr_read(DC2 + m * 16 + 4 * p);
-        const int img = m / 100, qq = m - 100 * (m / 100), win = qq >> 2, d = qq & 3;
-        const int py = win / 5, px = win - 5 * (win / 5);
-        pix[h] = P1 + ((img * 14 + 2 * py + (d >> 1)) * 14 + 2 * px + (d & 1)) * 8 + 4 * (p & 1);
-      }
-      const bf16x8 av = cat8(ta[0], ta[1]);
+      const int mA = 32 * s + 8 * g + q;
+      const bf16x8 av = cat8(tr_read(DC2 + mA * 16 + 4 * p), tr_read(DC2 + (mA + 4) * 16 + 4 * p));
+      const bf16* pb0 = P1 + (int)PX[mA] * 8;
+      const bf16* pb1 = P1 + (int)PX[mA + 4] * 8;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int T = w + 4 * k;
-        if (T <= 12) {
-          const int tap = 2 * T + (p >> 1);
-          const int toff = ((tap / 5) * 14 + (tap - 5 * (tap / 5))) * 8;
-          bf16x4 tb[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) tb[h] = tr_read(tap < 25 ? pix[h] + toff : KO);
-          acc[k] = mfma16x16x32(av, cat8(tb[0], tb[1]), acc[k]);
+        if (k < ntile) {
+          const bf16x4 t0 = tr_read(ones[k] ? KO : pb0 + toff[k]);
+          const bf16x4 t1 = tr_read(ones[k] ? KO : pb1 + toff[k]);
+          acc[k] = mfma16x16x32(av, cat8(t0, t1), acc[k]);
         }
       }
     }
     // D[row = output channel 4g + r][col i = (tap 2T + (i >> 3), channel i & 7)]
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int T = w + 4 * k;
-      if (T <= 12) {
+      if (k < ntile) {
+        const int T = w + 4 * k;
         const int tap = 2 * T + (i >> 3), c = i & 7;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -539,25 +525,12 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
       }
     }
   }
+  __syncthreads();  // phase E finished reading P1: it now receives dP1
+  LN_STAMP(8);
 
   // ---------------------------------------------------------------- phase F: conv2 data gradient
   {
-    bf16x8 bd[15];  // pair-banded B: column (b = i >> 3: output column 2X2 + b, channel c = i & 7)
     const int bcol = i >> 3, c = i & 7;
-#pragma unroll
-    for (int s = 0; s < 15; ++s) {
-      const int P = 2 * s + (g >> 1);
-      const int ky = P / 6, u = P - 6 * (P / 6);
-      const int kx = u - 1 + bcol;
-      const bool ok = kx >= 0 && kx < 5 && c < 6;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int n = 8 * (g & 1) + e;
-        bd[s][e] = f2bf(ok ? a.w2[n * 150 + (ky * 5 + kx) * 6 + c] : 0.f);
-      }
-    }
-    __syncthreads();  // phase E finished reading P1: it now receives dP1
-  LN_STAMP(8);
     for (int mt = w; mt < 49; mt += NT / 64) {
       const int m = 16 * mt + i;
       const int img = m / 98, rem = m - 98 * (m / 98);
@@ -581,68 +554,62 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
     }
   }
   __syncthreads();
+  build_shift1(Xs, Xs1);  // dC2 is no longer needed: the union takes the shifted input again
+  __syncthreads();
   LN_STAMP(9);
 
   // ---------------------------------------------------------------- phase G: conv1 weight gradient
+  // D[c][tap] = sum over (image, y, x) of dC1[c][y][x] X[y + ky][x + kx].  A fragment of lane
+  // (c = i, g) = dC1[c][y][8g .. 8g + 8) unpooled in registers from dP1 + codes (4 windows); B of lane
+  // (tap = 16T + i, g) = 4 dword reads of the input row y + ky at column 8g + kx (odd kx: the shifted
+  // copy).  No per-image staging, no barrier inside the loop.
   {
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    const bool a_ok = i < 6;
-    const int tap0 = i, tap1 = 16 + i;
-    for (int img = 0; img < IMG; ++img) {
-      // unpooled channel-major gradient dC1[c][y][x] (x >= 28 zero) of this image
-      for (int it = tid; it < 6 * 14 * 4; it += NT) {
-        const int c = it / 56, rem = it - 56 * (it / 56), py = rem >> 2, xc = rem & 3;
-        bf16x8 o0 = zero8(), o1 = zero8();
+    const int ca = i < 6 ? i : 5;
+    int boff[2];
+    const bf16* bsrc[2];
 #pragma unroll
-        for (int wd = 0; wd < 4; ++wd) {
-          const int px = 4 * xc + wd;
-          if (px < 14) {
-            const int pidx = (img * 14 + py) * 14 + px;
-            const unsigned code = (C1[pidx] >> (3 * c)) & 7u;
-            const bf16 v = P1[pidx * 8 + c];
-            o0[2 * wd] = code == 0 ? v : (bf16)0.f;
-            o0[2 * wd + 1] = code == 1 ? v : (bf16)0.f;
-            o1[2 * wd] = code == 2 ? v : (bf16)0.f;
-            o1[2 * wd + 1] = code == 3 ? v : (bf16)0.f;
-          }
-        }
-        st8(DC1 + (c * 28 + 2 * py) * 32 + 8 * xc, o0);
-        st8(DC1 + (c * 28 + 2 * py + 1) * 32 + 8 * xc, o1);
+    for (int T = 0; T < 2; ++T) {
+      const int tap = 16 * T + i;
+      if (tap < 25) {
+        const int ky = tap / 5, kx = tap - 5 * (tap / 5);
+        bsrc[T] = (kx & 1) ? Xs1 : Xs;
+        boff[T] = ky * 32 + 8 * g + (kx & ~1);
+      } else {
+        bsrc[T] = tap == 25 ? KO : KZ;
+        boff[T] = -1;
       }
-      // input rows shifted left by kx = 1..4 (aligned B-operand reads)
-      for (int it = tid; it < 4 * 32 * 4; it += NT) {
-        const int kk = it >> 7, rem = it & 127, yp = rem >> 2, xc = rem & 3;
-        const bf16* srow = Xs + img * 1024 + yp * 32 + 8 * xc;
-        const bf16x8 lo = ld8(srow), hi = ld8(srow + 8);
-        bf16 tmp[16];
+    }
+    for (int ry = w; ry < IMG * 28; ry += NT / 64) {
+      const int img = ry / 28, y = ry - 28 * (ry / 28);
+      // A: 4 pool windows (px = 4g .. 4g + 3) of row y / 2, channel ca
+      bf16x8 av;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          tmp[e] = lo[e];
-          tmp[e + 8] = hi[e];
-        }
-        bf16x8 o;
-        const int kx = kk + 1;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = tmp[e + kx];
-        st8(XK + (kk * 32 + yp) * 32 + 8 * xc, o);
+      for (int wd = 0; wd < 4; ++wd) {
+        const int px = 4 * g + wd;
+        const int pidx = (img * 14 + (y >> 1)) * 14 + (px < 14 ? px : 13);
+        const unsigned code = (C1[pidx] >> (3 * ca)) & 7u;
+        const bf16 v = (px < 14 && i < 6) ? P1[pidx * 8 + ca] : (bf16)0.f;
+        const unsigned dy = (unsigned)(y & 1) << 1;
+        av[2 * wd] = code == dy ? v : (bf16)0.f;
+        av[2 * wd + 1] = code == dy + 1u ? v : (bf16)0.f;
       }
-      __syncthreads();
-      for (int y = w; y < 28; y += NT / 64) {
-        const bf16x8 av = ld8(a_ok ? DC1 + (i * 28 + y) * 32 + 8 * g : KZ);
 #pragma unroll
-        for (int T = 0; T < 2; ++T) {
-          const int tap = T ? tap1 : tap0;
-          const bf16* bp;
-          if (tap < 25) {
-            const int ky = tap / 5, kx = tap - 5 * (tap / 5);
-            bp = (kx == 0 ? Xs + img * 1024 : XK + (kx - 1) * 1024) + (y + ky) * 32 + 8 * g;
-          } else {
-            bp = tap == 25 ? KO : KZ;
-          }
-          acc[T] = mfma16x16x32(av, ld8(bp), acc[T]);
+      for (int T = 0; T < 2; ++T) {
+        bf16x8 bv;
+        if (boff[T] >= 0) {
+          const unsigned* bp = reinterpret_cast<const unsigned*>(bsrc[T] + img * 1024 + y * 32 + boff[T]);
+          uint4 u;
+          u.x = bp[0];
+          u.y = bp[1];
+          u.z = bp[2];
+          u.w = bp[3];
+          bv = __builtin_bit_cast(bf16x8, u);
+        } else {
+          bv = ld8(bsrc[T]);
         }
+        acc[T] = mfma16x16x32(av, bv, acc[T]);
       }
-      __syncthreads();
     }
     // cross-wave sum: D[row = channel 4g + r][col = tap 16T + i]
 #pragma unroll
@@ -659,6 +626,35 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
     }
   }
   LN_STAMP(10);
+}
+
+// Conv weights of this step as MFMA B fragments ([NFRAG][64 lanes] of 8 bf16), one block per fragment.
+__global__ void __launch_bounds__(64) lenet_prep_kernel(const float* __restrict__ w1, const float* __restrict__ w2,
+                                                        bf16x8* __restrict__ frag) {
+  const int f = blockIdx.x, lane = threadIdx.x, i = lane & 15, g = lane >> 4;
+  bf16x8 o;
+  if (f < FR_C2) {  // conv1 banded: f = ky * 3 + T, column j = (x offset 2 (j & 7) [+ parity], channel 2T + (j >> 3))
+    const int ky = f / 3, T = f - 3 * (f / 3), c = 2 * T + (i >> 3), j8 = i & 7;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int kx = 8 * g + e - 2 * j8;
+      o[e] = f2bf((kx >= 0 && kx < 5) ? w1[c * 25 + ky * 5 + kx] : 0.f);
+    }
+  } else if (f < FR_DG) {  // conv2 forward: step s, column n = i, k = (tap 4s + g, channel e)
+    const int s = f - FR_C2, tap = 4 * s + g;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf((tap < 25 && e < 6) ? w2[i * 150 + tap * 6 + e] : 0.f);
+  } else {  // conv2 data gradient, pair-banded: column (b = i >> 3, c = i & 7), k = ((ky, u), n)
+    const int s = f - FR_DG, P = 2 * s + (g >> 1), ky = P / 6, u = P - 6 * (P / 6);
+    const int b = i >> 3, c = i & 7, kx = u - 1 + b;
+    const bool ok = P < 30 && kx >= 0 && kx < 5 && c < 6;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int n = 8 * (g & 1) + e;
+      o[e] = f2bf(ok ? w2[n * 150 + (ky * 5 + kx) * 6 + c] : 0.f);
+    }
+  }
+  frag[f * 64 + lane] = o;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -767,11 +763,15 @@ int lenet_blocks(int B) { return (B + IMG - 1) / IMG; }
 static unsigned long long* g_lenet_stamps_host = nullptr;
 void lenet_set_stamps(void* buf) { g_lenet_stamps_host = reinterpret_cast<unsigned long long*>(buf); }
 
+size_t lenet_frag_bytes() { return (size_t)NFRAG * 64 * 16; }
+
 hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   LeNetArgs a = a_in;
   a.stamps = g_lenet_stamps_host;
-  if (a.B <= 0 || a.ldt % 32 || a.ldt < a.B) return hipErrorInvalidValue;
+  if (a.B <= 0 || a.ldt % 32 || a.ldt < a.B || !a.frag || !a.ftab || !a.pxtab) return hipErrorInvalidValue;
   const int nblk = (a.B + IMG - 1) / IMG;
+  hipLaunchKernelGGL(lenet_prep_kernel, dim3(NFRAG), dim3(64), 0, st, a.w1, a.w2, reinterpret_cast<bf16x8*>(const_cast<void*>(a.frag)));
+  DFA_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(lenet_train_kernel, dim3(nblk), dim3(NT), LDS_BYTES, st, a);
   DFA_HIP_CHECK(hipGetLastError());
   r.nblk = nblk;

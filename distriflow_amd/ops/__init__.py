@@ -360,6 +360,43 @@ def lenet_blocks(B: int) -> int:
     return int(_C().lenet_blocks(int(B)))
 
 
+_LENET_TABLES = {}
+
+
+def lenet_tables(device):
+    """Constant index tables of the fused LeNet-5 kernel (built once per device):
+    ``ftab`` [98][2][16] u8 — conv2 data gradient: for pool1 pixel pair (y, X2), k-half and step s, the
+    window-major conv2 output row it gathers (255 = outside the 10x10 map);
+    ``pxtab`` [800] i16 — conv2 output row (image, window, position) -> pool1 pixel index;
+    ``frag`` — scratch for the per-step conv weight fragments (written by the kernel's prep launch)."""
+    key = str(device)
+    if key not in _LENET_TABLES:
+        import numpy as np
+
+        ft = np.full((98, 2, 16), 255, dtype=np.uint8)
+        for yx in range(98):
+            y, X2 = divmod(yx, 7)
+            for hf in range(2):
+                for s in range(16):
+                    P = 2 * s + hf
+                    if P >= 30:
+                        continue
+                    ky, u = divmod(P, 6)
+                    oy, ox = y - ky, 2 * X2 + 1 - u
+                    if 0 <= oy < 10 and 0 <= ox < 10:
+                        ft[yx, hf, s] = (((oy >> 1) * 5 + (ox >> 1)) << 2) + ((oy & 1) << 1) + (ox & 1)
+        px = np.zeros(800, dtype=np.int16)
+        for m in range(800):
+            img, q = divmod(m, 100)
+            win, d = divmod(q, 4)
+            py, pxx = divmod(win, 5)
+            px[m] = img * 196 + (2 * py + (d >> 1)) * 14 + 2 * pxx + (d & 1)
+        nbytes = int(_C().lenet_frag_bytes())
+        _LENET_TABLES[key] = (torch.from_numpy(ft.reshape(-1)).to(device), torch.from_numpy(px).to(device),
+                              torch.zeros(nbytes, dtype=torch.uint8, device=device))
+    return _LENET_TABLES[key]
+
+
 def lenet_train(x, labels, conv, dense_w, dense_wt, dense_b, conv_grads, dense_gw, dense_gb, hT, dzT, conv_part,
                 loss_part, stats, grad_scale):
     """Whole-network LeNet-5 training step on GPU (csrc/lenet_fused.hip, 2 launches): fills every
@@ -376,9 +413,10 @@ def lenet_train(x, labels, conv, dense_w, dense_wt, dense_b, conv_grads, dense_g
     else:
         lab = labels if labels.dtype == torch.int32 else labels.to(torch.int32)
     B = x.shape[0]
+    ftab, pxtab, frag = lenet_tables(stats.device)
     _C().lenet_train(src, idx, float(scale), lab, list(conv), list(dense_w), list(dense_wt), list(dense_b),
                      list(conv_grads), list(dense_gw), list(dense_gb), list(hT), list(dzT), conv_part, loss_part,
-                     stats, int(B), float(grad_scale))
+                     stats, frag, ftab, pxtab, int(B), float(grad_scale))
 
 
 def convpool_supported(H, W, C, KH, KW, pad, N) -> bool:

@@ -11,8 +11,8 @@ tagged with the version it was computed on, optionally with pre-update metrics (
 weights change only through server downloads; per-version upload counters
 (``num_updates`` / ``num_versions``); hyper-parameter precedence local config -> server -> defaults.
 
-MI355X design: the example buffer is a device ring (no host concat/slice), gradients are the
-engine's flat HBM buffer sent straight over RCCL, received weights are written into the flat
+MI355X design: the example buffer is a preallocated device FIFO (``utils.tensors.ExampleRing``: no
+per-call concat/slice reallocation), gradients are the engine's flat HBM buffer sent straight over RCCL, received weights are written into the flat
 master buffer and the bf16 compute copies refreshed by one kernel.  The async worker can hold the
 dataset itself (HBM resident) so only batch ids travel (``DataMsg.x is None``).
 """
@@ -220,38 +220,51 @@ class FederatedClient(AbstractWorker):
     per ``examplesPerUpdate`` examples, tagged with the current model version."""
 
     def setup(self):
+        from ..utils.tensors import ExampleRing
+
         super().setup()
         shape = tuple(self.model.input_shape)
         dev = getattr(self.model, "device", "cpu")
-        self.x = torch.empty((0,) + shape, device=dev)
-        self.y = torch.empty((0,), dtype=torch.int64, device=dev)
+        self.ring_x = ExampleRing(shape, torch.float32, dev)
+        self.ring_y = ExampleRing((), torch.int64, dev)
 
     def distributed_update(self, x: torch.Tensor, y: torch.Tensor):
-        from ..utils.tensors import add_rows, slice_with_empty
-
-        y = y.to(self.y.device)
-        single = tuple(x.shape) == tuple(self.x.shape[1:])  # one example (reference addRows accepts both)
+        dev = self.ring_x.buf.device
+        y = y.to(dev)
+        single = tuple(x.shape) == self.ring_x.unit_shape  # one example (reference addRows accepts both)
         if y.dim() > 1 or (single and y.numel() > 1):  # one-hot labels -> class ids
             y = y.argmax(dim=-1)
-        self.x = add_rows(self.x, x.to(self.x.device, self.x.dtype), self.x.shape[1:])
-        self.y = add_rows(self.y, y.long().reshape(-1), ())
+        self.ring_x.push(x.to(dev, torch.float32))
+        self.ring_y.push(y.long().reshape(-1))
+        if len(self.ring_x) != len(self.ring_y):
+            raise ValueError("examples and labels must have the same number of rows")
         per = int(self.hyperparam("examplesPerUpdate"))
-        while self.x.shape[0] >= per:
+        while len(self.ring_x) >= per:
             self.poll(0.0)
             version = self.model_version()
             vid = self.msg.version_id if self.msg else 0
-            xt, yt = self.x[:per], self.y[:per]
+            xt, yt = self.ring_x.peek(per), self.ring_y.peek(per)
             metrics = self.model.evaluate(xt, yt) if self.send_metrics else None
             grad = self.time("Fit model", lambda: self.model.fit_flat(xt, yt))
             self._upload(grad, vid, metrics=metrics, num_examples=per)
             self.version_update_counts[version] = self.version_update_counts.get(version, 0) + 1
-            self.x, self.y = slice_with_empty(self.x, per), slice_with_empty(self.y, per)
+            self.ring_x.pop(per)
+            self.ring_y.pop(per)
         self.poll(0.0)
 
     DistributedUpdate = distributed_update
 
+    @property
+    def x(self) -> torch.Tensor:
+        """Buffered, not yet uploaded examples (oldest first)."""
+        return self.ring_x.peek(len(self.ring_x))
+
+    @property
+    def y(self) -> torch.Tensor:
+        return self.ring_y.peek(len(self.ring_y))
+
     def num_examples(self) -> int:
-        return int(self.x.shape[0])
+        return len(self.ring_x)
 
     def num_examples_per_update(self) -> int:
         return int(self.hyperparam("examplesPerUpdate"))
