@@ -713,8 +713,8 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
                     std::vector<torch::Tensor> dense_wt, std::vector<torch::Tensor> dense_b,
                     std::vector<torch::Tensor> conv_grads, std::vector<torch::Tensor> dense_gw,
                     std::vector<torch::Tensor> dense_gb, std::vector<torch::Tensor> hT, std::vector<torch::Tensor> dzT,
-                    torch::Tensor conv_part, torch::Tensor loss_part, torch::Tensor stats, torch::Tensor frag,
-                    torch::Tensor ftab, torch::Tensor pxtab, int64_t B, double grad_scale) {
+                    torch::Tensor conv_part, torch::Tensor dense_part, torch::Tensor loss_part, torch::Tensor stats,
+                    torch::Tensor frag, torch::Tensor ftab, torch::Tensor pxtab, int64_t B, double grad_scale) {
   TORCH_CHECK(conv.size() == 4 && conv_grads.size() == 4, "lenet: conv = [w1, b1, w2, b2]");
   TORCH_CHECK(dense_w.size() == 3 && dense_wt.size() == 3 && dense_b.size() == 3 && dense_gw.size() == 3 &&
                   dense_gb.size() == 3 && hT.size() == 3 && dzT.size() == 3,
@@ -787,7 +787,7 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
   need(conv_part, at::kFloat, "lenet conv_part");
   need(loss_part, at::kFloat, "lenet loss_part");
   need(stats, at::kFloat, "lenet stats");
-  TORCH_CHECK(conv_part.numel() >= (int64_t)dfa::kLeNetConvParams * nblk, "lenet: conv_part too small");
+  TORCH_CHECK(conv_part.numel() >= (int64_t)dfa::kLeNetConvStride * nblk, "lenet: conv_part too small");
   TORCH_CHECK(loss_part.numel() >= 2 * nblk && stats.numel() >= 2, "lenet: loss buffers too small");
   a.conv_part = conv_part.data_ptr<float>();
   a.loss_part = loss_part.data_ptr<float>();
@@ -805,6 +805,7 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
   a.ldt = (int)ldt;
   a.grad_scale = (float)grad_scale;
   dfa::LeNetRedArgs r{};
+  (void)dense_part;  // kept in the signature; the dense gradients no longer need partials
   r.conv_part = a.conv_part;
   r.loss_part = a.loss_part;
   r.stats = stats.data_ptr<float>();
@@ -1176,6 +1177,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lenet_train", &lenet_train_py, "whole-network LeNet-5 training step (fwd + CE + bwd, 2 launches)");
   m.def("lenet_blocks", [](int64_t B) { return dfa::lenet_blocks((int)B); });
   m.def("lenet_frag_bytes", []() { return (int64_t)dfa::lenet_frag_bytes(); });
+  m.def("lenet_dense_part_floats", [](int64_t B) { return (int64_t)dfa::lenet_dense_part_floats((int)B); });
   m.def("gather_labels", &gather_labels_py);
   py::class_<P2PComm>(m, "P2PComm", "one-shot xGMI all-reduce over IPC-mapped peer buffers")
       .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("world"), py::arg("max_floats"),

@@ -254,6 +254,8 @@ hipError_t ps_apply(const PSArgs& a, hipStream_t st);
 // pool, dense 400-120-84-10, softmax-CE, full backward.  Conv weights are read from the fp32 master,
 // dense weights from the bf16 compute copies ([Npad16][Kpad32] and the dgrad layout).
 constexpr int kLeNetPW1 = 0, kLeNetPB1 = 150, kLeNetPW2 = 156, kLeNetPB2 = 2556, kLeNetConvParams = 2572;
+constexpr int kLeNetConvStride = 2576;  // floats per workgroup in the conv partial buffer
+constexpr int kLeNetMaxTiles = 288;
 struct LeNetArgs {
   const unsigned char* x_u8;  // [nrows][784] uint8 dataset read through idx (or null)
   const bf16* x_bf;           // [B][784] bf16 batch (when x_u8 is null)
@@ -264,7 +266,7 @@ struct LeNetArgs {
   const float *w1, *b1, *w2, *b2;  // fp32 master: conv1 [6][25], [6]; conv2 [16][150], [16]
   const bf16 *d1w, *d1wt, *d2w, *d2wt, *d3w, *d3wt;  // [128][416] [400][128] [96][128] [128][96] [16][96] [96][32]
   const float *d1b, *d2b, *d3b;
-  float* conv_part;           // [kLeNetConvParams][nblocks] per-workgroup conv gradient partials
+  float* conv_part;           // [nblocks][kLeNetConvStride] per-workgroup conv gradient partials
   float* loss_part;           // [nblocks][2]
   bf16 *h0T, *h1T, *h2T;      // [400|120|84][ldt] transposed dense inputs
   bf16 *dz1T, *dz2T, *dz3T;   // [120|84|10][ldt] transposed dense output gradients
@@ -290,7 +292,9 @@ struct LeNetRedArgs {
   float *g_w1, *g_b1, *g_w2, *g_b2;
   LeNetDense L[3];
   int nblk, ldt, nconv_blocks, dense_tiles;
+  int tile_of_block[kLeNetMaxTiles];  // XCD-aware placement of the dense weight-gradient tiles
 };
+int lenet_dense_part_floats(int B);
 size_t lenet_train_lds();
 int lenet_blocks(int B);
 hipError_t lenet_train(const LeNetArgs& a, LeNetRedArgs r, hipStream_t st);

@@ -27,6 +27,10 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
 namespace dfa {
 namespace {
 
@@ -130,23 +134,42 @@ __device__ __forceinline__ void pool4(float a00, float a01, float a10, float a11
   if (!(best > 0.f)) { best = 0.f; code = 4; }
 }
 
+// Weight fragments of one dense GEMM for the tiles t = w + 4 tt this wave owns, loaded ahead of use so
+// that the L2 latency of layer l + 1's weights hides behind layer l (W rows of 32 * KS elements).
+template <int KS, int NTW>
+struct DenseFrags {
+  bf16x8 b[NTW][KS];
+};
+template <int KS, int NTW>
+__device__ __forceinline__ void dense_load(DenseFrags<KS, NTW>& f, const bf16* __restrict__ W, int ntiles) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int tt = 0; tt < NTW; ++tt) {
+    const int t = w + 4 * tt;
+    if (t < ntiles) {
+      const bf16* wrow = W + (long long)(16 * t + i) * (32 * KS) + 8 * g;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) f.b[tt][s] = ld8(wrow + 32 * s);
+    }
+  }
+}
+
 // Z[8 rows][N] = A[8][Kpad] W^T (+bias, ReLU); A rows 8..15 of the MFMA tile read the zero row.
-template <int KS>
-__device__ __forceinline__ void dense_fwd(const bf16* A, int lda, const bf16* zr, const bf16* __restrict__ W,
+template <int KS, int NTW>
+__device__ __forceinline__ void dense_fwd(const DenseFrags<KS, NTW>& f, const bf16* A, int lda, const bf16* zr,
                                           const float* __restrict__ bias, int N, bool relu, bf16* out, int ldo,
                                           float* out32, bf16* __restrict__ hT, int ldt, int r0, int rows) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
   const int ntiles = (N + 15) / 16;
   const bf16* arow = (i < IMG ? A + i * lda : zr) + 8 * g;
-  for (int t = w; t < ntiles; t += NT / 64) {
-    const int n = 16 * t + i;
-    const bf16* wrow = W + (long long)n * (32 * KS) + 8 * g;
-    bf16x8 b[KS];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) b[s] = ld8(wrow + 32 * s);
+  for (int tt = 0; tt < NTW; ++tt) {
+    const int t = w + 4 * tt;
+    if (t >= ntiles) break;
+    const int n = 16 * t + i;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < KS; ++s) acc = mfma16x16x32(ld8(arow + 32 * s), b[s], acc);
+    for (int s = 0; s < KS; ++s) acc = mfma16x16x32(ld8(arow + 32 * s), f.b[tt][s], acc);
     if (g >= 2) continue;  // output rows 8..15 are padding
     const float bv = (bias != nullptr && n < N) ? bias[n] : 0.f;
     float v[4];
@@ -175,22 +198,21 @@ __device__ __forceinline__ void dense_fwd(const bf16* A, int lda, const bf16* zr
 }
 
 // dA[8][K] = dZ[8][32*KS] Wt^T, masked by (mask > 0); also dZ^T rows for the weight gradient.
-template <int KS>
-__device__ __forceinline__ void dense_bwd(const bf16* dZ, int ldz, const bf16* zr, const bf16* __restrict__ Wt, int K,
-                                          const bf16* mask, int ldm, bf16* out, int ldo, bf16* __restrict__ gT,
-                                          int ldt, int r0, int rows) {
+template <int KS, int NTW>
+__device__ __forceinline__ void dense_bwd(const DenseFrags<KS, NTW>& f, const bf16* dZ, int ldz, const bf16* zr,
+                                          int K, const bf16* mask, int ldm, bf16* out, int ldo,
+                                          bf16* __restrict__ gT, int ldt, int r0, int rows) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
   const int ktiles = (K + 15) / 16;
   const bf16* zrow = (i < IMG ? dZ + i * ldz : zr) + 8 * g;
-  for (int t = w; t < ktiles; t += NT / 64) {
-    const int j = 16 * t + i;
-    const bf16* wrow = Wt + (long long)j * (32 * KS) + 8 * g;
-    bf16x8 b[KS];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) b[s] = ld8(wrow + 32 * s);
+  for (int tt = 0; tt < NTW; ++tt) {
+    const int t = w + 4 * tt;
+    if (t >= ktiles) break;
+    const int j = 16 * t + i;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < KS; ++s) acc = mfma16x16x32(ld8(zrow + 32 * s), b[s], acc);
+    for (int s = 0; s < KS; ++s) acc = mfma16x16x32(ld8(zrow + 32 * s), f.b[tt][s], acc);
     if (g >= 2) continue;
     float v[4];
 #pragma unroll
@@ -244,7 +266,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
   const int rows = min(IMG, a.B - r0);
   const long long nb = gridDim.x;
   const bf16x8* __restrict__ frag = reinterpret_cast<const bf16x8*>(a.frag);
-  float* part = a.conv_part + blockIdx.x;  // transposed partials: parameter p at part[p * nb]
+  float* part = a.conv_part + (long long)blockIdx.x * kLeNetConvStride;  // this workgroup's partials
   unsigned long long* const stamps = a.stamps;
   LN_STAMP(0);
 
@@ -312,6 +334,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
   // A lane's 4 accumulator rows (y, y+1) x (parity 0, 1) are one 2x2 pool window.
   {
     const float b1c[3] = {WS[(i >> 3)], WS[2 + (i >> 3)], WS[4 + (i >> 3)]};
+#pragma unroll 2
     for (int u = w; u < 56; u += NT / 64) {
       const int mt = u >> 1, x0 = (u & 1) * 16;
       const int m = 16 * mt + i;
@@ -347,6 +370,8 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
   LN_STAMP(2);
 
   // ---------------------------------------------------------------- phase B: conv2 + ReLU + pool
+  DenseFrags<13, 2> f1;  // dense-1 weights: L2 latency hidden behind conv2
+  dense_load(f1, a.d1w, 8);
   {
     bf16x8 bw[7];
 #pragma unroll
@@ -358,6 +383,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
       toff[s] = tap < 25 ? ((tap / 5) * 14 + (tap - 5 * (tap / 5))) * 8 : 0;
     }
     const float b2 = WS[6 + i];
+#pragma unroll 2
     for (int mt = w; mt < 50; mt += NT / 64) {
       const bf16* abase = P1 + (int)PX[16 * mt + i] * 8;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -388,11 +414,21 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
       for (int r = 0; r < rows; ++r) dst[r] = H0[r * LD0 + k];
     }
   }
-  dense_fwd<13>(H0, LD0, ZR, a.d1w, a.d1b, 120, true, H1, LD1, nullptr, a.h1T, a.ldt, r0, rows);
+  DenseFrags<4, 2> f2;
+  DenseFrags<3, 1> f3;
+  dense_load(f2, a.d2w, 6);
+  dense_load(f3, a.d3w, 1);
+  dense_fwd(f1, H0, LD0, ZR, a.d1b, 120, true, H1, LD1, nullptr, a.h1T, a.ldt, r0, rows);
   __syncthreads();
-  dense_fwd<4>(H1, LD1, ZR, a.d2w, a.d2b, 84, true, H2, LD2, nullptr, a.h2T, a.ldt, r0, rows);
+  DenseFrags<1, 2> g3;
+  DenseFrags<3, 2> g2;
+  dense_load(g3, a.d3wt, 6);
+  dense_load(g2, a.d2wt, 8);
+  dense_fwd(f2, H1, LD1, ZR, a.d2b, 84, true, H2, LD2, nullptr, a.h2T, a.ldt, r0, rows);
   __syncthreads();
-  dense_fwd<3>(H2, LD2, ZR, a.d3w, a.d3b, 10, false, nullptr, 0, LG, nullptr, a.ldt, r0, rows);
+  DenseFrags<4, 7> g1;  // dense-1 data-gradient weights: loads overlap dense-3 and the loss
+  dense_load(g1, a.d1wt, 25);
+  dense_fwd(f3, H2, LD2, ZR, a.d3b, 10, false, nullptr, 0, LG, nullptr, a.ldt, r0, rows);
   __syncthreads();
   LN_STAMP(4);
   if (tid < IMG) {
@@ -435,11 +471,11 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
   }
   __syncthreads();
   LN_STAMP(5);
-  dense_bwd<1>(Z3, LD3, ZR, a.d3wt, 84, H2, LD2, Z2, LD2, a.dz2T, a.ldt, r0, rows);
+  dense_bwd(g3, Z3, LD3, ZR, 84, H2, LD2, Z2, LD2, a.dz2T, a.ldt, r0, rows);
   __syncthreads();
-  dense_bwd<3>(Z2, LD2, ZR, a.d2wt, 120, H1, LD1, Z1, LD1, a.dz1T, a.ldt, r0, rows);
+  dense_bwd(g2, Z2, LD2, ZR, 120, H1, LD1, Z1, LD1, a.dz1T, a.ldt, r0, rows);
   __syncthreads();
-  dense_bwd<4>(Z1, LD1, ZR, a.d1wt, 400, H0, LD0, H0, LD0, nullptr, 0, r0, rows);  // in place: dP2
+  dense_bwd(g1, Z1, LD1, ZR, 400, H0, LD0, H0, LD0, nullptr, 0, r0, rows);  // in place: dP2
   __syncthreads();
   LN_STAMP(6);
 
@@ -519,8 +555,8 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = 4 * g + r;
-          if (tap < 25 && c < 6) part[(long long)(kLeNetPW2 + n * 150 + tap * 6 + c) * nb] = acc[k][r];
-          else if (tap == 25 && c == 0) part[(long long)(kLeNetPB2 + n) * nb] = acc[k][r];
+          if (tap < 25 && c < 6) part[(long long)(kLeNetPW2 + n * 150 + tap * 6 + c) ] = acc[k][r];
+          else if (tap == 25 && c == 0) part[(long long)(kLeNetPB2 + n) ] = acc[k][r];
         }
       }
     }
@@ -531,15 +567,17 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
   // ---------------------------------------------------------------- phase F: conv2 data gradient
   {
     const int bcol = i >> 3, c = i & 7;
+#pragma unroll 2
     for (int mt = w; mt < 49; mt += NT / 64) {
       const int m = 16 * mt + i;
       const int img = m / 98, rem = m - 98 * (m / 98);
-      const unsigned char* tb = FT + (rem * 2 + (g >> 1)) * 16;
+      const uint4 tv = *reinterpret_cast<const uint4*>(FT + (rem * 2 + (g >> 1)) * 16);
+      const unsigned tw[4] = {tv.x, tv.y, tv.z, tv.w};
       const bf16* dbase = DC2 + img * 1600 + 8 * (g & 1);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 15; ++s) {
-        const unsigned t = tb[s];
+        const unsigned t = (tw[s >> 2] >> (8 * (s & 3))) & 255u;
         acc = mfma16x16x32(ld8(t == 255u ? KZ : dbase + t * 16), bd[s], acc);
       }
       if (c < 6) {
@@ -580,35 +618,44 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
         boff[T] = -1;
       }
     }
-    for (int ry = w; ry < IMG * 28; ry += NT / 64) {
-      const int img = ry / 28, y = ry - 28 * (ry / 28);
-      // A: 4 pool windows (px = 4g .. 4g + 3) of row y / 2, channel ca
-      bf16x8 av;
+#pragma unroll 2
+    for (int rp = w; rp < IMG * 14; rp += NT / 64) {
+      const int img = rp / 14, py = rp - 14 * (rp / 14);
+      // A rows y = 2 py (dy = 0) and 2 py + 1 (dy = 1) from the same 4 pool windows px = 4g .. 4g + 3
+      const int p0 = (img * 14 + py) * 14 + 4 * g;
+      const uint2 cA = *reinterpret_cast<const uint2*>(C1 + p0);
+      const uint2 cB = *reinterpret_cast<const uint2*>(C1 + p0 + 2);
+      const unsigned cw[4] = {cA.x, cA.y, cB.x, cB.y};
+      bf16x8 a0, a1;
 #pragma unroll
       for (int wd = 0; wd < 4; ++wd) {
-        const int px = 4 * g + wd;
-        const int pidx = (img * 14 + (y >> 1)) * 14 + (px < 14 ? px : 13);
-        const unsigned code = (C1[pidx] >> (3 * ca)) & 7u;
-        const bf16 v = (px < 14 && i < 6) ? P1[pidx * 8 + ca] : (bf16)0.f;
-        const unsigned dy = (unsigned)(y & 1) << 1;
-        av[2 * wd] = code == dy ? v : (bf16)0.f;
-        av[2 * wd + 1] = code == dy + 1u ? v : (bf16)0.f;
+        const bool ok = 4 * g + wd < 14 && i < 6;
+        const unsigned code = (cw[wd] >> (3 * ca)) & 7u;
+        const bf16 v = ok ? P1[(p0 + wd) * 8 + ca] : (bf16)0.f;
+        a0[2 * wd] = code == 0u ? v : (bf16)0.f;
+        a0[2 * wd + 1] = code == 1u ? v : (bf16)0.f;
+        a1[2 * wd] = code == 2u ? v : (bf16)0.f;
+        a1[2 * wd + 1] = code == 3u ? v : (bf16)0.f;
       }
 #pragma unroll
-      for (int T = 0; T < 2; ++T) {
-        bf16x8 bv;
-        if (boff[T] >= 0) {
-          const unsigned* bp = reinterpret_cast<const unsigned*>(bsrc[T] + img * 1024 + y * 32 + boff[T]);
-          uint4 u;
-          u.x = bp[0];
-          u.y = bp[1];
-          u.z = bp[2];
-          u.w = bp[3];
-          bv = __builtin_bit_cast(bf16x8, u);
-        } else {
-          bv = ld8(bsrc[T]);
+      for (int dy = 0; dy < 2; ++dy) {
+        const int y = 2 * py + dy;
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+          bf16x8 bv;
+          if (boff[T] >= 0) {
+            const unsigned* bp = reinterpret_cast<const unsigned*>(bsrc[T] + img * 1024 + y * 32 + boff[T]);
+            uint4 u;
+            u.x = bp[0];
+            u.y = bp[1];
+            u.z = bp[2];
+            u.w = bp[3];
+            bv = __builtin_bit_cast(bf16x8, u);
+          } else {
+            bv = ld8(bsrc[T]);
+          }
+          acc[T] = mfma16x16x32(dy ? a1 : a0, bv, acc[T]);
         }
-        acc[T] = mfma16x16x32(av, bv, acc[T]);
       }
     }
     // cross-wave sum: D[row = channel 4g + r][col = tap 16T + i]
@@ -621,136 +668,166 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
       const int c = e >> 5, col = e & 31;
       const float v = RED[(0 * 16 + c) * 32 + col] + RED[(1 * 16 + c) * 32 + col] + RED[(2 * 16 + c) * 32 + col] +
                       RED[(3 * 16 + c) * 32 + col];
-      if (col < 25) part[(long long)(kLeNetPW1 + c * 25 + col) * nb] = v;
-      else if (col == 25) part[(long long)(kLeNetPB1 + c) * nb] = v;
+      if (col < 25) part[(long long)(kLeNetPW1 + c * 25 + col) ] = v;
+      else if (col == 25) part[(long long)(kLeNetPB1 + c) ] = v;
     }
   }
   LN_STAMP(10);
 }
 
-// Conv weights of this step as MFMA B fragments ([NFRAG][64 lanes] of 8 bf16), one block per fragment.
-__global__ void __launch_bounds__(64) lenet_prep_kernel(const float* __restrict__ w1, const float* __restrict__ w2,
+// Conv weights of this step as MFMA B fragments ([NFRAG][64 lanes] of 8 bf16): one block, the 2550
+// fp32 weights staged in LDS by coalesced loads, then every fragment lane built from LDS.
+constexpr int PT = 1024;
+__global__ void __launch_bounds__(PT) lenet_prep_kernel(const float* __restrict__ w1g, const float* __restrict__ w2g,
                                                         bf16x8* __restrict__ frag) {
-  const int f = blockIdx.x, lane = threadIdx.x, i = lane & 15, g = lane >> 4;
-  bf16x8 o;
-  if (f < FR_C2) {  // conv1 banded: f = ky * 3 + T, column j = (x offset 2 (j & 7) [+ parity], channel 2T + (j >> 3))
-    const int ky = f / 3, T = f - 3 * (f / 3), c = 2 * T + (i >> 3), j8 = i & 7;
+  __shared__ float w1[150];
+  __shared__ float w2[2400];
+  for (int e = threadIdx.x; e < 150; e += PT) w1[e] = w1g[e];
+  for (int e = threadIdx.x; e < 2400; e += PT) w2[e] = w2g[e];
+  __syncthreads();
+  for (int fl = threadIdx.x; fl < NFRAG * 64; fl += PT) {
+    const int f = fl >> 6, lane = fl & 63, i = lane & 15, g = lane >> 4;
+    bf16x8 o;
+    if (f < FR_C2) {  // conv1 banded: f = ky * 3 + T, column j = (x offset 2 (j & 7) [+ parity], channel 2T + (j >> 3))
+      const int ky = f / 3, T = f - 3 * (f / 3), c = 2 * T + (i >> 3), j8 = i & 7;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int kx = 8 * g + e - 2 * j8;
-      o[e] = f2bf((kx >= 0 && kx < 5) ? w1[c * 25 + ky * 5 + kx] : 0.f);
+      for (int e = 0; e < 8; ++e) {
+        const int kx = 8 * g + e - 2 * j8;
+        o[e] = f2bf((kx >= 0 && kx < 5) ? w1[c * 25 + ky * 5 + kx] : 0.f);
+      }
+    } else if (f < FR_DG) {  // conv2 forward: step s, column n = i, k = (tap 4s + g, channel e)
+      const int s = f - FR_C2, tap = 4 * s + g;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf((tap < 25 && e < 6) ? w2[i * 150 + tap * 6 + e] : 0.f);
+    } else {  // conv2 data gradient, pair-banded: column (b = i >> 3, c = i & 7), k = ((ky, u), n)
+      const int s = f - FR_DG, P = 2 * s + (g >> 1), ky = P / 6, u = P - 6 * (P / 6);
+      const int b = i >> 3, c = i & 7, kx = u - 1 + b;
+      const bool ok = P < 30 && kx >= 0 && kx < 5 && c < 6;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int n = 8 * (g & 1) + e;
+        o[e] = f2bf(ok ? w2[n * 150 + (ky * 5 + kx) * 6 + c] : 0.f);
+      }
     }
-  } else if (f < FR_DG) {  // conv2 forward: step s, column n = i, k = (tap 4s + g, channel e)
-    const int s = f - FR_C2, tap = 4 * s + g;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = f2bf((tap < 25 && e < 6) ? w2[i * 150 + tap * 6 + e] : 0.f);
-  } else {  // conv2 data gradient, pair-banded: column (b = i >> 3, c = i & 7), k = ((ky, u), n)
-    const int s = f - FR_DG, P = 2 * s + (g >> 1), ky = P / 6, u = P - 6 * (P / 6);
-    const int b = i >> 3, c = i & 7, kx = u - 1 + b;
-    const bool ok = P < 30 && kx >= 0 && kx < 5 && c < 6;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int n = 8 * (g & 1) + e;
-      o[e] = f2bf(ok ? w2[n * 150 + (ky * 5 + kx) * 6 + c] : 0.f);
-    }
+    frag[fl] = o;
   }
-  frag[f * 64 + lane] = o;
 }
 
 // ------------------------------------------------------------------------------------------------
-// Reductions: blocks [0, nconv) one wave per conv parameter (sum over the workgroup partials,
-// fixed order), then one block per 16x16 tile of a dense weight gradient (K = batch, 16 waves split
-// it, LDS combine), then one block for the loss partials.  Deterministic.
+// Reductions in one launch, deterministic (fixed summation order everywhere):
+//   blocks [0, dense_tiles)  one 16x16 tile of a dense weight gradient each (K = batch split over 16
+//                 waves, LDS combine; bias = a column of ones).  Tiles are placed by a host table so
+//                 that all tiles reading the same 16 activation rows run on one XCD: every XCD then
+//                 fetches its share of H^T once and dZ^T once into its own L2 and re-reads them there.
+//   next nconv_blocks        64 conv parameters each: thread (p, q) sums workgroup partials q, q + 16, ...
+//                 of parameter p (rows of 64 consecutive floats per wave-load), LDS combine.
+//   last block               loss partials -> stats.
 constexpr int RT = 1024;
 
 __global__ void __launch_bounds__(RT) lenet_reduce_kernel(LeNetRedArgs a) {
   __shared__ float red[16][16][17];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int blk = blockIdx.x;
+  if (blk < a.dense_tiles) {
+    int tile = a.tile_of_block[blk];
+    int l = 0;
+    if (tile >= a.L[0].tiles) {
+      tile -= a.L[0].tiles;
+      l = 1;
+      if (tile >= a.L[1].tiles) {
+        tile -= a.L[1].tiles;
+        l = 2;
+      }
+    }
+    const LeNetDense& L = a.L[l];
+    const int ktiles = (L.K + 1 + 15) / 16;
+    const int tk = tile / ((L.N + 15) / 16), tn = tile - ((L.N + 15) / 16) * tk;  // tn fastest
+    const int n = 16 * tn + (lane & 15), k = 16 * tk + (lane & 15);
+    const bf16* arow = L.dzT + (long long)min(n, L.N - 1) * a.ldt + 8 * (lane >> 4);
+    const bf16* brow = L.hT + (long long)min(k, L.K - 1) * a.ldt + 8 * (lane >> 4);
+    const bool a_ok = n < L.N, b_ones = k == L.K, b_ok = k < L.K;
+    bf16x8 ones, zeros = zero8();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
+    const int steps = a.ldt / 32;
+    const int per = (steps + 15) / 16;
+    const int s0 = wid * per, s1 = min(steps, s0 + per);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s = s0; s < s1; s += 8) {
+      bf16x8 av[8], bv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int ss = min(s + u, s1 - 1);
+        av[u] = ld8(arow + 32 * ss);
+        bv[u] = ld8(brow + 32 * ss);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bool live = s + u < s1;
+        acc = mfma16x16x32((a_ok && live) ? av[u] : zeros, b_ok ? bv[u] : (b_ones ? ones : zeros), acc);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wid][4 * (lane >> 4) + r][lane & 15] = acc[r];
+    __syncthreads();
+    const int t = threadIdx.x;
+    (void)ktiles;
+    if (t < 256) {
+      const int rn = t >> 4, ck = t & 15;
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 16; ++ww) v += red[ww][rn][ck];
+      const int on = 16 * tn + rn, ok = 16 * tk + ck;
+      if (on < L.N) {
+        if (ok < L.K) L.gw[(long long)on * L.K + ok] = v;
+        else if (ok == L.K) L.gb[on] = v;
+      }
+    }
+    return;
+  }
+  blk -= a.dense_tiles;
   if (blk < a.nconv_blocks) {
-    const int p = blk * (RT / 64) + wid;
-    if (p >= kLeNetConvParams) return;
-    const float* src = a.conv_part + (long long)p * a.nblk;
+    float* sred = &red[0][0][0];  // [16][64]
+    const int p = blk * 64 + lane;
     float s = 0.f;
-    for (int k = lane; k < a.nblk; k += 64) s += src[k];
-    s = wave_sum(s);
-    if (lane == 0) {
+    if (p < kLeNetConvParams) {
+      // 32 workgroup rows per pass, all loads in flight before the (fixed-order) sum
+      for (int q0 = wid; q0 < a.nblk; q0 += 16 * 32) {
+        float v[32];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          const int q = q0 + 16 * j;
+          v[j] = q < a.nblk ? a.conv_part[(long long)q * kLeNetConvStride + p] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 32; ++j) s += v[j];
+      }
+    }
+    sred[wid * 64 + lane] = s;
+    __syncthreads();
+    if (wid == 0 && p < kLeNetConvParams) {
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 16; ++ww) v += sred[ww * 64 + lane];
       float* dst = p < kLeNetPB1 ? a.g_w1 + p
                    : p < kLeNetPW2 ? a.g_b1 + (p - kLeNetPB1)
                    : p < kLeNetPB2 ? a.g_w2 + (p - kLeNetPW2)
                                    : a.g_b2 + (p - kLeNetPB2);
-      *dst = s;
+      *dst = v;
     }
     return;
   }
-  blk -= a.nconv_blocks;
-  if (blk == a.dense_tiles) {  // loss partials -> stats
-    if (wid == 0) {
-      float l = 0.f, c = 0.f;
-      for (int k = lane; k < a.nblk; k += 64) {
-        l += a.loss_part[2 * k];
-        c += a.loss_part[2 * k + 1];
-      }
-      l = wave_sum(l);
-      c = wave_sum(c);
-      if (lane == 0) {
-        a.stats[0] = l;
-        a.stats[1] = c;
-      }
+  if (wid == 0) {  // loss partials -> stats
+    float l = 0.f, c = 0.f;
+    for (int k = lane; k < a.nblk; k += 64) {
+      l += a.loss_part[2 * k];
+      c += a.loss_part[2 * k + 1];
     }
-    return;
-  }
-  // dense weight-gradient tile: layer l, tile (tn, tk); dW[n][k] = sum_b dZ^T[n][b] H^T[k][b], k == K: bias
-  int l = 0, tile = blk;
-  if (tile >= a.L[0].tiles) {
-    tile -= a.L[0].tiles;
-    l = 1;
-    if (tile >= a.L[1].tiles) {
-      tile -= a.L[1].tiles;
-      l = 2;
-    }
-  }
-  const LeNetDense L = a.L[l];
-  const int ktiles = (L.K + 1 + 15) / 16;
-  const int tn = tile / ktiles, tk = tile - tn * ktiles;
-  const int n = 16 * tn + (lane & 15), k = 16 * tk + (lane & 15);
-  const bf16* arow = L.dzT + (long long)min(n, L.N - 1) * a.ldt + 8 * (lane >> 4);
-  const bf16* brow = L.hT + (long long)min(k, L.K - 1) * a.ldt + 8 * (lane >> 4);
-  const bool a_ok = n < L.N, b_ones = k == L.K, b_ok = k < L.K;
-  bf16x8 ones, zeros = zero8();
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
-  const int steps = a.ldt / 32;
-  const int per = (steps + 15) / 16;
-  const int s0 = wid * per, s1 = min(steps, s0 + per);
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int s = s0; s < s1; s += 8) {
-    bf16x8 av[8], bv[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int ss = min(s + u, s1 - 1);
-      av[u] = ld8(arow + 32 * ss);
-      bv[u] = ld8(brow + 32 * ss);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const bool live = s + u < s1;
-      acc = mfma16x16x32((a_ok && live) ? av[u] : zeros, b_ok ? bv[u] : (b_ones ? ones : zeros), acc);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) red[wid][4 * (lane >> 4) + r][lane & 15] = acc[r];
-  __syncthreads();
-  const int t = threadIdx.x;
-  if (t < 256) {
-    const int rn = t >> 4, ck = t & 15;
-    float v = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < 16; ++ww) v += red[ww][rn][ck];
-    const int on = 16 * tn + rn, ok = 16 * tk + ck;
-    if (on < L.N) {
-      if (ok < L.K) L.gw[(long long)on * L.K + ok] = v;
-      else if (ok == L.K) L.gb[on] = v;
+    l = wave_sum(l);
+    c = wave_sum(c);
+    if (lane == 0) {
+      a.stats[0] = l;
+      a.stats[1] = c;
     }
   }
 }
@@ -764,25 +841,54 @@ static unsigned long long* g_lenet_stamps_host = nullptr;
 void lenet_set_stamps(void* buf) { g_lenet_stamps_host = reinterpret_cast<unsigned long long*>(buf); }
 
 size_t lenet_frag_bytes() { return (size_t)NFRAG * 64 * 16; }
+int lenet_dense_part_floats(int B) { (void)B; return 0; }
 
 hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   LeNetArgs a = a_in;
   a.stamps = g_lenet_stamps_host;
   if (a.B <= 0 || a.ldt % 32 || a.ldt < a.B || !a.frag || !a.ftab || !a.pxtab) return hipErrorInvalidValue;
   const int nblk = (a.B + IMG - 1) / IMG;
-  hipLaunchKernelGGL(lenet_prep_kernel, dim3(NFRAG), dim3(64), 0, st, a.w1, a.w2, reinterpret_cast<bf16x8*>(const_cast<void*>(a.frag)));
+  hipLaunchKernelGGL(lenet_prep_kernel, dim3(1), dim3(PT), 0, st, a.w1, a.w2, reinterpret_cast<bf16x8*>(const_cast<void*>(a.frag)));
   DFA_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(lenet_train_kernel, dim3(nblk), dim3(NT), LDS_BYTES, st, a);
   DFA_HIP_CHECK(hipGetLastError());
   r.nblk = nblk;
   r.ldt = a.ldt;
-  r.nconv_blocks = (kLeNetConvParams + RT / 64 - 1) / (RT / 64);
-  r.dense_tiles = 0;
+  r.nconv_blocks = (kLeNetConvParams + 63) / 64;
+  // dense tiles in (layer, tk, tn) order, tn fastest; XCD x (= block id mod 8) takes the tiles with
+  // tk = x (mod 8) of every layer, so all 16-row groups of H^T stay in one L2
+  int tiles_per_layer[3], base = 0;
+  std::vector<int> by_xcd[8];
   for (int l = 0; l < 3; ++l) {
-    r.L[l].tiles = ((r.L[l].N + 15) / 16) * ((r.L[l].K + 1 + 15) / 16);
-    r.dense_tiles += r.L[l].tiles;
+    const int nt = (r.L[l].N + 15) / 16, kt = (r.L[l].K + 1 + 15) / 16;
+    r.L[l].tiles = nt * kt;
+    tiles_per_layer[l] = nt * kt;
+    for (int tk = 0; tk < kt; ++tk)
+      for (int tn = 0; tn < nt; ++tn) by_xcd[tk % 8].push_back(base + tk * nt + tn);
+    base += nt * kt;
   }
-  hipLaunchKernelGGL(lenet_reduce_kernel, dim3(r.nconv_blocks + r.dense_tiles + 1), dim3(RT), 0, st, r);
+  (void)tiles_per_layer;
+  r.dense_tiles = base;
+  if (r.dense_tiles > kLeNetMaxTiles) return hipErrorInvalidValue;
+  size_t maxq = 0;
+  for (auto& v : by_xcd) maxq = std::max(maxq, v.size());
+  int b = 0;
+  std::vector<int> order;
+  for (size_t slot = 0; slot < maxq; ++slot)
+    for (int x = 0; x < 8; ++x)
+      if (slot < by_xcd[x].size()) order.push_back(by_xcd[x][slot]);
+  for (int t : order) r.tile_of_block[b++] = t;
+  // measurement aid: DISTRIFLOW_LENET_RED_SKIP=1 launches no dense tiles, =2 no conv blocks (wrong gradients)
+  static const int skip = [] {
+    const char* e = getenv("DISTRIFLOW_LENET_RED_SKIP");
+    return e ? atoi(e) : 0;
+  }();
+  if (skip & 1) {
+    r.dense_tiles = 0;
+  }
+  const int nconv = (skip & 2) ? 0 : r.nconv_blocks;
+  if (skip & 2) r.nconv_blocks = 0;
+  hipLaunchKernelGGL(lenet_reduce_kernel, dim3(r.dense_tiles + nconv + 1), dim3(RT), 0, st, r);
   return hipGetLastError();
 }
 

@@ -202,7 +202,8 @@ class Net:
             self.head_loss_part = torch.zeros(2 * ((B + 15) // 16), dtype=torch.float32, device=self.device)
         if self.lenet_fused:
             nblk = ops.lenet_blocks(B)
-            self.lenet_conv_part = torch.empty(2572 * nblk, dtype=torch.float32, device=self.device)
+            self.lenet_conv_part = torch.empty(2576 * nblk, dtype=torch.float32, device=self.device)
+            self.lenet_dense_part = torch.empty(1, dtype=torch.float32, device=self.device)
             self.lenet_loss_part = torch.zeros(2 * nblk, dtype=torch.float32, device=self.device)
         self._bound_B = B
         self.graphs = {}
@@ -269,7 +270,8 @@ class Net:
                         [st.weight_t(f"{d.name}/kernel") for d in dense], [st[f"{d.name}/bias"] for d in dense],
                         cgrads, [st.grad_matrix(f"{d.name}/kernel") for d in dense],
                         [st.gradient(f"{d.name}/bias") for d in dense], [self.head_xT] + self.head_hT[:2],
-                        self.head_dzT, self.lenet_conv_part, self.lenet_loss_part, self.stats, 1.0 / B)
+                        self.head_dzT, self.lenet_conv_part, self.lenet_dense_part, self.lenet_loss_part, self.stats,
+                        1.0 / B)
         if grad_ready is not None:
             for i in range(len(self.exec_layers) - 1, -1, -1):
                 grad_ready(i)

@@ -397,8 +397,12 @@ def lenet_tables(device):
     return _LENET_TABLES[key]
 
 
+def lenet_dense_part_floats(B: int) -> int:
+    return int(_C().lenet_dense_part_floats(int(B)))
+
+
 def lenet_train(x, labels, conv, dense_w, dense_wt, dense_b, conv_grads, dense_gw, dense_gb, hT, dzT, conv_part,
-                loss_part, stats, grad_scale):
+                dense_part, loss_part, stats, grad_scale):
     """Whole-network LeNet-5 training step on GPU (csrc/lenet_fused.hip, 2 launches): fills every
     gradient and ``stats`` = [loss sum, correct].  ``x``: bf16 batch [B,28,28,1] or a :class:`GatherRef`
     over a uint8 dataset; ``labels``: int32 [B] or a :class:`LabelRef` through the same indices."""
@@ -415,8 +419,8 @@ def lenet_train(x, labels, conv, dense_w, dense_wt, dense_b, conv_grads, dense_g
     B = x.shape[0]
     ftab, pxtab, frag = lenet_tables(stats.device)
     _C().lenet_train(src, idx, float(scale), lab, list(conv), list(dense_w), list(dense_wt), list(dense_b),
-                     list(conv_grads), list(dense_gw), list(dense_gb), list(hT), list(dzT), conv_part, loss_part,
-                     stats, frag, ftab, pxtab, int(B), float(grad_scale))
+                     list(conv_grads), list(dense_gw), list(dense_gb), list(hT), list(dzT), conv_part, dense_part,
+                     loss_part, stats, frag, ftab, pxtab, int(B), float(grad_scale))
 
 
 def convpool_supported(H, W, C, KH, KW, pad, N) -> bool:
