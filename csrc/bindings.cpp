@@ -824,6 +824,16 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
   check_hip(dfa::lenet_train(a, r, cur_stream()), "lenet_train");
 }
 
+void classifier_metrics_py(torch::Tensor z, torch::Tensor labels, int64_t kind, bool softmax, torch::Tensor out) {
+  need(z, at::kFloat, "metrics logits");
+  need(labels, at::kInt, "metrics labels");
+  need(out, at::kFloat, "metrics out");
+  TORCH_CHECK(z.dim() == 2 && labels.numel() == z.size(0) && out.numel() >= 2, "metrics: z [B][C], labels [B]");
+  check_hip(dfa::classifier_metrics(z.data_ptr<float>(), labels.data_ptr<int>(), (int)z.size(0), (int)z.size(1),
+                                    (int)kind, softmax ? 1 : 0, out.data_ptr<float>(), cur_stream()),
+            "classifier_metrics");
+}
+
 bool convpool_supported_py(int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t pad, int64_t N) {
   return dfa::convpool_supported(H, W, C, KH, KW, pad, N);
 }
@@ -1174,6 +1184,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, "data-gradient weight layout of the fused conv+pool kernel: (pair, row length K2pad)");
   m.def("convpool_supported", &convpool_supported_py);
   m.def("head_train", &head_train_py, "fused dense head: forward + softmax-CE + backward (2 launches)");
+  m.def("classifier_metrics", &classifier_metrics_py, "[loss sum, correct] of a classifier batch (one launch)");
   m.def("lenet_train", &lenet_train_py, "whole-network LeNet-5 training step (fwd + CE + bwd, 2 launches)");
   m.def("lenet_blocks", [](int64_t B) { return dfa::lenet_blocks((int)B); });
   m.def("lenet_frag_bytes", []() { return (int64_t)dfa::lenet_frag_bytes(); });

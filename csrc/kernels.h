@@ -301,6 +301,14 @@ hipError_t lenet_train(const LeNetArgs& a, LeNetRedArgs r, hipStream_t st);
 void lenet_set_stamps(void* buf);
 size_t lenet_frag_bytes();
 
+// Classifier evaluation metrics (csrc/metrics.hip): out = [sum of the per-example loss, correct].
+enum MetricKind {
+  kMetricMSE = 0, kMetricAbs = 1, kMetricHinge = 2, kMetricHuber = 3, kMetricLog = 4, kMetricSigmoidCE = 5,
+  kMetricSoftmaxCE = 6, kMetricCategoricalCE = 7
+};
+hipError_t classifier_metrics(const float* z, const int* labels, int B, int C, int kind, int softmax, float* out,
+                              hipStream_t st);
+
 // Direct convolution for C_in <= 4 (csrc/smallc.hip); igemm_fwd / igemm_wgrad dispatch to it.
 bool smallc_fwd_supported(const IGemmArgs& a, int mode);
 hipError_t smallc_fwd(const IGemmArgs& a, hipStream_t st);

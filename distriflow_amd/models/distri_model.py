@@ -21,6 +21,8 @@ Implementations:
 """
 from __future__ import annotations
 
+import warnings
+
 import os
 import time
 from abc import ABC, abstractmethod
@@ -201,10 +203,15 @@ def fetch_model(src: ModelSource, device=None) -> Net:
     raise TypeError(f"cannot fetch a model from {type(src).__name__}")
 
 
+_CE_LOSSES = {"softmaxCrossEntropy", "categorical_crossentropy", "categoricalCrossentropy"}
+_WARNED_LOSSES: set = set()
+
+
 class EngineModel(DistriModel):
     """The MI355X engine behind the DistriModel contract (reference DistributedTfModel)."""
 
-    def __init__(self, model: ModelSource, compile_config: Optional[dict] = None, device=None):
+    def __init__(self, model: ModelSource, compile_config: Optional[dict] = None, device=None,
+                 strict_loss: bool = False):
         self._src = model
         self._device = device
         self.compile = compile_args(compile_config)
@@ -213,6 +220,19 @@ class EngineModel(DistriModel):
         self.net: Optional[Net] = model if isinstance(model, Net) else None
         self.momentum = 0.0
         self.weight_decay = 0.0
+        loss = self.compile["loss"]
+        if loss not in _CE_LOSSES:
+            # the reference's fit() always optimises softmax cross-entropy and the
+            # compile loss (default meanSquaredError) only feeds evaluate(); the engine keeps that contract
+            # but says so once instead of silently training a different loss than the one configured
+            if strict_loss:
+                raise ValueError(f"EngineModel trains softmax cross-entropy on logits; compile loss {loss!r} "
+                                 "is not trainable by the engine")
+            if loss not in _WARNED_LOSSES:
+                _WARNED_LOSSES.add(loss)
+                warnings.warn(f"EngineModel trains softmax cross-entropy on logits; the compile loss {loss!r} is "
+                              "used for evaluate() metrics only (reference fit(), models.ts:137-142)",
+                              stacklevel=2)
 
     def fetch_initial(self):
         if self.net is None:
@@ -281,9 +301,21 @@ class EngineModel(DistriModel):
         return net.predict(xx)
 
     def evaluate(self, x, y) -> list[float]:
-        """[compiled loss, accuracy] on (x, y) — the reference's model.evaluate with the compile args."""
+        """[compiled loss, accuracy] on (x, y) — the reference's model.evaluate with the compile args.
+        GPU: the engine's forward kernels + one metrics launch (csrc/metrics.hip), no framework ops."""
         net = self._need()
         xx, yy = self._prep(x, y)
+        n = xx.shape[0]
+        loss = self.compile["loss"]
+        if net.is_gpu and loss in ops.METRIC_KINDS:
+            z = net._forward_eval(xx.to(net.dtype) if not isinstance(xx, ops.GatherRef) else xx)
+            if not hasattr(self, "_metric_buf") or self._metric_buf.device != z.device:
+                self._metric_buf = torch.zeros(2, dtype=torch.float32, device=z.device)
+            st = ops.classifier_metrics(z, yy, loss, net.final_softmax, self._metric_buf).tolist()
+            out = [st[0] / max(n, 1)]
+            if "accuracy" in self.compile["metrics"] or "acc" in self.compile["metrics"]:
+                out.append(st[1] / max(n, 1))
+            return out
         probs = net.predict(xx)
         labels = torch.nn.functional.one_hot(yy.long(), net.num_classes).float()
         out = [float(self.loss_fn(labels, probs).mean())]

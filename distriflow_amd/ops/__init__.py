@@ -351,6 +351,28 @@ def head_train(w, wt, b, gw, gb, hT, dzT, K, N, x, x_relu, xT, dx, logits, label
                     bool(x_relu), xT, dx, logits, labels, idx, float(grad_scale), loss_part, stats, int(phases))
 
 
+METRIC_KINDS = {"meanSquaredError": 0, "mse": 0, "absoluteDifference": 1, "hingeLoss": 2, "huberLoss": 3,
+                "logLoss": 4, "sigmoidCrossEntropy": 5, "softmaxCrossEntropy": 6, "categorical_crossentropy": 7,
+                "categoricalCrossentropy": 7}
+
+
+def classifier_metrics(z, labels, loss: str, softmax: bool, out):
+    """[sum over the batch of the compiled loss, number correct] of fp32 model outputs ``z`` [B][C]
+    against int labels (one launch on GPU, csrc/metrics.hip).  ``softmax``: the model output is
+    softmax(z).  Returns ``out`` (device [2]); CPU uses the torch loss registry."""
+    if z.is_cuda:
+        _C().classifier_metrics(z.contiguous(), labels.to(torch.int32).contiguous(), METRIC_KINDS[loss], bool(softmax),
+                                out)
+        return out
+    from ..losses import accuracy, get_loss
+
+    p = torch.softmax(z.float(), dim=1) if softmax else z.float()
+    onehot = torch.nn.functional.one_hot(labels.long(), z.shape[1]).float()
+    out[0] = get_loss(loss)(onehot, p).sum()
+    out[1] = accuracy(labels, p).sum()
+    return out
+
+
 def lenet_supported() -> bool:
     m = native.get(build_if_missing=False)
     return m is not None and hasattr(m, "lenet_train")

@@ -216,3 +216,72 @@ def test_debug_sync_mode(monkeypatch):
     st = net.compute_gradients(x, y)
     assert torch.isfinite(st).all()
     assert isinstance(ops._C(), ops._DebugSync)
+
+
+def _rel(a, b):
+    """(max-abs relative error, relative L2 error) of a against the reference b."""
+    a, b = a.detach().double().cpu().flatten(), b.detach().double().cpu().flatten()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12)), float((a - b).norm() / (b.norm() + 1e-30))
+
+
+@pytest.mark.parametrize("name,B", [("resnet18_cifar", 16), ("keras_cnn", 16), ("lenet5", 32)])
+def test_per_layer_numerics_against_cpu(name, B, monkeypatch):
+    """every executed layer of the GPU engine against the fp32 CPU reference layer, fed
+    the GPU's own bf16 input (forward) and upstream gradient (backward), so errors cannot compound:
+    per-layer max relative error of the output, the input gradient and each parameter gradient."""
+    from distriflow_amd import ops
+    from distriflow_amd.models.net import Net
+    from distriflow_amd.models.zoo import MODELS
+
+    monkeypatch.setenv("DISTRIFLOW_LENET_FUSED", "0")  # the per-layer kernels (the fused one: test_lenet_fused_gpu)
+    g = build_model(name, device="cuda", seed=3)
+    layers, shape = MODELS[name]()
+    c = Net(layers, shape, device="cpu", name=name, seed=3, compute_dtype=torch.bfloat16)
+    c.store.master.copy_(c.store.master.to(torch.bfloat16).float())
+    g.store.set_flat(c.store.master.cuda())
+    for net in (g, c):
+        net.bind(B)
+    torch.manual_seed(0)
+    x = torch.rand((B,) + tuple(g.input_shape)).to(torch.bfloat16)
+    y = torch.randint(0, g.num_classes, (B,), dtype=torch.int32)
+    hs = [x.cuda()]
+    h = hs[0]
+    for l in g.exec_layers:
+        h = l.forward(h, True)
+        hs.append(h.clone())
+    stats = torch.zeros(2, device="cuda")
+    dl = torch.empty(B, g.num_classes, dtype=g.dtype, device="cuda")
+    ops.softmax_ce(hs[-1].float(), y.cuda(), dl, stats, 1.0 / B)
+    ds = [None] * (len(g.exec_layers) + 1)
+    dxs = [None] * len(g.exec_layers)
+    d = dl
+    for i in range(len(g.exec_layers) - 1, -1, -1):
+        ds[i + 1] = d.clone()
+        d = g.exec_layers[i].backward(d)
+        dxs[i] = d.clone() if d is not None else None
+    torch.cuda.synchronize()
+    # leaf layers: max-abs relative error <= 5% of the tensor's largest element.  A ResidualBlock runs two
+    # conv + BN + ReLU stages internally, where a pre-activation within bf16 rounding of 0 can take the
+    # other ReLU branch on one side (a full-size difference at that element), so composite layers are
+    # held to the relative L2 error instead; every tensor must also be within 2% in L2.
+    from distriflow_amd.models.layers import ResidualBlock
+
+    worst, bad = {}, {}
+    for i, (lg, lc) in enumerate(zip(g.exec_layers, c.exec_layers)):
+        composite = isinstance(lg, ResidualBlock)
+        out = lc.forward(hs[i].cpu(), True)
+        res = {f"{lg.name}:out": _rel(hs[i + 1], out)}
+        dx = lc.backward(ds[i + 1].cpu())
+        if lg.need_dx and dxs[i] is not None and dx is not None:
+            res[f"{lg.name}:dx"] = _rel(dxs[i], dx)
+        for spec in lc.specs() if hasattr(lc, "specs") else []:
+            gc = c.store.gradient(spec.name)
+            if gc.norm() > 1e-8:
+                res[spec.name] = _rel(g.store.gradient(spec.name), gc)
+        for k, (mx, l2) in res.items():
+            worst[k] = (mx, l2)
+            if l2 > 0.02 or (not composite and mx > 0.05):
+                bad[k] = (round(mx, 4), round(l2, 5))
+    print(name, "max rel err", round(max(m for m, _ in worst.values()), 4), "max L2 rel err",
+          round(max(l for _, l in worst.values()), 5))
+    assert not bad, bad

@@ -203,3 +203,40 @@ def test_fedavg_device_engine_two_procs():
     assert r[0]["graph"] == "full"
     assert torch.equal(r[0]["w"], r[1]["w"])  # every rank ends a round with the same averaged model
     assert r[0]["acc"] > 0.3  # loss fell and the averaged model beats chance well on all 10 classes
+
+
+def _fedavg_average_worker(rank, world, port, out_dir):
+    _init(rank, world, port)
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.fedavg import FedAvgTrainer
+
+    dev = torch.device("cuda", 0)
+    net = build_model("lenet5", device=dev, seed=0)
+    tr = FedAvgTrainer(net, lr=0.1, local_steps=1, graph="none", allreduce="p2p")
+    g = torch.Generator().manual_seed(100 + rank)
+    mine = torch.randn(net.store.total, generator=g)
+    net.store.master.copy_(mine.to(dev))
+    tr.average()
+    torch.cuda.synchronize()
+    tr.check_comm()
+    torch.save({"mine": mine, "avg": net.store.master.cpu(), "path": tr.allreduce_path},
+               os.path.join(out_dir, f"f{rank}.pt"))
+    import torch.distributed as dist
+
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_fedavg_average_is_the_mean_of_rank_masters():
+    """the device FedAvg engine's average() equals the CPU mean of the ranks' masters
+    (one-shot xGMI all-reduce, rank-order sums, then the 1/world scale), on every rank."""
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_fedavg_average_worker, args=(world, _port(), d), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"f{i}.pt"), weights_only=True) for i in range(world)]
+    ref = torch.stack([x["mine"] for x in r]).double().mean(0).float()
+    for x in r:
+        assert x["path"] == "p2p"
+        torch.testing.assert_close(x["avg"], ref, rtol=1e-6, atol=1e-6)
+    assert torch.equal(r[0]["avg"], r[1]["avg"]) and torch.equal(r[0]["avg"], r[2]["avg"])
