@@ -3,8 +3,8 @@
 //
 // Two launches per direction:
 //   stats  : every workgroup reduces a row range into an fp32 partial slab [2][C]; the slabs are
-//            then combined inside the same launch by last-arriver hand-offs (agent-scope release,
-//            ticket counter, agent-scope acquire): the last of every 16 workgroups sums its
+//            then combined inside the same launch by last-arriver hand-offs (write-through sc1 slab
+//            stores, ticket counter, sc1 loads: no fences): the last of every 16 workgroups sums its
 //            group's slabs, and the last group reducer sums the (<= 16) group slabs in fp64 and
 //            finalises — forward: mean, invstd and the running statistics; backward: dgamma/dbeta
 //            straight into the flat gradient buffer plus the per-channel coefficients of
@@ -34,24 +34,27 @@ static int bn_grid(int M, int rpp) {
   return g;
 }
 
-// Publish this workgroup's global stores and draw a ticket from `counter`; returns true (in every
-// thread) in the last of `n` arrivers, which has then acquired the others' stores and re-armed the
+// Hand-off without fences (cdna_hip_programming.md Guideline 16, sc1 form): every slab word is
+// stored write-through (relaxed agent-scope atomic store = sc1) and drained by every storing wave
+// before the barrier; lane 0 then draws a ticket.  The last of `n` arrivers reads the slabs with sc1
+// loads (relaxed agent-scope atomic loads bypass this CU's L1), so neither side pays the agent-scope
+// release (an L2 writeback) or acquire that the round-1 version spent per workgroup.  It re-arms the
 // counter to 0 for the next launch.
+__device__ __forceinline__ void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ bool bn_last_arriver(unsigned* counter, unsigned n, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned tk = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *flag = (tk == n - 1) ? 1 : 0;
-    if (*flag) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (*flag) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
   return *flag != 0;
 }
 
@@ -151,8 +154,8 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
       u += ls[r * C + c];
       v += lq[r * C + c];
     }
-    slab[c] = u;
-    slab[C + c] = v;
+    st_sc1(slab + c, u);
+    st_sc1(slab + C + c, v);
   }
 
   // ---- level 1: the last of each group of 16 workgroups sums the group's slabs
@@ -164,11 +167,11 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
   for (int col = t; col < ncol; col += 256) {
     float v[BN_GROUP];
 #pragma unroll
-    for (int j = 0; j < BN_GROUP; ++j) v[j] = a.ws[(long long)(gbeg + min(j, gn - 1)) * ncol + col];  // all loads issued
+    for (int j = 0; j < BN_GROUP; ++j) v[j] = ld_sc1(a.ws + (long long)(gbeg + min(j, gn - 1)) * ncol + col);
     float u = 0.f;
 #pragma unroll
     for (int j = 0; j < BN_GROUP; ++j) u += j < gn ? v[j] : 0.f;
-    gslab[(long long)grp * ncol + col] = u;
+    st_sc1(gslab + (long long)grp * ncol + col, u);
   }
 
   // ---- level 2: the last group reducer sums the group slabs in fp64 and finalises
@@ -180,8 +183,8 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
 #pragma unroll
       for (int j = 0; j < BN_GROUP; ++j) {
         const long long base = (long long)min(g0 + j, ngrp - 1) * ncol;
-        su[j] = gslab[base + c];
-        qu[j] = gslab[base + C + c];
+        su[j] = ld_sc1(gslab + base + c);
+        qu[j] = ld_sc1(gslab + base + C + c);
       }
 #pragma unroll
       for (int j = 0; j < BN_GROUP; ++j) {

@@ -42,7 +42,11 @@ class DataParallelTrainer:
         # bucket size: small models still get >= 2 buckets (the head's gradient all-reduce then overlaps
         # the convolution backward); large ones use up to 32 MB (few, large RCCL calls over xGMI)
         total_bytes = net.store.total * 4
-        if bucket_mb is None:
+        if bucket_mb is None and getattr(net, "lenet_fused", False):
+            # the fused LeNet-5 step produces every gradient at once: nothing to overlap, so ONE bucket
+            # (one all-reduce launch over xGMI instead of several latency-bound ones)
+            self.bucket_bytes = total_bytes
+        elif bucket_mb is None:
             self.bucket_bytes = int(min(32 << 20, max(64 << 10, total_bytes // 4)))
         else:
             self.bucket_bytes = int(bucket_mb * (1 << 20))
