@@ -44,8 +44,10 @@ class DataParallelTrainer:
         total_bytes = net.store.total * 4
         if bucket_mb is None and getattr(net, "lenet_fused", False):
             # the fused LeNet-5 step produces every gradient at once: nothing to overlap, so ONE bucket
-            # (one all-reduce launch over xGMI instead of several latency-bound ones)
+            # (one all-reduce launch over xGMI instead of several latency-bound ones), issued in stream
+            # order after the reduction launch (no side-stream hop)
             self.bucket_bytes = total_bytes
+            self.overlap = False
         elif bucket_mb is None:
             self.bucket_bytes = int(min(32 << 20, max(64 << 10, total_bytes // 4)))
         else:
