@@ -265,7 +265,9 @@ void gap_bwd_py(torch::Tensor dy, torch::Tensor dx, int64_t B, int64_t HW, int64
 void sgd_multi_py(torch::Tensor descs, int64_t ndesc, int64_t total_blocks, torch::Tensor master, torch::Tensor grad,
                   c10::optional<torch::Tensor> mom, torch::Tensor wbf, torch::Tensor hyper, bool apply_update,
                   c10::optional<torch::Tensor> idx_stream, c10::optional<torch::Tensor> idx_cursor,
-                  c10::optional<torch::Tensor> idx_dst, c10::optional<torch::Tensor> descs_host) {
+                  c10::optional<torch::Tensor> idx_dst, c10::optional<torch::Tensor> descs_host,
+                  c10::optional<torch::Tensor> lenet_frag, int64_t frag_w1, int64_t frag_w2,
+                  c10::optional<torch::Tensor> lenet_snap) {
   TORCH_CHECK(descs.is_cuda() && descs.scalar_type() == at::kLong && descs.is_contiguous(), "descs must be int64 GPU");
   const dfa::ParamDesc* hd = nullptr;
   if (descs_host.has_value() && descs_host->defined()) {  // same table, host copy: passed in the kernel arguments
@@ -302,9 +304,27 @@ void sgd_multi_py(torch::Tensor descs, int64_t ndesc, int64_t total_blocks, torc
     is.B = (int)idx_dst->numel();
     is.nsteps = (int)idx_stream->size(0);
   }
+  if (lenet_frag.has_value() && lenet_frag->defined()) {
+    TORCH_CHECK(lenet_frag->is_cuda() && lenet_frag->is_contiguous() &&
+                    (size_t)lenet_frag->nbytes() >= dfa::lenet_frag_bytes(),
+                "lenet_frag: fragment buffer too small");
+    TORCH_CHECK(frag_w1 >= 0 && frag_w1 + 150 <= master.numel() && frag_w2 >= 0 && frag_w2 + 2400 <= master.numel(),
+                "lenet_frag: conv kernel offsets out of range");
+    TORCH_CHECK(!apply_update || (lenet_snap.has_value() && lenet_snap->defined()),
+                "lenet_frag: an update needs the pre-update snapshot (lenet_snap)");
+    if (lenet_snap.has_value() && lenet_snap->defined()) {
+      need(*lenet_snap, at::kFloat, "lenet_snap");
+      TORCH_CHECK(lenet_snap->numel() >= 2 * 2550, "lenet_snap must hold 2 x 2550 floats");
+      is.snap = lenet_snap->data_ptr<float>();
+    }
+    is.frag = lenet_frag->data_ptr();
+    is.frag_w1 = frag_w1;
+    is.frag_w2 = frag_w2;
+  }
   check_hip(dfa::sgd_multi(reinterpret_cast<const dfa::ParamDesc*>(descs.data_ptr()), (int)ndesc, (int)total_blocks,
                            master.data_ptr<float>(), grad.data_ptr<float>(), mp, (dfa::bf16*)wbf.data_ptr(),
-                           hyper.data_ptr<float>(), apply_update ? 1 : 0, cur_stream(), is.src ? &is : nullptr, hd),
+                           hyper.data_ptr<float>(), apply_update ? 1 : 0, cur_stream(), (is.src || is.frag) ? &is : nullptr,
+                           hd),
             "sgd_multi");
 }
 
@@ -714,7 +734,8 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
                     std::vector<torch::Tensor> conv_grads, std::vector<torch::Tensor> dense_gw,
                     std::vector<torch::Tensor> dense_gb, std::vector<torch::Tensor> hT, std::vector<torch::Tensor> dzT,
                     torch::Tensor conv_part, torch::Tensor dense_part, torch::Tensor loss_part, torch::Tensor stats,
-                    torch::Tensor frag, torch::Tensor ftab, torch::Tensor pxtab, int64_t B, double grad_scale) {
+                    torch::Tensor frag, torch::Tensor ftab, torch::Tensor pxtab, int64_t B, double grad_scale,
+                    bool prep, c10::optional<torch::Tensor> snap, std::vector<torch::Tensor> conv_mom) {
   TORCH_CHECK(conv.size() == 4 && conv_grads.size() == 4, "lenet: conv = [w1, b1, w2, b2]");
   TORCH_CHECK(dense_w.size() == 3 && dense_wt.size() == 3 && dense_b.size() == 3 && dense_gw.size() == 3 &&
                   dense_gb.size() == 3 && hT.size() == 3 && dzT.size() == 3,
@@ -799,6 +820,7 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
   TORCH_CHECK(ftab.is_cuda() && ftab.scalar_type() == at::kByte && ftab.numel() == 98 * 2 * 16, "lenet: ftab");
   TORCH_CHECK(pxtab.is_cuda() && pxtab.scalar_type() == at::kShort && pxtab.numel() == 800, "lenet: pxtab");
   a.frag = frag.data_ptr();
+  a.prep = prep ? 1 : 0;
   a.ftab = ftab.data_ptr<uint8_t>();
   a.pxtab = reinterpret_cast<const unsigned short*>(pxtab.data_ptr());
   a.B = (int)B;
@@ -820,6 +842,22 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
     r.L[l].gb = dense_gb[l].data_ptr<float>();
     r.L[l].N = (int)NK[l][0];
     r.L[l].K = (int)NK[l][1];
+  }
+  // optional pre-update snapshot of the conv kernels (weights, momentum) for the optimizer's fragment rebuild
+  r.w1 = a.w1;
+  r.w2 = a.w2;
+  if (snap.has_value() && snap->defined()) {
+    need(*snap, at::kFloat, "lenet snap");
+    TORCH_CHECK(snap->numel() >= 2 * 2550, "lenet: snap must hold 2 x 2550 floats");
+    r.snap = snap->data_ptr<float>();
+    TORCH_CHECK(conv_mom.empty() || conv_mom.size() == 2, "lenet: conv_mom = [m1, m2] or []");
+    if (conv_mom.size() == 2) {
+      need(conv_mom[0], at::kFloat, "lenet m1");
+      need(conv_mom[1], at::kFloat, "lenet m2");
+      TORCH_CHECK(conv_mom[0].numel() == 150 && conv_mom[1].numel() == 2400, "lenet: conv momentum sizes");
+      r.m1 = conv_mom[0].data_ptr<float>();
+      r.m2 = conv_mom[1].data_ptr<float>();
+    }
   }
   check_hip(dfa::lenet_train(a, r, cur_stream()), "lenet_train");
 }
@@ -1144,7 +1182,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_multi", &sgd_multi_py, py::arg("descs"), py::arg("ndesc"), py::arg("total_blocks"), py::arg("master"),
         py::arg("grad"), py::arg("mom"), py::arg("wbf"), py::arg("hyper"), py::arg("apply_update"),
         py::arg("idx_stream") = py::none(), py::arg("idx_cursor") = py::none(), py::arg("idx_dst") = py::none(),
-        py::arg("descs_host") = py::none());
+        py::arg("descs_host") = py::none(), py::arg("lenet_frag") = py::none(), py::arg("frag_w1") = 0,
+        py::arg("frag_w2") = 0, py::arg("lenet_snap") = py::none());
   m.def("sum_buffers", &sum_buffers_py);
   m.def("axpby", &axpby_py);
   m.def("bn_stats_fwd", &bn_stats_fwd_py, "BN forward statistics (partials + last-workgroup finalize, one launch)");
@@ -1185,7 +1224,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("convpool_supported", &convpool_supported_py);
   m.def("head_train", &head_train_py, "fused dense head: forward + softmax-CE + backward (2 launches)");
   m.def("classifier_metrics", &classifier_metrics_py, "[loss sum, correct] of a classifier batch (one launch)");
-  m.def("lenet_train", &lenet_train_py, "whole-network LeNet-5 training step (fwd + CE + bwd, 2 launches)");
+  m.def("lenet_train", &lenet_train_py, "whole-network LeNet-5 training step (fwd + CE + bwd, 2 launches)",
+        py::arg("x"), py::arg("idx"), py::arg("scale"), py::arg("labels"), py::arg("conv"), py::arg("dense_w"),
+        py::arg("dense_wt"), py::arg("dense_b"), py::arg("conv_grads"), py::arg("dense_gw"), py::arg("dense_gb"),
+        py::arg("hT"), py::arg("dzT"), py::arg("conv_part"), py::arg("dense_part"), py::arg("loss_part"),
+        py::arg("stats"), py::arg("frag"), py::arg("ftab"), py::arg("pxtab"), py::arg("B"), py::arg("grad_scale"),
+        py::arg("prep") = true, py::arg("snap") = py::none(),
+        py::arg("conv_mom") = std::vector<torch::Tensor>{});
   m.def("lenet_blocks", [](int64_t B) { return dfa::lenet_blocks((int)B); });
   m.def("lenet_frag_bytes", []() { return (int64_t)dfa::lenet_frag_bytes(); });
   m.def("lenet_dense_part_floats", [](int64_t B) { return (int64_t)dfa::lenet_dense_part_floats((int)B); });

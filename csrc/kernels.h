@@ -88,6 +88,11 @@ struct IndexStream {  // next-batch staging folded into the optimizer launch (cs
   long long* cursor;     // device step cursor
   long long* dst;        // [B] static index buffer read by the step
   int B, nsteps;
+  // fused LeNet-5 conv-weight fragments rebuilt from the updated weights (csrc/lenet_frag.h); frag null = off
+  void* frag;
+  long long frag_w1, frag_w2;  // offsets of the conv1 / conv2 kernels in grad (and master / momentum)
+  const float* snap;           // [2][2550] pre-update weights / momentum (lenet_reduce_kernel); read
+                               // instead of master, which this same launch overwrites
 };
 hipError_t sgd_multi(const ParamDesc* descs, int ndesc, int total_blocks, float* master, const float* grad,
                      float* mom_buf, bf16* wbf, const float* hyper, int apply_update, hipStream_t st,
@@ -271,6 +276,7 @@ struct LeNetArgs {
   bf16 *h0T, *h1T, *h2T;      // [400|120|84][ldt] transposed dense inputs
   bf16 *dz1T, *dz2T, *dz3T;   // [120|84|10][ldt] transposed dense output gradients
   float* logits;              // [B][10] (nullable)
+  int prep;                   // 1: launch the fragment prep kernel first (0: the optimizer rebuilt them)
   const void* frag;           // [37][64] x 8 bf16 conv weight fragments of this step (written by the prep launch)
   const unsigned char* ftab;  // [98][2][16] conv2 dgrad gather table (lenet_tables)
   const unsigned short* pxtab;  // [800] conv2 output row -> pool1 pixel (lenet_tables)
@@ -293,6 +299,9 @@ struct LeNetRedArgs {
   LeNetDense L[3];
   int nblk, ldt, nconv_blocks, dense_tiles;
   int tile_of_block[kLeNetMaxTiles];  // XCD-aware placement of the dense weight-gradient tiles
+  // optional snapshot [2][2550] of the conv kernels' weights (w1, w2) and momentum (m1, m2; null = 0)
+  const float *w1, *w2, *m1, *m2;
+  float* snap;
 };
 int lenet_dense_part_floats(int B);
 size_t lenet_train_lds();

@@ -26,6 +26,7 @@
 //                        workgroups), dense weight gradients over the batch (MFMA, K = batch), loss.
 #include "common.h"
 #include "kernels.h"
+#include "lenet_frag.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -36,8 +37,6 @@ namespace {
 
 constexpr int IMG = 8;     // images per workgroup
 constexpr int NT = 256;    // threads per workgroup
-constexpr int NFRAG = 37;  // prep fragments: conv1 banded [5 ky][3 channel pairs], conv2 fwd [7], dgrad [15]
-constexpr int FR_C1 = 0, FR_C2 = 15, FR_DG = 22;
 // LDS carve (bytes), every offset 16-byte aligned
 constexpr int XS_ELEMS = IMG * 1024 + 32;           // [8][32][32] padded input (+ tail pad)
 constexpr int OFF_XS = 0;
@@ -675,42 +674,16 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
   LN_STAMP(10);
 }
 
-// Conv weights of this step as MFMA B fragments ([NFRAG][64 lanes] of 8 bf16): one block, the 2550
-// fp32 weights staged in LDS by coalesced loads, then every fragment lane built from LDS.
+// Conv weights of this step as MFMA B fragments: one block (csrc/lenet_frag.h).  Only launched when
+// the optimizer does not rebuild them (the fused step's SGD launch normally does, see optim.hip).
 constexpr int PT = 1024;
 __global__ void __launch_bounds__(PT) lenet_prep_kernel(const float* __restrict__ w1g, const float* __restrict__ w2g,
                                                         bf16x8* __restrict__ frag) {
-  __shared__ float w1[150];
-  __shared__ float w2[2400];
-  for (int e = threadIdx.x; e < 150; e += PT) w1[e] = w1g[e];
-  for (int e = threadIdx.x; e < 2400; e += PT) w2[e] = w2g[e];
+  __shared__ float w[kLeNetConvW];
+  for (int e = threadIdx.x; e < 150; e += PT) w[e] = w1g[e];
+  for (int e = threadIdx.x; e < 2400; e += PT) w[150 + e] = w2g[e];
   __syncthreads();
-  for (int fl = threadIdx.x; fl < NFRAG * 64; fl += PT) {
-    const int f = fl >> 6, lane = fl & 63, i = lane & 15, g = lane >> 4;
-    bf16x8 o;
-    if (f < FR_C2) {  // conv1 banded: f = ky * 3 + T, column j = (x offset 2 (j & 7) [+ parity], channel 2T + (j >> 3))
-      const int ky = f / 3, T = f - 3 * (f / 3), c = 2 * T + (i >> 3), j8 = i & 7;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int kx = 8 * g + e - 2 * j8;
-        o[e] = f2bf((kx >= 0 && kx < 5) ? w1[c * 25 + ky * 5 + kx] : 0.f);
-      }
-    } else if (f < FR_DG) {  // conv2 forward: step s, column n = i, k = (tap 4s + g, channel e)
-      const int s = f - FR_C2, tap = 4 * s + g;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf((tap < 25 && e < 6) ? w2[i * 150 + tap * 6 + e] : 0.f);
-    } else {  // conv2 data gradient, pair-banded: column (b = i >> 3, c = i & 7), k = ((ky, u), n)
-      const int s = f - FR_DG, P = 2 * s + (g >> 1), ky = P / 6, u = P - 6 * (P / 6);
-      const int b = i >> 3, c = i & 7, kx = u - 1 + b;
-      const bool ok = P < 30 && kx >= 0 && kx < 5 && c < 6;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int n = 8 * (g & 1) + e;
-        o[e] = f2bf(ok ? w2[n * 150 + (ky * 5 + kx) * 6 + c] : 0.f);
-      }
-    }
-    frag[fl] = o;
-  }
+  lenet_build_frags(w, frag, threadIdx.x, PT);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -814,6 +787,14 @@ __global__ void __launch_bounds__(RT) lenet_reduce_kernel(LeNetRedArgs a) {
                    : p < kLeNetPB2 ? a.g_w2 + (p - kLeNetPW2)
                                    : a.g_b2 + (p - kLeNetPB2);
       *dst = v;
+      // the conv kernels' weights and momentum as this gradient saw them: the optimizer launch
+      // rebuilds the next step's fragments from these (no read of state it is overwriting)
+      const int wj = p < kLeNetPB1 ? p : (p >= kLeNetPW2 && p < kLeNetPB2) ? 150 + (p - kLeNetPW2) : -1;
+      if (a.snap != nullptr && wj >= 0) {
+        const long long o = wj < 150 ? wj : wj - 150;
+        a.snap[wj] = wj < 150 ? a.w1[o] : a.w2[o];
+        a.snap[kLeNetConvW + wj] = a.m1 == nullptr ? 0.f : (wj < 150 ? a.m1[o] : a.m2[o]);
+      }
     }
     return;
   }
@@ -848,8 +829,11 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   a.stamps = g_lenet_stamps_host;
   if (a.B <= 0 || a.ldt % 32 || a.ldt < a.B || !a.frag || !a.ftab || !a.pxtab) return hipErrorInvalidValue;
   const int nblk = (a.B + IMG - 1) / IMG;
-  hipLaunchKernelGGL(lenet_prep_kernel, dim3(1), dim3(PT), 0, st, a.w1, a.w2, reinterpret_cast<bf16x8*>(const_cast<void*>(a.frag)));
-  DFA_HIP_CHECK(hipGetLastError());
+  if (a.prep) {
+    hipLaunchKernelGGL(lenet_prep_kernel, dim3(1), dim3(PT), 0, st, a.w1, a.w2,
+                       reinterpret_cast<bf16x8*>(const_cast<void*>(a.frag)));
+    DFA_HIP_CHECK(hipGetLastError());
+  }
   hipLaunchKernelGGL(lenet_train_kernel, dim3(nblk), dim3(NT), LDS_BYTES, st, a);
   DFA_HIP_CHECK(hipGetLastError());
   r.nblk = nblk;

@@ -12,6 +12,7 @@
 //     sees learning-rate changes without re-capture.
 #include "common.h"
 #include "kernels.h"
+#include "lenet_frag.h"
 
 namespace dfa {
 
@@ -25,6 +26,55 @@ __device__ __forceinline__ int find_desc(const DT& d, int n, int bid) {
     if (d[mid].block_start <= bid) lo = mid; else hi = mid - 1;
   }
   return lo;
+}
+
+// The bf16 compute copies of element i (value w) of a matrix parameter.
+__device__ __forceinline__ void emit_copies(const ParamDesc& d, int i, float w, bf16* __restrict__ wbf) {
+  if (d.bf_off < 0) return;
+  const int K = d.T * d.Ci;
+  const int n = i / K;
+  const int kk = i - n * K;
+  const bf16 wb = f2bf(w);
+  if ((d.pad_ >> 28) & 1) {  // tile-mode layouts, element-wise (the LeNet fragment workgroup's path)
+    const int t = kk / d.Ci, ci = kk - t * d.Ci;
+    wbf[d.bf_off + (long long)n * round_up(K, 32) + kk] = wb;
+    wbf[d.bft_off + (long long)ci * round_up(d.T * d.N, 32) + t * d.N + n] = wb;
+    return;
+  }
+  // d.pad_ = KW | Cp << 16 (KW > 0): the primary copy uses the row-segment layout of the fused
+  // conv+pool forward, [Npad16][round32(KH * round8(KW*Cp))], column ky*round8(KW*Cp) + kx*Cp + ci
+  // d.pad_ = KW | Cp << 16 | pair << 30: pair layout (N <= 8) = 16 rows, rows 8+n hold channel n
+  // shifted right by one kernel column (the fused conv+pool forward computes pixels x and x+1)
+  const int rKW = d.pad_ & 0xffff;
+  // d.pad_ bit 29: the dgrad copy uses the conv+pool dgrad pair layout (csrc/convpool.hip make_dgrad),
+  // [16][round32(KH*(KW+1)*N)]: row ci col (a*(KW+1) + KW-1-kx)*N + n and row 8+ci col (a*(KW+1) + KW-kx)*N + n,
+  // a = KH-1-ky (the kernel flip of the transposed convolution)
+  const int rCp = ((d.pad_ >> 16) & 0xfff) > 0 ? ((d.pad_ >> 16) & 0xfff) : d.Ci;
+  const bool rpair = (d.pad_ >> 30) & 1;
+  const bool tpair = rKW > 0 && ((d.pad_ >> 29) & 1);
+  const int RLp = rKW > 0 ? round_up((rKW + (rpair ? 1 : 0)) * rCp, 8) : K;
+  const int Kpad = round_up(rKW > 0 ? (d.T / rKW) * RLp : K, 32);
+  const int KpadT = round_up(tpair ? (d.T / rKW) * (rKW + 1) * d.N : d.T * d.N, 32);
+  int col = kk;
+  if (rKW > 0) {
+    const int t = kk / d.Ci, ci = kk - (kk / d.Ci) * d.Ci;
+    const int ky = t / rKW, kx = t - (t / rKW) * rKW;
+    col = ky * RLp + kx * rCp + ci;
+  }
+  wbf[d.bf_off + (long long)n * Kpad + col] = wb;
+  if (rpair) wbf[d.bf_off + (long long)(n + 8) * Kpad + col + rCp] = wb;
+  if (d.bft_off >= 0) {
+    const int t = kk / d.Ci;
+    const int ci = kk - t * d.Ci;
+    if (tpair) {
+      const int ky = t / rKW, kx = t - ky * rKW;
+      const int c0 = ((d.T / rKW - 1 - ky) * (rKW + 1) + rKW - 1 - kx) * d.N + n;
+      wbf[d.bft_off + (long long)ci * KpadT + c0] = wb;
+      wbf[d.bft_off + (long long)(ci + 8) * KpadT + c0 + d.N] = wb;
+    } else {
+      wbf[d.bft_off + (long long)ci * KpadT + t * d.N + n] = wb;
+    }
+  }
 }
 
 // hyper = [lr, momentum, weight_decay, grad_scale, nesterov]
@@ -45,14 +95,9 @@ __device__ __forceinline__ void sgd_multi_body(const DT& descs, int ndesc,
   auto update = [&](int i) -> float {
     float w = master[d.off + i];
     if (apply_update) {
-      float g = grad[d.off + i] * gs;
-      if (wd != 0.f) g += wd * w;
-      if (mom != 0.f) {
-        float v = mom * mom_buf[d.off + i] + g;
-        mom_buf[d.off + i] = v;
-        g = nesterov ? g + mom * v : v;
-      }
-      w -= lr * g;
+      float v = 0.f;
+      w = sgd_new_weight(w, grad[d.off + i], mom != 0.f ? mom_buf[d.off + i] : 0.f, lr, mom, wd, gs, nesterov, &v);
+      if (mom != 0.f) mom_buf[d.off + i] = v;
       master[d.off + i] = w;
     }
     return w;
@@ -89,50 +134,11 @@ __device__ __forceinline__ void sgd_multi_body(const DT& descs, int ndesc,
     }
     return;
   }
-  // d.pad_ = KW | Cp << 16 (KW > 0): the primary copy uses the row-segment layout of the fused
-  // conv+pool forward, [Npad16][round32(KH * round8(KW*Cp))], column ky*round8(KW*Cp) + kx*Cp + ci
-  // d.pad_ = KW | Cp << 16 | pair << 30: pair layout (N <= 8) = 16 rows, rows 8+n hold channel n
-  // shifted right by one kernel column (the fused conv+pool forward computes pixels x and x+1)
-  const int rKW = d.pad_ & 0xffff;
-  // d.pad_ bit 29: the dgrad copy uses the conv+pool dgrad pair layout (csrc/convpool.hip make_dgrad),
-  // [16][round32(KH*(KW+1)*N)]: row ci col (a*(KW+1) + KW-1-kx)*N + n and row 8+ci col (a*(KW+1) + KW-kx)*N + n,
-  // a = KH-1-ky (the kernel flip of the transposed convolution)
-  const int rCp = ((d.pad_ >> 16) & 0xfff) > 0 ? ((d.pad_ >> 16) & 0xfff) : d.Ci;
-  const bool rpair = (d.pad_ >> 30) & 1;
-  const bool tpair = rKW > 0 && ((d.pad_ >> 29) & 1);
-  const int RLp = rKW > 0 ? round_up((rKW + (rpair ? 1 : 0)) * rCp, 8) : K;
-  const int Kpad = round_up(rKW > 0 ? (d.T / rKW) * RLp : K, 32);
-  const int KpadT = round_up(tpair ? (d.T / rKW) * (rKW + 1) * d.N : d.T * d.N, 32);
 #pragma unroll
   for (int r = 0; r < SGD_ELEMS_PER_BLOCK / 256; ++r) {
     const int i = base + r * 256 + threadIdx.x;
     if (i >= d.numel) break;
-    const float w = update(i);
-    if (d.bf_off >= 0) {
-      const int n = i / K;
-      const int kk = i - n * K;
-      const bf16 wb = f2bf(w);
-      int col = kk;
-      if (rKW > 0) {
-        const int t = kk / d.Ci, ci = kk - (kk / d.Ci) * d.Ci;
-        const int ky = t / rKW, kx = t - (t / rKW) * rKW;
-        col = ky * RLp + kx * rCp + ci;
-      }
-      wbf[d.bf_off + (long long)n * Kpad + col] = wb;
-      if (rpair) wbf[d.bf_off + (long long)(n + 8) * Kpad + col + rCp] = wb;
-      if (d.bft_off >= 0) {
-        const int t = kk / d.Ci;
-        const int ci = kk - t * d.Ci;
-        if (tpair) {
-          const int ky = t / rKW, kx = t - ky * rKW;
-          const int c0 = ((d.T / rKW - 1 - ky) * (rKW + 1) + rKW - 1 - kx) * d.N + n;
-          wbf[d.bft_off + (long long)ci * KpadT + c0] = wb;
-          wbf[d.bft_off + (long long)(ci + 8) * KpadT + c0 + d.N] = wb;
-        } else {
-          wbf[d.bft_off + (long long)ci * KpadT + t * d.N + n] = wb;
-        }
-      }
-    }
+    emit_copies(d, i, update(i), wbf);
   }
 }
 
@@ -165,6 +171,32 @@ __device__ __forceinline__ void index_stream_body(const IndexStream& is) {
   if (threadIdx.x == 0) *is.cursor = next;
 }
 
+// Fused LeNet-5: the conv-weight MFMA fragments of the next step, kLeNetFragBlocks extra workgroups,
+// one fragment lane per thread.  Each new weight is recomputed with the owning workgroup's exact
+// (non-contracted) update from the pre-update snapshot the reduce kernel took: nothing here reads
+// master / momentum, which the owners overwrite in this same launch.  apply_update == 0 (compute
+// copy refresh, master not written) reads master directly.
+constexpr int kLeNetFragBlocks = (kLeNetFragLanes + 255) / 256;
+
+__device__ __forceinline__ void lenet_frag_body(const IndexStream& is, int fb, const float* __restrict__ master,
+                                                const float* __restrict__ grad, const float* __restrict__ hyper,
+                                                int apply_update) {
+  const int fl = fb * 256 + threadIdx.x;
+  if (fl >= kLeNetFragLanes) return;
+  bf16x8* frag = reinterpret_cast<bf16x8*>(is.frag);
+  if (!apply_update) {
+    frag[fl] = lenet_frag_lane(fl, [&](int j) { return master[j < 150 ? is.frag_w1 + j : is.frag_w2 + (j - 150)]; });
+    return;
+  }
+  const float lr = hyper[0], mom = hyper[1], wd = hyper[2], gs = hyper[3];
+  const bool nesterov = hyper[4] != 0.f;
+  frag[fl] = lenet_frag_lane(fl, [&](int j) {
+    const float g = grad[j < 150 ? is.frag_w1 + j : is.frag_w2 + (j - 150)];
+    return sgd_new_weight(is.snap[j], g, mom != 0.f ? is.snap[kLeNetConvW + j] : 0.f, lr, mom, wd, gs, nesterov,
+                          nullptr);
+  });
+}
+
 template <bool INL>
 __global__ void __launch_bounds__(256) sgd_multi_stream_kernel(const ParamDesc* __restrict__ descs,
                                                                const ParamDescTable tab, int ndesc,
@@ -180,18 +212,29 @@ __global__ void __launch_bounds__(256) sgd_multi_stream_kernel(const ParamDesc* 
       sgd_multi_body(descs, ndesc, master, grad, mom_buf, wbf, hyper, apply_update, blockIdx.x);
     return;
   }
-  if (is.src != nullptr) index_stream_body(is);  // the single index-stream workgroup
+  int fb = blockIdx.x - total_blocks;
+  if (is.src != nullptr) {
+    if (fb == 0) {
+      index_stream_body(is);  // the single index-stream workgroup
+      return;
+    }
+    --fb;
+  }
+  if (is.frag != nullptr) lenet_frag_body(is, fb, master, grad, hyper, apply_update);
 }
 
 hipError_t sgd_multi(const ParamDesc* descs, int ndesc, int total_blocks, float* master, const float* grad,
                      float* mom_buf, bf16* wbf, const float* hyper, int apply_update, hipStream_t st,
                      const IndexStream* is, const ParamDesc* host_descs) {
   const bool stream = is != nullptr && is->src != nullptr;
+  const bool frag = is != nullptr && is->frag != nullptr;
   total_blocks = max(total_blocks, 0);
-  if ((ndesc <= 0 || total_blocks <= 0) && !stream) return hipSuccess;
+  if ((ndesc <= 0 || total_blocks <= 0) && !stream && !frag) return hipSuccess;
   IndexStream isv{};
-  if (stream) isv = *is;
-  const int grid = total_blocks + (stream ? 1 : 0);
+  if (is != nullptr) isv = *is;
+  if (!stream) isv.src = nullptr;
+  if (frag && apply_update && is->snap == nullptr) return hipErrorInvalidValue;
+  const int grid = total_blocks + (stream ? 1 : 0) + (frag ? kLeNetFragBlocks : 0);
   if (host_descs != nullptr && ndesc <= kInlineDescs) {
     ParamDescTable tab{};
     for (int i = 0; i < ndesc; ++i) tab.d[i] = host_descs[i];

@@ -42,6 +42,14 @@ class Net:
         for l in self.exec_layers:
             specs += l.specs()
         self.store = ParamStore(specs, self.device, compute_bf16=self.is_gpu, seed=seed)
+        if self.lenet_fused:
+            # the optimizer launch rebuilds the fused step's conv-weight fragments (no prep launch per step)
+            c1, c2 = self.exec_layers[0], self.exec_layers[1]
+            frag = torch.zeros(ops.lenet_frag_bytes(), dtype=torch.uint8, device=self.device)
+            self.store.lenet_frag = (frag, self.store.offsets[f"{c1.name}/kernel"],
+                                     self.store.offsets[f"{c2.name}/kernel"])
+            self.store.lenet_snap = torch.zeros(2 * 2550, dtype=torch.float32, device=self.device)
+            self.store.refresh_compute()
         for l in self.exec_layers:
             if isinstance(l, ResidualBlock):
                 l.bind_store(self.store)
@@ -271,7 +279,11 @@ class Net:
                         cgrads, [st.grad_matrix(f"{d.name}/kernel") for d in dense],
                         [st.gradient(f"{d.name}/bias") for d in dense], [self.head_xT] + self.head_hT[:2],
                         self.head_dzT, self.lenet_conv_part, self.lenet_dense_part, self.lenet_loss_part, self.stats,
-                        1.0 / B)
+                        1.0 / B, frag=st.lenet_frag[0] if st.lenet_frag is not None else None,
+                        prep=st.lenet_frag is None or st.lenet_state == "stale", snap=st.lenet_snap,
+                        conv_mom=st.lenet_conv_momentum())
+        if st.lenet_frag is not None:
+            st.lenet_state = "snap"
         if grad_ready is not None:
             for i in range(len(self.exec_layers) - 1, -1, -1):
                 grad_ready(i)

@@ -218,12 +218,41 @@ class ParamStore:
         if any(frozen):
             raise NotImplementedError("non-trainable matrix parameters are not supported yet")
 
+    # fused LeNet-5 (csrc/lenet_fused.hip): (frag buffer, conv1 kernel offset, conv2 kernel offset).  The
+    # optimizer launch rebuilds the conv-weight MFMA fragments of the next step from the pre-update
+    # snapshot ``lenet_snap`` the step's reduce kernel took.  ``lenet_state``: "fresh" = fragments match
+    # the master; "snap" = also a snapshot of the current master / momentum exists (a fused step ran);
+    # "stale" = the master changed without a rebuild (the next fused step launches its prep kernel).
+    lenet_frag = None
+    lenet_snap = None
+    lenet_state = "stale"
+
+    def _frag_kw(self, update: bool) -> dict:
+        if self.lenet_frag is None:
+            return {}
+        if update and self.lenet_state != "snap":
+            self.lenet_state = "stale"  # gradient not from a fused step: no snapshot to rebuild from
+            return {}
+        buf, o1, o2 = self.lenet_frag
+        self.lenet_state = "fresh"
+        kw = {"lenet_frag": buf, "frag_w1": int(o1), "frag_w2": int(o2)}
+        if update:
+            kw["lenet_snap"] = self.lenet_snap
+        return kw
+
+    def lenet_conv_momentum(self) -> list:
+        """Momentum views of the two conv kernels (for the fused step's snapshot); [] without momentum."""
+        if self.momentum is None or self.lenet_frag is None:
+            return []
+        _, o1, o2 = self.lenet_frag
+        return [self.momentum[o1: o1 + 150], self.momentum[o2: o2 + 2400]]
+
     def refresh_compute(self):
         """Re-emit the bf16 compute copies from the fp32 master (after init / set_vars / load)."""
         if not self.compute_bf16:
             return
         native.require().sgd_multi(self._descs, self._ndesc, self._sgd_blocks, self.master, self.grad, None,
-                                   self.wbf, self.hyper, False, descs_host=self._descs_host)
+                                   self.wbf, self.hyper, False, descs_host=self._descs_host, **self._frag_kw(False))
 
     # ------------------------------------------------------------------ optimiser
     def set_hyper(self, lr, momentum=0.0, weight_decay=0.0, grad_scale=1.0, nesterov=False):
@@ -242,7 +271,7 @@ class ParamStore:
             src, cur, dst = index_stream if index_stream is not None else (None, None, None)
             native.require().sgd_multi(self._descs, self._ndesc, self._sgd_blocks, self.master, self.grad,
                                        self.momentum, self.wbf, self.hyper, True, src, cur, dst,
-                                       self._descs_host)
+                                       self._descs_host, **self._frag_kw(True))
             return
         if index_stream is not None:
             src, cur, dst = index_stream

@@ -378,6 +378,10 @@ def lenet_supported() -> bool:
     return m is not None and hasattr(m, "lenet_train")
 
 
+def lenet_frag_bytes() -> int:
+    return int(_C().lenet_frag_bytes())
+
+
 def lenet_blocks(B: int) -> int:
     return int(_C().lenet_blocks(int(B)))
 
@@ -424,7 +428,7 @@ def lenet_dense_part_floats(B: int) -> int:
 
 
 def lenet_train(x, labels, conv, dense_w, dense_wt, dense_b, conv_grads, dense_gw, dense_gb, hT, dzT, conv_part,
-                dense_part, loss_part, stats, grad_scale):
+                dense_part, loss_part, stats, grad_scale, frag=None, prep=True, snap=None, conv_mom=()):
     """Whole-network LeNet-5 training step on GPU (csrc/lenet_fused.hip, 2 launches): fills every
     gradient and ``stats`` = [loss sum, correct].  ``x``: bf16 batch [B,28,28,1] or a :class:`GatherRef`
     over a uint8 dataset; ``labels``: int32 [B] or a :class:`LabelRef` through the same indices."""
@@ -439,10 +443,14 @@ def lenet_train(x, labels, conv, dense_w, dense_wt, dense_b, conv_grads, dense_g
     else:
         lab = labels if labels.dtype == torch.int32 else labels.to(torch.int32)
     B = x.shape[0]
-    ftab, pxtab, frag = lenet_tables(stats.device)
+    ftab, pxtab, scratch = lenet_tables(stats.device)
+    # ``frag``: the fragment buffer the optimizer rebuilds (ParamStore.lenet_frag), refreshed by the prep
+    # launch only when ``prep``; None = prep into scratch.  ``snap`` [2][2550]: the reduce kernel stores the
+    # conv kernels' weights and momentum (``conv_mom``) there for the optimizer's rebuild.
     _C().lenet_train(src, idx, float(scale), lab, list(conv), list(dense_w), list(dense_wt), list(dense_b),
                      list(conv_grads), list(dense_gw), list(dense_gb), list(hT), list(dzT), conv_part, dense_part,
-                     loss_part, stats, frag, ftab, pxtab, int(B), float(grad_scale))
+                     loss_part, stats, scratch if frag is None else frag, ftab, pxtab, int(B), float(grad_scale),
+                     prep=bool(prep) or frag is None, snap=snap, conv_mom=list(conv_mom))
 
 
 def convpool_supported(H, W, C, KH, KW, pad, N) -> bool:

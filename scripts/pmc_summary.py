@@ -15,7 +15,7 @@ for d in dirs:
 cols = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
         "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_MFMA",
         "SQ_LDS_BANK_CONFLICT", "GRBM_GUI_ACTIVE", "SQ_WAIT_INST_LDS", "SQ_INSTS_SMEM", "SQ_INSTS_BRANCH",
-        "SQ_VALU_MFMA_BUSY_CYCLES", "FETCH_SIZE"]
+        "SQ_VALU_MFMA_BUSY_CYCLES", "FETCH_SIZE", "SQ_LDS_IDX_ACTIVE"]
 for k, c in sorted(vals.items()):
     print(k)
     print("   " + "  ".join(f"{n.replace('SQ_', '')}={sum(c[n]) / len(c[n]):.3g}" for n in cols if c.get(n)))

@@ -112,3 +112,51 @@ def test_fused_lenet_trains():
         losses.append(float(st[0].item()) / 512)
     assert tr.graph_mode == "full"
     assert sum(losses[-5:]) < 0.9 * sum(losses[:5]), losses
+
+
+def test_optimizer_built_fragments_match_prep():
+    """The SGD launch owns the conv-kernel updates and rebuilds the fused step's weight fragments: after
+    momentum steps they equal, bitwise, the fragments the prep kernel builds from the updated master,
+    and the master equals a store updated without the fragment workgroup."""
+    from distriflow_amd import ops
+    from distriflow_amd.models.zoo import build_model
+
+    B = 256
+    g, _ = _nets(B)
+    assert g.store.lenet_frag is not None
+    ref = build_model("lenet5", device="cuda", seed=3)
+    ref.store.lenet_frag = None
+    ref.store.set_flat(g.store.master.clone())
+    for s in (g.store, ref.store):
+        s.set_hyper(0.05, momentum=0.9, weight_decay=1e-4, grad_scale=1.0, nesterov=True)
+    x, y = _batch(B, seed=2)
+    for _ in range(3):
+        g.compute_gradients(x.cuda(), y.cuda())
+        ref.store.grad.copy_(g.store.grad)
+        g.store.sgd_step()
+        ref.store.sgd_step()
+    torch.cuda.synchronize()
+    assert torch.equal(g.store.master, ref.store.master)
+    assert torch.equal(g.store.wbf, ref.store.wbf)
+    assert g.store.lenet_state == "fresh"
+    built = g.store.lenet_frag[0].clone()
+    # prep path: frag=None -> the kernel's prep launch writes the scratch fragments from the master
+    keep = g.store.lenet_frag
+    g.store.lenet_frag = None
+    g.compute_gradients(x.cuda(), y.cuda())
+    torch.cuda.synchronize()
+    _, _, scratch = ops.lenet_tables(torch.device("cuda", 0))
+    assert torch.equal(built, scratch[: built.numel()])
+    # an update without a fused step's snapshot leaves the fragments stale: the next step preps them
+    g.store.lenet_frag = keep
+    g.store.lenet_state = "fresh"
+    g.store.sgd_step()
+    assert g.store.lenet_state == "stale"
+    g.compute_gradients(x.cuda(), y.cuda())
+    assert g.store.lenet_state == "snap"
+    keep[0].zero_()
+    g.store.refresh_compute()
+    g.store.lenet_frag = None
+    g.compute_gradients(x.cuda(), y.cuda())
+    torch.cuda.synchronize()
+    assert torch.equal(keep[0], scratch[: built.numel()])
