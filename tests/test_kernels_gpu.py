@@ -132,6 +132,8 @@ CONVS = [  # B, H, W, C, N, k, stride, pad
     (4, 28, 28, 1, 6, 5, 1, 2),
     (8, 14, 14, 6, 16, 5, 1, 0),
     (4, 28, 28, 1, 32, 3, 1, 0),
+    (5, 28, 28, 1, 32, 3, 1, 1),
+    (3, 30, 17, 1, 32, 3, 1, 0),
     (4, 26, 26, 32, 32, 3, 1, 0),
     (2, 32, 32, 3, 64, 3, 1, 1),
     (2, 16, 16, 64, 128, 3, 2, 1),
