@@ -37,10 +37,21 @@ void fill_geom(std::vector<int64_t> g, int* dst) {
   for (int i = 0; i < 9; ++i) dst[i] = (int)g[i];
 }
 
+dfa::DropSpec drop_from(double p, int64_t seed, const c10::optional<torch::Tensor>& step) {
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0,1)");
+  const long long* sp = nullptr;
+  if (step.has_value() && step->defined()) {
+    need(*step, at::kLong, "dropout step");
+    sp = reinterpret_cast<const long long*>(step->data_ptr());
+  }
+  return dfa::make_drop((float)p, (unsigned long long)seed, sp);
+}
+
 void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tensor> bias,
                   c10::optional<torch::Tensor> mask, torch::Tensor out, int64_t M, int64_t N, int64_t K, int64_t Kpad,
                   int64_t lda, int64_t ldc, std::vector<int64_t> geom, int64_t mode, bool relu, double alpha,
-                  c10::optional<torch::Tensor> res, c10::optional<torch::Tensor> resmask) {
+                  c10::optional<torch::Tensor> res, c10::optional<torch::Tensor> resmask, double drop_p,
+                  int64_t drop_seed, c10::optional<torch::Tensor> drop_step) {
   need(src, at::kBFloat16, "src");
   need(w, at::kBFloat16, "w");
   TORCH_CHECK(out.is_cuda() && out.is_contiguous(), "out must be a contiguous GPU tensor");
@@ -90,6 +101,8 @@ void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tenso
   a.relu = relu ? 1 : 0;
   a.out_f32 = out.scalar_type() == at::kFloat ? 1 : 0;
   a.alpha = (float)alpha;
+  a.drop = drop_from(drop_p, drop_seed, drop_step);
+  TORCH_CHECK(!a.drop.on || (ldc == N && !a.out_f32), "folded dropout needs a dense bf16 output (ldc == N)");
   // split-K partials for the under-filled (small-M, long-K) shapes: PyTorch's caching allocator is
   // stream ordered and graph-capture aware, so the scratch is safe to drop right after the launch
   torch::Tensor splitk;
@@ -137,12 +150,14 @@ void igemm_wgrad_py(torch::Tensor dy, torch::Tensor src, torch::Tensor gw, c10::
             "igemm_wgrad");
 }
 
-void maxpool_fwd_py(torch::Tensor x, torch::Tensor y, int64_t B, int64_t H, int64_t W, int64_t C, int64_t P) {
+void maxpool_fwd_py(torch::Tensor x, torch::Tensor y, int64_t B, int64_t H, int64_t W, int64_t C, int64_t P,
+                    double drop_p, int64_t drop_seed, c10::optional<torch::Tensor> drop_step) {
   need(x, at::kBFloat16, "x");
   need(y, at::kBFloat16, "y");
   TORCH_CHECK(P > 0 && H >= P && W >= P, "bad pool geometry");
   TORCH_CHECK(x.numel() >= B * H * W * C && y.numel() >= B * (H / P) * (W / P) * C, "pool buffers too small");
-  check_hip(dfa::maxpool_fwd((const dfa::bf16*)x.data_ptr(), (dfa::bf16*)y.data_ptr(), B, H, W, C, P, cur_stream()),
+  check_hip(dfa::maxpool_fwd((const dfa::bf16*)x.data_ptr(), (dfa::bf16*)y.data_ptr(), B, H, W, C, P, cur_stream(),
+                             drop_from(drop_p, drop_seed, drop_step)),
             "maxpool_fwd");
 }
 
@@ -204,7 +219,8 @@ void dropout_py(torch::Tensor x, torch::Tensor y, double p, int64_t seed, c10::o
 }
 
 void gather_batch_py(torch::Tensor data, c10::optional<torch::Tensor> labels, torch::Tensor idx, torch::Tensor out,
-                     c10::optional<torch::Tensor> out_labels, int64_t B, int64_t row, double scale) {
+                     c10::optional<torch::Tensor> out_labels, int64_t B, int64_t row, double scale,
+                     c10::optional<torch::Tensor> step_inc) {
   TORCH_CHECK(data.is_cuda() && data.is_contiguous(), "data must be a contiguous GPU tensor");
   const bool u8 = data.scalar_type() == at::kByte;
   TORCH_CHECK(u8 || data.scalar_type() == at::kBFloat16, "data must be uint8 or bf16");
@@ -222,7 +238,10 @@ void gather_batch_py(torch::Tensor data, c10::optional<torch::Tensor> labels, to
     olp = out_labels->data_ptr<int>();
   }
   check_hip(dfa::gather_batch(data.data_ptr(), u8 ? 1 : 0, lp, reinterpret_cast<const long long*>(idx.data_ptr<int64_t>()), (dfa::bf16*)out.data_ptr(),
-                              olp, B, row, (float)scale, (long long)data.size(0), cur_stream()),
+                              olp, B, row, (float)scale, (long long)data.size(0), cur_stream(),
+                              step_inc.has_value() && step_inc->defined()
+                                  ? reinterpret_cast<long long*>(step_inc->data_ptr<int64_t>())
+                                  : nullptr),
             "gather_batch");
 }
 
@@ -628,7 +647,8 @@ void head_train_py(std::vector<torch::Tensor> w, std::vector<c10::optional<torch
                    std::vector<torch::Tensor> dzT, std::vector<int64_t> K, std::vector<int64_t> N, torch::Tensor x,
                    bool x_relu, torch::Tensor xT, c10::optional<torch::Tensor> dx,
                    c10::optional<torch::Tensor> logits, torch::Tensor labels, c10::optional<torch::Tensor> idx,
-                   double grad_scale, torch::Tensor loss_part, torch::Tensor stats, int64_t phases) {
+                   double grad_scale, torch::Tensor loss_part, torch::Tensor stats, int64_t phases,
+                   double dx_scale) {
   const int nl = (int)w.size();
   TORCH_CHECK(phases >= 1 && phases <= 3, "head: phases must be 1, 2 or 3");
   TORCH_CHECK(nl >= 1 && nl <= dfa::kHeadMaxLayers, "head: 1..", dfa::kHeadMaxLayers, " layers");
@@ -722,6 +742,7 @@ void head_train_py(std::vector<torch::Tensor> w, std::vector<c10::optional<torch
   TORCH_CHECK(stats.numel() >= 2, "head: stats must hold 2 floats");
   a.stats = stats.data_ptr<float>();
   TORCH_CHECK(dfa::head_train_lds(a) <= 160 * 1024, "head: LDS footprint too large");
+  a.dx_scale = (float)dx_scale;
   check_hip(dfa::head_train(a, (int)phases, cur_stream()), "head_train");
 }
 
@@ -1168,13 +1189,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("igemm_fwd", &igemm_fwd_py, "implicit-GEMM MFMA (dense/conv fwd, dgrad)", py::arg("src"), py::arg("w"),
         py::arg("bias"), py::arg("mask"), py::arg("out"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("Kpad"),
         py::arg("lda"), py::arg("ldc"), py::arg("geom"), py::arg("mode"), py::arg("relu"), py::arg("alpha"),
-        py::arg("res") = py::none(), py::arg("resmask") = py::none());
+        py::arg("res") = py::none(), py::arg("resmask") = py::none(), py::arg("drop_p") = 0.0,
+        py::arg("drop_seed") = 0, py::arg("drop_step") = py::none());
   m.def("igemm_wgrad", &igemm_wgrad_py, "implicit-GEMM MFMA weight gradient (split-m slabs + reduce)");
-  m.def("maxpool_fwd", &maxpool_fwd_py);
+  m.def("maxpool_fwd", &maxpool_fwd_py, py::arg("x"), py::arg("y"), py::arg("B"), py::arg("H"), py::arg("W"),
+        py::arg("C"), py::arg("P"), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0,
+        py::arg("drop_step") = py::none());
   m.def("maxpool_bwd", &maxpool_bwd_py);
   m.def("softmax_ce", &softmax_ce_py);
   m.def("dropout", &dropout_py);
-  m.def("gather_batch", &gather_batch_py);
+  m.def("gather_batch", &gather_batch_py, py::arg("data"), py::arg("labels"), py::arg("idx"), py::arg("out"),
+        py::arg("out_labels"), py::arg("B"), py::arg("row"), py::arg("scale"), py::arg("step_inc") = py::none());
   m.def("add_act", &add_act_py);
   m.def("relu_bwd", &relu_bwd_py);
   m.def("gap_fwd", &gap_fwd_py);
@@ -1222,7 +1247,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return std::make_tuple(pair, K2pad);
   }, "data-gradient weight layout of the fused conv+pool kernel: (pair, row length K2pad)");
   m.def("convpool_supported", &convpool_supported_py);
-  m.def("head_train", &head_train_py, "fused dense head: forward + softmax-CE + backward (2 launches)");
+  m.def("head_train", &head_train_py, "fused dense head: forward + softmax-CE + backward (2 launches)",
+        py::arg("w"), py::arg("wt"), py::arg("b"), py::arg("gw"), py::arg("gb"), py::arg("hT"), py::arg("dzT"),
+        py::arg("K"), py::arg("N"), py::arg("x"), py::arg("x_relu"), py::arg("xT"), py::arg("dx"), py::arg("logits"),
+        py::arg("labels"), py::arg("idx"), py::arg("grad_scale"), py::arg("loss_part"), py::arg("stats"),
+        py::arg("phases"), py::arg("dx_scale") = 1.0);
   m.def("classifier_metrics", &classifier_metrics_py, "[loss sum, correct] of a classifier batch (one launch)");
   m.def("lenet_train", &lenet_train_py, "whole-network LeNet-5 training step (fwd + CE + bwd, 2 launches)",
         py::arg("x"), py::arg("idx"), py::arg("scale"), py::arg("labels"), py::arg("conv"), py::arg("dense_w"),

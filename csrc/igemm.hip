@@ -530,9 +530,22 @@ static hipError_t launch_fwd_mode(const IGemmArgs& a, hipStream_t st) {
   return launch_fwd_cfg<128, 128, 2, 2, MODE, VEC>(a, st);
 }
 
+static hipError_t igemm_fwd_nodrop(const IGemmArgs& a, int mode, hipStream_t st);
+
 hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0) return hipSuccess;
-  if (igemm64_supported(a, mode)) return igemm64(a, mode, st);
+  if (a.drop.on && (a.out_f32 || a.ldc != a.N)) return hipErrorInvalidValue;
+  if (a.pool_code) return igemm64_pool_supported(a) && mode == MODE_FWD ? igemm64(a, mode, st) : hipErrorInvalidValue;
+  if (igemm64_supported(a, mode)) return igemm64(a, mode, st);  // dropout in its epilogues
+  if (!a.drop.on) return igemm_fwd_nodrop(a, mode, st);
+  IGemmArgs b = a;
+  b.drop = DropSpec{};
+  DFA_HIP_CHECK(igemm_fwd_nodrop(b, mode, st));
+  bf16* o = reinterpret_cast<bf16*>(a.out);
+  return dropout(o, o, nullptr, (long long)a.M * a.N, a.drop.p, a.drop.seed, a.drop.step, st);
+}
+
+static hipError_t igemm_fwd_nodrop(const IGemmArgs& a, int mode, hipStream_t st) {
   if (smallc_fwd_supported(a, mode)) return smallc_fwd(a, st);
   const bool aligned = ((uintptr_t)a.src & 15) == 0;
   if (mode == MODE_DIRECT) {

@@ -52,8 +52,14 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chu
 template <int BM, int BN>
 constexpr int igemm64_occ() { return (160 * 1024) / ((BM + BN) * 256) > 4 ? 4 : (160 * 1024) / ((BM + BN) * 256); }
 
-template <int BM, int BN, int MODE, int D, bool SPLIT>
+// POOL (conv forward + 2x2 max-pool, the Keras CNN's conv2 -> pool): output rows are taken in
+// pool-window-major order, m = (b, window, position), so the four pixels of a window are rows 4q..4q+3
+// of a 16-row MFMA block, i.e. four adjacent lanes; the epilogue reduces them with two lane shuffles
+// and writes only the pooled map [M/4][N] and a 1-byte argmax code per pooled element (4 = no
+// gradient: the ReLU'd max is 0).  d_ow then divides by the pooled width.
+template <int BM, int BN, int MODE, int D, bool SPLIT, bool POOL = false>
 __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(IGemmArgs a, FastDiv d_ow, FastDiv d_ohw) {
+  static_assert(!POOL || (MODE == MODE_FWD && !SPLIT), "pooled epilogue: plain conv forward only");
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / (WM * 16), TN = BN / (WN * 16);
   constexpr int AP = BM / 32, BP = BN / 32;  // 16-byte chunks per thread and step (8 chunks per 64-deep row)
@@ -94,8 +100,16 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
     } else {
       const unsigned b = fdiv(mm, d_ohw);
       const unsigned rem = mm - b * (unsigned)(a.OH * a.OW);
-      const unsigned oh = fdiv(rem, d_ow);
-      const int ow = (int)(rem - oh * (unsigned)a.OW);
+      unsigned oh;
+      int ow;
+      if (POOL) {  // rem = 4 * (ph * OW/2 + pw) + 2 * dy + dx
+        const unsigned win = rem >> 2, ph = fdiv(win, d_ow);
+        oh = 2 * ph + ((rem >> 1) & 1);
+        ow = 2 * (int)(win - ph * (unsigned)(a.OW >> 1)) + (int)(rem & 1);
+      } else {
+        oh = fdiv(rem, d_ow);
+        ow = (int)(rem - oh * (unsigned)a.OW);
+      }
       rbase[i] = (long long)b * a.SH * a.SW * a.SC;
       if (MODE == MODE_FWD) {
         rh[i] = (int)oh * a.stride - a.pad;
@@ -263,6 +277,52 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
     return;
   }
 
+  if (POOL) {
+    typedef __bf16 bf16x4_p __attribute__((ext_vector_type(4)));
+    const unsigned long long dseed = a.drop.on ? drop_seed(a.drop.seed, a.drop.step) : 0ull;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = m0 + wm * TM * 16 + i * 16 + fr;  // the window's rows are lanes fr & ~3 .. + 3
+      const long long prow = row >> 2;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col0 = n0 + wn * TN * 16 + j * 16 + fq * 4;
+        float mx[4];
+        int pc[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // the conv output as the unfused path stored it (bf16), then the first max of the window
+          const float v = (float)f2bf(acc[i][j][r] * a.alpha + ((a.bias && col0 + r < a.N) ? a.bias[col0 + r] : 0.f));
+          float m = fmaxf(v, __shfl_xor(v, 1));
+          m = fmaxf(m, __shfl_xor(m, 2));
+          int p = v == m ? (fr & 3) : 4;
+          p = min(p, __shfl_xor(p, 1));
+          p = min(p, __shfl_xor(p, 2));
+          mx[r] = m;
+          pc[r] = p;
+        }
+        if ((fr & 3) || row >= a.M || col0 >= a.N) continue;
+        bf16x4_p ov;
+        unsigned codes = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float o = mx[r];
+          int cd = pc[r];
+          if (a.relu) {
+            if (!(o > 0.f)) cd = 4;
+            o = fmaxf(o, 0.f);
+          }
+          if (a.drop.on) o = drop_keep(dseed, a.drop.thresh, prow * a.N + col0 + r) ? (float)f2bf(o) * a.drop.scale : 0.f;
+          ov[r] = f2bf(o);
+          codes |= (unsigned)cd << (8 * r);
+        }
+        *reinterpret_cast<bf16x4_p*>(reinterpret_cast<bf16*>(a.out) + prow * a.ldc + col0) = ov;
+        *reinterpret_cast<unsigned*>(a.pool_code + prow * a.N + col0) = codes;
+      }
+    }
+    return;
+  }
+
   // epilogue.  The weights are the MFMA's A operand, so the 16x16 C/D layout puts 4 consecutive output
   // COLUMNS (n = 4 * (lane >> 4) + r) of one output row (m = lane & 15) in a lane: every lane moves
   // one 8-byte bf16x4 (16-byte f32x4) store and 8-byte residual / mask loads instead of four 2-byte ones.
@@ -300,6 +360,11 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
           for (int r = 0; r < 4; ++r)
             if (!((float)mk[r] > 0.f)) v[r] = 0.f;
         }
+        if (a.drop.on) {
+          const unsigned long long ds = drop_seed(a.drop.seed, a.drop.step);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = drop_keep(ds, a.drop.thresh, o + r) ? (float)f2bf(v[r]) * a.drop.scale : 0.f;
+        }
         if (a.out_f32) {
           *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
         } else {
@@ -320,6 +385,8 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
         }
         if (a.relu) x = fmaxf(x, 0.f);
         if (a.mask && !((float)a.mask[o + r] > 0.f)) x = 0.f;
+        if (a.drop.on)
+          x = drop_keep(drop_seed(a.drop.seed, a.drop.step), a.drop.thresh, o + r) ? (float)f2bf(x) * a.drop.scale : 0.f;
         if (a.out_f32)
           reinterpret_cast<float*>(a.out)[o + r] = x;
         else
@@ -329,6 +396,7 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
   }
 }
 
+// (a folded dropout rounds the activation to bf16 before scaling, as the standalone pass saw it)
 // split-K combine: out = epi(sum_s ws[s]) in a fixed split order (deterministic), 4 columns per thread
 __global__ void __launch_bounds__(256) igemm64_splitk_epilogue_kernel(IGemmArgs a) {
   typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
@@ -361,6 +429,11 @@ __global__ void __launch_bounds__(256) igemm64_splitk_epilogue_kernel(IGemmArgs 
       for (int r = 0; r < 4; ++r)
         if (!((float)mk[r] > 0.f)) v[r] = 0.f;
     }
+    if (a.drop.on) {
+      const unsigned long long ds = drop_seed(a.drop.seed, a.drop.step);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = drop_keep(ds, a.drop.thresh, o + r) ? (float)f2bf(v[r]) * a.drop.scale : 0.f;
+    }
     if (a.out_f32) {
       *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
     } else {
@@ -376,12 +449,16 @@ __global__ void __launch_bounds__(256) igemm64_splitk_epilogue_kernel(IGemmArgs 
 // M = B*8*8 or B*4*4 with K up to 4608) leave one wave per SIMD waiting on every step
 template <int BM, int BN>
 static int splitk_for(const IGemmArgs& a) {
+  if (a.pool_code) return 1;
   const long long tiles = (long long)cdiv(a.M, BM) * cdiv(a.N, BN);
   const int nk = cdiv(a.K, 64);
   if (a.N % 4 || a.ldc % 4 || tiles >= 512 || nk < 32) return 1;
   if (((uintptr_t)a.out & 15) || (((uintptr_t)a.res | (uintptr_t)a.resmask | (uintptr_t)a.mask) & 7)) return 1;
   int s = 1;
   while (s < 4 && tiles * s * 2 <= 1024 && nk / (s * 2) >= 16) s *= 2;
+  // severely under-filled (the Keras CNN's 9216 -> 128 dense: 16 tiles): up to 16 splits of >= 4 steps
+  if (tiles * s < 256)
+    while (s < 16 && tiles * s * 2 <= 512 && nk / (s * 2) >= 4) s *= 2;
   return s;
 }
 
@@ -390,6 +467,11 @@ hipError_t launch64(IGemmArgs a, hipStream_t st) {
   const FastDiv d_ow = make_fastdiv((unsigned)max(a.OW, 1)), d_ohw = make_fastdiv((unsigned)max(a.OH * a.OW, 1));
   const int blocks = cdiv(a.M, BM) * cdiv(a.N, BN);
   constexpr int D = kIgemm64Stages;
+  if (MODE == MODE_FWD && a.pool_code != nullptr) {
+    hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE_FWD, D, false, true>), dim3(blocks), dim3(256), 0, st, a,
+                       make_fastdiv((unsigned)max(a.OW / 2, 1)), d_ohw);
+    return hipGetLastError();
+  }
   const int s = a.splitk_ws ? splitk_for<BM, BN>(a) : 1;
   if (s > 1) {
     a.splits = s;
@@ -422,6 +504,11 @@ long long igemm64_splitk_floats(const IGemmArgs& a, int mode) {
   if ((long long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 512) return 0;  // 128 x 128 tiles: already filled
   const int s = splitk_for<64, 128>(a);
   return s > 1 ? (long long)s * a.M * a.N : 0;
+}
+
+bool igemm64_pool_supported(const IGemmArgs& a) {
+  return igemm64_supported(a, MODE_FWD) && a.OH % 2 == 0 && a.OW % 2 == 0 && a.N % 4 == 0 && a.ldc == a.N &&
+         !a.out_f32 && !a.mask && !a.res && ((uintptr_t)a.out & 7) == 0 && ((uintptr_t)a.pool_code & 3) == 0;
 }
 
 bool igemm64_supported(const IGemmArgs& a, int mode) {

@@ -13,6 +13,28 @@ namespace dfa {
 
 enum { MODE_DIRECT = 0, MODE_FWD = 1, MODE_DGRAD = 2 };
 
+// Dropout folded into a producer's epilogue (same mask as csrc/layers.hip dropout_kernel: element i of
+// the produced tensor is kept when hash(seed ^ step * 0x9E3779B1, i) >= thresh, kept values * scale)
+struct DropSpec {
+  int on;
+  unsigned thresh;  // p * 2^32
+  float p, scale;   // scale = 1 / (1 - p)
+  unsigned long long seed;
+  const long long* step;  // device step counter (nullable)
+};
+inline DropSpec make_drop(float p, unsigned long long seed, const long long* step) {
+  DropSpec d{};
+  if (p > 0.f) {
+    d.on = 1;
+    d.thresh = (unsigned)((double)p * 4294967296.0);
+    d.p = p;
+    d.scale = 1.f / (1.f - p);
+    d.seed = seed;
+    d.step = step;
+  }
+  return d;
+}
+
 struct IGemmArgs {
   const bf16* src;   // A source: [M][lda] (direct) or NHWC [B][SH][SW][SC] (conv gathers)
   const bf16* w;     // [Npad16][Kpad32] bf16, zero padded
@@ -27,6 +49,8 @@ struct IGemmArgs {
   float alpha;
   float* splitk_ws;  // igemm64 split-K partials [splits][M][N] (nullptr: no split)
   int splits;
+  DropSpec drop;     // dropout after the activation (requires ldc == N, bf16 out)
+  uint8_t* pool_code;  // conv forward + 2x2 max-pool (igemm64 POOL): out = pooled [M/4][N], code [M/4][N]
 };
 
 struct WgradArgs {
@@ -61,6 +85,9 @@ struct ParamDescTable {
 hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st);
 // 64-deep-step variant for the vectorizable cases (csrc/igemm64.hip); igemm_fwd dispatches to it
 bool igemm64_supported(const IGemmArgs& a, int mode);
+bool igemm64_pool_supported(const IGemmArgs& a);
+// dY of a pooled conv from the pooled gradient and the argmax codes (NHWC, 2x2 windows)
+hipError_t unpool2(const bf16* dyp, const uint8_t* code, bf16* dy, int B, int OH, int OW, int N, hipStream_t st);
 hipError_t igemm64(const IGemmArgs& a, int mode, hipStream_t st);
 // fp32 floats of split-K workspace igemm64 wants for this problem (0: no split); the caller allocates
 // them and passes the buffer in IGemmArgs::splitk_ws
@@ -69,7 +96,8 @@ hipError_t igemm_wgrad(const WgradArgs& a, int mode, float* workspace, size_t ws
 // conv weight gradient with transposed LDS reads (csrc/wgrad_tr.hip): conv, C % 8 == 0, no bias
 bool wgrad_tr_supported(const WgradArgs& a, int mode);
 hipError_t wgrad_tr(const WgradArgs& a, float* workspace, size_t ws_floats, hipStream_t st);
-hipError_t maxpool_fwd(const bf16* x, bf16* y, int B, int H, int W, int C, int P, hipStream_t st);
+hipError_t maxpool_fwd(const bf16* x, bf16* y, int B, int H, int W, int C, int P, hipStream_t st,
+                       DropSpec drop = DropSpec{});
 hipError_t maxpool_bwd(const bf16* x, const bf16* dy, bf16* dx, int B, int H, int W, int C, int P, int relu_fused,
                        hipStream_t st);
 hipError_t softmax_ce(const float* logits, const int* labels, bf16* dlogits, float* stats, int B, int C, int ldl,
@@ -77,7 +105,8 @@ hipError_t softmax_ce(const float* logits, const int* labels, bf16* dlogits, flo
 hipError_t dropout(const bf16* x, bf16* y, const bf16* mask, long long n, float p, unsigned long long seed,
                    const long long* step, hipStream_t st);
 hipError_t gather_batch(const void* data, int data_is_u8, const int* labels, const long long* idx, bf16* out,
-                        int* out_labels, int B, int row, float scale, long long nrows, hipStream_t st);
+                        int* out_labels, int B, int row, float scale, long long nrows, hipStream_t st,
+                        long long* step_inc = nullptr);
 hipError_t gather_labels(const int* labels, const long long* idx, int* out, int B, long long nrows, hipStream_t st);
 hipError_t add_act(const bf16* a, const bf16* b, bf16* out, long long n, int relu, hipStream_t st);
 hipError_t relu_bwd(const bf16* y, const bf16* dy, bf16* dx, long long n, hipStream_t st);
@@ -160,6 +189,7 @@ struct HeadArgs {
   const long long* idx;
   long long nrows;
   float grad_scale;     // d(loss)/d(logit) scale, 1/B for the mean
+  float dx_scale;       // extra dX scale (a folded dropout's 1/(1-p); 0 = 1)
   float* loss_part;     // [nblocks][2]
   float* stats;         // [2] = (loss sum, correct)
   unsigned long long* stamps;  // profiling aid (head_set_stamps): per-block phase clocks, or null

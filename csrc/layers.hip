@@ -17,7 +17,8 @@ namespace dfa {
 // MaxPool (pool == stride, 'valid'), NHWC bf16.  One thread per (output pixel, 8-channel chunk).
 template <bool VEC>
 __global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int B, int H, int W,
-                                   int C, int OH, int OW, int P) {
+                                   int C, int OH, int OW, int P, DropSpec drop) {
+  const unsigned long long ds = drop.on ? drop_seed(drop.seed, drop.step) : 0ull;
   const int CC = VEC ? C / 8 : C;
   const long long total = (long long)B * OH * OW * CC;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -40,12 +41,17 @@ __global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict_
         }
       bf16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(m[j]);
+      for (int j = 0; j < 8; ++j) {
+        // folded dropout: the pooled value rounds to bf16 first, as the standalone dropout saw it
+        if (drop.on) m[j] = drop_keep(ds, drop.thresh, i * 8 + j) ? (float)f2bf(m[j]) * drop.scale : 0.f;
+        o[j] = f2bf(m[j]);
+      }
       *reinterpret_cast<bf16x8*>(y + i * 8) = o;
     } else {
       float m = -INFINITY;
       for (int ph = 0; ph < P; ++ph)
         for (int pw = 0; pw < P; ++pw) m = fmaxf(m, (float)base[((long long)ph * W + pw) * C + cc]);
+      if (drop.on) m = drop_keep(ds, drop.thresh, i) ? (float)f2bf(m) * drop.scale : 0.f;
       y[i] = f2bf(m);
     }
   }
@@ -111,6 +117,38 @@ __global__ void maxpool_bwd_kernel(const bf16* __restrict__ x, const bf16* __res
   }
 }
 
+// dY of a conv whose 2x2 max-pool was fused into its forward epilogue (igemm64 POOL): every pooled
+// gradient goes to the window position its code names (code 4 = none: the ReLU'd max was 0).
+// One thread per (pooled pixel, 8 channels): a 16-byte gradient load, an 8-byte code load, four
+// 16-byte stores.
+__global__ void unpool2_kernel(const bf16* __restrict__ dyp, const uint8_t* __restrict__ code, bf16* __restrict__ dy,
+                               int B, int OH, int OW, int N) {
+  const int PH = OH / 2, PW = OW / 2, NC = N / 8;
+  const long long total = (long long)B * PH * PW * NC;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % NC);
+    const long long prow = i / NC;
+    const int pw = (int)(prow % PW);
+    const long long t = prow / PW;
+    const int ph = (int)(t % PH);
+    const long long b = t / PH;
+    const bf16x8 g = *reinterpret_cast<const bf16x8*>(dyp + prow * N + cc * 8);
+    const uint2 cw = *reinterpret_cast<const uint2*>(code + prow * N + cc * 8);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned cd = ((j < 4 ? cw.x : cw.y) >> (8 * (j & 3))) & 0xff;
+        o[j] = cd == (unsigned)p ? g[j] : (bf16)0.f;
+      }
+      const long long px = (b * OH + 2 * ph + (p >> 1)) * OW + 2 * pw + (p & 1);
+      *reinterpret_cast<bf16x8*>(dy + px * N + cc * 8) = o;
+    }
+  }
+}
+
 static int grid_for(long long total, int block = 256) {
   long long g = (total + block - 1) / block;
   if (g > 8192) g = 8192;
@@ -118,15 +156,25 @@ static int grid_for(long long total, int block = 256) {
   return (int)g;
 }
 
-hipError_t maxpool_fwd(const bf16* x, bf16* y, int B, int H, int W, int C, int P, hipStream_t st) {
+hipError_t maxpool_fwd(const bf16* x, bf16* y, int B, int H, int W, int C, int P, hipStream_t st, DropSpec drop) {
   const int OH = H / P, OW = W / P;
   const bool vec = C % 8 == 0;
   const long long total = (long long)B * OH * OW * (vec ? C / 8 : C);
   if (total == 0) return hipSuccess;
   if (vec)
-    hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(grid_for(total)), dim3(256), 0, st, x, y, B, H, W, C, OH, OW, P);
+    hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(grid_for(total)), dim3(256), 0, st, x, y, B, H, W, C, OH, OW, P,
+                       drop);
   else
-    hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3(grid_for(total)), dim3(256), 0, st, x, y, B, H, W, C, OH, OW, P);
+    hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3(grid_for(total)), dim3(256), 0, st, x, y, B, H, W, C, OH, OW,
+                       P, drop);
+  return hipGetLastError();
+}
+
+hipError_t unpool2(const bf16* dyp, const uint8_t* code, bf16* dy, int B, int OH, int OW, int N, hipStream_t st) {
+  if (OH % 2 || OW % 2 || N % 8) return hipErrorInvalidValue;
+  const long long total = (long long)B * (OH / 2) * (OW / 2) * (N / 8);
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(unpool2_kernel, dim3(grid_for(total)), dim3(256), 0, st, dyp, code, dy, B, OH, OW, N);
   return hipGetLastError();
 }
 
@@ -284,7 +332,10 @@ __device__ __forceinline__ long long clamp_row(long long r, long long nrows) {
 
 template <typename T>
 __global__ void gather_rows_kernel(const T* __restrict__ data, const long long* __restrict__ idx,
-                                   bf16* __restrict__ out, int B, int row, float scale, long long nrows) {
+                                   bf16* __restrict__ out, int B, int row, float scale, long long nrows,
+                                   long long* __restrict__ step_inc) {
+  // the step's first launch advances the device step counter (dropout masks of the step read it)
+  if (step_inc && blockIdx.x == 0 && threadIdx.x == 0) step_inc[0] += 1;
   const int per = row;  // elements per row
   const long long total = (long long)B * per;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -296,7 +347,9 @@ __global__ void gather_rows_kernel(const T* __restrict__ data, const long long* 
 }
 
 __global__ void gather_rows_bf16_vec_kernel(const bf16* __restrict__ data, const long long* __restrict__ idx,
-                                            bf16* __restrict__ out, int B, int row8, long long nrows) {
+                                            bf16* __restrict__ out, int B, int row8, long long nrows,
+                                            long long* __restrict__ step_inc) {
+  if (step_inc && blockIdx.x == 0 && threadIdx.x == 0) step_inc[0] += 1;
   const long long total = (long long)B * row8;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -313,18 +366,19 @@ __global__ void gather_labels_kernel(const int* __restrict__ labels, const long 
 }
 
 hipError_t gather_batch(const void* data, int data_is_u8, const int* labels, const long long* idx, bf16* out,
-                        int* out_labels, int B, int row, float scale, long long nrows, hipStream_t st) {
+                        int* out_labels, int B, int row, float scale, long long nrows, hipStream_t st,
+                        long long* step_inc) {
   if (B <= 0) return hipSuccess;
   const long long total = (long long)B * row;
   if (data_is_u8) {
     hipLaunchKernelGGL(gather_rows_kernel<uint8_t>, dim3(grid_for(total)), dim3(256), 0, st,
-                       (const uint8_t*)data, idx, out, B, row, scale, nrows);
+                       (const uint8_t*)data, idx, out, B, row, scale, nrows, step_inc);
   } else if (row % 8 == 0 && scale == 1.f) {
     hipLaunchKernelGGL(gather_rows_bf16_vec_kernel, dim3(grid_for(total / 8)), dim3(256), 0, st, (const bf16*)data,
-                       idx, out, B, row / 8, nrows);
+                       idx, out, B, row / 8, nrows, step_inc);
   } else {
     hipLaunchKernelGGL(gather_rows_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16*)data, idx,
-                       out, B, row, scale, nrows);
+                       out, B, row, scale, nrows, step_inc);
   }
   DFA_HIP_CHECK(hipGetLastError());
   if (labels && out_labels) {

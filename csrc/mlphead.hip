@@ -90,7 +90,8 @@ __device__ __forceinline__ void head_gemm_fwd(const bf16* A, int lda, const bf16
 template <int KSMAX>
 __device__ __forceinline__ void head_gemm_bwd(const bf16* dZ, int ldz, const bf16* __restrict__ Wt, int ldwt, int K,
                                               const bf16* mask, int ldm, bf16* out, int ldo, bf16* __restrict__ gout,
-                                              int ldg, bf16* __restrict__ gT, int ldt, int r0, int rows) {
+                                              int ldg, bf16* __restrict__ gT, int ldt, int r0, int rows,
+                                              float scale = 1.f) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int ks = ldwt / 32;
   const int ktiles = (K + 15) / 16;
@@ -114,6 +115,7 @@ __device__ __forceinline__ void head_gemm_bwd(const bf16* dZ, int ldz, const bf1
       v[r] = acc[r];
       if (mask && !((float)mask[row * ldm + j] > 0.f)) v[r] = 0.f;
       if (j >= K) v[r] = 0.f;
+      if (scale != 1.f) v[r] = (float)f2bf(v[r]) * scale;  // a folded dropout's 1/(1-p)
       if (out) out[row * ldo + j] = f2bf(v[r]);
       if (gout && j < K && row < rows) gout[(long long)(r0 + row) * ldg + j] = f2bf(v[r]);
     }
@@ -271,7 +273,7 @@ __global__ void __launch_bounds__(1024) head_train_kernel(HeadArgs a) {
       if (l == 0) {
         if (a.dx)
           head_gemm_bwd<4>(dzs[0], ld[0], L.wt, L.ldwt, L.K, a.x_relu ? xs : nullptr, ldx, nullptr, 0, a.dx, L.K,
-                           nullptr, 0, r0, rows);
+                           nullptr, 0, r0, rows, a.dx_scale != 0.f ? a.dx_scale : 1.f);
       } else {
         const int lp = l > 0 ? l - 1 : 0;
         head_gemm_bwd<4>(dzs[l], ld[l], L.wt, L.ldwt, L.K, hs[lp], ld[lp], dzs[lp], ld[lp], nullptr, 0, a.L[lp].dzT,

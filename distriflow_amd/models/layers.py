@@ -34,6 +34,10 @@ class Layer:
         self.out_shape: tuple = ()
         self.relu = False          # output passed through a fused ReLU
         self.in_relu = False       # input is a ReLU output (apply relu' in backward)
+        # a Dropout that follows this layer, folded into its forward epilogue (Net._fold_dropout); the
+        # consumer then applies the dropout backward: relu'(its input) * dx_scale = keep / (1 - p)
+        self.drop: Optional["Dropout"] = None
+        self.dx_scale = 1.0
         self.need_dx = True
         self.store = None
         self.x: Optional[torch.Tensor] = None
@@ -76,6 +80,12 @@ class Layer:
 
     def config(self) -> dict:
         return {}
+
+    def drop_spec(self, training: bool):
+        d = self.drop
+        if d is None or not training or d.rate <= 0:
+            return None
+        return d.spec()
 
 
 class Dense(Layer):
@@ -124,7 +134,8 @@ class Dense(Layer):
         xf = x.reshape(x.shape[0], self.in_features)
         st = self.store
         b = st[f"{self.name}/bias"] if self.use_bias else None
-        ops.dense_fwd(xf, st.weight(f"{self.name}/kernel"), b, self.out, relu=self.relu)
+        ops.dense_fwd(xf, st.weight(f"{self.name}/kernel"), b, self.out, relu=self.relu,
+                      drop=self.drop_spec(training))
         return self.out
 
     def backward(self, dy):
@@ -137,7 +148,7 @@ class Dense(Layer):
             return None
         dxf = self.dx.view(self.dx.shape[0], self.in_features)
         mask = self.x.reshape(dxf.shape) if self.in_relu else None
-        ops.dense_dgrad(dy, st.weight(kn), st.weight_t(kn), dxf, mask=mask)
+        ops.dense_dgrad(dy, st.weight(kn), st.weight_t(kn), dxf, mask=mask, alpha=self.dx_scale)
         return self.dx
 
     def config(self):
@@ -248,7 +259,7 @@ class MaxPooling2D(Layer):
 
     def forward(self, x, training):
         self.x = x
-        ops.maxpool_fwd(x, self.out, self.p)
+        ops.maxpool_fwd(x, self.out, self.p, drop=self.drop_spec(training))
         return self.out
 
     def backward(self, dy):
@@ -273,6 +284,10 @@ class Dropout(Layer):
 
     def _seed(self):
         return (self.base_seed * 1000003 + zlib.crc32(self.name.encode()) % 100003) & 0x7FFFFFFFFFFF
+
+    def spec(self):
+        """(rate, seed, device step) of the mask, for a producer that folds this dropout in."""
+        return (self.rate, self._seed(), self.step_dev)
 
     def forward(self, x, training):
         self.x = x

@@ -12,6 +12,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Callable, Optional
 
+import os
+
 import torch
 
 from .. import ops
@@ -59,9 +61,11 @@ class Net:
         self.step_dev = torch.zeros((), dtype=torch.int64, device=self.device)
         self.has_dropout = False
         for l in self._all_leaf_layers():
-            if isinstance(l, Dropout):
-                l.step_dev = self.step_dev
-                self.has_dropout = True
+            for d in (l, l.drop):
+                if isinstance(d, Dropout):
+                    d.step_dev = self.step_dev
+                    self.has_dropout = True
+        self._gather_step = None  # dropout step counter advanced by the step's gather launch
         self._bound_B = None
         self.graphs: dict = {}
         # side streams for weight gradients that run concurrently with the data-gradient chain
@@ -113,6 +117,8 @@ class Net:
         for j, l in enumerate(execd):
             l.need_dx = j > 0
             l.in_relu = j > 0 and execd[j - 1].relu
+        if self.fuse and self.is_gpu and os.environ.get("DISTRIFLOW_FOLD_DROPOUT", "1") != "0":
+            execd = self._fold_dropout(execd)
         self.exec_layers = execd
         self.output_shape = shape
         self.head_start = self._plan_head(execd) if self.fuse else None
@@ -146,17 +152,47 @@ class Net:
         <= 16 classes, hidden widths <= 256, input width a multiple of 8 and <= 1024."""
         if not self.is_gpu or not ops.head_supported():
             return None
-        j = len(execd)
-        while j > 0 and isinstance(execd[j - 1], Dense) and len(execd) - j < 4:
-            j -= 1
-        head = execd[j:]
-        if not head or head[-1].units > 16 or head[-1].relu:
-            return None
-        if any(not l.relu for l in head[:-1]) or any(l.units > 256 for l in head[:-1]):
-            return None
-        if head[0].in_features % 8 or head[0].in_features > 1024:
-            return None
-        return j
+        j0 = len(execd)
+        while j0 > 0 and isinstance(execd[j0 - 1], Dense) and len(execd) - j0 < 4:
+            j0 -= 1
+        for j in range(j0, len(execd)):  # the longest trailing chain the head kernels can take
+            head = execd[j:]
+            if head[-1].units > 16 or head[-1].relu:
+                return None
+            if any(not l.relu for l in head[:-1]) or any(l.units > 256 for l in head[:-1]):
+                continue
+            if any(l.drop is not None for l in head):  # a folded dropout inside the chain
+                continue
+            if head[0].in_features % 8 or head[0].in_features > 1024:
+                continue
+            return j
+        return None
+
+    @staticmethod
+    def _fold_dropout(execd):
+        """Fold each Dropout into its producer's epilogue (Dense+ReLU: igemm epilogues; MaxPooling2D over
+        a ReLU output: the pool kernel) when a Dense consumes it.  Forward: the producer writes
+        x * keep / (1 - p).  Backward: the kept elements are exactly those where the folded output is
+        > 0 (the producer's output is a ReLU output), so the consumer's data gradient takes relu' of its
+        own input plus the 1/(1-p) scale, and no dropout launch remains in either direction."""
+        out = []
+        i = 0
+        while i < len(execd):
+            l = execd[i]
+            prev = out[-1] if out else None
+            nxt = execd[i + 1] if i + 1 < len(execd) else None
+            if (isinstance(l, Dropout) and l.rate > 0 and prev is not None and prev.drop is None
+                    and isinstance(nxt, Dense)
+                    and ((isinstance(prev, Dense) and prev.relu and not prev.out_f32)
+                         or (isinstance(prev, MaxPooling2D) and prev.in_relu))):
+                prev.drop = l
+                nxt.in_relu = True
+                nxt.dx_scale = 1.0 / (1.0 - l.rate)
+                i += 1
+                continue
+            out.append(l)
+            i += 1
+        return out
 
     @staticmethod
     def _fuse_conv_pool(execd):
@@ -222,11 +258,15 @@ class Net:
         :class:`ops.GatherRef` (rows of the HBM dataset; fused into the first layer when it can)."""
         self.bind(x.shape[0])
         if isinstance(x, ops.GatherRef) and not isinstance(self.exec_layers[0], FusedConvPool):
-            x = x.materialise(self.x_buf)
+            x = x.materialise(self.x_buf, step_inc=self._take_gather_step())
         h = x
         for l in self.exec_layers:
             h = l.forward(h, training)
         return h
+
+    def _take_gather_step(self):
+        s, self._gather_step = self._gather_step, None
+        return s
 
     def backward(self, dlogits: torch.Tensor, grad_ready: Optional[Callable[[int], None]] = None):
         """Backprop dlogits; fills ``store.grad``.  ``grad_ready(i)`` fires after layer i's grads are final
@@ -249,7 +289,11 @@ class Net:
         if not isinstance(x, ops.GatherRef) and x.dtype != self.dtype:
             x = x.to(self.dtype)
         if self.has_dropout:
-            self.step_dev.add_(1)
+            if (self.is_gpu and isinstance(x, ops.GatherRef) and not self.lenet_fused
+                    and not isinstance(self.exec_layers[0], FusedConvPool)):
+                self._gather_step = self.step_dev  # advanced by the gather launch (no extra kernel)
+            else:
+                self.step_dev.add_(1)
         if self.lenet_fused:
             return self._compute_gradients_lenet(x, labels, grad_ready)
         if self.head_start is not None:
@@ -294,7 +338,7 @@ class Net:
         chain, then all head weight gradients), then the body's backward from the head's dX."""
         self.bind(x.shape[0])
         if isinstance(x, ops.GatherRef) and not isinstance(self.exec_layers[0], FusedConvPool):
-            x = x.materialise(self.x_buf)
+            x = x.materialise(self.x_buf, step_inc=self._take_gather_step())
         h = x
         for l in self.exec_layers[: self.head_start]:
             h = l.forward(h, True)
@@ -312,7 +356,8 @@ class Net:
             gw=[st.grad_matrix(f"{l.name}/kernel") for l in head],
             gb=[st.gradient(f"{l.name}/bias") if l.use_bias else None for l in head],
             hT=self.head_hT, dzT=self.head_dzT, K=[l.in_features for l in head], N=[l.units for l in head],
-            x=h, x_relu=first.in_relu, xT=self.head_xT, dx=first.dx if first.need_dx else None,
+            x=h, x_relu=first.in_relu, dx_scale=first.dx_scale, xT=self.head_xT,
+            dx=first.dx if first.need_dx else None,
             logits=head[-1].out, labels=lab, idx=idx, grad_scale=1.0 / x.shape[0],
             loss_part=self.head_loss_part, stats=self.stats)
         head_ids = range(len(self.exec_layers) - 1, self.head_start - 1, -1)

@@ -66,25 +66,30 @@ def conv_out_hw(H, W, KH, KW, stride, pad):
 
 
 # ----------------------------------------------------------------------------------- dense
-def dense_fwd(x, w, bias, out, relu=False):
-    """out[B][N] = act(x[B][K] @ W^T + b); out may be bf16 or fp32 (logits)."""
+def dense_fwd(x, w, bias, out, relu=False, drop=None):
+    """out[B][N] = act(x[B][K] @ W^T + b); out may be bf16 or fp32 (logits).  ``drop = (p, seed, step)``:
+    a Dropout that follows, folded into the epilogue (the mask of :func:`dropout` on ``out``)."""
     B, K = x.shape[0], x.shape[-1]
     N = out.shape[-1]
     if x.is_cuda:
-        _C().igemm_fwd(x, w, bias, None, out, B, N, K, w.shape[1], K, N, _geom(), MODE_DIRECT, relu, 1.0)
+        dkw = {} if drop is None else {"drop_p": float(drop[0]), "drop_seed": int(drop[1]), "drop_step": drop[2]}
+        _C().igemm_fwd(x, w, bias, None, out, B, N, K, w.shape[1], K, N, _geom(), MODE_DIRECT, relu, 1.0, **dkw)
     else:
         out.copy_(ref.dense_fwd(x, w, bias, relu))
+        if drop is not None:
+            dropout(out, out, drop[0], drop[1], step=drop[2])
     return out
 
 
-def dense_dgrad(dy, w, wt, out, mask=None):
-    """out[B][K] = (dy[B][N] @ W) * relu'(mask)."""
+def dense_dgrad(dy, w, wt, out, mask=None, alpha=1.0):
+    """out[B][K] = alpha * (dy[B][N] @ W) * relu'(mask)."""
     B, N = dy.shape[0], dy.shape[-1]
     K = out.shape[-1]
     if dy.is_cuda:
-        _C().igemm_fwd(dy, wt, None, mask, out, B, K, N, wt.shape[1], N, K, _geom(), MODE_DIRECT, False, 1.0)
+        _C().igemm_fwd(dy, wt, None, mask, out, B, K, N, wt.shape[1], N, K, _geom(), MODE_DIRECT, False,
+                       float(alpha))
     else:
-        out.copy_(ref.dense_dgrad(dy, w, K, mask))
+        out.copy_(ref.dense_dgrad(dy, w, K, mask) * alpha)
     return out
 
 
@@ -153,12 +158,16 @@ def conv_wgrad(dy, x, gw, gb, workspace, KH, KW, stride=1, pad=0, scale=1.0):
 
 
 # ----------------------------------------------------------------------------------- pooling etc.
-def maxpool_fwd(x, out, P):
+def maxpool_fwd(x, out, P, drop=None):
+    """``drop = (p, seed, step)``: a Dropout that follows, folded in (same mask as :func:`dropout`)."""
     B, H, W, C = x.shape
     if x.is_cuda:
-        _C().maxpool_fwd(x, out, B, H, W, C, P)
+        dkw = {} if drop is None else {"drop_p": float(drop[0]), "drop_seed": int(drop[1]), "drop_step": drop[2]}
+        _C().maxpool_fwd(x, out, B, H, W, C, P, **dkw)
     else:
         out.copy_(ref.maxpool_fwd(x, P))
+        if drop is not None:
+            dropout(out, out, drop[0], drop[1], step=drop[2])
     return out
 
 
@@ -196,13 +205,16 @@ def dropout(x, out, p, seed, mask=None, step=None):
     return out
 
 
-def gather_batch(data, labels, idx, out, out_labels, scale=1.0):
-    """out[b] = data[idx[b]] (uint8 -> bf16 * scale on the fly); out_labels[b] = labels[idx[b]]."""
+def gather_batch(data, labels, idx, out, out_labels, scale=1.0, step_inc=None):
+    """out[b] = data[idx[b]] (uint8 -> bf16 * scale on the fly); out_labels[b] = labels[idx[b]].
+    ``step_inc``: a device int64 counter the launch advances by one (the engine's dropout step)."""
     B = idx.shape[0]
     row = out[0].numel()
     if out.is_cuda:
-        _C().gather_batch(data, labels, idx, out, out_labels, B, row, scale)
+        _C().gather_batch(data, labels, idx, out, out_labels, B, row, scale, step_inc=step_inc)
     else:
+        if step_inc is not None:
+            step_inc.add_(1)
         out.copy_((data.index_select(0, idx).float() * scale).reshape(out.shape))
         if labels is not None:
             out_labels.copy_(labels.index_select(0, idx))
@@ -319,8 +331,8 @@ class GatherRef:
         self.device = data.device
         self.is_cuda = data.is_cuda
 
-    def materialise(self, out):
-        return gather_batch(self.data, None, self.idx, out, None, self.scale)
+    def materialise(self, out, step_inc=None):
+        return gather_batch(self.data, None, self.idx, out, None, self.scale, step_inc=step_inc)
 
 
 class LabelRef:
@@ -341,14 +353,15 @@ def head_supported() -> bool:
 
 
 def head_train(w, wt, b, gw, gb, hT, dzT, K, N, x, x_relu, xT, dx, logits, labels, idx, grad_scale, loss_part,
-               stats, phases=3):
+               stats, phases=3, dx_scale=1.0):
     """Fused dense head on GPU (csrc/mlphead.hip): forward + softmax-CE + backward of a Dense chain.
     phases bit 1: forward, loss, backward data chain (dx, logits, H^T/dZ^T); bit 2: weight/bias
     gradients gw/gb (batch-mean scaled via grad_scale) and stats.  Each phase is one launch on the
     current stream, so the two can be placed on different streams."""
     _C().head_train(list(w), list(wt), list(b), list(gw), list(gb), list(hT), list(dzT), list(K), list(N),
                     x.reshape(x.shape[0], -1) if x.is_contiguous() else x.contiguous().reshape(x.shape[0], -1),
-                    bool(x_relu), xT, dx, logits, labels, idx, float(grad_scale), loss_part, stats, int(phases))
+                    bool(x_relu), xT, dx, logits, labels, idx, float(grad_scale), loss_part, stats, int(phases),
+                    dx_scale=float(dx_scale))
 
 
 METRIC_KINDS = {"meanSquaredError": 0, "mse": 0, "absoluteDifference": 1, "hingeLoss": 2, "huberLoss": 3,
