@@ -51,14 +51,23 @@ void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tenso
                   c10::optional<torch::Tensor> mask, torch::Tensor out, int64_t M, int64_t N, int64_t K, int64_t Kpad,
                   int64_t lda, int64_t ldc, std::vector<int64_t> geom, int64_t mode, bool relu, double alpha,
                   c10::optional<torch::Tensor> res, c10::optional<torch::Tensor> resmask, double drop_p,
-                  int64_t drop_seed, c10::optional<torch::Tensor> drop_step) {
+                  int64_t drop_seed, c10::optional<torch::Tensor> drop_step, c10::optional<torch::Tensor> pool_code) {
   need(src, at::kBFloat16, "src");
   need(w, at::kBFloat16, "w");
   TORCH_CHECK(out.is_cuda() && out.is_contiguous(), "out must be a contiguous GPU tensor");
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "out must be bf16 or fp32");
   TORCH_CHECK(Kpad % 32 == 0 && Kpad >= K, "Kpad must be a multiple of 32 and >= K");
   TORCH_CHECK(w.numel() >= ((N + 15) / 16 * 16) * Kpad, "weight buffer smaller than [Npad16][Kpad]");
-  TORCH_CHECK(out.numel() >= (M - 1) * ldc + N, "out too small for [M][ldc]");
+  const bool pooled = pool_code.has_value() && pool_code->defined();
+  if (pooled) {
+    TORCH_CHECK(mode == 1 && M % 4 == 0 && ldc == N, "pooled conv: forward conv, M % 4 == 0, ldc == N");
+    TORCH_CHECK(pool_code->is_cuda() && pool_code->is_contiguous() && pool_code->scalar_type() == at::kByte &&
+                    pool_code->numel() >= M / 4 * N,
+                "pool_code must be a uint8 GPU tensor of [M/4][N]");
+    TORCH_CHECK(out.numel() >= M / 4 * N, "pooled out too small for [M/4][N]");
+  } else {
+    TORCH_CHECK(out.numel() >= (M - 1) * ldc + N, "out too small for [M][ldc]");
+  }
   TORCH_CHECK(ldc >= N, "ldc < N");
   dfa::IGemmArgs a{};
   int g[9];
@@ -102,6 +111,10 @@ void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tenso
   a.out_f32 = out.scalar_type() == at::kFloat ? 1 : 0;
   a.alpha = (float)alpha;
   a.drop = drop_from(drop_p, drop_seed, drop_step);
+  if (pooled) {
+    a.pool_code = pool_code->data_ptr<uint8_t>();
+    TORCH_CHECK(dfa::igemm64_pool_supported(a), "pooled conv: unsupported geometry / alignment");
+  }
   TORCH_CHECK(!a.drop.on || (ldc == N && !a.out_f32), "folded dropout needs a dense bf16 output (ldc == N)");
   // split-K partials for the under-filled (small-M, long-K) shapes: PyTorch's caching allocator is
   // stream ordered and graph-capture aware, so the scratch is safe to drop right after the launch
@@ -1190,7 +1203,28 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias"), py::arg("mask"), py::arg("out"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("Kpad"),
         py::arg("lda"), py::arg("ldc"), py::arg("geom"), py::arg("mode"), py::arg("relu"), py::arg("alpha"),
         py::arg("res") = py::none(), py::arg("resmask") = py::none(), py::arg("drop_p") = 0.0,
-        py::arg("drop_seed") = 0, py::arg("drop_step") = py::none());
+        py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pool_code") = py::none());
+  m.def("igemm64_pool_supported", [](int64_t H, int64_t W, int64_t C, int64_t OH, int64_t OW, int64_t K, int64_t N) {
+    dfa::IGemmArgs a{};
+    a.SH = (int)H; a.SW = (int)W; a.SC = (int)C; a.OH = (int)OH; a.OW = (int)OW; a.M = 4; a.N = (int)N; a.ldc = (int)N;
+    a.K = (int)K; a.Kpad = (int)((K + 31) / 32 * 32);
+    static dfa::bf16 probe[8] __attribute__((aligned(16)));
+    static uint8_t codep[4] __attribute__((aligned(4)));
+    a.src = probe; a.w = probe; a.out = probe; a.pool_code = codep;
+    return dfa::igemm64_pool_supported(a) && N % 8 == 0;
+  });
+  m.def("unpool2", [](torch::Tensor dyp, torch::Tensor code, torch::Tensor dy) {
+    need(dyp, at::kBFloat16, "unpool dyp");
+    need(dy, at::kBFloat16, "unpool dy");
+    TORCH_CHECK(dy.dim() == 4 && code.is_cuda() && code.is_contiguous() && code.scalar_type() == at::kByte,
+                "unpool2: dy [B][OH][OW][N], code uint8");
+    const int64_t B = dy.size(0), OH = dy.size(1), OW = dy.size(2), N = dy.size(3);
+    TORCH_CHECK(dyp.numel() == B * (OH / 2) * (OW / 2) * N && code.numel() == dyp.numel(), "unpool2: sizes");
+    check_hip(dfa::unpool2(reinterpret_cast<const dfa::bf16*>(dyp.data_ptr()), code.data_ptr<uint8_t>(),
+                           reinterpret_cast<dfa::bf16*>(dy.data_ptr()), (int)B, (int)OH, (int)OW, (int)N,
+                           cur_stream()),
+              "unpool2");
+  });
   m.def("igemm_wgrad", &igemm_wgrad_py, "implicit-GEMM MFMA weight gradient (split-m slabs + reduce)");
   m.def("maxpool_fwd", &maxpool_fwd_py, py::arg("x"), py::arg("y"), py::arg("B"), py::arg("H"), py::arg("W"),
         py::arg("C"), py::arg("P"), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0,

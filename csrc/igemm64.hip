@@ -45,6 +45,12 @@ __device__ __forceinline__ u32x4_t gload16(const void* p) {
   return r;
 }
 
+// lane exchanges inside groups of 4 lanes (DPP quad_perm: VALU latency, no LDS round trip)
+__device__ __forceinline__ int quad_xor1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ int quad_xor2(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false); }
+__device__ __forceinline__ float quad_xor1(float v) { return __int_as_float(quad_xor1(__float_as_int(v))); }
+__device__ __forceinline__ float quad_xor2(float v) { return __int_as_float(quad_xor2(__float_as_int(v))); }
+
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
 // occupancy the LDS footprint allows (2 x (BM + BN) x 128 B per workgroup): 4 workgroups of 40 KB, 3 of
@@ -293,11 +299,11 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
         for (int r = 0; r < 4; ++r) {
           // the conv output as the unfused path stored it (bf16), then the first max of the window
           const float v = (float)f2bf(acc[i][j][r] * a.alpha + ((a.bias && col0 + r < a.N) ? a.bias[col0 + r] : 0.f));
-          float m = fmaxf(v, __shfl_xor(v, 1));
-          m = fmaxf(m, __shfl_xor(m, 2));
+          float m = fmaxf(v, quad_xor1(v));
+          m = fmaxf(m, quad_xor2(m));
           int p = v == m ? (fr & 3) : 4;
-          p = min(p, __shfl_xor(p, 1));
-          p = min(p, __shfl_xor(p, 2));
+          p = min(p, quad_xor1(p));
+          p = min(p, quad_xor2(p));
           mx[r] = m;
           pc[r] = p;
         }

@@ -597,3 +597,54 @@ class FusedConvPool(Layer):
     def backward(self, dy, defer=None):
         self.backward_weights(dy, defer)
         return self.backward_data(dy)
+
+
+class ConvPoolGemm(Layer):
+    """Conv2D(stride 1, +bias, ReLU) followed by MaxPooling2D(2) for C % 8 == 0 (the Keras CNN's conv2,
+    /root/reference/experiment/mnist/model.json: conv2d_2 -> max_pooling2d_1): the igemm64 forward
+    reduces each 2x2 window in its epilogue (csrc/igemm64.hip POOL), so only the pooled map and a
+    1-byte argmax code per pooled element reach HBM and no max-pool launch remains.  Backward: one
+    unpool launch rebuilds the conv's output gradient from the codes, then the conv's own weight- and
+    data-gradient kernels.  A following Dropout can fold in (Net._fold_dropout).  Parameter names are the
+    Conv2D's (checkpoint-compatible)."""
+    has_params = True
+
+    def __init__(self, conv: "Conv2D", pool: "MaxPooling2D"):
+        super().__init__(conv.name)
+        self.conv, self.pool = conv, pool
+        self.use_bias = conv.use_bias
+        self.in_shape = conv.in_shape
+        self.out_shape = pool.out_shape
+        self.relu = False  # relu' is carried by the codes (4 = no gradient)
+
+    def specs(self):
+        self.conv.need_dx = self.need_dx
+        return self.conv.specs()
+
+    def alloc(self, B, device, dtype, ws):
+        c = self.conv
+        c.in_relu, c.need_dx, c.ws, c.store = self.in_relu, self.need_dx, ws, self.store
+        c.dx = torch.empty((B,) + c.in_shape, device=device, dtype=dtype) if self.need_dx else None
+        self.out = torch.empty((B,) + self.out_shape, device=device, dtype=dtype)
+        self.code = torch.empty((B,) + self.out_shape, device=device, dtype=torch.uint8)
+        self.dy_full = torch.empty((B,) + self.conv.out_shape, device=device, dtype=dtype)
+        self.dx = self.conv.dx
+
+    def forward(self, x, training):
+        self.x = x
+        c = self.conv
+        c.x = x
+        st = self.store
+        b = st[f"{c.name}/bias"] if c.use_bias else None
+        ops.conv_pool_fwd(x, st.weight(f"{c.name}/kernel"), b, self.out, self.code, c.k, c.k, c.stride, c.pad,
+                          relu=c.relu, drop=self.drop_spec(training))
+        return self.out
+
+    def backward(self, dy):
+        ops.unpool2(dy.reshape(self.out.shape), self.code, self.dy_full)
+        self.conv.store = self.store
+        return self.conv.backward(self.dy_full)
+
+    def config(self):
+        return self.conv.config()
+

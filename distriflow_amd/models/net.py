@@ -17,7 +17,8 @@ import os
 import torch
 
 from .. import ops
-from .layers import (Activation, BatchNorm, Conv2D, Dense, Dropout, Flatten, FusedConvPool, Layer, MaxPooling2D,
+from .layers import (Activation, BatchNorm, Conv2D, ConvPoolGemm, Dense, Dropout, Flatten, FusedConvPool, Layer,
+                     MaxPooling2D,
                      ResidualBlock)
 from .params import ParamStore
 
@@ -184,7 +185,8 @@ class Net:
             if (isinstance(l, Dropout) and l.rate > 0 and prev is not None and prev.drop is None
                     and isinstance(nxt, Dense)
                     and ((isinstance(prev, Dense) and prev.relu and not prev.out_f32)
-                         or (isinstance(prev, MaxPooling2D) and prev.in_relu))):
+                         or (isinstance(prev, MaxPooling2D) and prev.in_relu)
+                         or (isinstance(prev, ConvPoolGemm) and prev.conv.relu))):
                 prev.drop = l
                 nxt.in_relu = True
                 nxt.dx_scale = 1.0 / (1.0 - l.rate)
@@ -208,6 +210,13 @@ class Net:
                 out.append(FusedConvPool(l, nxt))
                 i += 2
                 continue
+            if (isinstance(l, Conv2D) and isinstance(nxt, MaxPooling2D) and l.relu and l.stride == 1 and nxt.p == 2
+                    and l.out_shape[0] % 2 == 0 and l.out_shape[1] % 2 == 0
+                    and ops.conv_pool_supported(l.in_shape[0], l.in_shape[1], l.in_shape[2], l.k, l.k, l.stride,
+                                                l.pad, l.filters)):
+                out.append(ConvPoolGemm(l, nxt))
+                i += 2
+                continue
             out.append(l)
             i += 1
         return out
@@ -224,7 +233,8 @@ class Net:
         if self._bound_B == B:
             return
         # split-m weight-gradient slabs: room for 4 slabs of the largest conv kernel (>= 16 MB)
-        nk = max([l.filters * l.k * l.k * l.in_shape[2] for l in self._all_leaf_layers() if isinstance(l, Conv2D)]
+        convs = [l.conv if isinstance(l, ConvPoolGemm) else l for l in self._all_leaf_layers()]
+        nk = max([l.filters * l.k * l.k * l.in_shape[2] for l in convs if isinstance(l, Conv2D)]
                  + [0])
         ws_wgrad = torch.empty(max(1 << 22, 4 * nk), dtype=torch.float32, device=self.device)
         maxC = max([l.C for l in self._all_leaf_layers() if isinstance(l, BatchNorm)] + [8])
@@ -502,7 +512,7 @@ class Net:
             if isinstance(l, Dense):
                 f = 2 * l.in_features * l.units
                 return f * (3 if l.need_dx else 2)
-            if isinstance(l, FusedConvPool):
+            if isinstance(l, (FusedConvPool, ConvPoolGemm)):
                 c = l.conv
                 OH, OW, N = c.out_shape
                 f = 2 * OH * OW * N * c.k * c.k * c.in_shape[2]

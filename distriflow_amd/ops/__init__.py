@@ -120,6 +120,52 @@ def conv_fwd(x, w, bias, out, KH, KW, stride=1, pad=0, relu=False):
     return out
 
 
+def conv_pool_supported(H, W, C, KH, KW, stride, pad, N) -> bool:
+    """Conv + 2x2 max-pool in the igemm64 epilogue (pooled map + argmax codes only)."""
+    m = native.get(build_if_missing=False)
+    if m is None or not hasattr(m, "igemm64_pool_supported") or stride != 1:
+        return False
+    OH, OW = conv_out_hw(H, W, KH, KW, stride, pad)
+    return bool(m.igemm64_pool_supported(H, W, C, OH, OW, KH * KW * C, N))
+
+
+def conv_pool_fwd(x, w, bias, out, code, KH, KW, stride=1, pad=0, relu=True, drop=None):
+    """conv(+bias, ReLU) then 2x2 max-pool [then a folded dropout]: ``out`` = pooled [B][OH/2][OW/2][N],
+    ``code`` = argmax position 0..3 per pooled element (4 = no gradient)."""
+    B, H, W, C = x.shape
+    _, PH, PW, N = out.shape
+    OH, OW = 2 * PH, 2 * PW
+    if x.is_cuda:
+        K = KH * KW * C
+        dkw = {} if drop is None else {"drop_p": float(drop[0]), "drop_seed": int(drop[1]), "drop_step": drop[2]}
+        _C().igemm_fwd(x, w, bias, None, out, B * OH * OW, N, K, w.shape[1], 0, N,
+                       _geom(H, W, C, OH, OW, KH, KW, stride, pad), MODE_FWD, relu, 1.0, pool_code=code, **dkw)
+    else:
+        y = ref.conv_fwd(x, w, bias, KH, KW, stride, pad, relu).to(out.dtype).float()
+        win = y.reshape(B, PH, 2, PW, 2, N).permute(0, 1, 3, 5, 2, 4).reshape(B, PH, PW, N, 4)
+        mx, am = win.max(dim=-1)  # first max
+        if relu:
+            am = torch.where(mx > 0, am, torch.full_like(am, 4))
+        out.copy_(mx)
+        code.copy_(am.to(torch.uint8))
+        if drop is not None:
+            dropout(out, out, drop[0], drop[1], step=drop[2])
+    return out
+
+
+def unpool2(dyp, code, dy):
+    """dy [B][OH][OW][N]: each pooled gradient at the window position its code names."""
+    if dy.is_cuda:
+        _C().unpool2(dyp.contiguous(), code, dy)
+    else:
+        B, OH, OW, N = dy.shape
+        g = dyp.float().reshape(B, OH // 2, OW // 2, N, 1)
+        sel = (code.long().reshape(B, OH // 2, OW // 2, N, 1) == torch.arange(4).reshape(1, 1, 1, 1, 4)).float()
+        full = (g * sel).reshape(B, OH // 2, OW // 2, N, 2, 2).permute(0, 1, 4, 2, 5, 3).reshape(B, OH, OW, N)
+        dy.copy_(full)
+    return dy
+
+
 def conv_dgrad(dy, w, wt, out, KH, KW, stride=1, pad=0, mask=None, residual=None, residual_mask=None):
     """dX (NHWC [B][H][W][C]) of a conv whose output gradient is dy [B][OH][OW][N].
 

@@ -49,14 +49,43 @@ def test_maxpool_dropout_is_the_standalone_mask(p):
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("B,H,C,N,pad,drop", [(4, 26, 32, 64, 0, None), (3, 14, 16, 32, 1, 0.25),
+                                               (2, 12, 8, 16, 0, 0.5)])
+def test_pooled_conv_epilogue_equals_conv_then_pool(B, H, C, N, pad, drop):
+    """igemm64 POOL: the pooled map equals conv (bf16 out) -> max-pool [-> dropout], bitwise; the unpooled
+    gradient from its codes equals maxpool_bwd over the unpooled conv output (relu fused)."""
+    x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
+    w = torch.randn(N, 9 * C, device=dev) / (9 * C) ** 0.5
+    b = torch.randn(N, device=dev) * 0.1
+    OH = H + 2 * pad - 2
+    assert ops.conv_pool_supported(H, H, C, 3, 3, 1, pad, N)
+    y = torch.empty(B, OH, OH, N, dtype=torch.bfloat16, device=dev)
+    ops.conv_fwd(x, _pad_w(w), b, y, 3, 3, 1, pad, relu=True)
+    step = torch.tensor(5, dtype=torch.int64, device=dev)
+    dspec = None if drop is None else (drop, 77, step)
+    ref = torch.empty(B, OH // 2, OH // 2, N, dtype=torch.bfloat16, device=dev)
+    ops.maxpool_fwd(y, ref, 2, drop=dspec)
+    out = torch.empty_like(ref)
+    code = torch.empty(ref.shape, dtype=torch.uint8, device=dev)
+    ops.conv_pool_fwd(x, _pad_w(w), b, out, code, 3, 3, 1, pad, relu=True, drop=dspec)
+    dyp = torch.randn(ref.shape, device=dev).to(torch.bfloat16)
+    d_ref = torch.empty_like(y)
+    ops.maxpool_bwd(y, dyp, d_ref, 2, relu_fused=True)
+    d_out = torch.empty_like(y)
+    ops.unpool2(dyp, code, d_out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert torch.equal(d_out, d_ref)
+
+
 def test_keras_cnn_plan_has_no_dropout_launch():
-    from distriflow_amd.models.layers import Dense, Dropout, MaxPooling2D
+    from distriflow_amd.models.layers import ConvPoolGemm, Dense, Dropout, MaxPooling2D
     from distriflow_amd.models.zoo import build_model
 
     net = build_model("keras_cnn", device=dev, seed=0)
     kinds = [type(l) for l in net.exec_layers]
-    assert Dropout not in kinds
-    pool = next(l for l in net.exec_layers if isinstance(l, MaxPooling2D))
+    assert Dropout not in kinds and MaxPooling2D not in kinds
+    pool = next(l for l in net.exec_layers if isinstance(l, ConvPoolGemm))
     assert pool.drop is not None and pool.drop.rate == 0.25
     dense = [l for l in net.exec_layers if isinstance(l, Dense)]
     assert dense[0].drop is not None and dense[0].in_relu and abs(dense[0].dx_scale - 1 / 0.75) < 1e-12
