@@ -896,6 +896,83 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
   check_hip(dfa::lenet_train(a, r, cur_stream()), "lenet_train");
 }
 
+// The reference CNN's conv block (csrc/kcnn_fused.hip).  x: uint8 dataset [nrows][28][28][1] (idx
+// required), bf16 dataset rows (idx + scale), or a bf16 batch [B][28][28][1].
+static dfa::KcnnArgs kcnn_args(torch::Tensor x, c10::optional<torch::Tensor> idx, double scale, int64_t B,
+                               torch::Tensor w1, torch::Tensor b1, int64_t kpad1, torch::Tensor code) {
+  dfa::KcnnArgs a{};
+  TORCH_CHECK(B > 0 && B < (1 << 30), "kcnn: bad batch");
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.numel() % 784 == 0, "kcnn: x must be [.][28][28][1] on GPU");
+  if (idx.has_value() && idx->defined()) {
+    need(*idx, at::kLong, "kcnn idx");
+    TORCH_CHECK(idx->numel() == B, "kcnn: idx must have B entries");
+    a.idx = reinterpret_cast<const long long*>(idx->data_ptr());
+  }
+  if (x.scalar_type() == at::kByte) {
+    TORCH_CHECK(a.idx, "kcnn: a uint8 dataset needs batch indices");
+    a.x_u8 = x.data_ptr<uint8_t>();
+  } else {
+    TORCH_CHECK(x.scalar_type() == at::kBFloat16, "kcnn: x must be uint8 or bf16");
+    a.x_bf = reinterpret_cast<const dfa::bf16*>(x.data_ptr());
+    TORCH_CHECK(a.idx || x.numel() == B * 784, "kcnn: x must be [B][28][28][1]");
+  }
+  a.nrows = x.numel() / 784;
+  a.scale = (float)scale;
+  need(w1, at::kBFloat16, "kcnn w1");
+  need(b1, at::kFloat, "kcnn b1");
+  TORCH_CHECK(kpad1 >= 9 && w1.numel() >= 32 * kpad1 && b1.numel() == 32, "kcnn: conv1 weights [32][kpad1]");
+  a.w1 = reinterpret_cast<const dfa::bf16*>(w1.data_ptr());
+  a.b1 = b1.data_ptr<float>();
+  a.kpad1 = (int)kpad1;
+  TORCH_CHECK(code.is_cuda() && code.is_contiguous() && code.scalar_type() == at::kByte && code.numel() == B * 144 * 32,
+              "kcnn: code must be uint8 [B][12][12][32]");
+  a.code = code.data_ptr<uint8_t>();
+  a.B = (int)B;
+  return a;
+}
+
+void kcnn_fwd_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double scale, int64_t B, torch::Tensor w1,
+                 torch::Tensor b1, int64_t kpad1, torch::Tensor w2, torch::Tensor b2, torch::Tensor pooled,
+                 torch::Tensor code, double drop_p, int64_t drop_seed, c10::optional<torch::Tensor> drop_step) {
+  dfa::KcnnArgs a = kcnn_args(x, idx, scale, B, w1, b1, kpad1, code);
+  need(w2, at::kBFloat16, "kcnn w2");
+  need(b2, at::kFloat, "kcnn b2");
+  need(pooled, at::kBFloat16, "kcnn pooled");
+  TORCH_CHECK(w2.numel() >= 32 * 288 && b2.numel() == 32 && pooled.numel() == B * 144 * 32, "kcnn: conv2 / pooled");
+  a.w2 = reinterpret_cast<const dfa::bf16*>(w2.data_ptr());
+  a.b2 = b2.data_ptr<float>();
+  a.pooled = reinterpret_cast<dfa::bf16*>(pooled.data_ptr());
+  a.drop = drop_from(drop_p, drop_seed, drop_step);
+  check_hip(dfa::kcnn_fwd(a, cur_stream()), "kcnn_fwd");
+}
+
+void kcnn_bwd_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double scale, int64_t B, torch::Tensor w1,
+                 torch::Tensor b1, int64_t kpad1, torch::Tensor w2t, torch::Tensor dyp, torch::Tensor code,
+                 torch::Tensor slabs, torch::Tensor g_w1, torch::Tensor g_b1, torch::Tensor g_w2, torch::Tensor g_b2,
+                 c10::optional<torch::Tensor> step_inc) {
+  dfa::KcnnArgs a = kcnn_args(x, idx, scale, B, w1, b1, kpad1, code);
+  need(w2t, at::kBFloat16, "kcnn w2t");
+  need(dyp, at::kBFloat16, "kcnn dyp");
+  need(slabs, at::kFloat, "kcnn slabs");
+  TORCH_CHECK(w2t.numel() >= 32 * 288 && dyp.numel() == B * 144 * 32, "kcnn: dgrad weights / pooled gradient");
+  TORCH_CHECK((size_t)slabs.numel() >= dfa::kcnn_slab_floats((int)B), "kcnn: slab workspace too small");
+  for (auto* t : {&g_w1, &g_b1, &g_w2, &g_b2}) need(*t, at::kFloat, "kcnn grad");
+  TORCH_CHECK(g_w1.numel() == 288 && g_b1.numel() == 32 && g_w2.numel() == 32 * 288 && g_b2.numel() == 32,
+              "kcnn: gradient sizes");
+  a.w2t = reinterpret_cast<const dfa::bf16*>(w2t.data_ptr());
+  a.dyp = reinterpret_cast<const dfa::bf16*>(dyp.data_ptr());
+  a.slab2 = slabs.data_ptr<float>();
+  a.slab1 = a.slab2 + (size_t)dfa::kcnn_blocks((int)B) * 32 * 289;
+  long long* sp = nullptr;
+  if (step_inc.has_value() && step_inc->defined()) {
+    need(*step_inc, at::kLong, "kcnn step");
+    sp = reinterpret_cast<long long*>(step_inc->data_ptr());
+  }
+  check_hip(dfa::kcnn_bwd(a, g_w1.data_ptr<float>(), g_b1.data_ptr<float>(), g_w2.data_ptr<float>(),
+                          g_b2.data_ptr<float>(), sp, cur_stream()),
+            "kcnn_bwd");
+}
+
 void classifier_metrics_py(torch::Tensor z, torch::Tensor labels, int64_t kind, bool softmax, torch::Tensor out) {
   need(z, at::kFloat, "metrics logits");
   need(labels, at::kInt, "metrics labels");
@@ -1286,6 +1363,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("K"), py::arg("N"), py::arg("x"), py::arg("x_relu"), py::arg("xT"), py::arg("dx"), py::arg("logits"),
         py::arg("labels"), py::arg("idx"), py::arg("grad_scale"), py::arg("loss_part"), py::arg("stats"),
         py::arg("phases"), py::arg("dx_scale") = 1.0);
+  m.def("kcnn_fwd", &kcnn_fwd_py, "reference CNN conv block forward (conv1 + conv2 + pool [+ dropout], 1 launch)",
+        py::arg("x"), py::arg("idx"), py::arg("scale"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("kpad1"),
+        py::arg("w2"), py::arg("b2"), py::arg("pooled"), py::arg("code"), py::arg("drop_p") = 0.0,
+        py::arg("drop_seed") = 0, py::arg("drop_step") = py::none());
+  m.def("kcnn_bwd", &kcnn_bwd_py, "reference CNN conv block backward (both weight gradients, 2 launches)",
+        py::arg("x"), py::arg("idx"), py::arg("scale"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("kpad1"),
+        py::arg("w2t"), py::arg("dyp"), py::arg("code"), py::arg("slabs"), py::arg("g_w1"), py::arg("g_b1"),
+        py::arg("g_w2"), py::arg("g_b2"), py::arg("step_inc") = py::none());
+  m.def("kcnn_slab_floats", [](int64_t B) { return (int64_t)dfa::kcnn_slab_floats((int)B); });
   m.def("classifier_metrics", &classifier_metrics_py, "[loss sum, correct] of a classifier batch (one launch)");
   m.def("lenet_train", &lenet_train_py, "whole-network LeNet-5 training step (fwd + CE + bwd, 2 launches)",
         py::arg("x"), py::arg("idx"), py::arg("scale"), py::arg("labels"), py::arg("conv"), py::arg("dense_w"),

@@ -1,0 +1,410 @@
+// The reference CNN's convolution block in two launches per direction (gfx950 / MI355X).
+//
+// /root/reference/experiment/mnist/model.json: conv2d_1 (3x3x1 -> 32, ReLU) -> conv2d_2 (3x3x32 -> 32,
+// ReLU) -> max_pooling2d_1 (2x2) [-> dropout_1, folded in].  Per-layer kernels move every activation
+// through HBM (conv1's 26x26x32 output is 44 MB per 1024 images, written once and read three times) and
+// run conv2 as short implicit GEMMs (K = 288) whose per-workgroup prologue/epilogue dominate.  Here a
+// workgroup keeps one image at a time entirely in LDS:
+//
+//   kcnn_fwd  (persistent, 2 images per workgroup at B = 1024)
+//     x0 (uint8 dataset row through the batch index, or bf16)  -> LDS
+//     conv1 + bias + ReLU on the VALU (72 weights per thread)  -> X1 [676][32] bf16 in LDS (never in HBM)
+//     conv2 on MFMA 16x16x32: one k-step per tap (32 channels), the 18 B fragments (9 taps x 2 channel
+//     halves) stay in registers, A fragments are 16-byte LDS reads of X1.  Output pixels are taken
+//     pool-window-major, so the four pixels of a 2x2 window are the four accumulator rows of one lane:
+//     max-pool, argmax code, ReLU and the folded dropout happen in registers and only the pooled map
+//     [144][32] and a 1-byte code per pooled element are written.
+//   kcnn_bwd  (persistent)
+//     x0 -> LDS, conv1 recomputed into X1 (cheaper than storing and re-reading it), the conv2 output
+//     gradient dY2 [576][32] expanded in LDS from the pooled gradient and the codes (conv2 bias
+//     gradient summed on the way), then
+//       conv2 weight gradient  MFMA, D[n][(tap, ci)] over 18 pixel blocks of 32 per image; both operands
+//                              come from ds_read_b64_tr_b16 (transposing 4-row blocks in the read);
+//                              accumulators stay in registers across the workgroup's images
+//       conv2 data gradient    MFMA, one k-step per tap (32 output channels) against the dgrad weight
+//                              copy, x relu'(X1), rounded to bf16 as the per-layer path stores it, and
+//       conv1 weight gradient  consumed in registers: 10 FMAs (9 taps + bias) per element against x0,
+//                              so dX1 never exists in HBM either
+//     each workgroup writes one slab of conv2 [32][289] and conv1 [32][10] partial sums
+//   kcnn_reduce  sums the slabs in a fixed order (deterministic), writes the four gradients and
+//     advances the dropout step counter (the last reader of the step's masks has run).
+//
+// Forward results equal the per-layer path bit for bit (same conv1 FMA order, same conv2 k order, the
+// conv output rounded to bf16 before the max exactly as it was stored); the weight gradients are the
+// same sums in a different fp32 order.  LDS in kcnn_bwd: 1.5 + 42.3 + 36 KB = 80 KB, two workgroups
+// per CU.
+#include "common.h"
+#include "kernels.h"
+
+namespace dfa {
+
+namespace {
+
+constexpr int KT = 256;
+constexpr int H0 = 28, H1 = 26, H2 = 24, PW = 12, C = 32;
+constexpr int NP0 = H0 * H0, NP1 = H1 * H1, NP2 = H2 * H2, NPP = PW * PW;  // 784, 676, 576, 144
+constexpr int K2 = 9 * C;                                                   // 288
+constexpr int S2 = K2 + 1, S1 = 10;  // slab row lengths: conv2 (288 + bias), conv1 (9 + bias)
+
+typedef __bf16 bf16x4_vs __attribute__((__vector_size__(8)));
+
+__device__ __forceinline__ bf16x4 tr_read(const bf16* p) {
+  auto* lp = (__attribute__((address_space(3))) bf16*)(const_cast<bf16*>(p));
+  const bf16x4_vs v =
+      __builtin_amdgcn_ds_read_tr16_b64_v4bf16(reinterpret_cast<__attribute__((address_space(3))) bf16x4_vs*>(lp));
+  return __builtin_bit_cast(bf16x4, v);
+}
+__device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    r[e] = a[e];
+    r[e + 4] = b[e];
+  }
+  return r;
+}
+__device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// [pixel][32] bf16 LDS maps with the 16-byte chunk index XOR-swizzled by the pixel: the 16 pixels one
+// fragment read touches spread over more bank groups.  Element (pix, ch); a 4- or 8-element piece
+// starting at ch % 4 == 0 stays inside one chunk.
+__device__ __forceinline__ int xs(int pix, int ch) { return pix * C + ((((ch >> 3) ^ ((pix >> 1) & 3))) << 3) + (ch & 7); }
+
+__device__ __forceinline__ long long src_row(const KcnnArgs& a, int b) {
+  if (!a.idx) return b;
+  long long r = a.idx[b];
+  return r < 0 ? 0 : (r >= a.nrows ? a.nrows - 1 : r);
+}
+
+// x0 of image b as bf16 (the gather kernel's rounding: bf16(u8 * scale))
+__device__ __forceinline__ void stage_x0(const KcnnArgs& a, int b, bf16* x0) {
+  const long long row = src_row(a, b);
+  for (int e = threadIdx.x; e < NP0; e += KT) {
+    if (a.x_u8)
+      x0[e] = f2bf((float)a.x_u8[row * NP0 + e] * a.scale);
+    else
+      x0[e] = a.idx ? f2bf((float)a.x_bf[row * NP0 + e] * a.scale) : a.x_bf[row * NP0 + e];
+  }
+}
+
+// conv1 + bias + ReLU -> X1 (LDS).  Thread (ps = tid >> 2, g = tid & 3): channels 8g..8g+7 of pixels
+// ps, ps + 64, ...; the FMA chain is the per-layer kernel's (smallc.hip c1_fwd_kernel), so X1 is equal
+// bit for bit.
+__device__ __forceinline__ void conv1_to_lds(const KcnnArgs& a, const bf16* x0, bf16* x1) {
+  const int g = threadIdx.x & 3, ps = threadIdx.x >> 2;
+  float w[8][9], bias[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w[j][k] = (float)a.w1[(8 * g + j) * a.kpad1 + k];
+    bias[j] = a.b1[8 * g + j];
+  }
+  for (int p = ps; p < NP1; p += 64) {
+    const int oy = p / H1, ox = p - oy * H1;
+    float xv[9];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) xv[3 * ky + kx] = (float)x0[(oy + ky) * H0 + ox + kx];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc = fmaf(xv[k], w[j][k], acc);
+      o[j] = f2bf(fmaxf(acc * 1.f + bias[j], 0.f));
+    }
+    *reinterpret_cast<bf16x8*>(x1 + xs(p, 8 * g)) = o;
+  }
+}
+
+__global__ void __launch_bounds__(KT, 2) kcnn_fwd_kernel(KcnnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 x0[NP0];
+  __shared__ __attribute__((aligned(16))) bf16 x1[NP1 * C];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
+  // conv2 B fragments: tap t, channel half h -> B[k = 8G..8G+7 of tap t][n = 16h + i]
+  bf16x8 bw[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) bw[t][h] = ld8(a.w2 + (16 * h + i) * K2 + t * C + 8 * G);
+  const float bias2[2] = {a.b2[i], a.b2[16 + i]};
+  const unsigned long long dseed = a.drop.on ? drop_seed(a.drop.seed, a.drop.step) : 0ull;
+  // this lane's A row in a tile of 4 windows: window j = i >> 2, position r = i & 3
+  const int jw = i >> 2, rp = i & 3;
+  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+    stage_x0(a, b, x0);
+    __syncthreads();
+    conv1_to_lds(a, x0, x1);
+    __syncthreads();
+    for (int t = wid; t < NPP / 4; t += 4) {
+      const int q0 = 4 * t, ph = q0 / PW, pw0 = q0 - ph * PW;
+      const int oy = 2 * ph + (rp >> 1), ox = 2 * (pw0 + jw) + (rp & 1);
+      f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const bf16x8 af = ld8(x1 + xs((oy + ky) * H1 + ox + kx, 8 * G));
+          acc[0] = mfma16x16x32(af, bw[3 * ky + kx][0], acc[0]);
+          acc[1] = mfma16x16x32(af, bw[3 * ky + kx][1], acc[1]);
+        }
+      // lane holds rows 4G..4G+3 = the four positions of window q0 + G, channel 16h + i
+      const long long prow = (long long)b * NPP + q0 + G;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float m = -INFINITY;
+        int cd = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = (float)f2bf(acc[h][r] * 1.f + bias2[h]);
+          if (v > m) {
+            m = v;
+            cd = r;
+          }
+        }
+        if (!(m > 0.f)) cd = 4;  // ReLU'd max is 0: no gradient
+        float o = fmaxf(m, 0.f);
+        const int n = 16 * h + i;
+        if (a.drop.on) o = drop_keep(dseed, a.drop.thresh, prow * C + n) ? (float)f2bf(o) * a.drop.scale : 0.f;
+        a.pooled[prow * C + n] = f2bf(o);
+        a.code[prow * C + n] = (uint8_t)cd;
+      }
+    }
+    __syncthreads();  // x0 / x1 are rewritten for the next image
+  }
+}
+
+__global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 x0[NP0];
+  __shared__ __attribute__((aligned(16))) bf16 x1[NP1 * C];
+  __shared__ __attribute__((aligned(16))) bf16 dy2[NP2 * C];
+  __shared__ __attribute__((aligned(16))) bf16 zc[8];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, G = lane >> 4, i = lane & 15;
+  if (tid < 8) zc[tid] = (bf16)0.f;
+  // conv2 weight gradient: this wave's output channel half hn and input channel half hc, all 9 taps
+  const int hn = wid & 1, hc = wid >> 1;
+  f32x4 acc2[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float db2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) db2[j] = 0.f;
+  float acc1[2][10];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) acc1[h][k] = 0.f;
+  const int c8 = tid & 3;  // this thread's 8-channel group in the dY2 expansion (256 % 4 == 0)
+
+  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+    // ---- stage x0; expand dY2 from the pooled gradient and the codes (conv2 bias gradient on the way)
+    stage_x0(a, b, x0);
+    for (int e = tid; e < NPP * 4; e += KT) {
+      const int q = e >> 2;
+      const long long o = ((long long)b * NPP + q) * C + 8 * c8;
+      const bf16x8 gv = ld8(a.dyp + o);
+      const uint2 cw = *reinterpret_cast<const uint2*>(a.code + o);
+      const int ph = q / PW, pw = q - ph * PW;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        bf16x8 ov;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const unsigned cd = ((j < 4 ? cw.x : cw.y) >> (8 * (j & 3))) & 0xffu;
+          ov[j] = cd == (unsigned)p ? gv[j] : (bf16)0.f;
+          if (cd == (unsigned)p) db2[j] += (float)gv[j];
+        }
+        const int pix = (2 * ph + (p >> 1)) * H2 + 2 * pw + (p & 1);
+        *reinterpret_cast<bf16x8*>(dy2 + xs(pix, 8 * c8)) = ov;
+      }
+    }
+    __syncthreads();
+    conv1_to_lds(a, x0, x1);
+    __syncthreads();
+
+    // ---- conv2 weight gradient: D[n][(tap, ci)] += dY2^T[n][p] X1[p + tap][ci], 18 blocks of 32 pixels
+    for (int k0 = 0; k0 < NP2 / 32; ++k0) {
+      int pb[2], pa[2];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int P = k0 * 32 + 8 * G + 4 * hf + (i >> 2);
+        const int oy = P / H2, ox = P - oy * H2;
+        pa[hf] = P;
+        pb[hf] = oy * H1 + ox;
+      }
+      const bf16x8 af = cat8(tr_read(dy2 + xs(pa[0], 16 * hn + 4 * (i & 3))),
+                             tr_read(dy2 + xs(pa[1], 16 * hn + 4 * (i & 3))));
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int d = ky * H1 + kx;
+          const bf16x8 bf = cat8(tr_read(x1 + xs(pb[0] + d, 16 * hc + 4 * (i & 3))),
+                                 tr_read(x1 + xs(pb[1] + d, 16 * hc + 4 * (i & 3))));
+          acc2[3 * ky + kx] = mfma16x16x32(af, bf, acc2[3 * ky + kx]);
+        }
+    }
+
+    // ---- conv2 data gradient x relu'(X1) -> conv1 weight gradient, 43 tiles of 16 X1 pixels
+    {
+      bf16x8 bt[9][2];  // B[k = (tap, n = 8G..8G+7)][ci = 16h + i] from the dgrad copy [ci][tap * 32 + n]
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) bt[t][h] = ld8(a.w2t + (16 * h + i) * K2 + t * C + 8 * G);
+      for (int T = wid; T < (NP1 + 15) / 16; T += 4) {
+        const int X = T * 16 + i;
+        const int iy = X / H1, ix = X - iy * H1;
+        f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const int sy = iy - ky, sx = ix - kx;
+            const bool ok = X < NP1 && (unsigned)sy < (unsigned)H2 && (unsigned)sx < (unsigned)H2;
+            const bf16x8 af = ld8(ok ? dy2 + xs(sy * H2 + sx, 8 * G) : zc);
+            acc[0] = mfma16x16x32(af, bt[3 * ky + kx][0], acc[0]);
+            acc[1] = mfma16x16x32(af, bt[3 * ky + kx][1], acc[1]);
+          }
+        // lane holds pixels T*16 + 4G + r, channel 16h + i
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int Xr = T * 16 + 4 * G + r;
+          if (Xr >= NP1) continue;
+          const int ry = Xr / H1, rx = Xr - ry * H1;
+          float xv[9];
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) xv[3 * ky + kx] = (float)x0[(ry + ky) * H0 + rx + kx];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const bool live = (float)x1[xs(Xr, 16 * h + i)] > 0.f;
+            const float gval = live ? (float)f2bf(acc[h][r]) : 0.f;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) acc1[h][k] = fmaf(gval, xv[k], acc1[h][k]);
+            acc1[h][9] += gval;
+          }
+        }
+      }
+    }
+    __syncthreads();  // LDS is rewritten for the next image
+  }
+
+  // ---- per-workgroup slabs
+  float* s2 = a.slab2 + (long long)blockIdx.x * C * S2;
+  float* s1 = a.slab1 + (long long)blockIdx.x * C * S1;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s2[(16 * hn + 4 * G + r) * S2 + t * C + 16 * hc + i] = acc2[t][r];
+  // conv2 bias: threads sharing c8 (lane bits 0-1) -> xor over lane bits 2-5, then the 4 waves
+  float* red = reinterpret_cast<float*>(x1);  // LDS reuse (after the final barrier)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float v = db2[j];
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 8);
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane < 4) red[(wid * 4 + lane) * 8 + j] = v;
+  }
+  // conv1: lanes sharing i (lane bits 4-5 = G)
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      float v = acc1[h][k];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lane < 16) red[128 + (wid * 32 + 16 * h + lane) * 10 + k] = v;
+    }
+  __syncthreads();
+  if (tid < C) {
+    const int grp = tid >> 3, j = tid & 7;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) v += red[(w * 4 + grp) * 8 + j];
+    s2[tid * S2 + K2] = v;
+  }
+  for (int e = tid; e < C * S1; e += KT) {
+    const int ci = e / S1, k = e - ci * S1;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) v += red[128 + (w * 32 + ci) * 10 + k];
+    s1[e] = v;
+  }
+}
+
+// Slabs -> gradients.  64 outputs per workgroup, the 16 waves each sum slabs w, w + 16, ... (fixed
+// order), then a fixed-order combine in LDS.
+__global__ void __launch_bounds__(1024) kcnn_reduce_kernel(const float* __restrict__ slab2,
+                                                           const float* __restrict__ slab1, int nslab, float* g_w2,
+                                                           float* g_b2, float* g_w1, float* g_b1,
+                                                           long long* step_inc) {
+  __shared__ float part[16][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int o = blockIdx.x * 64 + lane;  // output index over [conv2 32 x 289][conv1 32 x 10]
+  const int n2 = C * S2, n1 = C * S1;
+  float s = 0.f;
+  if (o < n2 + n1) {
+    const float* src = o < n2 ? slab2 + o : slab1 + (o - n2);
+    const long long stride = o < n2 ? n2 : n1;
+    for (int q0 = wid; q0 < nslab; q0 += 16 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = q0 + 16 * u;
+        v[u] = q < nslab ? src[(long long)q * stride] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+  }
+  part[wid][lane] = s;
+  __syncthreads();
+  if (wid == 0 && o < n2 + n1) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) v += part[w][lane];
+    if (o < n2) {
+      const int n = o / S2, k = o - n * S2;
+      if (k < K2) g_w2[n * K2 + k] = v;
+      else g_b2[n] = v;
+    } else {
+      const int n = (o - n2) / S1, k = (o - n2) - n * S1;
+      if (k < 9) g_w1[n * 9 + k] = v;
+      else g_b1[n] = v;
+    }
+  }
+  if (step_inc && blockIdx.x == 0 && threadIdx.x == 0) step_inc[0] += 1;
+}
+
+}  // namespace
+
+int kcnn_blocks(int B) { return B < 512 ? B : 512; }
+size_t kcnn_slab_floats(int B) { return (size_t)kcnn_blocks(B) * C * (S2 + S1); }
+
+hipError_t kcnn_fwd(const KcnnArgs& a, hipStream_t st) {
+  if (a.B <= 0 || (!a.x_u8 && !a.x_bf) || !a.w1 || !a.b1 || !a.w2 || !a.b2 || !a.pooled || !a.code || a.kpad1 < 9)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kcnn_fwd_kernel, dim3(kcnn_blocks(a.B)), dim3(KT), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t kcnn_bwd(const KcnnArgs& a, float* g_w1, float* g_b1, float* g_w2, float* g_b2, long long* step_inc,
+                    hipStream_t st) {
+  if (a.B <= 0 || (!a.x_u8 && !a.x_bf) || !a.w1 || !a.b1 || !a.w2t || !a.dyp || !a.code || !a.slab2 || !a.slab1 ||
+      !g_w1 || !g_b1 || !g_w2 || !g_b2)
+    return hipErrorInvalidValue;
+  const int nb = kcnn_blocks(a.B);
+  hipLaunchKernelGGL(kcnn_bwd_kernel, dim3(nb), dim3(KT), 0, st, a);
+  DFA_HIP_CHECK(hipGetLastError());
+  const int outs = C * (S2 + S1);
+  hipLaunchKernelGGL(kcnn_reduce_kernel, dim3(cdiv(outs, 64)), dim3(1024), 0, st, a.slab2, a.slab1, nb, g_w2, g_b2,
+                     g_w1, g_b1, step_inc);
+  return hipGetLastError();
+}
+
+}  // namespace dfa

@@ -333,6 +333,32 @@ struct LeNetRedArgs {
   const float *w1, *w2, *m1, *m2;
   float* snap;
 };
+// The reference CNN's conv block (csrc/kcnn_fused.hip): conv1 3x3x1->32 + ReLU, conv2 3x3x32->32 + ReLU,
+// 2x2 max-pool [+ folded dropout], input 28x28x1, in one forward and one backward launch (+ reduce).
+struct KcnnArgs {
+  const uint8_t* x_u8;  // uint8 dataset [nrows][784] (read through idx), or
+  const bf16* x_bf;     // bf16 rows [.][784] (through idx with scale, or the batch itself)
+  const long long* idx;
+  long long nrows;
+  float scale;
+  const bf16* w1;   // conv1 compute copy [32][kpad1] (k = tap)
+  const float* b1;  // [32]
+  const bf16* w2;   // conv2 compute copy [32][288] (k = tap * 32 + ci)
+  const bf16* w2t;  // conv2 dgrad copy [32 ci][288] (tap * 32 + n)
+  const float* b2;
+  bf16* pooled;     // [B][144][32]
+  uint8_t* code;    // [B][144][32] argmax position 0..3, 4 = no gradient
+  const bf16* dyp;  // [B][144][32] gradient of the pooled (post-dropout) map
+  float* slab2;     // [blocks][32][289]
+  float* slab1;     // [blocks][32][10]
+  int B, kpad1;
+  DropSpec drop;
+};
+int kcnn_blocks(int B);
+size_t kcnn_slab_floats(int B);
+hipError_t kcnn_fwd(const KcnnArgs& a, hipStream_t st);
+hipError_t kcnn_bwd(const KcnnArgs& a, float* g_w1, float* g_b1, float* g_w2, float* g_b2, long long* step_inc,
+                    hipStream_t st);
 int lenet_dense_part_floats(int B);
 size_t lenet_train_lds();
 int lenet_blocks(int B);

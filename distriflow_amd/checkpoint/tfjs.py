@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from ..models.keras import keras_config_from_layers
-from ..models.layers import BatchNorm, Conv2D, ConvPoolGemm, Dense, FusedConvPool, ResidualBlock
+from ..models.layers import BatchNorm, Conv2D, ConvPoolGemm, Dense, FusedConvPool, KerasConvBlock, ResidualBlock
 
 FORMAT = "layers-model"
 GENERATED_BY = "distriflow_amd"
@@ -31,7 +31,7 @@ GENERATED_BY = "distriflow_amd"
 
 def _engine_to_keras(spec_name: str, value: torch.Tensor, layer) -> np.ndarray:
     v = value.detach().float().cpu()
-    conv = isinstance(layer, (Conv2D, FusedConvPool, ConvPoolGemm))
+    conv = isinstance(layer, (Conv2D, FusedConvPool, ConvPoolGemm, KerasConvBlock))
     if spec_name.endswith("/kernel") and conv:
         return v.permute(1, 2, 3, 0).contiguous().numpy()          # OHWI -> HWIO
     if spec_name.endswith("/kernel") and isinstance(layer, Dense):
@@ -41,7 +41,7 @@ def _engine_to_keras(spec_name: str, value: torch.Tensor, layer) -> np.ndarray:
 
 def _keras_to_engine(spec_name: str, arr: np.ndarray, layer, engine_shape) -> torch.Tensor:
     t = torch.from_numpy(np.ascontiguousarray(arr)).float()
-    conv = isinstance(layer, (Conv2D, FusedConvPool, ConvPoolGemm))
+    conv = isinstance(layer, (Conv2D, FusedConvPool, ConvPoolGemm, KerasConvBlock))
     if spec_name.endswith("/kernel") and conv:
         t = t.permute(3, 0, 1, 2)                                  # HWIO -> OHWI
     elif spec_name.endswith("/kernel") and isinstance(layer, Dense):

@@ -648,3 +648,60 @@ class ConvPoolGemm(Layer):
     def config(self):
         return self.conv.config()
 
+
+class KerasConvBlock(Layer):
+    """conv2d_1 (3x3x1 -> 32, ReLU) -> conv2d_2 (3x3x32 -> 32, ReLU) -> max_pooling2d_1 (2x2) of the
+    reference CNN (/root/reference/experiment/mnist/model.json) on 28x28x1 inputs, as one layer of two
+    launches forward / backward (csrc/kcnn_fused.hip): conv1's activation and gradient live only in LDS,
+    conv2's output only as the pooled map plus argmax codes.  Reads dataset rows through the batch index
+    (no gather launch).  A following Dropout folds in (Net._fold_dropout); the backward's reduce advances
+    the dropout step.  Parameters keep both convs' names (checkpoint-compatible).  GPU only."""
+    has_params = True
+
+    def __init__(self, conv1: "Conv2D", conv2: "Conv2D", pool: "MaxPooling2D"):
+        super().__init__(conv1.name)
+        self.conv1, self.conv2, self.pool = conv1, conv2, pool
+        self.in_shape = conv1.in_shape
+        self.out_shape = pool.out_shape
+        self.relu = False  # relu' rides in the codes
+        self.step_inc = None
+
+    @staticmethod
+    def matches(c1, c2) -> bool:
+        def conv_ok(c, shape, cin):
+            return (isinstance(c, Conv2D) and c.k == 3 and c.stride == 1 and c.pad == 0 and c.relu and c.use_bias
+                    and c.filters == 32 and tuple(c.in_shape) == shape and c.in_shape[2] == cin)
+        return conv_ok(c1, (28, 28, 1), 1) and conv_ok(c2, (26, 26, 32), 32)
+
+    def specs(self):
+        self.conv1.need_dx = False
+        self.conv2.need_dx = True  # the backward reads conv2's data-gradient weight copy
+        return self.conv1.specs() + self.conv2.specs()
+
+    def alloc(self, B, device, dtype, ws):
+        self.out = torch.empty((B,) + self.out_shape, device=device, dtype=dtype)
+        self.code = torch.empty((B,) + self.out_shape, device=device, dtype=torch.uint8)
+        self.slabs = torch.empty(ops.kcnn_slab_floats(B), dtype=torch.float32, device=device)
+        self.dx = None
+
+    def _w(self):
+        st, c1, c2 = self.store, self.conv1.name, self.conv2.name
+        return st.weight(f"{c1}/kernel"), st[f"{c1}/bias"], st.weight(f"{c2}/kernel"), st[f"{c2}/bias"]
+
+    def forward(self, x, training):
+        self.x = x
+        w1, b1, w2, b2 = self._w()
+        ops.kcnn_fwd(x, w1, b1, w2, b2, self.out, self.code, drop=self.drop_spec(training))
+        return self.out
+
+    def backward(self, dy):
+        st, c1, c2 = self.store, self.conv1.name, self.conv2.name
+        w1, b1, _, _ = self._w()
+        ops.kcnn_bwd(self.x, w1, b1, st.weight_t(f"{c2}/kernel"), dy.reshape(self.out.shape), self.code, self.slabs,
+                     st.gradient(f"{c1}/kernel"), st.gradient(f"{c1}/bias"), st.gradient(f"{c2}/kernel"),
+                     st.gradient(f"{c2}/bias"), step_inc=self.step_inc)
+        return None
+
+    def config(self):
+        return self.conv1.config()
+

@@ -17,8 +17,8 @@ import os
 import torch
 
 from .. import ops
-from .layers import (Activation, BatchNorm, Conv2D, ConvPoolGemm, Dense, Dropout, Flatten, FusedConvPool, Layer,
-                     MaxPooling2D,
+from .layers import (Activation, BatchNorm, Conv2D, ConvPoolGemm, Dense, Dropout, Flatten, FusedConvPool,
+                     KerasConvBlock, Layer, MaxPooling2D,
                      ResidualBlock)
 from .params import ParamStore
 
@@ -105,6 +105,10 @@ class Net:
             raise ValueError("empty model")
         if self.fuse:
             execd = self._fuse_conv_pool(execd)
+            if (self.is_gpu and len(execd) >= 2 and isinstance(execd[1], ConvPoolGemm) and ops.kcnn_supported()
+                    and os.environ.get("DISTRIFLOW_KCNN_FUSED", "1") != "0"
+                    and KerasConvBlock.matches(execd[0], execd[1].conv)):
+                execd = [KerasConvBlock(execd[0], execd[1].conv, execd[1].pool)] + execd[2:]
         last = execd[-1]
         if isinstance(last, Dense):
             if last.activation == "softmax":
@@ -186,7 +190,8 @@ class Net:
                     and isinstance(nxt, Dense)
                     and ((isinstance(prev, Dense) and prev.relu and not prev.out_f32)
                          or (isinstance(prev, MaxPooling2D) and prev.in_relu)
-                         or (isinstance(prev, ConvPoolGemm) and prev.conv.relu))):
+                         or (isinstance(prev, ConvPoolGemm) and prev.conv.relu)
+                         or isinstance(prev, KerasConvBlock))):
                 prev.drop = l
                 nxt.in_relu = True
                 nxt.dx_scale = 1.0 / (1.0 - l.rate)
@@ -233,7 +238,9 @@ class Net:
         if self._bound_B == B:
             return
         # split-m weight-gradient slabs: room for 4 slabs of the largest conv kernel (>= 16 MB)
-        convs = [l.conv if isinstance(l, ConvPoolGemm) else l for l in self._all_leaf_layers()]
+        convs = [c for l in self._all_leaf_layers()
+                 for c in ((l.conv,) if isinstance(l, ConvPoolGemm) else
+                           (l.conv1, l.conv2) if isinstance(l, KerasConvBlock) else (l,))]
         nk = max([l.filters * l.k * l.k * l.in_shape[2] for l in convs if isinstance(l, Conv2D)]
                  + [0])
         ws_wgrad = torch.empty(max(1 << 22, 4 * nk), dtype=torch.float32, device=self.device)
@@ -267,7 +274,7 @@ class Net:
         """Returns fp32 logits [B][classes] (a view of an engine buffer).  ``x`` is a tensor or an
         :class:`ops.GatherRef` (rows of the HBM dataset; fused into the first layer when it can)."""
         self.bind(x.shape[0])
-        if isinstance(x, ops.GatherRef) and not isinstance(self.exec_layers[0], FusedConvPool):
+        if isinstance(x, ops.GatherRef) and not isinstance(self.exec_layers[0], (FusedConvPool, KerasConvBlock)):
             x = x.materialise(self.x_buf, step_inc=self._take_gather_step())
         h = x
         for l in self.exec_layers:
@@ -298,9 +305,11 @@ class Net:
         ``labels``: int tensor [B], or an :class:`ops.LabelRef` (dataset labels + batch indices)."""
         if not isinstance(x, ops.GatherRef) and x.dtype != self.dtype:
             x = x.to(self.dtype)
-        if self.has_dropout:
+        if self.has_dropout and isinstance(self.exec_layers[0], KerasConvBlock):
+            self.exec_layers[0].step_inc = self.step_dev  # advanced by the block's backward reduce
+        elif self.has_dropout:
             if (self.is_gpu and isinstance(x, ops.GatherRef) and not self.lenet_fused
-                    and not isinstance(self.exec_layers[0], FusedConvPool)):
+                    and not isinstance(self.exec_layers[0], (FusedConvPool, KerasConvBlock))):
                 self._gather_step = self.step_dev  # advanced by the gather launch (no extra kernel)
             else:
                 self.step_dev.add_(1)
@@ -347,7 +356,7 @@ class Net:
         """Body layers one by one, then the fused dense head (2 launches: forward + CE + backward data
         chain, then all head weight gradients), then the body's backward from the head's dX."""
         self.bind(x.shape[0])
-        if isinstance(x, ops.GatherRef) and not isinstance(self.exec_layers[0], FusedConvPool):
+        if isinstance(x, ops.GatherRef) and not isinstance(self.exec_layers[0], (FusedConvPool, KerasConvBlock)):
             x = x.materialise(self.x_buf, step_inc=self._take_gather_step())
         h = x
         for l in self.exec_layers[: self.head_start]:
@@ -524,5 +533,8 @@ class Net:
             return 0
 
         for l in self._all_leaf_layers():
+            if isinstance(l, KerasConvBlock):
+                total += layer_flops(l.conv1) + layer_flops(l.conv2)
+                continue
             total += layer_flops(l)
         return total

@@ -166,6 +166,39 @@ def unpool2(dyp, code, dy):
     return dy
 
 
+def kcnn_supported() -> bool:
+    m = native.get(build_if_missing=False)
+    return m is not None and hasattr(m, "kcnn_fwd")
+
+
+def _kc_in(x):
+    if isinstance(x, GatherRef):
+        return x.data, x.idx, x.scale
+    return x, None, 1.0
+
+
+def kcnn_fwd(x, w1, b1, w2, b2, out, code, drop=None):
+    """The reference CNN's conv block forward on GPU (csrc/kcnn_fused.hip): conv1 + ReLU, conv2 + ReLU,
+    2x2 max-pool [+ folded dropout] -> pooled ``out`` [B][12][12][32] and argmax ``code``.  ``x``: a
+    :class:`GatherRef` (uint8 dataset rows, read in-kernel) or a bf16 batch [B][28][28][1]."""
+    src, idx, scale = _kc_in(x)
+    dkw = {} if drop is None else {"drop_p": float(drop[0]), "drop_seed": int(drop[1]), "drop_step": drop[2]}
+    _C().kcnn_fwd(src, idx, float(scale), int(out.shape[0]), w1, b1, int(w1.shape[1]), w2, b2, out, code, **dkw)
+    return out
+
+
+def kcnn_slab_floats(B: int) -> int:
+    return int(_C().kcnn_slab_floats(int(B)))
+
+
+def kcnn_bwd(x, w1, b1, w2t, dyp, code, slabs, g_w1, g_b1, g_w2, g_b2, step_inc=None):
+    """Both conv weight gradients of the block from the pooled gradient ``dyp`` (one backward launch +
+    one deterministic slab reduction, which also advances ``step_inc``)."""
+    src, idx, scale = _kc_in(x)
+    _C().kcnn_bwd(src, idx, float(scale), int(dyp.shape[0]), w1, b1, int(w1.shape[1]), w2t, dyp.contiguous(), code,
+                  slabs, g_w1, g_b1, g_w2, g_b2, step_inc=step_inc)
+
+
 def conv_dgrad(dy, w, wt, out, KH, KW, stride=1, pad=0, mask=None, residual=None, residual_mask=None):
     """dX (NHWC [B][H][W][C]) of a conv whose output gradient is dy [B][OH][OW][N].
 

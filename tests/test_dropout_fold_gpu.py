@@ -79,13 +79,13 @@ def test_pooled_conv_epilogue_equals_conv_then_pool(B, H, C, N, pad, drop):
 
 
 def test_keras_cnn_plan_has_no_dropout_launch():
-    from distriflow_amd.models.layers import ConvPoolGemm, Dense, Dropout, MaxPooling2D
+    from distriflow_amd.models.layers import ConvPoolGemm, Dense, Dropout, KerasConvBlock, MaxPooling2D
     from distriflow_amd.models.zoo import build_model
 
     net = build_model("keras_cnn", device=dev, seed=0)
     kinds = [type(l) for l in net.exec_layers]
     assert Dropout not in kinds and MaxPooling2D not in kinds
-    pool = next(l for l in net.exec_layers if isinstance(l, ConvPoolGemm))
+    pool = next(l for l in net.exec_layers if isinstance(l, (ConvPoolGemm, KerasConvBlock)))
     assert pool.drop is not None and pool.drop.rate == 0.25
     dense = [l for l in net.exec_layers if isinstance(l, Dense)]
     assert dense[0].drop is not None and dense[0].in_relu and abs(dense[0].dx_scale - 1 / 0.75) < 1e-12

@@ -236,6 +236,7 @@ def test_per_layer_numerics_against_cpu(name, B, monkeypatch):
     monkeypatch.setenv("DISTRIFLOW_LENET_FUSED", "0")  # the per-layer kernels (the fused one: test_lenet_fused_gpu)
     # layer-for-layer pairing with the CPU plan (folded dropouts: tests/test_dropout_fold_gpu.py)
     monkeypatch.setenv("DISTRIFLOW_FOLD_DROPOUT", "0")
+    monkeypatch.setenv("DISTRIFLOW_KCNN_FUSED", "0")  # the fused conv block: tests/test_kcnn_fused_gpu.py
     g = build_model(name, device="cuda", seed=3)
     layers, shape = MODELS[name]()
     c = Net(layers, shape, device="cpu", name=name, seed=3, compute_dtype=torch.bfloat16)

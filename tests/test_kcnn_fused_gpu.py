@@ -1,0 +1,79 @@
+"""The reference CNN's fused conv block (csrc/kcnn_fused.hip) against the per-layer kernels it replaces
+(conv1 image-resident kernel, conv2 igemm64 with the pooled epilogue, unpool + conv2 weight / data
+gradient + conv1 weight gradient): the forward (pooled map, codes, hence the loss and every dense-layer
+gradient) is equal bit for bit, the two conv layers' weight gradients agree to fp32 summation order."""
+import pytest
+import torch
+
+from distriflow_amd import ops
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda", 0)
+
+
+def _pair(monkeypatch, seed=3):
+    from distriflow_amd.models.layers import KerasConvBlock
+    from distriflow_amd.models.zoo import build_model
+
+    f = build_model("keras_cnn", device=dev, seed=seed)
+    assert isinstance(f.exec_layers[0], KerasConvBlock)
+    monkeypatch.setenv("DISTRIFLOW_KCNN_FUSED", "0")
+    p = build_model("keras_cnn", device=dev, seed=seed)
+    monkeypatch.delenv("DISTRIFLOW_KCNN_FUSED")
+    assert not isinstance(p.exec_layers[0], KerasConvBlock)
+    p.store.set_flat(f.store.master.clone())
+    return f, p
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / (b.double().norm() + 1e-30))
+
+
+@pytest.mark.parametrize("B", [64, 200])
+def test_kcnn_block_matches_per_layer_path(monkeypatch, B):
+    from distriflow_amd.data.synthetic import synthetic_mnist
+
+    f, p = _pair(monkeypatch)
+    data, labels = synthetic_mnist(4096, seed=5, device=dev)
+    idx = torch.randperm(4096, device=dev)[:B]
+    x, y = ops.GatherRef(data, idx, 1 / 255.0, (28, 28, 1)), ops.LabelRef(labels, idx)
+    # same dropout masks: the fused step reads the counter before advancing it, the per-layer step's
+    # gather advances it first
+    f.step_dev.fill_(5)
+    p.step_dev.fill_(4)
+    sf = f.compute_gradients(x, y).clone()
+    sp = p.compute_gradients(x, y).clone()
+    torch.cuda.synchronize()
+    assert int(f.step_dev.item()) == 6 and int(p.step_dev.item()) == 5
+    assert torch.equal(f.exec_layers[0].out, p.exec_layers[1].out)  # pooled (+ dropout) map
+    assert torch.equal(f.exec_layers[0].code, p.exec_layers[1].code)
+    assert torch.equal(sf, sp)
+    for s in f.store.specs:
+        gf, gp = f.store.gradient(s.name), p.store.gradient(s.name)
+        if s.name.startswith("conv2d"):
+            assert _rel(gf, gp) < 2e-3, (s.name, _rel(gf, gp))
+        else:
+            assert torch.equal(gf, gp), s.name
+
+
+def test_kcnn_block_bf16_batch_input_and_training(monkeypatch):
+    """A bf16 batch (no index) takes the same path; a few SGD steps reduce the loss."""
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
+
+    f, p = _pair(monkeypatch)
+    data, labels = synthetic_mnist(2048, seed=1, device=dev)
+    xb = (data[:96].float() / 255.0).to(torch.bfloat16)
+    yb = labels[:96]
+    f.step_dev.fill_(2)  # read, then advanced by the block's reduce
+    p.step_dev.fill_(1)  # advanced (torch add) before the per-layer step reads it
+    sf = f.compute_gradients(xb, yb).clone()
+    sp = p.compute_gradients(xb, yb).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(sf, sp)
+    tr = DataParallelTrainer(f, lr=0.05, graph="full")
+    tr.bind_dataset(data, labels, 256, scale=1.0 / 255.0)
+    tr.bind_index_stream(epoch_permutations(2048, 256, 30, dev, seed=0))
+    losses = [float(tr.step()[0].item()) / 256 for _ in range(30)]
+    assert tr.graph_mode == "full"
+    assert sum(losses[-5:]) < 0.9 * sum(losses[:5]), losses
