@@ -37,21 +37,22 @@ void fill_geom(std::vector<int64_t> g, int* dst) {
   for (int i = 0; i < 9; ++i) dst[i] = (int)g[i];
 }
 
-dfa::DropSpec drop_from(double p, int64_t seed, const c10::optional<torch::Tensor>& step) {
+dfa::DropSpec drop_from(double p, int64_t seed, const c10::optional<torch::Tensor>& step, int64_t step_add) {
   TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0,1)");
   const long long* sp = nullptr;
   if (step.has_value() && step->defined()) {
     need(*step, at::kLong, "dropout step");
     sp = reinterpret_cast<const long long*>(step->data_ptr());
   }
-  return dfa::make_drop((float)p, (unsigned long long)seed, sp);
+  return dfa::make_drop((float)p, (unsigned long long)seed, sp, (int)step_add);
 }
 
 void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tensor> bias,
                   c10::optional<torch::Tensor> mask, torch::Tensor out, int64_t M, int64_t N, int64_t K, int64_t Kpad,
                   int64_t lda, int64_t ldc, std::vector<int64_t> geom, int64_t mode, bool relu, double alpha,
                   c10::optional<torch::Tensor> res, c10::optional<torch::Tensor> resmask, double drop_p,
-                  int64_t drop_seed, c10::optional<torch::Tensor> drop_step, c10::optional<torch::Tensor> pool_code) {
+                  int64_t drop_seed, c10::optional<torch::Tensor> drop_step, c10::optional<torch::Tensor> pool_code,
+                  int64_t drop_step_add) {
   need(src, at::kBFloat16, "src");
   need(w, at::kBFloat16, "w");
   TORCH_CHECK(out.is_cuda() && out.is_contiguous(), "out must be a contiguous GPU tensor");
@@ -110,7 +111,7 @@ void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tenso
   a.relu = relu ? 1 : 0;
   a.out_f32 = out.scalar_type() == at::kFloat ? 1 : 0;
   a.alpha = (float)alpha;
-  a.drop = drop_from(drop_p, drop_seed, drop_step);
+  a.drop = drop_from(drop_p, drop_seed, drop_step, drop_step_add);
   if (pooled) {
     a.pool_code = pool_code->data_ptr<uint8_t>();
     TORCH_CHECK(dfa::igemm64_pool_supported(a), "pooled conv: unsupported geometry / alignment");
@@ -164,13 +165,13 @@ void igemm_wgrad_py(torch::Tensor dy, torch::Tensor src, torch::Tensor gw, c10::
 }
 
 void maxpool_fwd_py(torch::Tensor x, torch::Tensor y, int64_t B, int64_t H, int64_t W, int64_t C, int64_t P,
-                    double drop_p, int64_t drop_seed, c10::optional<torch::Tensor> drop_step) {
+                    double drop_p, int64_t drop_seed, c10::optional<torch::Tensor> drop_step, int64_t drop_step_add) {
   need(x, at::kBFloat16, "x");
   need(y, at::kBFloat16, "y");
   TORCH_CHECK(P > 0 && H >= P && W >= P, "bad pool geometry");
   TORCH_CHECK(x.numel() >= B * H * W * C && y.numel() >= B * (H / P) * (W / P) * C, "pool buffers too small");
   check_hip(dfa::maxpool_fwd((const dfa::bf16*)x.data_ptr(), (dfa::bf16*)y.data_ptr(), B, H, W, C, P, cur_stream(),
-                             drop_from(drop_p, drop_seed, drop_step)),
+                             drop_from(drop_p, drop_seed, drop_step, drop_step_add)),
             "maxpool_fwd");
 }
 
@@ -933,7 +934,8 @@ static dfa::KcnnArgs kcnn_args(torch::Tensor x, c10::optional<torch::Tensor> idx
 
 void kcnn_fwd_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double scale, int64_t B, torch::Tensor w1,
                  torch::Tensor b1, int64_t kpad1, torch::Tensor w2, torch::Tensor b2, torch::Tensor pooled,
-                 torch::Tensor code, double drop_p, int64_t drop_seed, c10::optional<torch::Tensor> drop_step) {
+                 torch::Tensor code, double drop_p, int64_t drop_seed, c10::optional<torch::Tensor> drop_step,
+                 int64_t drop_step_add) {
   dfa::KcnnArgs a = kcnn_args(x, idx, scale, B, w1, b1, kpad1, code);
   need(w2, at::kBFloat16, "kcnn w2");
   need(b2, at::kFloat, "kcnn b2");
@@ -942,7 +944,7 @@ void kcnn_fwd_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double scale
   a.w2 = reinterpret_cast<const dfa::bf16*>(w2.data_ptr());
   a.b2 = b2.data_ptr<float>();
   a.pooled = reinterpret_cast<dfa::bf16*>(pooled.data_ptr());
-  a.drop = drop_from(drop_p, drop_seed, drop_step);
+  a.drop = drop_from(drop_p, drop_seed, drop_step, drop_step_add);
   check_hip(dfa::kcnn_fwd(a, cur_stream()), "kcnn_fwd");
 }
 
@@ -1280,7 +1282,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias"), py::arg("mask"), py::arg("out"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("Kpad"),
         py::arg("lda"), py::arg("ldc"), py::arg("geom"), py::arg("mode"), py::arg("relu"), py::arg("alpha"),
         py::arg("res") = py::none(), py::arg("resmask") = py::none(), py::arg("drop_p") = 0.0,
-        py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pool_code") = py::none());
+        py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pool_code") = py::none(),
+        py::arg("drop_step_add") = 0);
   m.def("igemm64_pool_supported", [](int64_t H, int64_t W, int64_t C, int64_t OH, int64_t OW, int64_t K, int64_t N) {
     dfa::IGemmArgs a{};
     a.SH = (int)H; a.SW = (int)W; a.SC = (int)C; a.OH = (int)OH; a.OW = (int)OW; a.M = 4; a.N = (int)N; a.ldc = (int)N;
@@ -1305,7 +1308,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("igemm_wgrad", &igemm_wgrad_py, "implicit-GEMM MFMA weight gradient (split-m slabs + reduce)");
   m.def("maxpool_fwd", &maxpool_fwd_py, py::arg("x"), py::arg("y"), py::arg("B"), py::arg("H"), py::arg("W"),
         py::arg("C"), py::arg("P"), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0,
-        py::arg("drop_step") = py::none());
+        py::arg("drop_step") = py::none(), py::arg("drop_step_add") = 0);
   m.def("maxpool_bwd", &maxpool_bwd_py);
   m.def("softmax_ce", &softmax_ce_py);
   m.def("dropout", &dropout_py);
@@ -1366,11 +1369,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("kcnn_fwd", &kcnn_fwd_py, "reference CNN conv block forward (conv1 + conv2 + pool [+ dropout], 1 launch)",
         py::arg("x"), py::arg("idx"), py::arg("scale"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("kpad1"),
         py::arg("w2"), py::arg("b2"), py::arg("pooled"), py::arg("code"), py::arg("drop_p") = 0.0,
-        py::arg("drop_seed") = 0, py::arg("drop_step") = py::none());
+        py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("drop_step_add") = 0);
   m.def("kcnn_bwd", &kcnn_bwd_py, "reference CNN conv block backward (both weight gradients, 2 launches)",
         py::arg("x"), py::arg("idx"), py::arg("scale"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("kpad1"),
         py::arg("w2t"), py::arg("dyp"), py::arg("code"), py::arg("slabs"), py::arg("g_w1"), py::arg("g_b1"),
         py::arg("g_w2"), py::arg("g_b2"), py::arg("step_inc") = py::none());
+  m.def("kcnn_set_debug", &dfa::kcnn_set_debug, "measurement aid: skip parts of the conv-block backward");
   m.def("kcnn_slab_floats", [](int64_t B) { return (int64_t)dfa::kcnn_slab_floats((int)B); });
   m.def("classifier_metrics", &classifier_metrics_py, "[loss sum, correct] of a classifier batch (one launch)");
   m.def("lenet_train", &lenet_train_py, "whole-network LeNet-5 training step (fwd + CE + bwd, 2 launches)",

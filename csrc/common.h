@@ -92,8 +92,8 @@ __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
 }
 
 // Folded dropout (kernels.h DropSpec): the per-launch seed and the keep test of element i
-__device__ __forceinline__ unsigned long long drop_seed(unsigned long long seed0, const long long* step) {
-  return seed0 ^ (step ? (unsigned long long)step[0] * 0x9E3779B1ull : 0ull);
+__device__ __forceinline__ unsigned long long drop_seed(unsigned long long seed0, const long long* step, int add = 0) {
+  return seed0 ^ (step ? (unsigned long long)(step[0] + add) * 0x9E3779B1ull : 0ull);
 }
 __device__ __forceinline__ bool drop_keep(unsigned long long seed, unsigned thresh, long long i) {
   return hash_u32(seed, (uint64_t)i) >= thresh;

@@ -285,7 +285,7 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
 
   if (POOL) {
     typedef __bf16 bf16x4_p __attribute__((ext_vector_type(4)));
-    const unsigned long long dseed = a.drop.on ? drop_seed(a.drop.seed, a.drop.step) : 0ull;
+    const unsigned long long dseed = a.drop.on ? drop_seed(a.drop.seed, a.drop.step, a.drop.step_add) : 0ull;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int row = m0 + wm * TM * 16 + i * 16 + fr;  // the window's rows are lanes fr & ~3 .. + 3
@@ -367,7 +367,7 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
             if (!((float)mk[r] > 0.f)) v[r] = 0.f;
         }
         if (a.drop.on) {
-          const unsigned long long ds = drop_seed(a.drop.seed, a.drop.step);
+          const unsigned long long ds = drop_seed(a.drop.seed, a.drop.step, a.drop.step_add);
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = drop_keep(ds, a.drop.thresh, o + r) ? (float)f2bf(v[r]) * a.drop.scale : 0.f;
         }
@@ -392,7 +392,7 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
         if (a.relu) x = fmaxf(x, 0.f);
         if (a.mask && !((float)a.mask[o + r] > 0.f)) x = 0.f;
         if (a.drop.on)
-          x = drop_keep(drop_seed(a.drop.seed, a.drop.step), a.drop.thresh, o + r) ? (float)f2bf(x) * a.drop.scale : 0.f;
+          x = drop_keep(drop_seed(a.drop.seed, a.drop.step, a.drop.step_add), a.drop.thresh, o + r) ? (float)f2bf(x) * a.drop.scale : 0.f;
         if (a.out_f32)
           reinterpret_cast<float*>(a.out)[o + r] = x;
         else
@@ -436,7 +436,7 @@ __global__ void __launch_bounds__(256) igemm64_splitk_epilogue_kernel(IGemmArgs 
         if (!((float)mk[r] > 0.f)) v[r] = 0.f;
     }
     if (a.drop.on) {
-      const unsigned long long ds = drop_seed(a.drop.seed, a.drop.step);
+      const unsigned long long ds = drop_seed(a.drop.seed, a.drop.step, a.drop.step_add);
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = drop_keep(ds, a.drop.thresh, o + r) ? (float)f2bf(v[r]) * a.drop.scale : 0.f;
     }

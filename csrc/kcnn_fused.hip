@@ -46,6 +46,10 @@ constexpr int NP0 = H0 * H0, NP1 = H1 * H1, NP2 = H2 * H2, NPP = PW * PW;  // 78
 constexpr int K2 = 9 * C;                                                   // 288
 constexpr int S2 = K2 + 1, S1 = 10;  // slab row lengths: conv2 (288 + bias), conv1 (9 + bias)
 
+// measurement aid (kcnn_set_debug): bit 0 skips the conv2 weight gradient, bit 1 the data gradient +
+// conv1 weight gradient, bit 2 the conv1 recompute, bit 3 the dY2 expansion (results are then wrong)
+int g_kcnn_debug = 0;
+
 typedef __bf16 bf16x4_vs __attribute__((__vector_size__(8)));
 
 __device__ __forceinline__ bf16x4 tr_read(const bf16* p) {
@@ -65,10 +69,16 @@ __device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
 }
 __device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-// [pixel][32] bf16 LDS maps with the 16-byte chunk index XOR-swizzled by the pixel: the 16 pixels one
-// fragment read touches spread over more bank groups.  Element (pix, ch); a 4- or 8-element piece
-// starting at ch % 4 == 0 stays inside one chunk.
-__device__ __forceinline__ int xs(int pix, int ch) { return pix * C + ((((ch >> 3) ^ ((pix >> 1) & 3))) << 3) + (ch & 7); }
+// [pixel][32] bf16 LDS maps (X1 26x26, dY2 24x24) with the 16-byte chunk index XOR-swizzled by the
+// pixel's image row: f(row) = 2 (row & 1) + ((row >> 1) & 1).  The transposed 4-row reads of the weight
+// gradient (4 consecutive pixels of one row per 16-lane group, adjacent rows in the two groups of a
+// half-wave) then hit disjoint bank halves, and the 16-byte reads of a 4x4 pixel tile spread over all
+// 64 banks.  Since f depends on row & 3 only, the swizzle of a lane's pixel folds into constants when
+// the tile origin row is a multiple of 4.
+__device__ __forceinline__ int swf(int row) { return ((row & 1) << 1) | ((row >> 1) & 1); }
+__device__ __forceinline__ int xsr(int pix, int row, int ch) {
+  return pix * C + ((((ch >> 3) ^ swf(row))) << 3) + (ch & 7);
+}
 
 __device__ __forceinline__ long long src_row(const KcnnArgs& a, int b) {
   if (!a.idx) return b;
@@ -76,14 +86,31 @@ __device__ __forceinline__ long long src_row(const KcnnArgs& a, int b) {
   return r < 0 ? 0 : (r >= a.nrows ? a.nrows - 1 : r);
 }
 
-// x0 of image b as bf16 (the gather kernel's rounding: bf16(u8 * scale))
-__device__ __forceinline__ void stage_x0(const KcnnArgs& a, int b, bf16* x0) {
+// x0 of image b as bf16 (the gather kernel's rounding: bf16(u8 * scale)), in two halves so that the
+// next image's loads are in flight while the current one is processed
+constexpr int X0_PER = (NP0 + KT - 1) / KT;  // 4 elements per thread
+struct X0Regs {
+  float v[X0_PER];
+};
+__device__ __forceinline__ X0Regs load_x0(const KcnnArgs& a, int b) {
+  X0Regs r;
+  if (b >= a.B) return r;
   const long long row = src_row(a, b);
-  for (int e = threadIdx.x; e < NP0; e += KT) {
+#pragma unroll
+  for (int u = 0; u < X0_PER; ++u) {
+    const int e = min((int)threadIdx.x + KT * u, NP0 - 1);
     if (a.x_u8)
-      x0[e] = f2bf((float)a.x_u8[row * NP0 + e] * a.scale);
+      r.v[u] = (float)a.x_u8[row * NP0 + e] * a.scale;
     else
-      x0[e] = a.idx ? f2bf((float)a.x_bf[row * NP0 + e] * a.scale) : a.x_bf[row * NP0 + e];
+      r.v[u] = a.idx ? (float)a.x_bf[row * NP0 + e] * a.scale : (float)a.x_bf[row * NP0 + e];
+  }
+  return r;
+}
+__device__ __forceinline__ void store_x0(const X0Regs& r, bf16* x0) {
+#pragma unroll
+  for (int u = 0; u < X0_PER; ++u) {
+    const int e = threadIdx.x + KT * u;
+    if (e < NP0) x0[e] = f2bf(r.v[u]);
   }
 }
 
@@ -114,7 +141,7 @@ __device__ __forceinline__ void conv1_to_lds(const KcnnArgs& a, const bf16* x0, 
       for (int k = 0; k < 9; ++k) acc = fmaf(xv[k], w[j][k], acc);
       o[j] = f2bf(fmaxf(acc * 1.f + bias[j], 0.f));
     }
-    *reinterpret_cast<bf16x8*>(x1 + xs(p, 8 * g)) = o;
+    *reinterpret_cast<bf16x8*>(x1 + xsr(p, oy, 8 * g)) = o;
   }
 }
 
@@ -129,11 +156,13 @@ __global__ void __launch_bounds__(KT, 2) kcnn_fwd_kernel(KcnnArgs a) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) bw[t][h] = ld8(a.w2 + (16 * h + i) * K2 + t * C + 8 * G);
   const float bias2[2] = {a.b2[i], a.b2[16 + i]};
-  const unsigned long long dseed = a.drop.on ? drop_seed(a.drop.seed, a.drop.step) : 0ull;
+  const unsigned long long dseed = a.drop.on ? drop_seed(a.drop.seed, a.drop.step, a.drop.step_add) : 0ull;
   // this lane's A row in a tile of 4 windows: window j = i >> 2, position r = i & 3
   const int jw = i >> 2, rp = i & 3;
+  X0Regs xr = load_x0(a, blockIdx.x);
   for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
-    stage_x0(a, b, x0);
+    store_x0(xr, x0);
+    xr = load_x0(a, b + gridDim.x);  // next image: in flight during this one
     __syncthreads();
     conv1_to_lds(a, x0, x1);
     __syncthreads();
@@ -145,7 +174,7 @@ __global__ void __launch_bounds__(KT, 2) kcnn_fwd_kernel(KcnnArgs a) {
       for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
-          const bf16x8 af = ld8(x1 + xs((oy + ky) * H1 + ox + kx, 8 * G));
+          const bf16x8 af = ld8(x1 + xsr((oy + ky) * H1 + ox + kx, oy + ky, 8 * G));
           acc[0] = mfma16x16x32(af, bw[3 * ky + kx][0], acc[0]);
           acc[1] = mfma16x16x32(af, bw[3 * ky + kx][1], acc[1]);
         }
@@ -175,7 +204,7 @@ __global__ void __launch_bounds__(KT, 2) kcnn_fwd_kernel(KcnnArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
+__global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a, int dbg) {
   __shared__ __attribute__((aligned(16))) bf16 x0[NP0];
   __shared__ __attribute__((aligned(16))) bf16 x1[NP1 * C];
   __shared__ __attribute__((aligned(16))) bf16 dy2[NP2 * C];
@@ -190,17 +219,15 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
   float db2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) db2[j] = 0.f;
-  float acc1[2][10];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int k = 0; k < 10; ++k) acc1[h][k] = 0.f;
+  f32x4 acc1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // conv1 D[ci = 16h + 4G + r][tap1 = i]
   const int c8 = tid & 3;  // this thread's 8-channel group in the dY2 expansion (256 % 4 == 0)
 
+  X0Regs xr = load_x0(a, blockIdx.x);
   for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
     // ---- stage x0; expand dY2 from the pooled gradient and the codes (conv2 bias gradient on the way)
-    stage_x0(a, b, x0);
-    for (int e = tid; e < NPP * 4; e += KT) {
+    store_x0(xr, x0);
+    xr = load_x0(a, b + gridDim.x);
+    for (int e = tid; e < ((dbg & 8) ? 0 : NPP * 4); e += KT) {
       const int q = e >> 2;
       const long long o = ((long long)b * NPP + q) * C + 8 * c8;
       const bf16x8 gv = ld8(a.dyp + o);
@@ -215,77 +242,104 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
           ov[j] = cd == (unsigned)p ? gv[j] : (bf16)0.f;
           if (cd == (unsigned)p) db2[j] += (float)gv[j];
         }
-        const int pix = (2 * ph + (p >> 1)) * H2 + 2 * pw + (p & 1);
-        *reinterpret_cast<bf16x8*>(dy2 + xs(pix, 8 * c8)) = ov;
+        const int py = 2 * ph + (p >> 1);
+        *reinterpret_cast<bf16x8*>(dy2 + xsr(py * H2 + 2 * pw + (p & 1), py, 8 * c8)) = ov;
       }
     }
     __syncthreads();
-    conv1_to_lds(a, x0, x1);
+    if (!(dbg & 4)) conv1_to_lds(a, x0, x1);
     __syncthreads();
 
-    // ---- conv2 weight gradient: D[n][(tap, ci)] += dY2^T[n][p] X1[p + tap][ci], 18 blocks of 32 pixels
-    for (int k0 = 0; k0 < NP2 / 32; ++k0) {
-      int pb[2], pa[2];
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        const int P = k0 * 32 + 8 * G + 4 * hf + (i >> 2);
-        const int oy = P / H2, ox = P - oy * H2;
-        pa[hf] = P;
-        pb[hf] = oy * H1 + ox;
-      }
-      const bf16x8 af = cat8(tr_read(dy2 + xs(pa[0], 16 * hn + 4 * (i & 3))),
-                             tr_read(dy2 + xs(pa[1], 16 * hn + 4 * (i & 3))));
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int d = ky * H1 + kx;
-          const bf16x8 bf = cat8(tr_read(x1 + xs(pb[0] + d, 16 * hc + 4 * (i & 3))),
-                                 tr_read(x1 + xs(pb[1] + d, 16 * hc + 4 * (i & 3))));
-          acc2[3 * ky + kx] = mfma16x16x32(af, bf, acc2[3 * ky + kx]);
+    // ---- conv2 weight gradient: D[n][(tap, ci)] += dY2^T[n][p] X1[p + tap][ci] over 18 blocks of 32 output
+    // pixels, block = 4 rows x 8 columns: k slot 8G + 4hf + r is pixel (oy0 + G, ox0 + 4hf + r), so the
+    // lane's addresses are a per-block uniform offset plus lane / tap constants
+    {
+      const int q = i >> 2, cq = 4 * (i & 3);
+#pragma unroll 1
+      for (int k0 = 0; k0 < ((dbg & 1) ? 0 : NP2 / 32); ++k0) {
+        const int oy0 = 4 * (k0 / 3), ox0 = 8 * (k0 % 3);
+        bf16x8 af;
+        {
+          const int row = oy0 + G;
+          const bf16x4 lo = tr_read(dy2 + xsr(row * H2 + ox0 + q, row, 16 * hn + cq));
+          const bf16x4 hi = tr_read(dy2 + xsr(row * H2 + ox0 + 4 + q, row, 16 * hn + cq));
+          af = cat8(lo, hi);
         }
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const int row = oy0 + G + ky;
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const bf16x4 lo = tr_read(x1 + xsr(row * H1 + ox0 + q + kx, row, 16 * hc + cq));
+            const bf16x4 hi = tr_read(x1 + xsr(row * H1 + ox0 + 4 + q + kx, row, 16 * hc + cq));
+            acc2[3 * ky + kx] = mfma16x16x32(af, cat8(lo, hi), acc2[3 * ky + kx]);
+          }
+        }
+      }
     }
 
-    // ---- conv2 data gradient x relu'(X1) -> conv1 weight gradient, 43 tiles of 16 X1 pixels
+    // ---- conv2 data gradient x relu'(X1) over 4x4 pixel tiles of X1 (7 x 7 tiles cover 26 x 26), and the
+    // conv1 weight gradient on MFMA from pairs of tiles: D1[ci][tap1] += g[ci][pixel] x0[pixel + tap1]
+    // (tap1 = 9 is the bias: a ones column).  A row i = pixel (4ty + i/4, 4tx + i%4); the dgrad D layout
+    // puts pixels (4ty + G, 4tx + r) of channel 16h + i in lane (G, i), which is already the conv1 A
+    // fragment of two tiles (k slot 8G + e: tile e / 4, column e % 4).
     {
       bf16x8 bt[9][2];  // B[k = (tap, n = 8G..8G+7)][ci = 16h + i] from the dgrad copy [ci][tap * 32 + n]
 #pragma unroll
       for (int t = 0; t < 9; ++t)
 #pragma unroll
         for (int h = 0; h < 2; ++h) bt[t][h] = ld8(a.w2t + (16 * h + i) * K2 + t * C + 8 * G);
-      for (int T = wid; T < (NP1 + 15) / 16; T += 4) {
-        const int X = T * 16 + i;
-        const int iy = X / H1, ix = X - iy * H1;
-        f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      const int ty1 = i / 3, tx1 = i - 3 * (i / 3);  // this lane's conv1 tap (column of the conv1 B operand)
+#pragma unroll 1
+      for (int T0 = wid; T0 < ((dbg & 2) ? 0 : 49); T0 += 8) {
+        bf16 gv[2][2][4];  // [tile of the pair][h][r]
+        int py[2], px0[2];
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
+        for (int u = 0; u < 2; ++u) {
+          const int T = T0 + 4 * u;
+          const int ty = T / 7, tx = T - 7 * (T / 7);
+          const int iy = 4 * ty + (i >> 2), ix = 4 * tx + (i & 3);
+          f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+          if (T < 49) {
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            const int sy = iy - ky, sx = ix - kx;
-            const bool ok = X < NP1 && (unsigned)sy < (unsigned)H2 && (unsigned)sx < (unsigned)H2;
-            const bf16x8 af = ld8(ok ? dy2 + xs(sy * H2 + sx, 8 * G) : zc);
-            acc[0] = mfma16x16x32(af, bt[3 * ky + kx][0], acc[0]);
-            acc[1] = mfma16x16x32(af, bt[3 * ky + kx][1], acc[1]);
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+              for (int kx = 0; kx < 3; ++kx) {
+                const int sy = iy - ky, sx = ix - kx;
+                const bool ok = iy < H1 && ix < H1 && (unsigned)sy < (unsigned)H2 && (unsigned)sx < (unsigned)H2;
+                const bf16x8 af = ld8(ok ? dy2 + xsr(sy * H2 + sx, sy, 8 * G) : zc);
+                acc[0] = mfma16x16x32(af, bt[3 * ky + kx][0], acc[0]);
+                acc[1] = mfma16x16x32(af, bt[3 * ky + kx][1], acc[1]);
+              }
           }
-        // lane holds pixels T*16 + 4G + r, channel 16h + i
+          const int ry = 4 * ty + G;
+          py[u] = ry < H1 ? ry : H1 - 1;
+          px0[u] = 4 * tx;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int Xr = T * 16 + 4 * G + r;
-          if (Xr >= NP1) continue;
-          const int ry = Xr / H1, rx = Xr - ry * H1;
-          float xv[9];
+          for (int r = 0; r < 4; ++r) {
+            const int rx = 4 * tx + r;
+            const bool valid = T < 49 && ry < H1 && rx < H1;
 #pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-            for (int kx = 0; kx < 3; ++kx) xv[3 * ky + kx] = (float)x0[(ry + ky) * H0 + rx + kx];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const bool live = (float)x1[xs(Xr, 16 * h + i)] > 0.f;
-            const float gval = live ? (float)f2bf(acc[h][r]) : 0.f;
-#pragma unroll
-            for (int k = 0; k < 9; ++k) acc1[h][k] = fmaf(gval, xv[k], acc1[h][k]);
-            acc1[h][9] += gval;
+            for (int h = 0; h < 2; ++h) {
+              const bool live = valid && (float)x1[xsr(ry * H1 + rx, ry, 16 * h + i)] > 0.f;
+              gv[u][h][r] = live ? f2bf(acc[h][r]) : (bf16)0.f;
+            }
           }
+        }
+        // conv1 B operand: B[8G + e][tap1 = i] = x0 at (pixel e) + tap1, 1 for the bias column
+        bf16x8 bx;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int u = e >> 2;
+          const int cx = min(px0[u] + (e & 3), H1 - 1);
+          bx[e] = i < 9 ? x0[(py[u] + ty1) * H0 + cx + tx1] : (i == 9 ? (bf16)1.f : (bf16)0.f);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          bf16x8 ag;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ag[e] = gv[e >> 2][h][e & 3];
+          acc1[h] = mfma16x16x32(ag, bx, acc1[h]);
         }
       }
     }
@@ -310,16 +364,13 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
     v += __shfl_xor(v, 32);
     if (lane < 4) red[(wid * 4 + lane) * 8 + j] = v;
   }
-  // conv1: lanes sharing i (lane bits 4-5 = G)
+  // conv1: lane (G, i) owns ci = 16h + 4G + r, tap1 = i (< 10); the 4 waves are summed below
+  if (i < S1) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      float v = acc1[h][k];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      if (lane < 16) red[128 + (wid * 32 + 16 * h + lane) * 10 + k] = v;
-    }
+      for (int r = 0; r < 4; ++r) red[128 + (wid * 32 + 16 * h + 4 * G + r) * 10 + i] = acc1[h][r];
+  }
   __syncthreads();
   if (tid < C) {
     const int grp = tid >> 3, j = tid & 7;
@@ -383,6 +434,7 @@ __global__ void __launch_bounds__(1024) kcnn_reduce_kernel(const float* __restri
 
 }  // namespace
 
+void kcnn_set_debug(int mask) { g_kcnn_debug = mask; }
 int kcnn_blocks(int B) { return B < 512 ? B : 512; }
 size_t kcnn_slab_floats(int B) { return (size_t)kcnn_blocks(B) * C * (S2 + S1); }
 
@@ -399,7 +451,7 @@ hipError_t kcnn_bwd(const KcnnArgs& a, float* g_w1, float* g_b1, float* g_w2, fl
       !g_w1 || !g_b1 || !g_w2 || !g_b2)
     return hipErrorInvalidValue;
   const int nb = kcnn_blocks(a.B);
-  hipLaunchKernelGGL(kcnn_bwd_kernel, dim3(nb), dim3(KT), 0, st, a);
+  hipLaunchKernelGGL(kcnn_bwd_kernel, dim3(nb), dim3(KT), 0, st, a, g_kcnn_debug);
   DFA_HIP_CHECK(hipGetLastError());
   const int outs = C * (S2 + S1);
   hipLaunchKernelGGL(kcnn_reduce_kernel, dim3(cdiv(outs, 64)), dim3(1024), 0, st, a.slab2, a.slab1, nb, g_w2, g_b2,

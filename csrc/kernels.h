@@ -21,8 +21,9 @@ struct DropSpec {
   float p, scale;   // scale = 1 / (1 - p)
   unsigned long long seed;
   const long long* step;  // device step counter (nullable)
+  int step_add;           // masks use step[0] + step_add (1 when the counter advances at the END of a step)
 };
-inline DropSpec make_drop(float p, unsigned long long seed, const long long* step) {
+inline DropSpec make_drop(float p, unsigned long long seed, const long long* step, int step_add = 0) {
   DropSpec d{};
   if (p > 0.f) {
     d.on = 1;
@@ -31,6 +32,7 @@ inline DropSpec make_drop(float p, unsigned long long seed, const long long* ste
     d.scale = 1.f / (1.f - p);
     d.seed = seed;
     d.step = step;
+    d.step_add = step_add;
   }
   return d;
 }
@@ -355,6 +357,7 @@ struct KcnnArgs {
   DropSpec drop;
 };
 int kcnn_blocks(int B);
+void kcnn_set_debug(int mask);
 size_t kcnn_slab_floats(int B);
 hipError_t kcnn_fwd(const KcnnArgs& a, hipStream_t st);
 hipError_t kcnn_bwd(const KcnnArgs& a, float* g_w1, float* g_b1, float* g_w2, float* g_b2, long long* step_inc,

@@ -18,7 +18,7 @@ namespace dfa {
 template <bool VEC>
 __global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int B, int H, int W,
                                    int C, int OH, int OW, int P, DropSpec drop) {
-  const unsigned long long ds = drop.on ? drop_seed(drop.seed, drop.step) : 0ull;
+  const unsigned long long ds = drop.on ? drop_seed(drop.seed, drop.step, drop.step_add) : 0ull;
   const int CC = VEC ? C / 8 : C;
   const long long total = (long long)B * OH * OW * CC;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;

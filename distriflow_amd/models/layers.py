@@ -280,6 +280,7 @@ class Dropout(Layer):
         self.rate = float(rate)
         self.base_seed = seed
         self.step = 0
+        self.step_add = 0  # 1 when the engine advances the step counter at the end of the step
         self.active = False
 
     def _seed(self):
@@ -287,7 +288,7 @@ class Dropout(Layer):
 
     def spec(self):
         """(rate, seed, device step) of the mask, for a producer that folds this dropout in."""
-        return (self.rate, self._seed(), self.step_dev)
+        return (self.rate, self._seed(), self.step_dev, self.step_add)
 
     def forward(self, x, training):
         self.x = x

@@ -306,7 +306,12 @@ class Net:
         if not isinstance(x, ops.GatherRef) and x.dtype != self.dtype:
             x = x.to(self.dtype)
         if self.has_dropout and isinstance(self.exec_layers[0], KerasConvBlock):
-            self.exec_layers[0].step_inc = self.step_dev  # advanced by the block's backward reduce
+            # advanced by the block's backward reduce, so this step's masks read step + 1 (the value
+            # the other paths advance to before their step)
+            self.exec_layers[0].step_inc = self.step_dev
+            for l in self._all_leaf_layers():
+                if l.drop is not None:
+                    l.drop.step_add = 1
         elif self.has_dropout:
             if (self.is_gpu and isinstance(x, ops.GatherRef) and not self.lenet_fused
                     and not isinstance(self.exec_layers[0], (FusedConvPool, KerasConvBlock))):

@@ -66,18 +66,26 @@ def conv_out_hw(H, W, KH, KW, stride, pad):
 
 
 # ----------------------------------------------------------------------------------- dense
+def _drop_kw(drop) -> dict:
+    """Keyword arguments of a folded dropout ``(p, seed, step[, step_add])`` for the native launchers."""
+    if drop is None:
+        return {}
+    return {"drop_p": float(drop[0]), "drop_seed": int(drop[1]), "drop_step": drop[2],
+            "drop_step_add": int(drop[3]) if len(drop) > 3 else 0}
+
+
 def dense_fwd(x, w, bias, out, relu=False, drop=None):
     """out[B][N] = act(x[B][K] @ W^T + b); out may be bf16 or fp32 (logits).  ``drop = (p, seed, step)``:
     a Dropout that follows, folded into the epilogue (the mask of :func:`dropout` on ``out``)."""
     B, K = x.shape[0], x.shape[-1]
     N = out.shape[-1]
     if x.is_cuda:
-        dkw = {} if drop is None else {"drop_p": float(drop[0]), "drop_seed": int(drop[1]), "drop_step": drop[2]}
+        dkw = _drop_kw(drop)
         _C().igemm_fwd(x, w, bias, None, out, B, N, K, w.shape[1], K, N, _geom(), MODE_DIRECT, relu, 1.0, **dkw)
     else:
         out.copy_(ref.dense_fwd(x, w, bias, relu))
         if drop is not None:
-            dropout(out, out, drop[0], drop[1], step=drop[2])
+            dropout(out, out, drop[0], drop[1], step=drop[2], step_add=drop[3] if len(drop) > 3 else 0)
     return out
 
 
@@ -137,7 +145,7 @@ def conv_pool_fwd(x, w, bias, out, code, KH, KW, stride=1, pad=0, relu=True, dro
     OH, OW = 2 * PH, 2 * PW
     if x.is_cuda:
         K = KH * KW * C
-        dkw = {} if drop is None else {"drop_p": float(drop[0]), "drop_seed": int(drop[1]), "drop_step": drop[2]}
+        dkw = _drop_kw(drop)
         _C().igemm_fwd(x, w, bias, None, out, B * OH * OW, N, K, w.shape[1], 0, N,
                        _geom(H, W, C, OH, OW, KH, KW, stride, pad), MODE_FWD, relu, 1.0, pool_code=code, **dkw)
     else:
@@ -149,7 +157,7 @@ def conv_pool_fwd(x, w, bias, out, code, KH, KW, stride=1, pad=0, relu=True, dro
         out.copy_(mx)
         code.copy_(am.to(torch.uint8))
         if drop is not None:
-            dropout(out, out, drop[0], drop[1], step=drop[2])
+            dropout(out, out, drop[0], drop[1], step=drop[2], step_add=drop[3] if len(drop) > 3 else 0)
     return out
 
 
@@ -182,7 +190,7 @@ def kcnn_fwd(x, w1, b1, w2, b2, out, code, drop=None):
     2x2 max-pool [+ folded dropout] -> pooled ``out`` [B][12][12][32] and argmax ``code``.  ``x``: a
     :class:`GatherRef` (uint8 dataset rows, read in-kernel) or a bf16 batch [B][28][28][1]."""
     src, idx, scale = _kc_in(x)
-    dkw = {} if drop is None else {"drop_p": float(drop[0]), "drop_seed": int(drop[1]), "drop_step": drop[2]}
+    dkw = _drop_kw(drop)
     _C().kcnn_fwd(src, idx, float(scale), int(out.shape[0]), w1, b1, int(w1.shape[1]), w2, b2, out, code, **dkw)
     return out
 
@@ -241,12 +249,12 @@ def maxpool_fwd(x, out, P, drop=None):
     """``drop = (p, seed, step)``: a Dropout that follows, folded in (same mask as :func:`dropout`)."""
     B, H, W, C = x.shape
     if x.is_cuda:
-        dkw = {} if drop is None else {"drop_p": float(drop[0]), "drop_seed": int(drop[1]), "drop_step": drop[2]}
+        dkw = _drop_kw(drop)
         _C().maxpool_fwd(x, out, B, H, W, C, P, **dkw)
     else:
         out.copy_(ref.maxpool_fwd(x, P))
         if drop is not None:
-            dropout(out, out, drop[0], drop[1], step=drop[2])
+            dropout(out, out, drop[0], drop[1], step=drop[2], step_add=drop[3] if len(drop) > 3 else 0)
     return out
 
 
@@ -274,12 +282,14 @@ def softmax_ce(logits, labels, dlogits=None, stats=None, grad_scale=1.0):
             stats[1] += corr
 
 
-def dropout(x, out, p, seed, mask=None, step=None):
+def dropout(x, out, p, seed, mask=None, step=None, step_add=0):
     """out = x * keep(seed ^ step, i) / (1 - p) [* relu'(mask)]; ``step`` is a device int64 scalar."""
     if x.is_cuda:
+        if step_add:
+            raise ValueError("step_add is for folded dropouts only")
         _C().dropout(x, out, p, seed, mask, step)
     else:
-        s = seed ^ (int(step.item()) * 0x9E3779B1 if step is not None else 0)
+        s = seed ^ ((int(step.item()) + step_add) * 0x9E3779B1 if step is not None else 0)
         out.copy_(ref.dropout(x, p, s, mask).reshape(out.shape))
     return out
 

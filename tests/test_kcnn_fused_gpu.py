@@ -37,14 +37,14 @@ def test_kcnn_block_matches_per_layer_path(monkeypatch, B):
     data, labels = synthetic_mnist(4096, seed=5, device=dev)
     idx = torch.randperm(4096, device=dev)[:B]
     x, y = ops.GatherRef(data, idx, 1 / 255.0, (28, 28, 1)), ops.LabelRef(labels, idx)
-    # same dropout masks: the fused step reads the counter before advancing it, the per-layer step's
-    # gather advances it first
+    # same dropout masks: the fused step's masks read counter + 1 and its reduce advances the counter at
+    # the end; the per-layer step's gather advances it first
     f.step_dev.fill_(5)
-    p.step_dev.fill_(4)
+    p.step_dev.fill_(5)
     sf = f.compute_gradients(x, y).clone()
     sp = p.compute_gradients(x, y).clone()
     torch.cuda.synchronize()
-    assert int(f.step_dev.item()) == 6 and int(p.step_dev.item()) == 5
+    assert int(f.step_dev.item()) == 6 and int(p.step_dev.item()) == 6
     assert torch.equal(f.exec_layers[0].out, p.exec_layers[1].out)  # pooled (+ dropout) map
     assert torch.equal(f.exec_layers[0].code, p.exec_layers[1].code)
     assert torch.equal(sf, sp)
@@ -65,8 +65,8 @@ def test_kcnn_block_bf16_batch_input_and_training(monkeypatch):
     data, labels = synthetic_mnist(2048, seed=1, device=dev)
     xb = (data[:96].float() / 255.0).to(torch.bfloat16)
     yb = labels[:96]
-    f.step_dev.fill_(2)  # read, then advanced by the block's reduce
-    p.step_dev.fill_(1)  # advanced (torch add) before the per-layer step reads it
+    f.step_dev.fill_(2)  # masks read 3, then the block's reduce advances the counter
+    p.step_dev.fill_(2)  # advanced (torch add) to 3 before the per-layer step reads it
     sf = f.compute_gradients(xb, yb).clone()
     sp = p.compute_gradients(xb, yb).clone()
     torch.cuda.synchronize()
