@@ -101,6 +101,7 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_spawn_ranks(args.gpus))
 
+    from distriflow_amd.data.dataset import DistriDataset
     from distriflow_amd.data.synthetic import synthetic_cifar10, synthetic_mnist
     from distriflow_amd.models.zoo import build_model
     from distriflow_amd.parallel.comm import init_distributed, shutdown
@@ -138,9 +139,11 @@ def main():
         else:
             tr = DataParallelTrainer(net, lr=args.lr, graph=args.graph, overlap=not args.no_overlap,
                                      allreduce=args.allreduce)
-            tr.bind_dataset(data, labels, B, scale=1.0 / 255.0)
-            # device-resident batch schedule: each step's optimizer launch stages the next step's indices
-            tr.bind_index_stream(epoch_permutations(data.shape[0], B, total, dev, seed=rank))
+            # device-resident batch schedule from this rank's DistriDataset (FCFS dispenser, per-epoch
+            # shuffle): each step's optimizer launch stages the next step's indices
+            epochs = -(-total // (data.shape[0] // B))
+            ds = DistriDataset(data, labels, {"batchSize": B, "epochs": epochs}, shuffle=True, seed=rank)
+            tr.bind_distri_dataset(ds, scale=1.0 / 255.0)
         return tr
 
     def timed(tr, steps):

@@ -220,7 +220,8 @@ def run_sync(args) -> dict:
     from .checkpoint.tfjs import load_layers_model_weights, save_layers_model
     from .models.zoo import build_model
     from .parallel.comm import init_distributed, shutdown
-    from .parallel.data_parallel import DataParallelTrainer, epoch_permutations
+    from .data.dataset import DistriDataset
+    from .parallel.data_parallel import DataParallelTrainer
 
     env = init_distributed(device=_device(args), watchdog=True)
     rank, world, dev = env.rank, env.world_size, env.device
@@ -243,16 +244,22 @@ def run_sync(args) -> dict:
     graph = args.graph or "full"
     tr = DataParallelTrainer(net, lr=args.lr, momentum=args.momentum, graph=graph if dev.type == "cuda" else "none")
     scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
-    tr.bind_dataset(x, y, B, scale=scale)
+    if start_epoch < args.epochs:
+        # the DistriDataset's dispenser (epochs, per-epoch shuffle, FCFS order, completion) becomes the
+        # device index stream: batch k of the schedule goes to rank k % world, and every step's optimizer
+        # launch stages the next step's indices (no host work per step)
+        ds = DistriDataset(x, y, {"batchSize": B, "epochs": args.epochs - start_epoch}, shuffle=True,
+                           seed=args.seed + start_epoch)
+        tr.bind_distri_dataset(ds, rank, world, scale=scale)
+        steps_per_epoch = tr.steps_per_epoch
     step = 0
     t0 = time.perf_counter()
     seen = 0
     last_loss = float("nan")
     for epoch in range(start_epoch, args.epochs):
-        perm = epoch_permutations(n, B * world, steps_per_epoch, dev, seed=args.seed + epoch)
         for i in range(steps_per_epoch):
             faults.step(step)
-            st = tr.step_indices(perm[i, rank * B:(rank + 1) * B])
+            st = tr.step()
             step += 1
             seen += B * world
             if args.steps and step >= args.steps:

@@ -54,6 +54,14 @@ class DataParallelTrainer:
             self.bucket_bytes = int(bucket_mb * (1 << 20))
         self._build_buckets()
         self._setup_p2p(allreduce, int(p2p_max_mb * (1 << 20)))
+        # gloo cannot run inside a hipGraph capture (it stages device tensors through the host): with a
+        # gloo process group on GPUs (the one-GPU rehearsal mode) any bucket that is not on the one-shot
+        # p2p path makes the step "split" (compute graph, eager all-reduce, SGD graph) from the start
+        if (self.world > 1 and self.net.is_gpu and self.graph_mode == "full" and dist.is_initialized()
+                and dist.get_backend(self.group) == "gloo"
+                and any(self.p2p is None or (hi - lo) * 4 > self.p2p_limit for _, lo, hi in self.buckets)):
+            self.graph_mode = "split"
+            self.capture_error = "gloo collectives are not capturable"
         self._works = []
         self._graph = None
         self._graph_B = None
@@ -252,20 +260,51 @@ class DataParallelTrainer:
             self._index_stream[1].copy_(cursor)
         torch.cuda.synchronize(net.device)
         g = torch.cuda.CUDAGraph()
-        if self.graph_mode == "full":
-            with torch.cuda.graph(g):
-                self._gather()
-                self.stats = self._step_body(self.xb, self.yb)
-            self._graph = (g, None)
-        else:  # split: compute graph, eager all-reduce, SGD graph
-            g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._gather()
-                self.stats = self.net.compute_gradients(self.xb, self.yb)
-            with torch.cuda.graph(g2):
-                self.net.store.sgd_step(self._index_stream)
-            self._graph = (g, g2)
+        cs = torch.cuda.Stream(device=net.device)  # our own capture stream: a failed capture can be ended
+        try:
+            if self.graph_mode == "full":
+                with torch.cuda.graph(g, stream=cs):
+                    self._gather()
+                    self.stats = self._step_body(self.xb, self.yb)
+                self._graph = (g, None)
+            else:  # split: compute graph, eager all-reduce, SGD graph
+                g2 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=cs):
+                    self._gather()
+                    self.stats = self.net.compute_gradients(self.xb, self.yb)
+                with torch.cuda.graph(g2, stream=cs):
+                    self.net.store.sgd_step(self._index_stream)
+                self._graph = (g, g2)
+        except Exception:
+            # a collective that cannot be captured (e.g. gloo on device tensors) leaves the capture open
+            # on ``cs``, which would make every later allocation fail: end it before falling back
+            with torch.cuda.stream(cs):
+                if torch.cuda.is_current_stream_capturing():
+                    try:
+                        g.capture_end()
+                    except Exception:
+                        pass
+            net.restore_state(snap)
+            self.idx.copy_(idx0)
+            if cursor is not None:
+                self._index_stream[1].copy_(cursor)
+            raise
         torch.cuda.synchronize(net.device)
+
+    def bind_distri_dataset(self, ds, rank: int = 0, world: int = 1, scale: Optional[float] = None):
+        """Train from a :class:`~distriflow_amd.data.dataset.DistriDataset`: its tensors become the
+        HBM-resident dataset and its dispenser's epochs / shuffles / FCFS order the device index stream
+        (reference DistributedDataset, /root/reference/src/server/dataset.ts:47-96).  Returns the
+        number of steps in the schedule; ``steps_per_epoch`` is set for epoch bookkeeping."""
+        if scale is None:
+            scale = 1.0 / 255.0 if ds.x.dtype == torch.uint8 else 1.0
+        self.bind_dataset(ds.x, ds.y, ds.batch_size, scale=scale)
+        epochs_left = max(1, ds.epochs - ds.epoch)
+        stream = ds.index_stream(rank, world, device=self.net.device)
+        self.bind_index_stream(stream)
+        self.steps_per_epoch = max(1, stream.shape[0] // epochs_left)
+        self.schedule_steps = int(stream.shape[0])
+        return self.schedule_steps
 
     def bind_index_stream(self, stream: torch.Tensor):
         """Device-resident batch schedule ``stream`` [nsteps][B] (int64, this rank's rows): the step's

@@ -77,3 +77,55 @@ def test_non_iid_shards_cover_each_example_once():
     allidx = torch.cat(shards).sort().values
     assert torch.equal(allidx, torch.arange(1000))
     assert all(len(torch.unique(y[s])) <= 4 for s in shards)
+
+
+def test_index_stream_covers_epochs_and_splits_ranks():
+    """The sync engine's device schedule comes from the dispenser: every full batch of every epoch
+    exactly once, batch k on rank k % world, per-epoch shuffles, and the dispenser ends done."""
+    import torch
+
+    from distriflow_amd.data.dataset import DistriDataset
+
+    n, B, E = 100, 8, 3  # 12 full batches + a ragged one per epoch
+    x, y = torch.arange(n).float().view(n, 1), torch.arange(n)
+    streams = []
+    for r in range(2):
+        ds = DistriDataset(x, y, {"batchSize": B, "epochs": E}, shuffle=True, seed=7)
+        streams.append(ds.index_stream(rank=r, world=2))
+        assert ds.done
+    a, b = streams
+    assert a.shape == b.shape == (E * 12 // 2, B)
+    for e in range(E):  # per epoch the two ranks' batches are disjoint rows of one permutation
+        rows = torch.cat([a[e * 6:(e + 1) * 6].flatten(), b[e * 6:(e + 1) * 6].flatten()])
+        assert rows.unique().numel() == 96
+    assert not torch.equal(a[:6], a[6:12])  # reshuffled per epoch
+
+
+def test_index_stream_refuses_preprocess_callbacks():
+    import pytest
+    import torch
+
+    from distriflow_amd.data.dataset import DistriDataset
+
+    ds = DistriDataset(torch.zeros(16, 1), torch.zeros(16), {"batchSize": 4, "epochs": 1})
+    ds.add_preprocess_callback(lambda b: b)
+    with pytest.raises(ValueError):
+        ds.index_stream()
+
+
+def test_trainer_binds_a_distri_dataset_cpu():
+    import torch
+
+    from distriflow_amd.data.dataset import DistriDataset
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer
+
+    net = build_model("mlp_mnist", device="cpu", seed=0)
+    data, labels = synthetic_mnist(512, seed=0, device="cpu")
+    ds = DistriDataset(data, labels, {"batchSize": 64, "epochs": 2}, shuffle=True, seed=1)
+    tr = DataParallelTrainer(net, lr=0.1, graph="none")
+    steps = tr.bind_distri_dataset(ds)
+    assert steps == 16 and tr.steps_per_epoch == 8
+    losses = [float(tr.step()[0]) / 64 for _ in range(steps)]
+    assert losses[-1] < losses[0]
