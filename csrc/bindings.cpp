@@ -770,7 +770,12 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
                     std::vector<torch::Tensor> dense_gb, std::vector<torch::Tensor> hT, std::vector<torch::Tensor> dzT,
                     torch::Tensor conv_part, torch::Tensor dense_part, torch::Tensor loss_part, torch::Tensor stats,
                     torch::Tensor frag, torch::Tensor ftab, torch::Tensor pxtab, int64_t B, double grad_scale,
-                    bool prep, c10::optional<torch::Tensor> snap, std::vector<torch::Tensor> conv_mom) {
+                    bool prep, c10::optional<torch::Tensor> snap, std::vector<torch::Tensor> conv_mom,
+                    c10::optional<torch::Tensor> sgd_master, c10::optional<torch::Tensor> sgd_mom,
+                    c10::optional<torch::Tensor> sgd_wbf, c10::optional<torch::Tensor> sgd_hyper,
+                    c10::optional<torch::Tensor> sgd_descs, c10::optional<torch::Tensor> idx_stream,
+                    c10::optional<torch::Tensor> idx_cursor, c10::optional<torch::Tensor> idx_dst,
+                    c10::optional<torch::Tensor> sgd_ticket, c10::optional<torch::Tensor> sgd_stage) {
   TORCH_CHECK(conv.size() == 4 && conv_grads.size() == 4, "lenet: conv = [w1, b1, w2, b2]");
   TORCH_CHECK(dense_w.size() == 3 && dense_wt.size() == 3 && dense_b.size() == 3 && dense_gw.size() == 3 &&
                   dense_gb.size() == 3 && hT.size() == 3 && dzT.size() == 3,
@@ -893,6 +898,49 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
       r.m1 = conv_mom[0].data_ptr<float>();
       r.m2 = conv_mom[1].data_ptr<float>();
     }
+  }
+  if (sgd_master.has_value() && sgd_master->defined()) {
+    // single-rank fast path: the reduce kernel applies the SGD update (see LeNetSgd)
+    need(*sgd_master, at::kFloat, "lenet sgd master");
+    TORCH_CHECK(sgd_wbf.has_value() && sgd_hyper.has_value() && sgd_descs.has_value() && sgd_ticket.has_value() &&
+                    sgd_stage.has_value(),
+                "lenet sgd: wbf, hyper, descs, ticket and stage are required");
+    need(*sgd_wbf, at::kBFloat16, "lenet sgd wbf");
+    need(*sgd_hyper, at::kFloat, "lenet sgd hyper");
+    need(*sgd_stage, at::kFloat, "lenet sgd stage");
+    TORCH_CHECK(sgd_stage->numel() >= 2550 && sgd_hyper->numel() >= 5, "lenet sgd: stage / hyper sizes");
+    TORCH_CHECK(sgd_ticket->is_cuda() && sgd_ticket->scalar_type() == at::kInt && sgd_ticket->numel() >= 1,
+                "lenet sgd: ticket must be an int32 GPU tensor");
+    const torch::Tensor& dh = *sgd_descs;
+    TORCH_CHECK(!dh.is_cuda() && dh.scalar_type() == at::kLong && dh.is_contiguous() &&
+                    dh.numel() * 8 >= 10 * (int64_t)sizeof(dfa::ParamDesc),
+                "lenet sgd: descs must be the host int64 table of the 10 parameters");
+    r.sgd_on = 1;
+    r.sgd.master = sgd_master->data_ptr<float>();
+    r.sgd.mom = (sgd_mom.has_value() && sgd_mom->defined()) ? sgd_mom->data_ptr<float>() : nullptr;
+    r.sgd.wbf = reinterpret_cast<dfa::bf16*>(sgd_wbf->data_ptr());
+    r.sgd.hyper = sgd_hyper->data_ptr<float>();
+    const auto* hd = reinterpret_cast<const dfa::ParamDesc*>(dh.data_ptr());
+    for (int k = 0; k < 10; ++k) {
+      r.sgd.d[k] = hd[k];
+      TORCH_CHECK(hd[k].off >= 0 && hd[k].off + hd[k].numel <= sgd_master->numel(), "lenet sgd: descriptor range");
+    }
+    TORCH_CHECK(r.sgd.d[0].off == conv[0].data_ptr<float>() - r.sgd.master &&
+                    r.sgd.d[2].off == conv[2].data_ptr<float>() - r.sgd.master,
+                "lenet sgd: descriptors do not match the conv parameters");
+    if (idx_stream.has_value() && idx_stream->defined()) {
+      need(*idx_stream, at::kLong, "lenet idx_stream");
+      TORCH_CHECK(idx_cursor.has_value() && idx_dst.has_value(), "lenet sgd: index stream needs cursor and dst");
+      TORCH_CHECK(idx_stream->dim() == 2 && idx_stream->size(1) == idx_dst->numel(), "lenet sgd: stream shape");
+      r.sgd.src = reinterpret_cast<const long long*>(idx_stream->data_ptr());
+      r.sgd.cursor = reinterpret_cast<long long*>(idx_cursor->data_ptr());
+      r.sgd.dst = reinterpret_cast<long long*>(idx_dst->data_ptr());
+      r.sgd.B = (int)idx_dst->numel();
+      r.sgd.nsteps = (int)idx_stream->size(0);
+    }
+    r.sgd.frag = frag.data_ptr();
+    r.sgd.ticket = reinterpret_cast<unsigned*>(sgd_ticket->data_ptr<int>());
+    r.sgd.stage = sgd_stage->data_ptr<float>();
   }
   check_hip(dfa::lenet_train(a, r, cur_stream()), "lenet_train");
 }
@@ -1383,7 +1431,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("hT"), py::arg("dzT"), py::arg("conv_part"), py::arg("dense_part"), py::arg("loss_part"),
         py::arg("stats"), py::arg("frag"), py::arg("ftab"), py::arg("pxtab"), py::arg("B"), py::arg("grad_scale"),
         py::arg("prep") = true, py::arg("snap") = py::none(),
-        py::arg("conv_mom") = std::vector<torch::Tensor>{});
+        py::arg("conv_mom") = std::vector<torch::Tensor>{}, py::arg("sgd_master") = py::none(),
+        py::arg("sgd_mom") = py::none(), py::arg("sgd_wbf") = py::none(), py::arg("sgd_hyper") = py::none(),
+        py::arg("sgd_descs") = py::none(), py::arg("idx_stream") = py::none(), py::arg("idx_cursor") = py::none(),
+        py::arg("idx_dst") = py::none(), py::arg("sgd_ticket") = py::none(), py::arg("sgd_stage") = py::none());
   m.def("lenet_blocks", [](int64_t B) { return dfa::lenet_blocks((int)B); });
   m.def("lenet_frag_bytes", []() { return (int64_t)dfa::lenet_frag_bytes(); });
   m.def("lenet_dense_part_floats", [](int64_t B) { return (int64_t)dfa::lenet_dense_part_floats((int)B); });

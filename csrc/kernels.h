@@ -323,6 +323,23 @@ struct LeNetDense {
   float* gb;  // [N]
   int N, K, tiles;
 };
+// Single-rank fast path of the fused LeNet-5 step: the reduce kernel applies the SGD update to every
+// parameter it finalises (no optimizer launch), stages the next batch's indices and, in its last conv
+// workgroup, rebuilds the conv-weight MFMA fragments of the next step.
+struct LeNetSgd {
+  float* master;
+  float* mom;          // null without momentum
+  bf16* wbf;
+  const float* hyper;  // [lr, momentum, wd, grad_scale, nesterov]
+  ParamDesc d[10];     // w1, b1, w2, b2, dense (w, b) x 3 (ParamStore order)
+  const long long* src;  // index stream [nsteps][B] (null = off), cursor, dst
+  long long* cursor;
+  long long* dst;
+  int B, nsteps;
+  void* frag;          // fragment buffer of the next step
+  unsigned* ticket;    // conv-workgroup arrival counter (re-armed by the last)
+  float* stage;        // [2550] the new conv weights, handed to the last conv workgroup
+};
 struct LeNetRedArgs {
   const float* conv_part;
   const float* loss_part;
@@ -334,6 +351,8 @@ struct LeNetRedArgs {
   // optional snapshot [2][2550] of the conv kernels' weights (w1, w2) and momentum (m1, m2; null = 0)
   const float *w1, *w2, *m1, *m2;
   float* snap;
+  int sgd_on;
+  LeNetSgd sgd;
 };
 // The reference CNN's conv block (csrc/kcnn_fused.hip): conv1 3x3x1->32 + ReLU, conv2 3x3x32->32 + ReLU,
 // 2x2 max-pool [+ folded dropout], input 28x28x1, in one forward and one backward launch (+ reduce).

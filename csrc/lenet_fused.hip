@@ -27,6 +27,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "lenet_frag.h"
+#include "optim_device.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -697,6 +698,12 @@ __global__ void __launch_bounds__(PT) lenet_prep_kernel(const float* __restrict_
 //   last block               loss partials -> stats.
 constexpr int RT = 1024;
 
+// write-through hand-off (as csrc/bn.hip): sc1 stores drained before the ticket, sc1 loads after it
+__device__ __forceinline__ void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ void __launch_bounds__(RT) lenet_reduce_kernel(LeNetRedArgs a) {
   __shared__ float red[16][16][17];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -754,6 +761,9 @@ __global__ void __launch_bounds__(RT) lenet_reduce_kernel(LeNetRedArgs a) {
       if (on < L.N) {
         if (ok < L.K) L.gw[(long long)on * L.K + ok] = v;
         else if (ok == L.K) L.gb[on] = v;
+        if (a.sgd_on && ok <= L.K)  // single-rank fast path: the update of this element, here
+          sgd_apply_one(a.sgd.d[4 + 2 * l + (ok == L.K ? 1 : 0)], ok < L.K ? on * L.K + ok : on, v, a.sgd.master,
+                        a.sgd.mom, a.sgd.wbf, a.sgd.hyper);
       }
     }
     return;
@@ -790,12 +800,46 @@ __global__ void __launch_bounds__(RT) lenet_reduce_kernel(LeNetRedArgs a) {
       // the conv kernels' weights and momentum as this gradient saw them: the optimizer launch
       // rebuilds the next step's fragments from these (no read of state it is overwriting)
       const int wj = p < kLeNetPB1 ? p : (p >= kLeNetPW2 && p < kLeNetPB2) ? 150 + (p - kLeNetPW2) : -1;
-      if (a.snap != nullptr && wj >= 0) {
+      if (a.sgd_on) {
+        const int di = p < kLeNetPB1 ? 0 : p < kLeNetPW2 ? 1 : p < kLeNetPB2 ? 2 : 3;
+        const int i = p - (di == 0 ? 0 : di == 1 ? kLeNetPB1 : di == 2 ? kLeNetPW2 : kLeNetPB2);
+        const float nw = sgd_apply_one(a.sgd.d[di], i, v, a.sgd.master, a.sgd.mom, a.sgd.wbf, a.sgd.hyper);
+        if (wj >= 0) st_sc1(a.sgd.stage + wj, nw);
+      } else if (a.snap != nullptr && wj >= 0) {
         const long long o = wj < 150 ? wj : wj - 150;
         a.snap[wj] = wj < 150 ? a.w1[o] : a.w2[o];
         a.snap[kLeNetConvW + wj] = a.m1 == nullptr ? 0.f : (wj < 150 ? a.m1[o] : a.m2[o]);
       }
     }
+    if (a.sgd_on) {
+      // the last conv workgroup to finish rebuilds the next step's conv-weight fragments from the staged
+      // new weights (write-through stores drained before the ticket, write-through loads after it)
+      __shared__ int last;
+      __shared__ float wl[kLeNetConvW];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const unsigned tk = __hip_atomic_fetch_add(a.sgd.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = tk == (unsigned)a.nconv_blocks - 1;
+        if (last) __hip_atomic_store(a.sgd.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (last) {
+        for (int e = threadIdx.x; e < kLeNetConvW; e += RT) wl[e] = ld_sc1(a.sgd.stage + e);
+        __syncthreads();
+        lenet_build_frags(wl, reinterpret_cast<bf16x8*>(a.sgd.frag), threadIdx.x, RT);
+      }
+    }
+    return;
+  }
+  blk -= a.nconv_blocks;
+  if (blk == 1) {  // single-rank fast path: stage the next step's batch indices, advance the cursor
+    __shared__ long long nxt;
+    if (threadIdx.x == 0) nxt = (*a.sgd.cursor + 1) % a.sgd.nsteps;
+    __syncthreads();
+    const long long* src = a.sgd.src + nxt * a.sgd.B;
+    for (int i = threadIdx.x; i < a.sgd.B; i += RT) a.sgd.dst[i] = src[i];
+    if (threadIdx.x == 0) *a.sgd.cursor = nxt;
     return;
   }
   if (wid == 0) {  // loss partials -> stats
@@ -872,7 +916,10 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   }
   const int nconv = (skip & 2) ? 0 : r.nconv_blocks;
   if (skip & 2) r.nconv_blocks = 0;
-  hipLaunchKernelGGL(lenet_reduce_kernel, dim3(r.dense_tiles + nconv + 1), dim3(RT), 0, st, r);
+  if (r.sgd_on && (skip || !r.sgd.master || !r.sgd.wbf || !r.sgd.hyper || !r.sgd.frag || !r.sgd.ticket || !r.sgd.stage))
+    return hipErrorInvalidValue;
+  const int extra = (r.sgd_on && r.sgd.src) ? 1 : 0;  // the index-staging workgroup
+  hipLaunchKernelGGL(lenet_reduce_kernel, dim3(r.dense_tiles + nconv + 1 + extra), dim3(RT), 0, st, r);
   return hipGetLastError();
 }
 

@@ -331,7 +331,28 @@ class Net:
         self.backward(self.dlogits, grad_ready)
         return stats
 
-    def _compute_gradients_lenet(self, x, labels, grad_ready):
+    def compute_gradients_and_update(self, x, labels, index_stream=None):
+        """Single-rank fast path of the fused LeNet-5 step: gradients AND the SGD update (with the
+        store's device hyper-parameters) in the step's two launches (the reduce kernel applies the
+        update and rebuilds the next step's weight fragments; ``index_stream`` = (stream, cursor, dst)
+        is advanced by it too).  Same arithmetic as compute_gradients + ParamStore.sgd_step."""
+        if not self.lenet_fused:
+            raise RuntimeError("compute_gradients_and_update needs the fused LeNet-5 plan")
+        if self.has_dropout:
+            self.step_dev.add_(1)
+        st = self.store
+        if not hasattr(self, "_lenet_ticket"):
+            self._lenet_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._lenet_stage = torch.zeros(2550, dtype=torch.float32, device=self.device)
+        sgd = dict(sgd_master=st.master, sgd_mom=st.momentum, sgd_wbf=st.wbf, sgd_hyper=st.hyper,
+                   sgd_descs=st._descs_host, sgd_ticket=self._lenet_ticket, sgd_stage=self._lenet_stage)
+        if index_stream is not None:
+            sgd.update(idx_stream=index_stream[0], idx_cursor=index_stream[1], idx_dst=index_stream[2])
+        stats = self._compute_gradients_lenet(x, labels, None, sgd=sgd)
+        st.lenet_state = "fresh"  # the reduce kernel rebuilt the fragments from the new weights
+        return stats
+
+    def _compute_gradients_lenet(self, x, labels, grad_ready, sgd=None):
         """The whole LeNet-5 step in two launches (csrc/lenet_fused.hip); every gradient is final when
         they end, so all gradient hooks fire afterwards (one bucket's all-reduce)."""
         B = x.shape[0]
@@ -349,7 +370,7 @@ class Net:
                         self.head_dzT, self.lenet_conv_part, self.lenet_dense_part, self.lenet_loss_part, self.stats,
                         1.0 / B, frag=st.lenet_frag[0] if st.lenet_frag is not None else None,
                         prep=st.lenet_frag is None or st.lenet_state == "stale", snap=st.lenet_snap,
-                        conv_mom=st.lenet_conv_momentum())
+                        conv_mom=st.lenet_conv_momentum(), sgd=sgd if st.lenet_frag is not None else None)
         if st.lenet_frag is not None:
             st.lenet_state = "snap"
         if grad_ready is not None:

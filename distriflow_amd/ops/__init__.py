@@ -530,7 +530,7 @@ def lenet_dense_part_floats(B: int) -> int:
 
 
 def lenet_train(x, labels, conv, dense_w, dense_wt, dense_b, conv_grads, dense_gw, dense_gb, hT, dzT, conv_part,
-                dense_part, loss_part, stats, grad_scale, frag=None, prep=True, snap=None, conv_mom=()):
+                dense_part, loss_part, stats, grad_scale, frag=None, prep=True, snap=None, conv_mom=(), sgd=None):
     """Whole-network LeNet-5 training step on GPU (csrc/lenet_fused.hip, 2 launches): fills every
     gradient and ``stats`` = [loss sum, correct].  ``x``: bf16 batch [B,28,28,1] or a :class:`GatherRef`
     over a uint8 dataset; ``labels``: int32 [B] or a :class:`LabelRef` through the same indices."""
@@ -552,7 +552,7 @@ def lenet_train(x, labels, conv, dense_w, dense_wt, dense_b, conv_grads, dense_g
     _C().lenet_train(src, idx, float(scale), lab, list(conv), list(dense_w), list(dense_wt), list(dense_b),
                      list(conv_grads), list(dense_gw), list(dense_gb), list(hT), list(dzT), conv_part, dense_part,
                      loss_part, stats, scratch if frag is None else frag, ftab, pxtab, int(B), float(grad_scale),
-                     prep=bool(prep) or frag is None, snap=snap, conv_mom=list(conv_mom))
+                     prep=bool(prep) or frag is None, snap=snap, conv_mom=list(conv_mom), **(sgd or {}))
 
 
 def convpool_supported(H, W, C, KH, KW, pad, N) -> bool:

@@ -19,6 +19,7 @@ MI355X specifics:
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Optional
 
@@ -167,11 +168,17 @@ class DataParallelTrainer:
     # ------------------------------------------------------------------ one step
     phase_timer = None  # utils.logging.PhaseTimer: per-phase GPU time of eager steps
 
+    # single rank + fused LeNet-5: the reduce kernel applies the update itself (no optimizer launch)
+    fused_update = os.environ.get("DISTRIFLOW_LENET_FUSED_UPDATE", "0") != "0"
+
     def _step_body(self, x, y):
         hook = self._grad_ready if (self.overlap and self.world > 1) else None
         pt = self.phase_timer
         if pt is not None and torch.cuda.is_current_stream_capturing():
             pt = None
+        if (self.world == 1 and pt is None and self.fused_update and getattr(self.net, "lenet_fused", False)
+                and self.net.store.lenet_frag is not None):
+            return self.net.compute_gradients_and_update(x, y, self._index_stream)
         if pt is not None:
             pt.start("compute")  # forward + loss + backward (the fused head runs all three)
         stats = self.net.compute_gradients(x, y, grad_ready=hook)

@@ -160,3 +160,36 @@ def test_optimizer_built_fragments_match_prep():
     g.compute_gradients(x.cuda(), y.cuda())
     torch.cuda.synchronize()
     assert torch.equal(keep[0], scratch[: built.numel()])
+
+
+def test_single_rank_fused_update_matches_separate_sgd():
+    """The reduce kernel's in-place SGD (single-rank fast path) gives bit-identical weights, momentum,
+    compute copies and next-step fragments to compute_gradients + the optimizer launch, and advances
+    the index stream the same way."""
+    from distriflow_amd import ops
+    from distriflow_amd.data.synthetic import synthetic_mnist
+
+    B = 256
+    g, _ = _nets(B)
+    h, _ = _nets(B)
+    h.store.set_flat(g.store.master.clone())
+    for s in (g.store, h.store):
+        s.set_hyper(0.05, momentum=0.9, weight_decay=1e-4, grad_scale=1.0, nesterov=False)
+    data, labels = synthetic_mnist(2048, seed=4, device="cuda")
+    stream = torch.randperm(2048, device="cuda")[: 4 * B].view(4, B).contiguous()
+    idx_g, idx_h = stream[0].clone(), stream[0].clone()
+    cur_g = torch.zeros(1, dtype=torch.int64, device="cuda")
+    cur_h = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for _ in range(3):
+        xg = ops.GatherRef(data, idx_g, 1 / 255.0, (28, 28, 1))
+        xh = ops.GatherRef(data, idx_h, 1 / 255.0, (28, 28, 1))
+        sg = g.compute_gradients_and_update(xg, ops.LabelRef(labels, idx_g), (stream, cur_g, idx_g)).clone()
+        sh = h.compute_gradients(xh, ops.LabelRef(labels, idx_h)).clone()
+        h.store.sgd_step((stream, cur_h, idx_h))
+        torch.cuda.synchronize()
+        assert torch.equal(sg, sh)
+        assert torch.equal(g.store.master, h.store.master)
+        assert torch.equal(g.store.momentum, h.store.momentum)
+        assert torch.equal(g.store.wbf, h.store.wbf)
+        assert torch.equal(g.store.lenet_frag[0], h.store.lenet_frag[0])
+        assert torch.equal(idx_g, idx_h) and torch.equal(cur_g, cur_h)
