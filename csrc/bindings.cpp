@@ -52,7 +52,7 @@ void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tenso
                   int64_t lda, int64_t ldc, std::vector<int64_t> geom, int64_t mode, bool relu, double alpha,
                   c10::optional<torch::Tensor> res, c10::optional<torch::Tensor> resmask, double drop_p,
                   int64_t drop_seed, c10::optional<torch::Tensor> drop_step, c10::optional<torch::Tensor> pool_code,
-                  int64_t drop_step_add) {
+                  int64_t drop_step_add, c10::optional<torch::Tensor> bn_part) {
   need(src, at::kBFloat16, "src");
   need(w, at::kBFloat16, "w");
   TORCH_CHECK(out.is_cuda() && out.is_contiguous(), "out must be a contiguous GPU tensor");
@@ -115,6 +115,13 @@ void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tenso
   if (pooled) {
     a.pool_code = pool_code->data_ptr<uint8_t>();
     TORCH_CHECK(dfa::igemm64_pool_supported(a), "pooled conv: unsupported geometry / alignment");
+  }
+  if (bn_part.has_value() && bn_part->defined()) {
+    need(*bn_part, at::kFloat, "bn_part");
+    const int ntm = dfa::igemm64_bn_tiles(a, (int)mode);
+    TORCH_CHECK(ntm > 0, "bn_part: this conv cannot emit BatchNorm partials");
+    TORCH_CHECK(bn_part->numel() >= (int64_t)ntm * 2 * N, "bn_part too small");
+    a.bn_part = bn_part->data_ptr<float>();
   }
   TORCH_CHECK(!a.drop.on || (ldc == N && !a.out_f32), "folded dropout needs a dense bf16 output (ldc == N)");
   // split-K partials for the under-filled (small-M, long-K) shapes: PyTorch's caching allocator is
@@ -1331,7 +1338,31 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lda"), py::arg("ldc"), py::arg("geom"), py::arg("mode"), py::arg("relu"), py::arg("alpha"),
         py::arg("res") = py::none(), py::arg("resmask") = py::none(), py::arg("drop_p") = 0.0,
         py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pool_code") = py::none(),
-        py::arg("drop_step_add") = 0);
+        py::arg("drop_step_add") = 0, py::arg("bn_part") = py::none());
+  m.def("igemm64_bn_tiles", [](int64_t M, int64_t N, int64_t K, int64_t Kpad, std::vector<int64_t> geom, int64_t mode) {
+    dfa::IGemmArgs a{};
+    int g[9];
+    fill_geom(geom, g);
+    a.SH = g[0]; a.SW = g[1]; a.SC = g[2]; a.OH = g[3]; a.OW = g[4]; a.KH = g[5]; a.KW = g[6]; a.stride = g[7];
+    a.pad = g[8];
+    a.M = (int)M; a.N = (int)N; a.K = (int)K; a.Kpad = (int)Kpad; a.ldc = (int)N;
+    static dfa::bf16 probe[8] __attribute__((aligned(16)));
+    a.src = probe; a.w = probe; a.out = probe;
+    return dfa::igemm64_bn_tiles(a, (int)mode);
+  });
+  m.def("bn_finalize_partials", [](torch::Tensor part, int64_t ntm, int64_t C, int64_t M, torch::Tensor mean,
+                                   torch::Tensor invstd, c10::optional<torch::Tensor> run_mean,
+                                   c10::optional<torch::Tensor> run_var, double momentum, double eps) {
+    need(part, at::kFloat, "bn part");
+    need(mean, at::kFloat, "bn mean");
+    need(invstd, at::kFloat, "bn invstd");
+    TORCH_CHECK(part.numel() >= ntm * 2 * C && mean.numel() >= C && invstd.numel() >= C, "bn_finalize: sizes");
+    check_hip(dfa::bn_finalize_partials(part.data_ptr<float>(), (int)ntm, (int)C, M, mean.data_ptr<float>(),
+                                        invstd.data_ptr<float>(), const_cast<float*>(cptr<float>(run_mean)),
+                                        const_cast<float*>(cptr<float>(run_var)),
+                                        (float)momentum, (float)eps, cur_stream()),
+              "bn_finalize_partials");
+  });
   m.def("igemm64_pool_supported", [](int64_t H, int64_t W, int64_t C, int64_t OH, int64_t OW, int64_t K, int64_t N) {
     dfa::IGemmArgs a{};
     a.SH = (int)H; a.SW = (int)W; a.SC = (int)C; a.OH = (int)OH; a.OW = (int)OW; a.M = 4; a.N = (int)N; a.ldc = (int)N;

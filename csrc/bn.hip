@@ -217,6 +217,66 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
   }
 }
 
+// BatchNorm forward statistics from the partial sums the producing conv's epilogue emitted
+// (IGemmArgs::bn_part, [ntm][2][C]): per channel a fixed-order fp64 sum over the row tiles (16 waves
+// of a workgroup take every 16th tile, 8 loads in flight each, combined in wave order), then the same
+// finalisation as bn_stats_kernel<0>.  Replaces a full read of the conv output.
+__global__ void __launch_bounds__(1024) bn_finalize_partials_kernel(const float* __restrict__ part, int ntm, int C,
+                                                                    long long M, float* mean, float* invstd,
+                                                                    float* run_mean, float* run_var, float momentum,
+                                                                    float eps) {
+  __shared__ double ps[16][64], pq[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    for (int t0 = w; t0 < ntm; t0 += 16 * 8) {
+      float u[8], v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int t = min(t0 + 16 * k, ntm - 1);
+        u[k] = part[((long long)t * 2) * C + c];
+        v[k] = part[((long long)t * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (t0 + 16 * k < ntm) {
+          s += (double)u[k];
+          q += (double)v[k];
+        }
+    }
+  }
+  ps[w][lane] = s;
+  pq[w][lane] = q;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    double S = 0.0, Q = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      S += ps[k][lane];
+      Q += pq[k][lane];
+    }
+    const double m = S / M;
+    double var = Q / M - m * m;
+    if (var < 0.0) var = 0.0;
+    mean[c] = (float)m;
+    invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (run_mean) {
+      const double unb = M > 1 ? var * M / (M - 1) : var;
+      run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * m);
+      run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
+    }
+  }
+}
+
+hipError_t bn_finalize_partials(const float* part, int ntm, int C, long long M, float* mean, float* invstd,
+                                float* run_mean, float* run_var, float momentum, float eps, hipStream_t st) {
+  if (ntm <= 0 || C <= 0 || M <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_finalize_partials_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, st, part, ntm, C, M, mean, invstd,
+                     run_mean, run_var, momentum, eps);
+  return hipGetLastError();
+}
+
 __device__ __forceinline__ void bn_affine(const BnApplyArgs& a, const float* g, const float* b, const float* m,
                                           const float* v, int c, float& sa, float& sb) {
   const float is = a.eval ? rsqrtf(v[c] + a.eps) : v[c];

@@ -400,6 +400,65 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
       }
     }
   }
+
+  // BatchNorm statistics of this tile's stored outputs (sum, sum of squares per channel), so the BN
+  // layer after this conv needs no statistics pass over its input: the 16 rows of a lane group by
+  // lane shuffles, the WM row-waves of a column block through LDS, one partial row per row tile.
+  if (a.bn_part) {
+    float s[TN][4], q[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[j][r] = q[j][r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = m0 + wm * TM * 16 + i * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col0 = n0 + wn * TN * 16 + j * 16 + fq * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = (float)f2bf(acc[i][j][r] * a.alpha + ((a.bias && col0 + r < a.N) ? a.bias[col0 + r] : 0.f));
+          if (row >= a.M || col0 + r >= a.N) v = 0.f;
+          s[j][r] += v;
+          q[j][r] += v * v;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          s[j][r] += __shfl_xor(s[j][r], off);
+          q[j][r] += __shfl_xor(q[j][r], off);
+        }
+    float* red = reinterpret_cast<float*>(lds);  // the k loop ended with a barrier: LDS is free
+    if (fr == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int cl = wn * TN * 16 + j * 16 + fq * 4 + r;
+          red[(wm * BN + cl) * 2] = s[j][r];
+          red[(wm * BN + cl) * 2 + 1] = q[j][r];
+        }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      const int col = n0 + c;
+      if (col >= a.N) continue;
+      float S = 0.f, Q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        S += red[(w * BN + c) * 2];
+        Q += red[(w * BN + c) * 2 + 1];
+      }
+      a.bn_part[((long long)tile_m * 2) * a.N + col] = S;
+      a.bn_part[((long long)tile_m * 2 + 1) * a.N + col] = Q;
+    }
+  }
 }
 
 // (a folded dropout rounds the activation to bf16 before scaling, as the standalone pass saw it)
@@ -455,7 +514,7 @@ __global__ void __launch_bounds__(256) igemm64_splitk_epilogue_kernel(IGemmArgs 
 // M = B*8*8 or B*4*4 with K up to 4608) leave one wave per SIMD waiting on every step
 template <int BM, int BN>
 static int splitk_for(const IGemmArgs& a) {
-  if (a.pool_code) return 1;
+  if (a.pool_code || a.bn_part) return 1;
   const long long tiles = (long long)cdiv(a.M, BM) * cdiv(a.N, BN);
   const int nk = cdiv(a.K, 64);
   if (a.N % 4 || a.ldc % 4 || tiles >= 512 || nk < 32) return 1;
@@ -510,6 +569,12 @@ long long igemm64_splitk_floats(const IGemmArgs& a, int mode) {
   if ((long long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 512) return 0;  // 128 x 128 tiles: already filled
   const int s = splitk_for<64, 128>(a);
   return s > 1 ? (long long)s * a.M * a.N : 0;
+}
+
+int igemm64_bn_tiles(const IGemmArgs& a, int mode) {
+  if (!igemm64_supported(a, mode) || a.pool_code || a.relu || a.mask || a.res || a.drop.on || a.out_f32) return 0;
+  const int BM = (a.N <= 64 || (long long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 512) ? 128 : 64;  // launch64_mode
+  return cdiv(a.M, BM);
 }
 
 bool igemm64_pool_supported(const IGemmArgs& a) {

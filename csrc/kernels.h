@@ -53,6 +53,8 @@ struct IGemmArgs {
   int splits;
   DropSpec drop;     // dropout after the activation (requires ldc == N, bf16 out)
   uint8_t* pool_code;  // conv forward + 2x2 max-pool (igemm64 POOL): out = pooled [M/4][N], code [M/4][N]
+  float* bn_part;      // BatchNorm statistics of the stored output: per row tile [ntm][2][N] (sum, sum of
+                       // squares); igemm64 only, no split-K / activation (bn_finalize_partials)
 };
 
 struct WgradArgs {
@@ -88,6 +90,10 @@ hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st);
 // 64-deep-step variant for the vectorizable cases (csrc/igemm64.hip); igemm_fwd dispatches to it
 bool igemm64_supported(const IGemmArgs& a, int mode);
 bool igemm64_pool_supported(const IGemmArgs& a);
+// row tiles (= BatchNorm partial rows) of the igemm64 launch for this problem, 0 if it cannot emit them
+int igemm64_bn_tiles(const IGemmArgs& a, int mode);
+hipError_t bn_finalize_partials(const float* part, int ntm, int C, long long M, float* mean, float* invstd,
+                                float* run_mean, float* run_var, float momentum, float eps, hipStream_t st);
 // dY of a pooled conv from the pooled gradient and the argmax codes (NHWC, 2x2 windows)
 hipError_t unpool2(const bf16* dyp, const uint8_t* code, bf16* dy, int B, int OH, int OW, int N, hipStream_t st);
 hipError_t igemm64(const IGemmArgs& a, int mode, hipStream_t st);

@@ -16,13 +16,19 @@ Execution model (MI355X-first):
 from __future__ import annotations
 
 import math
+import os
 import zlib
 from typing import Optional
 
 import torch
 
 from .. import ops
-from .params import ParamSpec
+from .params import ParamSpec, primary_kpad
+
+
+def primary_kpad_of(conv) -> int:
+    """Row length of a conv's forward compute copy (the igemm launch's Kpad)."""
+    return primary_kpad(conv.specs()[0])
 
 
 class Layer:
@@ -213,13 +219,28 @@ class Conv2D(Layer):
     def alloc(self, B, device, dtype, ws):
         super().alloc(B, device, dtype, ws)
         self.ws = ws
+        # BatchNorm statistics from the forward epilogue (csrc/igemm64.hip bn_part): row tiles of the launch
+        self._bn_ntm = 0
+        if (torch.device(device).type == "cuda" and not self.relu
+                and os.environ.get("DISTRIFLOW_BN_EPILOGUE", "0") != "0"):
+            H, W, C = self.in_shape
+            OH, OW, N = self.out_shape
+            kpad = primary_kpad_of(self)
+            self._bn_ntm = ops.conv_bn_tiles(B, H, W, C, OH, OW, N, self.k, self.k, self.stride, self.pad, kpad)
+            if self._bn_ntm:
+                self.bn_part = torch.empty(self._bn_ntm * 2 * N, dtype=torch.float32, device=device)
 
-    def forward(self, x, training):
+    def forward(self, x, training, bn: Optional["BatchNorm"] = None):
+        """``bn``: the BatchNorm that consumes this output; in training its batch statistics come from this
+        launch's epilogue when the kernel can emit them (no statistics pass over the output)."""
         self.x = x
         st = self.store
         b = st[f"{self.name}/bias"] if self.use_bias else None
+        part = self.bn_part if (bn is not None and training and self._bn_ntm) else None
         ops.conv_fwd(x, st.weight(f"{self.name}/kernel"), b, self.out, self.k, self.k, self.stride, self.pad,
-                     relu=self.relu)
+                     relu=self.relu, bn_part=part)
+        if part is not None:
+            bn.stats_from_partials(part, self._bn_ntm, self.out)
         return self.out
 
     def backward(self, dy, residual=None, residual_mask=None, dx_mask=None):
@@ -384,10 +405,20 @@ class BatchNorm(Layer):
                      residual.reshape(-1, self.C) if residual is not None else None, rbn, not training, self.eps)
         return out
 
+    def stats_from_partials(self, part, ntm, x):
+        """Batch statistics from the producing conv's epilogue partial sums (replaces :meth:`stats`)."""
+        self.x = x
+        ops.bn_finalize_partials(part, ntm, self.C, x.numel() // self.C, self.mean, self.invstd, self.run_mean,
+                                 self.run_var, self.momentum, self.eps)
+        self._stats_ready = True
+
+    _stats_ready = False
+
     def forward(self, x, training):
         self.x = x
-        if training:
+        if training and not self._stats_ready:
             self.stats(x)
+        self._stats_ready = False
         return self.apply(x, self.out, training)
 
     def backward(self, dy, mask=None):
@@ -491,18 +522,20 @@ class ResidualBlock(Layer):
 
     def forward(self, x, training):
         self.x = x
-        h = self.conv1.forward(x, training)
+        h = self.conv1.forward(x, training, bn=self.bn1)
         h = self.bn1.forward(h, training)
-        h = self.conv2.forward(h, training)
+        h = self.conv2.forward(h, training, bn=self.bn2)
         self.bn2.x = h
-        if training:
+        if training and not self.bn2._stats_ready:
             self.bn2.stats(h)
+        self.bn2._stats_ready = False
         r, rbn = x, None
         if self.proj is not None:
-            p = self.proj.forward(x, training)
+            p = self.proj.forward(x, training, bn=self.proj_bn)
             self.proj_bn.x = p
-            if training:
+            if training and not self.proj_bn._stats_ready:
                 self.proj_bn.stats(p)
+            self.proj_bn._stats_ready = False
             r, rbn = p, self.proj_bn
         # one streaming pass: out = relu(bn2(h) + shortcut), shortcut = x or proj_bn(proj(x))
         self.bn2.apply(h, self.out, training, residual=r, residual_bn=rbn, relu=True)

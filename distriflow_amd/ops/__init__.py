@@ -115,17 +115,34 @@ def dense_wgrad(dy, x, gw, gb, workspace=None, scale=1.0):
 
 
 # ----------------------------------------------------------------------------------- conv2d
-def conv_fwd(x, w, bias, out, KH, KW, stride=1, pad=0, relu=False):
-    """NHWC conv: out[B][OH][OW][N]; w = [Npad][Kpad] with K = KH*KW*C."""
+def conv_fwd(x, w, bias, out, KH, KW, stride=1, pad=0, relu=False, bn_part=None):
+    """NHWC conv: out[B][OH][OW][N]; w = [Npad][Kpad] with K = KH*KW*C.  ``bn_part``: buffer for the
+    per-row-tile BatchNorm partial sums of the output (:func:`conv_bn_tiles` rows of [2][N])."""
     B, H, W, C = x.shape
     _, OH, OW, N = out.shape
     if x.is_cuda:
         K = KH * KW * C
+        kw = {} if bn_part is None else {"bn_part": bn_part}
         _C().igemm_fwd(x, w, bias, None, out, B * OH * OW, N, K, w.shape[1], 0, N,
-                       _geom(H, W, C, OH, OW, KH, KW, stride, pad), MODE_FWD, relu, 1.0)
+                       _geom(H, W, C, OH, OW, KH, KW, stride, pad), MODE_FWD, relu, 1.0, **kw)
     else:
         out.copy_(ref.conv_fwd(x, w, bias, KH, KW, stride, pad, relu))
     return out
+
+
+def conv_bn_tiles(B, H, W, C, OH, OW, N, KH, KW, stride, pad, Kpad) -> int:
+    """Row tiles of the conv forward launch when it can emit BatchNorm partial sums (0: it cannot)."""
+    m = native.get(build_if_missing=False)
+    if m is None or not hasattr(m, "igemm64_bn_tiles"):
+        return 0
+    return int(m.igemm64_bn_tiles(B * OH * OW, N, KH * KW * C, Kpad, _geom(H, W, C, OH, OW, KH, KW, stride, pad),
+                                  MODE_FWD))
+
+
+def bn_finalize_partials(part, ntm, C, M, mean, invstd, run_mean, run_var, momentum, eps):
+    """mean / invstd (+ running statistics) from a conv epilogue's partial sums (csrc/bn.hip)."""
+    _C().bn_finalize_partials(part, int(ntm), int(C), int(M), mean, invstd, run_mean, run_var, float(momentum),
+                              float(eps))
 
 
 def conv_pool_supported(H, W, C, KH, KW, stride, pad, N) -> bool:
