@@ -169,7 +169,7 @@ class DataParallelTrainer:
     phase_timer = None  # utils.logging.PhaseTimer: per-phase GPU time of eager steps
 
     # single rank + fused LeNet-5: the reduce kernel applies the update itself (no optimizer launch)
-    fused_update = os.environ.get("DISTRIFLOW_LENET_FUSED_UPDATE", "0") != "0"
+    fused_update = os.environ.get("DISTRIFLOW_LENET_FUSED_UPDATE", "1") != "0"
 
     def _step_body(self, x, y):
         hook = self._grad_ready if (self.overlap and self.world > 1) else None

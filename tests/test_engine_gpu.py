@@ -313,7 +313,7 @@ def test_bn_statistics_from_conv_epilogue(monkeypatch):
     b, sb, bnb, fb = run("1")
     assert fa == 0 and fb > 0
     for u, v in zip(bna, bnb):
-        torch.testing.assert_close(v.mean, u.mean, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(v.mean, u.mean, rtol=1e-3, atol=1e-4)  # fp32 sums in another order
         torch.testing.assert_close(v.invstd, u.invstd, rtol=1e-3, atol=1e-4)
         torch.testing.assert_close(v.run_var, u.run_var, rtol=1e-3, atol=1e-5)
     assert abs(float(sa[0]) - float(sb[0])) <= 1e-2 * abs(float(sa[0]))
