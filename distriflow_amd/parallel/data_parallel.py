@@ -58,7 +58,8 @@ class DataParallelTrainer:
         # gloo cannot run inside a hipGraph capture (it stages device tensors through the host): with a
         # gloo process group on GPUs (the one-GPU rehearsal mode) any bucket that is not on the one-shot
         # p2p path makes the step "split" (compute graph, eager all-reduce, SGD graph) from the start
-        if (self.world > 1 and self.net.is_gpu and self.graph_mode == "full" and dist.is_initialized()
+        if (self.world > 1 and self.net.is_gpu and self.graph_mode == "full" and self._step_all_reduces
+                and dist.is_initialized()
                 and dist.get_backend(self.group) == "gloo"
                 and any(self.p2p is None or (hi - lo) * 4 > self.p2p_limit for _, lo, hi in self.buckets)):
             self.graph_mode = "split"
@@ -167,6 +168,9 @@ class DataParallelTrainer:
 
     # ------------------------------------------------------------------ one step
     phase_timer = None  # utils.logging.PhaseTimer: per-phase GPU time of eager steps
+
+    # the step contains the gradient all-reduce (subclasses that exchange gradients otherwise say False)
+    _step_all_reduces = True
 
     # single rank + fused LeNet-5: the reduce kernel applies the update itself (no optimizer launch)
     fused_update = os.environ.get("DISTRIFLOW_LENET_FUSED_UPDATE", "1") != "0"
