@@ -573,6 +573,7 @@ long long igemm64_splitk_floats(const IGemmArgs& a, int mode) {
 
 int igemm64_bn_tiles(const IGemmArgs& a, int mode) {
   if (!igemm64_supported(a, mode) || a.pool_code || a.relu || a.mask || a.res || a.drop.on || a.out_f32) return 0;
+  if (igemm64_splitk_floats(a, mode) > 0) return 0;  // split-K launches keep the statistics pass
   const int BM = (a.N <= 64 || (long long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 512) ? 128 : 64;  // launch64_mode
   return cdiv(a.M, BM);
 }
