@@ -118,17 +118,13 @@ __device__ __forceinline__ void store_x0(const X0Regs& r, bf16* x0) {
 // ps, ps + 64, ...; the FMA chain is the per-layer kernel's (smallc.hip c1_fwd_kernel), so X1 is equal
 // bit for bit.
 __device__ __forceinline__ void conv1_to_lds(const KcnnArgs& a, const bf16* x0, bf16* x1) {
-  // channel pairs in packed fp32 (v_pk_fma_f32: two FMAs per lane per instruction, each the same
-  // single-rounding fma as the scalar chain)
-  typedef float f2 __attribute__((ext_vector_type(2)));
   const int g = threadIdx.x & 3, ps = threadIdx.x >> 2;
-  f2 w[4][9], bias[4];
+  float w[8][9], bias[8];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < 8; ++j) {
 #pragma unroll
-    for (int k = 0; k < 9; ++k)
-      w[j][k] = f2{(float)a.w1[(8 * g + 2 * j) * a.kpad1 + k], (float)a.w1[(8 * g + 2 * j + 1) * a.kpad1 + k]};
-    bias[j] = f2{a.b1[8 * g + 2 * j], a.b1[8 * g + 2 * j + 1]};
+    for (int k = 0; k < 9; ++k) w[j][k] = (float)a.w1[(8 * g + j) * a.kpad1 + k];
+    bias[j] = a.b1[8 * g + j];
   }
   for (int p = ps; p < NP1; p += 64) {
     const int oy = p / H1, ox = p - oy * H1;
@@ -139,13 +135,11 @@ __device__ __forceinline__ void conv1_to_lds(const KcnnArgs& a, const bf16* x0, 
       for (int kx = 0; kx < 3; ++kx) xv[3 * ky + kx] = (float)x0[(oy + ky) * H0 + ox + kx];
     bf16x8 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      f2 acc = {0.f, 0.f};
+    for (int j = 0; j < 8; ++j) {
+      float acc = 0.f;
 #pragma unroll
-      for (int k = 0; k < 9; ++k) acc = __builtin_elementwise_fma(f2{xv[k], xv[k]}, w[j][k], acc);
-      const f2 v = acc + bias[j];
-      o[2 * j] = f2bf(fmaxf(v.x, 0.f));
-      o[2 * j + 1] = f2bf(fmaxf(v.y, 0.f));
+      for (int k = 0; k < 9; ++k) acc = fmaf(xv[k], w[j][k], acc);
+      o[j] = f2bf(fmaxf(acc * 1.f + bias[j], 0.f));
     }
     *reinterpret_cast<bf16x8*>(x1 + xsr(p, oy, 8 * g)) = o;
   }

@@ -35,7 +35,10 @@ def main():
     idx = torch.randperm(60000, device="cuda")[:B]
     x = ops.GatherRef(data, idx, 1 / 255.0, (28, 28, 1))
     dy = (torch.randn(B, 12, 12, 32, device="cuda") * 1e-3).to(torch.bfloat16)
-    print(f"fwd          {timed(lambda: blk.forward(x, True)):8.1f} us")
+    for mask, name in [(0, "fwd (all)"), (32, "- stores"), (16, "- conv2"), (48, "- conv2+st"), (112, "- +conv1")]:
+        m.kcnn_set_debug(mask)
+        print(f"{name:<12} {timed(lambda: blk.forward(x, True)):8.1f} us")
+    m.kcnn_set_debug(0)
     blk.forward(x, True)
     for mask, name in [(0, "bwd (all)"), (1, "- conv2 wgrad"), (2, "- dgrad+c1"), (3, "- both"), (7, "- +conv1"),
                        (15, "- +expand")]:
