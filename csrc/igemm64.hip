@@ -45,6 +45,29 @@ __device__ __forceinline__ u32x4_t gload16(const void* p) {
   return r;
 }
 
+// FAST path operand loads: raw buffer loads through a wave-uniform descriptor.  The per-k-step part of
+// the address is one uniform byte offset (SGPR soffset for the weights, one v_add for the activation
+// rows) and a masked-out chunk is an out-of-range voffset (>= num_records): the hardware returns zeros,
+// so no select between a data pointer and a zero constant and no 64-bit address math per load.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+constexpr unsigned kOOB = 0x80000000u;
+
+__device__ __forceinline__ i32x4_t make_rsrc(const void* base, unsigned bytes) {
+  const unsigned long long a = (unsigned long long)(uintptr_t)base;
+  i32x4_t r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((unsigned)(a >> 32) & 0xFFFFu));  // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+
+__device__ __forceinline__ u32x4_t bload16(i32x4_t rsrc, unsigned voff, unsigned soff) {
+  u32x4_t r;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(r) : "v"(voff), "s"(rsrc), "s"(soff) : "memory");
+  return r;
+}
+
 // lane exchanges inside groups of 4 lanes (DPP quad_perm: VALU latency, no LDS round trip)
 __device__ __forceinline__ int quad_xor1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
 __device__ __forceinline__ int quad_xor2(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false); }
@@ -63,9 +86,22 @@ constexpr int igemm64_occ() { return (160 * 1024) / ((BM + BN) * 256) > 4 ? 4 : 
 // of a 16-row MFMA block, i.e. four adjacent lanes; the epilogue reduces them with two lane shuffles
 // and writes only the pooled map [M/4][N] and a 1-byte argmax code per pooled element (4 = no
 // gradient: the ReLU'd max is 0).  d_ow then divides by the pooled width.
-template <int BM, int BN, int MODE, int D, bool SPLIT, bool POOL = false>
+//
+// FAST (conv gathers with SC % 64 == 0, K == KH*KW*SC, stride-1 data gradient or any forward): every
+// 64-deep k step is one filter tap (kh, kw) and one 64-channel block, so the step's address delta is the
+// same for every row and lane.  A row keeps a 32-bit byte offset and a bitmask of the taps that land
+// inside the image; a step costs ~4 VALU per activation row and none per weight row (the k offset is
+// the SGPR soffset), against ~23 VALU per MFMA of the generic gather (igemm64 PMC/ISA, round 2).
+//
+// PAR (FAST stride-2 data gradient): dX pixels of one parity class (ih % 2, iw % 2) receive only the
+// taps with kh = ih + pad (mod 2), kw likewise, so the output rows are grouped by class (class-major
+// tiles, rows (b, y, x) -> pixel (b, 2y + py, 2x + px)) and every tile runs only its class's taps:
+// 9 -> 1/2/2/4 taps for a 3x3 kernel instead of issuing MFMAs on the 3/4 of the gather that is zero.
+template <int BM, int BN, int MODE, int D, bool SPLIT, bool POOL = false, bool FAST = false, bool PAR = false>
 __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(IGemmArgs a, FastDiv d_ow, FastDiv d_ohw) {
   static_assert(!POOL || (MODE == MODE_FWD && !SPLIT), "pooled epilogue: plain conv forward only");
+  static_assert(!FAST || MODE != MODE_DIRECT, "FAST: conv gathers only");
+  static_assert(!PAR || (FAST && MODE == MODE_DGRAD && !SPLIT && !POOL), "PAR: FAST stride-2 data gradient");
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / (WM * 16), TN = BN / (WN * 16);
   constexpr int AP = BM / 32, BP = BN / 32;  // 16-byte chunks per thread and step (8 chunks per 64-deep row)
@@ -74,9 +110,32 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int ntn = cdiv(a.N, BN), ntm = cdiv(a.M, BM);
+  const int ntn = cdiv(a.N, BN);
+  // PAR: class (py, px) of this tile, its row count and size; the tiles of class 0 come first
+  int py = 0, px = 0, Mrows = a.M, cHc = 1, cWc = 1;
+  int ntm = cdiv(a.M, BM), ptiles = 0;
+  if constexpr (PAR) {
+    const int nimg = a.M / (a.OH * a.OW);
+    int rest = xcd_remap(blockIdx.x, (int)gridDim.x);
+    ptiles = (int)gridDim.x;
+    for (int cl = 0; cl < 4; ++cl) {
+      const int hc = (a.OH - (cl >> 1) + 1) >> 1, wc = (a.OW - (cl & 1) + 1) >> 1;
+      const int mc = nimg * hc * wc, tc = cdiv(mc, BM) * ntn;
+      if (rest < tc || cl == 3) {
+        py = cl >> 1;
+        px = cl & 1;
+        Mrows = mc;
+        cHc = hc;
+        cWc = wc;
+        ntm = cdiv(mc, BM);
+        ptiles = rest;
+        break;
+      }
+      rest -= tc;
+    }
+  }
   const int nsplit = SPLIT ? a.splits : 1;
-  const int logical0 = xcd_remap(blockIdx.x, ntn * ntm * nsplit);
+  const int logical0 = PAR ? ptiles : xcd_remap(blockIdx.x, ntn * ntm * nsplit);
   const int split = SPLIT ? logical0 / (ntn * ntm) : 0;
   const int logical = SPLIT ? logical0 - split * (ntn * ntm) : logical0;
   const int tile_n = logical % ntn, tile_m = logical / ntn;
@@ -98,9 +157,16 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
 #pragma unroll
   for (int i = 0; i < AP; ++i) {
     const int m = m0 + r0 + 32 * i;
-    rval[i] = m < a.M;
-    const unsigned mm = (unsigned)min(m, a.M - 1);
-    if (MODE == MODE_DIRECT) {
+    rval[i] = m < Mrows;
+    const unsigned mm = (unsigned)min(m, Mrows - 1);
+    if (PAR) {  // class-local row (b, y, x); base pixel (y + qh, x + qw), taps at -(jh, jw)
+      const int b = (int)mm / (cHc * cWc);
+      const int rem = (int)mm - b * cHc * cWc;
+      const int y = rem / cWc, x = rem - (rem / cWc) * cWc;
+      rbase[i] = (long long)b * a.SH * a.SW * a.SC;
+      rh[i] = y + ((py + a.pad) >> 1);
+      rw[i] = x + ((px + a.pad) >> 1);
+    } else if (MODE == MODE_DIRECT) {
       rbase[i] = (long long)mm * a.lda;
       rh[i] = rw[i] = 0;
     } else {
@@ -127,6 +193,52 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
     }
     rptr[i] = a.src + rbase[i] + ((long long)rh[i] * a.SW + rw[i]) * a.SC;
   }
+  // FAST row state: byte offset of the row's tap-(0,0) pixel + this thread's chunk, and the taps in range
+  int roff[FAST ? AP : 1];
+  unsigned rtaps[FAST ? AP : 1];
+  int woff[FAST ? BP : 1];
+  i32x4_t rsA, rsB;
+  // uniform k-step state: tap (ukh, ukw) of the tap grid, channel block ucb.  The tap grid is
+  // kh = tkh0 + tstep * ukh (tnh taps), kw likewise: the whole filter, or one parity class's taps (PAR)
+  int ukh = 0, ukw = 0, ucb = 0;
+  int tkh0 = 0, tkw0 = 0, tnh = a.KH, tnw = a.KW;
+  constexpr int tstep = PAR ? 2 : 1;
+  if constexpr (PAR) {
+    tkh0 = (py + a.pad) & 1;
+    tkw0 = (px + a.pad) & 1;
+    tnh = a.KH > tkh0 ? (a.KH - tkh0 + 1) >> 1 : 0;
+    tnw = a.KW > tkw0 ? (a.KW - tkw0 + 1) >> 1 : 0;
+  }
+  if constexpr (FAST) {
+#pragma unroll
+    for (int i = 0; i < AP; ++i) {
+      roff[i] = (int)((rbase[i] + ((long long)rh[i] * a.SW + rw[i]) * a.SC) * 2) + 16 * c;
+      unsigned mk = 0;
+      if (rval[i]) {
+        for (int jh = 0; jh < tnh; ++jh)
+          for (int jw = 0; jw < tnw; ++jw) {
+            const int sh = MODE == MODE_FWD ? rh[i] + jh : rh[i] - jh;
+            const int sw = MODE == MODE_FWD ? rw[i] + jw : rw[i] - jw;
+            if ((unsigned)sh < (unsigned)a.SH && (unsigned)sw < (unsigned)a.SW) mk |= 1u << (jh * tnw + jw);
+          }
+      }
+      rtaps[i] = mk;
+    }
+    const int nimg = a.M / (a.OH * a.OW);
+    rsA = make_rsrc(a.src, (unsigned)((long long)nimg * a.SH * a.SW * a.SC * 2));
+    const int npad16 = round_up(a.N, 16);
+    rsB = make_rsrc(a.w, (unsigned)((long long)npad16 * a.Kpad * 2));
+#pragma unroll
+    for (int i = 0; i < BP; ++i) {
+      const int n = n0 + r0 + 32 * i;
+      woff[i] = n < npad16 ? (int)((long long)n * a.Kpad * 2) + 16 * c : (int)kOOB;
+    }
+    const int kb = kt_begin * 64;
+    const int t = kb / a.SC;
+    ucb = (kb - t * a.SC) >> 6;
+    ukh = t / a.KW;
+    ukw = t - ukh * a.KW;
+  }
   const bf16* wptr[BP];
   bool wval[BP];
   const int npad = round_up(a.N, 16);
@@ -150,6 +262,21 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
   // single wave per SIMD (the small-M layers launch one workgroup per CU)
   u32x4_t ra[D][AP], rb[D][BP];
   auto gload = [&](int st) {
+    if constexpr (FAST) {
+      const int tap = ukh * tnw + ukw;
+      const int tpix = ukh * a.SW + ukw;
+      const int toff = ((MODE == MODE_FWD ? tpix : -tpix) * a.SC + ucb * 64) * 2;
+#pragma unroll
+      for (int i = 0; i < AP; ++i) {
+        const unsigned vo = ((rtaps[i] >> tap) & 1u) ? (unsigned)(roff[i] + toff) : kOOB;
+        ra[st][i] = bload16(rsA, vo, 0u);
+      }
+      // this step's weight column in bytes (the weights' soffset)
+      const unsigned ks = (unsigned)((((tkh0 + tstep * ukh) * a.KW + tkw0 + tstep * ukw) * a.SC + ucb * 64) * 2);
+#pragma unroll
+      for (int i = 0; i < BP; ++i) rb[st][i] = bload16(rsB, (unsigned)woff[i], ks);
+      return;
+    }
     const bool kv = kk < a.K;
     // k-step offset of this thread's chunk relative to the row pointer (same for every row)
     const int koff = (MODE == MODE_FWD) ? (kh * a.SW + kw) * a.SC + ci : ci - (kh * a.SW + kw) * a.SC;
@@ -187,6 +314,16 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
   };
   auto advance = [&]() {
     kk += 64;
+    if constexpr (FAST) {
+      if (++ucb * 64 == a.SC) {
+        ucb = 0;
+        if (++ukw == tnw) {
+          ukw = 0;
+          ++ukh;
+        }
+      }
+      return;
+    }
     if (MODE != MODE_DIRECT) {
       ci += 64;
       while (ci >= a.SC) {
@@ -213,9 +350,10 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = max(kt_end - kt_begin, 0);  // k steps of this workgroup (a whole K without split-K)
+  // k steps of this workgroup (a whole K without split-K; the class's taps under PAR)
+  const int nk = PAR ? tnh * tnw * (a.SC >> 6) : max(kt_end - kt_begin, 0);
   // prologue: step 0 -> LDS[0]; steps 1..D in flight (register stage of step s = s % D)
-  gload(0);
+  if (nk > 0) gload(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   sstore(0, 0);
 #pragma unroll
@@ -338,12 +476,19 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int row = m0 + wm * TM * 16 + i * 16 + fr;
-    if (row >= a.M) continue;
+    if (row >= Mrows) continue;
+    long long orow = row;
+    if (PAR) {  // class-local row -> dX pixel (b, 2y + py, 2x + px)
+      const int b = row / (cHc * cWc);
+      const int rem = row - b * cHc * cWc;
+      const int y = rem / cWc, x = rem - (rem / cWc) * cWc;
+      orow = ((long long)b * a.OH + 2 * y + py) * a.OW + 2 * x + px;
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col0 = n0 + wn * TN * 16 + j * 16 + fq * 4;
       if (col0 >= a.N) continue;
-      const long long o = (long long)row * a.ldc + col0;
+      const long long o = orow * a.ldc + col0;
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * a.alpha + ((a.bias && col0 + r < a.N) ? a.bias[col0 + r] : 0.f);
@@ -527,6 +672,18 @@ static int splitk_for(const IGemmArgs& a) {
   return s;
 }
 
+// FAST gather eligibility (see igemm64_kernel): whole 64-channel blocks per tap, <= 32 taps, stride-1
+// data gradient, and operands addressable with 32-bit byte offsets below the out-of-range marker
+static bool igemm64_fast_ok(const IGemmArgs& a, int mode) {
+  if (mode == MODE_DIRECT || a.SC % 64 || a.K != a.KH * a.KW * a.SC || a.KH * a.KW > 32 || a.Kpad < a.K) return false;
+  if (mode == MODE_DGRAD && a.stride != 1 && a.stride != 2) return false;
+  if (a.OH <= 0 || a.OW <= 0 || a.M % (a.OH * a.OW)) return false;
+  if (const char* e = getenv("DISTRIFLOW_IGEMM_FAST"); e && e[0] == '0') return false;
+  const long long sbytes = (long long)(a.M / (a.OH * a.OW)) * a.SH * a.SW * a.SC * 2;
+  const long long wbytes = (long long)round_up(a.N, 16) * a.Kpad * 2;
+  return sbytes < (1LL << 30) && wbytes < (1LL << 30);
+}
+
 template <int BM, int BN, int MODE>
 hipError_t launch64(IGemmArgs a, hipStream_t st) {
   const FastDiv d_ow = make_fastdiv((unsigned)max(a.OW, 1)), d_ohw = make_fastdiv((unsigned)max(a.OH * a.OW, 1));
@@ -537,17 +694,43 @@ hipError_t launch64(IGemmArgs a, hipStream_t st) {
                        make_fastdiv((unsigned)max(a.OW / 2, 1)), d_ohw);
     return hipGetLastError();
   }
+  constexpr bool kFastMode = MODE != MODE_DIRECT;
+  const bool fast = kFastMode && igemm64_fast_ok(a, MODE);
+  if (MODE == MODE_DGRAD && a.stride == 2) {
+    if (!fast) {
+      hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE, D, false>), dim3(blocks), dim3(256), 0, st, a, d_ow, d_ohw);
+      return hipGetLastError();
+    }
+    // parity classes: grid = sum of the 4 classes' tiles (no split-K)
+    const int nimg = a.M / (a.OH * a.OW);
+    int grid = 0;
+    for (int cl = 0; cl < 4; ++cl) {
+      const int hc = (a.OH - (cl >> 1) + 1) >> 1, wc = (a.OW - (cl & 1) + 1) >> 1;
+      grid += cdiv(nimg * hc * wc, BM) * cdiv(a.N, BN);
+    }
+    constexpr int kParMode = MODE == MODE_DGRAD ? MODE_DGRAD : MODE_FWD;
+    hipLaunchKernelGGL((igemm64_kernel<BM, BN, kParMode, D, false, false, true, MODE == MODE_DGRAD>), dim3(grid),
+                       dim3(256), 0, st, a, d_ow, d_ohw);
+    return hipGetLastError();
+  }
   const int s = a.splitk_ws ? splitk_for<BM, BN>(a) : 1;
   if (s > 1) {
     a.splits = s;
-    hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE, D, true>), dim3(blocks * s), dim3(256), 0, st, a, d_ow, d_ohw);
+    if (fast)
+      hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE, D, true, false, kFastMode>), dim3(blocks * s), dim3(256), 0, st, a, d_ow, d_ohw);
+    else
+      hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE, D, true>), dim3(blocks * s), dim3(256), 0, st, a, d_ow, d_ohw);
     DFA_HIP_CHECK(hipGetLastError());
     const long long total4 = (long long)a.M * (a.N / 4);
     const int grid = (int)min((total4 + 255) / 256, 4096LL);
     hipLaunchKernelGGL(igemm64_splitk_epilogue_kernel, dim3(grid), dim3(256), 0, st, a);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE, D, false>), dim3(blocks), dim3(256), 0, st, a, d_ow, d_ohw);
+  // (prefetch depths 3 and 4 measured equal to 2 on every ResNet-18 shape: scripts/convbench.py)
+  if (fast)
+    hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE, D, false, false, kFastMode>), dim3(blocks), dim3(256), 0, st, a, d_ow, d_ohw);
+  else
+    hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE, D, false>), dim3(blocks), dim3(256), 0, st, a, d_ow, d_ohw);
   return hipGetLastError();
 }
 

@@ -139,6 +139,14 @@ CONVS = [  # B, H, W, C, N, k, stride, pad
     (2, 16, 16, 64, 128, 3, 2, 1),
     (2, 8, 8, 64, 128, 1, 2, 0),
     (3, 9, 7, 16, 24, 3, 2, 1),
+    # 64-channel multiples at stride 1: the igemm64 FAST gather (buffer loads, per-row tap masks) in
+    # both the forward and the data gradient
+    (2, 8, 8, 128, 64, 3, 1, 1),
+    (3, 10, 6, 64, 64, 3, 1, 1),
+    (2, 5, 7, 64, 128, 1, 1, 0),
+    # stride-2 data gradients over parity classes (igemm64 PAR): odd sizes, zero-tap classes of a 1x1
+    (3, 9, 7, 64, 64, 3, 2, 1),
+    (2, 7, 9, 128, 64, 1, 2, 0),
 ]
 
 
@@ -353,17 +361,20 @@ def test_bn_apply_residual_join(proj):
     _close(y, torch.relu(e))
 
 
-def test_conv_dgrad_residual_epilogue():
-    """ResNet block join in the dgrad epilogue: dx = (conv^T dy + res * [resmask > 0]) * [mask > 0]."""
+@pytest.mark.parametrize("s", [1, 2])
+def test_conv_dgrad_residual_epilogue(s):
+    """ResNet block join in the dgrad epilogue: dx = (conv^T dy + res * [resmask > 0]) * [mask > 0]
+    (stride 2: the parity-class data gradient, whose epilogue remaps rows to pixels)."""
     B, H, W, C, N, k = 4, 16, 16, 64, 64, 3
-    dy = torch.randn(B, H, W, N, device=dev).to(torch.bfloat16)
+    OH, OW = ops.conv_out_hw(H, W, k, k, s, 1)
+    dy = torch.randn(B, OH, OW, N, device=dev).to(torch.bfloat16)
     w = torch.randn(N, k * k * C, device=dev) / (k * k * N) ** 0.5
     res = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
     rmask = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
     mask = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
     out = torch.empty(B, H, W, C, device=dev, dtype=torch.bfloat16)
-    ops.conv_dgrad(dy, None, _pad_wt(w, N, k * k, C), out, k, k, 1, 1, mask=mask, residual=res, residual_mask=rmask)
-    exp = ref.conv_dgrad(dy.float(), w.to(torch.bfloat16).float(), (B, H, W, C), k, k, 1, 1, None)
+    ops.conv_dgrad(dy, None, _pad_wt(w, N, k * k, C), out, k, k, s, 1, mask=mask, residual=res, residual_mask=rmask)
+    exp = ref.conv_dgrad(dy.float(), w.to(torch.bfloat16).float(), (B, H, W, C), k, k, s, 1, None)
     exp = (exp + res.float() * (rmask.float() > 0)) * (mask.float() > 0)
     _close(out, exp)
 
