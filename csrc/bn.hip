@@ -27,8 +27,18 @@ static bool bn_vec(int C) { return C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) =
 
 static int bn_rows_per_pass(int C, bool vec) { return 256 / (vec ? C / 8 : C); }
 
+// rows per thread of the statistics pass (default 16; DISTRIFLOW_BN_RPT overrides, read once)
+static int bn_rows_per_thread() {
+  static const int r = [] {
+    const char* e = getenv("DISTRIFLOW_BN_RPT");
+    const int v = e ? atoi(e) : 16;
+    return v >= 1 && v <= 64 ? v : 16;
+  }();
+  return r;
+}
+
 static int bn_grid(int M, int rpp) {
-  int g = cdiv(M, rpp * 16);
+  int g = cdiv(M, rpp * bn_rows_per_thread());
   if (g > BN_MAX_G) g = BN_MAX_G;
   if (g < 1) g = 1;
   return g;

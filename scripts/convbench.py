@@ -44,7 +44,10 @@ SHAPES = [  # name, B, H, W, C, N, k, stride, pad
 def main():
     ws = torch.empty(1 << 25, device=dev)
     tot = 0.0
+    only = sys.argv[1] if len(sys.argv) > 1 else None
     for name, B, H, W, C, N, k, s, p in SHAPES:
+        if only and name != only:
+            continue
         OH, OW = ops.conv_out_hw(H, W, k, k, s, p)
         x = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
         w = torch.randn(N, k * k * C, device=dev) / (k * k * C) ** 0.5
