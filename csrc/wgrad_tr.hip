@@ -55,17 +55,16 @@ __device__ __forceinline__ u32x4_t gload16_tr(const void* p) {
 constexpr int kWgradStages = 2;  // register prefetch depth (m-steps in flight)
 
 // workgroups per CU the LDS allows (2 x 64 rows x (SN + SK) bf16 each): register cap to match
-template <int BN, int BK>
+template <int BN, int BK, int BM = 64>
 constexpr int wgrad_tr_occ() {
-  return (160 * 1024) / (2 * 64 * (tr_stride(BN) + tr_stride(BK)) * 2) > 4
+  return (160 * 1024) / (2 * BM * (tr_stride(BN) + tr_stride(BK)) * 2) > 4
              ? 4
-             : (160 * 1024) / (2 * 64 * (tr_stride(BN) + tr_stride(BK)) * 2);
+             : (160 * 1024) / (2 * BM * (tr_stride(BN) + tr_stride(BK)) * 2);
 }
 
-template <int BN, int BK, int WN, int WK>
-__global__ void __launch_bounds__(256, (wgrad_tr_occ<BN, BK>())) wgrad_tr_kernel(WgradArgs a, FastDiv d_ow, FastDiv d_ohw) {
+template <int BN, int BK, int WN, int WK, int BM = 64>
+__global__ void __launch_bounds__(256, (wgrad_tr_occ<BN, BK, BM>())) wgrad_tr_kernel(WgradArgs a, FastDiv d_ow, FastDiv d_ohw) {
   constexpr int D = kWgradStages;
-  constexpr int BM = 64;
   constexpr int SN = tr_stride(BN), SK = tr_stride(BK);
   constexpr int TN = BN / (WN * 16), TK = BK / (WK * 16);
   constexpr int DC = BN / 8, XC = BK / 8;      // 16-byte chunks per tile row
@@ -220,21 +219,25 @@ __global__ void __launch_bounds__(256, (wgrad_tr_occ<BN, BK>())) wgrad_tr_kernel
   }
 }
 
-template <int BN, int BK, int WN, int WK>
+template <int BN, int BK, int WN, int WK, int BM = 64>
 hipError_t launch_wgrad_tr(WgradArgs a, float* ws, size_t ws_floats, hipStream_t st) {
   const int Kt = a.K + (a.with_bias ? 1 : 0);
   const int tiles = cdiv(a.N, BN) * cdiv(a.K + (a.with_bias ? 8 : 0), BK);
-  // about two workgroups per CU (73.7 KB of LDS each), each reducing >= 256 rows
-  int splits = cdiv(512, tiles);
+  // about two workgroups per CU (73.7 KB of LDS each at BM = 64), each reducing >= 256 rows
+  static const int target = [] {
+    const char* e = getenv("DISTRIFLOW_WGRAD_WG");
+    return e ? atoi(e) : 512;
+  }();
+  int splits = cdiv(target, tiles);
   splits = min(splits, cdiv(a.M, 256));
   splits = max(splits, 1);
   while (splits > 1 && (size_t)splits * a.N * Kt > ws_floats) --splits;
-  a.m_per_split = round_up(cdiv(a.M, splits), 64);
+  a.m_per_split = round_up(cdiv(a.M, splits), BM);
   splits = cdiv(a.M, a.m_per_split);
   a.splits = splits;
   a.partial = ws;
   const FastDiv d_ow = make_fastdiv((unsigned)a.OW), d_ohw = make_fastdiv((unsigned)(a.OH * a.OW));
-  hipLaunchKernelGGL((wgrad_tr_kernel<BN, BK, WN, WK>), dim3(tiles * splits), dim3(256), 0, st, a, d_ow, d_ohw);
+  hipLaunchKernelGGL((wgrad_tr_kernel<BN, BK, WN, WK, BM>), dim3(tiles * splits), dim3(256), 0, st, a, d_ow, d_ohw);
   DFA_HIP_CHECK(hipGetLastError());
   if (splits > 1) DFA_HIP_CHECK(slab_reduce(ws, a.gw, a.with_bias ? a.gb : nullptr, a.N, a.K, Kt, splits, a.scale, st));
   return hipSuccess;
@@ -250,7 +253,11 @@ bool wgrad_tr_supported(const WgradArgs& a, int mode) {
 hipError_t wgrad_tr(const WgradArgs& a, float* ws, size_t ws_floats, hipStream_t st) {
   if (a.N >= 128) return launch_wgrad_tr<128, 128, 2, 2>(a, ws, ws_floats, st);
   if (a.N <= 32) return launch_wgrad_tr<32, 128, 1, 4>(a, ws, ws_floats, st);  // Keras CNN conv2: no empty rows
-  return launch_wgrad_tr<64, 128, 2, 2>(a, ws, ws_floats, st);
+  // 64-channel tiles step 32 rows at a time: 36.9 KB of LDS -> 4 workgroups per CU (ResNet layer 1:
+  // 104 -> 82 us).  The 128 x 128 tile at 32 rows would need more than the 128 VGPRs of 4 workgroups per
+  // CU and spills, which the inline-asm loads (destinations unprotected until their counted wait)
+  // cannot tolerate: it stays at 64 rows.
+  return launch_wgrad_tr<64, 128, 2, 2, 32>(a, ws, ws_floats, st);
 }
 
 }  // namespace dfa

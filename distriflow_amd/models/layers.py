@@ -40,6 +40,7 @@ class Layer:
         self.out_shape: tuple = ()
         self.relu = False          # output passed through a fused ReLU
         self.in_relu = False       # input is a ReLU output (apply relu' in backward)
+        self.grad_premasked = False  # relu' of this layer's output already applied to dy by the consumer
         # a Dropout that follows this layer, folded into its forward epilogue (Net._fold_dropout); the
         # consumer then applies the dropout backward: relu'(its input) * dx_scale = keep / (1 - p)
         self.drop: Optional["Dropout"] = None
@@ -246,12 +247,20 @@ class Conv2D(Layer):
     def backward(self, dy, residual=None, residual_mask=None, dx_mask=None):
         """``residual`` / ``residual_mask`` / ``dx_mask``: the ResNet block join fused into the dgrad
         epilogue, dx = (conv^T dy + residual * [residual_mask > 0]) * [dx_mask > 0]."""
+        self.backward_weights(dy)
+        return self.backward_data(dy, residual, residual_mask, dx_mask)
+
+    def backward_weights(self, dy):
         st = self.store
         kn = f"{self.name}/kernel"
         gb = st.gradient(f"{self.name}/bias") if self.use_bias else None
         ops.conv_wgrad(dy, self.x, st.grad_matrix(kn), gb, self.ws.wgrad, self.k, self.k, self.stride, self.pad)
+
+    def backward_data(self, dy, residual=None, residual_mask=None, dx_mask=None):
         if not self.need_dx:
             return None
+        st = self.store
+        kn = f"{self.name}/kernel"
         mask = dx_mask if dx_mask is not None else (self.x if self.in_relu else None)
         ops.conv_dgrad(dy, st.weight(kn), st.weight_t(kn), self.dx, self.k, self.k, self.stride, self.pad,
                        mask=mask, residual=residual, residual_mask=residual_mask)
@@ -424,7 +433,7 @@ class BatchNorm(Layer):
     def backward(self, dy, mask=None):
         """``mask``: relu' source applied to dy (default: this layer's own output when it ends in ReLU)."""
         st = self.store
-        if mask is None and self.relu:
+        if mask is None and self.relu and not self.grad_premasked:
             mask = self.out
         ops.bn_bwd(self.x.reshape(-1, self.C), mask.reshape(-1, self.C) if mask is not None else None,
                    dy.reshape(-1, self.C), self.dx.view(-1, self.C), st[f"{self.name}/gamma"], self.mean, self.invstd,
@@ -464,6 +473,8 @@ class ResidualBlock(Layer):
     kernel (``add_act``) and its relu' is applied once to the incoming gradient.
     """
     has_params = True
+
+    side_stream = None  # set by the engine: stream for the weight gradients (None: in order on the main stream)
 
     def __init__(self, filters: int, stride: int = 1, name=None):
         super().__init__(name or "block")
@@ -542,23 +553,43 @@ class ResidualBlock(Layer):
         return self.out
 
     def backward(self, dy):
-        # relu' of the block output is applied inside both BN backward passes (mask = block output)
-        d = self.bn2.backward(dy, mask=self.out)
-        d = self.conv2.backward(d)
+        # relu' of the block output is applied inside both BN backward passes (mask = block output),
+        # unless the consumer already applied it to dy (grad_premasked: the next block's dgrad epilogue or
+        # the pooling backward masks with this block's output)
+        omask = None if self.grad_premasked else self.out
+        side = self.side_stream
+        if side is not None:
+            main = torch.cuda.current_stream(side.device)
+
+        def weights(conv, g):
+            # weight gradients on the side stream (the engine joins it before the gradients are read):
+            # they overlap the latency-bound BatchNorm passes and data gradients of the main chain
+            if side is None:
+                conv.backward_weights(g)
+                return
+            side.wait_event(main.record_event())
+            with torch.cuda.stream(side):
+                conv.backward_weights(g)
+
+        d = self.bn2.backward(dy, mask=omask)
+        weights(self.conv2, d)
+        d = self.conv2.backward_data(d)
         d = self.bn1.backward(d)
         ds = None
         if self.proj is not None:
-            ds = self.proj.backward(self.proj_bn.backward(dy, mask=self.out))
+            p = self.proj_bn.backward(dy, mask=omask)
+            weights(self.proj, p)
+            ds = self.proj.backward_data(p)
+        weights(self.conv1, d)
         if not self.need_dx:
-            self.conv1.backward(d)
             return None
         # conv1's dgrad epilogue joins the branches: dx = (conv1^T d + shortcut grad) * relu'(x), where the
         # shortcut gradient is proj^T(...) or the identity path's dy * relu'(out)
         if self.proj is not None:
             res, res_mask = ds, None
         else:
-            res, res_mask = dy, self.out
-        self.conv1.backward(d, residual=res, residual_mask=res_mask, dx_mask=self.x if self.in_relu else None)
+            res, res_mask = dy, omask
+        self.conv1.backward_data(d, residual=res, residual_mask=res_mask, dx_mask=self.x if self.in_relu else None)
         return self.dx
 
     def config(self):

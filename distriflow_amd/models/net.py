@@ -122,6 +122,10 @@ class Net:
         for j, l in enumerate(execd):
             l.need_dx = j > 0
             l.in_relu = j > 0 and execd[j - 1].relu
+        # a ReLU producer whose consumer applies relu' of its input receives an already masked gradient:
+        # its own backward can skip re-reading its output as the mask (ResNet blocks / BatchNorm+ReLU)
+        for j, l in enumerate(execd):
+            l.grad_premasked = bool(l.relu and j + 1 < len(execd) and execd[j + 1].in_relu)
         if self.fuse and self.is_gpu and os.environ.get("DISTRIFLOW_FOLD_DROPOUT", "1") != "0":
             execd = self._fold_dropout(execd)
         self.exec_layers = execd
@@ -378,6 +382,14 @@ class Net:
                 grad_ready(i)
         return self.stats
 
+    def _wgrad_side(self, layer):
+        """Side stream for ``layer``'s weight gradients (ResNet blocks on the GPU), else None.
+        ``DISTRIFLOW_WGRAD_OVERLAP=0`` keeps them in order on the main stream."""
+        if not isinstance(layer, ResidualBlock):
+            return None
+        on = self.is_gpu and os.environ.get("DISTRIFLOW_WGRAD_OVERLAP", "1") != "0"
+        return self._side[0] if on else None
+
     def _compute_gradients_head(self, x, labels, grad_ready):
         """Body layers one by one, then the fused dense head (2 launches: forward + CE + backward data
         chain, then all head weight gradients), then the body's backward from the head's dX."""
@@ -415,6 +427,7 @@ class Net:
             # fused conv+pool weight gradients defer their split-m slab reductions; consecutive ones are
             # flushed in ONE launch right before the next gradient hook needs them (or at the end)
             pending, waiting = [], []
+            side_used = False
             for i in range(self.head_start - 1, -1, -1):
                 l = self.exec_layers[i]
                 if isinstance(l, FusedConvPool) and self.is_gpu:
@@ -423,13 +436,32 @@ class Net:
                     continue
                 if pending:
                     ops.flush_slab_reductions(pending)
-                d = l.backward(d)
+                wside = self._wgrad_side(l)
+                if side_used and (wside is None or grad_ready is not None):
+                    # join the weight-gradient stream before a gradient hook or a layer that shares its
+                    # workspace (the stem conv's wgrad) runs on the main stream
+                    torch.cuda.current_stream(self.device).wait_stream(self._side[0])
+                    side_used = False
+                if wside is not None:
+                    l.side_stream = wside  # only for this call: other backward paths run in order
+                    try:
+                        d = l.backward(d)
+                    finally:
+                        l.side_stream = None
+                else:
+                    d = l.backward(d)
+                side_used = side_used or wside is not None
                 if grad_ready is not None:
+                    if side_used:
+                        torch.cuda.current_stream(self.device).wait_stream(self._side[0])
+                        side_used = False
                     for j in waiting + [i]:
                         grad_ready(j)
                 waiting = []
             if pending:
                 ops.flush_slab_reductions(pending)
+            if side_used:
+                torch.cuda.current_stream(self.device).wait_stream(self._side[0])
             if grad_ready is not None:
                 for j in waiting:
                     grad_ready(j)
