@@ -55,15 +55,16 @@ __device__ __forceinline__ u32x4_t gload16_tr(const void* p) {
 constexpr int kWgradStages = 2;  // register prefetch depth (m-steps in flight)
 
 // workgroups per CU the LDS allows (2 x 64 rows x (SN + SK) bf16 each): register cap to match
-template <int BN, int BK, int BM = 64>
+// (capped at MAXOCC: the register budget of MAXOCC workgroups must hold the kernel without spills)
+template <int BN, int BK, int BM = 64, int MAXOCC = 4>
 constexpr int wgrad_tr_occ() {
-  return (160 * 1024) / (2 * BM * (tr_stride(BN) + tr_stride(BK)) * 2) > 4
-             ? 4
+  return (160 * 1024) / (2 * BM * (tr_stride(BN) + tr_stride(BK)) * 2) > MAXOCC
+             ? MAXOCC
              : (160 * 1024) / (2 * BM * (tr_stride(BN) + tr_stride(BK)) * 2);
 }
 
-template <int BN, int BK, int WN, int WK, int BM = 64>
-__global__ void __launch_bounds__(256, (wgrad_tr_occ<BN, BK, BM>())) wgrad_tr_kernel(WgradArgs a, FastDiv d_ow, FastDiv d_ohw) {
+template <int BN, int BK, int WN, int WK, int BM = 64, int MAXOCC = 4>
+__global__ void __launch_bounds__(256, (wgrad_tr_occ<BN, BK, BM, MAXOCC>())) wgrad_tr_kernel(WgradArgs a, FastDiv d_ow, FastDiv d_ohw) {
   constexpr int D = kWgradStages;
   constexpr int SN = tr_stride(BN), SK = tr_stride(BK);
   constexpr int TN = BN / (WN * 16), TK = BK / (WK * 16);
@@ -219,7 +220,7 @@ __global__ void __launch_bounds__(256, (wgrad_tr_occ<BN, BK, BM>())) wgrad_tr_ke
   }
 }
 
-template <int BN, int BK, int WN, int WK, int BM = 64>
+template <int BN, int BK, int WN, int WK, int BM = 64, int MAXOCC = 4>
 hipError_t launch_wgrad_tr(WgradArgs a, float* ws, size_t ws_floats, hipStream_t st) {
   const int Kt = a.K + (a.with_bias ? 1 : 0);
   const int tiles = cdiv(a.N, BN) * cdiv(a.K + (a.with_bias ? 8 : 0), BK);
@@ -237,7 +238,7 @@ hipError_t launch_wgrad_tr(WgradArgs a, float* ws, size_t ws_floats, hipStream_t
   a.splits = splits;
   a.partial = ws;
   const FastDiv d_ow = make_fastdiv((unsigned)a.OW), d_ohw = make_fastdiv((unsigned)(a.OH * a.OW));
-  hipLaunchKernelGGL((wgrad_tr_kernel<BN, BK, WN, WK, BM>), dim3(tiles * splits), dim3(256), 0, st, a, d_ow, d_ohw);
+  hipLaunchKernelGGL((wgrad_tr_kernel<BN, BK, WN, WK, BM, MAXOCC>), dim3(tiles * splits), dim3(256), 0, st, a, d_ow, d_ohw);
   DFA_HIP_CHECK(hipGetLastError());
   if (splits > 1) DFA_HIP_CHECK(slab_reduce(ws, a.gw, a.with_bias ? a.gb : nullptr, a.N, a.K, Kt, splits, a.scale, st));
   return hipSuccess;
@@ -251,6 +252,12 @@ bool wgrad_tr_supported(const WgradArgs& a, int mode) {
 }
 
 hipError_t wgrad_tr(const WgradArgs& a, float* ws, size_t ws_floats, hipStream_t st) {
+  static const int t128 = [] {
+    const char* e = getenv("DISTRIFLOW_WGRAD128");
+    return e ? atoi(e) : 32;
+  }();
+  // 128 x 128 tiles at 32 rows per step, 3 workgroups per CU (170 VGPRs each: no spills)
+  if (a.N >= 128 && t128 == 32) return launch_wgrad_tr<128, 128, 2, 2, 32, 3>(a, ws, ws_floats, st);
   if (a.N >= 128) return launch_wgrad_tr<128, 128, 2, 2>(a, ws, ws_floats, st);
   if (a.N <= 32) return launch_wgrad_tr<32, 128, 1, 4>(a, ws, ws_floats, st);  // Keras CNN conv2: no empty rows
   // 64-channel tiles step 32 rows at a time: 36.9 KB of LDS -> 4 workgroups per CU (ResNet layer 1:
