@@ -15,6 +15,7 @@ Execution model (MI355X-first):
 """
 from __future__ import annotations
 
+import copy
 import math
 import os
 import zlib
@@ -475,6 +476,7 @@ class ResidualBlock(Layer):
     has_params = True
 
     side_stream = None  # set by the engine: stream for the weight gradients (None: in order on the main stream)
+    proj_stream = None  # set by the engine: stream for the projection shortcut branch (None: in order)
 
     def __init__(self, filters: int, stride: int = 1, name=None):
         super().__init__(name or "block")
@@ -527,12 +529,34 @@ class ResidualBlock(Layer):
             self.proj.need_dx = self.need_dx
         for l in self.sublayers():
             l.alloc(B, device, dtype, ws)
+        if self.proj is not None:
+            # the projection branch may run on its own stream (proj_stream): its BatchNorm gets a private
+            # statistics workspace so it never shares slabs with bn1 / bn2 on the main stream
+            pws = copy.copy(ws)
+            pws.bn = torch.empty_like(ws.bn)
+            self.proj_bn.ws = pws
         self.out = torch.empty((B,) + self.out_shape, device=device, dtype=dtype)
         # conv1's data gradient IS the block's: its dgrad epilogue adds the shortcut gradient and relu'(x)
         self.dx = self.conv1.dx if self.need_dx else None
 
+    def _proj_forward(self, x, training):
+        p = self.proj.forward(x, training, bn=self.proj_bn)
+        self.proj_bn.x = p
+        if training and not self.proj_bn._stats_ready:
+            self.proj_bn.stats(p)
+        self.proj_bn._stats_ready = False
+        return p
+
     def forward(self, x, training):
         self.x = x
+        ps = self.proj_stream if self.proj is not None else None
+        pev = None
+        if ps is not None:  # projection shortcut concurrently with conv1 -> bn1 -> conv2 -> bn2 statistics
+            main = torch.cuda.current_stream(ps.device)
+            ps.wait_event(main.record_event())
+            with torch.cuda.stream(ps):
+                p = self._proj_forward(x, training)
+                pev = ps.record_event()
         h = self.conv1.forward(x, training, bn=self.bn1)
         h = self.bn1.forward(h, training)
         h = self.conv2.forward(h, training, bn=self.bn2)
@@ -542,11 +566,10 @@ class ResidualBlock(Layer):
         self.bn2._stats_ready = False
         r, rbn = x, None
         if self.proj is not None:
-            p = self.proj.forward(x, training, bn=self.proj_bn)
-            self.proj_bn.x = p
-            if training and not self.proj_bn._stats_ready:
-                self.proj_bn.stats(p)
-            self.proj_bn._stats_ready = False
+            if pev is not None:
+                main.wait_event(pev)
+            else:
+                p = self._proj_forward(x, training)
             r, rbn = p, self.proj_bn
         # one streaming pass: out = relu(bn2(h) + shortcut), shortcut = x or proj_bn(proj(x))
         self.bn2.apply(h, self.out, training, residual=r, residual_bn=rbn, relu=True)
@@ -558,8 +581,7 @@ class ResidualBlock(Layer):
         # the pooling backward masks with this block's output)
         omask = None if self.grad_premasked else self.out
         side = self.side_stream
-        if side is not None:
-            main = torch.cuda.current_stream(side.device)
+        ps = self.proj_stream if self.proj is not None else None
 
         def weights(conv, g):
             # weight gradients on the side stream (the engine joins it before the gradients are read):
@@ -567,19 +589,31 @@ class ResidualBlock(Layer):
             if side is None:
                 conv.backward_weights(g)
                 return
-            side.wait_event(main.record_event())
+            side.wait_event(torch.cuda.current_stream(side.device).record_event())
             with torch.cuda.stream(side):
                 conv.backward_weights(g)
 
+        def proj_branch():
+            p = self.proj_bn.backward(dy, mask=omask)
+            weights(self.proj, p)
+            return self.proj.backward_data(p)
+
+        ds = pev = None
+        if ps is not None:  # the projection branch needs only dy: run it beside bn2 -> conv2 -> bn1
+            main = torch.cuda.current_stream(ps.device)
+            ps.wait_event(main.record_event())
+            with torch.cuda.stream(ps):
+                ds = proj_branch()
+                pev = ps.record_event()
         d = self.bn2.backward(dy, mask=omask)
         weights(self.conv2, d)
         d = self.conv2.backward_data(d)
         d = self.bn1.backward(d)
-        ds = None
         if self.proj is not None:
-            p = self.proj_bn.backward(dy, mask=omask)
-            weights(self.proj, p)
-            ds = self.proj.backward_data(p)
+            if pev is not None:
+                main.wait_event(pev)
+            else:
+                ds = proj_branch()
         weights(self.conv1, d)
         if not self.need_dx:
             return None

@@ -390,6 +390,13 @@ class Net:
         on = self.is_gpu and os.environ.get("DISTRIFLOW_WGRAD_OVERLAP", "1") != "0"
         return self._side[0] if on else None
 
+    def _proj_side(self, layer):
+        """Stream for a ResNet block's projection shortcut branch (joined inside the block), else None.
+        ``DISTRIFLOW_PROJ_OVERLAP=0`` keeps it in order."""
+        if not (isinstance(layer, ResidualBlock) and layer.proj is not None and self.is_gpu):
+            return None
+        return self._side[1] if os.environ.get("DISTRIFLOW_PROJ_OVERLAP", "1") != "0" else None
+
     def _compute_gradients_head(self, x, labels, grad_ready):
         """Body layers one by one, then the fused dense head (2 launches: forward + CE + backward data
         chain, then all head weight gradients), then the body's backward from the head's dX."""
@@ -398,7 +405,15 @@ class Net:
             x = x.materialise(self.x_buf, step_inc=self._take_gather_step())
         h = x
         for l in self.exec_layers[: self.head_start]:
-            h = l.forward(h, True)
+            ps = self._proj_side(l)
+            if ps is not None:
+                l.proj_stream = ps  # only for this call (joined inside the block)
+                try:
+                    h = l.forward(h, True)
+                finally:
+                    l.proj_stream = None
+            else:
+                h = l.forward(h, True)
         head = self.exec_layers[self.head_start:]
         if isinstance(labels, ops.LabelRef):
             lab, idx = labels.labels, labels.idx
@@ -444,10 +459,11 @@ class Net:
                     side_used = False
                 if wside is not None:
                     l.side_stream = wside  # only for this call: other backward paths run in order
+                    l.proj_stream = self._proj_side(l)
                     try:
                         d = l.backward(d)
                     finally:
-                        l.side_stream = None
+                        l.side_stream = l.proj_stream = None
                 else:
                     d = l.backward(d)
                 side_used = side_used or wside is not None
