@@ -748,7 +748,11 @@ hipError_t launch64_mode(const IGemmArgs& a, hipStream_t st) {
 }  // namespace
 
 long long igemm64_splitk_floats(const IGemmArgs& a, int mode) {
-  if (!igemm64_supported(a, mode) || a.N <= 64) return 0;
+  static const bool off = [] {
+    const char* e = getenv("DISTRIFLOW_IGEMM_SPLITK");
+    return e && e[0] == '0';
+  }();
+  if (off || !igemm64_supported(a, mode) || a.N <= 64) return 0;
   if ((long long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 512) return 0;  // 128 x 128 tiles: already filled
   const int s = splitk_for<64, 128>(a);
   return s > 1 ? (long long)s * a.M * a.N : 0;
