@@ -147,16 +147,25 @@ def main():
         return tr
 
     def timed(tr, steps):
-        """W untimed warm-up steps, then ``steps`` timed ones between barrier + device syncs; max over ranks."""
-        for _ in range(args.warmup):
-            tr.step()
+        """W untimed warm-up steps, then ``steps`` timed ones between barrier + device syncs; max over ranks.
+        The sync trainer replays its steps from multi-step hipGraphs (captured here, before timing)."""
+        multi = getattr(tr, "SUPPORTS_MULTISTEP", False) and os.environ.get("DISTRIFLOW_MULTISTEP", "1") != "0"
+        if multi:
+            tr.prepare_run(steps)
+            tr.run(args.warmup)
+        else:
+            for _ in range(args.warmup):
+                tr.step()
         sync()
         if world > 1:
             dist.barrier()
         sync()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            st = tr.step()
+        if multi:
+            st = tr.run(steps)
+        else:
+            for _ in range(steps):
+                st = tr.step()
         sync()
         if world > 1:
             dist.barrier()
@@ -216,6 +225,7 @@ def main():
                 "parallelism": f"dp{world}" if args.mode == "sync" else f"async-ps{world}",
                 "optimizer": "sgd",
                 "graph": trainer.graph_mode,
+                "steps_per_graph": getattr(trainer, "_multi_u", 0) or 1,
                 "allreduce": trainer.allreduce_path if world > 1 else None,
                 "params": net.num_params(),
             },

@@ -37,6 +37,7 @@ from .data_parallel import DataParallelTrainer
 class AsyncPSTrainer(DataParallelTrainer):
     _step_all_reduces = False  # gradients go to the parameter server, not through a collective
     fused_update = False       # the update is the parameter server's apply
+    SUPPORTS_MULTISTEP = False  # one graph per step (bench times it step by step)
 
     def __init__(self, net, lr: float = 0.001, max_staleness: int = 4, group=None, server_rank: int = 0,
                  graph: str = "full", timeout_s: float = 30.0):

@@ -66,6 +66,7 @@ class DataParallelTrainer:
             self.capture_error = "gloo collectives are not capturable"
         self._works = []
         self._graph = None
+        self._multi, self._multi_u = None, 0  # multi-step graph (prepare_run)
         self._graph_B = None
         self._index_stream = None
         self.steps = 0
@@ -328,6 +329,7 @@ class DataParallelTrainer:
         self.idx.copy_(stream[0])
         if self._index_stream is None or self._index_stream[0].shape != stream.shape:
             self._graph = None  # the captured optimizer launch references the stream buffers
+            self._multi, self._multi_u = None, 0
         self._index_stream = (stream, cursor, self.idx)
 
     def step(self):
@@ -383,6 +385,7 @@ class DataParallelTrainer:
                 return
             self._works = []
             self._graph = None
+            self._multi, self._multi_u = None, 0
             if self.graph_mode == "full":
                 self.graph_mode = "split"
             else:
@@ -390,6 +393,73 @@ class DataParallelTrainer:
                 self._gather()
                 self._last_eager = self._step_body(self.xb, self.yb)
                 return
+
+    # ------------------------------------------------------------------ multi-step graphs
+    MAX_STEPS_PER_GRAPH = 64
+    SUPPORTS_MULTISTEP = True
+
+    def prepare_run(self, n: int):
+        """Capture (outside any timed region) the graph :meth:`run` replays for ``n`` steps: up to
+        MAX_STEPS_PER_GRAPH consecutive full training steps unrolled into ONE hipGraph, so a run of n
+        steps is ceil(n / U) graph launches instead of n (the launch-bound inner loop of a small model
+        stays on the device).  Every step in it is the complete captured step (gather, forward,
+        backward, gradient exchange, update); the batch cursor, dropout counters and one-shot
+        all-reduce epochs all advance on the device.  Only in ``full`` graph mode."""
+        if self.graph_mode != "full" or not self.net.is_gpu or self._index_stream is None:
+            return
+        if self._graph is None:
+            self._capture_with_fallback()
+        u = max(1, min(int(n), self.MAX_STEPS_PER_GRAPH))
+        if self.graph_mode != "full" or self._graph is None or u <= 1 or self._multi_u == u:
+            return
+        net = self.net
+        snap = net.snapshot_state()
+        cursor = self._index_stream[1].clone() if self._index_stream is not None else None
+        idx0 = self.idx.clone()
+        torch.cuda.synchronize(net.device)
+        g = torch.cuda.CUDAGraph()
+        cs = torch.cuda.Stream(device=net.device)
+        ok = True
+        try:
+            with torch.cuda.graph(g, stream=cs):
+                for _ in range(u):
+                    self._gather()
+                    self.stats = self._step_body(self.xb, self.yb)
+        except Exception as e:
+            with torch.cuda.stream(cs):
+                if torch.cuda.is_current_stream_capturing():
+                    try:
+                        g.capture_end()
+                    except Exception:
+                        pass
+            self.capture_error = repr(e)
+            ok = False
+        torch.cuda.synchronize(net.device)
+        # capturing launches nothing, but restore anyway: the step state must be as before
+        net.restore_state(snap)
+        self.idx.copy_(idx0)
+        if cursor is not None:
+            self._index_stream[1].copy_(cursor)
+        if self.world > 1:  # all ranks use multi-step graphs or none do (identical collective sequences)
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=net.device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+            ok = bool(flag.item())
+        torch.cuda.synchronize(net.device)
+        self._multi = g if ok else None
+        self._multi_u = u if ok else 0
+
+    def run(self, n: int):
+        """``n`` training steps: multi-step graph replays (see :meth:`prepare_run`) plus single steps."""
+        st = None
+        if self._multi is not None and self._multi_u > 1:
+            for _ in range(n // self._multi_u):
+                self._multi.replay()
+                self.steps += self._multi_u
+                st = self.stats
+            n -= (n // self._multi_u) * self._multi_u
+        for _ in range(n):
+            st = self.step()
+        return st
 
     def _replay(self):
         g, g2 = self._graph

@@ -187,6 +187,35 @@ def test_index_stream_matches_explicit_indices():
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("name,B", [("lenet5", 256), ("keras_cnn", 64), ("resnet18_cifar", 32)])
+def test_multistep_graph_matches_single_steps(name, B):
+    """prepare_run(u) + run(n) (u steps unrolled into one hipGraph, bench.py's timed loop) trains exactly
+    like n single-step replays: same batches in the same order, bit-identical weights (ResNet: also the
+    side-stream weight gradients and the projection branch inside the unrolled graph)."""
+    from distriflow_amd.data.synthetic import synthetic_cifar10, synthetic_mnist
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
+
+    mk = synthetic_cifar10 if name == "resnet18_cifar" else synthetic_mnist
+    data, labels = mk(2048, device="cuda")
+    perm = epoch_permutations(2048, B, 16, "cuda", seed=2)
+    outs = []
+    for multi in (False, True):
+        net = build_model(name, device="cuda", seed=0)
+        tr = DataParallelTrainer(net, lr=0.05, graph="full")
+        tr.bind_dataset(data, labels, B, scale=1 / 255)
+        tr.bind_index_stream(perm)
+        if multi:
+            tr.prepare_run(4)
+            assert tr._multi_u == 4
+            tr.run(10)  # 2 multi-step replays + 2 single steps
+        else:
+            for _ in range(10):
+                tr.step()
+        torch.cuda.synchronize()
+        outs.append(net.store.master.clone())
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("name,B", [("lenet5", 512), ("keras_cnn", 64), ("resnet18_cifar", 32)])
 def test_gradients_are_bitwise_deterministic(name, B):
     """every reduction (split-m slabs, BN last-arriver sums, head weight gradients) runs in a
