@@ -37,7 +37,7 @@ from .data_parallel import DataParallelTrainer
 class AsyncPSTrainer(DataParallelTrainer):
     _step_all_reduces = False  # gradients go to the parameter server, not through a collective
     fused_update = False       # the update is the parameter server's apply
-    SUPPORTS_MULTISTEP = False  # one graph per step (bench times it step by step)
+    SUPPORTS_MULTISTEP = True  # the whole PS protocol of a step is device work: steps unroll like sync ones
 
     def __init__(self, net, lr: float = 0.001, max_staleness: int = 4, group=None, server_rank: int = 0,
                  graph: str = "full", timeout_s: float = 30.0):
@@ -95,6 +95,10 @@ class AsyncPSTrainer(DataParallelTrainer):
         self.epochs = int(epochs)
         self.ps.set_schedule(int(perm.shape[0]), self.epochs)
         self._graph = None
+        self._multi, self._multi_u = None, 0
+
+    def _has_schedule(self) -> bool:
+        return self._perm is not None
 
     # ------------------------------------------------------------------ one step
     def _gather(self):

@@ -405,7 +405,7 @@ class DataParallelTrainer:
         stays on the device).  Every step in it is the complete captured step (gather, forward,
         backward, gradient exchange, update); the batch cursor, dropout counters and one-shot
         all-reduce epochs all advance on the device.  Only in ``full`` graph mode."""
-        if self.graph_mode != "full" or not self.net.is_gpu or self._index_stream is None:
+        if self.graph_mode != "full" or not self.net.is_gpu or not self._has_schedule():
             return
         if self._graph is None:
             self._capture_with_fallback()
@@ -447,6 +447,9 @@ class DataParallelTrainer:
         torch.cuda.synchronize(net.device)
         self._multi = g if ok else None
         self._multi_u = u if ok else 0
+
+    def _has_schedule(self) -> bool:
+        return self._index_stream is not None
 
     def run(self, n: int):
         """``n`` training steps: multi-step graph replays (see :meth:`prepare_run`) plus single steps."""

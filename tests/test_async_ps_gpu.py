@@ -50,6 +50,38 @@ def test_async_single_worker_matches_sync_sgd():
     torch.testing.assert_close(w, s.store.master, rtol=1e-5, atol=1e-6)
 
 
+def test_async_multistep_graph_matches_single_steps():
+    """prepare_run(u) + run(n): u whole PS steps (pull, train, reduce, locked apply) unrolled into one
+    graph give the same shared master, version and dispatch counters as n single-step replays."""
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.async_ps import AsyncPSTrainer
+    from distriflow_amd.parallel.data_parallel import epoch_permutations
+
+    dev = torch.device("cuda", 0)
+    data, labels = synthetic_mnist(4096, seed=3, device=dev)
+    perm = epoch_permutations(4096, 256, 16, dev, seed=1)
+    res = []
+    for multi in (False, True):
+        net = build_model("lenet5", device=dev, seed=0)
+        tr = AsyncPSTrainer(net, lr=0.05, max_staleness=0, graph="full")
+        tr.bind_dataset(data, labels, 256, scale=1.0 / 255.0)
+        tr.bind_schedule(perm)
+        if multi:
+            tr.prepare_run(4)
+            assert tr._multi_u == 4
+            tr.run(10)
+        else:
+            for _ in range(10):
+                tr.step()
+        torch.cuda.synchronize()
+        st = tr.ps_stats()
+        res.append((tr.pull_master().clone(), st["version"], st["accepted"], st["cursor"], st["error"]))
+    assert res[0][1:] == res[1][1:], (res[0][1:], res[1][1:])
+    assert res[0][4] == 0
+    assert torch.equal(res[0][0], res[1][0])
+
+
 def _worker(rank, world, port, out_dir, max_stale, steps):
     import torch.distributed as dist
 
