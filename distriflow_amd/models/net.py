@@ -70,7 +70,8 @@ class Net:
         self._bound_B = None
         self.graphs: dict = {}
         # side streams for weight gradients that run concurrently with the data-gradient chain
-        self.concurrent_backward = False  # measured: cross-stream joins cost more than the overlap wins (LeNet-5)
+        # measured: cross-stream joins cost more than the overlap wins (LeNet-5); DISTRIFLOW_CONCURRENT_BACKWARD=1 on
+        self.concurrent_backward = os.environ.get("DISTRIFLOW_CONCURRENT_BACKWARD", "0") == "1"
         self._side = [torch.cuda.Stream(device=self.device) for _ in range(3)] if self.is_gpu else []
 
     # ------------------------------------------------------------------ planning / fusion
