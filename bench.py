@@ -150,6 +150,11 @@ def main():
         """W untimed warm-up steps, then ``steps`` timed ones between barrier + device syncs; max over ranks.
         The sync trainer replays its steps from multi-step hipGraphs (captured here, before timing)."""
         multi = getattr(tr, "SUPPORTS_MULTISTEP", False) and os.environ.get("DISTRIFLOW_MULTISTEP", "1") != "0"
+        # ranks time-sharing one device (rehearsals) must yield the GPU at graph boundaries: a long unrolled
+        # graph whose one-shot all-reduce spins on a descheduled peer's flag runs at the hardware
+        # scheduler's time-slice (measured: 4 ranks on one GPU, 0.48 -> 14.9 ms per step)
+        if world > 1 and dev.type == "cuda" and torch.cuda.device_count() < world:
+            multi = False
         if multi:
             tr.prepare_run(steps)
             tr.run(args.warmup)
