@@ -678,7 +678,11 @@ static bool igemm64_fast_ok(const IGemmArgs& a, int mode) {
   if (mode == MODE_DIRECT || a.SC % 64 || a.K != a.KH * a.KW * a.SC || a.KH * a.KW > 32 || a.Kpad < a.K) return false;
   if (mode == MODE_DGRAD && a.stride != 1 && a.stride != 2) return false;
   if (a.OH <= 0 || a.OW <= 0 || a.M % (a.OH * a.OW)) return false;
-  if (const char* e = getenv("DISTRIFLOW_IGEMM_FAST"); e && e[0] == '0') return false;
+  static const bool off = [] {
+    const char* e = getenv("DISTRIFLOW_IGEMM_FAST");
+    return e && e[0] == '0';
+  }();
+  if (off) return false;
   const long long sbytes = (long long)(a.M / (a.OH * a.OW)) * a.SH * a.SW * a.SC * 2;
   const long long wbytes = (long long)round_up(a.N, 16) * a.Kpad * 2;
   return sbytes < (1LL << 30) && wbytes < (1LL << 30);
