@@ -1076,8 +1076,22 @@ __global__ void __launch_bounds__(256) slab_reduce_thread_kernel(const float* __
   const int total = N * Kt;
   const int o = blockIdx.x * 256 + threadIdx.x;
   if (o >= total) return;
+  // 16 slab loads in flight per thread (issued before any add; a launch of one workgroup per CU is
+  // latency bound otherwise), summed into 4 accumulators in a fixed order: deterministic
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   int p = 0;
+  for (; p + 15 < S; p += 16) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = partial[(long long)(p + j) * total + o];
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) {
+      a0 += v[j];
+      a1 += v[j + 1];
+      a2 += v[j + 2];
+      a3 += v[j + 3];
+    }
+  }
   for (; p + 3 < S; p += 4) {
     a0 += partial[(long long)p * total + o];
     a1 += partial[(long long)(p + 1) * total + o];
