@@ -96,6 +96,11 @@ def main():
                     help="after timing, run this many EAGER steps with hipEvent phase timers and report the "
                          "data/compute/comm/update breakdown (diagnostic, not part of the timed number)")
     args = ap.parse_args()
+    # measurement aids that skip work (wrong gradients) must never reach a reported number
+    if os.environ.get("DISTRIFLOW_LENET_RED_SKIP", "0") not in ("", "0"):
+        print("bench: DISTRIFLOW_LENET_RED_SKIP is a diagnostic that skips work; refusing to run",
+              file=sys.stderr, flush=True)
+        sys.exit(3)
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
