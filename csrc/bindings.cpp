@@ -286,6 +286,89 @@ void relu_bwd_py(torch::Tensor y, torch::Tensor dy, torch::Tensor dx) {
             "relu_bwd");
 }
 
+// ---- generic Keras layers (csrc/act.hip)
+void act_fwd_py(torch::Tensor x, torch::Tensor y, int64_t kind) {
+  need(x, at::kBFloat16, "act x");
+  need(y, at::kBFloat16, "act y");
+  TORCH_CHECK(y.numel() >= x.numel(), "act: output too small");
+  TORCH_CHECK(kind >= dfa::kActLinear && kind <= dfa::kActExp, "act: unknown kind");
+  check_hip(dfa::act_fwd((const dfa::bf16*)x.data_ptr(), (dfa::bf16*)y.data_ptr(), x.numel(), (int)kind,
+                         cur_stream()),
+            "act_fwd");
+}
+
+void act_bwd_py(torch::Tensor x, torch::Tensor dy, torch::Tensor dx, int64_t kind, bool in_relu) {
+  need(x, at::kBFloat16, "act x");
+  need(dy, at::kBFloat16, "act dy");
+  need(dx, at::kBFloat16, "act dx");
+  TORCH_CHECK(dy.numel() == x.numel() && dx.numel() >= x.numel(), "act_bwd: size mismatch");
+  TORCH_CHECK(kind >= dfa::kActLinear && kind <= dfa::kActExp, "act: unknown kind");
+  check_hip(dfa::act_bwd((const dfa::bf16*)x.data_ptr(), (const dfa::bf16*)dy.data_ptr(), (dfa::bf16*)dx.data_ptr(),
+                         x.numel(), (int)kind, in_relu ? 1 : 0, cur_stream()),
+            "act_bwd");
+}
+
+void sigmoid_ce_py(torch::Tensor logits, torch::Tensor labels, c10::optional<torch::Tensor> dlogits,
+                   c10::optional<torch::Tensor> stats, int64_t B, int64_t C, int64_t ldl, int64_t ldg,
+                   double grad_scale) {
+  need(logits, at::kFloat, "logits");
+  need(labels, at::kInt, "labels");
+  TORCH_CHECK(B > 0 && C > 0 && ldl >= C && ldg >= C, "sigmoid_ce: bad shape");
+  TORCH_CHECK(logits.numel() >= (B - 1) * ldl + C && labels.numel() >= B, "sigmoid_ce inputs too small");
+  dfa::bf16* dl = nullptr;
+  if (dlogits.has_value() && dlogits->defined()) {
+    need(*dlogits, at::kBFloat16, "dlogits");
+    TORCH_CHECK(dlogits->numel() >= (B - 1) * ldg + C, "dlogits too small");
+    dl = (dfa::bf16*)dlogits->data_ptr();
+  }
+  float* sp = nullptr;
+  if (stats.has_value() && stats->defined()) {
+    need(*stats, at::kFloat, "stats");
+    TORCH_CHECK(stats->numel() >= 2, "stats needs 2 floats");
+    sp = stats->data_ptr<float>();
+  }
+  check_hip(dfa::sigmoid_ce(logits.data_ptr<float>(), labels.data_ptr<int>(), dl, sp, B, C, ldl, ldg,
+                            (float)grad_scale, cur_stream()),
+            "sigmoid_ce");
+}
+
+static dfa::Pool2DGeom pool_geom(const std::vector<int64_t>& g) {
+  TORCH_CHECK(g.size() == 12, "pool2d: geom = [B, H, W, C, OH, OW, ph, pw, sh, sw, pt, pl]");
+  dfa::Pool2DGeom p{};
+  p.B = (int)g[0]; p.H = (int)g[1]; p.W = (int)g[2]; p.C = (int)g[3]; p.OH = (int)g[4]; p.OW = (int)g[5];
+  p.ph = (int)g[6]; p.pw = (int)g[7]; p.sh = (int)g[8]; p.sw = (int)g[9]; p.pt = (int)g[10]; p.pl = (int)g[11];
+  TORCH_CHECK(p.B > 0 && p.H > 0 && p.W > 0 && p.C > 0 && p.OH > 0 && p.OW > 0 && p.ph > 0 && p.pw > 0 && p.sh > 0 &&
+                  p.sw > 0 && p.pt >= 0 && p.pl >= 0 && p.pt < p.ph && p.pl < p.pw,
+              "pool2d: bad geometry");
+  // every window starts inside the padded image
+  TORCH_CHECK((p.OH - 1) * p.sh - p.pt < p.H && (p.OW - 1) * p.sw - p.pl < p.W, "pool2d: output too large");
+  return p;
+}
+
+void pool2d_fwd_py(torch::Tensor x, torch::Tensor y, std::vector<int64_t> geom, bool avg) {
+  const dfa::Pool2DGeom g = pool_geom(geom);
+  need(x, at::kBFloat16, "pool x");
+  need(y, at::kBFloat16, "pool y");
+  TORCH_CHECK(x.numel() == (int64_t)g.B * g.H * g.W * g.C && y.numel() == (int64_t)g.B * g.OH * g.OW * g.C,
+              "pool2d: tensor sizes do not match the geometry");
+  check_hip(dfa::pool2d_fwd((const dfa::bf16*)x.data_ptr(), (dfa::bf16*)y.data_ptr(), g, avg ? 1 : 0, cur_stream()),
+            "pool2d_fwd");
+}
+
+void pool2d_bwd_py(torch::Tensor x, torch::Tensor dy, torch::Tensor dx, std::vector<int64_t> geom, bool avg,
+                   bool in_relu) {
+  const dfa::Pool2DGeom g = pool_geom(geom);
+  need(x, at::kBFloat16, "pool x");
+  need(dy, at::kBFloat16, "pool dy");
+  need(dx, at::kBFloat16, "pool dx");
+  TORCH_CHECK(x.numel() == (int64_t)g.B * g.H * g.W * g.C && dx.numel() == x.numel() &&
+                  dy.numel() == (int64_t)g.B * g.OH * g.OW * g.C,
+              "pool2d: tensor sizes do not match the geometry");
+  check_hip(dfa::pool2d_bwd((const dfa::bf16*)x.data_ptr(), (const dfa::bf16*)dy.data_ptr(), (dfa::bf16*)dx.data_ptr(),
+                            g, avg ? 1 : 0, in_relu ? 1 : 0, cur_stream()),
+            "pool2d_bwd");
+}
+
 void gap_fwd_py(torch::Tensor x, torch::Tensor y, int64_t B, int64_t HW, int64_t C) {
   need(x, at::kBFloat16, "x");
   need(y, at::kBFloat16, "y");
@@ -307,7 +390,8 @@ void sgd_multi_py(torch::Tensor descs, int64_t ndesc, int64_t total_blocks, torc
                   c10::optional<torch::Tensor> idx_stream, c10::optional<torch::Tensor> idx_cursor,
                   c10::optional<torch::Tensor> idx_dst, c10::optional<torch::Tensor> descs_host,
                   c10::optional<torch::Tensor> lenet_frag, int64_t frag_w1, int64_t frag_w2,
-                  c10::optional<torch::Tensor> lenet_snap) {
+                  c10::optional<torch::Tensor> lenet_snap, c10::optional<torch::Tensor> step_stats,
+                  c10::optional<torch::Tensor> run_stats) {
   TORCH_CHECK(descs.is_cuda() && descs.scalar_type() == at::kLong && descs.is_contiguous(), "descs must be int64 GPU");
   const dfa::ParamDesc* hd = nullptr;
   if (descs_host.has_value() && descs_host->defined()) {  // same table, host copy: passed in the kernel arguments
@@ -343,6 +427,14 @@ void sgd_multi_py(torch::Tensor descs, int64_t ndesc, int64_t total_blocks, torc
     is.dst = reinterpret_cast<long long*>(idx_dst->data_ptr());
     is.B = (int)idx_dst->numel();
     is.nsteps = (int)idx_stream->size(0);
+    if (run_stats.has_value() && run_stats->defined()) {
+      TORCH_CHECK(step_stats.has_value() && step_stats->defined(), "run_stats needs step_stats");
+      need(*run_stats, at::kFloat, "run_stats");
+      need(*step_stats, at::kFloat, "step_stats");
+      TORCH_CHECK(run_stats->numel() >= 3 && step_stats->numel() >= 2, "run_stats [3] / step_stats [2]");
+      is.run_stats = run_stats->data_ptr<float>();
+      is.step_stats = step_stats->data_ptr<float>();
+    }
   }
   if (lenet_frag.has_value() && lenet_frag->defined()) {
     TORCH_CHECK(lenet_frag->is_cuda() && lenet_frag->is_contiguous() &&
@@ -767,9 +859,13 @@ void head_train_py(std::vector<torch::Tensor> w, std::vector<c10::optional<torch
   check_hip(dfa::head_train(a, (int)phases, cur_stream()), "head_train");
 }
 
+class P2PComm;
+static dfa::LLComm p2p_ll_args(const P2PComm& c);
+
 // Whole-network LeNet-5 training step (csrc/lenet_fused.hip): fills the gradients of all ten
 // parameters and stats = [loss sum, correct].  x: uint8 dataset [nrows][28][28][1] read through idx,
-// or a bf16 batch [B][28][28][1].
+// or a bf16 batch [B][28][28][1].  With ``sgd_*`` the reduce launch applies the update; with ``ll``
+// (a world > 1 P2PComm) it first sums every gradient over the ranks in-kernel (no all-reduce launch).
 void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double scale, torch::Tensor labels,
                     std::vector<torch::Tensor> conv, std::vector<torch::Tensor> dense_w,
                     std::vector<torch::Tensor> dense_wt, std::vector<torch::Tensor> dense_b,
@@ -782,7 +878,8 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
                     c10::optional<torch::Tensor> sgd_wbf, c10::optional<torch::Tensor> sgd_hyper,
                     c10::optional<torch::Tensor> sgd_descs, c10::optional<torch::Tensor> idx_stream,
                     c10::optional<torch::Tensor> idx_cursor, c10::optional<torch::Tensor> idx_dst,
-                    c10::optional<torch::Tensor> sgd_ticket, c10::optional<torch::Tensor> sgd_stage) {
+                    c10::optional<torch::Tensor> sgd_ticket, c10::optional<torch::Tensor> sgd_stage,
+                    const P2PComm* ll, int64_t exch_blocks, c10::optional<torch::Tensor> run_stats) {
   TORCH_CHECK(conv.size() == 4 && conv_grads.size() == 4, "lenet: conv = [w1, b1, w2, b2]");
   TORCH_CHECK(dense_w.size() == 3 && dense_wt.size() == 3 && dense_b.size() == 3 && dense_gw.size() == 3 &&
                   dense_gb.size() == 3 && hT.size() == 3 && dzT.size() == 3,
@@ -945,10 +1042,23 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
       r.sgd.B = (int)idx_dst->numel();
       r.sgd.nsteps = (int)idx_stream->size(0);
     }
+    if (run_stats.has_value() && run_stats->defined()) {
+      need(*run_stats, at::kFloat, "run_stats");
+      TORCH_CHECK(run_stats->numel() >= 3, "run_stats must hold [loss sum, correct, updates]");
+      r.sgd.run_stats = run_stats->data_ptr<float>();
+    }
     r.sgd.frag = frag.data_ptr();
     r.sgd.ticket = reinterpret_cast<unsigned*>(sgd_ticket->data_ptr<int>());
     r.sgd.stage = sgd_stage->data_ptr<float>();
   }
+  if (ll != nullptr) {
+    TORCH_CHECK(r.sgd_on, "lenet: the in-kernel LL exchange needs the fused update (sgd_* arguments)");
+    r.ll = p2p_ll_args(*ll);
+    TORCH_CHECK(r.ll.world > 1, "lenet: LL exchange needs world > 1");
+    r.ll_on = 1;
+  }
+  TORCH_CHECK(exch_blocks >= 0 && exch_blocks <= 512, "lenet: exch_blocks out of range");
+  r.exch_blocks = (int)exch_blocks;
   check_hip(dfa::lenet_train(a, r, cur_stream()), "lenet_train");
 }
 
@@ -1030,13 +1140,13 @@ void kcnn_bwd_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double scale
             "kcnn_bwd");
 }
 
-void classifier_metrics_py(torch::Tensor z, torch::Tensor labels, int64_t kind, bool softmax, torch::Tensor out) {
+void classifier_metrics_py(torch::Tensor z, torch::Tensor labels, int64_t kind, int64_t out_act, torch::Tensor out) {
   need(z, at::kFloat, "metrics logits");
   need(labels, at::kInt, "metrics labels");
   need(out, at::kFloat, "metrics out");
   TORCH_CHECK(z.dim() == 2 && labels.numel() == z.size(0) && out.numel() >= 2, "metrics: z [B][C], labels [B]");
   check_hip(dfa::classifier_metrics(z.data_ptr<float>(), labels.data_ptr<int>(), (int)z.size(0), (int)z.size(1),
-                                    (int)kind, softmax ? 1 : 0, out.data_ptr<float>(), cur_stream()),
+                                    (int)kind, (int)out_act, out.data_ptr<float>(), cur_stream()),
             "classifier_metrics");
 }
 
@@ -1072,15 +1182,20 @@ class HostFlag {
 // process group (parallel/p2p.py); every launch goes onto PyTorch's current stream (graph capturable).
 class P2PComm {
  public:
-  P2PComm(int64_t rank, int64_t world, int64_t max_floats, double timeout_s) : rank_((int)rank), world_((int)world) {
+  P2PComm(int64_t rank, int64_t world, int64_t max_floats, double timeout_s, int64_t ll_slots)
+      : rank_((int)rank), world_((int)world) {
     TORCH_CHECK(world >= 1 && world <= dfa::kP2PMaxRanks, "p2p: world must be in [1, 8]");
     TORCH_CHECK(rank >= 0 && rank < world, "p2p: bad rank");
     TORCH_CHECK(max_floats > 0 && max_floats <= (int64_t(1) << 28), "p2p: max_floats out of range");
+    TORCH_CHECK(ll_slots >= 0 && ll_slots <= 4096, "p2p: ll_slots out of range");
     check_hip(hipGetDevice(&dev_), "p2p getDevice");
     max_blocks_ = (int)((max_floats + dfa::kP2PChunk - 1) / dfa::kP2PChunk);
     half_ = (int64_t)max_blocks_ * dfa::kP2PChunk;
     flag_bytes_ = ((int64_t)max_blocks_ * dfa::kP2PMaxRanks * 4 + 4095) / 4096 * 4096;
-    bytes_ = flag_bytes_ + 2 * half_ * 4;
+    // in-kernel LL exchange region (csrc/ll_exchange.h) after the staging halves, in the same IPC export
+    ll_slots_ = (int)ll_slots;
+    ll_off_ = flag_bytes_ + 2 * half_ * 4;
+    bytes_ = ll_off_ + 2 * (int64_t)ll_slots_ * dfa::kP2PMaxRanks * dfa::kLLSlot * 8;
     void* p = nullptr;
     hipError_t e = hipExtMallocWithFlags(&p, (size_t)bytes_, hipDeviceMallocUncached);
     if (e != hipSuccess) {
@@ -1089,8 +1204,8 @@ class P2PComm {
     }
     local_ = (char*)p;
     check_hip(hipMemset(local_, 0, (size_t)bytes_), "p2p memset");
-    check_hip(hipMalloc((void**)&epochs_, (size_t)max_blocks_ * 4), "p2p epochs alloc");
-    check_hip(hipMemset(epochs_, 0, (size_t)max_blocks_ * 4), "p2p epochs memset");
+    check_hip(hipMalloc((void**)&epochs_, (size_t)(max_blocks_ + ll_slots_) * 4), "p2p epochs alloc");
+    check_hip(hipMemset(epochs_, 0, (size_t)(max_blocks_ + ll_slots_) * 4), "p2p epochs memset");
     check_hip(hipMalloc((void**)&err_, 4), "p2p err alloc");
     check_hip(hipMemset(err_, 0, 4), "p2p err memset");
     check_hip(hipDeviceSynchronize(), "p2p init sync");
@@ -1152,11 +1267,28 @@ class P2PComm {
   }
   int64_t host_error() const { return herr_.read(); }  // no HIP call: safe from a watchdog thread
   int64_t max_floats() const { return half_; }
+  int64_t ll_slots() const { return ll_slots_; }
   void set_timeout(double timeout_s) { timeout_ticks_ = (int64_t)(timeout_s * 1e8); }
+  // launch arguments of the in-kernel LL exchange (kernels that fold the all-reduce into their epilogue)
+  dfa::LLComm ll_args() const {
+    TORCH_CHECK(opened_ || world_ == 1, "p2p: open() the peer handles first");
+    TORCH_CHECK(ll_slots_ > 0, "p2p: communicator built without LL slots");
+    dfa::LLComm c{};
+    for (int r = 0; r < dfa::kP2PMaxRanks; ++r)
+      c.bases[r] = bases_[r] ? reinterpret_cast<unsigned long long*>(bases_[r] + ll_off_) : nullptr;
+    c.epochs = epochs_ + max_blocks_;
+    c.err = err_;
+    c.herr = herr_.device();
+    c.timeout_ticks = timeout_ticks_;
+    c.rank = rank_;
+    c.world = world_;
+    c.nslots = ll_slots_;
+    return c;
+  }
 
  private:
-  int rank_, world_, dev_ = 0, max_blocks_ = 0;
-  int64_t half_ = 0, flag_bytes_ = 0, bytes_ = 0, timeout_ticks_ = 0;
+  int rank_, world_, dev_ = 0, max_blocks_ = 0, ll_slots_ = 0;
+  int64_t half_ = 0, flag_bytes_ = 0, bytes_ = 0, timeout_ticks_ = 0, ll_off_ = 0;
   char* local_ = nullptr;
   char* bases_[dfa::kP2PMaxRanks];
   unsigned* epochs_ = nullptr;
@@ -1164,6 +1296,8 @@ class P2PComm {
   HostFlag herr_;
   bool opened_ = false;
 };
+
+static dfa::LLComm p2p_ll_args(const P2PComm& c) { return c.ll_args(); }
 
 // Device-resident async parameter server (csrc/async_ps.hip): the server rank owns the shared
 // seqlock / batch counter / fp32 master buffer (IPC exported); every rank maps it.
@@ -1401,7 +1535,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("grad"), py::arg("mom"), py::arg("wbf"), py::arg("hyper"), py::arg("apply_update"),
         py::arg("idx_stream") = py::none(), py::arg("idx_cursor") = py::none(), py::arg("idx_dst") = py::none(),
         py::arg("descs_host") = py::none(), py::arg("lenet_frag") = py::none(), py::arg("frag_w1") = 0,
-        py::arg("frag_w2") = 0, py::arg("lenet_snap") = py::none());
+        py::arg("frag_w2") = 0, py::arg("lenet_snap") = py::none(), py::arg("step_stats") = py::none(),
+        py::arg("run_stats") = py::none());
   m.def("sum_buffers", &sum_buffers_py);
   m.def("axpby", &axpby_py);
   m.def("bn_stats_fwd", &bn_stats_fwd_py, "BN forward statistics (partials + last-workgroup finalize, one launch)");
@@ -1455,7 +1590,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("g_w2"), py::arg("g_b2"), py::arg("step_inc") = py::none());
   m.def("kcnn_set_debug", &dfa::kcnn_set_debug, "measurement aid: skip parts of the conv-block backward");
   m.def("kcnn_slab_floats", [](int64_t B) { return (int64_t)dfa::kcnn_slab_floats((int)B); });
-  m.def("classifier_metrics", &classifier_metrics_py, "[loss sum, correct] of a classifier batch (one launch)");
+  m.def("classifier_metrics", &classifier_metrics_py,
+        "[loss sum, correct] of a classifier batch (one launch); out_act 0 logits, 1 softmax, 2 sigmoid output");
+  m.def("act_fwd", &act_fwd_py, "standalone activation y = act(x) (csrc/act.hip)");
+  m.def("act_bwd", &act_bwd_py, "dx = dy * act'(x) [* relu'(x)]");
+  m.def("sigmoid_ce", &sigmoid_ce_py, "sigmoid cross-entropy on logits vs one-hot labels (+ dlogits)");
+  m.def("pool2d_fwd", &pool2d_fwd_py, "general 2-D max / average pooling, any window / stride / padding");
+  m.def("pool2d_bwd", &pool2d_bwd_py, "backward of pool2d_fwd (input-centric, no atomics)");
   m.def("lenet_train", &lenet_train_py, "whole-network LeNet-5 training step (fwd + CE + bwd, 2 launches)",
         py::arg("x"), py::arg("idx"), py::arg("scale"), py::arg("labels"), py::arg("conv"), py::arg("dense_w"),
         py::arg("dense_wt"), py::arg("dense_b"), py::arg("conv_grads"), py::arg("dense_gw"), py::arg("dense_gb"),
@@ -1465,21 +1606,23 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("conv_mom") = std::vector<torch::Tensor>{}, py::arg("sgd_master") = py::none(),
         py::arg("sgd_mom") = py::none(), py::arg("sgd_wbf") = py::none(), py::arg("sgd_hyper") = py::none(),
         py::arg("sgd_descs") = py::none(), py::arg("idx_stream") = py::none(), py::arg("idx_cursor") = py::none(),
-        py::arg("idx_dst") = py::none(), py::arg("sgd_ticket") = py::none(), py::arg("sgd_stage") = py::none());
+        py::arg("idx_dst") = py::none(), py::arg("sgd_ticket") = py::none(), py::arg("sgd_stage") = py::none(),
+        py::arg("ll") = nullptr, py::arg("exch_blocks") = 0, py::arg("run_stats") = py::none());
   m.def("lenet_blocks", [](int64_t B) { return dfa::lenet_blocks((int)B); });
   m.def("lenet_frag_bytes", []() { return (int64_t)dfa::lenet_frag_bytes(); });
   m.def("lenet_dense_part_floats", [](int64_t B) { return (int64_t)dfa::lenet_dense_part_floats((int)B); });
   m.def("gather_labels", &gather_labels_py);
   py::class_<P2PComm>(m, "P2PComm", "one-shot xGMI all-reduce over IPC-mapped peer buffers")
-      .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("world"), py::arg("max_floats"),
-           py::arg("timeout_s") = 2.0)
+      .def(py::init<int64_t, int64_t, int64_t, double, int64_t>(), py::arg("rank"), py::arg("world"),
+           py::arg("max_floats"), py::arg("timeout_s") = 2.0, py::arg("ll_slots") = 512)
       .def("handle", &P2PComm::handle)
       .def("open", &P2PComm::open)
       .def("allreduce", &P2PComm::allreduce, py::arg("t"), py::arg("scale") = 1.0)
       .def("error", &P2PComm::error)
       .def("host_error", &P2PComm::host_error)
       .def("set_timeout", &P2PComm::set_timeout)
-      .def_property_readonly("max_floats", &P2PComm::max_floats);
+      .def_property_readonly("max_floats", &P2PComm::max_floats)
+      .def_property_readonly("ll_slots", &P2PComm::ll_slots);
   py::class_<PSComm>(m, "PSComm", "device-resident bounded-staleness parameter server over IPC/xGMI")
       .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("server_rank"), py::arg("n"),
            py::arg("timeout_s") = 30.0)

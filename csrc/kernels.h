@@ -130,6 +130,10 @@ struct IndexStream {  // next-batch staging folded into the optimizer launch (cs
   long long frag_w1, frag_w2;  // offsets of the conv1 / conv2 kernels in grad (and master / momentum)
   const float* snap;           // [2][2550] pre-update weights / momentum (lenet_reduce_kernel); read
                                // instead of master, which this same launch overwrites
+  // device run statistics (callbacks / metrics without extra launches): the index-stream workgroup adds
+  // this step's [loss sum, correct] to run_stats[0..1] and counts the applied update in run_stats[2]
+  const float* step_stats;
+  float* run_stats;
 };
 hipError_t sgd_multi(const ParamDesc* descs, int ndesc, int total_blocks, float* master, const float* grad,
                      float* mom_buf, bf16* wbf, const float* hyper, int apply_update, hipStream_t st,
@@ -257,6 +261,20 @@ struct P2PArgs {
 };
 hipError_t p2p_allreduce(const P2PArgs& a, hipStream_t st);
 
+// In-kernel low-latency exchange (csrc/ll_exchange.h): 8-byte {fp32 value, u32 epoch} granules that a
+// producing workgroup PUSHES into every peer's IPC-mapped region, so a reduction epilogue (the fused
+// LeNet-5 reduce, ...) sums the W ranks' values of its own slot without a separate all-reduce launch.
+// Region of rank r (inside its P2PComm allocation): [2 parities][nslots][kP2PMaxRanks src][kLLSlot].
+constexpr int kLLSlot = 256;  // granules per slot (one per thread of a 256-value epilogue)
+struct LLComm {
+  unsigned long long* bases[kP2PMaxRanks];  // bases[r] = rank r's LL region mapped into this process
+  unsigned* epochs;                         // [nslots] per-slot call counters (local)
+  int* err;                                 // sticky error word (shared with the P2P all-reduce)
+  int* herr;                                // host-mapped mirror
+  long long timeout_ticks;
+  int rank, world, nslots;
+};
+
 
 // Device-resident async parameter server (csrc/async_ps.hip).  seq / batch_ctr / ps_w live in the
 // server rank's IPC buffer (mapped into every rank); everything else is local.
@@ -342,6 +360,7 @@ struct LeNetSgd {
   long long* cursor;
   long long* dst;
   int B, nsteps;
+  float* run_stats;    // nullable: [loss sum, correct, updates] accumulated by the loss workgroup
   void* frag;          // fragment buffer of the next step
   unsigned* ticket;    // conv-workgroup arrival counter (re-armed by the last)
   float* stage;        // [2550] the new conv weights, handed to the last conv workgroup
@@ -359,6 +378,14 @@ struct LeNetRedArgs {
   float* snap;
   int sgd_on;
   LeNetSgd sgd;
+  // world > 1 (requires sgd_on): every dense tile / conv block sums its values over the ranks through
+  // the in-kernel LL exchange before applying the update, so a multi-rank step is still two launches;
+  // workgroup b uses LL slot b
+  int ll_on;
+  LLComm ll;
+  // exchanging workgroups (0 = one per slot); fewer when ranks time-share one GPU (each then owns up to
+  // 8 slots round-robin), so that every rank's waiting workgroups fit on the chip at once
+  int exch_blocks;
 };
 // The reference CNN's conv block (csrc/kcnn_fused.hip): conv1 3x3x1->32 + ReLU, conv2 3x3x32->32 + ReLU,
 // 2x2 max-pool [+ folded dropout], input 28x28x1, in one forward and one backward launch (+ reduce).
@@ -401,6 +428,23 @@ enum MetricKind {
 };
 hipError_t classifier_metrics(const float* z, const int* labels, int B, int C, int kind, int softmax, float* out,
                               hipStream_t st);
+
+// Generic Keras layers (csrc/act.hip): standalone activations, sigmoid-CE loss, general pooling.
+enum ActKind {
+  kActLinear = 0, kActRelu = 1, kActRelu6 = 2, kActSigmoid = 3, kActTanh = 4, kActElu = 5, kActSelu = 6,
+  kActSoftplus = 7, kActSoftsign = 8, kActHardSigmoid = 9, kActSwish = 10, kActExp = 11
+};
+hipError_t act_fwd(const bf16* x, bf16* y, long long n, int kind, hipStream_t st);
+hipError_t act_bwd(const bf16* x, const bf16* dy, bf16* dx, long long n, int kind, int in_relu, hipStream_t st);
+hipError_t sigmoid_ce(const float* logits, const int* labels, bf16* dlogits, float* stats, int B, int C, int ldl,
+                      int ldg, float grad_scale, hipStream_t st);
+struct Pool2DGeom {
+  int B, H, W, C, OH, OW;
+  int ph, pw, sh, sw, pt, pl;  // window, stride, top / left padding
+};
+hipError_t pool2d_fwd(const bf16* x, bf16* y, const Pool2DGeom& g, int avg, hipStream_t st);
+hipError_t pool2d_bwd(const bf16* x, const bf16* dy, bf16* dx, const Pool2DGeom& g, int avg, int in_relu,
+                      hipStream_t st);
 
 // Direct convolution for C_in <= 4 (csrc/smallc.hip); igemm_fwd / igemm_wgrad dispatch to it.
 bool smallc_fwd_supported(const IGemmArgs& a, int mode);

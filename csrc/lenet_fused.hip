@@ -27,6 +27,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "lenet_frag.h"
+#include "ll_exchange.h"
 #include "optim_device.h"
 
 #include <algorithm>
@@ -704,123 +705,202 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void __launch_bounds__(RT) lenet_reduce_kernel(LeNetRedArgs a) {
-  __shared__ float red[16][16][17];
+// ---- one exchange slot = one dense weight-gradient tile (16 x 16, threads t < 256 own an element each) or
+// one conv block (64 parameters, lanes of wave 0).  The value functions return this thread's local sum.
+
+// dense tile `slot`: K = batch split over the 16 waves, LDS combine (bias = a column of ones)
+__device__ __forceinline__ float dense_tile_value(const LeNetRedArgs& a, int slot, float (*red)[16][17]) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int blk = blockIdx.x;
-  if (blk < a.dense_tiles) {
-    int tile = a.tile_of_block[blk];
-    int l = 0;
-    if (tile >= a.L[0].tiles) {
-      tile -= a.L[0].tiles;
-      l = 1;
-      if (tile >= a.L[1].tiles) {
-        tile -= a.L[1].tiles;
-        l = 2;
-      }
+  int tile = a.tile_of_block[slot];
+  int l = 0;
+  if (tile >= a.L[0].tiles) {
+    tile -= a.L[0].tiles;
+    l = 1;
+    if (tile >= a.L[1].tiles) {
+      tile -= a.L[1].tiles;
+      l = 2;
     }
-    const LeNetDense& L = a.L[l];
-    const int ktiles = (L.K + 1 + 15) / 16;
-    const int tk = tile / ((L.N + 15) / 16), tn = tile - ((L.N + 15) / 16) * tk;  // tn fastest
-    const int n = 16 * tn + (lane & 15), k = 16 * tk + (lane & 15);
-    const bf16* arow = L.dzT + (long long)min(n, L.N - 1) * a.ldt + 8 * (lane >> 4);
-    const bf16* brow = L.hT + (long long)min(k, L.K - 1) * a.ldt + 8 * (lane >> 4);
-    const bool a_ok = n < L.N, b_ones = k == L.K, b_ok = k < L.K;
-    bf16x8 ones, zeros = zero8();
-#pragma unroll
-    for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
-    const int steps = a.ldt / 32;
-    const int per = (steps + 15) / 16;
-    const int s0 = wid * per, s1 = min(steps, s0 + per);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int s = s0; s < s1; s += 8) {
-      bf16x8 av[8], bv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int ss = min(s + u, s1 - 1);
-        av[u] = ld8(arow + 32 * ss);
-        bv[u] = ld8(brow + 32 * ss);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const bool live = s + u < s1;
-        acc = mfma16x16x32((a_ok && live) ? av[u] : zeros, b_ok ? bv[u] : (b_ones ? ones : zeros), acc);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[wid][4 * (lane >> 4) + r][lane & 15] = acc[r];
-    __syncthreads();
-    const int t = threadIdx.x;
-    (void)ktiles;
-    if (t < 256) {
-      const int rn = t >> 4, ck = t & 15;
-      float v = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < 16; ++ww) v += red[ww][rn][ck];
-      const int on = 16 * tn + rn, ok = 16 * tk + ck;
-      if (on < L.N) {
-        if (ok < L.K) L.gw[(long long)on * L.K + ok] = v;
-        else if (ok == L.K) L.gb[on] = v;
-        if (a.sgd_on && ok <= L.K)  // single-rank fast path: the update of this element, here
-          sgd_apply_one(a.sgd.d[4 + 2 * l + (ok == L.K ? 1 : 0)], ok < L.K ? on * L.K + ok : on, v, a.sgd.master,
-                        a.sgd.mom, a.sgd.wbf, a.sgd.hyper);
-      }
-    }
-    return;
   }
-  blk -= a.dense_tiles;
-  if (blk < a.nconv_blocks) {
-    float* sred = &red[0][0][0];  // [16][64]
-    const int p = blk * 64 + lane;
-    float s = 0.f;
-    if (p < kLeNetConvParams) {
-      // 32 workgroup rows per pass, all loads in flight before the (fixed-order) sum
-      for (int q0 = wid; q0 < a.nblk; q0 += 16 * 32) {
-        float v[32];
+  const LeNetDense& L = a.L[l];
+  const int tk = tile / ((L.N + 15) / 16), tn = tile - ((L.N + 15) / 16) * tk;  // tn fastest
+  const int n = 16 * tn + (lane & 15), k = 16 * tk + (lane & 15);
+  const bf16* arow = L.dzT + (long long)min(n, L.N - 1) * a.ldt + 8 * (lane >> 4);
+  const bf16* brow = L.hT + (long long)min(k, L.K - 1) * a.ldt + 8 * (lane >> 4);
+  const bool a_ok = n < L.N, b_ones = k == L.K, b_ok = k < L.K;
+  bf16x8 ones, zeros = zero8();
 #pragma unroll
-        for (int j = 0; j < 32; ++j) {
-          const int q = q0 + 16 * j;
-          v[j] = q < a.nblk ? a.conv_part[(long long)q * kLeNetConvStride + p] : 0.f;
-        }
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
+  const int steps = a.ldt / 32;
+  const int per = (steps + 15) / 16;
+  const int s0 = wid * per, s1 = min(steps, s0 + per);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int s = s0; s < s1; s += 8) {
+    bf16x8 av[8], bv[8];
 #pragma unroll
-        for (int j = 0; j < 32; ++j) s += v[j];
+    for (int u = 0; u < 8; ++u) {
+      const int ss = min(s + u, s1 - 1);
+      av[u] = ld8(arow + 32 * ss);
+      bv[u] = ld8(brow + 32 * ss);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool live = s + u < s1;
+      acc = mfma16x16x32((a_ok && live) ? av[u] : zeros, b_ok ? bv[u] : (b_ones ? ones : zeros), acc);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wid][4 * (lane >> 4) + r][lane & 15] = acc[r];
+  __syncthreads();
+  float v = 0.f;
+  if (threadIdx.x < 256) {
+    const int rn = threadIdx.x >> 4, ck = threadIdx.x & 15;
+#pragma unroll
+    for (int ww = 0; ww < 16; ++ww) v += red[ww][rn][ck];
+  }
+  return v;
+}
+
+__device__ __forceinline__ void dense_tile_apply(const LeNetRedArgs& a, int slot, float v) {
+  int tile = a.tile_of_block[slot];
+  int l = 0;
+  if (tile >= a.L[0].tiles) {
+    tile -= a.L[0].tiles;
+    l = 1;
+    if (tile >= a.L[1].tiles) {
+      tile -= a.L[1].tiles;
+      l = 2;
+    }
+  }
+  const LeNetDense& L = a.L[l];
+  const int tk = tile / ((L.N + 15) / 16), tn = tile - ((L.N + 15) / 16) * tk;
+  const int on = 16 * tn + (threadIdx.x >> 4), ok = 16 * tk + (threadIdx.x & 15);
+  if (on < L.N) {
+    if (ok < L.K) L.gw[(long long)on * L.K + ok] = v;
+    else if (ok == L.K) L.gb[on] = v;
+    if (a.sgd_on && ok <= L.K)  // fused update of this element
+      sgd_apply_one(a.sgd.d[4 + 2 * l + (ok == L.K ? 1 : 0)], ok < L.K ? on * L.K + ok : on, v, a.sgd.master,
+                    a.sgd.mom, a.sgd.wbf, a.sgd.hyper);
+  }
+}
+
+// conv block `cb`: 64 parameters; thread (p, q) sums workgroup partials q, q + 16, ... of parameter p
+__device__ __forceinline__ float conv_value(const LeNetRedArgs& a, int cb, float (*red)[16][17]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* sred = &red[0][0][0];  // [16][64]
+  const int p = cb * 64 + lane;
+  float s = 0.f;
+  if (p < kLeNetConvParams) {
+    // 32 workgroup rows per pass, all loads in flight before the (fixed-order) sum
+    for (int q0 = wid; q0 < a.nblk; q0 += 16 * 32) {
+      float v[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        const int q = q0 + 16 * j;
+        v[j] = q < a.nblk ? a.conv_part[(long long)q * kLeNetConvStride + p] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 32; ++j) s += v[j];
+    }
+  }
+  sred[wid * 64 + lane] = s;
+  __syncthreads();
+  float v = 0.f;
+  if (wid == 0) {
+#pragma unroll
+    for (int ww = 0; ww < 16; ++ww) v += sred[ww * 64 + lane];
+  }
+  return v;
+}
+
+__device__ __forceinline__ void conv_apply(const LeNetRedArgs& a, int cb, float v) {
+  const int p = cb * 64 + (threadIdx.x & 63);
+  if (p >= kLeNetConvParams) return;
+  float* dst = p < kLeNetPB1 ? a.g_w1 + p
+               : p < kLeNetPW2 ? a.g_b1 + (p - kLeNetPB1)
+               : p < kLeNetPB2 ? a.g_w2 + (p - kLeNetPW2)
+                               : a.g_b2 + (p - kLeNetPB2);
+  *dst = v;
+  const int wj = p < kLeNetPB1 ? p : (p >= kLeNetPW2 && p < kLeNetPB2) ? 150 + (p - kLeNetPW2) : -1;
+  if (a.sgd_on) {
+    const int di = p < kLeNetPB1 ? 0 : p < kLeNetPW2 ? 1 : p < kLeNetPB2 ? 2 : 3;
+    const int i = p - (di == 0 ? 0 : di == 1 ? kLeNetPB1 : di == 2 ? kLeNetPW2 : kLeNetPB2);
+    const float nw = sgd_apply_one(a.sgd.d[di], i, v, a.sgd.master, a.sgd.mom, a.sgd.wbf, a.sgd.hyper);
+    // the new conv weights, handed to the workgroup that rebuilds the next step's fragments
+    if (wj >= 0) st_sc1(a.sgd.stage + wj, nw);
+  } else if (a.snap != nullptr && wj >= 0) {
+    // the conv kernels' weights and momentum as this gradient saw them: the optimizer launch rebuilds
+    // the next step's fragments from these (no read of state it is overwriting)
+    const long long o = wj < 150 ? wj : wj - 150;
+    a.snap[wj] = wj < 150 ? a.w1[o] : a.w2[o];
+    a.snap[kLeNetConvW + wj] = a.m1 == nullptr ? 0.f : (wj < 150 ? a.m1[o] : a.m2[o]);
+  }
+}
+
+constexpr int kMaxSlotsPerBlock = 8;
+
+// Exchange workgroups [0, exch_blocks) own slots blockIdx.x + k * exch_blocks: all their slots' local
+// sums are computed and pushed to the peers first, then each is waited for, summed over the ranks and
+// applied (one round trip per workgroup, not per slot).  On a node with one rank per GPU exch_blocks ==
+// slots (one each, every workgroup resident); ranks that time-share one GPU use fewer, so that the
+// waiting workgroups of all ranks fit on the chip beside the peers' train kernels.
+// Then one workgroup: loss partials -> stats; one more (index stream bound): stage the next batch.
+__global__ void __launch_bounds__(RT, 8) lenet_reduce_kernel(LeNetRedArgs a) {
+  __shared__ float red[16][16][17];
+  __shared__ unsigned s_e;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nslot = a.dense_tiles + a.nconv_blocks;
+  const int nexch = a.exch_blocks;
+  if ((int)blockIdx.x < nexch) {
+    __shared__ float keep[kMaxSlotsPerBlock][256];  // this workgroup's local sums, per slot and position
+    __shared__ unsigned ep[kMaxSlotsPerBlock];
+#pragma unroll 1
+    for (int k = 0; k < kMaxSlotsPerBlock; ++k) {
+      const int slot = blockIdx.x + k * nexch;
+      if (slot >= nslot) break;  // uniform over the workgroup
+      __syncthreads();           // the previous slot's readers of red are done
+      const bool dense = slot < a.dense_tiles;
+      const float v = dense ? dense_tile_value(a, slot, red) : conv_value(a, slot - a.dense_tiles, red);
+      const bool owner = dense ? threadIdx.x < 256 : wid == 0;
+      if (owner) keep[k][threadIdx.x] = v;
+      if (a.ll_on) {
+        const unsigned e = ll_epoch(a.ll, slot, &s_e);
+        if (threadIdx.x == 0) ep[k] = e;
+        if (owner) ll_push(a.ll, slot, threadIdx.x, e, v);
       }
     }
-    sred[wid * 64 + lane] = s;
     __syncthreads();
-    if (wid == 0 && p < kLeNetConvParams) {
-      float v = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < 16; ++ww) v += sred[ww * 64 + lane];
-      float* dst = p < kLeNetPB1 ? a.g_w1 + p
-                   : p < kLeNetPW2 ? a.g_b1 + (p - kLeNetPB1)
-                   : p < kLeNetPB2 ? a.g_w2 + (p - kLeNetPW2)
-                                   : a.g_b2 + (p - kLeNetPB2);
-      *dst = v;
-      // the conv kernels' weights and momentum as this gradient saw them: the optimizer launch
-      // rebuilds the next step's fragments from these (no read of state it is overwriting)
-      const int wj = p < kLeNetPB1 ? p : (p >= kLeNetPW2 && p < kLeNetPB2) ? 150 + (p - kLeNetPW2) : -1;
-      if (a.sgd_on) {
-        const int di = p < kLeNetPB1 ? 0 : p < kLeNetPW2 ? 1 : p < kLeNetPB2 ? 2 : 3;
-        const int i = p - (di == 0 ? 0 : di == 1 ? kLeNetPB1 : di == 2 ? kLeNetPW2 : kLeNetPB2);
-        const float nw = sgd_apply_one(a.sgd.d[di], i, v, a.sgd.master, a.sgd.mom, a.sgd.wbf, a.sgd.hyper);
-        if (wj >= 0) st_sc1(a.sgd.stage + wj, nw);
-      } else if (a.snap != nullptr && wj >= 0) {
-        const long long o = wj < 150 ? wj : wj - 150;
-        a.snap[wj] = wj < 150 ? a.w1[o] : a.w2[o];
-        a.snap[kLeNetConvW + wj] = a.m1 == nullptr ? 0.f : (wj < 150 ? a.m1[o] : a.m2[o]);
+    int nconv_mine = 0;
+#pragma unroll 1
+    for (int k = 0; k < kMaxSlotsPerBlock; ++k) {
+      const int slot = blockIdx.x + k * nexch;
+      if (slot >= nslot) break;
+      const bool dense = slot < a.dense_tiles;
+      if (dense ? threadIdx.x < 256 : wid == 0) {
+        float v = keep[k][threadIdx.x];
+        bool ok = true;
+        if (a.ll_on) {  // the rank-order sum over the ranks (no all-reduce launch)
+          ok = ll_wait_sum(a.ll, slot, threadIdx.x, ep[k], v, v);
+          if (ok && threadIdx.x == 0) ll_commit(a.ll, slot, ep[k]);
+        }
+        if (ok) {
+          if (dense) dense_tile_apply(a, slot, v);
+          else conv_apply(a, slot - a.dense_tiles, v);
+        }
       }
+      if (!dense) ++nconv_mine;
     }
-    if (a.sgd_on) {
-      // the last conv workgroup to finish rebuilds the next step's conv-weight fragments from the staged
-      // new weights (write-through stores drained before the ticket, write-through loads after it)
+    if (a.sgd_on && nconv_mine > 0) {
+      // the workgroup that applies the last conv slot rebuilds the next step's conv-weight fragments from
+      // the staged new weights (write-through stores drained before the ticket, write-through loads
+      // after it: csrc/bn.hip's gfx950 hand-off)
       __shared__ int last;
       __shared__ float wl[kLeNetConvW];
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
-        const unsigned tk = __hip_atomic_fetch_add(a.sgd.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = tk == (unsigned)a.nconv_blocks - 1;
+        const unsigned tk =
+            __hip_atomic_fetch_add(a.sgd.ticket, (unsigned)nconv_mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = tk + (unsigned)nconv_mine == (unsigned)a.nconv_blocks;
         if (last) __hip_atomic_store(a.sgd.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
@@ -832,8 +912,8 @@ __global__ void __launch_bounds__(RT) lenet_reduce_kernel(LeNetRedArgs a) {
     }
     return;
   }
-  blk -= a.nconv_blocks;
-  if (blk == 1) {  // single-rank fast path: stage the next step's batch indices, advance the cursor
+  const int blk = blockIdx.x - nexch;
+  if (blk == 1) {  // fused update: stage the next step's batch indices, advance the cursor
     __shared__ long long nxt;
     if (threadIdx.x == 0) nxt = (*a.sgd.cursor + 1) % a.sgd.nsteps;
     __syncthreads();
@@ -853,6 +933,11 @@ __global__ void __launch_bounds__(RT) lenet_reduce_kernel(LeNetRedArgs a) {
     if (lane == 0) {
       a.stats[0] = l;
       a.stats[1] = c;
+      if (a.sgd_on && a.sgd.run_stats != nullptr) {  // device run statistics (trainer callbacks)
+        a.sgd.run_stats[0] += l;
+        a.sgd.run_stats[1] += c;
+        a.sgd.run_stats[2] += 1.f;
+      }
     }
   }
 }
@@ -906,20 +991,23 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
     for (int x = 0; x < 8; ++x)
       if (slot < by_xcd[x].size()) order.push_back(by_xcd[x][slot]);
   for (int t : order) r.tile_of_block[b++] = t;
-  // measurement aid: DISTRIFLOW_LENET_RED_SKIP=1 launches no dense tiles, =2 no conv blocks (wrong gradients)
-  static const int skip = [] {
-    const char* e = getenv("DISTRIFLOW_LENET_RED_SKIP");
-    return e ? atoi(e) : 0;
-  }();
-  if (skip & 1) {
-    r.dense_tiles = 0;
-  }
-  const int nconv = (skip & 2) ? 0 : r.nconv_blocks;
-  if (skip & 2) r.nconv_blocks = 0;
-  if (r.sgd_on && (skip || !r.sgd.master || !r.sgd.wbf || !r.sgd.hyper || !r.sgd.frag || !r.sgd.ticket || !r.sgd.stage))
+  if (r.sgd_on && (!r.sgd.master || !r.sgd.wbf || !r.sgd.hyper || !r.sgd.frag || !r.sgd.ticket || !r.sgd.stage))
     return hipErrorInvalidValue;
+  const int nslot = r.dense_tiles + r.nconv_blocks;
+  if (r.exch_blocks <= 0 || r.exch_blocks > nslot) r.exch_blocks = nslot;
+  if (r.exch_blocks * kMaxSlotsPerBlock < nslot) return hipErrorInvalidValue;
+  if (r.ll_on) {
+    // slot s is LL slot s.  Every exchanging workgroup must be resident at once on every rank (a waiting
+    // workgroup must never keep a peer's from being dispatched): 1024-thread workgroups at 64 VGPRs and
+    // 28 KB LDS run 2 per CU, so <= 512 on 256 CUs with one rank per GPU
+    if (!r.sgd_on || r.ll.world < 2 || r.ll.world > kP2PMaxRanks || r.ll.rank < 0 || r.ll.rank >= r.ll.world ||
+        !r.ll.epochs || !r.ll.err || nslot > r.ll.nslots || r.exch_blocks > 512)
+      return hipErrorInvalidValue;
+    for (int k = 0; k < r.ll.world; ++k)
+      if (!r.ll.bases[k]) return hipErrorInvalidValue;
+  }
   const int extra = (r.sgd_on && r.sgd.src) ? 1 : 0;  // the index-staging workgroup
-  hipLaunchKernelGGL(lenet_reduce_kernel, dim3(r.dense_tiles + nconv + 1 + extra), dim3(RT), 0, st, r);
+  hipLaunchKernelGGL(lenet_reduce_kernel, dim3(r.exch_blocks + 1 + extra), dim3(RT), 0, st, r);
   return hipGetLastError();
 }
 

@@ -49,8 +49,10 @@ __global__ void __launch_bounds__(MT) classifier_metrics_kernel(const float* __r
     }
     int y = labels[r];
     y = y < 0 ? 0 : (y >= C ? C - 1 : y);
-    corr += am == y ? 1.f : 0.f;  // argmax is invariant under the softmax
-    if (softmax || kind == kMetricSoftmaxCE) {
+    corr += am == y ? 1.f : 0.f;  // argmax is invariant under the softmax / sigmoid
+    if (softmax == 2) {  // the model ends in sigmoid: metrics of its probabilities
+      for (int c = 0; c < C; ++c) p[c] = 1.f / (1.f + __expf(-p[c]));
+    } else if (softmax || kind == kMetricSoftmaxCE) {
       float s = 0.f;
       for (int c = 0; c < C; ++c) s += __expf(p[c] - mx);
       if (kind == kMetricSoftmaxCE && !softmax) {  // logits in: -log softmax(z)_y

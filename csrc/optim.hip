@@ -120,7 +120,14 @@ __device__ __forceinline__ void index_stream_body(const IndexStream& is) {
     if (i < is.B) is.dst[i] = v[r];
   }
   for (int i = threadIdx.x + 256 * R; i < is.B; i += 256) is.dst[i] = src[i];
-  if (threadIdx.x == 0) *is.cursor = next;
+  if (threadIdx.x == 0) {
+    *is.cursor = next;
+    if (is.run_stats != nullptr) {  // this step's stats are final: every step kernel precedes this launch
+      is.run_stats[0] += is.step_stats[0];
+      is.run_stats[1] += is.step_stats[1];
+      is.run_stats[2] += 1.f;
+    }
+  }
 }
 
 // Fused LeNet-5: the conv-weight MFMA fragments of the next step, kLeNetFragBlocks extra workgroups,

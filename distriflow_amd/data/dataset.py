@@ -109,18 +109,20 @@ class DistriDataset:
 
     addPreprocessCallback = add_preprocess_callback
 
-    def index_stream(self, rank: int = 0, world: int = 1, device=None) -> torch.Tensor:
+    def index_stream(self, rank: int = 0, world: int = 1, device=None, with_epochs: bool = False):
         """Device batch schedule for the data-parallel engine (``DataParallelTrainer.bind_distri_dataset``):
         drains the dispenser in its FCFS order over every remaining epoch, giving the k-th dispensed
         full-size batch to rank k % world, and completes each batch as it is scheduled (the sync engine
         applies every step, so at-least-once dispatch is exactly-once here).  Returns this rank's
         [steps][batch_size] int64 example indices (the epochs' shuffles included); every rank gets the
         same number of steps.  A ragged last batch is skipped: a captured step has a fixed shape.
+        ``with_epochs``: also return, per step, the dataset epoch of that step's first global batch
+        (identical on every rank: epoch boundaries for checkpoints / barriers).
         Preprocess callbacks run on host-side Batch objects and cannot run inside a replayed device
         step, so they are refused here (the message-level roles apply them)."""
         if self.preprocess_callbacks:
             raise ValueError("preprocess callbacks need the message-level engine (roles), not the device stream")
-        rows, k = [], 0
+        rows, epochs, k = [], [], 0
         while True:
             done, b, epoch, start, size = self._disp.next()
             if done:
@@ -128,12 +130,15 @@ class DistriDataset:
             if size == self.batch_size:
                 if k % world == rank:
                     rows.append(self.example_indices(b))
+                if k % world == 0:
+                    epochs.append(int(epoch))
                 k += 1
             self._disp.complete(int(b), int(epoch))
         steps = k // world
         if steps == 0:
             raise ValueError("the dataset yields no full batch per rank")
-        return torch.stack(rows[:steps]).to(device if device is not None else self.x.device)
+        out = torch.stack(rows[:steps]).to(device if device is not None else self.x.device)
+        return (out, epochs[:steps]) if with_epochs else out
 
     def state(self) -> dict:
         return dict(self._disp.state())

@@ -231,52 +231,61 @@ def run_sync(args) -> dict:
     x, y = _load_data(args, dev)
     n = x.shape[0]
     B = args.batch
-    steps_per_epoch = n // (B * world)
-    start_epoch = 0
+    start_step = 0
     store = VersionedStore(args.save_dir) if args.save_dir else None
     if store is not None:
         store.setup()
         if args.resume and store.last() is not None:
             load_layers_model_weights(net, os.path.join(store.path(store.last()), "model.json"))
             rec = store.read_resume() or {}
-            start_epoch = int(rec.get("epoch", -1)) + 1
-            log.log(f"resumed from version {store.last()} at epoch {start_epoch}")
+            start_step = int(rec.get("step", 0))
+            log.log(f"resumed from version {store.last()} at step {start_step} (after epoch {rec.get('epoch')})")
     graph = args.graph or "full"
     tr = DataParallelTrainer(net, lr=args.lr, momentum=args.momentum, graph=graph if dev.type == "cuda" else "none")
     scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
-    if start_epoch < args.epochs:
-        # the DistriDataset's dispenser (epochs, per-epoch shuffle, FCFS order, completion) becomes the
-        # device index stream: batch k of the schedule goes to rank k % world, and every step's optimizer
-        # launch stages the next step's indices (no host work per step)
-        ds = DistriDataset(x, y, {"batchSize": B, "epochs": args.epochs - start_epoch}, shuffle=True,
-                           seed=args.seed + start_epoch)
-        tr.bind_distri_dataset(ds, rank, world, scale=scale)
-        steps_per_epoch = tr.steps_per_epoch
-    step = 0
+    # the DistriDataset's dispenser (epochs, per-epoch shuffle, FCFS order, completion) becomes the device
+    # index stream: batch k of the schedule goes to rank k % world, and every step's update launch stages
+    # the next step's indices (no host work per step).  The schedule is always built from the ORIGINAL seed
+    # and epoch count, and a resumed job skips the steps already taken: it trains on exactly the batches an
+    # uninterrupted job would have.
+    ds = DistriDataset(x, y, {"batchSize": B, "epochs": args.epochs}, shuffle=True, seed=args.seed)
+    tr.bind_dataset(ds.x, ds.y, B, scale=scale)
+    rows, row_epoch = ds.index_stream(rank, world, device=dev, with_epochs=True)
+    total = rows.shape[0]
+    start = min(start_step, total)
+    if start < total:
+        tr.bind_index_stream(rows[start:])
+    # per-replay statistics through the trainer callbacks (device counters, read back asynchronously)
+    tr.on_upload(lambda st: log.metric(event="upload", **st))
+    tr.on_new_version(lambda old, new: log.log(f"updated model: {old} -> {new}"))
+    step = start
     t0 = time.perf_counter()
     seen = 0
     last_loss = float("nan")
-    for epoch in range(start_epoch, args.epochs):
-        for i in range(steps_per_epoch):
-            faults.step(step)
-            st = tr.step()
-            step += 1
-            seen += B * world
-            if args.steps and step >= args.steps:
-                break
+    st = None
+    for i in range(start, total):
+        if args.steps and step >= args.steps:
+            break
+        faults.step(step)
+        st = tr.step()
+        step += 1
+        seen += B * world
+        epoch_end = i + 1 == total or row_epoch[i + 1] != row_epoch[i]
+        if not epoch_end and not (args.steps and step >= args.steps):
+            continue
+        epoch = row_epoch[i]
+        tr.flush_callbacks()
         last_loss = float(st[0]) / B
         el = time.perf_counter() - t0
         log.metric(event="epoch", epoch=epoch, step=step, loss=last_loss, images_per_s=seen / el)
         log.log(f"epoch {epoch}: loss {last_loss:.4f}, {seen / el:.0f} images/s")
-        if store is not None and rank == 0:
+        if epoch_end and store is not None and rank == 0:
             v = store.new_version()
             save_layers_model(net, store.path(v))
             store.mark_current(v)
             store.write_resume({"epoch": epoch, "step": step, "version": v})
         if world > 1:
             dist.barrier()
-        if args.steps and step >= args.steps:
-            break
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0

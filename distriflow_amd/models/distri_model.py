@@ -220,23 +220,35 @@ class EngineModel(DistriModel):
         self.net: Optional[Net] = model if isinstance(model, Net) else None
         self.momentum = 0.0
         self.weight_decay = 0.0
+        self._strict_loss = strict_loss
+        # checked now when the output is known (or cannot matter); a sigmoidCrossEntropy compile loss on a
+        # not-yet-fetched model is checked once fetch_initial() knows whether the model ends in sigmoid
+        if self.net is not None or self.compile["loss"] != "sigmoidCrossEntropy":
+            self._check_loss()
+
+    def _check_loss(self):
+        """the reference's fit() always optimises softmax cross-entropy and the
+        compile loss (default meanSquaredError) only feeds evaluate().  The engine trains the cross-entropy
+        that matches the model's output (softmax CE, or sigmoid CE for a model ending in sigmoid) and says
+        so once when the compile loss differs, instead of silently training another loss."""
         loss = self.compile["loss"]
-        if loss not in _CE_LOSSES:
-            # the reference's fit() always optimises softmax cross-entropy and the
-            # compile loss (default meanSquaredError) only feeds evaluate(); the engine keeps that contract
-            # but says so once instead of silently training a different loss than the one configured
-            if strict_loss:
-                raise ValueError(f"EngineModel trains softmax cross-entropy on logits; compile loss {loss!r} "
-                                 "is not trainable by the engine")
-            if loss not in _WARNED_LOSSES:
-                _WARNED_LOSSES.add(loss)
-                warnings.warn(f"EngineModel trains softmax cross-entropy on logits; the compile loss {loss!r} is "
-                              "used for evaluate() metrics only (reference fit(), models.ts:137-142)",
-                              stacklevel=2)
+        trained = "sigmoidCrossEntropy" if getattr(self.net, "final_act", "") == "sigmoid" else "softmax cross-entropy"
+        ok = loss == "sigmoidCrossEntropy" if trained == "sigmoidCrossEntropy" else loss in _CE_LOSSES
+        if ok:
+            return
+        if self._strict_loss:
+            raise ValueError(f"EngineModel trains {trained} on logits; compile loss {loss!r} "
+                             "is not trainable by the engine")
+        if (loss, trained) not in _WARNED_LOSSES:
+            _WARNED_LOSSES.add((loss, trained))
+            warnings.warn(f"EngineModel trains {trained} on logits; the compile loss {loss!r} is "
+                          "used for evaluate() metrics only (reference fit(), models.ts:137-142)", stacklevel=3)
 
     def fetch_initial(self):
         if self.net is None:
             self.net = fetch_model(self._src, self._device)
+            if self.compile["loss"] == "sigmoidCrossEntropy":
+                self._check_loss()
         self._sync_hyper()
         return self.net
 
@@ -311,7 +323,7 @@ class EngineModel(DistriModel):
             z = net._forward_eval(xx.to(net.dtype) if not isinstance(xx, ops.GatherRef) else xx)
             if not hasattr(self, "_metric_buf") or self._metric_buf.device != z.device:
                 self._metric_buf = torch.zeros(2, dtype=torch.float32, device=z.device)
-            st = ops.classifier_metrics(z, yy, loss, net.final_softmax, self._metric_buf).tolist()
+            st = ops.classifier_metrics(z, yy, loss, net.final_act, self._metric_buf).tolist()
             out = [st[0] / max(n, 1)]
             if "accuracy" in self.compile["metrics"] or "acc" in self.compile["metrics"]:
                 out.append(st[1] / max(n, 1))

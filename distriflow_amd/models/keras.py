@@ -1,13 +1,64 @@
 """Keras / tf.js ``LayersModel`` topology <-> engine layers.
 
-Reads the ``modelTopology`` of a tf.js ``model.json`` (Keras 2.x Sequential, as shipped in
-/root/reference/experiment/mnist/model.json:1) and writes it back, so a DistriFlow user's model files
-load directly.  Supported classes: InputLayer, Conv2D, Dense, Activation, MaxPooling2D, Dropout,
-Flatten, BatchNormalization (channels_last only).
+Reads the ``modelTopology`` of a tf.js ``model.json`` and writes it back, so a DistriFlow user's model
+files load directly.  The reference wraps any ``tf.LayersModel`` fetched by URL
+(/root/reference/src/common/utils.ts:236-244, src/common/models.ts:92-100); its shipped model is a
+Keras 2.1.4 Sequential (/root/reference/experiment/mnist/model.json:1).  Supported:
+
+* ``Sequential`` models, and functional ``Model`` / ``Functional`` graphs that are a single chain
+  (every layer consumes the previous one: what a Sequential exported through the functional API is);
+* InputLayer, Conv2D, Dense, Activation (relu, relu6, sigmoid, tanh, elu, selu, softplus, softsign,
+  hard_sigmoid, swish / silu, exponential, linear; softmax / sigmoid as the output), MaxPooling2D and
+  AveragePooling2D (any pool / strides, 'valid' or 'same'), GlobalAveragePooling2D,
+  GlobalMaxPooling2D, Dropout, Flatten, BatchNormalization — channels_last only.
 """
 from __future__ import annotations
 
-from .layers import Activation, BatchNorm, Conv2D, Dense, Dropout, Flatten, Layer, MaxPooling2D
+from .layers import (Activation, AveragePooling2D, BatchNorm, Conv2D, Dense, Dropout, Flatten,
+                     GlobalAveragePooling2D, GlobalMaxPooling2D, Layer, MaxPooling2D)
+
+
+def _chain_order(layer_cfgs: list, model_cfg: dict) -> list:
+    """Layers of a functional graph in execution order; raises unless the graph is one chain."""
+    by_name = {lc.get("name") or lc["config"].get("name"): lc for lc in layer_cfgs}
+
+    def parents(lc):
+        nodes = lc.get("inbound_nodes") or []
+        if not nodes:
+            return []
+        if len(nodes) != 1:
+            raise NotImplementedError(f"layer {lc['config'].get('name')!r} is applied more than once (shared layer)")
+        node = nodes[0]
+        if isinstance(node, dict):  # Keras 3 style {"args": [...], "kwargs": {}}
+            args = node.get("args", [])
+            names = [a["config"]["keras_history"][0] for a in args if isinstance(a, dict) and "config" in a]
+        else:  # Keras 2 style [[name, node_index, tensor_index, kwargs], ...]
+            names = [inb[0] for inb in node]
+        return names
+
+    outs = model_cfg.get("output_layers") or []
+    if len(outs) != 1:
+        raise NotImplementedError("functional models must have exactly one output")
+    order = []
+    name = outs[0][0] if isinstance(outs[0], (list, tuple)) else outs[0]
+    seen = set()
+    while True:
+        if name in seen:
+            raise ValueError("cycle in the layer graph")
+        seen.add(name)
+        lc = by_name[name]
+        order.append(lc)
+        ps = parents(lc)
+        if not ps:
+            break
+        if len(ps) != 1:
+            raise NotImplementedError(f"layer {name!r} has {len(ps)} inputs: only single-chain graphs are supported "
+                                      "(no Add / Concatenate joins)")
+        name = ps[0]
+    order.reverse()
+    if len(order) != len(layer_cfgs):
+        raise NotImplementedError("functional graph has branches that do not reach the output")
+    return order
 
 
 def _init_name(cfg):
@@ -35,9 +86,11 @@ def layers_from_keras(model_config: dict) -> tuple[list[Layer], tuple]:
         model_config = model_config["model_config"]
     cls = model_config.get("class_name")
     cfg = model_config.get("config")
-    if cls not in ("Sequential", None):
-        raise NotImplementedError(f"only Sequential models are supported, got {cls}")
     layer_cfgs = cfg["layers"] if isinstance(cfg, dict) else cfg
+    if cls in ("Model", "Functional"):
+        layer_cfgs = _chain_order(layer_cfgs, cfg)
+    elif cls not in ("Sequential", None):
+        raise NotImplementedError(f"model class {cls!r} (supported: Sequential, single-chain functional Model)")
     layers: list[Layer] = []
     input_shape = None
     for lc in layer_cfgs:
@@ -61,10 +114,14 @@ def layers_from_keras(model_config: dict) -> tuple[list[Layer], tuple]:
                                 kernel_initializer=_init_name(c)))
         elif k == "Activation":
             layers.append(Activation(c["activation"], name=name))
-        elif k == "MaxPooling2D":
-            if c.get("padding", "valid") != "valid":
-                raise NotImplementedError("MaxPooling2D padding='same'")
-            layers.append(MaxPooling2D(tuple(c.get("pool_size", [2, 2])), c.get("strides"), name=name))
+        elif k in ("MaxPooling2D", "AveragePooling2D"):
+            cls_ = MaxPooling2D if k == "MaxPooling2D" else AveragePooling2D
+            layers.append(cls_(tuple(c.get("pool_size", [2, 2])), c.get("strides"), c.get("padding", "valid"),
+                               name=name))
+        elif k == "GlobalAveragePooling2D":
+            layers.append(GlobalAveragePooling2D(name=name))
+        elif k == "GlobalMaxPooling2D":
+            layers.append(GlobalMaxPooling2D(name=name))
         elif k == "Dropout":
             layers.append(Dropout(c["rate"], name=name))
         elif k == "Flatten":
@@ -106,9 +163,15 @@ def keras_config_from_layers(layers: list[Layer], input_shape: tuple, name: str 
         elif isinstance(l, Activation):
             cls = "Activation"
             c.update(l.config())
+        elif isinstance(l, GlobalMaxPooling2D):
+            cls = "GlobalMaxPooling2D"
+            c["data_format"] = "channels_last"
         elif isinstance(l, MaxPooling2D):
-            cls = "MaxPooling2D"
+            cls = "AveragePooling2D" if isinstance(l, AveragePooling2D) else "MaxPooling2D"
             c.update(l.config())
+            c["data_format"] = "channels_last"
+        elif isinstance(l, GlobalAveragePooling2D):
+            cls = "GlobalAveragePooling2D"
             c["data_format"] = "channels_last"
         elif isinstance(l, Dropout):
             cls = "Dropout"

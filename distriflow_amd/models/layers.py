@@ -110,8 +110,10 @@ class Dense(Layer):
         self.out_f32 = False  # final logits layer writes fp32
         if activation == "relu":
             self.relu = True
-        elif activation not in ("linear", None, "softmax"):
+        elif activation not in ops.ACT_KINDS and activation != "softmax":
             raise NotImplementedError(f"Dense activation {activation!r}")
+        # any other activation runs as its own streaming launch after the GEMM (Net._plan inserts it), or
+        # folds into the loss when it ends the model (sigmoid / softmax)
 
     def build(self, in_shape):
         self.in_shape = tuple(in_shape)
@@ -183,7 +185,7 @@ class Conv2D(Layer):
         self.kernel_initializer = kernel_initializer
         if activation == "relu":
             self.relu = True
-        elif activation not in ("linear", None):
+        elif activation not in ops.ACT_KINDS:
             raise NotImplementedError(f"Conv2D activation {activation!r}")
 
     def build(self, in_shape):
@@ -273,34 +275,75 @@ class Conv2D(Layer):
                 "activation": self.activation, "use_bias": self.use_bias}
 
 
+def _pair(v, default=None):
+    if v is None:
+        return default
+    return (int(v[0]), int(v[1])) if isinstance(v, (list, tuple)) else (int(v), int(v))
+
+
 class MaxPooling2D(Layer):
-    def __init__(self, pool_size=2, strides=None, name=None):
-        super().__init__(name or "max_pooling2d")
-        p = pool_size[0] if isinstance(pool_size, (list, tuple)) else pool_size
-        s = strides[0] if isinstance(strides, (list, tuple)) else (strides or p)
-        if p != s:
-            raise NotImplementedError("MaxPooling2D requires pool_size == strides")
-        self.p = int(p)
+    """Keras MaxPooling2D: any pool_size / strides, 'valid' or 'same' padding.  Square pool == stride,
+    'valid' (the MNIST CNNs) takes the vectorised max-pool kernels, which also fold a following Dropout
+    and the fused conv+pool plans; everything else the general pooling kernels (csrc/act.hip)."""
+    avg = False
+
+    def __init__(self, pool_size=2, strides=None, padding="valid", name=None):
+        super().__init__(name or ("average_pooling2d" if self.avg else "max_pooling2d"))
+        self.pool = _pair(pool_size)
+        self.strides = _pair(strides, self.pool)
+        self.padding = padding
+        if padding not in ("valid", "same"):
+            raise NotImplementedError(f"pooling padding {padding!r}")
+        # the fast square case keeps the historical attribute name
+        self.p = self.pool[0] if (self.pool[0] == self.pool[1] == self.strides[0] == self.strides[1]
+                                  and padding == "valid" and not self.avg) else 0
+
+    @property
+    def simple(self) -> bool:
+        return self.p > 0
 
     def build(self, in_shape):
         H, W, C = in_shape
         self.in_shape = (H, W, C)
-        self.out_shape = (H // self.p, W // self.p, C)
+        if self.simple:
+            self.out_shape = (H // self.p, W // self.p, C)
+        else:
+            g = ops.pool_geometry(1, H, W, C, self.pool, self.strides, self.padding)
+            self.out_shape = (g[4], g[5], C)
         return self.out_shape
+
+    def _geom(self, B):
+        H, W, C = self.in_shape
+        return ops.pool_geometry(B, H, W, C, self.pool, self.strides, self.padding)
 
     def forward(self, x, training):
         self.x = x
-        ops.maxpool_fwd(x, self.out, self.p, drop=self.drop_spec(training))
+        if self.simple:
+            ops.maxpool_fwd(x, self.out, self.p, drop=self.drop_spec(training))
+            return self.out
+        ops.pool2d_fwd(x, self.out, self._geom(x.shape[0]), avg=self.avg)
+        d = self.drop_spec(training)
+        if d is not None:
+            ops.dropout(self.out, self.out, d[0], d[1], step=d[2], step_add=d[3] if len(d) > 3 else 0)
         return self.out
 
     def backward(self, dy):
         if not self.need_dx:
             return None
-        ops.maxpool_bwd(self.x, dy, self.dx, self.p, relu_fused=self.in_relu)
+        if self.simple:
+            ops.maxpool_bwd(self.x, dy, self.dx, self.p, relu_fused=self.in_relu)
+        else:
+            ops.pool2d_bwd(self.x, dy.reshape(self.out.shape), self.dx, self._geom(self.x.shape[0]), avg=self.avg,
+                           in_relu=self.in_relu)
         return self.dx
 
     def config(self):
-        return {"pool_size": [self.p, self.p], "strides": [self.p, self.p], "padding": "valid"}
+        return {"pool_size": list(self.pool), "strides": list(self.strides), "padding": self.padding}
+
+
+class AveragePooling2D(MaxPooling2D):
+    """Keras AveragePooling2D ('same' padding averages over the in-image pixels only, as TensorFlow)."""
+    avg = True
 
 
 class Dropout(Layer):
@@ -355,11 +398,28 @@ class Flatten(Layer):
 
 
 class Activation(Layer):
-    """Standalone activation; the engine fuses relu into the producer, softmax into the loss."""
+    """Keras Activation.  The engine fuses relu into the producer's epilogue and a final softmax /
+    sigmoid into the loss; any other placement executes here as one streaming launch forward
+    (y = act(x)) and one backward (dx = dy * act'(x), csrc/act.hip)."""
 
-    def __init__(self, activation: str, name=None):
+    def __init__(self, activation: str, name=None, implicit: bool = False):
         super().__init__(name or "activation")
+        if activation not in ops.ACT_KINDS and activation != "softmax":
+            raise NotImplementedError(f"activation {activation!r}")
         self.activation = activation
+        self.implicit = implicit  # split off a Dense / Conv2D activation (not a Keras layer of its own)
+
+    def forward(self, x, training):
+        self.x = x
+        ops.act_fwd(x, self.out.view(x.shape), self.activation)
+        return self.out
+
+    def backward(self, dy):
+        if not self.need_dx:
+            return None
+        ops.act_bwd(self.x, dy.reshape(self.x.shape), self.dx.view(self.x.shape), self.activation,
+                    in_relu=self.in_relu)
+        return self.dx
 
     def config(self):
         return {"activation": self.activation}
@@ -443,6 +503,24 @@ class BatchNorm(Layer):
         if self.in_relu:
             raise NotImplementedError("BatchNorm after a fused ReLU")
         return self.dx
+
+
+class GlobalMaxPooling2D(MaxPooling2D):
+    """Keras GlobalMaxPooling2D: a max over the whole H x W map (general pooling kernel), output [C]."""
+
+    def __init__(self, name=None):
+        super().__init__(1, 1, "valid", name=name or "global_max_pooling2d")
+        self.p = 0
+
+    def build(self, in_shape):
+        H, W, C = in_shape
+        self.in_shape = (H, W, C)
+        self.pool = self.strides = (H, W)
+        self.out_shape = (C,)
+        return self.out_shape
+
+    def config(self):
+        return {}
 
 
 class GlobalAveragePooling2D(Layer):

@@ -75,12 +75,26 @@ class Net:
         self._side = [torch.cuda.Stream(device=self.device) for _ in range(3)] if self.is_gpu else []
 
     # ------------------------------------------------------------------ planning / fusion
+    @property
+    def final_softmax(self) -> bool:
+        return self.final_act == "softmax"
+
     def _plan(self):
         shape = self.input_shape
         execd: list[Layer] = []
-        pending = list(self.layers_all)
+        # a Dense / Conv2D activation other than relu / linear runs as its own streaming launch right after
+        # the GEMM, unless it ends the model (softmax / sigmoid fold into the loss)
+        pending = []
+        for j, l in enumerate(self.layers_all):
+            pending.append(l)
+            act = getattr(l, "activation", None) if isinstance(l, (Dense, Conv2D)) else None
+            last = j == len(self.layers_all) - 1
+            if act not in (None, "linear", "relu") and not (last and act in ("softmax", "sigmoid")):
+                if act == "softmax":
+                    raise NotImplementedError("a softmax activation is only supported on the output layer")
+                pending.append(Activation(act, name=f"{l.name}/{act}", implicit=True))
         i = 0
-        self.final_softmax = False
+        self.final_act = "linear"  # what the model applies to the logits: linear | softmax | sigmoid
         while i < len(pending):
             l = pending[i]
             shape = l.build(shape)
@@ -94,10 +108,12 @@ class Net:
                     pass
                 elif act == "relu" and prev is not None and prev.can_fuse_relu() and not prev.relu:
                     prev.relu = True  # fused into the producer's epilogue (config() keeps the Keras view)
-                elif act == "softmax" and i == len(pending) - 1:
-                    self.final_softmax = True
+                elif act in ("softmax", "sigmoid") and i == len(pending) - 1:
+                    self.final_act = act  # folded into the training loss / applied by predict()
+                elif act == "softmax":
+                    raise NotImplementedError("a softmax activation is only supported on the output layer")
                 else:
-                    raise NotImplementedError(f"cannot place activation {act!r} after {type(prev).__name__}")
+                    execd.append(l)  # its own launch (csrc/act.hip)
                 i += 1
                 continue
             execd.append(l)
@@ -112,8 +128,8 @@ class Net:
                 execd = [KerasConvBlock(execd[0], execd[1].conv, execd[1].pool)] + execd[2:]
         last = execd[-1]
         if isinstance(last, Dense):
-            if last.activation == "softmax":
-                self.final_softmax = True
+            if last.activation in ("softmax", "sigmoid"):
+                self.final_act = last.activation
             last.out_f32 = True
             if last.relu:
                 raise ValueError("the logits layer must not end in ReLU")
@@ -142,6 +158,8 @@ class Net:
 
         if not self.is_gpu or os.environ.get("DISTRIFLOW_LENET_FUSED", "1") == "0" or not ops.lenet_supported():
             return False
+        if self.final_act == "sigmoid":  # the fused kernel trains softmax cross-entropy
+            return False
         if self.input_shape != (28, 28, 1) or len(execd) != 5:
             return False
         c1, c2, d1, d2, d3 = execd
@@ -160,7 +178,7 @@ class Net:
         """Index of the first layer of the trailing Dense chain trained by the fused head kernels
         (csrc/mlphead.hip), or None.  Conditions: <= 4 Dense layers, ReLU on all but the logits layer,
         <= 16 classes, hidden widths <= 256, input width a multiple of 8 and <= 1024."""
-        if not self.is_gpu or not ops.head_supported():
+        if not self.is_gpu or not ops.head_supported() or self.final_act == "sigmoid":
             return None
         j0 = len(execd)
         while j0 > 0 and isinstance(execd[j0 - 1], Dense) and len(execd) - j0 < 4:
@@ -300,9 +318,15 @@ class Net:
                 grad_ready(i)
 
     def loss_and_grad(self, logits, labels, grad_scale: Optional[float] = None):
+        """The training loss on the logits: softmax cross-entropy (a final softmax or linear output) or,
+        for a model that ends in sigmoid, sigmoid cross-entropy against the one-hot labels."""
         B = logits.shape[0]
         self.stats.zero_()
-        ops.softmax_ce(logits, labels, self.dlogits, self.stats, 1.0 / B if grad_scale is None else grad_scale)
+        gs = 1.0 / B if grad_scale is None else grad_scale
+        if self.final_act == "sigmoid":
+            ops.sigmoid_ce(logits, labels, self.dlogits, self.stats, gs)
+        else:
+            ops.softmax_ce(logits, labels, self.dlogits, self.stats, gs)
         return self.stats
 
     def compute_gradients(self, x, labels, grad_ready=None):
@@ -336,11 +360,13 @@ class Net:
         self.backward(self.dlogits, grad_ready)
         return stats
 
-    def compute_gradients_and_update(self, x, labels, index_stream=None):
-        """Single-rank fast path of the fused LeNet-5 step: gradients AND the SGD update (with the
-        store's device hyper-parameters) in the step's two launches (the reduce kernel applies the
-        update and rebuilds the next step's weight fragments; ``index_stream`` = (stream, cursor, dst)
-        is advanced by it too).  Same arithmetic as compute_gradients + ParamStore.sgd_step."""
+    def compute_gradients_and_update(self, x, labels, index_stream=None, ll=None, run_stats=None):
+        """Fused LeNet-5 step: gradients AND the SGD update (with the store's device hyper-parameters)
+        in the step's two launches (the reduce kernel applies the update and rebuilds the next step's
+        weight fragments; ``index_stream`` = (stream, cursor, dst) is advanced by it too).  Same
+        arithmetic as compute_gradients + ParamStore.sgd_step.  ``ll``: a world > 1 native P2PComm —
+        the reduce kernel then sums every gradient over the ranks in its epilogue (csrc/ll_exchange.h),
+        so a data-parallel step is still two launches, equal to compute_gradients + all-reduce + SGD."""
         if not self.lenet_fused:
             raise RuntimeError("compute_gradients_and_update needs the fused LeNet-5 plan")
         if self.has_dropout:
@@ -353,6 +379,11 @@ class Net:
                    sgd_descs=st._descs_host, sgd_ticket=self._lenet_ticket, sgd_stage=self._lenet_stage)
         if index_stream is not None:
             sgd.update(idx_stream=index_stream[0], idx_cursor=index_stream[1], idx_dst=index_stream[2])
+        if ll is not None:
+            sgd["ll"] = ll
+            sgd["exch_blocks"] = int(getattr(self, "lenet_exch_blocks", 0))
+        if run_stats is not None:
+            sgd["run_stats"] = run_stats
         stats = self._compute_gradients_lenet(x, labels, None, sgd=sgd)
         st.lenet_state = "fresh"  # the reduce kernel rebuilt the fragments from the new weights
         return stats
@@ -525,7 +556,10 @@ class Net:
             yb = labels[s: s + batch_size].to(self.device, torch.int32)
             logits = self._forward_eval(xb)
             st = torch.zeros(2, dtype=torch.float32, device=self.device)
-            ops.softmax_ce(logits, yb, None, st, 1.0)
+            if self.final_act == "sigmoid":
+                ops.sigmoid_ce(logits, yb, None, st, 1.0)
+            else:
+                ops.softmax_ce(logits, yb, None, st, 1.0)
             loss += float(st[0])
             correct += float(st[1])
         return loss / max(n, 1), correct / max(n, 1)
@@ -554,7 +588,8 @@ class Net:
         for s in range(0, x.shape[0], batch_size):
             xb = x[s: s + batch_size].to(self.device, self.dtype)
             z = self._forward_eval(xb)
-            outs.append(torch.softmax(z, dim=1) if self.final_softmax else z)
+            outs.append(torch.softmax(z, dim=1) if self.final_act == "softmax" else
+                        torch.sigmoid(z) if self.final_act == "sigmoid" else z)
         return torch.cat(outs)
 
     # ------------------------------------------------------------------ mutable state

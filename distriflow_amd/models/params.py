@@ -263,21 +263,29 @@ class ParamStore:
         if momentum != 0.0 and self.momentum is None:
             self.momentum = torch.zeros_like(self.master)
 
-    def sgd_step(self, index_stream=None):
+    def sgd_step(self, index_stream=None, run_stats=None):
         """w -= lr * (grad_scale * g [+ wd w]) (momentum optional); uses the device-side hyper tensor.
         ``index_stream = (stream [nsteps][B], cursor [1], dst [B])`` (GPU): the same launch stages the
-        next step's batch indices into ``dst`` and advances ``cursor`` (csrc/optim.hip)."""
+        next step's batch indices into ``dst`` and advances ``cursor`` (csrc/optim.hip).
+        ``run_stats = (step_stats [2], run [3])``: that workgroup also accumulates the step's
+        [loss sum, correct] and counts the update (device run statistics, no extra launch)."""
         if self.compute_bf16:
             src, cur, dst = index_stream if index_stream is not None else (None, None, None)
+            kw = self._frag_kw(True)
+            if run_stats is not None and src is not None:
+                kw.update(step_stats=run_stats[0], run_stats=run_stats[1])
             native.require().sgd_multi(self._descs, self._ndesc, self._sgd_blocks, self.master, self.grad,
                                        self.momentum, self.wbf, self.hyper, True, src, cur, dst,
-                                       self._descs_host, **self._frag_kw(True))
+                                       self._descs_host, **kw)
             return
         if index_stream is not None:
             src, cur, dst = index_stream
             nxt = (int(cur[0]) + 1) % src.shape[0]
             dst.copy_(src[nxt])
             cur.fill_(nxt)
+            if run_stats is not None:
+                run_stats[1][:2] += run_stats[0][:2]
+                run_stats[1][2] += 1.0
         lr, mom, wd, gs, nest = self._hyper_host
         if not hasattr(self, "_valid"):
             self._valid = torch.zeros(self.total, dtype=torch.bool, device=self.device)

@@ -336,6 +336,123 @@ def add_act(a, b, out, relu=False):
     return out
 
 
+# ---- generic Keras layers (csrc/act.hip); codes match kernels.h ActKind
+ACT_KINDS = {"linear": 0, None: 0, "relu": 1, "relu6": 2, "sigmoid": 3, "tanh": 4, "elu": 5, "selu": 6,
+             "softplus": 7, "softsign": 8, "hard_sigmoid": 9, "hardSigmoid": 9, "swish": 10, "silu": 10,
+             "exponential": 11}
+
+
+def _act_ref(kind: int, x):
+    import torch.nn.functional as F
+
+    f = {0: lambda v: v, 1: F.relu, 2: lambda v: v.clamp(0.0, 6.0), 3: torch.sigmoid, 4: torch.tanh, 5: F.elu,
+         6: F.selu, 7: F.softplus, 8: F.softsign, 9: lambda v: (0.2 * v + 0.5).clamp(0.0, 1.0), 10: F.silu,
+         11: torch.exp}[kind]
+    return f(x)
+
+
+def act_fwd(x, out, activation):
+    """out = act(x) for the Keras activations in ACT_KINDS (one streaming launch on GPU)."""
+    kind = ACT_KINDS[activation]
+    if x.is_cuda:
+        _C().act_fwd(x.contiguous(), out, kind)
+    else:
+        out.copy_(_act_ref(kind, x.float()).to(out.dtype))
+    return out
+
+
+def act_bwd(x, dy, dx, activation, in_relu=False):
+    """dx = dy * act'(x) [* relu'(x) when x is itself a fused-ReLU output]."""
+    kind = ACT_KINDS[activation]
+    if x.is_cuda:
+        _C().act_bwd(x.contiguous(), dy.contiguous(), dx, kind, bool(in_relu))
+    else:
+        xv = x.float().detach().requires_grad_(True)
+        y = _act_ref(kind, xv)
+        (g,) = torch.autograd.grad(y, xv, dy.float())
+        if in_relu:
+            g = g * (x.float() > 0)
+        dx.copy_(g.to(dx.dtype))
+    return dx
+
+
+def sigmoid_ce(logits, labels, dlogits=None, stats=None, grad_scale=1.0):
+    """Sigmoid cross-entropy on logits vs one-hot(labels), summed over classes: dlogits = (sigmoid(z) -
+    onehot) * grad_scale; stats += [loss_sum, #correct (argmax)]."""
+    B, C = logits.shape
+    if logits.is_cuda:
+        ldg = dlogits.shape[-1] if dlogits is not None else C
+        _C().sigmoid_ce(logits, labels.to(torch.int32), dlogits, stats, B, C, C, ldg, grad_scale)
+    else:
+        z = logits.float()
+        t = torch.nn.functional.one_hot(labels.long().clamp(0, C - 1), C).float()
+        loss = (z.clamp_min(0) - z * t + torch.log1p(torch.exp(-z.abs()))).sum()
+        if dlogits is not None:
+            dlogits.copy_(((torch.sigmoid(z) - t) * grad_scale).to(dlogits.dtype))
+        if stats is not None:
+            stats[0] += loss
+            stats[1] += (z.argmax(1) == labels.long()).float().sum()
+    return stats
+
+
+def pool_geometry(B, H, W, C, pool, strides, padding):
+    """[B, H, W, C, OH, OW, ph, pw, sh, sw, pt, pl] of a Keras/TF pooling layer ('valid' | 'same')."""
+    ph, pw = pool
+    sh, sw = strides
+    if padding == "same":
+        OH, OW = -(-H // sh), -(-W // sw)
+        tot_h = max((OH - 1) * sh + ph - H, 0)
+        tot_w = max((OW - 1) * sw + pw - W, 0)
+        pt, pl = tot_h // 2, tot_w // 2  # TF: the odd pixel of padding goes bottom / right
+    elif padding == "valid":
+        OH, OW = (H - ph) // sh + 1, (W - pw) // sw + 1
+        pt = pl = 0
+    else:
+        raise ValueError(f"pooling padding {padding!r}")
+    if OH < 1 or OW < 1:
+        raise ValueError(f"pool {pool} / {strides} does not fit a {H}x{W} input")
+    return [B, H, W, C, OH, OW, ph, pw, sh, sw, pt, pl]
+
+
+def _pool_ref(x, g, avg):
+    B, H, W, C, OH, OW, ph, pw, sh, sw, pt, pl = g
+    xf = x.float().permute(0, 3, 1, 2)
+    pb, pr = max((OH - 1) * sh + ph - H - pt, 0), max((OW - 1) * sw + pw - W - pl, 0)
+    if avg:
+        ones = torch.ones(1, 1, H, W, dtype=xf.dtype, device=xf.device)
+        num = torch.nn.functional.avg_pool2d(torch.nn.functional.pad(xf, (pl, pr, pt, pb)), (ph, pw), (sh, sw),
+                                             divisor_override=1)
+        cnt = torch.nn.functional.avg_pool2d(torch.nn.functional.pad(ones, (pl, pr, pt, pb)), (ph, pw), (sh, sw),
+                                             divisor_override=1)
+        y = num / cnt.clamp_min(1.0)
+    else:
+        y = torch.nn.functional.max_pool2d(torch.nn.functional.pad(xf, (pl, pr, pt, pb), value=float("-inf")),
+                                           (ph, pw), (sh, sw))
+    return y[:, :, :OH, :OW].permute(0, 2, 3, 1)
+
+
+def pool2d_fwd(x, out, geom, avg=False):
+    """General 2-D pooling (max / average; any window, stride and 'valid' / 'same' padding), NHWC."""
+    if x.is_cuda:
+        _C().pool2d_fwd(x.contiguous(), out, [int(v) for v in geom], bool(avg))
+    else:
+        out.copy_(_pool_ref(x, geom, avg).reshape(out.shape).to(out.dtype))
+    return out
+
+
+def pool2d_bwd(x, dy, dx, geom, avg=False, in_relu=False):
+    if x.is_cuda:
+        _C().pool2d_bwd(x.contiguous(), dy.contiguous(), dx, [int(v) for v in geom], bool(avg), bool(in_relu))
+    else:
+        xv = x.float().detach().requires_grad_(True)
+        y = _pool_ref(xv, geom, avg)
+        (g,) = torch.autograd.grad(y, xv, dy.float().reshape(y.shape))
+        if in_relu:
+            g = g * (x.float() > 0)
+        dx.copy_(g.reshape(dx.shape).to(dx.dtype))
+    return dx
+
+
 def relu_bwd(y, dy, dx):
     if y.is_cuda:
         _C().relu_bwd(y, dy, dx)
@@ -475,17 +592,22 @@ METRIC_KINDS = {"meanSquaredError": 0, "mse": 0, "absoluteDifference": 1, "hinge
                 "categoricalCrossentropy": 7}
 
 
-def classifier_metrics(z, labels, loss: str, softmax: bool, out):
+def classifier_metrics(z, labels, loss: str, softmax, out):
     """[sum over the batch of the compiled loss, number correct] of fp32 model outputs ``z`` [B][C]
     against int labels (one launch on GPU, csrc/metrics.hip).  ``softmax``: the model output is
     softmax(z).  Returns ``out`` (device [2]); CPU uses the torch loss registry."""
     if z.is_cuda:
-        _C().classifier_metrics(z.contiguous(), labels.to(torch.int32).contiguous(), METRIC_KINDS[loss], bool(softmax),
+        # softmax: False / True (model ends in softmax) or the output activation name ("sigmoid")
+        out_act = 2 if softmax == "sigmoid" else (1 if softmax in (True, "softmax") else 0)
+        _C().classifier_metrics(z.contiguous(), labels.to(torch.int32).contiguous(), METRIC_KINDS[loss], out_act,
                                 out)
         return out
     from ..losses import accuracy, get_loss
 
-    p = torch.softmax(z.float(), dim=1) if softmax else z.float()
+    if softmax == "sigmoid":
+        p = torch.sigmoid(z.float())
+    else:
+        p = torch.softmax(z.float(), dim=1) if softmax in (True, "softmax") else z.float()
     onehot = torch.nn.functional.one_hot(labels.long(), z.shape[1]).float()
     out[0] = get_loss(loss)(onehot, p).sum()
     out[1] = accuracy(labels, p).sum()

@@ -68,9 +68,9 @@ class AsyncPSTrainer(DataParallelTrainer):
             err = e
         self._agree(err, "IPC open")
         self._perm = None
-        from .watchdog import register_probe
+        from .watchdog import register_owner_probe
 
-        register_probe("async_ps", self.ps.host_error)
+        register_owner_probe("async_ps", self, lambda o: o.ps.host_error())
 
     def _agree(self, err, what):
         ok = err is None

@@ -83,14 +83,22 @@ def shutdown():
     global _ENV
     from .watchdog import active
 
+    from .watchdog import clear_probes
+
     wd = active()
     if wd is not None:
-        wd.stop()  # normal completion: peers stop watching this rank
+        # normal completion: peers stop watching this rank, but this rank keeps watching them until the
+        # final barrier returns (a peer that dies during shutdown still ends the job promptly)
+        wd.mark_done()
     if dist.is_initialized():
         try:
             dist.barrier()
         except Exception:
             pass
+    if wd is not None:
+        wd.stop()
+    clear_probes()
+    if dist.is_initialized():
         dist.destroy_process_group()
     _ENV = None
 

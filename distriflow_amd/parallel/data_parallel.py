@@ -70,6 +70,13 @@ class DataParallelTrainer:
         self._graph_B = None
         self._index_stream = None
         self.steps = 0
+        # device run statistics [loss sum, correct, updates, -]: accumulated inside the step's own last
+        # launch (no extra launch), read back asynchronously per replay when callbacks are registered
+        self.run_stats = torch.zeros(4, dtype=torch.float32, device=net.device)
+        self._version_cbs, self._upload_cbs = [], []
+        self._cb_pending = []
+        self._cb_ring = None
+        self._cb_last = None
         if broadcast_init and self.world > 1:
             dist.broadcast(net.store.master, src=0, group=group)
             net.store.refresh_compute()
@@ -121,6 +128,12 @@ class DataParallelTrainer:
         else:
             self._comm_stream = torch.cuda.Stream(device=self.net.device)
             self._p2p_pending = False
+            # ranks that time-share one GPU (rehearsals): the fused LeNet-5 reduce runs fewer exchanging
+            # workgroups (each owning several slots) so that every rank's waiting workgroups fit on the chip
+            # beside the peers' train kernels; with one rank per GPU every slot gets its own workgroup
+            ndev = max(1, torch.cuda.device_count())
+            share = -(-self.world // ndev) if ndev < self.world else 1
+            self.net.lenet_exch_blocks = 0 if share == 1 else max(48, 256 // share)
 
     def _reduce(self, t: torch.Tensor, async_op: bool):
         if self.p2p is not None and t.numel() * 4 <= self.p2p_limit:
@@ -181,9 +194,11 @@ class DataParallelTrainer:
         pt = self.phase_timer
         if pt is not None and torch.cuda.is_current_stream_capturing():
             pt = None
-        if (self.world == 1 and pt is None and self.fused_update and getattr(self.net, "lenet_fused", False)
-                and self.net.store.lenet_frag is not None):
-            return self.net.compute_gradients_and_update(x, y, self._index_stream)
+        if pt is None and self._fused_step_ok():
+            # the whole step in two launches; at world > 1 the reduce kernel sums the gradients over the
+            # ranks itself (in-kernel LL exchange over xGMI) before applying the update
+            ll = self.p2p.comm if (self.world > 1 and self._step_all_reduces) else None
+            return self.net.compute_gradients_and_update(x, y, self._index_stream, ll=ll, run_stats=self.run_stats)
         if pt is not None:
             pt.start("compute")  # forward + loss + backward (the fused head runs all three)
         stats = self.net.compute_gradients(x, y, grad_ready=hook)
@@ -194,10 +209,29 @@ class DataParallelTrainer:
         if pt is not None:
             pt.stop("comm")
             pt.start("update")
-        self.net.store.sgd_step(self._index_stream)
+        self.net.store.sgd_step(self._index_stream, run_stats=(stats, self.run_stats))
         if pt is not None:
             pt.stop("update")
         return stats
+
+    def _fused_step_ok(self) -> bool:
+        """The fused LeNet-5 step (train + reduce/exchange/update: two launches) is usable: single rank,
+        or every rank on the one-shot p2p path (its communicator carries the LL exchange slots)."""
+        if not (self.fused_update and getattr(self.net, "lenet_fused", False)
+                and self.net.store.lenet_frag is not None):
+            return False
+        if self.world == 1 or not self._step_all_reduces:
+            return True  # no exchange inside the step (single rank, FedAvg local steps)
+        return (self.p2p is not None and getattr(self.p2p.comm, "ll_slots", 0) >= 512
+                and self.net.store.total * 4 <= self.p2p_limit)
+
+    @property
+    def step_launches(self) -> str:
+        """What one training step is made of (diagnostic, reported by bench.py)."""
+        if self._fused_step_ok():
+            return ("train+reduce/exchange/update" if self.world > 1 and self._step_all_reduces
+                    else "train+reduce/update")
+        return "compute+allreduce+sgd" if self.world > 1 else "compute+sgd"
 
     def timed_eager_steps(self, n: int) -> dict:
         """Per-phase GPU milliseconds per step over ``n`` eager (uncaptured) steps on the bound index
@@ -258,6 +292,7 @@ class DataParallelTrainer:
         # warm-up on a side stream (allocator, RCCL communicators, kernel code objects); the warm-up
         # steps are not training steps: the engine state is restored before capture
         snap = net.snapshot_state()
+        rs0 = self.run_stats.clone()
         cursor = self._index_stream[1].clone() if self._index_stream is not None else None
         idx0 = self.idx.clone()
         with torch.cuda.stream(s):
@@ -267,6 +302,7 @@ class DataParallelTrainer:
         torch.cuda.current_stream(net.device).wait_stream(s)
         torch.cuda.synchronize(net.device)
         net.restore_state(snap)
+        self.run_stats.copy_(rs0)
         self.idx.copy_(idx0)
         if cursor is not None:
             self._index_stream[1].copy_(cursor)
@@ -297,6 +333,7 @@ class DataParallelTrainer:
                     except Exception:
                         pass
             net.restore_state(snap)
+            self.run_stats.copy_(rs0)
             self.idx.copy_(idx0)
             if cursor is not None:
                 self._index_stream[1].copy_(cursor)
@@ -337,14 +374,16 @@ class DataParallelTrainer:
         if self._index_stream is None:
             raise RuntimeError("bind_index_stream() first")
         self.steps += 1
+        _beat(self.steps)
         if self.graph_mode == "none":
             self._gather()
-            return self._step_body(self.xb, self.yb)
-        if self._graph is None:
-            self._capture_with_fallback()
+            st = self._step_body(self.xb, self.yb)
+        else:
             if self._graph is None:
-                return self._last_eager
-        return self._replay()
+                self._capture_with_fallback()
+            st = self._last_eager if self._graph is None else self._replay()
+        self._after_replay(1)
+        return st
 
     def step_indices(self, idx: torch.Tensor):
         """One training step on dataset rows ``idx`` (device int64 [B])."""
@@ -393,6 +432,69 @@ class DataParallelTrainer:
                 self._gather()
                 self._last_eager = self._step_body(self.xb, self.yb)
                 return
+
+    # ------------------------------------------------------------------ callbacks (no launches in the step)
+    def on_new_version(self, cb):
+        """``cb(old_version, new_version)`` once per replay (reference AbstractServer.onNewVersion,
+        /root/reference/src/server/abstract_server.ts:67-69,105-109).  A version is one applied update."""
+        self._version_cbs.append(cb)
+
+    def on_upload(self, cb):
+        """``cb(stats)`` once per replay with the replay's device statistics (reference onUpload with the
+        clients' metrics, abstract_server.ts:77-79,111-115): version, steps, images, loss (mean per
+        example), accuracy, updates counted on the device, rank, world."""
+        self._upload_cbs.append(cb)
+
+    onNewVersion = on_new_version
+    onUpload = on_upload
+
+    def _after_replay(self, nsteps: int):
+        """Queue an asynchronous read-back of the device run statistics after a replay of ``nsteps`` steps
+        (a copy into pinned memory behind the replay, outside the captured step) and fire the callbacks of
+        every replay whose copy has landed.  Nothing happens without registered callbacks."""
+        if not (self._version_cbs or self._upload_cbs):
+            return
+        v1 = self.steps
+        if self.net.is_gpu:
+            if self._cb_ring is None:
+                self._cb_ring = [torch.empty(4, dtype=torch.float32, pin_memory=True) for _ in range(16)]
+                self._cb_next = 0
+            if len(self._cb_pending) >= len(self._cb_ring):
+                self._drain_callbacks(block_one=True)
+            buf = self._cb_ring[self._cb_next]
+            self._cb_next = (self._cb_next + 1) % len(self._cb_ring)
+            buf.copy_(self.run_stats, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._cb_pending.append((ev, buf, v1 - nsteps, v1, nsteps))
+        else:
+            self._cb_pending.append((None, self.run_stats.clone(), v1 - nsteps, v1, nsteps))
+        self._drain_callbacks()
+
+    def _drain_callbacks(self, block: bool = False, block_one: bool = False):
+        while self._cb_pending:
+            ev, buf, v0, v1, n = self._cb_pending[0]
+            if ev is not None and not ev.query():
+                if not (block or block_one):
+                    return
+                ev.synchronize()
+            self._cb_pending.pop(0)
+            cur = buf.tolist()
+            last = self._cb_last or [0.0, 0.0, 0.0, 0.0]
+            self._cb_last = cur
+            dl, dc, du = cur[0] - last[0], cur[1] - last[1], cur[2] - last[2]
+            images = n * self.B
+            st = {"version": v1, "steps": n, "images": images * self.world, "loss": dl / max(images, 1),
+                  "accuracy": dc / max(images, 1), "updates": int(round(du)), "rank": self.rank, "world": self.world}
+            for cb in self._version_cbs:
+                cb(v0, v1)
+            for cb in self._upload_cbs:
+                cb(st)
+            block_one = False
+
+    def flush_callbacks(self):
+        """Fire the callbacks of every replay issued so far (waits for their read-backs)."""
+        self._drain_callbacks(block=True)
 
     # ------------------------------------------------------------------ multi-step graphs
     MAX_STEPS_PER_GRAPH = 64
@@ -458,6 +560,8 @@ class DataParallelTrainer:
             for _ in range(n // self._multi_u):
                 self._multi.replay()
                 self.steps += self._multi_u
+                _beat(self.steps)
+                self._after_replay(self._multi_u)
                 st = self.stats
             n -= (n // self._multi_u) * self._multi_u
         for _ in range(n):
@@ -468,10 +572,17 @@ class DataParallelTrainer:
         g, g2 = self._graph
         g.replay()
         if g2 is not None:
-            if self.world > 1:
+            if self.world > 1 and self._step_all_reduces:
                 self._reduce(self.net.store.grad, async_op=False)
             g2.replay()
         return self.stats
+
+
+def _beat(step: int):
+    """Progress beat for the dead-peer / stall watchdog (parallel/watchdog.py; no-op without one)."""
+    from .watchdog import beat
+
+    beat(step)
 
 
 def epoch_permutations(n: int, batch: int, steps: int, device, seed: int = 0):

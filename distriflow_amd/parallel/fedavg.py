@@ -24,6 +24,8 @@ from .data_parallel import DataParallelTrainer
 
 
 class FedAvgTrainer(DataParallelTrainer):
+    _step_all_reduces = False  # local steps exchange nothing (the fused LeNet-5 step stays local)
+
     def __init__(self, net, lr: float = 0.05, local_steps: int = 20, group=None, graph: str = "full",
                  allreduce: str = "auto"):
         super().__init__(net, lr=lr, group=group, overlap=False, graph=graph, allreduce=allreduce)

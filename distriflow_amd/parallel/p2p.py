@@ -38,7 +38,8 @@ def _agree(ok: bool, group, device) -> bool:
 class P2PAllReduce:
     """In-place SUM all-reduce of fp32 GPU tensors of up to ``max_bytes`` over IPC-mapped peer buffers."""
 
-    def __init__(self, group=None, max_bytes: int = 8 << 20, timeout_s: float = 30.0, self_test: bool = True):
+    def __init__(self, group=None, max_bytes: int = 8 << 20, timeout_s: float = 30.0, self_test: bool = True,
+                 ll_slots: int = 512):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -56,7 +57,9 @@ class P2PAllReduce:
         comm, handle = None, b""
         if ok:
             try:
-                comm = native.require().P2PComm(self.rank, self.world, self.max_floats, timeout_s)
+                # + ll_slots slots of the in-kernel LL exchange (csrc/ll_exchange.h) for kernels that
+                # fold the all-reduce into their own epilogue (the fused LeNet-5 reduce)
+                comm = native.require().P2PComm(self.rank, self.world, self.max_floats, timeout_s, ll_slots)
                 handle = comm.handle()
             except Exception as e:  # e.g. IPC export refused by the driver
                 ok, why = False, f"alloc/export: {e!r}"
@@ -81,10 +84,21 @@ class P2PAllReduce:
             if not passed:
                 self.comm = None
                 self.reason = self.reason or "self-test mismatch"
+        self._probe = None
         if self.comm is not None:
-            from .watchdog import register_probe
+            from .watchdog import register_owner_probe
 
-            register_probe(f"p2p_allreduce@{id(self):x}", self.comm.host_error)
+            self._probe = register_owner_probe(
+                "p2p_allreduce", self, lambda o: o.comm.host_error() if o.comm is not None else 0)
+
+    def close(self):
+        """Release the IPC mappings and stop the watchdog reading this communicator's error word."""
+        from .watchdog import unregister_probe
+
+        if getattr(self, "_probe", None):
+            unregister_probe(self._probe)
+            self._probe = None
+        self.comm = None
 
     @property
     def ok(self) -> bool:

@@ -44,6 +44,33 @@ def unregister_probe(name: str):
     _PROBES.pop(name, None)
 
 
+def clear_probes():
+    """Forget every probe (end of a job inside a long-lived interpreter: tests, in-process restarts)."""
+    _PROBES.clear()
+
+
+_PROBE_SEQ = [0]
+
+
+def register_owner_probe(kind: str, owner, read: Callable[[object], int]) -> str:
+    """Register a probe that holds only a weak reference to ``owner``: it reads ``read(owner)`` while the
+    owner lives and unregisters itself once the owner is collected, so a torn-down communicator (and its
+    sticky error word) can neither be kept alive by the watchdog nor fire it later.  Returns the key
+    (unique per registration, unlike ``id()`` values, which the interpreter reuses)."""
+    import weakref
+
+    _PROBE_SEQ[0] += 1
+    key = f"{kind}#{_PROBE_SEQ[0]}"
+    ref = weakref.ref(owner, lambda _r, k=key: _PROBES.pop(k, None))
+
+    def probe() -> int:
+        o = ref()
+        return 0 if o is None else int(read(o))
+
+    _PROBES[key] = probe
+    return key
+
+
 def active() -> Optional["PeerWatchdog"]:
     return _ACTIVE
 
@@ -75,6 +102,7 @@ class PeerWatchdog:
         self._store = None
         self._step = -1
         self._step_t = time.monotonic()
+        self._done_marked = False
         self.failure: Optional[str] = None
 
     # ------------------------------------------------------------------ public
@@ -94,17 +122,26 @@ class PeerWatchdog:
             self._step = step
             self._step_t = time.monotonic()
 
-    def stop(self):
-        """Normal completion: mark this rank done (peers stop watching it) and end the thread."""
-        global _ACTIVE
-        self._stop.set()
-        if self._thread is not None:
-            self._thread.join(5 * self.interval_s + 1.0)
+    def mark_done(self):
+        """This rank completed normally: peers stop counting its heartbeat.  The thread keeps watching
+        the peers (shutdown() calls this BEFORE its final barrier, so a peer that dies while the others
+        wait there is still caught within ``dead_after_s``)."""
+        if self._done_marked:
+            return
+        self._done_marked = True
         try:
             if self._store is not None:
                 self._store.add(self._key("done", self.rank), 1)
         except Exception:
             pass
+
+    def stop(self):
+        """Normal completion: mark this rank done (peers stop watching it) and end the thread."""
+        global _ACTIVE
+        self.mark_done()
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(5 * self.interval_s + 1.0)
         if _ACTIVE is self:
             _ACTIVE = None
 

@@ -256,12 +256,14 @@ class FederatedClient(AbstractWorker):
 
     @property
     def x(self) -> torch.Tensor:
-        """Buffered, not yet uploaded examples (oldest first)."""
-        return self.ring_x.peek(len(self.ring_x))
+        """Buffered, not yet uploaded examples (oldest first): an independent copy.  The zero-copy view
+        of the ring (``ring_x.peek``) is for the internal fit path only; a later push / peek or a ring
+        growth would change a view under a caller that keeps it."""
+        return self.ring_x.peek(len(self.ring_x)).clone()
 
     @property
     def y(self) -> torch.Tensor:
-        return self.ring_y.peek(len(self.ring_y))
+        return self.ring_y.peek(len(self.ring_y)).clone()
 
     def num_examples(self) -> int:
         return len(self.ring_x)

@@ -84,3 +84,22 @@ def test_fedavg_device_engine_two_ranks_cpu():
     out = _last_json(p.stdout)
     assert out["engine"] == "device" and out["clients"] == 2 and out["rounds"] == 4
     assert out["test_accuracy"] > 0.3
+
+
+@pytest.mark.timeout(900)
+def test_resumed_job_matches_uninterrupted_job(tmp_path):
+    """a job killed mid-epoch and resumed from its last checkpoint trains on exactly the batches
+    of an uninterrupted job (the schedule is rebuilt from the original seed and the resumed job skips the
+    steps already taken), so both end with bit-identical weights."""
+    common = ["sync", "--model", "mlp_mnist", "--num-examples", "2048", "--batch", "64", "--epochs", "3",
+              "--device", "cpu"]
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    p = _run(["--nproc", "2"] + common + ["--save-dir", a])
+    assert p.returncode == 0, p.stderr[-3000:]
+    p = _run(["--nproc", "2", "--max-restarts", "1"] + common +
+             ["--save-dir", b, "--fault-kill-rank", "0", "--fault-kill-step", "25"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "[fault] rank 0 killed" in p.stderr and "exited with 17" in p.stderr
+    wa = open(os.path.join(a, "current", "weights.bin"), "rb").read()
+    wb = open(os.path.join(b, "current", "weights.bin"), "rb").read()
+    assert len(wa) > 0 and wa == wb

@@ -1,36 +1,37 @@
 """One-shot xGMI all-reduce (csrc/allreduce_p2p.hip, parallel/p2p.py) on a real MI355X.
 
-The GPU box has one GPU, so the ranks are two processes sharing cuda:0: the IPC export/import,
-the flag protocol, the double-buffered staging and graph capture are all exercised exactly as on an
-8-GPU node (only the transport under the peer loads differs: local HBM instead of xGMI).  The
-control plane is gloo (RCCL refuses two ranks on one device).
+On a node with a GPU per rank every rank gets its own device and the process group is RCCL, so the
+peer loads and flags cross xGMI (tests/mp_util.py).  On the one-GPU test box the ranks are processes
+sharing cuda:0: the IPC export/import, the flag protocol, the double-buffered staging and graph
+capture are all exercised exactly as on an 8-GPU node (only the transport under the peer loads
+differs: local HBM instead of xGMI), with a gloo control plane (RCCL refuses two ranks on one device).
 """
 import os
-import socket
 import tempfile
 
 import pytest
 import torch
 import torch.multiprocessing as mp
 
+from mp_util import free_port, init_rank
+
 pytestmark = pytest.mark.gpu
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return free_port()
 
 
 def _init(rank, world, port):
+    """cuda:rank + RCCL when the box has a GPU per rank, else ranks share cuda:0 over gloo (mp_util)."""
     import torch.distributed as dist
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    global DEV
+    DEV = init_rank(rank, world, port)
     return dist
+
+
+DEV = torch.device("cuda", 0)
 
 
 def _primitive_worker(rank, world, port, out_dir):
@@ -40,7 +41,7 @@ def _primitive_worker(rank, world, port, out_dir):
     p = P2PAllReduce(max_bytes=1 << 20, timeout_s=10.0)
     res = {"ok": p.ok, "reason": p.reason}
     if p.ok:
-        dev = torch.device("cuda", 0)
+        dev = DEV
         g = torch.Generator().manual_seed(7)
         base = torch.randn(world, 100_003, generator=g)
         # eager, with scale
@@ -84,7 +85,7 @@ def _timeout_worker(rank, world, port, out_dir):
     p = P2PAllReduce(max_bytes=64 << 10, timeout_s=0.5, self_test=False)
     flag = None
     if p.ok and rank == 0:
-        x = torch.ones(4096, device="cuda:0")
+        x = torch.ones(4096, device=DEV)
         p.all_reduce(x)  # rank 1 never joins
         # the host-mapped mirror shows the timeout while the kernel may still be running, with no HIP
         # call (this is what the watchdog thread polls)
@@ -109,7 +110,7 @@ def _trainer_worker(rank, world, port, out_dir):
     from distriflow_amd.models.zoo import build_model
     from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
 
-    dev = torch.device("cuda", 0)
+    dev = DEV
     net = build_model("lenet5", device=dev, seed=rank)  # different init: the broadcast must fix it
     data, labels = synthetic_mnist(4096, seed=3, device=dev)
     tr = DataParallelTrainer(net, lr=0.05, graph="full", allreduce="p2p")
@@ -168,7 +169,7 @@ def _fedavg_gpu_worker(rank, world, port, out_dir):
     from distriflow_amd.models.zoo import build_model
     from distriflow_amd.parallel.fedavg import FedAvgTrainer
 
-    dev = torch.device("cuda", 0)
+    dev = DEV
     data, labels = synthetic_mnist(8192, seed=3, device=dev)
     shard = non_iid_shards(labels, world, 5, seed=0)[rank].to(dev)
     B, rounds, local = 256, 10, 20
@@ -210,7 +211,7 @@ def _fedavg_average_worker(rank, world, port, out_dir):
     from distriflow_amd.models.zoo import build_model
     from distriflow_amd.parallel.fedavg import FedAvgTrainer
 
-    dev = torch.device("cuda", 0)
+    dev = DEV
     net = build_model("lenet5", device=dev, seed=0)
     tr = FedAvgTrainer(net, lr=0.1, local_steps=1, graph="none", allreduce="p2p")
     g = torch.Generator().manual_seed(100 + rank)

@@ -127,3 +127,57 @@ def test_progress_stall_and_clean_stop():
     time.sleep(1.0)
     wd2.stop()
     assert not seen
+
+
+@pytest.mark.timeout(60)
+def test_dropped_comm_with_sticky_error_does_not_fire_later_watchdog():
+    """a communicator torn down with its sticky error word set must neither stay alive in the
+    probe table nor make a later watchdog in the same interpreter exit a healthy job."""
+    import gc
+    import weakref
+
+    from distriflow_amd.parallel import watchdog as W
+
+    class FakeComm:  # a torn-down P2PComm / PSComm whose host error word stayed set
+        err = 1
+
+    c = FakeComm()
+    ref = weakref.ref(c)
+    key = W.register_owner_probe("fake_comm", c, lambda o: o.err)
+    assert key in W._PROBES
+    del c
+    gc.collect()
+    assert ref() is None, "the probe table kept the communicator alive"
+    assert key not in W._PROBES
+    store, port = _store()
+    seen = []
+    wd = W.PeerWatchdog(0, 2, dead_after_s=30.0, interval_s=0.05, port=port, prefix="t4", on_fail=seen.append).start()
+    store.add("t4/hb/1", 1)
+    time.sleep(0.5)
+    wd.stop()
+    assert not seen
+    # keys are unique per registration (id() values get reused)
+    a, b = FakeComm(), FakeComm()
+    ka = W.register_owner_probe("x", a, lambda o: 0)
+    kb = W.register_owner_probe("x", b, lambda o: 0)
+    assert ka != kb
+    W.clear_probes()
+    assert not W._PROBES
+
+
+@pytest.mark.timeout(60)
+def test_mark_done_keeps_watching_peers():
+    """shutdown() marks the rank done before its final barrier but keeps watching the peers until then."""
+    from distriflow_amd.parallel.watchdog import PeerWatchdog
+
+    store, port = _store()
+    seen = []
+    wd = PeerWatchdog(0, 2, dead_after_s=0.3, interval_s=0.05, port=port, prefix="t5", on_fail=seen.append).start()
+    store.add("t5/hb/1", 1)
+    wd.mark_done()
+    assert store.add("t5/done/0", 0) == 1
+    t0 = time.time()
+    while not seen and time.time() - t0 < 5:
+        time.sleep(0.02)
+    wd.stop()
+    assert seen and "peer rank 1" in seen[0]
