@@ -102,6 +102,7 @@ def main():
         sys.exit(_spawn_ranks(args.gpus))
 
     from distriflow_amd.data.dataset import DistriDataset
+    from distriflow_amd.diagnostics import active as diag_active, on as diag_on
     from distriflow_amd.data.synthetic import synthetic_cifar10, synthetic_mnist
     from distriflow_amd.models.zoo import build_model
     from distriflow_amd.parallel.comm import init_distributed, shutdown
@@ -151,7 +152,7 @@ def main():
     def timed(tr, steps):
         """W untimed warm-up steps, then ``steps`` timed ones between barrier + device syncs; max over ranks.
         The sync trainer replays its steps from multi-step hipGraphs (captured here, before timing)."""
-        multi = getattr(tr, "SUPPORTS_MULTISTEP", False) and os.environ.get("DISTRIFLOW_MULTISTEP", "1") != "0"
+        multi = getattr(tr, "SUPPORTS_MULTISTEP", False) and diag_on("multistep")
         # ranks time-sharing one device (rehearsals) must yield the GPU at graph boundaries: a long unrolled
         # graph whose one-shot all-reduce spins on a descheduled peer's flag runs at the hardware
         # scheduler's time-slice (measured: 4 ranks on one GPU, 0.48 -> 14.9 ms per step)
@@ -244,6 +245,8 @@ def main():
             out["async"] = async_rec
         if phases is not None:
             out["phases_ms_eager"] = phases
+        if diag_active():
+            out["diagnostics"] = diag_active()  # a diagnostic run: never a production number
         if args.json_extra:
             out["extra"] = {"final_loss": loss, "train_tflops": value * net.flops_per_example() / 1e12,
                             "capture_error": getattr(trainer, "capture_error", None)}

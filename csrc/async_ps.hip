@@ -31,18 +31,14 @@
 // u32 claimed_epoch[kPSMaxBatches].
 #include "common.h"
 #include "kernels.h"
+#include "ps_device.h"
 
 namespace dfa {
 namespace {
 
 constexpr int kPSBlock = 256;
 constexpr int kPSUnroll = 4;  // float4 loads in flight per thread per round
-// local scratch words (PSArgs::scratch, u32 index)
-constexpr int kPSPullDone = 0, kPSApplyDone = 1, kPSEpoch = 2, kPSDecision = 3, kPSLockedSeq = 4, kPSSlots = 64;
-
-__device__ __forceinline__ unsigned ld_acq(const unsigned* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
+__device__ __forceinline__ unsigned ld_acq(const unsigned* p) { return ps_ld_acq(p); }
 
 // Multi-workgroup snapshot.  Every workgroup copies its slice of the committed version's buffer between
 // two reads of the version word and records the version; the last workgroup to finish checks that all
@@ -65,69 +61,6 @@ __device__ void copy_slice(const float* __restrict__ src, float* __restrict__ ds
       const long long i = base + (long long)u * nt;
       if (i < hi4) d4[i] = v[u];
     }
-  }
-}
-
-// At-least-once FCFS dispatch (/root/reference/src/server/dataset.ts:47-67).  The shared cursor
-// (batch_ctr) walks the batch ids of the current dataset epoch round and round; a batch stays
-// incomplete until ps_apply ADMITS a gradient for it, so batches whose gradient was rejected as too
-// stale (or is still in flight) come round again on the next lap, and the epoch only advances
-// once every batch is complete.  Wave 0 of the block reads 64 completion words per remote round
-// trip, claims the first incomplete batch after the cursor and moves the cursor past the completed
-// ones it skipped.  Two claimers can land on the same incomplete batch near the end of an epoch;
-// the second gradient then counts as a duplicate (applied, not re-completed).
-__device__ void claim_microbatch(const PSArgs& a, int t, long long* s_bid) {
-  __shared__ unsigned long long s_c;
-  __shared__ unsigned s_e;
-  __shared__ int s_k;  // >= 0: claimed offset from the cursor; -1: chunk all complete; -2: finished
-  const long long nb = a.nbatches;
-  const int rounds = (int)((nb + 63) / 64) + 2;
-  for (int r = 0;; ++r) {
-    if (t == 0) {
-      s_c = __hip_atomic_fetch_add(a.batch_ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      s_e = __hip_atomic_load(a.sched, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    __syncthreads();
-    const unsigned e = s_e;
-    const unsigned long long c = s_c;
-    if (t < 64) {
-      int k;
-      if (a.max_epochs > 0 && e >= (unsigned)a.max_epochs) {
-        k = -2;
-      } else {
-        const long long j = (long long)((c + (unsigned long long)t) % (unsigned long long)nb);
-        const unsigned d = t < nb ? ld_acq(a.done_epoch + j) : 0xffffffffu;
-        const unsigned long long inc = __ballot(d < e + 1u);  // incomplete in epoch e
-        k = inc ? (int)__builtin_ctzll(inc) : (r + 1 >= rounds ? 0 : -1);
-      }
-      if (t == 0) s_k = k;
-    }
-    __syncthreads();
-    const int k = s_k;
-    if (k == -2) {
-      if (t == 0) *s_bid = -1;
-      return;
-    }
-    if (k >= 0) {
-      if (t == 0) {
-        const long long bb = (long long)((c + (unsigned long long)k) % (unsigned long long)nb);
-        if (k > 0) {  // move the shared cursor past the completed batches this claim stepped over
-          __hip_atomic_fetch_add(a.batch_ctr, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_fetch_add(a.sched_ctr + 2, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        const unsigned prev = __hip_atomic_exchange(a.claimed_epoch + bb, e + 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_SYSTEM);
-        if (prev == e + 1u)  // dispatched before in this epoch and not complete: a re-dispatch
-          __hip_atomic_fetch_add(a.sched_ctr + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        *s_bid = ((long long)e << 32) | bb;
-      }
-      return;
-    }
-    if (t == 0) {  // the whole 64-batch chunk is complete: skip it
-      __hip_atomic_fetch_add(a.batch_ctr, 63ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_fetch_add(a.sched_ctr + 2, 64ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    __syncthreads();  // s_c / s_e / s_k are rewritten by the next round
   }
 }
 
@@ -244,28 +177,6 @@ __global__ __launch_bounds__(kPSBlock) void ps_fetch_pull_kernel(PSArgs a) {
 // others wait for that decision on a local word tagged with this launch's epoch, apply their slice, and
 // the last workgroup to finish publishes version + 1 (releases the lock).  The grid is small (<= 64
 // workgroups), so all of it is resident and the decision wait cannot starve workgroup 0.
-// Completion accounting for an admitted gradient; runs in one thread while it holds the writer lock,
-// so every completion is serialised.  A gradient claimed in an older epoch, or for a batch another
-// worker already completed, is applied but counted as a duplicate.
-__device__ void complete_microbatch(const PSArgs& a, long long bid) {
-  const unsigned e = (unsigned)(bid >> 32);
-  const long long bb = bid & 0xffffffffLL;
-  const unsigned cur = __hip_atomic_load(a.sched, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (e != cur || ld_acq(a.done_epoch + bb) == e + 1u) {
-    __hip_atomic_fetch_add(a.sched_ctr + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return;
-  }
-  __hip_atomic_store(a.done_epoch + bb, e + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_fetch_add(a.sched_ctr + 0, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  const unsigned n = __hip_atomic_load(a.sched + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
-  if ((long long)n >= a.nbatches) {  // every batch of epoch e applied: next epoch
-    __hip_atomic_store(a.sched + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(a.sched, e + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  } else {
-    __hip_atomic_store(a.sched + 1, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
 __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
   const int t = threadIdx.x, b = blockIdx.x, G = gridDim.x;
   __shared__ unsigned s_dec;  // 1 = apply, 2 = stale (rejected), 3 = error

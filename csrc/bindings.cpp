@@ -861,6 +861,9 @@ void head_train_py(std::vector<torch::Tensor> w, std::vector<c10::optional<torch
 
 class P2PComm;
 static dfa::LLComm p2p_ll_args(const P2PComm& c);
+class PSComm;
+static dfa::PSArgs ps_lenet_args(const PSComm& c, const torch::Tensor& perm, const torch::Tensor& idx, double lr,
+                                 int64_t max_stale);
 
 // Whole-network LeNet-5 training step (csrc/lenet_fused.hip): fills the gradients of all ten
 // parameters and stats = [loss sum, correct].  x: uint8 dataset [nrows][28][28][1] read through idx,
@@ -879,7 +882,9 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
                     c10::optional<torch::Tensor> sgd_descs, c10::optional<torch::Tensor> idx_stream,
                     c10::optional<torch::Tensor> idx_cursor, c10::optional<torch::Tensor> idx_dst,
                     c10::optional<torch::Tensor> sgd_ticket, c10::optional<torch::Tensor> sgd_stage,
-                    const P2PComm* ll, int64_t exch_blocks, c10::optional<torch::Tensor> run_stats) {
+                    const P2PComm* ll, int64_t exch_blocks, c10::optional<torch::Tensor> run_stats,
+                    const PSComm* ps, c10::optional<torch::Tensor> ps_perm, c10::optional<torch::Tensor> ps_idx,
+                    double ps_lr, int64_t ps_max_stale) {
   TORCH_CHECK(conv.size() == 4 && conv_grads.size() == 4, "lenet: conv = [w1, b1, w2, b2]");
   TORCH_CHECK(dense_w.size() == 3 && dense_wt.size() == 3 && dense_b.size() == 3 && dense_gw.size() == 3 &&
                   dense_gb.size() == 3 && hT.size() == 3 && dzT.size() == 3,
@@ -1056,6 +1061,18 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
     r.ll = p2p_ll_args(*ll);
     TORCH_CHECK(r.ll.world > 1, "lenet: LL exchange needs world > 1");
     r.ll_on = 1;
+  }
+  if (ps != nullptr) {
+    TORCH_CHECK(r.sgd_on && !r.ll_on, "lenet: the parameter-server mode needs the fused update and no LL exchange");
+    TORCH_CHECK(r.sgd.mom == nullptr, "lenet: the parameter server applies plain SGD (no momentum)");
+    TORCH_CHECK(!(idx_stream.has_value() && idx_stream->defined()),
+                "lenet: the parameter server stages the next microbatch itself (no index stream)");
+    TORCH_CHECK(ps_perm.has_value() && ps_perm->defined() && ps_idx.has_value() && ps_idx->defined(),
+                "lenet: the parameter-server mode needs the microbatch table and the index buffer");
+    TORCH_CHECK(a.idx == reinterpret_cast<const long long*>(ps_idx->data_ptr()),
+                "lenet: the parameter server must stage into the batch index buffer the step reads");
+    r.ps = ps_lenet_args(*ps, *ps_perm, *ps_idx, ps_lr, ps_max_stale);
+    r.ps_on = 1;
   }
   TORCH_CHECK(exch_blocks >= 0 && exch_blocks <= 512, "lenet: exch_blocks out of range");
   r.exch_blocks = (int)exch_blocks;
@@ -1405,6 +1422,26 @@ class PSComm {
     a.max_stale = (int)max_stale;
     check_hip(dfa::ps_apply(a, cur_stream()), "ps_apply");
   }
+  // device view of this rank's counters [accepted, rejected, sum staleness, max staleness, torn, err,
+  // no-op steps, -] (int64): read back asynchronously by the trainer's callbacks
+  torch::Tensor stats_tensor() const {
+    return torch::from_blob(local_ + 64, {8}, torch::TensorOptions().dtype(torch::kLong).device(torch::kCUDA, dev_));
+  }
+  // launch arguments of the fused LeNet-5 reduce in parameter-server mode (lenet_train_py)
+  dfa::PSArgs lenet_args(const torch::Tensor& perm, const torch::Tensor& idx, double lr, int64_t max_stale) const {
+    dfa::PSArgs a = args();
+    need(perm, at::kLong, "ps perm");
+    need(idx, at::kLong, "ps idx");
+    TORCH_CHECK(perm.dim() == 2 && perm.size(1) == idx.numel() && idx.numel() % 2 == 0, "ps: perm [nbatches][B]");
+    TORCH_CHECK(nbatches_ == 0 || perm.size(0) == nbatches_, "ps: perm rows != scheduled nbatches");
+    a.perm = reinterpret_cast<const long long*>(perm.data_ptr());
+    a.idx = reinterpret_cast<long long*>(idx.data_ptr());
+    a.nbatches = perm.size(0);
+    a.B = (int)idx.numel();
+    a.lr = (float)lr;
+    a.max_stale = (int)max_stale;
+    return a;
+  }
   // [accepted, rejected, sum staleness, max staleness, torn retries, err, version, batches claimed]
   std::vector<int64_t> stats() const {
     unsigned long long h[8] = {0};
@@ -1462,6 +1499,11 @@ class PSComm {
   char* shared_ = nullptr;
   char* local_ = nullptr;
 };
+
+static dfa::PSArgs ps_lenet_args(const PSComm& c, const torch::Tensor& perm, const torch::Tensor& idx, double lr,
+                                 int64_t max_stale) {
+  return c.lenet_args(perm, idx, lr, max_stale);
+}
 
 }  // namespace
 
@@ -1607,7 +1649,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sgd_mom") = py::none(), py::arg("sgd_wbf") = py::none(), py::arg("sgd_hyper") = py::none(),
         py::arg("sgd_descs") = py::none(), py::arg("idx_stream") = py::none(), py::arg("idx_cursor") = py::none(),
         py::arg("idx_dst") = py::none(), py::arg("sgd_ticket") = py::none(), py::arg("sgd_stage") = py::none(),
-        py::arg("ll") = nullptr, py::arg("exch_blocks") = 0, py::arg("run_stats") = py::none());
+        py::arg("ll") = nullptr, py::arg("exch_blocks") = 0, py::arg("run_stats") = py::none(),
+        py::arg("ps") = nullptr, py::arg("ps_perm") = py::none(), py::arg("ps_idx") = py::none(),
+        py::arg("ps_lr") = 0.0, py::arg("ps_max_stale") = -1);
   m.def("lenet_blocks", [](int64_t B) { return dfa::lenet_blocks((int)B); });
   m.def("lenet_frag_bytes", []() { return (int64_t)dfa::lenet_frag_bytes(); });
   m.def("lenet_dense_part_floats", [](int64_t B) { return (int64_t)dfa::lenet_dense_part_floats((int)B); });
@@ -1636,6 +1680,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_schedule", &PSComm::set_schedule, py::arg("nbatches"), py::arg("max_epochs") = 0)
       .def("schedule_stats", &PSComm::schedule_stats)
       .def("done_epochs", &PSComm::done_epochs)
-      .def("copy_master", &PSComm::copy_master);
+      .def("copy_master", &PSComm::copy_master)
+      .def("stats_tensor", &PSComm::stats_tensor);
   dfa::register_runtime(m);
 }

@@ -17,6 +17,7 @@
 //            apply fuses relu' of a mask tensor into g = dy * (mask > 0).
 #include "common.h"
 #include "kernels.h"
+#include "diag.h"
 
 namespace dfa {
 
@@ -27,11 +28,10 @@ static bool bn_vec(int C) { return C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) =
 
 static int bn_rows_per_pass(int C, bool vec) { return 256 / (vec ? C / 8 : C); }
 
-// rows per thread of the statistics pass (default 16; DISTRIFLOW_BN_RPT overrides, read once)
+// rows per thread of the statistics pass (default 16; diagnostic bn_rpt, csrc/diag.h)
 static int bn_rows_per_thread() {
   static const int r = [] {
-    const char* e = getenv("DISTRIFLOW_BN_RPT");
-    const int v = e ? atoi(e) : 16;
+    const int v = diag_int("bn_rpt", 16);
     return v >= 1 && v <= 64 ? v : 16;
   }();
   return r;

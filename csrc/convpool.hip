@@ -30,6 +30,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "diag.h"
 
 #include <array>
 #include <map>
@@ -1391,16 +1392,12 @@ struct Sizing {
   size_t lds;
 };
 
-// Tuning overrides (measurement only): DISTRIFLOW_CP_WPC caps workgroups per CU, DISTRIFLOW_CP_MINIMGS
-// raises the images per group (fewer, longer-lived workgroups amortise the per-workgroup setup).
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : dflt;
-}
+// Tuning overrides (measurement only, csrc/diag.h): cp_wpc caps workgroups per CU, cp_minimgs raises
+// the images per group (fewer, longer-lived workgroups amortise the per-workgroup setup).
 
 static Sizing size_persistent(const void* kern, int B, size_t fixed, size_t per_img, size_t min_lds, int cap) {
-  static const int wpc_cap = max(1, env_int("DISTRIFLOW_CP_WPC", 8));
-  static const int min_imgs = max(1, env_int("DISTRIFLOW_CP_MINIMGS", 1));
+  static const int wpc_cap = max(1, diag_int("cp_wpc", 8));
+  static const int min_imgs = max(1, diag_int("cp_minimgs", 1));
   const int wpc = min(wpc_cap, blocks_per_cu(kern, 0));
   const size_t budget = (160 * 1024) / wpc;
   int fit = (int)max((size_t)1, (budget > fixed ? budget - fixed : 0) / per_img);

@@ -1,0 +1,29 @@
+// The one diagnostic switchboard of the native code: DISTRIFLOW_DIAG="name=value,name=value".
+//
+// Measurement aids only (A/B of kernel variants that were measured neutral or slower, tile-size
+// sweeps): production never sets DISTRIFLOW_DIAG, and every switch defaults to the shipped path.  Kept
+// in one place so that the alternative code paths are discoverable and documented (docs/RESULTS.md);
+// the Python side reads the same variable through distriflow_amd/diagnostics.py.
+//   igemm_fast=0    igemm64 without the FAST gather           igemm_splitk=0  igemm64 without split-K
+//   bn_rpt=N        BatchNorm statistics rows per thread      wgrad_wg=N      wgrad_tr workgroup target
+//   wgrad128=N      wgrad_tr 128x128 tile rows per step       cp_wpc=N        convpool workgroups per CU cap
+//   cp_minimgs=N    convpool images per workgroup floor
+#pragma once
+#include <cstdlib>
+#include <cstring>
+
+namespace dfa {
+
+inline int diag_int(const char* name, int dflt) {
+  const char* s = getenv("DISTRIFLOW_DIAG");
+  if (!s || !*s) return dflt;
+  const size_t n = strlen(name);
+  while (*s) {
+    while (*s == ',' || *s == ' ') ++s;
+    if (strncmp(s, name, n) == 0 && s[n] == '=') return atoi(s + n + 1);
+    while (*s && *s != ',') ++s;
+  }
+  return dflt;
+}
+
+}  // namespace dfa

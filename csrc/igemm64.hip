@@ -21,6 +21,7 @@
 //     the weights as the MFMA A operand so each lane stores 4 adjacent output channels at once
 #include "common.h"
 #include "kernels.h"
+#include "diag.h"
 
 namespace dfa {
 
@@ -678,10 +679,7 @@ static bool igemm64_fast_ok(const IGemmArgs& a, int mode) {
   if (mode == MODE_DIRECT || a.SC % 64 || a.K != a.KH * a.KW * a.SC || a.KH * a.KW > 32 || a.Kpad < a.K) return false;
   if (mode == MODE_DGRAD && a.stride != 1 && a.stride != 2) return false;
   if (a.OH <= 0 || a.OW <= 0 || a.M % (a.OH * a.OW)) return false;
-  static const bool off = [] {
-    const char* e = getenv("DISTRIFLOW_IGEMM_FAST");
-    return e && e[0] == '0';
-  }();
+  static const bool off = diag_int("igemm_fast", 1) == 0;
   if (off) return false;
   const long long sbytes = (long long)(a.M / (a.OH * a.OW)) * a.SH * a.SW * a.SC * 2;
   const long long wbytes = (long long)round_up(a.N, 16) * a.Kpad * 2;
@@ -752,10 +750,7 @@ hipError_t launch64_mode(const IGemmArgs& a, hipStream_t st) {
 }  // namespace
 
 long long igemm64_splitk_floats(const IGemmArgs& a, int mode) {
-  static const bool off = [] {
-    const char* e = getenv("DISTRIFLOW_IGEMM_SPLITK");
-    return e && e[0] == '0';
-  }();
+  static const bool off = diag_int("igemm_splitk", 1) == 0;
   if (off || !igemm64_supported(a, mode) || a.N <= 64) return 0;
   if ((long long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 512) return 0;  // 128 x 128 tiles: already filled
   const int s = splitk_for<64, 128>(a);

@@ -386,6 +386,13 @@ struct LeNetRedArgs {
   // exchanging workgroups (0 = one per slot); fewer when ranks time-share one GPU (each then owns up to
   // 8 slots round-robin), so that every rank's waiting workgroups fit on the chip at once
   int exch_blocks;
+  // asynchronous SGD against the device parameter server (requires sgd_on for the compute-copy layout):
+  // the gradient is applied to the SHARED master under the PS writer lock (staleness bound ps.max_stale,
+  // w <- w - ps.lr * g), the local master / bf16 copies / conv fragments are refreshed from the version
+  // just written (or, for a rejected gradient, the current one), and the next microbatch is claimed and
+  // staged: an async step is train + this launch (csrc/lenet_fused.hip, protocol csrc/ps_device.h)
+  int ps_on;
+  PSArgs ps;
 };
 // The reference CNN's conv block (csrc/kcnn_fused.hip): conv1 3x3x1->32 + ReLU, conv2 3x3x32->32 + ReLU,
 // 2x2 max-pool [+ folded dropout], input 28x28x1, in one forward and one backward launch (+ reduce).

@@ -29,6 +29,7 @@
 #include "lenet_frag.h"
 #include "ll_exchange.h"
 #include "optim_device.h"
+#include "ps_device.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -38,7 +39,9 @@ namespace dfa {
 namespace {
 
 constexpr int IMG = 8;     // images per workgroup
-constexpr int NT = 256;    // threads per workgroup
+constexpr int NT = 512;    // threads per workgroup: 8 waves, 2 workgroups per CU = 4 waves per SIMD
+constexpr int NW = NT / 64;
+constexpr int ccdiv(int a, int b) { return (a + b - 1) / b; }
 // LDS carve (bytes), every offset 16-byte aligned
 constexpr int XS_ELEMS = IMG * 1024 + 32;           // [8][32][32] padded input (+ tail pad)
 constexpr int OFF_XS = 0;
@@ -135,7 +138,7 @@ __device__ __forceinline__ void pool4(float a00, float a01, float a10, float a11
   if (!(best > 0.f)) { best = 0.f; code = 4; }
 }
 
-// Weight fragments of one dense GEMM for the tiles t = w + 4 tt this wave owns, loaded ahead of use so
+// Weight fragments of one dense GEMM for the tiles t = w + NW tt this wave owns, loaded ahead of use so
 // that the L2 latency of layer l + 1's weights hides behind layer l (W rows of 32 * KS elements).
 template <int KS, int NTW>
 struct DenseFrags {
@@ -146,7 +149,7 @@ __device__ __forceinline__ void dense_load(DenseFrags<KS, NTW>& f, const bf16* _
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int tt = 0; tt < NTW; ++tt) {
-    const int t = w + 4 * tt;
+    const int t = w + NW * tt;
     if (t < ntiles) {
       const bf16* wrow = W + (long long)(16 * t + i) * (32 * KS) + 8 * g;
 #pragma unroll
@@ -165,7 +168,7 @@ __device__ __forceinline__ void dense_fwd(const DenseFrags<KS, NTW>& f, const bf
   const bf16* arow = (i < IMG ? A + i * lda : zr) + 8 * g;
 #pragma unroll
   for (int tt = 0; tt < NTW; ++tt) {
-    const int t = w + 4 * tt;
+    const int t = w + NW * tt;
     if (t >= ntiles) break;
     const int n = 16 * t + i;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -208,7 +211,7 @@ __device__ __forceinline__ void dense_bwd(const DenseFrags<KS, NTW>& f, const bf
   const bf16* zrow = (i < IMG ? dZ + i * ldz : zr) + 8 * g;
 #pragma unroll
   for (int tt = 0; tt < NTW; ++tt) {
-    const int t = w + 4 * tt;
+    const int t = w + NW * tt;
     if (t >= ktiles) break;
     const int j = 16 * t + i;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -239,7 +242,7 @@ __device__ __forceinline__ void dense_bwd(const DenseFrags<KS, NTW>& f, const bf
   }
 }
 
-__global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
+__global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* Xs = reinterpret_cast<bf16*>(smem + OFF_XS);
   bf16* Xs1 = reinterpret_cast<bf16*>(smem + OFF_XS1);
@@ -371,7 +374,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
   LN_STAMP(2);
 
   // ---------------------------------------------------------------- phase B: conv2 + ReLU + pool
-  DenseFrags<13, 2> f1;  // dense-1 weights: L2 latency hidden behind conv2
+  DenseFrags<13, ccdiv(8, NW)> f1;  // dense-1 weights: L2 latency hidden behind conv2
   dense_load(f1, a.d1w, 8);
   {
     bf16x8 bw[7];
@@ -415,19 +418,19 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
       for (int r = 0; r < rows; ++r) dst[r] = H0[r * LD0 + k];
     }
   }
-  DenseFrags<4, 2> f2;
+  DenseFrags<4, ccdiv(6, NW)> f2;
   DenseFrags<3, 1> f3;
   dense_load(f2, a.d2w, 6);
   dense_load(f3, a.d3w, 1);
   dense_fwd(f1, H0, LD0, ZR, a.d1b, 120, true, H1, LD1, nullptr, a.h1T, a.ldt, r0, rows);
   __syncthreads();
-  DenseFrags<1, 2> g3;
-  DenseFrags<3, 2> g2;
+  DenseFrags<1, ccdiv(6, NW)> g3;
+  DenseFrags<3, ccdiv(8, NW)> g2;
   dense_load(g3, a.d3wt, 6);
   dense_load(g2, a.d2wt, 8);
   dense_fwd(f2, H1, LD1, ZR, a.d2b, 84, true, H2, LD2, nullptr, a.h2T, a.ldt, r0, rows);
   __syncthreads();
-  DenseFrags<4, 7> g1;  // dense-1 data-gradient weights: loads overlap dense-3 and the loss
+  DenseFrags<4, ccdiv(25, NW)> g1;  // dense-1 data-gradient weights: loads overlap dense-3 and the loss
   dense_load(g1, a.d1wt, 25);
   dense_fwd(f3, H2, LD2, ZR, a.d3b, 10, false, nullptr, 0, LG, nullptr, a.ldt, r0, rows);
   __syncthreads();
@@ -514,24 +517,25 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
 
   // ---------------------------------------------------------------- phase E: conv2 weight gradient
   // dW2[n][(tap, c)] = sum_m dC2[m][n] im2col(P1)[m][(tap, c)]: both operands by transposed reads;
-  // wave w owns the 16-column tiles T = w + 4k (taps 2T, 2T + 1); tap 25 is the bias column of ones.
+  // wave w owns the 16-column tiles T = w + NW k (taps 2T, 2T + 1); tap 25 is the bias column of ones.
   bf16x8 bd[15];  // conv2 data-gradient fragments for phase F, in flight during this phase
 #pragma unroll
   for (int s = 0; s < 15; ++s) bd[s] = frag[(FR_DG + s) * 64 + lane];
   {
     const int q = (lane & 15) >> 2, p = lane & 3;
-    int toff[4];
-    bool ones[4];
+    constexpr int KT = ccdiv(13, NW);  // column tiles per wave (13 tiles: taps 0..24 + the bias column)
+    int toff[KT];
+    bool ones[KT];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int tap = 2 * (w + 4 * k) + (p >> 1);
+    for (int k = 0; k < KT; ++k) {
+      const int tap = 2 * (w + NW * k) + (p >> 1);
       ones[k] = tap >= 25;
       toff[k] = tap < 25 ? ((tap / 5) * 14 + (tap - 5 * (tap / 5))) * 8 + 4 * (p & 1) : 0;
     }
-    const int ntile = w == 0 ? 4 : 3;
-    f32x4 acc[4];
+    const int ntile = (13 - w + NW - 1) / NW;
+    f32x4 acc[KT];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) acc[k] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < KT; ++k) acc[k] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 5
     for (int s = 0; s < 25; ++s) {
       const int mA = 32 * s + 8 * g + q;
@@ -539,7 +543,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
       const bf16* pb0 = P1 + (int)PX[mA] * 8;
       const bf16* pb1 = P1 + (int)PX[mA + 4] * 8;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < KT; ++k) {
         if (k < ntile) {
           const bf16x4 t0 = tr_read(ones[k] ? KO : pb0 + toff[k]);
           const bf16x4 t1 = tr_read(ones[k] ? KO : pb1 + toff[k]);
@@ -549,9 +553,9 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
     }
     // D[row = output channel 4g + r][col i = (tap 2T + (i >> 3), channel i & 7)]
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < KT; ++k) {
       if (k < ntile) {
-        const int T = w + 4 * k;
+        const int T = w + NW * k;
         const int tap = 2 * T + (i >> 3), c = i & 7;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -659,11 +663,24 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LeNetArgs a) {
         }
       }
     }
-    // cross-wave sum: D[row = channel 4g + r][col = tap 16T + i]
+    // cross-wave sum: D[row = channel 4g + r][col = tap 16T + i]; waves w and w + 4 share slot w & 3
+    // (the upper half writes, then the lower half adds in place: a [4][16][32] buffer for 8 waves)
+    if (w >= 4) {
 #pragma unroll
-    for (int T = 0; T < 2; ++T)
+      for (int T = 0; T < 2; ++T)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) RED[(w * 16 + 4 * g + r) * 32 + 16 * T + i] = acc[T][r];
+        for (int r = 0; r < 4; ++r) RED[((w & 3) * 16 + 4 * g + r) * 32 + 16 * T + i] = acc[T][r];
+    }
+    __syncthreads();
+    if (w < 4) {
+#pragma unroll
+      for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float* q = RED + (w * 16 + 4 * g + r) * 32 + 16 * T + i;
+          *q = (NW > 4 ? *q : 0.f) + acc[T][r];
+        }
+    }
     __syncthreads();
     for (int e = tid; e < 6 * 32; e += NT) {
       const int c = e >> 5, col = e & 31;
@@ -836,6 +853,159 @@ __device__ __forceinline__ void conv_apply(const LeNetRedArgs& a, int cb, float 
   }
 }
 
+// ---- asynchronous SGD against the device parameter server (LeNetRedArgs::ps_on) ------------------------
+// Decision codes: the gradient is admitted (apply + refresh from the new version), rejected as too stale
+// (refresh from the current version; the writer lock is held while the copies are read), the schedule
+// is finished (no-op), or a wait timed out (no-op, error bits set).
+constexpr unsigned kPSAccept = 1, kPSReject = 2, kPSFailed = 3, kPSFinished = 4;
+
+// Every exchanging workgroup (and the staging workgroup) learns this launch's decision.  Workgroup 0
+// takes the writer lock (seqlock CAS on the server's word), checks staleness = version_now -
+// version_pulled against the bound and completes the microbatch under the lock; the others wait for
+// the decision word tagged with this launch's epoch (local, agent scope: all of them are resident).
+__device__ void lenet_ps_decide(const LeNetRedArgs& a, unsigned* s_dec, unsigned* s_seq) {
+  const PSArgs& p = a.ps;
+  if (threadIdx.x == 0) {
+    const unsigned ep = __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const unsigned long long t0 = wall_clock64();
+    unsigned dec = kPSFailed, s = 0;
+    if (blockIdx.x == 0) {
+      const long long bid = *p.bid_out;
+      if (p.done_epoch != nullptr && bid < 0) {  // dataset finished: a no-op step (no lock taken)
+        dec = kPSFinished;
+        p.stats[6] += 1;
+      } else {
+        for (;;) {
+          s = ps_ld_acq(p.seq);
+          if (!(s & 1u)) {
+            unsigned expected = s;
+            if (__hip_atomic_compare_exchange_strong(p.seq, &expected, s + 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_SYSTEM)) {
+              const unsigned stale = (s >> 1) - *p.vpulled;
+              if ((int)stale <= p.max_stale || p.max_stale < 0) {
+                dec = kPSAccept;
+                p.stats[0] += 1;
+                p.stats[2] += stale;
+                if (stale > p.stats[3]) p.stats[3] = stale;
+                if (p.done_epoch != nullptr) complete_microbatch(p, bid);  // under the writer lock
+              } else {
+                dec = kPSReject;  // keep the lock until every workgroup has copied version s / 2
+                p.stats[1] += 1;
+              }
+              break;
+            }
+          }
+          if (wall_clock64() - t0 > (unsigned long long)p.timeout_ticks) {
+            atomicOr(p.stats + 5, 4ull);
+            if (p.herr) __hip_atomic_store(p.herr, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __hip_atomic_store(p.scratch + kPSLockedSeq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      for (;;) {
+        const unsigned d = __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if ((d >> 3) == ep) {
+          dec = d & 7u;
+          break;
+        }
+        if (wall_clock64() - t0 > 2ull * (unsigned long long)p.timeout_ticks) {
+          atomicOr(p.stats + 5, 8ull);
+          if (p.herr) __hip_atomic_store(p.herr, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s = __hip_atomic_load(p.scratch + kPSLockedSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *s_dec = dec;
+    *s_seq = s;
+  }
+  __syncthreads();
+}
+
+// One parameter element on the PS: w_new = w[v] - lr * g into buffer (v + 1) % 3 of the shared master
+// (admitted) or the current w[v] (rejected); either way the local master and its bf16 compute copies
+// become that version.  Returns the local weight.
+__device__ __forceinline__ float lenet_ps_elem(const LeNetRedArgs& a, const ParamDesc& d, int i, float g,
+                                               unsigned dec, unsigned seq) {
+  const PSArgs& p = a.ps;
+  const unsigned v = seq >> 1;
+  const long long off = d.off + i;
+  const float w = p.ps_w[(long long)(v % 3u) * p.nstride + off];
+  float wn = w;
+  if (dec == kPSAccept) {
+    wn = w - p.lr * g;
+    p.ps_w[(long long)((v + 1u) % 3u) * p.nstride + off] = wn;
+  }
+  a.sgd.master[off] = wn;
+  emit_copies(d, i, wn, a.sgd.wbf);
+  return wn;
+}
+
+__device__ __forceinline__ void dense_tile_ps(const LeNetRedArgs& a, int slot, float g, unsigned dec, unsigned seq) {
+  int tile = a.tile_of_block[slot];
+  int l = 0;
+  if (tile >= a.L[0].tiles) {
+    tile -= a.L[0].tiles;
+    l = 1;
+    if (tile >= a.L[1].tiles) {
+      tile -= a.L[1].tiles;
+      l = 2;
+    }
+  }
+  const LeNetDense& L = a.L[l];
+  const int tk = tile / ((L.N + 15) / 16), tn = tile - ((L.N + 15) / 16) * tk;
+  const int on = 16 * tn + (threadIdx.x >> 4), ok = 16 * tk + (threadIdx.x & 15);
+  if (on >= L.N || ok > L.K) return;
+  if (ok < L.K) L.gw[(long long)on * L.K + ok] = g;
+  else L.gb[on] = g;
+  lenet_ps_elem(a, a.sgd.d[4 + 2 * l + (ok == L.K ? 1 : 0)], ok < L.K ? on * L.K + ok : on, g, dec, seq);
+}
+
+__device__ __forceinline__ void conv_ps(const LeNetRedArgs& a, int cb, float g, unsigned dec, unsigned seq) {
+  const int p = cb * 64 + (threadIdx.x & 63);
+  if (p >= kLeNetConvParams) return;
+  float* dst = p < kLeNetPB1 ? a.g_w1 + p
+               : p < kLeNetPW2 ? a.g_b1 + (p - kLeNetPB1)
+               : p < kLeNetPB2 ? a.g_w2 + (p - kLeNetPW2)
+                               : a.g_b2 + (p - kLeNetPB2);
+  *dst = g;
+  const int di = p < kLeNetPB1 ? 0 : p < kLeNetPW2 ? 1 : p < kLeNetPB2 ? 2 : 3;
+  const int i = p - (di == 0 ? 0 : di == 1 ? kLeNetPB1 : di == 2 ? kLeNetPW2 : kLeNetPB2);
+  const float w = lenet_ps_elem(a, a.sgd.d[di], i, g, dec, seq);
+  const int wj = p < kLeNetPB1 ? p : (p >= kLeNetPW2 && p < kLeNetPB2) ? 150 + (p - kLeNetPW2) : -1;
+  if (wj >= 0) st_sc1(a.sgd.stage + wj, w);  // the next step's conv fragments are built from these
+}
+
+// Arrival of one of the nexch + 1 protocol workgroups (exchanging + staging): the last one publishes
+// version v + 1 (admitted) or releases the lock (rejected) and records the pulled version.
+__device__ void lenet_ps_arrive(const LeNetRedArgs& a, int arrivals, unsigned dec, unsigned seq) {
+  const PSArgs& p = a.ps;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this thread's shared-master stores visible system-wide
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(p.scratch + kPSApplyDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (unsigned)arrivals - 1) {
+      __hip_atomic_store(p.scratch + kPSApplyDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.scratch + kPSEpoch, __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT) + 1u,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // every workgroup's release happened before the unlock
+      if (dec == kPSAccept) {
+        *p.vpulled = (seq >> 1) + 1u;
+        __hip_atomic_store(p.seq, seq + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else if (dec == kPSReject) {
+        *p.vpulled = seq >> 1;
+        __hip_atomic_store(p.seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+}
+
 constexpr int kMaxSlotsPerBlock = 8;
 
 // Exchange workgroups [0, exch_blocks) own slots blockIdx.x + k * exch_blocks: all their slots' local
@@ -870,11 +1040,22 @@ __global__ void __launch_bounds__(RT, 8) lenet_reduce_kernel(LeNetRedArgs a) {
     }
     __syncthreads();
     int nconv_mine = 0;
+    __shared__ unsigned s_dec, s_seq;
+    if (a.ps_on) lenet_ps_decide(a, &s_dec, &s_seq);
+    const unsigned dec = a.ps_on ? s_dec : 0u, seq = a.ps_on ? s_seq : 0u;
 #pragma unroll 1
     for (int k = 0; k < kMaxSlotsPerBlock; ++k) {
       const int slot = blockIdx.x + k * nexch;
       if (slot >= nslot) break;
       const bool dense = slot < a.dense_tiles;
+      if (a.ps_on) {
+        if ((dense ? threadIdx.x < 256 : wid == 0) && (dec == kPSAccept || dec == kPSReject)) {
+          if (dense) dense_tile_ps(a, slot, keep[k][threadIdx.x], dec, seq);
+          else conv_ps(a, slot - a.dense_tiles, keep[k][threadIdx.x], dec, seq);
+        }
+        if (!dense) ++nconv_mine;
+        continue;
+      }
       if (dense ? threadIdx.x < 256 : wid == 0) {
         float v = keep[k][threadIdx.x];
         bool ok = true;
@@ -889,7 +1070,8 @@ __global__ void __launch_bounds__(RT, 8) lenet_reduce_kernel(LeNetRedArgs a) {
       }
       if (!dense) ++nconv_mine;
     }
-    if (a.sgd_on && nconv_mine > 0) {
+    if (a.ps_on) lenet_ps_arrive(a, nexch + 1, dec, seq);
+    if (a.sgd_on && nconv_mine > 0 && (!a.ps_on || dec == kPSAccept || dec == kPSReject)) {
       // the workgroup that applies the last conv slot rebuilds the next step's conv-weight fragments from
       // the staged new weights (write-through stores drained before the ticket, write-through loads
       // after it: csrc/bn.hip's gfx950 hand-off)
@@ -913,6 +1095,24 @@ __global__ void __launch_bounds__(RT, 8) lenet_reduce_kernel(LeNetRedArgs a) {
     return;
   }
   const int blk = blockIdx.x - nexch;
+  if (blk == 1 && a.ps_on) {
+    // async: once this launch's decision is known (the current microbatch is completed under the lock),
+    // claim the next microbatch FCFS on the server and stage its example indices
+    __shared__ unsigned s_dec, s_seq;
+    __shared__ long long s_bid;
+    lenet_ps_decide(a, &s_dec, &s_seq);
+    if (a.ps.done_epoch != nullptr) {
+      claim_microbatch(a.ps, threadIdx.x, &s_bid);
+    } else if (threadIdx.x == 0) {
+      s_bid = (long long)(__hip_atomic_fetch_add(a.ps.batch_ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) %
+                          (unsigned long long)(a.ps.nbatches > 0 ? a.ps.nbatches : 1));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *a.ps.bid_out = s_bid;
+    ps_stage_indices(a.ps, s_bid, threadIdx.x, RT);
+    lenet_ps_arrive(a, nexch + 1, s_dec, s_seq);
+    return;
+  }
   if (blk == 1) {  // fused update: stage the next step's batch indices, advance the cursor
     __shared__ long long nxt;
     if (threadIdx.x == 0) nxt = (*a.sgd.cursor + 1) % a.sgd.nsteps;
@@ -1006,7 +1206,13 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
     for (int k = 0; k < r.ll.world; ++k)
       if (!r.ll.bases[k]) return hipErrorInvalidValue;
   }
-  const int extra = (r.sgd_on && r.sgd.src) ? 1 : 0;  // the index-staging workgroup
+  if (r.ps_on) {
+    // async PS: every protocol workgroup must be resident at once (workgroup 0's decision is awaited)
+    if (!r.sgd_on || r.ll_on || r.sgd.src || !r.ps.seq || !r.ps.ps_w || !r.ps.vpulled || !r.ps.bid_out ||
+        !r.ps.stats || !r.ps.scratch || r.exch_blocks + 1 > 512 || r.sgd.mom)
+      return hipErrorInvalidValue;
+  }
+  const int extra = ((r.sgd_on && r.sgd.src) || r.ps_on) ? 1 : 0;  // the index-staging workgroup
   hipLaunchKernelGGL(lenet_reduce_kernel, dim3(r.exch_blocks + 1 + extra), dim3(RT), 0, st, r);
   return hipGetLastError();
 }

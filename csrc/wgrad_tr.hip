@@ -23,6 +23,7 @@
 //     tails read a 16-byte zero constant instead (address select: no load under a branch)
 #include "common.h"
 #include "kernels.h"
+#include "diag.h"
 
 namespace dfa {
 
@@ -225,10 +226,7 @@ hipError_t launch_wgrad_tr(WgradArgs a, float* ws, size_t ws_floats, hipStream_t
   const int Kt = a.K + (a.with_bias ? 1 : 0);
   const int tiles = cdiv(a.N, BN) * cdiv(a.K + (a.with_bias ? 8 : 0), BK);
   // about two workgroups per CU (73.7 KB of LDS each at BM = 64), each reducing >= 256 rows
-  static const int target = [] {
-    const char* e = getenv("DISTRIFLOW_WGRAD_WG");
-    return e ? atoi(e) : 512;
-  }();
+  static const int target = diag_int("wgrad_wg", 512);
   int splits = cdiv(target, tiles);
   splits = min(splits, cdiv(a.M, 256));
   splits = max(splits, 1);
@@ -252,10 +250,7 @@ bool wgrad_tr_supported(const WgradArgs& a, int mode) {
 }
 
 hipError_t wgrad_tr(const WgradArgs& a, float* ws, size_t ws_floats, hipStream_t st) {
-  static const int t128 = [] {
-    const char* e = getenv("DISTRIFLOW_WGRAD128");
-    return e ? atoi(e) : 32;
-  }();
+  static const int t128 = diag_int("wgrad128", 32);
   // 128 x 128 tiles at 32 rows per step, 3 workgroups per CU (170 VGPRs each: no spills)
   if (a.N >= 128 && t128 == 32) return launch_wgrad_tr<128, 128, 2, 2, 32, 3>(a, ws, ws_floats, st);
   if (a.N >= 128) return launch_wgrad_tr<128, 128, 2, 2>(a, ws, ws_floats, st);

@@ -1,0 +1,48 @@
+"""The one diagnostic switchboard: ``DISTRIFLOW_DIAG="name=value,name=value"``.
+
+Measurement aids only — A/B switches for engine variants that were measured (docs/RESULTS.md) and
+either lost or came out neutral, plus the escape hatches of the fused fast paths.  Production never
+sets ``DISTRIFLOW_DIAG``; every switch defaults to the shipped path.  The native kernels read the same
+variable (csrc/diag.h).  User-facing configuration (``DISTRIFLOW_BACKEND``, ``DISTRIFLOW_ALLREDUCE``,
+the watchdog timeouts, ``DISTRIFLOW_METRICS``, ``DISTRIFLOW_DEBUG_SYNC``) is not here: see config.py.
+
+Python switches (default in brackets):
+  lenet_fused [1]          whole-network LeNet-5 kernels (0: per-layer kernels)
+  lenet_fused_update [1]   the reduce launch applies the SGD update (0: separate optimizer launch)
+  async_fused [1]          async PS step = train + reduce/apply (0: pull / compute / apply launches)
+  kcnn_fused [1]           the reference CNN's conv block as one forward + one backward kernel
+  fold_dropout [1]         dropout folded into producer epilogues
+  multistep [1]            bench.py unrolls up to 64 steps per hipGraph (0: one replay per step)
+  wgrad_overlap [1]        ResNet weight gradients on a side stream
+  proj_overlap [1]         ResNet projection shortcut on a side stream
+  concurrent_backward [0]  head weight gradients on side streams (measured slower)
+  bn_epilogue [0]          BatchNorm statistics from the conv epilogue (measured neutral / slower)
+"""
+from __future__ import annotations
+
+import os
+
+_DEFAULTS = {"lenet_fused": 1, "lenet_fused_update": 1, "async_fused": 1, "kcnn_fused": 1, "fold_dropout": 1,
+             "multistep": 1, "wgrad_overlap": 1, "proj_overlap": 1, "concurrent_backward": 0, "bn_epilogue": 0}
+
+
+def diag(name: str) -> int:
+    """Value of switch ``name`` (its documented default unless DISTRIFLOW_DIAG overrides it)."""
+    if name not in _DEFAULTS:
+        raise KeyError(f"unknown diagnostic switch {name!r}")
+    spec = os.environ.get("DISTRIFLOW_DIAG", "")
+    for item in spec.split(","):
+        k, _, v = item.strip().partition("=")
+        if k == name and v:
+            return int(v)
+    return _DEFAULTS[name]
+
+
+def on(name: str) -> bool:
+    return diag(name) != 0
+
+
+def active() -> dict:
+    """Every switch set away from its default (recorded by bench.py so a diagnostic run is never
+    mistaken for a production number)."""
+    return {k: diag(k) for k in _DEFAULTS if diag(k) != _DEFAULTS[k]}

@@ -328,6 +328,8 @@ def run_async_device(args) -> dict:
     tr.bind_dataset(x, y, B, scale=1.0 / 255.0 if x.dtype == torch.uint8 else 1.0)
     # one table row per microbatch id of an epoch; at-least-once dispatch per epoch on the device
     tr.bind_schedule(epoch_permutations(n, B, nb, dev, seed=args.seed), epochs=args.epochs)
+    # per-replay JSONL through the trainer callbacks (device counters, read back asynchronously)
+    tr.on_upload(lambda st: log.metric(event="upload", **st))
     faults = Faults(args, rank)
     cap = 4 * nb * args.epochs + 64  # a healthy run ends long before: every claim is a real step
     t0 = time.perf_counter()
@@ -342,6 +344,7 @@ def run_async_device(args) -> dict:
         if steps >= cap:
             raise RuntimeError(f"async PS did not finish {args.epochs} epochs in {steps} steps: {tr.ps_stats()}")
     torch.cuda.synchronize(dev)
+    tr.flush_callbacks()
     el = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -355,6 +358,7 @@ def run_async_device(args) -> dict:
         out = dict(mode="async", engine="device", world=world, steps_per_rank=steps,
                    images_per_s=world * steps * B / max(el, 1e-9), last_loss=float(st[0]) / B,
                    eval_loss=float(loss), eval_accuracy=float(acc), max_staleness_bound=args.max_staleness,
+                   capture_warmup=tr.capture_warmup if tr.graph_mode == "full" else 0, step=tr.step_launches,
                    **tr.ps_stats())
         log.metric(event="async_done", **out)
         print(json.dumps(out), flush=True)

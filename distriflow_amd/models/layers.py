@@ -24,6 +24,7 @@ from typing import Optional
 import torch
 
 from .. import ops
+from ..diagnostics import on as diag_on
 from .params import ParamSpec, primary_kpad
 
 
@@ -226,7 +227,7 @@ class Conv2D(Layer):
         # BatchNorm statistics from the forward epilogue (csrc/igemm64.hip bn_part): row tiles of the launch
         self._bn_ntm = 0
         if (torch.device(device).type == "cuda" and not self.relu
-                and os.environ.get("DISTRIFLOW_BN_EPILOGUE", "0") != "0"):
+                and diag_on("bn_epilogue")):
             H, W, C = self.in_shape
             OH, OW, N = self.out_shape
             kpad = primary_kpad_of(self)

@@ -17,6 +17,7 @@ import os
 import torch
 
 from .. import ops
+from ..diagnostics import on as diag_on
 from .layers import (Activation, BatchNorm, Conv2D, ConvPoolGemm, Dense, Dropout, Flatten, FusedConvPool,
                      KerasConvBlock, Layer, MaxPooling2D,
                      ResidualBlock)
@@ -70,8 +71,8 @@ class Net:
         self._bound_B = None
         self.graphs: dict = {}
         # side streams for weight gradients that run concurrently with the data-gradient chain
-        # measured: cross-stream joins cost more than the overlap wins (LeNet-5); DISTRIFLOW_CONCURRENT_BACKWARD=1 on
-        self.concurrent_backward = os.environ.get("DISTRIFLOW_CONCURRENT_BACKWARD", "0") == "1"
+        # measured: cross-stream joins cost more than the overlap wins (LeNet-5); DISTRIFLOW_DIAG=concurrent_backward=1 on
+        self.concurrent_backward = diag_on("concurrent_backward")
         self._side = [torch.cuda.Stream(device=self.device) for _ in range(3)] if self.is_gpu else []
 
     # ------------------------------------------------------------------ planning / fusion
@@ -123,7 +124,7 @@ class Net:
         if self.fuse:
             execd = self._fuse_conv_pool(execd)
             if (self.is_gpu and len(execd) >= 2 and isinstance(execd[1], ConvPoolGemm) and ops.kcnn_supported()
-                    and os.environ.get("DISTRIFLOW_KCNN_FUSED", "1") != "0"
+                    and diag_on("kcnn_fused")
                     and KerasConvBlock.matches(execd[0], execd[1].conv)):
                 execd = [KerasConvBlock(execd[0], execd[1].conv, execd[1].pool)] + execd[2:]
         last = execd[-1]
@@ -143,7 +144,7 @@ class Net:
         # its own backward can skip re-reading its output as the mask (ResNet blocks / BatchNorm+ReLU)
         for j, l in enumerate(execd):
             l.grad_premasked = bool(l.relu and j + 1 < len(execd) and execd[j + 1].in_relu)
-        if self.fuse and self.is_gpu and os.environ.get("DISTRIFLOW_FOLD_DROPOUT", "1") != "0":
+        if self.fuse and self.is_gpu and diag_on("fold_dropout"):
             execd = self._fold_dropout(execd)
         self.exec_layers = execd
         self.output_shape = shape
@@ -153,10 +154,10 @@ class Net:
     def _plan_lenet(self, execd) -> bool:
         """True when the executed graph is exactly LeNet-5 (conv5x5x6 'same' + relu + pool, conv5x5x16 +
         relu + pool, dense 120 relu, 84 relu, 10) on the GPU: the whole training step then runs as
-        two launches (csrc/lenet_fused.hip).  ``DISTRIFLOW_LENET_FUSED=0`` keeps the per-layer kernels."""
+        two launches (csrc/lenet_fused.hip).  ``DISTRIFLOW_DIAG=lenet_fused=0`` keeps the per-layer kernels."""
         import os
 
-        if not self.is_gpu or os.environ.get("DISTRIFLOW_LENET_FUSED", "1") == "0" or not ops.lenet_supported():
+        if not self.is_gpu or not diag_on("lenet_fused") or not ops.lenet_supported():
             return False
         if self.final_act == "sigmoid":  # the fused kernel trains softmax cross-entropy
             return False
@@ -360,7 +361,7 @@ class Net:
         self.backward(self.dlogits, grad_ready)
         return stats
 
-    def compute_gradients_and_update(self, x, labels, index_stream=None, ll=None, run_stats=None):
+    def compute_gradients_and_update(self, x, labels, index_stream=None, ll=None, run_stats=None, ps=None):
         """Fused LeNet-5 step: gradients AND the SGD update (with the store's device hyper-parameters)
         in the step's two launches (the reduce kernel applies the update and rebuilds the next step's
         weight fragments; ``index_stream`` = (stream, cursor, dst) is advanced by it too).  Same
@@ -381,9 +382,14 @@ class Net:
             sgd.update(idx_stream=index_stream[0], idx_cursor=index_stream[1], idx_dst=index_stream[2])
         if ll is not None:
             sgd["ll"] = ll
+        if ll is not None or ps is not None:
             sgd["exch_blocks"] = int(getattr(self, "lenet_exch_blocks", 0))
         if run_stats is not None:
             sgd["run_stats"] = run_stats
+        if ps is not None:
+            # asynchronous SGD: the reduce launch applies the gradient to the parameter server's shared
+            # master (dict: ps, ps_perm, ps_idx, ps_lr, ps_max_stale; parallel/async_ps.py)
+            sgd.update(ps)
         stats = self._compute_gradients_lenet(x, labels, None, sgd=sgd)
         st.lenet_state = "fresh"  # the reduce kernel rebuilt the fragments from the new weights
         return stats
@@ -416,18 +422,18 @@ class Net:
 
     def _wgrad_side(self, layer):
         """Side stream for ``layer``'s weight gradients (ResNet blocks on the GPU), else None.
-        ``DISTRIFLOW_WGRAD_OVERLAP=0`` keeps them in order on the main stream."""
+        ``DISTRIFLOW_DIAG=wgrad_overlap=0`` keeps them in order on the main stream."""
         if not isinstance(layer, ResidualBlock):
             return None
-        on = self.is_gpu and os.environ.get("DISTRIFLOW_WGRAD_OVERLAP", "1") != "0"
+        on = self.is_gpu and diag_on("wgrad_overlap")
         return self._side[0] if on else None
 
     def _proj_side(self, layer):
         """Stream for a ResNet block's projection shortcut branch (joined inside the block), else None.
-        ``DISTRIFLOW_PROJ_OVERLAP=0`` keeps it in order."""
+        ``DISTRIFLOW_DIAG=proj_overlap=0`` keeps it in order."""
         if not (isinstance(layer, ResidualBlock) and layer.proj is not None and self.is_gpu):
             return None
-        return self._side[1] if os.environ.get("DISTRIFLOW_PROJ_OVERLAP", "1") != "0" else None
+        return self._side[1] if diag_on("proj_overlap") else None
 
     def _compute_gradients_head(self, x, labels, grad_ready):
         """Body layers one by one, then the fused dense head (2 launches: forward + CE + backward data

@@ -345,8 +345,11 @@ ACT_KINDS = {"linear": 0, None: 0, "relu": 1, "relu6": 2, "sigmoid": 3, "tanh": 
 def _act_ref(kind: int, x):
     import torch.nn.functional as F
 
-    f = {0: lambda v: v, 1: F.relu, 2: lambda v: v.clamp(0.0, 6.0), 3: torch.sigmoid, 4: torch.tanh, 5: F.elu,
-         6: F.selu, 7: F.softplus, 8: F.softsign, 9: lambda v: (0.2 * v + 0.5).clamp(0.0, 1.0), 10: F.silu,
+    def clip(v, lo, hi):  # TensorFlow's gradient of a clipped activation: zero AT the corners too
+        return torch.where((v > lo) & (v < hi), v, v.clamp(lo, hi).detach())
+
+    f = {0: lambda v: v, 1: F.relu, 2: lambda v: clip(v, 0.0, 6.0), 3: torch.sigmoid, 4: torch.tanh, 5: F.elu,
+         6: F.selu, 7: F.softplus, 8: F.softsign, 9: lambda v: clip(0.2 * v + 0.5, 0.0, 1.0), 10: F.silu,
          11: torch.exp}[kind]
     return f(x)
 

@@ -11,14 +11,16 @@ This is the throughput path.  The message-level roles (``parallel/server.py``/``
 the reference's protocol and callbacks.  On one MI355X node the server state is a single IPC-exported
 buffer in the server rank's HBM: a seqlock version word, the FCFS microbatch counter and the fp32
 master weights.  Every rank maps it over xGMI (csrc/async_ps.hip).  A worker step is a bare hipGraph
-replay of four device stages, with no host round trip:
+replay of device stages, with no host round trip.
 
-  1. ``ps_fetch_pull``: claim the next microbatch id (remote atomic), stage its example indices, and
-     copy a consistent weight snapshot together with its version;
-  2. re-emit the bf16 compute copies;
-  3. forward, loss and backward (the same fused kernels as the synchronous trainer);
-  4. ``ps_apply``: under the writer lock, reject the gradient if ``version_now - version_pulled >
-     max_staleness``, otherwise ``w -= lr * g`` on the shared master and publish ``version + 1``.
+Fused LeNet-5 (the headline model): TWO launches per step, the same shape as a synchronous step.
+  1. the whole-network train kernel (forward, loss, backward of the claimed microbatch);
+  2. the reduce kernel in parameter-server mode (csrc/lenet_fused.hip): it reduces the gradient, takes
+     the writer lock, rejects it if ``version_now - version_pulled > max_staleness`` or applies
+     ``w -= lr * g`` to the shared master, refreshes the local master / bf16 copies / conv fragments
+     from the version it just wrote (or the current one), publishes ``version + 1``, and claims and
+     stages the next microbatch.  A one-time prologue (pull + refresh) precedes the first step.
+Other models: ``ps_fetch_pull`` (claim + snapshot), bf16 refresh, the model's kernels, ``ps_apply``.
 
 Ranks never wait for each other except for the short writer lock.  A slow rank only makes its own
 gradients staler, which the bound then rejects.
@@ -31,6 +33,7 @@ import torch
 import torch.distributed as dist
 
 from .. import native
+from ..diagnostics import on as diag_on
 from .data_parallel import DataParallelTrainer
 
 
@@ -68,6 +71,21 @@ class AsyncPSTrainer(DataParallelTrainer):
             err = e
         self._agree(err, "IPC open")
         self._perm = None
+        # fused LeNet-5: the reduce launch is the parameter server's apply (2 launches per step)
+        import os
+
+        self.fused_ps = (bool(getattr(net, "lenet_fused", False)) and net.store.lenet_frag is not None
+                         and diag_on("async_fused"))
+        if self.fused_ps:
+            self.capture_warmup = 0  # a warm-up step would apply real gradients to the shared master
+            # ranks that time-share one GPU: fewer protocol workgroups per rank (each owning several
+            # slots), so every rank's workgroups waiting for its lock decision fit on the chip beside the
+            # lock holder's (one rank per GPU: one workgroup per slot, all resident)
+            ndev = max(1, torch.cuda.device_count())
+            share = -(-self.world // ndev) if ndev < self.world else 1
+            net.lenet_exch_blocks = 0 if share == 1 else max(48, 256 // share)
+        self._primed = False
+        self._ps_stats_dev = self.ps.stats_tensor()  # device view of this rank's PS counters (callbacks)
         from .watchdog import register_owner_probe
 
         register_owner_probe("async_ps", self, lambda o: o.ps.host_error())
@@ -96,20 +114,44 @@ class AsyncPSTrainer(DataParallelTrainer):
         self.ps.set_schedule(int(perm.shape[0]), self.epochs)
         self._graph = None
         self._multi, self._multi_u = None, 0
+        self._primed = False
 
     def _has_schedule(self) -> bool:
         return self._perm is not None
 
     # ------------------------------------------------------------------ one step
+    def _prime(self):
+        """Fused path prologue (eager, once per schedule): claim the first microbatch and pull the master
+        into the local weights and compute copies; every later step's reduce launch does both itself."""
+        if self.fused_ps and not self._primed:
+            self.ps.fetch_pull(self.net.store.master, self._perm, self.idx)
+            self.net.store.refresh_compute()
+            self._primed = True
+
     def _gather(self):
+        if self.fused_ps:
+            super()._gather()  # labels through the staged indices (no launch)
+            return
         self.ps.fetch_pull(self.net.store.master, self._perm, self.idx)
         self.net.store.refresh_compute()
         super()._gather()
 
     def _step_body(self, x, y):
+        if self.fused_ps:
+            ps = dict(ps=self.ps, ps_perm=self._perm, ps_idx=self.idx, ps_lr=float(self.lr),
+                      ps_max_stale=int(self.max_staleness))
+            return self.net.compute_gradients_and_update(x, y, None, run_stats=self.run_stats, ps=ps)
         stats = self.net.compute_gradients(x, y)
         self.ps.apply(self.net.store.grad, self.lr, self.max_staleness)
         return stats
+
+    @property
+    def step_launches(self) -> str:
+        return "train+reduce/ps-apply/refresh/claim" if self.fused_ps else "pull+refresh+compute+ps-apply"
+
+    def prepare_run(self, n: int):
+        self._prime()
+        super().prepare_run(n)
 
     def _capture_with_fallback(self):
         try:
@@ -125,15 +167,32 @@ class AsyncPSTrainer(DataParallelTrainer):
     def step(self):
         if self._perm is None:
             raise RuntimeError("bind_schedule() first")
+        self._prime()
         self.steps += 1
         if self.graph_mode == "none":
             self._gather()
-            return self._step_body(self.xb, self.yb)
-        if self._graph is None:
-            self._capture_with_fallback()
+            st = self._step_body(self.xb, self.yb)
+        else:
             if self._graph is None:
-                return self._last_eager
-        return self._replay()
+                self._capture_with_fallback()
+            st = self._last_eager if self._graph is None else self._replay()
+        self._after_replay(1)
+        return st
+
+    # ------------------------------------------------------------------ callbacks
+    def _cb_sources(self) -> list:
+        # + the parameter server's local counters [accepted, rejected, sum staleness, max staleness, ...]
+        return [self.run_stats, self._ps_stats_dev]
+
+    def _cb_stats(self, cur, last, v0, v1, n) -> dict:
+        """Per replay: this rank's admitted / rejected gradients and their staleness, the loss of the
+        steps, and the versions it published (a version = one admitted gradient anywhere in the job)."""
+        st = super()._cb_stats(cur, last, v0, v1, n)
+        acc, rej = cur[1][0] - last[1][0], cur[1][1] - last[1][1]
+        st.update(accepted=int(acc), rejected=int(rej),
+                  mean_staleness=(cur[1][2] - last[1][2]) / acc if acc else 0.0, max_staleness=int(cur[1][3]),
+                  updates=int(acc))
+        return st
 
     # ------------------------------------------------------------------ state
     def ps_stats(self) -> dict:

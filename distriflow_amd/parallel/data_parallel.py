@@ -27,6 +27,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
+from ..diagnostics import on as _diag_on
 
 
 class DataParallelTrainer:
@@ -185,9 +186,12 @@ class DataParallelTrainer:
 
     # the step contains the gradient all-reduce (subclasses that exchange gradients otherwise say False)
     _step_all_reduces = True
+    # eager warm-up steps before a capture (allocator / communicators / code objects); their effect on the
+    # engine state is undone.  A subclass whose step mutates state outside the engine sets 0.
+    capture_warmup = 3
 
     # single rank + fused LeNet-5: the reduce kernel applies the update itself (no optimizer launch)
-    fused_update = os.environ.get("DISTRIFLOW_LENET_FUSED_UPDATE", "1") != "0"
+    fused_update = _diag_on("lenet_fused_update")
 
     def _step_body(self, x, y):
         hook = self._grad_ready if (self.overlap and self.world > 1) else None
@@ -296,7 +300,7 @@ class DataParallelTrainer:
         cursor = self._index_stream[1].clone() if self._index_stream is not None else None
         idx0 = self.idx.clone()
         with torch.cuda.stream(s):
-            for _ in range(3):
+            for _ in range(self.capture_warmup):
                 self._gather()
                 self._step_body(self.xb, self.yb)
         torch.cuda.current_stream(net.device).wait_stream(s)
@@ -448,44 +452,56 @@ class DataParallelTrainer:
     onNewVersion = on_new_version
     onUpload = on_upload
 
+    def _cb_sources(self) -> list:
+        """Device tensors read back per replay for the callbacks (subclasses add their counters)."""
+        return [self.run_stats]
+
+    def _cb_stats(self, cur: list, last: list, v0: int, v1: int, n: int) -> dict:
+        """The on_upload payload of one replay from the read-back sources (cumulative device counters:
+        this replay = cur - last)."""
+        dl, dc, du = (cur[0][k] - last[0][k] for k in range(3))
+        images = n * self.B
+        return {"version": v1, "steps": n, "images": images * self.world, "loss": dl / max(images, 1),
+                "accuracy": dc / max(images, 1), "updates": int(round(du)), "rank": self.rank, "world": self.world}
+
     def _after_replay(self, nsteps: int):
-        """Queue an asynchronous read-back of the device run statistics after a replay of ``nsteps`` steps
-        (a copy into pinned memory behind the replay, outside the captured step) and fire the callbacks of
+        """Queue an asynchronous read-back of the device counters after a replay of ``nsteps`` steps (a
+        copy into pinned memory behind the replay, outside the captured step) and fire the callbacks of
         every replay whose copy has landed.  Nothing happens without registered callbacks."""
         if not (self._version_cbs or self._upload_cbs):
             return
         v1 = self.steps
+        srcs = self._cb_sources()
         if self.net.is_gpu:
             if self._cb_ring is None:
-                self._cb_ring = [torch.empty(4, dtype=torch.float32, pin_memory=True) for _ in range(16)]
+                self._cb_ring = [[torch.empty(t.numel(), dtype=t.dtype, pin_memory=True) for t in srcs]
+                                 for _ in range(16)]
                 self._cb_next = 0
             if len(self._cb_pending) >= len(self._cb_ring):
                 self._drain_callbacks(block_one=True)
-            buf = self._cb_ring[self._cb_next]
+            bufs = self._cb_ring[self._cb_next]
             self._cb_next = (self._cb_next + 1) % len(self._cb_ring)
-            buf.copy_(self.run_stats, non_blocking=True)
+            for b, t in zip(bufs, srcs):
+                b.copy_(t.reshape(-1), non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
-            self._cb_pending.append((ev, buf, v1 - nsteps, v1, nsteps))
+            self._cb_pending.append((ev, bufs, v1 - nsteps, v1, nsteps))
         else:
-            self._cb_pending.append((None, self.run_stats.clone(), v1 - nsteps, v1, nsteps))
+            self._cb_pending.append((None, [t.reshape(-1).clone() for t in srcs], v1 - nsteps, v1, nsteps))
         self._drain_callbacks()
 
     def _drain_callbacks(self, block: bool = False, block_one: bool = False):
         while self._cb_pending:
-            ev, buf, v0, v1, n = self._cb_pending[0]
+            ev, bufs, v0, v1, n = self._cb_pending[0]
             if ev is not None and not ev.query():
                 if not (block or block_one):
                     return
                 ev.synchronize()
             self._cb_pending.pop(0)
-            cur = buf.tolist()
-            last = self._cb_last or [0.0, 0.0, 0.0, 0.0]
+            cur = [b.tolist() for b in bufs]
+            last = self._cb_last or [[0] * len(c) for c in cur]
             self._cb_last = cur
-            dl, dc, du = cur[0] - last[0], cur[1] - last[1], cur[2] - last[2]
-            images = n * self.B
-            st = {"version": v1, "steps": n, "images": images * self.world, "loss": dl / max(images, 1),
-                  "accuracy": dc / max(images, 1), "updates": int(round(du)), "rank": self.rank, "world": self.world}
+            st = self._cb_stats(cur, last, v0, v1, n)
             for cb in self._version_cbs:
                 cb(v0, v1)
             for cb in self._upload_cbs:

@@ -262,10 +262,10 @@ def test_per_layer_numerics_against_cpu(name, B, monkeypatch):
     from distriflow_amd.models.net import Net
     from distriflow_amd.models.zoo import MODELS
 
-    monkeypatch.setenv("DISTRIFLOW_LENET_FUSED", "0")  # the per-layer kernels (the fused one: test_lenet_fused_gpu)
-    # layer-for-layer pairing with the CPU plan (folded dropouts: tests/test_dropout_fold_gpu.py)
-    monkeypatch.setenv("DISTRIFLOW_FOLD_DROPOUT", "0")
-    monkeypatch.setenv("DISTRIFLOW_KCNN_FUSED", "0")  # the fused conv block: tests/test_kcnn_fused_gpu.py
+    # per-layer kernels (the fused LeNet-5: test_lenet_fused_gpu; the fused conv block:
+    # tests/test_kcnn_fused_gpu.py) and layer-for-layer pairing with the CPU plan (folded dropouts:
+    # tests/test_dropout_fold_gpu.py)
+    monkeypatch.setenv("DISTRIFLOW_DIAG", "lenet_fused=0,fold_dropout=0,kcnn_fused=0")
     g = build_model(name, device="cuda", seed=3)
     layers, shape = MODELS[name]()
     c = Net(layers, shape, device="cpu", name=name, seed=3, compute_dtype=torch.bfloat16)
@@ -325,7 +325,7 @@ def test_bn_statistics_from_conv_epilogue(monkeypatch):
     statistics of the conv's stored output."""
     from distriflow_amd.models.layers import ResidualBlock
 
-    monkeypatch.setenv("DISTRIFLOW_BN_EPILOGUE", "1")
+    monkeypatch.setenv("DISTRIFLOW_DIAG", "bn_epilogue=1")
     net = build_model("resnet18_cifar", device="cuda", seed=5)
     B = 16
     net.bind(B)

@@ -17,9 +17,9 @@ def _pair(monkeypatch, seed=3):
 
     f = build_model("keras_cnn", device=dev, seed=seed)
     assert isinstance(f.exec_layers[0], KerasConvBlock)
-    monkeypatch.setenv("DISTRIFLOW_KCNN_FUSED", "0")
+    monkeypatch.setenv("DISTRIFLOW_DIAG", "kcnn_fused=0")
     p = build_model("keras_cnn", device=dev, seed=seed)
-    monkeypatch.delenv("DISTRIFLOW_KCNN_FUSED")
+    monkeypatch.delenv("DISTRIFLOW_DIAG")
     assert not isinstance(p.exec_layers[0], KerasConvBlock)
     p.store.set_flat(f.store.master.clone())
     return f, p

@@ -31,8 +31,12 @@ ACTS = ["tanh", "sigmoid", "elu", "selu", "softplus", "softsign", "hard_sigmoid"
 
 def _torch_act(name, h):
     return {"tanh": torch.tanh, "sigmoid": torch.sigmoid, "elu": F.elu, "selu": F.selu, "softplus": F.softplus,
-            "softsign": F.softsign, "hard_sigmoid": lambda v: (0.2 * v + 0.5).clamp(0, 1), "swish": F.silu,
-            "relu6": lambda v: v.clamp(0, 6), "relu": F.relu, "linear": lambda v: v}[name](h)
+            "softsign": F.softsign, "hard_sigmoid": lambda v: _clip(0.2 * v + 0.5, 0, 1), "swish": F.silu,
+            "relu6": lambda v: _clip(v, 0, 6), "relu": F.relu, "linear": lambda v: v}[name](h)
+
+
+def _clip(v, lo, hi):  # TensorFlow's gradient of relu6 / hard_sigmoid is zero at the corners
+    return torch.where((v > lo) & (v < hi), v, v.clamp(lo, hi).detach())
 
 
 @pytest.mark.parametrize("act", ACTS)

@@ -103,3 +103,17 @@ def test_resumed_job_matches_uninterrupted_job(tmp_path):
     wa = open(os.path.join(a, "current", "weights.bin"), "rb").read()
     wb = open(os.path.join(b, "current", "weights.bin"), "rb").read()
     assert len(wa) > 0 and wa == wb
+
+
+@pytest.mark.timeout(600)
+def test_sync_metrics_jsonl_has_per_step_upload_records(tmp_path):
+    """The device engine's callbacks (DataParallelTrainer.on_upload) write one JSONL record per replay:
+    versions advance by the replay's steps and every record carries loss / accuracy (VERDICT r2 #7)."""
+    m = str(tmp_path / "m.jsonl")
+    p = _run(["--nproc", "2", "sync", "--model", "mlp_mnist", "--num-examples", "1024", "--batch", "64",
+              "--epochs", "1", "--device", "cpu", "--metrics", m])
+    assert p.returncode == 0, p.stderr[-3000:]
+    recs = [json.loads(l) for l in open(m)]
+    ups = [r for r in recs if r.get("event") == "upload" and r.get("rank") == 0]
+    assert [u["version"] for u in ups] == list(range(1, 9))  # 1024 / 64 / 2 ranks = 8 steps, one per replay
+    assert all(u["updates"] == 1 and u["world"] == 2 and 0.0 <= u["accuracy"] <= 1.0 for u in ups)

@@ -58,7 +58,7 @@ def test_fused_lenet_matches_per_layer_kernels(monkeypatch):
 
     B = 256
     g, _ = _nets(B)
-    monkeypatch.setenv("DISTRIFLOW_LENET_FUSED", "0")
+    monkeypatch.setenv("DISTRIFLOW_DIAG", "lenet_fused=0")
     p = build_model("lenet5", device="cuda", seed=3)
     assert not p.lenet_fused
     p.store.set_flat(g.store.master.clone())
