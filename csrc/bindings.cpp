@@ -881,7 +881,6 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
                     c10::optional<torch::Tensor> sgd_wbf, c10::optional<torch::Tensor> sgd_hyper,
                     c10::optional<torch::Tensor> sgd_descs, c10::optional<torch::Tensor> idx_stream,
                     c10::optional<torch::Tensor> idx_cursor, c10::optional<torch::Tensor> idx_dst,
-                    c10::optional<torch::Tensor> sgd_ticket, c10::optional<torch::Tensor> sgd_stage,
                     const P2PComm* ll, int64_t exch_blocks, c10::optional<torch::Tensor> run_stats,
                     const PSComm* ps, c10::optional<torch::Tensor> ps_perm, c10::optional<torch::Tensor> ps_idx,
                     double ps_lr, int64_t ps_max_stale) {
@@ -957,7 +956,10 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
   need(conv_part, at::kFloat, "lenet conv_part");
   need(loss_part, at::kFloat, "lenet loss_part");
   need(stats, at::kFloat, "lenet stats");
-  TORCH_CHECK(conv_part.numel() >= (int64_t)dfa::kLeNetConvStride * nblk, "lenet: conv_part too small");
+  const int64_t part_ld = (nblk + 511) / 512 * 512;
+  TORCH_CHECK(conv_part.numel() >= (int64_t)dfa::kLeNetConvParams * part_ld,
+              "lenet: conv_part must hold [2572][round_up(nblocks, 512)] floats (zero initialised)");
+  a.part_ld = (int)part_ld;
   TORCH_CHECK(loss_part.numel() >= 2 * nblk && stats.numel() >= 2, "lenet: loss buffers too small");
   a.conv_part = conv_part.data_ptr<float>();
   a.loss_part = loss_part.data_ptr<float>();
@@ -978,6 +980,7 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
   dfa::LeNetRedArgs r{};
   (void)dense_part;  // kept in the signature; the dense gradients no longer need partials
   r.conv_part = a.conv_part;
+  r.part_ld = a.part_ld;
   r.loss_part = a.loss_part;
   r.stats = stats.data_ptr<float>();
   r.g_w1 = conv_grads[0].data_ptr<float>();
@@ -1011,15 +1014,11 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
   if (sgd_master.has_value() && sgd_master->defined()) {
     // single-rank fast path: the reduce kernel applies the SGD update (see LeNetSgd)
     need(*sgd_master, at::kFloat, "lenet sgd master");
-    TORCH_CHECK(sgd_wbf.has_value() && sgd_hyper.has_value() && sgd_descs.has_value() && sgd_ticket.has_value() &&
-                    sgd_stage.has_value(),
-                "lenet sgd: wbf, hyper, descs, ticket and stage are required");
+    TORCH_CHECK(sgd_wbf.has_value() && sgd_hyper.has_value() && sgd_descs.has_value(),
+                "lenet sgd: wbf, hyper and descs are required");
     need(*sgd_wbf, at::kBFloat16, "lenet sgd wbf");
     need(*sgd_hyper, at::kFloat, "lenet sgd hyper");
-    need(*sgd_stage, at::kFloat, "lenet sgd stage");
-    TORCH_CHECK(sgd_stage->numel() >= 2550 && sgd_hyper->numel() >= 5, "lenet sgd: stage / hyper sizes");
-    TORCH_CHECK(sgd_ticket->is_cuda() && sgd_ticket->scalar_type() == at::kInt && sgd_ticket->numel() >= 1,
-                "lenet sgd: ticket must be an int32 GPU tensor");
+    TORCH_CHECK(sgd_hyper->numel() >= 5, "lenet sgd: hyper size");
     const torch::Tensor& dh = *sgd_descs;
     TORCH_CHECK(!dh.is_cuda() && dh.scalar_type() == at::kLong && dh.is_contiguous() &&
                     dh.numel() * 8 >= 10 * (int64_t)sizeof(dfa::ParamDesc),
@@ -1053,8 +1052,6 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
       r.sgd.run_stats = run_stats->data_ptr<float>();
     }
     r.sgd.frag = frag.data_ptr();
-    r.sgd.ticket = reinterpret_cast<unsigned*>(sgd_ticket->data_ptr<int>());
-    r.sgd.stage = sgd_stage->data_ptr<float>();
   }
   if (ll != nullptr) {
     TORCH_CHECK(r.sgd_on, "lenet: the in-kernel LL exchange needs the fused update (sgd_* arguments)");
@@ -1648,8 +1645,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("conv_mom") = std::vector<torch::Tensor>{}, py::arg("sgd_master") = py::none(),
         py::arg("sgd_mom") = py::none(), py::arg("sgd_wbf") = py::none(), py::arg("sgd_hyper") = py::none(),
         py::arg("sgd_descs") = py::none(), py::arg("idx_stream") = py::none(), py::arg("idx_cursor") = py::none(),
-        py::arg("idx_dst") = py::none(), py::arg("sgd_ticket") = py::none(), py::arg("sgd_stage") = py::none(),
-        py::arg("ll") = nullptr, py::arg("exch_blocks") = 0, py::arg("run_stats") = py::none(),
+        py::arg("idx_dst") = py::none(), py::arg("ll") = nullptr, py::arg("exch_blocks") = 0, py::arg("run_stats") = py::none(),
         py::arg("ps") = nullptr, py::arg("ps_perm") = py::none(), py::arg("ps_idx") = py::none(),
         py::arg("ps_lr") = 0.0, py::arg("ps_max_stale") = -1);
   m.def("lenet_blocks", [](int64_t B) { return dfa::lenet_blocks((int)B); });

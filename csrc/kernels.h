@@ -315,7 +315,6 @@ hipError_t ps_apply(const PSArgs& a, hipStream_t st);
 // pool, dense 400-120-84-10, softmax-CE, full backward.  Conv weights are read from the fp32 master,
 // dense weights from the bf16 compute copies ([Npad16][Kpad32] and the dgrad layout).
 constexpr int kLeNetPW1 = 0, kLeNetPB1 = 150, kLeNetPW2 = 156, kLeNetPB2 = 2556, kLeNetConvParams = 2572;
-constexpr int kLeNetConvStride = 2576;  // floats per workgroup in the conv partial buffer
 constexpr int kLeNetMaxTiles = 288;
 struct LeNetArgs {
   const unsigned char* x_u8;  // [nrows][784] uint8 dataset read through idx (or null)
@@ -327,7 +326,9 @@ struct LeNetArgs {
   const float *w1, *b1, *w2, *b2;  // fp32 master: conv1 [6][25], [6]; conv2 [16][150], [16]
   const bf16 *d1w, *d1wt, *d2w, *d2wt, *d3w, *d3wt;  // [128][416] [400][128] [96][128] [128][96] [16][96] [96][32]
   const float *d1b, *d2b, *d3b;
-  float* conv_part;           // [nblocks][kLeNetConvStride] per-workgroup conv gradient partials
+  float* conv_part;           // [kLeNetConvParams][part_ld] per-workgroup conv gradient partials, parameter
+                              // major: the reduce reads each parameter's workgroup partials contiguously
+  int part_ld;                // >= nblocks, a multiple of 512 (padding stays zero)
   float* loss_part;           // [nblocks][2]
   bf16 *h0T, *h1T, *h2T;      // [400|120|84][ldt] transposed dense inputs
   bf16 *dz1T, *dz2T, *dz3T;   // [120|84|10][ldt] transposed dense output gradients
@@ -347,9 +348,9 @@ struct LeNetDense {
   float* gb;  // [N]
   int N, K, tiles;
 };
-// Single-rank fast path of the fused LeNet-5 step: the reduce kernel applies the SGD update to every
-// parameter it finalises (no optimizer launch), stages the next batch's indices and, in its last conv
-// workgroup, rebuilds the conv-weight MFMA fragments of the next step.
+// Fused update of the LeNet-5 step: the reduce kernel applies the SGD update to every parameter it
+// finalises (no optimizer launch), stages the next batch's indices and scatters every updated conv
+// weight into the next step's MFMA fragments (lenet_frag_scatter).
 struct LeNetSgd {
   float* master;
   float* mom;          // null without momentum
@@ -362,11 +363,10 @@ struct LeNetSgd {
   int B, nsteps;
   float* run_stats;    // nullable: [loss sum, correct, updates] accumulated by the loss workgroup
   void* frag;          // fragment buffer of the next step
-  unsigned* ticket;    // conv-workgroup arrival counter (re-armed by the last)
-  float* stage;        // [2550] the new conv weights, handed to the last conv workgroup
 };
 struct LeNetRedArgs {
-  const float* conv_part;
+  const float* conv_part;  // [kLeNetConvParams][part_ld]
+  int part_ld;
   const float* loss_part;
   float* stats;  // [2] loss sum, correct
   float *g_w1, *g_b1, *g_w2, *g_b2;
@@ -393,6 +393,9 @@ struct LeNetRedArgs {
   // staged: an async step is train + this launch (csrc/lenet_fused.hip, protocol csrc/ps_device.h)
   int ps_on;
   PSArgs ps;
+  unsigned long long* stamps;  // diagnostic: [grid][8] s_memtime per phase (scripts/lenetstamps.py), or null
+  int probe;                   // diagnostic (DISTRIFLOW_DIAG lenet_red_probe): 1 dense tiles skip their loads,
+                               // 2 conv blocks skip theirs (wrong gradients: timing experiments only)
 };
 // The reference CNN's conv block (csrc/kcnn_fused.hip): conv1 3x3x1->32 + ReLU, conv2 3x3x32->32 + ReLU,
 // 2x2 max-pool [+ folded dropout], input 28x28x1, in one forward and one backward launch (+ reduce).

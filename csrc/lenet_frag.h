@@ -45,6 +45,36 @@ __device__ __forceinline__ bf16x8 lenet_frag_lane(int fl, W&& wt) {
   return o;
 }
 
+// Inverse of lenet_frag_lane: store bf16(w) of conv weight j into every fragment element that holds it
+// (conv1: 8 banded positions; conv2: 1 forward + 2 pair-banded data-gradient positions).  The update
+// workgroup that owns weight j scatters it right after updating it, so the next step's fragments are
+// complete when the launch ends (no last-arriver rebuild); elements that hold no weight stay zero from
+// the buffer's initial build.
+__device__ __forceinline__ void lenet_frag_scatter(void* frag_buf, int j, float w) {
+  bf16* fr = reinterpret_cast<bf16*>(frag_buf);
+  const bf16 v = f2bf(w);
+  auto put = [&](int f, int lane, int e) { fr[((f * 64) + lane) * 8 + e] = v; };
+  if (j < 150) {  // conv1 [c][ky][kx]
+    const int c = j / 25, r = j - 25 * c, ky = r / 5, kx = r - 5 * ky;
+    const int f = ky * 3 + (c >> 1);
+#pragma unroll
+    for (int j8 = 0; j8 < 8; ++j8) {
+      const int t = kx + 2 * j8;
+      put(f, (t >> 3) * 16 + (c & 1) * 8 + j8, t & 7);
+    }
+    return;
+  }
+  // conv2 [n][tap = ky * 5 + kx][c]
+  const int q = j - 150, n = q / 150, r = q - 150 * n, tap = r / 6, c = r - 6 * tap;
+  put(FR_C2 + (tap >> 2), (tap & 3) * 16 + n, c);
+  const int ky = tap / 5, kx = tap - 5 * ky;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int P = ky * 6 + kx + 1 - b;
+    put(FR_DG + (P >> 1), ((P & 1) * 2 + (n >> 3)) * 16 + b * 8 + c, n & 7);
+  }
+}
+
 // w: the 2550 conv weights (any memory); nt threads of a block build every fragment
 __device__ __forceinline__ void lenet_build_frags(const float* w, bf16x8* __restrict__ frag, int tid, int nt) {
   for (int fl = tid; fl < kLeNetFragLanes; fl += nt) frag[fl] = lenet_frag_lane(fl, [&](int j) { return w[j]; });

@@ -25,6 +25,7 @@
 //   lenet_reduce_kernel  deterministic reductions: conv partials (one wave per parameter over all
 //                        workgroups), dense weight gradients over the batch (MFMA, K = batch), loss.
 #include "common.h"
+#include "diag.h"
 #include "kernels.h"
 #include "lenet_frag.h"
 #include "ll_exchange.h"
@@ -270,7 +271,8 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   const int rows = min(IMG, a.B - r0);
   const long long nb = gridDim.x;
   const bf16x8* __restrict__ frag = reinterpret_cast<const bf16x8*>(a.frag);
-  float* part = a.conv_part + (long long)blockIdx.x * kLeNetConvStride;  // this workgroup's partials
+  float* part = a.conv_part + blockIdx.x;  // this workgroup's partials: parameter p at part[p * part_ld]
+  const long long pld = a.part_ld;
   unsigned long long* const stamps = a.stamps;
   LN_STAMP(0);
 
@@ -560,8 +562,8 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = 4 * g + r;
-          if (tap < 25 && c < 6) part[(long long)(kLeNetPW2 + n * 150 + tap * 6 + c) ] = acc[k][r];
-          else if (tap == 25 && c == 0) part[(long long)(kLeNetPB2 + n) ] = acc[k][r];
+          if (tap < 25 && c < 6) part[(long long)(kLeNetPW2 + n * 150 + tap * 6 + c) * pld] = acc[k][r];
+          else if (tap == 25 && c == 0) part[(long long)(kLeNetPB2 + n) * pld] = acc[k][r];
         }
       }
     }
@@ -686,8 +688,8 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
       const int c = e >> 5, col = e & 31;
       const float v = RED[(0 * 16 + c) * 32 + col] + RED[(1 * 16 + c) * 32 + col] + RED[(2 * 16 + c) * 32 + col] +
                       RED[(3 * 16 + c) * 32 + col];
-      if (col < 25) part[(long long)(kLeNetPW1 + c * 25 + col) ] = v;
-      else if (col == 25) part[(long long)(kLeNetPB1 + c) ] = v;
+      if (col < 25) part[(long long)(kLeNetPW1 + c * 25 + col) * pld] = v;
+      else if (col == 25) part[(long long)(kLeNetPB1 + c) * pld] = v;
     }
   }
   LN_STAMP(10);
@@ -711,16 +713,11 @@ __global__ void __launch_bounds__(PT) lenet_prep_kernel(const float* __restrict_
 //                 waves, LDS combine; bias = a column of ones).  Tiles are placed by a host table so
 //                 that all tiles reading the same 16 activation rows run on one XCD: every XCD then
 //                 fetches its share of H^T once and dZ^T once into its own L2 and re-reads them there.
-//   next nconv_blocks        64 conv parameters each: thread (p, q) sums workgroup partials q, q + 16, ...
-//                 of parameter p (rows of 64 consecutive floats per wave-load), LDS combine.
+//   next nconv_blocks        64 conv parameters each: wave w sums the contiguous partial rows of
+//                 parameters 4w .. 4w + 3 (parameter-major partial layout), butterfly combine.
 //   last block               loss partials -> stats.
 constexpr int RT = 1024;
 
-// write-through hand-off (as csrc/bn.hip): sc1 stores drained before the ticket, sc1 loads after it
-__device__ __forceinline__ void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // ---- one exchange slot = one dense weight-gradient tile (16 x 16, threads t < 256 own an element each) or
 // one conv block (64 parameters, lanes of wave 0).  The value functions return this thread's local sum.
@@ -751,7 +748,7 @@ __device__ __forceinline__ float dense_tile_value(const LeNetRedArgs& a, int slo
   const int per = (steps + 15) / 16;
   const int s0 = wid * per, s1 = min(steps, s0 + per);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int s = s0; s < s1; s += 8) {
+  for (int s = s0; s < (a.probe == 1 ? s0 : s1); s += 8) {
     bf16x8 av[8], bv[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -800,33 +797,33 @@ __device__ __forceinline__ void dense_tile_apply(const LeNetRedArgs& a, int slot
   }
 }
 
-// conv block `cb`: 64 parameters; thread (p, q) sums workgroup partials q, q + 16, ... of parameter p
+// conv block `cb`: 64 parameters; wave w sums parameters 4w .. 4w + 3, each over its contiguous row of
+// workgroup partials (16-byte loads, all in flight, fixed-order lane sums + butterfly: deterministic)
 __device__ __forceinline__ float conv_value(const LeNetRedArgs& a, int cb, float (*red)[16][17]) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float* sred = &red[0][0][0];  // [16][64]
-  const int p = cb * 64 + lane;
-  float s = 0.f;
-  if (p < kLeNetConvParams) {
-    // 32 workgroup rows per pass, all loads in flight before the (fixed-order) sum
-    for (int q0 = wid; q0 < a.nblk; q0 += 16 * 32) {
-      float v[32];
+  float* sred = &red[0][0][0];
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int q0 = 0; q0 < (a.probe == 2 ? 0 : a.part_ld); q0 += 512) {
+    f32x4 x[4][2];
 #pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const int q = q0 + 16 * j;
-        v[j] = q < a.nblk ? a.conv_part[(long long)q * kLeNetConvStride + p] : 0.f;
-      }
-#pragma unroll
-      for (int j = 0; j < 32; ++j) s += v[j];
+    for (int j = 0; j < 4; ++j) {
+      const int p = min(cb * 64 + 4 * wid + j, kLeNetConvParams - 1);
+      const f32x4* row = reinterpret_cast<const f32x4*>(a.conv_part + (long long)p * a.part_ld + q0 + lane * 8);
+      x[j][0] = row[0];
+      x[j][1] = row[1];
     }
-  }
-  sred[wid * 64 + lane] = s;
-  __syncthreads();
-  float v = 0.f;
-  if (wid == 0) {
 #pragma unroll
-    for (int ww = 0; ww < 16; ++ww) v += sred[ww * 64 + lane];
+    for (int j = 0; j < 4; ++j)
+      s[j] += ((x[j][0][0] + x[j][0][1]) + (x[j][0][2] + x[j][0][3])) +
+              ((x[j][1][0] + x[j][1][1]) + (x[j][1][2] + x[j][1][3]));
   }
-  return v;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float t = wave_sum(s[j]);
+    if (lane == 0) sred[4 * wid + j] = t;
+  }
+  __syncthreads();
+  return wid == 0 ? sred[lane] : 0.f;
 }
 
 __device__ __forceinline__ void conv_apply(const LeNetRedArgs& a, int cb, float v) {
@@ -842,8 +839,8 @@ __device__ __forceinline__ void conv_apply(const LeNetRedArgs& a, int cb, float 
     const int di = p < kLeNetPB1 ? 0 : p < kLeNetPW2 ? 1 : p < kLeNetPB2 ? 2 : 3;
     const int i = p - (di == 0 ? 0 : di == 1 ? kLeNetPB1 : di == 2 ? kLeNetPW2 : kLeNetPB2);
     const float nw = sgd_apply_one(a.sgd.d[di], i, v, a.sgd.master, a.sgd.mom, a.sgd.wbf, a.sgd.hyper);
-    // the new conv weights, handed to the workgroup that rebuilds the next step's fragments
-    if (wj >= 0) st_sc1(a.sgd.stage + wj, nw);
+    // the new conv weight goes straight into the next step's MFMA fragments
+    if (wj >= 0) lenet_frag_scatter(a.sgd.frag, wj, nw);
   } else if (a.snap != nullptr && wj >= 0) {
     // the conv kernels' weights and momentum as this gradient saw them: the optimizer launch rebuilds
     // the next step's fragments from these (no read of state it is overwriting)
@@ -863,7 +860,7 @@ constexpr unsigned kPSAccept = 1, kPSReject = 2, kPSFailed = 3, kPSFinished = 4;
 // takes the writer lock (seqlock CAS on the server's word), checks staleness = version_now -
 // version_pulled against the bound and completes the microbatch under the lock; the others wait for
 // the decision word tagged with this launch's epoch (local, agent scope: all of them are resident).
-__device__ void lenet_ps_decide(const LeNetRedArgs& a, unsigned* s_dec, unsigned* s_seq) {
+__device__ void lenet_ps_decide(const LeNetRedArgs& a, unsigned* s_dec, unsigned* s_seq, bool after_completion = false) {
   const PSArgs& p = a.ps;
   if (threadIdx.x == 0) {
     const unsigned ep = __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
@@ -882,15 +879,17 @@ __device__ void lenet_ps_decide(const LeNetRedArgs& a, unsigned* s_dec, unsigned
             if (__hip_atomic_compare_exchange_strong(p.seq, &expected, s + 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_SYSTEM)) {
               const unsigned stale = (s >> 1) - *p.vpulled;
-              if ((int)stale <= p.max_stale || p.max_stale < 0) {
-                dec = kPSAccept;
+              dec = ((int)stale <= p.max_stale || p.max_stale < 0) ? kPSAccept : kPSReject;
+              // the appliers need only the decision: publish it first, then do the bookkeeping
+              __hip_atomic_store(p.scratch + kPSLockedSeq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(p.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+              if (dec == kPSAccept) {
                 p.stats[0] += 1;
                 p.stats[2] += stale;
                 if (stale > p.stats[3]) p.stats[3] = stale;
                 if (p.done_epoch != nullptr) complete_microbatch(p, bid);  // under the writer lock
               } else {
-                dec = kPSReject;  // keep the lock until every workgroup has copied version s / 2
-                p.stats[1] += 1;
+                p.stats[1] += 1;  // rejected: the lock is held until every workgroup copied version s / 2
               }
               break;
             }
@@ -903,12 +902,24 @@ __device__ void lenet_ps_decide(const LeNetRedArgs& a, unsigned* s_dec, unsigned
           __builtin_amdgcn_s_sleep(1);
         }
       }
-      __hip_atomic_store(p.scratch + kPSLockedSeq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (dec != kPSAccept && dec != kPSReject) {  // no lock taken: finished schedule or timeout
+        __hip_atomic_store(p.scratch + kPSLockedSeq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // the microbatch bookkeeping is done: the staging workgroup may claim the next one
+      __hip_atomic_store(p.scratch + kPSCompleted, ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      for (;;) {
-        const unsigned d = __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned* word = p.scratch + (after_completion ? kPSCompleted : kPSDecision);
+      for (;;) {  // relaxed polls, one acquire once the word matches (acquire polls cost every poller an
+                  // L1 invalidate per iteration)
+        const unsigned w = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned d = after_completion
+                               ? (w == ep ? __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT)
+                                          : 0u)
+                               : w;
         if ((d >> 3) == ep) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           dec = d & 7u;
           break;
         }
@@ -978,14 +989,17 @@ __device__ __forceinline__ void conv_ps(const LeNetRedArgs& a, int cb, float g, 
   const int i = p - (di == 0 ? 0 : di == 1 ? kLeNetPB1 : di == 2 ? kLeNetPW2 : kLeNetPB2);
   const float w = lenet_ps_elem(a, a.sgd.d[di], i, g, dec, seq);
   const int wj = p < kLeNetPB1 ? p : (p >= kLeNetPW2 && p < kLeNetPB2) ? 150 + (p - kLeNetPW2) : -1;
-  if (wj >= 0) st_sc1(a.sgd.stage + wj, w);  // the next step's conv fragments are built from these
+  if (wj >= 0) lenet_frag_scatter(a.sgd.frag, wj, w);  // the next step's conv fragments
 }
 
 // Arrival of one of the nexch + 1 protocol workgroups (exchanging + staging): the last one publishes
 // version v + 1 (admitted) or releases the lock (rejected) and records the pulled version.
 __device__ void lenet_ps_arrive(const LeNetRedArgs& a, int arrivals, unsigned dec, unsigned seq) {
   const PSArgs& p = a.ps;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this thread's shared-master stores visible system-wide
+  // every storing wave drains its shared-master stores (uncached / fine-grained memory: complete at the
+  // server's HBM once acknowledged), then the arrival ticket; the last arriver's system-scope release
+  // store of the version word orders all of them before the publish (no per-workgroup L2 write-back)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned prev = __hip_atomic_fetch_add(p.scratch + kPSApplyDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
@@ -994,7 +1008,7 @@ __device__ void lenet_ps_arrive(const LeNetRedArgs& a, int arrivals, unsigned de
       __hip_atomic_store(p.scratch + kPSEpoch, __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED,
                                                                  __HIP_MEMORY_SCOPE_AGENT) + 1u,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // every workgroup's release happened before the unlock
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every workgroup's arrival happened before the unlock
       if (dec == kPSAccept) {
         *p.vpulled = (seq >> 1) + 1u;
         __hip_atomic_store(p.seq, seq + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1014,10 +1028,28 @@ constexpr int kMaxSlotsPerBlock = 8;
 // slots (one each, every workgroup resident); ranks that time-share one GPU use fewer, so that the
 // waiting workgroups of all ranks fit on the chip beside the peers' train kernels.
 // Then one workgroup: loss partials -> stats; one more (index stream bound): stage the next batch.
+// diagnostic phase clocks of the reduce launch: stamps[block][slot] (0 start, 1 local sums pushed,
+// 2 decision / exchange done, 3 applied, 4 end, 5 all waves started, 6 first slot summed)
+#define LR_STAMP(slot)                                                            \
+  do {                                                                            \
+    if (a.stamps) {                                                               \
+      __builtin_amdgcn_sched_barrier(0);                                          \
+      unsigned long long t_;                                                      \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+      __builtin_amdgcn_sched_barrier(0);                                          \
+      if (threadIdx.x == 0) a.stamps[blockIdx.x * 8 + (slot)] = t_;               \
+    }                                                                             \
+  } while (0)
+
 __global__ void __launch_bounds__(RT, 8) lenet_reduce_kernel(LeNetRedArgs a) {
   __shared__ float red[16][16][17];
   __shared__ unsigned s_e;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  LR_STAMP(0);
+  if (a.stamps) {
+    __syncthreads();
+    LR_STAMP(5);  // every wave of the workgroup has started
+  }
   const int nslot = a.dense_tiles + a.nconv_blocks;
   const int nexch = a.exch_blocks;
   if ((int)blockIdx.x < nexch) {
@@ -1030,6 +1062,7 @@ __global__ void __launch_bounds__(RT, 8) lenet_reduce_kernel(LeNetRedArgs a) {
       __syncthreads();           // the previous slot's readers of red are done
       const bool dense = slot < a.dense_tiles;
       const float v = dense ? dense_tile_value(a, slot, red) : conv_value(a, slot - a.dense_tiles, red);
+      if (k == 0) LR_STAMP(6);  // the first slot's partial sums are in
       const bool owner = dense ? threadIdx.x < 256 : wid == 0;
       if (owner) keep[k][threadIdx.x] = v;
       if (a.ll_on) {
@@ -1039,9 +1072,10 @@ __global__ void __launch_bounds__(RT, 8) lenet_reduce_kernel(LeNetRedArgs a) {
       }
     }
     __syncthreads();
-    int nconv_mine = 0;
+    LR_STAMP(1);
     __shared__ unsigned s_dec, s_seq;
     if (a.ps_on) lenet_ps_decide(a, &s_dec, &s_seq);
+    LR_STAMP(2);
     const unsigned dec = a.ps_on ? s_dec : 0u, seq = a.ps_on ? s_seq : 0u;
 #pragma unroll 1
     for (int k = 0; k < kMaxSlotsPerBlock; ++k) {
@@ -1053,7 +1087,6 @@ __global__ void __launch_bounds__(RT, 8) lenet_reduce_kernel(LeNetRedArgs a) {
           if (dense) dense_tile_ps(a, slot, keep[k][threadIdx.x], dec, seq);
           else conv_ps(a, slot - a.dense_tiles, keep[k][threadIdx.x], dec, seq);
         }
-        if (!dense) ++nconv_mine;
         continue;
       }
       if (dense ? threadIdx.x < 256 : wid == 0) {
@@ -1068,30 +1101,10 @@ __global__ void __launch_bounds__(RT, 8) lenet_reduce_kernel(LeNetRedArgs a) {
           else conv_apply(a, slot - a.dense_tiles, v);
         }
       }
-      if (!dense) ++nconv_mine;
     }
+    LR_STAMP(3);
     if (a.ps_on) lenet_ps_arrive(a, nexch + 1, dec, seq);
-    if (a.sgd_on && nconv_mine > 0 && (!a.ps_on || dec == kPSAccept || dec == kPSReject)) {
-      // the workgroup that applies the last conv slot rebuilds the next step's conv-weight fragments from
-      // the staged new weights (write-through stores drained before the ticket, write-through loads
-      // after it: csrc/bn.hip's gfx950 hand-off)
-      __shared__ int last;
-      __shared__ float wl[kLeNetConvW];
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        const unsigned tk =
-            __hip_atomic_fetch_add(a.sgd.ticket, (unsigned)nconv_mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = tk + (unsigned)nconv_mine == (unsigned)a.nconv_blocks;
-        if (last) __hip_atomic_store(a.sgd.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-      if (last) {
-        for (int e = threadIdx.x; e < kLeNetConvW; e += RT) wl[e] = ld_sc1(a.sgd.stage + e);
-        __syncthreads();
-        lenet_build_frags(wl, reinterpret_cast<bf16x8*>(a.sgd.frag), threadIdx.x, RT);
-      }
-    }
+    LR_STAMP(4);
     return;
   }
   const int blk = blockIdx.x - nexch;
@@ -1100,7 +1113,7 @@ __global__ void __launch_bounds__(RT, 8) lenet_reduce_kernel(LeNetRedArgs a) {
     // claim the next microbatch FCFS on the server and stage its example indices
     __shared__ unsigned s_dec, s_seq;
     __shared__ long long s_bid;
-    lenet_ps_decide(a, &s_dec, &s_seq);
+    lenet_ps_decide(a, &s_dec, &s_seq, /*after_completion=*/true);
     if (a.ps.done_epoch != nullptr) {
       claim_microbatch(a.ps, threadIdx.x, &s_bid);
     } else if (threadIdx.x == 0) {
@@ -1156,6 +1169,9 @@ int lenet_dense_part_floats(int B) { (void)B; return 0; }
 hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   LeNetArgs a = a_in;
   a.stamps = g_lenet_stamps_host;
+  // the reduce launch's clocks follow the train kernel's [4096][16] region
+  r.stamps = g_lenet_stamps_host ? g_lenet_stamps_host + 4096 * 16 : nullptr;
+  r.probe = diag_int("lenet_red_probe", 0);
   if (a.B <= 0 || a.ldt % 32 || a.ldt < a.B || !a.frag || !a.ftab || !a.pxtab) return hipErrorInvalidValue;
   const int nblk = (a.B + IMG - 1) / IMG;
   if (a.prep) {
@@ -1191,7 +1207,7 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
     for (int x = 0; x < 8; ++x)
       if (slot < by_xcd[x].size()) order.push_back(by_xcd[x][slot]);
   for (int t : order) r.tile_of_block[b++] = t;
-  if (r.sgd_on && (!r.sgd.master || !r.sgd.wbf || !r.sgd.hyper || !r.sgd.frag || !r.sgd.ticket || !r.sgd.stage))
+  if (r.sgd_on && (!r.sgd.master || !r.sgd.wbf || !r.sgd.hyper || !r.sgd.frag))
     return hipErrorInvalidValue;
   const int nslot = r.dense_tiles + r.nconv_blocks;
   if (r.exch_blocks <= 0 || r.exch_blocks > nslot) r.exch_blocks = nslot;

@@ -8,7 +8,8 @@
 namespace dfa {
 
 // local scratch words (PSArgs::scratch, u32 index)
-constexpr int kPSPullDone = 0, kPSApplyDone = 1, kPSEpoch = 2, kPSDecision = 3, kPSLockedSeq = 4, kPSSlots = 64;
+constexpr int kPSPullDone = 0, kPSApplyDone = 1, kPSEpoch = 2, kPSDecision = 3, kPSLockedSeq = 4, kPSCompleted = 5,
+              kPSSlots = 64;
 
 __device__ __forceinline__ unsigned ps_ld_acq(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -287,7 +287,9 @@ class Net:
             self.head_loss_part = torch.zeros(2 * ((B + 15) // 16), dtype=torch.float32, device=self.device)
         if self.lenet_fused:
             nblk = ops.lenet_blocks(B)
-            self.lenet_conv_part = torch.empty(2576 * nblk, dtype=torch.float32, device=self.device)
+            # [2572 conv parameters][round_up(workgroups, 512)]: parameter-major, zero padding never written
+            self.lenet_conv_part = torch.zeros(2572 * ((nblk + 511) // 512 * 512), dtype=torch.float32,
+                                               device=self.device)
             self.lenet_dense_part = torch.empty(1, dtype=torch.float32, device=self.device)
             self.lenet_loss_part = torch.zeros(2 * nblk, dtype=torch.float32, device=self.device)
         self._bound_B = B
@@ -373,11 +375,8 @@ class Net:
         if self.has_dropout:
             self.step_dev.add_(1)
         st = self.store
-        if not hasattr(self, "_lenet_ticket"):
-            self._lenet_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
-            self._lenet_stage = torch.zeros(2550, dtype=torch.float32, device=self.device)
         sgd = dict(sgd_master=st.master, sgd_mom=st.momentum, sgd_wbf=st.wbf, sgd_hyper=st.hyper,
-                   sgd_descs=st._descs_host, sgd_ticket=self._lenet_ticket, sgd_stage=self._lenet_stage)
+                   sgd_descs=st._descs_host)
         if index_stream is not None:
             sgd.update(idx_stream=index_stream[0], idx_cursor=index_stream[1], idx_dst=index_stream[2])
         if ll is not None:

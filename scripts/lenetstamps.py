@@ -55,6 +55,46 @@ def main():
         col = d[:, k]
         print(f"  {name:<12} median {np.median(col):8.0f}  p90 {np.percentile(col, 90):8.0f}  "
               f"share {np.median(col) / np.median(tot) * 100:5.1f}%")
+    # reduce launch (fused update path: the trainer's step), clocks at [4096 * 16 + block * 8 + slot]
+    if len(sys.argv) > 2 and sys.argv[2] == "step":
+        from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
+
+        tr = DataParallelTrainer(net, lr=0.01, graph="none")
+        tr.bind_dataset(data, labels, B, scale=1 / 255.0)
+        tr.bind_index_stream(epoch_permutations(60000, B, 8, "cuda", seed=0))
+        for _ in range(3):
+            tr.step()
+        torch.cuda.synchronize()
+        buf.zero_()
+        m.convpool_set_stamps(buf)
+        tr.step()
+        torch.cuda.synchronize()
+        m.convpool_set_stamps(None)
+        t_end_train = buf[: nblk * 16].view(nblk, 16).cpu().numpy().astype(np.int64)[:, 10].max()
+        r = buf[4096 * 16: 4096 * 16 + 512 * 8].view(512, 8).cpu().numpy().astype(np.int64)
+        kinds = np.array(["dense"] * 262 + ["conv"] * 41 + ["loss", "stage"] + ["-"] * (512 - 305))
+        valid = r[:, 0] > 0
+        for kind in ("dense", "conv", "loss", "stage"):
+            sel = valid & (kinds == kind)
+            if sel.any():
+                life = np.where(r[sel, 4] > 0, r[sel, 4], np.where(r[sel, 3] > 0, r[sel, 3], r[sel, 1])) - r[sel, 0]
+                sums = r[sel, 1] - r[sel, 0]
+                print(f"  {kind:<6} blocks {sel.sum():4d}: local sums median {np.median(sums):7.0f} max {sums.max():7.0f};"
+                      f" lifetime median {np.median(life):7.0f} max {life.max():7.0f}")
+                if kind in ("dense", "conv"):
+                    wl, s1 = r[sel, 5] - r[sel, 0], r[sel, 6] - r[sel, 5]
+                    print(f"         waves started after median {np.median(wl):7.0f} max {wl.max():7.0f}; first slot "
+                          f"summed median {np.median(s1):7.0f} max {s1.max():7.0f}")
+        r = r[r[:, 0] > 0]
+        print(f"reduce launch: {r.shape[0]} stamped workgroups; first start {r[:, 0].min() - t_end_train} after the "
+              f"last train workgroup's end; start spread {r[:, 0].max() - r[:, 0].min()}")
+        ends = np.where(r[:, 4] > 0, r[:, 4], r[:, 3])
+        print(f"  ends: median {np.median(ends - r[:, 0].min()):.0f}  max {ends.max() - r[:, 0].min():.0f} after the first start")
+        for k, name in enumerate(["local sums", "decision/exchange", "apply", "arrive"]):
+            ok = (r[:, k + 1] > 0) & (r[:, k] > 0)
+            col = r[ok, k + 1] - r[ok, k]
+            if col.size:
+                print(f"  {name:<18} median {np.median(col):8.0f}  p90 {np.percentile(col, 90):8.0f}  max {col.max():8.0f}")
 
 
 if __name__ == "__main__":
