@@ -890,7 +890,10 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
               "lenet: three dense layers");
   TORCH_CHECK(B > 0 && B < (1 << 30), "lenet: bad batch");
   dfa::LeNetArgs a{};
-  const int64_t ldt = (B + 31) / 32 * 32;
+  const int64_t ldt = (B + 31) / 32 * 32;  // batch columns of H^T / dZ^T the reduce sums over
+  // row stride of H^T / dZ^T: any multiple of 32 >= ldt (the trainer pads it off a power of two)
+  const int64_t lds = hT.size() == 3 && hT[0].dim() == 2 ? hT[0].size(1) : 0;
+  TORCH_CHECK(lds >= ldt && lds % 32 == 0, "lenet: hT rows must hold round32(B) columns, stride a multiple of 32");
   if (x.scalar_type() == at::kByte) {
     TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.numel() % 784 == 0, "lenet: uint8 dataset [N][28][28][1]");
     a.x_u8 = x.data_ptr<uint8_t>();
@@ -943,8 +946,8 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
                 "lenet: dense grad size");
     need(hT[l], at::kBFloat16, "lenet hT");
     need(dzT[l], at::kBFloat16, "lenet dzT");
-    TORCH_CHECK(hT[l].dim() == 2 && hT[l].size(0) == NK[l][1] && hT[l].size(1) == ldt, "lenet: hT shape");
-    TORCH_CHECK(dzT[l].dim() == 2 && dzT[l].size(0) == NK[l][0] && dzT[l].size(1) == ldt, "lenet: dzT shape");
+    TORCH_CHECK(hT[l].dim() == 2 && hT[l].size(0) == NK[l][1] && hT[l].size(1) == lds, "lenet: hT shape");
+    TORCH_CHECK(dzT[l].dim() == 2 && dzT[l].size(0) == NK[l][0] && dzT[l].size(1) == lds, "lenet: dzT shape");
     dw[l] = reinterpret_cast<const dfa::bf16*>(dense_w[l].data_ptr());
     dwt[l] = reinterpret_cast<const dfa::bf16*>(dense_wt[l].data_ptr());
     db[l] = dense_b[l].data_ptr<float>();
@@ -956,10 +959,7 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
   need(conv_part, at::kFloat, "lenet conv_part");
   need(loss_part, at::kFloat, "lenet loss_part");
   need(stats, at::kFloat, "lenet stats");
-  const int64_t part_ld = (nblk + 511) / 512 * 512;
-  TORCH_CHECK(conv_part.numel() >= (int64_t)dfa::kLeNetConvParams * part_ld,
-              "lenet: conv_part must hold [2572][round_up(nblocks, 512)] floats (zero initialised)");
-  a.part_ld = (int)part_ld;
+  TORCH_CHECK(conv_part.numel() >= (int64_t)dfa::kLeNetConvStride * nblk, "lenet: conv_part too small");
   TORCH_CHECK(loss_part.numel() >= 2 * nblk && stats.numel() >= 2, "lenet: loss buffers too small");
   a.conv_part = conv_part.data_ptr<float>();
   a.loss_part = loss_part.data_ptr<float>();
@@ -975,12 +975,17 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
   a.ftab = ftab.data_ptr<uint8_t>();
   a.pxtab = reinterpret_cast<const unsigned short*>(pxtab.data_ptr());
   a.B = (int)B;
-  a.ldt = (int)ldt;
+  a.ldt = (int)lds;
   a.grad_scale = (float)grad_scale;
   dfa::LeNetRedArgs r{};
-  (void)dense_part;  // kept in the signature; the dense gradients no longer need partials
+  r.kcols = (int)ldt;
+  // reduce scratch: job slabs, then the arrival tickets (zero-initialised by the trainer)
+  need(dense_part, at::kFloat, "lenet dense_part");
+  TORCH_CHECK(dense_part.numel() >= dfa::lenet_dense_part_floats((int)B),
+              "lenet: dense_part must hold lenet_dense_part_floats(B) zero-initialised floats");
+  r.slabs = dense_part.data_ptr<float>();
+  r.tickets = reinterpret_cast<unsigned*>(dense_part.data_ptr<float>() + dfa::lenet_red_slab_floats());
   r.conv_part = a.conv_part;
-  r.part_ld = a.part_ld;
   r.loss_part = a.loss_part;
   r.stats = stats.data_ptr<float>();
   r.g_w1 = conv_grads[0].data_ptr<float>();
@@ -1654,7 +1659,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gather_labels", &gather_labels_py);
   py::class_<P2PComm>(m, "P2PComm", "one-shot xGMI all-reduce over IPC-mapped peer buffers")
       .def(py::init<int64_t, int64_t, int64_t, double, int64_t>(), py::arg("rank"), py::arg("world"),
-           py::arg("max_floats"), py::arg("timeout_s") = 2.0, py::arg("ll_slots") = 512)
+           py::arg("max_floats"), py::arg("timeout_s") = 2.0, py::arg("ll_slots") = 256)
       .def("handle", &P2PComm::handle)
       .def("open", &P2PComm::open)
       .def("allreduce", &P2PComm::allreduce, py::arg("t"), py::arg("scale") = 1.0)

@@ -265,7 +265,7 @@ hipError_t p2p_allreduce(const P2PArgs& a, hipStream_t st);
 // producing workgroup PUSHES into every peer's IPC-mapped region, so a reduction epilogue (the fused
 // LeNet-5 reduce, ...) sums the W ranks' values of its own slot without a separate all-reduce launch.
 // Region of rank r (inside its P2PComm allocation): [2 parities][nslots][kP2PMaxRanks src][kLLSlot].
-constexpr int kLLSlot = 256;  // granules per slot (one per thread of a 256-value epilogue)
+constexpr int kLLSlot = 1024;  // granules per slot (one per thread of a 1024-thread epilogue)
 struct LLComm {
   unsigned long long* bases[kP2PMaxRanks];  // bases[r] = rank r's LL region mapped into this process
   unsigned* epochs;                         // [nslots] per-slot call counters (local)
@@ -315,7 +315,7 @@ hipError_t ps_apply(const PSArgs& a, hipStream_t st);
 // pool, dense 400-120-84-10, softmax-CE, full backward.  Conv weights are read from the fp32 master,
 // dense weights from the bf16 compute copies ([Npad16][Kpad32] and the dgrad layout).
 constexpr int kLeNetPW1 = 0, kLeNetPB1 = 150, kLeNetPW2 = 156, kLeNetPB2 = 2556, kLeNetConvParams = 2572;
-constexpr int kLeNetMaxTiles = 288;
+constexpr int kLeNetConvStride = 2576;  // floats per workgroup row of the conv partial buffer
 struct LeNetArgs {
   const unsigned char* x_u8;  // [nrows][784] uint8 dataset read through idx (or null)
   const bf16* x_bf;           // [B][784] bf16 batch (when x_u8 is null)
@@ -326,9 +326,7 @@ struct LeNetArgs {
   const float *w1, *b1, *w2, *b2;  // fp32 master: conv1 [6][25], [6]; conv2 [16][150], [16]
   const bf16 *d1w, *d1wt, *d2w, *d2wt, *d3w, *d3wt;  // [128][416] [400][128] [96][128] [128][96] [16][96] [96][32]
   const float *d1b, *d2b, *d3b;
-  float* conv_part;           // [kLeNetConvParams][part_ld] per-workgroup conv gradient partials, parameter
-                              // major: the reduce reads each parameter's workgroup partials contiguously
-  int part_ld;                // >= nblocks, a multiple of 512 (padding stays zero)
+  float* conv_part;           // [nblocks][kLeNetConvStride] per-workgroup conv gradient partials
   float* loss_part;           // [nblocks][2]
   bf16 *h0T, *h1T, *h2T;      // [400|120|84][ldt] transposed dense inputs
   bf16 *dz1T, *dz2T, *dz3T;   // [120|84|10][ldt] transposed dense output gradients
@@ -364,27 +362,37 @@ struct LeNetSgd {
   float* run_stats;    // nullable: [loss sum, correct, updates] accumulated by the loss workgroup
   void* frag;          // fragment buffer of the next step
 };
+// Contiguous copy of what the reduce launch indexes at run time (filled by lenet_train from the fields
+// below): the kernel stages it into LDS with one parallel vector load from the kernel-argument segment.
+struct LeNetRedTab {
+  LeNetDense L[3];
+  float* g[10];    // gradient output per descriptor: w1, b1, w2, b2, dense (w, b) x 3
+  ParamDesc d[10];
+};
 struct LeNetRedArgs {
-  const float* conv_part;  // [kLeNetConvParams][part_ld]
-  int part_ld;
+  LeNetRedTab tab;
+  const float* conv_part;  // [nblk][kLeNetConvStride]
   const float* loss_part;
   float* stats;  // [2] loss sum, correct
   float *g_w1, *g_b1, *g_w2, *g_b2;
   LeNetDense L[3];
-  int nblk, ldt, nconv_blocks, dense_tiles;
-  int tile_of_block[kLeNetMaxTiles];  // XCD-aware placement of the dense weight-gradient tiles
+  int nblk, ldt, nconv_slots, dense_tiles;  // dense_tiles: 32 x 32 units (L[l].tiles per layer)
+  int kcols;       // batch columns summed (round32(B)); ldt is the row stride of H^T / dZ^T
+  int chunk_cols;  // batch columns per dense job (a multiple of 32; chunk c = XCD c's train workgroups)
+  float* slabs;      // [slots][8 chunks][1024] job partials (write-through), chunk 0 then the owner's sum
+  unsigned* tickets;  // [slots] arrival tickets, zero between launches (the last arriver resets)
   // optional snapshot [2][2550] of the conv kernels' weights (w1, w2) and momentum (m1, m2; null = 0)
   const float *w1, *w2, *m1, *m2;
   float* snap;
   int sgd_on;
   LeNetSgd sgd;
-  // world > 1 (requires sgd_on): every dense tile / conv block sums its values over the ranks through
-  // the in-kernel LL exchange before applying the update, so a multi-rank step is still two launches;
-  // workgroup b uses LL slot b
+  // world > 1 (requires sgd_on): the owner of every slot sums its values over the ranks through the
+  // in-kernel LL exchange (LL slot = slot) before applying the update, so a multi-rank step is still two
+  // launches
   int ll_on;
   LLComm ll;
-  // exchanging workgroups (0 = one per slot); fewer when ranks time-share one GPU (each then owns up to
-  // 8 slots round-robin), so that every rank's waiting workgroups fit on the chip at once
+  // job workgroups G (0 = one per job); fewer when ranks time-share one GPU (each then runs several jobs
+  // and owns up to 16 slots), so that every rank's waiting workgroups fit on the chip at once
   int exch_blocks;
   // asynchronous SGD against the device parameter server (requires sgd_on for the compute-copy layout):
   // the gradient is applied to the SHARED master under the PS writer lock (staleness bound ps.max_stale,
@@ -424,7 +432,8 @@ size_t kcnn_slab_floats(int B);
 hipError_t kcnn_fwd(const KcnnArgs& a, hipStream_t st);
 hipError_t kcnn_bwd(const KcnnArgs& a, float* g_w1, float* g_b1, float* g_w2, float* g_b2, long long* step_inc,
                     hipStream_t st);
-int lenet_dense_part_floats(int B);
+int lenet_dense_part_floats(int B);  // reduce scratch: job slabs + arrival tickets
+int lenet_red_slab_floats();
 size_t lenet_train_lds();
 int lenet_blocks(int B);
 hipError_t lenet_train(const LeNetArgs& a, LeNetRedArgs r, hipStream_t st);

@@ -80,18 +80,21 @@ __device__ __forceinline__ void lenet_build_frags(const float* w, bf16x8* __rest
   for (int fl = tid; fl < kLeNetFragLanes; fl += nt) frag[fl] = lenet_frag_lane(fl, [&](int j) { return w[j]; });
 }
 
-// The SGD update of one parameter with every operation rounded on its own (no contraction), so the
-// optimizer's fragment rebuild and the owning workgroup's update produce the same bits.
+// The SGD update of one parameter with every operation rounded on its own, so the optimizer's fragment
+// rebuild and the owning workgroup's update produce the same bits whatever they are inlined into.
+// (HIP's __fmul_rn / __fadd_rn are plain operators that -ffp-contract may still fuse into an FMA after
+// inlining; the pragma keeps the multiplies and adds created here separate.)
 __device__ __forceinline__ float sgd_new_weight(float w, float gr, float m, float lr, float mom, float wd, float gs,
                                                 bool nesterov, float* m_out) {
-  float g = __fmul_rn(gr, gs);
-  if (wd != 0.f) g = __fadd_rn(g, __fmul_rn(wd, w));
+#pragma clang fp contract(off)
+  float g = gr * gs;
+  if (wd != 0.f) g = g + wd * w;
   if (mom != 0.f) {
-    const float v = __fadd_rn(__fmul_rn(mom, m), g);
+    const float v = mom * m + g;
     if (m_out) *m_out = v;
-    g = nesterov ? __fadd_rn(g, __fmul_rn(mom, v)) : v;
+    g = nesterov ? g + mom * v : v;
   }
-  return __fsub_rn(w, __fmul_rn(lr, g));
+  return w - lr * g;
 }
 
 }  // namespace dfa

@@ -243,6 +243,16 @@ __device__ __forceinline__ void dense_bwd(const DenseFrags<KS, NTW>& f, const bf
   }
 }
 
+// Image group (IMG images) of train workgroup b of nb: XCD-aware, so that with round-robin dispatch
+// (XCD = b mod 8) the groups of XCD x are contiguous -- its workgroups write whole 128-byte lines of the
+// transposed activation / gradient rows (no line shared by two XCDs' L2s) and the reduce launch's
+// batch chunk x is exactly the columns XCD x wrote.  The tail (nb mod 8 workgroups) keeps b.
+__device__ __forceinline__ int lenet_img_group(int b, int nb) {
+  const int per = nb / 8;
+  if (b >= 8 * per) return b;
+  return (b & 7) * per + (b >> 3);
+}
+
 __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* Xs = reinterpret_cast<bf16*>(smem + OFF_XS);
@@ -267,12 +277,11 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   float* RED = reinterpret_cast<float*>(smem + OFF_RED);
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15, g = lane >> 4;
-  const int r0 = blockIdx.x * IMG;
+  const int r0 = lenet_img_group(blockIdx.x, gridDim.x) * IMG;
   const int rows = min(IMG, a.B - r0);
   const long long nb = gridDim.x;
   const bf16x8* __restrict__ frag = reinterpret_cast<const bf16x8*>(a.frag);
-  float* part = a.conv_part + blockIdx.x;  // this workgroup's partials: parameter p at part[p * part_ld]
-  const long long pld = a.part_ld;
+  float* part = a.conv_part + (long long)blockIdx.x * kLeNetConvStride;  // this workgroup's partials
   unsigned long long* const stamps = a.stamps;
   LN_STAMP(0);
 
@@ -562,8 +571,8 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = 4 * g + r;
-          if (tap < 25 && c < 6) part[(long long)(kLeNetPW2 + n * 150 + tap * 6 + c) * pld] = acc[k][r];
-          else if (tap == 25 && c == 0) part[(long long)(kLeNetPB2 + n) * pld] = acc[k][r];
+          if (tap < 25 && c < 6) part[(long long)(kLeNetPW2 + n * 150 + tap * 6 + c)] = acc[k][r];
+          else if (tap == 25 && c == 0) part[(long long)(kLeNetPB2 + n)] = acc[k][r];
         }
       }
     }
@@ -688,8 +697,8 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
       const int c = e >> 5, col = e & 31;
       const float v = RED[(0 * 16 + c) * 32 + col] + RED[(1 * 16 + c) * 32 + col] + RED[(2 * 16 + c) * 32 + col] +
                       RED[(3 * 16 + c) * 32 + col];
-      if (col < 25) part[(long long)(kLeNetPW1 + c * 25 + col) * pld] = v;
-      else if (col == 25) part[(long long)(kLeNetPB1 + c) * pld] = v;
+      if (col < 25) part[(long long)(kLeNetPW1 + c * 25 + col)] = v;
+      else if (col == 25) part[(long long)(kLeNetPB1 + c)] = v;
     }
   }
   LN_STAMP(10);
@@ -708,145 +717,224 @@ __global__ void __launch_bounds__(PT) lenet_prep_kernel(const float* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------------
-// Reductions in one launch, deterministic (fixed summation order everywhere):
-//   blocks [0, dense_tiles)  one 16x16 tile of a dense weight gradient each (K = batch split over 16
-//                 waves, LDS combine; bias = a column of ones).  Tiles are placed by a host table so
-//                 that all tiles reading the same 16 activation rows run on one XCD: every XCD then
-//                 fetches its share of H^T once and dZ^T once into its own L2 and re-reads them there.
-//   next nconv_blocks        64 conv parameters each: wave w sums the contiguous partial rows of
-//                 parameters 4w .. 4w + 3 (parameter-major partial layout), butterfly combine.
-//   last block               loss partials -> stats.
-constexpr int RT = 1024;
+// Reductions in one launch, deterministic (fixed summation order everywhere).
+//
+// Slots: [0, dense_tiles) are 32 x 32 units of the dense weight gradients dW = dZ^T H (bias = input
+// column K); then nconv_slots slots of 256 conv parameters.  Every slot is split into kChunks = 8 jobs:
+// dense job (u, c) sums batch columns [c * chunk_cols, (c + 1) * chunk_cols), conv job (s, c) the
+// partial rows of the train workgroups q = c (mod 8).  Job j = slot * 8 + c runs on workgroup j (mod G),
+// so with round-robin dispatch and G % 8 == 0 chunk c is always read on XCD c -- the XCD whose train
+// workgroups WROTE those columns / rows (the train kernel maps its image groups XCD-aware), and every
+// line of H^T / dZ^T / conv partials is fetched into exactly one L2.  (Placement is speed only: any
+// dispatch order gives the same bits.)  The jobs spread the ~5 MB of the step's activations over the
+// whole chip: per-CU load bandwidth from beyond L2, not the FLOPs, bounds this launch.
+//
+// Each job writes its partial as a write-through (sc1) slab and takes a ticket; the slot's last arriver
+// sums the 8 slabs in chunk order (sc1 loads), becomes the slot's OWNER, and -- multi-rank -- pushes the
+// local sums into the peers' LL slots (csrc/ll_exchange.h).  After its jobs a workgroup waits for the
+// rank sums of the slots it owns and applies the update (sync SGD, or the async PS decision).
+// Then one workgroup: loss partials -> stats; one more (index stream / async PS): stage the next batch.
+constexpr int RT = 256;          // reduce workgroup: 4 waves
+constexpr int kDU = 32;          // dense unit edge
+constexpr int kChunks = 8;       // jobs per slot
+constexpr int kConvPer = 256;    // conv parameters per slot
+constexpr int kSlotVals = 1024;  // values per slot (dense 32 x 32; conv slots use 256) = kLLSlot
+constexpr int kPerThread = kSlotVals / RT;
+constexpr int kMaxOwned = 16;    // slots one workgroup may own (host: G >= 8 * slots / kMaxOwned)
+static_assert(kSlotVals <= kLLSlot, "LL slot too small");
 
+// The element a thread finalises: descriptor index di into LeNetSgd::d (-1: none) and the element index
+// i inside that tensor.
+struct Owned {
+  int di, i;
+};
 
-// ---- one exchange slot = one dense weight-gradient tile (16 x 16, threads t < 256 own an element each) or
-// one conv block (64 parameters, lanes of wave 0).  The value functions return this thread's local sum.
+// Per-workgroup LDS copy of what the slots index at run time (dense layers, gradient outputs, update
+// descriptors, SGD hyper-parameters).  Indexing the by-value kernel argument with run-time values would
+// make the compiler copy the whole argument block into scratch for every thread; instead the contiguous
+// LeNetRedTab image is read straight from the kernel-argument segment, one dword per thread.
+struct RedTables : LeNetRedTab {
+  float hyper[5];  // lr, momentum, wd, grad_scale, nesterov (read once, not per element)
+};
 
-// dense tile `slot`: K = batch split over the 16 waves, LDS combine (bias = a column of ones)
-__device__ __forceinline__ float dense_tile_value(const LeNetRedArgs& a, int slot, float (*red)[16][17]) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int tile = a.tile_of_block[slot];
+__device__ __forceinline__ void stage_tables(const LeNetRedArgs& a, RedTables* t) {
+  constexpr int kWords = (int)(sizeof(LeNetRedTab) / 4);
+  static_assert(sizeof(LeNetRedTab) % 4 == 0 && kWords <= RT, "table image");
+  typedef const __attribute__((address_space(4))) char kchar;  // the constant (kernel-argument) address space
+  typedef const __attribute__((address_space(4))) int kint;
+  kint* src = (kint*)((kchar*)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(LeNetRedArgs, tab));
+  if ((int)threadIdx.x < kWords) reinterpret_cast<int*>(static_cast<LeNetRedTab*>(t))[threadIdx.x] = src[threadIdx.x];
+  if (a.sgd_on && threadIdx.x >= 64 && threadIdx.x < 69) t->hyper[threadIdx.x - 64] = a.sgd.hyper[threadIdx.x - 64];
+}
+
+// dense unit u -> layer, output tile row tn (32 outputs), input tile column tk (32 inputs; bias = input K)
+__device__ __forceinline__ int dense_unit(const RedTables& t, int u, int& tn, int& tk) {
   int l = 0;
-  if (tile >= a.L[0].tiles) {
-    tile -= a.L[0].tiles;
+  if (u >= t.L[0].tiles) {
+    u -= t.L[0].tiles;
     l = 1;
-    if (tile >= a.L[1].tiles) {
-      tile -= a.L[1].tiles;
+    if (u >= t.L[1].tiles) {
+      u -= t.L[1].tiles;
       l = 2;
     }
   }
-  const LeNetDense& L = a.L[l];
-  const int tk = tile / ((L.N + 15) / 16), tn = tile - ((L.N + 15) / 16) * tk;  // tn fastest
-  const int n = 16 * tn + (lane & 15), k = 16 * tk + (lane & 15);
-  const bf16* arow = L.dzT + (long long)min(n, L.N - 1) * a.ldt + 8 * (lane >> 4);
-  const bf16* brow = L.hT + (long long)min(k, L.K - 1) * a.ldt + 8 * (lane >> 4);
-  const bool a_ok = n < L.N, b_ones = k == L.K, b_ok = k < L.K;
+  const int nt = (t.L[l].N + kDU - 1) / kDU;
+  tk = u / nt;
+  tn = u - nt * tk;  // tn fastest
+  return l;
+}
+
+// the element of position pos (< kSlotVals) of `slot`
+__device__ __forceinline__ Owned owned_elem(const LeNetRedArgs& a, const RedTables& t, int slot, int pos) {
+  if (slot < a.dense_tiles) {
+    int tn, tk;
+    const int l = dense_unit(t, slot, tn, tk);
+    const int N = t.L[l].N, K = t.L[l].K;
+    const int on = kDU * tn + (pos >> 5), ok = kDU * tk + (pos & 31);
+    if (on >= N || ok > K) return {-1, 0};
+    return ok < K ? Owned{4 + 2 * l, on * K + ok} : Owned{5 + 2 * l, on};
+  }
+  const int p = (slot - a.dense_tiles) * kConvPer + pos;
+  if (pos >= kConvPer || p >= kLeNetConvParams) return {-1, 0};
+  if (p < kLeNetPB1) return {0, p};
+  if (p < kLeNetPW2) return {1, p - kLeNetPB1};
+  if (p < kLeNetPB2) return {2, p - kLeNetPW2};
+  return {3, p - kLeNetPB2};
+}
+
+// position of conv weight element (di, i) in the fragment buffer's weight numbering (-1: not a conv weight)
+__device__ __forceinline__ int conv_wj(Owned o) { return o.di == 0 ? o.i : o.di == 2 ? 150 + o.i : -1; }
+
+// Dense job (unit u, chunk c): this workgroup's partial of the unit over the chunk's batch columns.  The
+// chunk's K-steps are split over the 4 waves; each wave computes all four 16 x 16 sub-tiles of its steps
+// (every operand row it loads is used twice); LDS combine.  out[e] = partial of position t + 256 e.
+__device__ __forceinline__ void dense_job(const LeNetRedArgs& a, const RedTables& t, int u, int c, float* red,
+                                          float (&out)[kPerThread]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int tn, tk;
+  const int l = dense_unit(t, u, tn, tk);
+  const LeNetDense& L = t.L[l];
+  const int col0 = c * a.chunk_cols, col1 = min(a.kcols, col0 + a.chunk_cols);
+  const bf16* arow[2];
+  const bf16* brow[2];
+  bool a_ok[2], b_ok[2], b_one[2], a_any[2], b_any[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int n = kDU * tn + 16 * i + (lane & 15), k = kDU * tk + 16 * i + (lane & 15);
+    arow[i] = L.dzT + (long long)min(n, L.N - 1) * a.ldt + col0 + 8 * (lane >> 4);
+    brow[i] = L.hT + (long long)min(k, L.K - 1) * a.ldt + col0 + 8 * (lane >> 4);
+    a_ok[i] = n < L.N;
+    b_ok[i] = k < L.K;
+    b_one[i] = k == L.K;
+    a_any[i] = kDU * tn + 16 * i < L.N;  // wave-uniform: some row of this 16-row group is live
+    b_any[i] = kDU * tk + 16 * i < L.K;  // ... has a real (not bias / padding) input row
+  }
   bf16x8 ones, zeros = zero8();
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
-  const int steps = a.ldt / 32;
-  const int per = (steps + 15) / 16;
+  const int steps = col1 > col0 ? (col1 - col0) / 32 : 0;
+  const int per = (steps + 3) / 4;
   const int s0 = wid * per, s1 = min(steps, s0 + per);
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int s = s0; s < (a.probe == 1 ? s0 : s1); s += 8) {
-    bf16x8 av[8], bv[8];
+  f32x4 acc[2][2];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int ss = min(s + u, s1 - 1);
-      av[u] = ld8(arow + 32 * ss);
-      bv[u] = ld8(brow + 32 * ss);
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s = s0; s < (a.probe == 1 ? s0 : s1); s += 4) {
+    bf16x8 av[2][4], bv[2][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ss = min(s + q, s1 - 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        av[i][q] = a_any[i] ? ld8(arow[i] + 32 * ss) : zeros;
+        bv[i][q] = b_any[i] ? ld8(brow[i] + 32 * ss) : zeros;
+      }
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const bool live = s + u < s1;
-      acc = mfma16x16x32((a_ok && live) ? av[u] : zeros, b_ok ? bv[u] : (b_ones ? ones : zeros), acc);
+    for (int q = 0; q < 4; ++q) {
+      const bool live = s + q < s1;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = mfma16x16x32((a_ok[i] && live) ? av[i][q] : zeros,
+                                   b_ok[j] ? bv[j][q] : (b_one[j] ? ones : zeros), acc[i][j]);
     }
   }
+  // D[n][k] of sub-tile (i, j): row 16 i + 4 (lane >> 4) + r, column 16 j + (lane & 15); position = row * 32 + col
 #pragma unroll
-  for (int r = 0; r < 4; ++r) red[wid][4 * (lane >> 4) + r][lane & 15] = acc[r];
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[wid * kSlotVals + (16 * i + 4 * (lane >> 4) + r) * kDU + 16 * j + (lane & 15)] = acc[i][j][r];
   __syncthreads();
-  float v = 0.f;
-  if (threadIdx.x < 256) {
-    const int rn = threadIdx.x >> 4, ck = threadIdx.x & 15;
 #pragma unroll
-    for (int ww = 0; ww < 16; ++ww) v += red[ww][rn][ck];
-  }
-  return v;
-}
-
-__device__ __forceinline__ void dense_tile_apply(const LeNetRedArgs& a, int slot, float v) {
-  int tile = a.tile_of_block[slot];
-  int l = 0;
-  if (tile >= a.L[0].tiles) {
-    tile -= a.L[0].tiles;
-    l = 1;
-    if (tile >= a.L[1].tiles) {
-      tile -= a.L[1].tiles;
-      l = 2;
-    }
-  }
-  const LeNetDense& L = a.L[l];
-  const int tk = tile / ((L.N + 15) / 16), tn = tile - ((L.N + 15) / 16) * tk;
-  const int on = 16 * tn + (threadIdx.x >> 4), ok = 16 * tk + (threadIdx.x & 15);
-  if (on < L.N) {
-    if (ok < L.K) L.gw[(long long)on * L.K + ok] = v;
-    else if (ok == L.K) L.gb[on] = v;
-    if (a.sgd_on && ok <= L.K)  // fused update of this element
-      sgd_apply_one(a.sgd.d[4 + 2 * l + (ok == L.K ? 1 : 0)], ok < L.K ? on * L.K + ok : on, v, a.sgd.master,
-                    a.sgd.mom, a.sgd.wbf, a.sgd.hyper);
+  for (int e = 0; e < kPerThread; ++e) {
+    const int pos = threadIdx.x + RT * e;
+    out[e] = ((red[pos] + red[kSlotVals + pos]) + red[2 * kSlotVals + pos]) + red[3 * kSlotVals + pos];
   }
 }
 
-// conv block `cb`: 64 parameters; wave w sums parameters 4w .. 4w + 3, each over its contiguous row of
-// workgroup partials (16-byte loads, all in flight, fixed-order lane sums + butterfly: deterministic)
-__device__ __forceinline__ float conv_value(const LeNetRedArgs& a, int cb, float (*red)[16][17]) {
+// Conv job (slot s, chunk c): parameters 256 s .. 256 s + 255 over the train workgroups' partial rows
+// q = c, c + 8, ...: one row (1 KB) per wave-load, the rows split over the 4 waves, LDS combine.
+__device__ __forceinline__ void conv_job(const LeNetRedArgs& a, int s, int c, float* red, float (&out)[kPerThread]) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float* sred = &red[0][0][0];
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int q0 = 0; q0 < (a.probe == 2 ? 0 : a.part_ld); q0 += 512) {
-    f32x4 x[4][2];
+  const int p0 = s * kConvPer + 4 * lane;
+  const int pl = min(p0, kLeNetConvStride - 4);  // lanes past the last parameter read the row's padding
+  const int nrows = a.nblk > c ? (a.nblk - 1 - c) / kChunks + 1 : 0;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int i0 = wid; i0 < (a.probe == 2 ? 0 : nrows); i0 += 4 * 16) {
+    f32x4 v[16];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int p = min(cb * 64 + 4 * wid + j, kLeNetConvParams - 1);
-      const f32x4* row = reinterpret_cast<const f32x4*>(a.conv_part + (long long)p * a.part_ld + q0 + lane * 8);
-      x[j][0] = row[0];
-      x[j][1] = row[1];
+    for (int k = 0; k < 16; ++k) {
+      const int i = i0 + 4 * k;
+      v[k] = i < nrows ? *reinterpret_cast<const f32x4*>(a.conv_part + (long long)(c + kChunks * i) * kLeNetConvStride + pl)
+                       : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      s[j] += ((x[j][0][0] + x[j][0][1]) + (x[j][0][2] + x[j][0][3])) +
-              ((x[j][1][0] + x[j][1][1]) + (x[j][1][2] + x[j][1][3]));
+    for (int k = 0; k < 16; ++k) acc += v[k];
   }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float t = wave_sum(s[j]);
-    if (lane == 0) sred[4 * wid + j] = t;
-  }
+  *reinterpret_cast<f32x4*>(red + wid * kSlotVals + 4 * lane) = acc;
   __syncthreads();
-  return wid == 0 ? sred[lane] : 0.f;
+  const int pos = threadIdx.x;
+  out[0] = ((red[pos] + red[kSlotVals + pos]) + red[2 * kSlotVals + pos]) + red[3 * kSlotVals + pos];
+#pragma unroll
+  for (int e = 1; e < kPerThread; ++e) out[e] = 0.f;
 }
 
-__device__ __forceinline__ void conv_apply(const LeNetRedArgs& a, int cb, float v) {
-  const int p = cb * 64 + (threadIdx.x & 63);
-  if (p >= kLeNetConvParams) return;
-  float* dst = p < kLeNetPB1 ? a.g_w1 + p
-               : p < kLeNetPW2 ? a.g_b1 + (p - kLeNetPB1)
-               : p < kLeNetPB2 ? a.g_w2 + (p - kLeNetPW2)
-                               : a.g_b2 + (p - kLeNetPB2);
-  *dst = v;
-  const int wj = p < kLeNetPB1 ? p : (p >= kLeNetPW2 && p < kLeNetPB2) ? 150 + (p - kLeNetPW2) : -1;
+// Finalise element o with gradient v: store the gradient; with the fused update apply SGD to the
+// master (w_old / m_old prefetched, or loaded here), re-emit the bf16 copies and scatter conv weights into
+// the next step's MFMA fragments; otherwise snapshot what the optimizer launch needs.
+__device__ __forceinline__ void red_apply(const LeNetRedArgs& a, const RedTables& t, Owned o, float v, bool pre,
+                                          float w_old, float m_old) {
+  if (o.di < 0) return;
+  t.g[o.di][o.i] = v;
+  const int wj = conv_wj(o);
   if (a.sgd_on) {
-    const int di = p < kLeNetPB1 ? 0 : p < kLeNetPW2 ? 1 : p < kLeNetPB2 ? 2 : 3;
-    const int i = p - (di == 0 ? 0 : di == 1 ? kLeNetPB1 : di == 2 ? kLeNetPW2 : kLeNetPB2);
-    const float nw = sgd_apply_one(a.sgd.d[di], i, v, a.sgd.master, a.sgd.mom, a.sgd.wbf, a.sgd.hyper);
+    const ParamDesc& d = t.d[o.di];
+    const long long off = d.off + o.i;
+    if (!pre) {
+      w_old = a.sgd.master[off];
+      m_old = a.sgd.mom != nullptr ? a.sgd.mom[off] : 0.f;
+    }
+    const float* h = t.hyper;
+    const float lr = h[0], mom = h[1], wd = h[2], gs = h[3];
+    float m_new = 0.f;
+    const float nw = sgd_new_weight(w_old, v, mom != 0.f ? m_old : 0.f, lr, mom, wd, gs, h[4] != 0.f, &m_new);
+    if (mom != 0.f) a.sgd.mom[off] = m_new;
+    a.sgd.master[off] = nw;
+    emit_copies(d, o.i, nw, a.sgd.wbf);
     // the new conv weight goes straight into the next step's MFMA fragments
     if (wj >= 0) lenet_frag_scatter(a.sgd.frag, wj, nw);
   } else if (a.snap != nullptr && wj >= 0) {
     // the conv kernels' weights and momentum as this gradient saw them: the optimizer launch rebuilds
     // the next step's fragments from these (no read of state it is overwriting)
-    const long long o = wj < 150 ? wj : wj - 150;
-    a.snap[wj] = wj < 150 ? a.w1[o] : a.w2[o];
-    a.snap[kLeNetConvW + wj] = a.m1 == nullptr ? 0.f : (wj < 150 ? a.m1[o] : a.m2[o]);
+    const long long q = wj < 150 ? wj : wj - 150;
+    a.snap[wj] = wj < 150 ? a.w1[q] : a.w2[q];
+    a.snap[kLeNetConvW + wj] = a.m1 == nullptr ? 0.f : (wj < 150 ? a.m1[q] : a.m2[q]);
   }
 }
 
@@ -860,7 +948,7 @@ constexpr unsigned kPSAccept = 1, kPSReject = 2, kPSFailed = 3, kPSFinished = 4;
 // takes the writer lock (seqlock CAS on the server's word), checks staleness = version_now -
 // version_pulled against the bound and completes the microbatch under the lock; the others wait for
 // the decision word tagged with this launch's epoch (local, agent scope: all of them are resident).
-__device__ void lenet_ps_decide(const LeNetRedArgs& a, unsigned* s_dec, unsigned* s_seq, bool after_completion = false) {
+__device__ __forceinline__ void lenet_ps_decide(const LeNetRedArgs& a, unsigned* s_dec, unsigned* s_seq, bool after_completion = false) {
   const PSArgs& p = a.ps;
   if (threadIdx.x == 0) {
     const unsigned ep = __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
@@ -957,44 +1045,9 @@ __device__ __forceinline__ float lenet_ps_elem(const LeNetRedArgs& a, const Para
   return wn;
 }
 
-__device__ __forceinline__ void dense_tile_ps(const LeNetRedArgs& a, int slot, float g, unsigned dec, unsigned seq) {
-  int tile = a.tile_of_block[slot];
-  int l = 0;
-  if (tile >= a.L[0].tiles) {
-    tile -= a.L[0].tiles;
-    l = 1;
-    if (tile >= a.L[1].tiles) {
-      tile -= a.L[1].tiles;
-      l = 2;
-    }
-  }
-  const LeNetDense& L = a.L[l];
-  const int tk = tile / ((L.N + 15) / 16), tn = tile - ((L.N + 15) / 16) * tk;
-  const int on = 16 * tn + (threadIdx.x >> 4), ok = 16 * tk + (threadIdx.x & 15);
-  if (on >= L.N || ok > L.K) return;
-  if (ok < L.K) L.gw[(long long)on * L.K + ok] = g;
-  else L.gb[on] = g;
-  lenet_ps_elem(a, a.sgd.d[4 + 2 * l + (ok == L.K ? 1 : 0)], ok < L.K ? on * L.K + ok : on, g, dec, seq);
-}
-
-__device__ __forceinline__ void conv_ps(const LeNetRedArgs& a, int cb, float g, unsigned dec, unsigned seq) {
-  const int p = cb * 64 + (threadIdx.x & 63);
-  if (p >= kLeNetConvParams) return;
-  float* dst = p < kLeNetPB1 ? a.g_w1 + p
-               : p < kLeNetPW2 ? a.g_b1 + (p - kLeNetPB1)
-               : p < kLeNetPB2 ? a.g_w2 + (p - kLeNetPW2)
-                               : a.g_b2 + (p - kLeNetPB2);
-  *dst = g;
-  const int di = p < kLeNetPB1 ? 0 : p < kLeNetPW2 ? 1 : p < kLeNetPB2 ? 2 : 3;
-  const int i = p - (di == 0 ? 0 : di == 1 ? kLeNetPB1 : di == 2 ? kLeNetPW2 : kLeNetPB2);
-  const float w = lenet_ps_elem(a, a.sgd.d[di], i, g, dec, seq);
-  const int wj = p < kLeNetPB1 ? p : (p >= kLeNetPW2 && p < kLeNetPB2) ? 150 + (p - kLeNetPW2) : -1;
-  if (wj >= 0) lenet_frag_scatter(a.sgd.frag, wj, w);  // the next step's conv fragments
-}
-
-// Arrival of one of the nexch + 1 protocol workgroups (exchanging + staging): the last one publishes
+// Arrival of one of the G + 1 protocol workgroups (job workgroups + staging): the last one publishes
 // version v + 1 (admitted) or releases the lock (rejected) and records the pulled version.
-__device__ void lenet_ps_arrive(const LeNetRedArgs& a, int arrivals, unsigned dec, unsigned seq) {
+__device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, int arrivals) {
   const PSArgs& p = a.ps;
   // every storing wave drains its shared-master stores (uncached / fine-grained memory: complete at the
   // server's HBM once acknowledged), then the arrival ticket; the last arriver's system-scope release
@@ -1009,6 +1062,10 @@ __device__ void lenet_ps_arrive(const LeNetRedArgs& a, int arrivals, unsigned de
                                                                  __HIP_MEMORY_SCOPE_AGENT) + 1u,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every workgroup's arrival happened before the unlock
+      // this launch's decision (workgroup 0 published it before arriving; workgroups that own no slot
+      // never read it)
+      const unsigned dec = __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 7u;
+      const unsigned seq = __hip_atomic_load(p.scratch + kPSLockedSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (dec == kPSAccept) {
         *p.vpulled = (seq >> 1) + 1u;
         __hip_atomic_store(p.seq, seq + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1020,16 +1077,19 @@ __device__ void lenet_ps_arrive(const LeNetRedArgs& a, int arrivals, unsigned de
   }
 }
 
-constexpr int kMaxSlotsPerBlock = 8;
 
-// Exchange workgroups [0, exch_blocks) own slots blockIdx.x + k * exch_blocks: all their slots' local
-// sums are computed and pushed to the peers first, then each is waited for, summed over the ranks and
-// applied (one round trip per workgroup, not per slot).  On a node with one rank per GPU exch_blocks ==
-// slots (one each, every workgroup resident); ranks that time-share one GPU use fewer, so that the
-// waiting workgroups of all ranks fit on the chip beside the peers' train kernels.
-// Then one workgroup: loss partials -> stats; one more (index stream bound): stage the next batch.
-// diagnostic phase clocks of the reduce launch: stamps[block][slot] (0 start, 1 local sums pushed,
-// 2 decision / exchange done, 3 applied, 4 end, 5 all waves started, 6 first slot summed)
+// async PS: finalise element o with gradient g under this launch's decision
+__device__ __forceinline__ void red_ps(const LeNetRedArgs& a, const RedTables& t, Owned o, float g, unsigned dec,
+                                       unsigned seq) {
+  if (o.di < 0) return;
+  t.g[o.di][o.i] = g;
+  const float w = lenet_ps_elem(a, t.d[o.di], o.i, g, dec, seq);
+  const int wj = conv_wj(o);
+  if (wj >= 0) lenet_frag_scatter(a.sgd.frag, wj, w);  // the next step's conv fragments
+}
+
+// diagnostic phase clocks of the reduce launch: stamps[block][slot] (0 start, 1 jobs done, 2 decision,
+// 3 owned slots applied, 4 end, 6 first job's partial computed, 7 first ownership combine done)
 #define LR_STAMP(slot)                                                            \
   do {                                                                            \
     if (a.stamps) {                                                               \
@@ -1041,73 +1101,145 @@ constexpr int kMaxSlotsPerBlock = 8;
     }                                                                             \
   } while (0)
 
-__global__ void __launch_bounds__(RT, 8) lenet_reduce_kernel(LeNetRedArgs a) {
-  __shared__ float red[16][16][17];
+__global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
+  __shared__ float red[4 * kSlotVals];
+  __shared__ RedTables tabs;
+  __shared__ int owned[kMaxOwned];
+  __shared__ unsigned ep[kMaxOwned];
   __shared__ unsigned s_e;
+  __shared__ int s_last;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   LR_STAMP(0);
-  if (a.stamps) {
-    __syncthreads();
-    LR_STAMP(5);  // every wave of the workgroup has started
-  }
-  const int nslot = a.dense_tiles + a.nconv_blocks;
-  const int nexch = a.exch_blocks;
-  if ((int)blockIdx.x < nexch) {
-    __shared__ float keep[kMaxSlotsPerBlock][256];  // this workgroup's local sums, per slot and position
-    __shared__ unsigned ep[kMaxSlotsPerBlock];
+  const int nslot = a.dense_tiles + a.nconv_slots;
+  const int G = a.exch_blocks;
+  if ((int)blockIdx.x < G) {
+    stage_tables(a, &tabs);
+    // with the fused sync update, the first owned slot's master / momentum elements are loaded beside
+    // its slab loads
+    const bool pre = a.sgd_on && !a.ps_on;
+    __shared__ float w_pre[kPerThread][RT], m_pre[kPerThread][RT];  // (LDS: not live across the jobs in VGPRs)
+    __shared__ float own0[kPerThread][RT];  // the first owned slot's local sums
+    int nown = 0;
 #pragma unroll 1
-    for (int k = 0; k < kMaxSlotsPerBlock; ++k) {
-      const int slot = blockIdx.x + k * nexch;
-      if (slot >= nslot) break;  // uniform over the workgroup
-      __syncthreads();           // the previous slot's readers of red are done
-      const bool dense = slot < a.dense_tiles;
-      const float v = dense ? dense_tile_value(a, slot, red) : conv_value(a, slot - a.dense_tiles, red);
-      if (k == 0) LR_STAMP(6);  // the first slot's partial sums are in
-      const bool owner = dense ? threadIdx.x < 256 : wid == 0;
-      if (owner) keep[k][threadIdx.x] = v;
-      if (a.ll_on) {
-        const unsigned e = ll_epoch(a.ll, slot, &s_e);
-        if (threadIdx.x == 0) ep[k] = e;
-        if (owner) ll_push(a.ll, slot, threadIdx.x, e, v);
+    for (int j = blockIdx.x; j < nslot * kChunks; j += G) {
+      const int slot = j / kChunks, c = j - kChunks * (j / kChunks);
+      __syncthreads();  // red / tabs / s_last of the previous job
+      float part[kPerThread];
+      if (slot < a.dense_tiles) dense_job(a, tabs, slot, c, red, part);
+      else conv_job(a, slot - a.dense_tiles, c, red, part);
+      if (j == (int)blockIdx.x) LR_STAMP(6);
+      // publish the slab write-through, then the ticket (every storing wave drains first)
+      const int npos = slot < a.dense_tiles ? kPerThread : 1;
+      float* slab = a.slabs + (long long)slot * kChunks * kSlotVals;
+#pragma unroll
+      for (int e = 0; e < kPerThread; ++e)
+        if (e < npos)
+          __hip_atomic_store(slab + c * kSlotVals + threadIdx.x + RT * e, part[e], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(a.tickets + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == (unsigned)(kChunks - 1);
+        if (last) __hip_atomic_store(a.tickets + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = last;
       }
+      __syncthreads();
+      if (!s_last) continue;
+      // the slot's owner: local sum of the 8 slabs in chunk order
+      if (nown >= kMaxOwned) {  // host guarantees G >= 8 * nslot / kMaxOwned; never spin on a missing owner
+        if (threadIdx.x == 0 && a.ll_on) atomicOr(a.ll.err, 2);
+        continue;
+      }
+      if (nown == 0 && pre) {
+#pragma unroll
+        for (int e = 0; e < kPerThread; ++e) {
+          float w = 0.f, m = 0.f;
+          if (e < npos) {
+            const Owned o = owned_elem(a, tabs, slot, threadIdx.x + RT * e);
+            if (o.di >= 0) {
+              const long long off = tabs.d[o.di].off + o.i;
+              w = a.sgd.master[off];
+              m = a.sgd.mom != nullptr ? a.sgd.mom[off] : 0.f;
+            }
+          }
+          w_pre[e][threadIdx.x] = w;
+          m_pre[e][threadIdx.x] = m;
+        }
+      }
+      // write-through (sc1) buffer loads of the slabs, all in flight (an atomic load per value would wait
+      // for each one)
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, kChunks * kSlotVals * 4, 0x00020000);
+      float x[kChunks][kPerThread];
+#pragma unroll
+      for (int cc = 0; cc < kChunks; ++cc)
+#pragma unroll
+        for (int e = 0; e < kPerThread; ++e)
+          x[cc][e] = e < npos ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                              rs, (cc * kSlotVals + threadIdx.x + RT * e) * 4, 0, 16))
+                              : 0.f;
+      float v[kPerThread];
+#pragma unroll
+      for (int e = 0; e < kPerThread; ++e) {
+        v[e] = x[0][e];
+#pragma unroll
+        for (int cc = 1; cc < kChunks; ++cc) v[e] += x[cc][e];
+      }
+      // keep the local sums: the first owned slot's in LDS, later ones (shared-GPU runs) in chunk 0's slab
+      // (read back by the same threads after the jobs)
+#pragma unroll
+      for (int e = 0; e < kPerThread; ++e)
+        if (e < npos) {
+          if (nown == 0) own0[e][threadIdx.x] = v[e];
+          else slab[threadIdx.x + RT * e] = v[e];
+        }
+      if (a.ll_on) {
+        const unsigned ee = ll_epoch(a.ll, slot, &s_e);
+        if (threadIdx.x == 0) ep[nown] = ee;
+#pragma unroll
+        for (int e = 0; e < kPerThread; ++e)
+          if (e < npos) ll_push(a.ll, slot, threadIdx.x + RT * e, ee, v[e]);
+      }
+      if (threadIdx.x == 0) owned[nown] = slot;
+      ++nown;
+      if (nown == 1) LR_STAMP(7);
     }
     __syncthreads();
     LR_STAMP(1);
     __shared__ unsigned s_dec, s_seq;
-    if (a.ps_on) lenet_ps_decide(a, &s_dec, &s_seq);
+    if (a.ps_on && (nown > 0 || blockIdx.x == 0)) lenet_ps_decide(a, &s_dec, &s_seq);  // 0 takes the lock
     LR_STAMP(2);
     const unsigned dec = a.ps_on ? s_dec : 0u, seq = a.ps_on ? s_seq : 0u;
 #pragma unroll 1
-    for (int k = 0; k < kMaxSlotsPerBlock; ++k) {
-      const int slot = blockIdx.x + k * nexch;
-      if (slot >= nslot) break;
-      const bool dense = slot < a.dense_tiles;
-      if (a.ps_on) {
-        if ((dense ? threadIdx.x < 256 : wid == 0) && (dec == kPSAccept || dec == kPSReject)) {
-          if (dense) dense_tile_ps(a, slot, keep[k][threadIdx.x], dec, seq);
-          else conv_ps(a, slot - a.dense_tiles, keep[k][threadIdx.x], dec, seq);
+    for (int k = 0; k < nown; ++k) {
+      const int slot = owned[k];
+      const int npos = slot < a.dense_tiles ? kPerThread : 1;
+      const float* sum = a.slabs + (long long)slot * kChunks * kSlotVals;
+#pragma unroll
+      for (int e = 0; e < kPerThread; ++e) {
+        if (e >= npos) break;
+        const int pos = threadIdx.x + RT * e;
+        const Owned o = owned_elem(a, tabs, slot, pos);
+        float v = k == 0 ? own0[e][threadIdx.x] : sum[pos];
+        if (a.ps_on) {
+          if (dec == kPSAccept || dec == kPSReject) red_ps(a, tabs, o, v, dec, seq);
+          continue;
         }
-        continue;
-      }
-      if (dense ? threadIdx.x < 256 : wid == 0) {
-        float v = keep[k][threadIdx.x];
         bool ok = true;
-        if (a.ll_on) {  // the rank-order sum over the ranks (no all-reduce launch)
-          ok = ll_wait_sum(a.ll, slot, threadIdx.x, ep[k], v, v);
-          if (ok && threadIdx.x == 0) ll_commit(a.ll, slot, ep[k]);
-        }
-        if (ok) {
-          if (dense) dense_tile_apply(a, slot, v);
-          else conv_apply(a, slot - a.dense_tiles, v);
-        }
+        if (a.ll_on) ok = ll_wait_sum(a.ll, slot, pos, ep[k], v, v);  // the rank-order sum (no all-reduce launch)
+        if (ok) red_apply(a, tabs, o, v, k == 0 && pre, w_pre[e][threadIdx.x], m_pre[e][threadIdx.x]);
+      }
+      if (a.ll_on) {
+        __syncthreads();  // every position of the slot consumed before its epoch advances
+        ll_commit(a.ll, slot, ep[k]);
       }
     }
     LR_STAMP(3);
-    if (a.ps_on) lenet_ps_arrive(a, nexch + 1, dec, seq);
+    if (a.ps_on) lenet_ps_arrive(a, G + 1);
     LR_STAMP(4);
     return;
   }
-  const int blk = blockIdx.x - nexch;
+  const int blk = blockIdx.x - G;
   if (blk == 1 && a.ps_on) {
     // async: once this launch's decision is known (the current microbatch is completed under the lock),
     // claim the next microbatch FCFS on the server and stage its example indices
@@ -1123,27 +1255,45 @@ __global__ void __launch_bounds__(RT, 8) lenet_reduce_kernel(LeNetRedArgs a) {
     __syncthreads();
     if (threadIdx.x == 0) *a.ps.bid_out = s_bid;
     ps_stage_indices(a.ps, s_bid, threadIdx.x, RT);
-    lenet_ps_arrive(a, nexch + 1, s_dec, s_seq);
+    lenet_ps_arrive(a, G + 1);
+    LR_STAMP(1);
     return;
   }
   if (blk == 1) {  // fused update: stage the next step's batch indices, advance the cursor
     __shared__ long long nxt;
     if (threadIdx.x == 0) nxt = (*a.sgd.cursor + 1) % a.sgd.nsteps;
     __syncthreads();
-    const long long* src = a.sgd.src + nxt * a.sgd.B;
-    for (int i = threadIdx.x; i < a.sgd.B; i += RT) a.sgd.dst[i] = src[i];
+    copy_i64(a.sgd.dst, a.sgd.src + nxt * a.sgd.B, a.sgd.B, threadIdx.x, RT);
     if (threadIdx.x == 0) *a.sgd.cursor = nxt;
+    LR_STAMP(1);
     return;
   }
-  if (wid == 0) {  // loss partials -> stats
-    float l = 0.f, c = 0.f;
-    for (int k = lane; k < a.nblk; k += 64) {
-      l += a.loss_part[2 * k];
-      c += a.loss_part[2 * k + 1];
+  {  // loss partials -> stats: every load of the block in flight at once, fixed-order sums
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2* lp = reinterpret_cast<const f32x2*>(a.loss_part);
+    f32x2 acc = {0.f, 0.f};
+    for (int k0 = threadIdx.x; k0 < a.nblk; k0 += RT * 8) {
+      f32x2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = k0 + RT * u < a.nblk ? lp[k0 + RT * u] : f32x2{0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
     }
-    l = wave_sum(l);
-    c = wave_sum(c);
+    float l = wave_sum(acc.x), c = wave_sum(acc.y);
+    __shared__ float s_lc[2][RT / 64];
     if (lane == 0) {
+      s_lc[0][wid] = l;
+      s_lc[1][wid] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      l = s_lc[0][0];
+      c = s_lc[1][0];
+#pragma unroll
+      for (int w = 1; w < RT / 64; ++w) {
+        l += s_lc[0][w];
+        c += s_lc[1][w];
+      }
       a.stats[0] = l;
       a.stats[1] = c;
       if (a.sgd_on && a.sgd.run_stats != nullptr) {  // device run statistics (trainer callbacks)
@@ -1153,6 +1303,7 @@ __global__ void __launch_bounds__(RT, 8) lenet_reduce_kernel(LeNetRedArgs a) {
       }
     }
   }
+  LR_STAMP(1);
 }
 
 }  // namespace
@@ -1164,7 +1315,19 @@ static unsigned long long* g_lenet_stamps_host = nullptr;
 void lenet_set_stamps(void* buf) { g_lenet_stamps_host = reinterpret_cast<unsigned long long*>(buf); }
 
 size_t lenet_frag_bytes() { return (size_t)NFRAG * 64 * 16; }
-int lenet_dense_part_floats(int B) { (void)B; return 0; }
+
+// reduce scratch (the trainer's dense_part buffer, zero-initialised): job slabs + arrival tickets
+static int lenet_red_slots() {
+  const int NK[3][2] = {{120, 400}, {84, 120}, {10, 84}};
+  int n = (kLeNetConvParams + kConvPer - 1) / kConvPer;
+  for (auto& nk : NK) n += ((nk[0] + kDU - 1) / kDU) * ((nk[1] + 1 + kDU - 1) / kDU);
+  return n;
+}
+int lenet_dense_part_floats(int B) {
+  (void)B;
+  return lenet_red_slots() * kChunks * kSlotVals + (lenet_red_slots() + 3) / 4 * 4;
+}
+int lenet_red_slab_floats() { return lenet_red_slots() * kChunks * kSlotVals; }
 
 hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   LeNetArgs a = a_in;
@@ -1183,49 +1346,51 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   DFA_HIP_CHECK(hipGetLastError());
   r.nblk = nblk;
   r.ldt = a.ldt;
-  r.nconv_blocks = (kLeNetConvParams + 63) / 64;
-  // dense tiles in (layer, tk, tn) order, tn fastest; XCD x (= block id mod 8) takes the tiles with
-  // tk = x (mod 8) of every layer, so all 16-row groups of H^T stay in one L2
-  int tiles_per_layer[3], base = 0;
-  std::vector<int> by_xcd[8];
+  if (r.kcols <= 0 || r.kcols % 32 || r.kcols > a.ldt || r.kcols < a.B) return hipErrorInvalidValue;
+  r.nconv_slots = (kLeNetConvParams + kConvPer - 1) / kConvPer;
+  // dense units in (layer, tk, tn) order, tn fastest
+  int base = 0;
   for (int l = 0; l < 3; ++l) {
-    const int nt = (r.L[l].N + 15) / 16, kt = (r.L[l].K + 1 + 15) / 16;
-    r.L[l].tiles = nt * kt;
-    tiles_per_layer[l] = nt * kt;
-    for (int tk = 0; tk < kt; ++tk)
-      for (int tn = 0; tn < nt; ++tn) by_xcd[tk % 8].push_back(base + tk * nt + tn);
-    base += nt * kt;
+    r.L[l].tiles = ((r.L[l].N + kDU - 1) / kDU) * ((r.L[l].K + 1 + kDU - 1) / kDU);
+    base += r.L[l].tiles;
   }
-  (void)tiles_per_layer;
   r.dense_tiles = base;
-  if (r.dense_tiles > kLeNetMaxTiles) return hipErrorInvalidValue;
-  size_t maxq = 0;
-  for (auto& v : by_xcd) maxq = std::max(maxq, v.size());
-  int b = 0;
-  std::vector<int> order;
-  for (size_t slot = 0; slot < maxq; ++slot)
-    for (int x = 0; x < 8; ++x)
-      if (slot < by_xcd[x].size()) order.push_back(by_xcd[x][slot]);
-  for (int t : order) r.tile_of_block[b++] = t;
+  // the kernel's LDS table image
+  for (int l = 0; l < 3; ++l) {
+    r.tab.L[l] = r.L[l];
+    r.tab.g[4 + 2 * l] = r.L[l].gw;
+    r.tab.g[5 + 2 * l] = r.L[l].gb;
+  }
+  r.tab.g[0] = r.g_w1;
+  r.tab.g[1] = r.g_b1;
+  r.tab.g[2] = r.g_w2;
+  r.tab.g[3] = r.g_b2;
+  for (int j = 0; j < 10; ++j) r.tab.d[j] = r.sgd.d[j];
+  // chunk c of the batch = the columns of XCD c's train workgroups (lenet_img_group) when B = 4096
+  r.chunk_cols = ((r.kcols + kChunks - 1) / kChunks + 31) / 32 * 32;
+  if (!r.slabs || !r.tickets) return hipErrorInvalidValue;
   if (r.sgd_on && (!r.sgd.master || !r.sgd.wbf || !r.sgd.hyper || !r.sgd.frag))
     return hipErrorInvalidValue;
-  const int nslot = r.dense_tiles + r.nconv_blocks;
-  if (r.exch_blocks <= 0 || r.exch_blocks > nslot) r.exch_blocks = nslot;
-  if (r.exch_blocks * kMaxSlotsPerBlock < nslot) return hipErrorInvalidValue;
+  const int nslot = r.dense_tiles + r.nconv_slots;
+  const int njobs = nslot * kChunks;
+  if (r.exch_blocks <= 0 || r.exch_blocks > njobs) r.exch_blocks = njobs;
+  // a workgroup runs <= ceil(njobs / G) jobs, so it owns at most that many slots
+  if ((long long)r.exch_blocks * kMaxOwned < njobs) return hipErrorInvalidValue;
+  // 256-thread workgroups at <= 128 VGPRs and ~17 KB LDS: 4 per CU, 1024 on the chip
   if (r.ll_on) {
-    // slot s is LL slot s.  Every exchanging workgroup must be resident at once on every rank (a waiting
-    // workgroup must never keep a peer's from being dispatched): 1024-thread workgroups at 64 VGPRs and
-    // 28 KB LDS run 2 per CU, so <= 512 on 256 CUs with one rank per GPU
+    // slot s is LL slot s.  Every workgroup that owns a slot waits for the peers' sums of it, so all job
+    // workgroups must fit on the chip at once (a waiting owner must never keep a job it depends on, here
+    // or on a peer, from being dispatched)
     if (!r.sgd_on || r.ll.world < 2 || r.ll.world > kP2PMaxRanks || r.ll.rank < 0 || r.ll.rank >= r.ll.world ||
-        !r.ll.epochs || !r.ll.err || nslot > r.ll.nslots || r.exch_blocks > 512)
+        !r.ll.epochs || !r.ll.err || nslot > r.ll.nslots || r.exch_blocks + 2 > 1024)
       return hipErrorInvalidValue;
     for (int k = 0; k < r.ll.world; ++k)
       if (!r.ll.bases[k]) return hipErrorInvalidValue;
   }
   if (r.ps_on) {
-    // async PS: every protocol workgroup must be resident at once (workgroup 0's decision is awaited)
+    // async PS: the owners wait for workgroup 0's decision (dispatched first)
     if (!r.sgd_on || r.ll_on || r.sgd.src || !r.ps.seq || !r.ps.ps_w || !r.ps.vpulled || !r.ps.bid_out ||
-        !r.ps.stats || !r.ps.scratch || r.exch_blocks + 1 > 512 || r.sgd.mom)
+        !r.ps.stats || !r.ps.scratch || r.exch_blocks + 2 > 1024 || r.sgd.mom)
       return hipErrorInvalidValue;
   }
   const int extra = ((r.sgd_on && r.sgd.src) || r.ps_on) ? 1 : 0;  // the index-staging workgroup

@@ -102,21 +102,40 @@ __device__ inline void complete_microbatch(const PSArgs& a, long long bid) {
 
 // Stage microbatch `bid`'s example indices (perm row) into the static index buffer: 16-byte copies, all
 // loads of a thread in flight before its stores (B even, rows 16-byte aligned).  One workgroup.
+// Block-wide copy of n int64 with every load of a pass in flight before its stores (a plain strided copy
+// loop waits one memory round trip per iteration).  16-byte vectors when both ends are 16-byte aligned.
+__device__ inline void copy_i64(long long* __restrict__ dst, const long long* __restrict__ src, int n, int t, int nt) {
+  typedef long long i64x2 __attribute__((ext_vector_type(2)));
+  int done = 0;
+  if ((((unsigned long long)src | (unsigned long long)dst) & 15) == 0) {
+    const int nv = n >> 1;
+    const i64x2* s2 = reinterpret_cast<const i64x2*>(src);
+    i64x2* d2 = reinterpret_cast<i64x2*>(dst);
+    for (int base = t; base < nv; base += nt * 8) {
+      i64x2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (base + u * nt < nv) v[u] = s2[base + u * nt];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (base + u * nt < nv) d2[base + u * nt] = v[u];
+    }
+    done = 2 * nv;
+  }
+  for (int base = done + t; base < n; base += nt * 8) {
+    long long v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (base + u * nt < n) v[u] = src[base + u * nt];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (base + u * nt < n) dst[base + u * nt] = v[u];
+  }
+}
+
 __device__ inline void ps_stage_indices(const PSArgs& a, long long bid, int t, int nt) {
   if (a.perm == nullptr || bid < 0) return;
-  typedef long long i64x2 __attribute__((ext_vector_type(2)));
-  const i64x2* src = reinterpret_cast<const i64x2*>(a.perm + (bid & 0xffffffffLL) * a.B);
-  i64x2* dst = reinterpret_cast<i64x2*>(a.idx);
-  const int nv = a.B >> 1;
-  for (int base = t; base < nv; base += nt * 8) {
-    i64x2 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (base + u * nt < nv) v[u] = src[base + u * nt];
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (base + u * nt < nv) dst[base + u * nt] = v[u];
-  }
+  copy_i64(a.idx, a.perm + (bid & 0xffffffffLL) * a.B, a.B, t, nt);
 }
 
 }  // namespace dfa

@@ -279,6 +279,10 @@ class Net:
         self.y_buf = torch.empty((B,), dtype=torch.int32, device=self.device)
         if self.head_start is not None:
             ldt = (B + 31) // 32 * 32  # transposed activation / gradient buffers, zero tail columns
+            if self.lenet_fused:
+                # row stride 256 B past a multiple of 8 KB: the 16 rows of one MFMA operand load land on
+                # 16 different L2 channels instead of one (csrc/lenet_fused.hip dense_unit_value)
+                ldt += 128
             head = self.exec_layers[self.head_start:]
             z = lambda *shape: torch.zeros(shape, dtype=self.dtype, device=self.device)  # noqa: E731
             self.head_xT = z(head[0].in_features, ldt)
@@ -287,10 +291,10 @@ class Net:
             self.head_loss_part = torch.zeros(2 * ((B + 15) // 16), dtype=torch.float32, device=self.device)
         if self.lenet_fused:
             nblk = ops.lenet_blocks(B)
-            # [2572 conv parameters][round_up(workgroups, 512)]: parameter-major, zero padding never written
-            self.lenet_conv_part = torch.zeros(2572 * ((nblk + 511) // 512 * 512), dtype=torch.float32,
-                                               device=self.device)
-            self.lenet_dense_part = torch.empty(1, dtype=torch.float32, device=self.device)
+            self.lenet_conv_part = torch.empty(2576 * nblk, dtype=torch.float32, device=self.device)
+            # reduce-launch scratch: job partial slabs + arrival tickets (must start zeroed)
+            self.lenet_dense_part = torch.zeros(ops.lenet_dense_part_floats(B), dtype=torch.float32,
+                                                device=self.device)
             self.lenet_loss_part = torch.zeros(2 * nblk, dtype=torch.float32, device=self.device)
         self._bound_B = B
         self.graphs = {}

@@ -34,7 +34,7 @@ import torch.distributed as dist
 
 from .. import native
 from ..diagnostics import on as diag_on
-from .data_parallel import DataParallelTrainer
+from .data_parallel import DataParallelTrainer, shared_gpu_exch_blocks
 
 
 class AsyncPSTrainer(DataParallelTrainer):
@@ -81,9 +81,7 @@ class AsyncPSTrainer(DataParallelTrainer):
             # ranks that time-share one GPU: fewer protocol workgroups per rank (each owning several
             # slots), so every rank's workgroups waiting for its lock decision fit on the chip beside the
             # lock holder's (one rank per GPU: one workgroup per slot, all resident)
-            ndev = max(1, torch.cuda.device_count())
-            share = -(-self.world // ndev) if ndev < self.world else 1
-            net.lenet_exch_blocks = 0 if share == 1 else max(48, 256 // share)
+            net.lenet_exch_blocks = shared_gpu_exch_blocks(self.world)
         self._primed = False
         self._ps_stats_dev = self.ps.stats_tensor()  # device view of this rank's PS counters (callbacks)
         from .watchdog import register_owner_probe

@@ -132,9 +132,7 @@ class DataParallelTrainer:
             # ranks that time-share one GPU (rehearsals): the fused LeNet-5 reduce runs fewer exchanging
             # workgroups (each owning several slots) so that every rank's waiting workgroups fit on the chip
             # beside the peers' train kernels; with one rank per GPU every slot gets its own workgroup
-            ndev = max(1, torch.cuda.device_count())
-            share = -(-self.world // ndev) if ndev < self.world else 1
-            self.net.lenet_exch_blocks = 0 if share == 1 else max(48, 256 // share)
+            self.net.lenet_exch_blocks = shared_gpu_exch_blocks(self.world)
 
     def _reduce(self, t: torch.Tensor, async_op: bool):
         if self.p2p is not None and t.numel() * 4 <= self.p2p_limit:
@@ -226,7 +224,7 @@ class DataParallelTrainer:
             return False
         if self.world == 1 or not self._step_all_reduces:
             return True  # no exchange inside the step (single rank, FedAvg local steps)
-        return (self.p2p is not None and getattr(self.p2p.comm, "ll_slots", 0) >= 512
+        return (self.p2p is not None and getattr(self.p2p.comm, "ll_slots", 0) >= 256
                 and self.net.store.total * 4 <= self.p2p_limit)
 
     @property
@@ -599,6 +597,15 @@ def _beat(step: int):
     from .watchdog import beat
 
     beat(step)
+
+
+def shared_gpu_exch_blocks(world: int) -> int:
+    """Job workgroups of the fused LeNet-5 reduce launch per rank: 0 (one per job) with a GPU per rank;
+    with ranks time-sharing one GPU, few enough (a multiple of 8, each running <= 16 jobs) that every
+    rank's waiting workgroups (256 threads, 4 per CU) fit on the chip at once beside the peers' kernels."""
+    ndev = max(1, torch.cuda.device_count())
+    share = -(-world // ndev) if ndev < world else 1
+    return 0 if share == 1 else max(64, (512 // share) // 8 * 8)
 
 
 def epoch_permutations(n: int, batch: int, steps: int, device, seed: int = 0):

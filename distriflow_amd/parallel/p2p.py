@@ -39,7 +39,7 @@ class P2PAllReduce:
     """In-place SUM all-reduce of fp32 GPU tensors of up to ``max_bytes`` over IPC-mapped peer buffers."""
 
     def __init__(self, group=None, max_bytes: int = 8 << 20, timeout_s: float = 30.0, self_test: bool = True,
-                 ll_slots: int = 512):
+                 ll_slots: int = 256):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)

@@ -8,5 +8,5 @@ mkdir -p gpurun_out
 for p in 0 1 2; do
   echo "=== lenet_red_probe=$p"
   DISTRIFLOW_DIAG=lenet_red_probe=$p timeout -k 10 200 python scripts/lenetstamps.py 4096 step > gpurun_out/stamps_p$p.log 2>&1 || { tail -n 30 gpurun_out/stamps_p$p.log; exit 1; }
-  grep -A 12 "dense  blocks" gpurun_out/stamps_p$p.log
+  grep -A 10 "dense  jobs" gpurun_out/stamps_p$p.log
 done

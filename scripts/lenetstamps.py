@@ -41,7 +41,7 @@ def main():
 
     base = wall()
     nblk = ops.lenet_blocks(B)
-    buf = torch.zeros(max(nblk * 16, 4096 * 32), dtype=torch.int64, device="cuda")
+    buf = torch.zeros(4096 * 32, dtype=torch.int64, device="cuda")
     m.convpool_set_stamps(buf)
     stamped = wall(5)
     m.convpool_set_stamps(None)
@@ -71,26 +71,36 @@ def main():
         torch.cuda.synchronize()
         m.convpool_set_stamps(None)
         t_end_train = buf[: nblk * 16].view(nblk, 16).cpu().numpy().astype(np.int64)[:, 10].max()
-        r = buf[4096 * 16: 4096 * 16 + 512 * 8].view(512, 8).cpu().numpy().astype(np.int64)
-        kinds = np.array(["dense"] * 262 + ["conv"] * 41 + ["loss", "stage"] + ["-"] * (512 - 305))
+        G = 2048
+        r = buf[4096 * 16: 4096 * 16 + G * 8].view(G, 8).cpu().numpy().astype(np.int64)
+        # job workgroup j runs job j = slot * 8 + chunk: slots are 32 x 32 dense units of (400 -> 120),
+        # (120 -> 84), (84 -> 10) incl. bias, then 256-parameter conv slots; then loss, staging
+        nd = sum(-(-n // 32) * -(-(k + 1) // 32) for k, n in ((400, 120), (120, 84), (84, 10)))
+        nc = -(-2572 // 256)
+        nj = 8 * (nd + nc)
+        kinds = np.array(["dense"] * (8 * nd) + ["conv"] * (8 * nc) + ["loss", "stage"] + ["-"] * (G - nj - 2))
         valid = r[:, 0] > 0
-        for kind in ("dense", "conv", "loss", "stage"):
+        for kind in ("dense", "conv"):
             sel = valid & (kinds == kind)
             if sel.any():
-                life = np.where(r[sel, 4] > 0, r[sel, 4], np.where(r[sel, 3] > 0, r[sel, 3], r[sel, 1])) - r[sel, 0]
-                sums = r[sel, 1] - r[sel, 0]
-                print(f"  {kind:<6} blocks {sel.sum():4d}: local sums median {np.median(sums):7.0f} max {sums.max():7.0f};"
+                job = r[sel, 6] - r[sel, 0]
+                own = sel & (r[:, 7] > 0)
+                life = r[sel, 4] - r[sel, 0]
+                print(f"  {kind:<6} jobs {sel.sum():4d}: job median {np.median(job):7.0f} max {job.max():7.0f};"
                       f" lifetime median {np.median(life):7.0f} max {life.max():7.0f}")
-                if kind in ("dense", "conv"):
-                    wl, s1 = r[sel, 5] - r[sel, 0], r[sel, 6] - r[sel, 5]
-                    print(f"         waves started after median {np.median(wl):7.0f} max {wl.max():7.0f}; first slot "
-                          f"summed median {np.median(s1):7.0f} max {s1.max():7.0f}")
-        r = r[r[:, 0] > 0]
-        print(f"reduce launch: {r.shape[0]} stamped workgroups; first start {r[:, 0].min() - t_end_train} after the "
-              f"last train workgroup's end; start spread {r[:, 0].max() - r[:, 0].min()}")
-        ends = np.where(r[:, 4] > 0, r[:, 4], r[:, 3])
-        print(f"  ends: median {np.median(ends - r[:, 0].min()):.0f}  max {ends.max() - r[:, 0].min():.0f} after the first start")
-        for k, name in enumerate(["local sums", "decision/exchange", "apply", "arrive"]):
+                if own.any():
+                    comb = r[own, 7] - r[own, 6]
+                    app = r[own, 3] - r[own, 2]
+                    print(f"         owners {own.sum():4d}: ticket+combine median {np.median(comb):7.0f} max "
+                          f"{comb.max():7.0f}; apply median {np.median(app):7.0f} max {app.max():7.0f}")
+        for kind in ("loss", "stage"):
+            sel = valid & (kinds == kind)
+            if sel.any():
+                print(f"  {kind:<6} workgroup lifetime {int((r[sel, 1] - r[sel, 0])[0]):7d}")
+        r = r[valid]
+        print(f"reduce launch: {r.shape[0]} stamped workgroups (per-XCD clocks: only in-workgroup spans are "
+              f"meaningful)")
+        for k, name in enumerate(["jobs (all)", "decision", "apply", "arrive"]):
             ok = (r[:, k + 1] > 0) & (r[:, k] > 0)
             col = r[ok, k + 1] - r[ok, k]
             if col.size:

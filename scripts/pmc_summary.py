@@ -18,4 +18,5 @@ cols = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_
         "SQ_VALU_MFMA_BUSY_CYCLES", "FETCH_SIZE", "WRITE_SIZE", "SQ_LDS_IDX_ACTIVE"]
 for k, c in sorted(vals.items()):
     print(k)
-    print("   " + "  ".join(f"{n.replace('SQ_', '')}={sum(c[n]) / len(c[n]):.3g}" for n in cols if c.get(n)))
+    names = [n for n in cols if c.get(n)] + sorted(n for n in c if n not in cols)
+    print("   " + "  ".join(f"{n.replace('SQ_', '')}={sum(c[n]) / len(c[n]):.3g}" for n in names))
