@@ -260,6 +260,7 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < kPSUnroll; ++u) {
+#pragma clang fp contract(off)  // the same rounding as the fused reduce launch's ps_new_weight
         const long long i = base + (long long)u * kPSBlock;
         if (i < (hi >> 2)) wn[i] = v[u] - lr * gv[u];
       }

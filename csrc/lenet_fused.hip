@@ -905,33 +905,47 @@ __device__ __forceinline__ void conv_job(const LeNetRedArgs& a, int s, int c, fl
   for (int e = 1; e < kPerThread; ++e) out[e] = 0.f;
 }
 
-// Finalise element o with gradient v: store the gradient; with the fused update apply SGD to the
-// master (w_old / m_old prefetched, or loaded here), re-emit the bf16 copies and scatter conv weights into
-// the next step's MFMA fragments; otherwise snapshot what the optimizer launch needs.
-__device__ __forceinline__ void red_apply(const LeNetRedArgs& a, const RedTables& t, Owned o, float v, bool pre,
-                                          float w_old, float m_old) {
+// The new value w of element o becomes the local master and its bf16 compute copies (and, for a conv
+// weight, the next step's MFMA fragment).  Dense elements (di >= 4) take the tile-layout copy path only
+// (the launcher checks their descriptors): one small inlined body per position instead of the general
+// layout switch, which the conv slots (one position per thread) keep.
+template <bool DENSE>
+__device__ __forceinline__ void red_emit(const LeNetRedArgs& a, const RedTables& t, Owned o, float w) {
+  const ParamDesc& d = t.d[o.di];
+  a.sgd.master[d.off + o.i] = w;
+  if (DENSE) {
+    if (d.bf_off < 0) return;  // a bias
+    const int K = d.T * d.Ci;
+    const int n = o.i / K, kk = o.i - n * K;
+    const bf16 wb = f2bf(w);
+    a.sgd.wbf[d.bf_off + (long long)n * round_up(K, 32) + kk] = wb;
+    a.sgd.wbf[d.bft_off + (long long)kk * round_up(d.N, 32) + n] = wb;
+    return;
+  }
+  emit_copies(d, o.i, w, a.sgd.wbf);
+  const int wj = conv_wj(o);
+  if (wj >= 0) lenet_frag_scatter(a.sgd.frag, wj, w);
+}
+
+// Finalise element o with gradient v (sync): store the gradient; with the fused update apply SGD to the
+// master (w_old / m_old loaded by the caller) and emit the copies; otherwise snapshot what the optimizer
+// launch needs.
+template <bool DENSE>
+__device__ __forceinline__ void red_apply(const LeNetRedArgs& a, const RedTables& t, Owned o, float v, float w_old,
+                                          float m_old) {
   if (o.di < 0) return;
   t.g[o.di][o.i] = v;
-  const int wj = conv_wj(o);
   if (a.sgd_on) {
-    const ParamDesc& d = t.d[o.di];
-    const long long off = d.off + o.i;
-    if (!pre) {
-      w_old = a.sgd.master[off];
-      m_old = a.sgd.mom != nullptr ? a.sgd.mom[off] : 0.f;
-    }
     const float* h = t.hyper;
-    const float lr = h[0], mom = h[1], wd = h[2], gs = h[3];
+    const float mom = h[1];
     float m_new = 0.f;
-    const float nw = sgd_new_weight(w_old, v, mom != 0.f ? m_old : 0.f, lr, mom, wd, gs, h[4] != 0.f, &m_new);
-    if (mom != 0.f) a.sgd.mom[off] = m_new;
-    a.sgd.master[off] = nw;
-    emit_copies(d, o.i, nw, a.sgd.wbf);
-    // the new conv weight goes straight into the next step's MFMA fragments
-    if (wj >= 0) lenet_frag_scatter(a.sgd.frag, wj, nw);
-  } else if (a.snap != nullptr && wj >= 0) {
+    const float nw = sgd_new_weight(w_old, v, mom != 0.f ? m_old : 0.f, h[0], mom, h[2], h[3], h[4] != 0.f, &m_new);
+    if (mom != 0.f) a.sgd.mom[t.d[o.di].off + o.i] = m_new;
+    red_emit<DENSE>(a, t, o, nw);
+  } else if (!DENSE && a.snap != nullptr && conv_wj(o) >= 0) {
     // the conv kernels' weights and momentum as this gradient saw them: the optimizer launch rebuilds
     // the next step's fragments from these (no read of state it is overwriting)
+    const int wj = conv_wj(o);
     const long long q = wj < 150 ? wj : wj - 150;
     a.snap[wj] = wj < 150 ? a.w1[q] : a.w2[q];
     a.snap[kLeNetConvW + wj] = a.m1 == nullptr ? 0.f : (wj < 150 ? a.m1[q] : a.m2[q]);
@@ -1029,34 +1043,28 @@ __device__ __forceinline__ void lenet_ps_decide(const LeNetRedArgs& a, unsigned*
 // One parameter element on the PS: w_new = w[v] - lr * g into buffer (v + 1) % 3 of the shared master
 // (admitted) or the current w[v] (rejected); either way the local master and its bf16 compute copies
 // become that version.  Returns the local weight.
-__device__ __forceinline__ float lenet_ps_elem(const LeNetRedArgs& a, const ParamDesc& d, int i, float g,
-                                               unsigned dec, unsigned seq) {
-  const PSArgs& p = a.ps;
-  const unsigned v = seq >> 1;
-  const long long off = d.off + i;
-  const float w = p.ps_w[(long long)(v % 3u) * p.nstride + off];
-  float wn = w;
-  if (dec == kPSAccept) {
-    wn = w - p.lr * g;
-    p.ps_w[(long long)((v + 1u) % 3u) * p.nstride + off] = wn;
-  }
-  a.sgd.master[off] = wn;
-  emit_copies(d, i, wn, a.sgd.wbf);
-  return wn;
+__device__ __forceinline__ float ps_new_weight(float w, float g, float lr, bool accept) {
+#pragma clang fp contract(off)
+  return accept ? w - lr * g : w;
 }
 
-// Arrival of one of the G + 1 protocol workgroups (job workgroups + staging): the last one publishes
-// version v + 1 (admitted) or releases the lock (rejected) and records the pulled version.
-__device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, int arrivals) {
+
+// Protocol arrivals: the last one publishes version v + 1 (admitted) or releases the lock (rejected) and
+// records the pulled version.
+// Arrivals are counted per slot (its owner adds one when done with it) plus one for workgroup 0's decision
+// and one for the staging workgroup: `count` of them from this workgroup, `arrivals` in all.  Workgroups
+// that own nothing do not arrive.
+__device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, unsigned count, unsigned arrivals) {
   const PSArgs& p = a.ps;
   // every storing wave drains its shared-master stores (uncached / fine-grained memory: complete at the
-  // server's HBM once acknowledged), then the arrival ticket; the last arriver's system-scope release
-  // store of the version word orders all of them before the publish (no per-workgroup L2 write-back)
+  // server's HBM once acknowledged) and the decision words (write-through), then a relaxed arrival; the
+  // last arriver's acquire fence and system-scope release store of the version word order all of them
+  // before the publish (no per-workgroup L2 write-back or invalidate)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(p.scratch + kPSApplyDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == (unsigned)arrivals - 1) {
+  if (threadIdx.x == 0 && count > 0) {
+    const unsigned prev = __hip_atomic_fetch_add(p.scratch + kPSApplyDone, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev + count == arrivals) {
       __hip_atomic_store(p.scratch + kPSApplyDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(p.scratch + kPSEpoch, __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED,
                                                                  __HIP_MEMORY_SCOPE_AGENT) + 1u,
@@ -1078,15 +1086,6 @@ __device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, int arriv
 }
 
 
-// async PS: finalise element o with gradient g under this launch's decision
-__device__ __forceinline__ void red_ps(const LeNetRedArgs& a, const RedTables& t, Owned o, float g, unsigned dec,
-                                       unsigned seq) {
-  if (o.di < 0) return;
-  t.g[o.di][o.i] = g;
-  const float w = lenet_ps_elem(a, t.d[o.di], o.i, g, dec, seq);
-  const int wj = conv_wj(o);
-  if (wj >= 0) lenet_frag_scatter(a.sgd.frag, wj, w);  // the next step's conv fragments
-}
 
 // diagnostic phase clocks of the reduce launch: stamps[block][slot] (0 start, 1 jobs done, 2 decision,
 // 3 owned slots applied, 4 end, 6 first job's partial computed, 7 first ownership combine done)
@@ -1101,7 +1100,12 @@ __device__ __forceinline__ void red_ps(const LeNetRedArgs& a, const RedTables& t
     }                                                                             \
   } while (0)
 
+// MODE: 0 single rank, 1 in-kernel LL exchange over the ranks, 2 async parameter server.  One
+// instantiation per mode keeps every launch's code small (the instruction cache is shared with the train
+// kernel; each workgroup runs its path once, cold).
+template <int MODE>
 __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
+  constexpr bool LL = MODE == 1, PS = MODE == 2;
   __shared__ float red[4 * kSlotVals];
   __shared__ RedTables tabs;
   __shared__ int owned[kMaxOwned];
@@ -1116,10 +1120,10 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     stage_tables(a, &tabs);
     // with the fused sync update, the first owned slot's master / momentum elements are loaded beside
     // its slab loads
-    const bool pre = a.sgd_on && !a.ps_on;
+    const bool pre = a.sgd_on && !PS;
     __shared__ float w_pre[kPerThread][RT], m_pre[kPerThread][RT];  // (LDS: not live across the jobs in VGPRs)
     __shared__ float own0[kPerThread][RT];  // the first owned slot's local sums
-    int nown = 0;
+    int nown = 0, narr = 0;  // slots owned (kept) / slots this workgroup finished last (async PS arrivals)
 #pragma unroll 1
     for (int j = blockIdx.x; j < nslot * kChunks; j += G) {
       const int slot = j / kChunks, c = j - kChunks * (j / kChunks);
@@ -1146,9 +1150,10 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       }
       __syncthreads();
       if (!s_last) continue;
+      ++narr;
       // the slot's owner: local sum of the 8 slabs in chunk order
       if (nown >= kMaxOwned) {  // host guarantees G >= 8 * nslot / kMaxOwned; never spin on a missing owner
-        if (threadIdx.x == 0 && a.ll_on) atomicOr(a.ll.err, 2);
+        if (threadIdx.x == 0 && LL) atomicOr(a.ll.err, 2);
         continue;
       }
       if (nown == 0 && pre) {
@@ -1193,7 +1198,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
           if (nown == 0) own0[e][threadIdx.x] = v[e];
           else slab[threadIdx.x + RT * e] = v[e];
         }
-      if (a.ll_on) {
+      if (LL) {
         const unsigned ee = ll_epoch(a.ll, slot, &s_e);
         if (threadIdx.x == 0) ep[nown] = ee;
 #pragma unroll
@@ -1207,40 +1212,84 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     __syncthreads();
     LR_STAMP(1);
     __shared__ unsigned s_dec, s_seq;
-    if (a.ps_on && (nown > 0 || blockIdx.x == 0)) lenet_ps_decide(a, &s_dec, &s_seq);  // 0 takes the lock
+    if (PS && (nown > 0 || blockIdx.x == 0)) lenet_ps_decide(a, &s_dec, &s_seq);  // 0 takes the lock
     LR_STAMP(2);
-    const unsigned dec = a.ps_on ? s_dec : 0u, seq = a.ps_on ? s_seq : 0u;
+    const unsigned dec = PS ? s_dec : 0u, seq = PS ? s_seq : 0u;
 #pragma unroll 1
     for (int k = 0; k < nown; ++k) {
       const int slot = owned[k];
       const int npos = slot < a.dense_tiles ? kPerThread : 1;
       const float* sum = a.slabs + (long long)slot * kChunks * kSlotVals;
+      // gather every position's element, local sum and old weight first (all loads in flight), then
+      // the rank sums, then the arithmetic, then the stores: no load waits behind a store
+      Owned o[kPerThread];
+      float v[kPerThread], w0[kPerThread], m0[kPerThread];
 #pragma unroll
       for (int e = 0; e < kPerThread; ++e) {
-        if (e >= npos) break;
         const int pos = threadIdx.x + RT * e;
-        const Owned o = owned_elem(a, tabs, slot, pos);
-        float v = k == 0 ? own0[e][threadIdx.x] : sum[pos];
-        if (a.ps_on) {
-          if (dec == kPSAccept || dec == kPSReject) red_ps(a, tabs, o, v, dec, seq);
-          continue;
+        o[e] = e < npos ? owned_elem(a, tabs, slot, pos) : Owned{-1, 0};
+        v[e] = e < npos ? (k == 0 ? own0[e][threadIdx.x] : sum[pos]) : 0.f;
+        w0[e] = m0[e] = 0.f;
+        if (a.sgd_on && !PS && o[e].di >= 0) {
+          if (k == 0 && pre) {
+            w0[e] = w_pre[e][threadIdx.x];
+            m0[e] = m_pre[e][threadIdx.x];
+          } else {
+            const long long off = tabs.d[o[e].di].off + o[e].i;
+            w0[e] = a.sgd.master[off];
+            m0[e] = a.sgd.mom != nullptr ? a.sgd.mom[off] : 0.f;
+          }
         }
-        bool ok = true;
-        if (a.ll_on) ok = ll_wait_sum(a.ll, slot, pos, ep[k], v, v);  // the rank-order sum (no all-reduce launch)
-        if (ok) red_apply(a, tabs, o, v, k == 0 && pre, w_pre[e][threadIdx.x], m_pre[e][threadIdx.x]);
       }
-      if (a.ll_on) {
+      if (PS) {
+        if (dec == kPSAccept || dec == kPSReject) {
+          // version seq / 2 of every element first (the shared master is uncached: one round trip for
+          // all of them), then the new version, local master, compute copies and fragments
+          const PSArgs& p = a.ps;
+          const long long vb = (long long)((seq >> 1) % 3u) * p.nstride;
+          const long long nb = (long long)(((seq >> 1) + 1u) % 3u) * p.nstride;
+          float wv[kPerThread];
+#pragma unroll
+          for (int e = 0; e < kPerThread; ++e)
+            wv[e] = o[e].di >= 0 ? p.ps_w[vb + tabs.d[o[e].di].off + o[e].i] : 0.f;
+#pragma unroll
+          for (int e = 0; e < kPerThread; ++e) {
+            if (o[e].di < 0) continue;
+            tabs.g[o[e].di][o[e].i] = v[e];
+            const float wn = ps_new_weight(wv[e], v[e], p.lr, dec == kPSAccept);
+            if (dec == kPSAccept) p.ps_w[nb + tabs.d[o[e].di].off + o[e].i] = wn;
+            if (npos > 1) red_emit<true>(a, tabs, o[e], wn);
+            else if (e == 0) red_emit<false>(a, tabs, o[e], wn);
+          }
+        }
+        continue;
+      }
+      bool ok[kPerThread];
+#pragma unroll
+      for (int e = 0; e < kPerThread; ++e) {
+        ok[e] = true;
+        // the rank-order sum over the ranks (no all-reduce launch)
+        if (LL && e < npos) ok[e] = ll_wait_sum(a.ll, slot, threadIdx.x + RT * e, ep[k], v[e], v[e]);
+      }
+      if (npos > 1) {  // a dense unit
+#pragma unroll
+        for (int e = 0; e < kPerThread; ++e)
+          if (ok[e]) red_apply<true>(a, tabs, o[e], v[e], w0[e], m0[e]);
+      } else if (ok[0]) {
+        red_apply<false>(a, tabs, o[0], v[0], w0[0], m0[0]);
+      }
+      if (LL) {
         __syncthreads();  // every position of the slot consumed before its epoch advances
         ll_commit(a.ll, slot, ep[k]);
       }
     }
     LR_STAMP(3);
-    if (a.ps_on) lenet_ps_arrive(a, G + 1);
+    if (PS) lenet_ps_arrive(a, (unsigned)(narr + (blockIdx.x == 0 ? 1 : 0)), (unsigned)(nslot + 2));
     LR_STAMP(4);
     return;
   }
   const int blk = blockIdx.x - G;
-  if (blk == 1 && a.ps_on) {
+  if (blk == 1 && PS) {
     // async: once this launch's decision is known (the current microbatch is completed under the lock),
     // claim the next microbatch FCFS on the server and stage its example indices
     __shared__ unsigned s_dec, s_seq;
@@ -1255,7 +1304,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     __syncthreads();
     if (threadIdx.x == 0) *a.ps.bid_out = s_bid;
     ps_stage_indices(a.ps, s_bid, threadIdx.x, RT);
-    lenet_ps_arrive(a, G + 1);
+    lenet_ps_arrive(a, 1u, (unsigned)(a.dense_tiles + a.nconv_slots + 2));
     LR_STAMP(1);
     return;
   }
@@ -1371,6 +1420,13 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   if (!r.slabs || !r.tickets) return hipErrorInvalidValue;
   if (r.sgd_on && (!r.sgd.master || !r.sgd.wbf || !r.sgd.hyper || !r.sgd.frag))
     return hipErrorInvalidValue;
+  if (r.sgd_on)  // dense weights: tile-layout compute copies (red_emit's fast path), biases: none
+    for (int l = 0; l < 3; ++l) {
+      const ParamDesc& dw = r.sgd.d[4 + 2 * l];
+      const ParamDesc& db = r.sgd.d[5 + 2 * l];
+      if (!((dw.pad_ >> 28) & 1) || dw.T != 1 || dw.bf_off < 0 || dw.bft_off < 0 || db.bf_off >= 0)
+        return hipErrorInvalidValue;
+    }
   const int nslot = r.dense_tiles + r.nconv_slots;
   const int njobs = nslot * kChunks;
   if (r.exch_blocks <= 0 || r.exch_blocks > njobs) r.exch_blocks = njobs;
@@ -1394,7 +1450,10 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
       return hipErrorInvalidValue;
   }
   const int extra = ((r.sgd_on && r.sgd.src) || r.ps_on) ? 1 : 0;  // the index-staging workgroup
-  hipLaunchKernelGGL(lenet_reduce_kernel, dim3(r.exch_blocks + 1 + extra), dim3(RT), 0, st, r);
+  const dim3 grid(r.exch_blocks + 1 + extra);
+  if (r.ll_on) hipLaunchKernelGGL(lenet_reduce_kernel<1>, grid, dim3(RT), 0, st, r);
+  else if (r.ps_on) hipLaunchKernelGGL(lenet_reduce_kernel<2>, grid, dim3(RT), 0, st, r);
+  else hipLaunchKernelGGL(lenet_reduce_kernel<0>, grid, dim3(RT), 0, st, r);
   return hipGetLastError();
 }
 
