@@ -53,7 +53,10 @@ constexpr int OFF_FT = OFF_K + 128;                 // conv2 dgrad table [98][2]
 constexpr int OFF_PX = OFF_FT + 98 * 2 * 16;        // conv2 output row -> P1 pixel [800] u16 (host-built)
 constexpr int OFF_W = OFF_PX + 800 * 2;             // f32: b1 [6], b2 [16]
 constexpr int OFF_U = OFF_W + 128;                  // phase-dependent union
-constexpr int OFF_XS1 = OFF_U;                      // phases A and G: input shifted left by one pixel
+// phases A and G: input shifted left by one pixel; 32 bytes into the union so that its rows sit 24 banks
+// from Xs's (the A-operand reads of phase A and the B-operand reads of phase G are then conflict-free:
+// scripts/lds_sim.py)
+constexpr int OFF_XS1 = OFF_U + 32;
 constexpr int LD0 = 424, LD1 = 136, LD2 = 104, LD3 = 40;  // dense row strides (elements)
 constexpr int OFF_H0 = OFF_U;
 constexpr int OFF_H1 = OFF_H0 + IMG * LD0 * 2;
@@ -67,8 +70,11 @@ constexpr int OFF_C2 = OFF_LG + IMG * 16 * 4;       // [8][25][16] u8 pool2 code
 constexpr int U_DENSE = OFF_C2 + IMG * 25 * 16 - OFF_U;
 constexpr int OFF_DC2 = OFF_U;                      // [800][16] bf16 conv2 output gradient
 constexpr int U_DC2 = 800 * 16 * 2;
-constexpr int OFF_RED = OFF_U + XS_ELEMS * 2;       // [4][16][32] f32 cross-wave conv1 wgrad sums
-constexpr int U_G = XS_ELEMS * 2 + 4 * 16 * 32 * 4;
+constexpr int OFF_RED = OFF_XS1 + XS_ELEMS * 2;     // [4][16][32] f32 cross-wave conv1 wgrad sums
+constexpr int U_G = 32 + XS_ELEMS * 2 + 4 * 16 * 32 * 4;
+// conv2 output-gradient rows r (image * 100 + window * 4 + position) are stored at row r ^ ((r >> 3) & 7):
+// the gathered A-operand reads of phase F then spread over the banks (scripts/lds_sim.py)
+__device__ __forceinline__ int dc2_row(int r) { return r ^ ((r >> 3) & 7); }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int LDS_BYTES = OFF_U + cmax(cmax(U_DENSE, U_DC2), U_G);
 static_assert(OFF_U % 16 == 0 && OFF_H1 % 16 == 0 && OFF_ZR % 16 == 0 && OFF_C2 % 16 == 0 && OFF_RED % 16 == 0 &&
@@ -518,7 +524,7 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
           bf16x8 o;
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = ((cd[k] >> (8 * e)) & 255u) == (unsigned)d ? dp[k][e] : (bf16)0.f;
-          st8(DC2 + ((img * 100 + win * 4 + d) * 16 + 8 * nh), o);
+          st8(DC2 + (dc2_row(img * 100 + win * 4 + d) * 16 + 8 * nh), o);
         }
       }
     }
@@ -550,7 +556,9 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
 #pragma unroll 5
     for (int s = 0; s < 25; ++s) {
       const int mA = 32 * s + 8 * g + q;
-      const bf16x8 av = cat8(tr_read(DC2 + mA * 16 + 4 * p), tr_read(DC2 + (mA + 4) * 16 + 4 * p));
+      // dc2_row(mA) and dc2_row(mA + 4): both rows lie in 8-row block 4 s + g
+      const int sx = (4 * s + g) & 7;
+      const bf16x8 av = cat8(tr_read(DC2 + (mA ^ sx) * 16 + 4 * p), tr_read(DC2 + ((mA + 4) ^ sx) * 16 + 4 * p));
       const bf16* pb0 = P1 + (int)PX[mA] * 8;
       const bf16* pb1 = P1 + (int)PX[mA + 4] * 8;
 #pragma unroll
@@ -589,12 +597,12 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
       const int img = m / 98, rem = m - 98 * (m / 98);
       const uint4 tv = *reinterpret_cast<const uint4*>(FT + (rem * 2 + (g >> 1)) * 16);
       const unsigned tw[4] = {tv.x, tv.y, tv.z, tv.w};
-      const bf16* dbase = DC2 + img * 1600 + 8 * (g & 1);
+      const bf16* dbase = DC2 + 8 * (g & 1);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 15; ++s) {
         const unsigned t = (tw[s >> 2] >> (8 * (s & 3))) & 255u;
-        acc = mfma16x16x32(ld8(t == 255u ? KZ : dbase + t * 16), bd[s], acc);
+        acc = mfma16x16x32(ld8(t == 255u ? KZ : dbase + dc2_row(img * 100 + (int)t) * 16), bd[s], acc);
       }
       if (c < 6) {
 #pragma unroll
@@ -615,25 +623,30 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   // ---------------------------------------------------------------- phase G: conv1 weight gradient
   // D[c][tap] = sum over (image, y, x) of dC1[c][y][x] X[y + ky][x + kx].  A fragment of lane
   // (c = i, g) = dC1[c][y][8g .. 8g + 8) unpooled in registers from dP1 + codes (4 windows); B of lane
-  // (tap = 16T + i, g) = 4 dword reads of the input row y + ky at column 8g + kx (odd kx: the shifted
-  // copy).  No per-image staging, no barrier inside the loop.
+  // (tap = 16T + i, g) = the input row y + ky from column 8g + kx (odd kx: the shifted copy).  No
+  // per-image staging, no barrier inside the loop.
   {
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     const int ca = i < 6 ? i : 5;
-    int boff[2];
-    const bf16* bsrc[2];
+    // B of lane (tap, g) = input row y + ky, columns 8g + kx .. + 7 (odd kx: the shifted copy, so the
+    // start is a whole dword): two aligned 16-byte reads of columns 8g .. 8g + 15 and a per-lane dword
+    // select (sh = kx >> 1) -- 16-byte reads are conflict-free here where four dword reads were not.
+    // Branch-free: every lane reads (taps >= 25 read tap 0's words), then the bias column of ones and
+    // the zero columns replace the value.
+    constexpr int kXs1 = (OFF_XS1 - OFF_XS) / 2;  // Xs1 - Xs in elements
+    int boff[2], bsh[2], bkind[2];                // kind: 0 input, 1 ones (bias column), 2 zeros
 #pragma unroll
     for (int T = 0; T < 2; ++T) {
       const int tap = 16 * T + i;
-      if (tap < 25) {
-        const int ky = tap / 5, kx = tap - 5 * (tap / 5);
-        bsrc[T] = (kx & 1) ? Xs1 : Xs;
-        boff[T] = ky * 32 + 8 * g + (kx & ~1);
-      } else {
-        bsrc[T] = tap == 25 ? KO : KZ;
-        boff[T] = -1;
-      }
+      const int tp = tap < 25 ? tap : 0;
+      const int ky = tp / 5, kx = tp - 5 * (tp / 5);
+      boff[T] = ((kx & 1) ? kXs1 : 0) + ky * 32 + 8 * g;
+      bsh[T] = kx >> 1;
+      bkind[T] = tap < 25 ? 0 : (tap == 25 ? 1 : 2);
     }
+    bf16x8 ones8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones8[e] = (bf16)1.f;
 #pragma unroll 2
     for (int rp = w; rp < IMG * 14; rp += NT / 64) {
       const int img = rp / 14, py = rp - 14 * (rp / 14);
@@ -647,7 +660,9 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
       for (int wd = 0; wd < 4; ++wd) {
         const bool ok = 4 * g + wd < 14 && i < 6;
         const unsigned code = (cw[wd] >> (3 * ca)) & 7u;
-        const bf16 v = ok ? P1[(p0 + wd) * 8 + ca] : (bf16)0.f;
+        const bf16 pv = P1[(p0 + wd) * 8 + ca];  // in bounds for every lane (windows 14, 15 are the
+                                                 // next row's first two or the tail), masked below
+        const bf16 v = ok ? pv : (bf16)0.f;
         a0[2 * wd] = code == 0u ? v : (bf16)0.f;
         a0[2 * wd + 1] = code == 1u ? v : (bf16)0.f;
         a1[2 * wd] = code == 2u ? v : (bf16)0.f;
@@ -658,18 +673,17 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
         const int y = 2 * py + dy;
 #pragma unroll
         for (int T = 0; T < 2; ++T) {
-          bf16x8 bv;
-          if (boff[T] >= 0) {
-            const unsigned* bp = reinterpret_cast<const unsigned*>(bsrc[T] + img * 1024 + y * 32 + boff[T]);
-            uint4 u;
-            u.x = bp[0];
-            u.y = bp[1];
-            u.z = bp[2];
-            u.w = bp[3];
-            bv = __builtin_bit_cast(bf16x8, u);
-          } else {
-            bv = ld8(bsrc[T]);
+          const uint4* bp = reinterpret_cast<const uint4*>(Xs + img * 1024 + y * 32 + boff[T]);
+          const uint4 c0 = bp[0], c1 = bp[1];
+          const unsigned sv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+          unsigned o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            o[j] = bsh[T] == 1 ? sv[j + 1] : sv[j];
+            o[j] = bsh[T] == 2 ? sv[j + 2] : o[j];
           }
+          bf16x8 bv = __builtin_bit_cast(bf16x8, uint4{o[0], o[1], o[2], o[3]});
+          bv = bkind[T] == 0 ? bv : (bkind[T] == 1 ? ones8 : zero8());
           acc[T] = mfma16x16x32(dy ? a1 : a0, bv, acc[T]);
         }
       }
