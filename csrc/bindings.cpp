@@ -52,7 +52,9 @@ void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tenso
                   int64_t lda, int64_t ldc, std::vector<int64_t> geom, int64_t mode, bool relu, double alpha,
                   c10::optional<torch::Tensor> res, c10::optional<torch::Tensor> resmask, double drop_p,
                   int64_t drop_seed, c10::optional<torch::Tensor> drop_step, c10::optional<torch::Tensor> pool_code,
-                  int64_t drop_step_add, c10::optional<torch::Tensor> bn_part) {
+                  int64_t drop_step_add, c10::optional<torch::Tensor> bn_ws, c10::optional<torch::Tensor> bn_ticket,
+                  int64_t bn_mode, std::vector<torch::Tensor> bn_vecs, c10::optional<torch::Tensor> bn_x,
+                  double bn_momentum, double bn_eps, double bn_gscale) {
   need(src, at::kBFloat16, "src");
   need(w, at::kBFloat16, "w");
   TORCH_CHECK(out.is_cuda() && out.is_contiguous(), "out must be a contiguous GPU tensor");
@@ -116,12 +118,51 @@ void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tenso
     a.pool_code = pool_code->data_ptr<uint8_t>();
     TORCH_CHECK(dfa::igemm64_pool_supported(a), "pooled conv: unsupported geometry / alignment");
   }
-  if (bn_part.has_value() && bn_part->defined()) {
-    need(*bn_part, at::kFloat, "bn_part");
-    const int ntm = dfa::igemm64_bn_tiles(a, (int)mode);
-    TORCH_CHECK(ntm > 0, "bn_part: this conv cannot emit BatchNorm partials");
-    TORCH_CHECK(bn_part->numel() >= (int64_t)ntm * 2 * N, "bn_part too small");
-    a.bn_part = bn_part->data_ptr<float>();
+  if (bn_ws.has_value() && bn_ws->defined()) {
+    // BatchNorm statistics finalised inside this launch (kernels.h BnEpi)
+    need(*bn_ws, at::kFloat, "bn_ws");
+    TORCH_CHECK(bn_ticket.has_value() && bn_ticket->defined(), "bn_ws needs bn_ticket");
+    need(*bn_ticket, at::kInt, "bn_ticket");
+    int ntn = 0;
+    const int ntm = dfa::igemm64_bn_layout(a, (int)mode, &ntn);
+    TORCH_CHECK(ntm > 0, "bn: this conv launch cannot finalise BatchNorm statistics");
+    const int ngrp = (ntm + 15) / 16;
+    TORCH_CHECK(bn_ws->numel() >= (int64_t)(ntm + ngrp) * 2 * N, "bn_ws too small");
+    TORCH_CHECK(bn_ticket->numel() >= (int64_t)ntn * (1 + ngrp), "bn_ticket too small");
+    TORCH_CHECK(out.scalar_type() == at::kBFloat16, "bn: bf16 output");
+    dfa::BnEpi& e = a.bn;
+    e.part = bn_ws->data_ptr<float>();
+    e.ticket = reinterpret_cast<unsigned*>(bn_ticket->data_ptr<int>());
+    e.ntm = ntm;
+    e.ngrp = ngrp;
+    e.mode = (int)bn_mode;
+    e.momentum = (float)bn_momentum;
+    e.eps = (float)bn_eps;
+    e.gscale = (float)bn_gscale;
+    for (auto& v : bn_vecs) {
+      need(v, at::kFloat, "bn vector");
+      TORCH_CHECK(v.numel() >= N, "bn vector smaller than N");
+    }
+    if (bn_mode == 0) {
+      TORCH_CHECK(bn_vecs.size() == 4, "bn mode 0: [mean, invstd, run_mean, run_var]");
+      e.mean_out = bn_vecs[0].data_ptr<float>();
+      e.invstd_out = bn_vecs[1].data_ptr<float>();
+      e.run_mean = bn_vecs[2].data_ptr<float>();
+      e.run_var = bn_vecs[3].data_ptr<float>();
+    } else {
+      TORCH_CHECK(bn_mode == 1 && bn_vecs.size() == 6, "bn mode 1: [mean, invstd, gamma, dgamma, dbeta, coef]");
+      TORCH_CHECK(bn_x.has_value() && bn_x->defined(), "bn mode 1 needs the BN input");
+      need(*bn_x, at::kBFloat16, "bn_x");
+      TORCH_CHECK(bn_x->numel() >= (M - 1) * ldc + N, "bn_x too small");
+      TORCH_CHECK(bn_vecs[5].numel() >= 3 * N, "bn coef must hold [3][N]");
+      e.x = reinterpret_cast<const dfa::bf16*>(bn_x->data_ptr());
+      e.mean = bn_vecs[0].data_ptr<float>();
+      e.invstd = bn_vecs[1].data_ptr<float>();
+      e.gamma = bn_vecs[2].data_ptr<float>();
+      e.dgamma = bn_vecs[3].data_ptr<float>();
+      e.dbeta = bn_vecs[4].data_ptr<float>();
+      e.coef = bn_vecs[5].data_ptr<float>();
+    }
   }
   TORCH_CHECK(!a.drop.on || (ldc == N && !a.out_f32), "folded dropout needs a dense bf16 output (ldc == N)");
   // split-K partials for the under-filled (small-M, long-K) shapes: PyTorch's caching allocator is
@@ -1516,7 +1557,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lda"), py::arg("ldc"), py::arg("geom"), py::arg("mode"), py::arg("relu"), py::arg("alpha"),
         py::arg("res") = py::none(), py::arg("resmask") = py::none(), py::arg("drop_p") = 0.0,
         py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pool_code") = py::none(),
-        py::arg("drop_step_add") = 0, py::arg("bn_part") = py::none());
+        py::arg("drop_step_add") = 0, py::arg("bn_ws") = py::none(), py::arg("bn_ticket") = py::none(),
+        py::arg("bn_mode") = 0, py::arg("bn_vecs") = std::vector<torch::Tensor>{}, py::arg("bn_x") = py::none(),
+        py::arg("bn_momentum") = 0.1, py::arg("bn_eps") = 1e-5, py::arg("bn_gscale") = 1.0);
   m.def("igemm64_bn_tiles", [](int64_t M, int64_t N, int64_t K, int64_t Kpad, std::vector<int64_t> geom, int64_t mode) {
     dfa::IGemmArgs a{};
     int g[9];
@@ -1526,7 +1569,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     a.M = (int)M; a.N = (int)N; a.K = (int)K; a.Kpad = (int)Kpad; a.ldc = (int)N;
     static dfa::bf16 probe[8] __attribute__((aligned(16)));
     a.src = probe; a.w = probe; a.out = probe;
-    return dfa::igemm64_bn_tiles(a, (int)mode);
+    int ntn = 0;
+    const int ntm = dfa::igemm64_bn_layout(a, (int)mode, &ntn);
+    return std::make_tuple((int64_t)ntm, (int64_t)ntn);
   });
   m.def("bn_finalize_partials", [](torch::Tensor part, int64_t ntm, int64_t C, int64_t M, torch::Tensor mean,
                                    torch::Tensor invstd, c10::optional<torch::Tensor> run_mean,

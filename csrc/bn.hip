@@ -18,6 +18,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "diag.h"
+#include "bn_epi.h"
 
 namespace dfa {
 
@@ -44,28 +45,9 @@ static int bn_grid(int M, int rpp) {
   return g;
 }
 
-// Hand-off without fences (cdna_hip_programming.md Guideline 16, sc1 form): every slab word is
-// stored write-through (relaxed agent-scope atomic store = sc1) and drained by every storing wave
-// before the barrier; lane 0 then draws a ticket.  The last of `n` arrivers reads the slabs with sc1
-// loads (relaxed agent-scope atomic loads bypass this CU's L1), so neither side pays the agent-scope
-// release (an L2 writeback) or acquire that the round-1 version spent per workgroup.  It re-arms the
-// counter to 0 for the next launch.
-__device__ __forceinline__ void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
+// Hand-off without fences: st_sc1 / ld_sc1 / last_arriver (csrc/bn_epi.h).
 __device__ __forceinline__ bool bn_last_arriver(unsigned* counter, unsigned n, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned tk = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = (tk == n - 1) ? 1 : 0;
-    if (*flag) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
-  return *flag != 0;
+  return last_arriver(counter, n, flag);
 }
 
 // MODE 0: s += x, q += x*x.   MODE 1: g = dy * relu'(mask), xh = (x - mean) * invstd; s += g, q += g*xh.
@@ -228,7 +210,7 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
 }
 
 // BatchNorm forward statistics from the partial sums the producing conv's epilogue emitted
-// (IGemmArgs::bn_part, [ntm][2][C]): per channel a fixed-order fp64 sum over the row tiles (16 waves
+// ([ntm][2][C] row-tile partials, e.g. a BnEpi buffer): per channel a fixed-order fp64 sum over the row tiles (16 waves
 // of a workgroup take every 16th tile, 8 loads in flight each, combined in wave order), then the same
 // finalisation as bn_stats_kernel<0>.  Replaces a full read of the conv output.
 __global__ void __launch_bounds__(1024) bn_finalize_partials_kernel(const float* __restrict__ part, int ntm, int C,

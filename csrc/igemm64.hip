@@ -22,6 +22,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "diag.h"
+#include "bn_epi.h"
 
 namespace dfa {
 
@@ -547,62 +548,68 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
     }
   }
 
-  // BatchNorm statistics of this tile's stored outputs (sum, sum of squares per channel), so the BN
-  // layer after this conv needs no statistics pass over its input: the 16 rows of a lane group by
-  // lane shuffles, the WM row-waves of a column block through LDS, one partial row per row tile.
-  if (a.bn_part) {
-    float s[TN][4], q[TN][4];
+  // BatchNorm statistics of this tile's STORED outputs (kernels.h BnEpi), finalised inside the launch:
+  // the tile's output is re-read (its own stores, still in this XCD's L2) in 8-byte column chunks,
+  // mode 1 with the BN input alongside, reduced over the rows through LDS into one partial row per row
+  // tile, then the hierarchical last-arriver finalisation (csrc/bn_epi.h).
+  if constexpr (!SPLIT && !POOL && !PAR && BN >= 64) {  // (32-column tiles keep their occupancy)
+    if (a.bn.part) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's output stores are complete
+      __syncthreads();
+      typedef __bf16 bf16x4_b __attribute__((ext_vector_type(4)));
+      constexpr int NCH = BN / 4, RPP = 256 / NCH;
+      const int ch = tid % NCH, rs = tid / NCH;
+      const int col = n0 + 4 * ch;
+      float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f}, mu[4], is[4];
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s[j][r] = q[j][r] = 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int row = m0 + wm * TM * 16 + i * 16 + fr;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col0 = n0 + wn * TN * 16 + j * 16 + fq * 4;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = (float)f2bf(acc[i][j][r] * a.alpha + ((a.bias && col0 + r < a.N) ? a.bias[col0 + r] : 0.f));
-          if (row >= a.M || col0 + r >= a.N) v = 0.f;
-          s[j][r] += v;
-          q[j][r] += v * v;
-        }
+      for (int r = 0; r < 4; ++r) {
+        mu[r] = (a.bn.mode == 1 && col + r < a.N) ? a.bn.mean[col + r] : 0.f;
+        is[r] = (a.bn.mode == 1 && col + r < a.N) ? a.bn.invstd[col + r] : 1.f;
       }
-    }
+      const bf16* ob = reinterpret_cast<const bf16*>(a.out);
+      const int rend = min(m0 + BM, a.M);
+      if (col + 3 < a.N && (a.ldc & 3) == 0) {
+#pragma unroll 4
+        for (int row = m0 + rs; row < rend; row += RPP) {
+          const long long o = (long long)row * a.ldc + col;
+          const bf16x4_b yv = *reinterpret_cast<const bf16x4_b*>(ob + o);
+          bf16x4_b xv;
+          if (a.bn.mode == 1) xv = *reinterpret_cast<const bf16x4_b*>(a.bn.x + o);
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-          s[j][r] += __shfl_xor(s[j][r], off);
-          q[j][r] += __shfl_xor(q[j][r], off);
+          for (int r = 0; r < 4; ++r) {
+            const float y = (float)yv[r];
+            s4[r] += y;
+            q4[r] += a.bn.mode == 1 ? y * (((float)xv[r] - mu[r]) * is[r]) : y * y;
+          }
         }
-    float* red = reinterpret_cast<float*>(lds);  // the k loop ended with a barrier: LDS is free
-    if (fr == 0) {
+      } else {
+        for (int row = m0 + rs; row < rend; row += RPP)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int cl = wn * TN * 16 + j * 16 + fq * 4 + r;
-          red[(wm * BN + cl) * 2] = s[j][r];
-          red[(wm * BN + cl) * 2 + 1] = q[j][r];
-        }
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += 256) {
-      const int col = n0 + c;
-      if (col >= a.N) continue;
-      float S = 0.f, Q = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        S += red[(w * BN + c) * 2];
-        Q += red[(w * BN + c) * 2 + 1];
+          for (int r = 0; r < 4; ++r)
+            if (col + r < a.N) {
+              const long long o = (long long)row * a.ldc + col + r;
+              const float y = (float)ob[o];
+              s4[r] += y;
+              q4[r] += a.bn.mode == 1 ? y * (((float)a.bn.x[o] - mu[r]) * is[r]) : y * y;
+            }
       }
-      a.bn_part[((long long)tile_m * 2) * a.N + col] = S;
-      a.bn_part[((long long)tile_m * 2 + 1) * a.N + col] = Q;
+      float* red = reinterpret_cast<float*>(lds);  // the k loop ended with a barrier: LDS is free
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        red[(rs * BN + 4 * ch + r) * 2] = s4[r];
+        red[(rs * BN + 4 * ch + r) * 2 + 1] = q4[r];
+      }
+      __syncthreads();
+      for (int t = tid; t < 2 * BN; t += 256) {
+        const int which = t / BN, c = t - which * BN;
+        if (n0 + c >= a.N) continue;
+        float v = 0.f;
+        for (int w = 0; w < RPP; ++w) v += red[(w * BN + c) * 2 + which];  // fixed row-group order
+        st_sc1(a.bn.part + ((long long)tile_m * 2 + which) * a.N + n0 + c, v);
+      }
+      __shared__ int s_last;
+      bn_epi_finalize<256>(a.bn, a.N, a.M, tile_m, tile_n, n0, min(BN, a.N - n0), &s_last);
     }
   }
 }
@@ -660,7 +667,7 @@ __global__ void __launch_bounds__(256) igemm64_splitk_epilogue_kernel(IGemmArgs 
 // M = B*8*8 or B*4*4 with K up to 4608) leave one wave per SIMD waiting on every step
 template <int BM, int BN>
 static int splitk_for(const IGemmArgs& a) {
-  if (a.pool_code || a.bn_part) return 1;
+  if (a.pool_code || a.bn.part) return 1;
   const long long tiles = (long long)cdiv(a.M, BM) * cdiv(a.N, BN);
   const int nk = cdiv(a.K, 64);
   if (a.N % 4 || a.ldc % 4 || tiles >= 512 || nk < 32) return 1;
@@ -757,12 +764,21 @@ long long igemm64_splitk_floats(const IGemmArgs& a, int mode) {
   return s > 1 ? (long long)s * a.M * a.N : 0;
 }
 
-int igemm64_bn_tiles(const IGemmArgs& a, int mode) {
-  if (!igemm64_supported(a, mode) || a.pool_code || a.relu || a.mask || a.res || a.drop.on || a.out_f32) return 0;
-  if (igemm64_splitk_floats(a, mode) > 0) return 0;  // split-K launches keep the statistics pass
-  const int BM = (a.N <= 64 || (long long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 512) ? 128 : 64;  // launch64_mode
+// Row tiles (and column ranges) of the launch when it can finalise BatchNorm statistics of its output
+// (kernels.h BnEpi): conv forward or data gradient, bf16 output, no pooling, no split-K (those launches
+// keep the statistics pass) and no parity-class stride-2 data gradient.  0 = it cannot.
+int igemm64_bn_layout(const IGemmArgs& a, int mode, int* ntn) {
+  if (mode == MODE_DIRECT || !igemm64_supported(a, mode) || a.pool_code || a.out_f32) return 0;
+  if (igemm64_splitk_floats(a, mode) > 0) return 0;
+  if (mode == MODE_DGRAD && a.stride == 2 && igemm64_fast_ok(a, mode)) return 0;
+  if (a.N <= 32) return 0;  // 128 x 32 tiles are built without the statistics epilogue
+  // tile shape as launch64_mode picks it
+  const int BN = a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128);
+  const int BM = (a.N <= 64 || (long long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 512) ? 128 : 64;
+  if (ntn) *ntn = cdiv(a.N, BN);
   return cdiv(a.M, BM);
 }
+int igemm64_bn_tiles(const IGemmArgs& a, int mode) { return igemm64_bn_layout(a, mode, nullptr); }
 
 bool igemm64_pool_supported(const IGemmArgs& a) {
   return igemm64_supported(a, MODE_FWD) && a.OH % 2 == 0 && a.OW % 2 == 0 && a.N % 4 == 0 && a.ldc == a.N &&

@@ -37,6 +37,25 @@ inline DropSpec make_drop(float p, unsigned long long seed, const long long* ste
   return d;
 }
 
+// BatchNorm statistics emitted by the PRODUCING conv launch (csrc/bn_epi.h): every row tile reduces the
+// values it stored into a partial [2][N] row, and the launch's last arrivers (two fixed-order levels)
+// finalise them, so the BatchNorm that consumes the output needs neither a statistics pass over it nor a
+// finalize launch.  mode 0 (forward): sums of y and y^2 -> mean, invstd, running statistics.  mode 1
+// (backward, the conv producing the BN's output gradient g, relu' already applied): sums of g and
+// g * xhat with xhat = (x - mean) * invstd of the BN input x -> dgamma, dbeta and the coefficients of
+// dx = k1 g + k2 x + k3 (bn_dx).
+struct BnEpi {
+  float* part;        // [ntm][2][N] row-tile partials (write-through), then [ngrp][2][N] group partials
+  unsigned* ticket;   // [ncolgroups][1 + ngrp] arrival tickets, zero between launches (last arrivers re-arm)
+  int ntm, ngrp;      // row tiles of the launch, groups of 16 of them
+  int mode;
+  const bf16* x;                         // mode 1: the BN input [M][ldc]
+  const float *mean, *invstd, *gamma;    // mode 1 inputs (forward statistics, scale)
+  float *mean_out, *invstd_out, *run_mean, *run_var;  // mode 0 outputs
+  float *dgamma, *dbeta, *coef;          // mode 1 outputs (coef [3][N])
+  float momentum, eps, gscale;
+};
+
 struct IGemmArgs {
   const bf16* src;   // A source: [M][lda] (direct) or NHWC [B][SH][SW][SC] (conv gathers)
   const bf16* w;     // [Npad16][Kpad32] bf16, zero padded
@@ -53,8 +72,8 @@ struct IGemmArgs {
   int splits;
   DropSpec drop;     // dropout after the activation (requires ldc == N, bf16 out)
   uint8_t* pool_code;  // conv forward + 2x2 max-pool (igemm64 POOL): out = pooled [M/4][N], code [M/4][N]
-  float* bn_part;      // BatchNorm statistics of the stored output: per row tile [ntm][2][N] (sum, sum of
-                       // squares); igemm64 only, no split-K / activation (bn_finalize_partials)
+  BnEpi bn;            // BatchNorm statistics of the stored output, finalised inside the launch (bn.part
+                       // != nullptr: igemm64, no split-K / pooling / parity-class launch)
 };
 
 struct WgradArgs {
@@ -92,6 +111,7 @@ bool igemm64_supported(const IGemmArgs& a, int mode);
 bool igemm64_pool_supported(const IGemmArgs& a);
 // row tiles (= BatchNorm partial rows) of the igemm64 launch for this problem, 0 if it cannot emit them
 int igemm64_bn_tiles(const IGemmArgs& a, int mode);
+int igemm64_bn_layout(const IGemmArgs& a, int mode, int* ntn);
 hipError_t bn_finalize_partials(const float* part, int ntm, int C, long long M, float* mean, float* invstd,
                                 float* run_mean, float* run_var, float momentum, float eps, hipStream_t st);
 // dY of a pooled conv from the pooled gradient and the argmax codes (NHWC, 2x2 windows)

@@ -109,7 +109,8 @@ class DistriDataset:
 
     addPreprocessCallback = add_preprocess_callback
 
-    def index_stream(self, rank: int = 0, world: int = 1, device=None, with_epochs: bool = False):
+    def index_stream(self, rank: int = 0, world: int = 1, device=None, with_epochs: bool = False,
+                     allow_preprocess: bool = False):
         """Device batch schedule for the data-parallel engine (``DataParallelTrainer.bind_distri_dataset``):
         drains the dispenser in its FCFS order over every remaining epoch, giving the k-th dispensed
         full-size batch to rank k % world, and completes each batch as it is scheduled (the sync engine
@@ -118,10 +119,13 @@ class DistriDataset:
         same number of steps.  A ragged last batch is skipped: a captured step has a fixed shape.
         ``with_epochs``: also return, per step, the dataset epoch of that step's first global batch
         (identical on every rank: epoch boundaries for checkpoints / barriers).
-        Preprocess callbacks run on host-side Batch objects and cannot run inside a replayed device
-        step, so they are refused here (the message-level roles apply them)."""
-        if self.preprocess_callbacks:
-            raise ValueError("preprocess callbacks need the message-level engine (roles), not the device stream")
+        The stream carries indices only: the preprocess callbacks run on the gathered batch, so a caller
+        that applies them itself (``allow_preprocess``: the device engines'
+        ``DataParallelTrainer.add_preprocess_callback``) gets the stream; any other caller would drop them
+        silently and is refused."""
+        if self.preprocess_callbacks and not allow_preprocess:
+            raise ValueError("this dataset has preprocess callbacks: bind it with a trainer's bind_distri_dataset "
+                             "(which runs them on every device batch) or use the message-level roles")
         rows, epochs, k = [], [], 0
         while True:
             done, b, epoch, start, size = self._disp.next()

@@ -16,7 +16,10 @@ Python switches (default in brackets):
   wgrad_overlap [1]        ResNet weight gradients on a side stream
   proj_overlap [1]         ResNet projection shortcut on a side stream
   concurrent_backward [0]  head weight gradients on side streams (measured slower)
-  bn_epilogue [0]          BatchNorm statistics from the conv epilogue (measured neutral / slower)
+  bn_epilogue [0]          BatchNorm statistics finalised inside the producing conv launches instead of
+                           separate statistics passes (correct, but the write-through + ticket tail each
+                           conv workgroup then pays costs more than the passes: ResNet-18 B=256 72.3 k vs
+                           73 k images/s, profiles/r3/resnet18_bn_in_launch_step.txt)
 """
 from __future__ import annotations
 

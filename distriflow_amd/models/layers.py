@@ -25,12 +25,17 @@ import torch
 
 from .. import ops
 from ..diagnostics import on as diag_on
-from .params import ParamSpec, primary_kpad
+from .params import ParamSpec, dgrad_shape, primary_kpad
 
 
 def primary_kpad_of(conv) -> int:
     """Row length of a conv's forward compute copy (the igemm launch's Kpad)."""
     return primary_kpad(conv.specs()[0])
+
+
+def dgrad_kpad_of(conv) -> int:
+    """Row length of a conv's data-gradient compute copy (the dgrad launch's Kpad)."""
+    return dgrad_shape(conv.specs()[0])[1]
 
 
 class Layer:
@@ -224,29 +229,45 @@ class Conv2D(Layer):
     def alloc(self, B, device, dtype, ws):
         super().alloc(B, device, dtype, ws)
         self.ws = ws
-        # BatchNorm statistics from the forward epilogue (csrc/igemm64.hip bn_part): row tiles of the launch
-        self._bn_ntm = 0
-        if (torch.device(device).type == "cuda" and not self.relu
-                and diag_on("bn_epilogue")):
+        # BatchNorm statistics finalised inside this conv's own launches (csrc/bn_epi.h): the forward's for
+        # the BN that consumes the output, the data gradient's for the BN that produced the input
+        self._bn_fwd = self._bn_bwd = None
+        if torch.device(device).type == "cuda" and diag_on("bn_epilogue"):
             H, W, C = self.in_shape
             OH, OW, N = self.out_shape
             kpad = primary_kpad_of(self)
-            self._bn_ntm = ops.conv_bn_tiles(B, H, W, C, OH, OW, N, self.k, self.k, self.stride, self.pad, kpad)
-            if self._bn_ntm:
-                self.bn_part = torch.empty(self._bn_ntm * 2 * N, dtype=torch.float32, device=device)
+            z = lambda n, dt: torch.zeros(n, dtype=dt, device=device)  # noqa: E731
+            ntm, ntn = ops.conv_bn_layout(B, H, W, C, OH, OW, N, self.k, self.k, self.stride, self.pad, kpad)
+            if ntm:
+                ng = -(-ntm // 16)
+                self._bn_fwd = (z((ntm + ng) * 2 * N, torch.float32), z(ntn * (1 + ng), torch.int32))
+            if self.need_dx:
+                ntm, ntn = ops.conv_bn_layout(B, H, W, C, OH, OW, N, self.k, self.k, self.stride, self.pad,
+                                              dgrad_kpad_of(self), dgrad=True)
+                if ntm:
+                    ng = -(-ntm // 16)
+                    self._bn_bwd = (z((ntm + ng) * 2 * C, torch.float32), z(ntn * (1 + ng), torch.int32))
 
     def forward(self, x, training, bn: Optional["BatchNorm"] = None):
-        """``bn``: the BatchNorm that consumes this output; in training its batch statistics come from this
-        launch's epilogue when the kernel can emit them (no statistics pass over the output)."""
+        """``bn``: the BatchNorm that consumes this output; in training its batch statistics are finalised
+        inside this launch when it can (no statistics pass over the output, no finalize launch)."""
         self.x = x
         st = self.store
         b = st[f"{self.name}/bias"] if self.use_bias else None
-        part = self.bn_part if (bn is not None and training and self._bn_ntm) else None
+        spec = None
+        if bn is not None and training and self._bn_fwd is not None:
+            ws, tk = self._bn_fwd
+            spec = dict(ws=ws, ticket=tk, mode=0, vecs=[bn.mean, bn.invstd, bn.run_mean, bn.run_var],
+                        momentum=bn.momentum, eps=bn.eps)
         ops.conv_fwd(x, st.weight(f"{self.name}/kernel"), b, self.out, self.k, self.k, self.stride, self.pad,
-                     relu=self.relu, bn_part=part)
-        if part is not None:
-            bn.stats_from_partials(part, self._bn_ntm, self.out)
+                     relu=self.relu, bn=spec)
+        if spec is not None:
+            bn.x = self.out
+            bn._stats_ready = True
         return self.out
+
+    def can_emit_bn_grad(self) -> bool:
+        return self._bn_bwd is not None
 
     def backward(self, dy, residual=None, residual_mask=None, dx_mask=None):
         """``residual`` / ``residual_mask`` / ``dx_mask``: the ResNet block join fused into the dgrad
@@ -260,14 +281,22 @@ class Conv2D(Layer):
         gb = st.gradient(f"{self.name}/bias") if self.use_bias else None
         ops.conv_wgrad(dy, self.x, st.grad_matrix(kn), gb, self.ws.wgrad, self.k, self.k, self.stride, self.pad)
 
-    def backward_data(self, dy, residual=None, residual_mask=None, dx_mask=None):
+    def backward_data(self, dy, residual=None, residual_mask=None, dx_mask=None, bn: Optional["BatchNorm"] = None):
+        """``bn``: the BatchNorm whose output this layer consumed; its backward statistics (dgamma, dbeta,
+        dx coefficients) are finalised inside this launch over the stored (masked) gradient."""
         if not self.need_dx:
             return None
         st = self.store
         kn = f"{self.name}/kernel"
         mask = dx_mask if dx_mask is not None else (self.x if self.in_relu else None)
+        spec = None
+        if bn is not None:
+            ws, tk = self._bn_bwd
+            spec = dict(ws=ws, ticket=tk, mode=1, x=bn.x,
+                        vecs=[bn.mean, bn.invstd, st[f"{bn.name}/gamma"], st.gradient(f"{bn.name}/gamma"),
+                              st.gradient(f"{bn.name}/beta"), bn.coef])
         ops.conv_dgrad(dy, st.weight(kn), st.weight_t(kn), self.dx, self.k, self.k, self.stride, self.pad,
-                       mask=mask, residual=residual, residual_mask=residual_mask)
+                       mask=mask, residual=residual, residual_mask=residual_mask, bn=spec)
         return self.dx
 
     def config(self):
@@ -476,13 +505,6 @@ class BatchNorm(Layer):
                      residual.reshape(-1, self.C) if residual is not None else None, rbn, not training, self.eps)
         return out
 
-    def stats_from_partials(self, part, ntm, x):
-        """Batch statistics from the producing conv's epilogue partial sums (replaces :meth:`stats`)."""
-        self.x = x
-        ops.bn_finalize_partials(part, ntm, self.C, x.numel() // self.C, self.mean, self.invstd, self.run_mean,
-                                 self.run_var, self.momentum, self.eps)
-        self._stats_ready = True
-
     _stats_ready = False
 
     def forward(self, x, training):
@@ -491,6 +513,12 @@ class BatchNorm(Layer):
             self.stats(x)
         self._stats_ready = False
         return self.apply(x, self.out, training)
+
+    def backward_dx(self, g):
+        """dx from a gradient ``g`` (relu' already applied) whose statistics the producing conv launch
+        finalised (Conv2D.backward_data(bn=self)): the dx pass only."""
+        ops.bn_dx(self.x.reshape(-1, self.C), g.reshape(-1, self.C), self.dx.view(-1, self.C), self.coef)
+        return self.dx
 
     def backward(self, dy, mask=None):
         """``mask``: relu' source applied to dy (default: this layer's own output when it ends in ReLU)."""
@@ -686,8 +714,13 @@ class ResidualBlock(Layer):
                 pev = ps.record_event()
         d = self.bn2.backward(dy, mask=omask)
         weights(self.conv2, d)
-        d = self.conv2.backward_data(d)
-        d = self.bn1.backward(d)
+        if self.conv2.can_emit_bn_grad() and not self.bn1.grad_premasked:
+            # conv2's data gradient applies bn1's relu' and finalises bn1's backward statistics itself
+            d = self.conv2.backward_data(d, dx_mask=self.bn1.out, bn=self.bn1)
+            d = self.bn1.backward_dx(d)
+        else:
+            d = self.conv2.backward_data(d)
+            d = self.bn1.backward(d)
         if self.proj is not None:
             if pev is not None:
                 main.wait_event(pev)

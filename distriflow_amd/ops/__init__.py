@@ -115,28 +115,44 @@ def dense_wgrad(dy, x, gw, gb, workspace=None, scale=1.0):
 
 
 # ----------------------------------------------------------------------------------- conv2d
-def conv_fwd(x, w, bias, out, KH, KW, stride=1, pad=0, relu=False, bn_part=None):
-    """NHWC conv: out[B][OH][OW][N]; w = [Npad][Kpad] with K = KH*KW*C.  ``bn_part``: buffer for the
-    per-row-tile BatchNorm partial sums of the output (:func:`conv_bn_tiles` rows of [2][N])."""
+def _bn_kwargs(bn):
+    """igemm launch arguments of an in-launch BatchNorm statistics spec (kernels.h BnEpi):
+    ``bn`` = dict(ws, ticket, mode=0, vecs=[mean, invstd, run_mean, run_var], momentum, eps) or
+    dict(ws, ticket, mode=1, x=bn_input, vecs=[mean, invstd, gamma, dgamma, dbeta, coef], gscale)."""
+    if bn is None:
+        return {}
+    return dict(bn_ws=bn["ws"], bn_ticket=bn["ticket"], bn_mode=int(bn.get("mode", 0)), bn_vecs=list(bn["vecs"]),
+                bn_x=bn.get("x"), bn_momentum=float(bn.get("momentum", 0.1)), bn_eps=float(bn.get("eps", 1e-5)),
+                bn_gscale=float(bn.get("gscale", 1.0)))
+
+
+def conv_fwd(x, w, bias, out, KH, KW, stride=1, pad=0, relu=False, bn=None):
+    """NHWC conv: out[B][OH][OW][N]; w = [Npad][Kpad] with K = KH*KW*C.  ``bn``: the consuming
+    BatchNorm's statistics are finalised inside this launch (:func:`_bn_kwargs`, :func:`conv_bn_layout`)."""
     B, H, W, C = x.shape
     _, OH, OW, N = out.shape
     if x.is_cuda:
         K = KH * KW * C
-        kw = {} if bn_part is None else {"bn_part": bn_part}
         _C().igemm_fwd(x, w, bias, None, out, B * OH * OW, N, K, w.shape[1], 0, N,
-                       _geom(H, W, C, OH, OW, KH, KW, stride, pad), MODE_FWD, relu, 1.0, **kw)
+                       _geom(H, W, C, OH, OW, KH, KW, stride, pad), MODE_FWD, relu, 1.0, **_bn_kwargs(bn))
     else:
         out.copy_(ref.conv_fwd(x, w, bias, KH, KW, stride, pad, relu))
     return out
 
 
-def conv_bn_tiles(B, H, W, C, OH, OW, N, KH, KW, stride, pad, Kpad) -> int:
-    """Row tiles of the conv forward launch when it can emit BatchNorm partial sums (0: it cannot)."""
+def conv_bn_layout(B, H, W, C, OH, OW, N, KH, KW, stride, pad, Kpad, dgrad=False):
+    """(row tiles, column ranges) of the conv launch (forward, or the data gradient whose output is
+    [B][H][W][C] from an output gradient [B][OH][OW][N]) when it can finalise BatchNorm statistics of
+    its output inside the launch; (0, 0) when it cannot.  Sizes: ws (ntm + ceil(ntm / 16)) * 2 * channels
+    floats, tickets ntn * (1 + ceil(ntm / 16)) int32 (zero-initialised)."""
     m = native.get(build_if_missing=False)
     if m is None or not hasattr(m, "igemm64_bn_tiles"):
-        return 0
-    return int(m.igemm64_bn_tiles(B * OH * OW, N, KH * KW * C, Kpad, _geom(H, W, C, OH, OW, KH, KW, stride, pad),
-                                  MODE_FWD))
+        return 0, 0
+    if dgrad:
+        r = m.igemm64_bn_tiles(B * H * W, C, KH * KW * N, Kpad, _geom(OH, OW, N, H, W, KH, KW, stride, pad), MODE_DGRAD)
+    else:
+        r = m.igemm64_bn_tiles(B * OH * OW, N, KH * KW * C, Kpad, _geom(H, W, C, OH, OW, KH, KW, stride, pad), MODE_FWD)
+    return int(r[0]), int(r[1])
 
 
 def bn_finalize_partials(part, ntm, C, M, mean, invstd, run_mean, run_var, momentum, eps):
@@ -224,16 +240,19 @@ def kcnn_bwd(x, w1, b1, w2t, dyp, code, slabs, g_w1, g_b1, g_w2, g_b2, step_inc=
                   slabs, g_w1, g_b1, g_w2, g_b2, step_inc=step_inc)
 
 
-def conv_dgrad(dy, w, wt, out, KH, KW, stride=1, pad=0, mask=None, residual=None, residual_mask=None):
+def conv_dgrad(dy, w, wt, out, KH, KW, stride=1, pad=0, mask=None, residual=None, residual_mask=None, bn=None):
     """dX (NHWC [B][H][W][C]) of a conv whose output gradient is dy [B][OH][OW][N].
 
-    Epilogue (ResNet block join): dX = (conv^T dy + residual * [residual_mask > 0]) * [mask > 0]."""
+    Epilogue (ResNet block join): dX = (conv^T dy + residual * [residual_mask > 0]) * [mask > 0].
+    ``bn`` (mode 1): dX is the output gradient of a BatchNorm; its backward statistics are finalised
+    inside this launch (:func:`_bn_kwargs`)."""
     B, OH, OW, N = dy.shape
     _, H, W, C = out.shape
     if dy.is_cuda:
         K = KH * KW * N
         _C().igemm_fwd(dy, wt, None, mask, out, B * H * W, C, K, wt.shape[1], 0, C,
-                       _geom(OH, OW, N, H, W, KH, KW, stride, pad), MODE_DGRAD, False, 1.0, residual, residual_mask)
+                       _geom(OH, OW, N, H, W, KH, KW, stride, pad), MODE_DGRAD, False, 1.0, residual, residual_mask,
+                       **_bn_kwargs(bn))
     else:
         dx = ref.conv_dgrad(dy, w, out.shape, KH, KW, stride, pad, None)
         if residual is not None:
@@ -528,6 +547,16 @@ def bn_apply(x2d, y2d, gamma, beta, mean, invstd, relu=False, residual=None, res
             y = y + (aff(r, *residual_bn) if residual_bn is not None else r.float())
         y2d.copy_(torch.relu(y) if relu else y)
     return y2d
+
+
+def bn_dx(x2d, g2d, dx2d, coef):
+    """dx = k1 g + k2 x + k3 per channel (coef [3][C] from a finalised backward statistics pass)."""
+    M, C = x2d.shape
+    if x2d.is_cuda:
+        _C().bn_dx(x2d, None, g2d, dx2d, coef, M, C)
+    else:
+        dx2d.copy_(coef[:C] * g2d.float() + coef[C:2 * C] * x2d.float() + coef[2 * C:3 * C])
+    return dx2d
 
 
 def bn_bwd(x2d, mask2d, dy2d, dx2d, gamma, mean, invstd, dgamma, dbeta, ws, coef, counter, gscale=1.0):

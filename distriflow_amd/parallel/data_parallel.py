@@ -70,6 +70,7 @@ class DataParallelTrainer:
         self._multi, self._multi_u = None, 0  # multi-step graph (prepare_run)
         self._graph_B = None
         self._index_stream = None
+        self.preprocess_callbacks: list = []
         self.steps = 0
         # device run statistics [loss sum, correct, updates, -]: accumulated inside the step's own last
         # launch (no extra launch), read back asynchronously per replay when callbacks are registered
@@ -277,7 +278,44 @@ class DataParallelTrainer:
         else:
             self.xb = net.x_buf
 
+    # ------------------------------------------------------------------ preprocess callbacks on the device path
+    def add_preprocess_callback(self, cb):
+        """Run ``cb(Batch) -> Batch`` on every training batch, as the reference's dataset does on every
+        dispensed batch (/root/reference/src/server/dataset.ts:87-96).  On the device engine the batch is
+        gathered from the HBM dataset (one launch), ``Batch.x`` is its fp32 [B, ...] image tensor and
+        ``Batch.y`` its int32 labels, both on the GPU; ``Batch.batch`` is the device step cursor (a
+        1-element int64 tensor) and ``Batch.epoch`` is -1 (epochs are a host-side notion here).  The
+        callback must be made of device tensor ops with fixed shapes: it is captured into the step's
+        hipGraph and replayed with it.  It may return new tensors or modify ``x`` / ``y`` in place."""
+        self.preprocess_callbacks.append(cb)
+        self._graph = None  # the captured step must include it
+        self._multi, self._multi_u = None, 0
+
+    addPreprocessCallback = add_preprocess_callback
+
+    def _gather_preprocessed(self):
+        from ..data.dataset import Batch
+
+        net = self.net
+        xb, yb = net.x_buf, net.y_buf
+        ops.gather_batch(self.data, self.labels, self.idx, xb, yb, self.scale)
+        cursor = self._index_stream[1] if self._index_stream is not None else torch.zeros(1, dtype=torch.int64,
+                                                                                          device=xb.device)
+        b = Batch(cursor, -1, xb.float(), yb, 0, int(xb.shape[0]), self.idx)
+        for cb in self.preprocess_callbacks:
+            b = cb(b)
+        if tuple(b.x.shape) != tuple(xb.shape) or tuple(b.y.shape) != tuple(yb.shape):
+            raise ValueError("a preprocess callback must keep the batch shapes "
+                             f"(x {tuple(xb.shape)}, y {tuple(yb.shape)})")
+        xb.copy_(b.x)
+        if b.y is not yb:
+            yb.copy_(b.y)
+        self.xb, self.yb = xb, yb
+
     def _gather(self):
+        if self.preprocess_callbacks:
+            self._gather_preprocessed()
+            return
         if isinstance(self.xb, ops.GatherRef):
             if self.net.head_start is not None:
                 # the fused head reads labels through the index vector: no gather launch
@@ -350,8 +388,11 @@ class DataParallelTrainer:
         if scale is None:
             scale = 1.0 / 255.0 if ds.x.dtype == torch.uint8 else 1.0
         self.bind_dataset(ds.x, ds.y, ds.batch_size, scale=scale)
+        for cb in ds.preprocess_callbacks:  # the dataset's preprocess chain runs on every device batch
+            if cb not in self.preprocess_callbacks:
+                self.add_preprocess_callback(cb)
         epochs_left = max(1, ds.epochs - ds.epoch)
-        stream = ds.index_stream(rank, world, device=self.net.device)
+        stream = ds.index_stream(rank, world, device=self.net.device, allow_preprocess=True)
         self.bind_index_stream(stream)
         self.steps_per_epoch = max(1, stream.shape[0] // epochs_left)
         self.schedule_steps = int(stream.shape[0])

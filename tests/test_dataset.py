@@ -129,3 +129,63 @@ def test_trainer_binds_a_distri_dataset_cpu():
     assert steps == 16 and tr.steps_per_epoch == 8
     losses = [float(tr.step()[0]) / 64 for _ in range(steps)]
     assert losses[-1] < losses[0]
+
+
+def test_trainer_runs_dataset_preprocess_callbacks_cpu():
+    """The device engines run the dataset's preprocess chain on every batch (reference
+    /root/reference/src/server/dataset.ts:87-96): a step with a callback equals a plain step on the
+    batch the callback produced."""
+    import torch
+
+    from distriflow_amd.data.dataset import DistriDataset
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer
+
+    data, labels = synthetic_mnist(256, seed=3, device="cpu")
+    seen = []
+
+    def invert_and_shift(b):
+        seen.append((int(b.batch[0]), b.epoch, tuple(b.x.shape)))
+        b.x = 1.0 - b.x
+        b.y = (b.y + 1) % 10
+        return b
+
+    ds = DistriDataset(data, labels, {"batchSize": 32, "epochs": 1}, shuffle=False)
+    ds.add_preprocess_callback(invert_and_shift)
+    a = build_model("mlp_mnist", device="cpu", seed=0)
+    b = build_model("mlp_mnist", device="cpu", seed=0)
+    tr = DataParallelTrainer(a, lr=0.1, graph="none")
+    assert tr.bind_distri_dataset(ds) == 8
+    ref = DataParallelTrainer(b, lr=0.1, graph="none")
+    for k in range(3):
+        st = tr.step()
+        rows = torch.arange(32 * k, 32 * (k + 1))
+        x = 1.0 - data[rows].float().reshape(32, 28, 28, 1) / 255.0
+        y = ((labels[rows] + 1) % 10).to(torch.int32)
+        st_ref = ref.train_step(x.to(b.dtype).float(), y)
+        torch.testing.assert_close(st, st_ref)
+        torch.testing.assert_close(a.store.master, b.store.master)
+    assert [s[0] for s in seen] == [0, 1, 2] and all(s[1] == -1 and s[2] == (32, 28, 28, 1) for s in seen)
+
+
+def test_preprocess_callback_must_keep_shapes_cpu():
+    import pytest
+    import torch
+
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
+
+    data, labels = synthetic_mnist(128, seed=3, device="cpu")
+    tr = DataParallelTrainer(build_model("mlp_mnist", device="cpu", seed=0), lr=0.1, graph="none")
+    tr.bind_dataset(data, labels, 32, scale=1 / 255.0)
+    tr.bind_index_stream(epoch_permutations(128, 32, 4, "cpu", seed=0))
+
+    def crop(b):
+        b.x = b.x[:, :20]
+        return b
+
+    tr.add_preprocess_callback(crop)
+    with pytest.raises(ValueError):
+        tr.step()

@@ -320,8 +320,8 @@ def test_per_layer_numerics_against_cpu(name, B, monkeypatch):
 
 
 def test_bn_statistics_from_conv_epilogue(monkeypatch):
-    """BatchNorm batch statistics from the producing conv's epilogue partial sums (csrc/igemm64.hip
-    bn_part + csrc/bn.hip bn_finalize_partials), per conv of every ResNet-18 stage, against fp64
+    """BatchNorm batch statistics finalised inside the producing conv launch (csrc/igemm64.hip epilogue +
+    csrc/bn_epi.h, no statistics or finalize launch), per conv of every ResNet-18 stage, against fp64
     statistics of the conv's stored output."""
     from distriflow_amd.models.layers import ResidualBlock
 
@@ -334,7 +334,7 @@ def test_bn_statistics_from_conv_epilogue(monkeypatch):
     torch.manual_seed(2)
     for blk in blocks:
         for conv, bn in [(blk.conv1, blk.bn1), (blk.conv2, blk.bn2)]:
-            if not getattr(conv, "_bn_ntm", 0):
+            if conv._bn_fwd is None:
                 continue
             x = torch.relu(torch.randn((B,) + tuple(conv.in_shape), device="cuda")).to(torch.bfloat16)
             rm0, rv0 = bn.run_mean.clone(), bn.run_var.clone()
@@ -351,3 +351,43 @@ def test_bn_statistics_from_conv_epilogue(monkeypatch):
             bn._stats_ready = False
             checked += 1
     assert checked >= 8
+
+
+def test_bn_backward_statistics_from_dgrad_epilogue(monkeypatch):
+    """bn1's backward statistics (dgamma, dbeta, dx coefficients) finalised inside conv2's data-gradient
+    launch (mode 1 of csrc/bn_epi.h) equal the standalone statistics pass on the same gradient, and the
+    block's dx equals the unfused path's."""
+    from distriflow_amd import ops
+    from distriflow_amd.models.layers import ResidualBlock
+
+    monkeypatch.setenv("DISTRIFLOW_DIAG", "bn_epilogue=1")
+    net = build_model("resnet18_cifar", device="cuda", seed=6)
+    B = 16
+    net.bind(B)
+    st = net.store
+    blocks = [b for b in net.exec_layers if isinstance(b, ResidualBlock)]
+    checked = 0
+    torch.manual_seed(3)
+    for blk in blocks:
+        if not blk.conv2.can_emit_bn_grad():
+            continue
+        x = torch.relu(torch.randn((B,) + tuple(blk.conv1.in_shape), device="cuda")).to(torch.bfloat16)
+        h = blk.conv1.forward(x, True, bn=blk.bn1)
+        blk.bn1.forward(h, True)
+        d2 = (torch.randn((B,) + tuple(blk.conv2.out_shape), device="cuda") * 0.1).to(torch.bfloat16)
+        # fused: conv2's dgrad masks with relu'(bn1 out) and finalises bn1's backward statistics
+        g = blk.conv2.backward_data(d2, dx_mask=blk.bn1.out, bn=blk.bn1).clone()
+        dg, db, coef = (st.gradient(f"{blk.bn1.name}/gamma").clone(), st.gradient(f"{blk.bn1.name}/beta").clone(),
+                        blk.bn1.coef.clone())
+        dx_f = blk.bn1.backward_dx(g).clone()
+        # standalone: plain dgrad, then the statistics pass with the relu' mask
+        raw = blk.conv2.backward_data(d2).clone()
+        dx_s = blk.bn1.backward(raw).clone()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(g.float(), (raw.float() * (blk.bn1.out.float() > 0)), rtol=0, atol=0)
+        torch.testing.assert_close(dg, st.gradient(f"{blk.bn1.name}/gamma"), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(db, st.gradient(f"{blk.bn1.name}/beta"), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(coef, blk.bn1.coef, rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(dx_f.float(), dx_s.float(), rtol=2e-2, atol=1e-3)
+        checked += 1
+    assert checked >= 4
