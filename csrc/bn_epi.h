@@ -6,6 +6,12 @@
 // then draws a ticket.  The last of `n` arrivers reads the slabs with sc1 loads, so neither side pays an
 // agent-scope release (L2 write-back) or acquire.  The last arriver re-arms the counter for the next
 // launch.  Every sum runs in a fixed order (tile order, then group order): deterministic.
+// Memory-model note: the ordering this relies on -- write-through (sc1) stores drained by
+// s_waitcnt vmcnt(0) in every storing wave before a relaxed agent-scope ticket RMW, then sc1 loads in
+// the last arriver -- is the gfx950 hand-off form of cdna_hip_programming.md Guideline 16 (R1, counter
+// variant) and MI355X_MICROARCH.md's visibility rules, not a C++-memory-model happens-before: the
+// vmcnt drain is what makes the stores globally performed before the ticket.  This header is gfx950
+// only (the build targets nothing else); a port would put release / acquire on the ticket instead.
 #pragma once
 #include "common.h"
 #include "kernels.h"
