@@ -814,7 +814,8 @@ void head_train_py(std::vector<torch::Tensor> w, std::vector<c10::optional<torch
   const int64_t B = x.size(0);
   const int64_t ldt = (B + 31) / 32 * 32;
   TORCH_CHECK(x.numel() == B * K[0], "x must have B*K0 elements");
-  TORCH_CHECK(K[0] % 8 == 0 && K[0] <= 1024, "head: K0 must be a multiple of 8 and <= 1024");
+  // (the weight-gradient phase alone streams X^T: any K0; the forward phase stages X rows in LDS)
+  TORCH_CHECK(K[0] % 8 == 0 && (K[0] <= 1024 || phases == 2), "head: K0 must be a multiple of 8 and <= 1024");
   TORCH_CHECK(N[nl - 1] <= 16, "head: at most 16 classes");
   dfa::HeadArgs a{};
   a.nl = nl;
@@ -895,9 +896,139 @@ void head_train_py(std::vector<torch::Tensor> w, std::vector<c10::optional<torch
   need(stats, at::kFloat, "stats");
   TORCH_CHECK(stats.numel() >= 2, "head: stats must hold 2 floats");
   a.stats = stats.data_ptr<float>();
-  TORCH_CHECK(dfa::head_train_lds(a) <= 160 * 1024, "head: LDS footprint too large");
+  TORCH_CHECK(phases == 2 || dfa::head_train_lds(a) <= 160 * 1024, "head: LDS footprint too large");
   a.dx_scale = (float)dx_scale;
   check_hip(dfa::head_train(a, (int)phases, cur_stream()), "head_train");
+}
+
+// The reference CNN's dense head (csrc/khead.hip): forward, softmax-CE and both data gradients in one
+// launch; the weight gradients then come from head_train(phases=2) over (pT, h1T, dz1T, dz2T).
+void khead_train_py(torch::Tensor p, torch::Tensor pT, c10::optional<torch::Tensor> dp, torch::Tensor w1,
+                    torch::Tensor w1t, c10::optional<torch::Tensor> b1, torch::Tensor w2, torch::Tensor w2t,
+                    c10::optional<torch::Tensor> b2, double drop_p, int64_t drop_seed,
+                    c10::optional<torch::Tensor> drop_step, int64_t drop_step_add, double dh_scale, double dp_scale,
+                    bool dp_mask, torch::Tensor h1T, torch::Tensor dz1T, torch::Tensor dz2T,
+                    c10::optional<torch::Tensor> logits, torch::Tensor labels, c10::optional<torch::Tensor> idx,
+                    double grad_scale, torch::Tensor loss_part, torch::Tensor ws) {
+  need(p, at::kBFloat16, "p");
+  TORCH_CHECK(p.dim() >= 2, "p must be [B, ...]");
+  const int64_t B = p.size(0), K = p.numel() / std::max<int64_t>(B, 1);
+  const int64_t ldt = (B + 31) / 32 * 32;
+  const int64_t C = dz2T.size(0);
+  TORCH_CHECK(dfa::khead_supported((int)K, (int)C), "khead: K must be a multiple of 256 (LDS-bounded), 1 <= C <= 16");
+  const int N1 = dfa::kKHeadN1;
+  dfa::KHeadArgs a{};
+  a.B = (int)B;
+  a.K = (int)K;
+  a.C = (int)C;
+  a.ldt = (int)ldt;
+  a.p = reinterpret_cast<const dfa::bf16*>(p.data_ptr());
+  need(pT, at::kBFloat16, "pT");
+  TORCH_CHECK(pT.numel() >= K * ldt, "khead: pT must be [K][round32(B)]");
+  a.pT = reinterpret_cast<dfa::bf16*>(pT.data_ptr());
+  if (dp.has_value() && dp->defined()) {
+    need(*dp, at::kBFloat16, "dp");
+    TORCH_CHECK(dp->numel() >= B * K, "khead: dp too small");
+    a.dp = reinterpret_cast<dfa::bf16*>(dp->data_ptr());
+  }
+  need(w1, at::kBFloat16, "w1");
+  TORCH_CHECK(w1.dim() == 2 && w1.size(0) >= N1 && w1.size(1) >= K, "khead: w1 must be [128][>= K]");
+  a.w1 = reinterpret_cast<const dfa::bf16*>(w1.data_ptr());
+  a.ldw1 = (int)w1.size(1);
+  need(w1t, at::kBFloat16, "w1t");
+  TORCH_CHECK(w1t.dim() == 2 && w1t.size(0) >= K && w1t.size(1) == N1, "khead: w1t must be [>= K][128]");
+  a.w1t = reinterpret_cast<const dfa::bf16*>(w1t.data_ptr());
+  need(w2, at::kBFloat16, "w2");
+  TORCH_CHECK(w2.dim() == 2 && w2.size(0) >= 16 && w2.size(1) == N1, "khead: w2 must be [16][128]");
+  a.w2 = reinterpret_cast<const dfa::bf16*>(w2.data_ptr());
+  need(w2t, at::kBFloat16, "w2t");
+  TORCH_CHECK(w2t.dim() == 2 && w2t.size(0) >= N1 && w2t.size(1) == 32, "khead: w2t must be [128][32]");
+  a.w2t = reinterpret_cast<const dfa::bf16*>(w2t.data_ptr());
+  if (b1.has_value() && b1->defined()) {
+    need(*b1, at::kFloat, "b1");
+    TORCH_CHECK(b1->numel() >= N1, "khead: b1 too small");
+    a.b1 = b1->data_ptr<float>();
+  }
+  if (b2.has_value() && b2->defined()) {
+    need(*b2, at::kFloat, "b2");
+    TORCH_CHECK(b2->numel() >= C, "khead: b2 too small");
+    a.b2 = b2->data_ptr<float>();
+  }
+  a.drop = drop_from(drop_p, drop_seed, drop_step, drop_step_add);
+  a.dh_scale = (float)dh_scale;
+  a.dp_scale = (float)dp_scale;
+  a.dp_mask = dp_mask ? 1 : 0;
+  for (auto* t : {&h1T, &dz1T}) {
+    need(*t, at::kBFloat16, "h1T/dz1T");
+    TORCH_CHECK(t->numel() >= N1 * ldt, "khead: h1T / dz1T must be [128][round32(B)]");
+  }
+  need(dz2T, at::kBFloat16, "dz2T");
+  TORCH_CHECK(dz2T.numel() >= C * ldt, "khead: dz2T must be [C][round32(B)]");
+  a.h1T = reinterpret_cast<dfa::bf16*>(h1T.data_ptr());
+  a.dz1T = reinterpret_cast<dfa::bf16*>(dz1T.data_ptr());
+  a.dz2T = reinterpret_cast<dfa::bf16*>(dz2T.data_ptr());
+  if (logits.has_value() && logits->defined()) {
+    need(*logits, at::kFloat, "logits");
+    TORCH_CHECK(logits->numel() >= B * C, "khead: logits too small");
+    a.logits = logits->data_ptr<float>();
+  }
+  need(labels, at::kInt, "labels");
+  a.labels = labels.data_ptr<int>();
+  a.nrows = labels.numel();
+  if (idx.has_value() && idx->defined()) {
+    need(*idx, at::kLong, "idx");
+    TORCH_CHECK(idx->numel() >= B, "khead: idx too small");
+    a.idx = reinterpret_cast<const long long*>(idx->data_ptr());
+  } else {
+    TORCH_CHECK(labels.numel() >= B, "khead: labels too small");
+  }
+  a.grad_scale = (float)grad_scale;
+  need(loss_part, at::kFloat, "loss_part");
+  TORCH_CHECK(loss_part.numel() >= 2 * ((B + 15) / 16), "khead: loss_part must hold 2 floats per 16 rows");
+  a.loss_part = loss_part.data_ptr<float>();
+  need(ws, at::kFloat, "ws");
+  TORCH_CHECK(ws.numel() >= (int64_t)dfa::khead_ws_floats((int)B, (int)K), "khead: workspace too small");
+  const int64_t nt = (B + 31) / 32;
+  float* base = ws.data_ptr<float>();
+  a.slab = base;
+  a.dz1 = reinterpret_cast<dfa::bf16*>(base + nt * dfa::kKHeadChunks * 32 * N1);
+  a.sync = reinterpret_cast<unsigned*>(base + nt * dfa::kKHeadChunks * 32 * N1 + nt * 32 * N1 / 2);
+  check_hip(dfa::khead_train(a, cur_stream()), "khead_train");
+}
+
+// Weight gradients of that head (csrc/khead.hip khead_wgrad_kernel) + the stats reduction: one launch.
+void khead_wgrad_py(torch::Tensor pT, torch::Tensor h1T, torch::Tensor dz1T, torch::Tensor dz2T, torch::Tensor gw1,
+                    c10::optional<torch::Tensor> gb1, torch::Tensor gw2, c10::optional<torch::Tensor> gb2, int64_t B,
+                    int64_t K, int64_t C, torch::Tensor loss_part, torch::Tensor stats) {
+  const int64_t ldt = (B + 31) / 32 * 32;
+  const int N1 = dfa::kKHeadN1;
+  for (auto* t : {&pT, &h1T, &dz1T, &dz2T}) need(*t, at::kBFloat16, "khead wgrad operand");
+  TORCH_CHECK(pT.numel() >= K * ldt && h1T.numel() >= N1 * ldt && dz1T.numel() >= N1 * ldt &&
+                  dz2T.numel() >= C * ldt, "khead_wgrad: operands must be [rows][round32(B)]");
+  need(gw1, at::kFloat, "gw1");
+  need(gw2, at::kFloat, "gw2");
+  TORCH_CHECK(gw1.numel() >= N1 * K && gw2.numel() >= C * N1, "khead_wgrad: gradient buffers too small");
+  dfa::KHeadWgradArgs a{};
+  a.ldt = (int)ldt;
+  a.L[0] = {reinterpret_cast<const dfa::bf16*>(dz1T.data_ptr()), reinterpret_cast<const dfa::bf16*>(pT.data_ptr()),
+            gw1.data_ptr<float>(), nullptr, N1, (int)K, 0, 0};
+  a.L[1] = {reinterpret_cast<const dfa::bf16*>(dz2T.data_ptr()), reinterpret_cast<const dfa::bf16*>(h1T.data_ptr()),
+            gw2.data_ptr<float>(), nullptr, (int)C, N1, 0, 0};
+  if (gb1.has_value() && gb1->defined()) {
+    need(*gb1, at::kFloat, "gb1");
+    a.L[0].gb = gb1->data_ptr<float>();
+  }
+  if (gb2.has_value() && gb2->defined()) {
+    need(*gb2, at::kFloat, "gb2");
+    a.L[1].gb = gb2->data_ptr<float>();
+  }
+  need(loss_part, at::kFloat, "loss_part");
+  need(stats, at::kFloat, "stats");
+  a.nloss = (int)((B + 15) / 16);
+  TORCH_CHECK(loss_part.numel() >= 2 * a.nloss && stats.numel() >= 2, "khead_wgrad: loss_part / stats too small");
+  a.loss_part = loss_part.data_ptr<float>();
+  a.stats = stats.data_ptr<float>();
+  check_hip(dfa::khead_wgrad(a, cur_stream()), "khead_wgrad");
 }
 
 class P2PComm;
@@ -1669,7 +1800,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("K"), py::arg("N"), py::arg("x"), py::arg("x_relu"), py::arg("xT"), py::arg("dx"), py::arg("logits"),
         py::arg("labels"), py::arg("idx"), py::arg("grad_scale"), py::arg("loss_part"), py::arg("stats"),
         py::arg("phases"), py::arg("dx_scale") = 1.0);
-  m.def("kcnn_fwd", &kcnn_fwd_py, "reference CNN conv block forward (conv1 + conv2 + pool [+ dropout], 1 launch)",
+  m.def("khead_train", &khead_train_py,
+        "reference CNN dense head: forward + softmax-CE + both data gradients (1 launch, split-K)", py::arg("p"),
+        py::arg("pT"), py::arg("dp"), py::arg("w1"), py::arg("w1t"), py::arg("b1"), py::arg("w2"), py::arg("w2t"),
+        py::arg("b2"), py::arg("drop_p"), py::arg("drop_seed"), py::arg("drop_step"), py::arg("drop_step_add"),
+        py::arg("dh_scale"), py::arg("dp_scale"), py::arg("dp_mask"),
+        py::arg("h1T"), py::arg("dz1T"), py::arg("dz2T"), py::arg("logits"), py::arg("labels"), py::arg("idx"),
+        py::arg("grad_scale"), py::arg("loss_part"), py::arg("ws"));
+  m.def("khead_wgrad", &khead_wgrad_py, "reference CNN dense head: weight gradients + loss stats (1 launch)");
+  m.def("khead_set_stamps", [](c10::optional<torch::Tensor> buf) {
+    dfa::khead_set_stamps(buf.has_value() && buf->defined() ? buf->data_ptr() : nullptr);
+  }, "profiling aid: per-workgroup phase clocks of the khead launch into buf ([G][16] int64), None = off");
+  m.def("khead_ws_floats", [](int64_t B, int64_t K) { return (int64_t)dfa::khead_ws_floats((int)B, (int)K); });
+  m.def("khead_supported", [](int64_t K, int64_t C) { return dfa::khead_supported((int)K, (int)C); });
+  m.def("kcnn_fwd", &kcnn_fwd_py,"reference CNN conv block forward (conv1 + conv2 + pool [+ dropout], 1 launch)",
         py::arg("x"), py::arg("idx"), py::arg("scale"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("kpad1"),
         py::arg("w2"), py::arg("b2"), py::arg("pooled"), py::arg("code"), py::arg("drop_p") = 0.0,
         py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("drop_step_add") = 0);

@@ -452,6 +452,56 @@ size_t kcnn_slab_floats(int B);
 hipError_t kcnn_fwd(const KcnnArgs& a, hipStream_t st);
 hipError_t kcnn_bwd(const KcnnArgs& a, float* g_w1, float* g_b1, float* g_w2, float* g_b2, long long* step_inc,
                     hipStream_t st);
+// The reference CNN's dense head (csrc/khead.hip): dense 4608 -> 128 ReLU [+ folded dropout] -> dense C
+// softmax-CE, forward, loss and both data gradients in ONE launch (split-K over 8 workgroups per 32 rows).
+constexpr int kKHeadRows = 32, kKHeadChunks = 8, kKHeadN1 = 128;
+struct KHeadArgs {
+  const bf16* p;      // [B][K] dense1 input
+  bf16* pT;           // [K][ldt] its transpose (dense1 weight-gradient operand)
+  bf16* dp;           // [B][K] dense1 data gradient (nullable)
+  const bf16* w1;     // [128][ldw1] forward layout
+  const bf16* w1t;    // [>= K][128] data-gradient layout
+  const float* b1;    // [128] (nullable)
+  const bf16* w2;     // [16][128]
+  const bf16* w2t;    // [128][32]
+  const float* b2;    // [C] (nullable)
+  DropSpec drop;      // dropout after dense1 (folded into its epilogue)
+  float dh_scale;     // dense2's dX scale (the folded dropout's 1/(1-p); 1 = none)
+  float dp_scale;     // dense1's dX scale (a dropout folded below dense1; 1 = none)
+  int dp_mask;        // relu'(P) on dense1's dX
+  bf16 *h1T, *dz1T, *dz2T;  // [128][ldt], [128][ldt], [C][ldt]
+  float* logits;      // [B][C] fp32 (nullable)
+  const int* labels;  // labels (through idx when idx != null)
+  const long long* idx;
+  long long nrows;
+  float grad_scale;
+  float* loss_part;   // [cdiv(B, 16)][2] (the fused head kernels' layout)
+  float* slab;        // [ntiles][8][32 * 128] split-K partials
+  bf16* dz1;          // [ntiles][32][128] published dZ1 tiles
+  unsigned* sync;     // [ntiles] tickets, [ntiles] flags, {launch tag, finished workgroups}
+  unsigned long long* stamps;  // profiling aid (khead_set_stamps): [G][16] phase clocks, or null
+  int B, K, C, ldt, ldw1, ntiles, G;
+};
+void khead_set_stamps(void* buf);
+// Weight gradients of that head (csrc/khead.hip khead_wgrad_kernel): dW = dZ^T X over the whole batch
+// in 64 x 32 output tiles (bias = the column k == K of ones), plus the loss partials -> stats.
+struct KHeadWgradLayer {
+  const bf16* a;  // dZ^T [N][ldt]
+  const bf16* b;  // X^T [K][ldt]
+  float *gw, *gb;  // [N][K], [N] (nullable)
+  int N, K, nblk, kblk;
+};
+struct KHeadWgradArgs {
+  KHeadWgradLayer L[2];
+  int ldt, jobs, nloss;
+  const float* loss_part;
+  float* stats;
+};
+hipError_t khead_wgrad(KHeadWgradArgs a, hipStream_t st);
+size_t khead_ws_floats(int B, int K);
+size_t khead_lds(int K);
+bool khead_supported(int K, int C);
+hipError_t khead_train(KHeadArgs a, hipStream_t st);
 int lenet_dense_part_floats(int B);  // reduce scratch: job slabs + arrival tickets
 int lenet_red_slab_floats();
 size_t lenet_train_lds();

@@ -12,6 +12,8 @@ Python switches (default in brackets):
   async_fused [1]          async PS step = train + reduce/apply (0: pull / compute / apply launches)
   kcnn_fused [1]           the reference CNN's conv block as one forward + one backward kernel
   fold_dropout [1]         dropout folded into producer epilogues
+  khead_fused [1]          the reference CNN's dense head (4608 -> 128 -> C + CE) as one split-K launch
+                           plus the fused head weight-gradient launch (0: per-layer GEMMs + head kernels)
   multistep [1]            bench.py unrolls up to 64 steps per hipGraph (0: one replay per step)
   wgrad_overlap [1]        ResNet weight gradients on a side stream
   proj_overlap [1]         ResNet projection shortcut on a side stream
@@ -25,7 +27,7 @@ from __future__ import annotations
 
 import os
 
-_DEFAULTS = {"lenet_fused": 1, "lenet_fused_update": 1, "async_fused": 1, "kcnn_fused": 1, "fold_dropout": 1,
+_DEFAULTS = {"lenet_fused": 1, "lenet_fused_update": 1, "async_fused": 1, "kcnn_fused": 1, "khead_fused": 1, "fold_dropout": 1,
              "multistep": 1, "wgrad_overlap": 1, "proj_overlap": 1, "concurrent_backward": 0, "bn_epilogue": 0}
 
 

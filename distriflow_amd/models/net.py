@@ -149,6 +149,9 @@ class Net:
         self.exec_layers = execd
         self.output_shape = shape
         self.head_start = self._plan_head(execd) if self.fuse else None
+        self.khead = self._plan_khead(execd) if self.fuse else False
+        if self.khead:
+            self.head_start = len(execd) - 2
         self.lenet_fused = self._plan_lenet(execd) if self.fuse else False
 
     def _plan_lenet(self, execd) -> bool:
@@ -196,6 +199,23 @@ class Net:
                 continue
             return j
         return None
+
+    def _plan_khead(self, execd) -> bool:
+        """True when the graph ends in the reference CNN's dense head -- Dense(K -> 128, ReLU) [+ folded
+        Dropout] -> Dense(128 -> C <= 16) logits with softmax-CE, K a multiple of 256 -- on the GPU: the
+        head's forward, loss and both data gradients then run as ONE split-K launch (csrc/khead.hip) and
+        its weight gradients as the fused head weight-gradient launch.  ``DISTRIFLOW_DIAG=khead_fused=0``
+        keeps the per-layer path."""
+        if not self.is_gpu or not diag_on("khead_fused") or self.final_act == "sigmoid" or len(execd) < 3:
+            return False
+        d1, d2 = execd[-2], execd[-1]
+        if not (isinstance(d1, Dense) and isinstance(d2, Dense)):
+            return False
+        if not (d1.relu and d1.units == 128 and not d1.out_f32 and d2.drop is None and not d2.relu):
+            return False
+        if d1.drop is not None and not d2.in_relu:
+            return False
+        return d2.units <= 16 and d1.need_dx and ops.khead_supported(d1.in_features, d2.units)
 
     @staticmethod
     def _fold_dropout(execd):
@@ -289,6 +309,9 @@ class Net:
             self.head_hT = [z(l.units, ldt) for l in head[:-1]] + [None]
             self.head_dzT = [z(l.units, ldt) for l in head]
             self.head_loss_part = torch.zeros(2 * ((B + 15) // 16), dtype=torch.float32, device=self.device)
+            if self.khead:  # split-K slabs, published dZ1 tiles, tickets / flags / launch tag (zeroed)
+                self.khead_ws = torch.zeros(ops.khead_ws_floats(B, head[0].in_features), dtype=torch.float32,
+                                            device=self.device)
         if self.lenet_fused:
             nblk = ops.lenet_blocks(B)
             self.lenet_conv_part = torch.empty(2576 * nblk, dtype=torch.float32, device=self.device)
@@ -475,7 +498,7 @@ class Net:
             loss_part=self.head_loss_part, stats=self.stats)
         head_ids = range(len(self.exec_layers) - 1, self.head_start - 1, -1)
         if not self.concurrent_backward:
-            ops.head_train(**args, phases=3)
+            self._head_launch(args, head, h, lab, idx, 3)
             if grad_ready is not None:
                 for i in head_ids:
                     grad_ready(i)
@@ -528,12 +551,12 @@ class Net:
         # hooks (bucketed all-reduce) fire after the join: a bucket spans layers whose gradients
         # complete on different streams.
         main = torch.cuda.current_stream(self.device)
-        ops.head_train(**args, phases=1)
+        self._head_launch(args, head, h, lab, idx, 1)
         ev = main.record_event()
         side = self._side
         side[0].wait_event(ev)
         with torch.cuda.stream(side[0]):
-            ops.head_train(**args, phases=2)
+            self._head_launch(args, head, h, lab, idx, 2)
         d = first.dx if first.need_dx else None
         k = 1
         for i in range(self.head_start - 1, -1, -1):
@@ -553,6 +576,31 @@ class Net:
             for i in range(len(self.exec_layers) - 1, -1, -1):
                 grad_ready(i)
         return self.stats
+
+    def _head_launch(self, args, head, x, labels, idx, phases):
+        """The dense head's launches: bit 1 forward + loss + data gradients, bit 2 weight gradients +
+        stats (csrc/mlphead.hip; the reference CNN's head: csrc/khead.hip)."""
+        if not self.khead:
+            ops.head_train(**args, phases=phases)
+            return
+        if phases & 1:
+            st = self.store
+            d1, d2 = head
+            ops.khead_train(x, self.head_xT, d1.dx, st.weight(f"{d1.name}/kernel"), st.weight_t(f"{d1.name}/kernel"),
+                            st[f"{d1.name}/bias"] if d1.use_bias else None, st.weight(f"{d2.name}/kernel"),
+                            st.weight_t(f"{d2.name}/kernel"), st[f"{d2.name}/bias"] if d2.use_bias else None,
+                            self.head_hT[0], self.head_dzT[0], self.head_dzT[1], d2.out, labels, idx,
+                            args["grad_scale"], self.head_loss_part, self.khead_ws, drop=d1.drop_spec(True),
+                            dh_scale=d2.dx_scale, dp_scale=d1.dx_scale, dp_mask=d1.in_relu)
+        if phases & 2:
+            st = self.store
+            d1, d2 = head
+            ops.khead_wgrad(self.head_xT, self.head_hT[0], self.head_dzT[0], self.head_dzT[1],
+                            st.grad_matrix(f"{d1.name}/kernel"),
+                            st.gradient(f"{d1.name}/bias") if d1.use_bias else None,
+                            st.grad_matrix(f"{d2.name}/kernel"),
+                            st.gradient(f"{d2.name}/bias") if d2.use_bias else None,
+                            x.shape[0], d1.in_features, d2.units, self.head_loss_part, self.stats)
 
     @torch.no_grad()
     def evaluate(self, x, labels, batch_size: int = 4096):

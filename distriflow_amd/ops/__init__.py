@@ -619,6 +619,34 @@ def head_train(w, wt, b, gw, gb, hT, dzT, K, N, x, x_relu, xT, dx, logits, label
                     dx_scale=float(dx_scale))
 
 
+def khead_supported(K: int, C: int) -> bool:
+    m = native.get(build_if_missing=False)
+    return m is not None and hasattr(m, "khead_train") and bool(m.khead_supported(int(K), int(C)))
+
+
+def khead_ws_floats(B: int, K: int) -> int:
+    return int(_C().khead_ws_floats(int(B), int(K)))
+
+
+def khead_train(p, pT, dp, w1, w1t, b1, w2, w2t, b2, h1T, dz1T, dz2T, logits, labels, idx, grad_scale, loss_part, ws,
+                drop=None, dh_scale=1.0, dp_scale=1.0, dp_mask=False):
+    """The reference CNN's dense head on GPU (csrc/khead.hip): dense1 (K -> 128, ReLU, folded ``drop``),
+    dense2 (128 -> C) and softmax-CE, forward + loss + both data gradients in ONE launch (split-K over 8
+    workgroups per 32 batch rows).  Writes logits, the loss partials, dP (``dp``) and the weight-gradient
+    operands P^T / H1^T / dZ1^T / dZ2^T that :func:`head_train` (phases=2) turns into gw / gb / stats."""
+    dk = _drop_kw(drop)
+    _C().khead_train(p.reshape(p.shape[0], -1), pT, dp, w1, w1t, b1, w2, w2t, b2, dk.get("drop_p", 0.0),
+                     dk.get("drop_seed", 0), dk.get("drop_step"), dk.get("drop_step_add", 0), float(dh_scale),
+                     float(dp_scale), bool(dp_mask), h1T, dz1T, dz2T, logits, labels, idx, float(grad_scale),
+                     loss_part, ws)
+
+
+def khead_wgrad(pT, h1T, dz1T, dz2T, gw1, gb1, gw2, gb2, B, K, C, loss_part, stats):
+    """Weight / bias gradients of the :func:`khead_train` head from its transposed operands, and the
+    loss partials -> stats (one launch, csrc/khead.hip)."""
+    _C().khead_wgrad(pT, h1T, dz1T, dz2T, gw1, gb1, gw2, gb2, int(B), int(K), int(C), loss_part, stats)
+
+
 METRIC_KINDS = {"meanSquaredError": 0, "mse": 0, "absoluteDifference": 1, "hingeLoss": 2, "huberLoss": 3,
                 "logLoss": 4, "sigmoidCrossEntropy": 5, "softmaxCrossEntropy": 6, "categorical_crossentropy": 7,
                 "categoricalCrossentropy": 7}

@@ -89,7 +89,9 @@ def test_keras_cnn_plan_has_no_dropout_launch():
     assert pool.drop is not None and pool.drop.rate == 0.25
     dense = [l for l in net.exec_layers if isinstance(l, Dense)]
     assert dense[0].drop is not None and dense[0].in_relu and abs(dense[0].dx_scale - 1 / 0.75) < 1e-12
-    assert net.head_start == len(net.exec_layers) - 1  # the logits layer alone is the fused head
+    # the reference CNN's two dense layers form the split-K head (csrc/khead.hip); otherwise the logits
+    # layer alone is the fused head
+    assert net.khead and net.head_start == len(net.exec_layers) - 2
     assert dense[1].in_relu and dense[1].dx_scale == 2.0
 
 
