@@ -1,0 +1,270 @@
+// 3x3 / stride-1 / pad-1 convolution forward and data gradient with halo-tiled LDS staging (gfx950).
+//
+//   FWD:   Y[p][co]  = sum_{tap, ci} X[p + off(tap)][ci] * W[co][tap][ci]
+//   DGRAD: dX[p][ci] = sum_{tap, co} dY[p + off(tap)][co] * Wt[ci][8 - tap][co]   (flipped taps)
+// the reference's tf.js conv2d forward and the data gradient of its autodiff (SURVEY §2.4 O3/O8,
+// /root/reference/src/common/models.ts:137-142), for the ResNet-18 CIFAR 3x3 stride-1 convs.
+//
+// igemm64.hip gathers the im2col rows of every tap from L2: a 128-pixel tile fetches its input 9 times
+// per 64-channel block, and the per-CU L2->LDS rate (~70 GB/s) bounds it at 240-600 TF/s.  Here:
+//   * a workgroup owns 128 consecutive output pixels (TI images x R rows x W columns) x BN output
+//     channels; per 64-channel input block it stages the input halo TI x (R+2) x (W+2) once (zero
+//     padding materialised) and runs all nine taps against it as shifted row reads
+//   * the weights of one (channel block, tap) step are staged per step (double buffer, XOR-swizzled
+//     128-byte rows as in igemm64); they are the MFMA A operand, so each lane ends with 4 consecutive
+//     output channels of one pixel (8-byte stores, 8-byte residual / mask loads in the epilogue)
+//   * halo rows are 72 bf16 (36 dwords) apart and MFMA column j of pixel tile t is pixel 2j + (t & 1)
+//     (+32 for t >= 2): the 16 rows a ds_read_b128 lane group reads, at two consecutive 16-byte chunks,
+//     land on 16 distinct 4-bank slots for any tap shift (slot = 9 row + chunk mod 16; the two chunks
+//     differ in parity)
+//   * the halo is single-buffered: the next block's halo sits in registers from the first tap of the
+//     current block and is stored after its ninth (one extra barrier per 9 steps); LDS = halo +
+//     2 weight buffers <= 74 KB, so two workgroups share a CU
+//   * 4 waves as 2 (pixel halves of 64) x 2 (channel halves of BN/2)
+//   * epilogue as igemm64: alpha, residual join (res * [resmask > 0]), ReLU, relu'(mask)
+#include "common.h"
+#include "kernels.h"
+#include "diag.h"
+
+namespace dfa {
+
+namespace {
+
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ u32x4_t kZeroC3 = {0u, 0u, 0u, 0u};  // source of every zero-padding chunk
+
+__device__ __forceinline__ u32x4_t cload16(const void* p) {
+  u32x4_t r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+
+constexpr int kCP = 128;              // output pixels per workgroup
+constexpr int kCS = 72;               // halo row stride (bf16)
+constexpr int kCXP = 9;               // halo staging passes of 32 rows
+constexpr int kCXR = 32 * kCXP;       // halo rows (>= TI * (R+2) * (W+2))
+
+struct C3P {
+  const bf16* src;   // NHWC [.][H][W][Cin]
+  const bf16* w;     // [Cout_pad][Kpad]: column tapW * Cin + ci
+  const bf16* res;
+  const bf16* resmask;
+  const bf16* mask;
+  bf16* out;         // [M][ldc]
+  int H, W, Cin, Cout, Kpad, ldc;
+  int R, HW2, HR2, hrows, rows_per_tile;
+  int ntiles, nco;
+  int relu;
+  float alpha;
+};
+
+__device__ __forceinline__ int wswz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3); }
+
+template <int BN, bool FLIP>
+__global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
+  constexpr int TN = BN / 32;          // 16-channel tiles per wave
+  constexpr int WP = BN * 8 / 256;     // weight staging passes (32 rows each)
+  __shared__ __attribute__((aligned(16))) bf16 lds[kCXR * kCS + 2 * BN * 64];
+  bf16* hs = lds;
+  bf16* wsb = lds + kCXR * kCS;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int logical = xcd_remap(blockIdx.x, p.ntiles * p.nco);
+  const int tile = logical / p.nco, cob = logical % p.nco;
+  const int co0 = cob * BN;
+  const int ncb = p.Cin / 64;
+  const int S = 9 * ncb;
+
+  // ---- staging map
+  const int ch = tid & 7, r8 = tid >> 3;
+  const int gr0 = tile * p.rows_per_tile, oh0 = gr0 % p.H;
+  const bf16* hsrc[kCXP];
+  bool hval[kCXP];
+#pragma unroll
+  for (int i = 0; i < kCXP; ++i) {
+    const int j = r8 + 32 * i;
+    const int per = p.HR2 * p.HW2;
+    const int slot = j / per, rem = j - slot * per;
+    const int hr = rem / p.HW2, hc = rem - hr * p.HW2;
+    const int ih = oh0 + hr - 1, iw = hc - 1;
+    hval[i] = j < p.hrows && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+    hsrc[i] = p.src + ((long long)(gr0 + slot * p.R + hr - 1) * p.W + iw) * p.Cin + ch * 8;
+  }
+  const bf16* wsrc = p.w + (long long)(co0 + r8) * p.Kpad + ch * 8;
+
+  u32x4_t rh[kCXP], rw[WP];
+  auto load_halo = [&](int cb) {
+#pragma unroll
+    for (int i = 0; i < kCXP; ++i) rh[i] = cload16(hval[i] ? (const void*)(hsrc[i] + cb * 64) : (const void*)&kZeroC3);
+  };
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int i = 0; i < kCXP; ++i)
+      if (r8 + 32 * i < p.hrows) *reinterpret_cast<u32x4_t*>(hs + (r8 + 32 * i) * kCS + ch * 8) = rh[i];
+  };
+  auto load_w = [&](int s) {
+    const int cb = s / 9, tap = s - cb * 9;
+    const int col = (FLIP ? 8 - tap : tap) * p.Cin + cb * 64;
+#pragma unroll
+    for (int i = 0; i < WP; ++i) rw[i] = cload16(wsrc + (long long)(32 * i) * p.Kpad + col);
+  };
+  auto store_w = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < WP; ++i) *reinterpret_cast<u32x4_t*>(wsb + buf * BN * 64 + wswz(r8 + 32 * i, ch)) = rw[i];
+  };
+
+  // ---- fragment map (16x16x32: lane l holds row / column l & 15, k chunk l >> 4 (+4 for the high half))
+  const int fl = lane & 15, fc = lane >> 4;
+  int hoff[4];  // halo row (x kCS) of this lane's pixel in each of the wave's 4 pixel tiles
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int s = wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
+    const int rw_ = p.R * p.W;
+    const int slot = s / rw_, rr = (s - slot * rw_) / p.W, cc = s % p.W;
+    hoff[t] = ((slot * p.HR2 + rr) * p.HW2 + cc) * kCS + fc * 8;
+  }
+  int woff[TN][2];
+#pragma unroll
+  for (int u = 0; u < TN; ++u)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) woff[u][h] = wswz(wn * (BN / 2) + 16 * u + fl, fc + 4 * h);
+
+  f32x4 acc[TN][4];
+#pragma unroll
+  for (int u = 0; u < TN; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_halo(0);
+  load_w(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  store_halo();
+  store_w(0);
+  if (S > 1) load_w(1);
+  if (ncb > 1) load_halo(1);
+  __syncthreads();
+  for (int s = 0; s < S; ++s) {
+    const int cb = s / 9, tap = s - cb * 9;
+    const int kh = tap / 3, kw = tap - kh * 3;
+    const int toff = (kh * p.HW2 + kw) * kCS;
+    const bf16* wb = wsb + (s & 1) * BN * 64;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 fa[TN], fb[4];
+#pragma unroll
+      for (int u = 0; u < TN; ++u) fa[u] = *reinterpret_cast<const bf16x8*>(wb + woff[u][h]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) fb[t] = *reinterpret_cast<const bf16x8*>(hs + hoff[t] + toff + 32 * h);
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[u][t] = mfma16x16x32(fa[u], fb[t], acc[u][t]);
+    }
+    if (s + 1 < S) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      store_w((s + 1) & 1);
+      if (tap == 8) {  // next channel block: every wave is done with this halo
+        __syncthreads();
+        store_halo();
+      }
+    }
+    __syncthreads();
+    if (s + 2 < S) load_w(s + 2);
+    if (tap == 8 && cb + 2 < ncb) load_halo(cb + 2);
+  }
+
+  // C/D layout: row (output channel) 4 * (lane >> 4) + r, column (pixel) lane & 15
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int s = wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
+    const long long m = (long long)tile * kCP + s;
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+      const int co = co0 + wn * (BN / 2) + 16 * u + 4 * fc;
+      const long long o = m * p.ldc + co;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[u][t][r] * p.alpha;
+      if (p.res) {
+        const bf16x4_t rv = *reinterpret_cast<const bf16x4_t*>(p.res + o);
+        bf16x4_t rm;
+        if (p.resmask) rm = *reinterpret_cast<const bf16x4_t*>(p.resmask + o);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (!p.resmask || (float)rm[r] > 0.f) v[r] += (float)rv[r];
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (p.mask) {
+        const bf16x4_t mk = *reinterpret_cast<const bf16x4_t*>(p.mask + o);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (!((float)mk[r] > 0.f)) v[r] = 0.f;
+      }
+      bf16x4_t ov;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ov[r] = f2bf(v[r]);
+      *reinterpret_cast<bf16x4_t*>(p.out + o) = ov;
+    }
+  }
+}
+
+bool c3_geom(int H, int W, int& R, int& TI) {
+  if (W < 4 || W > 64 || kCP % W != 0) return false;
+  const int rpt = kCP / W;
+  if (rpt <= H) {
+    if (H % rpt != 0) return false;
+    R = rpt, TI = 1;
+  } else {
+    if (rpt % H != 0) return false;
+    R = H, TI = rpt / H;
+  }
+  return TI * (R + 2) * (W + 2) <= kCXR;
+}
+
+}  // namespace
+
+bool conv3_halo_supported(const IGemmArgs& a, int mode) {
+  static const int on = diag_int("conv_halo", 1);
+  int R, TI;
+  if (!on || (mode != MODE_FWD && mode != MODE_DGRAD)) return false;
+  return a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.SH == a.OH && a.SW == a.OW && a.SC % 64 == 0 &&
+         a.N % 64 == 0 && a.K == 9 * a.SC && a.Kpad >= a.K && a.Kpad % 8 == 0 && a.ldc % 4 == 0 && !a.bias &&
+         !a.out_f32 && !a.drop.on && !a.pool_code && !a.bn.part &&
+         a.M % kCP == 0 && a.M % (a.OH * a.OW) == 0 && c3_geom(a.OH, a.OW, R, TI) &&
+         ((uintptr_t)a.src & 15) == 0 && ((uintptr_t)a.w & 15) == 0 && ((uintptr_t)a.out & 7) == 0 &&
+         (((uintptr_t)a.res | (uintptr_t)a.resmask | (uintptr_t)a.mask) & 7) == 0;
+}
+
+hipError_t conv3_halo(const IGemmArgs& a, int mode, hipStream_t st) {
+  C3P p;
+  int R = 0, TI = 0;
+  c3_geom(a.OH, a.OW, R, TI);
+  p.src = a.src, p.w = a.w, p.res = a.res, p.resmask = a.resmask, p.mask = a.mask;
+  p.out = reinterpret_cast<bf16*>(a.out);
+  p.H = a.OH, p.W = a.OW, p.Cin = a.SC, p.Cout = a.N, p.Kpad = a.Kpad, p.ldc = a.ldc;
+  p.R = R, p.HW2 = a.OW + 2, p.HR2 = R + 2, p.hrows = TI * (R + 2) * (a.OW + 2), p.rows_per_tile = kCP / a.OW;
+  p.ntiles = a.M / kCP;
+  p.relu = a.relu;
+  p.alpha = a.alpha;
+  // 128-channel tiles while that still gives >= 2 workgroups per CU
+  const bool wide = a.N % 128 == 0 && (long long)p.ntiles * (a.N / 128) >= 512;
+  const bool flip = mode == MODE_DGRAD;
+  if (wide) {
+    p.nco = a.N / 128;
+    if (flip) hipLaunchKernelGGL((conv3_halo_kernel<128, true>), dim3(p.ntiles * p.nco), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((conv3_halo_kernel<128, false>), dim3(p.ntiles * p.nco), dim3(256), 0, st, p);
+  } else {
+    p.nco = a.N / 64;
+    if (flip) hipLaunchKernelGGL((conv3_halo_kernel<64, true>), dim3(p.ntiles * p.nco), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((conv3_halo_kernel<64, false>), dim3(p.ntiles * p.nco), dim3(256), 0, st, p);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace dfa

@@ -536,6 +536,7 @@ hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0) return hipSuccess;
   if (a.drop.on && (a.out_f32 || a.ldc != a.N)) return hipErrorInvalidValue;
   if (a.pool_code) return igemm64_pool_supported(a) && mode == MODE_FWD ? igemm64(a, mode, st) : hipErrorInvalidValue;
+  if (conv3_halo_supported(a, mode)) return conv3_halo(a, mode, st);
   if (igemm64_supported(a, mode)) return igemm64(a, mode, st);  // dropout in its epilogues
   if (!a.drop.on) return igemm_fwd_nodrop(a, mode, st);
   IGemmArgs b = a;
@@ -600,6 +601,7 @@ hipError_t igemm_wgrad(const WgradArgs& a, int mode, float* workspace, size_t ws
     const bool xvec = ((uintptr_t)a.src & 15) == 0 && a.lda % 8 == 0;
     return launch_wgrad_x<MODE_DIRECT>(a, dvec, xvec, workspace, ws_floats, st);
   }
+  if (wgrad_halo_supported(a, mode)) return wgrad_halo(a, workspace, ws_floats, st);
   if (wgrad_tr_supported(a, mode)) return wgrad_tr(a, workspace, ws_floats, st);
   if (smallc_wgrad_supported(a, mode)) return smallc_wgrad(a, workspace, ws_floats, st);
   const bool xvec = ((uintptr_t)a.src & 15) == 0 && a.SC % 8 == 0;

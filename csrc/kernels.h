@@ -124,6 +124,12 @@ hipError_t igemm_wgrad(const WgradArgs& a, int mode, float* workspace, size_t ws
 // conv weight gradient with transposed LDS reads (csrc/wgrad_tr.hip): conv, C % 8 == 0, no bias
 bool wgrad_tr_supported(const WgradArgs& a, int mode);
 hipError_t wgrad_tr(const WgradArgs& a, float* workspace, size_t ws_floats, hipStream_t st);
+// 3x3 stride-1 pad-1 conv weight gradient, halo-tiled LDS staging (csrc/wgrad_halo.hip): C, N % 64 == 0
+bool wgrad_halo_supported(const WgradArgs& a, int mode);
+// 3x3 stride-1 pad-1 conv forward / data gradient, halo-tiled LDS staging (csrc/conv3_halo.hip)
+bool conv3_halo_supported(const IGemmArgs& a, int mode);
+hipError_t conv3_halo(const IGemmArgs& a, int mode, hipStream_t st);
+hipError_t wgrad_halo(const WgradArgs& a, float* workspace, size_t ws_floats, hipStream_t st);
 hipError_t maxpool_fwd(const bf16* x, bf16* y, int B, int H, int W, int C, int P, hipStream_t st,
                        DropSpec drop = DropSpec{});
 hipError_t maxpool_bwd(const bf16* x, const bf16* dy, bf16* dx, int B, int H, int W, int C, int P, int relu_fused,

@@ -13,7 +13,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-ASM_LOAD_FILES = ["igemm64.hip", "wgrad_tr.hip"]
+ASM_LOAD_FILES = ["igemm64.hip", "wgrad_tr.hip", "wgrad_halo.hip", "conv3_halo.hip"]
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC) or shutil.which("true") is None, reason="hipcc not available")

@@ -212,6 +212,28 @@ def test_conv_wgrad_transposed_reads(B, H, W, C, N, k, s, p):
     _close(gw, 0.5 * ew, 1e-3, 1e-3)
 
 
+WGRAD_HALO = [  # B, H, W, C, N, ws floats: 3x3 stride-1 shapes on the halo-tiled kernel (csrc/wgrad_halo.hip)
+    (8, 32, 32, 64, 64, 1 << 24),     # ResNet layer 1: 2 rows x 32 per tile
+    (4, 16, 16, 128, 128, 1 << 24),   # layer 2: 4 rows x 16
+    (2, 8, 8, 256, 256, 1 << 24),     # layer 3: one whole image per tile
+    (16, 4, 4, 512, 512, 1 << 24),    # layer 4: four images per tile
+    (8, 8, 8, 64, 192, 1 << 24),      # three co blocks
+    (4, 32, 32, 128, 64, 1 << 24),    # C != N
+    (4, 16, 16, 64, 64, 1),           # no slab room: one split writes the gradient directly
+]
+
+
+@pytest.mark.parametrize("B,H,W,C,N,wsf", WGRAD_HALO)
+def test_conv_wgrad_halo(B, H, W, C, N, wsf):
+    dy = torch.randn(B, H, W, N, device=dev).to(torch.bfloat16)
+    x = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    gw = torch.full((N, 9 * C), float("nan"), device=dev)
+    ws = torch.empty(wsf, device=dev)
+    ops.conv_wgrad(dy, x, gw, None, ws, 3, 3, 1, 1, scale=0.5)
+    ew, _ = ref.conv_wgrad(dy.float(), x.float(), 3, 3, 1, 1, with_bias=False)
+    _close(gw, 0.5 * ew, 1e-3, 1e-3)
+
+
 @pytest.mark.parametrize("B,H,W,C,N,k,s,p", [(64, 26, 26, 32, 32, 3, 1, 0), (8, 16, 16, 64, 128, 3, 2, 1),
                                               (3, 9, 7, 16, 24, 3, 2, 1)])
 def test_conv_wgrad_transposed_reads_with_bias(B, H, W, C, N, k, s, p):
@@ -376,6 +398,45 @@ def test_conv_dgrad_residual_epilogue(s):
     ops.conv_dgrad(dy, None, _pad_wt(w, N, k * k, C), out, k, k, s, 1, mask=mask, residual=res, residual_mask=rmask)
     exp = ref.conv_dgrad(dy.float(), w.to(torch.bfloat16).float(), (B, H, W, C), k, k, s, 1, None)
     exp = (exp + res.float() * (rmask.float() > 0)) * (mask.float() > 0)
+    _close(out, exp)
+
+
+CONV_HALO = [  # B, H, W, C, N: 3x3 stride-1 shapes on the halo-tiled kernel (csrc/conv3_halo.hip)
+    (4, 32, 32, 64, 64),      # ResNet layer 1: 4 rows x 32 per 128-pixel tile
+    (4, 16, 16, 128, 128),    # layer 2: 8 rows x 16, two input channel blocks
+    (4, 8, 8, 256, 256),      # layer 3: two images per tile
+    (16, 4, 4, 512, 512),     # layer 4: eight images per tile, 288 halo rows
+    (8, 16, 16, 64, 128),     # C != N
+    (4, 16, 16, 128, 64),
+    (256, 16, 16, 128, 128),  # >= 512 tiles of 128 channels: the 128-wide variant
+]
+
+
+@pytest.mark.parametrize("B,H,W,C,N", CONV_HALO)
+@pytest.mark.parametrize("relu", [False, True])
+def test_conv_halo_fwd(B, H, W, C, N, relu):
+    x = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    w = torch.randn(N, 9 * C, device=dev) / (9 * C) ** 0.5
+    out = torch.full((B, H, W, N), float("nan"), device=dev, dtype=torch.bfloat16)
+    ops.conv_fwd(x, _pad_w(w), None, out, 3, 3, 1, 1, relu)
+    _close(out, ref.conv_fwd(x.float(), w.to(torch.bfloat16).float(), None, 3, 3, 1, 1, relu))
+
+
+@pytest.mark.parametrize("B,H,W,C,N", CONV_HALO)
+@pytest.mark.parametrize("join", [False, True])
+def test_conv_halo_dgrad(B, H, W, C, N, join):
+    """Flipped-tap data gradient; ``join``: the ResNet block join dx = (conv^T dy + res * [resmask > 0]) *
+    [mask > 0] in the epilogue."""
+    dy = torch.randn(B, H, W, N, device=dev).to(torch.bfloat16)
+    w = torch.randn(N, 9 * C, device=dev) / (9 * N) ** 0.5
+    res = rmask = mask = None
+    if join:
+        res, rmask, mask = (torch.randn(B, H, W, C, device=dev).to(torch.bfloat16) for _ in range(3))
+    out = torch.full((B, H, W, C), float("nan"), device=dev, dtype=torch.bfloat16)
+    ops.conv_dgrad(dy, None, _pad_wt(w, N, 9, C), out, 3, 3, 1, 1, mask=mask, residual=res, residual_mask=rmask)
+    exp = ref.conv_dgrad(dy.float(), w.to(torch.bfloat16).float(), (B, H, W, C), 3, 3, 1, 1, None)
+    if join:
+        exp = (exp + res.float() * (rmask.float() > 0)) * (mask.float() > 0)
     _close(out, exp)
 
 
