@@ -11,7 +11,7 @@
 //     channels; per 64-channel input block it stages the input halo TI x (R+2) x (W+2) once (zero
 //     padding materialised) and runs all nine taps against it as shifted row reads
 //   * the weights of one (channel block, tap) step are staged per step (double buffer, XOR-swizzled
-//     128-byte rows as in igemm64); they are the MFMA A operand, so each lane ends with 4 consecutive
+//     128-byte rows as in igemm64), loaded into registers one step ahead; they are the MFMA A operand, so each lane ends with 4 consecutive
 //     output channels of one pixel (8-byte stores, 8-byte residual / mask loads in the epilogue)
 //   * halo rows are 72 bf16 (36 dwords) apart and MFMA column j of pixel tile t is pixel 2j + (t & 1)
 //     (+32 for t >= 2): the 16 rows a ds_read_b128 lane group reads, at two consecutive 16-byte chunks,
@@ -56,6 +56,8 @@ struct C3P {
   int H, W, Cin, Cout, Kpad, ldc;
   int R, HW2, HR2, hrows, rows_per_tile;
   int ntiles, nco;
+  int ks, cbs;       // split over input channel blocks: ks splits of cbs blocks (ks > 1: raw fp32 partials)
+  float* ws;         // [ks][M][Cout] partials, summed + epilogue by igemm64_splitk_combine
   int relu;
   float alpha;
 };
@@ -72,12 +74,15 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int logical = xcd_remap(blockIdx.x, p.ntiles * p.nco);
-  const int tile = logical / p.nco, cob = logical % p.nco;
+  const int logical = xcd_remap(blockIdx.x, p.ntiles * p.nco * p.ks);
+  const int ksp = logical / (p.ntiles * p.nco), lt = logical - ksp * (p.ntiles * p.nco);
+  const int tile = lt / p.nco, cob = lt % p.nco;
   const int co0 = cob * BN;
-  const int ncb = p.Cin / 64;
+  const int cbb = ksp * p.cbs;                               // this split's first input channel block
+  const int ncb = max(0, min(p.Cin / 64 - cbb, p.cbs));      // blocks of this split
   const int S = 9 * ncb;
 
+  const FDiv fper(p.HR2 * p.HW2), fhw2(p.HW2), frw(p.R * p.W), fw(p.W);
   // ---- staging map
   const int ch = tid & 7, r8 = tid >> 3;
   const int gr0 = tile * p.rows_per_tile, oh0 = gr0 % p.H;
@@ -86,9 +91,8 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
 #pragma unroll
   for (int i = 0; i < kCXP; ++i) {
     const int j = r8 + 32 * i;
-    const int per = p.HR2 * p.HW2;
-    const int slot = j / per, rem = j - slot * per;
-    const int hr = rem / p.HW2, hc = rem - hr * p.HW2;
+    const int slot = fper.div(j), rem = j - slot * fper.d;  // (float-reciprocal division: 3 VALU)
+    const int hr = fhw2.div(rem), hc = rem - hr * p.HW2;
     const int ih = oh0 + hr - 1, iw = hc - 1;
     hval[i] = j < p.hrows && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
     hsrc[i] = p.src + ((long long)(gr0 + slot * p.R + hr - 1) * p.W + iw) * p.Cin + ch * 8;
@@ -98,7 +102,8 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
   u32x4_t rh[kCXP], rw[WP];
   auto load_halo = [&](int cb) {
 #pragma unroll
-    for (int i = 0; i < kCXP; ++i) rh[i] = cload16(hval[i] ? (const void*)(hsrc[i] + cb * 64) : (const void*)&kZeroC3);
+    for (int i = 0; i < kCXP; ++i)
+      rh[i] = cload16(hval[i] ? (const void*)(hsrc[i] + (cbb + cb) * 64) : (const void*)&kZeroC3);
   };
   auto store_halo = [&]() {
 #pragma unroll
@@ -107,7 +112,7 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
   };
   auto load_w = [&](int s) {
     const int cb = s / 9, tap = s - cb * 9;
-    const int col = (FLIP ? 8 - tap : tap) * p.Cin + cb * 64;
+    const int col = (FLIP ? 8 - tap : tap) * p.Cin + (cbb + cb) * 64;
 #pragma unroll
     for (int i = 0; i < WP; ++i) rw[i] = cload16(wsrc + (long long)(32 * i) * p.Kpad + col);
   };
@@ -122,8 +127,7 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int s = wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
-    const int rw_ = p.R * p.W;
-    const int slot = s / rw_, rr = (s - slot * rw_) / p.W, cc = s % p.W;
+    const int slot = frw.div(s), q = s - slot * frw.d, rr = fw.div(q), cc = q - rr * p.W;
     hoff[t] = ((slot * p.HR2 + rr) * p.HW2 + cc) * kCS + fc * 8;
   }
   int woff[TN][2];
@@ -138,6 +142,8 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // (a two-step register ring for the weights with counted vmcnt waits measured slower on every layer:
+  // the loads are not what a step waits for)
   load_halo(0);
   load_w(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -184,6 +190,10 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
 #pragma unroll
     for (int u = 0; u < TN; ++u) {
       const int co = co0 + wn * (BN / 2) + 16 * u + 4 * fc;
+      if (p.ks > 1) {  // raw partial of this split's channel blocks
+        *reinterpret_cast<f32x4*>(p.ws + ((long long)ksp * p.ntiles * kCP + m) * p.Cout + co) = acc[u][t];
+        continue;
+      }
       const long long o = m * p.ldc + co;
       float v[4];
 #pragma unroll
@@ -255,14 +265,34 @@ hipError_t conv3_halo(const IGemmArgs& a, int mode, hipStream_t st) {
   // 128-channel tiles while that still gives >= 2 workgroups per CU
   const bool wide = a.N % 128 == 0 && (long long)p.ntiles * (a.N / 128) >= 512;
   const bool flip = mode == MODE_DGRAD;
+  p.nco = a.N / (wide ? 128 : 64);
+  // under-filled launches (ResNet layer 4: 256 workgroups of 72 steps) split the input channel blocks
+  // over workgroups when the caller provides igemm64's split-K workspace; a fixed-order combine applies
+  // the epilogue
+  const int ncb = a.SC / 64;
+  p.ks = 1, p.cbs = ncb, p.ws = nullptr;
+  static const int ksplit = diag_int("conv_halo_splitk", 1);
+  if (ksplit && a.splitk_ws && p.ntiles * p.nco < 512) {
+    const long long wsf = igemm64_splitk_floats(a, mode);  // what the caller allocated
+    int ks = 1;
+    while (ks < 4 && ncb % (2 * ks) == 0 && (long long)p.ntiles * p.nco * ks * 2 <= 1024 &&
+           (long long)(2 * ks) * a.M * a.N <= wsf)
+      ks *= 2;
+    if (ks > 1) p.ks = ks, p.cbs = ncb / ks, p.ws = a.splitk_ws;
+  }
+  const dim3 grid(p.ntiles * p.nco * p.ks);
   if (wide) {
-    p.nco = a.N / 128;
-    if (flip) hipLaunchKernelGGL((conv3_halo_kernel<128, true>), dim3(p.ntiles * p.nco), dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((conv3_halo_kernel<128, false>), dim3(p.ntiles * p.nco), dim3(256), 0, st, p);
+    if (flip) hipLaunchKernelGGL((conv3_halo_kernel<128, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((conv3_halo_kernel<128, false>), grid, dim3(256), 0, st, p);
   } else {
-    p.nco = a.N / 64;
-    if (flip) hipLaunchKernelGGL((conv3_halo_kernel<64, true>), dim3(p.ntiles * p.nco), dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((conv3_halo_kernel<64, false>), dim3(p.ntiles * p.nco), dim3(256), 0, st, p);
+    if (flip) hipLaunchKernelGGL((conv3_halo_kernel<64, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((conv3_halo_kernel<64, false>), grid, dim3(256), 0, st, p);
+  }
+  DFA_HIP_CHECK(hipGetLastError());
+  if (p.ks > 1) {
+    IGemmArgs c = a;
+    c.splits = p.ks;
+    return igemm64_splitk_combine(c, st);
   }
   return hipGetLastError();
 }

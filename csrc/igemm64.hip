@@ -756,6 +756,13 @@ hipError_t launch64_mode(const IGemmArgs& a, hipStream_t st) {
 
 }  // namespace
 
+hipError_t igemm64_splitk_combine(const IGemmArgs& a, hipStream_t st) {
+  const long long total4 = (long long)a.M * (a.N / 4);
+  const int grid = (int)min((total4 + 255) / 256, 4096LL);
+  hipLaunchKernelGGL(igemm64_splitk_epilogue_kernel, dim3(grid), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 long long igemm64_splitk_floats(const IGemmArgs& a, int mode) {
   static const bool off = diag_int("igemm_splitk", 1) == 0;
   if (off || !igemm64_supported(a, mode) || a.N <= 64) return 0;

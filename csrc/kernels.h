@@ -120,6 +120,8 @@ hipError_t igemm64(const IGemmArgs& a, int mode, hipStream_t st);
 // fp32 floats of split-K workspace igemm64 wants for this problem (0: no split); the caller allocates
 // them and passes the buffer in IGemmArgs::splitk_ws
 long long igemm64_splitk_floats(const IGemmArgs& a, int mode);
+// out = epilogue(sum over a.splits of a.splitk_ws[s][M][N]) in a fixed order (igemm64's split-K combine)
+hipError_t igemm64_splitk_combine(const IGemmArgs& a, hipStream_t st);
 hipError_t igemm_wgrad(const WgradArgs& a, int mode, float* workspace, size_t ws_floats, hipStream_t st);
 // conv weight gradient with transposed LDS reads (csrc/wgrad_tr.hip): conv, C % 8 == 0, no bias
 bool wgrad_tr_supported(const WgradArgs& a, int mode);

@@ -21,8 +21,12 @@
 //     accumulators (144 VGPRs); per 32-pixel step it reads the 4 dY fragments once (reused 9x) and one
 //     X fragment per tap (reused 4x): 13 fragments per 36 v_mfma_f32_16x16x32_bf16
 //   * LDS rows of 64 channels at a stride of 80 bf16 (40 dwords: 8 consecutive rows of a transposed
-//     read sit on 8 disjoint 8-bank groups), two buffers of (64 + 160) rows = 70 KB: 2 workgroups per CU;
+//     read sit on 8 disjoint 8-bank groups), two buffers of (64 + 160) rows = 70 KB per 4-wave group;
 //     the next tile's loads are in registers while the current one computes, one barrier per tile
+//   * a workgroup is two such groups (8 waves, 140 KB, one per CU) that walk alternate tiles and sum
+//     their blocks through LDS at the end: every CU holds 8 waves but writes one slab, not two — the
+//     fp32 slabs (147 KB per workgroup, written and re-read by slab_reduce) are what bounded the
+//     4-wave version at 39-45 us on ResNet layers 2-4
 //   * the pixel range is split over workgroups (channel block fastest in the XCD-aware order, so the
 //     workgroups of one XCD share the same dY / X rows in L2); splits > 1 write fp32 slabs that
 //     slab_reduce sums in a fixed order (deterministic)
@@ -69,16 +73,26 @@ struct HaloP {
   float scale;
 };
 
-__global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(HaloP p) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * kHBuf];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+// G groups of 4 waves share one output block: group gi walks tiles t0 + gi, t0 + gi + G, ... with its own
+// LDS buffers, and the groups' partial blocks are summed through LDS before the one slab store (G = 2:
+// 8 waves per CU at half the slab bytes of two 4-wave workgroups)
+template <int G>
+__global__ void __launch_bounds__(256 * G, 2 / G) wgrad_halo_kernel(HaloP p) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[G * 2 * kHBuf];
+  const int gi = threadIdx.x >> 8;
+  const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
   const int logical = xcd_remap(blockIdx.x, p.cblocks * p.splits);
   const int cb = logical % p.cblocks, split = logical / p.cblocks;
   const int n0 = (cb / p.cib_n) * 64, c0 = (cb % p.cib_n) * 64;
-  const int t0 = split * p.tps;
-  const int nt = max(0, min(p.ntiles, t0 + p.tps) - t0);
+  const int tb = split * p.tps;
+  const int ntb = max(0, min(p.ntiles, tb + p.tps) - tb);
+  const int t0 = tb + gi;                            // this group's tiles: t0, t0 + G, ...
+  const int nt = ntb > gi ? (ntb - gi + G - 1) / G : 0;
+  const int iters = (ntb + G - 1) / G;               // barrier count, the same for every group
   const int K = 9 * p.C;
+  bf16* glds = lds + gi * 2 * kHBuf;
 
+  const FDiv fper(p.HR2 * p.HW2), fhw2(p.HW2), frw(p.R * p.W), fw(p.W);
   // ---- staging map: thread = (row group r, 16-byte chunk ch) of 64-channel rows
   const int ch = tid & 7, r8 = tid >> 3;
   const bf16* dyb = p.dy + n0 + ch * 8;
@@ -87,9 +101,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(HaloP p) {
 #pragma unroll
   for (int i = 0; i < kHXP; ++i) {
     const int j = r8 + 32 * i;
-    const int per = p.HR2 * p.HW2;
-    const int slot = j / per, rem = j - slot * per;
-    const int hr = rem / p.HW2, hc = rem - hr * p.HW2;
+    const int slot = fper.div(j), rem = j - slot * fper.d;  // (float-reciprocal division: 3 VALU)
+    const int hr = fhw2.div(rem), hc = rem - hr * p.HW2;
     xro[i] = slot * p.R + hr - 1;
     xhr[i] = j < p.hrows ? hr - 1 : -(1 << 20);  // rows past the halo load nothing
     xiw[i] = hc - 1;
@@ -110,7 +123,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(HaloP p) {
     }
   };
   auto sstore = [&](int buf) {
-    bf16* ds = lds + buf * kHBuf;
+    bf16* ds = glds + buf * kHBuf;
     bf16* xs = ds + kHP * kHS;
 #pragma unroll
     for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4_t*>(ds + (r8 + 32 * i) * kHS + ch * 8) = rd[i];
@@ -127,8 +140,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(HaloP p) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int s = sub * 32 + 16 * h + 4 * g + q;  // pixel slot of the tile
-      const int rw = p.R * p.W;
-      const int slot = s / rw, rr = (s - slot * rw) / p.W, cc = s % p.W;
+      const int slot = frw.div(s), q = s - slot * frw.d, rr = fw.div(q), cc = q - rr * p.W;
       aoff[sub][h] = s * kHS + 4 * pp;
       boff[sub][h] = kHP * kHS + ((slot * p.HR2 + rr) * p.HW2 + cc) * kHS + 4 * pp + wid * 16;
     }
@@ -144,38 +156,66 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(HaloP p) {
     gload(t0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     sstore(0);
-    if (nt > 1) gload(t0 + 1);
+    if (nt > 1) gload(t0 + G);
   }
   __syncthreads();
-  for (int it = 0; it < nt; ++it) {
-    const bf16* base = lds + (it & 1) * kHBuf;
+  for (int it = 0; it < iters; ++it) {
+    if (it < nt) {
+      const bf16* base = glds + (it & 1) * kHBuf;
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      bf16x8 fa[4];
+      for (int sub = 0; sub < 2; ++sub) {
+        bf16x8 fa[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bf16x4 lo = tr_read_h(base + aoff[sub][0] + i * 16);
-        const bf16x4 hi = tr_read_h(base + aoff[sub][1] + i * 16);
-        fa[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          const int o = kh * tap_row + kw * kHS;
-          const bf16x4 lo = tr_read_h(base + boff[sub][0] + o);
-          const bf16x4 hi = tr_read_h(base + boff[sub][1] + o);
-          const bf16x8 fb = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[i][kh * 3 + kw] = mfma16x16x32(fa[i], fb, acc[i][kh * 3 + kw]);
+        for (int i = 0; i < 4; ++i) {
+          const bf16x4 lo = tr_read_h(base + aoff[sub][0] + i * 16);
+          const bf16x4 hi = tr_read_h(base + aoff[sub][1] + i * 16);
+          fa[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
         }
-    }
-    if (it + 1 < nt) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      sstore((it + 1) & 1);
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const int o = kh * tap_row + kw * kHS;
+            const bf16x4 lo = tr_read_h(base + boff[sub][0] + o);
+            const bf16x4 hi = tr_read_h(base + boff[sub][1] + o);
+            const bf16x8 fb = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i][kh * 3 + kw] = mfma16x16x32(fa[i], fb, acc[i][kh * 3 + kw]);
+          }
+      }
+      if (it + 1 < nt) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        sstore((it + 1) & 1);
+      }
     }
     __syncthreads();
-    if (it + 2 < nt) gload(t0 + it + 2);
+    if (it + 2 < nt) gload(t0 + (it + 2) * G);
+  }
+
+  if (G > 1) {  // group 1 hands its block to group 0 through LDS, half (co tiles 0-1, then 2-3) at a time
+    float* red = reinterpret_cast<float*>(lds);  // [wave][72 registers][64 lanes]
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (gi == 1) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[(wid * 72 + (i * 9 + t) * 4 + r) * 64 + lane] = acc[2 * half + i][t][r];
+      }
+      __syncthreads();
+      if (gi == 0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[2 * half + i][t][r] += red[(wid * 72 + (i * 9 + t) * 4 + r) * 64 + lane];
+      }
+      __syncthreads();
+    }
+    if (gi != 0) return;
   }
 
   // C/D layout of the 16x16 MFMA: column (ci) = lane & 15, row (co) = 4 * (lane >> 4) + r
@@ -229,8 +269,9 @@ hipError_t wgrad_halo(const WgradArgs& a, float* ws, size_t ws_floats, hipStream
   p.cib_n = a.SC / 64;
   p.cblocks = (a.N / 64) * p.cib_n;
   p.scale = a.scale;
-  // two workgroups per CU (70 KB of LDS each), bounded by the slab workspace
-  static const int target = diag_int("halo_wg", 512);
+  // one 8-wave workgroup per CU (140 KB of LDS), bounded by the slab workspace
+  static const int groups = diag_int("halo_groups", 2) == 1 ? 1 : 2;
+  static const int target = diag_int("halo_wg", groups == 2 ? 256 : 512);
   const long long per_split = (long long)a.N * a.K;
   int splits = max(1, cdiv(target, p.cblocks));
   splits = min(splits, p.ntiles);
@@ -239,7 +280,10 @@ hipError_t wgrad_halo(const WgradArgs& a, float* ws, size_t ws_floats, hipStream
   splits = cdiv(p.ntiles, p.tps);
   p.splits = splits;
   p.out = splits > 1 ? ws : a.gw;
-  hipLaunchKernelGGL(wgrad_halo_kernel, dim3(p.cblocks * splits), dim3(256), 0, st, p);
+  if (groups == 2)
+    hipLaunchKernelGGL(wgrad_halo_kernel<2>, dim3(p.cblocks * splits), dim3(512), 0, st, p);
+  else
+    hipLaunchKernelGGL(wgrad_halo_kernel<1>, dim3(p.cblocks * splits), dim3(256), 0, st, p);
   DFA_HIP_CHECK(hipGetLastError());
   if (splits > 1) DFA_HIP_CHECK(slab_reduce(ws, a.gw, nullptr, a.N, a.K, a.K, splits, a.scale, st));
   return hipSuccess;
