@@ -56,6 +56,7 @@ struct C3P {
   int H, W, Cin, Cout, Kpad, ldc;
   int R, HW2, HR2, hrows, rows_per_tile;
   int ntiles, nco;
+  int tps;           // tiles per workgroup (the persistent 64 -> 64 kernel)
   int ks, cbs;       // split over input channel blocks: ks splits of cbs blocks (ks > 1: raw fp32 partials)
   float* ws;         // [ks][M][Cout] partials, summed + epilogue by igemm64_splitk_combine
   int relu;
@@ -63,6 +64,36 @@ struct C3P {
 };
 
 __device__ __forceinline__ int wswz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3); }
+
+// epilogue of 4 consecutive output channels of one pixel (as igemm64): alpha, residual join, ReLU, relu'
+__device__ __forceinline__ void c3_store(const C3P& p, long long m, int co, const f32x4& a) {
+  const long long o = m * p.ldc + co;
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = a[r] * p.alpha;
+  if (p.res) {
+    const bf16x4_t rv = *reinterpret_cast<const bf16x4_t*>(p.res + o);
+    bf16x4_t rm;
+    if (p.resmask) rm = *reinterpret_cast<const bf16x4_t*>(p.resmask + o);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (!p.resmask || (float)rm[r] > 0.f) v[r] += (float)rv[r];
+  }
+  if (p.relu) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+  }
+  if (p.mask) {
+    const bf16x4_t mk = *reinterpret_cast<const bf16x4_t*>(p.mask + o);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (!((float)mk[r] > 0.f)) v[r] = 0.f;
+  }
+  bf16x4_t ov;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) ov[r] = f2bf(v[r]);
+  *reinterpret_cast<bf16x4_t*>(p.out + o) = ov;
+}
 
 template <int BN, bool FLIP>
 __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
@@ -194,33 +225,139 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
         *reinterpret_cast<f32x4*>(p.ws + ((long long)ksp * p.ntiles * kCP + m) * p.Cout + co) = acc[u][t];
         continue;
       }
-      const long long o = m * p.ldc + co;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[u][t][r] * p.alpha;
-      if (p.res) {
-        const bf16x4_t rv = *reinterpret_cast<const bf16x4_t*>(p.res + o);
-        bf16x4_t rm;
-        if (p.resmask) rm = *reinterpret_cast<const bf16x4_t*>(p.resmask + o);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (!p.resmask || (float)rm[r] > 0.f) v[r] += (float)rv[r];
-      }
-      if (p.relu) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-      }
-      if (p.mask) {
-        const bf16x4_t mk = *reinterpret_cast<const bf16x4_t*>(p.mask + o);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (!((float)mk[r] > 0.f)) v[r] = 0.f;
-      }
-      bf16x4_t ov;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ov[r] = f2bf(v[r]);
-      *reinterpret_cast<bf16x4_t*>(p.out + o) = ov;
+      c3_store(p, m, co, acc[u][t]);
     }
+  }
+}
+
+// 64 -> 64 channels (ResNet layer 1, forward and data gradient): the whole 9 x 64 x 64 weight block
+// (72 KB) stays in LDS for the workgroup's life, so a tap is MFMAs on LDS reads with no staging and no
+// barrier.  A persistent workgroup of two 4-wave groups walks 2 x tpw 128-pixel tiles; each group owns
+// one halo buffer and prefetches its next tile's halo into registers while it computes the current one
+// (the per-tile setup and the halo latency were most of a 9-step workgroup's life in the tiled kernel).
+constexpr int kC64XP = 7;             // halo staging passes per group (224 rows)
+constexpr int kC64XR = 32 * kC64XP;
+
+template <bool FLIP>
+__global__ void __launch_bounds__(512, 1) conv3_halo_c64_kernel(C3P p) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[9 * 64 * 64 + 2 * kC64XR * kCS];
+  bf16* wl = lds;  // [tap][co][64 ci], XOR-swizzled 128-byte rows
+  const int gi = threadIdx.x >> 8;
+  const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  bf16* hs = lds + 9 * 64 * 64 + gi * kC64XR * kCS;
+  const int tb = blockIdx.x * p.tps;                          // this workgroup's first tile
+  const int nt = max(0, min(p.ntiles, tb + p.tps) - tb);
+  const int iters = (nt + 1) / 2;                             // group gi: tiles tb + 2 it + gi
+
+  // ---- weights: 576 rows (tap, co) x 8 chunks, 9 per thread
+  {
+    u32x4_t rw[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int idx = threadIdx.x + 512 * i, row = idx >> 3, ch = idx & 7;
+      const int tap = row >> 6, co = row & 63;
+      rw[i] = cload16(p.w + (long long)co * p.Kpad + (FLIP ? 8 - tap : tap) * 64 + ch * 8);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int idx = threadIdx.x + 512 * i, row = idx >> 3, ch = idx & 7;
+      *reinterpret_cast<u32x4_t*>(wl + (row >> 6) * 4096 + wswz(row & 63, ch)) = rw[i];
+    }
+  }
+
+  // ---- halo staging map (tile independent part)
+  const FDiv fper(p.HR2 * p.HW2), fhw2(p.HW2), frw(p.R * p.W), fw(p.W);
+  const int ch = tid & 7, r8 = tid >> 3;
+  int xro[kC64XP], xhr[kC64XP], xiw[kC64XP];
+#pragma unroll
+  for (int i = 0; i < kC64XP; ++i) {
+    const int j = r8 + 32 * i;
+    const int slot = fper.div(j), rem = j - slot * fper.d;
+    const int hr = fhw2.div(rem), hc = rem - hr * p.HW2;
+    xro[i] = slot * p.R + hr - 1;
+    xhr[i] = j < p.hrows ? hr - 1 : -(1 << 20);
+    xiw[i] = hc - 1;
+  }
+  u32x4_t rh[kC64XP];
+  auto load_halo = [&](int t) {
+    const int gr0 = t * p.rows_per_tile, oh0 = gr0 % p.H;
+#pragma unroll
+    for (int i = 0; i < kC64XP; ++i) {
+      const int ih = oh0 + xhr[i];
+      const bool v = (unsigned)ih < (unsigned)p.H && (unsigned)xiw[i] < (unsigned)p.W;
+      rh[i] = cload16(v ? (const void*)(p.src + ((long long)(gr0 + xro[i]) * p.W + xiw[i]) * 64 + ch * 8)
+                        : (const void*)&kZeroC3);
+    }
+  };
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int i = 0; i < kC64XP; ++i)
+      if (r8 + 32 * i < p.hrows) *reinterpret_cast<u32x4_t*>(hs + (r8 + 32 * i) * kCS + ch * 8) = rh[i];
+  };
+
+  // ---- fragment map (as conv3_halo_kernel<64>)
+  const int fl = lane & 15, fc = lane >> 4;
+  int hoff[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int s = wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
+    const int slot = frw.div(s), q = s - slot * frw.d, rr = fw.div(q), cc = q - rr * p.W;
+    hoff[t] = ((slot * p.HR2 + rr) * p.HW2 + cc) * kCS + fc * 8;
+  }
+  int woff[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) woff[u][h] = wswz(wn * 32 + 16 * u + fl, fc + 4 * h);
+
+  if (nt > gi) load_halo(tb + gi);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (nt > gi) store_halo();
+  __syncthreads();
+  for (int it = 0; it < iters; ++it) {
+    const int t = tb + 2 * it + gi;
+    const bool cur = 2 * it + gi < nt, nxt = 2 * (it + 1) + gi < nt;
+    if (nxt) load_halo(t + 2);
+    if (cur) {
+      f32x4 acc[2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[u][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int toff = (kh * p.HW2 + kw) * kCS;
+          const bf16* wt = wl + (kh * 3 + kw) * 4096;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            bf16x8 fa[2], fb[4];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) fa[u] = *reinterpret_cast<const bf16x8*>(wt + woff[u][h]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) fb[q] = *reinterpret_cast<const bf16x8*>(hs + hoff[q] + toff + 32 * h);
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) acc[u][q] = mfma16x16x32(fa[u], fb[q], acc[u][q]);
+          }
+        }
+      __syncthreads();  // this group's waves are done with the halo
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (nxt) store_halo();
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const long long m = (long long)t * kCP + wm * 64 + 32 * (q >> 1) + 2 * fl + (q & 1);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) c3_store(p, m, wn * 32 + 16 * u + 4 * fc, acc[u][q]);
+      }
+    } else {
+      __syncthreads();
+    }
+    __syncthreads();
   }
 }
 
@@ -262,6 +399,16 @@ hipError_t conv3_halo(const IGemmArgs& a, int mode, hipStream_t st) {
   p.ntiles = a.M / kCP;
   p.relu = a.relu;
   p.alpha = a.alpha;
+  static const int c64 = diag_int("conv_halo_c64", 1);
+  if (c64 && a.SC == 64 && a.N == 64 && p.hrows <= kC64XR && p.ntiles >= 512) {
+    // weights resident: one 8-wave workgroup per CU, tiles split evenly (an even count per workgroup)
+    p.tps = 2 * cdiv(p.ntiles, 2 * 256);
+    p.nco = 1, p.ks = 1, p.cbs = 1, p.ws = nullptr;
+    const dim3 grid(cdiv(p.ntiles, p.tps));
+    if (mode == MODE_DGRAD) hipLaunchKernelGGL(conv3_halo_c64_kernel<true>, grid, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL(conv3_halo_c64_kernel<false>, grid, dim3(512), 0, st, p);
+    return hipGetLastError();
+  }
   // 128-channel tiles while that still gives >= 2 workgroups per CU
   const bool wide = a.N % 128 == 0 && (long long)p.ntiles * (a.N / 128) >= 512;
   const bool flip = mode == MODE_DGRAD;

@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 cd "$R"
 export DISTRIFLOW_SKIP_BUILD=1
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "halo or splitk or wgrad" \
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "halo or splitk or wgrad or conv" \
   > gpurun_out/t_q.log 2>&1 || { grep -E "FAILED|Error|assert" gpurun_out/t_q.log | head -n 30; tail -n 30 gpurun_out/t_q.log; exit 1; }
 tail -n 1 gpurun_out/t_q.log
 timeout -k 10 200 python scripts/convbench.py > gpurun_out/cb_q.txt 2>&1 || { tail -n 20 gpurun_out/cb_q.txt; exit 1; }

@@ -409,6 +409,8 @@ CONV_HALO = [  # B, H, W, C, N: 3x3 stride-1 shapes on the halo-tiled kernel (cs
     (8, 16, 16, 64, 128),     # C != N
     (4, 16, 16, 128, 64),
     (256, 16, 16, 128, 128),  # >= 512 tiles of 128 channels: the 128-wide variant
+    (64, 32, 32, 64, 64),     # >= 512 tiles of 64 -> 64: the weights-resident persistent kernel
+    (260, 16, 16, 64, 64),    # same, 16x16 images, a partial last workgroup
 ]
 
 
