@@ -24,6 +24,7 @@
 // stale cache line, and writes from a remote GPU land directly in HBM.
 #include "common.h"
 #include "kernels.h"
+#include "ll_exchange.h"
 
 namespace dfa {
 namespace {
@@ -114,7 +115,29 @@ __global__ __launch_bounds__(kThreads) void p2p_allreduce_kernel(P2PArgs a) {
   if (t == 0) a.epochs[b] = e;
 }
 
+// Startup self-test of the in-kernel LL exchange (csrc/ll_exchange.h) that the fused LeNet-5 reduce
+// launch folds into its epilogue: one slot per workgroup, one granule per thread, the same push /
+// poll / rank-order sum.  Every rank runs the same calls on the same slots, so the per-slot epochs stay
+// in step for the kernels that use the slots afterwards.
+__global__ void __launch_bounds__(kLLSlot) ll_selftest_kernel(LLComm c, const float* in, float* out) {
+  __shared__ unsigned s_e;
+  const int slot = blockIdx.x;
+  const unsigned e = ll_epoch(c, slot, &s_e);
+  const long long i = (long long)slot * kLLSlot + threadIdx.x;
+  float o = 0.f;
+  ll_allreduce(c, slot, threadIdx.x, e, in[i], o);
+  out[i] = o;
+  __syncthreads();
+  ll_commit(c, slot, e);
+}
+
 }  // namespace
+
+hipError_t ll_selftest(const LLComm& c, const float* in, float* out, int nslots, hipStream_t st) {
+  if (nslots <= 0 || nslots > c.nslots) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ll_selftest_kernel, dim3(nslots), dim3(kLLSlot), 0, st, c, in, out);
+  return hipGetLastError();
+}
 
 hipError_t p2p_allreduce(const P2PArgs& a, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;

@@ -1457,6 +1457,16 @@ class P2PComm {
     return v;
   }
   int64_t host_error() const { return herr_.read(); }  // no HIP call: safe from a watchdog thread
+  // LL exchange self-test over the first in.numel() / kLLSlot slots (every rank the same call)
+  void ll_selftest(torch::Tensor in, torch::Tensor out) {
+    need(in, at::kFloat, "ll in");
+    need(out, at::kFloat, "ll out");
+    TORCH_CHECK(in.numel() == out.numel() && in.numel() % dfa::kLLSlot == 0, "ll: whole slots of kLLSlot floats");
+    TORCH_CHECK(in.get_device() == dev_ && out.get_device() == dev_, "ll: tensors on the wrong device");
+    const int ns = (int)(in.numel() / dfa::kLLSlot);
+    TORCH_CHECK(ns >= 1 && ns <= ll_slots_, "ll: more slots than the communicator holds");
+    check_hip(dfa::ll_selftest(ll_args(), in.data_ptr<float>(), out.data_ptr<float>(), ns, cur_stream()), "ll_selftest");
+  }
   int64_t max_floats() const { return half_; }
   int64_t ll_slots() const { return ll_slots_; }
   void set_timeout(double timeout_s) { timeout_ticks_ = (int64_t)(timeout_s * 1e8); }
@@ -1854,6 +1864,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("allreduce", &P2PComm::allreduce, py::arg("t"), py::arg("scale") = 1.0)
       .def("error", &P2PComm::error)
       .def("host_error", &P2PComm::host_error)
+      .def("ll_selftest", &P2PComm::ll_selftest, py::arg("inp"), py::arg("out"))
       .def("set_timeout", &P2PComm::set_timeout)
       .def_property_readonly("max_floats", &P2PComm::max_floats)
       .def_property_readonly("ll_slots", &P2PComm::ll_slots);

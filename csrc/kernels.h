@@ -302,6 +302,9 @@ struct LLComm {
   long long timeout_ticks;
   int rank, world, nslots;
 };
+// LL exchange self-test (csrc/allreduce_p2p.hip): out[slot][pos] = sum over ranks of in[slot][pos]
+hipError_t ll_selftest(const LLComm& c, const float* in, float* out, int nslots, hipStream_t st);
+
 
 
 // Device-resident async parameter server (csrc/async_ps.hip).  seq / batch_ctr / ps_w live in the

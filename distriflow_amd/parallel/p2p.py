@@ -79,7 +79,7 @@ class P2PAllReduce:
         if self_test:
             # a broken peer path shows up as a flag timeout: fail the self-test within seconds, not minutes
             comm.set_timeout(min(timeout_s, 5.0))
-            passed = self._self_test()
+            passed = self._self_test() and self._ll_self_test()
             comm.set_timeout(timeout_s)
             if not passed:
                 self.comm = None
@@ -115,6 +115,37 @@ class P2PAllReduce:
         """Raise if any launch saw a peer-flag timeout (the sticky device error word)."""
         if self.comm is not None and self.comm.error() != 0:
             raise RuntimeError("p2p all-reduce: a peer flag timed out (peer dead or stalled)")
+
+    def _ll_self_test(self) -> bool:
+        """The in-kernel LL exchange (csrc/ll_exchange.h) that the fused LeNet-5 reduce launch folds into
+        its epilogue, on its first slots, both parities.  A failure (mismatch or peer timeout: the error word
+        is shared with the all-reduce) disables the whole communicator, so the trainer falls back to RCCL."""
+        ok = True
+        try:
+            ns = min(4, int(self.comm.ll_slots))
+            if ns <= 0:
+                return True
+            n = ns * 1024  # kLLSlot granules per slot
+            g = torch.Generator(device="cpu")
+            for it in range(3):
+                g.manual_seed(4321 + it)
+                base = torch.randn(self.world, n, generator=g)
+                out = torch.empty(n, device=self.device)
+                self.comm.ll_selftest(base[self.rank].to(self.device), out)
+                torch.cuda.synchronize(self.device)
+                if self.comm.error() != 0:
+                    self.reason, ok = "peer timeout in the LL exchange self-test", False
+                    break
+                # rank-order fp32 sums: every rank must hold the same bits
+                ref = base[0].clone()
+                for r in range(1, self.world):
+                    ref += base[r]
+                if not torch.equal(out.cpu(), ref):
+                    self.reason, ok = "LL exchange self-test mismatch", False
+                    break
+        except Exception as e:
+            self.reason, ok = f"LL self-test: {e!r}", False
+        return _agree(ok, self.group, self.device)
 
     def _self_test(self) -> bool:
         ok = True
