@@ -16,7 +16,8 @@
 //   * halo rows are 72 bf16 (36 dwords) apart and MFMA column j of pixel tile t is pixel 2j + (t & 1)
 //     (+32 for t >= 2): the 16 rows a ds_read_b128 lane group reads, at two consecutive 16-byte chunks,
 //     land on 16 distinct 4-bank slots for any tap shift (slot = 9 row + chunk mod 16; the two chunks
-//     differ in parity)
+//     differ in parity); with W = 16 the image rows of the halo are W + 16 LDS rows apart so that the
+//     row crossing inside a lane group keeps that property
 //   * the halo is single-buffered: the next block's halo sits in registers from the first tap of the
 //     current block and is stored after its ninth (one extra barrier per 9 steps); LDS = halo +
 //     2 weight buffers <= 74 KB, so two workgroups share a CU
@@ -44,7 +45,8 @@ __device__ __forceinline__ u32x4_t cload16(const void* p) {
 constexpr int kCP = 128;              // output pixels per workgroup
 constexpr int kCS = 72;               // halo row stride (bf16)
 constexpr int kCXP = 9;               // halo staging passes of 32 rows
-constexpr int kCXR = 32 * kCXP;       // halo rows (>= TI * (R+2) * (W+2))
+constexpr int kCXR = 32 * kCXP;       // staged halo pixels (>= TI * (R+2) * (W+2))
+constexpr int kCXL = 320;             // LDS halo rows (>= TI * (R+2) * HWP)
 
 struct C3P {
   const bf16* src;   // NHWC [.][H][W][Cin]
@@ -55,6 +57,7 @@ struct C3P {
   bf16* out;         // [M][ldc]
   int H, W, Cin, Cout, Kpad, ldc;
   int R, HW2, HR2, hrows, rows_per_tile;
+  int HWP;           // LDS pitch of one halo image row, in rows (tiled kernel): W + 2, or W + 16 for W = 16
   int ntiles, nco;
   int tps;           // tiles per workgroup (the persistent 64 -> 64 kernel)
   int ks, cbs;       // split over input channel blocks: ks splits of cbs blocks (ks > 1: raw fp32 partials)
@@ -99,9 +102,9 @@ template <int BN, bool FLIP>
 __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
   constexpr int TN = BN / 32;          // 16-channel tiles per wave
   constexpr int WP = BN * 8 / 256;     // weight staging passes (32 rows each)
-  __shared__ __attribute__((aligned(16))) bf16 lds[kCXR * kCS + 2 * BN * 64];
+  __shared__ __attribute__((aligned(16))) bf16 lds[kCXL * kCS + 2 * BN * 64];
   bf16* hs = lds;
-  bf16* wsb = lds + kCXR * kCS;
+  bf16* wsb = lds + kCXL * kCS;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -119,6 +122,7 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
   const int gr0 = tile * p.rows_per_tile, oh0 = gr0 % p.H;
   const bf16* hsrc[kCXP];
   bool hval[kCXP];
+  int lrow[kCXP];  // LDS row of the staged pixel (image rows HWP apart)
 #pragma unroll
   for (int i = 0; i < kCXP; ++i) {
     const int j = r8 + 32 * i;
@@ -126,6 +130,7 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
     const int hr = fhw2.div(rem), hc = rem - hr * p.HW2;
     const int ih = oh0 + hr - 1, iw = hc - 1;
     hval[i] = j < p.hrows && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+    lrow[i] = (slot * p.HR2 + hr) * p.HWP + hc;
     hsrc[i] = p.src + ((long long)(gr0 + slot * p.R + hr - 1) * p.W + iw) * p.Cin + ch * 8;
   }
   const bf16* wsrc = p.w + (long long)(co0 + r8) * p.Kpad + ch * 8;
@@ -139,7 +144,7 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
   auto store_halo = [&]() {
 #pragma unroll
     for (int i = 0; i < kCXP; ++i)
-      if (r8 + 32 * i < p.hrows) *reinterpret_cast<u32x4_t*>(hs + (r8 + 32 * i) * kCS + ch * 8) = rh[i];
+      if (r8 + 32 * i < p.hrows) *reinterpret_cast<u32x4_t*>(hs + lrow[i] * kCS + ch * 8) = rh[i];
   };
   auto load_w = [&](int s) {
     const int cb = s / 9, tap = s - cb * 9;
@@ -159,7 +164,7 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
   for (int t = 0; t < 4; ++t) {
     const int s = wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
     const int slot = frw.div(s), q = s - slot * frw.d, rr = fw.div(q), cc = q - rr * p.W;
-    hoff[t] = ((slot * p.HR2 + rr) * p.HW2 + cc) * kCS + fc * 8;
+    hoff[t] = ((slot * p.HR2 + rr) * p.HWP + cc) * kCS + fc * 8;
   }
   int woff[TN][2];
 #pragma unroll
@@ -186,7 +191,7 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
   for (int s = 0; s < S; ++s) {
     const int cb = s / 9, tap = s - cb * 9;
     const int kh = tap / 3, kw = tap - kh * 3;
-    const int toff = (kh * p.HW2 + kw) * kCS;
+    const int toff = (kh * p.HWP + kw) * kCS;
     const bf16* wb = wsb + (s & 1) * BN * 64;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -371,7 +376,7 @@ bool c3_geom(int H, int W, int& R, int& TI) {
     if (rpt % H != 0) return false;
     R = H, TI = rpt / H;
   }
-  return TI * (R + 2) * (W + 2) <= kCXR;
+  return TI * (R + 2) * (W + 2) <= kCXR && TI * (R + 2) * (W == 16 ? 32 : W + 2) <= kCXL;
 }
 
 }  // namespace
@@ -396,6 +401,11 @@ hipError_t conv3_halo(const IGemmArgs& a, int mode, hipStream_t st) {
   p.out = reinterpret_cast<bf16*>(a.out);
   p.H = a.OH, p.W = a.OW, p.Cin = a.SC, p.Cout = a.N, p.Kpad = a.Kpad, p.ldc = a.ldc;
   p.R = R, p.HW2 = a.OW + 2, p.HR2 = R + 2, p.hrows = TI * (R + 2) * (a.OW + 2), p.rows_per_tile = kCP / a.OW;
+  // W = 16: the 32 pixels of a pixel-interleaved MFMA tile span two image rows; an image-row pitch of
+  // W + 16 halo rows keeps their bank slots 16 apart, so the two-chunk ds_read_b128 groups stay
+  // conflict-free (24 % conflict cycles on layer 2 with the W + 2 pitch)
+  static const int pitch16 = diag_int("conv_halo_pitch16", 1);
+  p.HWP = (a.OW == 16 && pitch16) ? 32 : a.OW + 2;
   p.ntiles = a.M / kCP;
   p.relu = a.relu;
   p.alpha = a.alpha;
@@ -421,8 +431,9 @@ hipError_t conv3_halo(const IGemmArgs& a, int mode, hipStream_t st) {
   static const int ksplit = diag_int("conv_halo_splitk", 1);
   if (ksplit && a.splitk_ws && p.ntiles * p.nco < 512) {
     const long long wsf = igemm64_splitk_floats(a, mode);  // what the caller allocated
+    static const int ksmax = diag_int("conv_halo_ks", 2);  // 2 measured faster than 4 (layer 4: 38.4 vs 43.1 us)
     int ks = 1;
-    while (ks < 4 && ncb % (2 * ks) == 0 && (long long)p.ntiles * p.nco * ks * 2 <= 1024 &&
+    while (ks < ksmax && ncb % (2 * ks) == 0 && (long long)p.ntiles * p.nco * ks * 2 <= 1024 &&
            (long long)(2 * ks) * a.M * a.N <= wsf)
       ks *= 2;
     if (ks > 1) p.ks = ks, p.cbs = ncb / ks, p.ws = a.splitk_ws;

@@ -8,6 +8,11 @@
 //   bn_rpt=N        BatchNorm statistics rows per thread      wgrad_wg=N      wgrad_tr workgroup target
 //   wgrad128=N      wgrad_tr 128x128 tile rows per step       cp_wpc=N        convpool workgroups per CU cap
 //   cp_minimgs=N    convpool images per workgroup floor
+//   wgrad_halo=0    3x3 weight gradients on wgrad_tr instead of the halo kernel
+//   halo_groups=1   halo weight gradient with 4-wave workgroups (default: two groups sharing a slab)
+//   halo_wg=N       halo weight-gradient workgroup target    conv_halo=0     3x3 fwd/dgrad on igemm64
+//   conv_halo_c64=0 no weights-resident 64->64 kernel        conv_halo_splitk=0 / conv_halo_ks=N
+//                                                            halo fwd/dgrad channel-block split (max N)
 #pragma once
 #include <cstdlib>
 #include <cstring>
