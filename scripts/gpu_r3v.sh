@@ -14,3 +14,9 @@ for i in 1 2; do
 timeout -k 10 120 python bench.py --model resnet18_cifar --batch-per-gpu 256 --steps 200 --warmup 10 --async-steps 0 > gpurun_out/b_rn_v.log 2>&1 || { tail -n 20 gpurun_out/b_rn_v.log; exit 1; }
 python3 -c "import json; d=json.loads(open('gpurun_out/b_rn_v.log').read().strip().splitlines()[-1]); print(round(d['value']), d['ms_per_step'])"
 done
+DISTRIFLOW_DIAG=conv_halo_pitch16=0 timeout -k 10 200 python scripts/convbench.py l2 > gpurun_out/cb_v2.txt 2>&1 || { tail -n 20 gpurun_out/cb_v2.txt; exit 1; }
+echo "pitch16=0: $(grep l2 gpurun_out/cb_v2.txt)"
+for i in 1 2; do
+DISTRIFLOW_DIAG=conv_halo_pitch16=0 timeout -k 10 120 python bench.py --model resnet18_cifar --batch-per-gpu 256 --steps 200 --warmup 10 --async-steps 0 > gpurun_out/b_rn_v.log 2>&1 || { tail -n 20 gpurun_out/b_rn_v.log; exit 1; }
+echo "pitch16=0: $(python3 -c "import json; d=json.loads(open('gpurun_out/b_rn_v.log').read().strip().splitlines()[-1]); print(round(d['value']), d['ms_per_step'])")"
+done
