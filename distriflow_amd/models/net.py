@@ -447,8 +447,10 @@ class Net:
         return self.stats
 
     def _wgrad_side(self, layer):
-        """Side stream for ``layer``'s weight gradients (ResNet blocks on the GPU), else None.
-        ``DISTRIFLOW_DIAG=wgrad_overlap=0`` keeps them in order on the main stream."""
+        """Side stream for ``layer``'s weight gradients (ResNet blocks on the GPU), else None.  Off by
+        default since the halo-tiled weight gradients (csrc/wgrad_halo.hip) fill whole CUs and the overlap
+        then slows the data-gradient chain more than it hides; ``DISTRIFLOW_DIAG=wgrad_overlap=1`` turns it
+        on."""
         if not isinstance(layer, ResidualBlock):
             return None
         on = self.is_gpu and diag_on("wgrad_overlap")
