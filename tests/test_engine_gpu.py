@@ -394,3 +394,20 @@ def test_bn_backward_statistics_from_dgrad_epilogue(monkeypatch):
         torch.testing.assert_close(dx_f.float(), dx_s.float(), rtol=2e-2, atol=1e-3)
         checked += 1
     assert checked >= 4
+
+
+def test_resnet_weight_gradient_overlap_matches_in_order(monkeypatch):
+    """ResNet-18 weight gradients on the side stream (``wgrad_overlap=1``) give the same gradients, bit for
+    bit, as the in-order default (same deterministic kernels; only the stream placement differs)."""
+    torch.manual_seed(0)
+    B = 16
+    x = torch.rand((B, 32, 32, 3), device="cuda").to(torch.bfloat16).float()
+    y = torch.randint(0, 10, (B,), dtype=torch.int32, device="cuda")
+    grads = []
+    for ov in ("0", "1"):
+        monkeypatch.setenv("DISTRIFLOW_DIAG", f"wgrad_overlap={ov}")
+        net = build_model("resnet18_cifar", device="cuda", seed=5)
+        net.compute_gradients(x, y)
+        torch.cuda.synchronize()
+        grads.append(net.store.grad.clone())
+    assert torch.equal(grads[0], grads[1])
