@@ -18,7 +18,8 @@ Python switches (default in brackets):
   wgrad_overlap [0]        ResNet weight gradients on a side stream (round 2: +3 %; with the halo-tiled
                            kernels, whose workgroups fill whole CUs, in-order is faster: 83.7 k vs 79.5 k
                            images/s, profiles/r3/resnet18_b256_stream_overlap_ab.txt)
-  proj_overlap [1]         ResNet projection shortcut on a side stream
+  proj_overlap [0]         ResNet projection shortcut on a side stream (in order is faster with the halo
+                           kernels: 87.0 k vs 85.0 k images/s, profiles/r3/resnet18_b256_inorder_ab.txt)
   concurrent_backward [0]  head weight gradients on side streams (measured slower)
   bn_epilogue [0]          BatchNorm statistics finalised inside the producing conv launches instead of
                            separate statistics passes (correct, but the write-through + ticket tail each
@@ -30,7 +31,7 @@ from __future__ import annotations
 import os
 
 _DEFAULTS = {"lenet_fused": 1, "lenet_fused_update": 1, "async_fused": 1, "kcnn_fused": 1, "khead_fused": 1, "fold_dropout": 1,
-             "multistep": 1, "wgrad_overlap": 0, "proj_overlap": 1, "concurrent_backward": 0, "bn_epilogue": 0}
+             "multistep": 1, "wgrad_overlap": 0, "proj_overlap": 0, "concurrent_backward": 0, "bn_epilogue": 0}
 
 
 def diag(name: str) -> int:

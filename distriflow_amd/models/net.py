@@ -458,7 +458,8 @@ class Net:
 
     def _proj_side(self, layer):
         """Stream for a ResNet block's projection shortcut branch (joined inside the block), else None.
-        ``DISTRIFLOW_DIAG=proj_overlap=0`` keeps it in order."""
+        Off by default (measured slower beside the halo-tiled kernels); ``DISTRIFLOW_DIAG=proj_overlap=1``
+        turns it on."""
         if not (isinstance(layer, ResidualBlock) and layer.proj is not None and self.is_gpu):
             return None
         return self._side[1] if diag_on("proj_overlap") else None
