@@ -48,6 +48,11 @@ def test_model_gradients_match_cpu(name, B, min_cos):
     assert all(coss[k] > 0.99 for k in last), coss
     bad = {k: v for k, v in coss.items() if v < min_cos}
     assert not bad, bad
+    # conv weight gradients are the tensors an inner-block kernel bug would corrupt; measured on MI355X
+    # (profiles/resnet18_grad_cosines.txt) every ResNet conv kernel is >= 0.97 against fp32, BN
+    # gamma/beta >= 0.93 (B=16 batch statistics amplify bf16 rounding), so hold conv kernels to 0.96.
+    conv_bad = {k: v for k, v in coss.items() if k.endswith("/kernel") and v < max(min_cos, 0.96)}
+    assert not conv_bad, conv_bad
 
 
 @pytest.mark.parametrize("name", ["lenet5", "keras_cnn", "resnet18_cifar"])
