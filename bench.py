@@ -235,6 +235,10 @@ def main():
                 "graph": trainer.graph_mode,
                 "steps_per_graph": getattr(trainer, "_multi_u", 0) or 1,
                 "allreduce": trainer.allreduce_path if world > 1 else None,
+                # why the one-shot / in-kernel exchange path was or was not taken, and the real-kernel
+                # self-test of the fused multi-rank step (parallel/data_parallel.py _verify_fused_exchange)
+                "p2p_reason": getattr(trainer, "p2p_reason", None) or None,
+                "fused_selftest": getattr(trainer, "fused_selftest", None) or None,
                 "step": trainer.step_launches,
                 "params": net.num_params(),
             },
@@ -247,6 +251,9 @@ def main():
             out["phases_ms_eager"] = phases
         if diag_active():
             out["diagnostics"] = diag_active()  # a diagnostic run: never a production number
+        if os.environ.get("DISTRIFLOW_DIAG", "").strip():
+            # verbatim, including switches only the native code reads (csrc/diag.h)
+            out["distriflow_diag"] = os.environ["DISTRIFLOW_DIAG"]
         if args.json_extra:
             out["extra"] = {"final_loss": loss, "train_tflops": value * net.flops_per_example() / 1e12,
                             "capture_error": getattr(trainer, "capture_error", None)}

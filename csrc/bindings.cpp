@@ -468,14 +468,15 @@ void sgd_multi_py(torch::Tensor descs, int64_t ndesc, int64_t total_blocks, torc
     is.dst = reinterpret_cast<long long*>(idx_dst->data_ptr());
     is.B = (int)idx_dst->numel();
     is.nsteps = (int)idx_stream->size(0);
-    if (run_stats.has_value() && run_stats->defined()) {
-      TORCH_CHECK(step_stats.has_value() && step_stats->defined(), "run_stats needs step_stats");
-      need(*run_stats, at::kFloat, "run_stats");
-      need(*step_stats, at::kFloat, "step_stats");
-      TORCH_CHECK(run_stats->numel() >= 3 && step_stats->numel() >= 2, "run_stats [3] / step_stats [2]");
-      is.run_stats = run_stats->data_ptr<float>();
-      is.step_stats = step_stats->data_ptr<float>();
-    }
+  }
+  // device run statistics, with or without an index stream (the same extra workgroup accumulates them)
+  if (run_stats.has_value() && run_stats->defined()) {
+    TORCH_CHECK(step_stats.has_value() && step_stats->defined(), "run_stats needs step_stats");
+    need(*run_stats, at::kFloat, "run_stats");
+    need(*step_stats, at::kFloat, "step_stats");
+    TORCH_CHECK(run_stats->numel() >= 3 && step_stats->numel() >= 2, "run_stats [3] / step_stats [2]");
+    is.run_stats = run_stats->data_ptr<float>();
+    is.step_stats = step_stats->data_ptr<float>();
   }
   if (lenet_frag.has_value() && lenet_frag->defined()) {
     TORCH_CHECK(lenet_frag->is_cuda() && lenet_frag->is_contiguous() &&
@@ -1500,58 +1501,82 @@ class P2PComm {
 
 static dfa::LLComm p2p_ll_args(const P2PComm& c) { return c.ll_args(); }
 
-// Device-resident async parameter server (csrc/async_ps.hip): the server rank owns the shared
-// seqlock / batch counter / fp32 master buffer (IPC exported); every rank maps it.
+// Device-resident async parameter server (csrc/async_ps.hip, csrc/ps_device.h).  The server rank owns
+// the control buffer (version word, FCFS cursor, completion arrays); EVERY rank owns one shard of the fp32
+// master (a contiguous, power-of-two-sized parameter range) in its own HBM.  Both kinds of buffer are
+// uncached, IPC exported and mapped into every rank, so the applies of different ranks land on
+// different shards in parallel over xGMI.  Each shard carries a 64-word self-test area after its range.
 class PSComm {
  public:
-  PSComm(int64_t rank, int64_t server_rank, int64_t n, double timeout_s)
-      : rank_((int)rank), server_((int)server_rank), n_(n) {
+  static constexpr int kTestWords = 64;
+  PSComm(int64_t rank, int64_t world, int64_t server_rank, int64_t n, double timeout_s)
+      : rank_((int)rank), world_((int)world), server_((int)server_rank), n_(n) {
     TORCH_CHECK(n > 0 && n % 4 == 0, "ps: n must be a positive multiple of 4");
+    TORCH_CHECK(world >= 1 && world <= dfa::kP2PMaxRanks, "ps: 1..8 ranks");
+    TORCH_CHECK(rank >= 0 && rank < world && server_rank >= 0 && server_rank < world, "ps: bad rank");
     check_hip(hipGetDevice(&dev_), "ps getDevice");
-    if (rank_ == server_) {
-      void* p = nullptr;
-      const size_t bytes = sched_off() + 2 * (size_t)dfa::kPSMaxBatches * 4;
-      hipError_t e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
-      if (e != hipSuccess) {
-        (void)hipGetLastError();
-        check_hip(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained), "ps alloc");
-      }
-      shared_ = (char*)p;
-      check_hip(hipMemset(shared_, 0, bytes), "ps memset");
-    }
+    // shard length: the smallest power of two >= 64 with world shards covering n
+    shift_ = 6;
+    while (((n_ - 1) >> shift_) >= world_) ++shift_;
+    if (rank_ == server_) shared_ = alloc_uncached(256 + 2 * (size_t)dfa::kPSMaxBatches * 4, "ps control");
+    own_ = (float*)alloc_uncached(((size_t)1 << shift_) * 4 + kTestWords * 4, "ps shard");
     check_hip(hipMalloc((void**)&local_, 4096), "ps local alloc");
     check_hip(hipMemset(local_, 0, 4096), "ps local memset");
     check_hip(hipDeviceSynchronize(), "ps init sync");
     timeout_ticks_ = (int64_t)(timeout_s * 1e8);
+    for (auto& p : shard_) p = nullptr;
   }
   ~PSComm() {
     if (shared_ && rank_ != server_) (void)hipIpcCloseMemHandle(shared_);
     if (shared_ && rank_ == server_) (void)hipFree(shared_);
+    for (int k = 0; k < world_; ++k)
+      if (shard_[k] && k != rank_) (void)hipIpcCloseMemHandle(shard_[k]);
+    if (own_) (void)hipFree(own_);
     if (local_) (void)hipFree(local_);
   }
   py::bytes handle() const {
-    TORCH_CHECK(rank_ == server_, "ps: only the server rank exports the shared buffer");
-    hipIpcMemHandle_t h;
-    check_hip(hipIpcGetMemHandle(&h, shared_), "hipIpcGetMemHandle");
-    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+    TORCH_CHECK(rank_ == server_, "ps: only the server rank exports the control buffer");
+    return export_handle(shared_);
   }
-  void open(const std::string& handle) {
-    if (rank_ == server_) return;
-    TORCH_CHECK(handle.size() == sizeof(hipIpcMemHandle_t), "ps: bad handle size");
-    hipIpcMemHandle_t h;
-    memcpy(&h, handle.data(), sizeof(h));
-    void* p = nullptr;
-    check_hip(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
-    shared_ = (char*)p;
+  py::bytes shard_handle() const { return export_handle(own_); }
+  // ctrl: the server's control-buffer handle; shards[k]: rank k's shard handle (every rank's, own included)
+  void open(const std::string& ctrl, std::vector<std::string> shards) {
+    TORCH_CHECK((int)shards.size() == world_, "ps: one shard handle per rank");
+    if (rank_ != server_) shared_ = (char*)open_handle(ctrl);
+    for (int k = 0; k < world_; ++k) shard_[k] = k == rank_ ? own_ : (float*)open_handle(shards[k]);
+    std::vector<float*> tab(dfa::kP2PMaxRanks, nullptr);
+    for (int k = 0; k < world_; ++k) tab[k] = shard_[k] + ((size_t)1 << shift_);  // self-test areas
+    check_hip(hipMemcpy(local_ + 2048, tab.data(), tab.size() * sizeof(float*), hipMemcpyHostToDevice), "ps tab");
   }
-  int64_t nstride() const { return (n_ + 63) / 64 * 64; }
-  // server only: seed the shared master (before any worker pulls): version 0 lives in buffer 0
+  int64_t shard_len() const { return (int64_t)1 << shift_; }
+  int64_t nshards_used() const { return (n_ - 1) / shard_len() + 1; }
+  // every rank: seed its own shard's range of the master (the ranks hold identical initial weights)
   void init_master(torch::Tensor w) {
-    TORCH_CHECK(rank_ == server_ && shared_, "ps: init_master on the server rank");
     need(w, at::kFloat, "ps master");
     TORCH_CHECK(w.numel() == n_, "ps: master size mismatch");
-    check_hip(hipMemcpy(shared_ + 256, w.data_ptr(), (size_t)n_ * 4, hipMemcpyDeviceToDevice), "ps init copy");
+    const int64_t lo = (int64_t)rank_ * shard_len(), hi = std::min<int64_t>(n_, lo + shard_len());
+    if (hi > lo)
+      check_hip(hipMemcpy(own_, w.data_ptr<float>() + lo, (size_t)(hi - lo) * 4, hipMemcpyDeviceToDevice), "ps init");
     check_hip(hipDeviceSynchronize(), "ps init sync");
+  }
+  // self-test of the element add on every shard (call on every rank between two barriers): every rank
+  // adds (rank + 1) * (j + 1) to word j of every shard's test area
+  void selftest_add() {
+    dfa::PSArgs a = args();
+    check_hip(dfa::ps_selftest_add(a, reinterpret_cast<float* const*>(local_ + 2048), kTestWords, (float)(rank_ + 1),
+                                   cur_stream()),
+              "ps selftest");
+    check_hip(hipStreamSynchronize(cur_stream()), "ps selftest sync");
+  }
+  // after every rank's selftest_add: each test word must hold (j + 1) * W (W + 1) / 2 exactly
+  bool selftest_check() const {
+    std::vector<float> v(kTestWords);
+    for (int k = 0; k < world_; ++k) {
+      check_hip(hipMemcpy(v.data(), shard_[k] + shard_len(), kTestWords * 4, hipMemcpyDeviceToHost), "ps selftest rd");
+      for (int j = 0; j < kTestWords; ++j)
+        if (v[j] != (float)((j + 1) * world_ * (world_ + 1) / 2)) return false;
+    }
+    return true;
   }
   int64_t host_error() const { return herr_.read(); }  // no HIP call: safe from a watchdog thread
   // Epoch-scoped at-least-once dispatch over `nbatches` microbatch ids, `max_epochs` dataset epochs
@@ -1561,6 +1586,13 @@ class PSComm {
     TORCH_CHECK(max_epochs >= 0, "ps: max_epochs must be >= 0");
     nbatches_ = nbatches;
     max_epochs_ = (int)max_epochs;
+  }
+  // the device learning rate the applies read (the trainer's hyper tensor; set_lr after capture holds)
+  void set_lr_source(torch::Tensor hyper) {
+    need(hyper, at::kFloat, "ps lr source");
+    TORCH_CHECK(hyper.numel() >= 1 && hyper.get_device() == dev_, "ps: lr source on this device");
+    lr_dev_ = hyper.data_ptr<float>();
+    lr_keep_ = hyper;
   }
   // [epoch, completed in epoch, completed, redispatched, skipped, duplicates, finished]
   std::vector<int64_t> schedule_stats() const {
@@ -1575,7 +1607,7 @@ class PSComm {
   std::vector<int64_t> done_epochs() const {
     std::vector<unsigned> v((size_t)nbatches_);
     if (nbatches_ > 0)
-      check_hip(hipMemcpy(v.data(), shared_ + sched_off(), (size_t)nbatches_ * 4, hipMemcpyDeviceToHost), "ps done");
+      check_hip(hipMemcpy(v.data(), shared_ + 256, (size_t)nbatches_ * 4, hipMemcpyDeviceToHost), "ps done");
     return std::vector<int64_t>(v.begin(), v.end());
   }
   void fetch_pull(torch::Tensor w, c10::optional<torch::Tensor> perm, c10::optional<torch::Tensor> idx) {
@@ -1606,8 +1638,8 @@ class PSComm {
     a.max_stale = (int)max_stale;
     check_hip(dfa::ps_apply(a, cur_stream()), "ps_apply");
   }
-  // device view of this rank's counters [accepted, rejected, sum staleness, max staleness, torn, err,
-  // no-op steps, -] (int64): read back asynchronously by the trainer's callbacks
+  // device view of this rank's counters [accepted, rejected, sum staleness, max staleness, admission CAS
+  // retries, err, no-op steps, -] (int64): read back asynchronously by the trainer's callbacks
   torch::Tensor stats_tensor() const {
     return torch::from_blob(local_ + 64, {8}, torch::TensorOptions().dtype(torch::kLong).device(torch::kCUDA, dev_));
   }
@@ -1626,62 +1658,93 @@ class PSComm {
     a.max_stale = (int)max_stale;
     return a;
   }
-  // [accepted, rejected, sum staleness, max staleness, torn retries, err, version, batches claimed]
+  // [accepted, rejected, sum staleness, max staleness, admission CAS retries, err, version, batch cursor,
+  //  no-op steps]
   std::vector<int64_t> stats() const {
     unsigned long long h[8] = {0};
     check_hip(hipMemcpy(h, local_ + 64, 64, hipMemcpyDeviceToHost), "ps stats");
-    unsigned seq = 0;
+    unsigned ver = 0;
     unsigned long long ctr = 0;
-    check_hip(hipMemcpy(&seq, shared_, 4, hipMemcpyDeviceToHost), "ps seq");
+    check_hip(hipMemcpy(&ver, shared_, 4, hipMemcpyDeviceToHost), "ps ver");
     check_hip(hipMemcpy(&ctr, shared_ + 16, 8, hipMemcpyDeviceToHost), "ps ctr");
     return {(int64_t)h[0], (int64_t)h[1], (int64_t)h[2], (int64_t)h[3], (int64_t)h[4], (int64_t)h[5],
-            (int64_t)(seq >> 1), (int64_t)ctr, (int64_t)h[6]};
+            (int64_t)ver, (int64_t)ctr, (int64_t)h[6]};
   }
-  // copy of the committed version (call while no worker is stepping)
+  // the master, gathered from the shards (call while no worker is stepping)
   void copy_master(torch::Tensor dst) const {
     need(dst, at::kFloat, "ps dst");
     TORCH_CHECK(dst.numel() == n_, "ps: dst size mismatch");
     check_hip(hipDeviceSynchronize(), "ps copy_master sync");
-    unsigned seq = 0;
-    check_hip(hipMemcpy(&seq, shared_, 4, hipMemcpyDeviceToHost), "ps seq");
-    const size_t off = 256 + (size_t)((seq >> 1) % 3u) * nstride() * 4;
-    check_hip(hipMemcpyAsync(dst.data_ptr(), shared_ + off, (size_t)n_ * 4, hipMemcpyDeviceToDevice, cur_stream()),
-              "ps copy_master");
+    for (int64_t k = 0; k < nshards_used(); ++k) {
+      const int64_t lo = k * shard_len(), hi = std::min<int64_t>(n_, lo + shard_len());
+      check_hip(hipMemcpyAsync(dst.data_ptr<float>() + lo, shard_[k], (size_t)(hi - lo) * 4, hipMemcpyDeviceToDevice,
+                               cur_stream()),
+                "ps copy_master");
+    }
   }
 
  private:
+  static char* alloc_uncached(size_t bytes, const char* what) {
+    void* p = nullptr;
+    hipError_t e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      check_hip(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained), what);
+    }
+    check_hip(hipMemset(p, 0, bytes), what);
+    return (char*)p;
+  }
+  static py::bytes export_handle(void* p) {
+    hipIpcMemHandle_t h;
+    check_hip(hipIpcGetMemHandle(&h, p), "hipIpcGetMemHandle");
+    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  }
+  static void* open_handle(const std::string& handle) {
+    TORCH_CHECK(handle.size() == sizeof(hipIpcMemHandle_t), "ps: bad handle size");
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle.data(), sizeof(h));
+    void* p = nullptr;
+    check_hip(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    return p;
+  }
   dfa::PSArgs args() const {
-    TORCH_CHECK(shared_ != nullptr, "ps: open() the server handle first");
+    TORCH_CHECK(shared_ != nullptr && shard_[rank_] != nullptr, "ps: open() the handles first");
     dfa::PSArgs a{};
-    a.seq = reinterpret_cast<unsigned*>(shared_);
+    a.ver = reinterpret_cast<unsigned*>(shared_);
     a.batch_ctr = reinterpret_cast<unsigned long long*>(shared_ + 16);
-    a.ps_w = reinterpret_cast<float*>(shared_ + 256);
+    for (int k = 0; k < world_; ++k) a.shard[k] = shard_[k];
+    a.shard_shift = shift_;
+    a.nshards = world_;
+    a.excl = world_ == 1 ? 1 : 0;
     a.n = n_;
-    a.nstride = nstride();
     a.vpulled = reinterpret_cast<unsigned*>(local_);
     a.bid_out = reinterpret_cast<long long*>(local_ + 8);
     a.stats = reinterpret_cast<unsigned long long*>(local_ + 64);
     a.scratch = reinterpret_cast<unsigned*>(local_ + 1024);
     a.timeout_ticks = timeout_ticks_;
     a.max_stale = -1;
+    a.lr_dev = lr_dev_;
     a.herr = reinterpret_cast<unsigned*>(herr_.device());
     if (nbatches_ > 0) {
       a.sched = reinterpret_cast<unsigned*>(shared_ + 32);
       a.sched_ctr = reinterpret_cast<unsigned long long*>(shared_ + 48);
-      a.done_epoch = reinterpret_cast<unsigned*>(shared_ + sched_off());
+      a.done_epoch = reinterpret_cast<unsigned*>(shared_ + 256);
       a.claimed_epoch = a.done_epoch + dfa::kPSMaxBatches;
       a.nbatches = nbatches_;
       a.max_epochs = max_epochs_;
     }
     return a;
   }
-  size_t sched_off() const { return 256 + 3 * (size_t)nstride() * 4; }
   HostFlag herr_;
-  int rank_, server_, dev_ = 0;
+  int rank_, world_, server_, dev_ = 0, shift_ = 6;
   int max_epochs_ = 0;
   int64_t n_, timeout_ticks_ = 0, nbatches_ = 0;
   char* shared_ = nullptr;
+  float* own_ = nullptr;
+  float* shard_[dfa::kP2PMaxRanks];
   char* local_ = nullptr;
+  float* lr_dev_ = nullptr;
+  torch::Tensor lr_keep_;
 };
 
 static dfa::PSArgs ps_lenet_args(const PSComm& c, const torch::Tensor& perm, const torch::Tensor& idx, double lr,
@@ -1708,8 +1771,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     a.SH = g[0]; a.SW = g[1]; a.SC = g[2]; a.OH = g[3]; a.OW = g[4]; a.KH = g[5]; a.KW = g[6]; a.stride = g[7];
     a.pad = g[8];
     a.M = (int)M; a.N = (int)N; a.K = (int)K; a.Kpad = (int)Kpad; a.ldc = (int)N;
-    static dfa::bf16 probe[8] __attribute__((aligned(16)));
-    a.src = probe; a.w = probe; a.out = probe;
+    static dfa::bf16 layout_dummy[8] __attribute__((aligned(16)));
+    a.src = layout_dummy; a.w = layout_dummy; a.out = layout_dummy;
     int ntn = 0;
     const int ntm = dfa::igemm64_bn_layout(a, (int)mode, &ntn);
     return std::make_tuple((int64_t)ntm, (int64_t)ntn);
@@ -1731,9 +1794,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     dfa::IGemmArgs a{};
     a.SH = (int)H; a.SW = (int)W; a.SC = (int)C; a.OH = (int)OH; a.OW = (int)OW; a.M = 4; a.N = (int)N; a.ldc = (int)N;
     a.K = (int)K; a.Kpad = (int)((K + 31) / 32 * 32);
-    static dfa::bf16 probe[8] __attribute__((aligned(16)));
+    static dfa::bf16 layout_dummy[8] __attribute__((aligned(16)));
     static uint8_t codep[4] __attribute__((aligned(4)));
-    a.src = probe; a.w = probe; a.out = probe; a.pool_code = codep;
+    a.src = layout_dummy; a.w = layout_dummy; a.out = layout_dummy; a.pool_code = codep;
     return dfa::igemm64_pool_supported(a) && N % 8 == 0;
   });
   m.def("unpool2", [](torch::Tensor dyp, torch::Tensor code, torch::Tensor dy) {
@@ -1780,7 +1843,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("geom"), py::arg("defer") = false);
   m.def("slab_reduce_multi", &slab_reduce_multi_py, "several deferred split-m slab reductions in one launch");
   m.def("convpool_dgrad", &convpool_dgrad_py, "data gradient through the fused conv+pool");
-  m.def("convpool_set_debug", &dfa::convpool_set_debug, "profiling aid: skip kernel phases (bit mask)");
   m.def("convpool_set_stamps", [](c10::optional<torch::Tensor> buf) {
     if (buf.has_value() && buf->defined()) {
       TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == at::kLong && buf->numel() >= 4096 * 32,
@@ -1831,7 +1893,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("idx"), py::arg("scale"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("kpad1"),
         py::arg("w2t"), py::arg("dyp"), py::arg("code"), py::arg("slabs"), py::arg("g_w1"), py::arg("g_b1"),
         py::arg("g_w2"), py::arg("g_b2"), py::arg("step_inc") = py::none());
-  m.def("kcnn_set_debug", &dfa::kcnn_set_debug, "measurement aid: skip parts of the conv-block backward");
   m.def("kcnn_slab_floats", [](int64_t B) { return (int64_t)dfa::kcnn_slab_floats((int)B); });
   m.def("classifier_metrics", &classifier_metrics_py,
         "[loss sum, correct] of a classifier batch (one launch); out_act 0 logits, 1 softmax, 2 sigmoid output");
@@ -1868,12 +1929,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_timeout", &P2PComm::set_timeout)
       .def_property_readonly("max_floats", &P2PComm::max_floats)
       .def_property_readonly("ll_slots", &P2PComm::ll_slots);
-  py::class_<PSComm>(m, "PSComm", "device-resident bounded-staleness parameter server over IPC/xGMI")
-      .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("server_rank"), py::arg("n"),
-           py::arg("timeout_s") = 30.0)
+  py::class_<PSComm>(m, "PSComm", "device-resident bounded-staleness parameter server, master sharded over the ranks")
+      .def(py::init<int64_t, int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("world"),
+           py::arg("server_rank"), py::arg("n"), py::arg("timeout_s") = 30.0)
       .def("handle", &PSComm::handle)
-      .def("open", &PSComm::open)
+      .def("shard_handle", &PSComm::shard_handle)
+      .def("open", &PSComm::open, py::arg("ctrl"), py::arg("shards"))
       .def("init_master", &PSComm::init_master)
+      .def("selftest_add", &PSComm::selftest_add)
+      .def("selftest_check", &PSComm::selftest_check)
+      .def("set_lr_source", &PSComm::set_lr_source)
+      .def_property_readonly("shard_len", &PSComm::shard_len)
+      .def_property_readonly("nshards_used", &PSComm::nshards_used)
       .def("fetch_pull", &PSComm::fetch_pull, py::arg("w"), py::arg("perm") = py::none(), py::arg("idx") = py::none())
       .def("apply", &PSComm::apply, py::arg("g"), py::arg("lr"), py::arg("max_stale"))
       .def("stats", &PSComm::stats)

@@ -50,13 +50,10 @@ struct CPGeom {
   int G, S, RowP, ystr, xs_img;  // G = gcd(C,8): copy ci is shifted by ci*G elements, S = 8/G copies
   int pair;                       // forward pair mode (N <= 8): cols 8-15 = pixel x+1 via shifted weights
   int wRLp, wKpad2;               // GLOBAL weight layout (row-segment, KW columns): round8(KW*Cp), row length
-  int dbg;                        // profiling aid: bit0 skip staging, bit1 skip shift build, 16/32 early exits
   unsigned long long* stamps;     // profiling aid: per-block s_memtime stamps [grid][32] (nullptr = off)
 };
 
-static int g_cp_debug = 0;
 static unsigned long long* g_cp_stamps = nullptr;
-void convpool_set_debug(int mask) { g_cp_debug = mask; }
 void convpool_set_stamps(void* buf) { g_cp_stamps = reinterpret_cast<unsigned long long*>(buf); }
 
 // Diagnostic phase stamps (cdna_hip_programming.md §7 "In-kernel stamps"): read SHARES, not lengths.
@@ -236,7 +233,6 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
   bf16* xs = reinterpret_cast<bf16*>(smem + round_up(gtiles * 16 * 4 + gtiles * 8, 16));  // [imgs][Hp][S][RowP]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   CP_STAMP(0);
-  if (g.dbg & 16) return;
 
   // ---- once per workgroup: tables, zero-bordered image slots, register-resident weights
   const FDiv dtpi(tpi), dPW(g.PW), dG(g.G);
@@ -314,10 +310,6 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
   }
   __syncthreads();
 
-  if (g.dbg & 32) {
-    if (bv[0] == 12345.f && koff[0] == 7 && blim[0] == 3) p[0] = bfr[0][0][0];
-    return;
-  }
   ImgPlan<CHM> plan;
   make_img_plan(plan, g, g.ystr, g.Cp);
   CP_STAMP(1);
@@ -325,15 +317,14 @@ __global__ void __launch_bounds__(256) convpool_fwd_kernel(CPGeom g, int vec, co
   // ---- persistent loop over groups of images
   for (int b0 = blockIdx.x * g.imgs; b0 < g.B; b0 += gridDim.x * g.imgs, ++grp) {
     const int nimg = min(g.imgs, g.B - b0);
-    if (g.dbg & 1) {
-    } else if (vec) {  // -> copy 0 of each row
+    if (vec) {  // -> copy 0 of each row
       stage_plan(xs, g.xs_img, plan, g, x, x_u8, idx, nrows, scale, b0, nimg, g.Cp);
     } else {
       stage_images(xs, g, x, x_u8, idx, nrows, scale, b0, nimg, g.xs_img, g.ystr, g.Cp);
     }
     __syncthreads();
     CP_STAMP(2 + 3 * grp);
-    if (g.S > 1 && !(g.dbg & 2)) {  // shifted copies of the interior rows (border rows stay zero in every copy)
+    if (g.S > 1) {  // shifted copies of the interior rows (border rows stay zero in every copy)
       const int lim_img = nimg * per_img;
 #pragma unroll
       for (int j = 0; j < BT; ++j) {
@@ -1305,7 +1296,6 @@ static const FwdLayout& choose_fwd_layout(const CPGeom& g0, bool pair) {
 
 static CPGeom make_geom(int B, int H, int W, int C, int KH, int KW, int pad, int N) {
   CPGeom g{};
-  g.dbg = g_cp_debug;
   g.stamps = g_cp_stamps;
   g.B = B; g.H = H; g.W = W; g.C = C; g.KH = KH; g.KW = KW; g.pad = pad; g.N = N;
   g.OH = H + 2 * pad - KH + 1;

@@ -46,9 +46,6 @@ constexpr int NP0 = H0 * H0, NP1 = H1 * H1, NP2 = H2 * H2, NPP = PW * PW;  // 78
 constexpr int K2 = 9 * C;                                                   // 288
 constexpr int S2 = K2 + 1, S1 = 10;  // slab row lengths: conv2 (288 + bias), conv1 (9 + bias)
 
-// measurement aid (kcnn_set_debug): bit 0 skips the conv2 weight gradient, bit 1 the data gradient +
-// conv1 weight gradient, bit 2 the conv1 recompute, bit 3 the dY2 expansion (results are then wrong)
-int g_kcnn_debug = 0;
 
 typedef __bf16 bf16x4_vs __attribute__((__vector_size__(8)));
 
@@ -204,7 +201,7 @@ __global__ void __launch_bounds__(KT, 2) kcnn_fwd_kernel(KcnnArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a, int dbg) {
+__global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 x0[NP0];
   __shared__ __attribute__((aligned(16))) bf16 x1[NP1 * C];
   __shared__ __attribute__((aligned(16))) bf16 dy2[NP2 * C];
@@ -227,7 +224,7 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a, int dbg) {
     // ---- stage x0; expand dY2 from the pooled gradient and the codes (conv2 bias gradient on the way)
     store_x0(xr, x0);
     xr = load_x0(a, b + gridDim.x);
-    for (int e = tid; e < ((dbg & 8) ? 0 : NPP * 4); e += KT) {
+    for (int e = tid; e < NPP * 4; e += KT) {
       const int q = e >> 2;
       const long long o = ((long long)b * NPP + q) * C + 8 * c8;
       const bf16x8 gv = ld8(a.dyp + o);
@@ -247,7 +244,7 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a, int dbg) {
       }
     }
     __syncthreads();
-    if (!(dbg & 4)) conv1_to_lds(a, x0, x1);
+    conv1_to_lds(a, x0, x1);
     __syncthreads();
 
     // ---- conv2 weight gradient: D[n][(tap, ci)] += dY2^T[n][p] X1[p + tap][ci] over 18 blocks of 32 output
@@ -256,7 +253,7 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a, int dbg) {
     {
       const int q = i >> 2, cq = 4 * (i & 3);
 #pragma unroll 1
-      for (int k0 = 0; k0 < ((dbg & 1) ? 0 : NP2 / 32); ++k0) {
+      for (int k0 = 0; k0 < NP2 / 32; ++k0) {
         const int oy0 = 4 * (k0 / 3), ox0 = 8 * (k0 % 3);
         bf16x8 af;
         {
@@ -291,7 +288,7 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a, int dbg) {
         for (int h = 0; h < 2; ++h) bt[t][h] = ld8(a.w2t + (16 * h + i) * K2 + t * C + 8 * G);
       const int ty1 = i / 3, tx1 = i - 3 * (i / 3);  // this lane's conv1 tap (column of the conv1 B operand)
 #pragma unroll 1
-      for (int T0 = wid; T0 < ((dbg & 2) ? 0 : 49); T0 += 8) {
+      for (int T0 = wid; T0 < 49; T0 += 8) {
         bf16 gv[2][2][4];  // [tile of the pair][h][r]
         int py[2], px0[2];
 #pragma unroll
@@ -434,7 +431,6 @@ __global__ void __launch_bounds__(1024) kcnn_reduce_kernel(const float* __restri
 
 }  // namespace
 
-void kcnn_set_debug(int mask) { g_kcnn_debug = mask; }
 int kcnn_blocks(int B) { return B < 512 ? B : 512; }
 size_t kcnn_slab_floats(int B) { return (size_t)kcnn_blocks(B) * C * (S2 + S1); }
 
@@ -451,7 +447,7 @@ hipError_t kcnn_bwd(const KcnnArgs& a, float* g_w1, float* g_b1, float* g_w2, fl
       !g_w1 || !g_b1 || !g_w2 || !g_b2)
     return hipErrorInvalidValue;
   const int nb = kcnn_blocks(a.B);
-  hipLaunchKernelGGL(kcnn_bwd_kernel, dim3(nb), dim3(KT), 0, st, a, g_kcnn_debug);
+  hipLaunchKernelGGL(kcnn_bwd_kernel, dim3(nb), dim3(KT), 0, st, a);
   DFA_HIP_CHECK(hipGetLastError());
   const int outs = C * (S2 + S1);
   hipLaunchKernelGGL(kcnn_reduce_kernel, dim3(cdiv(outs, 64)), dim3(1024), 0, st, a.slab2, a.slab1, nb, g_w2, g_b2,

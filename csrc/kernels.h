@@ -238,7 +238,6 @@ struct HeadArgs {
 size_t head_train_lds(const HeadArgs& a);
 hipError_t head_train(HeadArgs a, int phases, hipStream_t st);  // phases: 1 fwd/CE/bwd-data, 2 wgrad
 
-void convpool_set_debug(int mask);
 void convpool_set_stamps(void* buf);  // [grid][32] uint64 s_memtime stamps, nullptr = off
 // forward weight layout: [Npad16][Kpad2], column ky*RLp + kx*Cp + c (zero for c >= C) with
 // RLp = round8(KW*Cp); pair layout (N <= 8): RLp = round8((KW+1)*Cp) and rows 8+n = row n shifted by Cp
@@ -307,17 +306,24 @@ hipError_t ll_selftest(const LLComm& c, const float* in, float* out, int nslots,
 
 
 
-// Device-resident async parameter server (csrc/async_ps.hip).  seq / batch_ctr / ps_w live in the
-// server rank's IPC buffer (mapped into every rank); everything else is local.
+// Device-resident async parameter server (csrc/async_ps.hip, protocol csrc/ps_device.h).  The fp32 master is
+// SHARDED by contiguous parameter range: element i lives in shard i >> shard_shift, in that rank's HBM
+// (IPC-mapped into every rank), so the appliers of different ranks update different shards -- and, inside a
+// shard, different elements -- in parallel with lock-free per-element compare-and-swap adds (or plain
+// read-modify-writes when this rank is the only writer).  The admitted-gradient version counter `ver`,
+// the FCFS cursor and the completion arrays live in the server rank's control buffer; `ver` advances by
+// a lock-free CAS whose check is the staleness bound.  No lock is ever held across an apply.
 struct PSArgs {
-  unsigned* seq;                // seqlock word: odd = writer active, version = seq / 2
+  unsigned* ver;                // admitted-gradient counter (the model version), server control buffer
   unsigned long long* batch_ctr;  // FCFS microbatch counter
-  float* ps_w;                  // shared fp32 master, triple buffered [3][nstride] (version v in buffer v % 3)
+  float* shard[kP2PMaxRanks];   // shard k's base (element i at shard[i >> shard_shift][i & (2^shift - 1)])
+  int shard_shift, nshards;
+  int excl;                     // 1: this rank is the only writer (world 1): plain read-modify-write
   float* w;                     // local fp32 master [n] (pull destination)
   const float* g;               // local fp32 gradient [n]
   long long n;
-  unsigned* vpulled;            // local: version of the last pulled snapshot
-  unsigned long long* stats;    // local [8]: accepted, rejected, sum staleness, max staleness, torn retries, err,
+  unsigned* vpulled;            // local: version the local weights were last refreshed at
+  unsigned long long* stats;    // local [8]: accepted, rejected, sum staleness, max staleness, CAS retries, err,
                                 //            no-op steps after the schedule finished
   unsigned* herr;               // host-mapped mirror of the error bits (host watchdog, no HIP call)
   unsigned* scratch;            // local [64 + kPSMaxGrid] zero-initialised protocol words (async_ps.hip)
@@ -332,7 +338,9 @@ struct PSArgs {
   unsigned long long* sched_ctr;
   unsigned* done_epoch;
   unsigned* claimed_epoch;
-  long long nbatches, timeout_ticks, nstride;
+  const float* lr_dev;          // device learning rate (the store's hyper[0]); null: use lr
+  unsigned long long* stamps;   // diagnostic [8] s_memtime / wall-clock marks of the decision (or null)
+  long long nbatches, timeout_ticks;
   int B, max_stale, max_epochs;  // max_epochs 0 = unbounded
   float lr;
 };
@@ -340,6 +348,8 @@ constexpr int kPSMaxGrid = 64;
 constexpr long long kPSMaxBatches = 1 << 20;  // capacity of the shared completion arrays
 hipError_t ps_fetch_pull(const PSArgs& a, hipStream_t st);
 hipError_t ps_apply(const PSArgs& a, hipStream_t st);
+// shard self-test: every rank adds (rank + 1) * (j + 1) to word j of every shard's test area, n words
+hipError_t ps_selftest_add(const PSArgs& a, float* const* words, int n, float rank1, hipStream_t st);
 
 
 // Whole-network LeNet-5 training step (csrc/lenet_fused.hip): conv5x5x6 'same' + pool, conv5x5x16 +
@@ -433,8 +443,6 @@ struct LeNetRedArgs {
   int ps_on;
   PSArgs ps;
   unsigned long long* stamps;  // diagnostic: [grid][8] s_memtime per phase (scripts/lenetstamps.py), or null
-  int probe;                   // diagnostic (DISTRIFLOW_DIAG lenet_red_probe): 1 dense tiles skip their loads,
-                               // 2 conv blocks skip theirs (wrong gradients: timing experiments only)
 };
 // The reference CNN's conv block (csrc/kcnn_fused.hip): conv1 3x3x1->32 + ReLU, conv2 3x3x32->32 + ReLU,
 // 2x2 max-pool [+ folded dropout], input 28x28x1, in one forward and one backward launch (+ reduce).
@@ -458,7 +466,6 @@ struct KcnnArgs {
   DropSpec drop;
 };
 int kcnn_blocks(int B);
-void kcnn_set_debug(int mask);
 size_t kcnn_slab_floats(int B);
 hipError_t kcnn_fwd(const KcnnArgs& a, hipStream_t st);
 hipError_t kcnn_bwd(const KcnnArgs& a, float* g_w1, float* g_b1, float* g_w2, float* g_b2, long long* step_inc,

@@ -854,7 +854,7 @@ __device__ __forceinline__ void dense_job(const LeNetRedArgs& a, const RedTables
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int s = s0; s < (a.probe == 1 ? s0 : s1); s += 4) {
+  for (int s = s0; s < s1; s += 4) {
     bf16x8 av[2][4], bv[2][4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -900,7 +900,7 @@ __device__ __forceinline__ void conv_job(const LeNetRedArgs& a, int s, int c, fl
   const int pl = min(p0, kLeNetConvStride - 4);  // lanes past the last parameter read the row's padding
   const int nrows = a.nblk > c ? (a.nblk - 1 - c) / kChunks + 1 : 0;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int i0 = wid; i0 < (a.probe == 2 ? 0 : nrows); i0 += 4 * 16) {
+  for (int i0 = wid; i0 < nrows; i0 += 4 * 16) {
     f32x4 v[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -967,114 +967,43 @@ __device__ __forceinline__ void red_apply(const LeNetRedArgs& a, const RedTables
 }
 
 // ---- asynchronous SGD against the device parameter server (LeNetRedArgs::ps_on) ------------------------
-// Decision codes: the gradient is admitted (apply + refresh from the new version), rejected as too stale
-// (refresh from the current version; the writer lock is held while the copies are read), the schedule
-// is finished (no-op), or a wait timed out (no-op, error bits set).
-constexpr unsigned kPSAccept = 1, kPSReject = 2, kPSFailed = 3, kPSFinished = 4;
-
-// Every exchanging workgroup (and the staging workgroup) learns this launch's decision.  Workgroup 0
-// takes the writer lock (seqlock CAS on the server's word), checks staleness = version_now -
-// version_pulled against the bound and completes the microbatch under the lock; the others wait for
-// the decision word tagged with this launch's epoch (local, agent scope: all of them are resident).
-__device__ __forceinline__ void lenet_ps_decide(const LeNetRedArgs& a, unsigned* s_dec, unsigned* s_seq, bool after_completion = false) {
+// The staging workgroup admits or rejects this step's gradient (ps_admit: one lock-free CAS on the
+// shared version word, csrc/ps_device.h) as soon as the launch starts -- the decision does not depend on
+// the gradient's values -- and publishes the decision on a local word tagged with this launch's epoch.
+// The slot owners wait for it only after their jobs (so it is normally already there), then add
+// -lr * g to their elements of the sharded master and refresh the local copies from the values the adds
+// produced.  No lock is held: the owners of different ranks update the shards in parallel.
+__device__ __forceinline__ unsigned lenet_ps_wait(const LeNetRedArgs& a, unsigned* s_dec) {
   const PSArgs& p = a.ps;
   if (threadIdx.x == 0) {
     const unsigned ep = __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const unsigned long long t0 = wall_clock64();
-    unsigned dec = kPSFailed, s = 0;
-    if (blockIdx.x == 0) {
-      const long long bid = *p.bid_out;
-      if (p.done_epoch != nullptr && bid < 0) {  // dataset finished: a no-op step (no lock taken)
-        dec = kPSFinished;
-        p.stats[6] += 1;
-      } else {
-        for (;;) {
-          s = ps_ld_acq(p.seq);
-          if (!(s & 1u)) {
-            unsigned expected = s;
-            if (__hip_atomic_compare_exchange_strong(p.seq, &expected, s + 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_SYSTEM)) {
-              const unsigned stale = (s >> 1) - *p.vpulled;
-              dec = ((int)stale <= p.max_stale || p.max_stale < 0) ? kPSAccept : kPSReject;
-              // the appliers need only the decision: publish it first, then do the bookkeeping
-              __hip_atomic_store(p.scratch + kPSLockedSeq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              __hip_atomic_store(p.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-              if (dec == kPSAccept) {
-                p.stats[0] += 1;
-                p.stats[2] += stale;
-                if (stale > p.stats[3]) p.stats[3] = stale;
-                if (p.done_epoch != nullptr) complete_microbatch(p, bid);  // under the writer lock
-              } else {
-                p.stats[1] += 1;  // rejected: the lock is held until every workgroup copied version s / 2
-              }
-              break;
-            }
-          }
-          if (wall_clock64() - t0 > (unsigned long long)p.timeout_ticks) {
-            atomicOr(p.stats + 5, 4ull);
-            if (p.herr) __hip_atomic_store(p.herr, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
+    unsigned dec = kPSFailed;
+    for (;;) {  // relaxed polls, one acquire once the word matches
+      const unsigned w = __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((w >> 3) == ep) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        dec = w & 7u;
+        break;
       }
-      if (dec != kPSAccept && dec != kPSReject) {  // no lock taken: finished schedule or timeout
-        __hip_atomic_store(p.scratch + kPSLockedSeq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(p.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (wall_clock64() - t0 > 2ull * (unsigned long long)p.timeout_ticks) {
+        atomicOr(p.stats + 5, 8ull);
+        if (p.herr) __hip_atomic_store(p.herr, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
       }
-      // the microbatch bookkeeping is done: the staging workgroup may claim the next one
-      __hip_atomic_store(p.scratch + kPSCompleted, ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      const unsigned* word = p.scratch + (after_completion ? kPSCompleted : kPSDecision);
-      for (;;) {  // relaxed polls, one acquire once the word matches (acquire polls cost every poller an
-                  // L1 invalidate per iteration)
-        const unsigned w = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned d = after_completion
-                               ? (w == ep ? __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT)
-                                          : 0u)
-                               : w;
-        if ((d >> 3) == ep) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          dec = d & 7u;
-          break;
-        }
-        if (wall_clock64() - t0 > 2ull * (unsigned long long)p.timeout_ticks) {
-          atomicOr(p.stats + 5, 8ull);
-          if (p.herr) __hip_atomic_store(p.herr, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      s = __hip_atomic_load(p.scratch + kPSLockedSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_sleep(1);
     }
     *s_dec = dec;
-    *s_seq = s;
   }
   __syncthreads();
+  return *s_dec;
 }
 
-// One parameter element on the PS: w_new = w[v] - lr * g into buffer (v + 1) % 3 of the shared master
-// (admitted) or the current w[v] (rejected); either way the local master and its bf16 compute copies
-// become that version.  Returns the local weight.
-__device__ __forceinline__ float ps_new_weight(float w, float g, float lr, bool accept) {
-#pragma clang fp contract(off)
-  return accept ? w - lr * g : w;
-}
-
-
-// Protocol arrivals: the last one publishes version v + 1 (admitted) or releases the lock (rejected) and
-// records the pulled version.
-// Arrivals are counted per slot (its owner adds one when done with it) plus one for workgroup 0's decision
-// and one for the staging workgroup: `count` of them from this workgroup, `arrivals` in all.  Workgroups
-// that own nothing do not arrive.
+// Protocol arrivals: one per slot (its owner adds one when done with it) and one from the staging
+// workgroup; the last one advances this rank's launch epoch (the decision word's tag).  Workgroups that
+// own nothing do not arrive.
 __device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, unsigned count, unsigned arrivals) {
   const PSArgs& p = a.ps;
-  // every storing wave drains its shared-master stores (uncached / fine-grained memory: complete at the
-  // server's HBM once acknowledged) and the decision words (write-through), then a relaxed arrival; the
-  // last arriver's acquire fence and system-scope release store of the version word order all of them
-  // before the publish (no per-workgroup L2 write-back or invalidate)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0 && count > 0) {
     const unsigned prev = __hip_atomic_fetch_add(p.scratch + kPSApplyDone, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1083,35 +1012,22 @@ __device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, unsigned 
       __hip_atomic_store(p.scratch + kPSEpoch, __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED,
                                                                  __HIP_MEMORY_SCOPE_AGENT) + 1u,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every workgroup's arrival happened before the unlock
-      // this launch's decision (workgroup 0 published it before arriving; workgroups that own no slot
-      // never read it)
-      const unsigned dec = __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 7u;
-      const unsigned seq = __hip_atomic_load(p.scratch + kPSLockedSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (dec == kPSAccept) {
-        *p.vpulled = (seq >> 1) + 1u;
-        __hip_atomic_store(p.seq, seq + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      } else if (dec == kPSReject) {
-        *p.vpulled = seq >> 1;
-        __hip_atomic_store(p.seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
     }
   }
 }
 
-
-
-// diagnostic phase clocks of the reduce launch: stamps[block][slot] (0 start, 1 jobs done, 2 decision,
-// 3 owned slots applied, 4 end, 6 first job's partial computed, 7 first ownership combine done)
-#define LR_STAMP(slot)                                                            \
-  do {                                                                            \
-    if (a.stamps) {                                                               \
-      __builtin_amdgcn_sched_barrier(0);                                          \
-      unsigned long long t_;                                                      \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-      __builtin_amdgcn_sched_barrier(0);                                          \
-      if (threadIdx.x == 0) a.stamps[blockIdx.x * 8 + (slot)] = t_;               \
-    }                                                                             \
+// diagnostic phase clocks of the reduce launch (wall clock, 100 MHz, comparable across CUs):
+// stamps[block][16]: 0 start, 1 jobs done, 2 decision known, 3 owned slots applied, 4 end, 5 first owned
+// slot's rank sums in (LL), 6 first job's partial computed, 7 first ownership combine done; staging
+// workgroup (PS): 8 admission start, 9 admission done / decision published, 10 next batch staged
+#define LR_STAMP(slot)                                                              \
+  do {                                                                              \
+    if (a.stamps) {                                                                 \
+      __builtin_amdgcn_sched_barrier(0);                                            \
+      const unsigned long long t_ = wall_clock64();                                 \
+      __builtin_amdgcn_sched_barrier(0);                                            \
+      if (threadIdx.x == 0) a.stamps[blockIdx.x * 16 + (slot)] = t_;                \
+    }                                                                               \
   } while (0)
 
 // MODE: 0 single rank, 1 in-kernel LL exchange over the ranks, 2 async parameter server.  One
@@ -1126,11 +1042,13 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
   __shared__ unsigned ep[kMaxOwned];
   __shared__ unsigned s_e;
   __shared__ int s_last;
+  __shared__ float* s_shard[kP2PMaxRanks];  // PS: the master shards' bases (ps_elem)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   LR_STAMP(0);
   const int nslot = a.dense_tiles + a.nconv_slots;
   const int G = a.exch_blocks;
   if ((int)blockIdx.x < G) {
+    if (PS) ps_stage_shards(a.ps, s_shard);
     stage_tables(a, &tabs);
     // with the fused sync update, the first owned slot's master / momentum elements are loaded beside
     // its slab loads
@@ -1225,10 +1143,9 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     }
     __syncthreads();
     LR_STAMP(1);
-    __shared__ unsigned s_dec, s_seq;
-    if (PS && (nown > 0 || blockIdx.x == 0)) lenet_ps_decide(a, &s_dec, &s_seq);  // 0 takes the lock
+    __shared__ unsigned s_dec;
+    const unsigned dec = (PS && nown > 0) ? lenet_ps_wait(a, &s_dec) : 0u;
     LR_STAMP(2);
-    const unsigned dec = PS ? s_dec : 0u, seq = PS ? s_seq : 0u;
 #pragma unroll 1
     for (int k = 0; k < nown; ++k) {
       const int slot = owned[k];
@@ -1257,25 +1174,36 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       }
       if (PS) {
         if (dec == kPSAccept || dec == kPSReject) {
-          // version seq / 2 of every element first (the shared master is uncached: one round trip for
-          // all of them), then the new version, local master, compute copies and fragments
+          // the elements' shard addresses; admitted: every add in flight at once (w += -lr * g on the
+          // owning shard, the local copies take the value each add produced); rejected: the shards'
+          // current values.  The learning rate is the device hyper-parameter (set_lr after capture holds).
           const PSArgs& p = a.ps;
-          const long long vb = (long long)((seq >> 1) % 3u) * p.nstride;
-          const long long nb = (long long)(((seq >> 1) + 1u) % 3u) * p.nstride;
-          float wv[kPerThread];
+          float* pe[kPerThread];
+          float d[kPerThread], wn[kPerThread];
 #pragma unroll
-          for (int e = 0; e < kPerThread; ++e)
-            wv[e] = o[e].di >= 0 ? p.ps_w[vb + tabs.d[o[e].di].off + o[e].i] : 0.f;
+          for (int e = 0; e < kPerThread; ++e) {
+#pragma clang fp contract(off)
+            d[e] = -(tabs.hyper[0] * v[e]);
+            pe[e] = o[e].di >= 0 ? ps_elem(s_shard, p.shard_shift, tabs.d[o[e].di].off + o[e].i) : nullptr;
+          }
+          if (dec == kPSAccept) {
+            ps_add<kPerThread>(pe, d, wn, p.excl != 0, p);
+          } else {
+#pragma unroll
+            for (int e = 0; e < kPerThread; ++e)
+              wn[e] = pe[e] ? __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(pe[e]), __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_SYSTEM))
+                            : 0.f;
+          }
 #pragma unroll
           for (int e = 0; e < kPerThread; ++e) {
             if (o[e].di < 0) continue;
             tabs.g[o[e].di][o[e].i] = v[e];
-            const float wn = ps_new_weight(wv[e], v[e], p.lr, dec == kPSAccept);
-            if (dec == kPSAccept) p.ps_w[nb + tabs.d[o[e].di].off + o[e].i] = wn;
-            if (npos > 1) red_emit<true>(a, tabs, o[e], wn);
-            else if (e == 0) red_emit<false>(a, tabs, o[e], wn);
+            if (npos > 1) red_emit<true>(a, tabs, o[e], wn[e]);
+            else if (e == 0) red_emit<false>(a, tabs, o[e], wn[e]);
           }
         }
+        if (k == 0) LR_STAMP(5);
         continue;
       }
       bool ok[kPerThread];
@@ -1285,6 +1213,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
         // the rank-order sum over the ranks (no all-reduce launch)
         if (LL && e < npos) ok[e] = ll_wait_sum(a.ll, slot, threadIdx.x + RT * e, ep[k], v[e], v[e]);
       }
+      if (LL && k == 0) LR_STAMP(5);
       if (npos > 1) {  // a dense unit
 #pragma unroll
         for (int e = 0; e < kPerThread; ++e)
@@ -1298,17 +1227,27 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       }
     }
     LR_STAMP(3);
-    if (PS) lenet_ps_arrive(a, (unsigned)(narr + (blockIdx.x == 0 ? 1 : 0)), (unsigned)(nslot + 2));
+    if (PS) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's shard adds have landed
+      lenet_ps_arrive(a, (unsigned)narr, (unsigned)(nslot + 1));
+    }
     LR_STAMP(4);
     return;
   }
   const int blk = blockIdx.x - G;
   if (blk == 1 && PS) {
-    // async: once this launch's decision is known (the current microbatch is completed under the lock),
-    // claim the next microbatch FCFS on the server and stage its example indices
-    __shared__ unsigned s_dec, s_seq;
+    // async: admit or reject this step's gradient right away (lock-free CAS on the shared version; the
+    // owners pick the decision up after their jobs), complete its microbatch, then claim the next one FCFS
+    // on the server and stage its example indices
     __shared__ long long s_bid;
-    lenet_ps_decide(a, &s_dec, &s_seq, /*after_completion=*/true);
+    LR_STAMP(8);
+    if (threadIdx.x == 0) {
+      const unsigned ep = __hip_atomic_load(a.ps.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+      const unsigned dec = ps_admit(a.ps);
+      __hip_atomic_store(a.ps.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    LR_STAMP(9);
     if (a.ps.done_epoch != nullptr) {
       claim_microbatch(a.ps, threadIdx.x, &s_bid);
     } else if (threadIdx.x == 0) {
@@ -1318,7 +1257,8 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     __syncthreads();
     if (threadIdx.x == 0) *a.ps.bid_out = s_bid;
     ps_stage_indices(a.ps, s_bid, threadIdx.x, RT);
-    lenet_ps_arrive(a, 1u, (unsigned)(a.dense_tiles + a.nconv_slots + 2));
+    LR_STAMP(10);
+    lenet_ps_arrive(a, 1u, (unsigned)(a.dense_tiles + a.nconv_slots + 1));
     LR_STAMP(1);
     return;
   }
@@ -1397,7 +1337,6 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   a.stamps = g_lenet_stamps_host;
   // the reduce launch's clocks follow the train kernel's [4096][16] region
   r.stamps = g_lenet_stamps_host ? g_lenet_stamps_host + 4096 * 16 : nullptr;
-  r.probe = diag_int("lenet_red_probe", 0);
   if (a.B <= 0 || a.ldt % 32 || a.ldt < a.B || !a.frag || !a.ftab || !a.pxtab) return hipErrorInvalidValue;
   const int nblk = (a.B + IMG - 1) / IMG;
   if (a.prep) {
@@ -1459,9 +1398,12 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   }
   if (r.ps_on) {
     // async PS: the owners wait for workgroup 0's decision (dispatched first)
-    if (!r.sgd_on || r.ll_on || r.sgd.src || !r.ps.seq || !r.ps.ps_w || !r.ps.vpulled || !r.ps.bid_out ||
-        !r.ps.stats || !r.ps.scratch || r.exch_blocks + 2 > 1024 || r.sgd.mom)
+    if (!r.sgd_on || r.ll_on || r.sgd.src || !r.ps.ver || !r.ps.vpulled || !r.ps.bid_out || !r.ps.stats ||
+        !r.ps.scratch || r.exch_blocks + 2 > 1024 || r.sgd.mom || r.ps.nshards < 1 || r.ps.nshards > kP2PMaxRanks ||
+        r.ps.shard_shift < 6 || ((r.ps.n - 1) >> r.ps.shard_shift) >= r.ps.nshards)
       return hipErrorInvalidValue;
+    for (int k = 0; k < r.ps.nshards; ++k)
+      if (!r.ps.shard[k]) return hipErrorInvalidValue;
   }
   const int extra = ((r.sgd_on && r.sgd.src) || r.ps_on) ? 1 : 0;  // the index-staging workgroup
   const dim3 grid(r.exch_blocks + 1 + extra);

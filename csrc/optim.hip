@@ -99,6 +99,14 @@ __device__ __forceinline__ void sgd_multi_body(const DT& descs, int ndesc,
 // the static index buffer the step's first kernels read, then advances the cursor.  A replayed step
 // graph then needs no host-side copy (and no extra launch) to move to the next batch.
 __device__ __forceinline__ void index_stream_body(const IndexStream& is) {
+  if (is.src == nullptr) {  // run statistics only (no index stream bound)
+    if (threadIdx.x == 0 && is.run_stats != nullptr) {
+      is.run_stats[0] += is.step_stats[0];
+      is.run_stats[1] += is.step_stats[1];
+      is.run_stats[2] += 1.f;
+    }
+    return;
+  }
   __shared__ long long next;
   if (threadIdx.x == 0) {
     const long long c = *is.cursor;
@@ -172,7 +180,7 @@ __global__ void __launch_bounds__(256) sgd_multi_stream_kernel(const ParamDesc* 
     return;
   }
   int fb = blockIdx.x - total_blocks;
-  if (is.src != nullptr) {
+  if (is.src != nullptr || is.run_stats != nullptr) {
     if (fb == 0) {
       index_stream_body(is);  // the single index-stream workgroup
       return;
@@ -185,13 +193,14 @@ __global__ void __launch_bounds__(256) sgd_multi_stream_kernel(const ParamDesc* 
 hipError_t sgd_multi(const ParamDesc* descs, int ndesc, int total_blocks, float* master, const float* grad,
                      float* mom_buf, bf16* wbf, const float* hyper, int apply_update, hipStream_t st,
                      const IndexStream* is, const ParamDesc* host_descs) {
-  const bool stream = is != nullptr && is->src != nullptr;
+  // the extra workgroup: index staging and / or the run statistics
+  const bool stream = is != nullptr && (is->src != nullptr || is->run_stats != nullptr);
   const bool frag = is != nullptr && is->frag != nullptr;
   total_blocks = max(total_blocks, 0);
   if ((ndesc <= 0 || total_blocks <= 0) && !stream && !frag) return hipSuccess;
   IndexStream isv{};
   if (is != nullptr) isv = *is;
-  if (!stream) isv.src = nullptr;
+  if (!stream) isv.src = nullptr, isv.run_stats = nullptr;
   if (frag && apply_update && is->snap == nullptr) return hipErrorInvalidValue;
   const int grid = total_blocks + (stream ? 1 : 0) + (frag ? kLeNetFragBlocks : 0);
   if (host_descs != nullptr && ndesc <= kInlineDescs) {

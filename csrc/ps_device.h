@@ -1,6 +1,20 @@
 // Device-side protocol pieces of the parameter server shared by csrc/async_ps.hip (pull / apply
-// launches) and the fused LeNet-5 reduce kernel, which applies an admitted gradient to the shared
-// master itself (csrc/lenet_fused.hip): microbatch claims and completion accounting.
+// launches) and the fused LeNet-5 reduce kernel, which applies an admitted gradient to the sharded
+// master itself (csrc/lenet_fused.hip): the lock-free admission decision, the per-element shard adds,
+// microbatch claims and completion accounting.
+//
+// Reference: AsynchronousSGDServer applies every uploaded gradient on arrival and hands out the next
+// batch (/root/reference/src/server/asynchronousSGD_server.ts:65-82,95-108); the README's
+// maximumStaleness bound (/root/reference/README.md:27) is the admission check here.  Nothing in the
+// protocol holds a lock across an apply, so applies of different ranks proceed in parallel over xGMI:
+//   admission   one CAS on the shared version word `ver`: admitted iff ver - vpulled <= max_stale, and
+//               then ver -> ver + 1 (a failed CAS re-reads and re-checks);
+//   apply       per element, w += -(lr * g) on the owning shard: a plain read-modify-write when this
+//               rank is the only writer (world 1), else a compare-and-swap loop on the element's bits
+//               (no add is lost; adds of different ranks to one element serialise in memory only);
+//   refresh     the local master / compute copies take the value the add produced (admitted) or the
+//               shard's current value (rejected): every add that has landed is visible, an add admitted
+//               concurrently may be missing from some elements (at most world - 1 are in flight).
 #pragma once
 #include "common.h"
 #include "kernels.h"
@@ -8,8 +22,10 @@
 namespace dfa {
 
 // local scratch words (PSArgs::scratch, u32 index)
-constexpr int kPSPullDone = 0, kPSApplyDone = 1, kPSEpoch = 2, kPSDecision = 3, kPSLockedSeq = 4, kPSCompleted = 5,
-              kPSSlots = 64;
+constexpr int kPSPullDone = 0, kPSApplyDone = 1, kPSEpoch = 2, kPSDecision = 3, kPSSlots = 64;
+// decision codes: admitted (apply + refresh from the new values), rejected as too stale (refresh from the
+// current values), the schedule is finished (no-op), or a wait timed out (no-op, error bits set)
+constexpr unsigned kPSAccept = 1, kPSReject = 2, kPSFailed = 3, kPSFinished = 4;
 
 __device__ __forceinline__ unsigned ps_ld_acq(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -78,26 +94,141 @@ __device__ inline void claim_microbatch(const PSArgs& a, int t, long long* s_bid
   }
 }
 
-// Completion accounting for an admitted gradient; runs in one thread while it holds the writer lock,
-// so every completion is serialised.  A gradient claimed in an older epoch, or for a batch another
-// worker already completed, is applied but counted as a duplicate.
+// Completion accounting for an admitted gradient, lock-free (admissions of different ranks may run it
+// concurrently).  The exchange on done_epoch[b] makes exactly one admitted gradient per (batch, epoch)
+// the completing one; a gradient claimed in an older epoch, or for a batch another worker already
+// completed, is applied but counted as a duplicate.  The completion that brings the epoch's count to
+// nbatches resets the count and opens the next epoch (a completion of epoch e + 1 needs a claim made
+// after that release, so no completion of the new epoch is counted before the reset).
 __device__ inline void complete_microbatch(const PSArgs& a, long long bid) {
   const unsigned e = (unsigned)(bid >> 32);
   const long long bb = bid & 0xffffffffLL;
   const unsigned cur = __hip_atomic_load(a.sched, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (e != cur || ps_ld_acq(a.done_epoch + bb) == e + 1u) {
+  if (e != cur || __hip_atomic_exchange(a.done_epoch + bb, e + 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) == e + 1u) {
     __hip_atomic_fetch_add(a.sched_ctr + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
-  __hip_atomic_store(a.done_epoch + bb, e + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_fetch_add(a.sched_ctr + 0, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  const unsigned n = __hip_atomic_load(a.sched + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+  const unsigned n = __hip_atomic_fetch_add(a.sched + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
   if ((long long)n >= a.nbatches) {  // every batch of epoch e applied: next epoch
     __hip_atomic_store(a.sched + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(a.sched, e + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  } else {
-    __hip_atomic_store(a.sched + 1, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+// The admission decision for the gradient of microbatch *bid_out (one thread).  Lock-free: read the
+// version, check the staleness bound, CAS version -> version + 1; a CAS lost to another rank's admission
+// re-reads and re-checks.  Records vpulled (the version the refreshed local weights correspond to), the
+// counters and the microbatch completion.  Returns the decision code.
+__device__ inline unsigned ps_admit(const PSArgs& a) {
+  const long long bid = *a.bid_out;
+  if (a.done_epoch != nullptr && bid < 0) {  // dataset finished: a no-op step
+    a.stats[6] += 1;
+    return kPSFinished;
+  }
+  const unsigned long long t0 = wall_clock64();
+  const unsigned vp = *a.vpulled;
+  unsigned v = __hip_atomic_load(a.ver, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (;;) {
+    const unsigned stale = v - vp;
+    if (a.max_stale >= 0 && (int)stale > a.max_stale) {
+      a.stats[1] += 1;
+      *a.vpulled = v;  // the refresh reads the current values
+      return kPSReject;
+    }
+    unsigned expected = v;
+    if (__hip_atomic_compare_exchange_strong(a.ver, &expected, v + 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM)) {
+      a.stats[0] += 1;
+      a.stats[2] += stale;
+      if (stale > a.stats[3]) a.stats[3] = stale;
+      *a.vpulled = v + 1u;
+      if (a.done_epoch != nullptr) complete_microbatch(a, bid);
+      return kPSAccept;
+    }
+    v = expected;  // another rank admitted in between: re-check against its version
+    a.stats[4] += 1;
+    if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) {
+      atomicOr(a.stats + 5, 4ull);
+      if (a.herr) __hip_atomic_store(a.herr, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return kPSFailed;
+    }
+  }
+}
+
+// The shard bases into LDS (indexing the by-value kernel argument with a run-time shard number would
+// copy the whole argument block to scratch per thread).  Every thread of the workgroup calls it.
+__device__ __forceinline__ void ps_stage_shards(const PSArgs& a, float** tab) {
+  if (threadIdx.x < kP2PMaxRanks) {
+    float* v = nullptr;
+#pragma unroll
+    for (int k = 0; k < kP2PMaxRanks; ++k)
+      if ((int)threadIdx.x == k) v = a.shard[k];
+    tab[threadIdx.x] = v;
+  }
+  __syncthreads();
+}
+
+// Address of master element i (tab: the shard bases, staged in LDS by the caller)
+__device__ __forceinline__ float* ps_elem(float* const* tab, int shift, long long i) {
+  return tab[i >> shift] + (i & ((1LL << shift) - 1));
+}
+
+// w += d for N elements (p[e] null: skip), returning the new values.  Exclusive writer: plain loads, then
+// stores.  Shared: every element's load in flight, then every CAS in flight, re-trying the ones another
+// rank's add beat (bounded by the timeout; a timed-out element keeps its loaded value).
+template <int N>
+__device__ __forceinline__ void ps_add(float* const (&p)[N], const float (&d)[N], float (&out)[N], bool excl,
+                                       const PSArgs& a) {
+  unsigned cur[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e)
+    cur[e] = p[e] ? __hip_atomic_load(reinterpret_cast<unsigned*>(p[e]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+  if (excl) {
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+#pragma clang fp contract(off)
+      out[e] = __uint_as_float(cur[e]) + d[e];
+      if (p[e]) __hip_atomic_store(reinterpret_cast<unsigned*>(p[e]), __float_as_uint(out[e]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return;
+  }
+  unsigned pending = 0;
+#pragma unroll
+  for (int e = 0; e < N; ++e)
+    if (p[e]) pending |= 1u << e;
+  const unsigned long long t0 = wall_clock64();
+  while (pending) {
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+      if (!((pending >> e) & 1u)) continue;
+      float nw;
+      {
+#pragma clang fp contract(off)
+        nw = __uint_as_float(cur[e]) + d[e];
+      }
+      unsigned expected = cur[e];
+      if (__hip_atomic_compare_exchange_strong(reinterpret_cast<unsigned*>(p[e]), &expected, __float_as_uint(nw),
+                                               __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+        out[e] = nw;
+        pending &= ~(1u << e);
+      } else {
+        cur[e] = expected;
+      }
+    }
+    if (pending && wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) {
+      atomicOr(a.stats + 5, 16ull);
+      if (a.herr) __hip_atomic_store(a.herr, 16u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+      for (int e = 0; e < N; ++e)
+        if ((pending >> e) & 1u) out[e] = __uint_as_float(cur[e]);
+      break;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < N; ++e)
+    if (!p[e]) out[e] = 0.f;
 }
 
 // Stage microbatch `bid`'s example indices (perm row) into the static index buffer: 16-byte copies, all

@@ -68,6 +68,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--save-dir", default=None)
     p.add_argument("--resume", action="store_true")
     p.add_argument("--steps", type=int, default=0, help="stop after this many steps (0 = full epochs)")
+    p.add_argument("--min-updates", type=int, default=0,
+                   help="FedSGD count barrier on the device: K microbatches of --batch rows per version, split over "
+                        "the ranks (reference minUpdatesPerVersion; 0 = one per rank)")
 
     p = sub.add_parser("async", help="asynchronous parameter server, bounded staleness")
     common(p)
@@ -221,7 +224,7 @@ def run_sync(args) -> dict:
     from .models.zoo import build_model
     from .parallel.comm import init_distributed, shutdown
     from .data.dataset import DistriDataset
-    from .parallel.data_parallel import DataParallelTrainer
+    from .parallel.data_parallel import DataParallelTrainer, fedsgd_rows
 
     env = init_distributed(device=_device(args), watchdog=True)
     rank, world, dev = env.rank, env.world_size, env.device
@@ -241,7 +244,8 @@ def run_sync(args) -> dict:
             start_step = int(rec.get("step", 0))
             log.log(f"resumed from version {store.last()} at step {start_step} (after epoch {rec.get('epoch')})")
     graph = args.graph or "full"
-    tr = DataParallelTrainer(net, lr=args.lr, momentum=args.momentum, graph=graph if dev.type == "cuda" else "none")
+    tr = DataParallelTrainer(net, lr=args.lr, momentum=args.momentum, graph=graph if dev.type == "cuda" else "none",
+                             min_updates_per_version=args.min_updates or None)
     scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
     # the DistriDataset's dispenser (epochs, per-epoch shuffle, FCFS order, completion) becomes the device
     # index stream: batch k of the schedule goes to rank k % world, and every step's update launch stages
@@ -250,7 +254,11 @@ def run_sync(args) -> dict:
     # uninterrupted job would have.
     ds = DistriDataset(x, y, {"batchSize": B, "epochs": args.epochs}, shuffle=True, seed=args.seed)
     tr.bind_dataset(ds.x, ds.y, B, scale=scale)
-    rows, row_epoch = ds.index_stream(rank, world, device=dev, with_epochs=True)
+    if tr.min_updates is not None:  # K microbatches of the one FCFS stream per version (count barrier)
+        g_rows, g_epochs = ds.index_stream(0, 1, device=dev, with_epochs=True)
+        rows, row_epoch = fedsgd_rows(g_rows, tr.min_updates, rank, world, g_epochs)
+    else:
+        rows, row_epoch = ds.index_stream(rank, world, device=dev, with_epochs=True)
     total = rows.shape[0]
     start = min(start_step, total)
     if start < total:
@@ -259,23 +267,34 @@ def run_sync(args) -> dict:
     tr.on_upload(lambda st: log.metric(event="upload", **st))
     tr.on_new_version(lambda old, new: log.log(f"updated model: {old} -> {new}"))
     step = start
+    # without per-step fault hooks the steps between two epoch boundaries run as multi-step graph replays
+    # (no per-step host work in the loop); with faults injected, one step at a time
+    chunked = not (faults.kill or faults.delay)
+    if chunked:
+        tr.prepare_run(DataParallelTrainer.MAX_STEPS_PER_GRAPH)
     t0 = time.perf_counter()
     seen = 0
     last_loss = float("nan")
     st = None
-    for i in range(start, total):
-        if args.steps and step >= args.steps:
-            break
-        faults.step(step)
-        st = tr.step()
-        step += 1
-        seen += B * world
-        epoch_end = i + 1 == total or row_epoch[i + 1] != row_epoch[i]
-        if not epoch_end and not (args.steps and step >= args.steps):
-            continue
-        epoch = row_epoch[i]
+    limit = min(total, args.steps) if args.steps else total
+    i = start
+    while i < limit:
+        j = i + 1  # end (exclusive) of this chunk: the epoch's last step or the step limit
+        while j < limit and row_epoch[j] == row_epoch[i]:
+            j += 1
+        if chunked:
+            st = tr.run(j - i)
+        else:
+            for k in range(i, j):
+                faults.step(k)
+                st = tr.step()
+        seen += (j - i) * tr.images_per_step
+        step = j
+        epoch_end = j == total or row_epoch[j] != row_epoch[j - 1]
+        epoch = row_epoch[j - 1]
+        i = j
         tr.flush_callbacks()
-        last_loss = float(st[0]) / B
+        last_loss = float(st[0]) / tr.B
         el = time.perf_counter() - t0
         log.metric(event="epoch", epoch=epoch, step=step, loss=last_loss, images_per_s=seen / el)
         log.log(f"epoch {epoch}: loss {last_loss:.4f}, {seen / el:.0f} images/s")

@@ -347,12 +347,20 @@ class Net:
             if grad_ready is not None:
                 grad_ready(i)
 
+    # Scale of the per-example loss gradients: None = 1 / rows of the step (the mean loss).  A FedSGD step
+    # over several microbatches per rank (DataParallelTrainer min_updates_per_version) sets 1 / microbatch
+    # size, so the step's gradient is the SUM of its microbatches' mean-loss gradients.
+    loss_scale: Optional[float] = None
+
+    def _loss_scale(self, rows: int) -> float:
+        return 1.0 / rows if self.loss_scale is None else float(self.loss_scale)
+
     def loss_and_grad(self, logits, labels, grad_scale: Optional[float] = None):
         """The training loss on the logits: softmax cross-entropy (a final softmax or linear output) or,
         for a model that ends in sigmoid, sigmoid cross-entropy against the one-hot labels."""
         B = logits.shape[0]
         self.stats.zero_()
-        gs = 1.0 / B if grad_scale is None else grad_scale
+        gs = self._loss_scale(B) if grad_scale is None else grad_scale
         if self.final_act == "sigmoid":
             ops.sigmoid_ce(logits, labels, self.dlogits, self.stats, gs)
         else:
@@ -436,7 +444,7 @@ class Net:
                         cgrads, [st.grad_matrix(f"{d.name}/kernel") for d in dense],
                         [st.gradient(f"{d.name}/bias") for d in dense], [self.head_xT] + self.head_hT[:2],
                         self.head_dzT, self.lenet_conv_part, self.lenet_dense_part, self.lenet_loss_part, self.stats,
-                        1.0 / B, frag=st.lenet_frag[0] if st.lenet_frag is not None else None,
+                        self._loss_scale(B), frag=st.lenet_frag[0] if st.lenet_frag is not None else None,
                         prep=st.lenet_frag is None or st.lenet_state == "stale", snap=st.lenet_snap,
                         conv_mom=st.lenet_conv_momentum(), sgd=sgd if st.lenet_frag is not None else None)
         if st.lenet_frag is not None:
@@ -497,7 +505,7 @@ class Net:
             hT=self.head_hT, dzT=self.head_dzT, K=[l.in_features for l in head], N=[l.units for l in head],
             x=h, x_relu=first.in_relu, dx_scale=first.dx_scale, xT=self.head_xT,
             dx=first.dx if first.need_dx else None,
-            logits=head[-1].out, labels=lab, idx=idx, grad_scale=1.0 / x.shape[0],
+            logits=head[-1].out, labels=lab, idx=idx, grad_scale=self._loss_scale(x.shape[0]),
             loss_part=self.head_loss_part, stats=self.stats)
         head_ids = range(len(self.exec_layers) - 1, self.head_start - 1, -1)
         if not self.concurrent_backward:

@@ -272,7 +272,7 @@ class ParamStore:
         if self.compute_bf16:
             src, cur, dst = index_stream if index_stream is not None else (None, None, None)
             kw = self._frag_kw(True)
-            if run_stats is not None and src is not None:
+            if run_stats is not None:
                 kw.update(step_stats=run_stats[0], run_stats=run_stats[1])
             native.require().sgd_multi(self._descs, self._ndesc, self._sgd_blocks, self.master, self.grad,
                                        self.momentum, self.wbf, self.hyper, True, src, cur, dst,
@@ -283,9 +283,9 @@ class ParamStore:
             nxt = (int(cur[0]) + 1) % src.shape[0]
             dst.copy_(src[nxt])
             cur.fill_(nxt)
-            if run_stats is not None:
-                run_stats[1][:2] += run_stats[0][:2]
-                run_stats[1][2] += 1.0
+        if run_stats is not None:
+            run_stats[1][:2] += run_stats[0][:2]
+            run_stats[1][2] += 1.0
         lr, mom, wd, gs, nest = self._hyper_host
         if not hasattr(self, "_valid"):
             self._valid = torch.zeros(self.total, dtype=torch.bool, device=self.device)

@@ -8,22 +8,28 @@ batch, computes a gradient and uploads it
 (/root/reference/README.md:27) is the intended bound and is enforced here.
 
 This is the throughput path.  The message-level roles (``parallel/server.py``/``worker.py``) keep
-the reference's protocol and callbacks.  On one MI355X node the server state is a single IPC-exported
-buffer in the server rank's HBM: a seqlock version word, the FCFS microbatch counter and the fp32
-master weights.  Every rank maps it over xGMI (csrc/async_ps.hip).  A worker step is a bare hipGraph
-replay of device stages, with no host round trip.
+the reference's protocol and callbacks.  On one MI355X node the server is not a process: its state is
+device memory that every rank maps over xGMI (csrc/async_ps.hip, csrc/ps_device.h).  The server rank
+holds the control buffer (the version word = count of admitted gradients, the FCFS microbatch cursor,
+the completion arrays); the fp32 master is SHARDED by contiguous parameter range over all ranks' HBM, one
+shard per rank.  A gradient is admitted by one lock-free CAS on the version word (the staleness bound is
+its check) and applied element by element to the owning shards with CAS adds, so the applies of
+different ranks run in parallel: no rank ever holds a lock that another waits for.  A worker step is a
+bare hipGraph replay of device stages, with no host round trip.
 
 Fused LeNet-5 (the headline model): TWO launches per step, the same shape as a synchronous step.
   1. the whole-network train kernel (forward, loss, backward of the claimed microbatch);
-  2. the reduce kernel in parameter-server mode (csrc/lenet_fused.hip): it reduces the gradient, takes
-     the writer lock, rejects it if ``version_now - version_pulled > max_staleness`` or applies
-     ``w -= lr * g`` to the shared master, refreshes the local master / bf16 copies / conv fragments
-     from the version it just wrote (or the current one), publishes ``version + 1``, and claims and
-     stages the next microbatch.  A one-time prologue (pull + refresh) precedes the first step.
-Other models: ``ps_fetch_pull`` (claim + snapshot), bf16 refresh, the model's kernels, ``ps_apply``.
+  2. the reduce kernel in parameter-server mode (csrc/lenet_fused.hip): its staging workgroup admits the
+     gradient as the launch starts (``version_now - version_pulled <= max_staleness``), completes the
+     microbatch and claims / stages the next one; the slot owners reduce the gradient, add
+     ``-lr * g`` to their elements of the sharded master (rejected: read the current values) and refresh
+     the local master / bf16 copies / conv fragments from the result.  A one-time prologue (pull +
+     refresh) precedes the first step.
+Other models: ``ps_fetch_pull`` (claim + copy out of the shards), bf16 refresh, the model's kernels,
+``ps_apply`` (admit + sharded adds).
 
-Ranks never wait for each other except for the short writer lock.  A slow rank only makes its own
-gradients staler, which the bound then rejects.
+Ranks never wait for each other.  A slow rank only makes its own gradients staler, which the bound
+then rejects.  The admission CAS is the one serialisation point (one remote atomic per step per rank).
 """
 from __future__ import annotations
 
@@ -52,32 +58,47 @@ class AsyncPSTrainer(DataParallelTrainer):
         self.server_rank = server_rank
         # collective setup: every rank learns whether every other rank managed its part (no rank is left
         # waiting in a barrier that a failed peer never reaches)
-        err, handle = None, b""
+        err, handle, shard = None, b"", b""
         try:
-            self.ps = native.require().PSComm(self.rank, server_rank, net.store.total, timeout_s)
+            self.ps = native.require().PSComm(self.rank, self.world, server_rank, net.store.total, timeout_s)
             if self.rank == server_rank:
                 handle = self.ps.handle()
+            shard = self.ps.shard_handle()
         except Exception as e:
             err = e
         self._agree(err, "allocation/export")
-        objs = [handle]
+        ctrl = [handle]
+        shards = [shard] * self.world
         if self.world > 1:
-            dist.broadcast_object_list(objs, src=server_rank, group=group)
+            dist.broadcast_object_list(ctrl, src=server_rank, group=group)
+            dist.all_gather_object(shards, shard, group=group)
         try:
-            self.ps.open(objs[0])
-            if self.rank == server_rank:
-                self.ps.init_master(net.store.master)
+            self.ps.open(ctrl[0], shards)
+            self.ps.init_master(net.store.master)  # every rank seeds its own shard (identical weights)
+            self.ps.set_lr_source(net.store.hyper)  # applies read the device lr: set_lr holds after capture
         except Exception as e:
             err = e
         self._agree(err, "IPC open")
+        # the element add every apply uses, on every shard from every rank at once, against exact sums
+        ok = True
+        try:
+            self.ps.selftest_add()
+        except Exception as e:
+            err, ok = e, False
+        self._agree(err, "shard self-test")
+        if not self.ps.selftest_check():
+            err = RuntimeError("shard add self-test mismatch")
+        self._agree(err, "shard self-test check")
         self._perm = None
         # fused LeNet-5: the reduce launch is the parameter server's apply (2 launches per step)
         import os
 
         self.fused_ps = (bool(getattr(net, "lenet_fused", False)) and net.store.lenet_frag is not None
                          and diag_on("async_fused"))
+        # a warm-up step would claim a microbatch and apply a real gradient to the shared master: the
+        # capture warms up with a compute-only step instead (_capture)
+        self.capture_warmup = 0
         if self.fused_ps:
-            self.capture_warmup = 0  # a warm-up step would apply real gradients to the shared master
             # ranks that time-share one GPU: fewer protocol workgroups per rank (each owning several
             # slots), so every rank's workgroups waiting for its lock decision fit on the chip beside the
             # lock holder's (one rank per GPU: one workgroup per slot, all resident)
@@ -151,6 +172,17 @@ class AsyncPSTrainer(DataParallelTrainer):
         self._prime()
         super().prepare_run(n)
 
+    def _capture(self):
+        if not self.fused_ps:
+            # compute-only warm-up (allocator, code objects) with no claim and no apply; its effect on the
+            # local engine state is undone
+            snap = self.net.snapshot_state()
+            DataParallelTrainer._gather(self)
+            self.net.compute_gradients(self.xb, self.yb)
+            torch.cuda.synchronize(self.net.device)
+            self.net.restore_state(snap)
+        super()._capture()
+
     def _capture_with_fallback(self):
         try:
             self._capture()
@@ -194,10 +226,10 @@ class AsyncPSTrainer(DataParallelTrainer):
 
     # ------------------------------------------------------------------ state
     def ps_stats(self) -> dict:
-        acc, rej, ssum, smax, torn, err, version, cursor, noops = self.ps.stats()
+        acc, rej, ssum, smax, retries, err, version, cursor, noops = self.ps.stats()
         epoch, in_epoch, completed, redisp, skipped, dups, fin = self.ps.schedule_stats()
         return {"accepted": acc, "rejected": rej, "mean_staleness": ssum / acc if acc else 0.0,
-                "max_staleness": smax, "torn_retries": torn, "error": err, "version": version,
+                "max_staleness": smax, "admit_retries": retries, "error": err, "version": version,
                 "cursor": cursor, "noop_steps": noops, "epoch": epoch, "completed_in_epoch": in_epoch,
                 "completed": completed, "redispatched": redisp, "skipped": skipped, "duplicates": dups,
                 "finished": bool(fin)}
@@ -216,7 +248,7 @@ class AsyncPSTrainer(DataParallelTrainer):
             raise RuntimeError(f"async PS: device wait timed out (error bits {err:#x})")
 
     def pull_master(self, dst: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Copy the shared master into ``dst`` (default: this rank's store, compute copies refreshed)."""
+        """Gather the sharded master into ``dst`` (default: this rank's store, compute copies refreshed)."""
         if dst is None:
             self.ps.copy_master(self.net.store.master)
             self.net.store.refresh_compute()

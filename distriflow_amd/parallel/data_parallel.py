@@ -33,11 +33,24 @@ from ..diagnostics import on as _diag_on
 class DataParallelTrainer:
     def __init__(self, net, lr: float = 0.001, momentum: float = 0.0, weight_decay: float = 0.0,
                  group=None, bucket_mb: Optional[float] = None, overlap: bool = True, graph: str = "full",
-                 broadcast_init: bool = True, allreduce: str = "auto", p2p_max_mb: float = 4.0):
+                 broadcast_init: bool = True, allreduce: str = "auto", p2p_max_mb: float = 4.0,
+                 min_updates_per_version: Optional[int] = None):
         self.net = net
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # FedSGD count barrier on the device (reference FederatedServer: a version is the mean of
+        # minUpdatesPerVersion microbatch gradients of the current version, federated_server.ts:73-90,
+        # default 20, utils.ts:188-191).  K microbatches per version, split over the ranks as evenly as they
+        # go (rank r takes K // W + (r < K % W) of them, as one step over their concatenated rows); each
+        # microbatch's gradient is its mean loss's, the step sums them, the exchange sums over the ranks and
+        # the update scales by 1 / K.  Every gradient of a version is computed on that version, so the
+        # reference's stale-upload drop never has anything to drop.  None: one microbatch per rank (K = W).
+        self.min_updates = None if min_updates_per_version in (None, 0) else int(min_updates_per_version)
+        if self.min_updates is not None and self.min_updates < self.world:
+            raise ValueError(f"min_updates_per_version must be >= world ({self.world}), got {self.min_updates}")
+        self.micro_per_rank = ([self.min_updates // self.world + (1 if r < self.min_updates % self.world else 0)
+                                for r in range(self.world)] if self.min_updates is not None else [1] * self.world)
         self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
         self.overlap = overlap
         self.graph_mode = graph if net.is_gpu else "none"
@@ -82,7 +95,12 @@ class DataParallelTrainer:
         if broadcast_init and self.world > 1:
             dist.broadcast(net.store.master, src=0, group=group)
             net.store.refresh_compute()
-        net.store.set_hyper(lr, momentum, weight_decay, grad_scale=1.0 / self.world)
+        net.store.set_hyper(lr, momentum, weight_decay, grad_scale=self._grad_scale())
+
+    def _grad_scale(self) -> float:
+        """The update's gradient scale: the mean over the ranks' gradients (1 / W), or over the K
+        microbatches of a FedSGD version (1 / K)."""
+        return 1.0 / (self.min_updates if self.min_updates is not None else self.world)
 
     # ------------------------------------------------------------------ buckets
     def _build_buckets(self):
@@ -219,14 +237,102 @@ class DataParallelTrainer:
 
     def _fused_step_ok(self) -> bool:
         """The fused LeNet-5 step (train + reduce/exchange/update: two launches) is usable: single rank,
-        or every rank on the one-shot p2p path (its communicator carries the LL exchange slots)."""
+        or every rank on the one-shot p2p path (its communicator carries the LL exchange slots) and the
+        exchange passed its real-kernel self-test (:meth:`_verify_fused_exchange`)."""
         if not (self.fused_update and getattr(self.net, "lenet_fused", False)
                 and self.net.store.lenet_frag is not None):
             return False
         if self.world == 1 or not self._step_all_reduces:
             return True  # no exchange inside the step (single rank, FedAvg local steps)
         return (self.p2p is not None and getattr(self.p2p.comm, "ll_slots", 0) >= 256
-                and self.net.store.total * 4 <= self.p2p_limit)
+                and self.net.store.total * 4 <= self.p2p_limit and self.fused_selftest.get("ok", True))
+
+    # result of the fused exchange self-test ({} = not run yet; "ok": False disables the fused step)
+    fused_selftest: dict = {}
+
+    def _verify_fused_exchange(self):
+        """Real-kernel self-test of the multi-rank fused step, run once (collectively) before the first
+        step: the production reduce kernel with the production grid (one workgroup per job when every rank
+        has its own GPU) and the in-kernel exchange, on rank-distinct batches.  Its summed gradient must equal,
+        bit for bit, the rank-order sum of the ranks' local gradients (the same train / reduce kernels
+        without the exchange, gathered over the process group), and the updated weights must be
+        bit-identical on every rank.  On a mismatch or a peer timeout every rank falls back to the
+        unfused step (compute + one-shot all-reduce or RCCL + SGD).  The engine state is restored after.
+        Reference semantics held here: the synchronous server's mean of the K uploaded gradients
+        (/root/reference/src/server/federated_server.ts:92-117)."""
+        if self.fused_selftest or self.world == 1 or not self._step_all_reduces:
+            return
+        if not (self.fused_update and getattr(self.net, "lenet_fused", False) and self.net.store.lenet_frag is not None
+                and self.p2p is not None and getattr(self.p2p.comm, "ll_slots", 0) >= 256
+                and self.net.store.total * 4 <= self.p2p_limit):
+            return
+        net, dev = self.net, self.net.device
+        t0 = time.perf_counter()
+        res = {"ok": True, "why": "", "exch_blocks": int(getattr(net, "lenet_exch_blocks", 0))}
+        snap = net.snapshot_state()
+        idx0 = self.idx.clone()
+        cursor = self._index_stream[1].clone() if self._index_stream is not None else None
+        rs0 = self.run_stats.clone()
+        comm = self.p2p.comm
+        try:
+            n_rows = self.data.shape[0]
+            self.idx.copy_((torch.arange(self.B, device=dev, dtype=torch.int64) * 7919 + 104729 * self.rank + 17)
+                           % n_rows)
+            # local gradients through the same kernels without the exchange
+            self._gather()
+            net.compute_gradients(self.xb, self.yb)
+            torch.cuda.synchronize(dev)
+            g_local = net.store.grad.clone()
+            gloo = dist.get_backend(self.group) == "gloo"
+            parts = [torch.empty_like(g_local, device="cpu" if gloo else dev) for _ in range(self.world)]
+            dist.all_gather(parts, g_local.cpu() if gloo else g_local, group=self.group)
+            ref = parts[0].cpu().clone()
+            for r in range(1, self.world):
+                ref += parts[r].cpu()  # rank order, fp32: the in-kernel exchange's summation order
+            net.restore_state(snap)
+            comm.set_timeout(5.0)
+            self._gather()
+            net.compute_gradients_and_update(self.xb, self.yb, None, ll=comm)
+            torch.cuda.synchronize(dev)
+            if comm.error() != 0:
+                res.update(ok=False, why="peer timeout in the fused exchange self-test")
+            elif not torch.equal(net.store.grad.cpu(), ref):
+                bad = int((net.store.grad.cpu() != ref).sum())
+                res.update(ok=False, why=f"fused exchange self-test: {bad} gradient elements differ from the "
+                                         f"rank-order sum")
+            else:
+                w = net.store.master
+                lo, hi = w.clone(), w.clone()
+                if gloo:
+                    lo, hi = lo.cpu(), hi.cpu()
+                dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
+                dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
+                if not torch.equal(lo, hi):
+                    res.update(ok=False, why="fused exchange self-test: replicas differ after the update")
+        except Exception as e:  # noqa: BLE001 (any failure -> the unfused path)
+            res.update(ok=False, why=f"fused exchange self-test raised {e!r:.200}")
+        finally:
+            try:
+                comm.set_timeout(30.0)
+            except Exception:
+                pass
+            torch.cuda.synchronize(dev)
+            net.restore_state(snap)
+            self.idx.copy_(idx0)
+            if cursor is not None:
+                self._index_stream[1].copy_(cursor)
+            self.run_stats.copy_(rs0)
+        from .p2p import _agree
+
+        ok = _agree(res["ok"], self.group, dev)
+        if res["ok"] and not ok:
+            res.update(ok=False, why="a peer's fused exchange self-test failed")
+        res["ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+        self.fused_selftest = res
+        if not ok:
+            self.p2p_reason = res["why"]
+            self._graph = None
+            self._multi, self._multi_u = None, 0
 
     @property
     def step_launches(self) -> str:
@@ -256,7 +362,7 @@ class DataParallelTrainer:
 
     def set_lr(self, lr: float):
         self.lr = lr
-        self.net.store.set_hyper(lr, self.momentum, self.weight_decay, grad_scale=1.0 / self.world)
+        self.net.store.set_hyper(lr, self.momentum, self.weight_decay, grad_scale=self._grad_scale())
 
     def train_step(self, x: torch.Tensor, y: torch.Tensor):
         """Eager step on an explicit batch; returns device stats [loss_sum, correct]."""
@@ -265,8 +371,14 @@ class DataParallelTrainer:
 
     # ------------------------------------------------------------------ graph-captured step over an HBM dataset
     def bind_dataset(self, data: torch.Tensor, labels: torch.Tensor, batch_size: int, scale: float = 1.0):
-        """Attach an HBM-resident dataset (uint8/bf16 [N, ...], int32 labels); steps then take index batches."""
+        """Attach an HBM-resident dataset (uint8/bf16 [N, ...], int32 labels); steps then take index batches.
+        ``batch_size``: rows per step per rank; with ``min_updates_per_version`` it is the MICROBATCH size
+        and a step takes ``micro_per_rank[rank]`` microbatches (their rows concatenated)."""
         self.data, self.labels, self.scale = data, labels, scale
+        self.micro_B = batch_size
+        if self.min_updates is not None:
+            self.net.loss_scale = 1.0 / batch_size  # the step gradient = sum of its microbatches' means
+            batch_size *= self.micro_per_rank[self.rank]
         self.B = batch_size
         net = self.net
         net.bind(batch_size)
@@ -361,7 +473,7 @@ class DataParallelTrainer:
                     self._gather()
                     self.stats = self.net.compute_gradients(self.xb, self.yb)
                 with torch.cuda.graph(g2, stream=cs):
-                    self.net.store.sgd_step(self._index_stream)
+                    self.net.store.sgd_step(self._index_stream, run_stats=(self.stats, self.run_stats))
                 self._graph = (g, g2)
         except Exception:
             # a collective that cannot be captured (e.g. gloo on device tensors) leaves the capture open
@@ -392,7 +504,11 @@ class DataParallelTrainer:
             if cb not in self.preprocess_callbacks:
                 self.add_preprocess_callback(cb)
         epochs_left = max(1, ds.epochs - ds.epoch)
-        stream = ds.index_stream(rank, world, device=self.net.device, allow_preprocess=True)
+        if self.min_updates is not None:  # K microbatches of the one FCFS stream per version
+            stream = fedsgd_rows(ds.index_stream(0, 1, device=self.net.device, allow_preprocess=True),
+                                 self.min_updates, rank, world)
+        else:
+            stream = ds.index_stream(rank, world, device=self.net.device, allow_preprocess=True)
         self.bind_index_stream(stream)
         self.steps_per_epoch = max(1, stream.shape[0] // epochs_left)
         self.schedule_steps = int(stream.shape[0])
@@ -416,6 +532,7 @@ class DataParallelTrainer:
         """One training step on the next batch of the bound index stream."""
         if self._index_stream is None:
             raise RuntimeError("bind_index_stream() first")
+        self._verify_fused_exchange()
         self.steps += 1
         _beat(self.steps)
         if self.graph_mode == "none":
@@ -432,6 +549,7 @@ class DataParallelTrainer:
         """One training step on dataset rows ``idx`` (device int64 [B])."""
         if self._index_stream is not None:
             raise RuntimeError("an index stream is bound: use step()")
+        self._verify_fused_exchange()
         self.idx.copy_(idx, non_blocking=True)
         self.steps += 1
         if self.graph_mode == "none":
@@ -449,6 +567,7 @@ class DataParallelTrainer:
         The ranks agree on every attempt (MIN of a success flag, outside any capture): if capture
         fails on one rank only, all of them fall back together, so no rank replays a graph whose
         collectives / one-shot epochs its peers never issue."""
+        self._verify_fused_exchange()
         while True:
             ok = True
             try:
@@ -500,8 +619,15 @@ class DataParallelTrainer:
         this replay = cur - last)."""
         dl, dc, du = (cur[0][k] - last[0][k] for k in range(3))
         images = n * self.B
-        return {"version": v1, "steps": n, "images": images * self.world, "loss": dl / max(images, 1),
+        return {"version": v1, "steps": n, "images": n * self.images_per_step, "loss": dl / max(images, 1),
                 "accuracy": dc / max(images, 1), "updates": int(round(du)), "rank": self.rank, "world": self.world}
+
+    @property
+    def images_per_step(self) -> int:
+        """Examples in one step over all ranks (one version)."""
+        if self.min_updates is not None:
+            return self.min_updates * self.micro_B
+        return self.B * self.world
 
     def _after_replay(self, nsteps: int):
         """Queue an asynchronous read-back of the device counters after a replay of ``nsteps`` steps (a
@@ -647,6 +773,25 @@ def shared_gpu_exch_blocks(world: int) -> int:
     ndev = max(1, torch.cuda.device_count())
     share = -(-world // ndev) if ndev < world else 1
     return 0 if share == 1 else max(64, (512 // share) // 8 * 8)
+
+
+def fedsgd_rows(global_rows: torch.Tensor, k: int, rank: int, world: int, epochs: Optional[list] = None):
+    """Per-version rows of one rank for a FedSGD count barrier of ``k`` microbatches per version:
+    ``global_rows`` [nb][B] is the one FCFS microbatch stream (every rank holds the same); version v takes
+    microbatches v*k .. v*k + k - 1, rank r the ``k // world + (r < k % world)`` of them after the lower
+    ranks' share, concatenated -> [nb // k][m_r * B].  ``epochs`` (per microbatch) -> also the epoch of
+    each version's first microbatch."""
+    counts = [k // world + (1 if r < k % world else 0) for r in range(world)]
+    off, m = sum(counts[:rank]), counts[rank]
+    nv = global_rows.shape[0] // k
+    if nv == 0:
+        raise ValueError(f"the stream has {global_rows.shape[0]} microbatches, fewer than one version of {k}")
+    ids = (torch.arange(nv, device=global_rows.device)[:, None] * k + off
+           + torch.arange(m, device=global_rows.device)[None, :])
+    rows = global_rows[ids.reshape(-1)].reshape(nv, m * global_rows.shape[1]).contiguous()
+    if epochs is None:
+        return rows
+    return rows, [epochs[v * k] for v in range(nv)]
 
 
 def epoch_permutations(n: int, batch: int, steps: int, device, seed: int = 0):

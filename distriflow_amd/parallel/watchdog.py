@@ -174,7 +174,10 @@ class PeerWatchdog:
                     v = 0
                 if v:
                     return self._fail(f"device error word {name} = {v:#x} (peer timed out on the device)")
-            if self.stall_after_s is not None and self._step >= 0 and now - self._step_t > self.stall_after_s:
+            # a rank that finished (waiting for slow peers in the final barrier, evaluating, checkpointing)
+            # makes no training progress by design: only the peers' liveness is watched then
+            if (self.stall_after_s is not None and not self._done_marked and self._step >= 0
+                    and now - self._step_t > self.stall_after_s):
                 return self._fail(f"no training progress for {now - self._step_t:.0f} s (step {self._step})")
             try:
                 self._store.add(self._key("hb", self.rank), 1)

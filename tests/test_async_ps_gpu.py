@@ -1,11 +1,12 @@
 """Device-resident bounded-staleness parameter server (csrc/async_ps.hip, parallel/async_ps.py) on MI355X.
 
-LeNet-5 takes the fused path: the reduce launch applies the gradient to the shared master under the
-writer lock, refreshes the local copies and claims the next microbatch (csrc/lenet_fused.hip PS mode);
-the MLP keeps the pull / compute / apply launches.  Multi-rank cases use a GPU per rank + RCCL when the
-box has them (tests/mp_util.py), else processes sharing cuda:0 over gloo: the IPC mapping, remote
-atomics, seqlock snapshots and the writer lock behave as on an 8-GPU node, only the loads travel
-through local HBM instead of xGMI."""
+The fp32 master is sharded over the ranks' HBM; a gradient is admitted by one lock-free CAS on the
+version word and applied with per-element adds to the owning shards (csrc/ps_device.h).  LeNet-5 takes
+the fused path: the reduce launch admits, applies, refreshes the local copies and claims the next
+microbatch (csrc/lenet_fused.hip PS mode); the MLP keeps the pull / compute / apply launches.
+Multi-rank cases use a GPU per rank + RCCL when the box has them (tests/mp_util.py), else processes
+sharing cuda:0 over gloo: the IPC mappings, remote atomics and CAS adds behave as on an 8-GPU node,
+only the loads travel through local HBM instead of xGMI."""
 import os
 import tempfile
 
@@ -180,12 +181,14 @@ def _epoch_worker(rank, world, port, out_dir, epochs, nb):
     dist.destroy_process_group()
 
 
-@pytest.mark.timeout(240)
-def test_async_ps_every_batch_applied_once_per_epoch():
-    """4 workers at maximumStaleness 0 (many rejections): every batch id of every epoch ends with one
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [4, 8])
+def test_async_ps_every_batch_applied_once_per_epoch(world):
+    """4 / 8 workers at maximumStaleness 0 (many rejections): every batch id of every epoch ends with one
     admitted gradient, rejected batches are re-dispatched, and the run ends after the configured
-    epochs (reference DistributedDataset, /root/reference/src/server/dataset.ts:47-67)."""
-    world, epochs, nb = 4, 2, 16
+    epochs (reference DistributedDataset, /root/reference/src/server/dataset.ts:47-67).  The lock-free
+    completion accounting (csrc/ps_device.h complete_microbatch) is what 8 concurrent admitters race on."""
+    epochs, nb = 2, 16
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_epoch_worker, args=(world, _port(), d, epochs, nb), nprocs=world, join=True)
         r = [torch.load(os.path.join(d, f"r{i}.pt"), weights_only=True) for i in range(world)]
@@ -200,3 +203,42 @@ def test_async_ps_every_batch_applied_once_per_epoch():
     # round again (the re-dispatch path is exercised, not optional)
     assert rej > 0 and s["redispatched"] > 0
     assert all(x["steps"] < 20 * nb * epochs for x in r)
+
+
+def test_async_ps_master_is_sharded_and_set_lr_holds_after_capture():
+    """The master lives in power-of-two shards (one per rank; one rank: one shard covering it all), and
+    the fused PS apply reads the device learning rate: set_lr(0) after the graph capture freezes the
+    master on later replays (the rate was a frozen kernel argument)."""
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.async_ps import AsyncPSTrainer
+    from distriflow_amd.parallel.data_parallel import epoch_permutations
+
+    dev = torch.device("cuda", 0)
+    data, labels = synthetic_mnist(4096, seed=3, device=dev)
+    net = build_model("lenet5", device=dev, seed=0)
+    tr = AsyncPSTrainer(net, lr=0.05, max_staleness=0, graph="full")
+    n = net.store.total
+    assert tr.ps.shard_len >= n and tr.ps.nshards_used == 1
+    assert tr.ps.shard_len & (tr.ps.shard_len - 1) == 0
+    tr.bind_dataset(data, labels, 256, scale=1.0 / 255.0)
+    tr.bind_schedule(epoch_permutations(4096, 256, 16, dev, seed=1))
+    for _ in range(3):
+        tr.step()
+    torch.cuda.synchronize()
+    w3 = tr.pull_master(torch.empty_like(net.store.master)).clone()
+    torch.cuda.synchronize()
+    tr.set_lr(0.0)
+    for _ in range(3):
+        tr.step()
+    torch.cuda.synchronize()
+    w6 = tr.pull_master(torch.empty_like(net.store.master)).clone()
+    torch.cuda.synchronize()
+    assert tr.ps_stats()["accepted"] == 6
+    assert torch.equal(w3, w6), "set_lr(0) after capture still changed the master"
+    tr.set_lr(0.05)
+    tr.step()
+    torch.cuda.synchronize()
+    w7 = tr.pull_master(torch.empty_like(net.store.master)).clone()
+    torch.cuda.synchronize()
+    assert not torch.equal(w6, w7)

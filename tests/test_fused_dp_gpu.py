@@ -26,14 +26,14 @@ def _stream(world, B, steps):
     return torch.stack([torch.randperm(N_ROWS, generator=g)[: B * world] for _ in range(steps)])
 
 
-def _make(dev, B, rows, lr=0.05):
+def _make(dev, B, rows, lr=0.05, momentum=0.0):
     from distriflow_amd.data.synthetic import synthetic_mnist
     from distriflow_amd.models.zoo import build_model
     from distriflow_amd.parallel.data_parallel import DataParallelTrainer
 
     data, labels = synthetic_mnist(N_ROWS, seed=3, device=dev)
     net = build_model("lenet5", device=dev, seed=0)
-    tr = DataParallelTrainer(net, lr=lr, graph="full", allreduce="p2p")
+    tr = DataParallelTrainer(net, lr=lr, momentum=momentum, graph="full", allreduce="p2p")
     tr.bind_dataset(data, labels, B, scale=1.0 / 255.0)
     tr.bind_index_stream(rows.to(dev))
     return net, tr
@@ -59,21 +59,23 @@ def _multistep_worker(rank, world, port, out_dir, B):
     trB.check_comm()
     torch.save({"w0": w0, "wA": netA.store.master.cpu(), "wB": netB.store.master.cpu(),
                 "launches": trA.step_launches, "multi_u": trA._multi_u, "graph": trA.graph_mode,
-                "real": real_devices(world)},
+                "real": real_devices(world), "selftest": dict(trA.fused_selftest)},
                os.path.join(out_dir, f"m{rank}.pt"))
     finish()
 
 
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.timeout(420)
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_fused_exchange_multistep_graph_matches_single_steps(world):
     """prepare_run(4) + run(10) with the in-kernel exchange == 10 single-step replays, bit for bit, and
-    every rank holds the same weights (VERDICT r2 next-round #1)."""
+    every rank holds the same weights (VERDICT r2 next-round #1); world 8 is the driver's scaling-run rank
+    count (VERDICT r3 next-round #4).  The real-kernel exchange self-test passed on every rank."""
     B = 256 // world
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_multistep_worker, args=(world, free_port(), d, B), nprocs=world, join=True)
         r = [torch.load(os.path.join(d, f"m{i}.pt"), weights_only=True) for i in range(world)]
     for x in r:
+        assert x["selftest"].get("ok") is True, x["selftest"]
         assert x["launches"] == "train+reduce/exchange/update", x["launches"]
         assert x["graph"] == "full" and x["multi_u"] == 4
         assert torch.equal(x["wA"], x["wB"]), "multi-step graph diverged from single-step replays"
@@ -82,11 +84,11 @@ def test_fused_exchange_multistep_graph_matches_single_steps(world):
         assert torch.equal(x["wA"], r[0]["wA"]), "replicas diverged"
 
 
-def _union_worker(rank, world, port, out_dir, B, steps):
+def _union_worker(rank, world, port, out_dir, B, steps, momentum):
     dev = init_rank(rank, world, port)
     allrows = _stream(world, B, steps)
     mine = allrows[:, rank * B:(rank + 1) * B].contiguous()
-    net, tr = _make(dev, B, mine)
+    net, tr = _make(dev, B, mine, momentum=momentum)
     w0 = net.store.master.cpu()
     for _ in range(steps):
         tr.step()
@@ -97,18 +99,19 @@ def _union_worker(rank, world, port, out_dir, B, steps):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 4])
-def test_world_step_equals_single_rank_step_on_union_batch(world):
+@pytest.mark.parametrize("world,steps,momentum", [(2, 1, 0.0), (4, 1, 0.0), (2, 5, 0.9), (4, 5, 0.9)])
+def test_world_step_equals_single_rank_step_on_union_batch(world, steps, momentum):
     """W ranks x B rows == one rank on the W*B-row union batch (the mean gradient, fp32 master), up to
-    the fp32 summation order of the gradient reductions (VERDICT r2 next-round #1)."""
-    B, steps = 256 // world, 1
+    the fp32 summation order of the gradient reductions (VERDICT r2 next-round #1); also over 5 steps
+    with momentum, where the rank sums feed the momentum buffers (VERDICT r3 next-round #4)."""
+    B = 256 // world
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_union_worker, args=(world, free_port(), d, B, steps), nprocs=world, join=True)
+        mp.spawn(_union_worker, args=(world, free_port(), d, B, steps, momentum), nprocs=world, join=True)
         r = [torch.load(os.path.join(d, f"u{i}.pt"), weights_only=True) for i in range(world)]
     # single rank (no process group in this process) on the concatenated rows
     dev = torch.device("cuda", 0)
     allrows = _stream(world, B, steps)
-    net, tr = _make(dev, B * world, allrows)
+    net, tr = _make(dev, B * world, allrows, momentum=momentum)
     w0 = net.store.master.cpu()
     for _ in range(steps):
         tr.step()
@@ -194,3 +197,53 @@ def test_rccl_full_graph_data_parallel_training():
     assert r[0]["path"] == "rccl" and r[0]["graph"] == "full", r[0]
     assert r[0]["multi_u"] == 4
     assert torch.equal(r[0]["w"], r[1]["w"])
+
+
+def _fedsgd_worker(rank, world, port, out_dir, k, mb, steps):
+    dev = init_rank(rank, world, port)
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer, fedsgd_rows
+
+    g = torch.Generator().manual_seed(11)
+    micro = torch.stack([torch.randperm(N_ROWS, generator=g)[:mb] for _ in range(k * steps)])
+    data, labels = synthetic_mnist(N_ROWS, seed=3, device=dev)
+    net = build_model("lenet5", device=dev, seed=0)
+    tr = DataParallelTrainer(net, lr=0.05, graph="full", allreduce="p2p", min_updates_per_version=k)
+    tr.bind_dataset(data, labels, mb, scale=1.0 / 255.0)
+    tr.bind_index_stream(fedsgd_rows(micro, k, rank, world).to(dev))
+    w0 = net.store.master.cpu()
+    for _ in range(steps):
+        tr.step()
+    torch.cuda.synchronize()
+    tr.check_comm()
+    torch.save({"w0": w0, "w": net.store.master.cpu(), "launches": tr.step_launches, "B": tr.B},
+               os.path.join(out_dir, f"k{rank}.pt"))
+    finish()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("k", [8, 5])
+def test_fedsgd_count_barrier_fused_equals_union(k):
+    """Device FedSGD count barrier at W = 2: K microbatches per version (8: 4 + 4; 5: 3 + 2) through the
+    fused two-launch step with the in-kernel exchange equal one rank stepping on the union of the K
+    microbatches, relative error <= 1e-5 on the fp32 master (reference
+    federated_server.ts:73-90)."""
+    world, mb, steps = 2, 32, 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_fedsgd_worker, args=(world, free_port(), d, k, mb, steps), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"k{i}.pt"), weights_only=True) for i in range(world)]
+    assert r[0]["launches"] == "train+reduce/exchange/update"
+    assert r[0]["B"] == mb * (k // 2 + k % 2) and r[1]["B"] == mb * (k // 2)
+    assert torch.equal(r[0]["w"], r[1]["w"])
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(11)
+    micro = torch.stack([torch.randperm(N_ROWS, generator=g)[:mb] for _ in range(k * steps)])
+    net, tr = _make(dev, mb * k, micro.view(steps, k * mb))
+    for _ in range(steps):
+        tr.step()
+    torch.cuda.synchronize()
+    w1 = net.store.master.cpu()
+    rel = ((r[0]["w"] - w1).abs() / w1.abs().clamp_min(1e-3)).max().item()
+    assert rel <= 1e-5, f"master relative error {rel:.3e}"
+    assert (w1 - r[0]["w0"]).abs().max().item() > 0

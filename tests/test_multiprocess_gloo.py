@@ -148,3 +148,53 @@ def test_fedavg_average_is_the_mean_of_ranks():
     assert torch.equal(r[0]["before"], r[1]["before"])  # broadcast init
     torch.testing.assert_close(r[0]["after"], r[0]["before"] + 1.5)  # mean of +1 and +2
     assert torch.equal(r[0]["after"], r[1]["after"])
+
+
+def _fedsgd_worker(rank, world, port, out_dir, k, steps):
+    _init(rank, world, port)
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer, fedsgd_rows
+
+    net = build_model("mlp_mnist", "cpu", seed=0)
+    x, y = synthetic_mnist(512, seed=5)
+    tr = DataParallelTrainer(net, lr=0.1, graph="none", min_updates_per_version=k)
+    tr.bind_dataset(x, y, 16, scale=1.0 / 255)
+    g = torch.Generator().manual_seed(3)
+    micro = torch.randperm(512, generator=g)[: 16 * k * steps].view(k * steps, 16)
+    tr.bind_index_stream(fedsgd_rows(micro, k, rank, world))
+    for _ in range(steps):
+        tr.step()
+    torch.save({"w": net.store.master.clone(), "B": tr.B, "images": tr.images_per_step},
+               os.path.join(out_dir, f"f{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("k", [8, 5])
+def test_fedsgd_count_barrier_equals_union_of_k_microbatches(k):
+    """Device FedSGD count barrier (reference FederatedServer: the mean of minUpdatesPerVersion
+    microbatch gradients per version, federated_server.ts:73-90): W = 2 ranks sharing K microbatches of
+    16 rows per version (K = 5: 3 + 2, uneven) equal one rank stepping on the union of the K microbatches,
+    for every version."""
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+
+    world, steps = 2, 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_fedsgd_worker, args=(world, _port(), d, k, steps), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"f{i}.pt"), weights_only=True) for i in range(world)]
+    assert torch.equal(r[0]["w"], r[1]["w"])
+    assert r[0]["B"] == 16 * (k // 2 + k % 2) and r[1]["B"] == 16 * (k // 2)
+    assert r[0]["images"] == 16 * k
+    ref = build_model("mlp_mnist", "cpu", seed=0)
+    x, y = synthetic_mnist(512, seed=5)
+    g = torch.Generator().manual_seed(3)
+    micro = torch.randperm(512, generator=g)[: 16 * k * steps].view(k * steps, 16)
+    ref.store.set_hyper(0.1)
+    for v in range(steps):
+        rows = micro[v * k:(v + 1) * k].reshape(-1)
+        ref.compute_gradients(x[rows].float() / 255, y[rows])
+        ref.store.sgd_step()
+    torch.testing.assert_close(r[0]["w"], ref.store.master, rtol=1e-5, atol=1e-7)

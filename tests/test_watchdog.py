@@ -181,3 +181,22 @@ def test_mark_done_keeps_watching_peers():
         time.sleep(0.02)
     wd.stop()
     assert seen and "peer rank 1" in seen[0]
+
+
+def test_done_rank_waiting_on_slow_peer_is_not_a_stall():
+    """a rank that finished its steps (mark_done) and waits for a slow but live peer longer than
+    stall_after_s must not be failed for 'no training progress'; the live peer keeps beating."""
+    from distriflow_amd.parallel.watchdog import PeerWatchdog
+
+    store, port = _store()
+    seen = []
+    wd = PeerWatchdog(0, 2, dead_after_s=5.0, interval_s=0.05, port=port, prefix="t6", stall_after_s=0.2,
+                      on_fail=seen.append).start()
+    wd.beat(10)  # trained, then finished
+    wd.mark_done()
+    t0 = time.time()
+    while time.time() - t0 < 1.0:  # the peer is slow but alive: its heartbeat advances
+        store.add("t6/hb/1", 1)
+        time.sleep(0.05)
+    wd.stop()
+    assert not seen, seen
