@@ -307,6 +307,44 @@ void gather_batch_py(torch::Tensor data, c10::optional<torch::Tensor> labels, to
             "gather_batch");
 }
 
+// Keras merge layer (csrc/merge.hip): inputs [rows][w_i] bf16; fwd writes out, bwd writes grads[i]
+static dfa::MergeArgs merge_args(std::vector<torch::Tensor> ins, int64_t kind, int64_t cout) {
+  TORCH_CHECK(ins.size() >= 1 && ins.size() <= (size_t)dfa::kMergeMaxIn, "merge: 1..8 inputs");
+  dfa::MergeArgs a{};
+  a.n = (int)ins.size();
+  a.kind = (int)kind;
+  a.cout = (int)cout;
+  for (int i = 0; i < a.n; ++i) {
+    need(ins[i], at::kBFloat16, "merge input");
+    const int64_t w = ins[i].size(-1);
+    TORCH_CHECK(ins[i].numel() % w == 0, "merge: bad input");
+    if (i == 0) a.rows = ins[i].numel() / w;
+    TORCH_CHECK(ins[i].numel() / w == a.rows, "merge: inputs differ in rows");
+    a.w[i] = (int)w;
+    a.in[i] = (const dfa::bf16*)ins[i].data_ptr();
+  }
+  return a;
+}
+void merge_fwd_py(std::vector<torch::Tensor> ins, torch::Tensor out, int64_t kind) {
+  need(out, at::kBFloat16, "merge out");
+  dfa::MergeArgs a = merge_args(ins, kind, out.size(-1));
+  TORCH_CHECK(out.numel() == a.rows * (int64_t)a.cout, "merge: out size");
+  a.out = (dfa::bf16*)out.data_ptr();
+  check_hip(dfa::merge_fwd(a, cur_stream()), "merge_fwd");
+}
+void merge_bwd_py(std::vector<torch::Tensor> ins, torch::Tensor dy, std::vector<torch::Tensor> grads, int64_t kind) {
+  need(dy, at::kBFloat16, "merge dy");
+  dfa::MergeArgs a = merge_args(ins, kind, dy.size(-1));
+  TORCH_CHECK(grads.size() == ins.size() && dy.numel() == a.rows * (int64_t)a.cout, "merge: grads / dy size");
+  a.dy = (const dfa::bf16*)dy.data_ptr();
+  for (int i = 0; i < a.n; ++i) {
+    need(grads[i], at::kBFloat16, "merge grad");
+    TORCH_CHECK(grads[i].numel() == ins[i].numel(), "merge: grad size");
+    a.grad[i] = (dfa::bf16*)grads[i].data_ptr();
+  }
+  check_hip(dfa::merge_bwd(a, cur_stream()), "merge_bwd");
+}
+
 void add_act_py(torch::Tensor a, torch::Tensor b, torch::Tensor out, bool relu) {
   need(a, at::kBFloat16, "a");
   need(b, at::kBFloat16, "b");
@@ -1821,6 +1859,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gather_batch", &gather_batch_py, py::arg("data"), py::arg("labels"), py::arg("idx"), py::arg("out"),
         py::arg("out_labels"), py::arg("B"), py::arg("row"), py::arg("scale"), py::arg("step_inc") = py::none());
   m.def("add_act", &add_act_py);
+  m.def("merge_fwd", &merge_fwd_py, "Keras merge layer forward (Add / Subtract / Multiply / Average / Maximum / "
+        "Minimum / Concatenate)");
+  m.def("merge_bwd", &merge_bwd_py, "Keras merge layer: gradient of every input");
   m.def("relu_bwd", &relu_bwd_py);
   m.def("gap_fwd", &gap_fwd_py);
   m.def("gap_bwd", &gap_bwd_py);

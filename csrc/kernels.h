@@ -145,6 +145,23 @@ hipError_t gather_batch(const void* data, int data_is_u8, const int* labels, con
                         long long* step_inc = nullptr);
 hipError_t gather_labels(const int* labels, const long long* idx, int* out, int B, long long nrows, hipStream_t st);
 hipError_t add_act(const bf16* a, const bf16* b, bf16* out, long long n, int relu, hipStream_t st);
+// Keras merge layers (csrc/merge.hip): out[rows][cout] from n inputs [rows][w[i]] (elementwise kinds: every
+// w[i] == cout; Concatenate: the channels side by side, sum w[i] == cout).  merge_bwd writes grad[i] =
+// d out / d in_i * dy for every input (Concatenate: the channel slice).
+constexpr int kMergeMaxIn = 8;
+constexpr int kMergeAdd = 0, kMergeSubtract = 1, kMergeMultiply = 2, kMergeAverage = 3, kMergeMaximum = 4,
+              kMergeMinimum = 5, kMergeConcat = 6;
+struct MergeArgs {
+  const bf16* in[kMergeMaxIn];
+  bf16* grad[kMergeMaxIn];
+  const bf16* dy;
+  bf16* out;
+  int w[kMergeMaxIn];
+  long long rows;
+  int cout, n, kind;
+};
+hipError_t merge_fwd(const MergeArgs& a, hipStream_t st);
+hipError_t merge_bwd(const MergeArgs& a, hipStream_t st);
 hipError_t relu_bwd(const bf16* y, const bf16* dy, bf16* dx, long long n, hipStream_t st);
 hipError_t gap_fwd(const bf16* x, bf16* y, int B, int HW, int C, hipStream_t st);
 hipError_t gap_bwd(const bf16* dy, bf16* dx, int B, int HW, int C, hipStream_t st);
@@ -339,7 +356,6 @@ struct PSArgs {
   unsigned* done_epoch;
   unsigned* claimed_epoch;
   const float* lr_dev;          // device learning rate (the store's hyper[0]); null: use lr
-  unsigned long long* stamps;   // diagnostic [8] s_memtime / wall-clock marks of the decision (or null)
   long long nbatches, timeout_ticks;
   int B, max_stale, max_epochs;  // max_epochs 0 = unbounded
   float lr;
@@ -442,7 +458,7 @@ struct LeNetRedArgs {
   // staged: an async step is train + this launch (csrc/lenet_fused.hip, protocol csrc/ps_device.h)
   int ps_on;
   PSArgs ps;
-  unsigned long long* stamps;  // diagnostic: [grid][8] s_memtime per phase (scripts/lenetstamps.py), or null
+  unsigned long long* stamps;  // diagnostic: [grid][16] wall-clock marks per phase (scripts/lenetstamps.py), or null
 };
 // The reference CNN's conv block (csrc/kcnn_fused.hip): conv1 3x3x1->32 + ReLU, conv2 3x3x32->32 + ReLU,
 // 2x2 max-pool [+ folded dropout], input 28x28x1, in one forward and one backward launch (+ reduce).

@@ -53,7 +53,7 @@ def _weight_layers(net):
     """[(spec_name, layer)] in parameter order, plus BN moving statistics entries."""
     out = []
     for l in net.exec_layers:
-        subs = l.sublayers() if isinstance(l, ResidualBlock) else [l]
+        subs = l.sublayers() if hasattr(l, "sublayers") else [l]
         for s in subs:
             for spec in s.specs():
                 out.append((spec.name, s))

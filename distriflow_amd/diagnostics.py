@@ -15,6 +15,8 @@ Python switches (default in brackets):
   khead_fused [1]          the reference CNN's dense head (4608 -> 128 -> C + CE) as one split-K launch
                            plus the fused head weight-gradient launch (0: per-layer GEMMs + head kernels)
   multistep [1]            bench.py unrolls up to 64 steps per hipGraph (0: one replay per step)
+  fused_selftest [1]       real-kernel self-test of the multi-rank fused LeNet-5 step before its first use
+                           (0: trust the LL exchange's own setup self-test)
   wgrad_overlap [0]        ResNet weight gradients on a side stream (round 2: +3 %; with the halo-tiled
                            kernels, whose workgroups fill whole CUs, in-order is faster: 83.7 k vs 79.5 k
                            images/s, profiles/r3/resnet18_b256_stream_overlap_ab.txt)
@@ -31,7 +33,7 @@ from __future__ import annotations
 import os
 
 _DEFAULTS = {"lenet_fused": 1, "lenet_fused_update": 1, "async_fused": 1, "kcnn_fused": 1, "khead_fused": 1, "fold_dropout": 1,
-             "multistep": 1, "wgrad_overlap": 0, "proj_overlap": 0, "concurrent_backward": 0, "bn_epilogue": 0}
+             "multistep": 1, "fused_selftest": 1, "wgrad_overlap": 0, "proj_overlap": 0, "concurrent_backward": 0, "bn_epilogue": 0}
 
 
 def diag(name: str) -> int:

@@ -419,12 +419,26 @@ class Dropout(Layer):
 
 
 class Flatten(Layer):
-    """View only: consumers reshape their input; never executed."""
+    """View only: consumers reshape their input; never executed in a chain (inside a branching graph,
+    models/graph.py, forward / backward are reshapes of the same storage)."""
 
     def build(self, in_shape):
         self.in_shape = tuple(in_shape)
         self.out_shape = (int(math.prod(in_shape)),)
         return self.out_shape
+
+    def alloc(self, B, device, dtype, ws):
+        self.out = self.dx = None
+
+    def forward(self, x, training):
+        self.out = x.reshape((x.shape[0],) + self.out_shape)
+        return self.out
+
+    def backward(self, dy):
+        if not self.need_dx:
+            return None
+        self.dx = dy.reshape((dy.shape[0],) + self.in_shape)
+        return self.dx
 
 
 class Activation(Layer):

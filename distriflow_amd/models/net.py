@@ -55,7 +55,7 @@ class Net:
             self.store.lenet_snap = torch.zeros(2 * 2550, dtype=torch.float32, device=self.device)
             self.store.refresh_compute()
         for l in self.exec_layers:
-            if isinstance(l, ResidualBlock):
+            if hasattr(l, "bind_store"):  # composite layers: ResidualBlock, GraphLayer
                 l.bind_store(self.store)
             else:
                 l.store = self.store
@@ -272,7 +272,7 @@ class Net:
 
     def _all_leaf_layers(self):
         for l in self.exec_layers:
-            if isinstance(l, ResidualBlock):
+            if hasattr(l, "sublayers"):  # composite layers: ResidualBlock, GraphLayer
                 yield from l.sublayers()
             else:
                 yield l

@@ -355,6 +355,69 @@ def add_act(a, b, out, relu=False):
     return out
 
 
+# ---- Keras merge layers of branching graphs (csrc/merge.hip); codes match kernels.h kMerge*
+MERGE_KINDS = {"Add": 0, "Subtract": 1, "Multiply": 2, "Average": 3, "Maximum": 4, "Minimum": 5, "Concatenate": 6}
+
+
+def _merge_ref(kind: int, xs):
+    xs = [x.float() for x in xs]
+    if kind == 6:
+        return torch.cat(xs, dim=-1)
+    out = xs[0].clone()
+    for x in xs[1:]:
+        if kind in (0, 3):
+            out = out + x
+        elif kind == 1:
+            out = out - x
+        elif kind == 2:
+            out = out * x
+        elif kind == 4:
+            out = torch.maximum(out, x)
+        else:
+            out = torch.minimum(out, x)
+    return out / len(xs) if kind == 3 else out
+
+
+def merge_fwd(inputs, out, kind: str):
+    """out = merge(inputs) over the last axis layout [..., C] (one launch on GPU)."""
+    k = MERGE_KINDS[kind]
+    if out.is_cuda:
+        _C().merge_fwd([x.contiguous() for x in inputs], out, k)
+    else:
+        out.copy_(_merge_ref(k, inputs).to(out.dtype))
+    return out
+
+
+def merge_bwd(inputs, dy, grads, kind: str):
+    """grads[i] = d merge / d inputs[i] * dy (Maximum / Minimum: to the first input holding the extreme)."""
+    k = MERGE_KINDS[kind]
+    if dy.is_cuda:
+        _C().merge_bwd([x.contiguous() for x in inputs], dy.contiguous(), list(grads), k)
+        return grads
+    if k == 6:
+        off = 0
+        for x, g in zip(inputs, grads):
+            w = x.shape[-1]
+            g.copy_(dy[..., off:off + w])
+            off += w
+        return grads
+    if k in (4, 5):  # first extreme wins, as the kernel
+        xs = [x.float() for x in inputs]
+        ext = _merge_ref(k, inputs)
+        taken = torch.zeros_like(ext, dtype=torch.bool)
+        for x, g in zip(xs, grads):
+            hit = (x == ext) & ~taken
+            taken |= hit
+            g.copy_(torch.where(hit, dy.float(), torch.zeros_like(ext)).to(g.dtype))
+        return grads
+    xs = [x.float().detach().requires_grad_(True) for x in inputs]
+    y = _merge_ref(k, xs)
+    gs = torch.autograd.grad(y, xs, dy.float())
+    for g, v in zip(grads, gs):
+        g.copy_(v.to(g.dtype))
+    return grads
+
+
 # ---- generic Keras layers (csrc/act.hip); codes match kernels.h ActKind
 ACT_KINDS = {"linear": 0, None: 0, "relu": 1, "relu6": 2, "sigmoid": 3, "tanh": 4, "elu": 5, "selu": 6,
              "softplus": 7, "softsign": 8, "hard_sigmoid": 9, "hardSigmoid": 9, "swish": 10, "silu": 10,

@@ -260,7 +260,7 @@ class DataParallelTrainer:
         unfused step (compute + one-shot all-reduce or RCCL + SGD).  The engine state is restored after.
         Reference semantics held here: the synchronous server's mean of the K uploaded gradients
         (/root/reference/src/server/federated_server.ts:92-117)."""
-        if self.fused_selftest or self.world == 1 or not self._step_all_reduces:
+        if self.fused_selftest or self.world == 1 or not self._step_all_reduces or not _diag_on("fused_selftest"):
             return
         if not (self.fused_update and getattr(self.net, "lenet_fused", False) and self.net.store.lenet_frag is not None
                 and self.p2p is not None and getattr(self.p2p.comm, "ll_slots", 0) >= 256
@@ -439,14 +439,15 @@ class DataParallelTrainer:
 
     def _capture(self):
         net = self.net
-        s = torch.cuda.Stream(device=net.device)
-        s.wait_stream(torch.cuda.current_stream(net.device))
         # warm-up on a side stream (allocator, RCCL communicators, kernel code objects); the warm-up
-        # steps are not training steps: the engine state is restored before capture
+        # steps are not training steps: the engine state is restored before capture.  The side stream
+        # waits for the snapshot copies (taken on the current stream) before its first step.
         snap = net.snapshot_state()
         rs0 = self.run_stats.clone()
         cursor = self._index_stream[1].clone() if self._index_stream is not None else None
         idx0 = self.idx.clone()
+        s = torch.cuda.Stream(device=net.device)
+        s.wait_stream(torch.cuda.current_stream(net.device))
         with torch.cuda.stream(s):
             for _ in range(self.capture_warmup):
                 self._gather()

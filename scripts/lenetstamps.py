@@ -55,56 +55,57 @@ def main():
         col = d[:, k]
         print(f"  {name:<12} median {np.median(col):8.0f}  p90 {np.percentile(col, 90):8.0f}  "
               f"share {np.median(col) / np.median(tot) * 100:5.1f}%")
-    # reduce launch (fused update path: the trainer's step), clocks at [4096 * 16 + block * 8 + slot]
-    if len(sys.argv) > 2 and sys.argv[2] == "step":
-        from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
+    # reduce launch of the trainer's step: wall-clock stamps (100 MHz) at [4096 * 16 + block * 16 + slot]
+    if len(sys.argv) > 2 and sys.argv[2] in ("step", "async"):
+        reduce_stamps(m, net, data, labels, B, buf, sys.argv[2] == "async")
 
+
+def reduce_stamps(m, net, data, labels, B, buf, async_ps):
+    """Per-phase microseconds of the reduce launch (sync: fused update; async: parameter-server mode).
+    Slots: 0 start, 1 jobs done, 2 decision known, 3 owned slots applied, 4 end, 5 first owned slot's
+    rank sums in (LL) / first PS apply done, 6 first job's partial, 7 first ownership combine; staging
+    workgroup: 8 admission start, 9 admission done, 10 next batch staged."""
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
+
+    if async_ps:
+        from distriflow_amd.parallel.async_ps import AsyncPSTrainer
+
+        tr = AsyncPSTrainer(net, lr=0.01, max_staleness=4, graph="none")
+        tr.bind_dataset(data, labels, B, scale=1 / 255.0)
+        tr.bind_schedule(epoch_permutations(60000, B, 60000 // B, "cuda", seed=0))
+    else:
         tr = DataParallelTrainer(net, lr=0.01, graph="none")
         tr.bind_dataset(data, labels, B, scale=1 / 255.0)
         tr.bind_index_stream(epoch_permutations(60000, B, 8, "cuda", seed=0))
-        for _ in range(3):
-            tr.step()
-        torch.cuda.synchronize()
+    for _ in range(3):
+        tr.step()
+    torch.cuda.synchronize()
+    rows = []
+    for _ in range(5):
         buf.zero_()
         m.convpool_set_stamps(buf)
         tr.step()
         torch.cuda.synchronize()
         m.convpool_set_stamps(None)
-        t_end_train = buf[: nblk * 16].view(nblk, 16).cpu().numpy().astype(np.int64)[:, 10].max()
-        G = 2048
-        r = buf[4096 * 16: 4096 * 16 + G * 8].view(G, 8).cpu().numpy().astype(np.int64)
-        # job workgroup j runs job j = slot * 8 + chunk: slots are 32 x 32 dense units of (400 -> 120),
-        # (120 -> 84), (84 -> 10) incl. bias, then 256-parameter conv slots; then loss, staging
-        nd = sum(-(-n // 32) * -(-(k + 1) // 32) for k, n in ((400, 120), (120, 84), (84, 10)))
-        nc = -(-2572 // 256)
-        nj = 8 * (nd + nc)
-        kinds = np.array(["dense"] * (8 * nd) + ["conv"] * (8 * nc) + ["loss", "stage"] + ["-"] * (G - nj - 2))
+        rows.append(buf[4096 * 16: 4096 * 16 + 1024 * 16].view(1024, 16).cpu().numpy().astype(np.int64))
+    us = lambda v: v / 100.0  # noqa: E731  wall clock ticks -> us
+    print(f"reduce launch ({'async PS' if async_ps else 'sync'}), 5 steps, wall clock (us):")
+    for r in rows:
         valid = r[:, 0] > 0
-        for kind in ("dense", "conv"):
-            sel = valid & (kinds == kind)
-            if sel.any():
-                job = r[sel, 6] - r[sel, 0]
-                own = sel & (r[:, 7] > 0)
-                life = r[sel, 4] - r[sel, 0]
-                print(f"  {kind:<6} jobs {sel.sum():4d}: job median {np.median(job):7.0f} max {job.max():7.0f};"
-                      f" lifetime median {np.median(life):7.0f} max {life.max():7.0f}")
-                if own.any():
-                    comb = r[own, 7] - r[own, 6]
-                    app = r[own, 3] - r[own, 2]
-                    print(f"         owners {own.sum():4d}: ticket+combine median {np.median(comb):7.0f} max "
-                          f"{comb.max():7.0f}; apply median {np.median(app):7.0f} max {app.max():7.0f}")
-        for kind in ("loss", "stage"):
-            sel = valid & (kinds == kind)
-            if sel.any():
-                print(f"  {kind:<6} workgroup lifetime {int((r[sel, 1] - r[sel, 0])[0]):7d}")
-        r = r[valid]
-        print(f"reduce launch: {r.shape[0]} stamped workgroups (per-XCD clocks: only in-workgroup spans are "
-              f"meaningful)")
-        for k, name in enumerate(["jobs (all)", "decision", "apply", "arrive"]):
-            ok = (r[:, k + 1] > 0) & (r[:, k] > 0)
-            col = r[ok, k + 1] - r[ok, k]
-            if col.size:
-                print(f"  {name:<18} median {np.median(col):8.0f}  p90 {np.percentile(col, 90):8.0f}  max {col.max():8.0f}")
+        t0 = r[valid, 0].min()
+        end = r[valid][:, [1, 4]].max()
+        jobs = valid & (r[:, 6] > 0)
+        own = valid & (r[:, 2] > 0) & (r[:, 3] > 0)
+        line = [f"launch span {us(end - t0):6.2f}", f"first job done {us(np.median(r[jobs, 6] - t0)):5.2f} (median)",
+                f"jobs done {us(np.median(r[valid & (r[:, 1] > 0), 1] - t0)):5.2f} (median)"]
+        if own.any():
+            line.append(f"owners {own.sum()}: wait {us(np.median(r[own, 2] - r[own, 1])):5.2f} "
+                        f"apply {us(np.median(r[own, 3] - r[own, 2])):5.2f} max {us((r[own, 3] - r[own, 2]).max()):5.2f}")
+        st = valid & (r[:, 8] > 0)
+        if st.any():
+            line.append(f"admission {us(float(r[st, 9][0] - r[st, 8][0])):5.2f} (start +{us(float(r[st, 8][0] - t0)):5.2f}),"
+                        f" claim+stage {us(float(r[st, 10][0] - r[st, 9][0])):5.2f}")
+        print("  " + "; ".join(line))
 
 
 if __name__ == "__main__":

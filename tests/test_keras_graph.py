@@ -1,0 +1,113 @@
+"""Branching Keras functional graphs (VERDICT r3 Missing 5): merge layers (Add, Subtract, Multiply, Average,
+Maximum, Minimum, Concatenate) and fan-out, run as one GraphLayer between the chain head and tail
+(models/graph.py, kernels csrc/merge.hip).  The CPU fp32 engine is checked against torch autograd on the
+same graph; the GPU merge kernels against the fp32 reference in tests/test_kernels_gpu.py.
+
+Reference: ``fetchModel`` wraps any tf.LayersModel (/root/reference/src/common/utils.ts:236-244,
+src/common/models.ts:92-100)."""
+import json
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distriflow_amd.models.graph import GraphLayer
+from distriflow_amd.models.keras import layers_from_keras
+from distriflow_amd.models.net import Net
+
+
+def _functional(layers, input_shape, output):
+    """layers: [(class, name, cfg, [inbound names])] in any order; Keras 2 JSON."""
+    out = [{"class_name": "InputLayer", "name": "inp",
+            "config": {"name": "inp", "batch_input_shape": [None, *input_shape], "dtype": "float32"},
+            "inbound_nodes": []}]
+    for cls, name, cfg, ins in layers:
+        out.append({"class_name": cls, "name": name, "config": dict(cfg, name=name),
+                    "inbound_nodes": [[[i, 0, 0, {}] for i in ins]]})
+    return {"class_name": "Model", "config": {"name": "g", "layers": out, "input_layers": [["inp", 0, 0]],
+                                              "output_layers": [[output, 0, 0]]}}
+
+
+def _conv(x, w, b, pad):
+    return F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), b, padding=pad).permute(0, 2, 3, 1)
+
+
+MERGES = {"Add": lambda a, b: a + b, "Subtract": lambda a, b: a - b, "Multiply": lambda a, b: a * b,
+          "Average": lambda a, b: (a + b) / 2, "Maximum": torch.maximum, "Minimum": torch.minimum}
+
+
+@pytest.mark.parametrize("merge", list(MERGES) + ["Concatenate"])
+def test_branching_graph_grads_match_autograd(merge):
+    """conv (relu, 3 consumers) -> two branches joined by ``merge`` -> tanh -> concat with the trunk ->
+    pool -> dense: every gradient and the loss equal torch autograd on the same weights."""
+    wa = 6 if merge != "Concatenate" else 4
+    topo = _functional([
+        ("Conv2D", "c1", {"filters": 6, "kernel_size": [3, 3], "activation": "relu", "padding": "same"}, ["inp"]),
+        ("Conv2D", "a1", {"filters": wa, "kernel_size": [3, 3], "activation": "relu", "padding": "same"}, ["c1"]),
+        ("Conv2D", "b1", {"filters": 6, "kernel_size": [1, 1], "activation": "tanh"}, ["c1"]),
+        (merge, "m", {"axis": -1} if merge == "Concatenate" else {}, ["a1", "b1"]),
+        ("Activation", "t", {"activation": "tanh"}, ["m"]),
+        ("Concatenate", "cat", {"axis": -1}, ["t", "c1"]),
+        ("MaxPooling2D", "p", {"pool_size": [2, 2]}, ["cat"]),
+        ("Flatten", "f", {}, ["p"]),
+        ("Dense", "d", {"units": 5, "activation": "softmax"}, ["f"]),
+    ], (6, 6, 2), "d")
+    layers, shape = layers_from_keras(topo)
+    assert any(isinstance(l, GraphLayer) for l in layers)
+    net = Net(layers, shape, device="cpu", seed=5)
+    x = torch.rand(4, 6, 6, 2)
+    y = torch.randint(0, 5, (4,))
+    st = net.compute_gradients(x, y)
+    P = {s.name: net.store[s.name].detach().clone().requires_grad_(True) for s in net.store.specs}
+    c1 = F.relu(_conv(x, P["c1/kernel"], P["c1/bias"], 1))
+    a1 = F.relu(_conv(c1, P["a1/kernel"], P["a1/bias"], 1))
+    b1 = torch.tanh(_conv(c1, P["b1/kernel"], P["b1/bias"], 0))
+    m = torch.cat([a1, b1], -1) if merge == "Concatenate" else MERGES[merge](a1, b1)
+    cat = torch.cat([torch.tanh(m), c1], -1)
+    p = F.max_pool2d(cat.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
+    z = F.linear(p.reshape(4, -1), P["d/kernel"], P["d/bias"])
+    loss = F.cross_entropy(z, y)
+    loss.backward()
+    assert abs(float(st[0]) / 4 - loss.item()) < 1e-4
+    for s in net.store.specs:
+        torch.testing.assert_close(net.store.gradient(s.name), P[s.name].grad, rtol=1e-4, atol=1e-5,
+                                   msg=lambda m, n=s.name: f"{n}: {m}")
+
+
+def test_residual_graph_trains_and_round_trips_through_tfjs_checkpoint():
+    """A residual (Add) functional model trains through the DistriModel API, and its tf.js checkpoint
+    (topology kept, weights by name) loads back into an equal model."""
+    from distriflow_amd.checkpoint.tfjs import save_layers_model
+    from distriflow_amd.models.distri_model import EngineModel, fetch_model
+
+    topo = _functional([
+        ("Dense", "h", {"units": 16, "activation": "relu"}, ["inp"]),
+        ("Dense", "r", {"units": 16, "activation": "relu"}, ["h"]),
+        ("Add", "add", {}, ["h", "r"]),
+        ("Dense", "out", {"units": 4, "activation": "softmax"}, ["add"]),
+    ], (8,), "out")
+    with tempfile.TemporaryDirectory() as d:
+        with open(os.path.join(d, "model.json"), "w") as f:
+            json.dump({"modelTopology": {"model_config": topo}, "weightsManifest": []}, f)
+        net = fetch_model(os.path.join(d, "model.json"), device="cpu")
+        m = EngineModel(net, {"learningRate": 0.1, "loss": "softmaxCrossEntropy"}, device="cpu")
+        g = torch.Generator().manual_seed(0)
+        x = torch.randn(64, 8, generator=g)
+        y = (x[:, 0] > 0).long() + 2 * (x[:, 1] > 0).long()
+        l0 = m.evaluate(x, y)[0]
+        for _ in range(40):
+            m.update(m.fit(x, y))
+        assert m.evaluate(x, y)[0] < l0
+        save_layers_model(net, os.path.join(d, "ck"))
+        net2 = fetch_model(os.path.join(d, "ck", "model.json"), device="cpu")
+        for s in net.store.specs:
+            torch.testing.assert_close(net2.store[s.name], net.store[s.name])
+
+
+def test_unsupported_graphs_still_raise():
+    two_out = _functional([("Dense", "a", {"units": 3}, ["inp"]), ("Dense", "b", {"units": 3}, ["inp"])], (4,), "a")
+    two_out["config"]["output_layers"].append(["b", 0, 0])
+    with pytest.raises(NotImplementedError):
+        layers_from_keras(two_out)
