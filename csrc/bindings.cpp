@@ -1180,7 +1180,7 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
   TORCH_CHECK(frag.is_cuda() && frag.is_contiguous() && (size_t)frag.nbytes() >= dfa::lenet_frag_bytes(),
               "lenet: fragment buffer too small");
   TORCH_CHECK(ftab.is_cuda() && ftab.scalar_type() == at::kByte && ftab.numel() == 98 * 2 * 16, "lenet: ftab");
-  TORCH_CHECK(pxtab.is_cuda() && pxtab.scalar_type() == at::kShort && pxtab.numel() == 800, "lenet: pxtab");
+  TORCH_CHECK(pxtab.is_cuda() && pxtab.scalar_type() == at::kShort && pxtab.numel() == 832, "lenet: pxtab");
   a.frag = frag.data_ptr();
   a.prep = prep ? 1 : 0;
   a.ftab = ftab.data_ptr<uint8_t>();

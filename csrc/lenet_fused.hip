@@ -48,11 +48,17 @@ constexpr int XS_ELEMS = IMG * 1024 + 32;           // [8][32][32] padded input 
 constexpr int OFF_XS = 0;
 constexpr int OFF_P1 = OFF_XS + XS_ELEMS * 2;       // [8][196][8] bf16 pool1 output, later its gradient
 constexpr int OFF_C1 = OFF_P1 + IMG * 196 * 16;     // [8][196] u32 pool1 codes (3 bits per channel)
-constexpr int OFF_K = OFF_C1 + IMG * 196 * 4;       // 64 B zeros, 32 B ones (bf16)
-constexpr int OFF_FT = OFF_K + 128;                 // conv2 dgrad table [98][2][16] u8 (host-built)
-constexpr int OFF_PX = OFF_FT + 98 * 2 * 16;        // conv2 output row -> P1 pixel [800] u16 (host-built)
-constexpr int OFF_W = OFF_PX + 800 * 2;             // f32: b1 [6], b2 [16]
-constexpr int OFF_U = OFF_W + 128;                  // phase-dependent union
+// conv2 output rows (the GEMM M of phases B / E / F) are numbered per image in blocks of DC2_RS = 104:
+// row m = image * 104 + t, t = window * 4 + position < 100 (t = 100 .. 103: padding, a zero gradient)
+constexpr int DC2_RS = 104;
+constexpr int NM = IMG * DC2_RS;                    // 832 padded conv2 output rows
+constexpr int OFF_K = OFF_C1 + IMG * 196 * 4;       // 32 B ones (bf16)
+constexpr int OFF_PX = OFF_K + 32;                  // conv2 output row -> P1 pixel [832] u16 (host-built)
+constexpr int OFF_FT = OFF_PX + NM * 2;             // conv2 dgrad table [98][2][16] u8 (host-built)
+constexpr int OFF_W = OFF_FT + 98 * 2 * 16;         // f32: b1 [6], b2 [16], then 8 int labels
+// the union starts where it always did (OFF_XS1's bank offset from Xs, and so phase A / G's
+// conflict-free reads, depend on it)
+constexpr int OFF_U = OFF_W + 128 + 32;
 // phases A and G: input shifted left by one pixel; 32 bytes into the union so that its rows sit 24 banks
 // from Xs's (the A-operand reads of phase A and the B-operand reads of phase G are then conflict-free:
 // scripts/lds_sim.py)
@@ -68,16 +74,17 @@ constexpr int OFF_ZR = OFF_Z1 + IMG * LD1 * 2;      // zero row [LD0] (A rows 8.
 constexpr int OFF_LG = OFF_ZR + LD0 * 2;            // [8][16] f32 logits
 constexpr int OFF_C2 = OFF_LG + IMG * 16 * 4;       // [8][25][16] u8 pool2 codes
 constexpr int U_DENSE = OFF_C2 + IMG * 25 * 16 - OFF_U;
-constexpr int OFF_DC2 = OFF_U;                      // [800][16] bf16 conv2 output gradient
-constexpr int U_DC2 = 800 * 16 * 2;
+constexpr int OFF_DC2 = OFF_U;                      // [832][16] bf16 conv2 output gradient (padded rows)
+constexpr int U_DC2 = NM * 16 * 2;
 constexpr int OFF_RED = OFF_XS1 + XS_ELEMS * 2;     // [4][16][32] f32 cross-wave conv1 wgrad sums
 constexpr int U_G = 32 + XS_ELEMS * 2 + 4 * 16 * 32 * 4;
-// conv2 output-gradient rows r (image * 100 + window * 4 + position) are stored at row r ^ ((r >> 3) & 7):
-// the gathered A-operand reads of phase F then spread over the banks (scripts/lds_sim.py)
+// conv2 output-gradient rows r (padded numbering) are stored at row r ^ ((r >> 3) & 7): the gathered
+// A-operand reads of phase F then spread over the banks (scripts/lds_sim.py); 104-row image blocks keep
+// every 8-row block inside one image.  The padding rows hold zeros: phase F's "no tap" entries read one.
 __device__ __forceinline__ int dc2_row(int r) { return r ^ ((r >> 3) & 7); }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int LDS_BYTES = OFF_U + cmax(cmax(U_DENSE, U_DC2), U_G);
-static_assert(OFF_U % 16 == 0 && OFF_H1 % 16 == 0 && OFF_ZR % 16 == 0 && OFF_C2 % 16 == 0 && OFF_RED % 16 == 0 &&
+static_assert(OFF_U == OFF_C1 + IMG * 196 * 4 + 128 + 98 * 2 * 16 + 800 * 2 + 128 && OFF_U % 16 == 0 && OFF_H1 % 16 == 0 && OFF_ZR % 16 == 0 && OFF_C2 % 16 == 0 && OFF_RED % 16 == 0 &&
                   OFF_PX % 16 == 0 && OFF_W % 16 == 0,
               "LDS carve must stay 16-byte aligned");
 static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
@@ -265,8 +272,7 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   bf16* Xs1 = reinterpret_cast<bf16*>(smem + OFF_XS1);
   bf16* P1 = reinterpret_cast<bf16*>(smem + OFF_P1);
   unsigned* C1 = reinterpret_cast<unsigned*>(smem + OFF_C1);
-  bf16* KZ = reinterpret_cast<bf16*>(smem + OFF_K);       // 32 zeros
-  bf16* KO = KZ + 32;                                       // 16 ones
+  bf16* KO = reinterpret_cast<bf16*>(smem + OFF_K);       // 16 ones
   unsigned char* FT = reinterpret_cast<unsigned char*>(smem + OFF_FT);
   unsigned short* PX = reinterpret_cast<unsigned short*>(smem + OFF_PX);
   float* WS = reinterpret_cast<float*>(smem + OFF_W);       // b1[6] b2[16]
@@ -299,7 +305,6 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   const bf16x8 z8 = zero8();
   for (int e = tid; e < (OFF_K - OFF_XS) / 16; e += NT) st8(Xs + 8 * e, z8);  // Xs, P1 (pad channels), C1
   for (int e = tid; e < (LDS_BYTES - OFF_U) / 16; e += NT) st8(reinterpret_cast<bf16*>(smem + OFF_U) + 8 * e, z8);
-  if (tid < 4) st8(KZ + 8 * tid, z8);
   if (tid < 2) {
     bf16x8 o;
 #pragma unroll
@@ -308,8 +313,20 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   }
   if (tid < 6) WS[tid] = a.b1[tid];
   if (tid < 16) WS[6 + tid] = a.b2[tid];
+  // labels of the 8 images (dependent loads idx -> label: issued here, read by the loss phase)
+  int* LBL = reinterpret_cast<int*>(WS + 24);
+  if (tid >= 64 && tid < 64 + IMG) {
+    const int r = tid - 64;
+    int y = 0;
+    if (r < rows) {
+      const long long src = a.idx ? a.idx[r0 + r] : (long long)(r0 + r);
+      y = a.labels[src < 0 ? 0 : (src >= a.nrows ? a.nrows - 1 : src)];
+      y = y < 0 ? 0 : (y > 9 ? 9 : y);
+    }
+    LBL[r] = y;
+  }
   if (tid < 98 * 2) reinterpret_cast<uint4*>(FT)[tid] = reinterpret_cast<const uint4*>(a.ftab)[tid];
-  if (tid < 100) reinterpret_cast<uint4*>(PX)[tid] = reinterpret_cast<const uint4*>(a.pxtab)[tid];
+  if (tid < NM / 8) reinterpret_cast<uint4*>(PX)[tid] = reinterpret_cast<const uint4*>(a.pxtab)[tid];
   __syncthreads();
   // input rows -> bf16, 2-pixel zero border ('same' padding)
   if (tid < IMG * 28) {
@@ -405,18 +422,20 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
     }
     const float b2 = WS[6 + i];
 #pragma unroll 2
-    for (int mt = w; mt < 50; mt += NT / 64) {
+    for (int mt = w; mt < NM / 16; mt += NT / 64) {  // padded rows: window 25 of an image is padding
       const bf16* abase = P1 + (int)PX[16 * mt + i] * 8;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 7; ++s) acc = mfma16x16x32(ld8(abase + toff[s]), bw[s], acc);
       const int m0 = 16 * mt + 4 * g;
-      const int img0 = m0 / 100, win0 = (m0 - 100 * (m0 / 100)) >> 2;
+      const int img0 = m0 / DC2_RS, win0 = (m0 - DC2_RS * img0) >> 2;
       float best;
       unsigned code;
       pool4(acc[0] + b2, acc[1] + b2, acc[2] + b2, acc[3] + b2, best, code);
-      H0[img0 * LD0 + win0 * 16 + i] = f2bf(best);
-      C2[(img0 * 25 + win0) * 16 + i] = (unsigned char)code;
+      if (win0 < 25) {
+        H0[img0 * LD0 + win0 * 16 + i] = f2bf(best);
+        C2[(img0 * 25 + win0) * 16 + i] = (unsigned char)code;
+      }
     }
   }
   __syncthreads();
@@ -447,49 +466,52 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   dense_load(g2, a.d2wt, 8);
   dense_fwd(f2, H1, LD1, ZR, a.d2b, 84, true, H2, LD2, nullptr, a.h2T, a.ldt, r0, rows);
   __syncthreads();
-  DenseFrags<4, ccdiv(25, NW)> g1;  // dense-1 data-gradient weights: loads overlap dense-3 and the loss
-  dense_load(g1, a.d1wt, 25);
   dense_fwd(f3, H2, LD2, ZR, a.d3b, 10, false, nullptr, 0, LG, nullptr, a.ldt, r0, rows);
   __syncthreads();
   LN_STAMP(4);
-  if (tid < IMG) {
-    const int r = tid;
-    float lsum = 0.f, corr = 0.f;
-    if (r < rows) {
-      const long long src = a.idx ? a.idx[r0 + r] : (long long)(r0 + r);
-      int y = a.labels[src < 0 ? 0 : (src >= a.nrows ? a.nrows - 1 : src)];
-      y = y < 0 ? 0 : (y > 9 ? 9 : y);
-      float mx = -INFINITY;
-      int am = 0;
-      for (int c = 0; c < 10; ++c) {
-        const float z = LG[r * 16 + c];
-        if (a.logits) a.logits[(long long)(r0 + r) * 10 + c] = z;
-        if (z > mx) { mx = z; am = c; }
-      }
-      float pr[10], s = 0.f;
-      for (int c = 0; c < 10; ++c) {
-        pr[c] = __expf(LG[r * 16 + c] - mx);
-        s += pr[c];
-      }
-      const float inv = 1.f / s;
-      lsum = -(LG[r * 16 + y] - mx - __logf(s));
-      corr = am == y ? 1.f : 0.f;
-      for (int c = 0; c < 10; ++c) {
-        const float gv = (pr[c] * inv - (c == y ? 1.f : 0.f)) * a.grad_scale;
-        Z3[r * LD3 + c] = f2bf(gv);
-        a.dz3T[(long long)c * a.ldt + r0 + r] = f2bf(gv);
-      }
-    }
+  // softmax-CE of the 8 images, 16 lanes per image (class c = lane & 15; waves 0 and 1): max / first
+  // argmax / sum of exponentials by shuffles inside the 16-lane group, one gradient element per lane
+  if (tid < IMG * 16) {
+    const int r = tid >> 4, c = tid & 15;
+    const bool live = r < rows;
+    const int y = LBL[r];
+    const float z = c < 10 ? LG[r * 16 + c] : -INFINITY;
+    if (a.logits && live && c < 10) a.logits[(long long)(r0 + r) * 10 + c] = z;
+    float mx = z;
 #pragma unroll
-    for (int o = 4; o > 0; o >>= 1) {
-      lsum += __shfl_xor(lsum, o, 8);
-      corr += __shfl_xor(corr, o, 8);
+    for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 16));
+    // first argmax: the lowest class of this image's 16-lane group holding the maximum
+    const unsigned long long hit = __ballot(z == mx);
+    const int am = __builtin_ctzll((hit >> (16 * (r & 3))) | 0x10000ull);
+    const float e = c < 10 ? __expf(z - mx) : 0.f;
+    float ssum = e;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) ssum += __shfl_xor(ssum, o, 16);
+    float lsum = (live && c == y) ? -(z - mx - __logf(ssum)) : 0.f;
+    float corr = (live && c == 0 && am == y) ? 1.f : 0.f;
+    if (live && c < 10) {
+      const float gv = (e * (1.f / ssum) - (c == y ? 1.f : 0.f)) * a.grad_scale;
+      Z3[r * LD3 + c] = f2bf(gv);
+      a.dz3T[(long long)c * a.ldt + r0 + r] = f2bf(gv);
     }
-    if (tid == 0) {
-      a.loss_part[2 * blockIdx.x] = lsum;
-      a.loss_part[2 * blockIdx.x + 1] = corr;
+    lsum = wave_sum(lsum);
+    corr = wave_sum(corr);
+    // per-wave sums into LG columns 14 / 15 of rows 0 and 4 (no lane reads a column >= 10)
+    if (lane == 0) {
+      LG[(w * 4) * 16 + 14] = lsum;
+      LG[(w * 4) * 16 + 15] = corr;
     }
   }
+  __syncthreads();
+  if (tid == 0) {
+    a.loss_part[2 * blockIdx.x] = LG[14] + LG[4 * 16 + 14];
+    a.loss_part[2 * blockIdx.x + 1] = LG[15] + LG[4 * 16 + 15];
+  }
+  // dense-1 data-gradient weights (64 VGPRs per lane): loaded after the loss, whose shuffles would
+  // otherwise push the live fragments past the 128-register budget; the loads overlap dense-3 / dense-2
+  // backward
+  DenseFrags<4, ccdiv(25, NW)> g1;
+  dense_load(g1, a.d1wt, 25);
   __syncthreads();
   LN_STAMP(5);
   dense_bwd(g3, Z3, LD3, ZR, 84, H2, LD2, Z2, LD2, a.dz2T, a.ldt, r0, rows);
@@ -524,10 +546,14 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
           bf16x8 o;
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = ((cd[k] >> (8 * e)) & 255u) == (unsigned)d ? dp[k][e] : (bf16)0.f;
-          st8(DC2 + (dc2_row(img * 100 + win * 4 + d) * 16 + 8 * nh), o);
+          st8(DC2 + (dc2_row(img * DC2_RS + win * 4 + d) * 16 + 8 * nh), o);
         }
       }
     }
+  }
+  if (tid < IMG * 8) {  // the 4 zero rows of every image block (after the overlaid H0 / codes were read)
+    const int img = tid >> 3, rr = (tid >> 1) & 3, nh = tid & 1;
+    st8(DC2 + (dc2_row(img * DC2_RS + 100 + rr) * 16 + 8 * nh), zero8());
   }
   __syncthreads();
   LN_STAMP(7);
@@ -553,19 +579,24 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
     f32x4 acc[KT];
 #pragma unroll
     for (int k = 0; k < KT; ++k) acc[k] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 5
-    for (int s = 0; s < 25; ++s) {
+    // the GEMM's M runs over the padded rows (26 steps of 32; the zero rows add nothing).  The bias
+    // column reads the ones block by an offset select (a pointer select compiled to a branch).
+    const unsigned ko = (unsigned)OFF_K;  // KO: 16 bf16 ones
+#pragma unroll 2
+    for (int s = 0; s < NM / 32; ++s) {
       const int mA = 32 * s + 8 * g + q;
       // dc2_row(mA) and dc2_row(mA + 4): both rows lie in 8-row block 4 s + g
       const int sx = (4 * s + g) & 7;
       const bf16x8 av = cat8(tr_read(DC2 + (mA ^ sx) * 16 + 4 * p), tr_read(DC2 + ((mA + 4) ^ sx) * 16 + 4 * p));
-      const bf16* pb0 = P1 + (int)PX[mA] * 8;
-      const bf16* pb1 = P1 + (int)PX[mA + 4] * 8;
+      const unsigned pb0 = (unsigned)OFF_P1 + 16u * (unsigned)PX[mA];
+      const unsigned pb1 = (unsigned)OFF_P1 + 16u * (unsigned)PX[mA + 4];
 #pragma unroll
       for (int k = 0; k < KT; ++k) {
         if (k < ntile) {
-          const bf16x4 t0 = tr_read(ones[k] ? KO : pb0 + toff[k]);
-          const bf16x4 t1 = tr_read(ones[k] ? KO : pb1 + toff[k]);
+          const unsigned o0 = ones[k] ? ko : pb0 + 2u * (unsigned)toff[k];
+          const unsigned o1 = ones[k] ? ko : pb1 + 2u * (unsigned)toff[k];
+          const bf16x4 t0 = tr_read(reinterpret_cast<const bf16*>(smem + o0));
+          const bf16x4 t1 = tr_read(reinterpret_cast<const bf16*>(smem + o1));
           acc[k] = mfma16x16x32(av, cat8(t0, t1), acc[k]);
         }
       }
@@ -597,12 +628,25 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
       const int img = m / 98, rem = m - 98 * (m / 98);
       const uint4 tv = *reinterpret_cast<const uint4*>(FT + (rem * 2 + (g >> 1)) * 16);
       const unsigned tw[4] = {tv.x, tv.y, tv.z, tv.w};
-      const bf16* dbase = DC2 + 8 * (g & 1);
+      // A row of step s: LDS byte offset computed branch-free (a t == 255 tap reads the zero block), read
+      // three steps ahead of its MFMA (a select of two addresses compiled to an exec-mask branch, and
+      // every read waited for its own data right before the MFMA: the LDS latency of all 15 steps was
+      // exposed in series)
+      // the table holds the row t inside the image (100, a zero padding row, for "no tap")
+      const unsigned dbase = (unsigned)OFF_DC2 + 16u * (unsigned)(g & 1);
+      const int rb = img * DC2_RS;
+      auto ldA = [&](int st) -> bf16x8 {
+        const int t = (int)((tw[st >> 2] >> (8 * (st & 3))) & 255u);
+        return *reinterpret_cast<const bf16x8*>(smem + dbase + 32u * (unsigned)dc2_row(rb + t));
+      };
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      bf16x8 a0 = ldA(0), a1 = ldA(1), a2 = ldA(2);
 #pragma unroll
       for (int s = 0; s < 15; ++s) {
-        const unsigned t = (tw[s >> 2] >> (8 * (s & 3))) & 255u;
-        acc = mfma16x16x32(ld8(t == 255u ? KZ : dbase + dc2_row(img * 100 + (int)t) * 16), bd[s], acc);
+        acc = mfma16x16x32(a0, bd[s], acc);
+        a0 = a1;
+        a1 = a2;
+        if (s + 3 < 15) a2 = ldA(s + 3);
       }
       if (c < 6) {
 #pragma unroll
@@ -644,9 +688,12 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
       bsh[T] = kx >> 1;
       bkind[T] = tap < 25 ? 0 : (tap == 25 ? 1 : 2);
     }
-    bf16x8 ones8;
+    unsigned bkeep[2], bset[2];  // word = (loaded & keep) | set: input columns, the ones column, zeros
 #pragma unroll
-    for (int e = 0; e < 8; ++e) ones8[e] = (bf16)1.f;
+    for (int T = 0; T < 2; ++T) {
+      bkeep[T] = bkind[T] == 0 ? 0xffffffffu : 0u;
+      bset[T] = bkind[T] == 1 ? 0x3f803f80u : 0u;  // two bf16 ones
+    }
 #pragma unroll 2
     for (int rp = w; rp < IMG * 14; rp += NT / 64) {
       const int img = rp / 14, py = rp - 14 * (rp / 14);
@@ -682,8 +729,11 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
             o[j] = bsh[T] == 1 ? sv[j + 1] : sv[j];
             o[j] = bsh[T] == 2 ? sv[j + 2] : o[j];
           }
-          bf16x8 bv = __builtin_bit_cast(bf16x8, uint4{o[0], o[1], o[2], o[3]});
-          bv = bkind[T] == 0 ? bv : (bkind[T] == 1 ? ones8 : zero8());
+          // the bias column of ones / the zero columns by per-lane masks (a select between the loaded
+          // words and constant vectors compiled to exec-mask branches in the loop)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = (o[j] & bkeep[T]) | bset[T];
+          const bf16x8 bv = __builtin_bit_cast(bf16x8, uint4{o[0], o[1], o[2], o[3]});
           acc[T] = mfma16x16x32(dy ? a1 : a0, bv, acc[T]);
         }
       }

@@ -756,14 +756,16 @@ _LENET_TABLES = {}
 def lenet_tables(device):
     """Constant index tables of the fused LeNet-5 kernel (built once per device):
     ``ftab`` [98][2][16] u8 — conv2 data gradient: for pool1 pixel pair (y, X2), k-half and step s, the
-    window-major conv2 output row it gathers (255 = outside the 10x10 map);
-    ``pxtab`` [800] i16 — conv2 output row (image, window, position) -> pool1 pixel index;
+    window-major conv2 output row t it gathers inside the image (outside the 10x10 map: 100, a zero
+    padding row of the image's 104-row block);
+    ``pxtab`` [832] i16 — padded conv2 output row (image * 104 + window * 4 + position) -> pool1 pixel
+    index (padding rows 100..103 of an image: its pixel 0, read against a zero gradient);
     ``frag`` — scratch for the per-step conv weight fragments (written by the kernel's prep launch)."""
     key = str(device)
     if key not in _LENET_TABLES:
         import numpy as np
 
-        ft = np.full((98, 2, 16), 255, dtype=np.uint8)
+        ft = np.full((98, 2, 16), 100, dtype=np.uint8)
         for yx in range(98):
             y, X2 = divmod(yx, 7)
             for hf in range(2):
@@ -775,9 +777,12 @@ def lenet_tables(device):
                     oy, ox = y - ky, 2 * X2 + 1 - u
                     if 0 <= oy < 10 and 0 <= ox < 10:
                         ft[yx, hf, s] = (((oy >> 1) * 5 + (ox >> 1)) << 2) + ((oy & 1) << 1) + (ox & 1)
-        px = np.zeros(800, dtype=np.int16)
-        for m in range(800):
-            img, q = divmod(m, 100)
+        px = np.zeros(832, dtype=np.int16)
+        for m in range(832):
+            img, q = divmod(m, 104)
+            if q >= 100:
+                px[m] = img * 196
+                continue
             win, d = divmod(q, 4)
             py, pxx = divmod(win, 5)
             px[m] = img * 196 + (2 * py + (d >> 1)) * 14 + 2 * pxx + (d & 1)

@@ -42,9 +42,9 @@ class DataParallelTrainer:
         # FedSGD count barrier on the device (reference FederatedServer: a version is the mean of
         # minUpdatesPerVersion microbatch gradients of the current version, federated_server.ts:73-90,
         # default 20, utils.ts:188-191).  K microbatches per version, split over the ranks as evenly as they
-        # go (rank r takes K // W + (r < K % W) of them, as one step over their concatenated rows); each
-        # microbatch's gradient is its mean loss's, the step sums them, the exchange sums over the ranks and
-        # the update scales by 1 / K.  Every gradient of a version is computed on that version, so the
+        # go (rank r takes K // W + (r < K % W) of them, as one step over their concatenated rows); every
+        # row's loss gradient is scaled by 1 / (K * microbatch), the step sums them and the exchange sums
+        # over the ranks: the mean of the K microbatch means.  Every gradient of a version is computed on that version, so the
         # reference's stale-upload drop never has anything to drop.  None: one microbatch per rank (K = W).
         self.min_updates = None if min_updates_per_version in (None, 0) else int(min_updates_per_version)
         if self.min_updates is not None and self.min_updates < self.world:
@@ -98,9 +98,9 @@ class DataParallelTrainer:
         net.store.set_hyper(lr, momentum, weight_decay, grad_scale=self._grad_scale())
 
     def _grad_scale(self) -> float:
-        """The update's gradient scale: the mean over the ranks' gradients (1 / W), or over the K
-        microbatches of a FedSGD version (1 / K)."""
-        return 1.0 / (self.min_updates if self.min_updates is not None else self.world)
+        """The update's gradient scale: the mean over the ranks' gradients (1 / W).  A FedSGD version of K
+        microbatches folds its 1 / K into the loss scale (bind_dataset), so the update takes the plain sum."""
+        return 1.0 if self.min_updates is not None else 1.0 / self.world
 
     # ------------------------------------------------------------------ buckets
     def _build_buckets(self):
@@ -260,7 +260,8 @@ class DataParallelTrainer:
         unfused step (compute + one-shot all-reduce or RCCL + SGD).  The engine state is restored after.
         Reference semantics held here: the synchronous server's mean of the K uploaded gradients
         (/root/reference/src/server/federated_server.ts:92-117)."""
-        if self.fused_selftest or self.world == 1 or not self._step_all_reduces or not _diag_on("fused_selftest"):
+        if (self.fused_selftest or self.world == 1 or not self._step_all_reduces or not _diag_on("fused_selftest")
+                or getattr(self, "data", None) is None):
             return
         if not (self.fused_update and getattr(self.net, "lenet_fused", False) and self.net.store.lenet_frag is not None
                 and self.p2p is not None and getattr(self.p2p.comm, "ll_slots", 0) >= 256
@@ -377,7 +378,10 @@ class DataParallelTrainer:
         self.data, self.labels, self.scale = data, labels, scale
         self.micro_B = batch_size
         if self.min_updates is not None:
-            self.net.loss_scale = 1.0 / batch_size  # the step gradient = sum of its microbatches' means
+            # the version's gradient = the mean of its K microbatches' mean-loss gradients: every row's loss
+            # gradient scaled by 1 / (K * microbatch) in the train kernel (the same bf16 rounding as one
+            # step on the union batch) and the ranks' sums added unscaled
+            self.net.loss_scale = 1.0 / (batch_size * self.min_updates)
             batch_size *= self.micro_per_rank[self.rank]
         self.B = batch_size
         net = self.net
@@ -389,6 +393,10 @@ class DataParallelTrainer:
             self.xb = ops.GatherRef(data, self.idx, scale, net.input_shape)
         else:
             self.xb = net.x_buf
+        # collective (every rank binds its dataset): the real-kernel check of the fused multi-rank step runs
+        # here, never hidden inside a step that only some ranks might take
+        self.fused_selftest = {}
+        self._verify_fused_exchange()
 
     # ------------------------------------------------------------------ preprocess callbacks on the device path
     def add_preprocess_callback(self, cb):
@@ -533,7 +541,6 @@ class DataParallelTrainer:
         """One training step on the next batch of the bound index stream."""
         if self._index_stream is None:
             raise RuntimeError("bind_index_stream() first")
-        self._verify_fused_exchange()
         self.steps += 1
         _beat(self.steps)
         if self.graph_mode == "none":
@@ -550,7 +557,6 @@ class DataParallelTrainer:
         """One training step on dataset rows ``idx`` (device int64 [B])."""
         if self._index_stream is not None:
             raise RuntimeError("an index stream is bound: use step()")
-        self._verify_fused_exchange()
         self.idx.copy_(idx, non_blocking=True)
         self.steps += 1
         if self.graph_mode == "none":
@@ -568,7 +574,6 @@ class DataParallelTrainer:
         The ranks agree on every attempt (MIN of a success flag, outside any capture): if capture
         fails on one rank only, all of them fall back together, so no rank replays a graph whose
         collectives / one-shot epochs its peers never issue."""
-        self._verify_fused_exchange()
         while True:
             ok = True
             try:

@@ -158,10 +158,14 @@ def test_functional_chain_model_loads_like_sequential():
     na, nb = Net(la, sa, device="cpu", seed=7), Net(lb, sb, device="cpu", seed=7)
     x = torch.rand(3, 6, 6, 1)
     torch.testing.assert_close(na.predict(x), nb.predict(x))
-    # a join (two inputs) is refused with a clear error
+    # a non-merge layer with two inputs is refused with a clear error (joins go through merge layers,
+    # tests/test_keras_graph.py), and so is a cycle
     bad = json.loads(json.dumps(func))
-    bad["config"]["layers"][-1]["inbound_nodes"] = [[["l0", 0, 0, {}], ["l1", 0, 0, {}]]]
+    bad["config"]["layers"][-1]["inbound_nodes"] = [[["l0", 0, 0, {}], ["inp", 0, 0, {}]]]
     with pytest.raises(NotImplementedError):
+        layers_from_keras(bad)
+    bad["config"]["layers"][-1]["inbound_nodes"] = [[["l1", 0, 0, {}]]]
+    with pytest.raises(ValueError):
         layers_from_keras(bad)
 
 

@@ -43,7 +43,7 @@ def _check(gnet, ref_grads, ref_stats, stats, tol_rel=0.03, min_cos=0.999):
     assert abs(float(stats[1]) - float(ref_stats[1])) <= 2
 
 
-@pytest.mark.parametrize("B", [128, 100])
+@pytest.mark.parametrize("B", [128, 100, 160, 96])
 def test_fused_lenet_matches_cpu_reference(B):
     g, c = _nets(B)
     x, y = _batch(B)
