@@ -56,9 +56,10 @@ constexpr int OFF_K = OFF_C1 + IMG * 196 * 4;       // 32 B ones (bf16)
 constexpr int OFF_PX = OFF_K + 32;                  // conv2 output row -> P1 pixel [832] u16 (host-built)
 constexpr int OFF_FT = OFF_PX + NM * 2;             // conv2 dgrad table [98][2][16] u8 (host-built)
 constexpr int OFF_W = OFF_FT + 98 * 2 * 16;         // f32: b1 [6], b2 [16], then 8 int labels
+constexpr int OFF_KZ = OFF_W + 128;                 // 32 B zeros (phase G's zero columns)
 // the union starts where it always did (OFF_XS1's bank offset from Xs, and so phase A / G's
 // conflict-free reads, depend on it)
-constexpr int OFF_U = OFF_W + 128 + 32;
+constexpr int OFF_U = OFF_KZ + 32;
 // phases A and G: input shifted left by one pixel; 32 bytes into the union so that its rows sit 24 banks
 // from Xs's (the A-operand reads of phase A and the B-operand reads of phase G are then conflict-free:
 // scripts/lds_sim.py)
@@ -78,13 +79,14 @@ constexpr int OFF_DC2 = OFF_U;                      // [832][16] bf16 conv2 outp
 constexpr int U_DC2 = NM * 16 * 2;
 constexpr int OFF_RED = OFF_XS1 + XS_ELEMS * 2;     // [4][16][32] f32 cross-wave conv1 wgrad sums
 constexpr int U_G = 32 + XS_ELEMS * 2 + 4 * 16 * 32 * 4;
-// conv2 output-gradient rows r (padded numbering) are stored at row r ^ ((r >> 3) & 7): the gathered
-// A-operand reads of phase F then spread over the banks (scripts/lds_sim.py); 104-row image blocks keep
-// every 8-row block inside one image.  The padding rows hold zeros: phase F's "no tap" entries read one.
-__device__ __forceinline__ int dc2_row(int r) { return r ^ ((r >> 3) & 7); }
+// conv2 output-gradient row t of an image is stored at row dc2_swz(t) of the image's 104-row block: the
+// gathered A-operand reads of phase F then spread over the banks (scripts/lds_sim.py), and phase F's
+// table holds the swizzled row itself (no per-step swizzle arithmetic).  The padding rows hold zeros:
+// phase F's "no tap" entries read one (dc2_swz(100) = 96).
+__device__ __forceinline__ int dc2_swz(int t) { return t ^ ((t >> 3) & 7); }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int LDS_BYTES = OFF_U + cmax(cmax(U_DENSE, U_DC2), U_G);
-static_assert(OFF_U == OFF_C1 + IMG * 196 * 4 + 128 + 98 * 2 * 16 + 800 * 2 + 128 && OFF_U % 16 == 0 && OFF_H1 % 16 == 0 && OFF_ZR % 16 == 0 && OFF_C2 % 16 == 0 && OFF_RED % 16 == 0 &&
+static_assert(OFF_U == OFF_C1 + IMG * 196 * 4 + 128 + 98 * 2 * 16 + 800 * 2 + 128 && OFF_U % 16 == 0 && OFF_KZ % 16 == 0 && OFF_H1 % 16 == 0 && OFF_ZR % 16 == 0 && OFF_C2 % 16 == 0 && OFF_RED % 16 == 0 &&
                   OFF_PX % 16 == 0 && OFF_W % 16 == 0,
               "LDS carve must stay 16-byte aligned");
 static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
@@ -288,7 +290,10 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   bf16* DC2 = reinterpret_cast<bf16*>(smem + OFF_DC2);
   float* RED = reinterpret_cast<float*>(smem + OFF_RED);
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15, g = lane >> 4;
+  // the wave index in an SGPR: loops and tile selects over it become scalar branches (tid >> 6 was
+  // treated as divergent: exec-mask branches, each waiting for all LDS reads in flight)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), i = lane & 15,
+            g = lane >> 4;
   const int r0 = lenet_img_group(blockIdx.x, gridDim.x) * IMG;
   const int rows = min(IMG, a.B - r0);
   const long long nb = gridDim.x;
@@ -310,6 +315,8 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = (bf16)1.f;
     st8(KO + 8 * tid, o);
+  } else if (tid < 4) {
+    st8(reinterpret_cast<bf16*>(smem + OFF_KZ) + 8 * (tid - 2), z8);
   }
   if (tid < 6) WS[tid] = a.b1[tid];
   if (tid < 16) WS[6 + tid] = a.b2[tid];
@@ -546,14 +553,14 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
           bf16x8 o;
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = ((cd[k] >> (8 * e)) & 255u) == (unsigned)d ? dp[k][e] : (bf16)0.f;
-          st8(DC2 + (dc2_row(img * DC2_RS + win * 4 + d) * 16 + 8 * nh), o);
+          st8(DC2 + ((img * DC2_RS + dc2_swz(win * 4 + d)) * 16 + 8 * nh), o);
         }
       }
     }
   }
   if (tid < IMG * 8) {  // the 4 zero rows of every image block (after the overlaid H0 / codes were read)
     const int img = tid >> 3, rr = (tid >> 1) & 3, nh = tid & 1;
-    st8(DC2 + (dc2_row(img * DC2_RS + 100 + rr) * 16 + 8 * nh), zero8());
+    st8(DC2 + ((img * DC2_RS + dc2_swz(100 + rr)) * 16 + 8 * nh), zero8());
   }
   __syncthreads();
   LN_STAMP(7);
@@ -580,26 +587,53 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
 #pragma unroll
     for (int k = 0; k < KT; ++k) acc[k] = {0.f, 0.f, 0.f, 0.f};
     // the GEMM's M runs over the padded rows (26 steps of 32; the zero rows add nothing).  The bias
-    // column reads the ones block by an offset select (a pointer select compiled to a branch).
+    // column reads the ones block by an offset select (a pointer select compiled to a branch).  Step
+    // s + 1's dC2 rows and pixel indices are read during step s: the P1 reads of a step depend on its
+    // pixel-index reads, a second LDS round trip that was exposed once per step.
     const unsigned ko = (unsigned)OFF_K;  // KO: 16 bf16 ones
-#pragma unroll 2
-    for (int s = 0; s < NM / 32; ++s) {
+    auto ldAv = [&](int s) -> bf16x8 {
       const int mA = 32 * s + 8 * g + q;
-      // dc2_row(mA) and dc2_row(mA + 4): both rows lie in 8-row block 4 s + g
-      const int sx = (4 * s + g) & 7;
-      const bf16x8 av = cat8(tr_read(DC2 + (mA ^ sx) * 16 + 4 * p), tr_read(DC2 + ((mA + 4) ^ sx) * 16 + 4 * p));
-      const unsigned pb0 = (unsigned)OFF_P1 + 16u * (unsigned)PX[mA];
-      const unsigned pb1 = (unsigned)OFF_P1 + 16u * (unsigned)PX[mA + 4];
+      // rows mA and mA + 4 lie in the 8-row block b = 4 s + g, block b - 13 img of image img = b / 13
+      const int b = 4 * s + g, sx = (b - 13 * ((b * 79) >> 10)) & 7;
+      return cat8(tr_read(DC2 + (mA ^ sx) * 16 + 4 * p), tr_read(DC2 + ((mA + 4) ^ sx) * 16 + 4 * p));
+    };
+    auto step = [&](const bf16x8& av, unsigned px0, unsigned px1) {
+      const unsigned pb0 = (unsigned)OFF_P1 + 16u * px0, pb1 = (unsigned)OFF_P1 + 16u * px1;
+      // every wave runs KT tiles (a wave with fewer real ones computes a ones-column tile it drops): all
+      // reads of the step are in flight before its first MFMA
+      bf16x4 t0[KT], t1[KT];
 #pragma unroll
       for (int k = 0; k < KT; ++k) {
-        if (k < ntile) {
-          const unsigned o0 = ones[k] ? ko : pb0 + 2u * (unsigned)toff[k];
-          const unsigned o1 = ones[k] ? ko : pb1 + 2u * (unsigned)toff[k];
-          const bf16x4 t0 = tr_read(reinterpret_cast<const bf16*>(smem + o0));
-          const bf16x4 t1 = tr_read(reinterpret_cast<const bf16*>(smem + o1));
-          acc[k] = mfma16x16x32(av, cat8(t0, t1), acc[k]);
-        }
+        const unsigned o0 = ones[k] ? ko : pb0 + 2u * (unsigned)toff[k];
+        const unsigned o1 = ones[k] ? ko : pb1 + 2u * (unsigned)toff[k];
+        t0[k] = tr_read(reinterpret_cast<const bf16*>(smem + o0));
+        t1[k] = tr_read(reinterpret_cast<const bf16*>(smem + o1));
       }
+#pragma unroll
+      for (int k = 0; k < KT; ++k) acc[k] = mfma16x16x32(av, cat8(t0[k], t1[k]), acc[k]);
+    };
+    // two register sets, steps 2j (set a) and 2j + 1 (set b): each step's reads were issued one step
+    // earlier (no register rotation, which waited for the prefetched data)
+    static_assert(NM / 32 % 2 == 0, "phase E pairs its steps");
+    const unsigned short* pxl = PX + 8 * g + q;
+    bf16x8 ava = ldAv(0);
+    unsigned pxa0 = pxl[0], pxa1 = pxl[4];
+#pragma unroll 1
+    for (int s = 0; s < NM / 32; s += 2) {
+      // (scheduling barriers keep the prefetches where they are: the scheduler otherwise hoists every LDS
+      // read to the top of the loop body and waits for all of them there)
+      const bf16x8 avb = ldAv(s + 1);
+      const unsigned pxb0 = pxl[32 * (s + 1)], pxb1 = pxl[32 * (s + 1) + 4];
+      __builtin_amdgcn_sched_barrier(0);
+      step(ava, pxa0, pxa1);
+      __builtin_amdgcn_sched_barrier(0);
+      const int sn = s + 2 < NM / 32 ? s + 2 : s;  // the last pair re-reads its own rows (unused)
+      ava = ldAv(sn);
+      pxa0 = pxl[32 * sn];
+      pxa1 = pxl[32 * sn + 4];
+      __builtin_amdgcn_sched_barrier(0);
+      step(avb, pxb0, pxb1);
+      __builtin_amdgcn_sched_barrier(0);
     }
     // D[row = output channel 4g + r][col i = (tap 2T + (i >> 3), channel i & 7)]
 #pragma unroll
@@ -632,12 +666,12 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
       // three steps ahead of its MFMA (a select of two addresses compiled to an exec-mask branch, and
       // every read waited for its own data right before the MFMA: the LDS latency of all 15 steps was
       // exposed in series)
-      // the table holds the row t inside the image (100, a zero padding row, for "no tap")
-      const unsigned dbase = (unsigned)OFF_DC2 + 16u * (unsigned)(g & 1);
-      const int rb = img * DC2_RS;
+      // the table holds the stored row dc2_swz(t) inside the image's block (96, a zero padding row, for
+      // "no tap")
+      const unsigned dbase = (unsigned)OFF_DC2 + 16u * (unsigned)(g & 1) + 32u * (unsigned)(img * DC2_RS);
       auto ldA = [&](int st) -> bf16x8 {
-        const int t = (int)((tw[st >> 2] >> (8 * (st & 3))) & 255u);
-        return *reinterpret_cast<const bf16x8*>(smem + dbase + 32u * (unsigned)dc2_row(rb + t));
+        const unsigned t = (tw[st >> 2] >> (8 * (st & 3))) & 255u;
+        return *reinterpret_cast<const bf16x8*>(smem + dbase + 32u * t);
       };
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       bf16x8 a0 = ldA(0), a1 = ldA(1), a2 = ldA(2);
@@ -651,10 +685,9 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
       if (c < 6) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+          // pixel (image, y, 2 X2 + bcol) of row mm = (image * 14 + y) * 7 + X2: index 2 mm + bcol
           const int mm = 16 * mt + 4 * g + r;
-          const int im = mm / 98, rm = mm - 98 * (mm / 98);
-          const int y = rm / 7, X2 = rm - 7 * (rm / 7);
-          P1[((im * 14 + y) * 14 + 2 * X2 + bcol) * 8 + c] = f2bf(acc[r]);
+          P1[(2 * mm + bcol) * 8 + c] = f2bf(acc[r]);
         }
       }
     }
@@ -673,27 +706,27 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     const int ca = i < 6 ? i : 5;
     // B of lane (tap, g) = input row y + ky, columns 8g + kx .. + 7 (odd kx: the shifted copy, so the
-    // start is a whole dword): two aligned 16-byte reads of columns 8g .. 8g + 15 and a per-lane dword
-    // select (sh = kx >> 1) -- 16-byte reads are conflict-free here where four dword reads were not.
-    // Branch-free: every lane reads (taps >= 25 read tap 0's words), then the bias column of ones and
-    // the zero columns replace the value.
+    // start is a whole dword): four dwords from a dword-aligned address (ds_read2_b32 pairs: no 16-byte
+    // alignment needed, no per-lane dword select).  The bias column (tap 25) reads the ones block, taps
+    // 26 .. 31 the zero block: one address select per read, no value masking.
     constexpr int kXs1 = (OFF_XS1 - OFF_XS) / 2;  // Xs1 - Xs in elements
-    int boff[2], bsh[2], bkind[2];                // kind: 0 input, 1 ones (bias column), 2 zeros
+    unsigned boff[2], bconst[2];
+    bool breal[2];
 #pragma unroll
     for (int T = 0; T < 2; ++T) {
       const int tap = 16 * T + i;
       const int tp = tap < 25 ? tap : 0;
       const int ky = tp / 5, kx = tp - 5 * (tp / 5);
-      boff[T] = ((kx & 1) ? kXs1 : 0) + ky * 32 + 8 * g;
-      bsh[T] = kx >> 1;
-      bkind[T] = tap < 25 ? 0 : (tap == 25 ? 1 : 2);
+      boff[T] = 2u * (unsigned)(((kx & 1) ? kXs1 : 0) + ky * 32 + 8 * g + 2 * (kx >> 1));  // bytes from Xs
+      breal[T] = tap < 25;
+      bconst[T] = tap == 25 ? (unsigned)OFF_K : (unsigned)OFF_KZ;
     }
-    unsigned bkeep[2], bset[2];  // word = (loaded & keep) | set: input columns, the ones column, zeros
+    // A: the 4 pool windows' dP1 values scattered by their argmax code (2 bits: position in the 2x2
+    // window): a dword of a0 / a1 holds the window's row dy = 0 / 1 pair, the value shifted to its x.
+    // Lanes past the 6 channels or the 14 windows take no value (code forced past 3).
+    unsigned cmask[4];
 #pragma unroll
-    for (int T = 0; T < 2; ++T) {
-      bkeep[T] = bkind[T] == 0 ? 0xffffffffu : 0u;
-      bset[T] = bkind[T] == 1 ? 0x3f803f80u : 0u;  // two bf16 ones
-    }
+    for (int wd = 0; wd < 4; ++wd) cmask[wd] = (4 * g + wd < 14 && i < 6) ? 0u : 4u;
 #pragma unroll 2
     for (int rp = w; rp < IMG * 14; rp += NT / 64) {
       const int img = rp / 14, py = rp - 14 * (rp / 14);
@@ -702,38 +735,25 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
       const uint2 cA = *reinterpret_cast<const uint2*>(C1 + p0);
       const uint2 cB = *reinterpret_cast<const uint2*>(C1 + p0 + 2);
       const unsigned cw[4] = {cA.x, cA.y, cB.x, cB.y};
-      bf16x8 a0, a1;
+      unsigned a0w[4], a1w[4];
 #pragma unroll
       for (int wd = 0; wd < 4; ++wd) {
-        const bool ok = 4 * g + wd < 14 && i < 6;
-        const unsigned code = (cw[wd] >> (3 * ca)) & 7u;
-        const bf16 pv = P1[(p0 + wd) * 8 + ca];  // in bounds for every lane (windows 14, 15 are the
-                                                 // next row's first two or the tail), masked below
-        const bf16 v = ok ? pv : (bf16)0.f;
-        a0[2 * wd] = code == 0u ? v : (bf16)0.f;
-        a0[2 * wd + 1] = code == 1u ? v : (bf16)0.f;
-        a1[2 * wd] = code == 2u ? v : (bf16)0.f;
-        a1[2 * wd + 1] = code == 3u ? v : (bf16)0.f;
+        const unsigned code = ((cw[wd] >> (3 * ca)) & 7u) | cmask[wd];
+        // in bounds for every lane (windows 14, 15 are the next row's first two or the tail)
+        const unsigned pv = *reinterpret_cast<const unsigned short*>(P1 + (p0 + wd) * 8 + ca);
+        const unsigned v = pv << ((code & 1u) << 4);
+        a0w[wd] = code == 0u || code == 1u ? v : 0u;
+        a1w[wd] = code == 2u || code == 3u ? v : 0u;
       }
+      const bf16x8 a0 = __builtin_bit_cast(bf16x8, uint4{a0w[0], a0w[1], a0w[2], a0w[3]});
+      const bf16x8 a1 = __builtin_bit_cast(bf16x8, uint4{a1w[0], a1w[1], a1w[2], a1w[3]});
 #pragma unroll
       for (int dy = 0; dy < 2; ++dy) {
-        const int y = 2 * py + dy;
+        const unsigned rowb = (unsigned)OFF_XS + 2u * (unsigned)(img * 1024 + (2 * py + dy) * 32);
 #pragma unroll
         for (int T = 0; T < 2; ++T) {
-          const uint4* bp = reinterpret_cast<const uint4*>(Xs + img * 1024 + y * 32 + boff[T]);
-          const uint4 c0 = bp[0], c1 = bp[1];
-          const unsigned sv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-          unsigned o[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            o[j] = bsh[T] == 1 ? sv[j + 1] : sv[j];
-            o[j] = bsh[T] == 2 ? sv[j + 2] : o[j];
-          }
-          // the bias column of ones / the zero columns by per-lane masks (a select between the loaded
-          // words and constant vectors compiled to exec-mask branches in the loop)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = (o[j] & bkeep[T]) | bset[T];
-          const bf16x8 bv = __builtin_bit_cast(bf16x8, uint4{o[0], o[1], o[2], o[3]});
+          const unsigned* bp = reinterpret_cast<const unsigned*>(smem + (breal[T] ? rowb + boff[T] : bconst[T]));
+          const bf16x8 bv = __builtin_bit_cast(bf16x8, uint4{bp[0], bp[1], bp[2], bp[3]});
           acc[T] = mfma16x16x32(dy ? a1 : a0, bv, acc[T]);
         }
       }

@@ -756,8 +756,8 @@ _LENET_TABLES = {}
 def lenet_tables(device):
     """Constant index tables of the fused LeNet-5 kernel (built once per device):
     ``ftab`` [98][2][16] u8 — conv2 data gradient: for pool1 pixel pair (y, X2), k-half and step s, the
-    window-major conv2 output row t it gathers inside the image (outside the 10x10 map: 100, a zero
-    padding row of the image's 104-row block);
+    stored row swz(t) = t ^ ((t >> 3) & 7) of the window-major conv2 output row t it gathers, inside the
+    image's 104-row block (outside the 10x10 map: swz(100) = 96, a zero padding row);
     ``pxtab`` [832] i16 — padded conv2 output row (image * 104 + window * 4 + position) -> pool1 pixel
     index (padding rows 100..103 of an image: its pixel 0, read against a zero gradient);
     ``frag`` — scratch for the per-step conv weight fragments (written by the kernel's prep launch)."""
@@ -765,7 +765,8 @@ def lenet_tables(device):
     if key not in _LENET_TABLES:
         import numpy as np
 
-        ft = np.full((98, 2, 16), 100, dtype=np.uint8)
+        swz = lambda t: t ^ ((t >> 3) & 7)  # noqa: E731  (csrc/lenet_fused.hip dc2_swz)
+        ft = np.full((98, 2, 16), swz(100), dtype=np.uint8)
         for yx in range(98):
             y, X2 = divmod(yx, 7)
             for hf in range(2):
@@ -776,7 +777,7 @@ def lenet_tables(device):
                     ky, u = divmod(P, 6)
                     oy, ox = y - ky, 2 * X2 + 1 - u
                     if 0 <= oy < 10 and 0 <= ox < 10:
-                        ft[yx, hf, s] = (((oy >> 1) * 5 + (ox >> 1)) << 2) + ((oy & 1) << 1) + (ox & 1)
+                        ft[yx, hf, s] = swz((((oy >> 1) * 5 + (ox >> 1)) << 2) + ((oy & 1) << 1) + (ox & 1))
         px = np.zeros(832, dtype=np.int16)
         for m in range(832):
             img, q = divmod(m, 104)

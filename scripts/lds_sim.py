@@ -18,17 +18,19 @@ OFF_XS = 0
 OFF_P1 = OFF_XS + XS_ELEMS * 2
 OFF_C1 = OFF_P1 + IMG * 196 * 16
 OFF_K = OFF_C1 + IMG * 196 * 4
-OFF_FT = OFF_K + 128
-OFF_PX = OFF_FT + 98 * 2 * 16
-OFF_W = OFF_PX + 800 * 2
-OFF_U = OFF_W + 128
+DC2_RS = 104
+NM = IMG * DC2_RS
+OFF_PX = OFF_K + 32
+OFF_FT = OFF_PX + NM * 2
+OFF_W = OFF_FT + 98 * 2 * 16
+OFF_U = OFF_W + 128 + 32
 OFF_XS1 = OFF_U + 32
 OFF_DC2 = OFF_U
 LD0, LD1, LD2, LD3 = 424, 136, 104, 40
 OFF_H0 = OFF_U
 OFF_ZR = OFF_U + IMG * LD0 * 2 + IMG * LD1 * 2 + IMG * LD2 * 2 + IMG * LD3 * 2 + IMG * LD2 * 2 + IMG * LD1 * 2
-KZ = OFF_K
-KO = OFF_K + 64
+KO = OFF_K
+KZ = OFF_W + 128
 
 B128_GROUPS = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
                list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32)),
@@ -98,9 +100,12 @@ def phase_a(ph):
 
 
 def pxtab():
-    px = np.zeros(800, dtype=np.int64)
-    for m in range(800):
-        img, q = divmod(m, 100)
+    px = np.zeros(NM, dtype=np.int64)
+    for m in range(NM):
+        img, q = divmod(m, DC2_RS)
+        if q >= 100:
+            px[m] = img * 196
+            continue
         win, d = divmod(q, 4)
         py, pxx = divmod(win, 5)
         px[m] = img * 196 + (2 * py + (d >> 1)) * 14 + 2 * pxx + (d & 1)
@@ -110,7 +115,7 @@ def pxtab():
 def phase_b(ph):
     PX = pxtab()
     for w in range(NW):
-        for mt in range(w, 50, NW):
+        for mt in range(w, NM // 16, NW):
             for s in range(7):
                 addr = []
                 for lane, i, g in lanes():
@@ -125,14 +130,15 @@ def phase_e(ph):
     KT = (13 + NW - 1) // NW
     for w in range(NW):
         ntile = (13 - w + NW - 1) // NW
-        for s in range(25):
+        for s in range(NM // 32):
             # A: two transposed reads of dC2
             for half in range(2):
                 addr = []
                 for lane, i, g in lanes():
                     q, p = (lane & 15) >> 2, lane & 3
                     mA = 32 * s + 8 * g + q + 4 * half
-                    addr.append(OFF_DC2 + 2 * (dc2_row(mA) * 16 + 4 * p))
+                    img, t = divmod(mA, DC2_RS)
+                    addr.append(OFF_DC2 + 2 * ((img * DC2_RS + dc2_swz(t)) * 16 + 4 * p))
                 ph.add("tr", addr)
             for k in range(KT):
                 if k >= ntile:
@@ -152,7 +158,7 @@ def phase_e(ph):
 
 
 def ftab():
-    ft = np.full((98, 2, 16), 255, dtype=np.int64)
+    ft = np.full((98, 2, 16), 100, dtype=np.int64)
     for yx in range(98):
         y, X2 = divmod(yx, 7)
         for hf in range(2):
@@ -167,8 +173,8 @@ def ftab():
     return ft
 
 
-def dc2_row(r):
-    return r ^ ((r >> 3) & 7)
+def dc2_swz(t):
+    return t ^ ((t >> 3) & 7)
 
 
 def phase_f(ph):
@@ -181,7 +187,7 @@ def phase_f(ph):
                     m = 16 * mt + i
                     img, rem = divmod(m, 98)
                     t = int(FT[rem, g >> 1, s])
-                    addr.append(KZ if t == 255 else OFF_DC2 + 2 * (dc2_row(img * 100 + t) * 16 + 8 * (g & 1)))
+                    addr.append(OFF_DC2 + 2 * ((img * DC2_RS + dc2_swz(t)) * 16 + 8 * (g & 1)))
                 ph.add("b128", addr)
 
 
@@ -201,17 +207,17 @@ def phase_g(ph):
             for dy in range(2):
                 y = 2 * py + dy
                 for T in range(2):
-                    for h in range(2):  # two aligned 16-byte reads per lane (dword select in registers)
+                    for h in range(2):  # two ds_read2_b32 (dwords 0, 1 and 2, 3) from a dword-aligned start
                         addr = []
                         for lane, i, g in lanes():
                             tap = 16 * T + i
                             if tap < 25:
                                 ky, kx = divmod(tap, 5)
-                                base = OFF_XS1 if kx & 1 else OFF_XS
-                                addr.append(base + 2 * (img * 1024 + y * 32 + ky * 32 + 8 * g) + 16 * h)
+                                base = (OFF_XS1 if kx & 1 else OFF_XS) + 2 * (img * 1024 + y * 32 + ky * 32 + 8 * g)
+                                addr.append(base + 4 * (kx >> 1) + 8 * h)
                             else:
-                                addr.append(None)
-                        ph.add("b128", addr)
+                                addr.append((KO if tap == 25 else KZ) + 8 * h)
+                        ph.add("b64", addr)
 
 
 def main():
