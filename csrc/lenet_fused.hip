@@ -308,7 +308,13 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
 #pragma unroll
   for (int f = 0; f < 15; ++f) bc[f] = frag[(FR_C1 + f) * 64 + lane];
   const bf16x8 z8 = zero8();
-  for (int e = tid; e < (OFF_K - OFF_XS) / 16; e += NT) st8(Xs + 8 * e, z8);  // Xs, P1 (pad channels), C1
+  // Xs, P1, C1.  P1's channel 6 holds ones: phase E's im2col column (tap 0, channel 6) is then all ones
+  // and gives the conv2 bias gradient (conv2's weights of channels 6, 7 are zero, phase F writes channels
+  // 0 .. 5 only, phase G reads them only)
+  bf16x8 one6 = z8;
+  one6[6] = (bf16)1.f;
+  for (int e = tid; e < (OFF_K - OFF_XS) / 16; e += NT)
+    st8(Xs + 8 * e, (e >= OFF_P1 / 16 && e < OFF_C1 / 16) ? one6 : z8);
   for (int e = tid; e < (LDS_BYTES - OFF_U) / 16; e += NT) st8(reinterpret_cast<bf16*>(smem + OFF_U) + 8 * e, z8);
   if (tid < 2) {
     bf16x8 o;
@@ -573,24 +579,20 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   for (int s = 0; s < 15; ++s) bd[s] = frag[(FR_DG + s) * 64 + lane];
   {
     const int q = (lane & 15) >> 2, p = lane & 3;
-    constexpr int KT = ccdiv(13, NW);  // column tiles per wave (13 tiles: taps 0..24 + the bias column)
-    int toff[KT];
-    bool ones[KT];
+    constexpr int KT = ccdiv(13, NW);  // column tiles per wave (13 tiles: taps 0..25, tap 25 unused)
+    int toff[KT];  // element offset of the lane's tap (taps >= 25: tap 0, its column is dropped)
 #pragma unroll
     for (int k = 0; k < KT; ++k) {
       const int tap = 2 * (w + NW * k) + (p >> 1);
-      ones[k] = tap >= 25;
-      toff[k] = tap < 25 ? ((tap / 5) * 14 + (tap - 5 * (tap / 5))) * 8 + 4 * (p & 1) : 0;
+      toff[k] = tap < 25 ? ((tap / 5) * 14 + (tap - 5 * (tap / 5))) * 8 + 4 * (p & 1) : 4 * (p & 1);
     }
     const int ntile = (13 - w + NW - 1) / NW;
     f32x4 acc[KT];
 #pragma unroll
     for (int k = 0; k < KT; ++k) acc[k] = {0.f, 0.f, 0.f, 0.f};
-    // the GEMM's M runs over the padded rows (26 steps of 32; the zero rows add nothing).  The bias
-    // column reads the ones block by an offset select (a pointer select compiled to a branch).  Step
-    // s + 1's dC2 rows and pixel indices are read during step s: the P1 reads of a step depend on its
+    // the GEMM's M runs over the padded rows (26 steps of 32; the zero rows add nothing).  Step s + 1's
+    // dC2 rows and pixel indices are read during step s: the P1 reads of a step depend on its
     // pixel-index reads, a second LDS round trip that was exposed once per step.
-    const unsigned ko = (unsigned)OFF_K;  // KO: 16 bf16 ones
     auto ldAv = [&](int s) -> bf16x8 {
       const int mA = 32 * s + 8 * g + q;
       // rows mA and mA + 4 lie in the 8-row block b = 4 s + g, block b - 13 img of image img = b / 13
@@ -598,16 +600,15 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
       return cat8(tr_read(DC2 + (mA ^ sx) * 16 + 4 * p), tr_read(DC2 + ((mA + 4) ^ sx) * 16 + 4 * p));
     };
     auto step = [&](const bf16x8& av, unsigned px0, unsigned px1) {
-      const unsigned pb0 = (unsigned)OFF_P1 + 16u * px0, pb1 = (unsigned)OFF_P1 + 16u * px1;
-      // every wave runs KT tiles (a wave with fewer real ones computes a ones-column tile it drops): all
-      // reads of the step are in flight before its first MFMA
+      const bf16* pb0 = P1 + 8 * px0;
+      const bf16* pb1 = P1 + 8 * px1;
+      // every wave runs KT tiles (a wave with fewer real ones computes a tile it drops): all reads of the
+      // step are in flight before its first MFMA
       bf16x4 t0[KT], t1[KT];
 #pragma unroll
       for (int k = 0; k < KT; ++k) {
-        const unsigned o0 = ones[k] ? ko : pb0 + 2u * (unsigned)toff[k];
-        const unsigned o1 = ones[k] ? ko : pb1 + 2u * (unsigned)toff[k];
-        t0[k] = tr_read(reinterpret_cast<const bf16*>(smem + o0));
-        t1[k] = tr_read(reinterpret_cast<const bf16*>(smem + o1));
+        t0[k] = tr_read(pb0 + toff[k]);
+        t1[k] = tr_read(pb1 + toff[k]);
       }
 #pragma unroll
       for (int k = 0; k < KT; ++k) acc[k] = mfma16x16x32(av, cat8(t0[k], t1[k]), acc[k]);
@@ -635,7 +636,8 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
       step(avb, pxb0, pxb1);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // D[row = output channel 4g + r][col i = (tap 2T + (i >> 3), channel i & 7)]
+    // D[row = output channel 4g + r][col i = (tap 2T + (i >> 3), channel i & 7)]; the bias gradient is
+    // column (tap 0, channel 6), P1's ones
 #pragma unroll
     for (int k = 0; k < KT; ++k) {
       if (k < ntile) {
@@ -645,7 +647,7 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
         for (int r = 0; r < 4; ++r) {
           const int n = 4 * g + r;
           if (tap < 25 && c < 6) part[(long long)(kLeNetPW2 + n * 150 + tap * 6 + c)] = acc[k][r];
-          else if (tap == 25 && c == 0) part[(long long)(kLeNetPB2 + n)] = acc[k][r];
+          else if (tap == 0 && c == 6) part[(long long)(kLeNetPB2 + n)] = acc[k][r];
         }
       }
     }
