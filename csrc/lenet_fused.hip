@@ -85,15 +85,21 @@ constexpr int U_G = 32 + XS_ELEMS * 2 + 4 * 16 * 32 * 4;
 // phase F's "no tap" entries read one (dc2_swz(100) = 96).
 __device__ __forceinline__ int dc2_swz(int t) { return t ^ ((t >> 3) & 7); }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int LDS_BYTES = OFF_U + cmax(cmax(U_DENSE, U_DC2), U_G);
-static_assert(OFF_U == OFF_C1 + IMG * 196 * 4 + 128 + 98 * 2 * 16 + 800 * 2 + 128 && OFF_U % 16 == 0 && OFF_KZ % 16 == 0 && OFF_H1 % 16 == 0 && OFF_ZR % 16 == 0 && OFF_C2 % 16 == 0 && OFF_RED % 16 == 0 &&
+// dense biases (f32: dense-1 [120], dense-2 [84], dense-3 [10]), staged in phase 0: read from LDS, a
+// bias load never waits behind the weight prefetches issued before it
+constexpr int OFF_DB = OFF_U + (cmax(cmax(U_DENSE, U_DC2), U_G) + 15) / 16 * 16;
+constexpr int OFF_ST = OFF_DB + 864;                // u64 [16] diagnostic phase clocks (LN_STAMP)
+constexpr int LDS_BYTES = OFF_ST + 128;
+static_assert(OFF_U == OFF_C1 + IMG * 196 * 4 + 128 + 98 * 2 * 16 + 800 * 2 + 128 && OFF_U % 16 == 0 && OFF_KZ % 16 == 0 && OFF_H1 % 16 == 0 && OFF_ZR % 16 == 0 && OFF_C2 % 16 == 0 && OFF_RED % 16 == 0 && OFF_DB % 16 == 0 && OFF_ST % 16 == 0 &&
                   OFF_PX % 16 == 0 && OFF_W % 16 == 0,
               "LDS carve must stay 16-byte aligned");
 static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
 
 typedef __bf16 bf16x4_vs __attribute__((__vector_size__(8)));
 
-// diagnostic per-phase clocks (scripts/lenetstamps.py): [grid][16] s_memtime after each phase's barrier
+// diagnostic per-phase clocks (scripts/lenetstamps.py): [grid][16] s_memtime after each phase's barrier,
+// kept in LDS and written out at the end (a global store mid-kernel makes the compiler's wait-count pass
+// wait for every load in flight at the next join, stamps or not)
 #define LN_STAMP(slot)                                                            \
   do {                                                                            \
     if (stamps) {                                                                 \
@@ -101,9 +107,28 @@ typedef __bf16 bf16x4_vs __attribute__((__vector_size__(8)));
       unsigned long long t_;                                                      \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
       __builtin_amdgcn_sched_barrier(0);                                          \
-      if (threadIdx.x == 0) stamps[blockIdx.x * 16 + (slot)] = t_;                \
+      if (threadIdx.x == 0) STMP[(slot)] = t_;                                    \
     }                                                                             \
   } while (0)
+
+// 16-lane (DPP row) reductions: every lane of the row gets the result (xor 1, xor 2, half-row mirror,
+// row mirror: four VALU data moves instead of four LDS permute round trips)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  return fmaxf(v, dpp_f<0x140>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  return v + dpp_f<0x140>(v);
+}
 
 __device__ __forceinline__ bf16x4 tr_read(const bf16* p) {
   auto* lp = (__attribute__((address_space(3))) bf16*)(const_cast<bf16*>(p));
@@ -300,13 +325,49 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   const bf16x8* __restrict__ frag = reinterpret_cast<const bf16x8*>(a.frag);
   float* part = a.conv_part + (long long)blockIdx.x * kLeNetConvStride;  // this workgroup's partials
   unsigned long long* const stamps = a.stamps;
+  unsigned long long* const STMP = reinterpret_cast<unsigned long long*>(smem + OFF_ST);
   LN_STAMP(0);
 
   // ---------------------------------------------------------------- phase 0: zero fills, staging
-  // conv1 B fragments of this step (lenet_prep_kernel): in flight while the images load
+  // Global loads in dependency order (a wait for one load also waits for every load issued before it):
+  // first the indices, then the tables / biases, the conv1 fragments and, once its index is back, this
+  // thread's input row; everything lands in registers and is stored to LDS after the zero fills.
+  const int ximg = tid / 28, xrow = tid - 28 * (tid / 28);  // input row of this thread
+  const bool xload = tid < IMG * 28 && ximg < rows;
+  const bool lload = tid >= 256 && tid < 256 + IMG && tid - 256 < rows;  // label of image tid - 256
+  long long xsrc = 0, lsrc = 0;
+  if (xload) xsrc = a.idx ? a.idx[r0 + ximg] : (long long)(r0 + ximg);
+  if (lload) lsrc = a.idx ? a.idx[r0 + tid - 256] : (long long)(r0 + tid - 256);
+  uint4 tabv = {0u, 0u, 0u, 0u};
+  if (tid < 98 * 2) tabv = reinterpret_cast<const uint4*>(a.ftab)[tid];
+  else if (tid >= 264 && tid < 264 + NM / 8) tabv = reinterpret_cast<const uint4*>(a.pxtab)[tid - 264];
+  static_assert(98 * 2 <= 256 && 264 + NM / 8 <= 448 && 448 + 22 <= NT, "phase 0 staging thread ranges");
+  float biasv = 0.f, dbv = 0.f;
+  if (tid >= 448 && tid < 448 + 22) biasv = *(tid < 454 ? a.b1 + (tid - 448) : a.b2 + (tid - 454));
+  if (tid < 214) dbv = *(tid < 120 ? a.d1b + tid : (tid < 204 ? a.d2b + (tid - 120) : a.d3b + (tid - 204)));
+  // conv1 B fragments of this step (lenet_prep_kernel)
   bf16x8 bc[15];
 #pragma unroll
   for (int f = 0; f < 15; ++f) bc[f] = frag[(FR_C1 + f) * 64 + lane];
+  int lbl = 0;
+  if (lload) lbl = a.labels[lsrc < 0 ? 0 : (lsrc >= a.nrows ? a.nrows - 1 : lsrc)];
+  unsigned xv[14];
+  if (xload) {
+    const long long src = xsrc < 0 ? 0 : (xsrc >= a.nrows ? a.nrows - 1 : xsrc);
+    if (a.x_u8 != nullptr) {
+      const unsigned* p = reinterpret_cast<const unsigned*>(a.x_u8 + src * 784 + xrow * 28);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) xv[k] = p[k];
+    } else {
+      const uint2* p = reinterpret_cast<const uint2*>(a.x_bf + src * 784 + xrow * 28);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        const uint2 v = p[k];
+        xv[2 * k] = v.x;
+        xv[2 * k + 1] = v.y;
+      }
+    }
+  }
   const bf16x8 z8 = zero8();
   // Xs, P1, C1.  P1's channel 6 holds ones: phase E's im2col column (tap 0, channel 6) is then all ones
   // and gives the conv2 bias gradient (conv2's weights of channels 6, 7 are zero, phase F writes channels
@@ -315,7 +376,7 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   one6[6] = (bf16)1.f;
   for (int e = tid; e < (OFF_K - OFF_XS) / 16; e += NT)
     st8(Xs + 8 * e, (e >= OFF_P1 / 16 && e < OFF_C1 / 16) ? one6 : z8);
-  for (int e = tid; e < (LDS_BYTES - OFF_U) / 16; e += NT) st8(reinterpret_cast<bf16*>(smem + OFF_U) + 8 * e, z8);
+  for (int e = tid; e < (OFF_DB - OFF_U) / 16; e += NT) st8(reinterpret_cast<bf16*>(smem + OFF_U) + 8 * e, z8);
   if (tid < 2) {
     bf16x8 o;
 #pragma unroll
@@ -324,54 +385,32 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   } else if (tid < 4) {
     st8(reinterpret_cast<bf16*>(smem + OFF_KZ) + 8 * (tid - 2), z8);
   }
-  if (tid < 6) WS[tid] = a.b1[tid];
-  if (tid < 16) WS[6 + tid] = a.b2[tid];
-  // labels of the 8 images (dependent loads idx -> label: issued here, read by the loss phase)
+  if (tid < 98 * 2) reinterpret_cast<uint4*>(FT)[tid] = tabv;
+  else if (tid >= 264 && tid < 264 + NM / 8) reinterpret_cast<uint4*>(PX)[tid - 264] = tabv;
+  if (tid >= 448 && tid < 448 + 22) WS[tid - 448] = biasv;  // b1 [6], b2 [16]
+  float* DB = reinterpret_cast<float*>(smem + OFF_DB);
+  if (tid < 214) DB[tid] = dbv;
+  // labels of the 8 images (read by the loss phase)
   int* LBL = reinterpret_cast<int*>(WS + 24);
-  if (tid >= 64 && tid < 64 + IMG) {
-    const int r = tid - 64;
-    int y = 0;
-    if (r < rows) {
-      const long long src = a.idx ? a.idx[r0 + r] : (long long)(r0 + r);
-      y = a.labels[src < 0 ? 0 : (src >= a.nrows ? a.nrows - 1 : src)];
-      y = y < 0 ? 0 : (y > 9 ? 9 : y);
-    }
-    LBL[r] = y;
-  }
-  if (tid < 98 * 2) reinterpret_cast<uint4*>(FT)[tid] = reinterpret_cast<const uint4*>(a.ftab)[tid];
-  if (tid < NM / 8) reinterpret_cast<uint4*>(PX)[tid] = reinterpret_cast<const uint4*>(a.pxtab)[tid];
+  if (tid >= 256 && tid < 256 + IMG) LBL[tid - 256] = lbl < 0 ? 0 : (lbl > 9 ? 9 : lbl);
   __syncthreads();
   // input rows -> bf16, 2-pixel zero border ('same' padding)
-  if (tid < IMG * 28) {
-    const int img = tid / 28, y = tid - 28 * (tid / 28);
-    if (img < rows) {
-      long long src = a.idx ? a.idx[r0 + img] : (long long)(r0 + img);
-      src = src < 0 ? 0 : (src >= a.nrows ? a.nrows - 1 : src);
-      unsigned* dst = reinterpret_cast<unsigned*>(Xs + img * 1024 + (y + 2) * 32 + 2);
-      if (a.x_u8 != nullptr) {
-        const unsigned* p = reinterpret_cast<const unsigned*>(a.x_u8 + src * 784 + y * 28);
-        unsigned v[7];
+  if (xload) {
+    unsigned* dst = reinterpret_cast<unsigned*>(Xs + ximg * 1024 + (xrow + 2) * 32 + 2);
+    if (a.x_u8 != nullptr) {
 #pragma unroll
-        for (int k = 0; k < 7; ++k) v[k] = p[k];
+      for (int k = 0; k < 7; ++k)
 #pragma unroll
-        for (int k = 0; k < 7; ++k)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const float f0 = (float)((v[k] >> (16 * h)) & 255u) * a.scale;
-            const float f1 = (float)((v[k] >> (16 * h + 8)) & 255u) * a.scale;
-            const unsigned lo = __builtin_bit_cast(unsigned short, f2bf(f0));
-            const unsigned hi = __builtin_bit_cast(unsigned short, f2bf(f1));
-            dst[2 * k + h] = lo | (hi << 16);
-          }
-      } else {
-        const uint2* p = reinterpret_cast<const uint2*>(a.x_bf + src * 784 + y * 28);
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {
-          const uint2 v = p[k];
-          dst[2 * k] = v.x;
-          dst[2 * k + 1] = v.y;
+        for (int h = 0; h < 2; ++h) {
+          const float f0 = (float)((xv[k] >> (16 * h)) & 255u) * a.scale;
+          const float f1 = (float)((xv[k] >> (16 * h + 8)) & 255u) * a.scale;
+          const unsigned lo = __builtin_bit_cast(unsigned short, f2bf(f0));
+          const unsigned hi = __builtin_bit_cast(unsigned short, f2bf(f1));
+          dst[2 * k + h] = lo | (hi << 16);
         }
-      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 14; ++k) dst[k] = xv[k];
     }
   }
   __syncthreads();
@@ -421,12 +460,14 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   LN_STAMP(2);
 
   // ---------------------------------------------------------------- phase B: conv2 + ReLU + pool
-  DenseFrags<13, ccdiv(8, NW)> f1;  // dense-1 weights: L2 latency hidden behind conv2
+  // conv2 fragments first, then the dense-1 weights (L2 latency hidden behind conv2): a wait for the
+  // fragments then never waits for the dense-1 loads
+  bf16x8 bw[7];
+#pragma unroll
+  for (int s = 0; s < 7; ++s) bw[s] = frag[(FR_C2 + s) * 64 + lane];
+  DenseFrags<13, ccdiv(8, NW)> f1;
   dense_load(f1, a.d1w, 8);
   {
-    bf16x8 bw[7];
-#pragma unroll
-    for (int s = 0; s < 7; ++s) bw[s] = frag[(FR_C2 + s) * 64 + lane];
     int toff[7];
 #pragma unroll
     for (int s = 0; s < 7; ++s) {
@@ -471,54 +512,50 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   DenseFrags<3, 1> f3;
   dense_load(f2, a.d2w, 6);
   dense_load(f3, a.d3w, 1);
-  dense_fwd(f1, H0, LD0, ZR, a.d1b, 120, true, H1, LD1, nullptr, a.h1T, a.ldt, r0, rows);
+  dense_fwd(f1, H0, LD0, ZR, DB, 120, true, H1, LD1, nullptr, a.h1T, a.ldt, r0, rows);
   __syncthreads();
   DenseFrags<1, ccdiv(6, NW)> g3;
   DenseFrags<3, ccdiv(8, NW)> g2;
   dense_load(g3, a.d3wt, 6);
   dense_load(g2, a.d2wt, 8);
-  dense_fwd(f2, H1, LD1, ZR, a.d2b, 84, true, H2, LD2, nullptr, a.h2T, a.ldt, r0, rows);
+  dense_fwd(f2, H1, LD1, ZR, DB + 120, 84, true, H2, LD2, nullptr, a.h2T, a.ldt, r0, rows);
   __syncthreads();
-  dense_fwd(f3, H2, LD2, ZR, a.d3b, 10, false, nullptr, 0, LG, nullptr, a.ldt, r0, rows);
+  dense_fwd(f3, H2, LD2, ZR, DB + 204, 10, false, nullptr, 0, LG, nullptr, a.ldt, r0, rows);
   __syncthreads();
   LN_STAMP(4);
   // softmax-CE of the 8 images, 16 lanes per image (class c = lane & 15; waves 0 and 1): max / first
-  // argmax / sum of exponentials by shuffles inside the 16-lane group, one gradient element per lane
+  // argmax / sum of exponentials by DPP row reductions, one gradient element per lane; the image's loss
+  // and hit go to LG columns 14 / 15 of its row (no lane reads a column >= 10)
   if (tid < IMG * 16) {
     const int r = tid >> 4, c = tid & 15;
     const bool live = r < rows;
     const int y = LBL[r];
     const float z = c < 10 ? LG[r * 16 + c] : -INFINITY;
     if (a.logits && live && c < 10) a.logits[(long long)(r0 + r) * 10 + c] = z;
-    float mx = z;
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 16));
+    const float mx = row16_max(z);
     // first argmax: the lowest class of this image's 16-lane group holding the maximum
     const unsigned long long hit = __ballot(z == mx);
     const int am = __builtin_ctzll((hit >> (16 * (r & 3))) | 0x10000ull);
     const float e = c < 10 ? __expf(z - mx) : 0.f;
-    float ssum = e;
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) ssum += __shfl_xor(ssum, o, 16);
-    float lsum = (live && c == y) ? -(z - mx - __logf(ssum)) : 0.f;
-    float corr = (live && c == 0 && am == y) ? 1.f : 0.f;
+    const float ssum = row16_sum(e);
     if (live && c < 10) {
       const float gv = (e * (1.f / ssum) - (c == y ? 1.f : 0.f)) * a.grad_scale;
       Z3[r * LD3 + c] = f2bf(gv);
       a.dz3T[(long long)c * a.ldt + r0 + r] = f2bf(gv);
     }
-    lsum = wave_sum(lsum);
-    corr = wave_sum(corr);
-    // per-wave sums into LG columns 14 / 15 of rows 0 and 4 (no lane reads a column >= 10)
-    if (lane == 0) {
-      LG[(w * 4) * 16 + 14] = lsum;
-      LG[(w * 4) * 16 + 15] = corr;
-    }
+    if (c == y) LG[r * 16 + 14] = live ? -(z - mx - __logf(ssum)) : 0.f;
+    if (c == 15) LG[r * 16 + 15] = (live && am == y) ? 1.f : 0.f;
   }
   __syncthreads();
   if (tid == 0) {
-    a.loss_part[2 * blockIdx.x] = LG[14] + LG[4 * 16 + 14];
-    a.loss_part[2 * blockIdx.x + 1] = LG[15] + LG[4 * 16 + 15];
+    float ls = 0.f, cs = 0.f;
+#pragma unroll
+    for (int r = 0; r < IMG; ++r) {
+      ls += LG[r * 16 + 14];
+      cs += LG[r * 16 + 15];
+    }
+    a.loss_part[2 * blockIdx.x] = ls;
+    a.loss_part[2 * blockIdx.x + 1] = cs;
   }
   // dense-1 data-gradient weights (64 VGPRs per lane): loaded after the loss, whose shuffles would
   // otherwise push the live fragments past the 128-register budget; the loads overlap dense-3 / dense-2
@@ -788,6 +825,7 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
     }
   }
   LN_STAMP(10);
+  if (stamps && tid < 11) stamps[blockIdx.x * 16 + tid] = STMP[tid];
 }
 
 // Conv weights of this step as MFMA B fragments: one block (csrc/lenet_frag.h).  Only launched when
