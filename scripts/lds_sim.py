@@ -125,7 +125,8 @@ def phase_b(ph):
                 ph.add("b128", addr)
 
 
-def phase_e(ph):
+def phase_e(ph, ph2=None):
+    """A (dC2) reads into ph, the im2col B (P1) reads into ph2 (default: ph too)."""
     PX = pxtab()
     KT = (13 + NW - 1) // NW
     for w in range(NW):
@@ -140,21 +141,17 @@ def phase_e(ph):
                     img, t = divmod(mA, DC2_RS)
                     addr.append(OFF_DC2 + 2 * ((img * DC2_RS + dc2_swz(t)) * 16 + 4 * p))
                 ph.add("tr", addr)
-            for k in range(KT):
-                if k >= ntile:
-                    continue
+            for k in range(KT):  # every wave runs KT tiles (taps >= 25 read tap 0's pixel, dropped)
                 for half in range(2):
                     addr = []
                     for lane, i, g in lanes():
                         q, p = (lane & 15) >> 2, lane & 3
                         mA = 32 * s + 8 * g + q + 4 * half
                         tap = 2 * (w + NW * k) + (p >> 1)
-                        if tap >= 25:
-                            addr.append(KO)
-                        else:
-                            toff = ((tap // 5) * 14 + tap % 5) * 8 + 4 * (p & 1)
-                            addr.append(OFF_P1 + 2 * (int(PX[mA]) * 8 + toff))
-                    ph.add("tr", addr)
+                        tp = tap if tap < 25 else 0
+                        toff = ((tp // 5) * 14 + tp % 5) * 8 + 4 * (p & 1)
+                        addr.append(OFF_P1 + 2 * (int(PX[mA]) * 8 + toff))
+                    (ph2 if ph2 is not None else ph).add("tr", addr)
 
 
 def ftab():
@@ -226,8 +223,17 @@ def main():
                      ("E conv2 wgrad (tr reads)", phase_e), ("F conv2 dgrad (A reads)", phase_f),
                      ("G conv1 wgrad", phase_g)]:
         ph = Phase(name)
-        fn(ph)
+        if fn is phase_e:
+            ph_b = Phase("  of which im2col (P1) reads")
+            fn(ph, ph_b)
+            ph.cyc += ph_b.cyc
+            ph.ideal += ph_b.ideal
+            ph.n += ph_b.n
+        else:
+            fn(ph)
         c, k = ph.report()
+        if fn is phase_e:
+            ph_b.report()
         tot += c
         conf += k
     print(f"{'modelled total':<28} {'':13} LDS cycles {tot:7d}  conflict {conf:7d} ({100.0 * conf / tot:5.1f} %)")
