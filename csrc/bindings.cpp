@@ -666,6 +666,96 @@ void bn_apply_py(torch::Tensor x, torch::Tensor y, torch::Tensor gamma, torch::T
   check_hip(dfa::bn_apply(a, cur_stream()), "bn_apply");
 }
 
+// statistics + apply in one launch (training forward): y = act(bn(x) [+ r | + bn_r(r)]); the generation
+// word of the in-launch hand-off is counter[64]
+void bn_fwd_fused_py(torch::Tensor x, torch::Tensor y, torch::Tensor gamma, torch::Tensor beta, torch::Tensor mean,
+                     torch::Tensor invstd, c10::optional<torch::Tensor> run_mean, c10::optional<torch::Tensor> run_var,
+                     c10::optional<torch::Tensor> r, c10::optional<torch::Tensor> rgamma,
+                     c10::optional<torch::Tensor> rbeta, c10::optional<torch::Tensor> rmean,
+                     c10::optional<torch::Tensor> rinvstd, torch::Tensor ws, torch::Tensor counter, int64_t M,
+                     int64_t C, bool relu, double momentum, double eps) {
+  TORCH_CHECK(dfa::bn_fused_ok((int)C), "bn_fwd_fused: C must be a multiple of 8 (<= 1024)");
+  bn_check_act(x, M * C, "x");
+  bn_check_act(y, M * C, "y");
+  for (auto* t : {&gamma, &beta, &mean, &invstd}) bn_check_vec(*t, C, "bn vector");
+  const bool run = run_mean.has_value() && run_mean->defined();
+  if (run) {
+    bn_check_vec(*run_mean, C, "run_mean");
+    TORCH_CHECK(run_var.has_value() && run_var->defined(), "run_var required with run_mean");
+    bn_check_vec(*run_var, C, "run_var");
+  }
+  bn_check_stats_ws(ws, counter, M, C);
+  TORCH_CHECK(counter.numel() >= 65, "bn_fwd_fused: counter needs 65 words (generation at 64)");
+  TORCH_CHECK(ws.numel() >= (1008 + 63) * 2 * C, "bn_fwd_fused: workspace needs (1008 + 63) x 2C floats");
+  dfa::BnStatsArgs a{};
+  a.x = (const dfa::bf16*)x.data_ptr();
+  a.mean_out = mean.data_ptr<float>();
+  a.invstd_out = invstd.data_ptr<float>();
+  a.run_mean = run ? run_mean->data_ptr<float>() : nullptr;
+  a.run_var = run ? run_var->data_ptr<float>() : nullptr;
+  a.ws = ws.data_ptr<float>();
+  a.counter = reinterpret_cast<unsigned*>(counter.data_ptr<int>());
+  a.M = (int)M; a.C = (int)C; a.momentum = (float)momentum; a.eps = (float)eps;
+  dfa::BnApplyArgs p{};
+  p.x = a.x;
+  p.y = (dfa::bf16*)y.data_ptr();
+  p.gamma = gamma.data_ptr<float>();
+  p.beta = beta.data_ptr<float>();
+  p.mean = a.mean_out;
+  p.invstd = a.invstd_out;
+  if (r.has_value() && r->defined()) {
+    bn_check_act(*r, M * C, "residual");
+    p.r = (const dfa::bf16*)r->data_ptr();
+    if (rgamma.has_value() && rgamma->defined()) {
+      for (auto* t : {&rgamma, &rbeta, &rmean, &rinvstd}) {
+        TORCH_CHECK(t->has_value() && (*t)->defined(), "residual BN needs gamma, beta, mean, invstd");
+        bn_check_vec(**t, C, "residual bn vector");
+      }
+      p.rgamma = rgamma->data_ptr<float>();
+      p.rbeta = rbeta->data_ptr<float>();
+      p.rmean = rmean->data_ptr<float>();
+      p.rinvstd = rinvstd->data_ptr<float>();
+    }
+  }
+  p.M = (int)M; p.C = (int)C; p.relu = relu ? 1 : 0; p.eval = 0; p.eps = (float)eps;
+  check_hip(dfa::bn_fwd_fused(a, p, a.counter + 64, cur_stream()), "bn_fwd_fused");
+}
+
+// backward statistics + dx in one launch; generation word counter[64]
+void bn_bwd_fused_py(torch::Tensor x, c10::optional<torch::Tensor> mask, torch::Tensor dy, torch::Tensor dx,
+                     torch::Tensor gamma, torch::Tensor mean, torch::Tensor invstd, torch::Tensor dgamma,
+                     torch::Tensor dbeta, torch::Tensor coef, torch::Tensor ws, torch::Tensor counter, int64_t M,
+                     int64_t C, double gscale) {
+  TORCH_CHECK(dfa::bn_fused_ok((int)C), "bn_bwd_fused: C must be a multiple of 8 (<= 1024)");
+  bn_check_act(x, M * C, "x");
+  bn_check_act(dy, M * C, "dy");
+  bn_check_act(dx, M * C, "dx");
+  if (mask.has_value() && mask->defined()) bn_check_act(*mask, M * C, "mask");
+  bn_check_vec(gamma, C, "gamma");
+  bn_check_vec(mean, C, "mean");
+  bn_check_vec(invstd, C, "invstd");
+  bn_check_vec(dgamma, C, "dgamma");
+  bn_check_vec(dbeta, C, "dbeta");
+  bn_check_vec(coef, 3 * C, "coef");
+  bn_check_stats_ws(ws, counter, M, C);
+  TORCH_CHECK(counter.numel() >= 65, "bn_bwd_fused: counter needs 65 words (generation at 64)");
+  TORCH_CHECK(ws.numel() >= (1008 + 63) * 2 * C, "bn_bwd_fused: workspace needs (1008 + 63) x 2C floats");
+  dfa::BnStatsArgs a{};
+  a.x = (const dfa::bf16*)x.data_ptr();
+  a.mask = cptr<dfa::bf16>(mask);
+  a.dy = (const dfa::bf16*)dy.data_ptr();
+  a.gamma = gamma.data_ptr<float>();
+  a.mean = mean.data_ptr<float>();
+  a.invstd = invstd.data_ptr<float>();
+  a.dgamma = dgamma.data_ptr<float>();
+  a.dbeta = dbeta.data_ptr<float>();
+  a.coef = coef.data_ptr<float>();
+  a.ws = ws.data_ptr<float>();
+  a.counter = reinterpret_cast<unsigned*>(counter.data_ptr<int>());
+  a.M = (int)M; a.C = (int)C; a.gscale = (float)gscale;
+  check_hip(dfa::bn_bwd_fused(a, (dfa::bf16*)dx.data_ptr(), a.counter + 64, cur_stream()), "bn_bwd_fused");
+}
+
 void bn_dx_py(torch::Tensor x, c10::optional<torch::Tensor> mask, torch::Tensor dy, torch::Tensor dx,
               torch::Tensor coef, int64_t M, int64_t C) {
   bn_check_act(x, M * C, "x");
@@ -1877,6 +1967,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_stats_bwd", &bn_stats_bwd_py, "BN backward statistics: dgamma, dbeta and dx coefficients");
   m.def("bn_apply", &bn_apply_py, "BN normalize (+ residual join, + ReLU)");
   m.def("bn_dx", &bn_dx_py, "BN input gradient dx = k1*g + k2*x + k3");
+  m.def("bn_fwd_fused", &bn_fwd_fused_py, "BN training forward: statistics + apply in one launch");
+  m.def("bn_bwd_fused", &bn_bwd_fused_py, "BN backward: statistics + dx in one launch");
   m.def("bn_stats_grid", &dfa::bn_stats_grid, "partial-slab count of a BN statistics launch");
   m.def("convpool_fwd", &convpool_fwd_py, "fused conv+bias+relu+maxpool2x2 (pooled map + argmax codes)");
   m.def("convpool_wgrad", &convpool_wgrad_py, "weight gradient through the fused conv+pool", py::arg("x"),

@@ -51,9 +51,11 @@ __device__ __forceinline__ bool bn_last_arriver(unsigned* counter, unsigned n, i
 }
 
 // MODE 0: s += x, q += x*x.   MODE 1: g = dy * relu'(mask), xh = (x - mean) * invstd; s += g, q += g*xh.
-template <int MODE, bool VEC>
-__global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
-  __shared__ __attribute__((aligned(16))) float lsq[4096];
+// The statistics body; returns true in the one workgroup that finalised (the last arriver of the last
+// group).  FUSED: every workgroup reaches the end (no early return), so that it can wait for the
+// finalisation and run the apply pass of the same launch.
+template <int MODE, bool VEC, bool FUSED>
+__device__ __forceinline__ bool bn_stats_body(const BnStatsArgs& a, float* lsq) {
   __shared__ int last;
   float* ls = lsq;
   float* lq = lsq + 2048;
@@ -155,7 +157,7 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
   const int gbeg = grp * BN_GROUP, gn = min(BN_GROUP, G - gbeg);
   const int ngrp = cdiv(G, BN_GROUP);
   float* gslab = a.ws + (long long)G * ncol;  // [ngrp][2C]
-  if (!bn_last_arriver(a.counter + 1 + grp, (unsigned)gn, &last)) return;
+  if (!bn_last_arriver(a.counter + 1 + grp, (unsigned)gn, &last)) return false;
   for (int col = t; col < ncol; col += 256) {
     float v[BN_GROUP];
 #pragma unroll
@@ -167,7 +169,7 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
   }
 
   // ---- level 2: the last group reducer sums the group slabs in fp64 and finalises
-  if (!bn_last_arriver(a.counter, (unsigned)ngrp, &last)) return;
+  if (!bn_last_arriver(a.counter, (unsigned)ngrp, &last)) return false;
   for (int c = t; c < C; c += 256) {
     double sv = 0.0, qv = 0.0;
     for (int g0 = 0; g0 < ngrp; g0 += BN_GROUP) {
@@ -190,8 +192,8 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
       const double m = sv / M;
       double var = qv / M - m * m;
       if (var < 0.0) var = 0.0;
-      a.mean_out[c] = (float)m;
-      a.invstd_out[c] = (float)(1.0 / sqrt(var + (double)a.eps));
+      st_sc1(a.mean_out + c, (float)m);  // write-through: a fused apply pass reads them in this launch
+      st_sc1(a.invstd_out + c, (float)(1.0 / sqrt(var + (double)a.eps)));
       if (a.run_mean) {
         const double unb = M > 1 ? var * M / (M - 1) : var;
         a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * m);
@@ -202,9 +204,110 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
       a.dgamma[c] = (float)qv * a.gscale;
       const double isd = a.invstd[c], gam = a.gamma[c], m = a.mean[c];
       const double k1 = gam * isd;
-      a.coef[c] = (float)k1;
-      a.coef[C + c] = (float)(-k1 * isd * qv / M);
-      a.coef[2 * C + c] = (float)(k1 * (m * isd * qv / M - sv / M));
+      st_sc1(a.coef + c, (float)k1);
+      st_sc1(a.coef + C + c, (float)(-k1 * isd * qv / M));
+      st_sc1(a.coef + 2 * C + c, (float)(k1 * (m * isd * qv / M - sv / M)));
+    }
+  }
+  return true;
+}
+
+template <int MODE, bool VEC>
+__global__ void __launch_bounds__(256) bn_stats_kernel(BnStatsArgs a) {
+  __shared__ __attribute__((aligned(16))) float lsq[4096];
+  bn_stats_body<MODE, VEC, false>(a, lsq);
+}
+
+// Statistics and the streaming pass in ONE launch (C % 8 == 0): every workgroup computes its partials,
+// the last arriver finalises as above and bumps the generation word; the others wait for it (all
+// workgroups of the launch are resident: G <= 1008 workgroups of 256 threads) and then stream over the
+// same rows they reduced (mostly still in their XCD's L2).  Forward: y = act(bn(x) [+ r | + bn_r(r)]);
+// backward: dx = k1 * g + k2 * x + k3.  The finalised per-channel values are read write-through.
+// gen: a word that only ever increments (no reset between launches or graph replays).
+template <int MODE, int RES>
+__global__ void __launch_bounds__(256, 4) bn_fused_kernel(BnStatsArgs a, BnApplyArgs p, bf16* __restrict__ dx,
+                                                       unsigned* gen) {
+  __shared__ __attribute__((aligned(16))) float lsq[4096];
+  __shared__ unsigned g0;
+  if (threadIdx.x == 0) g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();  // the generation is read before this workgroup's arrival can complete the count
+  const bool fin = bn_stats_body<MODE, true, true>(a, lsq);
+  if (fin) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the finalised values are written through
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    if (threadIdx.x == 0) {
+      // bounded: a launch that could not make every workgroup resident ends (wrong, not hung)
+      for (unsigned it = 0; it < (1u << 24); ++it) {
+        if (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != g0) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+  }
+  const int C = a.C, M = a.M;
+  const int cpr = C / 8, rpp = 256 / cpr;
+  const int t = threadIdx.x, chunk = t % cpr, rsub = t / cpr;
+  if (rsub >= rpp) return;
+  const int c0 = chunk * 8;
+  float k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (MODE == 0) {
+      const float m = ld_sc1(a.mean_out + c0 + j), is = ld_sc1(a.invstd_out + c0 + j);
+      k1[j] = p.gamma[c0 + j] * is;
+      k2[j] = p.beta[c0 + j] - m * k1[j];
+      k3[j] = 0.f;
+      if (RES == 2) {
+        const float ra = p.rgamma[c0 + j] * p.rinvstd[c0 + j];
+        k3[j] = ra;
+      }
+    } else {
+      k1[j] = ld_sc1(a.coef + c0 + j);
+      k2[j] = ld_sc1(a.coef + C + c0 + j);
+      k3[j] = ld_sc1(a.coef + 2 * C + c0 + j);
+    }
+  }
+  float rb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) rb[j] = RES == 2 ? p.rbeta[c0 + j] - p.rmean[c0 + j] * k3[j] : 0.f;
+  // the rows this thread reduced, U at a time: every load of a round in flight before the first store
+  constexpr int U = MODE == 0 ? 8 : 4;  // backward: three tensors per row (x, dy, mask) within 128 VGPRs
+  const long long step = (long long)gridDim.x * rpp;
+  for (long long r = (long long)blockIdx.x * rpp + rsub; r < M; r += U * step) {
+    bf16x8 xv[U], v1[U], v2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long rr = r + u * step;
+      const long long o = (rr < M ? rr : r) * C + c0;
+      xv[u] = *reinterpret_cast<const bf16x8*>(a.x + o);
+      if (MODE == 0 && RES) v1[u] = *reinterpret_cast<const bf16x8*>(p.r + o);
+      if (MODE == 1) {
+        v1[u] = *reinterpret_cast<const bf16x8*>(a.dy + o);
+        if (a.mask) v2[u] = *reinterpret_cast<const bf16x8*>(a.mask + o);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long rr = r + u * step;
+      if (rr >= M) break;
+      const long long o = rr * C + c0;
+      bf16x8 out;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (MODE == 0) {
+          float v = (float)xv[u][j] * k1[j] + k2[j];
+          if (RES == 1) v += (float)v1[u][j];
+          if (RES == 2) v += (float)v1[u][j] * k3[j] + rb[j];
+          if (p.relu) v = fmaxf(v, 0.f);
+          out[j] = f2bf(v);
+        } else {
+          const float g = (a.mask && !((float)v2[u][j] > 0.f)) ? 0.f : (float)v1[u][j];
+          out[j] = f2bf(k1[j] * g + k2[j] * (float)xv[u][j] + k3[j]);
+        }
+      }
+      *reinterpret_cast<bf16x8*>((MODE == 0 ? p.y : dx) + o) = out;
     }
   }
 }
@@ -396,6 +499,58 @@ hipError_t bn_stats(const BnStatsArgs& a, int mode, hipStream_t st) {
       hipLaunchKernelGGL((bn_stats_kernel<1, false>), dim3(G), dim3(256), 0, st, a);
   }
   return hipGetLastError();
+}
+
+bool bn_fused_ok(int C) { return bn_vec(C) && C <= 1024; }
+
+// fused launches: ~8 rows per thread (one round of loads per phase), at most 1008 workgroups of 256
+// threads (4 per CU: every workgroup is resident for the in-launch hand-off; 1 + 63 ticket words, the
+// generation word is word 64)
+static int bn_fused_grid(int M, int C) {
+  int g = cdiv(M, bn_rows_per_pass(C, true) * 4);
+  return g < 1 ? 1 : (g > 1008 ? 1008 : g);
+}
+
+// workgroups of kernel K the device holds at once (occupancy x CUs, queried once): the fused launch's
+// grid never exceeds it, so that every workgroup is resident while the others wait for the hand-off
+template <typename K>
+static int bn_resident_cap(K kernel) {
+  static int cap = -1;
+  if (cap < 0) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess) per_cu = 1;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 1;
+    // three quarters of the device: other streams' kernels (a concurrent all-reduce, a side-stream
+    // branch) may hold CUs; the wait is bounded besides (a launch that still could not place every
+    // workgroup ends slow, not hung)
+    cap = per_cu * cus * 3 / 4;
+    if (cap < 1) cap = 1;
+  }
+  return cap;
+}
+
+template <int MODE, int RES>
+static hipError_t bn_fused_launch(const BnStatsArgs& a, const BnApplyArgs& p, bf16* dx, unsigned* gen, hipStream_t st) {
+  int G = bn_fused_grid(a.M, a.C);
+  const int cap = bn_resident_cap(bn_fused_kernel<MODE, RES>);
+  if (G > cap) G = cap;
+  hipLaunchKernelGGL((bn_fused_kernel<MODE, RES>), dim3(G), dim3(256), 0, st, a, p, dx, gen);
+  return hipGetLastError();
+}
+
+hipError_t bn_fwd_fused(const BnStatsArgs& a, const BnApplyArgs& p, unsigned* gen, hipStream_t st) {
+  if (!bn_fused_ok(a.C) || a.M <= 0 || p.C != a.C || p.M != a.M || p.eval || !gen) return hipErrorInvalidValue;
+  const int res = p.r == nullptr ? 0 : (p.rgamma == nullptr ? 1 : 2);
+  if (res == 0) return bn_fused_launch<0, 0>(a, p, nullptr, gen, st);
+  if (res == 1) return bn_fused_launch<0, 1>(a, p, nullptr, gen, st);
+  return bn_fused_launch<0, 2>(a, p, nullptr, gen, st);
+}
+
+hipError_t bn_bwd_fused(const BnStatsArgs& a, bf16* dx, unsigned* gen, hipStream_t st) {
+  if (!bn_fused_ok(a.C) || a.M <= 0 || !dx || !gen) return hipErrorInvalidValue;
+  BnApplyArgs p{};
+  return bn_fused_launch<1, 0>(a, p, dx, gen, st);
 }
 
 hipError_t bn_apply(const BnApplyArgs& a, hipStream_t st) {

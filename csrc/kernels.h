@@ -221,6 +221,11 @@ hipError_t bn_stats(const BnStatsArgs& a, int mode, hipStream_t st);  // mode 0 
 hipError_t bn_apply(const BnApplyArgs& a, hipStream_t st);
 hipError_t bn_dx(const bf16* x, const bf16* mask, const bf16* dy, bf16* dx, const float* coef, int M, int C,
                  hipStream_t st);
+// statistics + apply (forward) / statistics + dx (backward) in one launch (C % 8 == 0, training mode);
+// gen: a monotonically increasing generation word (any value to start, never reset)
+bool bn_fused_ok(int C);
+hipError_t bn_fwd_fused(const BnStatsArgs& a, const BnApplyArgs& p, unsigned* gen, hipStream_t st);
+hipError_t bn_bwd_fused(const BnStatsArgs& a, bf16* dx, unsigned* gen, hipStream_t st);
 
 // fused Conv2D(+bias+ReLU)+MaxPool2x2 for small channel counts (convpool.hip)
 // ---- fused dense head (csrc/mlphead.hip)

@@ -23,6 +23,10 @@ Python switches (default in brackets):
   proj_overlap [0]         ResNet projection shortcut on a side stream (in order is faster with the halo
                            kernels: 87.0 k vs 85.0 k images/s, profiles/r3/resnet18_b256_inorder_ab.txt)
   concurrent_backward [0]  head weight gradients on side streams (measured slower)
+  bn_fused [0]             BatchNorm statistics and the apply / dx pass in one launch (in-launch hand-off to
+                           the resident workgroups).  Correct (tests/test_kernels_gpu.py), but the hand-off
+                           chain stays and the streaming pass runs at the statistics grid: ResNet-18 B=256
+                           83.4 k vs 85.0 k images/s (profiles/r4/resnet18_bn_fused_ab.txt)
   bn_epilogue [0]          BatchNorm statistics finalised inside the producing conv launches instead of
                            separate statistics passes (correct, but the write-through + ticket tail each
                            conv workgroup then pays costs more than the passes: ResNet-18 B=256 72.3 k vs
@@ -33,7 +37,8 @@ from __future__ import annotations
 import os
 
 _DEFAULTS = {"lenet_fused": 1, "lenet_fused_update": 1, "async_fused": 1, "kcnn_fused": 1, "khead_fused": 1, "fold_dropout": 1,
-             "multistep": 1, "fused_selftest": 1, "wgrad_overlap": 0, "proj_overlap": 0, "concurrent_backward": 0, "bn_epilogue": 0}
+             "multistep": 1, "fused_selftest": 1, "wgrad_overlap": 0, "proj_overlap": 0, "concurrent_backward": 0, "bn_epilogue": 0,
+             "bn_fused": 0}
 
 
 def diag(name: str) -> int:

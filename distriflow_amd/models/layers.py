@@ -521,8 +521,24 @@ class BatchNorm(Layer):
 
     _stats_ready = False
 
+    def fused_forward(self, x, out, residual=None, residual_bn=None, relu=None) -> bool:
+        """Training statistics + apply in one launch when the fused kernel covers this shape (the
+        statistics were not already produced by the conv epilogue); False: nothing launched."""
+        if self._stats_ready or not ops.bn_fused_ok(self.C, x.device):
+            return False
+        self.x = x
+        st = self.store
+        rbn = residual_bn.affine(True) if residual_bn is not None else None
+        ops.bn_fwd_fused(x.reshape(-1, self.C), out.view(-1, self.C), st[f"{self.name}/gamma"], st[f"{self.name}/beta"],
+                         self.mean, self.invstd, self.run_mean, self.run_var, self.ws.bn, self.counter[0],
+                         self.relu if relu is None else relu,
+                         residual.reshape(-1, self.C) if residual is not None else None, rbn, self.momentum, self.eps)
+        return True
+
     def forward(self, x, training):
         self.x = x
+        if training and self.fused_forward(x, self.out):
+            return self.out
         if training and not self._stats_ready:
             self.stats(x)
         self._stats_ready = False
@@ -682,9 +698,6 @@ class ResidualBlock(Layer):
         h = self.bn1.forward(h, training)
         h = self.conv2.forward(h, training, bn=self.bn2)
         self.bn2.x = h
-        if training and not self.bn2._stats_ready:
-            self.bn2.stats(h)
-        self.bn2._stats_ready = False
         r, rbn = x, None
         if self.proj is not None:
             if pev is not None:
@@ -692,7 +705,13 @@ class ResidualBlock(Layer):
             else:
                 p = self._proj_forward(x, training)
             r, rbn = p, self.proj_bn
-        # one streaming pass: out = relu(bn2(h) + shortcut), shortcut = x or proj_bn(proj(x))
+        # out = relu(bn2(h) + shortcut), shortcut = x or proj_bn(proj(x)): bn2's statistics and this
+        # streaming pass in one launch when the fused kernel covers the shape
+        if training and self.bn2.fused_forward(h, self.out, residual=r, residual_bn=rbn, relu=True):
+            return self.out
+        if training and not self.bn2._stats_ready:
+            self.bn2.stats(h)
+        self.bn2._stats_ready = False
         self.bn2.apply(h, self.out, training, residual=r, residual_bn=rbn, relu=True)
         return self.out
 

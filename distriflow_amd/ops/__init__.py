@@ -612,6 +612,26 @@ def bn_apply(x2d, y2d, gamma, beta, mean, invstd, relu=False, residual=None, res
     return y2d
 
 
+def bn_fused_ok(C: int, device) -> bool:
+    """Statistics + streaming pass in one launch (csrc/bn.hip bn_fused_kernel): GPU, C % 8 == 0."""
+    from ..diagnostics import on as diag_on
+
+    return torch.device(device).type == "cuda" and C % 8 == 0 and C <= 1024 and diag_on("bn_fused")
+
+
+def bn_fwd_fused(x2d, y2d, gamma, beta, mean, invstd, run_mean, run_var, ws, counter, relu=False, residual=None,
+                 residual_bn=None, momentum=0.1, eps=1e-5):
+    """Training forward in one launch: batch statistics (mean, invstd, running statistics) and
+    y = act(bn(x) [+ r | + bn_r(r)]).  ``counter``: the layer's 65-word ticket row (word 64: generation)."""
+    M, C = x2d.shape
+    rg = rb = rm = ri = None
+    if residual_bn is not None:
+        rg, rb, rm, ri = residual_bn
+    _C().bn_fwd_fused(x2d, y2d, gamma, beta, mean, invstd, run_mean, run_var, residual, rg, rb, rm, ri, ws, counter,
+                      M, C, relu, momentum, eps)
+    return y2d
+
+
 def bn_dx(x2d, g2d, dx2d, coef):
     """dx = k1 g + k2 x + k3 per channel (coef [3][C] from a finalised backward statistics pass)."""
     M, C = x2d.shape
@@ -626,7 +646,9 @@ def bn_bwd(x2d, mask2d, dy2d, dx2d, gamma, mean, invstd, dgamma, dbeta, ws, coef
     """Backward of y = bn(x): dx, dgamma, dbeta (scaled by gscale) from dy; g = dy * (mask > 0) when a
     mask (relu' source) is given.  GPU: statistics launch (which also writes the dx coefficients) + dx pass."""
     M, C = x2d.shape
-    if x2d.is_cuda:
+    if x2d.is_cuda and bn_fused_ok(C, x2d.device) and counter.numel() >= BN_COUNTERS:
+        _C().bn_bwd_fused(x2d, mask2d, dy2d, dx2d, gamma, mean, invstd, dgamma, dbeta, coef, ws, counter, M, C, gscale)
+    elif x2d.is_cuda:
         _C().bn_stats_bwd(x2d, mask2d, dy2d, gamma, mean, invstd, dgamma, dbeta, coef, ws, counter, M, C, gscale)
         _C().bn_dx(x2d, mask2d, dy2d, dx2d, coef, M, C)
     else:

@@ -1,0 +1,18 @@
+#!/usr/bin/env bash
+# fused BatchNorm (statistics + apply / dx in one launch): kernel + engine tests, ResNet-18 bench + breakdown
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+cd "$R"
+export DISTRIFLOW_SKIP_BUILD=1
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -k "bn" tests/test_engine_gpu.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/t_r4j.log 2>&1 || { tail -n 40 gpurun_out/t_r4j.log; exit 1; }
+tail -n 2 gpurun_out/t_r4j.log
+timeout -k 10 120 python3 bench.py --model resnet18_cifar --batch-per-gpu 256 --steps 100 --warmup 10 > gpurun_out/b_rn.json 2> gpurun_out/b_rn.err || { tail -n 20 gpurun_out/b_rn.err; exit 1; }
+cat gpurun_out/b_rn.json
+cd /tmp && export TMPDIR=/tmp
+rm -rf $R/gpurun_out/prof_rn
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_rn -o k --output-format csv -- python3 $R/bench.py --model resnet18_cifar --batch-per-gpu 256 --steps 20 --warmup 3 --async-steps 0 > $R/gpurun_out/prof_rn.log 2>&1 || { tail -n 20 $R/gpurun_out/prof_rn.log; exit 1; }
+cd $R
+f=$(find gpurun_out/prof_rn -name '*kernel_trace.csv' | head -n 1)
+python3 scripts/step_breakdown.py "$f" sgd_multi --order > gpurun_out/prof_rn.txt
+head -n 30 gpurun_out/prof_rn.txt

@@ -355,7 +355,7 @@ def test_batchnorm(M, C, relu):
     dg = torch.empty(C, device=dev)
     db = torch.empty(C, device=dev)
     ops.bn_bwd(x, y if relu else None, dy, dx, g, mean, inv, dg, db, ws, coef, cnt[1])
-    assert int(cnt[1].abs().sum()) == 0
+    assert int(cnt[1][:64].abs().sum()) == 0  # word 64: the fused launch's generation (only increments)
     gin = dy.float() * (y.float() > 0) if relu else dy.float()
     edx, esg, esb = ref.batchnorm_bwd(x.float(), gin, g, emu, einv)
     _close(dx, edx, 3e-2, 3e-2)
@@ -365,6 +365,65 @@ def test_batchnorm(M, C, relu):
     ops.bn_apply(x, y, g, b, rm, rv, relu=relu, eval_mode=True)
     ee = (x.float() - rm) * torch.rsqrt(rv + 1e-5) * g + b
     _close(y, torch.relu(ee) if relu else ee)
+
+
+@pytest.mark.parametrize("M,C", [(32768, 64), (8192, 128), (4096, 512), (40, 64)])
+@pytest.mark.parametrize("res", [0, 1, 2])
+def test_bn_fused_forward_matches_two_launches(M, C, res):
+    """Statistics + apply in one launch (csrc/bn.hip bn_fused_kernel, in-launch hand-off) == the
+    statistics launch + the apply launch: mean / invstd / running statistics to fp32 summation order (the
+    fused launch has its own, larger grid), output to one bf16 ulp; three launches in a row (the
+    generation word keeps counting, tickets re-arm)."""
+    torch.manual_seed(C + res)
+    x = torch.randn(M, C, device=dev).to(torch.bfloat16)
+    r = torch.randn(M, C, device=dev).to(torch.bfloat16) if res else None
+    g, b = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
+    rbn = (torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev), torch.randn(C, device=dev),
+           torch.rand(C, device=dev) + 0.5) if res == 2 else None
+    ws = torch.empty(ops.bn_workspace_floats(C), device=dev)
+    outs = []
+    for fused in (False, True):
+        cnt = torch.zeros(2, ops.BN_COUNTERS, dtype=torch.int32, device=dev)
+        mean, inv = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        y = torch.empty_like(x)
+        for _ in range(3):
+            if fused:
+                ops.bn_fwd_fused(x, y, g, b, mean, inv, rm, rv, ws, cnt[0], relu=True, residual=r, residual_bn=rbn)
+            else:
+                ops.bn_stats_fwd(x, mean, inv, rm, rv, ws, cnt[0], 0.1, 1e-5)
+                ops.bn_apply(x, y, g, b, mean, inv, relu=True, residual=r, residual_bn=rbn)
+        torch.cuda.synchronize()
+        assert int(cnt[0][:64].abs().sum()) == 0
+        outs.append((y.float(), mean.clone(), inv.clone(), rm.clone(), rv.clone()))
+    (y0, m0, i0, rm0, rv0), (y1, m1, i1, rm1, rv1) = outs
+    for u, v in ((m0, m1), (i0, i1), (rm0, rm1), (rv0, rv1)):
+        torch.testing.assert_close(v, u, rtol=1e-5, atol=1e-6)
+    assert ((y1 - y0).abs() <= y0.abs() * 2 ** -7 + 1e-5).all()
+
+
+@pytest.mark.parametrize("M,C", [(32768, 64), (4096, 512)])
+def test_bn_fused_backward_matches_two_launches(M, C, monkeypatch):
+    """Backward statistics + dx in one launch == the statistics launch + the dx launch."""
+    torch.manual_seed(C)
+    x = torch.randn(M, C, device=dev).to(torch.bfloat16)
+    mask = torch.randn(M, C, device=dev).to(torch.bfloat16)
+    dy = torch.randn(M, C, device=dev).to(torch.bfloat16)
+    g = torch.rand(C, device=dev) + 0.5
+    mean, inv = x.float().mean(0), torch.rsqrt(x.float().var(0, unbiased=False) + 1e-5)
+    ws = torch.empty(ops.bn_workspace_floats(C), device=dev)
+    outs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("DISTRIFLOW_DIAG", f"bn_fused={fused}")
+        cnt = torch.zeros(2, ops.BN_COUNTERS, dtype=torch.int32, device=dev)
+        dx, dg, db, coef = torch.empty_like(x), torch.empty(C, device=dev), torch.empty(C, device=dev), torch.empty(3 * C, device=dev)
+        for _ in range(2):
+            ops.bn_bwd(x, mask, dy, dx, g, mean, inv, dg, db, ws, coef, cnt[1])
+        torch.cuda.synchronize()
+        outs.append((dx.float(), dg.clone(), db.clone(), coef.clone()))
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
+    assert ((outs[1][0] - outs[0][0]).abs() <= outs[0][0].abs() * 2 ** -6 + 1e-4).all()
 
 
 @pytest.mark.parametrize("proj", [False, True])
