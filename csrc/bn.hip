@@ -38,9 +38,18 @@ static int bn_rows_per_thread() {
   return r;
 }
 
+// workgroup cap of a statistics launch (default BN_MAX_G; diagnostic bn_max_g <= 1008: 1 + 63 tickets)
+static int bn_max_g() {
+  static const int g = [] {
+    const int v = diag_int("bn_max_g", BN_MAX_G);
+    return v >= 16 && v <= 1008 ? v : BN_MAX_G;
+  }();
+  return g;
+}
+
 static int bn_grid(int M, int rpp) {
   int g = cdiv(M, rpp * bn_rows_per_thread());
-  if (g > BN_MAX_G) g = BN_MAX_G;
+  if (g > bn_max_g()) g = bn_max_g();
   if (g < 1) g = 1;
   return g;
 }

@@ -6,6 +6,7 @@
 // the Python side reads the same variable through distriflow_amd/diagnostics.py.
 //   igemm_fast=0    igemm64 without the FAST gather           igemm_splitk=0  igemm64 without split-K
 //   bn_rpt=N        BatchNorm statistics rows per thread      wgrad_wg=N      wgrad_tr workgroup target
+//   bn_max_g=N      BatchNorm statistics workgroup cap (16..1008, default 255)
 //   wgrad128=N      wgrad_tr 128x128 tile rows per step       cp_wpc=N        convpool workgroups per CU cap
 //   cp_minimgs=N    convpool images per workgroup floor
 //   wgrad_halo=0    3x3 weight gradients on wgrad_tr instead of the halo kernel
