@@ -737,68 +737,64 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   LN_STAMP(9);
 
   // ---------------------------------------------------------------- phase G: conv1 weight gradient
-  // D[c][tap] = sum over (image, y, x) of dC1[c][y][x] X[y + ky][x + kx].  A fragment of lane
-  // (c = i, g) = dC1[c][y][8g .. 8g + 8) unpooled in registers from dP1 + codes (4 windows); B of lane
-  // (tap = 16T + i, g) = the input row y + ky from column 8g + kx (odd kx: the shifted copy).  No
-  // per-image staging, no barrier inside the loop.
+  // dW1[c][ky][kx] = sum over (image, y, x) of dC1[c][y][x] X[y + ky][x + kx].  The two rows y = 2 py + dy
+  // of a pool-window row are stacked in the GEMM's M: row (c, dy) = dy * 6 + c, and X row 2 py + dy + ky
+  // is the extended tap ky' = dy + ky (0 .. 5) of row 2 py, so ONE B operand (30 extended taps + a ones
+  // column) serves both rows: D[(c, dy)][(ky', kx)], and dW1[c][ky][kx] = D[(c, 0)][(ky, kx)] +
+  // D[(c, 1)][(ky + 1, kx)] in the final sum (2 MFMAs per window row instead of 4).  A of lane (row i, g) =
+  // dC1[c][2 py + dy][8g .. 8g + 8) unpooled in registers from dP1 + codes (4 windows); no per-image
+  // staging, no barrier inside the loop.
   {
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    const int ca = i < 6 ? i : 5;
-    // B of lane (tap, g) = input row y + ky, columns 8g + kx .. + 7 (odd kx: the shifted copy, so the
-    // start is a whole dword): four dwords from a dword-aligned address (ds_read2_b32 pairs: no 16-byte
-    // alignment needed, no per-lane dword select).  The bias column (tap 25) reads the ones block, taps
-    // 26 .. 31 the zero block: one address select per read, no value masking.
+    const int gdy = i >= 6 && i < 12 ? 1 : 0;  // this lane's A row (c, dy)
+    const int ca = i < 6 ? i : (i < 12 ? i - 6 : 5);
+    // B of lane (extended tap e = 16T + i, g) = input row 2 py + ky', columns 8g + kx .. + 7 (odd kx: the
+    // shifted copy, so the start is a whole dword): four dwords from a dword-aligned address
+    // (ds_read2_b32 pairs).  Column 30 (the bias) reads the ones block, column 31 the zero block.
     constexpr int kXs1 = (OFF_XS1 - OFF_XS) / 2;  // Xs1 - Xs in elements
     unsigned boff[2], bconst[2];
     bool breal[2];
 #pragma unroll
     for (int T = 0; T < 2; ++T) {
-      const int tap = 16 * T + i;
-      const int tp = tap < 25 ? tap : 0;
-      const int ky = tp / 5, kx = tp - 5 * (tp / 5);
+      const int e = 16 * T + i;
+      const int ep = e < 30 ? e : 0;
+      const int ky = ep / 5, kx = ep - 5 * (ep / 5);
       boff[T] = 2u * (unsigned)(((kx & 1) ? kXs1 : 0) + ky * 32 + 8 * g + 2 * (kx >> 1));  // bytes from Xs
-      breal[T] = tap < 25;
-      bconst[T] = tap == 25 ? (unsigned)OFF_K : (unsigned)OFF_KZ;
+      breal[T] = e < 30;
+      bconst[T] = e == 30 ? (unsigned)OFF_K : (unsigned)OFF_KZ;
     }
-    // A: the 4 pool windows' dP1 values scattered by their argmax code (2 bits: position in the 2x2
-    // window): a dword of a0 / a1 holds the window's row dy = 0 / 1 pair, the value shifted to its x.
-    // Lanes past the 6 channels or the 14 windows take no value (code forced past 3).
+    // A: the window's dP1 value goes to position code (2 bits: dy * 2 + dx) of the 2x2 window; a lane of
+    // row dy takes it when code - 2 dy is 0 or 1 (its dx).  Lanes past the 12 rows or the 14 windows take
+    // no value (code forced past 3).
     unsigned cmask[4];
 #pragma unroll
-    for (int wd = 0; wd < 4; ++wd) cmask[wd] = (4 * g + wd < 14 && i < 6) ? 0u : 4u;
+    for (int wd = 0; wd < 4; ++wd) cmask[wd] = (4 * g + wd < 14 && i < 12) ? 0u : 8u;
 #pragma unroll 2
     for (int rp = w; rp < IMG * 14; rp += NT / 64) {
       const int img = rp / 14, py = rp - 14 * (rp / 14);
-      // A rows y = 2 py (dy = 0) and 2 py + 1 (dy = 1) from the same 4 pool windows px = 4g .. 4g + 3
       const int p0 = (img * 14 + py) * 14 + 4 * g;
       const uint2 cA = *reinterpret_cast<const uint2*>(C1 + p0);
       const uint2 cB = *reinterpret_cast<const uint2*>(C1 + p0 + 2);
       const unsigned cw[4] = {cA.x, cA.y, cB.x, cB.y};
-      unsigned a0w[4], a1w[4];
+      unsigned aw[4];
 #pragma unroll
       for (int wd = 0; wd < 4; ++wd) {
-        const unsigned code = ((cw[wd] >> (3 * ca)) & 7u) | cmask[wd];
+        const unsigned sel = (((cw[wd] >> (3 * ca)) & 7u) | cmask[wd]) - 2u * (unsigned)gdy;
         // in bounds for every lane (windows 14, 15 are the next row's first two or the tail)
         const unsigned pv = *reinterpret_cast<const unsigned short*>(P1 + (p0 + wd) * 8 + ca);
-        const unsigned v = pv << ((code & 1u) << 4);
-        a0w[wd] = code == 0u || code == 1u ? v : 0u;
-        a1w[wd] = code == 2u || code == 3u ? v : 0u;
+        aw[wd] = sel < 2u ? pv << (sel << 4) : 0u;
       }
-      const bf16x8 a0 = __builtin_bit_cast(bf16x8, uint4{a0w[0], a0w[1], a0w[2], a0w[3]});
-      const bf16x8 a1 = __builtin_bit_cast(bf16x8, uint4{a1w[0], a1w[1], a1w[2], a1w[3]});
+      const bf16x8 av = __builtin_bit_cast(bf16x8, uint4{aw[0], aw[1], aw[2], aw[3]});
+      const unsigned rowb = (unsigned)OFF_XS + 2u * (unsigned)(img * 1024 + 2 * py * 32);
 #pragma unroll
-      for (int dy = 0; dy < 2; ++dy) {
-        const unsigned rowb = (unsigned)OFF_XS + 2u * (unsigned)(img * 1024 + (2 * py + dy) * 32);
-#pragma unroll
-        for (int T = 0; T < 2; ++T) {
-          const unsigned* bp = reinterpret_cast<const unsigned*>(smem + (breal[T] ? rowb + boff[T] : bconst[T]));
-          const bf16x8 bv = __builtin_bit_cast(bf16x8, uint4{bp[0], bp[1], bp[2], bp[3]});
-          acc[T] = mfma16x16x32(dy ? a1 : a0, bv, acc[T]);
-        }
+      for (int T = 0; T < 2; ++T) {
+        const unsigned* bp = reinterpret_cast<const unsigned*>(smem + (breal[T] ? rowb + boff[T] : bconst[T]));
+        const bf16x8 bv = __builtin_bit_cast(bf16x8, uint4{bp[0], bp[1], bp[2], bp[3]});
+        acc[T] = mfma16x16x32(av, bv, acc[T]);
       }
     }
-    // cross-wave sum: D[row = channel 4g + r][col = tap 16T + i]; waves w and w + 4 share slot w & 3
-    // (the upper half writes, then the lower half adds in place: a [4][16][32] buffer for 8 waves)
+    // cross-wave sum: D[row = (c, dy) 4g + r][col = extended tap 16T + i]; waves w and w + 4 share slot
+    // w & 3 (the upper half writes, then the lower half adds in place: a [4][16][32] buffer for 8 waves)
     if (w >= 4) {
 #pragma unroll
       for (int T = 0; T < 2; ++T)
@@ -816,12 +812,14 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
         }
     }
     __syncthreads();
-    for (int e = tid; e < 6 * 32; e += NT) {
-      const int c = e >> 5, col = e & 31;
-      const float v = RED[(0 * 16 + c) * 32 + col] + RED[(1 * 16 + c) * 32 + col] + RED[(2 * 16 + c) * 32 + col] +
-                      RED[(3 * 16 + c) * 32 + col];
-      if (col < 25) part[(long long)(kLeNetPW1 + c * 25 + col)] = v;
-      else if (col == 25) part[(long long)(kLeNetPB1 + c)] = v;
+    auto S = [&](int row, int col) {
+      return RED[(0 * 16 + row) * 32 + col] + RED[(1 * 16 + row) * 32 + col] + RED[(2 * 16 + row) * 32 + col] +
+             RED[(3 * 16 + row) * 32 + col];
+    };
+    for (int e = tid; e < 6 * 26; e += NT) {
+      const int c = e / 26, t = e - 26 * (e / 26);  // t < 25: tap (ky, kx); t == 25: the bias
+      if (t < 25) part[(long long)(kLeNetPW1 + c * 25 + t)] = S(c, t) + S(6 + c, t + 5);
+      else part[(long long)(kLeNetPB1 + c)] = S(c, 30) + S(6 + c, 30);
     }
   }
   LN_STAMP(10);

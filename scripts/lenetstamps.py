@@ -96,7 +96,13 @@ def reduce_stamps(m, net, data, labels, B, buf, async_ps):
         end = r[valid][:, [1, 4]].max()
         jobs = valid & (r[:, 6] > 0)
         own = valid & (r[:, 2] > 0) & (r[:, 3] > 0)
-        line = [f"launch span {us(end - t0):6.2f}", f"first job done {us(np.median(r[jobs, 6] - t0)):5.2f} (median)",
+        ends = r[valid][:, [1, 4]].max(axis=1)
+        line = [f"launch span {us(end - t0):6.2f}",
+                f"starts +{us(np.median(r[valid, 0] - t0)):5.2f} med / +{us((r[valid, 0] - t0).max()):5.2f} max",
+                f"first job {us(np.median(r[jobs, 6] - r[jobs, 0])):5.2f} (median, from own start)",
+                f"ends +{us(np.median(ends - t0)):5.2f} med, last block {int(np.argmax(np.where(valid, r[:, [1, 4]].max(axis=1), 0)))}"
+                f" of {int(valid.sum())}, job blocks end max +{us((ends[:-2] - t0).max()):5.2f}",
+                f"first job done {us(np.median(r[jobs, 6] - t0)):5.2f} (median)",
                 f"jobs done {us(np.median(r[valid & (r[:, 1] > 0), 1] - t0)):5.2f} (median)"]
         if own.any():
             line.append(f"owners {own.sum()}: wait {us(np.median(r[own, 2] - r[own, 1])):5.2f} "
@@ -106,6 +112,9 @@ def reduce_stamps(m, net, data, labels, B, buf, async_ps):
             line.append(f"admission {us(float(r[st, 9][0] - r[st, 8][0])):5.2f} (start +{us(float(r[st, 8][0] - t0)):5.2f}),"
                         f" claim+stage {us(float(r[st, 10][0] - r[st, 9][0])):5.2f}")
         print("  " + "; ".join(line))
+        lb = int(np.argmax(np.where(valid, r[:, [1, 4]].max(axis=1), 0)))
+        rel = {k: (us(float(r[lb, k] - t0)) if r[lb, k] > 0 else None) for k in (0, 6, 7, 1, 2, 3, 5, 4)}
+        print(f"    last block {lb}: " + ", ".join(f"s{k} {v:.2f}" for k, v in rel.items() if v is not None))
 
 
 if __name__ == "__main__":
