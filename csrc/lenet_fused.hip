@@ -1196,6 +1196,19 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
         if (threadIdx.x == 0 && LL) atomicOr(a.ll.err, 2);
         continue;
       }
+      // write-through (sc1) buffer loads of the slabs, all in flight (an atomic load per value would wait
+      // for each one); the first owned slot's old master / momentum values (fused update) are loaded right
+      // behind them, so both arrive in one memory round trip (loading and parking those in LDS first had
+      // the slab loads wait a whole round trip behind them)
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, kChunks * kSlotVals * 4, 0x00020000);
+      float x[kChunks][kPerThread];
+#pragma unroll
+      for (int cc = 0; cc < kChunks; ++cc)
+#pragma unroll
+        for (int e = 0; e < kPerThread; ++e)
+          x[cc][e] = e < npos ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                              rs, (cc * kSlotVals + threadIdx.x + RT * e) * 4, 0, 16))
+                              : 0.f;
       if (nown == 0 && pre) {
 #pragma unroll
         for (int e = 0; e < kPerThread; ++e) {
@@ -1212,17 +1225,6 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
           m_pre[e][threadIdx.x] = m;
         }
       }
-      // write-through (sc1) buffer loads of the slabs, all in flight (an atomic load per value would wait
-      // for each one)
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, kChunks * kSlotVals * 4, 0x00020000);
-      float x[kChunks][kPerThread];
-#pragma unroll
-      for (int cc = 0; cc < kChunks; ++cc)
-#pragma unroll
-        for (int e = 0; e < kPerThread; ++e)
-          x[cc][e] = e < npos ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                              rs, (cc * kSlotVals + threadIdx.x + RT * e) * 4, 0, 16))
-                              : 0.f;
       float v[kPerThread];
 #pragma unroll
       for (int e = 0; e < kPerThread; ++e) {
