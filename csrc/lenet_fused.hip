@@ -932,14 +932,14 @@ __device__ __forceinline__ int conv_wj(Owned o) { return o.di == 0 ? o.i : o.di 
 // (every operand row it loads is used twice); LDS combine.  out[e] = partial of position t + 256 e.
 __device__ __forceinline__ void dense_job(const LeNetRedArgs& a, const RedTables& t, int u, int c, float* red,
                                           float (&out)[kPerThread]) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   int tn, tk;
   const int l = dense_unit(t, u, tn, tk);
   const LeNetDense& L = t.L[l];
   const int col0 = c * a.chunk_cols, col1 = min(a.kcols, col0 + a.chunk_cols);
   const bf16* arow[2];
   const bf16* brow[2];
-  bool a_ok[2], b_ok[2], b_one[2], a_any[2], b_any[2];
+  bool a_ok[2], b_ok[2], b_one[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int n = kDU * tn + 16 * i + (lane & 15), k = kDU * tk + 16 * i + (lane & 15);
@@ -948,8 +948,6 @@ __device__ __forceinline__ void dense_job(const LeNetRedArgs& a, const RedTables
     a_ok[i] = n < L.N;
     b_ok[i] = k < L.K;
     b_one[i] = k == L.K;
-    a_any[i] = kDU * tn + 16 * i < L.N;  // wave-uniform: some row of this 16-row group is live
-    b_any[i] = kDU * tk + 16 * i < L.K;  // ... has a real (not bias / padding) input row
   }
   bf16x8 ones, zeros = zero8();
 #pragma unroll
@@ -964,13 +962,16 @@ __device__ __forceinline__ void dense_job(const LeNetRedArgs& a, const RedTables
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int s = s0; s < s1; s += 4) {
     bf16x8 av[2][4], bv[2][4];
+    // unconditional loads (the rows are clamped to valid ones; the MFMA operand selects below drop the
+    // padding): a load under a per-group condition compiled to an exec-mask branch per load, each waiting
+    // for the one before it
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int ss = min(s + q, s1 - 1);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        av[i][q] = a_any[i] ? ld8(arow[i] + 32 * ss) : zeros;
-        bv[i][q] = b_any[i] ? ld8(brow[i] + 32 * ss) : zeros;
+        av[i][q] = ld8(arow[i] + 32 * ss);
+        bv[i][q] = ld8(brow[i] + 32 * ss);
       }
     }
 #pragma unroll
@@ -1003,21 +1004,23 @@ __device__ __forceinline__ void dense_job(const LeNetRedArgs& a, const RedTables
 // Conv job (slot s, chunk c): parameters 256 s .. 256 s + 255 over the train workgroups' partial rows
 // q = c, c + 8, ...: one row (1 KB) per wave-load, the rows split over the 4 waves, LDS combine.
 __device__ __forceinline__ void conv_job(const LeNetRedArgs& a, int s, int c, float* red, float (&out)[kPerThread]) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int p0 = s * kConvPer + 4 * lane;
   const int pl = min(p0, kLeNetConvStride - 4);  // lanes past the last parameter read the row's padding
   const int nrows = a.nblk > c ? (a.nblk - 1 - c) / kChunks + 1 : 0;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int i0 = wid; i0 < nrows; i0 += 4 * 16) {
+    // every load of the round unconditional (rows clamped, the padding ones dropped below): a per-row
+    // condition compiled to an exec-mask branch per load, each waiting for the one before it
     f32x4 v[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      const int i = i0 + 4 * k;
-      v[k] = i < nrows ? *reinterpret_cast<const f32x4*>(a.conv_part + (long long)(c + kChunks * i) * kLeNetConvStride + pl)
-                       : f32x4{0.f, 0.f, 0.f, 0.f};
+      const int i = min(i0 + 4 * k, nrows - 1);
+      v[k] = *reinterpret_cast<const f32x4*>(a.conv_part + (long long)(c + kChunks * i) * kLeNetConvStride + pl);
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) acc += v[k];
+    for (int k = 0; k < 16; ++k)
+      if (i0 + 4 * k < nrows) acc += v[k];
   }
   *reinterpret_cast<f32x4*>(red + wid * kSlotVals + 4 * lane) = acc;
   __syncthreads();
@@ -1128,14 +1131,21 @@ __device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, unsigned 
 // stamps[block][16]: 0 start, 1 jobs done, 2 decision known, 3 owned slots applied, 4 end, 5 first owned
 // slot's rank sums in (LL), 6 first job's partial computed, 7 first ownership combine done; staging
 // workgroup (PS): 8 admission start, 9 admission done / decision published, 10 next batch staged
+// (kept in LDS and written out when the workgroup ends: a global store mid-kernel makes the compiler's
+// wait-count pass wait for every load in flight at the next join, stamps or not)
 #define LR_STAMP(slot)                                                              \
   do {                                                                              \
     if (a.stamps) {                                                                 \
       __builtin_amdgcn_sched_barrier(0);                                            \
       const unsigned long long t_ = wall_clock64();                                 \
       __builtin_amdgcn_sched_barrier(0);                                            \
-      if (threadIdx.x == 0) a.stamps[blockIdx.x * 16 + (slot)] = t_;                \
+      if (threadIdx.x == 0) lr_st[(slot)] = t_;                                     \
     }                                                                               \
+  } while (0)
+#define LR_FLUSH()                                                                  \
+  do {                                                                              \
+    if (a.stamps && threadIdx.x == 0)                                               \
+      for (int k_ = 0; k_ < 16; ++k_) a.stamps[blockIdx.x * 16 + k_] = lr_st[k_];   \
   } while (0)
 
 // MODE: 0 single rank, 1 in-kernel LL exchange over the ranks, 2 async parameter server.  One
@@ -1151,7 +1161,9 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
   __shared__ unsigned s_e;
   __shared__ int s_last;
   __shared__ float* s_shard[kP2PMaxRanks];  // PS: the master shards' bases (ps_elem)
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
+  __shared__ unsigned long long lr_st[16];
+  if (a.stamps && threadIdx.x < 16) lr_st[threadIdx.x] = 0ull;  // (only thread 0 writes them afterwards)
   LR_STAMP(0);
   const int nslot = a.dense_tiles + a.nconv_slots;
   const int G = a.exch_blocks;
@@ -1342,6 +1354,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       lenet_ps_arrive(a, (unsigned)narr, (unsigned)(nslot + 1));
     }
     LR_STAMP(4);
+    LR_FLUSH();
     return;
   }
   const int blk = blockIdx.x - G;
@@ -1370,6 +1383,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     LR_STAMP(10);
     lenet_ps_arrive(a, 1u, (unsigned)(a.dense_tiles + a.nconv_slots + 1));
     LR_STAMP(1);
+    LR_FLUSH();
     return;
   }
   if (blk == 1) {  // fused update: stage the next step's batch indices, advance the cursor
@@ -1379,6 +1393,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     copy_i64(a.sgd.dst, a.sgd.src + nxt * a.sgd.B, a.sgd.B, threadIdx.x, RT);
     if (threadIdx.x == 0) *a.sgd.cursor = nxt;
     LR_STAMP(1);
+    LR_FLUSH();
     return;
   }
   {  // loss partials -> stats: every load of the block in flight at once, fixed-order sums
@@ -1417,6 +1432,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     }
   }
   LR_STAMP(1);
+  LR_FLUSH();
 }
 
 }  // namespace
