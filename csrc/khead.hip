@@ -261,7 +261,8 @@ void khead_set_stamps(void* buf) { g_khead_stamps = reinterpret_cast<unsigned lo
 template <int KSC>
 __global__ void __launch_bounds__(KT) khead_train_kernel(KHeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, tid = threadIdx.x;
+  // the wave index in an SGPR: per-wave tile counts become scalar branches
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), tid = threadIdx.x;
   const int KC = a.K / KCH, KS = KC / 32;
   const KHeadLds s = carve(smem, KC);
   unsigned* tickets = a.sync;
