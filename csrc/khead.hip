@@ -282,10 +282,14 @@ __global__ void __launch_bounds__(KT) khead_train_kernel(KHeadArgs a) {
     // ---- stage P[r0 .. r0 + 32)[kc0 .. kc0 + KC) (rows past B zero): every load in flight, then LDS
     const int c8n = KC / 8;
     {
+      // the staging indices computed here, per job (opaque to loop-invariant motion): hoisted out of the job
+      // loop, the 12 row / column pairs were spilled to scratch and reloaded one memory latency apart
+      int tid_j = tid;
+      asm volatile("" : "+v"(tid_j));
       bf16x8 v[kStageMax];
 #pragma unroll
       for (int i = 0; i < kStageMax; ++i) {
-        const int e = tid + KT * i, r = e / c8n, c8 = 8 * (e - r * c8n);
+        const int e = tid_j + KT * i, r = e / c8n, c8 = 8 * (e - r * c8n);
         if (e < KR * c8n) {
           if (r0 + r < a.B) {
             v[i] = ld16(a.p + (long long)(r0 + r) * a.K + kc0 + c8);
@@ -297,7 +301,7 @@ __global__ void __launch_bounds__(KT) khead_train_kernel(KHeadArgs a) {
       }
 #pragma unroll
       for (int i = 0; i < kStageMax; ++i) {
-        const int e = tid + KT * i, r = e / c8n, c8 = 8 * (e - r * c8n);
+        const int e = tid_j + KT * i, r = e / c8n, c8 = 8 * (e - r * c8n);
         if (e < KR * c8n) *reinterpret_cast<bf16x8*>(s.ps + r * s.ldp + c8) = v[i];
       }
     }
