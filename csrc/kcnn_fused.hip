@@ -83,31 +83,39 @@ __device__ __forceinline__ long long src_row(const KcnnArgs& a, int b) {
   return r < 0 ? 0 : (r >= a.nrows ? a.nrows - 1 : r);
 }
 
-// x0 of image b as bf16 (the gather kernel's rounding: bf16(u8 * scale)), in two halves so that the
-// next image's loads are in flight while the current one is processed
+// x0 of image b as bf16 (the gather kernel's rounding: bf16(u8 * scale)), loaded one image ahead: the
+// raw bytes / bf16 bits stay in registers and are converted only when stored (converting at load time
+// made every load wait for its data right away, one memory latency per element, and the prefetch of
+// the next image was no prefetch at all)
 constexpr int X0_PER = (NP0 + KT - 1) / KT;  // 4 elements per thread
 struct X0Regs {
-  float v[X0_PER];
+  unsigned v[X0_PER];
 };
 __device__ __forceinline__ X0Regs load_x0(const KcnnArgs& a, int b) {
   X0Regs r;
   if (b >= a.B) return r;
   const long long row = src_row(a, b);
+  if (a.x_u8) {
 #pragma unroll
-  for (int u = 0; u < X0_PER; ++u) {
-    const int e = min((int)threadIdx.x + KT * u, NP0 - 1);
-    if (a.x_u8)
-      r.v[u] = (float)a.x_u8[row * NP0 + e] * a.scale;
-    else
-      r.v[u] = a.idx ? (float)a.x_bf[row * NP0 + e] * a.scale : (float)a.x_bf[row * NP0 + e];
+    for (int u = 0; u < X0_PER; ++u) r.v[u] = a.x_u8[row * NP0 + min((int)threadIdx.x + KT * u, NP0 - 1)];
+  } else {
+    const unsigned short* xb = reinterpret_cast<const unsigned short*>(a.x_bf);
+#pragma unroll
+    for (int u = 0; u < X0_PER; ++u) r.v[u] = xb[row * NP0 + min((int)threadIdx.x + KT * u, NP0 - 1)];
   }
   return r;
 }
-__device__ __forceinline__ void store_x0(const X0Regs& r, bf16* x0) {
+__device__ __forceinline__ void store_x0(const KcnnArgs& a, const X0Regs& r, bf16* x0) {
 #pragma unroll
   for (int u = 0; u < X0_PER; ++u) {
     const int e = threadIdx.x + KT * u;
-    if (e < NP0) x0[e] = f2bf(r.v[u]);
+    float f;
+    if (a.x_u8) f = (float)r.v[u] * a.scale;
+    else {
+      f = __builtin_bit_cast(float, r.v[u] << 16);  // bf16 bits -> fp32
+      if (a.idx) f *= a.scale;
+    }
+    if (e < NP0) x0[e] = f2bf(f);
   }
 }
 
@@ -158,7 +166,7 @@ __global__ void __launch_bounds__(KT, 2) kcnn_fwd_kernel(KcnnArgs a) {
   const int jw = i >> 2, rp = i & 3;
   X0Regs xr = load_x0(a, blockIdx.x);
   for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
-    store_x0(xr, x0);
+    store_x0(a, xr, x0);
     xr = load_x0(a, b + gridDim.x);  // next image: in flight during this one
     __syncthreads();
     conv1_to_lds(a, x0, x1);
@@ -222,7 +230,7 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
   X0Regs xr = load_x0(a, blockIdx.x);
   for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
     // ---- stage x0; expand dY2 from the pooled gradient and the codes (conv2 bias gradient on the way)
-    store_x0(xr, x0);
+    store_x0(a, xr, x0);
     xr = load_x0(a, b + gridDim.x);
     for (int e = tid; e < NPP * 4; e += KT) {
       const int q = e >> 2;
