@@ -117,14 +117,20 @@ struct ALoader {
         if (off >= 0) v = *reinterpret_cast<const bf16x8*>(a.src + off);
       }
     } else {
+      // every element load unconditional (invalid ones read element 0 and are zeroed): a load under a
+      // per-element condition compiled to an exec-mask branch and a wait per element
+      bf16 x[8];
+      bool ok[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        if (k + j < a.K) {
-          const int e = lut[k + j];
-          const long long off = conv_off(a, e >> 24, (e >> 16) & 0xff, e & 0xffff);
-          if (off >= 0) v[j] = a.src[off];
-        }
+        const bool kok = k + j < a.K;
+        const int e = lut[kok ? k + j : 0];
+        const long long off = conv_off(a, e >> 24, (e >> 16) & 0xff, e & 0xffff);
+        ok[j] = kok && off >= 0;
+        x[j] = a.src[ok[j] ? off : 0];
       }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = ok[j] ? x[j] : (bf16)0.0f;
     }
     return v;
   }
@@ -394,15 +400,19 @@ __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradArgs a) {
           if ((unsigned)sh < (unsigned)a.SH && (unsigned)sw < (unsigned)a.SW)
             v = *reinterpret_cast<const bf16x8*>(a.src + img + ((long long)sh * a.SW + sw) * a.SC + (e & 0xffff));
         } else {
+          // every element load unconditional (invalid ones read element 0 and are zeroed): a load under
+          // a per-element condition compiled to an exec-mask branch and a wait per element
+          bf16 xv[8];
+          bool ok[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const int e = xe[i][j];
-            if (e >= 0) {
-              const int sh = r0 + (e >> 24), sw = r1 + ((e >> 16) & 0xff);
-              if ((unsigned)sh < (unsigned)a.SH && (unsigned)sw < (unsigned)a.SW)
-                v[j] = a.src[img + ((long long)sh * a.SW + sw) * a.SC + (e & 0xffff)];
-            }
+            const int sh = r0 + ((e >> 24) & 0xff), sw = r1 + ((e >> 16) & 0xff);
+            ok[j] = e >= 0 && (unsigned)sh < (unsigned)a.SH && (unsigned)sw < (unsigned)a.SW;
+            xv[j] = a.src[ok[j] ? img + ((long long)sh * a.SW + sw) * a.SC + (e & 0xffff) : 0];
           }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = ok[j] ? xv[j] : (bf16)0.f;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j)
