@@ -392,7 +392,7 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   if (tid < 214) DB[tid] = dbv;
   // labels of the 8 images (read by the loss phase)
   int* LBL = reinterpret_cast<int*>(WS + 24);
-  if (tid >= 256 && tid < 256 + IMG) LBL[tid - 256] = lbl < 0 ? 0 : (lbl > 9 ? 9 : lbl);
+  if (tid >= 256 && tid < 256 + IMG) LBL[tid - 256] = lbl;  // clamped where read (no wait for it here)
   __syncthreads();
   // input rows -> bf16, 2-pixel zero border ('same' padding)
   if (xload) {
@@ -529,7 +529,7 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   if (tid < IMG * 16) {
     const int r = tid >> 4, c = tid & 15;
     const bool live = r < rows;
-    const int y = LBL[r];
+    const int y = min(max(LBL[r], 0), 9);
     const float z = c < 10 ? LG[r * 16 + c] : -INFINITY;
     if (a.logits && live && c < 10) a.logits[(long long)(r0 + r) * 10 + c] = z;
     const float mx = row16_max(z);
