@@ -98,11 +98,17 @@ __device__ __forceinline__ void c3_store(const C3P& p, long long m, int co, cons
   *reinterpret_cast<bf16x4_t*>(p.out + o) = ov;
 }
 
-template <int BN, bool FLIP>
+// ROW: one step is a kernel row (3 taps, 48 MFMAs per wave at BN = 64) instead of one tap (16): the
+// row's weights sit in one LDS buffer (the next row in registers, stored between two barriers), so a
+// step pays 2 barriers and one weight wait per 48 MFMAs instead of 1 and 1 per 16.  LDS at BN = 64:
+// 46 KB halo + 24 KB = 70 KB, still two workgroups per CU.
+template <int BN, bool FLIP, bool ROW>
 __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
   constexpr int TN = BN / 32;          // 16-channel tiles per wave
   constexpr int WP = BN * 8 / 256;     // weight staging passes (32 rows each)
-  __shared__ __attribute__((aligned(16))) bf16 lds[kCXL * kCS + 2 * BN * 64];
+  constexpr int NWB = ROW ? 3 : 2;     // weight buffers (BN x 64 each): the row's 3 taps / a double buffer
+  constexpr int RW = ROW ? 3 * WP : WP;
+  __shared__ __attribute__((aligned(16))) bf16 lds[kCXL * kCS + NWB * BN * 64];
   bf16* hs = lds;
   bf16* wsb = lds + kCXL * kCS;
 
@@ -135,7 +141,7 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
   }
   const bf16* wsrc = p.w + (long long)(co0 + r8) * p.Kpad + ch * 8;
 
-  u32x4_t rh[kCXP], rw[WP];
+  u32x4_t rh[kCXP], rw[RW];
   auto load_halo = [&](int cb) {
 #pragma unroll
     for (int i = 0; i < kCXP; ++i)
@@ -155,6 +161,23 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
   auto store_w = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < WP; ++i) *reinterpret_cast<u32x4_t*>(wsb + buf * BN * 64 + wswz(r8 + 32 * i, ch)) = rw[i];
+  };
+  auto load_wrow = [&](int s3) {  // ROW: the 3 taps of kernel row kh of channel block cb
+    const int cb = s3 / 3, kh = s3 - cb * 3;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int tap = 3 * kh + kw;
+      const int col = (FLIP ? 8 - tap : tap) * p.Cin + (cbb + cb) * 64;
+#pragma unroll
+      for (int i = 0; i < WP; ++i) rw[kw * WP + i] = cload16(wsrc + (long long)(32 * i) * p.Kpad + col);
+    }
+  };
+  auto store_wrow = [&]() {
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+      for (int i = 0; i < WP; ++i)
+        *reinterpret_cast<u32x4_t*>(wsb + kw * BN * 64 + wswz(r8 + 32 * i, ch)) = rw[(kw * WP + i) % RW];
   };
 
   // ---- fragment map (16x16x32: lane l holds row / column l & 15, k chunk l >> 4 (+4 for the high half))
@@ -178,6 +201,46 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  auto mma = [&](const bf16* wb, int toff) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 fa[TN], fb[4];
+#pragma unroll
+      for (int u = 0; u < TN; ++u) fa[u] = *reinterpret_cast<const bf16x8*>(wb + woff[u][h]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) fb[t] = *reinterpret_cast<const bf16x8*>(hs + hoff[t] + toff + 32 * h);
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[u][t] = mfma16x16x32(fa[u], fb[t], acc[u][t]);
+    }
+  };
+
+  if constexpr (ROW) {
+    const int S3 = 3 * ncb;
+    load_halo(0);
+    load_wrow(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_halo();
+    store_wrow();
+    if (S3 > 1) load_wrow(1);
+    if (ncb > 1) load_halo(1);
+    __syncthreads();
+    for (int s3 = 0; s3 < S3; ++s3) {
+      const int cb = s3 / 3, kh = s3 - cb * 3;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) mma(wsb + kw * BN * 64, (kh * p.HWP + kw) * kCS);
+      if (s3 + 1 < S3) {
+        __syncthreads();  // every wave is done with this row's weights (and, after kh = 2, the halo)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        store_wrow();
+        if (kh == 2) store_halo();
+        __syncthreads();
+        if (s3 + 2 < S3) load_wrow(s3 + 2);
+        if (kh == 2 && cb + 2 < ncb) load_halo(cb + 2);
+      }
+    }
+  } else {
   // (a two-step register ring for the weights with counted vmcnt waits measured slower on every layer:
   // the loads are not what a step waits for)
   load_halo(0);
@@ -192,19 +255,7 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
     const int cb = s / 9, tap = s - cb * 9;
     const int kh = tap / 3, kw = tap - kh * 3;
     const int toff = (kh * p.HWP + kw) * kCS;
-    const bf16* wb = wsb + (s & 1) * BN * 64;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      bf16x8 fa[TN], fb[4];
-#pragma unroll
-      for (int u = 0; u < TN; ++u) fa[u] = *reinterpret_cast<const bf16x8*>(wb + woff[u][h]);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) fb[t] = *reinterpret_cast<const bf16x8*>(hs + hoff[t] + toff + 32 * h);
-#pragma unroll
-      for (int u = 0; u < TN; ++u)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[u][t] = mfma16x16x32(fa[u], fb[t], acc[u][t]);
-    }
+    mma(wsb + (s & 1) * BN * 64, toff);
     if (s + 1 < S) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       store_w((s + 1) & 1);
@@ -216,6 +267,7 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
     __syncthreads();
     if (s + 2 < S) load_w(s + 2);
     if (tap == 8 && cb + 2 < ncb) load_halo(cb + 2);
+  }
   }
 
   // C/D layout: row (output channel) 4 * (lane >> 4) + r, column (pixel) lane & 15
@@ -440,11 +492,17 @@ hipError_t conv3_halo(const IGemmArgs& a, int mode, hipStream_t st) {
   }
   const dim3 grid(p.ntiles * p.nco * p.ks);
   if (wide) {
-    if (flip) hipLaunchKernelGGL((conv3_halo_kernel<128, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((conv3_halo_kernel<128, false>), grid, dim3(256), 0, st, p);
+    if (flip) hipLaunchKernelGGL((conv3_halo_kernel<128, true, false>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((conv3_halo_kernel<128, false, false>), grid, dim3(256), 0, st, p);
   } else {
-    if (flip) hipLaunchKernelGGL((conv3_halo_kernel<64, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((conv3_halo_kernel<64, false>), grid, dim3(256), 0, st, p);
+    static const int row = diag_int("conv_halo_row", 1);  // a kernel row per step (conv3_halo_kernel ROW)
+    if (row) {
+      if (flip) hipLaunchKernelGGL((conv3_halo_kernel<64, true, true>), grid, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((conv3_halo_kernel<64, false, true>), grid, dim3(256), 0, st, p);
+    } else {
+      if (flip) hipLaunchKernelGGL((conv3_halo_kernel<64, true, false>), grid, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((conv3_halo_kernel<64, false, false>), grid, dim3(256), 0, st, p);
+    }
   }
   DFA_HIP_CHECK(hipGetLastError());
   if (p.ks > 1) {
