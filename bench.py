@@ -70,6 +70,46 @@ def _spawn_ranks(n: int) -> int:
     return rc
 
 
+# every fused fast path off: the per-layer kernels and the BatchNorm statistics passes (the guard's
+# reference engine)
+_UNFUSED = "lenet_fused=0,kcnn_fused=0,khead_fused=0,fold_dropout=0,bn_acc=0"
+
+
+def correctness_guard(model: str, B: int, dev, data, labels) -> dict:
+    """One training step's gradient of the benchmarked engine against the per-layer kernels (every fused
+    path off) on the same weights and the same B-image batch of the benchmark's data: the flat-gradient
+    cosine and the loss must agree.  Catches a fast but wrong kernel at the benchmarked shape."""
+    from distriflow_amd.models.zoo import build_model
+
+    torch.manual_seed(1234)
+    idx = torch.randint(0, data.shape[0], (B,), device=dev)
+    x = (data[idx].float() / 255.0).to(torch.bfloat16).float()
+    y = labels[idx].to(torch.int32)
+    fast = build_model(model, device=dev, seed=0)
+    old = os.environ.get("DISTRIFLOW_DIAG")
+    os.environ["DISTRIFLOW_DIAG"] = ",".join(v for v in (old, _UNFUSED) if v)
+    try:
+        ref = build_model(model, device=dev, seed=0)
+    finally:
+        if old is None:
+            os.environ.pop("DISTRIFLOW_DIAG", None)
+        else:
+            os.environ["DISTRIFLOW_DIAG"] = old
+    ref.store.set_flat(fast.store.master)
+    s_fast = fast.compute_gradients(x, y).float().cpu()
+    g_fast = fast.store.grad.double().clone()
+    s_ref = ref.compute_gradients(x, y).float().cpu()
+    g_ref = ref.store.grad.double()
+    cos = float((g_fast @ g_ref) / (g_fast.norm() * g_ref.norm() + 1e-30))
+    rel = float((g_fast - g_ref).norm() / (g_ref.norm() + 1e-30))
+    lf, lr_ = float(s_fast[0]) / B, float(s_ref[0]) / B
+    finite = bool(torch.isfinite(g_fast).all()) and bool(torch.isfinite(s_fast).all())
+    # bf16 activations: the two engines round at different points (fused layers keep more in fp32)
+    ok = finite and cos >= 0.99 and abs(lf - lr_) <= 0.02 * abs(lr_) + 1e-3
+    return {"ok": ok, "grad_cosine": round(cos, 6), "grad_rel_l2": round(rel, 6), "loss": round(lf, 6),
+            "loss_per_layer": round(lr_, 6), "finite": finite, "batch": B, "reference": "per-layer kernels"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -92,6 +132,9 @@ def main():
                     help="after the sync measurement, also time this many steps of the async parameter-server "
                          "engine and report the async speedup (default: --steps; 0 disables)")
     ap.add_argument("--json-extra", action="store_true", help="add diagnostic fields")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the correctness guard (1-step gradient vs the per-layer kernels); the loss and "
+                         "finiteness checks of the timed run always run")
     ap.add_argument("--phases", type=int, default=0,
                     help="after timing, run this many EAGER steps with hipEvent phase timers and report the "
                          "data/compute/comm/update breakdown (diagnostic, not part of the timed number)")
@@ -189,11 +232,18 @@ def main():
     trainer = make_trainer(args.mode, net)
     elapsed, st = timed(trainer, args.steps)
     loss = float(st[0].item()) / B
+    # the timed run's own health: a finite loss and finite weights after the last timed step
+    w_finite = bool(torch.isfinite(net.store.master).all()) if args.mode == "sync" else True
+    check = {"final_loss_finite": bool(torch.isfinite(torch.tensor(loss))), "weights_finite": w_finite}
     ms = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
     phases = None
     if args.phases > 0 and args.mode == "sync" and dev.type == "cuda":
         phases = {k: round(v, 4) for k, v in trainer.timed_eager_steps(args.phases).items()}
+    if not args.no_check and dev.type == "cuda":
+        check["gradient"] = correctness_guard(args.model, B, dev, data, labels)
+    check["ok"] = (check["final_loss_finite"] and check["weights_finite"]
+                   and check.get("gradient", {"ok": True})["ok"])
     async_rec = None
     async_steps = args.steps if args.async_steps is None else args.async_steps
     if args.mode == "sync" and async_steps > 0 and dev.type == "cuda":
@@ -219,6 +269,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
+            "final_loss": round(loss, 6),
+            "check": check,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
@@ -259,6 +311,9 @@ def main():
                             "capture_error": getattr(trainer, "capture_error", None)}
         print(json.dumps(out), flush=True)
     shutdown()
+    if not check["ok"]:
+        print(f"bench: correctness check FAILED: {check}", file=sys.stderr, flush=True)
+        sys.exit(4)
 
 
 if __name__ == "__main__":

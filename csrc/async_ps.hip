@@ -11,11 +11,13 @@
 // FCFS cursor and the completion arrays sit in the server rank's control buffer.  A worker's whole step
 // is device work that it replays from its own hipGraph at its own pace:
 //   ps_fetch_pull  claim the next microbatch id with a remote atomic (the FCFS dispenser), stage its
-//                  example indices, record the version and copy the current master out of the shards;
+//                  example indices; every workgroup reads the fully-applied count, then copies its slice
+//                  of the current master out of the shards (vp = the minimum count, ps_device.h);
 //   (forward / backward kernels of the model)
-//   ps_apply       admit the gradient with one lock-free CAS on the version word (staleness bound), then
-//                  every workgroup adds -lr * g to its slice of the shards, element by element
-//                  (csrc/ps_device.h: plain RMW at world 1, CAS adds otherwise).
+//   ps_apply       admit the gradient with one lock-free CAS on the version word (staleness bound
+//                  ver - vp), then every workgroup adds -lr * g to its slice of the shards, element by
+//                  element (csrc/ps_device.h: plain RMW at world 1, CAS adds otherwise); the last one to
+//                  finish publishes the gradient as fully applied.
 // No lock is held across an apply, so ranks never serialise behind one another.  Every wait is bounded
 // by a wall-clock timeout that sets a sticky error word instead of spinning forever.  Both kernels spread
 // the weights over up to 64 workgroups (one workgroup moves only ~60 GB/s of uncached / remote traffic).
@@ -23,7 +25,7 @@
 // Microbatch dispatch is at-least-once and epoch scoped (claim_microbatch / complete_microbatch):
 // a batch is complete only once a gradient for it is admitted; rejected ones are dispatched again.
 //
-// Control buffer layout (server rank): [0] u32 version, [16] u64 batch cursor, [32] u32 dataset epoch,
+// Control buffer layout (server rank): [0] u32 version, [8] u32 fully applied, [16] u64 batch cursor, [32] u32 dataset epoch,
 // [36] u32 batches completed in it, [48] u64 completed / redispatched / skipped / duplicate counters,
 // [256] u32 done_epoch[kPSMaxBatches], then u32 claimed_epoch[kPSMaxBatches].
 #include "common.h"
@@ -52,14 +54,12 @@ __global__ __launch_bounds__(kPSBlock) void ps_fetch_pull_kernel(PSArgs a) {
                           (unsigned long long)(a.nbatches > 0 ? a.nbatches : 1));
     }
     __syncthreads();
-    if (t == 0) {
-      *a.bid_out = s_bid;
-      // the version BEFORE the copy: every add admitted up to it has at least been admitted, so the
-      // staleness of this gradient is counted conservatively
-      *a.vpulled = __hip_atomic_load(a.ver, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (t == 0) *a.bid_out = s_bid;
     ps_stage_indices(a, s_bid, t, kPSBlock);
   }
+  // every workgroup: the fully applied count BEFORE its own slice copy (ps_device.h: vp = the minimum)
+  if (t == 0) ps_note_refresh(a, ps_read_applied(a));
+  __syncthreads();
   const long long per = ((a.n + 4LL * G - 1) / (4LL * G)) * 4;  // slice length, multiple of 4
   const long long lo = b * per, hi = lo + per < a.n ? lo + per : a.n;
   f32x4* d4 = reinterpret_cast<f32x4*>(a.w);
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
       unsigned d = 0;
       for (;;) {
         d = __hip_atomic_load(a.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((d >> 3) == ep) break;
+        if (ps_epoch_eq(d, ep)) break;
         if (wall_clock64() - t0 > 2ull * (unsigned long long)a.timeout_ticks) {
           atomicOr(a.stats + 5, 8ull);
           if (a.herr) __hip_atomic_store(a.herr, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -140,6 +140,8 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
     if (s_last) {
       a.scratch[kPSApplyDone] = 0;
       a.scratch[kPSEpoch] += 1u;
+      // every workgroup drained its adds before arriving: the gradient is now fully applied
+      if (s_dec == kPSAccept) ps_publish_applied(a);
     }
   }
 }

@@ -54,7 +54,9 @@ void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tenso
                   int64_t drop_seed, c10::optional<torch::Tensor> drop_step, c10::optional<torch::Tensor> pool_code,
                   int64_t drop_step_add, c10::optional<torch::Tensor> bn_ws, c10::optional<torch::Tensor> bn_ticket,
                   int64_t bn_mode, std::vector<torch::Tensor> bn_vecs, c10::optional<torch::Tensor> bn_x,
-                  double bn_momentum, double bn_eps, double bn_gscale) {
+                  double bn_momentum, double bn_eps, double bn_gscale, c10::optional<torch::Tensor> bacc,
+                  int64_t bacc_mode, std::vector<torch::Tensor> bacc_in, c10::optional<torch::Tensor> bacc2,
+                  std::vector<torch::Tensor> bacc2_in) {
   need(src, at::kBFloat16, "src");
   need(w, at::kBFloat16, "w");
   TORCH_CHECK(out.is_cuda() && out.is_contiguous(), "out must be a contiguous GPU tensor");
@@ -163,6 +165,37 @@ void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tenso
       e.dbeta = bn_vecs[4].data_ptr<float>();
       e.coef = bn_vecs[5].data_ptr<float>();
     }
+  }
+  if (bacc.has_value() && bacc->defined()) {
+    // BatchNorm sums accumulated by the epilogue (kernels.h BnAcc): acc [nrep][2][N] fp64; mode 1 inputs
+    // [x, mean, invstd] of the BatchNorm (and of a second one sharing the gradient)
+    need(*bacc, at::kDouble, "bacc");
+    TORCH_CHECK(bacc->numel() % (2 * N) == 0, "bacc must be [nrep][2][N]");
+    dfa::BnAcc& e = a.bacc;
+    e.acc = bacc->data_ptr<double>();
+    e.nrep = (int)(bacc->numel() / (2 * N));
+    e.mode = (int)bacc_mode;
+    TORCH_CHECK(bacc_mode == 0 || bacc_mode == 1, "bacc_mode 0 (forward) or 1 (backward)");
+    auto inputs = [&](const std::vector<torch::Tensor>& v, const dfa::bf16** x, const float** mu, const float** is) {
+      TORCH_CHECK(v.size() == 3, "bacc mode 1 inputs: [x, mean, invstd]");
+      need(v[0], at::kBFloat16, "bacc x");
+      TORCH_CHECK(v[0].numel() >= (M - 1) * ldc + N, "bacc x too small");
+      need(v[1], at::kFloat, "bacc mean");
+      need(v[2], at::kFloat, "bacc invstd");
+      TORCH_CHECK(v[1].numel() >= N && v[2].numel() >= N, "bacc mean / invstd smaller than N");
+      *x = reinterpret_cast<const dfa::bf16*>(v[0].data_ptr());
+      *mu = v[1].data_ptr<float>();
+      *is = v[2].data_ptr<float>();
+    };
+    if (bacc_mode == 1) inputs(bacc_in, &e.x, &e.mean, &e.invstd);
+    if (bacc2.has_value() && bacc2->defined()) {
+      TORCH_CHECK(bacc_mode == 1, "a second BatchNorm's sums: backward only");
+      need(*bacc2, at::kDouble, "bacc2");
+      TORCH_CHECK(bacc2->numel() == bacc->numel(), "bacc2 must match bacc");
+      e.acc2 = bacc2->data_ptr<double>();
+      inputs(bacc2_in, &e.x2, &e.mean2, &e.invstd2);
+    }
+    TORCH_CHECK(dfa::igemm_bacc_ok(a, (int)mode), "bacc: this launch cannot accumulate BatchNorm sums");
   }
   TORCH_CHECK(!a.drop.on || (ldc == N && !a.out_f32), "folded dropout needs a dense bf16 output (ldc == N)");
   // split-K partials for the under-filled (small-M, long-K) shapes: PyTorch's caching allocator is
@@ -766,6 +799,129 @@ void bn_dx_py(torch::Tensor x, c10::optional<torch::Tensor> mask, torch::Tensor 
   check_hip(dfa::bn_dx((const dfa::bf16*)x.data_ptr(), cptr<dfa::bf16>(mask), (const dfa::bf16*)dy.data_ptr(),
                        (dfa::bf16*)dx.data_ptr(), coef.data_ptr<float>(), (int)M, (int)C, cur_stream()),
             "bn_dx");
+}
+
+// BatchNorm consumers that finalise epilogue-accumulated sums (csrc/bn.hip, kernels.h BnAccFin)
+static dfa::BnAccFin bn_fin(const torch::Tensor& acc, const c10::optional<torch::Tensor>& zero, int64_t C) {
+  need(acc, at::kDouble, "bn acc");
+  TORCH_CHECK(acc.numel() % (2 * C) == 0 && acc.numel() / (2 * C) <= dfa::kBnAccMaxRep, "bn acc must be [nrep][2][C]");
+  dfa::BnAccFin f{};
+  f.acc = acc.data_ptr<double>();
+  f.nrep = (int)(acc.numel() / (2 * C));
+  if (zero.has_value() && zero->defined()) {
+    need(*zero, at::kDouble, "bn acc zero");
+    TORCH_CHECK(zero->numel() == acc.numel(), "bn acc zero must match acc");
+    f.zero = zero->data_ptr<double>();
+  }
+  return f;
+}
+
+// y = act(bn(x) [+ r | + bn_r(r)]) in training mode, statistics from the producer's sums; workgroup 0
+// writes mean / invstd / running statistics (of the residual BN too) and clears `zero` / `rzero`
+void bn_apply_acc_py(torch::Tensor x, torch::Tensor y, torch::Tensor gamma, torch::Tensor beta, torch::Tensor acc,
+                     c10::optional<torch::Tensor> zero, torch::Tensor mean, torch::Tensor invstd,
+                     c10::optional<torch::Tensor> run_mean, c10::optional<torch::Tensor> run_var,
+                     c10::optional<torch::Tensor> r, std::vector<torch::Tensor> rbn, int64_t M, int64_t C, bool relu,
+                     double momentum, double eps) {
+  TORCH_CHECK(C % 8 == 0 && C <= 1024, "bn_apply_acc: C % 8 == 0, C <= 1024");
+  bn_check_act(x, M * C, "x");
+  bn_check_act(y, M * C, "y");
+  for (auto* t : {&gamma, &beta, &mean, &invstd}) bn_check_vec(*t, C, "bn vector");
+  dfa::BnApplyArgs a{};
+  a.x = (const dfa::bf16*)x.data_ptr();
+  a.y = (dfa::bf16*)y.data_ptr();
+  a.gamma = gamma.data_ptr<float>();
+  a.beta = beta.data_ptr<float>();
+  a.M = (int)M; a.C = (int)C; a.relu = relu ? 1 : 0; a.eval = 0; a.eps = (float)eps;
+  dfa::BnAccFin f = bn_fin(acc, zero, C);
+  f.mean = mean.data_ptr<float>();
+  f.invstd = invstd.data_ptr<float>();
+  const bool run = run_mean.has_value() && run_mean->defined();
+  if (run) {
+    bn_check_vec(*run_mean, C, "run_mean");
+    TORCH_CHECK(run_var.has_value() && run_var->defined(), "run_var with run_mean");
+    bn_check_vec(*run_var, C, "run_var");
+    f.run_mean = run_mean->data_ptr<float>();
+    f.run_var = run_var->data_ptr<float>();
+  }
+  f.momentum = (float)momentum;
+  f.eps = (float)eps;
+  dfa::BnAccFin fr{};
+  const bool has_rbn = !rbn.empty();
+  if (r.has_value() && r->defined()) {
+    bn_check_act(*r, M * C, "residual");
+    a.r = (const dfa::bf16*)r->data_ptr();
+    if (has_rbn) {
+      // [gamma, beta, acc, zero (or empty), mean, invstd, run_mean, run_var]
+      TORCH_CHECK(rbn.size() == 8, "residual BN: [gamma, beta, acc, zero, mean, invstd, run_mean, run_var]");
+      for (int i : {0, 1, 4, 5, 6, 7}) bn_check_vec(rbn[i], C, "residual bn vector");
+      a.rgamma = rbn[0].data_ptr<float>();
+      a.rbeta = rbn[1].data_ptr<float>();
+      fr = bn_fin(rbn[2], rbn[3].numel() ? c10::optional<torch::Tensor>(rbn[3]) : c10::nullopt, C);
+      fr.mean = rbn[4].data_ptr<float>();
+      fr.invstd = rbn[5].data_ptr<float>();
+      fr.run_mean = rbn[6].data_ptr<float>();
+      fr.run_var = rbn[7].data_ptr<float>();
+      fr.momentum = (float)momentum;
+      fr.eps = (float)eps;
+      a.rmean = fr.mean;  // non-null marks RES 2
+      a.rinvstd = fr.invstd;
+    }
+  } else {
+    TORCH_CHECK(!has_rbn, "residual BN without a residual");
+  }
+  check_hip(dfa::bn_apply_acc(a, f, has_rbn ? &fr : nullptr, cur_stream()), "bn_apply_acc");
+}
+
+// dx = k1 g + k2 x + k3 from the producer's backward sums; workgroup 0 writes dgamma / dbeta (x gscale) and
+// coef, and clears `zero`
+void bn_dx_acc_py(torch::Tensor x, torch::Tensor g, torch::Tensor dx, torch::Tensor acc,
+                  c10::optional<torch::Tensor> zero, torch::Tensor gamma, torch::Tensor mean, torch::Tensor invstd,
+                  torch::Tensor dgamma, torch::Tensor dbeta, torch::Tensor coef, int64_t M, int64_t C, double gscale) {
+  TORCH_CHECK(C % 8 == 0 && C <= 1024, "bn_dx_acc: C % 8 == 0, C <= 1024");
+  bn_check_act(x, M * C, "x");
+  bn_check_act(g, M * C, "g");
+  bn_check_act(dx, M * C, "dx");
+  for (auto* t : {&gamma, &mean, &invstd, &dgamma, &dbeta}) bn_check_vec(*t, C, "bn vector");
+  bn_check_vec(coef, 3 * C, "coef");
+  dfa::BnAccFin f = bn_fin(acc, zero, C);
+  f.mean = mean.data_ptr<float>();
+  f.invstd = invstd.data_ptr<float>();
+  f.gamma = gamma.data_ptr<float>();
+  f.dgamma = dgamma.data_ptr<float>();
+  f.dbeta = dbeta.data_ptr<float>();
+  f.coef = coef.data_ptr<float>();
+  f.gscale = (float)gscale;
+  check_hip(dfa::bn_dx_acc((const dfa::bf16*)x.data_ptr(), (const dfa::bf16*)g.data_ptr(), (dfa::bf16*)dx.data_ptr(),
+                           f, (int)M, (int)C, cur_stream()),
+            "bn_dx_acc");
+}
+
+// GAP backward with relu' (mask) and the BatchNorm backward sums of the result (ResNet's last block)
+void gap_bwd_bn_py(torch::Tensor dy, torch::Tensor mask, torch::Tensor dx, int64_t B, int64_t HW, int64_t C,
+                   torch::Tensor acc, std::vector<torch::Tensor> bn_in) {
+  need(dy, at::kBFloat16, "dy");
+  need(mask, at::kBFloat16, "mask");
+  need(dx, at::kBFloat16, "dx");
+  TORCH_CHECK(dy.numel() >= B * C && mask.numel() >= B * HW * C && dx.numel() >= B * HW * C, "gap_bwd_bn sizes");
+  TORCH_CHECK(C % 4 == 0 && C <= 1024 && 256 % (C / 4) == 0, "gap_bwd_bn: C / 4 must divide 256");
+  need(acc, at::kDouble, "bn acc");
+  TORCH_CHECK(acc.numel() % (2 * C) == 0, "bn acc must be [nrep][2][C]");
+  TORCH_CHECK(bn_in.size() == 3, "gap_bwd_bn: [x, mean, invstd]");
+  need(bn_in[0], at::kBFloat16, "bn x");
+  TORCH_CHECK(bn_in[0].numel() >= B * HW * C, "bn x too small");
+  bn_check_vec(bn_in[1], C, "bn mean");
+  bn_check_vec(bn_in[2], C, "bn invstd");
+  dfa::BnAcc e{};
+  e.acc = acc.data_ptr<double>();
+  e.nrep = (int)(acc.numel() / (2 * C));
+  e.mode = 1;
+  e.x = (const dfa::bf16*)bn_in[0].data_ptr();
+  e.mean = bn_in[1].data_ptr<float>();
+  e.invstd = bn_in[2].data_ptr<float>();
+  check_hip(dfa::gap_bwd_bn((const dfa::bf16*)dy.data_ptr(), (const dfa::bf16*)mask.data_ptr(),
+                            (dfa::bf16*)dx.data_ptr(), (int)B, (int)HW, (int)C, e, cur_stream()),
+            "gap_bwd_bn");
 }
 
 // geometry: [B, H, W, C, KH, KW, pad, N]
@@ -1650,6 +1806,8 @@ class PSComm {
     own_ = (float*)alloc_uncached(((size_t)1 << shift_) * 4 + kTestWords * 4, "ps shard");
     check_hip(hipMalloc((void**)&local_, 4096), "ps local alloc");
     check_hip(hipMemset(local_, 0, 4096), "ps local memset");
+    // kPSVMin (csrc/ps_device.h): no refresh recorded yet
+    check_hip(hipMemset(local_ + 1024 + 4 * dfa::kPSVMinWord, 0xff, 4), "ps vmin init");
     check_hip(hipDeviceSynchronize(), "ps init sync");
     timeout_ticks_ = (int64_t)(timeout_s * 1e8);
     for (auto& p : shard_) p = nullptr;
@@ -1768,6 +1926,19 @@ class PSComm {
   }
   // device view of this rank's counters [accepted, rejected, sum staleness, max staleness, admission CAS
   // retries, err, no-op steps, -] (int64): read back asynchronously by the trainer's callbacks
+  // audit rows (version at admission, vp, decision) of this rank's next `rows` decisions, written by the
+  // admission itself (tests: the true staleness of every admitted gradient); an empty tensor disables it
+  void set_audit(torch::Tensor rows) {
+    if (!rows.defined() || rows.numel() == 0) {
+      audit_ = nullptr, audit_cap_ = 0, audit_keep_ = torch::Tensor();
+      return;
+    }
+    need(rows, at::kInt, "ps audit");
+    TORCH_CHECK(rows.dim() == 2 && rows.size(1) == 3 && rows.get_device() == dev_, "ps: audit rows [n][3] int32");
+    audit_ = reinterpret_cast<unsigned*>(rows.data_ptr<int>());
+    audit_cap_ = rows.size(0);
+    audit_keep_ = rows;
+  }
   torch::Tensor stats_tensor() const {
     return torch::from_blob(local_ + 64, {8}, torch::TensorOptions().dtype(torch::kLong).device(torch::kCUDA, dev_));
   }
@@ -1787,16 +1958,16 @@ class PSComm {
     return a;
   }
   // [accepted, rejected, sum staleness, max staleness, admission CAS retries, err, version, batch cursor,
-  //  no-op steps]
+  //  no-op steps, fully applied]
   std::vector<int64_t> stats() const {
     unsigned long long h[8] = {0};
     check_hip(hipMemcpy(h, local_ + 64, 64, hipMemcpyDeviceToHost), "ps stats");
-    unsigned ver = 0;
+    unsigned ver[3] = {0, 0, 0};
     unsigned long long ctr = 0;
-    check_hip(hipMemcpy(&ver, shared_, 4, hipMemcpyDeviceToHost), "ps ver");
+    check_hip(hipMemcpy(ver, shared_, 12, hipMemcpyDeviceToHost), "ps ver");
     check_hip(hipMemcpy(&ctr, shared_ + 16, 8, hipMemcpyDeviceToHost), "ps ctr");
     return {(int64_t)h[0], (int64_t)h[1], (int64_t)h[2], (int64_t)h[3], (int64_t)h[4], (int64_t)h[5],
-            (int64_t)ver, (int64_t)ctr, (int64_t)h[6]};
+            (int64_t)ver[0], (int64_t)ctr, (int64_t)h[6], (int64_t)ver[2]};
   }
   // the master, gathered from the shards (call while no worker is stepping)
   void copy_master(torch::Tensor dst) const {
@@ -1846,6 +2017,9 @@ class PSComm {
     a.excl = world_ == 1 ? 1 : 0;
     a.n = n_;
     a.vpulled = reinterpret_cast<unsigned*>(local_);
+    a.applied = reinterpret_cast<unsigned*>(shared_ + 8);  // control buffer word 2 (ps_device.h)
+    a.audit = audit_;
+    a.audit_cap = audit_cap_;
     a.bid_out = reinterpret_cast<long long*>(local_ + 8);
     a.stats = reinterpret_cast<unsigned long long*>(local_ + 64);
     a.scratch = reinterpret_cast<unsigned*>(local_ + 1024);
@@ -1873,6 +2047,9 @@ class PSComm {
   char* local_ = nullptr;
   float* lr_dev_ = nullptr;
   torch::Tensor lr_keep_;
+  unsigned* audit_ = nullptr;
+  int64_t audit_cap_ = 0;
+  torch::Tensor audit_keep_;
 };
 
 static dfa::PSArgs ps_lenet_args(const PSComm& c, const torch::Tensor& perm, const torch::Tensor& idx, double lr,
@@ -1891,7 +2068,31 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pool_code") = py::none(),
         py::arg("drop_step_add") = 0, py::arg("bn_ws") = py::none(), py::arg("bn_ticket") = py::none(),
         py::arg("bn_mode") = 0, py::arg("bn_vecs") = std::vector<torch::Tensor>{}, py::arg("bn_x") = py::none(),
-        py::arg("bn_momentum") = 0.1, py::arg("bn_eps") = 1e-5, py::arg("bn_gscale") = 1.0);
+        py::arg("bn_momentum") = 0.1, py::arg("bn_eps") = 1e-5, py::arg("bn_gscale") = 1.0,
+        py::arg("bacc") = py::none(), py::arg("bacc_mode") = 0, py::arg("bacc_in") = std::vector<torch::Tensor>{},
+        py::arg("bacc2") = py::none(), py::arg("bacc2_in") = std::vector<torch::Tensor>{});
+  m.def("igemm_bacc_supported", [](int64_t M, int64_t N, int64_t K, int64_t Kpad, std::vector<int64_t> geom,
+                                   int64_t mode, int64_t bacc_mode, bool two, bool has_res, bool has_mask) {
+    // the dispatch decision of igemm_fwd for a launch with these shapes (16-byte aligned operands)
+    dfa::IGemmArgs a{};
+    int g[9];
+    fill_geom(geom, g);
+    a.SH = g[0]; a.SW = g[1]; a.SC = g[2]; a.OH = g[3]; a.OW = g[4]; a.KH = g[5]; a.KW = g[6]; a.stride = g[7];
+    a.pad = g[8];
+    a.M = (int)M; a.N = (int)N; a.K = (int)K; a.Kpad = (int)Kpad; a.ldc = (int)N; a.lda = 0;
+    static dfa::bf16 dummy[8] __attribute__((aligned(16)));
+    static double dacc[2] __attribute__((aligned(16)));
+    static float dvec[2] __attribute__((aligned(16)));
+    a.src = dummy; a.w = dummy; a.out = dummy;
+    if (has_res) a.res = dummy;
+    if (has_mask) a.mask = dummy;
+    a.bacc.acc = dacc;
+    a.bacc.nrep = 1;
+    a.bacc.mode = (int)bacc_mode;
+    if (bacc_mode == 1) a.bacc.x = dummy, a.bacc.mean = dvec, a.bacc.invstd = dvec;
+    if (two) a.bacc.acc2 = dacc, a.bacc.x2 = dummy, a.bacc.mean2 = dvec, a.bacc.invstd2 = dvec;
+    return dfa::igemm_bacc_ok(a, (int)mode);
+  });
   m.def("igemm64_bn_tiles", [](int64_t M, int64_t N, int64_t K, int64_t Kpad, std::vector<int64_t> geom, int64_t mode) {
     dfa::IGemmArgs a{};
     int g[9];
@@ -1967,6 +2168,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_stats_bwd", &bn_stats_bwd_py, "BN backward statistics: dgamma, dbeta and dx coefficients");
   m.def("bn_apply", &bn_apply_py, "BN normalize (+ residual join, + ReLU)");
   m.def("bn_dx", &bn_dx_py, "BN input gradient dx = k1*g + k2*x + k3");
+  m.def("bn_apply_acc", &bn_apply_acc_py, "BN training apply, statistics finalised from epilogue-accumulated sums");
+  m.def("bn_dx_acc", &bn_dx_acc_py, "BN input gradient, coefficients finalised from epilogue-accumulated sums");
+  m.def("gap_bwd_bn", &gap_bwd_bn_py, "GAP backward with relu' and BatchNorm backward sums");
   m.def("bn_fwd_fused", &bn_fwd_fused_py, "BN training forward: statistics + apply in one launch");
   m.def("bn_bwd_fused", &bn_bwd_fused_py, "BN backward: statistics + dx in one launch");
   m.def("bn_stats_grid", &dfa::bn_stats_grid, "partial-slab count of a BN statistics launch");
@@ -2082,6 +2286,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("schedule_stats", &PSComm::schedule_stats)
       .def("done_epochs", &PSComm::done_epochs)
       .def("copy_master", &PSComm::copy_master)
-      .def("stats_tensor", &PSComm::stats_tensor);
+      .def("stats_tensor", &PSComm::stats_tensor)
+      .def("set_audit", &PSComm::set_audit, py::arg("rows"));
   dfa::register_runtime(m);
 }

@@ -15,10 +15,13 @@
 //            registers.  The forward apply optionally fuses the residual join of a ResNet block,
 //            y = relu(bn(x) + r) or relu(bn(x) + bn_r(r)) (projection shortcut), and the backward
 //            apply fuses relu' of a mask tensor into g = dy * (mask > 0).
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 #include "diag.h"
 #include "bn_epi.h"
+#include "bn_acc.h"
 
 namespace dfa {
 
@@ -592,6 +595,208 @@ hipError_t bn_dx(const bf16* x, const bf16* mask, const bf16* dy, bf16* dx, cons
   else
     hipLaunchKernelGGL(bn_dx_kernel<false>, dim3(ew_grid(n)), dim3(256), 0, st, x, mask, dy, dx, coef, (long long)M,
                        C);
+  return hipGetLastError();
+}
+
+// ---- consumers of epilogue-accumulated sums (kernels.h BnAcc / BnAccFin, csrc/bn_acc.h) ------------------
+// The producing conv added fp64 partials of [S, Q] into nrep replicas; every workgroup here finalises the
+// per-channel coefficients itself (threads c < C, replicas in fixed order) into LDS, then streams.  The
+// replica reads are C * nrep * 16 bytes per workgroup, so the grid is capped to keep them a few MB.
+constexpr int kBnAccMaxC = 1024;
+
+static int bn_acc_grid(long long nvec, int C, int nrep) {
+  long long g = (nvec + 255) / 256;
+  const long long cap = std::max(64LL, (8LL << 20) / ((long long)C * nrep * 16));
+  if (g > cap) g = cap;
+  if (g > 4096) g = 4096;
+  return (int)std::max(1LL, g);
+}
+
+__device__ __forceinline__ void bn_fin_sums(const BnAccFin& f, int C, int c, double& S, double& Q) {
+  S = 0.0, Q = 0.0;
+  for (int r = 0; r < f.nrep; ++r) {
+    S += f.acc[(long long)(2 * r) * C + c];
+    Q += f.acc[(long long)(2 * r + 1) * C + c];
+  }
+}
+
+// forward: mean / invstd of channel c (workgroup 0 also publishes them, updates the running statistics and
+// clears f.zero); returns the affine pair (sa, sb) of gamma, beta
+__device__ __forceinline__ void bn_fin_fwd(const BnAccFin& f, const float* gamma, const float* beta, int C, long long M,
+                                           int c, float& sa, float& sb) {
+  double S, Q;
+  bn_fin_sums(f, C, c, S, Q);
+  const double m = S / M;
+  double var = Q / M - m * m;
+  if (var < 0.0) var = 0.0;
+  const float is = (float)(1.0 / sqrt(var + (double)f.eps));
+  sa = gamma[c] * is;
+  sb = beta[c] - (float)m * sa;
+  if (blockIdx.x == 0) {
+    f.mean[c] = (float)m;
+    f.invstd[c] = is;
+    if (f.run_mean) {
+      const double unb = M > 1 ? var * M / (M - 1) : var;
+      f.run_mean[c] = (float)((1.0 - f.momentum) * f.run_mean[c] + f.momentum * m);
+      f.run_var[c] = (float)((1.0 - f.momentum) * f.run_var[c] + f.momentum * unb);
+    }
+    if (f.zero)
+      for (int r = 0; r < 2 * f.nrep; ++r) f.zero[(long long)r * C + c] = 0.0;
+  }
+}
+
+template <int RES>
+__global__ void __launch_bounds__(256) bn_apply_acc_kernel(BnApplyArgs a, BnAccFin f, BnAccFin fr) {
+  __shared__ float co[4][kBnAccMaxC];  // sa, sb, ra, rb
+  const int C = a.C;
+  const long long M = a.M;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float sa, sb, ra = 1.f, rb = 0.f;
+    bn_fin_fwd(f, a.gamma, a.beta, C, M, c, sa, sb);
+    if (RES == 2) bn_fin_fwd(fr, a.rgamma, a.rbeta, C, M, c, ra, rb);
+    co[0][c] = sa;
+    co[1][c] = sb;
+    co[2][c] = ra;
+    co[3][c] = rb;
+  }
+  __syncthreads();
+  const long long total = M * C / 8;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const int c0 = (int)(threadIdx.x % (C / 8)) * 8;  // constant: 256 and the grid stride are multiples of C/8
+  float sa[8], sb[8], ra[8], rb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sa[j] = co[0][c0 + j];
+    sb[j] = co[1][c0 + j];
+    ra[j] = co[2][c0 + j];
+    rb[j] = co[3][c0 + j];
+  }
+#pragma unroll 2
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += stride) {
+    const bf16x8 xv = reinterpret_cast<const bf16x8*>(a.x)[i];
+    bf16x8 rv;
+    if (RES) rv = reinterpret_cast<const bf16x8*>(a.r)[i];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = (float)xv[j] * sa[j] + sb[j];
+      if (RES) v += (float)rv[j] * ra[j] + rb[j];
+      if (a.relu) v = fmaxf(v, 0.f);
+      o[j] = f2bf(v);
+    }
+    reinterpret_cast<bf16x8*>(a.y)[i] = o;
+  }
+}
+
+hipError_t bn_apply_acc(const BnApplyArgs& a, const BnAccFin& f, const BnAccFin* fr, hipStream_t st) {
+  if (a.C % 8 || a.C > kBnAccMaxC || 256 % (a.C / 8) || a.M <= 0 || !f.acc || f.nrep < 1 || a.eval)
+    return hipErrorInvalidValue;
+  const int res = a.r == nullptr ? 0 : (fr == nullptr ? 1 : 2);
+  const int nrep = f.nrep + (fr ? fr->nrep : 0);
+  const int grid = bn_acc_grid((long long)a.M * a.C / 8, a.C, nrep);
+  const BnAccFin none{};
+  if (res == 0) hipLaunchKernelGGL(bn_apply_acc_kernel<0>, dim3(grid), dim3(256), 0, st, a, f, none);
+  else if (res == 1) hipLaunchKernelGGL(bn_apply_acc_kernel<1>, dim3(grid), dim3(256), 0, st, a, f, none);
+  else hipLaunchKernelGGL(bn_apply_acc_kernel<2>, dim3(grid), dim3(256), 0, st, a, f, *fr);
+  return hipGetLastError();
+}
+
+// backward: dx = k1 g + k2 x + k3, k from [S = sum g, Q = sum g * xhat]
+__global__ void __launch_bounds__(256) bn_dx_acc_kernel(const bf16* __restrict__ x, const bf16* __restrict__ g,
+                                                        bf16* __restrict__ dx, BnAccFin f, long long M, int C) {
+  __shared__ float k[3][kBnAccMaxC];
+  for (int c = threadIdx.x; c < C; c += 256) {
+    double S, Q;
+    bn_fin_sums(f, C, c, S, Q);
+    const double isd = f.invstd[c], gam = f.gamma[c], m = f.mean[c];
+    const double k1 = gam * isd;
+    const float a1 = (float)k1, a2 = (float)(-k1 * isd * Q / M), a3 = (float)(k1 * (m * isd * Q / M - S / M));
+    k[0][c] = a1;
+    k[1][c] = a2;
+    k[2][c] = a3;
+    if (blockIdx.x == 0) {
+      f.dbeta[c] = (float)S * f.gscale;
+      f.dgamma[c] = (float)Q * f.gscale;
+      if (f.coef) {
+        f.coef[c] = a1;
+        f.coef[C + c] = a2;
+        f.coef[2 * C + c] = a3;
+      }
+      if (f.zero)
+        for (int r = 0; r < 2 * f.nrep; ++r) f.zero[(long long)r * C + c] = 0.0;
+    }
+  }
+  __syncthreads();
+  const long long total = M * C / 8;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const int c0 = (int)(threadIdx.x % (C / 8)) * 8;
+  float k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    k1[j] = k[0][c0 + j];
+    k2[j] = k[1][c0 + j];
+    k3[j] = k[2][c0 + j];
+  }
+#pragma unroll 2
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += stride) {
+    const bf16x8 xv = reinterpret_cast<const bf16x8*>(x)[i];
+    const bf16x8 gv = reinterpret_cast<const bf16x8*>(g)[i];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(k1[j] * (float)gv[j] + k2[j] * (float)xv[j] + k3[j]);
+    reinterpret_cast<bf16x8*>(dx)[i] = o;
+  }
+}
+
+hipError_t bn_dx_acc(const bf16* x, const bf16* g, bf16* dx, const BnAccFin& f, int M, int C, hipStream_t st) {
+  if (C % 8 || C > kBnAccMaxC || 256 % (C / 8) || M <= 0 || !f.acc || f.nrep < 1 || !f.gamma || !f.dgamma)
+    return hipErrorInvalidValue;
+  const int grid = bn_acc_grid((long long)M * C / 8, C, f.nrep);
+  hipLaunchKernelGGL(bn_dx_acc_kernel, dim3(grid), dim3(256), 0, st, x, g, dx, f, (long long)M, C);
+  return hipGetLastError();
+}
+
+// GAP backward (dx[b][p][c] = dy[b][c] / HW) with relu' of the block output and the BatchNorm backward sums
+// of dx: a thread keeps one 4-channel group (256 % (C / 4) == 0) over its rows, the workgroup reduces the
+// groups through LDS slots (csrc/bn_acc.h)
+__global__ void __launch_bounds__(256) gap_bwd_bn_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ mask,
+                                                         bf16* __restrict__ dx, int B, int HW, int C, BnAcc e) {
+  __shared__ float red[3 * 1024];
+  const int cpr = C / 4, rpb = 256 / cpr;
+  const int c4 = (int)(threadIdx.x % cpr) * 4;
+  const float inv = 1.f / HW;
+  BnAccLane bl;
+  bacc_zero(bl);
+  const BnAccChan bc = bacc_chan(e, c4);
+  const long long rows = (long long)B * HW;
+  for (long long r = (long long)blockIdx.x * rpb + threadIdx.x / cpr; r < rows; r += (long long)gridDim.x * rpb) {
+    const long long o = r * C + c4;
+    const long long b = r / HW;
+    const bacc_bf16x4 g = *reinterpret_cast<const bacc_bf16x4*>(dy + b * C + c4);
+    const bacc_bf16x4 mk = *reinterpret_cast<const bacc_bf16x4*>(mask + o);
+    bacc_bf16x4 ov;
+    float sv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ov[j] = f2bf((float)mk[j] > 0.f ? (float)g[j] * inv : 0.f);
+      sv[j] = (float)ov[j];
+    }
+    *reinterpret_cast<bacc_bf16x4*>(dx + o) = ov;
+    bacc_add4(bl, e, bc, o, sv);
+  }
+  bacc_stash(red, threadIdx.x / cpr, C, c4, bl);
+  __syncthreads();
+  bacc_flush(e, red, rpb, C, 0, C, threadIdx.x, 256);
+}
+
+hipError_t gap_bwd_bn(const bf16* dy, const bf16* mask, bf16* dx, int B, int HW, int C, const BnAcc& bacc,
+                      hipStream_t st) {
+  if (C % 4 || C > 1024 || 256 % (C / 4) || !bacc.acc || bacc.mode != 1 || bacc.acc2 || bacc.nrep < 1)
+    return hipErrorInvalidValue;
+  const long long rows = (long long)B * HW;
+  const int rpb = 256 / (C / 4);
+  const int grid = (int)std::min<long long>(std::max<long long>(1, (rows + rpb - 1) / rpb), 256);
+  hipLaunchKernelGGL(gap_bwd_bn_kernel, dim3(grid), dim3(256), 0, st, dy, mask, dx, B, HW, C, bacc);
   return hipGetLastError();
 }
 

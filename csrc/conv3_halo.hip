@@ -26,6 +26,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "diag.h"
+#include "bn_acc.h"
 
 namespace dfa {
 
@@ -64,12 +65,14 @@ struct C3P {
   float* ws;         // [ks][M][Cout] partials, summed + epilogue by igemm64_splitk_combine
   int relu;
   float alpha;
+  BnAcc bacc;        // BatchNorm sums of the stored output (ks == 1; csrc/bn_acc.h)
 };
 
 __device__ __forceinline__ int wswz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
-// epilogue of 4 consecutive output channels of one pixel (as igemm64): alpha, residual join, ReLU, relu'
-__device__ __forceinline__ void c3_store(const C3P& p, long long m, int co, const f32x4& a) {
+// epilogue of 4 consecutive output channels of one pixel (as igemm64): alpha, residual join, ReLU, relu';
+// `stored` receives the values as stored (bf16-rounded)
+__device__ __forceinline__ void c3_store(const C3P& p, long long m, int co, const f32x4& a, float (&stored)[4]) {
   const long long o = m * p.ldc + co;
   float v[4];
 #pragma unroll
@@ -94,7 +97,10 @@ __device__ __forceinline__ void c3_store(const C3P& p, long long m, int co, cons
   }
   bf16x4_t ov;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) ov[r] = f2bf(v[r]);
+  for (int r = 0; r < 4; ++r) {
+    ov[r] = f2bf(v[r]);
+    stored[r] = (float)ov[r];
+  }
   *reinterpret_cast<bf16x4_t*>(p.out + o) = ov;
 }
 
@@ -271,6 +277,33 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
   }
 
   // C/D layout: row (output channel) 4 * (lane >> 4) + r, column (pixel) lane & 15
+  if (p.ks == 1 && p.bacc.acc) {
+    // BatchNorm sums of the stored values (csrc/bn_acc.h): per channel group u over the lane's 4 pixels,
+    // the 16 lanes of the group, then the two pixel-half waves through LDS slots
+    const bool two = p.bacc.acc2 != nullptr;
+    float* red = reinterpret_cast<float*>(lds);
+    __syncthreads();  // every wave is done with the halo / weights: LDS is free
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+      const int cl = wn * (BN / 2) + 16 * u + 4 * fc;
+      const BnAccChan bc = bacc_chan(p.bacc, co0 + cl);
+      BnAccLane bl;
+      bacc_zero(bl);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int s = wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
+        const long long m = (long long)tile * kCP + s;
+        float sv[4];
+        c3_store(p, m, co0 + cl, acc[u][t], sv);
+        bacc_add4(bl, p.bacc, bc, m * p.ldc + co0 + cl, sv);
+      }
+      bacc_reduce16(bl, two);
+      if (fl == 0) bacc_stash(red, wm, BN, cl, bl);
+    }
+    __syncthreads();
+    bacc_flush(p.bacc, red, 2, BN, co0, p.Cout, tid, 256);
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int s = wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
@@ -282,7 +315,8 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
         *reinterpret_cast<f32x4*>(p.ws + ((long long)ksp * p.ntiles * kCP + m) * p.Cout + co) = acc[u][t];
         continue;
       }
-      c3_store(p, m, co, acc[u][t]);
+      float sv[4];
+      c3_store(p, m, co, acc[u][t], sv);
     }
   }
 }
@@ -369,6 +403,15 @@ __global__ void __launch_bounds__(512, 1) conv3_halo_c64_kernel(C3P p) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) woff[u][h] = wswz(wn * 32 + 16 * u + fl, fc + 4 * h);
 
+  // BatchNorm sums of every stored value of this workgroup's tiles (csrc/bn_acc.h), kept per lane
+  const bool bacc = p.bacc.acc != nullptr, two = p.bacc.acc2 != nullptr;
+  BnAccLane bl[2];
+  BnAccChan bc[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    bacc_zero(bl[u]);
+    if (bacc) bc[u] = bacc_chan(p.bacc, wn * 32 + 16 * u + 4 * fc);
+  }
   if (nt > gi) load_halo(tb + gi);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (nt > gi) store_halo();
@@ -409,12 +452,26 @@ __global__ void __launch_bounds__(512, 1) conv3_halo_c64_kernel(C3P p) {
       for (int q = 0; q < 4; ++q) {
         const long long m = (long long)t * kCP + wm * 64 + 32 * (q >> 1) + 2 * fl + (q & 1);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) c3_store(p, m, wn * 32 + 16 * u + 4 * fc, acc[u][q]);
+        for (int u = 0; u < 2; ++u) {
+          float sv[4];
+          c3_store(p, m, wn * 32 + 16 * u + 4 * fc, acc[u][q], sv);
+          if (bacc) bacc_add4(bl[u], p.bacc, bc[u], m * p.ldc + wn * 32 + 16 * u + 4 * fc, sv);
+        }
       }
     } else {
       __syncthreads();
     }
     __syncthreads();
+  }
+  if (bacc) {  // the loop ended with a barrier: the halo buffers are free
+    float* red = reinterpret_cast<float*>(lds + 9 * 64 * 64);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      bacc_reduce16(bl[u], two);
+      if (fl == 0) bacc_stash(red, gi * 2 + wm, 64, wn * 32 + 16 * u + 4 * fc, bl[u]);
+    }
+    __syncthreads();
+    bacc_flush(p.bacc, red, 4, 64, 0, 64, threadIdx.x, 512);
   }
 }
 
@@ -461,6 +518,7 @@ hipError_t conv3_halo(const IGemmArgs& a, int mode, hipStream_t st) {
   p.ntiles = a.M / kCP;
   p.relu = a.relu;
   p.alpha = a.alpha;
+  p.bacc = a.bacc;
   static const int c64 = diag_int("conv_halo_c64", 1);
   if (c64 && a.SC == 64 && a.N == 64 && p.hrows <= kC64XR && p.ntiles >= 512) {
     // weights resident: one 8-wave workgroup per CU, tiles split evenly (an even count per workgroup)
@@ -505,7 +563,7 @@ hipError_t conv3_halo(const IGemmArgs& a, int mode, hipStream_t st) {
     }
   }
   DFA_HIP_CHECK(hipGetLastError());
-  if (p.ks > 1) {
+  if (p.ks > 1) {  // the combine applies the epilogue (and the BatchNorm sums)
     IGemmArgs c = a;
     c.splits = p.ks;
     return igemm64_splitk_combine(c, st);

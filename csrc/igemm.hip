@@ -20,6 +20,7 @@
 // fragment reads), XCD-aware block remap so tiles sharing an A panel share an L2.
 #include "common.h"
 #include "kernels.h"
+#include "bn_acc.h"
 
 namespace dfa {
 
@@ -262,11 +263,17 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(IGemmArgs a) {
   }
 
   // epilogue: C/D layout of 16x16 MFMA: col = lane&15, row = 4*(lane>>4) + r
+  // (with a.bacc: forward BatchNorm sums of the stored values, csrc/bn_acc.h -- one channel per lane
+  // here, so the lanes of a channel are l, l ^ 16, l ^ 32, l ^ 48, then the WM wave rows via LDS)
+  const bool bacc = a.bacc.acc != nullptr;
+  float* red = reinterpret_cast<float*>(smem);
+  if (bacc) __syncthreads();  // LDS is free after the k loop
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
+  for (int j = 0; j < TN; ++j) {
+    float bs = 0.f, bq = 0.f;
+    const int col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
+    for (int i = 0; i < TM; ++i) {
       if (col >= a.N) continue;
       const float bv = a.bias ? a.bias[col] : 0.f;
 #pragma unroll
@@ -281,12 +288,33 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(IGemmArgs a) {
         }
         if (a.relu) v = fmaxf(v, 0.f);
         if (a.mask && !((float)a.mask[o] > 0.f)) v = 0.f;
-        if (a.out_f32)
+        if (a.out_f32) {
           reinterpret_cast<float*>(a.out)[o] = v;
-        else
-          reinterpret_cast<bf16*>(a.out)[o] = f2bf(v);
+        } else {
+          const bf16 ob = f2bf(v);
+          reinterpret_cast<bf16*>(a.out)[o] = ob;
+          const float sv = (float)ob;
+          bs += sv;
+          bq += sv * sv;
+        }
       }
     }
+    if (bacc) {
+      bs += __shfl_xor(bs, 16);
+      bq += __shfl_xor(bq, 16);
+      bs += __shfl_xor(bs, 32);
+      bq += __shfl_xor(bq, 32);
+      if (lane < 16) {
+        float* p = red + ((long long)wm * BN + wn * TN * 16 + j * 16 + lane) * 3;
+        p[0] = bs;
+        p[1] = bq;
+        p[2] = 0.f;
+      }
+    }
+  }
+  if (bacc) {
+    __syncthreads();
+    bacc_flush(a.bacc, red, WM, BN, n0, a.N, tid, 256);
   }
 }
 
@@ -542,8 +570,25 @@ static hipError_t launch_fwd_mode(const IGemmArgs& a, hipStream_t st) {
 
 static hipError_t igemm_fwd_nodrop(const IGemmArgs& a, int mode, hipStream_t st);
 
+// Can this igemm_fwd call accumulate BatchNorm sums of its output (a.bacc, csrc/bn_acc.h)?  The halo and
+// igemm64 kernels (and their split-K combine) in both modes, with the vectorised bf16 epilogue; the
+// generic kernel the forward sums only.
+bool igemm_bacc_ok(const IGemmArgs& a, int mode) {
+  if (mode == MODE_DIRECT || a.out_f32 || a.drop.on || a.pool_code || a.bn.part || a.M <= 0 || a.N <= 0) return false;
+  if (a.bacc.nrep < 1 || a.bacc.nrep > kBnAccMaxRep || (a.bacc.mode == 1 && (!a.bacc.x || !a.bacc.mean))) return false;
+  if (a.bacc.acc2 && (a.bacc.mode != 1 || !a.bacc.x2 || !a.bacc.mean2)) return false;
+  if (conv3_halo_supported(a, mode) || igemm64_supported(a, mode)) {
+    if ((a.ldc & 3) || (a.N & 3) || ((uintptr_t)a.out & 15) ||
+        (((uintptr_t)a.res | (uintptr_t)a.resmask | (uintptr_t)a.mask | (uintptr_t)a.bacc.x | (uintptr_t)a.bacc.x2) & 7))
+      return false;
+    return a.N <= 1024 && 256 % (a.N / 4) == 0;  // (a split-K combine may apply the epilogue)
+  }
+  return mode == MODE_FWD && a.bacc.mode == 0 && !smallc_fwd_supported(a, mode);
+}
+
 hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0) return hipSuccess;
+  if (a.bacc.acc && !igemm_bacc_ok(a, mode)) return hipErrorInvalidValue;
   if (a.drop.on && (a.out_f32 || a.ldc != a.N)) return hipErrorInvalidValue;
   if (a.pool_code) return igemm64_pool_supported(a) && mode == MODE_FWD ? igemm64(a, mode, st) : hipErrorInvalidValue;
   if (conv3_halo_supported(a, mode)) return conv3_halo(a, mode, st);

@@ -23,6 +23,7 @@
 #include "kernels.h"
 #include "diag.h"
 #include "bn_epi.h"
+#include "bn_acc.h"
 
 namespace dfa {
 
@@ -475,6 +476,71 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
   const bool vec = (a.ldc & 3) == 0 && ((uintptr_t)a.out & 15) == 0 &&
                    (((uintptr_t)a.res | (uintptr_t)a.resmask | (uintptr_t)a.mask) & 7) == 0;
   typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+  if (a.bacc.acc) {
+    // BatchNorm sums of the stored values (csrc/bn_acc.h; the host admits only the vectorised epilogue,
+    // bf16 output, no dropout): per column group j over the lane's rows, the 16 lanes of the group, then
+    // the WM wave rows through LDS slots
+    const bool two = a.bacc.acc2 != nullptr;
+    float* red = reinterpret_cast<float*>(lds);
+    __syncthreads();  // LDS is free after the k loop
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cl = wn * TN * 16 + j * 16 + fq * 4;
+      const int col0 = n0 + cl;
+      const bool colok = col0 + 3 < a.N;
+      const BnAccChan bc = bacc_chan(a.bacc, colok ? col0 : 0);
+      BnAccLane bl;
+      bacc_zero(bl);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = m0 + wm * TM * 16 + i * 16 + fr;
+        if (row >= Mrows || !colok) continue;
+        long long orow = row;
+        if (PAR) {
+          const int b = row / (cHc * cWc);
+          const int rem = row - b * cHc * cWc;
+          const int y = rem / cWc, x = rem - (rem / cWc) * cWc;
+          orow = ((long long)b * a.OH + 2 * y + py) * a.OW + 2 * x + px;
+        }
+        const long long o = orow * a.ldc + col0;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * a.alpha + (a.bias ? a.bias[col0 + r] : 0.f);
+        if (a.res) {
+          const bf16x4_t rv = *reinterpret_cast<const bf16x4_t*>(a.res + o);
+          bf16x4_t rm;
+          if (a.resmask) rm = *reinterpret_cast<const bf16x4_t*>(a.resmask + o);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (!a.resmask || (float)rm[r] > 0.f) v[r] += (float)rv[r];
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (a.mask) {
+          const bf16x4_t mk = *reinterpret_cast<const bf16x4_t*>(a.mask + o);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (!((float)mk[r] > 0.f)) v[r] = 0.f;
+        }
+        bf16x4_t ov;
+        float sv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ov[r] = f2bf(v[r]);
+          sv[r] = (float)ov[r];
+        }
+        *reinterpret_cast<bf16x4_t*>(reinterpret_cast<bf16*>(a.out) + o) = ov;
+        bacc_add4(bl, a.bacc, bc, o, sv);
+      }
+      bacc_reduce16(bl, two);
+      if (fr == 0) bacc_stash(red, wm, BN, cl, bl);
+    }
+    __syncthreads();
+    bacc_flush(a.bacc, red, WM, BN, n0, a.N, tid, 256);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int row = m0 + wm * TM * 16 + i * 16 + fr;
@@ -616,9 +682,18 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
 
 // (a folded dropout rounds the activation to bf16 before scaling, as the standalone pass saw it)
 // split-K combine: out = epi(sum_s ws[s]) in a fixed split order (deterministic), 4 columns per thread
+// With BatchNorm sums (a.bacc.acc; host: 256 % (N / 4) == 0, so a thread's columns never change over the
+// grid-stride loop) every thread accumulates its 4 columns over its rows; the workgroup reduces them
+// through LDS slots and adds one partial per column (csrc/bn_acc.h).
 __global__ void __launch_bounds__(256) igemm64_splitk_epilogue_kernel(IGemmArgs a) {
   typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
   const long long total4 = (long long)a.M * (a.N >> 2);
+  const bool bacc = a.bacc.acc != nullptr;
+  const int cpr = a.N >> 2;  // column groups per row
+  BnAccLane bl;
+  bacc_zero(bl);
+  BnAccChan bc;
+  if (bacc) bc = bacc_chan(a.bacc, (int)(threadIdx.x % cpr) * 4);
   for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < total4; q += (long long)gridDim.x * 256) {
     const long long row = q / (a.N >> 2);
     const int col0 = (int)(q - row * (a.N >> 2)) * 4;
@@ -656,11 +731,34 @@ __global__ void __launch_bounds__(256) igemm64_splitk_epilogue_kernel(IGemmArgs 
       *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
     } else {
       bf16x4_t ov;
+      float sv[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) ov[r] = f2bf(v[r]);
+      for (int r = 0; r < 4; ++r) {
+        ov[r] = f2bf(v[r]);
+        sv[r] = (float)ov[r];
+      }
       *reinterpret_cast<bf16x4_t*>(reinterpret_cast<bf16*>(a.out) + o) = ov;
+      if (bacc) bacc_add4(bl, a.bacc, bc, o, sv);
     }
   }
+  if (bacc) {
+    __shared__ float red[3 * 1024];  // (256 / cpr) slots x N columns x 3 = 3 * 1024 floats
+    const bool two = a.bacc.acc2 != nullptr;
+    bacc_stash(red, threadIdx.x / cpr, a.N, (int)(threadIdx.x % cpr) * 4, bl);
+    (void)two;
+    __syncthreads();
+    bacc_flush(a.bacc, red, 256 / cpr, a.N, 0, a.N, threadIdx.x, 256);
+  }
+}
+
+// the split-K combine's grid: with BatchNorm sums at most 512 workgroups (each adds one partial per column
+// and quantity: <= 512 / nrep adds per accumulator address)
+static int splitk_epi_grid(const IGemmArgs& a) {
+  const long long total4 = (long long)a.M * (a.N / 4);
+  return (int)min((total4 + 255) / 256, a.bacc.acc ? 512LL : 4096LL);
+}
+static bool bacc_combine_ok(const IGemmArgs& a) {
+  return a.N % 4 == 0 && a.N <= 1024 && 256 % (a.N / 4) == 0 && !a.out_f32 && !a.drop.on && a.ldc % 4 == 0;
 }
 
 // Split-K for under-filled launches: fewer than ~2 workgroups per CU and a long K (ResNet-18 layers 3-4:
@@ -730,9 +828,7 @@ hipError_t launch64(IGemmArgs a, hipStream_t st) {
     else
       hipLaunchKernelGGL((igemm64_kernel<BM, BN, MODE, D, true>), dim3(blocks * s), dim3(256), 0, st, a, d_ow, d_ohw);
     DFA_HIP_CHECK(hipGetLastError());
-    const long long total4 = (long long)a.M * (a.N / 4);
-    const int grid = (int)min((total4 + 255) / 256, 4096LL);
-    hipLaunchKernelGGL(igemm64_splitk_epilogue_kernel, dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(igemm64_splitk_epilogue_kernel, dim3(splitk_epi_grid(a)), dim3(256), 0, st, a);
     return hipGetLastError();
   }
   // (prefetch depths 3 and 4 measured equal to 2 on every ResNet-18 shape: scripts/convbench.py)
@@ -757,9 +853,8 @@ hipError_t launch64_mode(const IGemmArgs& a, hipStream_t st) {
 }  // namespace
 
 hipError_t igemm64_splitk_combine(const IGemmArgs& a, hipStream_t st) {
-  const long long total4 = (long long)a.M * (a.N / 4);
-  const int grid = (int)min((total4 + 255) / 256, 4096LL);
-  hipLaunchKernelGGL(igemm64_splitk_epilogue_kernel, dim3(grid), dim3(256), 0, st, a);
+  if (a.bacc.acc && !bacc_combine_ok(a)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(igemm64_splitk_epilogue_kernel, dim3(splitk_epi_grid(a)), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

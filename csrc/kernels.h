@@ -56,6 +56,25 @@ struct BnEpi {
   float momentum, eps, gscale;
 };
 
+// BatchNorm statistics accumulated in the PRODUCING kernel's epilogue (csrc/bn_acc.h): every workgroup
+// reduces the values it stored, per channel and in a fixed order, and adds them in fp64 into replica
+// (blockIdx % nrep) of `acc` (no ticket, no wait: the adds are fire-and-forget); the consuming pass
+// (bn_apply_acc / bn_dx_acc, csrc/bn.hip) finalises them in its prologue.  mode 0 (forward): [S = sum y,
+// Q = sum y^2]; mode 1 (backward, relu' already applied to the stored g): [S = sum g, Q = sum g * xhat],
+// xhat = (x - mean) * invstd of the BN input x -- for up to two BatchNorms that share g (a ResNet block's
+// bn2 and its projection BN read the same block-output gradient).  fp64 adds of fixed-order fp32
+// partials: the sums depend on arrival order only in the last bits of a double.
+struct BnAcc {
+  double* acc;       // [nrep][2][N] (nullptr: off)
+  double* acc2;      // mode 1: the second BatchNorm's [nrep][2][N] (nullptr: none)
+  const bf16* x;     // mode 1: BN input [M][ldc] at the output's positions
+  const float *mean, *invstd;
+  const bf16* x2;    // mode 1: the second BatchNorm's input
+  const float *mean2, *invstd2;
+  int nrep, mode;
+};
+constexpr int kBnAccMaxRep = 16;
+
 struct IGemmArgs {
   const bf16* src;   // A source: [M][lda] (direct) or NHWC [B][SH][SW][SC] (conv gathers)
   const bf16* w;     // [Npad16][Kpad32] bf16, zero padded
@@ -74,6 +93,7 @@ struct IGemmArgs {
   uint8_t* pool_code;  // conv forward + 2x2 max-pool (igemm64 POOL): out = pooled [M/4][N], code [M/4][N]
   BnEpi bn;            // BatchNorm statistics of the stored output, finalised inside the launch (bn.part
                        // != nullptr: igemm64, no split-K / pooling / parity-class launch)
+  BnAcc bacc;          // BatchNorm statistics of the stored output accumulated by the epilogue (bacc.acc)
 };
 
 struct WgradArgs {
@@ -106,6 +126,7 @@ struct ParamDescTable {
 };
 
 hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st);
+bool igemm_bacc_ok(const IGemmArgs& a, int mode);  // can the launch accumulate a.bacc (BatchNorm sums)
 // 64-deep-step variant for the vectorizable cases (csrc/igemm64.hip); igemm_fwd dispatches to it
 bool igemm64_supported(const IGemmArgs& a, int mode);
 bool igemm64_pool_supported(const IGemmArgs& a);
@@ -227,6 +248,29 @@ bool bn_fused_ok(int C);
 hipError_t bn_fwd_fused(const BnStatsArgs& a, const BnApplyArgs& p, unsigned* gen, hipStream_t st);
 hipError_t bn_bwd_fused(const BnStatsArgs& a, bf16* dx, unsigned* gen, hipStream_t st);
 
+// Consumers that finalise BnAcc sums in their prologue (csrc/bn.hip).  Every workgroup derives the
+// per-channel coefficients from the replicas itself (fixed replica order, fp64); workgroup 0 also writes
+// the finalised values (forward: mean, invstd, running statistics; backward: dgamma, dbeta, coef) and
+// clears `zero` (this BatchNorm's accumulator of the OTHER direction, dead until the producer of the next
+// step or pass refills it).
+struct BnAccFin {
+  const double* acc;  // [nrep][2][C]
+  double* zero;       // [nrep][2][C] cleared by workgroup 0 (nullable)
+  int nrep;
+  float *mean, *invstd, *run_mean, *run_var;  // forward: outputs (run_* nullable); backward: mean/invstd in
+  float momentum, eps;
+  const float* gamma;                         // backward
+  float *dgamma, *dbeta, *coef;               // backward outputs (coef [3][C], nullable)
+  float gscale;
+};
+// y = act(bn(x) [+ r | + bn_r(r)]) with batch statistics from f (and fr: the residual's BatchNorm, RES 2)
+hipError_t bn_apply_acc(const BnApplyArgs& a, const BnAccFin& f, const BnAccFin* fr, hipStream_t st);
+// dx = k1 g + k2 x + k3 with the coefficients from f's backward sums (g: relu' already applied)
+hipError_t bn_dx_acc(const bf16* x, const bf16* g, bf16* dx, const BnAccFin& f, int M, int C, hipStream_t st);
+// dx[b][p][c] = dy[b][c] / HW * [mask > 0], with BatchNorm backward sums of dx (gap backward of ResNet)
+hipError_t gap_bwd_bn(const bf16* dy, const bf16* mask, bf16* dx, int B, int HW, int C, const BnAcc& bacc,
+                      hipStream_t st);
+
 // fused Conv2D(+bias+ReLU)+MaxPool2x2 for small channel counts (convpool.hip)
 // ---- fused dense head (csrc/mlphead.hip)
 constexpr int kHeadMaxLayers = 4;
@@ -344,11 +388,14 @@ struct PSArgs {
   float* w;                     // local fp32 master [n] (pull destination)
   const float* g;               // local fp32 gradient [n]
   long long n;
-  unsigned* vpulled;            // local: version the local weights were last refreshed at
+  unsigned* vpulled;            // local: vp of the last admission (the applied count its weights contained)
+  unsigned* applied;            // shared: gradients whose every add has landed (ps_device.h; null: legacy)
+  unsigned* audit;              // optional local [audit_cap][3] (version at admission, vp, decision) rows
+  long long audit_cap;
   unsigned long long* stats;    // local [8]: accepted, rejected, sum staleness, max staleness, CAS retries, err,
                                 //            no-op steps after the schedule finished
   unsigned* herr;               // host-mapped mirror of the error bits (host watchdog, no HIP call)
-  unsigned* scratch;            // local [64 + kPSMaxGrid] zero-initialised protocol words (async_ps.hip)
+  unsigned* scratch;            // local [64 + kPSMaxGrid] protocol words (async_ps.hip; kPSVMin starts at ~0)
   const long long* perm;        // [nbatches][B] example ids (nullptr: no index staging)
   long long* idx;               // [B] staged ids of the claimed microbatch
   long long* bid_out;           // local: claimed microbatch (epoch << 32 | batch), -1 = dataset finished
@@ -366,6 +413,7 @@ struct PSArgs {
   float lr;
 };
 constexpr int kPSMaxGrid = 64;
+constexpr int kPSVMinWord = 4;  // scratch word of the refresh minimum (ps_device.h kPSVMin)
 constexpr long long kPSMaxBatches = 1 << 20;  // capacity of the shared completion arrays
 hipError_t ps_fetch_pull(const PSArgs& a, hipStream_t st);
 hipError_t ps_apply(const PSArgs& a, hipStream_t st);
@@ -457,10 +505,10 @@ struct LeNetRedArgs {
   // and owns up to 16 slots), so that every rank's waiting workgroups fit on the chip at once
   int exch_blocks;
   // asynchronous SGD against the device parameter server (requires sgd_on for the compute-copy layout):
-  // the gradient is applied to the SHARED master under the PS writer lock (staleness bound ps.max_stale,
-  // w <- w - ps.lr * g), the local master / bf16 copies / conv fragments are refreshed from the version
-  // just written (or, for a rejected gradient, the current one), and the next microbatch is claimed and
-  // staged: an async step is train + this launch (csrc/lenet_fused.hip, protocol csrc/ps_device.h)
+  // the gradient is admitted by the lock-free version CAS (staleness bound ps.max_stale) and added to the
+  // SHARDED master (w <- w - lr * g), the local master / bf16 copies / conv fragments are refreshed from
+  // the values the adds produced (or, for a rejected gradient, the current ones), and the next microbatch
+  // is claimed and staged: an async step is train + this launch (csrc/lenet_fused.hip, csrc/ps_device.h)
   int ps_on;
   PSArgs ps;
   unsigned long long* stamps;  // diagnostic: [grid][16] wall-clock marks per phase (scripts/lenetstamps.py), or null

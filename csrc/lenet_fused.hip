@@ -1084,7 +1084,7 @@ __device__ __forceinline__ void red_apply(const LeNetRedArgs& a, const RedTables
 // The slot owners wait for it only after their jobs (so it is normally already there), then add
 // -lr * g to their elements of the sharded master and refresh the local copies from the values the adds
 // produced.  No lock is held: the owners of different ranks update the shards in parallel.
-__device__ __forceinline__ unsigned lenet_ps_wait(const LeNetRedArgs& a, unsigned* s_dec) {
+__device__ __forceinline__ unsigned lenet_ps_wait(const LeNetRedArgs& a, unsigned* s_dec, unsigned applied0) {
   const PSArgs& p = a.ps;
   if (threadIdx.x == 0) {
     const unsigned ep = __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
@@ -1092,9 +1092,12 @@ __device__ __forceinline__ unsigned lenet_ps_wait(const LeNetRedArgs& a, unsigne
     unsigned dec = kPSFailed;
     for (;;) {  // relaxed polls, one acquire once the word matches
       const unsigned w = __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((w >> 3) == ep) {
+      if (ps_epoch_eq(w, ep)) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         dec = w & 7u;
+        // the refresh below (adds or reads of the shards) contains every gradient fully applied when this
+        // launch started (+ this one when admitted)
+        if (dec == kPSAccept || dec == kPSReject) ps_note_refresh(p, applied0 + (dec == kPSAccept ? 1u : 0u));
         break;
       }
       if (wall_clock64() - t0 > 2ull * (unsigned long long)p.timeout_ticks) {
@@ -1119,6 +1122,10 @@ __device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, unsigned 
   if (threadIdx.x == 0 && count > 0) {
     const unsigned prev = __hip_atomic_fetch_add(p.scratch + kPSApplyDone, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev + count == arrivals) {
+      // the last arrival: every owner drained its shard adds before arriving, so an admitted gradient is
+      // now fully applied (the decision word was published before any owner or the staging arrival)
+      const unsigned w = __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((w & 7u) == kPSAccept) ps_publish_applied(p);
       __hip_atomic_store(p.scratch + kPSApplyDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(p.scratch + kPSEpoch, __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED,
                                                                  __HIP_MEMORY_SCOPE_AGENT) + 1u,
@@ -1168,6 +1175,9 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
   const int nslot = a.dense_tiles + a.nconv_slots;
   const int G = a.exch_blocks;
   if ((int)blockIdx.x < G) {
+    // async PS: the fully applied count before any shard access of this launch (ps_device.h)
+    unsigned applied0 = 0;
+    if (PS && threadIdx.x == 0) applied0 = ps_read_applied(a.ps);
     if (PS) ps_stage_shards(a.ps, s_shard);
     stage_tables(a, &tabs);
     // with the fused sync update, the first owned slot's master / momentum elements are loaded beside
@@ -1266,7 +1276,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     __syncthreads();
     LR_STAMP(1);
     __shared__ unsigned s_dec;
-    const unsigned dec = (PS && nown > 0) ? lenet_ps_wait(a, &s_dec) : 0u;
+    const unsigned dec = (PS && nown > 0) ? lenet_ps_wait(a, &s_dec, applied0) : 0u;
     LR_STAMP(2);
 #pragma unroll 1
     for (int k = 0; k < nown; ++k) {

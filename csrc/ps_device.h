@@ -4,17 +4,24 @@
 // microbatch claims and completion accounting.
 //
 // Reference: AsynchronousSGDServer applies every uploaded gradient on arrival and hands out the next
-// batch (/root/reference/src/server/asynchronousSGD_server.ts:65-82,95-108); the README's
-// maximumStaleness bound (/root/reference/README.md:27) is the admission check here.  Nothing in the
-// protocol holds a lock across an apply, so applies of different ranks proceed in parallel over xGMI:
-//   admission   one CAS on the shared version word `ver`: admitted iff ver - vpulled <= max_stale, and
-//               then ver -> ver + 1 (a failed CAS re-reads and re-checks);
+// batch (/root/reference/src/server/asynchronousSGD_server.ts:65-82,95-108): a version only ever names
+// fully applied weights (updateModel applies, then save() bumps the version, :73-77,95-108).  The
+// README's maximumStaleness bound (/root/reference/README.md:27) is the admission check here.  Nothing
+// in the protocol holds a lock across an apply, so applies of different ranks proceed in parallel:
+//   admission   one CAS on the shared version word `ver` (= gradients admitted so far): admitted iff
+//               ver - vp <= max_stale, and then ver -> ver + 1 (a failed CAS re-reads and re-checks);
 //   apply       per element, w += -(lr * g) on the owning shard: a plain read-modify-write when this
 //               rank is the only writer (world 1), else a compare-and-swap loop on the element's bits
-//               (no add is lost; adds of different ranks to one element serialise in memory only);
-//   refresh     the local master / compute copies take the value the add produced (admitted) or the
-//               shard's current value (rejected): every add that has landed is visible, an add admitted
-//               concurrently may be missing from some elements (at most world - 1 are in flight).
+//               (no add is lost; adds of different ranks to one element serialise in memory only); when
+//               every add of an admitted gradient has landed, its last workgroup bumps the shared
+//               `applied` counter (the count of FULLY applied gradients);
+//   refresh     every workgroup that copies weights out of the shards (a pull, or the refresh of the
+//               fused reduce launch) first reads `applied` = A, then copies: the copy contains at least
+//               those A updates on every element (plus its own, when the refresh is its own admitted
+//               add).  vp = the minimum of A (+ own) over the refreshing workgroups (kPSVMin).
+// So `ver - vp` at admission bounds from above the number of admitted updates missing from ANY element
+// of the weights the gradient was computed on: the staleness bound holds exactly at every world size
+// (conservatively: an add in flight but partly landed counts as missing).
 #pragma once
 #include "common.h"
 #include "kernels.h"
@@ -22,13 +29,39 @@
 namespace dfa {
 
 // local scratch words (PSArgs::scratch, u32 index)
-constexpr int kPSPullDone = 0, kPSApplyDone = 1, kPSEpoch = 2, kPSDecision = 3, kPSSlots = 64;
+// kPSVMin: min over this step's refreshing workgroups of (applied read before the copy [+ 1 for its own
+// admitted add]); reset to kPSNoVer by the admission that consumes it
+constexpr int kPSPullDone = 0, kPSApplyDone = 1, kPSEpoch = 2, kPSDecision = 3, kPSVMin = kPSVMinWord, kPSSlots = 64;
+constexpr unsigned kPSNoVer = 0xffffffffu;
+// the decision word is (launch epoch << 3) | code: compare epochs modulo 2^29
+__device__ __forceinline__ bool ps_epoch_eq(unsigned word, unsigned ep) { return (word >> 3) == (ep & 0x1fffffffu); }
 // decision codes: admitted (apply + refresh from the new values), rejected as too stale (refresh from the
 // current values), the schedule is finished (no-op), or a wait timed out (no-op, error bits set)
 constexpr unsigned kPSAccept = 1, kPSReject = 2, kPSFailed = 3, kPSFinished = 4;
 
 __device__ __forceinline__ unsigned ps_ld_acq(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The fully applied count, read by thread 0 of every workgroup that refreshes weights from the shards
+// BEFORE any of its shard reads or adds (reading it earlier only makes the count more conservative, so the
+// fused reduce launch reads it at its start, where the load's latency hides behind the jobs).
+__device__ __forceinline__ unsigned ps_read_applied(const PSArgs& a) {
+  return a.applied ? __hip_atomic_load(a.applied, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+}
+// Records that this workgroup's refresh contains `count` fully applied gradients (the applied count it read
+// + 1 when the refresh values are the results of this rank's own admitted adds): kPSVMin = the minimum.
+__device__ __forceinline__ void ps_note_refresh(const PSArgs& a, unsigned count) {
+  if (a.applied != nullptr)
+    __hip_atomic_fetch_min(a.scratch + kPSVMin, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The last workgroup of an ADMITTED apply, after every add of the gradient has landed: each workgroup drained
+// its adds (CAS results returned / plain stores acknowledged, s_waitcnt vmcnt(0)) before its arrival, and
+// the shards are uncached memory, so nothing remains to be written back: a relaxed add orders behind them
+// (a system-scope release here would write back this XCD's L2, ~2-7 us on the critical path).
+__device__ __forceinline__ void ps_publish_applied(const PSArgs& a) {
+  if (a.applied != nullptr) __hip_atomic_fetch_add(a.applied, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // At-least-once FCFS dispatch (/root/reference/src/server/dataset.ts:47-67).  The shared cursor
@@ -117,23 +150,36 @@ __device__ inline void complete_microbatch(const PSArgs& a, long long bid) {
 }
 
 // The admission decision for the gradient of microbatch *bid_out (one thread).  Lock-free: read the
-// version, check the staleness bound, CAS version -> version + 1; a CAS lost to another rank's admission
-// re-reads and re-checks.  Records vpulled (the version the refreshed local weights correspond to), the
-// counters and the microbatch completion.  Returns the decision code.
+// version, check the staleness bound against vp (kPSVMin, see the header), CAS version -> version + 1; a
+// CAS lost to another rank's admission re-reads and re-checks.  Records vp in *vpulled, the counters, the
+// optional audit row and the microbatch completion.  Returns the decision code.
 __device__ inline unsigned ps_admit(const PSArgs& a) {
   const long long bid = *a.bid_out;
-  if (a.done_epoch != nullptr && bid < 0) {  // dataset finished: a no-op step
+  const unsigned long long k = a.stats[0] + a.stats[1];  // this rank's decision index
+  if (a.done_epoch != nullptr && bid < 0) {  // dataset finished: a no-op step (no refresh follows)
     a.stats[6] += 1;
     return kPSFinished;
   }
   const unsigned long long t0 = wall_clock64();
-  const unsigned vp = *a.vpulled;
+  unsigned vp = __hip_atomic_load(a.scratch + kPSVMin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (vp == kPSNoVer) vp = 0;  // no refresh recorded (never on a well-formed step): count from version 0
+  // consumed: this step's refreshers record afresh (they run after the decision, which is published
+  // with release semantics behind this store)
+  __hip_atomic_store(a.scratch + kPSVMin, kPSNoVer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  *a.vpulled = vp;
   unsigned v = __hip_atomic_load(a.ver, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  auto audit = [&](unsigned dec) {
+    if (a.audit != nullptr && k < (unsigned long long)a.audit_cap) {
+      a.audit[3 * k] = v;
+      a.audit[3 * k + 1] = vp;
+      a.audit[3 * k + 2] = dec;
+    }
+  };
   for (;;) {
     const unsigned stale = v - vp;
     if (a.max_stale >= 0 && (int)stale > a.max_stale) {
       a.stats[1] += 1;
-      *a.vpulled = v;  // the refresh reads the current values
+      audit(kPSReject);
       return kPSReject;
     }
     unsigned expected = v;
@@ -142,7 +188,7 @@ __device__ inline unsigned ps_admit(const PSArgs& a) {
       a.stats[0] += 1;
       a.stats[2] += stale;
       if (stale > a.stats[3]) a.stats[3] = stale;
-      *a.vpulled = v + 1u;
+      audit(kPSAccept);
       if (a.done_epoch != nullptr) complete_microbatch(a, bid);
       return kPSAccept;
     }

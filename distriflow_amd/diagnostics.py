@@ -27,6 +27,10 @@ Python switches (default in brackets):
                            the resident workgroups).  Correct (tests/test_kernels_gpu.py), but the hand-off
                            chain stays and the streaming pass runs at the statistics grid: ResNet-18 B=256
                            83.4 k vs 85.0 k images/s (profiles/r4/resnet18_bn_fused_ab.txt)
+  bn_acc [1]               BatchNorm statistics accumulated by the producing kernels' epilogues (fp64 adds into
+                           replicas, csrc/bn_acc.h) and finalised by the consuming apply / dx pass: no
+                           statistics launches (0: the statistics passes of csrc/bn.hip, bitwise reproducible)
+  bn_acc_rep [8]           accumulator replicas per BatchNorm and direction (1..16)
   bn_epilogue [0]          BatchNorm statistics finalised inside the producing conv launches instead of
                            separate statistics passes (correct, but the write-through + ticket tail each
                            conv workgroup then pays costs more than the passes: ResNet-18 B=256 72.3 k vs
@@ -38,7 +42,7 @@ import os
 
 _DEFAULTS = {"lenet_fused": 1, "lenet_fused_update": 1, "async_fused": 1, "kcnn_fused": 1, "khead_fused": 1, "fold_dropout": 1,
              "multistep": 1, "fused_selftest": 1, "wgrad_overlap": 0, "proj_overlap": 0, "concurrent_backward": 0, "bn_epilogue": 0,
-             "bn_fused": 0}
+             "bn_fused": 0, "bn_acc": 1, "bn_acc_rep": 8}
 
 
 def diag(name: str) -> int:

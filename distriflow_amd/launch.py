@@ -351,13 +351,24 @@ def run_async_device(args) -> dict:
     tr.on_upload(lambda st: log.metric(event="upload", **st))
     faults = Faults(args, rank)
     cap = 4 * nb * args.epochs + 64  # a healthy run ends long before: every claim is a real step
+    # without per-step fault hooks the steps run as multi-step graph replays, like the sync loop (no
+    # per-step host work); the host only polls finished() between chunks.  Steps after the last epoch are
+    # device no-ops.
+    chunked = not (faults.kill or faults.delay)
+    chunk = 32 if chunked else 8
+    if chunked:
+        tr.prepare_run(chunk)
     t0 = time.perf_counter()
     steps = 0
     while True:
-        for _ in range(8):
-            faults.step(steps)
-            st = tr.step()
-            steps += 1
+        if chunked:
+            st = tr.run(chunk)
+            steps += chunk
+        else:
+            for _ in range(chunk):
+                faults.step(steps)
+                st = tr.step()
+                steps += 1
         if tr.finished():
             break
         if steps >= cap:
@@ -378,6 +389,7 @@ def run_async_device(args) -> dict:
                    images_per_s=world * steps * B / max(el, 1e-9), last_loss=float(st[0]) / B,
                    eval_loss=float(loss), eval_accuracy=float(acc), max_staleness_bound=args.max_staleness,
                    capture_warmup=tr.capture_warmup if tr.graph_mode == "full" else 0, step=tr.step_launches,
+                   graph=tr.graph_mode, capture_error=getattr(tr, "capture_error", None),
                    **tr.ps_stats())
         log.metric(event="async_done", **out)
         print(json.dumps(out), flush=True)

@@ -29,11 +29,12 @@ class Merge(Layer):
     """A Keras merge layer: ``kind`` in ops.MERGE_KINDS; inputs share the batch and spatial shape
     (Concatenate: channels, the last axis, side by side)."""
 
-    def __init__(self, kind: str, name=None):
+    def __init__(self, kind: str, name=None, axis: int = -1):
         if kind not in ops.MERGE_KINDS:
             raise NotImplementedError(f"Keras merge layer {kind}")
         super().__init__(name or kind.lower())
         self.kind = kind
+        self.axis = int(axis)  # Keras axis, batch axis included (Concatenate only)
         self.in_shapes: list = []
 
     def build_multi(self, shapes: list) -> tuple:
@@ -43,6 +44,14 @@ class Merge(Layer):
         if self.kind == "Subtract" and len(shapes) != 2:
             raise ValueError("Subtract takes exactly two inputs")
         if self.kind == "Concatenate":
+            # Keras counts the batch axis: rank-r inputs (r = len(shape) + 1) concatenate on the last axis
+            # when axis is -1 or r - 1; any other axis is not the channel / feature axis
+            ranks = {len(s) + 1 for s in shapes}
+            if len(ranks) != 1:
+                raise ValueError(f"Concatenate inputs of different rank: {shapes}")
+            r = ranks.pop()
+            if self.axis not in (-1, r - 1):
+                raise NotImplementedError(f"Concatenate on axis {self.axis} of rank-{r} inputs (only the last axis)")
             lead = {s[:-1] for s in shapes}
             if len(lead) != 1:
                 raise ValueError(f"Concatenate inputs differ outside the channel axis: {shapes}")

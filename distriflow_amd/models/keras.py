@@ -119,9 +119,8 @@ def _make_layer(k: str, c: dict) -> Layer:
     if k == "BatchNormalization":
         return BatchNorm(momentum=1.0 - c.get("momentum", 0.99), eps=c.get("epsilon", 1e-3), name=name)
     if k in _MERGES:
-        if k == "Concatenate" and c.get("axis", -1) not in (-1, 3):
-            raise NotImplementedError("Concatenate on an axis other than the channels")
-        return Merge(k, name=name)
+        # the axis is checked against the inputs' rank when the graph is built (Merge.build_multi)
+        return Merge(k, name=name, axis=int(c.get("axis", -1)) if k == "Concatenate" else -1)
     raise NotImplementedError(f"Keras layer {k}")
 
 

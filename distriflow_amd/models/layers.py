@@ -226,9 +226,28 @@ class Conv2D(Layer):
             s.append(ParamSpec(f"{self.name}/bias", (self.filters,), "vector", init="zeros"))
         return s
 
+    fwd_bn = None  # the BatchNorm that consumes this conv's output in a layer chain (Net._plan)
+
+    def bacc_ok(self, dgrad: bool, mode: int, two: bool = False, has_res: bool = False, has_mask: bool = False) -> bool:
+        """Can this conv's forward (or data-gradient) launch accumulate the sums of a consuming BatchNorm in
+        its epilogue (csrc/bn_acc.h)?  Shape / dispatch dependent; cached per variant."""
+        if self.out is None or self.out.device.type != "cuda" or not diag_on("bn_acc"):
+            return False
+        key = (dgrad, mode, two, has_res, has_mask)
+        if key not in self._bacc_cache:
+            H, W, C = self.in_shape
+            OH, OW, N = self.out_shape
+            kp = dgrad_kpad_of(self) if dgrad else primary_kpad_of(self)
+            self._bacc_cache[key] = ops.conv_bacc_ok(self._B, H, W, C, OH, OW, N, self.k, self.k, self.stride, self.pad,
+                                                     kp, dgrad=dgrad, mode=mode, two=two, has_res=has_res,
+                                                     has_mask=has_mask)
+        return self._bacc_cache[key]
+
     def alloc(self, B, device, dtype, ws):
         super().alloc(B, device, dtype, ws)
         self.ws = ws
+        self._B = B
+        self._bacc_cache = {}
         # BatchNorm statistics finalised inside this conv's own launches (csrc/bn_epi.h): the forward's for
         # the BN that consumes the output, the data gradient's for the BN that produced the input
         self._bn_fwd = self._bn_bwd = None
@@ -249,21 +268,28 @@ class Conv2D(Layer):
                     self._bn_bwd = (z((ntm + ng) * 2 * C, torch.float32), z(ntn * (1 + ng), torch.int32))
 
     def forward(self, x, training, bn: Optional["BatchNorm"] = None):
-        """``bn``: the BatchNorm that consumes this output; in training its batch statistics are finalised
-        inside this launch when it can (no statistics pass over the output, no finalize launch)."""
+        """``bn``: the BatchNorm that consumes this output (default: ``fwd_bn``); in training its batch
+        statistics come from this launch when it can: the epilogue accumulates their sums (csrc/bn_acc.h,
+        default) or finalises them (``bn_epilogue`` diagnostic) -- no statistics pass over the output."""
         self.x = x
         st = self.store
         b = st[f"{self.name}/bias"] if self.use_bias else None
-        spec = None
+        bn = bn if bn is not None else self.fwd_bn
+        spec = bacc = None
         if bn is not None and training and self._bn_fwd is not None:
             ws, tk = self._bn_fwd
             spec = dict(ws=ws, ticket=tk, mode=0, vecs=[bn.mean, bn.invstd, bn.run_mean, bn.run_var],
                         momentum=bn.momentum, eps=bn.eps)
+        elif bn is not None and training and bn.acc_on and self.bacc_ok(False, 0):
+            bacc = dict(acc=bn.acc, mode=0)
         ops.conv_fwd(x, st.weight(f"{self.name}/kernel"), b, self.out, self.k, self.k, self.stride, self.pad,
-                     relu=self.relu, bn=spec)
+                     relu=self.relu, bn=spec, bacc=bacc)
         if spec is not None:
             bn.x = self.out
             bn._stats_ready = True
+        if bacc is not None:
+            bn.x = self.out
+            bn._fwd_acc_ready = True
         return self.out
 
     def can_emit_bn_grad(self) -> bool:
@@ -281,22 +307,35 @@ class Conv2D(Layer):
         gb = st.gradient(f"{self.name}/bias") if self.use_bias else None
         ops.conv_wgrad(dy, self.x, st.grad_matrix(kn), gb, self.ws.wgrad, self.k, self.k, self.stride, self.pad)
 
-    def backward_data(self, dy, residual=None, residual_mask=None, dx_mask=None, bn: Optional["BatchNorm"] = None):
+    def backward_data(self, dy, residual=None, residual_mask=None, dx_mask=None, bn: Optional["BatchNorm"] = None,
+                      bn_acc: Optional[list] = None):
         """``bn``: the BatchNorm whose output this layer consumed; its backward statistics (dgamma, dbeta,
-        dx coefficients) are finalised inside this launch over the stored (masked) gradient."""
+        dx coefficients) are finalised inside this launch over the stored (masked) gradient.  ``bn_acc``:
+        the (one or two) BatchNorms whose output gradient this data gradient IS (relu' applied by the
+        epilogue mask): the epilogue accumulates their backward sums (csrc/bn_acc.h) when it can."""
         if not self.need_dx:
             return None
         st = self.store
         kn = f"{self.name}/kernel"
         mask = dx_mask if dx_mask is not None else (self.x if self.in_relu else None)
-        spec = None
+        spec = bacc = None
         if bn is not None:
             ws, tk = self._bn_bwd
             spec = dict(ws=ws, ticket=tk, mode=1, x=bn.x,
                         vecs=[bn.mean, bn.invstd, st[f"{bn.name}/gamma"], st.gradient(f"{bn.name}/gamma"),
                               st.gradient(f"{bn.name}/beta"), bn.coef])
+        elif bn_acc and mask is not None and all(b.acc_on and b.x is not None for b in bn_acc) and len(bn_acc) <= 2 \
+                and self.bacc_ok(True, 1, two=len(bn_acc) == 2, has_res=residual is not None, has_mask=True):
+            b0 = bn_acc[0]
+            bacc = dict(acc=b0.acc_b, mode=1, x=b0.x, mean=b0.mean, invstd=b0.invstd)
+            if len(bn_acc) == 2:
+                b1 = bn_acc[1]
+                bacc.update(acc2=b1.acc_b, x2=b1.x, mean2=b1.mean, invstd2=b1.invstd)
         ops.conv_dgrad(dy, st.weight(kn), st.weight_t(kn), self.dx, self.k, self.k, self.stride, self.pad,
-                       mask=mask, residual=residual, residual_mask=residual_mask, bn=spec)
+                       mask=mask, residual=residual, residual_mask=residual_mask, bn=spec, bacc=bacc)
+        if bacc is not None:
+            for b in bn_acc:
+                b._bwd_acc_ready = True
         return self.dx
 
     def config(self):
@@ -499,6 +538,19 @@ class BatchNorm(Layer):
         self.coef = torch.zeros(3 * self.C, device=device)               # dx = k1*g + k2*x + k3
         # last-arriver ticket counters of the statistics launches (forward row 0, backward row 1)
         self.counter = torch.zeros(2, ops.BN_COUNTERS, dtype=torch.int32, device=device)
+        # sums accumulated by the producing kernels' epilogues (csrc/bn_acc.h): acc = forward [S, Q] of the
+        # conv output, acc_b = backward [S, Q] of the output gradient; each consumer clears the other one
+        C = self.C
+        self.acc_on = (torch.device(device).type == "cuda" and diag_on("bn_acc") and C % 8 == 0 and C <= 1024
+                       and 256 % (C // 8) == 0)
+        self.acc = self.acc_b = None
+        if self.acc_on:
+            from ..diagnostics import diag
+
+            nrep = max(1, min(16, diag("bn_acc_rep")))
+            self.acc_all = torch.zeros(2, nrep, 2, C, dtype=torch.float64, device=device)
+            self.acc, self.acc_b = self.acc_all[0], self.acc_all[1]
+        self._fwd_acc_ready = self._bwd_acc_ready = False
 
     def stats(self, x):
         """Training-mode batch statistics of ``x`` (and the running statistics); writes no output."""
@@ -535,8 +587,35 @@ class BatchNorm(Layer):
                          residual.reshape(-1, self.C) if residual is not None else None, rbn, self.momentum, self.eps)
         return True
 
+    def apply_acc(self, x, out, residual=None, residual_bn=None, relu=None):
+        """Training out = act(bn(x) [+ residual | + residual_bn(residual)]) with the statistics finalised from
+        the producers' accumulated sums (this BN's and the residual BN's): one launch, no statistics pass."""
+        st = self.store
+        rb = None
+        if residual_bn is not None:
+            r = residual_bn
+            rb = [st[f"{r.name}/gamma"], st[f"{r.name}/beta"], r.acc, r.acc_b, r.mean, r.invstd, r.run_mean, r.run_var]
+            r._fwd_acc_ready = False
+        self._fwd_acc_ready = False
+        ops.bn_apply_acc(x.reshape(-1, self.C), out.view(-1, self.C), st[f"{self.name}/gamma"], st[f"{self.name}/beta"],
+                         self.acc, self.acc_b, self.mean, self.invstd, self.run_mean, self.run_var,
+                         self.relu if relu is None else relu,
+                         residual.reshape(-1, self.C) if residual is not None else None, rb, self.momentum, self.eps)
+        return out
+
+    def drop_acc(self):
+        """This step's statistics take the other path: clear both accumulators (the producers only ever add
+        into zeroed ones), so a later step can use the accumulated path again."""
+        self._fwd_acc_ready = self._bwd_acc_ready = False
+        if self.acc_on:
+            self.acc_all.zero_()
+
     def forward(self, x, training):
         self.x = x
+        if training and self._fwd_acc_ready:  # the producer accumulated this batch's sums
+            return self.apply_acc(x, self.out)
+        if training and self.acc_on:
+            self.drop_acc()
         if training and self.fused_forward(x, self.out):
             return self.out
         if training and not self._stats_ready:
@@ -544,14 +623,31 @@ class BatchNorm(Layer):
         self._stats_ready = False
         return self.apply(x, self.out, training)
 
+    def _dx_from_acc(self, g):
+        """dx from a gradient g whose backward sums the producing kernel accumulated (relu' applied)."""
+        st = self.store
+        self._bwd_acc_ready = False
+        ops.bn_dx_acc(self.x.reshape(-1, self.C), g.reshape(-1, self.C), self.dx.view(-1, self.C), self.acc_b, self.acc,
+                      st[f"{self.name}/gamma"], self.mean, self.invstd, st.gradient(f"{self.name}/gamma"),
+                      st.gradient(f"{self.name}/beta"), self.coef)
+        return self.dx
+
     def backward_dx(self, g):
         """dx from a gradient ``g`` (relu' already applied) whose statistics the producing conv launch
-        finalised (Conv2D.backward_data(bn=self)): the dx pass only."""
+        finalised (Conv2D.backward_data(bn=self)) or accumulated (bn_acc=[self]): the dx pass only."""
+        if self._bwd_acc_ready:
+            return self._dx_from_acc(g)
         ops.bn_dx(self.x.reshape(-1, self.C), g.reshape(-1, self.C), self.dx.view(-1, self.C), self.coef)
         return self.dx
 
     def backward(self, dy, mask=None):
         """``mask``: relu' source applied to dy (default: this layer's own output when it ends in ReLU)."""
+        if self._bwd_acc_ready:  # dy is the premasked g whose sums its producer accumulated
+            if self.in_relu:
+                raise NotImplementedError("BatchNorm after a fused ReLU")
+            return self._dx_from_acc(dy)
+        if self.acc_on:
+            self.drop_acc()
         st = self.store
         if mask is None and self.relu and not self.grad_premasked:
             mask = self.out
@@ -597,6 +693,15 @@ class GlobalAveragePooling2D(Layer):
     def backward(self, dy):
         if not self.need_dx:
             return None
+        sinks = getattr(self, "dx_bn_sinks", None) or []
+        if (self.in_relu and len(sinks) == 1 and sinks[0].acc_on and sinks[0].x is not None and self.dx.is_cuda
+                and self.dx.shape[-1] <= 1024 and 256 % (self.dx.shape[-1] // 4) == 0):
+            # the relu' of the producing block's output and that block's last BatchNorm's backward sums in
+            # the same launch (its gradient g IS this dx)
+            b = sinks[0]
+            ops.gap_bwd_bn(dy, self.x, self.dx, b.acc_b, b.x, b.mean, b.invstd)
+            b._bwd_acc_ready = True
+            return self.dx
         ops.gap_bwd(dy, self.dx)
         if self.in_relu:
             ops.relu_bwd(self.x, self.dx, self.dx)
@@ -679,7 +784,7 @@ class ResidualBlock(Layer):
     def _proj_forward(self, x, training):
         p = self.proj.forward(x, training, bn=self.proj_bn)
         self.proj_bn.x = p
-        if training and not self.proj_bn._stats_ready:
+        if training and not self.proj_bn._stats_ready and not self.proj_bn._fwd_acc_ready:
             self.proj_bn.stats(p)
         self.proj_bn._stats_ready = False
         return p
@@ -705,8 +810,18 @@ class ResidualBlock(Layer):
             else:
                 p = self._proj_forward(x, training)
             r, rbn = p, self.proj_bn
-        # out = relu(bn2(h) + shortcut), shortcut = x or proj_bn(proj(x)): bn2's statistics and this
-        # streaming pass in one launch when the fused kernel covers the shape
+        # out = relu(bn2(h) + shortcut), shortcut = x or proj_bn(proj(x)): with the producers' accumulated
+        # sums one streaming launch finalises both BatchNorms' statistics and joins; else bn2's statistics
+        # and this streaming pass in one launch when the fused kernel covers the shape
+        if training and self.bn2._fwd_acc_ready and (rbn is None or rbn._fwd_acc_ready):
+            self.bn2.apply_acc(h, self.out, residual=r, residual_bn=rbn, relu=True)
+            return self.out
+        for b in (self.bn2, rbn):  # (only one of the two has accumulated sums: statistics passes instead)
+            if training and b is not None and b._fwd_acc_ready:
+                b.drop_acc()
+                b.stats(b.x)
+                if b is self.bn2:
+                    b._stats_ready = True
         if training and self.bn2.fused_forward(h, self.out, residual=r, residual_bn=rbn, relu=True):
             return self.out
         if training and not self.bn2._stats_ready:
@@ -747,7 +862,12 @@ class ResidualBlock(Layer):
                 pev = ps.record_event()
         d = self.bn2.backward(dy, mask=omask)
         weights(self.conv2, d)
-        if self.conv2.can_emit_bn_grad() and not self.bn1.grad_premasked:
+        if (self.bn1.acc_on and not self.bn1.grad_premasked
+                and self.conv2.bacc_ok(True, 1, two=False, has_res=False, has_mask=True)):
+            # conv2's data gradient applies bn1's relu' and accumulates bn1's backward sums (csrc/bn_acc.h)
+            d = self.conv2.backward_data(d, dx_mask=self.bn1.out, bn_acc=[self.bn1])
+            d = self.bn1.backward_dx(d)
+        elif self.conv2.can_emit_bn_grad() and not self.bn1.grad_premasked:
             # conv2's data gradient applies bn1's relu' and finalises bn1's backward statistics itself
             d = self.conv2.backward_data(d, dx_mask=self.bn1.out, bn=self.bn1)
             d = self.bn1.backward_dx(d)
@@ -768,7 +888,10 @@ class ResidualBlock(Layer):
             res, res_mask = ds, None
         else:
             res, res_mask = dy, omask
-        self.conv1.backward_data(d, residual=res, residual_mask=res_mask, dx_mask=self.x if self.in_relu else None)
+        # and, when the previous layer's BatchNorms consume this gradient (Net._plan: dx_bn_sinks), their
+        # backward sums accumulate in the same epilogue
+        self.conv1.backward_data(d, residual=res, residual_mask=res_mask, dx_mask=self.x if self.in_relu else None,
+                                 bn_acc=getattr(self, "dx_bn_sinks", None) if self.in_relu else None)
         return self.dx
 
     def config(self):

@@ -146,6 +146,20 @@ class Net:
             l.grad_premasked = bool(l.relu and j + 1 < len(execd) and execd[j + 1].in_relu)
         if self.fuse and self.is_gpu and diag_on("fold_dropout"):
             execd = self._fold_dropout(execd)
+        # BatchNorm sums accumulated by their producers' epilogues (csrc/bn_acc.h): the conv that feeds a
+        # BatchNorm in the chain, and the layer whose data gradient IS the output gradient of the previous
+        # layer's BatchNorms (relu' applied by that data gradient's mask: ResNet blocks, the GAP)
+        for j, l in enumerate(execd):
+            l.dx_bn_sinks = []
+            if isinstance(l, Conv2D) and j + 1 < len(execd) and isinstance(execd[j + 1], BatchNorm):
+                l.fwd_bn = execd[j + 1]
+            if j == 0 or not l.in_relu:
+                continue
+            prev = execd[j - 1]
+            if isinstance(prev, ResidualBlock):
+                l.dx_bn_sinks = [prev.bn2] + ([prev.proj_bn] if prev.proj is not None else [])
+            elif isinstance(prev, BatchNorm) and prev.relu and prev.grad_premasked:
+                l.dx_bn_sinks = [prev]
         self.exec_layers = execd
         self.output_shape = shape
         self.head_start = self._plan_head(execd) if self.fuse else None
@@ -323,10 +337,24 @@ class Net:
         self.graphs = {}
 
     # ------------------------------------------------------------------ compute
+    _bn_acc_dirty = False
+
+    def _bn_acc_begin(self):
+        """A training forward starts.  The BatchNorm accumulators are cleared by their consumers (each pass
+        clears the other direction's), which holds for every forward followed by its backward; after a
+        training forward whose backward never ran, clear them all first."""
+        if self._bn_acc_dirty:
+            for l in self._all_leaf_layers():
+                if isinstance(l, BatchNorm) and getattr(l, "acc_on", False):
+                    l.drop_acc()
+        self._bn_acc_dirty = True
+
     def forward(self, x, training: bool = False) -> torch.Tensor:
         """Returns fp32 logits [B][classes] (a view of an engine buffer).  ``x`` is a tensor or an
         :class:`ops.GatherRef` (rows of the HBM dataset; fused into the first layer when it can)."""
         self.bind(x.shape[0])
+        if training:
+            self._bn_acc_begin()
         if isinstance(x, ops.GatherRef) and not isinstance(self.exec_layers[0], (FusedConvPool, KerasConvBlock)):
             x = x.materialise(self.x_buf, step_inc=self._take_gather_step())
         h = x
@@ -346,6 +374,7 @@ class Net:
             d = self.exec_layers[i].backward(d)
             if grad_ready is not None:
                 grad_ready(i)
+        self._bn_acc_dirty = False
 
     # Scale of the per-example loss gradients: None = 1 / rows of the step (the mean loss).  A FedSGD step
     # over several microbatches per rank (DataParallelTrainer min_updates_per_version) sets 1 / microbatch
@@ -476,6 +505,7 @@ class Net:
         """Body layers one by one, then the fused dense head (2 launches: forward + CE + backward data
         chain, then all head weight gradients), then the body's backward from the head's dX."""
         self.bind(x.shape[0])
+        self._bn_acc_begin()
         if isinstance(x, ops.GatherRef) and not isinstance(self.exec_layers[0], (FusedConvPool, KerasConvBlock)):
             x = x.materialise(self.x_buf, step_inc=self._take_gather_step())
         h = x
@@ -556,6 +586,7 @@ class Net:
             if grad_ready is not None:
                 for j in waiting:
                     grad_ready(j)
+            self._bn_acc_dirty = False
             return self.stats
         # critical path on the main stream: head fwd/CE/bwd-data -> each body layer's data gradient;
         # weight gradients fork onto side streams as soon as their input gradient exists.  Gradient
@@ -586,6 +617,7 @@ class Net:
         if grad_ready is not None:
             for i in range(len(self.exec_layers) - 1, -1, -1):
                 grad_ready(i)
+        self._bn_acc_dirty = False
         return self.stats
 
     def _head_launch(self, args, head, x, labels, idx, phases):

@@ -126,15 +126,45 @@ def _bn_kwargs(bn):
                 bn_gscale=float(bn.get("gscale", 1.0)))
 
 
-def conv_fwd(x, w, bias, out, KH, KW, stride=1, pad=0, relu=False, bn=None):
+def _bacc_kwargs(bacc):
+    """igemm launch arguments of epilogue-accumulated BatchNorm sums (kernels.h BnAcc, csrc/bn_acc.h):
+    ``bacc`` = dict(acc=[nrep][2][N] float64, mode=0) or dict(acc, mode=1, x, mean, invstd[, acc2, x2, mean2,
+    invstd2]) -- mode 1 with the BatchNorm input(s) at the output's positions."""
+    if bacc is None:
+        return {}
+    kw = dict(bacc=bacc["acc"], bacc_mode=int(bacc.get("mode", 0)))
+    if kw["bacc_mode"] == 1:
+        kw["bacc_in"] = [bacc["x"], bacc["mean"], bacc["invstd"]]
+        if bacc.get("acc2") is not None:
+            kw.update(bacc2=bacc["acc2"], bacc2_in=[bacc["x2"], bacc["mean2"], bacc["invstd2"]])
+    return kw
+
+
+def conv_bacc_ok(B, H, W, C, OH, OW, N, KH, KW, stride, pad, Kpad, dgrad=False, mode=0, two=False,
+                 has_res=False, has_mask=False) -> bool:
+    """Can the conv launch (forward, or the data gradient with output [B][H][W][C]) accumulate BatchNorm
+    sums of its output in its epilogue (igemm_bacc_ok on the dispatch the launch will take)?"""
+    m = native.get(build_if_missing=False)
+    if m is None or not hasattr(m, "igemm_bacc_supported"):
+        return False
+    if dgrad:
+        return bool(m.igemm_bacc_supported(B * H * W, C, KH * KW * N, Kpad, _geom(OH, OW, N, H, W, KH, KW, stride, pad),
+                                           MODE_DGRAD, int(mode), bool(two), bool(has_res), bool(has_mask)))
+    return bool(m.igemm_bacc_supported(B * OH * OW, N, KH * KW * C, Kpad, _geom(H, W, C, OH, OW, KH, KW, stride, pad),
+                                       MODE_FWD, int(mode), bool(two), bool(has_res), bool(has_mask)))
+
+
+def conv_fwd(x, w, bias, out, KH, KW, stride=1, pad=0, relu=False, bn=None, bacc=None):
     """NHWC conv: out[B][OH][OW][N]; w = [Npad][Kpad] with K = KH*KW*C.  ``bn``: the consuming
-    BatchNorm's statistics are finalised inside this launch (:func:`_bn_kwargs`, :func:`conv_bn_layout`)."""
+    BatchNorm's statistics are finalised inside this launch (:func:`_bn_kwargs`, :func:`conv_bn_layout`).
+    ``bacc``: the consuming BatchNorm's sums are accumulated by the epilogue (:func:`_bacc_kwargs`)."""
     B, H, W, C = x.shape
     _, OH, OW, N = out.shape
     if x.is_cuda:
         K = KH * KW * C
         _C().igemm_fwd(x, w, bias, None, out, B * OH * OW, N, K, w.shape[1], 0, N,
-                       _geom(H, W, C, OH, OW, KH, KW, stride, pad), MODE_FWD, relu, 1.0, **_bn_kwargs(bn))
+                       _geom(H, W, C, OH, OW, KH, KW, stride, pad), MODE_FWD, relu, 1.0, **_bn_kwargs(bn),
+                       **_bacc_kwargs(bacc))
     else:
         out.copy_(ref.conv_fwd(x, w, bias, KH, KW, stride, pad, relu))
     return out
@@ -240,19 +270,21 @@ def kcnn_bwd(x, w1, b1, w2t, dyp, code, slabs, g_w1, g_b1, g_w2, g_b2, step_inc=
                   slabs, g_w1, g_b1, g_w2, g_b2, step_inc=step_inc)
 
 
-def conv_dgrad(dy, w, wt, out, KH, KW, stride=1, pad=0, mask=None, residual=None, residual_mask=None, bn=None):
+def conv_dgrad(dy, w, wt, out, KH, KW, stride=1, pad=0, mask=None, residual=None, residual_mask=None, bn=None,
+               bacc=None):
     """dX (NHWC [B][H][W][C]) of a conv whose output gradient is dy [B][OH][OW][N].
 
     Epilogue (ResNet block join): dX = (conv^T dy + residual * [residual_mask > 0]) * [mask > 0].
     ``bn`` (mode 1): dX is the output gradient of a BatchNorm; its backward statistics are finalised
-    inside this launch (:func:`_bn_kwargs`)."""
+    inside this launch (:func:`_bn_kwargs`).  ``bacc`` (mode 1): its backward sums are accumulated by
+    the epilogue instead (:func:`_bacc_kwargs`)."""
     B, OH, OW, N = dy.shape
     _, H, W, C = out.shape
     if dy.is_cuda:
         K = KH * KW * N
         _C().igemm_fwd(dy, wt, None, mask, out, B * H * W, C, K, wt.shape[1], 0, C,
                        _geom(OH, OW, N, H, W, KH, KW, stride, pad), MODE_DGRAD, False, 1.0, residual, residual_mask,
-                       **_bn_kwargs(bn))
+                       **_bn_kwargs(bn), **_bacc_kwargs(bacc))
     else:
         dx = ref.conv_dgrad(dy, w, out.shape, KH, KW, stride, pad, None)
         if residual is not None:
@@ -630,6 +662,37 @@ def bn_fwd_fused(x2d, y2d, gamma, beta, mean, invstd, run_mean, run_var, ws, cou
     _C().bn_fwd_fused(x2d, y2d, gamma, beta, mean, invstd, run_mean, run_var, residual, rg, rb, rm, ri, ws, counter,
                       M, C, relu, momentum, eps)
     return y2d
+
+
+def bn_apply_acc(x2d, y2d, gamma, beta, acc, zero, mean, invstd, run_mean, run_var, relu=False, residual=None,
+                 rbn=None, momentum=0.1, eps=1e-5):
+    """Training y = act(bn(x) [+ r | + bn_r(r)]) with the batch statistics finalised from the producing
+    conv's accumulated sums ``acc`` (csrc/bn.hip bn_apply_acc): writes mean / invstd / running statistics
+    and clears ``zero`` (the other direction's accumulator).  ``rbn``: the residual's BatchNorm as
+    [gamma, beta, acc, zero, mean, invstd, run_mean, run_var] (its statistics finalised the same way)."""
+    M, C = x2d.shape
+    z = zero if zero is not None else None
+    rb = list(rbn) if rbn is not None else []
+    if rb and rb[3] is None:
+        rb[3] = torch.empty(0, dtype=torch.float64, device=x2d.device)
+    _C().bn_apply_acc(x2d, y2d, gamma, beta, acc, z, mean, invstd, run_mean, run_var, residual, rb, M, C, relu,
+                      momentum, eps)
+    return y2d
+
+
+def bn_dx_acc(x2d, g2d, dx2d, acc, zero, gamma, mean, invstd, dgamma, dbeta, coef, gscale=1.0):
+    """dx = k1 g + k2 x + k3 with the coefficients finalised from the producer's backward sums ``acc``
+    (csrc/bn.hip bn_dx_acc); also writes dgamma, dbeta (x gscale) and coef, and clears ``zero``."""
+    M, C = x2d.shape
+    _C().bn_dx_acc(x2d, g2d, dx2d, acc, zero, gamma, mean, invstd, dgamma, dbeta, coef, M, C, gscale)
+    return dx2d
+
+
+def gap_bwd_bn(dy, mask, dx, acc, x, mean, invstd):
+    """GAP backward with relu'(mask) and the BatchNorm backward sums of dx (``x`` = that BN's input)."""
+    B, H, W, C = dx.shape
+    _C().gap_bwd_bn(dy.contiguous(), mask, dx, B, H * W, C, acc, [x, mean, invstd])
+    return dx
 
 
 def bn_dx(x2d, g2d, dx2d, coef):

@@ -30,6 +30,12 @@ Other models: ``ps_fetch_pull`` (claim + copy out of the shards), bf16 refresh, 
 
 Ranks never wait for each other.  A slow rank only makes its own gradients staler, which the bound
 then rejects.  The admission CAS is the one serialisation point (one remote atomic per step per rank).
+
+Staleness is exact (an upper bound that always holds): an admitted gradient's last workgroup bumps a
+shared ``applied`` counter once every one of its adds has landed, and every refresh records the applied
+count it read BEFORE copying; admission compares the version against the minimum of those counts, so
+``version - vp <= max_staleness`` bounds the updates missing from any element of the weights the
+gradient was computed on (csrc/ps_device.h).
 """
 from __future__ import annotations
 
@@ -96,12 +102,13 @@ class AsyncPSTrainer(DataParallelTrainer):
         self.fused_ps = (bool(getattr(net, "lenet_fused", False)) and net.store.lenet_frag is not None
                          and diag_on("async_fused"))
         # a warm-up step would claim a microbatch and apply a real gradient to the shared master: the
-        # capture warms up with a compute-only step instead (_capture)
+        # capture warms up with a compute-only step instead (_capture).  The reduce launch's owners wait for
+        # the staging workgroup's admission decision (no lock is taken), then add or read their slots.
         self.capture_warmup = 0
         if self.fused_ps:
             # ranks that time-share one GPU: fewer protocol workgroups per rank (each owning several
-            # slots), so every rank's workgroups waiting for its lock decision fit on the chip beside the
-            # lock holder's (one rank per GPU: one workgroup per slot, all resident)
+            # slots), so every rank's workgroups waiting for their admission decision fit on the chip beside
+            # the other ranks' (one rank per GPU: one workgroup per slot, all resident)
             net.lenet_exch_blocks = shared_gpu_exch_blocks(self.world)
         self._primed = False
         self._ps_stats_dev = self.ps.stats_tensor()  # device view of this rank's PS counters (callbacks)
@@ -170,6 +177,16 @@ class AsyncPSTrainer(DataParallelTrainer):
 
     def prepare_run(self, n: int):
         self._prime()
+        if self.graph_mode == "full" and self._graph is None and self._has_schedule():
+            # capture here WITHOUT the eager fallback step of _capture_with_fallback: a step taken outside
+            # step() / run() would be a real, uncounted parameter-server update
+            try:
+                self._capture()
+            except Exception as e:
+                torch.cuda.synchronize(self.net.device)
+                self.capture_error = repr(e)
+                self._graph = None
+                self.graph_mode = "none"
         super().prepare_run(n)
 
     def _capture(self):
@@ -226,10 +243,11 @@ class AsyncPSTrainer(DataParallelTrainer):
 
     # ------------------------------------------------------------------ state
     def ps_stats(self) -> dict:
-        acc, rej, ssum, smax, retries, err, version, cursor, noops = self.ps.stats()
+        acc, rej, ssum, smax, retries, err, version, cursor, noops, applied = self.ps.stats()
         epoch, in_epoch, completed, redisp, skipped, dups, fin = self.ps.schedule_stats()
         return {"accepted": acc, "rejected": rej, "mean_staleness": ssum / acc if acc else 0.0,
                 "max_staleness": smax, "admit_retries": retries, "error": err, "version": version,
+                "applied": applied,
                 "cursor": cursor, "noop_steps": noops, "epoch": epoch, "completed_in_epoch": in_epoch,
                 "completed": completed, "redispatched": redisp, "skipped": skipped, "duplicates": dups,
                 "finished": bool(fin)}

@@ -275,6 +275,13 @@ class DataParallelTrainer:
         cursor = self._index_stream[1].clone() if self._index_stream is not None else None
         rs0 = self.run_stats.clone()
         comm = self.p2p.comm
+        from .p2p import _agree
+
+        gloo = dist.get_backend(self.group) == "gloo"
+        # Every collective below is entered by EVERY rank: local work runs under try, and the ranks agree on
+        # its outcome before the next collective (a rank that raised must not leave its peers blocked in an
+        # all_gather it never reaches -- ADVICE r4).
+        g_local = None
         try:
             n_rows = self.data.shape[0]
             self.idx.copy_((torch.arange(self.B, device=dev, dtype=torch.int64) * 7919 + 104729 * self.rank + 17)
@@ -284,34 +291,40 @@ class DataParallelTrainer:
             net.compute_gradients(self.xb, self.yb)
             torch.cuda.synchronize(dev)
             g_local = net.store.grad.clone()
-            gloo = dist.get_backend(self.group) == "gloo"
-            parts = [torch.empty_like(g_local, device="cpu" if gloo else dev) for _ in range(self.world)]
-            dist.all_gather(parts, g_local.cpu() if gloo else g_local, group=self.group)
-            ref = parts[0].cpu().clone()
-            for r in range(1, self.world):
-                ref += parts[r].cpu()  # rank order, fp32: the in-kernel exchange's summation order
-            net.restore_state(snap)
-            comm.set_timeout(5.0)
-            self._gather()
-            net.compute_gradients_and_update(self.xb, self.yb, None, ll=comm)
-            torch.cuda.synchronize(dev)
-            if comm.error() != 0:
-                res.update(ok=False, why="peer timeout in the fused exchange self-test")
-            elif not torch.equal(net.store.grad.cpu(), ref):
-                bad = int((net.store.grad.cpu() != ref).sum())
-                res.update(ok=False, why=f"fused exchange self-test: {bad} gradient elements differ from the "
-                                         f"rank-order sum")
-            else:
+        except Exception as e:  # noqa: BLE001 (any failure -> the unfused path)
+            res.update(ok=False, why=f"fused exchange self-test (local gradient) raised {e!r:.200}")
+        try:
+            if _agree(res["ok"], self.group, dev):
+                parts = [torch.empty_like(g_local, device="cpu" if gloo else dev) for _ in range(self.world)]
+                dist.all_gather(parts, g_local.cpu() if gloo else g_local, group=self.group)
+                ref = parts[0].cpu().clone()
+                for r in range(1, self.world):
+                    ref += parts[r].cpu()  # rank order, fp32: the in-kernel exchange's summation order
+                net.restore_state(snap)
+                try:
+                    comm.set_timeout(5.0)
+                    self._gather()
+                    net.compute_gradients_and_update(self.xb, self.yb, None, ll=comm)
+                    torch.cuda.synchronize(dev)
+                    if comm.error() != 0:
+                        res.update(ok=False, why="peer timeout in the fused exchange self-test")
+                    elif not torch.equal(net.store.grad.cpu(), ref):
+                        bad = int((net.store.grad.cpu() != ref).sum())
+                        res.update(ok=False, why=f"fused exchange self-test: {bad} gradient elements differ from "
+                                                 f"the rank-order sum")
+                except Exception as e:  # noqa: BLE001
+                    res.update(ok=False, why=f"fused exchange self-test raised {e!r:.200}")
+                # replicas must agree bit for bit (every rank enters both reductions, failed or not)
                 w = net.store.master
                 lo, hi = w.clone(), w.clone()
                 if gloo:
                     lo, hi = lo.cpu(), hi.cpu()
                 dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
                 dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
-                if not torch.equal(lo, hi):
+                if res["ok"] and not torch.equal(lo, hi):
                     res.update(ok=False, why="fused exchange self-test: replicas differ after the update")
-        except Exception as e:  # noqa: BLE001 (any failure -> the unfused path)
-            res.update(ok=False, why=f"fused exchange self-test raised {e!r:.200}")
+            elif res["ok"]:
+                res.update(ok=False, why="a peer's fused exchange self-test failed (local gradient)")
         finally:
             try:
                 comm.set_timeout(30.0)
@@ -323,8 +336,6 @@ class DataParallelTrainer:
             if cursor is not None:
                 self._index_stream[1].copy_(cursor)
             self.run_stats.copy_(rs0)
-        from .p2p import _agree
-
         ok = _agree(res["ok"], self.group, dev)
         if res["ok"] and not ok:
             res.update(ok=False, why="a peer's fused exchange self-test failed")

@@ -416,3 +416,72 @@ def test_resnet_weight_gradient_overlap_matches_in_order(monkeypatch):
         torch.cuda.synchronize()
         grads.append(net.store.grad.clone())
     assert torch.equal(grads[0], grads[1])
+
+
+def _resnet_pair(monkeypatch, B, seed=7):
+    """Two ResNet-18s with identical weights: BatchNorm statistics accumulated by the producing kernels'
+    epilogues (csrc/bn_acc.h, the default) and by the standalone statistics passes (bn_acc=0)."""
+    nets = {}
+    for acc in ("1", "0"):
+        monkeypatch.setenv("DISTRIFLOW_DIAG", f"bn_acc={acc}")
+        nets[acc] = build_model("resnet18_cifar", device="cuda", seed=seed)
+    monkeypatch.delenv("DISTRIFLOW_DIAG")
+    nets["0"].store.set_flat(nets["1"].store.master)
+    return nets["1"], nets["0"]
+
+
+@pytest.mark.parametrize("B", [32, 256])
+def test_bn_acc_matches_statistics_passes(monkeypatch, B):
+    """BatchNorm statistics from the producers' epilogue sums (no bn_stats launch)
+    give the same gradients, batch statistics and running statistics as the statistics passes, over two
+    consecutive steps (the accumulators are cleared by their consumers in between), at the benchmarked
+    batch too."""
+    from distriflow_amd.models.layers import BatchNorm
+
+    a, b = _resnet_pair(monkeypatch, B)
+    torch.manual_seed(4)
+    for step in range(2):
+        x = torch.rand((B, 32, 32, 3), device="cuda").to(torch.bfloat16)
+        y = torch.randint(0, 10, (B,), dtype=torch.int32, device="cuda")
+        sa = a.compute_gradients(x, y).clone()
+        sb = b.compute_gradients(x, y).clone()
+        torch.cuda.synchronize()
+        bns_a = [l for l in a._all_leaf_layers() if isinstance(l, BatchNorm)]
+        bns_b = [l for l in b._all_leaf_layers() if isinstance(l, BatchNorm)]
+        assert all(l.acc_on for l in bns_a) and not any(l.acc_on for l in bns_b)
+        for la, lb in zip(bns_a, bns_b):
+            torch.testing.assert_close(la.mean, lb.mean, rtol=1e-4, atol=1e-5)
+            torch.testing.assert_close(la.invstd, lb.invstd, rtol=1e-3, atol=1e-4)
+            torch.testing.assert_close(la.run_var, lb.run_var, rtol=1e-4, atol=1e-5)
+        assert abs(float(sa[0]) - float(sb[0])) <= 1e-3 * abs(float(sb[0])) + 1e-3
+        ga, gb = a.store.grad.double(), b.store.grad.double()
+        rel = float((ga - gb).norm() / gb.norm())
+        cos = float((ga @ gb) / (ga.norm() * gb.norm()))
+        print(f"B={B} step {step}: grad rel L2 {rel:.2e}, cosine {cos:.8f}")
+        assert cos > 0.9999 and rel < 1e-2, (rel, cos)
+        # the SGD step, so that step 2 starts from new weights on both
+        for n in (a, b):
+            n.store.set_hyper(0.05)
+            n.store.sgd_step()
+
+
+def test_bn_acc_training_step_has_no_statistics_launch(monkeypatch):
+    """The accumulated path issues no standalone statistics pass: every BatchNorm of a training step
+    consumes producer sums (flags set by the producers, consumed by apply / dx)."""
+    from distriflow_amd.models.layers import BatchNorm
+
+    net = build_model("resnet18_cifar", device="cuda", seed=2)
+    calls = []
+    orig = BatchNorm.stats
+    monkeypatch.setattr(BatchNorm, "stats", lambda self, x: (calls.append(self.name), orig(self, x))[1])
+    orig_bwd = __import__("distriflow_amd.ops", fromlist=["bn_bwd"]).bn_bwd
+    import distriflow_amd.ops as ops
+
+    monkeypatch.setattr(ops, "bn_bwd", lambda *a, **k: (calls.append("bn_bwd"), orig_bwd(*a, **k))[1])
+    x = torch.rand((32, 32, 32, 3), device="cuda").to(torch.bfloat16)
+    y = torch.randint(0, 10, (32,), dtype=torch.int32, device="cuda")
+    for _ in range(2):
+        st = net.compute_gradients(x, y)
+    torch.cuda.synchronize()
+    assert torch.isfinite(st).all()
+    assert calls == [], calls

@@ -111,3 +111,25 @@ def test_unsupported_graphs_still_raise():
     two_out["config"]["output_layers"].append(["b", 0, 0])
     with pytest.raises(NotImplementedError):
         layers_from_keras(two_out)
+
+
+@pytest.mark.parametrize("axis,ok", [(-1, True), (1, True), (3, False), (0, False)])
+def test_concatenate_axis_resolved_against_input_rank(axis, ok):
+    """ADVICE r4: Keras counts the batch axis, so on rank-2 (Dense / Flatten) inputs the last axis is 1;
+    axis 3 there is not an axis of the inputs and must be refused, not silently accepted."""
+    topo = _functional([
+        ("Flatten", "f", {}, ["inp"]),
+        ("Dense", "a", {"units": 4, "activation": "relu"}, ["f"]),
+        ("Dense", "b", {"units": 3, "activation": "relu"}, ["f"]),
+        ("Concatenate", "cat", {"axis": axis}, ["a", "b"]),
+        ("Dense", "d", {"units": 5, "activation": "softmax"}, ["cat"]),
+    ], (4, 4, 1), "d")
+    if not ok:
+        with pytest.raises(NotImplementedError):
+            layers, shape = layers_from_keras(topo)
+            Net(layers, shape, device="cpu", seed=1)
+        return
+    layers, shape = layers_from_keras(topo)
+    net = Net(layers, shape, device="cpu", seed=1)
+    st = net.compute_gradients(torch.rand(2, 4, 4, 1), torch.tensor([0, 3], dtype=torch.int32))
+    assert torch.isfinite(st).all()
