@@ -1813,6 +1813,9 @@ class PSComm {
     for (auto& p : shard_) p = nullptr;
   }
   ~PSComm() {
+    for (int k = 0; k < world_; ++k)
+      if (fed_slot_[k] && k != rank_) (void)hipIpcCloseMemHandle(fed_slot_[k]);
+    if (fed_own_) (void)hipFree(fed_own_);
     if (shared_ && rank_ != server_) (void)hipIpcCloseMemHandle(shared_);
     if (shared_ && rank_ == server_) (void)hipFree(shared_);
     for (int k = 0; k < world_; ++k)
@@ -1942,6 +1945,89 @@ class PSComm {
   torch::Tensor stats_tensor() const {
     return torch::from_blob(local_ + 64, {8}, torch::TensorOptions().dtype(torch::kLong).device(torch::kCUDA, dev_));
   }
+  // ---- device FedSGD count barrier (csrc/fedsgd_ps.hip) on the same shards: K gradient slots per shard
+  // (every rank; call fed_init on every rank, exchange the handles, then fed_open)
+  py::bytes fed_init(int64_t K) {
+    TORCH_CHECK(K >= 1 && K <= dfa::kFedMaxK, "fedsgd: K must be 1..", dfa::kFedMaxK);
+    TORCH_CHECK(fed_own_ == nullptr, "fedsgd: already initialised");
+    fed_K_ = (int)K;
+    fed_own_ = (float*)alloc_uncached((size_t)K * ((size_t)1 << shift_) * 4, "fedsgd slots");
+    for (auto& p : fed_slot_) p = nullptr;
+    check_hip(hipMemset(local_ + 2560, 0, 1536), "fedsgd local");
+    check_hip(hipDeviceSynchronize(), "fedsgd init sync");
+    return export_handle(fed_own_);
+  }
+  void fed_open(std::vector<std::string> handles) {
+    TORCH_CHECK(fed_own_ != nullptr && (int)handles.size() == world_, "fedsgd: fed_init first, one handle per rank");
+    for (int k = 0; k < world_; ++k) fed_slot_[k] = k == rank_ ? fed_own_ : (float*)open_handle(handles[k]);
+  }
+  dfa::FedArgs fed_args() const {
+    TORCH_CHECK(fed_own_ != nullptr && fed_slot_[rank_] != nullptr, "fedsgd: fed_open first");
+    dfa::FedArgs a{};
+    a.seq = reinterpret_cast<unsigned*>(shared_ + 80);
+    a.tick = reinterpret_cast<unsigned long long*>(shared_ + 88);
+    a.land = reinterpret_cast<unsigned long long*>(shared_ + 96);
+    for (int k = 0; k < world_; ++k) a.shard[k] = shard_[k], a.slot[k] = fed_slot_[k];
+    a.shard_shift = shift_;
+    a.nshards = world_;
+    a.K = fed_K_;
+    a.n = n_;
+    a.scratch = reinterpret_cast<unsigned*>(local_ + 2560);
+    a.stats = reinterpret_cast<unsigned long long*>(local_ + 3584);
+    a.audit = fed_audit_;
+    a.audit_cap = fed_audit_cap_;
+    a.lr_dev = lr_dev_;
+    a.timeout_ticks = timeout_ticks_;
+    a.herr = reinterpret_cast<unsigned*>(herr_.device());
+    return a;
+  }
+  void fed_pull(torch::Tensor w) {
+    need(w, at::kFloat, "fedsgd local master");
+    TORCH_CHECK(w.numel() == n_ && w.get_device() == dev_, "fedsgd: local master mismatch");
+    dfa::FedArgs a = fed_args();
+    a.w = w.data_ptr<float>();
+    check_hip(dfa::fed_pull(a, cur_stream()), "fed_pull");
+  }
+  void fed_upload(torch::Tensor g) {
+    need(g, at::kFloat, "fedsgd grad");
+    TORCH_CHECK(g.numel() == n_ && g.get_device() == dev_, "fedsgd: gradient mismatch");
+    dfa::FedArgs a = fed_args();
+    a.g = g.data_ptr<float>();
+    check_hip(dfa::fed_upload(a, cur_stream()), "fed_upload");
+  }
+  void fed_apply(double lr) {
+    dfa::FedArgs a = fed_args();
+    a.lr = (float)lr;
+    check_hip(dfa::fed_apply(a, cur_stream()), "fed_apply");
+  }
+  void set_fed_audit(torch::Tensor rows) {
+    if (!rows.defined() || rows.numel() == 0) {
+      fed_audit_ = nullptr, fed_audit_cap_ = 0, fed_audit_keep_ = torch::Tensor();
+      return;
+    }
+    need(rows, at::kInt, "fedsgd audit");
+    TORCH_CHECK(rows.dim() == 2 && rows.size(1) == 3 && rows.get_device() == dev_, "fedsgd: audit rows [n][3] int32");
+    fed_audit_ = reinterpret_cast<unsigned*>(rows.data_ptr<int>());
+    fed_audit_cap_ = rows.size(0);
+    fed_audit_keep_ = rows;
+  }
+  // [admitted, stale, full, failed, versions applied by this rank, error bits, version seqlock word]
+  std::vector<int64_t> fed_stats() const {
+    unsigned long long h[8] = {0};
+    check_hip(hipMemcpy(h, local_ + 3584, 64, hipMemcpyDeviceToHost), "fedsgd stats");
+    unsigned seq = 0;
+    check_hip(hipMemcpy(&seq, shared_ + 80, 4, hipMemcpyDeviceToHost), "fedsgd seq");
+    return {(int64_t)h[0], (int64_t)h[1], (int64_t)h[2], (int64_t)h[3], (int64_t)h[4], (int64_t)h[7], (int64_t)seq};
+  }
+  // device view of [admitted, stale, full, failed, applied-by-me, -, -, err] (trainer callbacks)
+  torch::Tensor fed_stats_tensor() const {
+    return torch::from_blob(local_ + 3584, {8}, torch::TensorOptions().dtype(torch::kLong).device(torch::kCUDA, dev_));
+  }
+  // device view of the version seqlock word (int32; version = word / 2)
+  torch::Tensor fed_seq_tensor() const {
+    return torch::from_blob(shared_ + 80, {1}, torch::TensorOptions().dtype(torch::kInt).device(torch::kCUDA, dev_));
+  }
+
   // launch arguments of the fused LeNet-5 reduce in parameter-server mode (lenet_train_py)
   dfa::PSArgs lenet_args(const torch::Tensor& perm, const torch::Tensor& idx, double lr, int64_t max_stale) const {
     dfa::PSArgs a = args();
@@ -2050,6 +2136,12 @@ class PSComm {
   unsigned* audit_ = nullptr;
   int64_t audit_cap_ = 0;
   torch::Tensor audit_keep_;
+  int fed_K_ = 0;
+  float* fed_own_ = nullptr;
+  float* fed_slot_[dfa::kP2PMaxRanks] = {};
+  unsigned* fed_audit_ = nullptr;
+  int64_t fed_audit_cap_ = 0;
+  torch::Tensor fed_audit_keep_;
 };
 
 static dfa::PSArgs ps_lenet_args(const PSComm& c, const torch::Tensor& perm, const torch::Tensor& idx, double lr,
@@ -2287,6 +2379,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("done_epochs", &PSComm::done_epochs)
       .def("copy_master", &PSComm::copy_master)
       .def("stats_tensor", &PSComm::stats_tensor)
-      .def("set_audit", &PSComm::set_audit, py::arg("rows"));
+      .def("set_audit", &PSComm::set_audit, py::arg("rows"))
+      .def("fed_init", &PSComm::fed_init, py::arg("K"))
+      .def("fed_open", &PSComm::fed_open, py::arg("handles"))
+      .def("fed_pull", &PSComm::fed_pull)
+      .def("fed_upload", &PSComm::fed_upload)
+      .def("fed_apply", &PSComm::fed_apply, py::arg("lr"))
+      .def("set_fed_audit", &PSComm::set_fed_audit, py::arg("rows"))
+      .def("fed_stats", &PSComm::fed_stats)
+      .def("fed_stats_tensor", &PSComm::fed_stats_tensor)
+      .def("fed_seq_tensor", &PSComm::fed_seq_tensor);
   dfa::register_runtime(m);
 }

@@ -39,38 +39,42 @@ __device__ __forceinline__ BnAccChan bacc_chan(const BnAcc& e, int col) {
     c.is[r] = c.is2[r] = 1.f;
   }
   if (e.mode == 1) {
+    const float* m2 = e.acc2 ? e.mean2 : e.mean;
+    const float* i2 = e.acc2 ? e.invstd2 : e.invstd;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       c.mu[r] = e.mean[col + r];
       c.is[r] = e.invstd[col + r];
-      if (e.acc2) {
-        c.mu2[r] = e.mean2[col + r];
-        c.is2[r] = e.invstd2[col + r];
-      }
+      c.mu2[r] = m2[col + r];
+      c.is2[r] = i2[col + r];
     }
   }
   return c;
 }
 
-// v: the 4 values as STORED (bf16-rounded, masked) at element offset o of [M][ldc] (o % 4 == 0)
+// v: the 4 values as STORED (bf16-rounded, masked) at element offset o of [M][ldc] (o % 4 == 0).  The sums
+// are updated unconditionally (only the factor depends on the mode): a mode-dependent update made hipcc keep
+// the accumulators in scratch with a dynamic index.
 __device__ __forceinline__ void bacc_add4(BnAccLane& l, const BnAcc& e, const BnAccChan& c, long long o,
                                           const float (&v)[4]) {
-  if (e.mode == 0) {
+  float f[4], f2[4];
+  if (e.mode == 1) {  // Q: g * xhat (of the first / the second BatchNorm's input)
+    const bacc_bf16x4 xv = *reinterpret_cast<const bacc_bf16x4*>(e.x + o);
+    const bacc_bf16x4 xv2 = *reinterpret_cast<const bacc_bf16x4*>((e.acc2 ? e.x2 : e.x) + o);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      l.s[r] += v[r];
-      l.q[r] += v[r] * v[r];
+      f[r] = ((float)xv[r] - c.mu[r]) * c.is[r];
+      f2[r] = ((float)xv2[r] - c.mu2[r]) * c.is2[r];
     }
-    return;
+  } else {  // Q: y * y
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f[r] = f2[r] = v[r];
   }
-  const bacc_bf16x4 xv = *reinterpret_cast<const bacc_bf16x4*>(e.x + o);
-  bacc_bf16x4 xv2;
-  if (e.acc2) xv2 = *reinterpret_cast<const bacc_bf16x4*>(e.x2 + o);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     l.s[r] += v[r];
-    l.q[r] += v[r] * (((float)xv[r] - c.mu[r]) * c.is[r]);
-    if (e.acc2) l.q2[r] += v[r] * (((float)xv2[r] - c.mu2[r]) * c.is2[r]);
+    l.q[r] += v[r] * f[r];
+    l.q2[r] += v[r] * f2[r];
   }
 }
 
@@ -84,11 +88,12 @@ __device__ __forceinline__ float bacc_x16(float v) {
   return v;
 }
 __device__ __forceinline__ void bacc_reduce16(BnAccLane& l, bool two) {
+  (void)two;  // (Q2 reduced unconditionally: see bacc_add4)
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     l.s[r] = bacc_x16(l.s[r]);
     l.q[r] = bacc_x16(l.q[r]);
-    if (two) l.q2[r] = bacc_x16(l.q2[r]);
+    l.q2[r] = bacc_x16(l.q2[r]);
   }
 }
 

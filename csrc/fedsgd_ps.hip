@@ -1,0 +1,303 @@
+// Device FedSGD with a count barrier of K < W: the reference FederatedServer on the device parameter
+// server's memory (BASELINE.json configs[1] FedSGD semantics).
+//
+// Reference (/root/reference/src/server/federated_server.ts:71-117): an upload is accepted only when its
+// gradient was computed on the CURRENT model version and no update is in progress; after
+// minUpdatesPerVersion (K) accepted uploads the server averages them, applies w -= lr * mean, bumps the
+// version and broadcasts it.  Late uploads of an old version are dropped, so the barrier counts updates,
+// not workers: a slow or lost worker never blocks a version.
+//
+// MI355X design: no server process.  The fp32 master is sharded over the ranks' HBM (PSComm, the async
+// engine's shards); the version is a seqlock word in the control buffer (even 2v: version v stable, odd:
+// being applied).  Per step a rank
+//   fed_pull    copies the master with the seqlock (a copy that saw the word change is retried) and records
+//               the even word it copied under (every workgroup; a step whose workgroups saw different
+//               versions is dropped at upload);
+//   (the model's forward / backward on its own microbatch)
+//   fed_upload  takes a ticket for that version: one CAS on a (version << 32 | count) word -- stale
+//               version, update in progress or count >= K: dropped; else slot t = the count.  The admitted
+//               gradient is stored into slot t (sharded like the master, plain stores) and, once every
+//               element has landed, counted on a second (version | count) word; the K-th lander is this
+//               version's applier;
+//   fed_apply   (a no-op unless this rank is the applier) marks the version odd, adds -lr * mean of the K
+//               slots (fixed slot order: every element gets the same arithmetic whoever applies) into the
+//               master shards and publishes version v + 1 (even).
+// Every wait is bounded by a wall-clock timeout that sets a sticky error bit instead of spinning forever.
+#include "common.h"
+#include "kernels.h"
+#include "ps_device.h"
+
+namespace dfa {
+namespace {
+
+constexpr int kFedBlock = 256;
+constexpr unsigned kFedAdmit = 1, kFedStale = 2, kFedFull = 3, kFedFailed = 4;
+// local scratch words (FedArgs::scratch): decision word (epoch << 3 | code), the admitted slot, launch epoch,
+// arrivals of the upload / apply launches, the applier flag (version seqlock word + 1, 0 = not the applier),
+// and per pull workgroup the seqlock word it copied under
+constexpr int kFedDecision = 0, kFedSlot = 1, kFedEpoch = 2, kFedUpDone = 3, kFedApDone = 4, kFedApplier = 5,
+              kFedPulled = 64;
+
+__device__ __forceinline__ unsigned fed_ld(const unsigned* p) {
+  return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ float* fed_elem(float* const* tab, int shift, long long i, long long slot_off) {
+  return tab[i >> shift] + slot_off + (i & ((1LL << shift) - 1));
+}
+
+__device__ __forceinline__ void fed_stage(const FedArgs& a, float** master, float** slots) {
+  if (threadIdx.x < kP2PMaxRanks) {
+    float *m = nullptr, *s = nullptr;
+#pragma unroll
+    for (int k = 0; k < kP2PMaxRanks; ++k)
+      if ((int)threadIdx.x == k) m = a.shard[k], s = a.slot[k];
+    master[threadIdx.x] = m;
+    slots[threadIdx.x] = s;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void fed_fail(const FedArgs& a, unsigned bit) {
+  atomicOr(a.stats + 7, (unsigned long long)bit);
+  if (a.herr) __hip_atomic_store(a.herr, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// the slice of workgroup b of G: 4-aligned, never crossing a shard (shards are multiples of 64 elements)
+__device__ __forceinline__ void fed_slice(const FedArgs& a, int b, int G, long long& lo, long long& hi) {
+  const long long per = ((a.n + 4LL * G - 1) / (4LL * G)) * 4;
+  lo = b * per;
+  hi = lo + per < a.n ? lo + per : a.n;
+}
+
+__global__ __launch_bounds__(kFedBlock) void fed_pull_kernel(FedArgs a) {
+  __shared__ float* master[kP2PMaxRanks];
+  __shared__ float* slots[kP2PMaxRanks];
+  __shared__ unsigned s_seq;
+  __shared__ int s_ok;
+  fed_stage(a, master, slots);
+  long long lo, hi;
+  fed_slice(a, blockIdx.x, gridDim.x, lo, hi);
+  const unsigned long long t0 = wall_clock64();
+  for (int attempt = 0;; ++attempt) {
+    if (threadIdx.x == 0) {
+      unsigned s = fed_ld(a.seq);
+      while (s & 1u) {  // a version is being applied: wait for it
+        if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) break;
+        __builtin_amdgcn_s_sleep(2);
+        s = fed_ld(a.seq);
+      }
+      s_seq = s;
+    }
+    __syncthreads();
+    const unsigned s0 = s_seq;
+    for (long long i = lo + 4LL * threadIdx.x; i < hi; i += 4LL * kFedBlock) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(fed_elem(master, a.shard_shift, i, 0));
+      *reinterpret_cast<f32x4*>(a.w + i) = v;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the copy's loads returned before the re-check
+    __syncthreads();
+    if (threadIdx.x == 0) s_ok = fed_ld(a.seq) == s0 && !(s0 & 1u);
+    __syncthreads();
+    if (s_ok) break;
+    if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) {
+      if (threadIdx.x == 0) {
+        fed_fail(a, 1u);
+        s_seq = 1u;  // odd: the upload drops this step
+      }
+      __syncthreads();
+      break;
+    }
+  }
+  if (threadIdx.x == 0) a.scratch[kFedPulled + blockIdx.x] = s_seq;
+}
+
+// admission (one thread): the ticket of version word s (even) on the (version << 32 | count) word
+__device__ inline unsigned fed_admit(const FedArgs& a, int pull_blocks, unsigned* slot_out, unsigned* vp_out) {
+  const unsigned vp = a.scratch[kFedPulled];
+  *vp_out = vp;
+  bool torn = (vp & 1u) != 0;
+  for (int b = 1; b < pull_blocks; ++b) torn |= a.scratch[kFedPulled + b] != vp;
+  if (torn || fed_ld(a.seq) != vp) return kFedStale;
+  unsigned long long w = __hip_atomic_load(a.tick, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned long long t0 = wall_clock64();
+  for (;;) {
+    const unsigned tag = (unsigned)(w >> 32), cnt = (unsigned)w;
+    unsigned long long nw;
+    unsigned t;
+    if (tag == vp) {
+      if (cnt >= (unsigned)a.K) return kFedFull;
+      t = cnt;
+      nw = w + 1ull;
+    } else if ((int)(tag - vp) < 0) {  // the first upload of version vp
+      t = 0;
+      nw = ((unsigned long long)vp << 32) | 1ull;
+    } else {
+      return kFedStale;  // the word already names a newer version
+    }
+    if (__hip_atomic_compare_exchange_strong(a.tick, &w, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM)) {
+      // (the version cannot close before this ticket lands: closing takes K landed tickets < K, and this
+      // is one of them -- so an admitted gradient must always land, or the version never closes)
+      *slot_out = t;
+      return kFedAdmit;
+    }
+    if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) return kFedFailed;
+  }
+}
+
+__global__ __launch_bounds__(kFedBlock) void fed_upload_kernel(FedArgs a, int pull_blocks) {
+  __shared__ float* master[kP2PMaxRanks];
+  __shared__ float* slots[kP2PMaxRanks];
+  __shared__ unsigned s_dec, s_slot, s_vp;
+  fed_stage(a, master, slots);
+  const int G = gridDim.x;
+  if (threadIdx.x == 0) {
+    const unsigned ep = __hip_atomic_load(a.scratch + kFedEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    if (blockIdx.x == 0) {
+      unsigned slot = 0, vp = 0;
+      const unsigned dec = fed_admit(a, pull_blocks, &slot, &vp);
+      const unsigned long long k = a.stats[0] + a.stats[1] + a.stats[2] + a.stats[3];
+      a.stats[dec == kFedAdmit ? 0 : dec == kFedStale ? 1 : dec == kFedFull ? 2 : 3] += 1;
+      if (dec == kFedFailed) fed_fail(a, 2u);
+      if (a.audit && k < (unsigned long long)a.audit_cap) {
+        a.audit[3 * k] = vp;
+        a.audit[3 * k + 1] = dec;
+        a.audit[3 * k + 2] = dec == kFedAdmit ? slot : 0xffffffffu;
+      }
+      a.scratch[kFedSlot] = slot;
+      a.scratch[kFedApplier] = 0;
+      __hip_atomic_store(a.scratch + kFedDecision, ((ep & 0x1fffffffu) << 3) | dec, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      s_dec = dec, s_slot = slot, s_vp = vp;
+    } else {
+      const unsigned long long t0 = wall_clock64();
+      unsigned d = 0;
+      for (;;) {
+        d = __hip_atomic_load(a.scratch + kFedDecision, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if ((d >> 3) == (ep & 0x1fffffffu)) break;
+        if (wall_clock64() - t0 > 2ull * (unsigned long long)a.timeout_ticks) {
+          fed_fail(a, 4u);
+          d = kFedFailed;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s_dec = d & 7u;
+      s_slot = a.scratch[kFedSlot];
+      s_vp = a.scratch[kFedPulled];
+    }
+  }
+  __syncthreads();
+  if (s_dec == kFedAdmit) {  // this workgroup's slice of the gradient into slot t
+    long long lo, hi;
+    fed_slice(a, blockIdx.x, G, lo, hi);
+    const long long soff = (long long)s_slot << a.shard_shift;
+    for (long long i = lo + 4LL * threadIdx.x; i < hi; i += 4LL * kFedBlock)
+      *reinterpret_cast<f32x4*>(fed_elem(slots, a.shard_shift, i, soff)) = *reinterpret_cast<const f32x4*>(a.g + i);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's slot stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(a.scratch + kFedUpDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (unsigned)G - 1) {  // the last workgroup: the whole gradient has landed
+      a.scratch[kFedUpDone] = 0;
+      a.scratch[kFedEpoch] += 1u;
+      if (s_dec == kFedAdmit) {
+        const unsigned vp = s_vp;
+        unsigned long long w = __hip_atomic_load(a.land, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        unsigned long long nw = 0;
+        for (;;) {
+          nw = ((unsigned)(w >> 32) == vp) ? w + 1ull : (((unsigned long long)vp << 32) | 1ull);
+          if (__hip_atomic_compare_exchange_strong(a.land, &w, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_SYSTEM))
+            break;
+        }
+        if ((unsigned)nw == (unsigned)a.K) a.scratch[kFedApplier] = vp + 1u;  // the K-th lander applies
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kFedBlock) void fed_apply_kernel(FedArgs a) {
+  __shared__ float* master[kP2PMaxRanks];
+  __shared__ float* slots[kP2PMaxRanks];
+  __shared__ unsigned s_app;
+  fed_stage(a, master, slots);
+  if (threadIdx.x == 0) s_app = a.scratch[kFedApplier];
+  __syncthreads();
+  if (s_app == 0) return;  // not this rank's version to apply (every workgroup returns)
+  const unsigned vp = s_app - 1u;
+  if (threadIdx.x == 0) {
+    // the version is being applied: odd (first workgroup to get here); pullers retry, uploads drop
+    unsigned e = vp;
+    __hip_atomic_compare_exchange_strong(a.seq, &e, vp + 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  long long lo, hi;
+  fed_slice(a, blockIdx.x, gridDim.x, lo, hi);
+  const float lr = a.lr_dev ? *a.lr_dev : a.lr;
+  const float invk = 1.f / (float)a.K;
+  for (long long i = lo + 4LL * threadIdx.x; i < hi; i += 4LL * kFedBlock) {
+    f32x4 s = *reinterpret_cast<const f32x4*>(fed_elem(slots, a.shard_shift, i, 0));
+    for (int t = 1; t < a.K; ++t)
+      s += *reinterpret_cast<const f32x4*>(fed_elem(slots, a.shard_shift, i, (long long)t << a.shard_shift));
+    float* m = fed_elem(master, a.shard_shift, i, 0);
+    f32x4 w = *reinterpret_cast<const f32x4*>(m);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma clang fp contract(off)
+      w[j] = w[j] - lr * (s[j] * invk);
+    }
+    *reinterpret_cast<f32x4*>(m) = w;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's master stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(a.scratch + kFedApDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {  // every element applied: publish version v + 1
+      a.scratch[kFedApDone] = 0;
+      a.scratch[kFedApplier] = 0;
+      __hip_atomic_store(a.seq, vp + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      a.stats[4] += 1;
+    }
+  }
+}
+
+int fed_grid(long long n) {
+  long long g = (n + 4095) / 4096;
+  return (int)(g < 1 ? 1 : (g > kPSMaxGrid ? kPSMaxGrid : g));
+}
+
+bool fed_ok(const FedArgs& a) {
+  if (a.nshards < 1 || a.nshards > kP2PMaxRanks || a.shard_shift < 6 || a.shard_shift > 30 || !a.seq || !a.tick ||
+      !a.land || a.K < 1 || a.K > kFedMaxK || a.n <= 0 || (a.n & 3) || ((a.n - 1) >> a.shard_shift) >= a.nshards)
+    return false;
+  for (int k = 0; k < a.nshards; ++k)
+    if (!a.shard[k] || !a.slot[k]) return false;
+  return true;
+}
+
+}  // namespace
+
+hipError_t fed_pull(const FedArgs& a, hipStream_t st) {
+  if (!fed_ok(a) || !a.w) return hipErrorInvalidValue;
+  fed_pull_kernel<<<fed_grid(a.n), kFedBlock, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t fed_upload(const FedArgs& a, hipStream_t st) {
+  if (!fed_ok(a) || !a.g) return hipErrorInvalidValue;
+  fed_upload_kernel<<<fed_grid(a.n), kFedBlock, 0, st>>>(a, fed_grid(a.n));
+  return hipGetLastError();
+}
+
+hipError_t fed_apply(const FedArgs& a, hipStream_t st) {
+  if (!fed_ok(a)) return hipErrorInvalidValue;
+  fed_apply_kernel<<<fed_grid(a.n), kFedBlock, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace dfa

@@ -413,6 +413,32 @@ struct PSArgs {
   float lr;
 };
 constexpr int kPSMaxGrid = 64;
+
+// Device FedSGD count barrier on the parameter server's shards (csrc/fedsgd_ps.hip): the reference
+// FederatedServer's version gate and K-upload barrier, K < W allowed (late uploads are dropped).
+constexpr int kFedMaxK = 64;
+struct FedArgs {
+  unsigned* seq;                 // control: version seqlock (2v: version v stable; odd: being applied)
+  unsigned long long* tick;      // control: (seq << 32) | tickets taken for that version
+  unsigned long long* land;      // control: (seq << 32) | admitted gradients landed in their slots
+  float* shard[kP2PMaxRanks];    // master shards (element i: shard[i >> shift][i & mask])
+  float* slot[kP2PMaxRanks];     // per rank: K slot shards (slot t of element i: slot[i >> shift][t << shift | i & mask])
+  int shard_shift, nshards, K;
+  long long n;
+  float* w;                      // local master (pull destination)
+  const float* g;                // local gradient (upload)
+  unsigned* scratch;             // local protocol words (fedsgd_ps.hip)
+  unsigned long long* stats;     // local [8]: admitted, stale, full, failed, versions applied, -, -, error bits
+  unsigned* audit;               // optional local rows [audit_cap][3]: (seqlock word pulled, decision, slot)
+  long long audit_cap;
+  const float* lr_dev;           // device learning rate (null: lr)
+  float lr;
+  long long timeout_ticks;
+  unsigned* herr;
+};
+hipError_t fed_pull(const FedArgs& a, hipStream_t st);
+hipError_t fed_upload(const FedArgs& a, hipStream_t st);
+hipError_t fed_apply(const FedArgs& a, hipStream_t st);
 constexpr int kPSVMinWord = 4;  // scratch word of the refresh minimum (ps_device.h kPSVMin)
 constexpr long long kPSMaxBatches = 1 << 20;  // capacity of the shared completion arrays
 hipError_t ps_fetch_pull(const PSArgs& a, hipStream_t st);

@@ -190,14 +190,14 @@ class AsyncPSTrainer(DataParallelTrainer):
         super().prepare_run(n)
 
     def _capture(self):
-        if not self.fused_ps:
-            # compute-only warm-up (allocator, code objects) with no claim and no apply; its effect on the
-            # local engine state is undone
-            snap = self.net.snapshot_state()
-            DataParallelTrainer._gather(self)
-            self.net.compute_gradients(self.xb, self.yb)
-            torch.cuda.synchronize(self.net.device)
-            self.net.restore_state(snap)
+        # compute-only warm-up (allocator, code objects, the fused kernels' host-built tables for this batch
+        # size -- built with a synchronous copy, which a capture refuses) with no claim and no apply; its
+        # effect on the local engine state is undone
+        snap = self.net.snapshot_state()
+        DataParallelTrainer._gather(self)
+        self.net.compute_gradients(self.xb, self.yb)
+        torch.cuda.synchronize(self.net.device)
+        self.net.restore_state(snap)
         super()._capture()
 
     def _capture_with_fallback(self):

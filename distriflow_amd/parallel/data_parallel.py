@@ -684,11 +684,18 @@ class DataParallelTrainer:
             last = self._cb_last or [[0] * len(c) for c in cur]
             self._cb_last = cur
             st = self._cb_stats(cur, last, v0, v1, n)
-            for cb in self._version_cbs:
-                cb(v0, v1)
+            change = self._version_change(cur, last, v0, v1)
+            if change is not None:
+                for cb in self._version_cbs:
+                    cb(*change)
             for cb in self._upload_cbs:
                 cb(st)
             block_one = False
+
+    def _version_change(self, cur: list, last: list, v0: int, v1: int):
+        """(old, new) version of one replay for on_new_version, or None when the replay published none (a
+        synchronous step always publishes one: the versions are the step counts)."""
+        return v0, v1
 
     def flush_callbacks(self):
         """Fire the callbacks of every replay issued so far (waits for their read-backs)."""

@@ -148,6 +148,7 @@ def test_launcher_async_device_engine():
     out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert out["engine"] == "device" and out["error"] == 0, out
     print("launcher async:", {k: out.get(k) for k in ("graph", "capture_error", "steps_per_rank", "accepted")})
+    assert out["graph"] == "full", out.get("capture_error")  # the launcher replays captured steps
     # + graph warm-up steps; steps after the last epoch finished are no-ops
     assert out["accepted"] + out["rejected"] + out["noop_steps"] == out["steps_per_rank"] + out["capture_warmup"]
     assert out["finished"] and out["epoch"] == 3 and out["completed"] == 3 * (16384 // 512)

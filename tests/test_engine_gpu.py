@@ -425,6 +425,7 @@ def _resnet_pair(monkeypatch, B, seed=7):
     for acc in ("1", "0"):
         monkeypatch.setenv("DISTRIFLOW_DIAG", f"bn_acc={acc}")
         nets[acc] = build_model("resnet18_cifar", device="cuda", seed=seed)
+        nets[acc].bind(B)  # (the layers read the switch when their buffers are allocated)
     monkeypatch.delenv("DISTRIFLOW_DIAG")
     nets["0"].store.set_flat(nets["1"].store.master)
     return nets["1"], nets["0"]
