@@ -31,3 +31,23 @@ def test_inline_asm_load_kernels_do_not_spill(src, tmp_path):
     assert names and len(scratch) >= len(names)
     spilled = [n for n, s in zip(names, scratch) if s > 0]
     assert not spilled, f"kernels with scratch (spills) in {src}: {spilled}"
+
+
+# kernels carrying the BatchNorm epilogue sums (csrc/bn_acc.h) or the FedSGD protocol: a guarded
+# accumulate once kept its sums in scratch with a dynamic index (every igemm64 variant, 12 bytes)
+NO_SCRATCH_FILES = ["bn.hip", "igemm.hip", "fedsgd_ps.hip", "async_ps.hip", "lenet_fused.hip"]
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("src", NO_SCRATCH_FILES)
+def test_epilogue_sum_kernels_do_not_use_scratch(src, tmp_path):
+    out = tmp_path / "k.s"
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
+                    "-I", os.path.join(ROOT, "csrc"), os.path.join(ROOT, "csrc", src), "-o", str(out)],
+                   check=True, capture_output=True, timeout=600)
+    asm = out.read_text()
+    names = re.findall(r"^(_Z\S*kernel\S*):", asm, flags=re.M)
+    scratch = [int(x) for x in re.findall(r"; ScratchSize: (\d+)", asm)]
+    assert names and len(scratch) >= len(names)
+    spilled = [n for n, s in zip(names, scratch) if s > 0]
+    assert not spilled, f"kernels with scratch in {src}: {spilled}"
