@@ -1340,7 +1340,7 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
                     c10::optional<torch::Tensor> idx_cursor, c10::optional<torch::Tensor> idx_dst,
                     const P2PComm* ll, int64_t exch_blocks, c10::optional<torch::Tensor> run_stats,
                     const PSComm* ps, c10::optional<torch::Tensor> ps_perm, c10::optional<torch::Tensor> ps_idx,
-                    double ps_lr, int64_t ps_max_stale) {
+                    double ps_lr, int64_t ps_max_stale, bool red_succ) {
   TORCH_CHECK(conv.size() == 4 && conv_grads.size() == 4, "lenet: conv = [w1, b1, w2, b2]");
   TORCH_CHECK(dense_w.size() == 3 && dense_wt.size() == 3 && dense_b.size() == 3 && dense_gw.size() == 3 &&
                   dense_gb.size() == 3 && hT.size() == 3 && dzT.size() == 3,
@@ -1440,8 +1440,8 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
   need(dense_part, at::kFloat, "lenet dense_part");
   TORCH_CHECK(dense_part.numel() >= dfa::lenet_dense_part_floats((int)B),
               "lenet: dense_part must hold lenet_dense_part_floats(B) zero-initialised floats");
-  r.slabs = dense_part.data_ptr<float>();
-  r.tickets = reinterpret_cast<unsigned*>(dense_part.data_ptr<float>() + dfa::lenet_red_slab_floats());
+  dfa::lenet_red_bind_scratch(dense_part.data_ptr<float>(), r);
+  r.succ = red_succ ? 1 : 0;  // (the launcher falls back to tickets where successor ownership cannot run)
   r.conv_part = a.conv_part;
   r.loss_part = a.loss_part;
   r.stats = stats.data_ptr<float>();
@@ -1680,8 +1680,10 @@ class P2PComm {
     }
     local_ = (char*)p;
     check_hip(hipMemset(local_, 0, (size_t)bytes_), "p2p memset");
-    check_hip(hipMalloc((void**)&epochs_, (size_t)(max_blocks_ + ll_slots_) * 4), "p2p epochs alloc");
-    check_hip(hipMemset(epochs_, 0, (size_t)(max_blocks_ + ll_slots_) * 4), "p2p epochs memset");
+    // per-block counters, then per-slot LL counters, then per-(slot, part) LL counters
+    const size_t nep = (size_t)max_blocks_ + (size_t)ll_slots_ * (1 + dfa::kLLParts);
+    check_hip(hipMalloc((void**)&epochs_, nep * 4), "p2p epochs alloc");
+    check_hip(hipMemset(epochs_, 0, nep * 4), "p2p epochs memset");
     check_hip(hipMalloc((void**)&err_, 4), "p2p err alloc");
     check_hip(hipMemset(err_, 0, 4), "p2p err memset");
     check_hip(hipDeviceSynchronize(), "p2p init sync");
@@ -1763,6 +1765,7 @@ class P2PComm {
     for (int r = 0; r < dfa::kP2PMaxRanks; ++r)
       c.bases[r] = bases_[r] ? reinterpret_cast<unsigned long long*>(bases_[r] + ll_off_) : nullptr;
     c.epochs = epochs_ + max_blocks_;
+    c.part_epochs = epochs_ + max_blocks_ + ll_slots_;
     c.err = err_;
     c.herr = herr_.device();
     c.timeout_ticks = timeout_ticks_;
@@ -2341,7 +2344,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sgd_descs") = py::none(), py::arg("idx_stream") = py::none(), py::arg("idx_cursor") = py::none(),
         py::arg("idx_dst") = py::none(), py::arg("ll") = nullptr, py::arg("exch_blocks") = 0, py::arg("run_stats") = py::none(),
         py::arg("ps") = nullptr, py::arg("ps_perm") = py::none(), py::arg("ps_idx") = py::none(),
-        py::arg("ps_lr") = 0.0, py::arg("ps_max_stale") = -1);
+        py::arg("ps_lr") = 0.0, py::arg("ps_max_stale") = -1, py::arg("red_succ") = true);
   m.def("lenet_blocks", [](int64_t B) { return dfa::lenet_blocks((int)B); });
   m.def("lenet_frag_bytes", []() { return (int64_t)dfa::lenet_frag_bytes(); });
   m.def("lenet_dense_part_floats", [](int64_t B) { return (int64_t)dfa::lenet_dense_part_floats((int)B); });

@@ -604,19 +604,28 @@ hipError_t bn_dx(const bf16* x, const bf16* mask, const bf16* dy, bf16* dx, cons
 // replica reads are C * nrep * 16 bytes per workgroup, so the grid is capped to keep them a few MB.
 constexpr int kBnAccMaxC = 1024;
 
+// kBnVecs 8-channel vectors per thread per batch; the grid gives every thread about one batch (all of
+// its loads in flight at once), within [256, 4096] workgroups
+constexpr int kBnVecs = 4;
 static int bn_acc_grid(long long nvec, int C, int nrep) {
-  long long g = (nvec + 255) / 256;
-  const long long cap = std::max(64LL, (8LL << 20) / ((long long)C * nrep * 16));
-  if (g > cap) g = cap;
-  if (g > 4096) g = 4096;
-  return (int)std::max(1LL, g);
+  (void)C, (void)nrep;
+  long long g = (nvec + 256LL * kBnVecs - 1) / (256LL * kBnVecs);
+  return (int)std::min(4096LL, std::max(256LL, g));
 }
 
+// the nrep replicas of [S, Q] of channel c, summed in replica order (all loads issued together)
 __device__ __forceinline__ void bn_fin_sums(const BnAccFin& f, int C, int c, double& S, double& Q) {
+  double s[kBnAccMaxRep], q[kBnAccMaxRep];
+#pragma unroll
+  for (int r = 0; r < kBnAccMaxRep; ++r) {
+    s[r] = r < f.nrep ? f.acc[(long long)(2 * r) * C + c] : 0.0;
+    q[r] = r < f.nrep ? f.acc[(long long)(2 * r + 1) * C + c] : 0.0;
+  }
   S = 0.0, Q = 0.0;
-  for (int r = 0; r < f.nrep; ++r) {
-    S += f.acc[(long long)(2 * r) * C + c];
-    Q += f.acc[(long long)(2 * r + 1) * C + c];
+#pragma unroll
+  for (int r = 0; r < kBnAccMaxRep; ++r) {
+    S += s[r];
+    Q += q[r];
   }
 }
 
@@ -645,11 +654,30 @@ __device__ __forceinline__ void bn_fin_fwd(const BnAccFin& f, const float* gamma
   }
 }
 
+// The streaming part of both consumers: a thread's vectors i = i0 + k * stride in batches of kBnVecs, every
+// load of a batch issued before its stores (a load behind a store waits for that store too); the first
+// batch's loads go out BEFORE the statistics are finalised (they do not depend on them), so the prologue's
+// replica reads and the first tensor reads share one round trip.
 template <int RES>
 __global__ void __launch_bounds__(256) bn_apply_acc_kernel(BnApplyArgs a, BnAccFin f, BnAccFin fr) {
   __shared__ float co[4][kBnAccMaxC];  // sa, sb, ra, rb
   const int C = a.C;
   const long long M = a.M;
+  const long long total = M * C / 8;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long i0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const bf16x8* xs = reinterpret_cast<const bf16x8*>(a.x);
+  const bf16x8* rs = reinterpret_cast<const bf16x8*>(a.r);
+  bf16x8 xv[kBnVecs], rv[kBnVecs];
+  auto load = [&](long long base) {
+#pragma unroll
+    for (int k = 0; k < kBnVecs; ++k) {
+      const long long i = min(base + k * stride, total - 1);  // (clamped: not stored)
+      xv[k] = xs[i];
+      if (RES) rv[k] = rs[i];
+    }
+  };
+  load(i0);
   for (int c = threadIdx.x; c < C; c += 256) {
     float sa, sb, ra = 1.f, rb = 0.f;
     bn_fin_fwd(f, a.gamma, a.beta, C, M, c, sa, sb);
@@ -660,8 +688,6 @@ __global__ void __launch_bounds__(256) bn_apply_acc_kernel(BnApplyArgs a, BnAccF
     co[3][c] = rb;
   }
   __syncthreads();
-  const long long total = M * C / 8;
-  const long long stride = (long long)gridDim.x * blockDim.x;
   const int c0 = (int)(threadIdx.x % (C / 8)) * 8;  // constant: 256 and the grid stride are multiples of C/8
   float sa[8], sb[8], ra[8], rb[8];
 #pragma unroll
@@ -671,25 +697,29 @@ __global__ void __launch_bounds__(256) bn_apply_acc_kernel(BnApplyArgs a, BnAccF
     ra[j] = co[2][c0 + j];
     rb[j] = co[3][c0 + j];
   }
-#pragma unroll 2
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += stride) {
-    const bf16x8 xv = reinterpret_cast<const bf16x8*>(a.x)[i];
-    bf16x8 rv;
-    if (RES) rv = reinterpret_cast<const bf16x8*>(a.r)[i];
-    bf16x8 o;
+  bf16x8* ys = reinterpret_cast<bf16x8*>(a.y);
+  for (long long base = i0; base < total; base += kBnVecs * stride) {
+    if (base != i0) load(base);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = (float)xv[j] * sa[j] + sb[j];
-      if (RES) v += (float)rv[j] * ra[j] + rb[j];
-      if (a.relu) v = fmaxf(v, 0.f);
-      o[j] = f2bf(v);
+    for (int k = 0; k < kBnVecs; ++k) {
+      const long long i = base + k * stride;
+      if (i >= total) break;
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = (float)xv[k][j] * sa[j] + sb[j];
+        if (RES) v += (float)rv[k][j] * ra[j] + rb[j];
+        if (a.relu) v = fmaxf(v, 0.f);
+        o[j] = f2bf(v);
+      }
+      ys[i] = o;
     }
-    reinterpret_cast<bf16x8*>(a.y)[i] = o;
   }
 }
 
 hipError_t bn_apply_acc(const BnApplyArgs& a, const BnAccFin& f, const BnAccFin* fr, hipStream_t st) {
-  if (a.C % 8 || a.C > kBnAccMaxC || 256 % (a.C / 8) || a.M <= 0 || !f.acc || f.nrep < 1 || a.eval)
+  if (a.C % 8 || a.C > kBnAccMaxC || 256 % (a.C / 8) || a.M <= 0 || !f.acc || f.nrep < 1 ||
+      f.nrep > kBnAccMaxRep || (fr && (fr->nrep < 1 || fr->nrep > kBnAccMaxRep)) || a.eval)
     return hipErrorInvalidValue;
   const int res = a.r == nullptr ? 0 : (fr == nullptr ? 1 : 2);
   const int nrep = f.nrep + (fr ? fr->nrep : 0);
@@ -705,6 +735,21 @@ hipError_t bn_apply_acc(const BnApplyArgs& a, const BnAccFin& f, const BnAccFin*
 __global__ void __launch_bounds__(256) bn_dx_acc_kernel(const bf16* __restrict__ x, const bf16* __restrict__ g,
                                                         bf16* __restrict__ dx, BnAccFin f, long long M, int C) {
   __shared__ float k[3][kBnAccMaxC];
+  const long long total = M * C / 8;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long i0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const bf16x8* xs = reinterpret_cast<const bf16x8*>(x);
+  const bf16x8* gs = reinterpret_cast<const bf16x8*>(g);
+  bf16x8 xv[kBnVecs], gv[kBnVecs];
+  auto load = [&](long long base) {
+#pragma unroll
+    for (int kk = 0; kk < kBnVecs; ++kk) {
+      const long long i = min(base + kk * stride, total - 1);  // (clamped: not stored)
+      xv[kk] = xs[i];
+      gv[kk] = gs[i];
+    }
+  };
+  load(i0);
   for (int c = threadIdx.x; c < C; c += 256) {
     double S, Q;
     bn_fin_sums(f, C, c, S, Q);
@@ -727,8 +772,6 @@ __global__ void __launch_bounds__(256) bn_dx_acc_kernel(const bf16* __restrict__
     }
   }
   __syncthreads();
-  const long long total = M * C / 8;
-  const long long stride = (long long)gridDim.x * blockDim.x;
   const int c0 = (int)(threadIdx.x % (C / 8)) * 8;
   float k1[8], k2[8], k3[8];
 #pragma unroll
@@ -737,19 +780,24 @@ __global__ void __launch_bounds__(256) bn_dx_acc_kernel(const bf16* __restrict__
     k2[j] = k[1][c0 + j];
     k3[j] = k[2][c0 + j];
   }
-#pragma unroll 2
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += stride) {
-    const bf16x8 xv = reinterpret_cast<const bf16x8*>(x)[i];
-    const bf16x8 gv = reinterpret_cast<const bf16x8*>(g)[i];
-    bf16x8 o;
+  bf16x8* ds = reinterpret_cast<bf16x8*>(dx);
+  for (long long base = i0; base < total; base += kBnVecs * stride) {
+    if (base != i0) load(base);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(k1[j] * (float)gv[j] + k2[j] * (float)xv[j] + k3[j]);
-    reinterpret_cast<bf16x8*>(dx)[i] = o;
+    for (int kk = 0; kk < kBnVecs; ++kk) {
+      const long long i = base + kk * stride;
+      if (i >= total) break;
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(k1[j] * (float)gv[kk][j] + k2[j] * (float)xv[kk][j] + k3[j]);
+      ds[i] = o;
+    }
   }
 }
 
 hipError_t bn_dx_acc(const bf16* x, const bf16* g, bf16* dx, const BnAccFin& f, int M, int C, hipStream_t st) {
-  if (C % 8 || C > kBnAccMaxC || 256 % (C / 8) || M <= 0 || !f.acc || f.nrep < 1 || !f.gamma || !f.dgamma)
+  if (C % 8 || C > kBnAccMaxC || 256 % (C / 8) || M <= 0 || !f.acc || f.nrep < 1 || f.nrep > kBnAccMaxRep ||
+      !f.gamma || !f.dgamma)
     return hipErrorInvalidValue;
   const int grid = bn_acc_grid((long long)M * C / 8, C, f.nrep);
   hipLaunchKernelGGL(bn_dx_acc_kernel, dim3(grid), dim3(256), 0, st, x, g, dx, f, (long long)M, C);

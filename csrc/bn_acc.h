@@ -52,19 +52,37 @@ __device__ __forceinline__ BnAccChan bacc_chan(const BnAcc& e, int col) {
   return c;
 }
 
-// v: the 4 values as STORED (bf16-rounded, masked) at element offset o of [M][ldc] (o % 4 == 0).  The sums
-// are updated unconditionally (only the factor depends on the mode): a mode-dependent update made hipcc keep
-// the accumulators in scratch with a dynamic index.
-__device__ __forceinline__ void bacc_add4(BnAccLane& l, const BnAcc& e, const BnAccChan& c, long long o,
-                                          const float (&v)[4]) {
+// the BatchNorm inputs x (and x2) at element offset o (mode 1).  Epilogues load these for ALL their
+// elements before their first store: a load issued behind a store waits for that store too (one vmcnt
+// counter), so a load / compute / store sequence per element serialised a round trip per element (the
+// ResNet-18 data-gradient convs ran at half their speed).
+struct BnAccX {
+  bacc_bf16x4 x, x2;
+};
+__device__ __forceinline__ BnAccX bacc_loadx(const BnAcc& e, long long o) {
+  BnAccX r;
+  if (e.mode == 1) {
+    r.x = *reinterpret_cast<const bacc_bf16x4*>(e.x + o);
+    // (one BatchNorm: the second factor is the first; no second read of the same tensor)
+    r.x2 = e.acc2 ? *reinterpret_cast<const bacc_bf16x4*>(e.x2 + o) : r.x;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r.x[k] = r.x2[k] = (__bf16)0.f;
+  }
+  return r;
+}
+
+// v: the 4 values as STORED (bf16-rounded, masked) at element offset o of [M][ldc] (o % 4 == 0), xs their
+// bacc_loadx.  The sums are updated unconditionally (only the factor depends on the mode): a mode-dependent
+// update made hipcc keep the accumulators in scratch with a dynamic index.
+__device__ __forceinline__ void bacc_add4x(BnAccLane& l, const BnAcc& e, const BnAccChan& c, const BnAccX& xs,
+                                           const float (&v)[4]) {
   float f[4], f2[4];
   if (e.mode == 1) {  // Q: g * xhat (of the first / the second BatchNorm's input)
-    const bacc_bf16x4 xv = *reinterpret_cast<const bacc_bf16x4*>(e.x + o);
-    const bacc_bf16x4 xv2 = *reinterpret_cast<const bacc_bf16x4*>((e.acc2 ? e.x2 : e.x) + o);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      f[r] = ((float)xv[r] - c.mu[r]) * c.is[r];
-      f2[r] = ((float)xv2[r] - c.mu2[r]) * c.is2[r];
+      f[r] = ((float)xs.x[r] - c.mu[r]) * c.is[r];
+      f2[r] = ((float)xs.x2[r] - c.mu2[r]) * c.is2[r];
     }
   } else {  // Q: y * y
 #pragma unroll
@@ -76,6 +94,10 @@ __device__ __forceinline__ void bacc_add4(BnAccLane& l, const BnAcc& e, const Bn
     l.q[r] += v[r] * f[r];
     l.q2[r] += v[r] * f2[r];
   }
+}
+__device__ __forceinline__ void bacc_add4(BnAccLane& l, const BnAcc& e, const BnAccChan& c, long long o,
+                                          const float (&v)[4]) {
+  bacc_add4x(l, e, c, bacc_loadx(e, o), v);
 }
 
 // sum over the lanes l ^ m, m in {1, 2, 4, 8} (the 16 lanes of an MFMA 16x16 C/D row group that hold

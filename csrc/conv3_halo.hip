@@ -71,29 +71,61 @@ struct C3P {
 __device__ __forceinline__ int wswz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
 // epilogue of 4 consecutive output channels of one pixel (as igemm64): alpha, residual join, ReLU, relu';
-// `stored` receives the values as stored (bf16-rounded)
-__device__ __forceinline__ void c3_store(const C3P& p, long long m, int co, const f32x4& a, float (&stored)[4]) {
-  const long long o = m * p.ldc + co;
+// `stored` receives the values as stored (bf16-rounded).  The loads (c3_preload) are issued for all of a
+// lane's elements before the first store: a load behind a store waits for that store too (csrc/bn_acc.h).
+struct C3Pre {
+  bf16x4_t rv, rm, mk;
+};
+// (every tensor the epilogue touches is [M][ldc] bf16 under 4 GB -- conv3_halo_supported -- so one 32-bit
+// byte offset per element serves all of them: an SGPR base + VGPR offset per load instead of a 64-bit
+// address register pair per pointer and element)
+template <typename T>
+__device__ __forceinline__ const T& c3_at(const void* base, unsigned boff) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + boff);
+}
+__device__ __forceinline__ unsigned c3_boff(const C3P& p, long long m, int co) {
+  return (unsigned)(m * p.ldc + co) * 2u;
+}
+__device__ __forceinline__ C3Pre c3_preload(const C3P& p, unsigned boff) {
+  C3Pre q;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) q.rv[r] = q.rm[r] = q.mk[r] = (__bf16)1.f;
+  if (p.res) {
+    q.rv = c3_at<bf16x4_t>(p.res, boff);
+    if (p.resmask) q.rm = c3_at<bf16x4_t>(p.resmask, boff);
+  }
+  if (p.mask) q.mk = c3_at<bf16x4_t>(p.mask, boff);
+  return q;
+}
+__device__ __forceinline__ BnAccX c3_loadx(const BnAcc& e, unsigned boff) {
+  BnAccX r;
+  if (e.mode == 1) {
+    r.x = c3_at<bacc_bf16x4>(e.x, boff);
+    r.x2 = e.acc2 ? c3_at<bacc_bf16x4>(e.x2, boff) : r.x;  // (one BatchNorm: no second read of x)
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r.x[k] = r.x2[k] = (__bf16)0.f;
+  }
+  return r;
+}
+__device__ __forceinline__ void c3_store_pre(const C3P& p, unsigned boff, const f32x4& a, const C3Pre& q,
+                                             float (&stored)[4]) {
   float v[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) v[r] = a[r] * p.alpha;
   if (p.res) {
-    const bf16x4_t rv = *reinterpret_cast<const bf16x4_t*>(p.res + o);
-    bf16x4_t rm;
-    if (p.resmask) rm = *reinterpret_cast<const bf16x4_t*>(p.resmask + o);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (!p.resmask || (float)rm[r] > 0.f) v[r] += (float)rv[r];
+      if (!p.resmask || (float)q.rm[r] > 0.f) v[r] += (float)q.rv[r];
   }
   if (p.relu) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
   }
   if (p.mask) {
-    const bf16x4_t mk = *reinterpret_cast<const bf16x4_t*>(p.mask + o);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (!((float)mk[r] > 0.f)) v[r] = 0.f;
+      if (!((float)q.mk[r] > 0.f)) v[r] = 0.f;
   }
   bf16x4_t ov;
 #pragma unroll
@@ -101,7 +133,7 @@ __device__ __forceinline__ void c3_store(const C3P& p, long long m, int co, cons
     ov[r] = f2bf(v[r]);
     stored[r] = (float)ov[r];
   }
-  *reinterpret_cast<bf16x4_t*>(p.out + o) = ov;
+  *reinterpret_cast<bf16x4_t*>(reinterpret_cast<char*>(p.out) + boff) = ov;
 }
 
 // ROW: one step is a kernel row (3 taps, 48 MFMAs per wave at BN = 64) instead of one tap (16): the
@@ -283,40 +315,72 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
     const bool two = p.bacc.acc2 != nullptr;
     float* red = reinterpret_cast<float*>(lds);
     __syncthreads();  // every wave is done with the halo / weights: LDS is free
+    // the epilogue's loads (residual / mask, the BatchNorm inputs and statistics) in flight before the
+    // stores, in batches of UB channel groups (register budget): one round trip per batch
+    constexpr int UB = TN < 2 ? TN : 2;
 #pragma unroll
-    for (int u = 0; u < TN; ++u) {
-      const int cl = wn * (BN / 2) + 16 * u + 4 * fc;
-      const BnAccChan bc = bacc_chan(p.bacc, co0 + cl);
-      BnAccLane bl;
-      bacc_zero(bl);
+    for (int u0 = 0; u0 < TN; u0 += UB) {
+      C3Pre pre[UB][4];
+      BnAccX px[UB][4];
+      BnAccChan bc[UB];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int s = wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
-        const long long m = (long long)tile * kCP + s;
-        float sv[4];
-        c3_store(p, m, co0 + cl, acc[u][t], sv);
-        bacc_add4(bl, p.bacc, bc, m * p.ldc + co0 + cl, sv);
+      for (int du = 0; du < UB; ++du) {
+        const int co = co0 + wn * (BN / 2) + 16 * (u0 + du) + 4 * fc;
+        bc[du] = bacc_chan(p.bacc, co);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const unsigned bo = c3_boff(p, (long long)tile * kCP + wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1), co);
+          pre[du][t] = c3_preload(p, bo);
+          px[du][t] = c3_loadx(p.bacc, bo);
+        }
       }
-      bacc_reduce16(bl, two);
-      if (fl == 0) bacc_stash(red, wm, BN, cl, bl);
+#pragma unroll
+      for (int du = 0; du < UB; ++du) {
+        const int u = u0 + du;
+        const int cl = wn * (BN / 2) + 16 * u + 4 * fc;
+        BnAccLane bl;
+        bacc_zero(bl);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const long long m = (long long)tile * kCP + wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
+          float sv[4];
+          c3_store_pre(p, c3_boff(p, m, co0 + cl), acc[u][t], pre[du][t], sv);
+          bacc_add4x(bl, p.bacc, bc[du], px[du][t], sv);
+        }
+        bacc_reduce16(bl, two);
+        if (fl == 0) bacc_stash(red, wm, BN, cl, bl);
+      }
     }
     __syncthreads();
     bacc_flush(p.bacc, red, 2, BN, co0, p.Cout, tid, 256);
     return;
   }
+  if (p.ks > 1) {  // raw partials of this split's channel blocks
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const long long m = (long long)tile * kCP + wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
+#pragma unroll
+      for (int u = 0; u < TN; ++u) {
+        const int co = co0 + wn * (BN / 2) + 16 * u + 4 * fc;
+        *reinterpret_cast<f32x4*>(p.ws + ((long long)ksp * p.ntiles * kCP + m) * p.Cout + co) = acc[u][t];
+      }
+    }
+    return;
+  }
+  C3Pre pre[4][TN];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+      pre[t][u] = c3_preload(p, c3_boff(p, (long long)tile * kCP + wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1),
+                                        co0 + wn * (BN / 2) + 16 * u + 4 * fc));
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const int s = wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
-    const long long m = (long long)tile * kCP + s;
+    const long long m = (long long)tile * kCP + wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
 #pragma unroll
     for (int u = 0; u < TN; ++u) {
-      const int co = co0 + wn * (BN / 2) + 16 * u + 4 * fc;
-      if (p.ks > 1) {  // raw partial of this split's channel blocks
-        *reinterpret_cast<f32x4*>(p.ws + ((long long)ksp * p.ntiles * kCP + m) * p.Cout + co) = acc[u][t];
-        continue;
-      }
       float sv[4];
-      c3_store(p, m, co, acc[u][t], sv);
+      c3_store_pre(p, c3_boff(p, m, co0 + wn * (BN / 2) + 16 * u + 4 * fc), acc[u][t], pre[t][u], sv);
     }
   }
 }
@@ -361,24 +425,25 @@ __global__ void __launch_bounds__(512, 1) conv3_halo_c64_kernel(C3P p) {
   // ---- halo staging map (tile independent part)
   const FDiv fper(p.HR2 * p.HW2), fhw2(p.HW2), frw(p.R * p.W), fw(p.W);
   const int ch = tid & 7, r8 = tid >> 3;
-  int xro[kC64XP], xhr[kC64XP], xiw[kC64XP];
+  // (halo row hr - 1 and column hc - 1 packed as two 16-bit halves: the epilogue's preloads need the
+  // registers; a row past the halo gets -16384, which no image row offset brings back into range)
+  int xro[kC64XP], xhw[kC64XP];
 #pragma unroll
   for (int i = 0; i < kC64XP; ++i) {
     const int j = r8 + 32 * i;
     const int slot = fper.div(j), rem = j - slot * fper.d;
     const int hr = fhw2.div(rem), hc = rem - hr * p.HW2;
     xro[i] = slot * p.R + hr - 1;
-    xhr[i] = j < p.hrows ? hr - 1 : -(1 << 20);
-    xiw[i] = hc - 1;
+    xhw[i] = (int)((unsigned)(j < p.hrows ? hr - 1 : -16384) << 16) | ((hc - 1) & 0xffff);
   }
   u32x4_t rh[kC64XP];
   auto load_halo = [&](int t) {
     const int gr0 = t * p.rows_per_tile, oh0 = gr0 % p.H;
 #pragma unroll
     for (int i = 0; i < kC64XP; ++i) {
-      const int ih = oh0 + xhr[i];
-      const bool v = (unsigned)ih < (unsigned)p.H && (unsigned)xiw[i] < (unsigned)p.W;
-      rh[i] = cload16(v ? (const void*)(p.src + ((long long)(gr0 + xro[i]) * p.W + xiw[i]) * 64 + ch * 8)
+      const int ih = oh0 + (xhw[i] >> 16), iw = (int)(short)(xhw[i] & 0xffff);
+      const bool v = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      rh[i] = cload16(v ? (const void*)(p.src + ((long long)(gr0 + xro[i]) * p.W + iw) * 64 + ch * 8)
                         : (const void*)&kZeroC3);
     }
   };
@@ -403,15 +468,34 @@ __global__ void __launch_bounds__(512, 1) conv3_halo_c64_kernel(C3P p) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) woff[u][h] = wswz(wn * 32 + 16 * u + fl, fc + 4 * h);
 
-  // BatchNorm sums of every stored value of this workgroup's tiles (csrc/bn_acc.h), kept per lane
+  // BatchNorm sums of every stored value of this workgroup's tiles (csrc/bn_acc.h), kept per lane; the
+  // per-channel statistics they need (mode 1) sit in LDS, not in 32 registers for the kernel's life
   const bool bacc = p.bacc.acc != nullptr, two = p.bacc.acc2 != nullptr;
+  __shared__ float bcs[4][64];  // mean, invstd, mean2, invstd2
   BnAccLane bl[2];
-  BnAccChan bc[2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    bacc_zero(bl[u]);
-    if (bacc) bc[u] = bacc_chan(p.bacc, wn * 32 + 16 * u + 4 * fc);
+  for (int u = 0; u < 2; ++u) bacc_zero(bl[u]);
+  if (bacc && threadIdx.x < 16) {
+    const BnAccChan c = bacc_chan(p.bacc, 4 * threadIdx.x);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bcs[0][4 * threadIdx.x + r] = c.mu[r];
+      bcs[1][4 * threadIdx.x + r] = c.is[r];
+      bcs[2][4 * threadIdx.x + r] = c.mu2[r];
+      bcs[3][4 * threadIdx.x + r] = c.is2[r];
+    }
   }
+  auto chan = [&](int col) {
+    BnAccChan c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      c.mu[r] = bcs[0][col + r];
+      c.is[r] = bcs[1][col + r];
+      c.mu2[r] = bcs[2][col + r];
+      c.is2[r] = bcs[3][col + r];
+    }
+    return c;
+  };
   if (nt > gi) load_halo(tb + gi);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (nt > gi) store_halo();
@@ -448,14 +532,33 @@ __global__ void __launch_bounds__(512, 1) conv3_halo_c64_kernel(C3P p) {
       __syncthreads();  // this group's waves are done with the halo
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (nxt) store_halo();
+      // the epilogue's loads (mask / residual, BatchNorm inputs) in flight before the stores, in two
+      // batches of pixel tiles (register budget: the whole tile at once spilled); the next halo's
+      // registers are free by now
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const long long m = (long long)t * kCP + wm * 64 + 32 * (q >> 1) + 2 * fl + (q & 1);
+      for (int q0 = 0; q0 < 4; q0 += 2) {
+        C3Pre pre[2][2];
+        BnAccX px[2][2];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          float sv[4];
-          c3_store(p, m, wn * 32 + 16 * u + 4 * fc, acc[u][q], sv);
-          if (bacc) bacc_add4(bl[u], p.bacc, bc[u], m * p.ldc + wn * 32 + 16 * u + 4 * fc, sv);
+        for (int dq = 0; dq < 2; ++dq) {
+          const long long m = (long long)t * kCP + wm * 64 + 32 * ((q0 + dq) >> 1) + 2 * fl + ((q0 + dq) & 1);
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const unsigned bo = c3_boff(p, m, wn * 32 + 16 * u + 4 * fc);
+            pre[dq][u] = c3_preload(p, bo);
+            px[dq][u] = c3_loadx(p.bacc, bo);
+          }
+        }
+#pragma unroll
+        for (int dq = 0; dq < 2; ++dq) {
+          const int q = q0 + dq;
+          const long long m = (long long)t * kCP + wm * 64 + 32 * (q >> 1) + 2 * fl + (q & 1);
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            float sv[4];
+            c3_store_pre(p, c3_boff(p, m, wn * 32 + 16 * u + 4 * fc), acc[u][q], pre[dq][u], sv);
+            if (bacc) bacc_add4x(bl[u], p.bacc, chan(wn * 32 + 16 * u + 4 * fc), px[dq][u], sv);
+          }
         }
       }
     } else {
@@ -498,6 +601,7 @@ bool conv3_halo_supported(const IGemmArgs& a, int mode) {
          a.N % 64 == 0 && a.K == 9 * a.SC && a.Kpad >= a.K && a.Kpad % 8 == 0 && a.ldc % 4 == 0 && !a.bias &&
          !a.out_f32 && !a.drop.on && !a.pool_code && !a.bn.part &&
          a.M % kCP == 0 && a.M % (a.OH * a.OW) == 0 && c3_geom(a.OH, a.OW, R, TI) &&
+         (long long)a.M * a.ldc * 2 < (1LL << 32) &&  // one 32-bit byte offset per epilogue element
          ((uintptr_t)a.src & 15) == 0 && ((uintptr_t)a.w & 15) == 0 && ((uintptr_t)a.out & 7) == 0 &&
          (((uintptr_t)a.res | (uintptr_t)a.resmask | (uintptr_t)a.mask) & 7) == 0;
 }

@@ -42,6 +42,24 @@ __device__ __forceinline__ unsigned fed_ld(const unsigned* p) {
   return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The master shards and the slots live in other ranks' memory (IPC-mapped; on a shared GPU the importing
+// process may map them cacheable): every access to them is a system-scope one, so no XCD's L2 serves a
+// stale line and no store waits in one (4-byte relaxed atomics: global_load / store with sc0 sc1).
+__device__ __forceinline__ f32x4 fed_ld4(const float* p) {
+  f32x4 v;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    v[j] = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(const_cast<float*>(p)) + j, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM));
+  return v;
+}
+__device__ __forceinline__ void fed_st4(float* p, const f32x4& v) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    __hip_atomic_store(reinterpret_cast<unsigned*>(p) + j, __float_as_uint(v[j]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ float* fed_elem(float* const* tab, int shift, long long i, long long slot_off) {
   return tab[i >> shift] + slot_off + (i & ((1LL << shift) - 1));
 }
@@ -92,7 +110,7 @@ __global__ __launch_bounds__(kFedBlock) void fed_pull_kernel(FedArgs a) {
     __syncthreads();
     const unsigned s0 = s_seq;
     for (long long i = lo + 4LL * threadIdx.x; i < hi; i += 4LL * kFedBlock) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(fed_elem(master, a.shard_shift, i, 0));
+      const f32x4 v = fed_ld4(fed_elem(master, a.shard_shift, i, 0));
       *reinterpret_cast<f32x4*>(a.w + i) = v;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the copy's loads returned before the re-check
@@ -194,7 +212,7 @@ __global__ __launch_bounds__(kFedBlock) void fed_upload_kernel(FedArgs a, int pu
     fed_slice(a, blockIdx.x, G, lo, hi);
     const long long soff = (long long)s_slot << a.shard_shift;
     for (long long i = lo + 4LL * threadIdx.x; i < hi; i += 4LL * kFedBlock)
-      *reinterpret_cast<f32x4*>(fed_elem(slots, a.shard_shift, i, soff)) = *reinterpret_cast<const f32x4*>(a.g + i);
+      fed_st4(fed_elem(slots, a.shard_shift, i, soff), *reinterpret_cast<const f32x4*>(a.g + i));
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's slot stores have landed
   __syncthreads();
@@ -241,17 +259,16 @@ __global__ __launch_bounds__(kFedBlock) void fed_apply_kernel(FedArgs a) {
   const float lr = a.lr_dev ? *a.lr_dev : a.lr;
   const float invk = 1.f / (float)a.K;
   for (long long i = lo + 4LL * threadIdx.x; i < hi; i += 4LL * kFedBlock) {
-    f32x4 s = *reinterpret_cast<const f32x4*>(fed_elem(slots, a.shard_shift, i, 0));
-    for (int t = 1; t < a.K; ++t)
-      s += *reinterpret_cast<const f32x4*>(fed_elem(slots, a.shard_shift, i, (long long)t << a.shard_shift));
+    f32x4 s = fed_ld4(fed_elem(slots, a.shard_shift, i, 0));
+    for (int t = 1; t < a.K; ++t) s += fed_ld4(fed_elem(slots, a.shard_shift, i, (long long)t << a.shard_shift));
     float* m = fed_elem(master, a.shard_shift, i, 0);
-    f32x4 w = *reinterpret_cast<const f32x4*>(m);
+    f32x4 w = fed_ld4(m);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
 #pragma clang fp contract(off)
       w[j] = w[j] - lr * (s[j] * invk);
     }
-    *reinterpret_cast<f32x4*>(m) = w;
+    fed_st4(m, w);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's master stores have landed
   __syncthreads();

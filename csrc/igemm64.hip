@@ -488,13 +488,15 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
       const int cl = wn * TN * 16 + j * 16 + fq * 4;
       const int col0 = n0 + cl;
       const bool colok = col0 + 3 < a.N;
+      // this column group's loads (statistics, residual / masks, BatchNorm inputs) all in flight before
+      // its first store: a load behind a store waits for that store too (csrc/bn_acc.h)
       const BnAccChan bc = bacc_chan(a.bacc, colok ? col0 : 0);
-      BnAccLane bl;
-      bacc_zero(bl);
+      long long oo[TM];
+      bf16x4_t prv[TM], prm[TM], pmk[TM];
+      BnAccX pxs[TM];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int row = m0 + wm * TM * 16 + i * 16 + fr;
-        if (row >= Mrows || !colok) continue;
+        const int row = min(m0 + wm * TM * 16 + i * 16 + fr, Mrows - 1);  // (clamped: skipped below)
         long long orow = row;
         if (PAR) {
           const int b = row / (cHc * cWc);
@@ -502,27 +504,40 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
           const int y = rem / cWc, x = rem - (rem / cWc) * cWc;
           orow = ((long long)b * a.OH + 2 * y + py) * a.OW + 2 * x + px;
         }
-        const long long o = orow * a.ldc + col0;
+        const long long o = orow * a.ldc + (colok ? col0 : 0);
+        oo[i] = o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) prv[i][r] = prm[i][r] = pmk[i][r] = (__bf16)1.f;
+        if (a.res) {
+          prv[i] = *reinterpret_cast<const bf16x4_t*>(a.res + o);
+          if (a.resmask) prm[i] = *reinterpret_cast<const bf16x4_t*>(a.resmask + o);
+        }
+        if (a.mask) pmk[i] = *reinterpret_cast<const bf16x4_t*>(a.mask + o);
+        pxs[i] = bacc_loadx(a.bacc, o);
+      }
+      BnAccLane bl;
+      bacc_zero(bl);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = m0 + wm * TM * 16 + i * 16 + fr;
+        if (row >= Mrows || !colok) continue;
+        const long long o = oo[i];
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * a.alpha + (a.bias ? a.bias[col0 + r] : 0.f);
         if (a.res) {
-          const bf16x4_t rv = *reinterpret_cast<const bf16x4_t*>(a.res + o);
-          bf16x4_t rm;
-          if (a.resmask) rm = *reinterpret_cast<const bf16x4_t*>(a.resmask + o);
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (!a.resmask || (float)rm[r] > 0.f) v[r] += (float)rv[r];
+            if (!a.resmask || (float)prm[i][r] > 0.f) v[r] += (float)prv[i][r];
         }
         if (a.relu) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
         }
         if (a.mask) {
-          const bf16x4_t mk = *reinterpret_cast<const bf16x4_t*>(a.mask + o);
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (!((float)mk[r] > 0.f)) v[r] = 0.f;
+            if (!((float)pmk[i][r] > 0.f)) v[r] = 0.f;
         }
         bf16x4_t ov;
         float sv[4];
@@ -532,7 +547,7 @@ __global__ void __launch_bounds__(256, (igemm64_occ<BM, BN>())) igemm64_kernel(I
           sv[r] = (float)ov[r];
         }
         *reinterpret_cast<bf16x4_t*>(reinterpret_cast<bf16*>(a.out) + o) = ov;
-        bacc_add4(bl, a.bacc, bc, o, sv);
+        bacc_add4x(bl, a.bacc, bc, pxs[i], sv);
       }
       bacc_reduce16(bl, two);
       if (fr == 0) bacc_stash(red, wm, BN, cl, bl);
@@ -694,51 +709,79 @@ __global__ void __launch_bounds__(256) igemm64_splitk_epilogue_kernel(IGemmArgs 
   bacc_zero(bl);
   BnAccChan bc;
   if (bacc) bc = bacc_chan(a.bacc, (int)(threadIdx.x % cpr) * 4);
-  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < total4; q += (long long)gridDim.x * 256) {
-    const long long row = q / (a.N >> 2);
-    const int col0 = (int)(q - row * (a.N >> 2)) * 4;
-    f32x4 sacc = *reinterpret_cast<const f32x4*>(a.splitk_ws + row * a.N + col0);
-    for (int s = 1; s < a.splits; ++s)
-      sacc += *reinterpret_cast<const f32x4*>(a.splitk_ws + ((long long)s * a.M + row) * a.N + col0);
-    const long long o = row * a.ldc + col0;
-    float v[4];
+  // batches of U grid-stride iterations: every load of a batch (split partials, residual / masks,
+  // BatchNorm inputs) in flight before its first store (a load behind a store waits for it too)
+  constexpr int U = 4;
+  const long long gs = (long long)gridDim.x * 256;
+  for (long long q0 = (long long)blockIdx.x * 256 + threadIdx.x; q0 < total4; q0 += U * gs) {
+    f32x4 sacc[U];
+    bf16x4_t prv[U], prm[U], pmk[U];
+    BnAccX pxs[U];
+    long long oo[U];
+    int cc[U];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = sacc[r] * a.alpha + (a.bias ? a.bias[col0 + r] : 0.f);
-    if (a.res) {
-      const bf16x4_t rv = *reinterpret_cast<const bf16x4_t*>(a.res + o);
-      bf16x4_t rm;
-      if (a.resmask) rm = *reinterpret_cast<const bf16x4_t*>(a.resmask + o);
+    for (int u = 0; u < U; ++u) {
+      const long long q = min(q0 + u * gs, total4 - 1);  // (clamped: not stored below)
+      const long long row = q / (a.N >> 2);
+      const int col0 = (int)(q - row * (a.N >> 2)) * 4;
+      cc[u] = col0;
+      sacc[u] = *reinterpret_cast<const f32x4*>(a.splitk_ws + row * a.N + col0);
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (!a.resmask || (float)rm[r] > 0.f) v[r] += (float)rv[r];
-    }
-    if (a.relu) {
+      for (int s = 1; s < 4; ++s)  // (the common split counts unrolled so the loads issue together)
+        if (s < a.splits) sacc[u] += *reinterpret_cast<const f32x4*>(a.splitk_ws + ((long long)s * a.M + row) * a.N + col0);
+      for (int s = 4; s < a.splits; ++s)
+        sacc[u] += *reinterpret_cast<const f32x4*>(a.splitk_ws + ((long long)s * a.M + row) * a.N + col0);
+      const long long o = row * a.ldc + col0;
+      oo[u] = o;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-    }
-    if (a.mask) {
-      const bf16x4_t mk = *reinterpret_cast<const bf16x4_t*>(a.mask + o);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (!((float)mk[r] > 0.f)) v[r] = 0.f;
-    }
-    if (a.drop.on) {
-      const unsigned long long ds = drop_seed(a.drop.seed, a.drop.step, a.drop.step_add);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = drop_keep(ds, a.drop.thresh, o + r) ? (float)f2bf(v[r]) * a.drop.scale : 0.f;
-    }
-    if (a.out_f32) {
-      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
-    } else {
-      bf16x4_t ov;
-      float sv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        ov[r] = f2bf(v[r]);
-        sv[r] = (float)ov[r];
+      for (int r = 0; r < 4; ++r) prv[u][r] = prm[u][r] = pmk[u][r] = (__bf16)1.f;
+      if (a.res) {
+        prv[u] = *reinterpret_cast<const bf16x4_t*>(a.res + o);
+        if (a.resmask) prm[u] = *reinterpret_cast<const bf16x4_t*>(a.resmask + o);
       }
-      *reinterpret_cast<bf16x4_t*>(reinterpret_cast<bf16*>(a.out) + o) = ov;
-      if (bacc) bacc_add4(bl, a.bacc, bc, o, sv);
+      if (a.mask) pmk[u] = *reinterpret_cast<const bf16x4_t*>(a.mask + o);
+      if (bacc) pxs[u] = bacc_loadx(a.bacc, o);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (q0 + u * gs >= total4) break;
+      const int col0 = cc[u];
+      const long long o = oo[u];
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = sacc[u][r] * a.alpha + (a.bias ? a.bias[col0 + r] : 0.f);
+      if (a.res) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (!a.resmask || (float)prm[u][r] > 0.f) v[r] += (float)prv[u][r];
+      }
+      if (a.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (a.mask) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (!((float)pmk[u][r] > 0.f)) v[r] = 0.f;
+      }
+      if (a.drop.on) {
+        const unsigned long long ds = drop_seed(a.drop.seed, a.drop.step, a.drop.step_add);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = drop_keep(ds, a.drop.thresh, o + r) ? (float)f2bf(v[r]) * a.drop.scale : 0.f;
+      }
+      if (a.out_f32) {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
+      } else {
+        bf16x4_t ov;
+        float sv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ov[r] = f2bf(v[r]);
+          sv[r] = (float)ov[r];
+        }
+        *reinterpret_cast<bf16x4_t*>(reinterpret_cast<bf16*>(a.out) + o) = ov;
+        if (bacc) bacc_add4x(bl, a.bacc, bc, pxs[u], sv);
+      }
     }
   }
   if (bacc) {

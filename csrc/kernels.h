@@ -359,9 +359,11 @@ hipError_t p2p_allreduce(const P2PArgs& a, hipStream_t st);
 // LeNet-5 reduce, ...) sums the W ranks' values of its own slot without a separate all-reduce launch.
 // Region of rank r (inside its P2PComm allocation): [2 parities][nslots][kP2PMaxRanks src][kLLSlot].
 constexpr int kLLSlot = 1024;  // granules per slot (one per thread of a 1024-thread epilogue)
+constexpr int kLLParts = 8;    // owners a slot may be split over (LLComm::part_epochs)
 struct LLComm {
   unsigned long long* bases[kP2PMaxRanks];  // bases[r] = rank r's LL region mapped into this process
   unsigned* epochs;                         // [nslots] per-slot call counters (local)
+  unsigned* part_epochs;                    // [nslots][kLLParts] per-part counters (slots split over owners)
   int* err;                                 // sticky error word (shared with the P2P all-reduce)
   int* herr;                                // host-mapped mirror
   long long timeout_ticks;
@@ -538,6 +540,14 @@ struct LeNetRedArgs {
   int ps_on;
   PSArgs ps;
   unsigned long long* stamps;  // diagnostic: [grid][16] wall-clock marks per phase (scripts/lenetstamps.py), or null
+  // successor ownership (succ = 1; one job per workgroup): job (slot s, chunk c) publishes its partial as
+  // 8-byte {launch epoch, value} granules; the workgroups of slot s + 1 (plus one owner-only group after the
+  // last slot) each own one eighth of slot s's positions and sum its 8 chunks in chunk order (no ticket,
+  // no slab reload: one hand-off).  A workgroup waits only on lower-indexed ones.
+  int succ;
+  unsigned long long* gran;  // [slots][8 chunks][1024]
+  unsigned* gran_ep;         // [grid] per-workgroup launch counters (each workgroup reads / bumps its own)
+  unsigned* gran_err;        // sticky: a granule wait timed out
 };
 // The reference CNN's conv block (csrc/kcnn_fused.hip): conv1 3x3x1->32 + ReLU, conv2 3x3x32->32 + ReLU,
 // 2x2 max-pool [+ folded dropout], input 28x28x1, in one forward and one backward launch (+ reduce).
@@ -615,8 +625,8 @@ size_t khead_ws_floats(int B, int K);
 size_t khead_lds(int K);
 bool khead_supported(int K, int C);
 hipError_t khead_train(KHeadArgs a, hipStream_t st);
-int lenet_dense_part_floats(int B);  // reduce scratch: job slabs + arrival tickets
-int lenet_red_slab_floats();
+int lenet_dense_part_floats(int B);  // reduce scratch: job slabs, arrival tickets, granules, launch counters
+void lenet_red_bind_scratch(float* dense_part, LeNetRedArgs& r);  // points r's scratch fields into it
 size_t lenet_train_lds();
 int lenet_blocks(int B);
 hipError_t lenet_train(const LeNetArgs& a, LeNetRedArgs r, hipStream_t st);

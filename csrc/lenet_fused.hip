@@ -863,6 +863,7 @@ constexpr int kConvPer = 256;    // conv parameters per slot
 constexpr int kSlotVals = 1024;  // values per slot (dense 32 x 32; conv slots use 256) = kLLSlot
 constexpr int kPerThread = kSlotVals / RT;
 constexpr int kMaxOwned = 16;    // slots one workgroup may own (host: G >= 8 * slots / kMaxOwned)
+constexpr unsigned long long kSuccTimeoutTicks = 100000000ull;  // 1 s of wall_clock64: a granule wait never takes that
 static_assert(kSlotVals <= kLLSlot, "LL slot too small");
 
 // The element a thread finalises: descriptor index di into LeNetSgd::d (-1: none) and the element index
@@ -1185,6 +1186,132 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     const bool pre = a.sgd_on && !PS;
     __shared__ float w_pre[kPerThread][RT], m_pre[kPerThread][RT];  // (LDS: not live across the jobs in VGPRs)
     __shared__ float own0[kPerThread][RT];  // the first owned slot's local sums
+    __shared__ unsigned s_dec;
+    if (a.succ) {
+      // successor ownership: this workgroup's job (slot grp, chunk c), published as {epoch, value}
+      // granules, then its eighth of slot grp - 1 (positions [c * cnt, (c + 1) * cnt)): one hand-off from
+      // the 8 producers, no ticket and no slab reload.  Every wait is on lower-indexed workgroups, which
+      // publish before they wait, so in-order dispatch needs no co-residency.
+      const int grp = blockIdx.x / kChunks, c = blockIdx.x - kChunks * grp;
+      __shared__ unsigned s_ge, s_pe;
+      if (threadIdx.x == 0) s_ge = a.gran_ep[blockIdx.x] + 1u;
+      __syncthreads();
+      const unsigned ge = s_ge;
+      if (grp < nslot) {
+        float part[kPerThread];
+        if (grp < a.dense_tiles) dense_job(a, tabs, grp, c, red, part);
+        else conv_job(a, grp - a.dense_tiles, c, red, part);
+        LR_STAMP(6);
+        const int npos = grp < a.dense_tiles ? kPerThread : 1;
+        unsigned long long* g = a.gran + ((long long)grp * kChunks + c) * kSlotVals + threadIdx.x;
+#pragma unroll
+        for (int e = 0; e < kPerThread; ++e)
+          if (e < npos)
+            __hip_atomic_store(g + RT * e, ((unsigned long long)ge << 32) | __float_as_uint(part[e]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      }
+      LR_STAMP(1);
+      const int s = grp - 1;
+      if (s >= 0) {
+        const bool dense = s < a.dense_tiles;
+        const int cnt = dense ? kSlotVals / kChunks : kConvPer / kChunks;
+        const int pos = c * cnt + (int)threadIdx.x;
+        const bool mine = (int)threadIdx.x < cnt;
+        Owned o = mine ? owned_elem(a, tabs, s, pos) : Owned{-1, 0};
+        // the old master / momentum values load while the granules are awaited
+        float w0 = 0.f, m0 = 0.f, v = 0.f;
+        if (a.sgd_on && !PS && o.di >= 0) {
+          const long long off = tabs.d[o.di].off + o.i;
+          w0 = a.sgd.master[off];
+          m0 = a.sgd.mom != nullptr ? a.sgd.mom[off] : 0.f;
+        }
+        if (mine) {
+          const unsigned long long* g = a.gran + (long long)s * kChunks * kSlotVals + pos;
+          const unsigned long long t0 = wall_clock64();
+          for (;;) {  // every chunk's granule in flight per poll; the sum in chunk order (the ticket path's)
+            unsigned long long q[kChunks];
+#pragma unroll
+            for (int cc = 0; cc < kChunks; ++cc)
+              q[cc] = __hip_atomic_load(g + cc * kSlotVals, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool ok = true;
+#pragma unroll
+            for (int cc = 0; cc < kChunks; ++cc) ok = ok && (unsigned)(q[cc] >> 32) == ge;
+            if (ok) {
+              v = __uint_as_float((unsigned)q[0]);
+#pragma unroll
+              for (int cc = 1; cc < kChunks; ++cc) v += __uint_as_float((unsigned)q[cc]);
+              break;
+            }
+            if (wall_clock64() - t0 > kSuccTimeoutTicks) {  // never expected: flag it, leave the element
+              atomicOr(a.gran_err, 1u);
+              if (LL) atomicOr(a.ll.err, 2);
+              if (PS) atomicOr(a.ps.stats + 5, 16ull);
+              o.di = -1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+        }
+        LR_STAMP(7);
+        if (!PS) LR_STAMP(2);
+        if (PS) {
+          const unsigned dec = lenet_ps_wait(a, &s_dec, applied0);
+          LR_STAMP(2);
+          if (dec == kPSAccept || dec == kPSReject) {
+            const PSArgs& p = a.ps;
+            float* pe[1] = {o.di >= 0 ? ps_elem(s_shard, p.shard_shift, tabs.d[o.di].off + o.i) : nullptr};
+            float d[1], wn[1];
+            {
+#pragma clang fp contract(off)
+              d[0] = -(tabs.hyper[0] * v);
+            }
+            if (dec == kPSAccept) {
+              ps_add<1>(pe, d, wn, p.excl != 0, p);
+            } else {
+              wn[0] = pe[0] ? __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(pe[0]), __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_SYSTEM))
+                            : 0.f;
+            }
+            if (o.di >= 0) {
+              tabs.g[o.di][o.i] = v;
+              if (dense) red_emit<true>(a, tabs, o, wn[0]);
+              else red_emit<false>(a, tabs, o, wn[0]);
+            }
+          }
+          LR_STAMP(5);
+        } else {
+          bool ok = true;
+          unsigned ee = 0;
+          if (LL) {  // the rank-order sum of this eighth (its own LL epoch word)
+            if (threadIdx.x == 0) s_pe = a.ll.part_epochs[s * kLLParts + c] + 1u;
+            __syncthreads();
+            ee = s_pe;
+            if (mine) {
+              ll_push(a.ll, s, pos, ee, v);
+              ok = ll_wait_sum(a.ll, s, pos, ee, v, v);
+            }
+            LR_STAMP(5);
+          }
+          if (ok && o.di >= 0) {
+            if (dense) red_apply<true>(a, tabs, o, v, w0, m0);
+            else red_apply<false>(a, tabs, o, v, w0, m0);
+          }
+          if (LL) {
+            __syncthreads();  // every position consumed before the part's epoch advances
+            if (threadIdx.x == 0) a.ll.part_epochs[s * kLLParts + c] = ee;
+          }
+        }
+      }
+      LR_STAMP(3);
+      if (PS) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's shard adds have landed
+        lenet_ps_arrive(a, s >= 0 ? 1u : 0u, (unsigned)(nslot * kChunks + 1));
+      }
+      if (threadIdx.x == 0) a.gran_ep[blockIdx.x] = ge;
+      LR_STAMP(4);
+      LR_FLUSH();
+      return;
+    }
     int nown = 0, narr = 0;  // slots owned (kept) / slots this workgroup finished last (async PS arrivals)
 #pragma unroll 1
     for (int j = blockIdx.x; j < nslot * kChunks; j += G) {
@@ -1275,7 +1402,6 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     }
     __syncthreads();
     LR_STAMP(1);
-    __shared__ unsigned s_dec;
     const unsigned dec = (PS && nown > 0) ? lenet_ps_wait(a, &s_dec, applied0) : 0u;
     LR_STAMP(2);
 #pragma unroll 1
@@ -1391,7 +1517,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     if (threadIdx.x == 0) *a.ps.bid_out = s_bid;
     ps_stage_indices(a.ps, s_bid, threadIdx.x, RT);
     LR_STAMP(10);
-    lenet_ps_arrive(a, 1u, (unsigned)(a.dense_tiles + a.nconv_slots + 1));
+    lenet_ps_arrive(a, 1u, (unsigned)((a.succ ? nslot * kChunks : nslot) + 1));
     LR_STAMP(1);
     LR_FLUSH();
     return;
@@ -1462,11 +1588,25 @@ static int lenet_red_slots() {
   for (auto& nk : NK) n += ((nk[0] + kDU - 1) / kDU) * ((nk[1] + 1 + kDU - 1) / kDU);
   return n;
 }
+// [slabs: slots x 8 x 1024 f32][tickets: round4(slots)][granules: slots x 8 x 1024 u64][per-workgroup
+// launch counters: round4(8 x (slots + 1))][granule error word, padded to 4]
+static int lenet_red_slab_floats() { return lenet_red_slots() * kChunks * kSlotVals; }
+static int lenet_red_ep_words() { return (kChunks * (lenet_red_slots() + 1) + 3) / 4 * 4; }
 int lenet_dense_part_floats(int B) {
   (void)B;
-  return lenet_red_slots() * kChunks * kSlotVals + (lenet_red_slots() + 3) / 4 * 4;
+  return 3 * lenet_red_slab_floats() + (lenet_red_slots() + 3) / 4 * 4 + lenet_red_ep_words() + 4;
 }
-int lenet_red_slab_floats() { return lenet_red_slots() * kChunks * kSlotVals; }
+void lenet_red_bind_scratch(float* base, LeNetRedArgs& r) {
+  r.slabs = base;
+  base += lenet_red_slab_floats();
+  r.tickets = reinterpret_cast<unsigned*>(base);
+  base += (lenet_red_slots() + 3) / 4 * 4;
+  r.gran = reinterpret_cast<unsigned long long*>(base);  // 16-byte aligned (every term is a multiple of 4)
+  base += 2 * lenet_red_slab_floats();
+  r.gran_ep = reinterpret_cast<unsigned*>(base);
+  base += lenet_red_ep_words();
+  r.gran_err = reinterpret_cast<unsigned*>(base);
+}
 
 hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   LeNetArgs a = a_in;
@@ -1518,7 +1658,15 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
     }
   const int nslot = r.dense_tiles + r.nconv_slots;
   const int njobs = nslot * kChunks;
-  if (r.exch_blocks <= 0 || r.exch_blocks > njobs) r.exch_blocks = njobs;
+  // successor ownership needs one job per workgroup (not the time-shared grid of several ranks on one
+  // GPU) and, multi-rank, the per-part LL epoch words
+  // Async PS keeps the tickets: 8x the owners made the apply-done fan-in (one counter) the launch's tail
+  // (0.0862 vs 0.0799 ms per async step at B = 4096)
+  if (r.succ && (r.ps_on || !(r.exch_blocks <= 0 || r.exch_blocks >= njobs) || !r.gran || !r.gran_ep || !r.gran_err ||
+                 nslot > lenet_red_slots() || (r.ll_on && !r.ll.part_epochs)))
+    r.succ = 0;
+  if (r.succ) r.exch_blocks = njobs + kChunks;  // + the owner-only group of the last slot
+  else if (r.exch_blocks <= 0 || r.exch_blocks > njobs) r.exch_blocks = njobs;
   // a workgroup runs <= ceil(njobs / G) jobs, so it owns at most that many slots
   if ((long long)r.exch_blocks * kMaxOwned < njobs) return hipErrorInvalidValue;
   // 256-thread workgroups at <= 128 VGPRs and ~17 KB LDS: 4 per CU, 1024 on the chip

@@ -14,6 +14,8 @@ Python switches (default in brackets):
   fold_dropout [1]         dropout folded into producer epilogues
   khead_fused [1]          the reference CNN's dense head (4608 -> 128 -> C + CE) as one split-K launch
                            plus the fused head weight-gradient launch (0: per-layer GEMMs + head kernels)
+  lenet_succ [1]           LeNet-5 reduce launch: successor ownership (each slot's partials handed to the next
+                           slot's workgroups as {epoch, value} granules; 0: arrival tickets + slab reload)
   multistep [1]            bench.py unrolls up to 64 steps per hipGraph (0: one replay per step)
   fused_selftest [1]       real-kernel self-test of the multi-rank fused LeNet-5 step before its first use
                            (0: trust the LL exchange's own setup self-test)
@@ -41,7 +43,7 @@ from __future__ import annotations
 import os
 
 _DEFAULTS = {"lenet_fused": 1, "lenet_fused_update": 1, "async_fused": 1, "kcnn_fused": 1, "khead_fused": 1, "fold_dropout": 1,
-             "multistep": 1, "fused_selftest": 1, "wgrad_overlap": 0, "proj_overlap": 0, "concurrent_backward": 0, "bn_epilogue": 0,
+             "lenet_succ": 1, "multistep": 1, "fused_selftest": 1, "wgrad_overlap": 0, "proj_overlap": 0, "concurrent_backward": 0, "bn_epilogue": 0,
              "bn_fused": 0, "bn_acc": 1, "bn_acc_rep": 8}
 
 

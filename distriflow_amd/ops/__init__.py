@@ -14,6 +14,7 @@ from __future__ import annotations
 import torch
 
 from .. import native
+from ..diagnostics import on as _diag_on
 from . import reference as ref
 
 MODE_DIRECT, MODE_FWD, MODE_DGRAD = 0, 1, 2
@@ -905,7 +906,13 @@ def lenet_train(x, labels, conv, dense_w, dense_wt, dense_b, conv_grads, dense_g
     _C().lenet_train(src, idx, float(scale), lab, list(conv), list(dense_w), list(dense_wt), list(dense_b),
                      list(conv_grads), list(dense_gw), list(dense_gb), list(hT), list(dzT), conv_part, dense_part,
                      loss_part, stats, scratch if frag is None else frag, ftab, pxtab, int(B), float(grad_scale),
-                     prep=bool(prep) or frag is None, snap=snap, conv_mom=list(conv_mom), **(sgd or {}))
+                     prep=bool(prep) or frag is None, snap=snap, conv_mom=list(conv_mom),
+                     red_succ=_diag_on("lenet_succ"), **(sgd or {}))
+
+
+def lenet_red_error(dense_part) -> int:
+    """Sticky error word of the LeNet-5 reduce launch's granule hand-off (non-zero: a wait timed out)."""
+    return int(dense_part[-4:].view(torch.int32)[0].item())
 
 
 def convpool_supported(H, W, C, KH, KW, pad, N) -> bool:

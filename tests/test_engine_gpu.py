@@ -427,19 +427,52 @@ def _resnet_pair(monkeypatch, B, seed=7):
         nets[acc] = build_model("resnet18_cifar", device="cuda", seed=seed)
         nets[acc].bind(B)  # (the layers read the switch when their buffers are allocated)
     monkeypatch.delenv("DISTRIFLOW_DIAG")
-    nets["0"].store.set_flat(nets["1"].store.master)
+    w = nets["1"].store.master.to(torch.bfloat16).float()  # bf16-representable, so a CPU reference can match
+    nets["1"].store.set_flat(w)
+    nets["0"].store.set_flat(w)
     return nets["1"], nets["0"]
 
 
-@pytest.mark.parametrize("B", [32, 256])
-def test_bn_acc_matches_statistics_passes(monkeypatch, B):
-    """BatchNorm statistics from the producers' epilogue sums (no bn_stats launch)
-    give the same gradients, batch statistics and running statistics as the statistics passes, over two
-    consecutive steps (the accumulators are cleared by their consumers in between), at the benchmarked
-    batch too."""
-    from distriflow_amd.models.layers import BatchNorm
+def _cpu_reference_grads(net, x, y):
+    """Per-tensor gradients of the same ResNet-18 on the CPU fp32 reference path (bf16 buffers)."""
+    from distriflow_amd.models.net import Net
+    from distriflow_amd.models.zoo import MODELS
 
+    layers, shape = MODELS["resnet18_cifar"]()
+    c = Net(layers, shape, device="cpu", name="resnet18_cifar", seed=0, compute_dtype=torch.bfloat16)
+    c.store.master.copy_(net.store.master.cpu())
+    c.compute_gradients(x.float().cpu(), y.cpu())
+    return {s.name: c.store.gradient(s.name).clone() for s in c.store.specs}
+
+
+def _bn_grad_inputs(net):
+    """(BatchNorm, its output gradient g as stored by the producer) for every BatchNorm of ResNet-18."""
+    from distriflow_amd.models.layers import BatchNorm, ResidualBlock
+
+    ls = net.exec_layers
+    out = []
+    for i, l in enumerate(ls):
+        if isinstance(l, BatchNorm):
+            out.append((l, ls[i + 1].dx))
+        elif isinstance(l, ResidualBlock):
+            out.append((l.bn1, l.conv2.dx))
+            g = ls[i + 1].dx  # the next block's (or the GAP's) data gradient, relu' applied
+            out.append((l.bn2, g))
+            if l.proj is not None:
+                out.append((l.proj_bn, g))
+    return out
+
+
+@pytest.mark.parametrize("B", [32, 256])
+def test_bn_acc_statistics_exact_and_training_matches_passes(monkeypatch, B):
+    """BatchNorm statistics from the producers' epilogue sums (no bn_stats launch).
+    (1) Every BatchNorm's batch mean / invstd and its dgamma / dbeta equal fp64 sums over the very tensors
+    the engine stored (the conv output x; the masked output gradient g), over two consecutive steps (the
+    accumulators are cleared by their consumers in between), at the benchmarked batch too.  (2) The whole
+    step agrees with the statistics-pass engine on the same weights and batch (loss), and its per-tensor
+    gradients are as close to the fp32 CPU reference as the statistics-pass engine's are."""
     a, b = _resnet_pair(monkeypatch, B)
+    st = a.store
     torch.manual_seed(4)
     for step in range(2):
         x = torch.rand((B, 32, 32, 3), device="cuda").to(torch.bfloat16)
@@ -447,21 +480,36 @@ def test_bn_acc_matches_statistics_passes(monkeypatch, B):
         sa = a.compute_gradients(x, y).clone()
         sb = b.compute_gradients(x, y).clone()
         torch.cuda.synchronize()
-        bns_a = [l for l in a._all_leaf_layers() if isinstance(l, BatchNorm)]
-        bns_b = [l for l in b._all_leaf_layers() if isinstance(l, BatchNorm)]
-        assert all(l.acc_on for l in bns_a) and not any(l.acc_on for l in bns_b)
-        for la, lb in zip(bns_a, bns_b):
-            torch.testing.assert_close(la.mean, lb.mean, rtol=1e-4, atol=1e-5)
-            torch.testing.assert_close(la.invstd, lb.invstd, rtol=1e-3, atol=1e-4)
-            torch.testing.assert_close(la.run_var, lb.run_var, rtol=1e-4, atol=1e-5)
-        assert abs(float(sa[0]) - float(sb[0])) <= 1e-3 * abs(float(sb[0])) + 1e-3
-        ga, gb = a.store.grad.double(), b.store.grad.double()
-        rel = float((ga - gb).norm() / gb.norm())
-        cos = float((ga @ gb) / (ga.norm() * gb.norm()))
-        print(f"B={B} step {step}: grad rel L2 {rel:.2e}, cosine {cos:.8f}")
-        assert cos > 0.9999 and rel < 1e-2, (rel, cos)
-        # the SGD step, so that step 2 starts from new weights on both
-        for n in (a, b):
+        pairs = _bn_grad_inputs(a)
+        assert len(pairs) == 20 and all(bn.acc_on for bn, _ in pairs)
+        for bn, g in pairs:
+            xv = bn.x.double().reshape(-1, bn.C)
+            m = xv.mean(0)
+            var = (xv * xv).mean(0) - m * m
+            torch.testing.assert_close(bn.mean.double(), m, rtol=1e-4, atol=1e-5)
+            torch.testing.assert_close(bn.invstd.double(), 1.0 / torch.sqrt(var + bn.eps), rtol=1e-3, atol=1e-4)
+            gv = g.double().reshape(-1, bn.C)
+            xh = (xv - bn.mean.double()) * bn.invstd.double()
+            db, dg = gv.sum(0), (gv * xh).sum(0)
+            sc = float(db.abs().max()) + 1e-12
+            torch.testing.assert_close(st.gradient(f"{bn.name}/beta").double(), db, rtol=1e-3, atol=1e-4 * sc)
+            sc = float(dg.abs().max()) + 1e-12
+            torch.testing.assert_close(st.gradient(f"{bn.name}/gamma").double(), dg, rtol=1e-3, atol=1e-4 * sc)
+        assert abs(float(sa[0]) - float(sb[0])) <= 2e-3 * abs(float(sb[0])) + 1e-3
+        if step == 0:
+            # both engines against the fp32 CPU reference, tensor by tensor: small-batch BatchNorm amplifies
+            # bf16 rounding flips (test_model_gradients_match_cpu), so the two bf16 engines are not compared
+            # with each other; the accumulated statistics must be as close to fp32 as the passes are
+            ref = _cpu_reference_grads(a, x, y)
+            worst = {}
+            for tag, n in (("acc", a), ("passes", b)):
+                coss = {k: _cos(n.store.gradient(k).cpu(), r) for k, r in ref.items() if r.norm() > 1e-6}
+                conv = [v for k, v in coss.items() if k.endswith("/kernel")]
+                worst[tag] = (min(conv), sum(coss.values()) / len(coss))
+            print(f"B={B}: worst conv-kernel cosine / mean cosine vs fp32: {worst}")
+            assert worst["acc"][0] > 0.96 and worst["acc"][0] > worst["passes"][0] - 0.01, worst
+            assert worst["acc"][1] > worst["passes"][1] - 0.005, worst
+        for n in (a, b):  # an SGD step, so that step 2 starts from new weights on both
             n.store.set_hyper(0.05)
             n.store.sgd_step()
 

@@ -196,3 +196,42 @@ def test_single_rank_fused_update_matches_separate_sgd(B):
         assert torch.equal(g.store.wbf, h.store.wbf)
         assert torch.equal(g.store.lenet_frag[0], h.store.lenet_frag[0])
         assert torch.equal(idx_g, idx_h) and torch.equal(cur_g, cur_h)
+
+
+@pytest.mark.parametrize("B", [256, 4096])
+def test_reduce_successor_ownership_matches_tickets(monkeypatch, B):
+    """The reduce launch's successor ownership (each slot's 8 chunk partials handed to the next slot's
+    workgroups as {epoch, value} granules, csrc/lenet_fused.hip) sums in the same chunk order as the
+    ticket + slab path (lenet_succ=0): gradients, fused-update weights, momentum, compute copies and
+    fragments are bitwise equal over several steps, and no granule wait timed out."""
+    from distriflow_amd import ops
+    from distriflow_amd.data.synthetic import synthetic_mnist
+
+    g, _ = _nets(B)
+    h, _ = _nets(B)
+    h.store.set_flat(g.store.master.clone())
+    for s in (g.store, h.store):
+        s.set_hyper(0.05, momentum=0.9, weight_decay=1e-4, grad_scale=1.0, nesterov=False)
+    n = max(2048, 4 * B)
+    data, labels = synthetic_mnist(n, seed=6, device="cuda")
+    idx = torch.randperm(n, device="cuda")[:B].contiguous()
+    x = ops.GatherRef(data, idx, 1 / 255.0, (28, 28, 1))
+    y = ops.LabelRef(labels, idx)
+    for step in range(4):
+        fused = step >= 1  # a gradient-only step first, then fused-update steps
+        outs = []
+        for net, succ in ((g, "1"), (h, "0")):
+            monkeypatch.setenv("DISTRIFLOW_DIAG", f"lenet_succ={succ}")
+            st = net.compute_gradients_and_update(x, y) if fused else net.compute_gradients(x, y)
+            outs.append(st.clone())
+        monkeypatch.delenv("DISTRIFLOW_DIAG")
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1])
+        assert torch.equal(g.store.grad, h.store.grad), step
+        assert torch.equal(g.store.master, h.store.master), step
+        assert torch.equal(g.store.momentum, h.store.momentum)
+        assert torch.equal(g.store.wbf, h.store.wbf)
+        if fused:
+            assert torch.equal(g.store.lenet_frag[0], h.store.lenet_frag[0])
+    assert ops.lenet_red_error(g.lenet_dense_part) == 0
+    assert ops.lenet_red_error(h.lenet_dense_part) == 0
