@@ -44,6 +44,54 @@ __global__ __launch_bounds__(kPSBlock) void ps_fetch_pull_kernel(PSArgs a) {
   const int t = threadIdx.x, b = blockIdx.x, G = gridDim.x;
   __shared__ float* tab[kP2PMaxRanks];
   ps_stage_shards(a, tab);
+  // every workgroup: the fully applied count BEFORE its own slice copy (ps_device.h: vp = the minimum)
+  if (t == 0) ps_note_refresh(a, ps_read_applied(a));
+  // owner-applies: workgroup 0 takes the drain lock of every shard no other rank is draining (one CAS per
+  // shard) and decides, for each shard it holds, how many flagged sequence numbers (in order, from the
+  // first one not yet drained) this launch adds into it; the other workgroups take its decision.  Any
+  // stepping rank drains, so a rank that stops does not stall the others.
+  __shared__ unsigned s_P[kP2PMaxRanks], s_n[kP2PMaxRanks], s_pep;
+  if (a.owner_ring > 0 && t == 0) {
+    const unsigned R = (unsigned)a.owner_ring;
+    const unsigned pep = __hip_atomic_load(a.scratch + kPSPullEp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    s_pep = pep;
+    if (b == 0) {
+      for (int k = 0; k < a.nshards; ++k) {
+        unsigned P = 0, n = 0, free_ = 0;
+        if (__hip_atomic_compare_exchange_strong(a.dlock + k, &free_, (unsigned)a.rank + 1u, __ATOMIC_ACQUIRE,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          P = __hip_atomic_load(a.pref + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          const unsigned* fl = ps_inbox_flags(a, k);
+          while (n < R && __hip_atomic_load(const_cast<unsigned*>(fl) + (P + n) % R, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_SYSTEM) == P + n + 1u)
+            ++n;
+          if (n == 0) __hip_atomic_store(a.dlock + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        a.scratch[kPSDrainP + k] = P;
+        a.scratch[kPSDrainN + k] = n;
+        s_P[k] = P, s_n[k] = n;
+      }
+      __hip_atomic_store(a.scratch + kPSDrain, pep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const unsigned long long t0 = wall_clock64();
+      bool ok = true;
+      for (;;) {
+        if (__hip_atomic_load(a.scratch + kPSDrain, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pep) break;
+        if (wall_clock64() - t0 > 2ull * (unsigned long long)a.timeout_ticks) {
+          atomicOr(a.stats + 5, 32ull);
+          if (a.herr) __hip_atomic_store(a.herr, 32u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      for (int k = 0; k < a.nshards; ++k) {
+        s_P[k] = a.scratch[kPSDrainP + k];
+        s_n[k] = ok ? a.scratch[kPSDrainN + k] : 0u;  // (a timed-out workgroup only copies)
+      }
+    }
+  }
   if (b == 0) {
     // FCFS microbatch id (remote atomic on the server's cursor) + its example indices
     __shared__ long long s_bid;
@@ -57,11 +105,49 @@ __global__ __launch_bounds__(kPSBlock) void ps_fetch_pull_kernel(PSArgs a) {
     if (t == 0) *a.bid_out = s_bid;
     ps_stage_indices(a, s_bid, t, kPSBlock);
   }
-  // every workgroup: the fully applied count BEFORE its own slice copy (ps_device.h: vp = the minimum)
-  if (t == 0) ps_note_refresh(a, ps_read_applied(a));
   __syncthreads();
   const long long per = ((a.n + 4LL * G - 1) / (4LL * G)) * 4;  // slice length, multiple of 4
   const long long lo = b * per, hi = lo + per < a.n ? lo + per : a.n;
+  if (a.owner_ring > 0) {
+    // the shards this launch drains: add the flagged slots in sequence order (the lock holder is the
+    // shard's only writer), store them write-through for the peers' pulls; other shards: copy
+    const unsigned R = (unsigned)a.owner_ring;
+    const long long mask = (1LL << a.shard_shift) - 1;
+    for (long long i = lo + t; i < hi; i += kPSBlock) {
+      const int k = (int)(i >> a.shard_shift);
+      float* src = tab[k] + (i & mask);
+      float v = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(src), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_SYSTEM));
+      const unsigned nd = s_n[k];
+      if (nd > 0) {
+        const unsigned P = s_P[k];
+        for (unsigned j = 0; j < nd; ++j)
+          v += __uint_as_float(__hip_atomic_load(
+              reinterpret_cast<unsigned*>(a.inbox[k] + ((long long)((P + j) % R) << a.shard_shift) + (i & mask)),
+              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        __hip_atomic_store(reinterpret_cast<unsigned*>(src), __float_as_uint(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      a.w[i] = v;
+    }
+    // every shard store has landed before the drained counts are published and the locks released (a
+    // sender reuses a slot only once every shard has drained it: ring = max staleness + 2)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      const unsigned prev = __hip_atomic_fetch_add(a.scratch + kPSPullDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == (unsigned)G - 1) {
+        a.scratch[kPSPullDone] = 0;
+        for (int k = 0; k < a.nshards; ++k)
+          if (s_n[k] > 0) {
+            __hip_atomic_store(a.pref + k, s_P[k] + s_n[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.dlock + k, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        __hip_atomic_store(a.scratch + kPSPullEp, s_pep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    return;
+  }
   f32x4* d4 = reinterpret_cast<f32x4*>(a.w);
   for (long long base = (lo >> 2) + t; base < (hi >> 2); base += (long long)kPSBlock * kPSUnroll) {
     f32x4 v[kPSUnroll];
@@ -112,7 +198,30 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
     }
   }
   __syncthreads();
-  if (s_dec == kPSAccept) {
+  __shared__ unsigned s_q;
+  if (s_dec == kPSAccept && a.owner_ring > 0) {
+    // owner-applies: -lr * g into ring slot q % R of every owner's inbox (plain system-scope stores, no
+    // atomics); the last workgroup flags the slot at every owner once all of them have landed
+    if (t == 0) {
+      if (b != 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (kPSSeq is behind the decision)
+      s_q = a.scratch[kPSSeq];
+    }
+    __syncthreads();
+    const long long per = ((a.n + 4LL * G - 1) / (4LL * G)) * 4;
+    const long long lo = b * per, hi = lo + per < a.n ? lo + per : a.n;
+    const float lr = a.lr_dev ? *a.lr_dev : a.lr;
+    const long long soff = (long long)(s_q % (unsigned)a.owner_ring) << a.shard_shift;
+    const long long mask = (1LL << a.shard_shift) - 1;
+    for (long long i = lo + t; i < hi; i += kPSBlock) {
+      float d;
+      {
+#pragma clang fp contract(off)  // the same rounding as the CAS path
+        d = -(lr * a.g[i]);
+      }
+      __hip_atomic_store(reinterpret_cast<unsigned*>(a.inbox[i >> a.shard_shift] + soff + (i & mask)),
+                         __float_as_uint(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  } else if (s_dec == kPSAccept) {
     const long long per = ((a.n + 4LL * G - 1) / (4LL * G)) * 4;
     const long long lo = b * per, hi = lo + per < a.n ? lo + per : a.n;
     const float lr = a.lr_dev ? *a.lr_dev : a.lr;
@@ -142,6 +251,10 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
       a.scratch[kPSEpoch] += 1u;
       // every workgroup drained its adds before arriving: the gradient is now fully applied
       if (s_dec == kPSAccept) ps_publish_applied(a);
+      if (s_dec == kPSAccept && a.owner_ring > 0)  // every slot store has landed: flag it at every owner
+        for (int k = 0; k < a.nshards; ++k)
+          __hip_atomic_store(ps_inbox_flags(a, k) + s_q % (unsigned)a.owner_ring, s_q + 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -174,15 +287,29 @@ static bool ps_shards_ok(const PSArgs& a) {
   return true;
 }
 
+// owner-applies arguments: every owner's inbox, the drained counts, this rank, a ring of <= 255 slots (the
+// drain decision packs the count in 8 bits)
+static bool ps_owner_ok(const PSArgs& a) {
+  if (a.owner_ring <= 0) return true;
+  if (!a.pref || !a.dlock || a.rank < 0 || a.rank >= a.nshards || a.owner_ring > 255) return false;
+  for (int k = 0; k < a.nshards; ++k)
+    if (!a.inbox[k]) return false;
+  return true;
+}
+
 hipError_t ps_fetch_pull(const PSArgs& a, hipStream_t st) {
-  if (a.n <= 0 || (a.n & 3) || !ps_shards_ok(a) || (a.perm != nullptr && (a.B <= 0 || (a.B & 1) || a.nbatches <= 0)))
+  if (a.n <= 0 || (a.n & 3) || !ps_shards_ok(a) || !ps_owner_ok(a) ||
+      (a.perm != nullptr && (a.B <= 0 || (a.B & 1) || a.nbatches <= 0)))
     return hipErrorInvalidValue;
   ps_fetch_pull_kernel<<<ps_grid(a.n), kPSBlock, 0, st>>>(a);
   return hipGetLastError();
 }
 
 hipError_t ps_apply(const PSArgs& a, hipStream_t st) {
-  if (a.n <= 0 || (a.n & 3) || !ps_shards_ok(a)) return hipErrorInvalidValue;
+  if (a.n <= 0 || (a.n & 3) || !ps_shards_ok(a) || !ps_owner_ok(a)) return hipErrorInvalidValue;
+  // a slot is rewritten R sequence numbers later; every owner has drained it by then only if an admitted
+  // gradient is at most R - 2 behind (its pull saw min_k pref[k] >= q - max_stale)
+  if (a.owner_ring > 0 && (a.max_stale < 0 || a.owner_ring < a.max_stale + 2)) return hipErrorInvalidValue;
   ps_apply_kernel<<<ps_grid(a.n), kPSBlock, 0, st>>>(a);
   return hipGetLastError();
 }

@@ -1817,6 +1817,9 @@ class PSComm {
   }
   ~PSComm() {
     for (int k = 0; k < world_; ++k)
+      if (inbox_[k] && k != rank_) (void)hipIpcCloseMemHandle(inbox_[k]);
+    if (inbox_own_) (void)hipFree(inbox_own_);
+    for (int k = 0; k < world_; ++k)
       if (fed_slot_[k] && k != rank_) (void)hipIpcCloseMemHandle(fed_slot_[k]);
     if (fed_own_) (void)hipFree(fed_own_);
     if (shared_ && rank_ != server_) (void)hipIpcCloseMemHandle(shared_);
@@ -2031,6 +2034,32 @@ class PSComm {
     return torch::from_blob(shared_ + 80, {1}, torch::TensorOptions().dtype(torch::kInt).device(torch::kCUDA, dev_));
   }
 
+  // ---- owner-applies (csrc/async_ps.hip): an inbox of `ring` slots of this rank's shard length (+ ring
+  // flags) on every rank; call owner_init on every rank, exchange the handles, then owner_open
+  py::bytes owner_init(int64_t ring) {
+    TORCH_CHECK(ring >= 2 && ring <= 255, "ps owner-applies: ring must be 2..255");
+    TORCH_CHECK(inbox_own_ == nullptr, "ps owner-applies: already initialised");
+    owner_ring_ = (int)ring;
+    inbox_own_ = (float*)alloc_uncached((size_t)ring * ((size_t)1 << shift_) * 4 + (size_t)ring * 4 + 256,
+                                        "ps owner inbox");
+    return export_handle(inbox_own_);
+  }
+  void owner_open(std::vector<std::string> handles) {
+    TORCH_CHECK(inbox_own_ != nullptr && (int)handles.size() == world_, "ps owner-applies: owner_init first");
+    for (int k = 0; k < world_; ++k) inbox_[k] = k == rank_ ? inbox_own_ : (float*)open_handle(handles[k]);
+    owner_on_ = true;
+  }
+  bool owner_applies() const { return owner_on_; }
+  // the owner's drain alone (a pull into `w` without a microbatch claim): adds every flagged slot of this
+  // rank's inbox into its shard; after the last step of every rank, one drain per rank settles the master
+  void drain(torch::Tensor w) { fetch_pull(w, c10::nullopt, c10::nullopt); }
+  // [drained sequence count of every owner]
+  std::vector<int64_t> owner_prefix() const {
+    std::vector<unsigned> v(world_, 0);
+    check_hip(hipMemcpy(v.data(), shared_ + 192, (size_t)world_ * 4, hipMemcpyDeviceToHost), "ps pref");
+    return std::vector<int64_t>(v.begin(), v.end());
+  }
+
   // launch arguments of the fused LeNet-5 reduce in parameter-server mode (lenet_train_py)
   dfa::PSArgs lenet_args(const torch::Tensor& perm, const torch::Tensor& idx, double lr, int64_t max_stale) const {
     dfa::PSArgs a = args();
@@ -2116,6 +2145,13 @@ class PSComm {
     a.max_stale = -1;
     a.lr_dev = lr_dev_;
     a.herr = reinterpret_cast<unsigned*>(herr_.device());
+    a.rank = rank_;
+    if (owner_on_) {
+      a.owner_ring = owner_ring_;
+      a.pref = reinterpret_cast<unsigned*>(shared_ + 192);   // control words 48..55 (async_ps.hip layout)
+      a.dlock = reinterpret_cast<unsigned*>(shared_ + 224);  // control words 56..63
+      for (int k = 0; k < world_; ++k) a.inbox[k] = inbox_[k];
+    }
     if (nbatches_ > 0) {
       a.sched = reinterpret_cast<unsigned*>(shared_ + 32);
       a.sched_ctr = reinterpret_cast<unsigned long long*>(shared_ + 48);
@@ -2139,6 +2175,10 @@ class PSComm {
   unsigned* audit_ = nullptr;
   int64_t audit_cap_ = 0;
   torch::Tensor audit_keep_;
+  int owner_ring_ = 0;
+  bool owner_on_ = false;
+  float* inbox_own_ = nullptr;
+  float* inbox_[dfa::kP2PMaxRanks] = {};
   int fed_K_ = 0;
   float* fed_own_ = nullptr;
   float* fed_slot_[dfa::kP2PMaxRanks] = {};
@@ -2348,6 +2388,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lenet_blocks", [](int64_t B) { return dfa::lenet_blocks((int)B); });
   m.def("lenet_frag_bytes", []() { return (int64_t)dfa::lenet_frag_bytes(); });
   m.def("lenet_dense_part_floats", [](int64_t B) { return (int64_t)dfa::lenet_dense_part_floats((int)B); });
+  m.def("lenet_red_err_offset", []() { return (int64_t)dfa::lenet_red_err_offset(); });
   m.def("gather_labels", &gather_labels_py);
   py::class_<P2PComm>(m, "P2PComm", "one-shot xGMI all-reduce over IPC-mapped peer buffers")
       .def(py::init<int64_t, int64_t, int64_t, double, int64_t>(), py::arg("rank"), py::arg("world"),
@@ -2383,6 +2424,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("copy_master", &PSComm::copy_master)
       .def("stats_tensor", &PSComm::stats_tensor)
       .def("set_audit", &PSComm::set_audit, py::arg("rows"))
+      .def("owner_init", &PSComm::owner_init, py::arg("ring"))
+      .def("owner_open", &PSComm::owner_open)
+      .def("owner_applies", &PSComm::owner_applies)
+      .def("drain", &PSComm::drain)
+      .def("owner_prefix", &PSComm::owner_prefix)
       .def("fed_init", &PSComm::fed_init, py::arg("K"))
       .def("fed_open", &PSComm::fed_open, py::arg("handles"))
       .def("fed_pull", &PSComm::fed_pull)

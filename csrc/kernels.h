@@ -413,6 +413,14 @@ struct PSArgs {
   long long nbatches, timeout_ticks;
   int B, max_stale, max_epochs;  // max_epochs 0 = unbounded
   float lr;
+  // owner-applies (owner_ring > 0; csrc/async_ps.hip): no per-element remote atomics.  An admitted gradient
+  // of sequence number q is written (plain system-scope stores) into ring slot q % owner_ring of every
+  // shard's inbox, then flagged there; a pull that takes a shard's drain lock adds its flagged slots into
+  // the shard in sequence order and publishes how many are drained (pref[k]).  "Fully applied" = min pref.
+  float* inbox[kP2PMaxRanks];   // owner k's inbox: owner_ring slots of its shard length, then owner_ring flags
+  unsigned* pref;               // shared [nshards] drained-sequence counts
+  unsigned* dlock;              // shared [nshards] drain locks (0 free, rank + 1 held): any pulling rank drains
+  int owner_ring, rank;
 };
 constexpr int kPSMaxGrid = 64;
 
@@ -548,6 +556,7 @@ struct LeNetRedArgs {
   unsigned long long* gran;  // [slots][8 chunks][1024]
   unsigned* gran_ep;         // [grid] per-workgroup launch counters (each workgroup reads / bumps its own)
   unsigned* gran_err;        // sticky: a granule wait timed out
+  unsigned* slot_arr;        // [slots] async PS: owners of a slot done (the eighth arrives for the slot)
 };
 // The reference CNN's conv block (csrc/kcnn_fused.hip): conv1 3x3x1->32 + ReLU, conv2 3x3x32->32 + ReLU,
 // 2x2 max-pool [+ folded dropout], input 28x28x1, in one forward and one backward launch (+ reduce).
@@ -627,6 +636,7 @@ bool khead_supported(int K, int C);
 hipError_t khead_train(KHeadArgs a, hipStream_t st);
 int lenet_dense_part_floats(int B);  // reduce scratch: job slabs, arrival tickets, granules, launch counters
 void lenet_red_bind_scratch(float* dense_part, LeNetRedArgs& r);  // points r's scratch fields into it
+int lenet_red_err_offset();  // float offset of the granule error word in that scratch
 size_t lenet_train_lds();
 int lenet_blocks(int B);
 hipError_t lenet_train(const LeNetArgs& a, LeNetRedArgs r, hipStream_t st);

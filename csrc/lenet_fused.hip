@@ -1194,14 +1194,20 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       // publish before they wait, so in-order dispatch needs no co-residency.
       const int grp = blockIdx.x / kChunks, c = blockIdx.x - kChunks * grp;
       __shared__ unsigned s_ge, s_pe;
-      if (threadIdx.x == 0) s_ge = a.gran_ep[blockIdx.x] + 1u;
-      __syncthreads();
-      const unsigned ge = s_ge;
+      // this launch's epoch: the counter load goes out now and is waited for only after the job (a wait
+      // here put a whole memory round trip in front of every job)
+      const unsigned ge_prev = threadIdx.x == 0 ? a.gran_ep[blockIdx.x] : 0u;
+      __syncthreads();  // the tables staged above are read by every thread of the job
+      float part[kPerThread];
       if (grp < nslot) {
-        float part[kPerThread];
         if (grp < a.dense_tiles) dense_job(a, tabs, grp, c, red, part);
         else conv_job(a, grp - a.dense_tiles, c, red, part);
         LR_STAMP(6);
+      }
+      if (threadIdx.x == 0) s_ge = ge_prev + 1u;
+      __syncthreads();
+      const unsigned ge = s_ge;
+      if (grp < nslot) {
         const int npos = grp < a.dense_tiles ? kPerThread : 1;
         unsigned long long* g = a.gran + ((long long)grp * kChunks + c) * kSlotVals + threadIdx.x;
 #pragma unroll
@@ -1304,8 +1310,23 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       }
       LR_STAMP(3);
       if (PS) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's shard adds have landed
-        lenet_ps_arrive(a, s >= 0 ? 1u : 0u, (unsigned)(nslot * kChunks + 1));
+        // this workgroup's shard adds have landed; the slot's last owner of its 8 arrives for the slot (one
+        // counter per slot, then nslot + 1 arrivals on the launch's: a flat fan-in of 8 x nslot owners on
+        // one word was the launch's tail)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        __shared__ unsigned s_arr;
+        if (threadIdx.x == 0) {
+          unsigned n = 0;
+          if (s >= 0 && __hip_atomic_fetch_add(a.slot_arr + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                            (unsigned)(kChunks - 1)) {
+            __hip_atomic_store(a.slot_arr + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            n = 1;
+          }
+          s_arr = n;
+        }
+        __syncthreads();
+        lenet_ps_arrive(a, s_arr, (unsigned)(nslot + 1));
       }
       if (threadIdx.x == 0) a.gran_ep[blockIdx.x] = ge;
       LR_STAMP(4);
@@ -1517,7 +1538,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     if (threadIdx.x == 0) *a.ps.bid_out = s_bid;
     ps_stage_indices(a.ps, s_bid, threadIdx.x, RT);
     LR_STAMP(10);
-    lenet_ps_arrive(a, 1u, (unsigned)((a.succ ? nslot * kChunks : nslot) + 1));
+    lenet_ps_arrive(a, 1u, (unsigned)(nslot + 1));
     LR_STAMP(1);
     LR_FLUSH();
     return;
@@ -1589,12 +1610,15 @@ static int lenet_red_slots() {
   return n;
 }
 // [slabs: slots x 8 x 1024 f32][tickets: round4(slots)][granules: slots x 8 x 1024 u64][per-workgroup
-// launch counters: round4(8 x (slots + 1))][granule error word, padded to 4]
+// launch counters: round4(8 x (slots + 1))][granule error word, padded to 4][slot arrivals: round4(slots)]
 static int lenet_red_slab_floats() { return lenet_red_slots() * kChunks * kSlotVals; }
 static int lenet_red_ep_words() { return (kChunks * (lenet_red_slots() + 1) + 3) / 4 * 4; }
 int lenet_dense_part_floats(int B) {
   (void)B;
-  return 3 * lenet_red_slab_floats() + (lenet_red_slots() + 3) / 4 * 4 + lenet_red_ep_words() + 4;
+  return 3 * lenet_red_slab_floats() + 2 * ((lenet_red_slots() + 3) / 4 * 4) + lenet_red_ep_words() + 4;
+}
+int lenet_red_err_offset() {
+  return 3 * lenet_red_slab_floats() + (lenet_red_slots() + 3) / 4 * 4 + lenet_red_ep_words();
 }
 void lenet_red_bind_scratch(float* base, LeNetRedArgs& r) {
   r.slabs = base;
@@ -1606,6 +1630,8 @@ void lenet_red_bind_scratch(float* base, LeNetRedArgs& r) {
   r.gran_ep = reinterpret_cast<unsigned*>(base);
   base += lenet_red_ep_words();
   r.gran_err = reinterpret_cast<unsigned*>(base);
+  base += 4;
+  r.slot_arr = reinterpret_cast<unsigned*>(base);
 }
 
 hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
@@ -1660,10 +1686,8 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   const int njobs = nslot * kChunks;
   // successor ownership needs one job per workgroup (not the time-shared grid of several ranks on one
   // GPU) and, multi-rank, the per-part LL epoch words
-  // Async PS keeps the tickets: 8x the owners made the apply-done fan-in (one counter) the launch's tail
-  // (0.0862 vs 0.0799 ms per async step at B = 4096)
-  if (r.succ && (r.ps_on || !(r.exch_blocks <= 0 || r.exch_blocks >= njobs) || !r.gran || !r.gran_ep || !r.gran_err ||
-                 nslot > lenet_red_slots() || (r.ll_on && !r.ll.part_epochs)))
+  if (r.succ && (!(r.exch_blocks <= 0 || r.exch_blocks >= njobs) || !r.gran || !r.gran_ep || !r.gran_err ||
+                 !r.slot_arr || nslot > lenet_red_slots() || (r.ll_on && !r.ll.part_epochs)))
     r.succ = 0;
   if (r.succ) r.exch_blocks = njobs + kChunks;  // + the owner-only group of the last slot
   else if (r.exch_blocks <= 0 || r.exch_blocks > njobs) r.exch_blocks = njobs;
@@ -1688,6 +1712,7 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
       return hipErrorInvalidValue;
     for (int k = 0; k < r.ps.nshards; ++k)
       if (!r.ps.shard[k]) return hipErrorInvalidValue;
+    if (r.ps.owner_ring > 0) return hipErrorInvalidValue;  // owner-applies runs the generic pull / apply
   }
   const int extra = ((r.sgd_on && r.sgd.src) || r.ps_on) ? 1 : 0;  // the index-staging workgroup
   const dim3 grid(r.exch_blocks + 1 + extra);

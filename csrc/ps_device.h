@@ -32,6 +32,9 @@ namespace dfa {
 // kPSVMin: min over this step's refreshing workgroups of (applied read before the copy [+ 1 for its own
 // admitted add]); reset to kPSNoVer by the admission that consumes it
 constexpr int kPSPullDone = 0, kPSApplyDone = 1, kPSEpoch = 2, kPSDecision = 3, kPSVMin = kPSVMinWord, kPSSlots = 64;
+// owner-applies words: the admitted sequence number, the pull launches' epoch, the drain decision's epoch
+// and, per shard, the first sequence number and the count this launch drains
+constexpr int kPSSeq = 5, kPSPullEp = 6, kPSDrain = 7, kPSDrainP = 8, kPSDrainN = 16;  // (+ shard, < 8 each)
 constexpr unsigned kPSNoVer = 0xffffffffu;
 // the decision word is (launch epoch << 3) | code: compare epochs modulo 2^29
 __device__ __forceinline__ bool ps_epoch_eq(unsigned word, unsigned ep) { return (word >> 3) == (ep & 0x1fffffffu); }
@@ -47,7 +50,19 @@ __device__ __forceinline__ unsigned ps_ld_acq(const unsigned* p) {
 // BEFORE any of its shard reads or adds (reading it earlier only makes the count more conservative, so the
 // fused reduce launch reads it at its start, where the load's latency hides behind the jobs).
 __device__ __forceinline__ unsigned ps_read_applied(const PSArgs& a) {
+  if (a.owner_ring > 0) {  // owner-applies: every owner has drained at least the minimum
+    unsigned m = 0xffffffffu;
+    for (int k = 0; k < a.nshards; ++k) {
+      const unsigned p = __hip_atomic_load(a.pref + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      m = p < m ? p : m;
+    }
+    return m;
+  }
   return a.applied ? __hip_atomic_load(a.applied, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+}
+// owner k's inbox flags (after its owner_ring slots)
+__device__ __forceinline__ unsigned* ps_inbox_flags(const PSArgs& a, int k) {
+  return reinterpret_cast<unsigned*>(a.inbox[k] + ((long long)a.owner_ring << a.shard_shift));
 }
 // Records that this workgroup's refresh contains `count` fully applied gradients (the applied count it read
 // + 1 when the refresh values are the results of this rank's own admitted adds): kPSVMin = the minimum.
@@ -61,6 +76,7 @@ __device__ __forceinline__ void ps_note_refresh(const PSArgs& a, unsigned count)
 // the shards are uncached memory, so nothing remains to be written back: a relaxed add orders behind them
 // (a system-scope release here would write back this XCD's L2, ~2-7 us on the critical path).
 __device__ __forceinline__ void ps_publish_applied(const PSArgs& a) {
+  if (a.owner_ring > 0) return;  // owner-applies: the owners' drains publish (pref)
   if (a.applied != nullptr) __hip_atomic_fetch_add(a.applied, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -185,6 +201,7 @@ __device__ inline unsigned ps_admit(const PSArgs& a) {
     unsigned expected = v;
     if (__hip_atomic_compare_exchange_strong(a.ver, &expected, v + 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_SYSTEM)) {
+      a.scratch[kPSSeq] = v;  // this gradient's sequence number (owner-applies: its ring slot)
       a.stats[0] += 1;
       a.stats[2] += stale;
       if (stale > a.stats[3]) a.stats[3] = stale;

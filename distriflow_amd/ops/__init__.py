@@ -912,7 +912,8 @@ def lenet_train(x, labels, conv, dense_w, dense_wt, dense_b, conv_grads, dense_g
 
 def lenet_red_error(dense_part) -> int:
     """Sticky error word of the LeNet-5 reduce launch's granule hand-off (non-zero: a wait timed out)."""
-    return int(dense_part[-4:].view(torch.int32)[0].item())
+    o = int(_C().lenet_red_err_offset())  # (layout: csrc/lenet_fused.hip lenet_red_bind_scratch)
+    return int(dense_part[o:o + 1].view(torch.int32)[0].item())
 
 
 def convpool_supported(H, W, C, KH, KW, pad, N) -> bool:

@@ -55,7 +55,7 @@ class AsyncPSTrainer(DataParallelTrainer):
     SUPPORTS_MULTISTEP = True  # the whole PS protocol of a step is device work: steps unroll like sync ones
 
     def __init__(self, net, lr: float = 0.001, max_staleness: int = 4, group=None, server_rank: int = 0,
-                 graph: str = "full", timeout_s: float = 30.0):
+                 graph: str = "full", timeout_s: float = 30.0, owner_apply: Optional[bool] = None):
         if not net.is_gpu:
             raise RuntimeError("AsyncPSTrainer is the GPU path; use AsynchronousSGDServer/Client on CPU")
         super().__init__(net, lr=lr, group=group, overlap=False, graph="full" if graph == "split" else graph,
@@ -95,12 +95,34 @@ class AsyncPSTrainer(DataParallelTrainer):
         if not self.ps.selftest_check():
             err = RuntimeError("shard add self-test mismatch")
         self._agree(err, "shard self-test check")
+        # owner-applies (csrc/async_ps.hip; diag switch ps_owner_apply): admitted gradients go into the
+        # owners' inbox rings with plain stores, each owner adds them into its own shard during its next pull
+        # -- no remote atomics.  The ring holds max_staleness + 2 gradients (no slot is rewritten before
+        # every owner drained it); a bounded staleness is required.
+        self.owner_apply = diag_on("ps_owner_apply") if owner_apply is None else bool(owner_apply)
+        if self.owner_apply:
+            if self.max_staleness < 0:
+                raise ValueError("owner-applies needs a bounded max_staleness")
+            oh = b""
+            try:
+                oh = self.ps.owner_init(self.max_staleness + 2)
+            except Exception as e:
+                err = e
+            self._agree(err, "owner inbox allocation")
+            ohs = [oh] * self.world
+            if self.world > 1:
+                dist.all_gather_object(ohs, oh, group=group)
+            try:
+                self.ps.owner_open(ohs)
+            except Exception as e:
+                err = e
+            self._agree(err, "owner inbox open")
         self._perm = None
         # fused LeNet-5: the reduce launch is the parameter server's apply (2 launches per step)
         import os
 
         self.fused_ps = (bool(getattr(net, "lenet_fused", False)) and net.store.lenet_frag is not None
-                         and diag_on("async_fused"))
+                         and diag_on("async_fused") and not self.owner_apply)
         # a warm-up step would claim a microbatch and apply a real gradient to the shared master: the
         # capture warms up with a compute-only step instead (_capture).  The reduce launch's owners wait for
         # the staging workgroup's admission decision (no lock is taken), then add or read their slots.
@@ -247,7 +269,8 @@ class AsyncPSTrainer(DataParallelTrainer):
         epoch, in_epoch, completed, redisp, skipped, dups, fin = self.ps.schedule_stats()
         return {"accepted": acc, "rejected": rej, "mean_staleness": ssum / acc if acc else 0.0,
                 "max_staleness": smax, "admit_retries": retries, "error": err, "version": version,
-                "applied": applied,
+                "applied": min(self.ps.owner_prefix()) if self.owner_apply else applied,
+                "apply_path": "owner-applies" if self.owner_apply else "cas",
                 "cursor": cursor, "noop_steps": noops, "epoch": epoch, "completed_in_epoch": in_epoch,
                 "completed": completed, "redispatched": redisp, "skipped": skipped, "duplicates": dups,
                 "finished": bool(fin)}
@@ -264,6 +287,15 @@ class AsyncPSTrainer(DataParallelTrainer):
         err = self.ps.stats()[5]
         if err:
             raise RuntimeError(f"async PS: device wait timed out (error bits {err:#x})")
+
+    def drain(self):
+        """Owner-applies: add every gradient already flagged in this rank's inbox into its shard (the next
+        pull would).  After every rank's last step, one drain on every rank (between two barriers) leaves
+        the sharded master = w0 - lr * sum of the admitted gradients.  No-op on the CAS path."""
+        if self.owner_apply:
+            if not hasattr(self, "_drain_buf"):
+                self._drain_buf = torch.empty_like(self.net.store.master)
+            self.ps.drain(self._drain_buf)
 
     def pull_master(self, dst: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Gather the sharded master into ``dst`` (default: this rank's store, compute copies refreshed)."""

@@ -4,7 +4,8 @@ Reference FederatedServer (/root/reference/src/server/federated_server.ts:73-90)
 version are counted, stale ones dropped; after minUpdatesPerVersion of them the mean is applied and the
 version bumped -- the barrier counts updates, not workers, so a slow or lost worker never blocks a
 version.  Four processes share the box's GPU (gloo control plane; IPC-mapped shards and slots as on an
-8-GPU node): rank 3 is slowed down every step and rank 2 stops after three steps."""
+8-GPU node): rank 3 uploads its first gradients only after the others moved the version past the one it
+pulled (they must be dropped as stale), and rank 2 stops after three steps."""
 import os
 import tempfile
 import time
@@ -45,9 +46,18 @@ def _worker(rank, world, port, out_dir, K, steps, slow, dead, dead_after):
     dist.barrier()
     n = dead_after if rank == dead else steps
     for k in range(n):
-        if rank == slow:  # a straggler: its uploads reach the server late
+        if rank == slow and k < 4:
+            # a straggler: it pulls, then computes and uploads only after the others moved the version on
+            # (its first steps, while they are still running), so that upload is of a stale version
+            tr.idx.copy_(rows[k].to(dev))
+            tr._gather()
             torch.cuda.synchronize()
-            time.sleep(0.03)
+            v0, t0 = tr.version(), time.time()
+            while tr.version() == v0 and time.time() - t0 < 5.0:
+                time.sleep(0.002)
+            tr._step_body(tr.xb, tr.yb)
+            torch.cuda.synchronize()
+            continue
         tr.step_indices(rows[k].to(dev))
     torch.cuda.synchronize()
     tr.flush_callbacks()
