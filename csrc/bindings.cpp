@@ -1805,8 +1805,8 @@ class PSComm {
     // shard length: the smallest power of two >= 64 with world shards covering n
     shift_ = 6;
     while (((n_ - 1) >> shift_) >= world_) ++shift_;
-    if (rank_ == server_) shared_ = alloc_uncached(256 + 2 * (size_t)dfa::kPSMaxBatches * 4, "ps control");
-    own_ = (float*)alloc_uncached(((size_t)1 << shift_) * 4 + kTestWords * 4, "ps shard");
+    if (rank_ == server_) shared_ = alloc_shared(256 + 2 * (size_t)dfa::kPSMaxBatches * 4, "ps control");
+    own_ = (float*)alloc_shared(((size_t)1 << shift_) * 4 + kTestWords * 4, "ps shard");
     check_hip(hipMalloc((void**)&local_, 4096), "ps local alloc");
     check_hip(hipMemset(local_, 0, 4096), "ps local memset");
     // kPSVMin (csrc/ps_device.h): no refresh recorded yet
@@ -1957,7 +1957,7 @@ class PSComm {
     TORCH_CHECK(K >= 1 && K <= dfa::kFedMaxK, "fedsgd: K must be 1..", dfa::kFedMaxK);
     TORCH_CHECK(fed_own_ == nullptr, "fedsgd: already initialised");
     fed_K_ = (int)K;
-    fed_own_ = (float*)alloc_uncached((size_t)K * ((size_t)1 << shift_) * 4, "fedsgd slots");
+    fed_own_ = (float*)alloc_shared((size_t)K * ((size_t)1 << shift_) * 4, "fedsgd slots");
     for (auto& p : fed_slot_) p = nullptr;
     check_hip(hipMemset(local_ + 2560, 0, 1536), "fedsgd local");
     check_hip(hipDeviceSynchronize(), "fedsgd init sync");
@@ -2040,7 +2040,7 @@ class PSComm {
     TORCH_CHECK(ring >= 2 && ring <= 255, "ps owner-applies: ring must be 2..255");
     TORCH_CHECK(inbox_own_ == nullptr, "ps owner-applies: already initialised");
     owner_ring_ = (int)ring;
-    inbox_own_ = (float*)alloc_uncached((size_t)ring * ((size_t)1 << shift_) * 4 + (size_t)ring * 4 + 256,
+    inbox_own_ = (float*)alloc_shared((size_t)ring * ((size_t)1 << shift_) * 4 + (size_t)ring * 4 + 256,
                                         "ps owner inbox");
     return export_handle(inbox_own_);
   }
@@ -2101,6 +2101,17 @@ class PSComm {
   }
 
  private:
+  // Memory other processes map (world > 1): uncached, so every rank's access sees the others' without L2
+  // maintenance.  One rank alone shares it with nobody: plain (cached) device memory, whose accesses do not
+  // pay the uncached operation rate (~6 k per us chip-wide, profiles/r5/ps_cas_adds_per_us_1gpu.jsonl);
+  // IPC export works on either.
+  char* alloc_shared(size_t bytes, const char* what) const {
+    if (world_ > 1) return alloc_uncached(bytes, what);
+    void* p = nullptr;
+    check_hip(hipMalloc(&p, bytes), what);
+    check_hip(hipMemset(p, 0, bytes), what);
+    return (char*)p;
+  }
   static char* alloc_uncached(size_t bytes, const char* what) {
     void* p = nullptr;
     hipError_t e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);

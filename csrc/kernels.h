@@ -484,6 +484,10 @@ struct LeNetArgs {
   unsigned long long* stamps; // diagnostic phase clocks [grid][16] (lenet_set_stamps), or null
   int B, ldt;
   float grad_scale;
+  // async PS: one extra workgroup (index nblk) admits this step's gradient while the others train, so the
+  // reduce launch's owners find the decision already published (csrc/lenet_fused.hip)
+  int nblk, ps_admit;
+  PSArgs ps;
 };
 struct LeNetDense {
   const bf16* dzT;

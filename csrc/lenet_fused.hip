@@ -293,7 +293,27 @@ __device__ __forceinline__ int lenet_img_group(int b, int nb) {
   return (b & 7) * per + (b >> 3);
 }
 
+// async PS admission of this step's gradient (the extra workgroup of the train launch, see lenet_train):
+// lock-free CAS on the shared version, decision published for the reduce launch's owners (epoch-tagged
+// with that launch's epoch, which no one advances before it runs), the refresh minimum recorded, then the
+// microbatch's completion
+__device__ __forceinline__ void lenet_ps_admission(const PSArgs& p) {
+  const long long bid = *p.bid_out;  // (the reduce launch's claim workgroup overwrites it after the decision)
+  const unsigned applied0 = ps_read_applied(p);
+  const unsigned ep = __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const unsigned dec = ps_admit(p, false);  // (consumes the previous launch's record first)
+  // the owners refresh (add to or read the shards) only after this decision, so every one of their
+  // refreshes contains at least applied0 fully applied gradients (+ this one when admitted)
+  if (dec == kPSAccept || dec == kPSReject) ps_note_refresh(p, applied0 + (dec == kPSAccept ? 1u : 0u));
+  __hip_atomic_store(p.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (dec == kPSAccept && p.done_epoch != nullptr) complete_microbatch(p, bid);
+}
+
 __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs a) {
+  if ((int)blockIdx.x >= a.nblk) {  // async PS: the admission workgroup
+    if (a.ps_admit && threadIdx.x == 0) lenet_ps_admission(a.ps);
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* Xs = reinterpret_cast<bf16*>(smem + OFF_XS);
   bf16* Xs1 = reinterpret_cast<bf16*>(smem + OFF_XS1);
@@ -319,9 +339,8 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   // treated as divergent: exec-mask branches, each waiting for all LDS reads in flight)
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), i = lane & 15,
             g = lane >> 4;
-  const int r0 = lenet_img_group(blockIdx.x, gridDim.x) * IMG;
+  const int r0 = lenet_img_group(blockIdx.x, a.nblk) * IMG;
   const int rows = min(IMG, a.B - r0);
-  const long long nb = gridDim.x;
   const bf16x8* __restrict__ frag = reinterpret_cast<const bf16x8*>(a.frag);
   float* part = a.conv_part + (long long)blockIdx.x * kLeNetConvStride;  // this workgroup's partials
   unsigned long long* const stamps = a.stamps;
@@ -1085,7 +1104,7 @@ __device__ __forceinline__ void red_apply(const LeNetRedArgs& a, const RedTables
 // The slot owners wait for it only after their jobs (so it is normally already there), then add
 // -lr * g to their elements of the sharded master and refresh the local copies from the values the adds
 // produced.  No lock is held: the owners of different ranks update the shards in parallel.
-__device__ __forceinline__ unsigned lenet_ps_wait(const LeNetRedArgs& a, unsigned* s_dec, unsigned applied0) {
+__device__ __forceinline__ unsigned lenet_ps_wait(const LeNetRedArgs& a, unsigned* s_dec) {
   const PSArgs& p = a.ps;
   if (threadIdx.x == 0) {
     const unsigned ep = __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
@@ -1096,9 +1115,6 @@ __device__ __forceinline__ unsigned lenet_ps_wait(const LeNetRedArgs& a, unsigne
       if (ps_epoch_eq(w, ep)) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         dec = w & 7u;
-        // the refresh below (adds or reads of the shards) contains every gradient fully applied when this
-        // launch started (+ this one when admitted)
-        if (dec == kPSAccept || dec == kPSReject) ps_note_refresh(p, applied0 + (dec == kPSAccept ? 1u : 0u));
         break;
       }
       if (wall_clock64() - t0 > 2ull * (unsigned long long)p.timeout_ticks) {
@@ -1177,8 +1193,6 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
   const int G = a.exch_blocks;
   if ((int)blockIdx.x < G) {
     // async PS: the fully applied count before any shard access of this launch (ps_device.h)
-    unsigned applied0 = 0;
-    if (PS && threadIdx.x == 0) applied0 = ps_read_applied(a.ps);
     if (PS) ps_stage_shards(a.ps, s_shard);
     stage_tables(a, &tabs);
     // with the fused sync update, the first owned slot's master / momentum elements are loaded beside
@@ -1231,6 +1245,24 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
           w0 = a.sgd.master[off];
           m0 = a.sgd.mom != nullptr ? a.sgd.mom[off] : 0.f;
         }
+        // async PS: the shard is updated in groups of 4 consecutive positions per thread (uncached shard
+        // memory at world > 1 takes ~6 k operations per us chip-wide, profiles/r5: a contiguous aligned group
+        // of the exclusive writer is ONE 16-byte load and store); the group's addresses and current values
+        // load here, beside the granule wait
+        float* pg[4] = {nullptr, nullptr, nullptr, nullptr};
+        f32x4 curv = {0.f, 0.f, 0.f, 0.f};
+        bool vec = false;
+        const bool grp4 = PS && (int)threadIdx.x * 4 < cnt;
+        if (grp4) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const Owned oj = owned_elem(a, tabs, s, c * cnt + 4 * (int)threadIdx.x + j);
+            pg[j] = oj.di >= 0 ? ps_elem(s_shard, a.ps.shard_shift, tabs.d[oj.di].off + oj.i) : nullptr;
+          }
+          vec = a.ps.excl != 0 && pg[0] != nullptr && pg[1] == pg[0] + 1 && pg[2] == pg[0] + 2 && pg[3] == pg[0] + 3 &&
+                (reinterpret_cast<uintptr_t>(pg[0]) & 15) == 0;
+          if (vec) curv = *reinterpret_cast<const f32x4*>(pg[0]);
+        }
         if (mine) {
           const unsigned long long* g = a.gran + (long long)s * kChunks * kSlotVals + pos;
           const unsigned long long t0 = wall_clock64();
@@ -1261,27 +1293,42 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
         LR_STAMP(7);
         if (!PS) LR_STAMP(2);
         if (PS) {
-          const unsigned dec = lenet_ps_wait(a, &s_dec, applied0);
+          float* vb = red;        // [cnt] local sums (the jobs are done with red)
+          float* wb = red + 128;  // [cnt] the shard values after this step
+          if (mine) vb[threadIdx.x] = v;
+          const unsigned dec = lenet_ps_wait(a, &s_dec);  // (its barrier also publishes vb)
           LR_STAMP(2);
           if (dec == kPSAccept || dec == kPSReject) {
             const PSArgs& p = a.ps;
-            float* pe[1] = {o.di >= 0 ? ps_elem(s_shard, p.shard_shift, tabs.d[o.di].off + o.i) : nullptr};
-            float d[1], wn[1];
-            {
+            if (grp4) {
+              const int q0 = 4 * (int)threadIdx.x;
+              float d[4], wn[4];
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
 #pragma clang fp contract(off)
-              d[0] = -(tabs.hyper[0] * v);
+                d[j] = -(tabs.hyper[0] * vb[q0 + j]);
+              }
+              if (vec) {  // exclusive writer: the values loaded above are the shard's current ones
+#pragma unroll
+                for (int j = 0; j < 4; ++j) wn[j] = dec == kPSAccept ? curv[j] + d[j] : curv[j];
+                if (dec == kPSAccept) *reinterpret_cast<f32x4*>(pg[0]) = f32x4{wn[0], wn[1], wn[2], wn[3]};
+              } else if (dec == kPSAccept) {
+                ps_add<4>(pg, d, wn, p.excl != 0, p);
+              } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                  wn[j] = pg[j] ? __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(pg[j]), __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_SYSTEM))
+                                : 0.f;
+              }
+#pragma unroll
+              for (int j = 0; j < 4; ++j) wb[q0 + j] = wn[j];
             }
-            if (dec == kPSAccept) {
-              ps_add<1>(pe, d, wn, p.excl != 0, p);
-            } else {
-              wn[0] = pe[0] ? __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(pe[0]), __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_SYSTEM))
-                            : 0.f;
-            }
+            __syncthreads();
             if (o.di >= 0) {
               tabs.g[o.di][o.i] = v;
-              if (dense) red_emit<true>(a, tabs, o, wn[0]);
-              else red_emit<false>(a, tabs, o, wn[0]);
+              if (dense) red_emit<true>(a, tabs, o, wb[threadIdx.x]);
+              else red_emit<false>(a, tabs, o, wb[threadIdx.x]);
             }
           }
           LR_STAMP(5);
@@ -1311,7 +1358,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       LR_STAMP(3);
       if (PS) {
         // this workgroup's shard adds have landed; the slot's last owner of its 8 arrives for the slot (one
-        // counter per slot, then nslot + 1 arrivals on the launch's: a flat fan-in of 8 x nslot owners on
+        // counter per slot, then nslot + 2 arrivals on the launch's: a flat fan-in of 8 x nslot owners on
         // one word was the launch's tail)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -1326,7 +1373,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
           s_arr = n;
         }
         __syncthreads();
-        lenet_ps_arrive(a, s_arr, (unsigned)(nslot + 1));
+        lenet_ps_arrive(a, s_arr, (unsigned)(nslot + 2));
       }
       if (threadIdx.x == 0) a.gran_ep[blockIdx.x] = ge;
       LR_STAMP(4);
@@ -1423,7 +1470,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     }
     __syncthreads();
     LR_STAMP(1);
-    const unsigned dec = (PS && nown > 0) ? lenet_ps_wait(a, &s_dec, applied0) : 0u;
+    const unsigned dec = (PS && nown > 0) ? lenet_ps_wait(a, &s_dec) : 0u;
     LR_STAMP(2);
 #pragma unroll 1
     for (int k = 0; k < nown; ++k) {
@@ -1508,7 +1555,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     LR_STAMP(3);
     if (PS) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's shard adds have landed
-      lenet_ps_arrive(a, (unsigned)narr, (unsigned)(nslot + 1));
+      lenet_ps_arrive(a, (unsigned)narr, (unsigned)(nslot + 2));
     }
     LR_STAMP(4);
     LR_FLUSH();
@@ -1516,18 +1563,23 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
   }
   const int blk = blockIdx.x - G;
   if (blk == 1 && PS) {
-    // async: admit or reject this step's gradient right away (lock-free CAS on the shared version; the
-    // owners pick the decision up after their jobs), complete its microbatch, then claim the next one FCFS
-    // on the server and stage its example indices
-    __shared__ long long s_bid;
+    // async: the admission ran in the train launch (lenet_ps_admission); this workgroup's arrival keeps the
+    // launch epoch from advancing before the decision of this launch exists
     LR_STAMP(8);
-    if (threadIdx.x == 0) {
-      const unsigned ep = __hip_atomic_load(a.ps.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-      const unsigned dec = ps_admit(a.ps);
-      __hip_atomic_store(a.ps.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    LR_STAMP(9);
+    lenet_ps_arrive(a, 1u, (unsigned)(nslot + 2));
+    LR_STAMP(1);
+    LR_FLUSH();
+    return;
+  }
+  if (blk == 2 && PS) {
+    // beside the admission: claim the next microbatch FCFS on the server (its remote atomics no longer
+    // follow the admission's), then -- once the admission has read this step's microbatch id (its decision
+    // is out) -- publish the new id and stage its example indices
+    __shared__ long long s_bid;
+    __shared__ unsigned s_ep;
+    LR_STAMP(8);
+    if (threadIdx.x == 0)
+      s_ep = __hip_atomic_load(a.ps.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     if (a.ps.done_epoch != nullptr) {
       claim_microbatch(a.ps, threadIdx.x, &s_bid);
     } else if (threadIdx.x == 0) {
@@ -1535,11 +1587,23 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
                           (unsigned long long)(a.ps.nbatches > 0 ? a.ps.nbatches : 1));
     }
     __syncthreads();
-    if (threadIdx.x == 0) *a.ps.bid_out = s_bid;
+    LR_STAMP(9);
+    if (threadIdx.x == 0) {
+      // (the epoch cannot advance before this workgroup arrives: it is one of the launch's arrivals)
+      const unsigned long long t0 = wall_clock64();
+      while (!ps_epoch_eq(__hip_atomic_load(a.ps.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                          s_ep)) {
+        if (wall_clock64() - t0 > 2ull * (unsigned long long)a.ps.timeout_ticks) {
+          atomicOr(a.ps.stats + 5, 8ull);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      *a.ps.bid_out = s_bid;
+    }
     ps_stage_indices(a.ps, s_bid, threadIdx.x, RT);
     LR_STAMP(10);
-    lenet_ps_arrive(a, 1u, (unsigned)(nslot + 1));
-    LR_STAMP(1);
+    lenet_ps_arrive(a, 1u, (unsigned)(nslot + 2));
     LR_FLUSH();
     return;
   }
@@ -1646,7 +1710,13 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
                        reinterpret_cast<bf16x8*>(const_cast<void*>(a.frag)));
     DFA_HIP_CHECK(hipGetLastError());
   }
-  hipLaunchKernelGGL(lenet_train_kernel, dim3(nblk), dim3(NT), LDS_BYTES, st, a);
+  a.nblk = nblk;
+  a.ps_admit = r.ps_on;
+  // (the admission workgroup runs in this launch: its parameter-server words are checked here)
+  if (r.ps_on && (!r.ps.ver || !r.ps.vpulled || !r.ps.bid_out || !r.ps.stats || !r.ps.scratch))
+    return hipErrorInvalidValue;
+  if (r.ps_on) a.ps = r.ps;
+  hipLaunchKernelGGL(lenet_train_kernel, dim3(nblk + (r.ps_on ? 1 : 0)), dim3(NT), LDS_BYTES, st, a);
   DFA_HIP_CHECK(hipGetLastError());
   r.nblk = nblk;
   r.ldt = a.ldt;
@@ -1707,14 +1777,15 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   if (r.ps_on) {
     // async PS: the owners wait for workgroup 0's decision (dispatched first)
     if (!r.sgd_on || r.ll_on || r.sgd.src || !r.ps.ver || !r.ps.vpulled || !r.ps.bid_out || !r.ps.stats ||
-        !r.ps.scratch || r.exch_blocks + 2 > 1024 || r.sgd.mom || r.ps.nshards < 1 || r.ps.nshards > kP2PMaxRanks ||
+        !r.ps.scratch || r.exch_blocks + 3 > 1024 || r.sgd.mom || r.ps.nshards < 1 || r.ps.nshards > kP2PMaxRanks ||
         r.ps.shard_shift < 6 || ((r.ps.n - 1) >> r.ps.shard_shift) >= r.ps.nshards)
       return hipErrorInvalidValue;
     for (int k = 0; k < r.ps.nshards; ++k)
       if (!r.ps.shard[k]) return hipErrorInvalidValue;
     if (r.ps.owner_ring > 0) return hipErrorInvalidValue;  // owner-applies runs the generic pull / apply
   }
-  const int extra = ((r.sgd_on && r.sgd.src) || r.ps_on) ? 1 : 0;  // the index-staging workgroup
+  // the index-staging workgroup; async PS: the admission and the claim / staging workgroups
+  const int extra = r.ps_on ? 2 : ((r.sgd_on && r.sgd.src) ? 1 : 0);
   const dim3 grid(r.exch_blocks + 1 + extra);
   if (r.ll_on) hipLaunchKernelGGL(lenet_reduce_kernel<1>, grid, dim3(RT), 0, st, r);
   else if (r.ps_on) hipLaunchKernelGGL(lenet_reduce_kernel<2>, grid, dim3(RT), 0, st, r);

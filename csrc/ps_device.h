@@ -169,21 +169,24 @@ __device__ inline void complete_microbatch(const PSArgs& a, long long bid) {
 // version, check the staleness bound against vp (kPSVMin, see the header), CAS version -> version + 1; a
 // CAS lost to another rank's admission re-reads and re-checks.  Records vp in *vpulled, the counters, the
 // optional audit row and the microbatch completion.  Returns the decision code.
-__device__ inline unsigned ps_admit(const PSArgs& a) {
+__device__ inline unsigned ps_admit(const PSArgs& a, bool complete_now = true) {
+  // every independent load first (one memory round trip, not one per load: the admission is the async
+  // step's critical path), then the CAS
   const long long bid = *a.bid_out;
-  const unsigned long long k = a.stats[0] + a.stats[1];  // this rank's decision index
+  const unsigned long long s0 = a.stats[0], s1 = a.stats[1], s2 = a.stats[2], s3 = a.stats[3];
+  unsigned vp = __hip_atomic_load(a.scratch + kPSVMin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned v = __hip_atomic_load(a.ver, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned long long k = s0 + s1;  // this rank's decision index
   if (a.done_epoch != nullptr && bid < 0) {  // dataset finished: a no-op step (no refresh follows)
     a.stats[6] += 1;
     return kPSFinished;
   }
   const unsigned long long t0 = wall_clock64();
-  unsigned vp = __hip_atomic_load(a.scratch + kPSVMin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (vp == kPSNoVer) vp = 0;  // no refresh recorded (never on a well-formed step): count from version 0
   // consumed: this step's refreshers record afresh (they run after the decision, which is published
   // with release semantics behind this store)
   __hip_atomic_store(a.scratch + kPSVMin, kPSNoVer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   *a.vpulled = vp;
-  unsigned v = __hip_atomic_load(a.ver, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   auto audit = [&](unsigned dec) {
     if (a.audit != nullptr && k < (unsigned long long)a.audit_cap) {
       a.audit[3 * k] = v;
@@ -191,10 +194,12 @@ __device__ inline unsigned ps_admit(const PSArgs& a) {
       a.audit[3 * k + 2] = dec;
     }
   };
+  unsigned long long retries = 0;
   for (;;) {
     const unsigned stale = v - vp;
     if (a.max_stale >= 0 && (int)stale > a.max_stale) {
-      a.stats[1] += 1;
+      a.stats[1] = s1 + 1;
+      if (retries) a.stats[4] += retries;
       audit(kPSReject);
       return kPSReject;
     }
@@ -202,16 +207,19 @@ __device__ inline unsigned ps_admit(const PSArgs& a) {
     if (__hip_atomic_compare_exchange_strong(a.ver, &expected, v + 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_SYSTEM)) {
       a.scratch[kPSSeq] = v;  // this gradient's sequence number (owner-applies: its ring slot)
-      a.stats[0] += 1;
-      a.stats[2] += stale;
-      if (stale > a.stats[3]) a.stats[3] = stale;
+      a.stats[0] = s0 + 1;
+      a.stats[2] = s2 + stale;
+      if (stale > s3) a.stats[3] = stale;
+      if (retries) a.stats[4] += retries;
       audit(kPSAccept);
-      if (a.done_epoch != nullptr) complete_microbatch(a, bid);
+      // (complete_now false: the caller completes the microbatch after publishing the decision)
+      if (a.done_epoch != nullptr && complete_now) complete_microbatch(a, bid);
       return kPSAccept;
     }
     v = expected;  // another rank admitted in between: re-check against its version
-    a.stats[4] += 1;
+    ++retries;
     if (wall_clock64() - t0 > (unsigned long long)a.timeout_ticks) {
+      a.stats[4] += retries;
       atomicOr(a.stats + 5, 4ull);
       if (a.herr) __hip_atomic_store(a.herr, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return kPSFailed;
