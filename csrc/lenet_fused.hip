@@ -1104,14 +1104,23 @@ __device__ __forceinline__ void red_apply(const LeNetRedArgs& a, const RedTables
 // The slot owners wait for it only after their jobs (so it is normally already there), then add
 // -lr * g to their elements of the sharded master and refresh the local copies from the values the adds
 // produced.  No lock is held: the owners of different ranks update the shards in parallel.
-__device__ __forceinline__ unsigned lenet_ps_wait(const LeNetRedArgs& a, unsigned* s_dec) {
+// ``pre`` (thread 0): the epoch and decision words as loaded at the workgroup's start, {epoch, decision}, or
+// nullptr.  The epoch cannot advance before every owner has passed this wait, and a decision published
+// by the train launch's admission workgroup is already there when the reduce launch starts, so the
+// common case costs no memory round trip here.
+__device__ __forceinline__ unsigned lenet_ps_wait(const LeNetRedArgs& a, unsigned* s_dec,
+                                                  const unsigned* pre = nullptr) {
   const PSArgs& p = a.ps;
   if (threadIdx.x == 0) {
-    const unsigned ep = __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const unsigned ep = (pre ? pre[0] : __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)) + 1u;
     const unsigned long long t0 = wall_clock64();
     unsigned dec = kPSFailed;
+    bool first = pre != nullptr;
     for (;;) {  // relaxed polls, one acquire once the word matches
-      const unsigned w = __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned w = first ? pre[1] : __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+      first = false;
       if (ps_epoch_eq(w, ep)) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         dec = w & 7u;
@@ -1133,7 +1142,8 @@ __device__ __forceinline__ unsigned lenet_ps_wait(const LeNetRedArgs& a, unsigne
 // Protocol arrivals: one per slot (its owner adds one when done with it) and one from the staging
 // workgroup; the last one advances this rank's launch epoch (the decision word's tag).  Workgroups that
 // own nothing do not arrive.
-__device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, unsigned count, unsigned arrivals) {
+__device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, unsigned count, unsigned arrivals,
+                                                int known_dec = -1) {
   const PSArgs& p = a.ps;
   __syncthreads();
   if (threadIdx.x == 0 && count > 0) {
@@ -1141,7 +1151,8 @@ __device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, unsigned 
     if (prev + count == arrivals) {
       // the last arrival: every owner drained its shard adds before arriving, so an admitted gradient is
       // now fully applied (the decision word was published before any owner or the staging arrival)
-      const unsigned w = __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned w = known_dec >= 0 ? (unsigned)known_dec
+                                        : __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if ((w & 7u) == kPSAccept) ps_publish_applied(p);
       __hip_atomic_store(p.scratch + kPSApplyDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(p.scratch + kPSEpoch, __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED,
@@ -1211,6 +1222,11 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       // this launch's epoch: the counter load goes out now and is waited for only after the job (a wait
       // here put a whole memory round trip in front of every job)
       const unsigned ge_prev = threadIdx.x == 0 ? a.gran_ep[blockIdx.x] : 0u;
+      unsigned ps_pre[2] = {0u, 0u};  // async PS: epoch and decision words, consumed after the job
+      if (PS && threadIdx.x == 0) {
+        ps_pre[0] = __hip_atomic_load(a.ps.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ps_pre[1] = __hip_atomic_load(a.ps.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       __syncthreads();  // the tables staged above are read by every thread of the job
       float part[kPerThread];
       if (grp < nslot) {
@@ -1250,14 +1266,25 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
         // of the exclusive writer is ONE 16-byte load and store); the group's addresses and current values
         // load here, beside the granule wait
         float* pg[4] = {nullptr, nullptr, nullptr, nullptr};
+        Owned og[4] = {{-1, 0}, {-1, 0}, {-1, 0}, {-1, 0}};
         f32x4 curv = {0.f, 0.f, 0.f, 0.f};
         bool vec = false;
-        const bool grp4 = PS && (int)threadIdx.x * 4 < cnt;
+        // (dense slots: 32 threads x 4 positions; conv slots, whose emits are long -- copies and the MFMA
+        // fragment -- one position per thread)
+        const bool grp4 = PS && dense && (int)threadIdx.x * 4 < cnt;
+        const bool one = PS && !dense && mine;
+        if (one) {
+          og[0] = o;
+          pg[0] = o.di >= 0 ? ps_elem(s_shard, a.ps.shard_shift, tabs.d[o.di].off + o.i) : nullptr;
+          if (a.ps.excl != 0 && pg[0] != nullptr)
+            curv[0] = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(pg[0]), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_SYSTEM));
+        }
         if (grp4) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const Owned oj = owned_elem(a, tabs, s, c * cnt + 4 * (int)threadIdx.x + j);
-            pg[j] = oj.di >= 0 ? ps_elem(s_shard, a.ps.shard_shift, tabs.d[oj.di].off + oj.i) : nullptr;
+            og[j] = owned_elem(a, tabs, s, c * cnt + 4 * (int)threadIdx.x + j);
+            pg[j] = og[j].di >= 0 ? ps_elem(s_shard, a.ps.shard_shift, tabs.d[og[j].di].off + og[j].i) : nullptr;
           }
           vec = a.ps.excl != 0 && pg[0] != nullptr && pg[1] == pg[0] + 1 && pg[2] == pg[0] + 2 && pg[3] == pg[0] + 3 &&
                 (reinterpret_cast<uintptr_t>(pg[0]) & 15) == 0;
@@ -1293,10 +1320,9 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
         LR_STAMP(7);
         if (!PS) LR_STAMP(2);
         if (PS) {
-          float* vb = red;        // [cnt] local sums (the jobs are done with red)
-          float* wb = red + 128;  // [cnt] the shard values after this step
+          float* vb = red;  // [cnt] local sums (the jobs are done with red)
           if (mine) vb[threadIdx.x] = v;
-          const unsigned dec = lenet_ps_wait(a, &s_dec);  // (its barrier also publishes vb)
+          const unsigned dec = lenet_ps_wait(a, &s_dec, ps_pre);  // (its barrier also publishes vb)
           LR_STAMP(2);
           if (dec == kPSAccept || dec == kPSReject) {
             const PSArgs& p = a.ps;
@@ -1321,14 +1347,40 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
                                                                     __HIP_MEMORY_SCOPE_SYSTEM))
                                 : 0.f;
               }
+              // the group's thread emits its 4 elements itself (no LDS hand-back and no barrier, whose
+              // release would wait for the shard store): gradient, local master, compute copies
 #pragma unroll
-              for (int j = 0; j < 4; ++j) wb[q0 + j] = wn[j];
-            }
-            __syncthreads();
-            if (o.di >= 0) {
-              tabs.g[o.di][o.i] = v;
-              if (dense) red_emit<true>(a, tabs, o, wb[threadIdx.x]);
-              else red_emit<false>(a, tabs, o, wb[threadIdx.x]);
+              for (int j = 0; j < 4; ++j)
+                if (og[j].di >= 0) {
+                  tabs.g[og[j].di][og[j].i] = vb[q0 + j];
+                  red_emit<true>(a, tabs, og[j], wn[j]);
+                }
+            } else if (one && pg[0] != nullptr) {
+              float d0, w1;
+              {
+#pragma clang fp contract(off)
+                d0 = -(tabs.hyper[0] * v);
+              }
+              if (p.excl != 0) {  // exclusive writer: the value loaded above is the shard's current one
+                {
+#pragma clang fp contract(off)
+                  w1 = dec == kPSAccept ? curv[0] + d0 : curv[0];
+                }
+                if (dec == kPSAccept)
+                  __hip_atomic_store(reinterpret_cast<unsigned*>(pg[0]), __float_as_uint(w1), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_SYSTEM);
+              } else if (dec == kPSAccept) {
+                float* const pp[1] = {pg[0]};
+                const float dd[1] = {d0};
+                float ww[1];
+                ps_add<1>(pp, dd, ww, false, p);
+                w1 = ww[0];
+              } else {
+                w1 = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(pg[0]), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_SYSTEM));
+              }
+              tabs.g[og[0].di][og[0].i] = v;
+              red_emit<false>(a, tabs, og[0], w1);
             }
           }
           LR_STAMP(5);
@@ -1373,7 +1425,8 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
           s_arr = n;
         }
         __syncthreads();
-        lenet_ps_arrive(a, s_arr, (unsigned)(nslot + 2));
+        // (a slot owner knows the decision; the count is > 0 only for one)
+        lenet_ps_arrive(a, s_arr, (unsigned)(nslot + 2), s >= 0 ? (int)s_dec : -1);
       }
       if (threadIdx.x == 0) a.gran_ep[blockIdx.x] = ge;
       LR_STAMP(4);

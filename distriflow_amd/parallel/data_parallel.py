@@ -510,6 +510,9 @@ class DataParallelTrainer:
             if cursor is not None:
                 self._index_stream[1].copy_(cursor)
             raise
+        for gr in self._graph:
+            if gr is not None:
+                ops.graph_upload(gr)
         torch.cuda.synchronize(net.device)
 
     def bind_distri_dataset(self, ds, rank: int = 0, world: int = 1, scale: Optional[float] = None):
@@ -751,6 +754,8 @@ class DataParallelTrainer:
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=net.device)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
             ok = bool(flag.item())
+        if ok:
+            ops.graph_upload(g)
         torch.cuda.synchronize(net.device)
         self._multi = g if ok else None
         self._multi_u = u if ok else 0
