@@ -2309,6 +2309,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("frag_w2") = 0, py::arg("lenet_snap") = py::none(), py::arg("step_stats") = py::none(),
         py::arg("run_stats") = py::none());
   m.def("sum_buffers", &sum_buffers_py);
+  m.def("graph_upload", [](uintptr_t exec) {
+    // stage an instantiated graph's kernel arguments / launch packets on the device now, outside any
+    // timed region, instead of on its first hipGraphLaunch
+    check_hip(hipGraphUpload(reinterpret_cast<hipGraphExec_t>(exec), cur_stream()), "hipGraphUpload");
+  }, "hipGraphUpload of a captured graph (torch.cuda.CUDAGraph.raw_cuda_graph_exec()) on the current stream");
   m.def("axpby", &axpby_py);
   m.def("bn_stats_fwd", &bn_stats_fwd_py, "BN forward statistics (partials + last-workgroup finalize, one launch)");
   m.def("bn_stats_bwd", &bn_stats_bwd_py, "BN backward statistics: dgamma, dbeta and dx coefficients");

@@ -393,6 +393,22 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
 constexpr int kC64XP = 7;             // halo staging passes per group (224 rows)
 constexpr int kC64XR = 32 * kC64XP;
 
+// Barrier of one 4-wave group of a workgroup (the workgroup-wide s_barrier would keep the two groups in
+// lockstep, so both would sit in their epilogues -- memory latency, no MFMA -- at the same time).  Lane 0
+// of each wave adds one to the group's LDS counter; the wave spins until it holds 4 * (barriers passed).
+// Release / acquire at workgroup scope order the group's LDS accesses around it.  A bounded spin: the
+// four waves of a resident workgroup always arrive, so the bound is never expected to be reached.
+__device__ __forceinline__ void group_sync4(unsigned* ctr, unsigned& gen) {
+  gen += 4u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (int spin = 0; spin < (1 << 24); ++spin) {
+    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= gen) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 template <bool FLIP>
 __global__ void __launch_bounds__(512, 1) conv3_halo_c64_kernel(C3P p) {
   __shared__ __attribute__((aligned(16))) bf16 lds[9 * 64 * 64 + 2 * kC64XR * kCS];
@@ -496,10 +512,15 @@ __global__ void __launch_bounds__(512, 1) conv3_halo_c64_kernel(C3P p) {
     }
     return c;
   };
+  __shared__ unsigned gsync[2];  // group barrier counters (group_sync4)
+  if (threadIdx.x < 2) gsync[threadIdx.x] = 0u;
+  unsigned ggen = 0u;
   if (nt > gi) load_halo(tb + gi);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (nt > gi) store_halo();
   __syncthreads();
+  // the two groups run their tiles independently from here (group barriers only): one group's
+  // epilogue overlaps the other's MFMAs
   for (int it = 0; it < iters; ++it) {
     const int t = tb + 2 * it + gi;
     const bool cur = 2 * it + gi < nt, nxt = 2 * (it + 1) + gi < nt;
@@ -529,7 +550,7 @@ __global__ void __launch_bounds__(512, 1) conv3_halo_c64_kernel(C3P p) {
               for (int q = 0; q < 4; ++q) acc[u][q] = mfma16x16x32(fa[u], fb[q], acc[u][q]);
           }
         }
-      __syncthreads();  // this group's waves are done with the halo
+      group_sync4(&gsync[gi], ggen);  // this group's waves are done with the halo
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (nxt) store_halo();
       // the epilogue's loads (mask / residual, BatchNorm inputs) in flight before the stores, in two
@@ -561,12 +582,13 @@ __global__ void __launch_bounds__(512, 1) conv3_halo_c64_kernel(C3P p) {
           }
         }
       }
+      group_sync4(&gsync[gi], ggen);  // the next halo is stored
     } else {
-      __syncthreads();
+      break;  // (this group has no tile left; the other may still be running)
     }
-    __syncthreads();
   }
-  if (bacc) {  // the loop ended with a barrier: the halo buffers are free
+  __syncthreads();  // both groups done
+  if (bacc) {  // the halo buffers are free
     float* red = reinterpret_cast<float*>(lds + 9 * 64 * 64);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {

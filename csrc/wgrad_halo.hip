@@ -73,6 +73,18 @@ struct HaloP {
   float scale;
 };
 
+// Barrier of one 4-wave group (see conv3_halo.hip group_sync4): the groups walk their tiles independently.
+__device__ __forceinline__ void wg_group_sync4(unsigned* ctr, unsigned& gen) {
+  gen += 4u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (int spin = 0; spin < (1 << 24); ++spin) {
+    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= gen) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // G groups of 4 waves share one output block: group gi walks tiles t0 + gi, t0 + gi + G, ... with its own
 // LDS buffers, and the groups' partial blocks are summed through LDS before the one slab store (G = 2:
 // 8 waves per CU at half the slab bytes of two 4-wave workgroups)
@@ -152,6 +164,9 @@ __global__ void __launch_bounds__(256 * G, 2 / G) wgrad_halo_kernel(HaloP p) {
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  __shared__ unsigned gsync[2];
+  if (threadIdx.x < 2) gsync[threadIdx.x] = 0u;
+  unsigned ggen = 0u;
   if (nt > 0) {
     gload(t0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -159,8 +174,9 @@ __global__ void __launch_bounds__(256 * G, 2 / G) wgrad_halo_kernel(HaloP p) {
     if (nt > 1) gload(t0 + G);
   }
   __syncthreads();
-  for (int it = 0; it < iters; ++it) {
-    if (it < nt) {
+  (void)iters;
+  for (int it = 0; it < nt; ++it) {  // group barriers only: the groups drift apart
+    {
       const bf16* base = glds + (it & 1) * kHBuf;
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
@@ -188,11 +204,13 @@ __global__ void __launch_bounds__(256 * G, 2 / G) wgrad_halo_kernel(HaloP p) {
         sstore((it + 1) & 1);
       }
     }
-    __syncthreads();
+    if (G > 1) wg_group_sync4(&gsync[gi], ggen);
+    else __syncthreads();
     if (it + 2 < nt) gload(t0 + (it + 2) * G);
   }
 
-  if (G > 1) {  // group 1 hands its block to group 0 through LDS, half (co tiles 0-1, then 2-3) at a time
+  if (G > 1) {
+    __syncthreads();  // both groups done with their buffers (red overlays them)  // group 1 hands its block to group 0 through LDS, half (co tiles 0-1, then 2-3) at a time
     float* red = reinterpret_cast<float*>(lds);  // [wave][72 registers][64 lanes]
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
