@@ -1324,64 +1324,83 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
           if (mine) vb[threadIdx.x] = v;
           const unsigned dec = lenet_ps_wait(a, &s_dec, ps_pre);  // (its barrier also publishes vb)
           LR_STAMP(2);
-          if (dec == kPSAccept || dec == kPSReject) {
-            const PSArgs& p = a.ps;
-            if (grp4) {
-              const int q0 = 4 * (int)threadIdx.x;
-              float d[4], wn[4];
+          const bool upd = dec == kPSAccept || dec == kPSReject;
+          const PSArgs& p = a.ps;
+          const int q0 = 4 * (int)threadIdx.x;
+          float wn[4] = {0.f, 0.f, 0.f, 0.f};  // the shard values after this step (emitted below)
+          if (upd && grp4) {
+            float d[4];
 #pragma unroll
-              for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < 4; ++j) {
 #pragma clang fp contract(off)
-                d[j] = -(tabs.hyper[0] * vb[q0 + j]);
-              }
-              if (vec) {  // exclusive writer: the values loaded above are the shard's current ones
+              d[j] = -(tabs.hyper[0] * vb[q0 + j]);
+            }
+            if (vec) {  // exclusive writer: the values loaded above are the shard's current ones
 #pragma unroll
-                for (int j = 0; j < 4; ++j) wn[j] = dec == kPSAccept ? curv[j] + d[j] : curv[j];
-                if (dec == kPSAccept) *reinterpret_cast<f32x4*>(pg[0]) = f32x4{wn[0], wn[1], wn[2], wn[3]};
-              } else if (dec == kPSAccept) {
-                ps_add<4>(pg, d, wn, p.excl != 0, p);
-              } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                  wn[j] = pg[j] ? __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(pg[j]), __ATOMIC_RELAXED,
-                                                                    __HIP_MEMORY_SCOPE_SYSTEM))
-                                : 0.f;
-              }
-              // the group's thread emits its 4 elements itself (no LDS hand-back and no barrier, whose
-              // release would wait for the shard store): gradient, local master, compute copies
+              for (int j = 0; j < 4; ++j) wn[j] = dec == kPSAccept ? curv[j] + d[j] : curv[j];
+              if (dec == kPSAccept) *reinterpret_cast<f32x4*>(pg[0]) = f32x4{wn[0], wn[1], wn[2], wn[3]};
+            } else if (dec == kPSAccept) {
+              ps_add<4>(pg, d, wn, p.excl != 0, p);
+            } else {
 #pragma unroll
               for (int j = 0; j < 4; ++j)
-                if (og[j].di >= 0) {
-                  tabs.g[og[j].di][og[j].i] = vb[q0 + j];
-                  red_emit<true>(a, tabs, og[j], wn[j]);
-                }
-            } else if (one && pg[0] != nullptr) {
-              float d0, w1;
+                wn[j] = pg[j] ? __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(pg[j]), __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_SYSTEM))
+                              : 0.f;
+            }
+          } else if (upd && one && pg[0] != nullptr) {
+            float d0;
+            {
+#pragma clang fp contract(off)
+              d0 = -(tabs.hyper[0] * v);
+            }
+            if (p.excl != 0) {  // exclusive writer: the value loaded above is the shard's current one
               {
 #pragma clang fp contract(off)
-                d0 = -(tabs.hyper[0] * v);
+                wn[0] = dec == kPSAccept ? curv[0] + d0 : curv[0];
               }
-              if (p.excl != 0) {  // exclusive writer: the value loaded above is the shard's current one
-                {
-#pragma clang fp contract(off)
-                  w1 = dec == kPSAccept ? curv[0] + d0 : curv[0];
-                }
-                if (dec == kPSAccept)
-                  __hip_atomic_store(reinterpret_cast<unsigned*>(pg[0]), __float_as_uint(w1), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_SYSTEM);
-              } else if (dec == kPSAccept) {
-                float* const pp[1] = {pg[0]};
-                const float dd[1] = {d0};
-                float ww[1];
-                ps_add<1>(pp, dd, ww, false, p);
-                w1 = ww[0];
-              } else {
-                w1 = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(pg[0]), __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_SYSTEM));
-              }
-              tabs.g[og[0].di][og[0].i] = v;
-              red_emit<false>(a, tabs, og[0], w1);
+              if (dec == kPSAccept)
+                __hip_atomic_store(reinterpret_cast<unsigned*>(pg[0]), __float_as_uint(wn[0]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            } else if (dec == kPSAccept) {
+              float* const pp[1] = {pg[0]};
+              const float dd[1] = {d0};
+              float ww[1];
+              ps_add<1>(pp, dd, ww, false, p);
+              wn[0] = ww[0];
+            } else {
+              wn[0] = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(pg[0]), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_SYSTEM));
             }
+          }
+          // this workgroup's shard adds have landed; the slot's last owner of its 8 arrives for the slot (one
+          // counter per slot, then nslot + 2 arrivals on the launch's: a flat fan-in of 8 x nslot owners on
+          // one word was the launch's tail).  The local emits (rank-private: gradient, local master, compute
+          // copies, read by the next launch) follow the arrival instead of delaying it.
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          __shared__ unsigned s_arr;
+          if (threadIdx.x == 0) {
+            unsigned n = 0;
+            if (__hip_atomic_fetch_add(a.slot_arr + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                (unsigned)(kChunks - 1)) {
+              __hip_atomic_store(a.slot_arr + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              n = 1;
+            }
+            s_arr = n;
+          }
+          __syncthreads();
+          lenet_ps_arrive(a, s_arr, (unsigned)(nslot + 2), (int)dec);  // (a slot owner knows the decision)
+          if (upd && grp4) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (og[j].di >= 0) {
+                tabs.g[og[j].di][og[j].i] = vb[q0 + j];
+                red_emit<true>(a, tabs, og[j], wn[j]);
+              }
+          } else if (upd && one && pg[0] != nullptr) {
+            tabs.g[og[0].di][og[0].i] = v;
+            red_emit<false>(a, tabs, og[0], wn[0]);
           }
           LR_STAMP(5);
         } else {
@@ -1408,26 +1427,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
         }
       }
       LR_STAMP(3);
-      if (PS) {
-        // this workgroup's shard adds have landed; the slot's last owner of its 8 arrives for the slot (one
-        // counter per slot, then nslot + 2 arrivals on the launch's: a flat fan-in of 8 x nslot owners on
-        // one word was the launch's tail)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        __shared__ unsigned s_arr;
-        if (threadIdx.x == 0) {
-          unsigned n = 0;
-          if (s >= 0 && __hip_atomic_fetch_add(a.slot_arr + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                            (unsigned)(kChunks - 1)) {
-            __hip_atomic_store(a.slot_arr + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            n = 1;
-          }
-          s_arr = n;
-        }
-        __syncthreads();
-        // (a slot owner knows the decision; the count is > 0 only for one)
-        lenet_ps_arrive(a, s_arr, (unsigned)(nslot + 2), s >= 0 ? (int)s_dec : -1);
-      }
+      // (async PS: the slot owners arrived above; workgroup 0 owns no slot)
       if (threadIdx.x == 0) a.gran_ep[blockIdx.x] = ge;
       LR_STAMP(4);
       LR_FLUSH();
