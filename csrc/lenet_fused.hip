@@ -1204,7 +1204,8 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
   const int G = a.exch_blocks;
   if ((int)blockIdx.x < G) {
     // async PS: the fully applied count before any shard access of this launch (ps_device.h)
-    if (PS) ps_stage_shards(a.ps, s_shard);
+    // (successor mode: the barrier after the tables publishes the shard table too)
+    if (PS) ps_stage_shards(a.ps, s_shard, !a.succ);
     stage_tables(a, &tabs);
     // with the fused sync update, the first owned slot's master / momentum elements are loaded beside
     // its slab loads
@@ -1328,6 +1329,10 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
           const PSArgs& p = a.ps;
           const int q0 = 4 * (int)threadIdx.x;
           float wn[4] = {0.f, 0.f, 0.f, 0.f};  // the shard values after this step (emitted below)
+          // an exclusive writer's slot arrival waits for nothing: it goes out now, beside the shard update
+          unsigned slot_prev = 0u;
+          if (p.excl && threadIdx.x == 0)
+            slot_prev = __hip_atomic_fetch_add(a.slot_arr + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (upd && grp4) {
             float d[4];
 #pragma unroll
@@ -1377,27 +1382,35 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
           // counter per slot, then nslot + 2 arrivals on the launch's: a flat fan-in of 8 x nslot owners on
           // one word was the launch's tail).  The local emits (rank-private: gradient, local master, compute
           // copies, read by the next launch) follow the arrival instead of delaying it.
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          // (an exclusive writer -- one rank -- has no concurrent reader of the shard: its next reader is this
+          // rank's next launch, after the kernel boundary; no drain)
+          LR_STAMP(11);
+          float* wb = red + 128;  // [cnt] the dense groups' new values, one emit per position below
+          if (upd && grp4)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wb[q0 + j] = wn[j];
+          if (!p.excl) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __syncthreads();
           __shared__ unsigned s_arr;
           if (threadIdx.x == 0) {
+            if (!p.excl)
+              slot_prev = __hip_atomic_fetch_add(a.slot_arr + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             unsigned n = 0;
-            if (__hip_atomic_fetch_add(a.slot_arr + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                (unsigned)(kChunks - 1)) {
+            if (slot_prev == (unsigned)(kChunks - 1)) {
               __hip_atomic_store(a.slot_arr + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               n = 1;
             }
             s_arr = n;
           }
           __syncthreads();
+          LR_STAMP(12);
           lenet_ps_arrive(a, s_arr, (unsigned)(nslot + 2), (int)dec);  // (a slot owner knows the decision)
-          if (upd && grp4) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (og[j].di >= 0) {
-                tabs.g[og[j].di][og[j].i] = vb[q0 + j];
-                red_emit<true>(a, tabs, og[j], wn[j]);
-              }
+          LR_STAMP(13);
+          if (upd && dense) {
+            if (mine && o.di >= 0) {
+              tabs.g[o.di][o.i] = v;
+              red_emit<true>(a, tabs, o, wb[threadIdx.x]);
+            }
           } else if (upd && one && pg[0] != nullptr) {
             tabs.g[og[0].di][og[0].i] = v;
             red_emit<false>(a, tabs, og[0], wn[0]);

@@ -229,7 +229,7 @@ __device__ inline unsigned ps_admit(const PSArgs& a, bool complete_now = true) {
 
 // The shard bases into LDS (indexing the by-value kernel argument with a run-time shard number would
 // copy the whole argument block to scratch per thread).  Every thread of the workgroup calls it.
-__device__ __forceinline__ void ps_stage_shards(const PSArgs& a, float** tab) {
+__device__ __forceinline__ void ps_stage_shards(const PSArgs& a, float** tab, bool barrier = true) {
   if (threadIdx.x < kP2PMaxRanks) {
     float* v = nullptr;
 #pragma unroll
@@ -237,7 +237,7 @@ __device__ __forceinline__ void ps_stage_shards(const PSArgs& a, float** tab) {
       if ((int)threadIdx.x == k) v = a.shard[k];
     tab[threadIdx.x] = v;
   }
-  __syncthreads();
+  if (barrier) __syncthreads();  // (false: the caller's next barrier publishes the table)
 }
 
 // Address of master element i (tab: the shard bases, staged in LDS by the caller)

@@ -107,13 +107,18 @@ def reduce_stamps(m, net, data, labels, B, buf, async_ps):
         if own.any():
             line.append(f"owners {own.sum()}: wait {us(np.median(r[own, 2] - r[own, 1])):5.2f} "
                         f"apply {us(np.median(r[own, 3] - r[own, 2])):5.2f} max {us((r[own, 3] - r[own, 2]).max()):5.2f}")
+        ps = own & (r[:, 11] > 0) & (r[:, 13] > 0)
+        if ps.any():  # async PS owners: shard update, slot arrival, launch arrival, local emits
+            line.append(f"PS rmw {us(np.median(r[ps, 11] - r[ps, 2])):5.2f} slot-arrive "
+                        f"{us(np.median(r[ps, 12] - r[ps, 11])):5.2f} arrive {us(np.median(r[ps, 13] - r[ps, 12])):5.2f} "
+                        f"emit {us(np.median(r[ps, 5] - r[ps, 13])):5.2f}")
         st = valid & (r[:, 8] > 0)
         if st.any():
             line.append(f"admission {us(float(r[st, 9][0] - r[st, 8][0])):5.2f} (start +{us(float(r[st, 8][0] - t0)):5.2f}),"
                         f" claim+stage {us(float(r[st, 10][0] - r[st, 9][0])):5.2f}")
         print("  " + "; ".join(line))
         lb = int(np.argmax(np.where(valid, r[:, [1, 4]].max(axis=1), 0)))
-        rel = {k: (us(float(r[lb, k] - t0)) if r[lb, k] > 0 else None) for k in (0, 6, 7, 1, 2, 3, 5, 4)}
+        rel = {k: (us(float(r[lb, k] - t0)) if r[lb, k] > 0 else None) for k in (0, 6, 7, 1, 2, 11, 12, 13, 3, 5, 4)}
         print(f"    last block {lb}: " + ", ".join(f"s{k} {v:.2f}" for k, v in rel.items() if v is not None))
 
 
