@@ -1223,11 +1223,6 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       // this launch's epoch: the counter load goes out now and is waited for only after the job (a wait
       // here put a whole memory round trip in front of every job)
       const unsigned ge_prev = threadIdx.x == 0 ? a.gran_ep[blockIdx.x] : 0u;
-      unsigned ps_pre[2] = {0u, 0u};  // async PS: epoch and decision words, consumed after the job
-      if (PS && threadIdx.x == 0) {
-        ps_pre[0] = __hip_atomic_load(a.ps.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ps_pre[1] = __hip_atomic_load(a.ps.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
       __syncthreads();  // the tables staged above are read by every thread of the job
       float part[kPerThread];
       if (grp < nslot) {
@@ -1248,6 +1243,13 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
                                __HIP_MEMORY_SCOPE_AGENT);
       }
       LR_STAMP(1);
+      // async PS: the epoch and decision words, loaded beside the granule polls below (issued before the
+      // job, their wait sat in front of the job's first operand wait)
+      unsigned ps_pre[2] = {0u, 0u};
+      if (PS && threadIdx.x == 0) {
+        ps_pre[0] = __hip_atomic_load(a.ps.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ps_pre[1] = __hip_atomic_load(a.ps.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       const int s = grp - 1;
       if (s >= 0) {
         const bool dense = s < a.dense_tiles;

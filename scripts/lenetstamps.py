@@ -117,6 +117,13 @@ def reduce_stamps(m, net, data, labels, B, buf, async_ps):
             line.append(f"admission {us(float(r[st, 9][0] - r[st, 8][0])):5.2f} (start +{us(float(r[st, 8][0] - t0)):5.2f}),"
                         f" claim+stage {us(float(r[st, 10][0] - r[st, 9][0])):5.2f}")
         print("  " + "; ".join(line))
+        jd = np.where(jobs, r[:, 6] - r[:, 0], 0)
+        segs = []
+        for b0 in range(0, int(valid.sum()), 64):
+            sel = jd[b0:b0 + 64][jd[b0:b0 + 64] > 0]
+            if sel.size:
+                segs.append(f"{b0}:{us(np.median(sel)):.1f}/{us(sel.max()):.1f}")
+        print("    job us by block (median/max): " + " ".join(segs))
         lb = int(np.argmax(np.where(valid, r[:, [1, 4]].max(axis=1), 0)))
         rel = {k: (us(float(r[lb, k] - t0)) if r[lb, k] > 0 else None) for k in (0, 6, 7, 1, 2, 11, 12, 13, 3, 5, 4)}
         print(f"    last block {lb}: " + ", ".join(f"s{k} {v:.2f}" for k, v in rel.items() if v is not None))
