@@ -168,12 +168,29 @@ __global__ __launch_bounds__(kPSBlock) void ps_fetch_pull_kernel(PSArgs a) {
 // the others wait for that decision on a local word tagged with this launch's epoch and then add their
 // slice; the last workgroup to finish advances the epoch.  The grid is small (<= 64 workgroups), so all of
 // it is resident and the decision wait cannot starve workgroup 0.
+constexpr int kPSExclGroups = 2;  // exclusive writer: float4 groups per thread prefetched before the decision
+
 __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
   const int t = threadIdx.x, b = blockIdx.x, G = gridDim.x;
   __shared__ float* tab[kP2PMaxRanks];
   __shared__ unsigned s_dec;
   __shared__ int s_last;
   ps_stage_shards(a, tab);
+  // the exclusive writer (one rank, cached shard memory, no concurrent reader): plain 16-byte read-modify-
+  // writes over a wide grid, this thread's first groups of gradient and shard values loaded while
+  // workgroup 0 decides (the per-element system-scope path took ~21 us for 600 k parameters)
+  const bool vexcl = a.excl != 0 && a.owner_ring <= 0;
+  const long long gstride = (long long)G * kPSBlock;
+  f32x4 gv[kPSExclGroups], wv[kPSExclGroups];
+  if (vexcl)
+#pragma unroll
+    for (int k = 0; k < kPSExclGroups; ++k) {
+      const long long i = 4 * ((long long)b * kPSBlock + t + k * gstride);
+      if (i < a.n) {
+        gv[k] = *reinterpret_cast<const f32x4*>(a.g + i);
+        wv[k] = *reinterpret_cast<const f32x4*>(ps_elem(tab, a.shard_shift, i));
+      }
+    }
   if (t == 0) {
     const unsigned ep = __hip_atomic_load(a.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     if (b == 0) {
@@ -220,6 +237,32 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
       }
       __hip_atomic_store(reinterpret_cast<unsigned*>(a.inbox[i >> a.shard_shift] + soff + (i & mask)),
                          __float_as_uint(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  } else if (s_dec == kPSAccept && vexcl) {
+    const float lr = a.lr_dev ? *a.lr_dev : a.lr;
+#pragma unroll
+    for (int k = 0; k < kPSExclGroups; ++k) {
+      const long long i = 4 * ((long long)b * kPSBlock + t + k * gstride);
+      if (i < a.n) {
+        f32x4 nw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma clang fp contract(off)  // the same rounding as the CAS path
+          nw[e] = wv[k][e] + -(lr * gv[k][e]);
+        }
+        *reinterpret_cast<f32x4*>(ps_elem(tab, a.shard_shift, i)) = nw;
+      }
+    }
+    for (long long i = 4 * ((long long)b * kPSBlock + t + kPSExclGroups * gstride); i < a.n; i += 4 * gstride) {
+      const f32x4 g4 = *reinterpret_cast<const f32x4*>(a.g + i);
+      float* wp = ps_elem(tab, a.shard_shift, i);
+      f32x4 w4 = *reinterpret_cast<const f32x4*>(wp);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma clang fp contract(off)
+        w4[e] = w4[e] + -(lr * g4[e]);
+      }
+      *reinterpret_cast<f32x4*>(wp) = w4;
     }
   } else if (s_dec == kPSAccept) {
     const long long per = ((a.n + 4LL * G - 1) / (4LL * G)) * 4;
@@ -310,7 +353,13 @@ hipError_t ps_apply(const PSArgs& a, hipStream_t st) {
   // a slot is rewritten R sequence numbers later; every owner has drained it by then only if an admitted
   // gradient is at most R - 2 behind (its pull saw min_k pref[k] >= q - max_stale)
   if (a.owner_ring > 0 && (a.max_stale < 0 || a.owner_ring < a.max_stale + 2)) return hipErrorInvalidValue;
-  ps_apply_kernel<<<ps_grid(a.n), kPSBlock, 0, st>>>(a);
+  // exclusive writer: one workgroup per 2 K elements (kPSExclGroups float4 per thread), at most 2048
+  int grid = ps_grid(a.n);
+  if (a.excl != 0 && a.owner_ring <= 0) {
+    const long long g = (a.n + 4LL * kPSBlock * kPSExclGroups - 1) / (4LL * kPSBlock * kPSExclGroups);
+    grid = (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+  }
+  ps_apply_kernel<<<grid, kPSBlock, 0, st>>>(a);
   return hipGetLastError();
 }
 
