@@ -37,6 +37,7 @@ namespace {
 
 constexpr int kPSBlock = 256;
 constexpr int kPSUnroll = 4;  // float4 loads in flight per thread per round
+constexpr int kPSExclGroups = 2;  // exclusive writer: float4 groups per thread issued at the kernel's start
 // Multi-workgroup pull: workgroup 0 claims the microbatch and records the version; every workgroup copies
 // its slice of the master out of the shards (4 float4 loads per thread in flight; a slice of 4-aligned
 // elements never crosses a shard boundary, shards being multiples of 64 elements).
@@ -44,6 +45,17 @@ __global__ __launch_bounds__(kPSBlock) void ps_fetch_pull_kernel(PSArgs a) {
   const int t = threadIdx.x, b = blockIdx.x, G = gridDim.x;
   __shared__ float* tab[kP2PMaxRanks];
   ps_stage_shards(a, tab);
+  // the exclusive writer (one rank): no add can land during this copy (the last apply ended with its
+  // launch), so the shard loads go out at once, over a wide grid, beside the claim and the version record
+  const bool vexcl = a.excl != 0 && a.owner_ring <= 0;
+  const long long gstride = (long long)G * kPSBlock;
+  f32x4 xv[kPSExclGroups];
+  if (vexcl)
+#pragma unroll
+    for (int k = 0; k < kPSExclGroups; ++k) {
+      const long long i = 4 * ((long long)b * kPSBlock + t + k * gstride);
+      if (i < a.n) xv[k] = *reinterpret_cast<const f32x4*>(ps_elem(tab, a.shard_shift, i));
+    }
   // every workgroup: the fully applied count BEFORE its own slice copy (ps_device.h: vp = the minimum)
   if (t == 0) ps_note_refresh(a, ps_read_applied(a));
   // owner-applies: workgroup 0 takes the drain lock of every shard no other rank is draining (one CAS per
@@ -104,6 +116,16 @@ __global__ __launch_bounds__(kPSBlock) void ps_fetch_pull_kernel(PSArgs a) {
     __syncthreads();
     if (t == 0) *a.bid_out = s_bid;
     ps_stage_indices(a, s_bid, t, kPSBlock);
+  }
+  if (vexcl) {
+#pragma unroll
+    for (int k = 0; k < kPSExclGroups; ++k) {
+      const long long i = 4 * ((long long)b * kPSBlock + t + k * gstride);
+      if (i < a.n) *reinterpret_cast<f32x4*>(a.w + i) = xv[k];
+    }
+    for (long long i = 4 * ((long long)b * kPSBlock + t + kPSExclGroups * gstride); i < a.n; i += 4 * gstride)
+      *reinterpret_cast<f32x4*>(a.w + i) = *reinterpret_cast<const f32x4*>(ps_elem(tab, a.shard_shift, i));
+    return;
   }
   __syncthreads();
   const long long per = ((a.n + 4LL * G - 1) / (4LL * G)) * 4;  // slice length, multiple of 4
@@ -168,8 +190,6 @@ __global__ __launch_bounds__(kPSBlock) void ps_fetch_pull_kernel(PSArgs a) {
 // the others wait for that decision on a local word tagged with this launch's epoch and then add their
 // slice; the last workgroup to finish advances the epoch.  The grid is small (<= 64 workgroups), so all of
 // it is resident and the decision wait cannot starve workgroup 0.
-constexpr int kPSExclGroups = 2;  // exclusive writer: float4 groups per thread prefetched before the decision
-
 __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
   const int t = threadIdx.x, b = blockIdx.x, G = gridDim.x;
   __shared__ float* tab[kP2PMaxRanks];
@@ -322,6 +342,14 @@ static int ps_grid(long long n) {
   return (int)(g < 1 ? 1 : (g > kPSMaxGrid ? kPSMaxGrid : g));
 }
 
+// exclusive writer: one workgroup per 2 K elements (kPSExclGroups float4 per thread), at most 2048;
+// otherwise ps_grid
+static int ps_excl_grid(const PSArgs& a) {
+  if (a.excl == 0 || a.owner_ring > 0) return ps_grid(a.n);
+  const long long g = (a.n + 4LL * kPSBlock * kPSExclGroups - 1) / (4LL * kPSBlock * kPSExclGroups);
+  return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+}
+
 static bool ps_shards_ok(const PSArgs& a) {
   if (a.nshards < 1 || a.nshards > kP2PMaxRanks || a.shard_shift < 6 || a.shard_shift > 30 || !a.ver) return false;
   if (((a.n - 1) >> a.shard_shift) >= a.nshards) return false;
@@ -344,7 +372,7 @@ hipError_t ps_fetch_pull(const PSArgs& a, hipStream_t st) {
   if (a.n <= 0 || (a.n & 3) || !ps_shards_ok(a) || !ps_owner_ok(a) ||
       (a.perm != nullptr && (a.B <= 0 || (a.B & 1) || a.nbatches <= 0)))
     return hipErrorInvalidValue;
-  ps_fetch_pull_kernel<<<ps_grid(a.n), kPSBlock, 0, st>>>(a);
+  ps_fetch_pull_kernel<<<ps_excl_grid(a), kPSBlock, 0, st>>>(a);
   return hipGetLastError();
 }
 
@@ -353,13 +381,7 @@ hipError_t ps_apply(const PSArgs& a, hipStream_t st) {
   // a slot is rewritten R sequence numbers later; every owner has drained it by then only if an admitted
   // gradient is at most R - 2 behind (its pull saw min_k pref[k] >= q - max_stale)
   if (a.owner_ring > 0 && (a.max_stale < 0 || a.owner_ring < a.max_stale + 2)) return hipErrorInvalidValue;
-  // exclusive writer: one workgroup per 2 K elements (kPSExclGroups float4 per thread), at most 2048
-  int grid = ps_grid(a.n);
-  if (a.excl != 0 && a.owner_ring <= 0) {
-    const long long g = (a.n + 4LL * kPSBlock * kPSExclGroups - 1) / (4LL * kPSBlock * kPSExclGroups);
-    grid = (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
-  }
-  ps_apply_kernel<<<grid, kPSBlock, 0, st>>>(a);
+  ps_apply_kernel<<<ps_excl_grid(a), kPSBlock, 0, st>>>(a);
   return hipGetLastError();
 }
 
