@@ -214,9 +214,16 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
   if (t == 0) {
     const unsigned ep = __hip_atomic_load(a.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     if (b == 0) {
-      const unsigned dec = ps_admit(a);
-      __hip_atomic_store(a.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      const long long bid = *a.bid_out;
+      const unsigned dec = ps_admit(a, false);
+      // owner-applies: the other workgroups read kPSSeq behind the decision (release); otherwise the word
+      // alone is consumed.  The microbatch completion follows the decision, off the critical path.
+      if (a.owner_ring > 0)
+        __hip_atomic_store(a.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        __hip_atomic_store(a.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_dec = dec;
+      if (dec == kPSAccept && a.done_epoch != nullptr) complete_microbatch(a, bid);
     } else {
       const unsigned long long t0 = wall_clock64();
       unsigned d = 0;
@@ -304,10 +311,12 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
       ps_add<kPSUnroll>(p, d, nw, a.excl != 0, a);
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // every add of this workgroup has landed (results returned / stores acknowledged) before its arrival; the
+  // exclusive writer's adds have no reader before the next launch
+  if (!vexcl) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(a.scratch + kPSApplyDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned prev = __hip_atomic_fetch_add(a.scratch + kPSApplyDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = prev == (unsigned)G - 1;
     if (s_last) {
       a.scratch[kPSApplyDone] = 0;

@@ -305,7 +305,9 @@ __device__ __forceinline__ void lenet_ps_admission(const PSArgs& p) {
   // the owners refresh (add to or read the shards) only after this decision, so every one of their
   // refreshes contains at least applied0 fully applied gradients (+ this one when admitted)
   if (dec == kPSAccept || dec == kPSReject) ps_note_refresh(p, applied0 + (dec == kPSAccept ? 1u : 0u));
-  __hip_atomic_store(p.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  // relaxed: the decision's readers are the next (reduce) launch, behind the kernel boundary (a release
+  // here wrote back this XCD's L2 under the running train kernel)
+  __hip_atomic_store(p.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (dec == kPSAccept && p.done_epoch != nullptr) complete_microbatch(p, bid);
 }
 
@@ -1121,9 +1123,8 @@ __device__ __forceinline__ unsigned lenet_ps_wait(const LeNetRedArgs& a, unsigne
       const unsigned w = first ? pre[1] : __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED,
                                                              __HIP_MEMORY_SCOPE_AGENT);
       first = false;
-      if (ps_epoch_eq(w, ep)) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        dec = w & 7u;
+      if (ps_epoch_eq(w, ep)) {  // (only the word itself is consumed: no acquire, which invalidated the L2
+        dec = w & 7u;              // of the owner's XCD under the other workgroups' jobs)
         break;
       }
       if (wall_clock64() - t0 > 2ull * (unsigned long long)p.timeout_ticks) {

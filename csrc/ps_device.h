@@ -45,6 +45,12 @@ constexpr unsigned kPSAccept = 1, kPSReject = 2, kPSFailed = 3, kPSFinished = 4;
 __device__ __forceinline__ unsigned ps_ld_acq(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// The exclusive writer (one rank: no other agent touches the server words) needs no acquire / release on
+// them: each system-scope acquire invalidates and each release writes back the issuing XCD's L2, several
+// microseconds on the async step's critical path.  These helpers drop the ordering when a.excl.
+__device__ __forceinline__ unsigned ps_ld_acq_x(const PSArgs& a, const unsigned* p) {
+  return a.excl ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : ps_ld_acq(p);
+}
 
 // The fully applied count, read by thread 0 of every workgroup that refreshes weights from the shards
 // BEFORE any of its shard reads or adds (reading it earlier only makes the count more conservative, so the
@@ -97,7 +103,7 @@ __device__ inline void claim_microbatch(const PSArgs& a, int t, long long* s_bid
   for (int r = 0;; ++r) {
     if (t == 0) {
       s_c = __hip_atomic_fetch_add(a.batch_ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      s_e = __hip_atomic_load(a.sched, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      s_e = ps_ld_acq_x(a, a.sched);
     }
     __syncthreads();
     const unsigned e = s_e;
@@ -108,7 +114,7 @@ __device__ inline void claim_microbatch(const PSArgs& a, int t, long long* s_bid
         k = -2;
       } else {
         const long long j = (long long)((c + (unsigned long long)t) % (unsigned long long)nb);
-        const unsigned d = t < nb ? ps_ld_acq(a.done_epoch + j) : 0xffffffffu;
+        const unsigned d = t < nb ? ps_ld_acq_x(a, a.done_epoch + j) : 0xffffffffu;
         const unsigned long long inc = __ballot(d < e + 1u);  // incomplete in epoch e
         k = inc ? (int)__builtin_ctzll(inc) : (r + 1 >= rounds ? 0 : -1);
       }
@@ -153,15 +159,22 @@ __device__ inline void complete_microbatch(const PSArgs& a, long long bid) {
   const unsigned e = (unsigned)(bid >> 32);
   const long long bb = bid & 0xffffffffLL;
   const unsigned cur = __hip_atomic_load(a.sched, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (e != cur || __hip_atomic_exchange(a.done_epoch + bb, e + 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) == e + 1u) {
+  unsigned prev_done;
+  if (a.excl)
+    prev_done = e != cur ? 0u : __hip_atomic_exchange(a.done_epoch + bb, e + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else
+    prev_done = e != cur ? 0u : __hip_atomic_exchange(a.done_epoch + bb, e + 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (e != cur || prev_done == e + 1u) {
     __hip_atomic_fetch_add(a.sched_ctr + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
   __hip_atomic_fetch_add(a.sched_ctr + 0, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  const unsigned n = __hip_atomic_fetch_add(a.sched + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+  const unsigned n = (a.excl ? __hip_atomic_fetch_add(a.sched + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                             : __hip_atomic_fetch_add(a.sched + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM)) + 1u;
   if ((long long)n >= a.nbatches) {  // every batch of epoch e applied: next epoch
     __hip_atomic_store(a.sched + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(a.sched, e + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (a.excl) __hip_atomic_store(a.sched, e + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else __hip_atomic_store(a.sched, e + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -204,8 +217,11 @@ __device__ inline unsigned ps_admit(const PSArgs& a, bool complete_now = true) {
       return kPSReject;
     }
     unsigned expected = v;
-    if (__hip_atomic_compare_exchange_strong(a.ver, &expected, v + 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_SYSTEM)) {
+    const bool won = a.excl ? __hip_atomic_compare_exchange_strong(a.ver, &expected, v + 1u, __ATOMIC_RELAXED,
+                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                            : __hip_atomic_compare_exchange_strong(a.ver, &expected, v + 1u, __ATOMIC_ACQ_REL,
+                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (won) {
       a.scratch[kPSSeq] = v;  // this gradient's sequence number (owner-applies: its ring slot)
       a.stats[0] = s0 + 1;
       a.stats[2] = s2 + stale;
