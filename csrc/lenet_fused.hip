@@ -1144,7 +1144,7 @@ __device__ __forceinline__ unsigned lenet_ps_wait(const LeNetRedArgs& a, unsigne
 // workgroup; the last one advances this rank's launch epoch (the decision word's tag).  Workgroups that
 // own nothing do not arrive.
 __device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, unsigned count, unsigned arrivals,
-                                                int known_dec = -1) {
+                                                int known_dec = -1, const unsigned* known_ep = nullptr) {
   const PSArgs& p = a.ps;
   __syncthreads();
   if (threadIdx.x == 0 && count > 0) {
@@ -1156,9 +1156,10 @@ __device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, unsigned 
                                         : __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if ((w & 7u) == kPSAccept) ps_publish_applied(p);
       __hip_atomic_store(p.scratch + kPSApplyDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p.scratch + kPSEpoch, __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_AGENT) + 1u,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // (known_ep: the epoch word as thread 0 of a slot owner loaded it; it cannot have moved since)
+      const unsigned ep0 = known_ep ? *known_ep
+                                    : __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.scratch + kPSEpoch, ep0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -1407,7 +1408,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
           }
           __syncthreads();
           LR_STAMP(12);
-          lenet_ps_arrive(a, s_arr, (unsigned)(nslot + 2), (int)dec);  // (a slot owner knows the decision)
+          lenet_ps_arrive(a, s_arr, (unsigned)(nslot + 2), (int)dec, ps_pre);  // (an owner knows both)
           LR_STAMP(13);
           if (upd && dense) {
             if (mine && o.di >= 0) {
