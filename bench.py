@@ -253,8 +253,15 @@ def main():
             atr = make_trainer("async", anet)
             ael, _ = timed(atr, async_steps)
             aval = world * B * async_steps / ael
+            # the sync trainer timed again right after, the same way: the GPU's clocks ramp up over the first
+            # ~15 ms of load (profiles/r5/lenet_clock_ramp.txt), so the first sync run is colder than the async
+            # one; the ratio compares the two adjacent runs
+            sel2, _ = timed(trainer, async_steps)
+            sval2 = world * B * async_steps / sel2
             async_rec = dict(images_per_s=round(aval, 1), ms_per_step=round(ael / async_steps * 1e3, 4),
-                             steps=async_steps, speedup_vs_sync=round(aval / value, 4),
+                             steps=async_steps, speedup_vs_sync=round(aval / sval2, 4),
+                             sync_rerun_ms_per_step=round(sel2 / async_steps * 1e3, 4),
+                             speedup_vs_first_sync=round(aval / value, 4),
                              max_staleness_bound=args.max_staleness, **atr.ps_stats())
         except Exception as e:  # reported, never fatal to the headline number
             async_rec = {"error": repr(e)[:300]}

@@ -20,6 +20,7 @@ Python switches (default in brackets):
   lenet_succ [1]           LeNet-5 reduce launch: successor ownership (each slot's partials handed to the next
                            slot's workgroups as {epoch, value} granules; 0: arrival tickets + slab reload)
   multistep [1]            bench.py unrolls up to 64 steps per hipGraph (0: one replay per step)
+  graph_steps [64]         most steps unrolled into one multi-step hipGraph
   fused_selftest [1]       real-kernel self-test of the multi-rank fused LeNet-5 step before its first use
                            (0: trust the LL exchange's own setup self-test)
   wgrad_overlap [0]        ResNet weight gradients on a side stream (round 2: +3 %; with the halo-tiled
@@ -46,7 +47,7 @@ from __future__ import annotations
 import os
 
 _DEFAULTS = {"lenet_fused": 1, "lenet_fused_update": 1, "async_fused": 1, "ps_owner_apply": 0, "kcnn_fused": 1, "khead_fused": 1, "fold_dropout": 1,
-             "lenet_succ": 1, "multistep": 1, "fused_selftest": 1, "wgrad_overlap": 0, "proj_overlap": 0, "concurrent_backward": 0, "bn_epilogue": 0,
+             "lenet_succ": 1, "multistep": 1, "graph_steps": 64, "fused_selftest": 1, "wgrad_overlap": 0, "proj_overlap": 0, "concurrent_backward": 0, "bn_epilogue": 0,
              "bn_fused": 0, "bn_acc": 1, "bn_acc_rep": 8}
 
 

@@ -719,7 +719,9 @@ class DataParallelTrainer:
             return
         if self._graph is None:
             self._capture_with_fallback()
-        u = max(1, min(int(n), self.MAX_STEPS_PER_GRAPH))
+        from ..diagnostics import diag
+
+        u = max(1, min(int(n), self.MAX_STEPS_PER_GRAPH, diag("graph_steps")))
         if self.graph_mode != "full" or self._graph is None or u <= 1 or self._multi_u == u:
             return
         net = self.net
