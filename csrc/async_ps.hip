@@ -331,6 +331,43 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
   }
 }
 
+// The exclusive writer's step (one rank; csrc/kernels.h ps_excl_step): the admission of this step's gradient
+// (vp: the applied count its weights contain, noted by the previous step's launch or the prologue's pull),
+// the refresh record of the NEXT step's weights (the optimizer launch that follows applies this gradient
+// when admitted: applied0 + 1 updates), the decision word the optimizer launch is gated on, the completion
+// and the next microbatch's claim and index staging.  One workgroup; no shard access (the gated optimizer
+// launch writes the new weights to the local master, its compute copies and the shard, in one pass).
+__global__ __launch_bounds__(kPSBlock) void ps_excl_step_kernel(PSArgs a) {
+  const int t = threadIdx.x;
+  __shared__ long long s_bid;
+  if (t == 0) {
+    const long long bid = *a.bid_out;
+    const unsigned applied0 = ps_read_applied(a);
+    const unsigned ep = __hip_atomic_load(a.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const unsigned dec = ps_admit(a, false);
+    if (dec == kPSAccept || dec == kPSReject) ps_note_refresh(a, applied0 + (dec == kPSAccept ? 1u : 0u));
+    // (relaxed: the next launch reads it, behind the kernel boundary)
+    __hip_atomic_store(a.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.scratch + kPSEpoch, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dec == kPSAccept) {
+      if (a.done_epoch != nullptr) complete_microbatch(a, bid);
+      // the gated update lands before anyone can read the count: this rank's next launch
+      ps_publish_applied(a);
+    }
+  }
+  __syncthreads();
+  if (a.perm == nullptr) return;
+  if (a.done_epoch != nullptr) {
+    claim_microbatch(a, t, &s_bid);
+  } else if (t == 0) {
+    s_bid = (long long)(__hip_atomic_fetch_add(a.batch_ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) %
+                        (unsigned long long)(a.nbatches > 0 ? a.nbatches : 1));
+  }
+  __syncthreads();
+  if (t == 0) *a.bid_out = s_bid;
+  ps_stage_indices(a, s_bid, t, kPSBlock);
+}
+
 // Shard self-test: thread j < n of workgroup k adds (rank + 1) * (j + 1) to word j of shard k's test area
 // through the same element add as the apply.
 __global__ void ps_selftest_kernel(PSArgs a, float* const* words, int n, float rank1) {
@@ -391,6 +428,14 @@ hipError_t ps_apply(const PSArgs& a, hipStream_t st) {
   // gradient is at most R - 2 behind (its pull saw min_k pref[k] >= q - max_stale)
   if (a.owner_ring > 0 && (a.max_stale < 0 || a.owner_ring < a.max_stale + 2)) return hipErrorInvalidValue;
   ps_apply_kernel<<<ps_excl_grid(a), kPSBlock, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t ps_excl_step(const PSArgs& a, hipStream_t st) {
+  if (a.excl == 0 || a.owner_ring > 0 || a.nshards != 1 || !ps_shards_ok(a) ||
+      (a.perm != nullptr && (a.B <= 0 || (a.B & 1) || a.nbatches <= 0)))
+    return hipErrorInvalidValue;
+  ps_excl_step_kernel<<<1, kPSBlock, 0, st>>>(a);
   return hipGetLastError();
 }
 

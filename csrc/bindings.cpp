@@ -503,7 +503,7 @@ void sgd_multi_py(torch::Tensor descs, int64_t ndesc, int64_t total_blocks, torc
                   c10::optional<torch::Tensor> idx_dst, c10::optional<torch::Tensor> descs_host,
                   c10::optional<torch::Tensor> lenet_frag, int64_t frag_w1, int64_t frag_w2,
                   c10::optional<torch::Tensor> lenet_snap, c10::optional<torch::Tensor> step_stats,
-                  c10::optional<torch::Tensor> run_stats) {
+                  c10::optional<torch::Tensor> run_stats, uintptr_t gate, uintptr_t mirror) {
   TORCH_CHECK(descs.is_cuda() && descs.scalar_type() == at::kLong && descs.is_contiguous(), "descs must be int64 GPU");
   const dfa::ParamDesc* hd = nullptr;
   if (descs_host.has_value() && descs_host->defined()) {  // same table, host copy: passed in the kernel arguments
@@ -566,10 +566,16 @@ void sgd_multi_py(torch::Tensor descs, int64_t ndesc, int64_t total_blocks, torc
     is.frag_w1 = frag_w1;
     is.frag_w2 = frag_w2;
   }
+  // async PS exclusive writer (PSComm.excl_gate / excl_mirror): the update gated on the admission word, the
+  // new weights mirrored into the rank's shard
+  TORCH_CHECK((gate == 0) == (mirror == 0), "sgd_multi: gate and mirror go together");
+  TORCH_CHECK(gate == 0 || (apply_update && !is.frag), "sgd_multi: a gated update without LeNet fragments");
+  is.gate = reinterpret_cast<const unsigned*>(gate);
+  is.mirror = reinterpret_cast<float*>(mirror);
+  const bool any = is.src || is.frag || is.run_stats || is.gate;
   check_hip(dfa::sgd_multi(reinterpret_cast<const dfa::ParamDesc*>(descs.data_ptr()), (int)ndesc, (int)total_blocks,
                            master.data_ptr<float>(), grad.data_ptr<float>(), mp, (dfa::bf16*)wbf.data_ptr(),
-                           hyper.data_ptr<float>(), apply_update ? 1 : 0, cur_stream(), (is.src || is.frag) ? &is : nullptr,
-                           hd),
+                           hyper.data_ptr<float>(), apply_update ? 1 : 0, cur_stream(), any ? &is : nullptr, hd),
             "sgd_multi");
 }
 
@@ -1924,6 +1930,34 @@ class PSComm {
     }
     check_hip(dfa::ps_fetch_pull(a, cur_stream()), "ps_fetch_pull");
   }
+  // exclusive writer (world 1): admission + next claim / index staging, one workgroup; the update is the
+  // optimizer launch gated on excl_gate() that mirrors the new weights into excl_mirror() (ps_excl_step)
+  void excl_step(int64_t max_stale, c10::optional<torch::Tensor> perm, c10::optional<torch::Tensor> idx) {
+    TORCH_CHECK(world_ == 1 && !owner_on_, "ps: the exclusive-writer step needs one rank (CAS path)");
+    dfa::PSArgs a = args();
+    a.max_stale = (int)max_stale;
+    if (perm.has_value() && perm->defined()) {
+      need(*perm, at::kLong, "ps perm");
+      TORCH_CHECK(idx.has_value() && idx->defined(), "ps: idx required with perm");
+      need(*idx, at::kLong, "ps idx");
+      TORCH_CHECK(perm->dim() == 2 && perm->size(1) == idx->numel(), "ps: perm must be [nbatches][B]");
+      TORCH_CHECK(idx->numel() % 2 == 0, "ps: batch size must be even");
+      TORCH_CHECK(nbatches_ == 0 || perm->size(0) == nbatches_, "ps: perm rows != scheduled nbatches");
+      a.perm = reinterpret_cast<const long long*>(perm->data_ptr());
+      a.idx = reinterpret_cast<long long*>(idx->data_ptr());
+      a.nbatches = perm->size(0);
+      a.B = (int)idx->numel();
+    }
+    check_hip(dfa::ps_excl_step(a, cur_stream()), "ps_excl_step");
+  }
+  uintptr_t excl_gate() const {
+    TORCH_CHECK(world_ == 1, "ps: one rank");
+    return reinterpret_cast<uintptr_t>(reinterpret_cast<unsigned*>(local_ + 1024) + dfa::kPSDecisionWord);
+  }
+  uintptr_t excl_mirror() const {
+    TORCH_CHECK(world_ == 1 && shard_[0] != nullptr, "ps: one rank, opened");
+    return reinterpret_cast<uintptr_t>(shard_[0]);
+  }
   void apply(torch::Tensor g, double lr, int64_t max_stale) {
     dfa::PSArgs a = args();
     need(g, at::kFloat, "ps grad");
@@ -2307,7 +2341,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("idx_stream") = py::none(), py::arg("idx_cursor") = py::none(), py::arg("idx_dst") = py::none(),
         py::arg("descs_host") = py::none(), py::arg("lenet_frag") = py::none(), py::arg("frag_w1") = 0,
         py::arg("frag_w2") = 0, py::arg("lenet_snap") = py::none(), py::arg("step_stats") = py::none(),
-        py::arg("run_stats") = py::none());
+        py::arg("run_stats") = py::none(), py::arg("gate") = 0, py::arg("mirror") = 0);
   m.def("sum_buffers", &sum_buffers_py);
   m.def("graph_upload", [](uintptr_t exec) {
     // stage an instantiated graph's kernel arguments / launch packets on the device now, outside any
@@ -2430,6 +2464,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_lr_source", &PSComm::set_lr_source)
       .def_property_readonly("shard_len", &PSComm::shard_len)
       .def_property_readonly("nshards_used", &PSComm::nshards_used)
+      .def("excl_step", &PSComm::excl_step, py::arg("max_stale"), py::arg("perm") = py::none(),
+           py::arg("idx") = py::none())
+      .def("excl_gate", &PSComm::excl_gate)
+      .def("excl_mirror", &PSComm::excl_mirror)
       .def("fetch_pull", &PSComm::fetch_pull, py::arg("w"), py::arg("perm") = py::none(), py::arg("idx") = py::none())
       .def("apply", &PSComm::apply, py::arg("g"), py::arg("lr"), py::arg("max_stale"))
       .def("stats", &PSComm::stats)

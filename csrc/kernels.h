@@ -200,6 +200,10 @@ struct IndexStream {  // next-batch staging folded into the optimizer launch (cs
   // this step's [loss sum, correct] to run_stats[0..1] and counts the applied update in run_stats[2]
   const float* step_stats;
   float* run_stats;
+  // async PS, exclusive writer (csrc/async_ps.hip ps_excl_step): the update runs only when the admission
+  // word *gate says accepted, and every new weight is also written to mirror (the rank's master shard)
+  const unsigned* gate;
+  float* mirror;
 };
 hipError_t sgd_multi(const ParamDesc* descs, int ndesc, int total_blocks, float* master, const float* grad,
                      float* mom_buf, bf16* wbf, const float* hyper, int apply_update, hipStream_t st,
@@ -450,9 +454,13 @@ hipError_t fed_pull(const FedArgs& a, hipStream_t st);
 hipError_t fed_upload(const FedArgs& a, hipStream_t st);
 hipError_t fed_apply(const FedArgs& a, hipStream_t st);
 constexpr int kPSVMinWord = 4;  // scratch word of the refresh minimum (ps_device.h kPSVMin)
+constexpr int kPSDecisionWord = 3;  // scratch word of the tagged admission decision (ps_device.h kPSDecision)
 constexpr long long kPSMaxBatches = 1 << 20;  // capacity of the shared completion arrays
 hipError_t ps_fetch_pull(const PSArgs& a, hipStream_t st);
 hipError_t ps_apply(const PSArgs& a, hipStream_t st);
+// exclusive writer (one rank): admission of this step's gradient, the next microbatch's claim and index
+// staging, in one workgroup; the update itself is the optimizer launch gated on the decision
+hipError_t ps_excl_step(const PSArgs& a, hipStream_t st);
 // shard self-test: every rank adds (rank + 1) * (j + 1) to word j of every shard's test area, n words
 hipError_t ps_selftest_add(const PSArgs& a, float* const* words, int n, float rank1, hipStream_t st);
 

@@ -34,7 +34,8 @@ template <typename DT>
 __device__ __forceinline__ void sgd_multi_body(const DT& descs, int ndesc,
                                                float* __restrict__ master, const float* __restrict__ grad,
                                                float* __restrict__ mom_buf, bf16* __restrict__ wbf,
-                                               const float* __restrict__ hyper, int apply_update, int bid) {
+                                               const float* __restrict__ hyper, int apply_update, int bid,
+                                               float* __restrict__ mirror = nullptr) {
   const int di = find_desc(descs, ndesc, bid);
   const ParamDesc d = descs[di];
   const int base = (bid - d.block_start) * SGD_ELEMS_PER_BLOCK;
@@ -51,6 +52,7 @@ __device__ __forceinline__ void sgd_multi_body(const DT& descs, int ndesc,
       w = sgd_new_weight(w, grad[d.off + i], mom != 0.f ? mom_buf[d.off + i] : 0.f, lr, mom, wd, gs, nesterov, &v);
       if (mom != 0.f) mom_buf[d.off + i] = v;
       master[d.off + i] = w;
+      if (mirror != nullptr) mirror[d.off + i] = w;
     }
     return w;
   };
@@ -173,10 +175,13 @@ __global__ void __launch_bounds__(256) sgd_multi_stream_kernel(const ParamDesc* 
                                                                const float* __restrict__ hyper, int apply_update,
                                                                int total_blocks, IndexStream is) {
   if ((int)blockIdx.x < total_blocks) {
+    // async PS exclusive writer: a rejected / finished step leaves the weights (and their copies) as they are
+    if (is.gate != nullptr && (__hip_atomic_load(is.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 7u) != 1u)
+      return;
     if (INL)
-      sgd_multi_body(tab.d, ndesc, master, grad, mom_buf, wbf, hyper, apply_update, blockIdx.x);
+      sgd_multi_body(tab.d, ndesc, master, grad, mom_buf, wbf, hyper, apply_update, blockIdx.x, is.mirror);
     else
-      sgd_multi_body(descs, ndesc, master, grad, mom_buf, wbf, hyper, apply_update, blockIdx.x);
+      sgd_multi_body(descs, ndesc, master, grad, mom_buf, wbf, hyper, apply_update, blockIdx.x, is.mirror);
     return;
   }
   int fb = blockIdx.x - total_blocks;
@@ -201,6 +206,7 @@ hipError_t sgd_multi(const ParamDesc* descs, int ndesc, int total_blocks, float*
   IndexStream isv{};
   if (is != nullptr) isv = *is;
   if (!stream) isv.src = nullptr, isv.run_stats = nullptr;
+  if ((isv.gate != nullptr || isv.mirror != nullptr) && (frag || !apply_update)) return hipErrorInvalidValue;
   if (frag && apply_update && is->snap == nullptr) return hipErrorInvalidValue;
   const int grid = total_blocks + (stream ? 1 : 0) + (frag ? kLeNetFragBlocks : 0);
   if (host_descs != nullptr && ndesc <= kInlineDescs) {

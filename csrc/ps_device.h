@@ -31,7 +31,7 @@ namespace dfa {
 // local scratch words (PSArgs::scratch, u32 index)
 // kPSVMin: min over this step's refreshing workgroups of (applied read before the copy [+ 1 for its own
 // admitted add]); reset to kPSNoVer by the admission that consumes it
-constexpr int kPSPullDone = 0, kPSApplyDone = 1, kPSEpoch = 2, kPSDecision = 3, kPSVMin = kPSVMinWord, kPSSlots = 64;
+constexpr int kPSPullDone = 0, kPSApplyDone = 1, kPSEpoch = 2, kPSDecision = kPSDecisionWord, kPSVMin = kPSVMinWord, kPSSlots = 64;
 // owner-applies words: the admitted sequence number, the pull launches' epoch, the drain decision's epoch
 // and, per shard, the first sequence number and the count this launch drains
 constexpr int kPSSeq = 5, kPSPullEp = 6, kPSDrain = 7, kPSDrainP = 8, kPSDrainN = 16;  // (+ shard, < 8 each)

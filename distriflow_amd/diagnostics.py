@@ -10,6 +10,9 @@ Python switches (default in brackets):
   lenet_fused [1]          whole-network LeNet-5 kernels (0: per-layer kernels)
   lenet_fused_update [1]   the reduce launch applies the SGD update (0: separate optimizer launch)
   async_fused [1]          async PS step = train + reduce/apply (0: pull / compute / apply launches)
+  ps_excl_fused [1]        async PS with one rank, models other than the fused LeNet-5: admission + next claim
+                           in one workgroup and the model's optimizer launch gated on the decision (0: pull /
+                           refresh / compute / ps_apply launches)
   ps_owner_apply [0]       async PS apply without remote atomics: gradients pushed into the shard owners'
                            inbox rings, each owner adds them into its shard during its next pull (the
                            default per-element CAS adds: profiles/r5/ps_cas_adds_per_us_1gpu.jsonl)
@@ -46,7 +49,7 @@ from __future__ import annotations
 
 import os
 
-_DEFAULTS = {"lenet_fused": 1, "lenet_fused_update": 1, "async_fused": 1, "ps_owner_apply": 0, "kcnn_fused": 1, "khead_fused": 1, "fold_dropout": 1,
+_DEFAULTS = {"lenet_fused": 1, "lenet_fused_update": 1, "async_fused": 1, "ps_owner_apply": 0, "ps_excl_fused": 1, "kcnn_fused": 1, "khead_fused": 1, "fold_dropout": 1,
              "lenet_succ": 1, "multistep": 1, "graph_steps": 64, "fused_selftest": 1, "wgrad_overlap": 0, "proj_overlap": 0, "concurrent_backward": 0, "bn_epilogue": 0,
              "bn_fused": 0, "bn_acc": 1, "bn_acc_rep": 8}
 

@@ -263,17 +263,22 @@ class ParamStore:
         if momentum != 0.0 and self.momentum is None:
             self.momentum = torch.zeros_like(self.master)
 
-    def sgd_step(self, index_stream=None, run_stats=None):
+    def sgd_step(self, index_stream=None, run_stats=None, ps_gate: int = 0, ps_mirror: int = 0):
         """w -= lr * (grad_scale * g [+ wd w]) (momentum optional); uses the device-side hyper tensor.
         ``index_stream = (stream [nsteps][B], cursor [1], dst [B])`` (GPU): the same launch stages the
         next step's batch indices into ``dst`` and advances ``cursor`` (csrc/optim.hip).
         ``run_stats = (step_stats [2], run [3])``: that workgroup also accumulates the step's
-        [loss sum, correct] and counts the update (device run statistics, no extra launch)."""
+        [loss sum, correct] and counts the update (device run statistics, no extra launch).
+        ``ps_gate`` / ``ps_mirror`` (device addresses, async PS with one rank: PSComm.excl_gate / excl_mirror):
+        the update runs only if the admission word says accepted, and the new weights are also written to
+        the parameter server's shard."""
         if self.compute_bf16:
             src, cur, dst = index_stream if index_stream is not None else (None, None, None)
             kw = self._frag_kw(True)
             if run_stats is not None:
                 kw.update(step_stats=run_stats[0], run_stats=run_stats[1])
+            if ps_gate:
+                kw.update(gate=int(ps_gate), mirror=int(ps_mirror))
             native.require().sgd_multi(self._descs, self._ndesc, self._sgd_blocks, self.master, self.grad,
                                        self.momentum, self.wbf, self.hyper, True, src, cur, dst,
                                        self._descs_host, **kw)

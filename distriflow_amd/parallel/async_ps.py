@@ -132,6 +132,13 @@ class AsyncPSTrainer(DataParallelTrainer):
             # slots), so every rank's workgroups waiting for their admission decision fit on the chip beside
             # the other ranks' (one rank per GPU: one workgroup per slot, all resident)
             net.lenet_exch_blocks = shared_gpu_exch_blocks(self.world)
+        # one rank, any other model: the exclusive writer's step -- admission + next claim in one workgroup,
+        # then the model's own optimizer launch gated on the decision, writing the new weights to the local
+        # master, the compute copies and the shard in one pass (no pull copy, no refresh, no separate apply)
+        h = net.store._hyper_host
+        self.excl_fused = (self.world == 1 and not self.fused_ps and not self.owner_apply
+                           and net.store.compute_bf16 and net.store.lenet_frag is None and diag_on("ps_excl_fused")
+                           and h[1] == 0.0 and h[2] == 0.0 and h[3] == 1.0)
         self._primed = False
         self._ps_stats_dev = self.ps.stats_tensor()  # device view of this rank's PS counters (callbacks)
         from .watchdog import register_owner_probe
@@ -170,14 +177,15 @@ class AsyncPSTrainer(DataParallelTrainer):
     # ------------------------------------------------------------------ one step
     def _prime(self):
         """Fused path prologue (eager, once per schedule): claim the first microbatch and pull the master
-        into the local weights and compute copies; every later step's reduce launch does both itself."""
-        if self.fused_ps and not self._primed:
+        into the local weights and compute copies; every later step's reduce launch (or, one rank: its
+        admission workgroup and gated optimizer launch) does both itself."""
+        if (self.fused_ps or self.excl_fused) and not self._primed:
             self.ps.fetch_pull(self.net.store.master, self._perm, self.idx)
             self.net.store.refresh_compute()
             self._primed = True
 
     def _gather(self):
-        if self.fused_ps:
+        if self.fused_ps or self.excl_fused:
             super()._gather()  # labels through the staged indices (no launch)
             return
         self.ps.fetch_pull(self.net.store.master, self._perm, self.idx)
@@ -190,12 +198,18 @@ class AsyncPSTrainer(DataParallelTrainer):
                       ps_max_stale=int(self.max_staleness))
             return self.net.compute_gradients_and_update(x, y, None, run_stats=self.run_stats, ps=ps)
         stats = self.net.compute_gradients(x, y)
+        if self.excl_fused:
+            self.ps.excl_step(int(self.max_staleness), self._perm, self.idx)
+            self.net.store.sgd_step(ps_gate=self.ps.excl_gate(), ps_mirror=self.ps.excl_mirror())
+            return stats
         self.ps.apply(self.net.store.grad, self.lr, self.max_staleness)
         return stats
 
     @property
     def step_launches(self) -> str:
-        return "train+reduce/ps-apply/refresh/claim" if self.fused_ps else "pull+refresh+compute+ps-apply"
+        if self.fused_ps:
+            return "train+reduce/ps-apply/refresh/claim"
+        return "compute+admit/claim+gated-update" if self.excl_fused else "pull+refresh+compute+ps-apply"
 
     def prepare_run(self, n: int):
         self._prime()

@@ -20,7 +20,7 @@ from mp_util import init_rank
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("model", ["lenet5", "mlp_mnist"])
+@pytest.mark.parametrize("model", ["lenet5", "mlp_mnist", "keras_cnn"])
 def test_async_single_worker_matches_sync_sgd(model):
     """One worker, staleness 0: asynchronous SGD degenerates to serial SGD on the same batch order
     (fused LeNet-5 path and the generic pull / apply path)."""
@@ -36,6 +36,7 @@ def test_async_single_worker_matches_sync_sgd(model):
     s = build_model(model, device=dev, seed=0)
     ta = AsyncPSTrainer(a, lr=0.05, max_staleness=0, graph="none")
     assert ta.fused_ps == (model == "lenet5")
+    assert ta.excl_fused == (model != "lenet5")  # one rank: admission + gated optimizer launch
     ta.bind_dataset(data, labels, 256, scale=1.0 / 255.0)
     ta.bind_schedule(perm)
     ts = DataParallelTrainer(s, lr=0.05, graph="none")
@@ -49,6 +50,39 @@ def test_async_single_worker_matches_sync_sgd(model):
     assert st["accepted"] == 12 and st["rejected"] == 0 and st["version"] == 12 and st["error"] == 0
     w = ta.pull_master().clone()
     torch.testing.assert_close(w, s.store.master, rtol=1e-5, atol=1e-6)
+
+
+def test_async_excl_fused_matches_generic_path(monkeypatch):
+    """One rank, a model without the fused LeNet-5 step: the exclusive writer's step (admission + claim in one
+    workgroup, the optimizer launch gated on the decision and mirroring into the shard) against the generic
+    pull / refresh / compute / ps_apply launches, replayed from a captured multi-step graph: the same
+    decisions and the same master (shard) within the update's rounding, and the local master equals the
+    shard exactly."""
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.async_ps import AsyncPSTrainer
+    from distriflow_amd.parallel.data_parallel import epoch_permutations
+
+    dev = torch.device("cuda", 0)
+    data, labels = synthetic_mnist(4096, seed=3, device=dev)
+    perm = epoch_permutations(4096, 256, 16, dev, seed=1)
+    res = {}
+    for fused in (0, 1):
+        monkeypatch.setenv("DISTRIFLOW_DIAG", f"ps_excl_fused={fused}")
+        net = build_model("keras_cnn", device=dev, seed=0)
+        tr = AsyncPSTrainer(net, lr=0.05, max_staleness=2, graph="full")
+        assert tr.excl_fused == bool(fused)
+        tr.bind_dataset(data, labels, 256, scale=1.0 / 255.0)
+        tr.bind_schedule(perm)
+        tr.prepare_run(8)
+        tr.run(16)
+        torch.cuda.synchronize()
+        st = tr.ps_stats()
+        assert st["accepted"] == 16 and st["rejected"] == 0 and st["error"] == 0, st
+        res[fused] = tr.pull_master(torch.empty_like(net.store.master)).clone()
+        if fused:
+            assert torch.equal(res[fused], net.store.master)
+    torch.testing.assert_close(res[1], res[0], rtol=1e-5, atol=1e-6)
 
 
 def test_async_multistep_graph_matches_single_steps():
