@@ -495,6 +495,9 @@ struct LeNetArgs {
   // async PS: one extra workgroup (index nblk) admits this step's gradient while the others train, so the
   // reduce launch's owners find the decision already published (csrc/lenet_fused.hip)
   int nblk, ps_admit;
+  // ps_admit with one rank (the exclusive writer, lenet_reduce_kernel<3>): the admission also advances the
+  // launch epoch and publishes the applied count itself (the reduce launch has no arrival protocol)
+  int ps_excl;
   PSArgs ps;
 };
 struct LeNetDense {
@@ -569,6 +572,9 @@ struct LeNetRedArgs {
   unsigned* gran_ep;         // [grid] per-workgroup launch counters (each workgroup reads / bumps its own)
   unsigned* gran_err;        // sticky: a granule wait timed out
   unsigned* slot_arr;        // [slots] async PS: owners of a slot done (the eighth arrives for the slot)
+  // async PS with one rank (mode 3: the synchronous owners' update gated on the train launch's admission):
+  // every new weight is also written here (the rank's master shard); null otherwise
+  float* mirror;
 };
 // The reference CNN's conv block (csrc/kcnn_fused.hip): conv1 3x3x1->32 + ReLU, conv2 3x3x32->32 + ReLU,
 // 2x2 max-pool [+ folded dropout], input 28x28x1, in one forward and one backward launch (+ reduce).

@@ -297,7 +297,7 @@ __device__ __forceinline__ int lenet_img_group(int b, int nb) {
 // lock-free CAS on the shared version, decision published for the reduce launch's owners (epoch-tagged
 // with that launch's epoch, which no one advances before it runs), the refresh minimum recorded, then the
 // microbatch's completion
-__device__ __forceinline__ void lenet_ps_admission(const PSArgs& p) {
+__device__ __forceinline__ void lenet_ps_admission(const PSArgs& p, bool excl) {
   const long long bid = *p.bid_out;  // (the reduce launch's claim workgroup overwrites it after the decision)
   const unsigned applied0 = ps_read_applied(p);
   const unsigned ep = __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
@@ -308,12 +308,19 @@ __device__ __forceinline__ void lenet_ps_admission(const PSArgs& p) {
   // relaxed: the decision's readers are the next (reduce) launch, behind the kernel boundary (a release
   // here wrote back this XCD's L2 under the running train kernel)
   __hip_atomic_store(p.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (excl) {
+    // one rank (reduce mode 3): this launch's epoch is current from here on, and the count of applied
+    // gradients can include this one already -- its only reader is this rank's next admission, which
+    // follows the reduce launch that applies it
+    __hip_atomic_store(p.scratch + kPSEpoch, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dec == kPSAccept) ps_publish_applied(p);
+  }
   if (dec == kPSAccept && p.done_epoch != nullptr) complete_microbatch(p, bid);
 }
 
 __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs a) {
   if ((int)blockIdx.x >= a.nblk) {  // async PS: the admission workgroup
-    if (a.ps_admit && threadIdx.x == 0) lenet_ps_admission(a.ps);
+    if (a.ps_admit && threadIdx.x == 0) lenet_ps_admission(a.ps, a.ps_excl != 0);
     return;
   }
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1060,6 +1067,7 @@ template <bool DENSE>
 __device__ __forceinline__ void red_emit(const LeNetRedArgs& a, const RedTables& t, Owned o, float w) {
   const ParamDesc& d = t.d[o.di];
   a.sgd.master[d.off + o.i] = w;
+  if (a.mirror != nullptr) a.mirror[d.off + o.i] = w;  // mode 3: the rank's master shard
   if (DENSE) {
     if (d.bf_off < 0) return;  // a bias
     const int K = d.T * d.Ci;
@@ -1190,7 +1198,10 @@ __device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, unsigned 
 // kernel; each workgroup runs its path once, cold).
 template <int MODE>
 __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
-  constexpr bool LL = MODE == 1, PS = MODE == 2;
+  // MODE 3 (async PS, one rank): the synchronous owners' fused update, gated on the train launch's admission
+  // decision and mirrored into the rank's master shard; no arrival protocol (the admission advanced the
+  // epoch and published the applied count, ps_device.h)
+  constexpr bool LL = MODE == 1, PS = MODE == 2, PSX = MODE == 3;
   __shared__ float red[4 * kSlotVals];
   __shared__ RedTables tabs;
   __shared__ int owned[kMaxOwned];
@@ -1225,6 +1236,13 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       // this launch's epoch: the counter load goes out now and is waited for only after the job (a wait
       // here put a whole memory round trip in front of every job)
       const unsigned ge_prev = threadIdx.x == 0 ? a.gran_ep[blockIdx.x] : 0u;
+      // mode 3: the admission's epoch and decision words (written by the train launch), consumed after the job
+      unsigned psx_ep = 0u, psx_dec = 0u;
+      if (PSX && threadIdx.x == 0) {
+        psx_ep = __hip_atomic_load(a.ps.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        psx_dec = __hip_atomic_load(a.ps.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __shared__ int s_gate;
       __syncthreads();  // the tables staged above are read by every thread of the job
       float part[kPerThread];
       if (grp < nslot) {
@@ -1232,7 +1250,14 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
         else conv_job(a, grp - a.dense_tiles, c, red, part);
         LR_STAMP(6);
       }
-      if (threadIdx.x == 0) s_ge = ge_prev + 1u;
+      if (threadIdx.x == 0) {
+        s_ge = ge_prev + 1u;
+        if (PSX) {
+          const bool mine_ep = ps_epoch_eq(psx_dec, psx_ep);
+          s_gate = mine_ep && (psx_dec & 7u) == kPSAccept;
+          if (!mine_ep && blockIdx.x == 0) atomicOr(a.ps.stats + 5, 8ull);  // (never expected: no update)
+        }
+      }
       __syncthreads();
       const unsigned ge = s_ge;
       if (grp < nslot) {
@@ -1433,7 +1458,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
             }
             LR_STAMP(5);
           }
-          if (ok && o.di >= 0) {
+          if (ok && o.di >= 0 && (!PSX || s_gate)) {
             if (dense) red_apply<true>(a, tabs, o, v, w0, m0);
             else red_apply<false>(a, tabs, o, v, w0, m0);
           }
@@ -1632,6 +1657,28 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     return;
   }
   const int blk = blockIdx.x - G;
+  if (blk == 1 && PSX) {
+    LR_FLUSH();
+    return;
+  }
+  if (blk == 2 && PSX) {
+    // mode 3: the admission (train launch) has read this step's microbatch id already: claim the next one
+    // and stage its example indices straight away
+    __shared__ long long s_bidx;
+    LR_STAMP(8);
+    if (a.ps.done_epoch != nullptr) {
+      claim_microbatch(a.ps, threadIdx.x, &s_bidx);
+    } else if (threadIdx.x == 0) {
+      s_bidx = (long long)(__hip_atomic_fetch_add(a.ps.batch_ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) %
+                           (unsigned long long)(a.ps.nbatches > 0 ? a.ps.nbatches : 1));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *a.ps.bid_out = s_bidx;
+    ps_stage_indices(a.ps, s_bidx, threadIdx.x, RT);
+    LR_STAMP(10);
+    LR_FLUSH();
+    return;
+  }
   if (blk == 1 && PS) {
     // async: the admission ran in the train launch (lenet_ps_admission); this workgroup's arrival keeps the
     // launch epoch from advancing before the decision of this launch exists
@@ -1786,8 +1833,6 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   if (r.ps_on && (!r.ps.ver || !r.ps.vpulled || !r.ps.bid_out || !r.ps.stats || !r.ps.scratch))
     return hipErrorInvalidValue;
   if (r.ps_on) a.ps = r.ps;
-  hipLaunchKernelGGL(lenet_train_kernel, dim3(nblk + (r.ps_on ? 1 : 0)), dim3(NT), LDS_BYTES, st, a);
-  DFA_HIP_CHECK(hipGetLastError());
   r.nblk = nblk;
   r.ldt = a.ldt;
   if (r.kcols <= 0 || r.kcols % 32 || r.kcols > a.ldt || r.kcols < a.B) return hipErrorInvalidValue;
@@ -1854,10 +1899,19 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
       if (!r.ps.shard[k]) return hipErrorInvalidValue;
     if (r.ps.owner_ring > 0) return hipErrorInvalidValue;  // owner-applies runs the generic pull / apply
   }
+  // async PS with one rank and successor ownership: mode 3 (the synchronous owners' update gated on the
+  // admission, mirrored into the one shard; the admission advances the epoch itself).  Decided before the
+  // train launch, whose admission workgroup runs the matching protocol.
+  const bool psx = r.ps_on && r.ps.excl != 0 && r.succ && r.ps.nshards == 1 && r.ps.owner_ring <= 0;
+  a.ps_excl = psx ? 1 : 0;
+  r.mirror = psx ? r.ps.shard[0] : nullptr;
+  hipLaunchKernelGGL(lenet_train_kernel, dim3(nblk + (r.ps_on ? 1 : 0)), dim3(NT), LDS_BYTES, st, a);
+  DFA_HIP_CHECK(hipGetLastError());
   // the index-staging workgroup; async PS: the admission and the claim / staging workgroups
   const int extra = r.ps_on ? 2 : ((r.sgd_on && r.sgd.src) ? 1 : 0);
   const dim3 grid(r.exch_blocks + 1 + extra);
   if (r.ll_on) hipLaunchKernelGGL(lenet_reduce_kernel<1>, grid, dim3(RT), 0, st, r);
+  else if (psx) hipLaunchKernelGGL(lenet_reduce_kernel<3>, grid, dim3(RT), 0, st, r);
   else if (r.ps_on) hipLaunchKernelGGL(lenet_reduce_kernel<2>, grid, dim3(RT), 0, st, r);
   else hipLaunchKernelGGL(lenet_reduce_kernel<0>, grid, dim3(RT), 0, st, r);
   return hipGetLastError();
