@@ -254,13 +254,16 @@ def main():
             ael, _ = timed(atr, async_steps)
             aval = world * B * async_steps / ael
             # the sync trainer timed again right after, the same way: the GPU's clocks ramp up over the first
-            # ~15 ms of load (profiles/r5/lenet_clock_ramp.txt), so the first sync run is colder than the async
-            # one; the ratio compares the two adjacent runs
+            # ~15 ms of load (profiles/r5/lenet_clock_ramp.txt), so the sync run before the async one is colder
+            # and the one after it warmer; the ratio is against their mean step time (the async run sits
+            # between them)
             sel2, _ = timed(trainer, async_steps)
-            sval2 = world * B * async_steps / sel2
-            async_rec = dict(images_per_s=round(aval, 1), ms_per_step=round(ael / async_steps * 1e3, 4),
-                             steps=async_steps, speedup_vs_sync=round(aval / sval2, 4),
+            sync_ms = 0.5 * (elapsed / args.steps + sel2 / async_steps) * 1e3
+            async_ms = ael / async_steps * 1e3
+            async_rec = dict(images_per_s=round(aval, 1), ms_per_step=round(async_ms, 4),
+                             steps=async_steps, speedup_vs_sync=round(sync_ms / async_ms, 4),
                              sync_rerun_ms_per_step=round(sel2 / async_steps * 1e3, 4),
+                             sync_bracket_ms_per_step=round(sync_ms, 4),
                              speedup_vs_first_sync=round(aval / value, 4),
                              max_staleness_bound=args.max_staleness, **atr.ps_stats())
         except Exception as e:  # reported, never fatal to the headline number
