@@ -58,11 +58,16 @@ def _C():
     return _DebugSync(mod) if _DEBUG else mod
 
 
-def graph_upload(g) -> None:
+def graph_upload(g) -> bool:
     """hipGraphUpload of a captured ``torch.cuda.CUDAGraph`` on the current stream: the graph's launch
     resources are staged on the device at capture time, so its first replay (often the first one inside a
-    timed region) costs what every later one does."""
-    _C().graph_upload(int(g.raw_cuda_graph_exec()))
+    timed region) costs what every later one does.  An optimisation only: a graph the runtime will not
+    upload (returns False) is replayed as it is."""
+    try:
+        _C().graph_upload(int(g.raw_cuda_graph_exec()))
+        return True
+    except (RuntimeError, AttributeError):
+        return False
 
 
 def _geom(SH=1, SW=1, SC=1, OH=1, OW=1, KH=1, KW=1, stride=1, pad=0):
