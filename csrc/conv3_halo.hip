@@ -63,6 +63,10 @@ struct C3P {
   int tps;           // tiles per workgroup (the persistent 64 -> 64 kernel)
   int ks, cbs;       // split over input channel blocks: ks splits of cbs blocks (ks > 1: raw fp32 partials)
   float* ws;         // [ks][M][Cout] partials, summed + epilogue by igemm64_splitk_combine
+  // ks > 1 with tick: no combine launch -- each split writes its partial through to memory and takes a
+  // ticket of its output tile; the tile's last arriver sums the partials in split order and runs the
+  // kernel's own epilogue (the last arriver resets the ticket)
+  unsigned* tick;
   int relu;
   float alpha;
   BnAcc bacc;        // BatchNorm sums of the stored output (ks == 1; csrc/bn_acc.h)
@@ -309,7 +313,47 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
   }
 
   // C/D layout: row (output channel) 4 * (lane >> 4) + r, column (pixel) lane & 15
-  if (p.ks == 1 && p.bacc.acc) {
+  if (p.ks > 1 && p.tick != nullptr) {
+    // the split-K partial written through (sc1) to the workspace, then the tile's ticket; only the last of
+    // the ks splits goes on, with the ks partials summed in split order (its own from registers)
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        p.ws, (short)0, (int)((long long)p.ks * p.ntiles * kCP * p.Cout * 4), 0x00020000);
+    auto woff = [&](int sp, int t, int u) -> int {
+      const long long m = (long long)tile * kCP + wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
+      const int co = co0 + wn * (BN / 2) + 16 * u + 4 * fc;
+      return (int)((((long long)sp * p.ntiles * kCP + m) * p.Cout + co) * 4);
+    };
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[u][t]), wr, woff(ksp, t, u), 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's partial stores are written through
+    __syncthreads();
+    __shared__ int s_last;
+    if (tid == 0) {
+      const unsigned prev = __hip_atomic_fetch_add(p.tick + lt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = prev == (unsigned)(p.ks - 1);
+      if (s_last) __hip_atomic_store(p.tick + lt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the ticket)
+    // ks == 2 (the host's condition): the other split's partial added to this one's -- p0 + p1 is the same
+    // fp32 value whichever of the two arrives last, so the result does not depend on the arrival order
+    const int other = 1 - ksp;
+    f32x4 part[4][TN];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+        part[t][u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, woff(other, t, u), 0, 16));
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u) acc[u][t] = ksp == 0 ? acc[u][t] + part[t][u] : part[t][u] + acc[u][t];
+  }
+  if ((p.ks == 1 || p.tick != nullptr) && p.bacc.acc) {
     // BatchNorm sums of the stored values (csrc/bn_acc.h): per channel group u over the lane's 4 pixels,
     // the 16 lanes of the group, then the two pixel-half waves through LDS slots
     const bool two = p.bacc.acc2 != nullptr;
@@ -355,7 +399,7 @@ __global__ void __launch_bounds__(256, 2) conv3_halo_kernel(C3P p) {
     bacc_flush(p.bacc, red, 2, BN, co0, p.Cout, tid, 256);
     return;
   }
-  if (p.ks > 1) {  // raw partials of this split's channel blocks
+  if (p.ks > 1 && p.tick == nullptr) {  // raw partials of this split's channel blocks (combine launch)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const long long m = (long long)tile * kCP + wm * 64 + 32 * (t >> 1) + 2 * fl + (t & 1);
@@ -600,6 +644,25 @@ __global__ void __launch_bounds__(512, 1) conv3_halo_c64_kernel(C3P p) {
   }
 }
 
+// per-tile tickets of the folded split-K combine: zeroed once, each tile's last arriver resets its own, so
+// the buffer is zero between launches (graph replays included).  Allocated outside any stream capture
+// (null -- the combine launch -- if the first request comes during one).
+constexpr int kC3Tickets = 1024;
+unsigned* c3_tickets(hipStream_t st) {
+  static unsigned* t = nullptr;
+  if (t != nullptr) return t;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  unsigned* b = nullptr;
+  if (hipMalloc(&b, kC3Tickets * sizeof(unsigned)) != hipSuccess) return nullptr;
+  if (hipMemset(b, 0, kC3Tickets * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(b);
+    return nullptr;
+  }
+  t = b;
+  return t;
+}
+
 bool c3_geom(int H, int W, int& R, int& TI) {
   if (W < 4 || W > 64 || kCP % W != 0) return false;
   const int rpt = kCP / W;
@@ -674,6 +737,13 @@ hipError_t conv3_halo(const IGemmArgs& a, int mode, hipStream_t st) {
       ks *= 2;
     if (ks > 1) p.ks = ks, p.cbs = ncb / ks, p.ws = a.splitk_ws;
   }
+  // two splits: the tile's last arriver combines and runs the epilogue in this launch (c3_tickets); the
+  // combine launch otherwise
+  p.tick = nullptr;
+  static const int fold = diag_int("conv_halo_fold", 1);
+  if (fold && p.ks == 2 && p.ntiles * p.nco <= kC3Tickets &&
+      (long long)p.ks * p.ntiles * kCP * p.Cout * 4 < (1LL << 31))
+    p.tick = c3_tickets(st);
   const dim3 grid(p.ntiles * p.nco * p.ks);
   if (wide) {
     if (flip) hipLaunchKernelGGL((conv3_halo_kernel<128, true, false>), grid, dim3(256), 0, st, p);
@@ -689,7 +759,7 @@ hipError_t conv3_halo(const IGemmArgs& a, int mode, hipStream_t st) {
     }
   }
   DFA_HIP_CHECK(hipGetLastError());
-  if (p.ks > 1) {  // the combine applies the epilogue (and the BatchNorm sums)
+  if (p.ks > 1 && p.tick == nullptr) {  // the combine applies the epilogue (and the BatchNorm sums)
     IGemmArgs c = a;
     c.splits = p.ks;
     return igemm64_splitk_combine(c, st);
