@@ -13,6 +13,7 @@
 //   halo_groups=1   halo weight gradient with 4-wave workgroups (default: two groups sharing a slab)
 //   halo_wg=N       halo weight-gradient workgroup target    conv_halo=0     3x3 fwd/dgrad on igemm64
 //   conv_halo_c64=0 no weights-resident 64->64 kernel        conv_halo_splitk=0 / conv_halo_ks=N
+//   conv_halo_fold=0 two-split halo convs combined by a separate launch (default: the last arriver)
 //                                                            halo fwd/dgrad channel-block split (max N)
 #pragma once
 #include <cstdlib>
