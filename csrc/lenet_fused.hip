@@ -869,8 +869,8 @@ __global__ void __launch_bounds__(PT) lenet_prep_kernel(const float* __restrict_
 // ------------------------------------------------------------------------------------------------
 // Reductions in one launch, deterministic (fixed summation order everywhere).
 //
-// Slots: [0, dense_tiles) are 32 x 32 units of the dense weight gradients dW = dZ^T H (bias = input
-// column K); then nconv_slots slots of 256 conv parameters.  Every slot is split into kChunks = 8 jobs:
+// Slots: dense_tiles 32 x 32 units of the dense weight gradients dW = dZ^T H (bias = input column K) and
+// nconv_slots slots of 256 conv parameters (conv slots first by default: slot_dense / slot_conv).  Every slot is split into kChunks = 8 jobs:
 // dense job (u, c) sums batch columns [c * chunk_cols, (c + 1) * chunk_cols), conv job (s, c) the
 // partial rows of the train workgroups q = c (mod 8).  Job j = slot * 8 + c runs on workgroup j (mod G),
 // so with round-robin dispatch and G % 8 == 0 chunk c is always read on XCD c -- the XCD whose train
@@ -935,17 +935,29 @@ __device__ __forceinline__ int dense_unit(const RedTables& t, int u, int& tn, in
   return l;
 }
 
+// Slot order (a.conv_first): the conv slots -- the longest jobs -- first, so they are dispatched first and
+// run on CUs not yet shared with other jobs; 0: the dense units first.  slot_dense(): the dense unit of a
+// slot, or -1 for a conv slot; slot_conv(): the conv slot index.
+__device__ __forceinline__ int slot_dense(const LeNetRedArgs& a, int slot) {
+  if (a.conv_first) return slot >= a.nconv_slots ? slot - a.nconv_slots : -1;
+  return slot < a.dense_tiles ? slot : -1;
+}
+__device__ __forceinline__ int slot_conv(const LeNetRedArgs& a, int slot) {
+  return a.conv_first ? slot : slot - a.dense_tiles;
+}
+
 // the element of position pos (< kSlotVals) of `slot`
 __device__ __forceinline__ Owned owned_elem(const LeNetRedArgs& a, const RedTables& t, int slot, int pos) {
-  if (slot < a.dense_tiles) {
+  const int du = slot_dense(a, slot);
+  if (du >= 0) {
     int tn, tk;
-    const int l = dense_unit(t, slot, tn, tk);
+    const int l = dense_unit(t, du, tn, tk);
     const int N = t.L[l].N, K = t.L[l].K;
     const int on = kDU * tn + (pos >> 5), ok = kDU * tk + (pos & 31);
     if (on >= N || ok > K) return {-1, 0};
     return ok < K ? Owned{4 + 2 * l, on * K + ok} : Owned{5 + 2 * l, on};
   }
-  const int p = (slot - a.dense_tiles) * kConvPer + pos;
+  const int p = slot_conv(a, slot) * kConvPer + pos;
   if (pos >= kConvPer || p >= kLeNetConvParams) return {-1, 0};
   if (p < kLeNetPB1) return {0, p};
   if (p < kLeNetPW2) return {1, p - kLeNetPB1};
@@ -1246,8 +1258,8 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       __syncthreads();  // the tables staged above are read by every thread of the job
       float part[kPerThread];
       if (grp < nslot) {
-        if (grp < a.dense_tiles) dense_job(a, tabs, grp, c, red, part);
-        else conv_job(a, grp - a.dense_tiles, c, red, part);
+        if (slot_dense(a, grp) >= 0) dense_job(a, tabs, slot_dense(a, grp), c, red, part);
+        else conv_job(a, slot_conv(a, grp), c, red, part);
         LR_STAMP(6);
       }
       if (threadIdx.x == 0) {
@@ -1261,7 +1273,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       __syncthreads();
       const unsigned ge = s_ge;
       if (grp < nslot) {
-        const int npos = grp < a.dense_tiles ? kPerThread : 1;
+        const int npos = slot_dense(a, grp) >= 0 ? kPerThread : 1;
         unsigned long long* g = a.gran + ((long long)grp * kChunks + c) * kSlotVals + threadIdx.x;
 #pragma unroll
         for (int e = 0; e < kPerThread; ++e)
@@ -1279,7 +1291,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       }
       const int s = grp - 1;
       if (s >= 0) {
-        const bool dense = s < a.dense_tiles;
+        const bool dense = slot_dense(a, s) >= 0;
         const int cnt = dense ? kSlotVals / kChunks : kConvPer / kChunks;
         const int pos = c * cnt + (int)threadIdx.x;
         const bool mine = (int)threadIdx.x < cnt;
@@ -1481,11 +1493,11 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       const int slot = j / kChunks, c = j - kChunks * (j / kChunks);
       __syncthreads();  // red / tabs / s_last of the previous job
       float part[kPerThread];
-      if (slot < a.dense_tiles) dense_job(a, tabs, slot, c, red, part);
-      else conv_job(a, slot - a.dense_tiles, c, red, part);
+      if (slot_dense(a, slot) >= 0) dense_job(a, tabs, slot_dense(a, slot), c, red, part);
+      else conv_job(a, slot_conv(a, slot), c, red, part);
       if (j == (int)blockIdx.x) LR_STAMP(6);
       // publish the slab write-through, then the ticket (every storing wave drains first)
-      const int npos = slot < a.dense_tiles ? kPerThread : 1;
+      const int npos = slot_dense(a, slot) >= 0 ? kPerThread : 1;
       float* slab = a.slabs + (long long)slot * kChunks * kSlotVals;
 #pragma unroll
       for (int e = 0; e < kPerThread; ++e)
@@ -1570,7 +1582,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
 #pragma unroll 1
     for (int k = 0; k < nown; ++k) {
       const int slot = owned[k];
-      const int npos = slot < a.dense_tiles ? kPerThread : 1;
+      const int npos = slot_dense(a, slot) >= 0 ? kPerThread : 1;
       const float* sum = a.slabs + (long long)slot * kChunks * kSlotVals;
       // gather every position's element, local sum and old weight first (all loads in flight), then
       // the rank sums, then the arithmetic, then the stores: no load waits behind a store
@@ -1844,6 +1856,8 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
     base += r.L[l].tiles;
   }
   r.dense_tiles = base;
+  static const int conv_first = diag_int("lenet_conv_first", 1);
+  r.conv_first = conv_first;
   // the kernel's LDS table image
   for (int l = 0; l < 3; ++l) {
     r.tab.L[l] = r.L[l];
