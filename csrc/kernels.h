@@ -568,7 +568,6 @@ struct LeNetRedArgs {
   // last slot) each own one eighth of slot s's positions and sum its 8 chunks in chunk order (no ticket,
   // no slab reload: one hand-off).  A workgroup waits only on lower-indexed ones.
   int succ;
-  int conv_first;            // slot order: the conv slots (the longest jobs) first (csrc/lenet_fused.hip)
   unsigned long long* gran;  // [slots][8 chunks][1024]
   unsigned* gran_ep;         // [grid] per-workgroup launch counters (each workgroup reads / bumps its own)
   unsigned* gran_err;        // sticky: a granule wait timed out
