@@ -307,23 +307,27 @@ __global__ void __launch_bounds__(KT) khead_train_kernel(KHeadArgs a) {
     }
     __syncthreads();
     KH_STAMP(1);
-    // ---- P^T: work item = (column pair, 8-row piece); 4 consecutive lanes write the 4 pieces of one pT
-    // row, so a store instruction covers 16 rows x 64 contiguous bytes (not 64 scattered 16-byte pieces)
-    for (int w = tid; w < KC * 2; w += KT) {
-      const int cp = w >> 2, q = w & 3;
-      unsigned v[8];
+    // ---- P^T (the weight-gradient launch's operand): work item = (column pair, 8-row piece); 4 consecutive
+    // lanes write the 4 pieces of one pT row, so a store instruction covers 16 rows x 64 contiguous bytes.
+    // Written after the ticket (waiters: while the owner works; the owner: after publishing dZ1), not
+    // before the partial -- its stores were drained with the slab's in front of every ticket.
+    auto write_pT = [&]() {
+      for (int w = tid; w < KC * 2; w += KT) {
+        const int cp = w >> 2, q = w & 3;
+        unsigned v[8];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) v[r] = *reinterpret_cast<const unsigned*>(s.ps + (8 * q + r) * s.ldp + 2 * cp);
-      bf16x8 lo, hi;
+        for (int r = 0; r < 8; ++r) v[r] = *reinterpret_cast<const unsigned*>(s.ps + (8 * q + r) * s.ldp + 2 * cp);
+        bf16x8 lo, hi;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        lo[r] = __builtin_bit_cast(bf16, (unsigned short)(v[r] & 0xffffu));
-        hi[r] = __builtin_bit_cast(bf16, (unsigned short)(v[r] >> 16));
+        for (int r = 0; r < 8; ++r) {
+          lo[r] = __builtin_bit_cast(bf16, (unsigned short)(v[r] & 0xffffu));
+          hi[r] = __builtin_bit_cast(bf16, (unsigned short)(v[r] >> 16));
+        }
+        bf16* d0 = a.pT + (long long)(kc0 + 2 * cp) * a.ldt + r0 + 8 * q;
+        *reinterpret_cast<bf16x8*>(d0) = lo;
+        *reinterpret_cast<bf16x8*>(d0 + a.ldt) = hi;
       }
-      bf16* d0 = a.pT + (long long)(kc0 + 2 * cp) * a.ldt + r0 + 8 * q;
-      *reinterpret_cast<bf16x8*>(d0) = lo;
-      *reinterpret_cast<bf16x8*>(d0 + a.ldt) = hi;
-    }
+    };
     KH_STAMP(2);
     // ---- Z1 partial: wave w owns n-tiles 2w, 2w + 1 for both m-tiles.  KSC > 0 (the chunk depth known
     // at compile time): every W1 operand load is issued before the first MFMA (one exposed latency);
@@ -404,9 +408,12 @@ __global__ void __launch_bounds__(KT) khead_train_kernel(KHeadArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) __hip_atomic_store(flags + rt, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (tid == 0) {
-      while (__hip_atomic_load(flags + rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag)
-        __builtin_amdgcn_s_sleep(2);
+      write_pT();
+    } else {
+      write_pT();
+      if (tid == 0)
+        while (__hip_atomic_load(flags + rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag)
+          __builtin_amdgcn_s_sleep(2);
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
