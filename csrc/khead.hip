@@ -400,6 +400,28 @@ __global__ void __launch_bounds__(KT) khead_train_kernel(KHeadArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
     const unsigned tag = s_tag;
     KH_STAMP(4);
+    // the dP phase's W1^T operands (KSC > 0: the first two rolling groups) do not depend on dZ1: the waiters
+    // issue them before they wait for the owner's flag, the owner right after publishing
+    const int ntl = KC / 16, cnt = (ntl - wid + 3) / 4;
+    const bf16* wt = a.w1t + (long long)(kc0 + 16 * wid + (lane & 15)) * N1 + 8 * (lane >> 4);
+    constexpr int NTW = (2 * KSC + 3) / 4;  // tiles of the busiest wave (KSC > 0)
+    constexpr int TG = 3, NG = KSC > 0 ? (NTW + TG - 1) / TG : 1;
+    bf16x8 bb[NG][TG][4];
+    auto load_g = [&](int g) {
+#pragma unroll
+      for (int t = 0; t < TG; ++t)
+        if (g * TG + t < NTW && g * TG + t < cnt)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) bb[g][t][k] = ld16(wt + (long long)(64 * (g * TG + t)) * N1 + 32 * k);
+    };
+    auto load_first = [&]() {
+      if constexpr (KSC > 0) {
+        if (a.dp) {
+          load_g(0);
+          if (NG > 1) load_g(1);
+        }
+      }
+    };
     if (s_last) {
       f32x4 z[4];
       khead_combine(a, rt, z);
@@ -408,8 +430,10 @@ __global__ void __launch_bounds__(KT) khead_train_kernel(KHeadArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) __hip_atomic_store(flags + rt, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      write_pT();
+      load_first();
+      if (!a.dp) write_pT();  // (with dP: after its dZ1 loads are issued, below)
     } else {
+      load_first();
       write_pT();
       if (tid == 0)
         while (__hip_atomic_load(flags + rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag)
@@ -433,14 +457,17 @@ __global__ void __launch_bounds__(KT) khead_train_kernel(KHeadArgs a) {
         for (int k = 0; k < 4; ++k)
           za[m][k] = __builtin_bit_cast(
               bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, ((16 * m + (lane & 15)) * N1 + 32 * k + 8 * (lane >> 4)) * 2, 0, 16));
+      if (s_last) {  // the owner's P^T, its reads of the P tile done before any wave overwrites it with dP
+        write_pT();
+        __syncthreads();
+      }
       if (a.stamps && first) {  // diagnostic split of the phase: dZ1 arrival, then the W1^T operands
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         KH_STAMP(9);
       }
-      // column tiles of the chunk: wave w takes w, w + 4, ...; KSC > 0: all of the wave's W1^T operand
-      // loads issued before the first MFMA; otherwise two tiles per group with ping-pong buffers
-      const int ntl = KC / 16, cnt = (ntl - wid + 3) / 4;
-      const bf16* wt = a.w1t + (long long)(kc0 + 16 * wid + (lane & 15)) * N1 + 8 * (lane >> 4);
+      // column tiles of the chunk: wave w takes w, w + 4, ...; KSC > 0: the wave's W1^T operands in
+      // rolling groups (the first two issued before the flag wait, above); otherwise two tiles per group
+      // with ping-pong buffers
       auto tile = [&](int i, const bf16x8* bb) {
         f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -470,18 +497,6 @@ __global__ void __launch_bounds__(KT) khead_train_kernel(KHeadArgs a) {
       if constexpr (KSC > 0) {
         // rolling groups of 3 tiles, two groups in flight: ~96 operand VGPRs live instead of 144 (all nine
         // tiles' operands at once spill)
-        constexpr int NTW = (2 * KSC + 3) / 4;  // tiles of the busiest wave
-        constexpr int TG = 3, NG = (NTW + TG - 1) / TG;
-        bf16x8 bb[NG][TG][4];
-        auto load_g = [&](int g) {
-#pragma unroll
-          for (int t = 0; t < TG; ++t)
-            if (g * TG + t < NTW && g * TG + t < cnt)
-#pragma unroll
-              for (int k = 0; k < 4; ++k) bb[g][t][k] = ld16(wt + (long long)(64 * (g * TG + t)) * N1 + 32 * k);
-        };
-        load_g(0);
-        if (NG > 1) load_g(1);
         __builtin_amdgcn_sched_barrier(0);
         if (a.stamps && first) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
