@@ -339,12 +339,15 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
 // launch writes the new weights to the local master, its compute copies and the shard, in one pass).
 __global__ __launch_bounds__(kPSBlock) void ps_excl_step_kernel(PSArgs a) {
   const int t = threadIdx.x;
-  __shared__ long long s_bid;
-  if (t == 0) {
+  if (blockIdx.x == 0) {  // the admission (one thread)
+    if (t != 0) return;
+    const unsigned c = __hip_atomic_load(a.scratch + kPSStepCtr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const long long bid = *a.bid_out;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the id is in a register before the claim may replace it
+    __hip_atomic_store(a.scratch + kPSBidRead, c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned applied0 = ps_read_applied(a);
     const unsigned ep = __hip_atomic_load(a.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    const unsigned dec = ps_admit(a, false);
+    const unsigned dec = ps_admit(a, false, &bid);
     if (dec == kPSAccept || dec == kPSReject) ps_note_refresh(a, applied0 + (dec == kPSAccept ? 1u : 0u));
     // (relaxed: the next launch reads it, behind the kernel boundary)
     __hip_atomic_store(a.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -354,9 +357,14 @@ __global__ __launch_bounds__(kPSBlock) void ps_excl_step_kernel(PSArgs a) {
       // the gated update lands before anyone can read the count: this rank's next launch
       ps_publish_applied(a);
     }
+    return;
   }
-  __syncthreads();
+  // the next microbatch's claim and index staging, beside the admission; the id word is replaced only once
+  // workgroup 0 (dispatched first) has read the current one
   if (a.perm == nullptr) return;
+  __shared__ long long s_bid;
+  __shared__ unsigned s_c;
+  if (t == 0) s_c = __hip_atomic_load(a.scratch + kPSStepCtr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (a.done_epoch != nullptr) {
     claim_microbatch(a, t, &s_bid);
   } else if (t == 0) {
@@ -364,7 +372,20 @@ __global__ __launch_bounds__(kPSBlock) void ps_excl_step_kernel(PSArgs a) {
                         (unsigned long long)(a.nbatches > 0 ? a.nbatches : 1));
   }
   __syncthreads();
-  if (t == 0) *a.bid_out = s_bid;
+  if (t == 0) {
+    const unsigned c = s_c;
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(a.scratch + kPSBidRead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != c + 1u) {
+      if (wall_clock64() - t0 > 2ull * (unsigned long long)a.timeout_ticks) {  // never expected
+        atomicOr(a.stats + 5, 8ull);
+        if (a.herr) __hip_atomic_store(a.herr, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    *a.bid_out = s_bid;
+    __hip_atomic_store(a.scratch + kPSStepCtr, c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   ps_stage_indices(a, s_bid, t, kPSBlock);
 }
 
@@ -435,7 +456,7 @@ hipError_t ps_excl_step(const PSArgs& a, hipStream_t st) {
   if (a.excl == 0 || a.owner_ring > 0 || a.nshards != 1 || !ps_shards_ok(a) ||
       (a.perm != nullptr && (a.B <= 0 || (a.B & 1) || a.nbatches <= 0)))
     return hipErrorInvalidValue;
-  ps_excl_step_kernel<<<1, kPSBlock, 0, st>>>(a);
+  ps_excl_step_kernel<<<2, kPSBlock, 0, st>>>(a);
   return hipGetLastError();
 }
 

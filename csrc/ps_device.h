@@ -35,6 +35,9 @@ constexpr int kPSPullDone = 0, kPSApplyDone = 1, kPSEpoch = 2, kPSDecision = kPS
 // owner-applies words: the admitted sequence number, the pull launches' epoch, the drain decision's epoch
 // and, per shard, the first sequence number and the count this launch drains
 constexpr int kPSSeq = 5, kPSPullEp = 6, kPSDrain = 7, kPSDrainP = 8, kPSDrainN = 16;  // (+ shard, < 8 each)
+// exclusive-writer step (async_ps.hip ps_excl_step): its claim workgroup's step counter, and the admission
+// workgroup's "microbatch id read" flag (= counter + 1) the claim waits for before overwriting the id
+constexpr int kPSStepCtr = 24, kPSBidRead = 25;
 constexpr unsigned kPSNoVer = 0xffffffffu;
 // the decision word is (launch epoch << 3) | code: compare epochs modulo 2^29
 __device__ __forceinline__ bool ps_epoch_eq(unsigned word, unsigned ep) { return (word >> 3) == (ep & 0x1fffffffu); }
@@ -182,10 +185,11 @@ __device__ inline void complete_microbatch(const PSArgs& a, long long bid) {
 // version, check the staleness bound against vp (kPSVMin, see the header), CAS version -> version + 1; a
 // CAS lost to another rank's admission re-reads and re-checks.  Records vp in *vpulled, the counters, the
 // optional audit row and the microbatch completion.  Returns the decision code.
-__device__ inline unsigned ps_admit(const PSArgs& a, bool complete_now = true) {
+__device__ inline unsigned ps_admit(const PSArgs& a, bool complete_now = true, const long long* bid_pre = nullptr) {
   // every independent load first (one memory round trip, not one per load: the admission is the async
-  // step's critical path), then the CAS
-  const long long bid = *a.bid_out;
+  // step's critical path), then the CAS.  bid_pre: the microbatch id as the caller read it (the id word
+  // may be rewritten by a concurrent claim once the caller has read it)
+  const long long bid = bid_pre ? *bid_pre : *a.bid_out;
   const unsigned long long s0 = a.stats[0], s1 = a.stats[1], s2 = a.stats[2], s3 = a.stats[3];
   unsigned vp = __hip_atomic_load(a.scratch + kPSVMin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned v = __hip_atomic_load(a.ver, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
