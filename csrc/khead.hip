@@ -468,31 +468,32 @@ __global__ void __launch_bounds__(KT) khead_train_kernel(KHeadArgs a) {
       // column tiles of the chunk: wave w takes w, w + 4, ...; KSC > 0: the wave's W1^T operands in
       // rolling groups (the first two issued before the flag wait, above); otherwise two tiles per group
       // with ping-pong buffers
+      // the tile transposed (W1^T as the A operand, dZ1 as B): a lane holds 4 consecutive columns of one
+      // row, so the mask read and the in-place dP write are one 8-byte LDS access each per 16-row half
+      // (were 8 + 8 two-byte accesses per tile)
       auto tile = [&](int i, const bf16x8* bb) {
         f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          d0 = mfma16x16x32(za[0][k], bb[k], d0);
-          d1 = mfma16x16x32(za[1][k], bb[k], d1);
+          d0 = mfma16x16x32(bb[k], za[0][k], d0);
+          d1 = mfma16x16x32(bb[k], za[1][k], d1);
         }
-        const int col = 16 * (wid + 4 * i) + (lane & 15);
-        bf16* pa = s.ps + 4 * (lane >> 4) * s.ldp + col;  // rows 4 * (lane >> 4) + r, and 16 more
-        float m[8];  // the tile's 8 mask values first (one LDS latency), then the 8 in-place writes
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          m[r] = (float)pa[r * s.ldp];
-          m[4 + r] = (float)pa[(16 + r) * s.ldp];
-        }
+        bf16* p0 = s.ps + (lane & 15) * s.ldp + 16 * (wid + 4 * i) + 4 * (lane >> 4);  // row lane & 15
+        bf16* p1 = p0 + 16 * s.ldp;                                                      // and 16 more
+        const bf16x4 m0 = *reinterpret_cast<const bf16x4*>(p0), m1 = *reinterpret_cast<const bf16x4*>(p1);
+        bf16x4 o0, o1;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v0 = d0[r] * a.dp_scale, v1 = d1[r] * a.dp_scale;
           if (a.dp_mask) {
-            if (!(m[r] > 0.f)) v0 = 0.f;
-            if (!(m[4 + r] > 0.f)) v1 = 0.f;
+            if (!((float)m0[r] > 0.f)) v0 = 0.f;
+            if (!((float)m1[r] > 0.f)) v1 = 0.f;
           }
-          pa[r * s.ldp] = f2bf(v0);
-          pa[(16 + r) * s.ldp] = f2bf(v1);
+          o0[r] = f2bf(v0);
+          o1[r] = f2bf(v1);
         }
+        *reinterpret_cast<bf16x4*>(p0) = o0;
+        *reinterpret_cast<bf16x4*>(p1) = o1;
       };
       if constexpr (KSC > 0) {
         // rolling groups of 3 tiles, two groups in flight: ~96 operand VGPRs live instead of 144 (all nine
