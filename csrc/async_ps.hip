@@ -335,16 +335,17 @@ __global__ __launch_bounds__(kPSBlock) void ps_apply_kernel(PSArgs a) {
 // (vp: the applied count its weights contain, noted by the previous step's launch or the prologue's pull),
 // the refresh record of the NEXT step's weights (the optimizer launch that follows applies this gradient
 // when admitted: applied0 + 1 updates), the decision word the optimizer launch is gated on, the completion
-// and the next microbatch's claim and index staging.  One workgroup; no shard access (the gated optimizer
+// and the next microbatch's claim and index staging.  Two workgroups; no shard access (the gated optimizer
 // launch writes the new weights to the local master, its compute copies and the shard, in one pass).
+// The claim waits for the admission's completion flag (kPSBidRead = step counter + 1, stored AFTER
+// complete_microbatch): a claim that ran beside the completion saw the epoch's last in-flight batch still
+// incomplete and dispatched it a second time (one extra "duplicate" update per epoch).
 __global__ __launch_bounds__(kPSBlock) void ps_excl_step_kernel(PSArgs a) {
   const int t = threadIdx.x;
   if (blockIdx.x == 0) {  // the admission (one thread)
     if (t != 0) return;
     const unsigned c = __hip_atomic_load(a.scratch + kPSStepCtr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const long long bid = *a.bid_out;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the id is in a register before the claim may replace it
-    __hip_atomic_store(a.scratch + kPSBidRead, c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned applied0 = ps_read_applied(a);
     const unsigned ep = __hip_atomic_load(a.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const unsigned dec = ps_admit(a, false, &bid);
@@ -357,23 +358,20 @@ __global__ __launch_bounds__(kPSBlock) void ps_excl_step_kernel(PSArgs a) {
       // the gated update lands before anyone can read the count: this rank's next launch
       ps_publish_applied(a);
     }
+    // the completion's system-scope writes (done_epoch, the epoch words: write-through, read by the claim
+    // with system-scope loads that bypass the caches) are acknowledged before the flag goes out (an agent-
+    // scope release would write back this XCD's L2 on the step's critical path)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(a.scratch + kPSBidRead, c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
-  // the next microbatch's claim and index staging, beside the admission; the id word is replaced only once
-  // workgroup 0 (dispatched first) has read the current one
+  // the next microbatch's claim and index staging, once workgroup 0 has read the current id AND completed it
   if (a.perm == nullptr) return;
   __shared__ long long s_bid;
   __shared__ unsigned s_c;
-  if (t == 0) s_c = __hip_atomic_load(a.scratch + kPSStepCtr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (a.done_epoch != nullptr) {
-    claim_microbatch(a, t, &s_bid);
-  } else if (t == 0) {
-    s_bid = (long long)(__hip_atomic_fetch_add(a.batch_ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) %
-                        (unsigned long long)(a.nbatches > 0 ? a.nbatches : 1));
-  }
-  __syncthreads();
   if (t == 0) {
-    const unsigned c = s_c;
+    const unsigned c = __hip_atomic_load(a.scratch + kPSStepCtr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_c = c;
     const unsigned long long t0 = wall_clock64();
     while (__hip_atomic_load(a.scratch + kPSBidRead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != c + 1u) {
       if (wall_clock64() - t0 > 2ull * (unsigned long long)a.timeout_ticks) {  // never expected
@@ -383,8 +381,18 @@ __global__ __launch_bounds__(kPSBlock) void ps_excl_step_kernel(PSArgs a) {
       }
       __builtin_amdgcn_s_sleep(1);
     }
+  }
+  __syncthreads();
+  if (a.done_epoch != nullptr) {
+    claim_microbatch(a, t, &s_bid);
+  } else if (t == 0) {
+    s_bid = (long long)(__hip_atomic_fetch_add(a.batch_ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) %
+                        (unsigned long long)(a.nbatches > 0 ? a.nbatches : 1));
+  }
+  __syncthreads();
+  if (t == 0) {
     *a.bid_out = s_bid;
-    __hip_atomic_store(a.scratch + kPSStepCtr, c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.scratch + kPSStepCtr, s_c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   ps_stage_indices(a, s_bid, t, kPSBlock);
 }

@@ -2007,6 +2007,7 @@ class PSComm {
     a.seq = reinterpret_cast<unsigned*>(shared_ + 80);
     a.tick = reinterpret_cast<unsigned long long*>(shared_ + 88);
     a.land = reinterpret_cast<unsigned long long*>(shared_ + 96);
+    a.bad = reinterpret_cast<unsigned long long*>(shared_ + 104);
     for (int k = 0; k < world_; ++k) a.shard[k] = shard_[k], a.slot[k] = fed_slot_[k];
     a.shard_shift = shift_;
     a.nshards = world_;
@@ -2028,11 +2029,14 @@ class PSComm {
     a.w = w.data_ptr<float>();
     check_hip(dfa::fed_pull(a, cur_stream()), "fed_pull");
   }
-  void fed_upload(torch::Tensor g) {
+  // drop_land: fault injection (tests) -- the ticket is taken, nothing is stored or landed (a rank that dies
+  // between its admission and its landing)
+  void fed_upload(torch::Tensor g, bool drop_land) {
     need(g, at::kFloat, "fedsgd grad");
     TORCH_CHECK(g.numel() == n_ && g.get_device() == dev_, "fedsgd: gradient mismatch");
     dfa::FedArgs a = fed_args();
     a.g = g.data_ptr<float>();
+    a.drop_land = drop_land ? 1 : 0;
     check_hip(dfa::fed_upload(a, cur_stream()), "fed_upload");
   }
   void fed_apply(double lr) {
@@ -2051,13 +2055,15 @@ class PSComm {
     fed_audit_cap_ = rows.size(0);
     fed_audit_keep_ = rows;
   }
-  // [admitted, stale, full, failed, versions applied by this rank, error bits, version seqlock word]
+  // [admitted, stale, full, failed, versions applied by this rank, error bits, version seqlock word,
+  //  stuck versions this rank recovered]
   std::vector<int64_t> fed_stats() const {
     unsigned long long h[8] = {0};
     check_hip(hipMemcpy(h, local_ + 3584, 64, hipMemcpyDeviceToHost), "fedsgd stats");
     unsigned seq = 0;
     check_hip(hipMemcpy(&seq, shared_ + 80, 4, hipMemcpyDeviceToHost), "fedsgd seq");
-    return {(int64_t)h[0], (int64_t)h[1], (int64_t)h[2], (int64_t)h[3], (int64_t)h[4], (int64_t)h[7], (int64_t)seq};
+    return {(int64_t)h[0], (int64_t)h[1], (int64_t)h[2], (int64_t)h[3], (int64_t)h[4], (int64_t)h[7], (int64_t)seq,
+            (int64_t)h[5]};
   }
   // device view of [admitted, stale, full, failed, applied-by-me, -, -, err] (trainer callbacks)
   torch::Tensor fed_stats_tensor() const {
@@ -2486,7 +2492,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("fed_init", &PSComm::fed_init, py::arg("K"))
       .def("fed_open", &PSComm::fed_open, py::arg("handles"))
       .def("fed_pull", &PSComm::fed_pull)
-      .def("fed_upload", &PSComm::fed_upload)
+      .def("fed_upload", &PSComm::fed_upload, py::arg("g"), py::arg("drop_land") = false)
       .def("fed_apply", &PSComm::fed_apply, py::arg("lr"))
       .def("set_fed_audit", &PSComm::set_fed_audit, py::arg("rows"))
       .def("fed_stats", &PSComm::fed_stats)

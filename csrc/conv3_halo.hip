@@ -23,6 +23,9 @@
 //     2 weight buffers <= 74 KB, so two workgroups share a CU
 //   * 4 waves as 2 (pixel halves of 64) x 2 (channel halves of BN/2)
 //   * epilogue as igemm64: alpha, residual join (res * [resmask > 0]), ReLU, relu'(mask)
+#include <map>
+#include <mutex>
+
 #include "common.h"
 #include "kernels.h"
 #include "diag.h"
@@ -645,21 +648,39 @@ __global__ void __launch_bounds__(512, 1) conv3_halo_c64_kernel(C3P p) {
 }
 
 // per-tile tickets of the folded split-K combine: zeroed once, each tile's last arriver resets its own, so
-// the buffer is zero between launches (graph replays included).  Allocated outside any stream capture
-// (null -- the combine launch -- if the first request comes during one).
+// a buffer is zero between launches (graph replays included).  One buffer per (device, stream): two folded
+// convs running at once on different streams, or on another device of the process, never share tickets
+// (ADVICE r5).  Each device's buffers come from a pool allocated and zeroed outside any stream capture at
+// the device's first request (null -- the combine launch -- if that request comes during a capture or
+// the pool is used up); a capture stream takes a pool buffer without any allocation.  Folded convs on
+// one stream run in stream order, so they share that stream's buffer safely.
 constexpr int kC3Tickets = 1024;
+constexpr int kC3Pool = 64;  // buffers per device (torch's stream pools are finite, so are the keys)
 unsigned* c3_tickets(hipStream_t st) {
-  static unsigned* t = nullptr;
-  if (t != nullptr) return t;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  unsigned* b = nullptr;
-  if (hipMalloc(&b, kC3Tickets * sizeof(unsigned)) != hipSuccess) return nullptr;
-  if (hipMemset(b, 0, kC3Tickets * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-    (void)hipFree(b);
-    return nullptr;
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, unsigned*> tab;
+  static std::map<int, std::pair<unsigned*, int>> pool;  // device -> (base, buffers handed out)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = tab.find({dev, st});
+  if (it != tab.end()) return it->second;
+  auto pit = pool.find(dev);
+  if (pit == pool.end()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    unsigned* b = nullptr;
+    const size_t bytes = (size_t)kC3Pool * kC3Tickets * sizeof(unsigned);
+    if (hipMalloc(&b, bytes) != hipSuccess) return nullptr;
+    if (hipMemset(b, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(b);
+      return nullptr;
+    }
+    pit = pool.emplace(dev, std::make_pair(b, 0)).first;
   }
-  t = b;
+  if (pit->second.second >= kC3Pool) return nullptr;
+  unsigned* t = pit->second.first + (size_t)pit->second.second++ * kC3Tickets;
+  tab[{dev, st}] = t;
   return t;
 }
 

@@ -430,11 +430,12 @@ constexpr int kPSMaxGrid = 64;
 
 // Device FedSGD count barrier on the parameter server's shards (csrc/fedsgd_ps.hip): the reference
 // FederatedServer's version gate and K-upload barrier, K < W allowed (late uploads are dropped).
-constexpr int kFedMaxK = 64;
+constexpr int kFedMaxK = 32;  // the landed / bad slot masks are 32-bit
 struct FedArgs {
   unsigned* seq;                 // control: version seqlock (2v: version v stable; odd: being applied)
   unsigned long long* tick;      // control: (seq << 32) | tickets taken for that version
-  unsigned long long* land;      // control: (seq << 32) | admitted gradients landed in their slots
+  unsigned long long* land;      // control: (seq << 32) | mask of the slots whose gradient has landed
+  unsigned long long* bad;       // control: (seq << 32) | mask of the slots landed as bad (torn or lost)
   float* shard[kP2PMaxRanks];    // master shards (element i: shard[i >> shift][i & mask])
   float* slot[kP2PMaxRanks];     // per rank: K slot shards (slot t of element i: slot[i >> shift][t << shift | i & mask])
   int shard_shift, nshards, K;
@@ -442,13 +443,15 @@ struct FedArgs {
   float* w;                      // local master (pull destination)
   const float* g;                // local gradient (upload)
   unsigned* scratch;             // local protocol words (fedsgd_ps.hip)
-  unsigned long long* stats;     // local [8]: admitted, stale, full, failed, versions applied, -, -, error bits
+  unsigned long long* stats;     // local [8]: admitted, stale, full, failed, versions applied, versions recovered,
+                                 //            -, error bits
   unsigned* audit;               // optional local rows [audit_cap][3]: (seqlock word pulled, decision, slot)
   long long audit_cap;
   const float* lr_dev;           // device learning rate (null: lr)
   float lr;
   long long timeout_ticks;
   unsigned* herr;
+  int drop_land;                 // fault injection (tests): take the ticket, then store and land nothing
 };
 hipError_t fed_pull(const FedArgs& a, hipStream_t st);
 hipError_t fed_upload(const FedArgs& a, hipStream_t st);

@@ -37,7 +37,7 @@ constexpr int kPSPullDone = 0, kPSApplyDone = 1, kPSEpoch = 2, kPSDecision = kPS
 constexpr int kPSSeq = 5, kPSPullEp = 6, kPSDrain = 7, kPSDrainP = 8, kPSDrainN = 16;  // (+ shard, < 8 each)
 // exclusive-writer step (async_ps.hip ps_excl_step): its claim workgroup's step counter, and the admission
 // workgroup's "microbatch id read" flag (= counter + 1) the claim waits for before overwriting the id
-constexpr int kPSStepCtr = 24, kPSBidRead = 25;
+constexpr int kPSStepCtr = 24, kPSBidRead = 25;  // kPSBidRead: "id read and completed" flag
 constexpr unsigned kPSNoVer = 0xffffffffu;
 // the decision word is (launch epoch << 3) | code: compare epochs modulo 2^29
 __device__ __forceinline__ bool ps_epoch_eq(unsigned word, unsigned ep) { return (word >> 3) == (ep & 0x1fffffffu); }

@@ -290,6 +290,7 @@ class Conv2D(Layer):
         if bacc is not None:
             bn.x = self.out
             bn._fwd_acc_ready = True
+            bn._acc_nz[0] = True
         return self.out
 
     def can_emit_bn_grad(self) -> bool:
@@ -336,6 +337,7 @@ class Conv2D(Layer):
         if bacc is not None:
             for b in bn_acc:
                 b._bwd_acc_ready = True
+                b._acc_nz[1] = True
         return self.dx
 
     def config(self):
@@ -551,6 +553,10 @@ class BatchNorm(Layer):
             self.acc_all = torch.zeros(2, nrep, 2, C, dtype=torch.float64, device=device)
             self.acc, self.acc_b = self.acc_all[0], self.acc_all[1]
         self._fwd_acc_ready = self._bwd_acc_ready = False
+        # "possibly non-zero" flags of acc / acc_b: set when a producer launch is given them, cleared by the
+        # consumer that zeroes them (bn_dx_acc clears acc, bn_apply_acc clears acc_b); drop_acc clears only
+        # what may hold sums (two memsets per BN per step for nothing)
+        self._acc_nz = [False, False]
 
     def stats(self, x):
         """Training-mode batch statistics of ``x`` (and the running statistics); writes no output."""
@@ -596,7 +602,9 @@ class BatchNorm(Layer):
             r = residual_bn
             rb = [st[f"{r.name}/gamma"], st[f"{r.name}/beta"], r.acc, r.acc_b, r.mean, r.invstd, r.run_mean, r.run_var]
             r._fwd_acc_ready = False
+            r._acc_nz[1] = False
         self._fwd_acc_ready = False
+        self._acc_nz[1] = False
         ops.bn_apply_acc(x.reshape(-1, self.C), out.view(-1, self.C), st[f"{self.name}/gamma"], st[f"{self.name}/beta"],
                          self.acc, self.acc_b, self.mean, self.invstd, self.run_mean, self.run_var,
                          self.relu if relu is None else relu,
@@ -604,11 +612,12 @@ class BatchNorm(Layer):
         return out
 
     def drop_acc(self):
-        """This step's statistics take the other path: clear both accumulators (the producers only ever add
-        into zeroed ones), so a later step can use the accumulated path again."""
+        """This step's statistics take the other path: clear the accumulators a producer may have added into
+        (the producers only ever add into zeroed ones), so a later step can use the accumulated path again."""
         self._fwd_acc_ready = self._bwd_acc_ready = False
-        if self.acc_on:
+        if self.acc_on and (self._acc_nz[0] or self._acc_nz[1]):
             self.acc_all.zero_()
+        self._acc_nz = [False, False]
 
     def forward(self, x, training):
         self.x = x
@@ -627,6 +636,7 @@ class BatchNorm(Layer):
         """dx from a gradient g whose backward sums the producing kernel accumulated (relu' applied)."""
         st = self.store
         self._bwd_acc_ready = False
+        self._acc_nz[0] = False
         ops.bn_dx_acc(self.x.reshape(-1, self.C), g.reshape(-1, self.C), self.dx.view(-1, self.C), self.acc_b, self.acc,
                       st[f"{self.name}/gamma"], self.mean, self.invstd, st.gradient(f"{self.name}/gamma"),
                       st.gradient(f"{self.name}/beta"), self.coef)
@@ -701,6 +711,7 @@ class GlobalAveragePooling2D(Layer):
             b = sinks[0]
             ops.gap_bwd_bn(dy, self.x, self.dx, b.acc_b, b.x, b.mean, b.invstd)
             b._bwd_acc_ready = True
+            b._acc_nz[1] = True
             return self.dx
         ops.gap_bwd(dy, self.dx)
         if self.in_relu:

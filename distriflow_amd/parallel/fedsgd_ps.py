@@ -44,8 +44,8 @@ class FedSGDDeviceTrainer(AsyncPSTrainer):
                          timeout_s=timeout_s)
         self.fused_ps = False  # the generic pull / compute / upload / apply step for every model
         self.K = int(min_updates_per_version)
-        if not 1 <= self.K <= 64:
-            raise ValueError("min_updates_per_version must be 1..64")
+        if not 1 <= self.K <= 32:
+            raise ValueError("min_updates_per_version must be 1..32")
         err, handle = None, b""
         try:
             handle = self.ps.fed_init(self.K)
@@ -115,9 +115,9 @@ class FedSGDDeviceTrainer(AsyncPSTrainer):
         return int(self.ps.fed_stats()[6]) // 2
 
     def fed_stats(self) -> dict:
-        adm, stale, full, failed, applied, err, seq = self.ps.fed_stats()
+        adm, stale, full, failed, applied, err, seq, recovered = self.ps.fed_stats()
         return {"admitted": adm, "stale": stale, "full": full, "failed": failed, "applied_here": applied,
-                "error": err, "version": seq // 2}
+                "error": err, "version": seq // 2, "recovered": recovered}
 
     def check_comm(self):
         err = self.ps.fed_stats()[5] | self.ps.stats()[5]

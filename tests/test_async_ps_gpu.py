@@ -85,6 +85,49 @@ def test_async_excl_fused_matches_generic_path(monkeypatch):
     torch.testing.assert_close(res[1], res[0], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("graph", ["none", "full"])
+def test_async_excl_epoch_boundary_no_duplicates(graph):
+    """the exclusive writer's claim ran beside the admission's completion, so at each epoch's end
+    the last in-flight batch looked incomplete and was dispatched (and applied) a second time.  One rank,
+    two epochs run to the end: every batch completes once per epoch, no duplicate, no extra update, and the
+    master equals serial SGD over the two epochs' batch order."""
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.async_ps import AsyncPSTrainer
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
+
+    dev = torch.device("cuda", 0)
+    nb, epochs = 8, 2
+    data, labels = synthetic_mnist(nb * 256, seed=3, device=dev)
+    perm = epoch_permutations(nb * 256, 256, nb, dev, seed=1)
+    a = build_model("keras_cnn", device=dev, seed=0)
+    ta = AsyncPSTrainer(a, lr=0.05, max_staleness=0, graph=graph)
+    assert ta.excl_fused
+    ta.bind_dataset(data, labels, 256, scale=1.0 / 255.0)
+    ta.bind_schedule(perm, epochs=epochs)
+    extra = 3
+    if graph == "full":
+        ta.prepare_run(4)
+        ta.run(nb * epochs + extra)
+    else:
+        for _ in range(nb * epochs + extra):
+            ta.step()
+    torch.cuda.synchronize()
+    st = ta.ps_stats()
+    assert ta.finished() and st["epoch"] == epochs and st["error"] == 0, st
+    assert st["duplicates"] == 0 and st["accepted"] == nb * epochs and st["completed"] == nb * epochs, st
+    assert st["noop_steps"] == extra and st["version"] == nb * epochs, st
+    assert ta.done_epochs() == [epochs] * nb
+    s = build_model("keras_cnn", device=dev, seed=0)
+    ts = DataParallelTrainer(s, lr=0.05, graph="none")
+    ts.bind_dataset(data, labels, 256, scale=1.0 / 255.0)
+    ts.bind_index_stream(perm)
+    for _ in range(nb * epochs):
+        ts.step()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(ta.pull_master().clone(), s.store.master, rtol=1e-5, atol=1e-6)
+
+
 def test_async_multistep_graph_matches_single_steps():
     """prepare_run(u) + run(n): u whole PS steps (pull, train, reduce, locked apply) unrolled into one
     graph give the same shared master, version and dispatch counters as n single-step replays."""

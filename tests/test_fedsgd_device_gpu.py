@@ -127,3 +127,117 @@ def test_device_fedsgd_k_lt_w_straggler_and_lost_rank():
         assert news == sorted(set(news)) and all(o < n for o, n in x["seen"]), x["seen"]
     print(f"versions {V}; admitted per rank {[x['fed']['admitted'] for x in r]}; "
           f"straggler stale/full {st['stale']}/{st['full']}")
+
+
+def _recovery_worker(rank, world, port, out_dir, K, mode, target):
+    """Rank 0 lands slot 0 of version 0; rank 2 then takes slot 1 and "dies": mode "applier" -- it lands
+    (and so claims the apply) but never runs fed_apply; mode "ticket" -- it takes the ticket and stores /
+    lands nothing (fault injection).  Ranks 0 and 1 keep stepping until the version reaches ``target``."""
+    import torch.distributed as dist
+
+    dev = init_rank(rank, world, port)
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+    from distriflow_amd.parallel.fedsgd_ps import FedSGDDeviceTrainer
+
+    data, labels = synthetic_mnist(N_ROWS, seed=3, device=dev)
+    net = build_model("lenet5", device=dev, seed=0)
+    tr = FedSGDDeviceTrainer(net, lr=LR, min_updates_per_version=K, graph="full", timeout_s=2.0)
+    tr.bind_dataset(data, labels, MB, scale=1.0 / 255.0)
+    cap = 200000
+    audit = torch.full((cap, 3), -1, dtype=torch.int32, device=dev)
+    tr.ps.set_fed_audit(audit)
+    rows = _rows(rank, 64)
+    used = []  # the row set of each upload, in audit-row order
+    dist.barrier()
+    n = 0
+    if rank == 0:
+        tr.step_indices(rows[0].to(dev))  # slot 0 of version 0
+        used.append(0)
+        n = 1
+    torch.cuda.synchronize()
+    dist.barrier()
+    if rank == 2:
+        tr.idx.copy_(rows[0].to(dev))
+        tr._gather()
+        tr.net.compute_gradients(tr.xb, tr.yb)
+        tr.ps.fed_upload(tr.net.store.grad, drop_land=(mode == "ticket"))  # ... and no fed_apply
+        used.append(0)
+        n = 1
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.time()
+    if rank in (0, 1):
+        k = 0
+        while tr.version() < target and time.time() - t0 < 90.0 and n < cap:
+            tr.step_indices(rows[(k + 1) % len(rows)].to(dev))
+            used.append((k + 1) % len(rows))
+            k += 1
+            n += 1
+    torch.cuda.synchronize()
+    dist.barrier()
+    res = dict(audit=audit[:n].cpu(), fed=tr.fed_stats(), n=n, rows=torch.stack(rows), used=torch.tensor(used, dtype=torch.long))
+    if rank == 0:
+        res["master"] = tr.pull_master(torch.empty_like(net.store.master)).cpu()
+        torch.cuda.synchronize()
+    torch.save(res, os.path.join(out_dir, f"f{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["applier", "ticket"])
+def test_device_fedsgd_recovers_lost_applier_or_ticket(mode):
+    """ADVICE r5 liveness: a rank that stops between its upload and fed_apply (it claimed the apply), or
+    between its admission and its landing, no longer wedges the version -- every other upload saw Full for
+    ever.  A surviving rank recovers the version after the timeout (missing tickets landed as bad slots and
+    left out of the mean; the apply claimed by the survivor), and the master equals the replay of the good
+    gradients of every version (reference: a lost worker never blocks a version,
+    /root/reference/src/server/federated_server.ts:87-90)."""
+    world, K, target = 3, 2, 4
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_recovery_worker, args=(world, free_port(), d, K, mode, target), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"f{i}.pt"), weights_only=True) for i in range(world)]
+    V = r[0]["fed"]["version"]
+    assert V >= target, [x["fed"] for x in r]
+    assert r[0]["fed"]["error"] == 0 and r[1]["fed"]["error"] == 0, [x["fed"] for x in r]
+    assert r[0]["fed"]["recovered"] + r[1]["fed"]["recovered"] == 1, [x["fed"] for x in r]
+    assert r[2]["fed"]["applied_here"] == 0
+    per_version = {}
+    for rank, x in enumerate(r):
+        a = x["audit"]
+        for k in range(x["n"]):
+            seq, dec, slot = (int(v) for v in a[k])
+            if dec == 1:
+                per_version.setdefault(seq // 2, []).append((slot, rank, k))
+    v0 = sorted(per_version[0])
+    assert [(s, rk) for s, rk, _ in v0] == [(0, 0), (1, 2)], v0
+    if mode == "ticket":  # the dead rank's ticket never landed: version 0 is the mean of slot 0 alone
+        per_version[0] = v0[:1]
+    from distriflow_amd.data.synthetic import synthetic_mnist
+    from distriflow_amd.models.zoo import build_model
+
+    dev = torch.device("cuda", 0)
+    data, labels = synthetic_mnist(N_ROWS, seed=3, device=dev)
+    net = build_model("lenet5", device=dev, seed=0)
+    rows = {rk: r[rk]["rows"][r[rk]["used"]] for rk in range(world)}
+    w = net.store.master.clone()
+    for v in range(V):
+        got = sorted(per_version[v])
+        if v > 0:
+            assert [s for s, _, _ in got] == list(range(K)), (v, got)
+        acc = None
+        for slot, rk, k in got:
+            idx = rows[rk][k].to(dev)
+            net.store.set_flat(w)
+            x = (data.index_select(0, idx).float() / 255.0).to(torch.bfloat16)
+            net.compute_gradients(x, labels.index_select(0, idx))
+            g = net.store.grad.clone()
+            acc = g if acc is None else acc + g
+        with torch.no_grad():
+            w = w - LR * (acc * (1.0 / len(got)))
+    torch.cuda.synchronize()
+    m = r[0]["master"].to(dev)
+    rel = ((m - w).abs() / w.abs().clamp_min(1e-3)).max().item()
+    assert rel <= 1e-5, f"master relative error {rel:.3e} against the replay of the good gradients"
+    print(f"{mode}: versions {V}, recovered by {[x['fed']['recovered'] for x in r]}")
