@@ -408,6 +408,56 @@ __global__ void ps_selftest_kernel(PSArgs a, float* const* words, int n, float r
   ps_add<1>(p, d, o, a.excl != 0, a);
 }
 
+// Apply-path calibration (AsyncPSTrainer setup, every rank at once, before the master is seeded): the two ways
+// an admitted gradient reaches the sharded master, over this model's n elements with a zero update (no value
+// changes), on the real topology:
+//   mode 0  the CAS path's per-element compare-and-swap adds on the owning shards (ps_add, shared form);
+//   mode 1  owner-applies: the plain store into the element's inbox ring slot R - 1, the shard load of the
+//           refresh and one inbox-slot load of the drain (each admitted gradient is drained once per element).
+__global__ __launch_bounds__(kPSBlock) void ps_calib_kernel(PSArgs a, int mode) {
+  __shared__ float* tab[kP2PMaxRanks];
+  __shared__ float* itab[kP2PMaxRanks];
+  if (mode == 1 && threadIdx.x < kP2PMaxRanks) {
+    float* v = nullptr;
+#pragma unroll
+    for (int k = 0; k < kP2PMaxRanks; ++k)
+      if ((int)threadIdx.x == k) v = a.inbox[k];
+    itab[threadIdx.x] = v;
+  }
+  ps_stage_shards(a, tab);
+  const int t = threadIdx.x, b = blockIdx.x, G = gridDim.x;
+  const long long per = ((a.n + 4LL * G - 1) / (4LL * G)) * 4;
+  const long long lo = b * per, hi = lo + per < a.n ? lo + per : a.n;
+  if (mode == 0) {
+    for (long long i0 = lo + t; i0 < hi; i0 += (long long)kPSBlock * kPSUnroll) {
+      float* p[kPSUnroll];
+      float d[kPSUnroll], nw[kPSUnroll];
+#pragma unroll
+      for (int u = 0; u < kPSUnroll; ++u) {
+        const long long i = i0 + (long long)u * kPSBlock;
+        p[u] = i < hi ? ps_elem(tab, a.shard_shift, i) : nullptr;
+        d[u] = 0.f;
+      }
+      ps_add<kPSUnroll>(p, d, nw, false, a);
+    }
+    return;
+  }
+  const long long mask = (1LL << a.shard_shift) - 1;
+  const unsigned R = (unsigned)a.owner_ring;
+  float acc = 0.f;
+  for (long long i = lo + t; i < hi; i += kPSBlock) {
+    const int k = (int)(i >> a.shard_shift);
+    __hip_atomic_store(reinterpret_cast<unsigned*>(itab[k] + ((long long)(R - 1) << a.shard_shift) + (i & mask)), 0u,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    acc += __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(tab[k] + (i & mask)), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM));
+    acc += __uint_as_float(__hip_atomic_load(
+        reinterpret_cast<unsigned*>(itab[k] + ((long long)(R - 2) << a.shard_shift) + (i & mask)), __ATOMIC_RELAXED,
+        __HIP_MEMORY_SCOPE_SYSTEM));
+  }
+  asm volatile("" ::"v"(acc));
+}
+
 }  // namespace
 
 // ~16 KB of weights per workgroup, at most kPSMaxGrid workgroups (all resident: the apply kernel's
@@ -465,6 +515,16 @@ hipError_t ps_excl_step(const PSArgs& a, hipStream_t st) {
       (a.perm != nullptr && (a.B <= 0 || (a.B & 1) || a.nbatches <= 0)))
     return hipErrorInvalidValue;
   ps_excl_step_kernel<<<2, kPSBlock, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t ps_calibrate(const PSArgs& a, int mode, hipStream_t st) {
+  if (a.n <= 0 || (a.n & 3) || !ps_shards_ok(a) || (mode != 0 && mode != 1) ||
+      (mode == 1 && (a.owner_ring < 2 || !ps_owner_ok(a))))
+    return hipErrorInvalidValue;
+  // the fused LeNet-5 reduce applies from ~600 workgroups at once: a wide grid (one float4 group per thread)
+  const long long g = (a.n + 4LL * kPSBlock - 1) / (4LL * kPSBlock);
+  ps_calib_kernel<<<(int)(g < 1 ? 1 : (g > 1024 ? 1024 : g)), kPSBlock, 0, st>>>(a, mode);
   return hipGetLastError();
 }
 

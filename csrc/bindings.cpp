@@ -2084,12 +2084,46 @@ class PSComm {
                                         "ps owner inbox");
     return export_handle(inbox_own_);
   }
-  void owner_open(std::vector<std::string> handles) {
+  // enable = false: map the inboxes only (the apply-path calibration), owner_enable() switches the path
+  void owner_open(std::vector<std::string> handles, bool enable) {
     TORCH_CHECK(inbox_own_ != nullptr && (int)handles.size() == world_, "ps owner-applies: owner_init first");
     for (int k = 0; k < world_; ++k) inbox_[k] = k == rank_ ? inbox_own_ : (float*)open_handle(handles[k]);
-    owner_on_ = true;
+    owner_on_ = enable;
+  }
+  void owner_enable(bool on) {
+    TORCH_CHECK(!on || (inbox_own_ != nullptr && inbox_[rank_] != nullptr), "ps owner-applies: owner_open first");
+    owner_on_ = on;
   }
   bool owner_applies() const { return owner_on_; }
+  // apply-path calibration (collective: every rank calls it at once, between barriers, before init_master):
+  // mean microseconds per launch of the CAS adds (mode 0) or the owner-applies traffic (mode 1, needs
+  // owner_init / owner_open) over this rank's n elements, `reps` launches after one warm-up launch
+  double calibrate(int64_t mode, int64_t reps) {
+    dfa::PSArgs a = args();
+    TORCH_CHECK(mode == 0 || mode == 1, "ps calibrate: mode 0 (CAS) or 1 (owner-applies)");
+    TORCH_CHECK(reps >= 1, "ps calibrate: reps >= 1");
+    if (mode == 1) {
+      TORCH_CHECK(inbox_own_ != nullptr && inbox_[rank_] != nullptr, "ps calibrate: owner_open first");
+      a.owner_ring = owner_ring_;
+      a.pref = reinterpret_cast<unsigned*>(shared_ + 192);
+      a.dlock = reinterpret_cast<unsigned*>(shared_ + 224);
+      for (int k = 0; k < world_; ++k) a.inbox[k] = inbox_[k];
+    }
+    hipStream_t st = cur_stream();
+    check_hip(dfa::ps_calibrate(a, (int)mode, st), "ps_calibrate");
+    hipEvent_t e0, e1;
+    check_hip(hipEventCreate(&e0), "calib event");
+    check_hip(hipEventCreate(&e1), "calib event");
+    check_hip(hipEventRecord(e0, st), "calib record");
+    for (int64_t r = 0; r < reps; ++r) check_hip(dfa::ps_calibrate(a, (int)mode, st), "ps_calibrate");
+    check_hip(hipEventRecord(e1, st), "calib record");
+    check_hip(hipEventSynchronize(e1), "calib sync");
+    float ms = 0.f;
+    check_hip(hipEventElapsedTime(&ms, e0, e1), "calib elapsed");
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return (double)ms * 1e3 / (double)reps;
+  }
   // the owner's drain alone (a pull into `w` without a microbatch claim): adds every flagged slot of this
   // rank's inbox into its shard; after the last step of every rank, one drain per rank settles the master
   void drain(torch::Tensor w) { fetch_pull(w, c10::nullopt, c10::nullopt); }
@@ -2485,10 +2519,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("stats_tensor", &PSComm::stats_tensor)
       .def("set_audit", &PSComm::set_audit, py::arg("rows"))
       .def("owner_init", &PSComm::owner_init, py::arg("ring"))
-      .def("owner_open", &PSComm::owner_open)
+      .def("owner_open", &PSComm::owner_open, py::arg("handles"), py::arg("enable") = true)
+      .def("owner_enable", &PSComm::owner_enable, py::arg("on"))
       .def("owner_applies", &PSComm::owner_applies)
       .def("drain", &PSComm::drain)
       .def("owner_prefix", &PSComm::owner_prefix)
+      .def("calibrate", &PSComm::calibrate, py::arg("mode"), py::arg("reps") = 20)
       .def("fed_init", &PSComm::fed_init, py::arg("K"))
       .def("fed_open", &PSComm::fed_open, py::arg("handles"))
       .def("fed_pull", &PSComm::fed_pull)

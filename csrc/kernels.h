@@ -460,6 +460,8 @@ constexpr int kPSVMinWord = 4;  // scratch word of the refresh minimum (ps_devic
 constexpr int kPSDecisionWord = 3;  // scratch word of the tagged admission decision (ps_device.h kPSDecision)
 constexpr long long kPSMaxBatches = 1 << 20;  // capacity of the shared completion arrays
 hipError_t ps_fetch_pull(const PSArgs& a, hipStream_t st);
+// apply-path calibration: mode 0 per-element CAS adds of 0, mode 1 owner-applies stores / loads (async_ps.hip)
+hipError_t ps_calibrate(const PSArgs& a, int mode, hipStream_t st);
 hipError_t ps_apply(const PSArgs& a, hipStream_t st);
 // exclusive writer (one rank): admission of this step's gradient, the next microbatch's claim and index
 // staging, in one workgroup; the update itself is the optimizer launch gated on the decision

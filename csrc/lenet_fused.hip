@@ -296,18 +296,56 @@ __device__ __forceinline__ int lenet_img_group(int b, int nb) {
 // async PS admission of this step's gradient (the extra workgroup of the train launch, see lenet_train):
 // lock-free CAS on the shared version, decision published for the reduce launch's owners (epoch-tagged
 // with that launch's epoch, which no one advances before it runs), the refresh minimum recorded, then the
-// microbatch's completion
+// microbatch's completion.
+// Owner-applies (p.owner_ring > 0, reduce mode 4): no per-element remote atomic anywhere.  After its decision
+// the admission takes the drain lock of every shard no other rank is draining (one CAS per shard) and decides
+// how many flagged inbox slots (in sequence order from the shard's drained prefix) the reduce launch adds into
+// it; the decisions go out as one {epoch, count, first} word per shard (ps_owner_drain_words), read by the
+// reduce launch's owners with one load -- no wait inside that launch.  The refresh the owners then emit
+// contains, on every element, each shard's drained prefix (P + n for the shards this launch drains, the
+// prefix read before any shard read otherwise) and -- when admitted with sequence number q and every prefix
+// is q -- this gradient itself, which the owners add to the values they emit: that count is the refresh
+// minimum (ps_device.h).  The own gradient reaches the shards through the inboxes: every owner stores
+// -lr * g of its elements into ring slot q % R of the element's shard inbox (plain system-scope stores), the
+// launch's last arrival flags the slot at every owner once they have all landed (lenet_ps_arrive).
+__device__ __forceinline__ void lenet_ps_owner_decide(const PSArgs& p, unsigned ep, unsigned dec) {
+  const unsigned R = (unsigned)p.owner_ring;
+  unsigned long long* dw = ps_owner_drain_words(p);
+  unsigned cnt = 0xffffffffu;
+  for (int k = 0; k < p.nshards; ++k) {
+    const unsigned pre = __hip_atomic_load(p.pref + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned P = 0, n = 0, c = pre, free_ = 0;
+    if (__hip_atomic_compare_exchange_strong(p.dlock + k, &free_, (unsigned)p.rank + 1u, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+      P = __hip_atomic_load(p.pref + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const unsigned* fl = ps_inbox_flags(p, k);
+      while (n < R && n < 255u &&
+             __hip_atomic_load(const_cast<unsigned*>(fl) + (P + n) % R, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ==
+                 P + n + 1u)
+        ++n;
+      if (n == 0) __hip_atomic_store(p.dlock + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      c = P + n;
+    }
+    __hip_atomic_store(dw + k, ps_owner_word(ep, n, P), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cnt = c < cnt ? c : cnt;
+  }
+  if (dec == kPSAccept && cnt == p.scratch[kPSSeq]) cnt += 1u;  // the owners add this gradient to what they emit
+  if (dec == kPSAccept || dec == kPSReject) ps_note_refresh(p, cnt);
+}
+
 __device__ __forceinline__ void lenet_ps_admission(const PSArgs& p, bool excl) {
   const long long bid = *p.bid_out;  // (the reduce launch's claim workgroup overwrites it after the decision)
   const unsigned applied0 = ps_read_applied(p);
   const unsigned ep = __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const unsigned dec = ps_admit(p, false);  // (consumes the previous launch's record first)
+  const bool owner = p.owner_ring > 0;
   // the owners refresh (add to or read the shards) only after this decision, so every one of their
   // refreshes contains at least applied0 fully applied gradients (+ this one when admitted)
-  if (dec == kPSAccept || dec == kPSReject) ps_note_refresh(p, applied0 + (dec == kPSAccept ? 1u : 0u));
+  if (!owner && (dec == kPSAccept || dec == kPSReject)) ps_note_refresh(p, applied0 + (dec == kPSAccept ? 1u : 0u));
   // relaxed: the decision's readers are the next (reduce) launch, behind the kernel boundary (a release
   // here wrote back this XCD's L2 under the running train kernel)
   __hip_atomic_store(p.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (owner) lenet_ps_owner_decide(p, ep, dec);
   if (excl) {
     // one rank (reduce mode 3): this launch's epoch is current from here on, and the count of applied
     // gradients can include this one already -- its only reader is this rank's next admission, which
@@ -1127,6 +1165,91 @@ __device__ __forceinline__ void red_apply(const LeNetRedArgs& a, const RedTables
 // nullptr.  The epoch cannot advance before every owner has passed this wait, and a decision published
 // by the train launch's admission workgroup is already there when the reduce launch starts, so the
 // common case costs no memory round trip here.
+// owner-applies (mode 4), the last arrival of the launch: every owner's shard and inbox stores have landed
+// (each drained before arriving), so the drained prefixes go out, then the drain locks are released (a
+// rank that takes a lock reads the prefix only after its CAS returned), and an admitted gradient's ring slot
+// is flagged at every owner
+__device__ __forceinline__ void lenet_ps_owner_publish(const PSArgs& p, bool admitted) {
+  const unsigned long long* dw = ps_owner_drain_words(p);
+  unsigned held = 0;
+  for (int k = 0; k < p.nshards; ++k) {
+    const unsigned long long w = __hip_atomic_load(const_cast<unsigned long long*>(dw) + k, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned n = (unsigned)(w >> 32) & 0xffu;
+    if (n) {
+      __hip_atomic_store(p.pref + k, (unsigned)w + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      held |= 1u << k;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int k = 0; k < p.nshards; ++k)
+    if ((held >> k) & 1u) __hip_atomic_store(p.dlock + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (admitted) {
+    const unsigned q = p.scratch[kPSSeq], R = (unsigned)p.owner_ring;
+    for (int k = 0; k < p.nshards; ++k)
+      __hip_atomic_store(ps_inbox_flags(p, k) + q % R, q + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// owner-applies: this launch's drain decision (written by the train launch's admission, so it is there when
+// the owners look): s_P / s_n per shard; a word of another epoch (never expected) drains nothing
+__device__ __forceinline__ void lenet_ps_owner_load(const PSArgs& p, unsigned ep, unsigned* s_P, unsigned* s_n) {
+  if ((int)threadIdx.x < p.nshards) {
+    const unsigned long long w = __hip_atomic_load(ps_owner_drain_words(p) + threadIdx.x, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+    const bool ok = ps_owner_word_ep(w) == (ep & 0xffffffu);
+    if (!ok) atomicOr(p.stats + 5, 64ull);
+    s_P[threadIdx.x] = (unsigned)w;
+    s_n[threadIdx.x] = ok ? ((unsigned)(w >> 32) & 0xffu) : 0u;
+  }
+}
+
+// owner-applies, one element gi of the master: the admitted -lr * g (d) into ring slot q % R of its shard's
+// inbox; the shard value, plus -- when this launch drains the shard -- its n flagged slots in sequence order
+// (stored back: the lock holder is the shard's only writer); returns the value the local copies take (+ d
+// when admitted: the gradient's own update, not yet in the shard)
+__device__ __forceinline__ float lenet_ps_owner_elem(const PSArgs& p, float* const* s_shard, float* const* s_inbox,
+                                                     const unsigned* s_P, const unsigned* s_n, long long gi, float d,
+                                                     bool put, unsigned q) {
+  const int k = (int)(gi >> p.shard_shift);
+  const long long off = gi & ((1LL << p.shard_shift) - 1);
+  const unsigned R = (unsigned)p.owner_ring;
+  if (put)
+    __hip_atomic_store(reinterpret_cast<unsigned*>(s_inbox[k] + ((long long)(q % R) << p.shard_shift) + off),
+                       __float_as_uint(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  unsigned* wp = reinterpret_cast<unsigned*>(s_shard[k] + off);
+  float v = __uint_as_float(__hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  const unsigned n = s_n[k];
+  if (n) {
+    const unsigned P = s_P[k];
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      x[j] = (unsigned)j < n ? __uint_as_float(__hip_atomic_load(
+                                   reinterpret_cast<unsigned*>(s_inbox[k] + ((long long)((P + j) % R) << p.shard_shift) + off),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+                             : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma clang fp contract(off)
+      if ((unsigned)j < n) v += x[j];
+    }
+    for (unsigned j = 8; j < n; ++j) {  // (rings longer than 8: the bound's rare tail)
+#pragma clang fp contract(off)
+      v += __uint_as_float(__hip_atomic_load(
+          reinterpret_cast<unsigned*>(s_inbox[k] + ((long long)((P + j) % R) << p.shard_shift) + off), __ATOMIC_RELAXED,
+          __HIP_MEMORY_SCOPE_SYSTEM));
+    }
+    __hip_atomic_store(wp, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  float out;
+  {
+#pragma clang fp contract(off)
+    out = put ? v + d : v;
+  }
+  return out;
+}
+
 __device__ __forceinline__ unsigned lenet_ps_wait(const LeNetRedArgs& a, unsigned* s_dec,
                                                   const unsigned* pre = nullptr) {
   const PSArgs& p = a.ps;
@@ -1172,6 +1295,7 @@ __device__ __forceinline__ void lenet_ps_arrive(const LeNetRedArgs& a, unsigned 
       const unsigned w = known_dec >= 0 ? (unsigned)known_dec
                                         : __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if ((w & 7u) == kPSAccept) ps_publish_applied(p);
+      if (p.owner_ring > 0) lenet_ps_owner_publish(p, (w & 7u) == kPSAccept);
       __hip_atomic_store(p.scratch + kPSApplyDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // (known_ep: the epoch word as thread 0 of a slot owner loaded it; it cannot have moved since)
       const unsigned ep0 = known_ep ? *known_ep
@@ -1210,7 +1334,9 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
   // MODE 3 (async PS, one rank): the synchronous owners' fused update, gated on the train launch's admission
   // decision and mirrored into the rank's master shard; no arrival protocol (the admission advanced the
   // epoch and published the applied count, ps_device.h)
-  constexpr bool LL = MODE == 1, PS = MODE == 2, PSX = MODE == 3;
+  // MODE 4 (async PS, owner-applies): mode 2's protocol with the shard updates through the owners' inboxes
+  // (lenet_ps_owner_elem: plain stores and loads, no per-element remote atomic)
+  constexpr bool LL = MODE == 1, PS = MODE == 2 || MODE == 4, PSX = MODE == 3, OWN = MODE == 4;
   __shared__ float red[4 * kSlotVals];
   __shared__ RedTables tabs;
   __shared__ int owned[kMaxOwned];
@@ -1218,6 +1344,7 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
   __shared__ unsigned s_e;
   __shared__ int s_last;
   __shared__ float* s_shard[kP2PMaxRanks];  // PS: the master shards' bases (ps_elem)
+  __shared__ float* s_inbox[kP2PMaxRanks];  // OWN: the owners' inbox bases
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   __shared__ unsigned long long lr_st[16];
   if (a.stamps && threadIdx.x < 16) lr_st[threadIdx.x] = 0ull;  // (only thread 0 writes them afterwards)
@@ -1227,6 +1354,13 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
   if ((int)blockIdx.x < G) {
     // async PS: the fully applied count before any shard access of this launch (ps_device.h)
     // (successor mode: the barrier after the tables publishes the shard table too)
+    if (OWN && threadIdx.x < kP2PMaxRanks) {
+      float* v = nullptr;
+#pragma unroll
+      for (int k = 0; k < kP2PMaxRanks; ++k)
+        if ((int)threadIdx.x == k) v = a.ps.inbox[k];
+      s_inbox[threadIdx.x] = v;
+    }
     if (PS) ps_stage_shards(a.ps, s_shard, !a.succ);
     stage_tables(a, &tabs);
     // with the fused sync update, the first owned slot's master / momentum elements are loaded beside
@@ -1370,9 +1504,42 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
           float wn[4] = {0.f, 0.f, 0.f, 0.f};  // the shard values after this step (emitted below)
           // an exclusive writer's slot arrival waits for nothing: it goes out now, beside the shard update
           unsigned slot_prev = 0u;
-          if (p.excl && threadIdx.x == 0)
+          if (p.excl && !OWN && threadIdx.x == 0)
             slot_prev = __hip_atomic_fetch_add(a.slot_arr + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (upd && grp4) {
+          if (OWN) {
+            // owner-applies: this launch's drain decision (the admission's), then per element the inbox store
+            // of -lr * g (admitted), the shard's drain (when this launch holds its lock) and the emitted value;
+            // the drain runs whatever the decision (the lock holder must add every slot it counted)
+            __shared__ unsigned s_oP[kP2PMaxRanks], s_on[kP2PMaxRanks], s_oq, s_oep;
+            if (threadIdx.x == 0) {
+              s_oq = p.scratch[kPSSeq];
+              s_oep = ps_pre[0] + 1u;
+            }
+            __syncthreads();
+            lenet_ps_owner_load(p, s_oep, s_oP, s_on);
+            __syncthreads();
+            const bool put = dec == kPSAccept;
+            const unsigned q = s_oq;
+            if (grp4) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (og[j].di >= 0) {
+                  float dj;
+                  {
+#pragma clang fp contract(off)
+                    dj = -(tabs.hyper[0] * vb[q0 + j]);
+                  }
+                  wn[j] = lenet_ps_owner_elem(p, s_shard, s_inbox, s_oP, s_on, tabs.d[og[j].di].off + og[j].i, dj, put, q);
+                }
+            } else if (one && og[0].di >= 0) {
+              float d0;
+              {
+#pragma clang fp contract(off)
+                d0 = -(tabs.hyper[0] * v);
+              }
+              wn[0] = lenet_ps_owner_elem(p, s_shard, s_inbox, s_oP, s_on, tabs.d[og[0].di].off + og[0].i, d0, put, q);
+            }
+          } else if (upd && grp4) {
             float d[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -1428,11 +1595,11 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
           if (upd && grp4)
 #pragma unroll
             for (int j = 0; j < 4; ++j) wb[q0 + j] = wn[j];
-          if (!p.excl) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (!p.excl || OWN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __syncthreads();
           __shared__ unsigned s_arr;
           if (threadIdx.x == 0) {
-            if (!p.excl)
+            if (!p.excl || OWN)
               slot_prev = __hip_atomic_fetch_add(a.slot_arr + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             unsigned n = 0;
             if (slot_prev == (unsigned)(kChunks - 1)) {
@@ -1581,6 +1748,16 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     __syncthreads();
     LR_STAMP(1);
     const unsigned dec = (PS && nown > 0) ? lenet_ps_wait(a, &s_dec) : 0u;
+    __shared__ unsigned s_tP[kP2PMaxRanks], s_tn[kP2PMaxRanks], s_tq, s_tep;
+    if (OWN && nown > 0) {  // owner-applies: the admission's drain decision (see the successor path)
+      if (threadIdx.x == 0) {
+        s_tq = a.ps.scratch[kPSSeq];
+        s_tep = __hip_atomic_load(a.ps.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+      }
+      __syncthreads();
+      lenet_ps_owner_load(a.ps, s_tep, s_tP, s_tn);
+      __syncthreads();
+    }
     LR_STAMP(2);
 #pragma unroll 1
     for (int k = 0; k < nown; ++k) {
@@ -1609,6 +1786,33 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
             m0[e] = a.sgd.mom != nullptr ? a.sgd.mom[off] : 0.f;
           }
         }
+      }
+      if (OWN) {
+        const PSArgs& p = a.ps;
+        float wn[kPerThread];
+#pragma unroll
+        for (int e = 0; e < kPerThread; ++e) {
+          wn[e] = 0.f;
+          if (o[e].di < 0) continue;
+          float d;
+          {
+#pragma clang fp contract(off)
+            d = -(tabs.hyper[0] * v[e]);
+          }
+          wn[e] = lenet_ps_owner_elem(p, s_shard, s_inbox, s_tP, s_tn, tabs.d[o[e].di].off + o[e].i, d,
+                                      dec == kPSAccept, s_tq);
+        }
+        if (dec == kPSAccept || dec == kPSReject) {
+#pragma unroll
+          for (int e = 0; e < kPerThread; ++e) {
+            if (o[e].di < 0) continue;
+            tabs.g[o[e].di][o[e].i] = v[e];
+            if (npos > 1) red_emit<true>(a, tabs, o[e], wn[e]);
+            else if (e == 0) red_emit<false>(a, tabs, o[e], wn[e]);
+          }
+        }
+        if (k == 0) LR_STAMP(5);
+        continue;
       }
       if (PS) {
         if (dec == kPSAccept || dec == kPSReject) {
@@ -1914,7 +2118,15 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
       return hipErrorInvalidValue;
     for (int k = 0; k < r.ps.nshards; ++k)
       if (!r.ps.shard[k]) return hipErrorInvalidValue;
-    if (r.ps.owner_ring > 0) return hipErrorInvalidValue;  // owner-applies runs the generic pull / apply
+    // owner-applies (mode 4): a ring slot is rewritten R sequence numbers later; every owner has drained it by
+    // then only if an admitted gradient is at most R - 2 behind (ps_apply's rule), and the inbox tables exist
+    if (r.ps.owner_ring > 0) {
+      if (r.ps.owner_ring > 255 || r.ps.max_stale < 0 || r.ps.owner_ring < r.ps.max_stale + 2 || !r.ps.pref ||
+          !r.ps.dlock || r.ps.rank < 0 || r.ps.rank >= r.ps.nshards)
+        return hipErrorInvalidValue;
+      for (int k = 0; k < r.ps.nshards; ++k)
+        if (!r.ps.inbox[k]) return hipErrorInvalidValue;
+    }
   }
   // async PS with one rank and successor ownership: mode 3 (the synchronous owners' update gated on the
   // admission, mirrored into the one shard; the admission advances the epoch itself).  Decided before the
@@ -1929,6 +2141,7 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   const dim3 grid(r.exch_blocks + 1 + extra);
   if (r.ll_on) hipLaunchKernelGGL(lenet_reduce_kernel<1>, grid, dim3(RT), 0, st, r);
   else if (psx) hipLaunchKernelGGL(lenet_reduce_kernel<3>, grid, dim3(RT), 0, st, r);
+  else if (r.ps_on && r.ps.owner_ring > 0) hipLaunchKernelGGL(lenet_reduce_kernel<4>, grid, dim3(RT), 0, st, r);
   else if (r.ps_on) hipLaunchKernelGGL(lenet_reduce_kernel<2>, grid, dim3(RT), 0, st, r);
   else hipLaunchKernelGGL(lenet_reduce_kernel<0>, grid, dim3(RT), 0, st, r);
   return hipGetLastError();

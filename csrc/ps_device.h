@@ -73,6 +73,16 @@ __device__ __forceinline__ unsigned ps_read_applied(const PSArgs& a) {
 __device__ __forceinline__ unsigned* ps_inbox_flags(const PSArgs& a, int k) {
   return reinterpret_cast<unsigned*>(a.inbox[k] + ((long long)a.owner_ring << a.shard_shift));
 }
+// owner-applies drain decisions of the fused LeNet-5 step (csrc/lenet_fused.hip mode 4): one u64 per shard in
+// the local scratch (u32 words 32..47), (launch epoch & 0xffffff) << 40 | count << 32 | first sequence number
+constexpr int kPSOwnerDrainWords = 32;
+__device__ __forceinline__ unsigned long long* ps_owner_drain_words(const PSArgs& a) {
+  return reinterpret_cast<unsigned long long*>(a.scratch + kPSOwnerDrainWords);
+}
+__device__ __forceinline__ unsigned long long ps_owner_word(unsigned ep, unsigned n, unsigned P) {
+  return ((unsigned long long)(ep & 0xffffffu) << 40) | ((unsigned long long)(n & 0xffu) << 32) | P;
+}
+__device__ __forceinline__ unsigned ps_owner_word_ep(unsigned long long w) { return (unsigned)(w >> 40); }
 // Records that this workgroup's refresh contains `count` fully applied gradients (the applied count it read
 // + 1 when the refresh values are the results of this rank's own admitted adds): kPSVMin = the minimum.
 __device__ __forceinline__ void ps_note_refresh(const PSArgs& a, unsigned count) {

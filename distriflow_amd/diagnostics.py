@@ -13,9 +13,10 @@ Python switches (default in brackets):
   ps_excl_fused [1]        async PS with one rank, models other than the fused LeNet-5: admission + next claim
                            in one workgroup and the model's optimizer launch gated on the decision (0: pull /
                            refresh / compute / ps_apply launches)
-  ps_owner_apply [0]       async PS apply without remote atomics: gradients pushed into the shard owners'
-                           inbox rings, each owner adds them into its shard during its next pull (the
-                           default per-element CAS adds: profiles/r5/ps_cas_adds_per_us_1gpu.jsonl)
+  ps_owner_apply [-1]      async PS apply path at world > 1: 1 owner-applies (gradients pushed into the shard
+                           owners' inbox rings with plain stores, drained into the shards in sequence order by
+                           the lock holder; no remote atomics), 0 per-element CAS adds, -1 both timed at setup on
+                           the real topology and the faster taken (AsyncPSTrainer._calibrate_apply)
   kcnn_fused [1]           the reference CNN's conv block as one forward + one backward kernel
   fold_dropout [1]         dropout folded into producer epilogues
   khead_fused [1]          the reference CNN's dense head (4608 -> 128 -> C + CE) as one split-K launch
@@ -49,7 +50,7 @@ from __future__ import annotations
 
 import os
 
-_DEFAULTS = {"lenet_fused": 1, "lenet_fused_update": 1, "async_fused": 1, "ps_owner_apply": 0, "ps_excl_fused": 1, "kcnn_fused": 1, "khead_fused": 1, "fold_dropout": 1,
+_DEFAULTS = {"lenet_fused": 1, "lenet_fused_update": 1, "async_fused": 1, "ps_owner_apply": -1, "ps_excl_fused": 1, "kcnn_fused": 1, "khead_fused": 1, "fold_dropout": 1,
              "lenet_succ": 1, "multistep": 1, "graph_steps": 64, "fused_selftest": 1, "wgrad_overlap": 0, "proj_overlap": 0, "concurrent_backward": 0, "bn_epilogue": 0,
              "bn_fused": 0, "bn_acc": 1, "bn_acc_rep": 8}
 

@@ -45,7 +45,7 @@ import torch
 import torch.distributed as dist
 
 from .. import native
-from ..diagnostics import on as diag_on
+from ..diagnostics import diag, on as diag_on
 from .data_parallel import DataParallelTrainer, shared_gpu_exch_blocks
 
 
@@ -80,7 +80,6 @@ class AsyncPSTrainer(DataParallelTrainer):
             dist.all_gather_object(shards, shard, group=group)
         try:
             self.ps.open(ctrl[0], shards)
-            self.ps.init_master(net.store.master)  # every rank seeds its own shard (identical weights)
             self.ps.set_lr_source(net.store.hyper)  # applies read the device lr: set_lr holds after capture
         except Exception as e:
             err = e
@@ -95,14 +94,23 @@ class AsyncPSTrainer(DataParallelTrainer):
         if not self.ps.selftest_check():
             err = RuntimeError("shard add self-test mismatch")
         self._agree(err, "shard self-test check")
-        # owner-applies (csrc/async_ps.hip; diag switch ps_owner_apply): admitted gradients go into the
-        # owners' inbox rings with plain stores, each owner adds them into its own shard during its next pull
-        # -- no remote atomics.  The ring holds max_staleness + 2 gradients (no slot is rewritten before
-        # every owner drained it); a bounded staleness is required.
-        self.owner_apply = diag_on("ps_owner_apply") if owner_apply is None else bool(owner_apply)
-        if self.owner_apply:
-            if self.max_staleness < 0:
-                raise ValueError("owner-applies needs a bounded max_staleness")
+        # Apply path (csrc/async_ps.hip, csrc/ps_device.h):
+        #   CAS            per-element compare-and-swap adds on the owning shards (7/8 of them remote at 8 ranks);
+        #   owner-applies  admitted gradients go into the owners' inbox rings with plain stores, each shard is
+        #                  drained (added in sequence order) by whichever rank holds its drain lock -- no remote
+        #                  atomics.  The ring holds max_staleness + 2 gradients; a bounded staleness is required.
+        # One rank: CAS (the exclusive writer's plain read-modify-writes).  Several: ``owner_apply`` / the diag
+        # switch ps_owner_apply (1 owner, 0 CAS) force a path; by default (-1) both are timed here, every rank at
+        # once on the real topology, over this model's size, and the faster one (max over ranks) is taken.
+        mode = diag("ps_owner_apply") if owner_apply is None else int(bool(owner_apply))
+        self.owner_apply = False
+        self.apply_calib = None
+        want_inbox = self.world > 1 and self.max_staleness >= 0 and mode != 0
+        if mode == 1 and self.max_staleness < 0:
+            raise ValueError("owner-applies needs a bounded max_staleness")
+        if mode == 1 and self.world == 1:
+            want_inbox = True
+        if want_inbox:
             oh = b""
             try:
                 oh = self.ps.owner_init(self.max_staleness + 2)
@@ -113,16 +121,30 @@ class AsyncPSTrainer(DataParallelTrainer):
             if self.world > 1:
                 dist.all_gather_object(ohs, oh, group=group)
             try:
-                self.ps.owner_open(ohs)
+                self.ps.owner_open(ohs, enable=False)
             except Exception as e:
                 err = e
             self._agree(err, "owner inbox open")
+            if mode == 1:
+                self.owner_apply = True
+            else:
+                self.apply_calib = self._calibrate_apply(group)
+                self.owner_apply = self.apply_calib["path"] == "owner-applies"
+            self.ps.owner_enable(self.owner_apply)
+        # every rank seeds its own shard (identical weights) -- after the calibration, which adds zeros to them
+        try:
+            self.ps.init_master(net.store.master)
+        except Exception as e:
+            err = e
+        self._agree(err, "master seed")
+        if self.world > 1:
+            dist.barrier(group=group)
         self._perm = None
         # fused LeNet-5: the reduce launch is the parameter server's apply (2 launches per step)
         import os
 
         self.fused_ps = (bool(getattr(net, "lenet_fused", False)) and net.store.lenet_frag is not None
-                         and diag_on("async_fused") and not self.owner_apply)
+                         and diag_on("async_fused"))
         # a warm-up step would claim a microbatch and apply a real gradient to the shared master: the
         # capture warms up with a compute-only step instead (_capture).  The reduce launch's owners wait for
         # the staging workgroup's admission decision (no lock is taken), then add or read their slots.
@@ -144,6 +166,28 @@ class AsyncPSTrainer(DataParallelTrainer):
         from .watchdog import register_owner_probe
 
         register_owner_probe("async_ps", self, lambda o: o.ps.host_error())
+
+    def _calibrate_apply(self, group, reps: int = 20) -> dict:
+        """Time both apply paths with every rank at once (collective; the shards are not seeded yet, the
+        update is zero): the per-element CAS adds and the owner-applies inbox / shard traffic over this
+        model's elements.  The decision is the max over ranks of each, so every rank takes the same path."""
+        res, err = [0.0, 0.0], None
+        for mode in (0, 1):
+            if self.world > 1:
+                dist.barrier(group=group)
+            try:
+                res[mode] = float(self.ps.calibrate(mode, reps))
+            except Exception as e:
+                err = e
+            self._agree(err, f"apply calibration ({'CAS' if mode == 0 else 'owner-applies'})")
+        t = torch.tensor(res, dtype=torch.float64)
+        if self.world > 1:
+            ts = [torch.zeros_like(t) for _ in range(self.world)]
+            dist.all_gather_object(ts, t, group=group)
+            t = torch.stack(ts).max(0).values
+        cas_us, own_us = float(t[0]), float(t[1])
+        return {"cas_us": round(cas_us, 2), "owner_us": round(own_us, 2),
+                "path": "owner-applies" if own_us < cas_us else "cas", "reps": reps}
 
     def _agree(self, err, what):
         ok = err is None
@@ -285,6 +329,7 @@ class AsyncPSTrainer(DataParallelTrainer):
                 "max_staleness": smax, "admit_retries": retries, "error": err, "version": version,
                 "applied": min(self.ps.owner_prefix()) if self.owner_apply else applied,
                 "apply_path": "owner-applies" if self.owner_apply else "cas",
+                "apply_calibration": self.apply_calib,
                 "cursor": cursor, "noop_steps": noops, "epoch": epoch, "completed_in_epoch": in_epoch,
                 "completed": completed, "redispatched": redisp, "skipped": skipped, "duplicates": dups,
                 "finished": bool(fin)}

@@ -41,7 +41,7 @@ class FedSGDDeviceTrainer(AsyncPSTrainer):
     def __init__(self, net, lr: float = 0.001, min_updates_per_version: int = 20, group=None, server_rank: int = 0,
                  graph: str = "full", timeout_s: float = 30.0):
         super().__init__(net, lr=lr, max_staleness=0, group=group, server_rank=server_rank, graph=graph,
-                         timeout_s=timeout_s)
+                         timeout_s=timeout_s, owner_apply=False)  # (the FedSGD slots, not the async apply)
         self.fused_ps = False  # the generic pull / compute / upload / apply step for every model
         self.K = int(min_updates_per_version)
         if not 1 <= self.K <= 32:
