@@ -14,7 +14,8 @@ def _cos(a, b):
 
 
 @pytest.mark.parametrize("name,B,min_cos", [("mlp_mnist", 64, 0.99), ("lenet5", 128, 0.99), ("keras_cnn", 32, 0.99),
-                                            ("resnet18_cifar", 16, 0.9)])
+                                            ("resnet18_cifar", 16, 0.9), ("resnet18_cifar", 256, 0.9),
+                                            ("keras_cnn", 1024, 0.99)])
 def test_model_gradients_match_cpu(name, B, min_cos):
     g = build_model(name, device="cuda", seed=3)
     from distriflow_amd.models.net import Net
@@ -144,6 +145,33 @@ def test_graph_captured_training_reduces_loss():
         if i % 20 == 0 or i == 119:
             losses.append(float(st[0]) / 256)
     assert losses[-1] < 0.5 * losses[0], losses
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("name,B,steps,lr", [("resnet18_cifar", 256, 60, 0.05), ("keras_cnn", 1024, 60, 0.02)])
+def test_training_at_benchmark_batch_reduces_loss(name, B, steps, lr):
+    """the bench configurations themselves train -- ResNet-18 at B = 256 (CIFAR-shaped) and
+    the reference CNN at B = 1024, graph-captured multi-step replays exactly as bench.py times them: the
+    loss falls and the weights stay finite."""
+    from distriflow_amd.data.synthetic import synthetic_cifar10, synthetic_mnist
+    from distriflow_amd.parallel.data_parallel import DataParallelTrainer, epoch_permutations
+
+    net = build_model(name, device="cuda", seed=0)
+    n = 8 * B
+    data, labels = (synthetic_cifar10 if name == "resnet18_cifar" else synthetic_mnist)(n, seed=1, device="cuda")
+    tr = DataParallelTrainer(net, lr=lr, graph="full")
+    tr.bind_dataset(data, labels, B, scale=1 / 255)
+    tr.bind_index_stream(epoch_permutations(n, B, steps, "cuda", seed=2))
+    tr.prepare_run(10)
+    first = float(tr.run(1)[0]) / B
+    losses = [first]
+    for _ in range((steps - 1) // 10):
+        losses.append(float(tr.run(10)[0]) / B)
+    torch.cuda.synchronize()
+    assert tr.graph_mode == "full"
+    assert torch.isfinite(net.store.master).all()
+    print(name, [round(v, 4) for v in losses])
+    assert losses[-1] < 0.7 * losses[0], losses
 
 
 @pytest.mark.parametrize("name,graph,lr", [("lenet5", "full", 0.05), ("mlp_mnist", "split", 0.05)])

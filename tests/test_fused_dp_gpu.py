@@ -96,7 +96,9 @@ def _union_worker(rank, world, port, out_dir, B, steps, momentum):
         tr.step()
     torch.cuda.synchronize()
     tr.check_comm()
-    torch.save({"w0": w0, "w": net.store.master.cpu(), "g": net.store.grad.cpu()}, os.path.join(out_dir, f"u{rank}.pt"))
+    torch.save({"w0": w0, "w": net.store.master.cpu(), "g": net.store.grad.cpu(),
+                "exch_blocks": int(getattr(net, "lenet_exch_blocks", -1)), "real": real_devices(world)},
+               os.path.join(out_dir, f"u{rank}.pt"))
     finish()
 
 
@@ -137,6 +139,32 @@ def test_world_step_equals_single_rank_step_on_union_batch(world, steps, momentu
         assert gerr <= 1e-4 * g_union.abs().max().item() + 1e-7, gerr
     for x in r[1:]:
         assert torch.equal(x["w"], r[0]["w"])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.skipif(not real_devices(2), reason="the distinct-GPU reduce grid (exch_blocks = 0: one workgroup per "
+                    "job, every slot its own owner) needs a GPU per rank -- two ranks' full grids (2 x ~640 "
+                    "workgroups at 4 per CU) do not fit one GPU at once, so a shared GPU runs the reduced grid")
+def test_distinct_gpu_reduce_grid_equals_union_batch():
+    """the grid the driver's multi-GPU runs take (lenet_exch_blocks = 0, successor
+    ownership with the in-kernel LL exchange) -- not only its start-up self-test -- against one rank on the
+    union batch, over 3 steps."""
+    world, steps, B = 2, 3, 128
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_union_worker, args=(world, free_port(), d, B, steps, 0.0), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"u{i}.pt"), weights_only=True) for i in range(world)]
+    assert all(x["real"] and x["exch_blocks"] == 0 for x in r), [(x["real"], x["exch_blocks"]) for x in r]
+    dev = torch.device("cuda", 0)
+    allrows = _stream(world, B, steps)
+    net, tr = _make(dev, B * world, allrows)
+    for _ in range(steps):
+        tr.step()
+    torch.cuda.synchronize()
+    w1 = net.store.master.cpu()
+    for x in r:
+        rel = ((x["w"] - w1).abs() / w1.abs().clamp_min(1e-3)).max().item()
+        assert rel <= 1e-5, rel
+    assert torch.equal(r[0]["w"], r[1]["w"])
 
 
 def _timeout_worker(rank, world, port, out_dir):
