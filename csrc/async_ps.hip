@@ -487,7 +487,7 @@ static bool ps_shards_ok(const PSArgs& a) {
 // drain decision packs the count in 8 bits)
 static bool ps_owner_ok(const PSArgs& a) {
   if (a.owner_ring <= 0) return true;
-  if (!a.pref || !a.dlock || a.rank < 0 || a.rank >= a.nshards || a.owner_ring > 255) return false;
+  if (!a.pref || !a.dlock || a.rank < 0 || a.owner_ring > 255) return false;  // (a joiner's id is >= nshards)
   for (int k = 0; k < a.nshards; ++k)
     if (!a.inbox[k]) return false;
   return true;

@@ -1802,17 +1802,24 @@ static dfa::LLComm p2p_ll_args(const P2PComm& c) { return c.ll_args(); }
 class PSComm {
  public:
   static constexpr int kTestWords = 64;
-  PSComm(int64_t rank, int64_t world, int64_t server_rank, int64_t n, double timeout_s)
-      : rank_((int)rank), world_((int)world), server_((int)server_rank), n_(n) {
+  // joiner: a worker outside the process group that attaches to a running server (late join, SURVEY §5.3
+  // elastic membership): `rank` is its id (>= world, used as its drain-lock id), it owns no shard, no inbox
+  // and no FedSGD slots, maps every member's, and never writes alone (no exclusive-writer shortcuts)
+  // joinable (members): workers may attach later -- the buffers are uncached even at one rank and the
+  // exclusive-writer shortcuts are off
+  PSComm(int64_t rank, int64_t world, int64_t server_rank, int64_t n, double timeout_s, bool joiner, bool joinable)
+      : rank_((int)rank), world_((int)world), server_((int)server_rank), n_(n), joiner_(joiner),
+        joinable_(joinable || joiner) {
     TORCH_CHECK(n > 0 && n % 4 == 0, "ps: n must be a positive multiple of 4");
     TORCH_CHECK(world >= 1 && world <= dfa::kP2PMaxRanks, "ps: 1..8 ranks");
-    TORCH_CHECK(rank >= 0 && rank < world && server_rank >= 0 && server_rank < world, "ps: bad rank");
+    TORCH_CHECK(server_rank >= 0 && server_rank < world, "ps: bad server rank");
+    TORCH_CHECK(joiner ? (rank >= world && rank < 1024) : (rank >= 0 && rank < world), "ps: bad rank");
     check_hip(hipGetDevice(&dev_), "ps getDevice");
     // shard length: the smallest power of two >= 64 with world shards covering n
     shift_ = 6;
     while (((n_ - 1) >> shift_) >= world_) ++shift_;
     if (rank_ == server_) shared_ = alloc_shared(256 + 2 * (size_t)dfa::kPSMaxBatches * 4, "ps control");
-    own_ = (float*)alloc_shared(((size_t)1 << shift_) * 4 + kTestWords * 4, "ps shard");
+    if (!joiner_) own_ = (float*)alloc_shared(((size_t)1 << shift_) * 4 + kTestWords * 4, "ps shard");
     check_hip(hipMalloc((void**)&local_, 4096), "ps local alloc");
     check_hip(hipMemset(local_, 0, 4096), "ps local memset");
     // kPSVMin (csrc/ps_device.h): no refresh recorded yet
@@ -1839,7 +1846,11 @@ class PSComm {
     TORCH_CHECK(rank_ == server_, "ps: only the server rank exports the control buffer");
     return export_handle(shared_);
   }
-  py::bytes shard_handle() const { return export_handle(own_); }
+  py::bytes shard_handle() const {
+    TORCH_CHECK(!joiner_, "ps: a joiner owns no shard");
+    return export_handle(own_);
+  }
+  bool joiner() const { return joiner_; }
   // ctrl: the server's control-buffer handle; shards[k]: rank k's shard handle (every rank's, own included)
   void open(const std::string& ctrl, std::vector<std::string> shards) {
     TORCH_CHECK((int)shards.size() == world_, "ps: one shard handle per rank");
@@ -1853,6 +1864,7 @@ class PSComm {
   int64_t nshards_used() const { return (n_ - 1) / shard_len() + 1; }
   // every rank: seed its own shard's range of the master (the ranks hold identical initial weights)
   void init_master(torch::Tensor w) {
+    TORCH_CHECK(!joiner_, "ps: a joiner seeds no shard (it pulls the current master)");
     need(w, at::kFloat, "ps master");
     TORCH_CHECK(w.numel() == n_, "ps: master size mismatch");
     const int64_t lo = (int64_t)rank_ * shard_len(), hi = std::min<int64_t>(n_, lo + shard_len());
@@ -1863,6 +1875,7 @@ class PSComm {
   // self-test of the element add on every shard (call on every rank between two barriers): every rank
   // adds (rank + 1) * (j + 1) to word j of every shard's test area
   void selftest_add() {
+    TORCH_CHECK(!joiner_, "ps: the shard self-test runs among the members");
     dfa::PSArgs a = args();
     check_hip(dfa::ps_selftest_add(a, reinterpret_cast<float* const*>(local_ + 2048), kTestWords, (float)(rank_ + 1),
                                    cur_stream()),
@@ -1997,12 +2010,18 @@ class PSComm {
     check_hip(hipDeviceSynchronize(), "fedsgd init sync");
     return export_handle(fed_own_);
   }
-  void fed_open(std::vector<std::string> handles) {
-    TORCH_CHECK(fed_own_ != nullptr && (int)handles.size() == world_, "fedsgd: fed_init first, one handle per rank");
+  void fed_open(std::vector<std::string> handles, int64_t K) {
+    TORCH_CHECK((joiner_ || fed_own_ != nullptr) && (int)handles.size() == world_,
+                "fedsgd: fed_init first (members), one handle per rank");
+    if (joiner_) {
+      TORCH_CHECK(K >= 1 && K <= dfa::kFedMaxK, "fedsgd: K must be 1..", dfa::kFedMaxK);
+      fed_K_ = (int)K;
+      check_hip(hipMemset(local_ + 2560, 0, 1536), "fedsgd local");
+    }
     for (int k = 0; k < world_; ++k) fed_slot_[k] = k == rank_ ? fed_own_ : (float*)open_handle(handles[k]);
   }
   dfa::FedArgs fed_args() const {
-    TORCH_CHECK(fed_own_ != nullptr && fed_slot_[rank_] != nullptr, "fedsgd: fed_open first");
+    TORCH_CHECK((joiner_ || fed_own_ != nullptr) && fed_slot_[0] != nullptr, "fedsgd: fed_open first");
     dfa::FedArgs a{};
     a.seq = reinterpret_cast<unsigned*>(shared_ + 80);
     a.tick = reinterpret_cast<unsigned long long*>(shared_ + 88);
@@ -2085,16 +2104,21 @@ class PSComm {
     return export_handle(inbox_own_);
   }
   // enable = false: map the inboxes only (the apply-path calibration), owner_enable() switches the path
-  void owner_open(std::vector<std::string> handles, bool enable) {
-    TORCH_CHECK(inbox_own_ != nullptr && (int)handles.size() == world_, "ps owner-applies: owner_init first");
+  void owner_open(std::vector<std::string> handles, bool enable, int64_t ring) {
+    TORCH_CHECK((joiner_ || inbox_own_ != nullptr) && (int)handles.size() == world_, "ps owner-applies: owner_init first");
+    if (joiner_) {
+      TORCH_CHECK(ring >= 2 && ring <= 255, "ps owner-applies: a joiner passes the members' ring length");
+      owner_ring_ = (int)ring;
+    }
     for (int k = 0; k < world_; ++k) inbox_[k] = k == rank_ ? inbox_own_ : (float*)open_handle(handles[k]);
     owner_on_ = enable;
   }
   void owner_enable(bool on) {
-    TORCH_CHECK(!on || (inbox_own_ != nullptr && inbox_[rank_] != nullptr), "ps owner-applies: owner_open first");
+    TORCH_CHECK(!on || inbox_[0] != nullptr, "ps owner-applies: owner_open first");
     owner_on_ = on;
   }
   bool owner_applies() const { return owner_on_; }
+  int64_t owner_ring() const { return owner_ring_; }
   // apply-path calibration (collective: every rank calls it at once, between barriers, before init_master):
   // mean microseconds per launch of the CAS adds (mode 0) or the owner-applies traffic (mode 1, needs
   // owner_init / owner_open) over this rank's n elements, `reps` launches after one warm-up launch
@@ -2103,7 +2127,7 @@ class PSComm {
     TORCH_CHECK(mode == 0 || mode == 1, "ps calibrate: mode 0 (CAS) or 1 (owner-applies)");
     TORCH_CHECK(reps >= 1, "ps calibrate: reps >= 1");
     if (mode == 1) {
-      TORCH_CHECK(inbox_own_ != nullptr && inbox_[rank_] != nullptr, "ps calibrate: owner_open first");
+      TORCH_CHECK(inbox_[0] != nullptr, "ps calibrate: owner_open first");
       a.owner_ring = owner_ring_;
       a.pref = reinterpret_cast<unsigned*>(shared_ + 192);
       a.dlock = reinterpret_cast<unsigned*>(shared_ + 224);
@@ -2180,7 +2204,7 @@ class PSComm {
   // pay the uncached operation rate (~6 k per us chip-wide, profiles/r5/ps_cas_adds_per_us_1gpu.jsonl);
   // IPC export works on either.
   char* alloc_shared(size_t bytes, const char* what) const {
-    if (world_ > 1) return alloc_uncached(bytes, what);
+    if (world_ > 1 || joinable_) return alloc_uncached(bytes, what);
     void* p = nullptr;
     check_hip(hipMalloc(&p, bytes), what);
     check_hip(hipMemset(p, 0, bytes), what);
@@ -2210,14 +2234,14 @@ class PSComm {
     return p;
   }
   dfa::PSArgs args() const {
-    TORCH_CHECK(shared_ != nullptr && shard_[rank_] != nullptr, "ps: open() the handles first");
+    TORCH_CHECK(shared_ != nullptr && shard_[0] != nullptr, "ps: open() the handles first");
     dfa::PSArgs a{};
     a.ver = reinterpret_cast<unsigned*>(shared_);
     a.batch_ctr = reinterpret_cast<unsigned long long*>(shared_ + 16);
     for (int k = 0; k < world_; ++k) a.shard[k] = shard_[k];
     a.shard_shift = shift_;
     a.nshards = world_;
-    a.excl = world_ == 1 ? 1 : 0;
+    a.excl = (world_ == 1 && !joinable_) ? 1 : 0;
     a.n = n_;
     a.vpulled = reinterpret_cast<unsigned*>(local_);
     a.applied = reinterpret_cast<unsigned*>(shared_ + 8);  // control buffer word 2 (ps_device.h)
@@ -2249,6 +2273,8 @@ class PSComm {
   }
   HostFlag herr_;
   int rank_, world_, server_, dev_ = 0, shift_ = 6;
+  bool joiner_ = false;
+  bool joinable_ = false;  // other processes may attach: uncached buffers, no exclusive-writer shortcuts
   int max_epochs_ = 0;
   int64_t n_, timeout_ticks_ = 0, nbatches_ = 0;
   char* shared_ = nullptr;
@@ -2493,8 +2519,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("max_floats", &P2PComm::max_floats)
       .def_property_readonly("ll_slots", &P2PComm::ll_slots);
   py::class_<PSComm>(m, "PSComm", "device-resident bounded-staleness parameter server, master sharded over the ranks")
-      .def(py::init<int64_t, int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("world"),
-           py::arg("server_rank"), py::arg("n"), py::arg("timeout_s") = 30.0)
+      .def(py::init<int64_t, int64_t, int64_t, int64_t, double, bool, bool>(), py::arg("rank"), py::arg("world"),
+           py::arg("server_rank"), py::arg("n"), py::arg("timeout_s") = 30.0, py::arg("joiner") = false,
+           py::arg("joinable") = false)
+      .def("joiner", &PSComm::joiner)
       .def("handle", &PSComm::handle)
       .def("shard_handle", &PSComm::shard_handle)
       .def("open", &PSComm::open, py::arg("ctrl"), py::arg("shards"))
@@ -2519,14 +2547,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("stats_tensor", &PSComm::stats_tensor)
       .def("set_audit", &PSComm::set_audit, py::arg("rows"))
       .def("owner_init", &PSComm::owner_init, py::arg("ring"))
-      .def("owner_open", &PSComm::owner_open, py::arg("handles"), py::arg("enable") = true)
+      .def("owner_open", &PSComm::owner_open, py::arg("handles"), py::arg("enable") = true, py::arg("ring") = 0)
       .def("owner_enable", &PSComm::owner_enable, py::arg("on"))
       .def("owner_applies", &PSComm::owner_applies)
+      .def("owner_ring", &PSComm::owner_ring)
       .def("drain", &PSComm::drain)
       .def("owner_prefix", &PSComm::owner_prefix)
       .def("calibrate", &PSComm::calibrate, py::arg("mode"), py::arg("reps") = 20)
       .def("fed_init", &PSComm::fed_init, py::arg("K"))
-      .def("fed_open", &PSComm::fed_open, py::arg("handles"))
+      .def("fed_open", &PSComm::fed_open, py::arg("handles"), py::arg("K") = 0)
       .def("fed_pull", &PSComm::fed_pull)
       .def("fed_upload", &PSComm::fed_upload, py::arg("g"), py::arg("drop_land") = false)
       .def("fed_apply", &PSComm::fed_apply, py::arg("lr"))

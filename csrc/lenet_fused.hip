@@ -2122,7 +2122,7 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
     // then only if an admitted gradient is at most R - 2 behind (ps_apply's rule), and the inbox tables exist
     if (r.ps.owner_ring > 0) {
       if (r.ps.owner_ring > 255 || r.ps.max_stale < 0 || r.ps.owner_ring < r.ps.max_stale + 2 || !r.ps.pref ||
-          !r.ps.dlock || r.ps.rank < 0 || r.ps.rank >= r.ps.nshards)
+          !r.ps.dlock || r.ps.rank < 0)
         return hipErrorInvalidValue;
       for (int k = 0; k < r.ps.nshards; ++k)
         if (!r.ps.inbox[k]) return hipErrorInvalidValue;

@@ -56,18 +56,25 @@ class AsyncPSTrainer(DataParallelTrainer):
     OWNER_MARGIN = 2.0         # calibration: owner-applies only when the CAS adds take over this factor longer
 
     def __init__(self, net, lr: float = 0.001, max_staleness: int = 4, group=None, server_rank: int = 0,
-                 graph: str = "full", timeout_s: float = 30.0, owner_apply: Optional[bool] = None):
+                 graph: str = "full", timeout_s: float = 30.0, owner_apply: Optional[bool] = None,
+                 joinable: bool = False):
+        """``joinable``: workers outside this process group may attach later (:meth:`publish` /
+        :meth:`attach`, parallel/elastic.py): uncached buffers and no exclusive-writer shortcuts even at one
+        rank."""
         if not net.is_gpu:
             raise RuntimeError("AsyncPSTrainer is the GPU path; use AsynchronousSGDServer/Client on CPU")
         super().__init__(net, lr=lr, group=group, overlap=False, graph="full" if graph == "split" else graph,
                          broadcast_init=True, allreduce="rccl")
         self.max_staleness = int(max_staleness)
         self.server_rank = server_rank
+        self.joinable, self.joiner = bool(joinable), False
+        self.timeout_s = float(timeout_s)
         # collective setup: every rank learns whether every other rank managed its part (no rank is left
         # waiting in a barrier that a failed peer never reaches)
         err, handle, shard = None, b"", b""
         try:
-            self.ps = native.require().PSComm(self.rank, self.world, server_rank, net.store.total, timeout_s)
+            self.ps = native.require().PSComm(self.rank, self.world, server_rank, net.store.total, timeout_s,
+                                              joinable=self.joinable)
             if self.rank == server_rank:
                 handle = self.ps.handle()
             shard = self.ps.shard_handle()
@@ -85,6 +92,7 @@ class AsyncPSTrainer(DataParallelTrainer):
         except Exception as e:
             err = e
         self._agree(err, "IPC open")
+        self._handles = {"ctrl": ctrl[0], "shards": shards, "inboxes": None}
         # the element add every apply uses, on every shard from every rank at once, against exact sums
         ok = True
         try:
@@ -121,6 +129,7 @@ class AsyncPSTrainer(DataParallelTrainer):
             ohs = [oh] * self.world
             if self.world > 1:
                 dist.all_gather_object(ohs, oh, group=group)
+            self._handles["inboxes"] = ohs
             try:
                 self.ps.owner_open(ohs, enable=False)
             except Exception as e:
@@ -140,10 +149,12 @@ class AsyncPSTrainer(DataParallelTrainer):
         self._agree(err, "master seed")
         if self.world > 1:
             dist.barrier(group=group)
+        self._finish_setup()
+
+    def _finish_setup(self):
+        net = self.net
         self._perm = None
         # fused LeNet-5: the reduce launch is the parameter server's apply (2 launches per step)
-        import os
-
         self.fused_ps = (bool(getattr(net, "lenet_fused", False)) and net.store.lenet_frag is not None
                          and diag_on("async_fused"))
         # a warm-up step would claim a microbatch and apply a real gradient to the shared master: the
@@ -159,7 +170,7 @@ class AsyncPSTrainer(DataParallelTrainer):
         # then the model's own optimizer launch gated on the decision, writing the new weights to the local
         # master, the compute copies and the shard in one pass (no pull copy, no refresh, no separate apply)
         h = net.store._hyper_host
-        self.excl_fused = (self.world == 1 and not self.fused_ps and not self.owner_apply
+        self.excl_fused = (self.world == 1 and not self.joinable and not self.fused_ps and not self.owner_apply
                            and net.store.compute_bf16 and net.store.lenet_frag is None and diag_on("ps_excl_fused")
                            and h[1] == 0.0 and h[2] == 0.0 and h[3] == 1.0)
         self._primed = False
@@ -167,6 +178,56 @@ class AsyncPSTrainer(DataParallelTrainer):
         from .watchdog import register_owner_probe
 
         register_owner_probe("async_ps", self, lambda o: o.ps.host_error())
+
+    # ------------------------------------------------------------------ elastic membership
+    def attach_meta(self) -> dict:
+        """What a joiner must agree on (parallel/elastic.py)."""
+        return {"n": int(self.net.store.total), "world": self.world, "server_rank": self.server_rank,
+                "max_staleness": self.max_staleness, "timeout_s": self.timeout_s,
+                "owner_ring": int(self.ps.owner_ring()) if self._handles["inboxes"] else 0,
+                "owner_on": bool(self.owner_apply), "fed_K": 0}
+
+    def publish(self, store, prefix: Optional[str] = None):
+        """Members (call on every rank; the server rank writes): publish the server's IPC handles so a worker
+        outside this process group can :meth:`attach` at any time (reference: a client may connect whenever,
+        /root/reference/src/server/asynchronousSGD_server.ts:50-63).  Needs ``joinable=True``."""
+        from . import elastic
+
+        if not self.joinable:
+            raise RuntimeError("publish(): create the trainer with joinable=True")
+        if self.rank == self.server_rank:
+            elastic.publish(store, self.attach_meta(), self._handles["ctrl"], self._handles["shards"],
+                            self._handles["inboxes"], self._handles.get("fed"), prefix=prefix or elastic.PREFIX)
+
+    @classmethod
+    def attach(cls, net, store, joiner_id: int, lr: Optional[float] = None, graph: str = "full",
+               prefix: Optional[str] = None, timeout_s: float = 60.0):
+        """A late-joining worker: a process OUTSIDE the members' process group maps the published server
+        (control buffer, every shard, every inbox) and steps against it like a member -- its first pull
+        copies the current master, its claims come from the shared FCFS cursor, its gradients face the same
+        staleness bound.  ``joiner_id`` (>= the members' world size, unique per joiner) is its drain-lock id."""
+        from . import elastic
+
+        rec = elastic.read(store, prefix or elastic.PREFIX, timeout_s)
+        m = rec["meta"]
+        if int(m["n"]) != net.store.total:
+            raise ValueError(f"attach: the server's master has {m['n']} elements, this model {net.store.total}")
+        self = cls.__new__(cls)
+        DataParallelTrainer.__init__(self, net, lr=0.001 if lr is None else lr, group=None, overlap=False,
+                                     graph="full" if graph == "split" else graph, broadcast_init=False,
+                                     allreduce="rccl")
+        self.max_staleness = int(m["max_staleness"])
+        self.server_rank = int(m["server_rank"])
+        self.joinable, self.joiner = True, True
+        self.timeout_s = float(m.get("timeout_s", 30.0))
+        self._attach_meta = m
+        self.ps = elastic.attach_ps(rec, joiner_id)
+        self.ps.set_lr_source(net.store.hyper)
+        self._handles = {"ctrl": rec["ctrl"], "shards": rec["shards"], "inboxes": rec["inboxes"]}
+        self.owner_apply = bool(m.get("owner_on", False))
+        self.apply_calib = None
+        self._finish_setup()
+        return self
 
     def _calibrate_apply(self, group, reps: int = 20) -> dict:
         """Time both apply paths with every rank at once (collective; the shards are not seeded yet, the

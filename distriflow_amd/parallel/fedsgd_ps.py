@@ -39,9 +39,10 @@ class FedSGDDeviceTrainer(AsyncPSTrainer):
     SUPPORTS_MULTISTEP = False  # the caller supplies each step's rows (step_indices)
 
     def __init__(self, net, lr: float = 0.001, min_updates_per_version: int = 20, group=None, server_rank: int = 0,
-                 graph: str = "full", timeout_s: float = 30.0):
+                 graph: str = "full", timeout_s: float = 30.0, joinable: bool = False):
         super().__init__(net, lr=lr, max_staleness=0, group=group, server_rank=server_rank, graph=graph,
-                         timeout_s=timeout_s, owner_apply=False)  # (the FedSGD slots, not the async apply)
+                         timeout_s=timeout_s, owner_apply=False,  # (the FedSGD slots, not the async apply)
+                         joinable=joinable)
         self.fused_ps = False  # the generic pull / compute / upload / apply step for every model
         self.K = int(min_updates_per_version)
         if not 1 <= self.K <= 32:
@@ -60,8 +61,28 @@ class FedSGDDeviceTrainer(AsyncPSTrainer):
         except Exception as e:
             err = e
         self._agree(err, "fedsgd slot IPC open")
+        self._handles["fed"] = handles
         self._fed_stats_dev = self.ps.fed_stats_tensor()
         self._seq_dev = self.ps.fed_seq_tensor()
+
+    def attach_meta(self) -> dict:
+        m = super().attach_meta()
+        m["fed_K"] = self.K
+        return m
+
+    @classmethod
+    def attach(cls, net, store, joiner_id: int, lr=None, graph: str = "full", prefix=None, timeout_s: float = 60.0):
+        """A late-joining FedSGD client (parallel/elastic.py): maps the members' shards and gradient slots;
+        its first pull is the current version, its uploads take tickets of the current version like a
+        member's (reference: a client may connect at any time, federated_server.ts:60-69)."""
+        self = super().attach(net, store, joiner_id, lr=lr, graph=graph, prefix=prefix, timeout_s=timeout_s)
+        self.fused_ps = False
+        self.K = int(self._attach_meta["fed_K"])
+        if self.K < 1:
+            raise RuntimeError("attach: the published server has no FedSGD slots")
+        self._fed_stats_dev = self.ps.fed_stats_tensor()
+        self._seq_dev = self.ps.fed_seq_tensor()
+        return self
 
     # ------------------------------------------------------------------ one step
     def _has_schedule(self) -> bool:
