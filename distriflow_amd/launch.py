@@ -77,10 +77,21 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--workers", type=int, default=2, help="worker threads when running in one process")
     p.add_argument("--max-staleness", type=int, default=-1)
     p.add_argument("--ship-data", action="store_true")
+    p.add_argument("--store-port", type=int, default=0,
+                   help="device engine: rank 0 hosts a TCPStore on this port and publishes the parameter server's "
+                        "handles there, so workers outside the job can attach later (launch join)")
+    p.add_argument("--wait-joiners", type=int, default=0,
+                   help="with --store-port: start stepping only once this many joiners have attached")
     p.add_argument("--engine", default="auto", choices=["auto", "device", "roles"],
                    help="device = GPU-resident parameter server (parallel/async_ps.py, every rank a worker); "
                         "roles = message-level AsynchronousSGDServer/Client (reference protocol); "
                         "auto = device on GPUs, roles on CPU")
+
+    p = sub.add_parser("join", help="a late-joining async worker: attach to a running device parameter server "
+                                    "(started with async --store-port) and train until its schedule finishes")
+    common(p)
+    p.add_argument("--store", required=True, help="HOST:PORT of the members' TCPStore")
+    p.add_argument("--joiner-id", type=int, default=64, help="unique id >= the members' world size")
 
     p = sub.add_parser("fedsgd", help="FederatedServer / FederatedClient (reference sync PS)")
     common(p)
@@ -343,7 +354,21 @@ def run_async_device(args) -> dict:
     n, B = x.shape[0], args.batch
     nb = n // B
     net = build_model(args.model, device=dev, seed=args.seed)
-    tr = AsyncPSTrainer(net, lr=args.lr, max_staleness=args.max_staleness, graph="full")
+    joinable = bool(getattr(args, "store_port", 0))
+    tr = AsyncPSTrainer(net, lr=args.lr, max_staleness=args.max_staleness, graph="full", joinable=joinable)
+    if joinable:  # late joiners (launch join) read the server's handles from this store
+        import datetime
+
+        store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), args.store_port, is_master=(rank == 0),
+                              wait_for_workers=False, timeout=datetime.timedelta(seconds=300))
+        tr.publish(store)
+        tr._store_keepalive = store
+        if args.wait_joiners > 0:
+            t_w = time.time()
+            while store.add("distriflow/ps/joined", 0) < args.wait_joiners:
+                if time.time() - t_w > 300:
+                    raise RuntimeError(f"async: {args.wait_joiners} joiner(s) did not attach within 300 s")
+                time.sleep(0.05)
     tr.bind_dataset(x, y, B, scale=1.0 / 255.0 if x.dtype == torch.uint8 else 1.0)
     # one table row per microbatch id of an epoch; at-least-once dispatch per epoch on the device
     tr.bind_schedule(epoch_permutations(n, B, nb, dev, seed=args.seed), epochs=args.epochs)
@@ -394,6 +419,42 @@ def run_async_device(args) -> dict:
         log.metric(event="async_done", **out)
         print(json.dumps(out), flush=True)
     shutdown()
+    return out
+
+
+def run_join(args) -> dict:
+    """A worker outside the members' process group (elastic scale-up, parallel/elastic.py): attach to the
+    published device parameter server, train on the shared FCFS schedule until it is finished."""
+    import torch
+
+    from .models.zoo import build_model
+    from .parallel import elastic
+    from .parallel.async_ps import AsyncPSTrainer
+    from .parallel.data_parallel import epoch_permutations
+
+    dev = torch.device("cuda", 0) if _device(args) == "cuda" else None
+    if dev is None:
+        raise RuntimeError("launch join: the device parameter server needs a GPU")
+    torch.cuda.set_device(dev)
+    host, port = args.store.rsplit(":", 1)
+    store = elastic.store_client(host, int(port))
+    x, y = _load_data(args, dev)
+    n, B = x.shape[0], args.batch
+    net = build_model(args.model, device=dev, seed=args.seed)
+    tr = AsyncPSTrainer.attach(net, store, joiner_id=args.joiner_id, lr=args.lr, graph="full")
+    tr.bind_dataset(x, y, B, scale=1.0 / 255.0 if x.dtype == torch.uint8 else 1.0)
+    tr.bind_schedule(epoch_permutations(n, B, n // B, dev, seed=args.seed), epochs=args.epochs)
+    v_join = tr.ps_stats()["version"]
+    store.add("distriflow/ps/joined", 1)  # (members started with --wait-joiners wait for this)
+    steps, cap = 0, 4 * (n // B) * args.epochs + 64
+    while not tr.finished() and steps < cap:
+        for _ in range(8):
+            tr.step()
+            steps += 1
+    torch.cuda.synchronize(dev)
+    tr.check_comm()
+    out = dict(mode="join", joiner_id=args.joiner_id, steps=steps, version_at_attach=v_join, **tr.ps_stats())
+    print(json.dumps(out), flush=True)
     return out
 
 
@@ -684,7 +745,7 @@ def run_fedavg(args) -> dict:
     return out or {}
 
 
-MODES = {"sync": run_sync, "async": run_async, "fedsgd": run_fedsgd, "fedavg": run_fedavg}
+MODES = {"sync": run_sync, "async": run_async, "join": run_join, "fedsgd": run_fedsgd, "fedavg": run_fedavg}
 
 
 def main(argv: Optional[list] = None) -> int:

@@ -231,3 +231,40 @@ def test_late_joiner_trains_lenet_through_the_trainer_api():
     assert r[0]["completed"] + r[0]["duplicates"] == acc
     assert all(x["finite"] for x in r)
     print(f"joiner admitted {j['accepted']} of {steps} (joined at version {j['v_join']}); total {acc}")
+
+
+@pytest.mark.timeout(240)
+def test_launch_join_cli():
+    """``launch async --store-port P --wait-joiners 1`` (one member) and ``launch join --store 127.0.0.1:P``
+    (a second process, no process group): both train the one FCFS schedule to its end; every batch of every
+    epoch completes once (the member's record), the joiner's gradients among them."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    sport = free_port()
+    common = ["--model", "lenet5", "--num-examples", "16384", "--batch", "256", "--epochs", "6", "--lr", "0.05"]
+    mem = subprocess.Popen([sys.executable, "-m", "distriflow_amd.launch", "--master-port", str(free_port()), "async",
+                            *common, "--max-staleness", "4", "--store-port", str(sport), "--wait-joiners", "1"],
+                           cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        j = subprocess.run([sys.executable, "-m", "distriflow_amd.launch", "join", *common, "--store",
+                            f"127.0.0.1:{sport}", "--joiner-id", "5"], cwd=root, env=env, capture_output=True,
+                           text=True, timeout=200)
+        mo, me = mem.communicate(timeout=200)
+    finally:
+        if mem.poll() is None:
+            mem.kill()
+    assert j.returncode == 0, j.stderr[-2000:]
+    assert mem.returncode == 0, me[-2000:]
+    jo = json.loads([l for l in j.stdout.splitlines() if l.startswith("{")][-1])
+    mo = json.loads([l for l in mo.splitlines() if l.startswith("{")][-1])
+    assert mo["finished"] and mo["epoch"] == 6 and mo["completed"] == 6 * (16384 // 256), mo
+    assert jo["error"] == 0 and mo["error"] == 0
+    assert jo["accepted"] > 0, jo
+    assert mo["version"] == mo["accepted"] + jo["accepted"]
+    print("member accepted", mo["accepted"], "joiner accepted", jo["accepted"], "eval", mo.get("eval_accuracy"))
