@@ -297,22 +297,25 @@ __device__ __forceinline__ int lenet_img_group(int b, int nb) {
 // lock-free CAS on the shared version, decision published for the reduce launch's owners (epoch-tagged
 // with that launch's epoch, which no one advances before it runs), the refresh minimum recorded, then the
 // microbatch's completion.
-// Owner-applies (p.owner_ring > 0, reduce mode 4): no per-element remote atomic anywhere.  After its decision
-// the admission takes the drain lock of every shard no other rank is draining (one CAS per shard) and decides
-// how many flagged inbox slots (in sequence order from the shard's drained prefix) the reduce launch adds into
-// it; the decisions go out as one {epoch, count, first} word per shard (ps_owner_drain_words), read by the
-// reduce launch's owners with one load -- no wait inside that launch.  The refresh the owners then emit
-// contains, on every element, each shard's drained prefix (P + n for the shards this launch drains, the
-// prefix read before any shard read otherwise) and -- when admitted with sequence number q and every prefix
-// is q -- this gradient itself, which the owners add to the values they emit: that count is the refresh
-// minimum (ps_device.h).  The own gradient reaches the shards through the inboxes: every owner stores
-// -lr * g of its elements into ring slot q % R of the element's shard inbox (plain system-scope stores), the
-// launch's last arrival flags the slot at every owner once they have all landed (lenet_ps_arrive).
-__device__ __forceinline__ void lenet_ps_owner_decide(const PSArgs& p, unsigned ep, unsigned dec) {
-  const unsigned R = (unsigned)p.owner_ring;
-  unsigned long long* dw = ps_owner_drain_words(p);
-  unsigned cnt = 0xffffffffu;
-  for (int k = 0; k < p.nshards; ++k) {
+// Owner-applies (p.owner_ring > 0, reduce mode 4): no per-element remote atomic anywhere.  At the start of the
+// reduce launch, workgroup 0 (dispatched first; one thread per shard, in parallel) takes the drain lock of every
+// shard nobody else is draining and decides how many flagged inbox slots (in sequence order from the shard's
+// drained prefix) this launch adds into it; the decisions go out as one {epoch, count, first} word per shard
+// (ps_owner_drain_words), which the slot owners read after their jobs.  Deciding here rather than at the
+// admission (the train launch's start, ~50 us earlier) keeps the locks for one reduce launch only and lets
+// the refresh include every gradient flagged until this launch starts.  The refresh the owners emit contains,
+// on every element, each shard's drained prefix (P + n for the shards this launch drains, the prefix read
+// before any shard read otherwise) and -- when admitted with sequence number q and every prefix is q -- this
+// gradient itself, which the owners add to the values they emit: that count is the refresh minimum
+// (ps_device.h).  The own gradient reaches the shards through the inboxes: every owner stores -lr * g of its
+// elements into ring slot q % R of the element's shard inbox (plain system-scope stores), the launch's last
+// arrival flags the slot at every owner once they have all landed (lenet_ps_arrive).
+// (threads 0 .. nshards - 1 of workgroup 0; s_cnt: LDS [kP2PMaxRanks])
+__device__ __forceinline__ void lenet_ps_owner_decide(const PSArgs& p, unsigned* s_cnt) {
+  const int k = threadIdx.x;
+  if (k < p.nshards) {
+    const unsigned ep = __hip_atomic_load(p.scratch + kPSEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const unsigned R = (unsigned)p.owner_ring;
     const unsigned pre = __hip_atomic_load(p.pref + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     unsigned P = 0, n = 0, c = pre, free_ = 0;
     if (__hip_atomic_compare_exchange_strong(p.dlock + k, &free_, (unsigned)p.rank + 1u, __ATOMIC_RELAXED,
@@ -326,11 +329,18 @@ __device__ __forceinline__ void lenet_ps_owner_decide(const PSArgs& p, unsigned 
       if (n == 0) __hip_atomic_store(p.dlock + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       c = P + n;
     }
-    __hip_atomic_store(dw + k, ps_owner_word(ep, n, P), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    cnt = c < cnt ? c : cnt;
+    __hip_atomic_store(ps_owner_drain_words(p) + k, ps_owner_word(ep, n, P), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_cnt[k] = c;
   }
-  if (dec == kPSAccept && cnt == p.scratch[kPSSeq]) cnt += 1u;  // the owners add this gradient to what they emit
-  if (dec == kPSAccept || dec == kPSReject) ps_note_refresh(p, cnt);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned cnt = 0xffffffffu;
+    for (int j = 0; j < p.nshards; ++j) cnt = s_cnt[j] < cnt ? s_cnt[j] : cnt;
+    // the admission ran in the train launch: its decision and sequence number are here
+    const unsigned dec = __hip_atomic_load(p.scratch + kPSDecision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 7u;
+    if (dec == kPSAccept && cnt == p.scratch[kPSSeq]) cnt += 1u;  // the owners add this gradient to what they emit
+    if (dec == kPSAccept || dec == kPSReject) ps_note_refresh(p, cnt);
+  }
 }
 
 __device__ __forceinline__ void lenet_ps_admission(const PSArgs& p, bool excl) {
@@ -345,7 +355,6 @@ __device__ __forceinline__ void lenet_ps_admission(const PSArgs& p, bool excl) {
   // relaxed: the decision's readers are the next (reduce) launch, behind the kernel boundary (a release
   // here wrote back this XCD's L2 under the running train kernel)
   __hip_atomic_store(p.scratch + kPSDecision, (ep << 3) | dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (owner) lenet_ps_owner_decide(p, ep, dec);
   if (excl) {
     // one rank (reduce mode 3): this launch's epoch is current from here on, and the count of applied
     // gradients can include this one already -- its only reader is this rank's next admission, which
@@ -1191,14 +1200,25 @@ __device__ __forceinline__ void lenet_ps_owner_publish(const PSArgs& p, bool adm
   }
 }
 
-// owner-applies: this launch's drain decision (written by the train launch's admission, so it is there when
-// the owners look): s_P / s_n per shard; a word of another epoch (never expected) drains nothing
+// owner-applies: this launch's drain decision (workgroup 0's, made at the launch's start -- normally long done
+// when an owner finishes its job): s_P / s_n per shard.  A wait that times out (never expected) drains nothing
+// there and sets an error bit.
 __device__ __forceinline__ void lenet_ps_owner_load(const PSArgs& p, unsigned ep, unsigned* s_P, unsigned* s_n) {
   if ((int)threadIdx.x < p.nshards) {
-    const unsigned long long w = __hip_atomic_load(ps_owner_drain_words(p) + threadIdx.x, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-    const bool ok = ps_owner_word_ep(w) == (ep & 0xffffffu);
-    if (!ok) atomicOr(p.stats + 5, 64ull);
+    unsigned long long* wp = ps_owner_drain_words(p) + threadIdx.x;
+    unsigned long long w = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool ok = ps_owner_word_ep(w) == (ep & 0xffffffu);
+    const unsigned long long t0 = ok ? 0ull : wall_clock64();
+    while (!ok) {
+      __builtin_amdgcn_s_sleep(1);
+      w = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = ps_owner_word_ep(w) == (ep & 0xffffffu);
+      if (!ok && wall_clock64() - t0 > 2ull * (unsigned long long)p.timeout_ticks) {
+        atomicOr(p.stats + 5, 64ull);
+        if (p.herr) __hip_atomic_store(p.herr, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
     s_P[threadIdx.x] = (unsigned)w;
     s_n[threadIdx.x] = ok ? ((unsigned)(w >> 32) & 0xffu) : 0u;
   }
@@ -1362,6 +1382,10 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
       s_inbox[threadIdx.x] = v;
     }
     if (PS) ps_stage_shards(a.ps, s_shard, !a.succ);
+    if (OWN && blockIdx.x == 0) {
+      __shared__ unsigned s_cnt[kP2PMaxRanks];
+      lenet_ps_owner_decide(a.ps, s_cnt);  // (its barrier also publishes the shard tables)
+    }
     stage_tables(a, &tabs);
     // with the fused sync update, the first owned slot's master / momentum elements are loaded beside
     // its slab loads
