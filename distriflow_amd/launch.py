@@ -648,6 +648,8 @@ def run_fedavg_device(args) -> dict:
                        graph="full" if dev.type == "cuda" else "none")
     tr.bind_dataset(x, y, B, scale=scale)
     tr.bind_index_stream(stream)
+    if dev.type == "cuda":
+        tr.prepare_run(args.local_steps)  # the local steps' multi-step graph, captured before the clock starts
     t0 = time.perf_counter()
     for _ in range(args.rounds):
         tr.run_round()

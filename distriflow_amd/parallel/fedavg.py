@@ -55,9 +55,11 @@ class FedAvgTrainer(DataParallelTrainer):
         self.rounds += 1
 
     def run_round(self):
-        """``local_steps`` captured local steps on the bound index stream, then the average."""
-        st = None
-        for _ in range(self.local_steps):
-            st = self.step()
+        """``local_steps`` captured local steps on the bound index stream, then the average.  The local steps
+        run as multi-step graph replays (:meth:`prepare_run`, up to 64 steps per launch): a round of 50 LeNet-5
+        steps was 50 graph launches, launch-bound at small batches."""
+        if self.graph_mode == "full" and self.net.is_gpu and self._multi_u != min(self.local_steps, 64):
+            self.prepare_run(self.local_steps)
+        st = self.run(self.local_steps)
         self.average()
         return st
