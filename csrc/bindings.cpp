@@ -32,9 +32,27 @@ const T* cptr(const c10::optional<torch::Tensor>& t) {
 }
 
 // geometry: [SH, SW, SC, OH, OW, KH, KW, stride, pad]
-void fill_geom(std::vector<int64_t> g, int* dst) {
-  TORCH_CHECK(g.size() == 9, "geometry must have 9 ints");
-  for (int i = 0; i < 9; ++i) dst[i] = (int)g[i];
+// Conv geometry [SH, SW, SC, OH, OW, KH, KW, stride, pad(, stride_w, pad_w)] (the launch's source / output
+// dims: for the data gradient the source is dY and the output dX).  stride / pad are the row stride and the
+// top padding; the output size may imply more padding at the bottom / right than at the top / left (Keras
+// 'same' with an odd total).  Anything but one stride, one symmetric padding and a square kernel is
+// 'irregular': the specialised kernels refuse it and the generic implicit GEMM runs.
+template <typename A>
+void set_conv_geom(A& a, const std::vector<int64_t>& geom, int mode) {
+  TORCH_CHECK(geom.size() == 9 || geom.size() == 11, "geometry must have 9 or 11 ints");
+  int g[11];
+  for (size_t i = 0; i < geom.size(); ++i) g[i] = (int)geom[i];
+  if (geom.size() == 9) g[9] = g[7], g[10] = g[8];
+  a.SH = g[0]; a.SW = g[1]; a.SC = g[2]; a.OH = g[3]; a.OW = g[4]; a.KH = g[5]; a.KW = g[6];
+  a.stride = g[7]; a.pad = g[8]; a.stride_w = g[9]; a.pad_w = g[10];
+  a.irregular = 0;
+  if (mode == dfa::MODE_DIRECT) return;
+  TORCH_CHECK(a.stride >= 1 && a.stride_w >= 1 && a.pad >= 0 && a.pad_w >= 0 && a.KH >= 1 && a.KW >= 1,
+              "conv geometry: stride >= 1, pad >= 0");
+  const bool fwd = mode == dfa::MODE_FWD;
+  const int ih = fwd ? a.SH : a.OH, iw = fwd ? a.SW : a.OW, oh = fwd ? a.OH : a.SH, ow = fwd ? a.OW : a.SW;
+  a.irregular = a.KH != a.KW || a.stride_w != a.stride || a.pad_w != a.pad ||
+                oh != (ih + 2 * a.pad - a.KH) / a.stride + 1 || ow != (iw + 2 * a.pad - a.KW) / a.stride + 1;
 }
 
 dfa::DropSpec drop_from(double p, int64_t seed, const c10::optional<torch::Tensor>& step, int64_t step_add) {
@@ -75,10 +93,7 @@ void igemm_fwd_py(torch::Tensor src, torch::Tensor w, c10::optional<torch::Tenso
   }
   TORCH_CHECK(ldc >= N, "ldc < N");
   dfa::IGemmArgs a{};
-  int g[9];
-  fill_geom(geom, g);
-  a.SH = g[0]; a.SW = g[1]; a.SC = g[2]; a.OH = g[3]; a.OW = g[4]; a.KH = g[5]; a.KW = g[6]; a.stride = g[7];
-  a.pad = g[8];
+  set_conv_geom(a, geom, (int)mode);
   if (mode == 0) {
     TORCH_CHECK(src.numel() >= (M - 1) * lda + K, "src too small for [M][lda]");
   } else {
@@ -219,10 +234,7 @@ void igemm_wgrad_py(torch::Tensor dy, torch::Tensor src, torch::Tensor gw, c10::
   TORCH_CHECK(gw.numel() >= N * K, "gw too small");
   TORCH_CHECK(dy.numel() >= (M - 1) * ldd + N, "dy too small");
   dfa::WgradArgs a{};
-  int g[9];
-  fill_geom(geom, g);
-  a.SH = g[0]; a.SW = g[1]; a.SC = g[2]; a.OH = g[3]; a.OW = g[4]; a.KH = g[5]; a.KW = g[6]; a.stride = g[7];
-  a.pad = g[8];
+  set_conv_geom(a, geom, (int)mode);
   if (mode == 0) {
     TORCH_CHECK(src.numel() >= (M - 1) * lda + K, "src too small");
   } else {
@@ -2321,10 +2333,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                    int64_t mode, int64_t bacc_mode, bool two, bool has_res, bool has_mask) {
     // the dispatch decision of igemm_fwd for a launch with these shapes (16-byte aligned operands)
     dfa::IGemmArgs a{};
-    int g[9];
-    fill_geom(geom, g);
-    a.SH = g[0]; a.SW = g[1]; a.SC = g[2]; a.OH = g[3]; a.OW = g[4]; a.KH = g[5]; a.KW = g[6]; a.stride = g[7];
-    a.pad = g[8];
+    set_conv_geom(a, geom, (int)mode);
     a.M = (int)M; a.N = (int)N; a.K = (int)K; a.Kpad = (int)Kpad; a.ldc = (int)N; a.lda = 0;
     static dfa::bf16 dummy[8] __attribute__((aligned(16)));
     static double dacc[2] __attribute__((aligned(16)));
@@ -2341,10 +2350,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("igemm64_bn_tiles", [](int64_t M, int64_t N, int64_t K, int64_t Kpad, std::vector<int64_t> geom, int64_t mode) {
     dfa::IGemmArgs a{};
-    int g[9];
-    fill_geom(geom, g);
-    a.SH = g[0]; a.SW = g[1]; a.SC = g[2]; a.OH = g[3]; a.OW = g[4]; a.KH = g[5]; a.KW = g[6]; a.stride = g[7];
-    a.pad = g[8];
+    set_conv_geom(a, geom, (int)mode);
     a.M = (int)M; a.N = (int)N; a.K = (int)K; a.Kpad = (int)Kpad; a.ldc = (int)N;
     static dfa::bf16 layout_dummy[8] __attribute__((aligned(16)));
     a.src = layout_dummy; a.w = layout_dummy; a.out = layout_dummy;

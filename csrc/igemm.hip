@@ -54,10 +54,10 @@ struct ALoader {
       rbase = (long long)b * a.SH * a.SW * a.SC;
       if (MODE == MODE_FWD) {
         r0 = oh * a.stride - a.pad;
-        r1 = ow * a.stride - a.pad;
+        r1 = ow * a.stride_w - a.pad_w;
       } else {
         r0 = oh + a.pad;
-        r1 = ow + a.pad;
+        r1 = ow + a.pad_w;
       }
     }
   }
@@ -87,10 +87,10 @@ struct ALoader {
     } else {  // DGRAD: dX(ih,iw) <- dY((ih+pad-kh)/s, (iw+pad-kw)/s)
       int th = r0 - kh_, tw = r1 - kw_;
       if (th < 0 || tw < 0) return -1;
-      if (a.stride > 1) {
-        if ((th % a.stride) | (tw % a.stride)) return -1;
+      if ((a.stride | a.stride_w) > 1) {
+        if ((th % a.stride) | (tw % a.stride_w)) return -1;
         th /= a.stride;
-        tw /= a.stride;
+        tw /= a.stride_w;
       }
       sh = th;
       sw = tw;
@@ -404,7 +404,7 @@ __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradArgs a) {
       const int oh = rem / a.OW;
       const int ow = rem - oh * a.OW;
       r0 = oh * a.stride - a.pad;
-      r1 = ow * a.stride - a.pad;
+      r1 = ow * a.stride_w - a.pad_w;
       img = (long long)b * a.SH * a.SW * a.SC;
     }
 #pragma unroll
@@ -577,22 +577,23 @@ bool igemm_bacc_ok(const IGemmArgs& a, int mode) {
   if (mode == MODE_DIRECT || a.out_f32 || a.drop.on || a.pool_code || a.bn.part || a.M <= 0 || a.N <= 0) return false;
   if (a.bacc.nrep < 1 || a.bacc.nrep > kBnAccMaxRep || (a.bacc.mode == 1 && (!a.bacc.x || !a.bacc.mean))) return false;
   if (a.bacc.acc2 && (a.bacc.mode != 1 || !a.bacc.x2 || !a.bacc.mean2)) return false;
-  if (conv3_halo_supported(a, mode) || igemm64_supported(a, mode)) {
+  if (!a.irregular && (conv3_halo_supported(a, mode) || igemm64_supported(a, mode))) {
     if ((a.ldc & 3) || (a.N & 3) || ((uintptr_t)a.out & 15) ||
         (((uintptr_t)a.res | (uintptr_t)a.resmask | (uintptr_t)a.mask | (uintptr_t)a.bacc.x | (uintptr_t)a.bacc.x2) & 7))
       return false;
     return a.N <= 1024 && 256 % (a.N / 4) == 0;  // (a split-K combine may apply the epilogue)
   }
-  return mode == MODE_FWD && a.bacc.mode == 0 && !smallc_fwd_supported(a, mode);
+  return mode == MODE_FWD && a.bacc.mode == 0 && (a.irregular || !smallc_fwd_supported(a, mode));
 }
 
 hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0) return hipSuccess;
   if (a.bacc.acc && !igemm_bacc_ok(a, mode)) return hipErrorInvalidValue;
   if (a.drop.on && (a.out_f32 || a.ldc != a.N)) return hipErrorInvalidValue;
+  if (a.irregular && (a.pool_code || a.bn.part)) return hipErrorInvalidValue;
   if (a.pool_code) return igemm64_pool_supported(a) && mode == MODE_FWD ? igemm64(a, mode, st) : hipErrorInvalidValue;
-  if (conv3_halo_supported(a, mode)) return conv3_halo(a, mode, st);
-  if (igemm64_supported(a, mode)) return igemm64(a, mode, st);  // dropout in its epilogues
+  if (!a.irregular && conv3_halo_supported(a, mode)) return conv3_halo(a, mode, st);
+  if (!a.irregular && igemm64_supported(a, mode)) return igemm64(a, mode, st);  // dropout in its epilogues
   if (!a.drop.on) return igemm_fwd_nodrop(a, mode, st);
   IGemmArgs b = a;
   b.drop = DropSpec{};
@@ -602,7 +603,7 @@ hipError_t igemm_fwd(const IGemmArgs& a, int mode, hipStream_t st) {
 }
 
 static hipError_t igemm_fwd_nodrop(const IGemmArgs& a, int mode, hipStream_t st) {
-  if (smallc_fwd_supported(a, mode)) return smallc_fwd(a, st);
+  if (!a.irregular && smallc_fwd_supported(a, mode)) return smallc_fwd(a, st);
   const bool aligned = ((uintptr_t)a.src & 15) == 0;
   if (mode == MODE_DIRECT) {
     const bool vec = aligned && a.lda % 8 == 0 && a.K % 8 == 0;
@@ -656,9 +657,11 @@ hipError_t igemm_wgrad(const WgradArgs& a, int mode, float* workspace, size_t ws
     const bool xvec = ((uintptr_t)a.src & 15) == 0 && a.lda % 8 == 0;
     return launch_wgrad_x<MODE_DIRECT>(a, dvec, xvec, workspace, ws_floats, st);
   }
-  if (wgrad_halo_supported(a, mode)) return wgrad_halo(a, workspace, ws_floats, st);
-  if (wgrad_tr_supported(a, mode)) return wgrad_tr(a, workspace, ws_floats, st);
-  if (smallc_wgrad_supported(a, mode)) return smallc_wgrad(a, workspace, ws_floats, st);
+  if (!a.irregular) {
+    if (wgrad_halo_supported(a, mode)) return wgrad_halo(a, workspace, ws_floats, st);
+    if (wgrad_tr_supported(a, mode)) return wgrad_tr(a, workspace, ws_floats, st);
+    if (smallc_wgrad_supported(a, mode)) return smallc_wgrad(a, workspace, ws_floats, st);
+  }
   const bool xvec = ((uintptr_t)a.src & 15) == 0 && a.SC % 8 == 0;
   return launch_wgrad_x<MODE_FWD>(a, dvec, xvec, workspace, ws_floats, st);
 }

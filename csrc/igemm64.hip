@@ -933,7 +933,7 @@ bool igemm64_pool_supported(const IGemmArgs& a) {
 bool igemm64_supported(const IGemmArgs& a, int mode) {
   if (((uintptr_t)a.src & 15) || ((uintptr_t)a.w & 15) || a.Kpad % 8 || a.M <= 0 || a.N <= 0) return false;
   if (mode == MODE_DIRECT) return a.lda % 8 == 0 && a.K % 8 == 0;
-  return a.SC % 8 == 0 && a.OH > 0 && a.OW > 0;
+  return !a.irregular && a.SC % 8 == 0 && a.OH > 0 && a.OW > 0;
 }
 
 hipError_t igemm64(const IGemmArgs& a, int mode, hipStream_t st) {

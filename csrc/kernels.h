@@ -85,6 +85,9 @@ struct IGemmArgs {
   void* out;         // [M][ldc] bf16 or fp32
   int M, N, K, Kpad, lda, ldc;
   int SH, SW, SC, OH, OW, KH, KW, stride, pad;
+  int stride_w, pad_w;  // column stride / left padding (stride, pad: row stride / top padding)
+  int irregular;        // 1: KH != KW, stride_w != stride, pad_w != pad or asymmetric (Keras 'same') padding --
+                        // only the generic kernels (igemm.hip) take such a geometry
   int relu, out_f32;
   float alpha;
   float* splitk_ws;  // igemm64 split-K partials [splits][M][N] (nullptr: no split)
@@ -104,6 +107,7 @@ struct WgradArgs {
   float* gb;          // [N] final bias grad or nullptr
   int M, N, K, ldd, lda;
   int SH, SW, SC, OH, OW, KH, KW, stride, pad;
+  int stride_w, pad_w, irregular;  // as IGemmArgs
   int m_per_split, splits, with_bias;
   float scale;
 };

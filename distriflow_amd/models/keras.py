@@ -10,7 +10,8 @@ Keras 2.1.4 Sequential (/root/reference/experiment/mnist/model.json:1).  Support
   Maximum, Minimum, Concatenate on the channel axis) or fan out from one layer to several (the
   branching region runs as one :class:`~distriflow_amd.models.graph.GraphLayer`, models/graph.py);
   the logits layer (the output) must be a Dense fed by a single chain;
-* InputLayer, Conv2D, Dense, Activation (relu, relu6, sigmoid, tanh, elu, selu, softplus, softsign,
+* InputLayer, Conv2D (any kernel size / strides pair, 'valid' or 'same' -- an odd 'same' total pads the
+  bottom / right, as TensorFlow does), Dense, Activation (relu, relu6, sigmoid, tanh, elu, selu, softplus, softsign,
   hard_sigmoid, swish / silu, exponential, linear; softmax / sigmoid as the output), MaxPooling2D and
   AveragePooling2D (any pool / strides, 'valid' or 'same'), GlobalAveragePooling2D,
   GlobalMaxPooling2D, Dropout, Flatten, BatchNormalization — channels_last only.

@@ -179,12 +179,13 @@ class Conv2D(Layer):
                  use_bias=True, name=None, kernel_initializer="glorot_uniform"):
         super().__init__(name or "conv2d")
         self.filters = int(filters)
-        ks = (kernel_size, kernel_size) if isinstance(kernel_size, int) else tuple(kernel_size)
-        st = (strides, strides) if isinstance(strides, int) else tuple(strides)
-        if ks[0] != ks[1] or st[0] != st[1]:
-            raise NotImplementedError("only square kernels / strides")
-        self.k = int(ks[0])
-        self.stride = int(st[0])
+        self.kh, self.kw = ops._pair(kernel_size)
+        self.sh, self.sw = ops._pair(strides)
+        # k / stride / pad: the square kernel, single stride and symmetric padding of a regular conv (what
+        # the fused and specialised paths match on); None when the geometry is not regular, which then runs
+        # on the generic implicit-GEMM kernels (csrc/igemm.hip) with per-axis strides and top/left padding
+        self.k = self.kh if self.kh == self.kw else None
+        self.stride = self.sh if self.sh == self.sw else None
         self.padding = padding
         self.activation = activation
         self.use_bias = use_bias
@@ -198,29 +199,34 @@ class Conv2D(Layer):
         H, W, C = in_shape
         self.in_shape = (H, W, C)
         if self.padding == "same":
-            OH = (H + self.stride - 1) // self.stride
-            OW = (W + self.stride - 1) // self.stride
-            total = max((OH - 1) * self.stride + self.k - H, 0)
-            if total % 2:
-                raise NotImplementedError("asymmetric 'same' padding")
-            self.pad = total // 2
-        elif self.padding == "valid":
-            self.pad = 0
+            (OH, OW), self.pads = ops.same_padding(H, W, self.kh, self.kw, (self.sh, self.sw))
         else:
-            self.pad = int(self.padding)
-        OH, OW = ops.conv_out_hw(H, W, self.k, self.k, self.stride, self.pad)
+            self.pads = (0, 0) if self.padding == "valid" else ops._pair(self.padding)
+            OH, OW = ops.conv_out_hw(H, W, self.kh, self.kw, (self.sh, self.sw), self.pads)
+        if OH < 1 or OW < 1:
+            raise ValueError(f"Conv2D {self.name}: input {H}x{W} too small for kernel {self.kh}x{self.kw}")
+        sym = (OH, OW) == ops.conv_out_hw(H, W, self.kh, self.kw, (self.sh, self.sw), self.pads)
+        self.pad = self.pads[0] if sym and self.pads[0] == self.pads[1] else None
+        self.regular = self.k is not None and self.stride is not None and self.pad is not None
         self.out_shape = (OH, OW, self.filters)
         return self.out_shape
+
+    @property
+    def geom(self):
+        """(KH, KW, stride, pad) as the conv ops take them: ints when regular, else per-axis tuples."""
+        if self.regular:
+            return self.k, self.k, self.stride, self.pad
+        return self.kh, self.kw, (self.sh, self.sw), self.pads
 
     def can_fuse_relu(self):
         return True
 
     def specs(self):
         H, W, C = self.in_shape
-        K = self.k * self.k * C
-        fan_in, fan_out = K, self.k * self.k * self.filters
-        s = [ParamSpec(f"{self.name}/kernel", (self.filters, self.k, self.k, C), "matrix",
-                       (self.filters, self.k * self.k, C), self.kernel_initializer, (fan_in, fan_out),
+        K = self.kh * self.kw * C
+        fan_in, fan_out = K, self.kh * self.kw * self.filters
+        s = [ParamSpec(f"{self.name}/kernel", (self.filters, self.kh, self.kw, C), "matrix",
+                       (self.filters, self.kh * self.kw, C), self.kernel_initializer, (fan_in, fan_out),
                        needs_dgrad=self.need_dx)]
         if self.use_bias:
             s.append(ParamSpec(f"{self.name}/bias", (self.filters,), "vector", init="zeros"))
@@ -231,7 +237,7 @@ class Conv2D(Layer):
     def bacc_ok(self, dgrad: bool, mode: int, two: bool = False, has_res: bool = False, has_mask: bool = False) -> bool:
         """Can this conv's forward (or data-gradient) launch accumulate the sums of a consuming BatchNorm in
         its epilogue (csrc/bn_acc.h)?  Shape / dispatch dependent; cached per variant."""
-        if self.out is None or self.out.device.type != "cuda" or not diag_on("bn_acc"):
+        if self.out is None or self.out.device.type != "cuda" or not diag_on("bn_acc") or not self.regular:
             return False
         key = (dgrad, mode, two, has_res, has_mask)
         if key not in self._bacc_cache:
@@ -251,7 +257,7 @@ class Conv2D(Layer):
         # BatchNorm statistics finalised inside this conv's own launches (csrc/bn_epi.h): the forward's for
         # the BN that consumes the output, the data gradient's for the BN that produced the input
         self._bn_fwd = self._bn_bwd = None
-        if torch.device(device).type == "cuda" and diag_on("bn_epilogue"):
+        if torch.device(device).type == "cuda" and diag_on("bn_epilogue") and self.regular:
             H, W, C = self.in_shape
             OH, OW, N = self.out_shape
             kpad = primary_kpad_of(self)
@@ -282,8 +288,8 @@ class Conv2D(Layer):
                         momentum=bn.momentum, eps=bn.eps)
         elif bn is not None and training and bn.acc_on and self.bacc_ok(False, 0):
             bacc = dict(acc=bn.acc, mode=0)
-        ops.conv_fwd(x, st.weight(f"{self.name}/kernel"), b, self.out, self.k, self.k, self.stride, self.pad,
-                     relu=self.relu, bn=spec, bacc=bacc)
+        ops.conv_fwd(x, st.weight(f"{self.name}/kernel"), b, self.out, *self.geom, relu=self.relu, bn=spec,
+                     bacc=bacc)
         if spec is not None:
             bn.x = self.out
             bn._stats_ready = True
@@ -306,7 +312,7 @@ class Conv2D(Layer):
         st = self.store
         kn = f"{self.name}/kernel"
         gb = st.gradient(f"{self.name}/bias") if self.use_bias else None
-        ops.conv_wgrad(dy, self.x, st.grad_matrix(kn), gb, self.ws.wgrad, self.k, self.k, self.stride, self.pad)
+        ops.conv_wgrad(dy, self.x, st.grad_matrix(kn), gb, self.ws.wgrad, *self.geom)
 
     def backward_data(self, dy, residual=None, residual_mask=None, dx_mask=None, bn: Optional["BatchNorm"] = None,
                       bn_acc: Optional[list] = None):
@@ -332,8 +338,8 @@ class Conv2D(Layer):
             if len(bn_acc) == 2:
                 b1 = bn_acc[1]
                 bacc.update(acc2=b1.acc_b, x2=b1.x, mean2=b1.mean, invstd2=b1.invstd)
-        ops.conv_dgrad(dy, st.weight(kn), st.weight_t(kn), self.dx, self.k, self.k, self.stride, self.pad,
-                       mask=mask, residual=residual, residual_mask=residual_mask, bn=spec, bacc=bacc)
+        ops.conv_dgrad(dy, st.weight(kn), st.weight_t(kn), self.dx, *self.geom, mask=mask, residual=residual,
+                       residual_mask=residual_mask, bn=spec, bacc=bacc)
         if bacc is not None:
             for b in bn_acc:
                 b._bwd_acc_ready = True
@@ -341,7 +347,7 @@ class Conv2D(Layer):
         return self.dx
 
     def config(self):
-        return {"filters": self.filters, "kernel_size": [self.k, self.k], "strides": [self.stride, self.stride],
+        return {"filters": self.filters, "kernel_size": [self.kh, self.kw], "strides": [self.sh, self.sw],
                 "padding": self.padding if isinstance(self.padding, str) else "valid",
                 "activation": self.activation, "use_bias": self.use_bias}
 

@@ -266,14 +266,16 @@ class Net:
         while i < len(execd):
             l = execd[i]
             nxt = execd[i + 1] if i + 1 < len(execd) else None
-            if (isinstance(l, Conv2D) and isinstance(nxt, MaxPooling2D) and l.relu and l.stride == 1 and nxt.p == 2
+            if (isinstance(l, Conv2D) and isinstance(nxt, MaxPooling2D) and l.relu and l.regular and l.stride == 1
+                    and nxt.p == 2
                     and l.out_shape[0] % 2 == 0 and l.out_shape[1] % 2 == 0
                     and ops.convpool_supported(l.in_shape[0], l.in_shape[1], l.in_shape[2], l.k, l.k, l.pad,
                                                l.filters)):
                 out.append(FusedConvPool(l, nxt))
                 i += 2
                 continue
-            if (isinstance(l, Conv2D) and isinstance(nxt, MaxPooling2D) and l.relu and l.stride == 1 and nxt.p == 2
+            if (isinstance(l, Conv2D) and isinstance(nxt, MaxPooling2D) and l.relu and l.regular and l.stride == 1
+                    and nxt.p == 2
                     and l.out_shape[0] % 2 == 0 and l.out_shape[1] % 2 == 0
                     and ops.conv_pool_supported(l.in_shape[0], l.in_shape[1], l.in_shape[2], l.k, l.k, l.stride,
                                                 l.pad, l.filters)):
@@ -299,7 +301,7 @@ class Net:
         convs = [c for l in self._all_leaf_layers()
                  for c in ((l.conv,) if isinstance(l, ConvPoolGemm) else
                            (l.conv1, l.conv2) if isinstance(l, KerasConvBlock) else (l,))]
-        nk = max([l.filters * l.k * l.k * l.in_shape[2] for l in convs if isinstance(l, Conv2D)]
+        nk = max([l.filters * l.kh * l.kw * l.in_shape[2] for l in convs if isinstance(l, Conv2D)]
                  + [0])
         ws_wgrad = torch.empty(max(1 << 22, 4 * nk), dtype=torch.float32, device=self.device)
         maxC = max([l.C for l in self._all_leaf_layers() if isinstance(l, BatchNorm)] + [8])
@@ -734,11 +736,11 @@ class Net:
             if isinstance(l, (FusedConvPool, ConvPoolGemm)):
                 c = l.conv
                 OH, OW, N = c.out_shape
-                f = 2 * OH * OW * N * c.k * c.k * c.in_shape[2]
+                f = 2 * OH * OW * N * c.kh * c.kw * c.in_shape[2]
                 return f * (3 if l.need_dx else 2)
             if isinstance(l, Conv2D):
                 OH, OW, N = l.out_shape
-                f = 2 * OH * OW * N * l.k * l.k * l.in_shape[2]
+                f = 2 * OH * OW * N * l.kh * l.kw * l.in_shape[2]
                 return f * (3 if l.need_dx else 2)
             return 0
 

@@ -70,12 +70,32 @@ def graph_upload(g) -> bool:
         return False
 
 
+def _pair(v):
+    return (int(v[0]), int(v[1])) if isinstance(v, (tuple, list)) else (int(v), int(v))
+
+
 def _geom(SH=1, SW=1, SC=1, OH=1, OW=1, KH=1, KW=1, stride=1, pad=0):
-    return [int(SH), int(SW), int(SC), int(OH), int(OW), int(KH), int(KW), int(stride), int(pad)]
+    """Native conv geometry.  ``stride`` = s or (row, column); ``pad`` = p or (top, left) -- the bottom /
+    right padding is whatever the output size implies (asymmetric Keras 'same')."""
+    (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
+    g = [int(SH), int(SW), int(SC), int(OH), int(OW), int(KH), int(KW), sh, ph]
+    return g if (sh, ph) == (sw, pw) else g + [sw, pw]
 
 
 def conv_out_hw(H, W, KH, KW, stride, pad):
-    return (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+    """Output size of a conv with symmetric padding ``pad`` = p or (ph, pw) and ``stride`` = s or (sh, sw)."""
+    (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
+    return (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
+
+
+def same_padding(H, W, KH, KW, stride):
+    """Keras / TF 'same': output ceil(in / stride); total padding max((out - 1) * s + k - in, 0) split with
+    the odd element at the bottom / right.  Returns ((OH, OW), (top, left))."""
+    sh, sw = _pair(stride)
+    OH, OW = -(-H // sh), -(-W // sw)
+    th = max((OH - 1) * sh + KH - H, 0)
+    tw = max((OW - 1) * sw + KW - W, 0)
+    return (OH, OW), (th // 2, tw // 2)
 
 
 # ----------------------------------------------------------------------------------- dense
@@ -179,7 +199,7 @@ def conv_fwd(x, w, bias, out, KH, KW, stride=1, pad=0, relu=False, bn=None, bacc
                        _geom(H, W, C, OH, OW, KH, KW, stride, pad), MODE_FWD, relu, 1.0, **_bn_kwargs(bn),
                        **_bacc_kwargs(bacc))
     else:
-        out.copy_(ref.conv_fwd(x, w, bias, KH, KW, stride, pad, relu))
+        out.copy_(ref.conv_fwd(x, w, bias, KH, KW, stride, pad, relu, out_hw=(OH, OW)))
     return out
 
 

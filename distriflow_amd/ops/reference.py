@@ -23,11 +23,37 @@ def conv_weight_4d(w2d, N, KH, KW, C):
     return w2d[:N, : KH * KW * C].reshape(N, KH, KW, C).permute(0, 3, 1, 2)
 
 
-def conv_fwd(x, w2d, bias, KH, KW, stride, pad, relu):
+def _conv_pad(x, KH, KW, stride, pad, OH, OW):
+    """NCHW input padded for a padding-free conv of output OH x OW: ``pad`` = (top, left); the bottom /
+    right padding (possibly negative = cropped rows that no output reads) follows from the output size."""
+    (sh, sw), (pt, pl) = _pair(stride), _pair(pad)
+    H, W = x.shape[2], x.shape[3]
+    pb = (OH - 1) * sh + KH - H - pt
+    pr = (OW - 1) * sw + KW - W - pl
+    return F.pad(x, (pl, pr, pt, pb))
+
+
+def _pair(v):
+    return (int(v[0]), int(v[1])) if isinstance(v, (tuple, list)) else (int(v), int(v))
+
+
+def _out_hw(H, W, KH, KW, stride, pad):
+    (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
+    return (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
+
+
+def _conv(xc, w4, bias, KH, KW, stride, pad, OH, OW):
+    return F.conv2d(_conv_pad(xc, KH, KW, stride, pad, OH, OW), w4, bias, stride=_pair(stride))
+
+
+def conv_fwd(x, w2d, bias, KH, KW, stride, pad, relu, out_hw=None):
+    """fp32 NHWC conv.  ``stride`` = s or (sh, sw); ``pad`` = p or (top, left); ``out_hw`` = (OH, OW)
+    (default: symmetric padding)."""
     B, H, W, C = x.shape
     N = bias.shape[0] if bias is not None else w2d.shape[0]
     w4 = conv_weight_4d(w2d.float(), N, KH, KW, C)
-    y = F.conv2d(_nchw(x.float()), w4, bias.float() if bias is not None else None, stride=stride, padding=pad)
+    OH, OW = out_hw or _out_hw(H, W, KH, KW, stride, pad)
+    y = _conv(_nchw(x.float()), w4, bias.float() if bias is not None else None, KH, KW, stride, pad, OH, OW)
     if relu:
         y = torch.relu(y)
     return _nhwc(y)
@@ -35,9 +61,12 @@ def conv_fwd(x, w2d, bias, KH, KW, stride, pad, relu):
 
 def conv_dgrad(dy, w2d, in_shape, KH, KW, stride, pad, mask=None):
     B, H, W, C = in_shape
-    N = dy.shape[-1]
+    _, OH, OW, N = dy.shape
     w4 = conv_weight_4d(w2d.float(), N, KH, KW, C)
-    dx = torch.nn.grad.conv2d_input((B, C, H, W), w4, _nchw(dy.float()), stride=stride, padding=pad)
+    xz = torch.zeros((B, C, H, W), dtype=torch.float32, device=dy.device, requires_grad=True)
+    with torch.enable_grad():
+        y = _conv(xz, w4, None, KH, KW, stride, pad, OH, OW)
+        dx, = torch.autograd.grad(y, xz, _nchw(dy.float()))
     dx = _nhwc(dx)
     if mask is not None:
         dx = dx * (mask.float() > 0)
@@ -46,8 +75,11 @@ def conv_dgrad(dy, w2d, in_shape, KH, KW, stride, pad, mask=None):
 
 def conv_wgrad(dy, x, KH, KW, stride, pad, with_bias=True):
     B, H, W, C = x.shape
-    N = dy.shape[-1]
-    gw = torch.nn.grad.conv2d_weight(_nchw(x.float()), (N, C, KH, KW), _nchw(dy.float()), stride=stride, padding=pad)
+    _, OH, OW, N = dy.shape
+    w4 = torch.zeros((N, C, KH, KW), dtype=torch.float32, device=dy.device, requires_grad=True)
+    with torch.enable_grad():
+        y = _conv(_nchw(x.float()), w4, None, KH, KW, stride, pad, OH, OW)
+        gw, = torch.autograd.grad(y, w4, _nchw(dy.float()))
     gw = gw.permute(0, 2, 3, 1).reshape(N, KH * KW * C)
     gb = dy.float().sum(dim=(0, 1, 2)) if with_bias else None
     return gw, gb
