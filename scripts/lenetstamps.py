@@ -26,6 +26,9 @@ def main():
     data, labels = synthetic_mnist(60000, seed=1, device="cuda")
     idx = torch.randperm(60000, device="cuda")[:B]
     x, y = ops.GatherRef(data, idx, 1 / 255.0, (28, 28, 1)), ops.LabelRef(labels, idx)
+    if "contig" in sys.argv[2:]:  # rows 0 .. B-1, no index indirection (what a pre-staged batch costs)
+        x.idx = None
+        y = labels[:B].to(torch.int32).contiguous()
 
     def wall(n=50):
         for _ in range(3):
