@@ -613,39 +613,55 @@ static int bn_acc_grid(long long nvec, int C, int nrep) {
   return (int)std::min(4096LL, std::max(256LL, g));
 }
 
-// the nrep replicas of [S, Q] of channel c, summed in replica order (all loads issued together)
-__device__ __forceinline__ void bn_fin_sums(const BnAccFin& f, int C, int c, double& S, double& Q) {
-  double s[kBnAccMaxRep], q[kBnAccMaxRep];
+// The nrep replicas of [S, Q] of the CPT channels c + 256 k of this thread, summed in replica order.  Every
+// load of a chunk of 8 replicas is issued before the first is used, at a clamped (always valid) address, its
+// value selected afterwards: with one branch per replica the compiler waited for each load in turn -- and,
+// vmcnt being in order, for the tensor loads issued before them -- a chain of round trips that cost 2-3 us
+// per launch on a tiny tensor (scripts/bn_microbench.py).  One chunk (nrep <= 8): one round trip.
+template <int CPT, int RC = 8>
+__device__ __forceinline__ void bn_fin_sums(const BnAccFin& f, int C, int c, double (&S)[CPT], double (&Q)[CPT]) {
 #pragma unroll
-  for (int r = 0; r < kBnAccMaxRep; ++r) {
-    s[r] = r < f.nrep ? f.acc[(long long)(2 * r) * C + c] : 0.0;
-    q[r] = r < f.nrep ? f.acc[(long long)(2 * r + 1) * C + c] : 0.0;
-  }
-  S = 0.0, Q = 0.0;
+  for (int k = 0; k < CPT; ++k) S[k] = 0.0, Q[k] = 0.0;
 #pragma unroll
-  for (int r = 0; r < kBnAccMaxRep; ++r) {
-    S += s[r];
-    Q += q[r];
+  for (int r0 = 0; r0 < kBnAccMaxRep; r0 += RC) {
+    if (r0 >= f.nrep) break;  // (uniform)
+    double s[CPT][RC], q[CPT][RC];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int cc = min(c + 256 * k, C - 1);
+#pragma unroll
+      for (int j = 0; j < RC; ++j) {
+        const long long rr = min(r0 + j, f.nrep - 1);
+        s[k][j] = f.acc[(2 * rr) * C + cc];
+        q[k][j] = f.acc[(2 * rr + 1) * C + cc];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CPT; ++k)
+#pragma unroll
+      for (int j = 0; j < RC; ++j) {
+        S[k] += r0 + j < f.nrep ? s[k][j] : 0.0;
+        Q[k] += r0 + j < f.nrep ? q[k][j] : 0.0;
+      }
   }
 }
 
-// forward: mean / invstd of channel c (workgroup 0 also publishes them, updates the running statistics and
-// clears f.zero); returns the affine pair (sa, sb) of gamma, beta
+// forward: mean / invstd of channel c from its sums (workgroup 0 also publishes them, updates the running
+// statistics and clears f.zero); returns the affine pair (sa, sb) of gamma, beta.  The moments are fp64
+// (S, Q and the cancellation in Q / M - m^2); invstd is an fp32 reciprocal square root of the variance.
 __device__ __forceinline__ void bn_fin_fwd(const BnAccFin& f, const float* gamma, const float* beta, int C, long long M,
-                                           int c, float& sa, float& sb) {
-  double S, Q;
-  bn_fin_sums(f, C, c, S, Q);
-  const double m = S / M;
-  double var = Q / M - m * m;
+                                           double invM, int c, double S, double Q, float& sa, float& sb) {
+  const double m = S * invM;
+  double var = Q * invM - m * m;
   if (var < 0.0) var = 0.0;
-  const float is = (float)(1.0 / sqrt(var + (double)f.eps));
+  const float is = rsqrtf((float)var + f.eps);
   sa = gamma[c] * is;
   sb = beta[c] - (float)m * sa;
   if (blockIdx.x == 0) {
     f.mean[c] = (float)m;
     f.invstd[c] = is;
     if (f.run_mean) {
-      const double unb = M > 1 ? var * M / (M - 1) : var;
+      const double unb = M > 1 ? var * ((double)M / (double)(M - 1)) : var;
       f.run_mean[c] = (float)((1.0 - f.momentum) * f.run_mean[c] + f.momentum * m);
       f.run_var[c] = (float)((1.0 - f.momentum) * f.run_var[c] + f.momentum * unb);
     }
@@ -654,12 +670,21 @@ __device__ __forceinline__ void bn_fin_fwd(const BnAccFin& f, const float* gamma
   }
 }
 
+// replicas per load batch of the finalisation
+#ifndef DFA_BN_FIN_RC
+#define DFA_BN_FIN_RC 8
+#endif
+constexpr int kBnFinRC = DFA_BN_FIN_RC;
+// channels per thread of the finalisation (256 threads)
+static int bn_cpt(int C) { return C <= 256 ? 1 : (C <= 512 ? 2 : 4); }
+
 // The streaming part of both consumers: a thread's vectors i = i0 + k * stride in batches of kBnVecs, every
 // load of a batch issued before its stores (a load behind a store waits for that store too); the first
 // batch's loads go out BEFORE the statistics are finalised (they do not depend on them), so the prologue's
 // replica reads and the first tensor reads share one round trip.
-template <int RES>
+template <int RES, int CPT>
 __global__ void __launch_bounds__(256) bn_apply_acc_kernel(BnApplyArgs a, BnAccFin f, BnAccFin fr) {
+  constexpr int RC = kBnFinRC;
   __shared__ float co[4][kBnAccMaxC];  // sa, sb, ra, rb
   const int C = a.C;
   const long long M = a.M;
@@ -678,14 +703,25 @@ __global__ void __launch_bounds__(256) bn_apply_acc_kernel(BnApplyArgs a, BnAccF
     }
   };
   load(i0);
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float sa, sb, ra = 1.f, rb = 0.f;
-    bn_fin_fwd(f, a.gamma, a.beta, C, M, c, sa, sb);
-    if (RES == 2) bn_fin_fwd(fr, a.rgamma, a.rbeta, C, M, c, ra, rb);
-    co[0][c] = sa;
-    co[1][c] = sb;
-    co[2][c] = ra;
-    co[3][c] = rb;
+  const double invM = 1.0 / (double)M;
+  {
+    const int c = threadIdx.x;
+    double S[CPT], Q[CPT], RS[CPT], RQ[CPT];
+    bn_fin_sums<CPT, RC>(f, C, c, S, Q);
+    if (RES == 2) bn_fin_sums<CPT, RC>(fr, C, c, RS, RQ);
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int ck = c + 256 * k;
+      if (ck < C) {
+        float sa, sb, ra = 1.f, rb = 0.f;
+        bn_fin_fwd(f, a.gamma, a.beta, C, M, invM, ck, S[k], Q[k], sa, sb);
+        if (RES == 2) bn_fin_fwd(fr, a.rgamma, a.rbeta, C, M, invM, ck, RS[k], RQ[k], ra, rb);
+        co[0][ck] = sa;
+        co[1][ck] = sb;
+        co[2][ck] = ra;
+        co[3][ck] = rb;
+      }
+    }
   }
   __syncthreads();
   const int c0 = (int)(threadIdx.x % (C / 8)) * 8;  // constant: 256 and the grid stride are multiples of C/8
@@ -694,8 +730,8 @@ __global__ void __launch_bounds__(256) bn_apply_acc_kernel(BnApplyArgs a, BnAccF
   for (int j = 0; j < 8; ++j) {
     sa[j] = co[0][c0 + j];
     sb[j] = co[1][c0 + j];
-    ra[j] = co[2][c0 + j];
-    rb[j] = co[3][c0 + j];
+    ra[j] = RES == 2 ? co[2][c0 + j] : 1.f;
+    rb[j] = RES == 2 ? co[3][c0 + j] : 0.f;
   }
   bf16x8* ys = reinterpret_cast<bf16x8*>(a.y);
   for (long long base = i0; base < total; base += kBnVecs * stride) {
@@ -708,7 +744,8 @@ __global__ void __launch_bounds__(256) bn_apply_acc_kernel(BnApplyArgs a, BnAccF
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float v = (float)xv[k][j] * sa[j] + sb[j];
-        if (RES) v += (float)rv[k][j] * ra[j] + rb[j];
+        if (RES == 1) v += (float)rv[k][j];  // (ra, rb = 1, 0: the same value)
+        if (RES == 2) v += (float)rv[k][j] * ra[j] + rb[j];
         if (a.relu) v = fmaxf(v, 0.f);
         o[j] = f2bf(v);
       }
@@ -725,13 +762,29 @@ hipError_t bn_apply_acc(const BnApplyArgs& a, const BnAccFin& f, const BnAccFin*
   const int nrep = f.nrep + (fr ? fr->nrep : 0);
   const int grid = bn_acc_grid((long long)a.M * a.C / 8, a.C, nrep);
   const BnAccFin none{};
-  if (res == 0) hipLaunchKernelGGL(bn_apply_acc_kernel<0>, dim3(grid), dim3(256), 0, st, a, f, none);
-  else if (res == 1) hipLaunchKernelGGL(bn_apply_acc_kernel<1>, dim3(grid), dim3(256), 0, st, a, f, none);
-  else hipLaunchKernelGGL(bn_apply_acc_kernel<2>, dim3(grid), dim3(256), 0, st, a, f, *fr);
+  const BnAccFin& g = fr ? *fr : none;
+#define DFA_BN_APPLY_ACC(R, CPT) \
+  hipLaunchKernelGGL((bn_apply_acc_kernel<R, CPT>), dim3(grid), dim3(256), 0, st, a, f, g)
+#define DFA_BN_APPLY_ACC_C(R)                      \
+  switch (bn_cpt(a.C)) {                           \
+    case 1: DFA_BN_APPLY_ACC(R, 1); break;         \
+    case 2: DFA_BN_APPLY_ACC(R, 2); break;         \
+    default: DFA_BN_APPLY_ACC(R, 4); break;        \
+  }
+  if (res == 0) {
+    DFA_BN_APPLY_ACC_C(0)
+  } else if (res == 1) {
+    DFA_BN_APPLY_ACC_C(1)
+  } else {
+    DFA_BN_APPLY_ACC_C(2)
+  }
+#undef DFA_BN_APPLY_ACC_C
+#undef DFA_BN_APPLY_ACC
   return hipGetLastError();
 }
 
 // backward: dx = k1 g + k2 x + k3, k from [S = sum g, Q = sum g * xhat]
+template <int CPT>
 __global__ void __launch_bounds__(256) bn_dx_acc_kernel(const bf16* __restrict__ x, const bf16* __restrict__ g,
                                                         bf16* __restrict__ dx, BnAccFin f, long long M, int C) {
   __shared__ float k[3][kBnAccMaxC];
@@ -750,25 +803,40 @@ __global__ void __launch_bounds__(256) bn_dx_acc_kernel(const bf16* __restrict__
     }
   };
   load(i0);
-  for (int c = threadIdx.x; c < C; c += 256) {
-    double S, Q;
-    bn_fin_sums(f, C, c, S, Q);
-    const double isd = f.invstd[c], gam = f.gamma[c], m = f.mean[c];
-    const double k1 = gam * isd;
-    const float a1 = (float)k1, a2 = (float)(-k1 * isd * Q / M), a3 = (float)(k1 * (m * isd * Q / M - S / M));
-    k[0][c] = a1;
-    k[1][c] = a2;
-    k[2][c] = a3;
-    if (blockIdx.x == 0) {
-      f.dbeta[c] = (float)S * f.gscale;
-      f.dgamma[c] = (float)Q * f.gscale;
-      if (f.coef) {
-        f.coef[c] = a1;
-        f.coef[C + c] = a2;
-        f.coef[2 * C + c] = a3;
+  {
+    const int c = threadIdx.x;
+    // the per-channel inputs of the coefficients, issued with the replica loads (clamped, one round trip)
+    float isd[CPT], gam[CPT], mn[CPT];
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const int cc = min(c + 256 * j, C - 1);
+      isd[j] = f.invstd[cc];
+      gam[j] = f.gamma[cc];
+      mn[j] = f.mean[cc];
+    }
+    double S[CPT], Q[CPT];
+    bn_fin_sums<CPT, kBnFinRC>(f, C, c, S, Q);
+    const double invM = 1.0 / (double)M;
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const int cj = c + 256 * j;
+      if (cj >= C) continue;
+      const double is = isd[j], k1 = (double)gam[j] * is, sm = S[j] * invM, qm = Q[j] * invM;
+      const float a1 = (float)k1, a2 = (float)(-k1 * is * qm), a3 = (float)(k1 * ((double)mn[j] * is * qm - sm));
+      k[0][cj] = a1;
+      k[1][cj] = a2;
+      k[2][cj] = a3;
+      if (blockIdx.x == 0) {
+        f.dbeta[cj] = (float)S[j] * f.gscale;
+        f.dgamma[cj] = (float)Q[j] * f.gscale;
+        if (f.coef) {
+          f.coef[cj] = a1;
+          f.coef[C + cj] = a2;
+          f.coef[2 * C + cj] = a3;
+        }
+        if (f.zero)
+          for (int r = 0; r < 2 * f.nrep; ++r) f.zero[(long long)r * C + cj] = 0.0;
       }
-      if (f.zero)
-        for (int r = 0; r < 2 * f.nrep; ++r) f.zero[(long long)r * C + c] = 0.0;
     }
   }
   __syncthreads();
@@ -800,7 +868,11 @@ hipError_t bn_dx_acc(const bf16* x, const bf16* g, bf16* dx, const BnAccFin& f, 
       !f.gamma || !f.dgamma)
     return hipErrorInvalidValue;
   const int grid = bn_acc_grid((long long)M * C / 8, C, f.nrep);
-  hipLaunchKernelGGL(bn_dx_acc_kernel, dim3(grid), dim3(256), 0, st, x, g, dx, f, (long long)M, C);
+  switch (bn_cpt(C)) {
+    case 1: hipLaunchKernelGGL(bn_dx_acc_kernel<1>, dim3(grid), dim3(256), 0, st, x, g, dx, f, (long long)M, C); break;
+    case 2: hipLaunchKernelGGL(bn_dx_acc_kernel<2>, dim3(grid), dim3(256), 0, st, x, g, dx, f, (long long)M, C); break;
+    default: hipLaunchKernelGGL(bn_dx_acc_kernel<4>, dim3(grid), dim3(256), 0, st, x, g, dx, f, (long long)M, C); break;
+  }
   return hipGetLastError();
 }
 
