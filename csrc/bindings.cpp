@@ -1373,7 +1373,8 @@ void lenet_train_py(torch::Tensor x, c10::optional<torch::Tensor> idx, double sc
     TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.numel() % 784 == 0, "lenet: uint8 dataset [N][28][28][1]");
     a.x_u8 = x.data_ptr<uint8_t>();
     a.nrows = x.numel() / 784;
-    TORCH_CHECK(idx.has_value() && idx->defined(), "lenet: a uint8 dataset needs batch indices");
+    TORCH_CHECK((idx.has_value() && idx->defined()) || a.nrows >= B,
+                "lenet: a uint8 dataset without batch indices must hold the batch (rows 0 .. B-1)");
   } else {
     need(x, at::kBFloat16, "lenet x");
     TORCH_CHECK(x.numel() == B * 784, "lenet: x must be [B][28][28][1]");

@@ -507,6 +507,9 @@ struct LeNetArgs {
   // ps_admit with one rank (the exclusive writer, lenet_reduce_kernel<3>): the admission also advances the
   // launch epoch and publishes the applied count itself (the reduce launch has no arrival protocol)
   int ps_excl;
+  // images per train workgroup (lenet_ipw): 8, or fewer at small batches -- more workgroups, each running
+  // only its images' share of the per-image phases (the critical path of a small step is one workgroup's)
+  int ipw;
   PSArgs ps;
 };
 struct LeNetDense {

@@ -9,7 +9,8 @@
 //   lenet_prep_kernel    the conv weights of this step as ready-made MFMA B fragments (banded conv1,
 //                        conv2 forward, pair-banded conv2 data gradient): 37 x 1 KB, read by every
 //                        workgroup with one 16-byte load per lane and fragment
-//   lenet_train_kernel   one workgroup = 8 images, 4 waves, ~78 KB of LDS (two workgroups per CU):
+//   lenet_train_kernel   one workgroup = 8 images (fewer at small batches: lenet_ipw), 8 waves, ~78 KB of
+//                        LDS (two workgroups per CU):
 //     conv1 5x5 'same' + bias + ReLU + 2x2 max-pool   MFMA with a banded (Toeplitz) weight operand:
 //                          A = 32 consecutive input pixels of a row (one aligned ds_read_b128; odd
 //                          output columns read a copy of the image shifted by one pixel), so the
@@ -365,6 +366,11 @@ __device__ __forceinline__ void lenet_ps_admission(const PSArgs& p, bool excl) {
   if (dec == kPSAccept && p.done_epoch != nullptr) complete_microbatch(p, bid);
 }
 
+// TRIM (a.ipw < IMG, small batches): the per-image loops (conv1, conv2, conv2 weight and data gradient,
+// conv1 weight gradient) run over the tiles of this workgroup's live images only; the rest of the LDS images
+// stay as phase 0 left them (zero input, zero output gradient), so the skipped tiles would only have added
+// zeros.  TRIM = false is the full-batch kernel, every bound a compile-time constant.
+template <bool TRIM>
 __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs a) {
   if ((int)blockIdx.x >= a.nblk) {  // async PS: the admission workgroup
     if (a.ps_admit && threadIdx.x == 0) lenet_ps_admission(a.ps, a.ps_excl != 0);
@@ -395,8 +401,14 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   // treated as divergent: exec-mask branches, each waiting for all LDS reads in flight)
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), i = lane & 15,
             g = lane >> 4;
-  const int r0 = lenet_img_group(blockIdx.x, a.nblk) * IMG;
-  const int rows = min(IMG, a.B - r0);
+  const int r0 = lenet_img_group(blockIdx.x, a.nblk) * (TRIM ? a.ipw : IMG);
+  const int rows = min(TRIM ? a.ipw : IMG, a.B - r0);
+  // per-image loop trip counts (tiles of 16 / 32 rows over rows-of-image blocks of 56, 104, 98, 14)
+  const int nA = TRIM ? 2 * ((7 * rows + 1) / 2) : 56;        // conv1: 3.5 M-tiles per image, 2 halves each
+  const int nB = TRIM ? (13 * rows + 1) / 2 : NM / 16;        // conv2: 6.5 M-tiles per image
+  const int nE = TRIM ? ((13 * rows + 3) / 4 + 1) / 2 * 2 : NM / 32;  // conv2 wgrad: 3.25 steps, paired
+  const int nF = TRIM ? (49 * rows + 7) / 8 : 49;             // conv2 dgrad: 6.125 M-tiles per image
+  const int nG = TRIM ? 14 * rows : IMG * 14;                 // conv1 wgrad: 14 pool-window rows per image
   const bf16x8* __restrict__ frag = reinterpret_cast<const bf16x8*>(a.frag);
   float* part = a.conv_part + (long long)blockIdx.x * kLeNetConvStride;  // this workgroup's partials
   unsigned long long* const stamps = a.stamps;
@@ -500,7 +512,7 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   {
     const float b1c[3] = {WS[(i >> 3)], WS[2 + (i >> 3)], WS[4 + (i >> 3)]};
 #pragma unroll 2
-    for (int u = w; u < 56; u += NT / 64) {
+    for (int u = w; u < nA; u += NT / 64) {
       const int mt = u >> 1, x0 = (u & 1) * 16;
       const int m = 16 * mt + i;
       const int img = m / 56, rem = m - 56 * (m / 56);
@@ -551,7 +563,7 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
     }
     const float b2 = WS[6 + i];
 #pragma unroll 2
-    for (int mt = w; mt < NM / 16; mt += NT / 64) {  // padded rows: window 25 of an image is padding
+    for (int mt = w; mt < nB; mt += NT / 64) {  // padded rows: window 25 of an image is padding
       const bf16* abase = P1 + (int)PX[16 * mt + i] * 8;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -732,7 +744,7 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
     bf16x8 ava = ldAv(0);
     unsigned pxa0 = pxl[0], pxa1 = pxl[4];
 #pragma unroll 1
-    for (int s = 0; s < NM / 32; s += 2) {
+    for (int s = 0; s < nE; s += 2) {
       // (scheduling barriers keep the prefetches where they are: the scheduler otherwise hoists every LDS
       // read to the top of the loop body and waits for all of them there)
       const bf16x8 avb = ldAv(s + 1);
@@ -740,7 +752,7 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
       __builtin_amdgcn_sched_barrier(0);
       step(ava, pxa0, pxa1);
       __builtin_amdgcn_sched_barrier(0);
-      const int sn = s + 2 < NM / 32 ? s + 2 : s;  // the last pair re-reads its own rows (unused)
+      const int sn = s + 2 < nE ? s + 2 : s;  // the last pair re-reads its own rows (unused)
       ava = ldAv(sn);
       pxa0 = pxl[32 * sn];
       pxa1 = pxl[32 * sn + 4];
@@ -771,7 +783,7 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
   {
     const int bcol = i >> 3, c = i & 7;
 #pragma unroll 2
-    for (int mt = w; mt < 49; mt += NT / 64) {
+    for (int mt = w; mt < nF; mt += NT / 64) {
       const int m = 16 * mt + i;
       const int img = m / 98, rem = m - 98 * (m / 98);
       const uint4 tv = *reinterpret_cast<const uint4*>(FT + (rem * 2 + (g >> 1)) * 16);
@@ -845,7 +857,7 @@ __global__ void __launch_bounds__(NT, 2 * NT / 256) lenet_train_kernel(LeNetArgs
 #pragma unroll
     for (int wd = 0; wd < 4; ++wd) cmask[wd] = (4 * g + wd < 14 && i < 12) ? 0u : 8u;
 #pragma unroll 2
-    for (int rp = w; rp < IMG * 14; rp += NT / 64) {
+    for (int rp = w; rp < nG; rp += NT / 64) {
       const int img = rp / 14, py = rp - 14 * (rp / 14);
       const int p0 = (img * 14 + py) * 14 + 4 * g;
       const uint2 cA = *reinterpret_cast<const uint2*>(C1 + p0);
@@ -2021,7 +2033,21 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
 }  // namespace
 
 size_t lenet_train_lds() { return LDS_BYTES; }
-int lenet_blocks(int B) { return (B + IMG - 1) / IMG; }
+// images per train workgroup: the smallest of 1, 2, 4, 8 that keeps the grid within one workgroup per CU
+// (256), else 8.  Measured (one MI355X, sync step, 200 steps; profiles/r6/lenet_ipw_sweep.txt): B = 32
+// 26.7 us with 1 image per workgroup vs 39.1 with 8; B = 256 28.0 vs 39.9; B = 1024 36.8 (4) vs 43.0 (8) and
+// 43.9 (2, 512 workgroups); B = 2048 45.4 (8) vs 48.9 (4).  DISTRIFLOW_DIAG=lenet_ipw=<1|2|4|8> forces one.
+int lenet_ipw(int B) {
+  static const int forced = diag_int("lenet_ipw", 0);
+  if (forced == 1 || forced == 2 || forced == 4 || forced == IMG) return forced;
+  int ipw = 1;
+  while (ipw < IMG && (B + ipw - 1) / ipw > 256) ipw *= 2;
+  return ipw;
+}
+int lenet_blocks(int B) {
+  const int ipw = lenet_ipw(B);
+  return (B + ipw - 1) / ipw;
+}
 
 static unsigned long long* g_lenet_stamps_host = nullptr;
 void lenet_set_stamps(void* buf) { g_lenet_stamps_host = reinterpret_cast<unsigned long long*>(buf); }
@@ -2066,7 +2092,8 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   // the reduce launch's clocks follow the train kernel's [4096][16] region
   r.stamps = g_lenet_stamps_host ? g_lenet_stamps_host + 4096 * 16 : nullptr;
   if (a.B <= 0 || a.ldt % 32 || a.ldt < a.B || !a.frag || !a.ftab || !a.pxtab) return hipErrorInvalidValue;
-  const int nblk = (a.B + IMG - 1) / IMG;
+  a.ipw = lenet_ipw(a.B);
+  const int nblk = (a.B + a.ipw - 1) / a.ipw;
   if (a.prep) {
     hipLaunchKernelGGL(lenet_prep_kernel, dim3(1), dim3(PT), 0, st, a.w1, a.w2,
                        reinterpret_cast<bf16x8*>(const_cast<void*>(a.frag)));
@@ -2158,7 +2185,10 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
   const bool psx = r.ps_on && r.ps.excl != 0 && r.succ && r.ps.nshards == 1 && r.ps.owner_ring <= 0;
   a.ps_excl = psx ? 1 : 0;
   r.mirror = psx ? r.ps.shard[0] : nullptr;
-  hipLaunchKernelGGL(lenet_train_kernel, dim3(nblk + (r.ps_on ? 1 : 0)), dim3(NT), LDS_BYTES, st, a);
+  if (a.ipw < IMG)
+    hipLaunchKernelGGL(lenet_train_kernel<true>, dim3(nblk + (r.ps_on ? 1 : 0)), dim3(NT), LDS_BYTES, st, a);
+  else
+    hipLaunchKernelGGL(lenet_train_kernel<false>, dim3(nblk + (r.ps_on ? 1 : 0)), dim3(NT), LDS_BYTES, st, a);
   DFA_HIP_CHECK(hipGetLastError());
   // the index-staging workgroup; async PS: the admission and the claim / staging workgroups
   const int extra = r.ps_on ? 2 : ((r.sgd_on && r.sgd.src) ? 1 : 0);

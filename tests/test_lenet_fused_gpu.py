@@ -43,10 +43,16 @@ def _check(gnet, ref_grads, ref_stats, stats, tol_rel=0.03, min_cos=0.999):
     assert abs(float(stats[1]) - float(ref_stats[1])) <= 2
 
 
-@pytest.mark.parametrize("B", [128, 100, 160, 96, 4096])
+@pytest.mark.parametrize("B", [128, 100, 160, 96, 4096, 32, 33, 500, 1000, 2049])
 def test_fused_lenet_matches_cpu_reference(B):
     """(B = 4096: the benchmarked configuration -- 512 train workgroups, 8 split-K chunks of 512 rows in the
-    reduce launch; VERDICT r4 Missing 4)"""
+    reduce launch; VERDICT r4 Missing 4.  Small batches run fewer images per workgroup with the per-image
+    loops trimmed to them (csrc/lenet_fused.hip lenet_ipw): B <= 256 one image, 500 two, 1000 four, 2049
+    eight with a one-image last workgroup)"""
+    from distriflow_amd import ops
+
+    ipw = {32: 1, 33: 1, 96: 1, 100: 1, 128: 1, 160: 1, 500: 2, 1000: 4, 2049: 8, 4096: 8}[B]
+    assert ops.lenet_blocks(B) == -(-B // ipw)
     g, c = _nets(B)
     x, y = _batch(B)
     sg = g.compute_gradients(x.cuda(), y.cuda()).clone()
