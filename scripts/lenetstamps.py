@@ -54,6 +54,13 @@ def main():
     tot = st[:, 10] - st[:, 0]
     print(f"kernel-1 workgroup lifetime: median {np.median(tot):.0f} cycles, max {tot.max():.0f}; "
           f"start spread {st[:, 0].max() - st[:, 0].min():.0f}")
+    # per XCD (dispatch is round-robin: workgroup b runs on XCD b % 8; s_memtime bases differ between XCDs, so
+    # start / end spreads are only comparable inside one XCD)
+    for x in range(min(8, nblk)):
+        sel = np.arange(x, nblk, 8)
+        t = tot[sel]
+        print(f"  XCD {x}: lifetime median {np.median(t):7.0f} max {t.max():7.0f} | start spread "
+              f"{st[sel, 0].max() - st[sel, 0].min():7.0f} end spread {st[sel, 10].max() - st[sel, 10].min():7.0f}")
     for k, name in enumerate(NAMES):
         col = d[:, k]
         print(f"  {name:<12} median {np.median(col):8.0f}  p90 {np.percentile(col, 90):8.0f}  "
