@@ -587,6 +587,9 @@ struct LeNetRedArgs {
   // async PS with one rank (mode 3: the synchronous owners' update gated on the train launch's admission):
   // every new weight is also written here (the rank's master shard); null otherwise
   float* mirror;
+  // small batches, one rank, sync (set by lenet_train): one workgroup per slot reduces it over the whole
+  // batch and applies its update itself (no 8-way split, no hand-off)
+  int solo;
 };
 // The reference CNN's conv block (csrc/kcnn_fused.hip): conv1 3x3x1->32 + ReLU, conv2 3x3x32->32 + ReLU,
 // 2x2 max-pool [+ folded dropout], input 28x28x1, in one forward and one backward launch (+ reduce).

@@ -1027,13 +1027,15 @@ __device__ __forceinline__ int conv_wj(Owned o) { return o.di == 0 ? o.i : o.di 
 // Dense job (unit u, chunk c): this workgroup's partial of the unit over the chunk's batch columns.  The
 // chunk's K-steps are split over the 4 waves; each wave computes all four 16 x 16 sub-tiles of its steps
 // (every operand row it loads is used twice); LDS combine.  out[e] = partial of position t + 256 e.
+// (nch = 1: the whole batch, the solo path)
 __device__ __forceinline__ void dense_job(const LeNetRedArgs& a, const RedTables& t, int u, int c, float* red,
-                                          float (&out)[kPerThread]) {
+                                          float (&out)[kPerThread], int nch = kChunks) {
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   int tn, tk;
   const int l = dense_unit(t, u, tn, tk);
   const LeNetDense& L = t.L[l];
-  const int col0 = c * a.chunk_cols, col1 = min(a.kcols, col0 + a.chunk_cols);
+  const int cw = nch == 1 ? a.kcols : a.chunk_cols;
+  const int col0 = c * cw, col1 = min(a.kcols, col0 + cw);
   const bf16* arow[2];
   const bf16* brow[2];
   bool a_ok[2], b_ok[2], b_one[2];
@@ -1100,11 +1102,12 @@ __device__ __forceinline__ void dense_job(const LeNetRedArgs& a, const RedTables
 
 // Conv job (slot s, chunk c): parameters 256 s .. 256 s + 255 over the train workgroups' partial rows
 // q = c, c + 8, ...: one row (1 KB) per wave-load, the rows split over the 4 waves, LDS combine.
-__device__ __forceinline__ void conv_job(const LeNetRedArgs& a, int s, int c, float* red, float (&out)[kPerThread]) {
+__device__ __forceinline__ void conv_job(const LeNetRedArgs& a, int s, int c, float* red, float (&out)[kPerThread],
+                                         int nch = kChunks) {
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int p0 = s * kConvPer + 4 * lane;
   const int pl = min(p0, kLeNetConvStride - 4);  // lanes past the last parameter read the row's padding
-  const int nrows = a.nblk > c ? (a.nblk - 1 - c) / kChunks + 1 : 0;
+  const int nrows = a.nblk > c ? (a.nblk - 1 - c) / nch + 1 : 0;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int i0 = wid; i0 < nrows; i0 += 4 * 16) {
     // every load of the round unconditional (rows clamped, the padding ones dropped below): a per-row
@@ -1113,7 +1116,7 @@ __device__ __forceinline__ void conv_job(const LeNetRedArgs& a, int s, int c, fl
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int i = min(i0 + 4 * k, nrows - 1);
-      v[k] = *reinterpret_cast<const f32x4*>(a.conv_part + (long long)(c + kChunks * i) * kLeNetConvStride + pl);
+      v[k] = *reinterpret_cast<const f32x4*>(a.conv_part + (long long)(c + nch * i) * kLeNetConvStride + pl);
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k)
@@ -1401,6 +1404,39 @@ __global__ void __launch_bounds__(RT, 4) lenet_reduce_kernel(LeNetRedArgs a) {
     stage_tables(a, &tabs);
     // with the fused sync update, the first owned slot's master / momentum elements are loaded beside
     // its slab loads
+    if (MODE == 0 && a.solo) {
+      // small batches: workgroup g reduces slot g over the whole batch (one job over every partial row /
+      // batch column) and applies the update of its positions itself -- no 8-way split, no granule hand-off
+      // (at B = 32 the hand-off between XCDs was ~2.5 us of a ~6 us launch)
+      const int slot = blockIdx.x;
+      const bool dense = slot_dense(a, slot) >= 0;
+      __syncthreads();  // the tables staged above
+      Owned o[kPerThread];
+      float w0[kPerThread], m0[kPerThread], v[kPerThread];
+#pragma unroll
+      for (int e = 0; e < kPerThread; ++e) {  // the old master / momentum load beside the job's operands
+        o[e] = (dense || e == 0) ? owned_elem(a, tabs, slot, (int)threadIdx.x + RT * e) : Owned{-1, 0};
+        w0[e] = m0[e] = 0.f;
+        if (a.sgd_on && o[e].di >= 0) {
+          const long long off = tabs.d[o[e].di].off + o[e].i;
+          w0[e] = a.sgd.master[off];
+          m0[e] = a.sgd.mom != nullptr ? a.sgd.mom[off] : 0.f;
+        }
+      }
+      if (dense) dense_job(a, tabs, slot_dense(a, slot), 0, red, v, 1);
+      else conv_job(a, slot_conv(a, slot), 0, red, v, 1);
+      LR_STAMP(6);
+      if (dense) {
+#pragma unroll
+        for (int e = 0; e < kPerThread; ++e) red_apply<true>(a, tabs, o[e], v[e], w0[e], m0[e]);
+      } else {
+        red_apply<false>(a, tabs, o[0], v[0], w0[0], m0[0]);
+      }
+      LR_STAMP(3);
+      LR_STAMP(4);
+      LR_FLUSH();
+      return;
+    }
     const bool pre = a.sgd_on && !PS;
     __shared__ float w_pre[kPerThread][RT], m_pre[kPerThread][RT];  // (LDS: not live across the jobs in VGPRs)
     __shared__ float own0[kPerThread][RT];  // the first owned slot's local sums
@@ -2148,6 +2184,14 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
     r.succ = 0;
   if (r.succ) r.exch_blocks = njobs + kChunks;  // + the owner-only group of the last slot
   else if (r.exch_blocks <= 0 || r.exch_blocks > njobs) r.exch_blocks = njobs;
+  // one rank, sync, small batch: one workgroup per slot (the whole-batch job: <= 64 partial rows and <= 512
+  // batch columns keep it to one load round per wave).  DISTRIFLOW_DIAG=lenet_solo=0|1 forces it off / on.
+  {
+    static const int solo_diag = diag_int("lenet_solo", -1);
+    const bool eligible = !r.ll_on && !r.ps_on;
+    r.solo = eligible && (solo_diag == 1 || (solo_diag != 0 && nblk <= 64 && r.kcols <= 512)) ? 1 : 0;
+    if (r.solo) r.exch_blocks = nslot;
+  }
   // a workgroup runs <= ceil(njobs / G) jobs, so it owns at most that many slots
   if ((long long)r.exch_blocks * kMaxOwned < njobs) return hipErrorInvalidValue;
   // 256-thread workgroups at <= 128 VGPRs and ~17 KB LDS: 4 per CU, 1024 on the chip
