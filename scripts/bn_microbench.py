@@ -10,7 +10,7 @@ import torch  # noqa: E402
 
 from distriflow_amd import ops  # noqa: E402
 
-SHAPES = [(256 * 32 * 32, 64), (256 * 16 * 16, 128), (256 * 8 * 8, 256), (256 * 4 * 4, 512)]
+SHAPES = [(64, 64), (64, 512), (256 * 32 * 32, 64), (256 * 16 * 16, 128), (256 * 8 * 8, 256), (256 * 4 * 4, 512)]
 
 
 def timed(fn, n=50):
