@@ -2184,11 +2184,14 @@ hipError_t lenet_train(const LeNetArgs& a_in, LeNetRedArgs r, hipStream_t st) {
     r.succ = 0;
   if (r.succ) r.exch_blocks = njobs + kChunks;  // + the owner-only group of the last slot
   else if (r.exch_blocks <= 0 || r.exch_blocks > njobs) r.exch_blocks = njobs;
-  // one rank, sync, small batch: one workgroup per slot (the whole-batch job: <= 64 partial rows and <= 512
-  // batch columns keep it to one load round per wave).  DISTRIFLOW_DIAG=lenet_solo=0|1 forces it off / on.
+  // one rank, sync, fused update, small batch: one workgroup per slot (the whole-batch job: <= 64 partial
+  // rows and <= 512 batch columns keep it to one load round per wave).  Its sums run in another fp32 order
+  // than the 8-way split's (deterministic), so the gradient-only launch -- the multi-rank exchange's
+  // self-test compares the exchange against it bit for bit -- keeps the split path.
+  // DISTRIFLOW_DIAG=lenet_solo=0|1 forces it off / on.
   {
     static const int solo_diag = diag_int("lenet_solo", -1);
-    const bool eligible = !r.ll_on && !r.ps_on;
+    const bool eligible = !r.ll_on && !r.ps_on && r.sgd_on;
     r.solo = eligible && (solo_diag == 1 || (solo_diag != 0 && nblk <= 64 && r.kcols <= 512)) ? 1 : 0;
     if (r.solo) r.exch_blocks = nslot;
   }
