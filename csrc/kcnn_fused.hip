@@ -6,7 +6,7 @@
 // run conv2 as short implicit GEMMs (K = 288) whose per-workgroup prologue/epilogue dominate.  Here a
 // workgroup keeps one image at a time entirely in LDS:
 //
-//   kcnn_fwd  (persistent, 2 images per workgroup at B = 1024)
+//   kcnn_fwd  (persistent, 768 workgroups: 3 per CU at 163 VGPRs, conv1 in two 4-channel passes)
 //     x0 (uint8 dataset row through the batch index, or bf16)  -> LDS
 //     conv1 + bias + ReLU on the VALU (72 weights per thread)  -> X1 [676][32] bf16 in LDS (never in HBM)
 //     conv2 on MFMA 16x16x32: one k-step per tap (32 channels), the 18 B fragments (9 taps x 2 channel
@@ -34,7 +34,10 @@
 // same sums in a different fp32 order.  LDS in kcnn_bwd: 1.5 + 42.3 + 36 KB = 80 KB, two workgroups
 // per CU.
 #include "common.h"
+#include "diag.h"
 #include "kernels.h"
+
+#include <algorithm>
 
 namespace dfa {
 
@@ -121,36 +124,42 @@ __device__ __forceinline__ void store_x0(const KcnnArgs& a, const X0Regs& r, bf1
 
 // conv1 + bias + ReLU -> X1 (LDS).  Thread (ps = tid >> 2, g = tid & 3): channels 8g..8g+7 of pixels
 // ps, ps + 64, ...; the FMA chain is the per-layer kernel's (smallc.hip c1_fwd_kernel), so X1 is equal
-// bit for bit.
+// bit for bit.  CPP: channels per pass (8, or 4 in two passes: half the weight registers -- 36 instead of
+// 72 -- for one more read of the 9 input pixels; the chains are the same)
+template <int CPP = 8>
 __device__ __forceinline__ void conv1_to_lds(const KcnnArgs& a, const bf16* x0, bf16* x1) {
   const int g = threadIdx.x & 3, ps = threadIdx.x >> 2;
-  float w[8][9], bias[8];
+#pragma unroll 1
+  for (int c0 = 8 * g; c0 < 8 * g + 8; c0 += CPP) {
+    float w[CPP][9], bias[CPP];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < CPP; ++j) {
 #pragma unroll
-    for (int k = 0; k < 9; ++k) w[j][k] = (float)a.w1[(8 * g + j) * a.kpad1 + k];
-    bias[j] = a.b1[8 * g + j];
-  }
-  for (int p = ps; p < NP1; p += 64) {
-    const int oy = p / H1, ox = p - oy * H1;
-    float xv[9];
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) xv[3 * ky + kx] = (float)x0[(oy + ky) * H0 + ox + kx];
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float acc = 0.f;
-#pragma unroll
-      for (int k = 0; k < 9; ++k) acc = fmaf(xv[k], w[j][k], acc);
-      o[j] = f2bf(fmaxf(acc * 1.f + bias[j], 0.f));
+      for (int k = 0; k < 9; ++k) w[j][k] = (float)a.w1[(c0 + j) * a.kpad1 + k];
+      bias[j] = a.b1[c0 + j];
     }
-    *reinterpret_cast<bf16x8*>(x1 + xsr(p, oy, 8 * g)) = o;
+    for (int p = ps; p < NP1; p += 64) {
+      const int oy = p / H1, ox = p - oy * H1;
+      float xv[9];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) xv[3 * ky + kx] = (float)x0[(oy + ky) * H0 + ox + kx];
+      typedef bf16 bfv __attribute__((ext_vector_type(CPP)));
+      bfv o;
+#pragma unroll
+      for (int j = 0; j < CPP; ++j) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) acc = fmaf(xv[k], w[j][k], acc);
+        o[j] = f2bf(fmaxf(acc * 1.f + bias[j], 0.f));
+      }
+      *reinterpret_cast<bfv*>(x1 + xsr(p, oy, c0)) = o;
+    }
   }
 }
 
-__global__ void __launch_bounds__(KT, 2) kcnn_fwd_kernel(KcnnArgs a) {
+__global__ void __launch_bounds__(KT, 3) kcnn_fwd_kernel(KcnnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 x0[NP0];
   __shared__ __attribute__((aligned(16))) bf16 x1[NP1 * C];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
@@ -169,7 +178,7 @@ __global__ void __launch_bounds__(KT, 2) kcnn_fwd_kernel(KcnnArgs a) {
     store_x0(a, xr, x0);
     xr = load_x0(a, b + gridDim.x);  // next image: in flight during this one
     __syncthreads();
-    conv1_to_lds(a, x0, x1);
+    conv1_to_lds<4>(a, x0, x1);
     __syncthreads();
     for (int t = wid; t < NPP / 4; t += 4) {
       const int q0 = 4 * t, ph = q0 / PW, pw0 = q0 - ph * PW;
@@ -445,7 +454,10 @@ size_t kcnn_slab_floats(int B) { return (size_t)kcnn_blocks(B) * C * (S2 + S1); 
 hipError_t kcnn_fwd(const KcnnArgs& a, hipStream_t st) {
   if (a.B <= 0 || (!a.x_u8 && !a.x_bf) || !a.w1 || !a.b1 || !a.w2 || !a.b2 || !a.pooled || !a.code || a.kpad1 < 9)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(kcnn_fwd_kernel, dim3(kcnn_blocks(a.B)), dim3(KT), 0, st, a);
+  // 3 workgroups per CU fit (163 VGPRs, 44 KB of LDS): the forward is not reduced through per-workgroup slabs,
+  // so its grid is free; DISTRIFLOW_DIAG=kcnn_fwd_wg=<n> sets it (default 768)
+  static const int fwd_wg = diag_int("kcnn_fwd_wg", 768);
+  hipLaunchKernelGGL(kcnn_fwd_kernel, dim3(std::min(a.B, std::max(1, fwd_wg))), dim3(KT), 0, st, a);
   return hipGetLastError();
 }
 
