@@ -559,9 +559,11 @@ __global__ void __launch_bounds__(KT) khead_train_kernel(KHeadArgs a) {
 // dW[n][k] = sum_b dZ^T[n][b] X^T[k][b] (k < K), db[n] = the k == K column (X^T row of ones).  One
 // workgroup per 64 x 32 output tile over the WHOLE batch (deterministic, no slabs): the 4 waves split
 // the batch, each keeps 8 tiles' accumulators and issues its 8 batch steps' operand loads at once, then a
-// fixed-order LDS combine.  Tiles sharing a 32-row X^T panel are adjacent on one XCD (xcd_remap).
+// fixed-order LDS combine.  Tiles sharing a 32-row X^T panel are adjacent on one XCD (xcd_remap).  Capped at
+// 256 VGPRs (2 workgroups per CU): the reference CNN's 295 tiles then run in one round, not two (16.7 ->
+// 14.6 us, profiles/r6/kernel_table_kc_after.txt).
 constexpr int WGN = 64, WGK = 32, WGS = 8;
-__global__ void __launch_bounds__(KT) khead_wgrad_kernel(KHeadWgradArgs a) {
+__global__ void __launch_bounds__(KT, 2) khead_wgrad_kernel(KHeadWgradArgs a) {
   __shared__ f32x4 red[4][8][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, tid = threadIdx.x;
   if ((int)blockIdx.x == a.jobs) {  // loss partials -> stats (fixed-order tree)
