@@ -143,3 +143,25 @@ def test_keras_round_trip_keeps_geometry():
 def test_native_geometry_encoding():
     assert ops._geom(8, 8, 3, 4, 4, 3, 3, 2, 1) == [8, 8, 3, 4, 4, 3, 3, 2, 1]
     assert ops._geom(9, 8, 3, 5, 8, 3, 5, (2, 1), (1, 2)) == [9, 8, 3, 5, 8, 3, 5, 2, 1, 1, 2]
+
+
+def test_tfjs_checkpoint_round_trip_keeps_non_square_kernels(tmp_path):
+    """A (3, 5) / stride (2, 1) Conv2D saves as Keras HWIO [3][5][C][N] and reloads into a fresh model that
+    computes the same function (rebuilt from the saved model.json's topology)."""
+    import json as _json
+
+    from distriflow_amd.checkpoint import load_layers_model_weights, save_layers_model
+
+    topo = _topo(9, 8, 3, (3, 5), (2, 1), "same")
+    layers, shape = layers_from_keras(topo)
+    a = Net(layers, shape, device="cpu", seed=1)
+    save_layers_model(a, str(tmp_path / "m"))
+    doc = _json.load(open(tmp_path / "m" / "model.json"))
+    shapes = {w["name"]: w["shape"] for w in doc["weightsManifest"][0]["weights"]}
+    assert shapes["c1/kernel"] == [3, 5, 3, 6] and shapes["c2/kernel"] == [1, 3, 6, 8]
+    layers_b, shape_b = layers_from_keras(doc["modelTopology"])
+    b = Net(layers_b, shape_b, device="cpu", seed=2)
+    load_layers_model_weights(b, str(tmp_path / "m" / "model.json"))
+    assert torch.equal(a.store.master, b.store.master)
+    x = torch.rand(3, 9, 8, 3)
+    torch.testing.assert_close(a.predict(x), b.predict(x))
