@@ -2475,6 +2475,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("h1T"), py::arg("dz1T"), py::arg("dz2T"), py::arg("logits"), py::arg("labels"), py::arg("idx"),
         py::arg("grad_scale"), py::arg("loss_part"), py::arg("ws"));
   m.def("khead_wgrad", &khead_wgrad_py, "reference CNN dense head: weight gradients + loss stats (1 launch)");
+  m.def("khead_set_grid_cap", [](int64_t cus) { dfa::khead_set_grid_cap((int)cus); },
+        "persistent dense-head grid cap (CUs) for ranks time-sharing one GPU; 0 = the whole chip");
   m.def("khead_set_stamps", [](c10::optional<torch::Tensor> buf) {
     dfa::khead_set_stamps(buf.has_value() && buf->defined() ? buf->data_ptr() : nullptr);
   }, "profiling aid: per-workgroup phase clocks of the khead launch into buf ([G][16] int64), None = off");

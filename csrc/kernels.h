@@ -648,6 +648,7 @@ struct KHeadArgs {
   int B, K, C, ldt, ldw1, ntiles, G;
 };
 void khead_set_stamps(void* buf);
+void khead_set_grid_cap(int cus);
 // Weight gradients of that head (csrc/khead.hip khead_wgrad_kernel): dW = dZ^T X over the whole batch
 // in 64 x 32 output tiles (bias = the column k == K of ones), plus the loss partials -> stats.
 struct KHeadWgradLayer {

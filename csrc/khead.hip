@@ -27,6 +27,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <algorithm>
+
 namespace dfa {
 namespace {
 
@@ -254,6 +256,11 @@ __device__ __forceinline__ void khead_owner(const KHeadArgs& a, const KHeadLds& 
 }  // namespace
 
 void khead_set_stamps(void* buf) { g_khead_stamps = reinterpret_cast<unsigned long long*>(buf); }
+// ranks time-sharing one GPU (rehearsals): each rank's persistent grid gets its share of the CUs, so the 8
+// jobs of a row tile can be resident together beside the other ranks' kernels (0: the whole chip)
+static int g_khead_cap = 0;
+constexpr unsigned long long kKHeadWaitTicks = 200000000ull;  // 2 s of wall_clock64 (100 MHz)
+void khead_set_grid_cap(int cus) { g_khead_cap = cus > 0 ? cus : 0; }
 
 // KSC: k-steps per chunk at compile time (0: run-time loops).  (Issuing the W1 / W1^T operand loads a
 // phase earlier -- behind the P loads, before the flag wait -- measured slower: the ~144 VGPRs they hold
@@ -435,9 +442,20 @@ __global__ void __launch_bounds__(KT) khead_train_kernel(KHeadArgs a) {
     } else {
       load_first();
       write_pT();
-      if (tid == 0)
-        while (__hip_atomic_load(flags + rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag)
+      if (tid == 0) {
+        // bounded: the owner runs concurrently by construction (persistent grid <= resident capacity), but a
+        // wait that never ends -- e.g. ranks time-sharing a GPU whose other kernels hold the CUs -- must not
+        // hang the device: past 2 s the tile is left (its results invalid) and the sticky error word, the
+        // workspace's word after the tag, is set (ops.khead_error reads it)
+        const unsigned long long t0 = wall_clock64();
+        while (__hip_atomic_load(flags + rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag) {
+          if (wall_clock64() - t0 > kKHeadWaitTicks) {
+            atomicOr(tagp + 1, 1u);
+            break;
+          }
           __builtin_amdgcn_s_sleep(2);
+        }
+      }
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -708,7 +726,7 @@ hipError_t khead_train(KHeadArgs a, hipStream_t st) {
   if (a.ldt < a.ntiles * KR) return hipErrorInvalidValue;
   // persistent grid: every workgroup resident (one per CU at most), a multiple of 8 so the 8 jobs of a row
   // tile are always in flight together
-  const int cap = khead_cus() / KCH * KCH;
+  const int cap = (g_khead_cap > 0 ? std::min(khead_cus(), g_khead_cap) : khead_cus()) / KCH * KCH;
   a.G = min(a.ntiles * KCH, cap);
   if (a.G < KCH) return hipErrorInvalidValue;
   a.stamps = g_khead_stamps;

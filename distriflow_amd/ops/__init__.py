@@ -809,6 +809,14 @@ def khead_ws_floats(B: int, K: int) -> int:
     return int(_C().khead_ws_floats(int(B), int(K)))
 
 
+def khead_error(ws: torch.Tensor, B: int) -> int:
+    """The dense-head launch's sticky error word (csrc/khead.hip): non-zero after a row tile's flag wait timed
+    out (its results invalid).  ``ws``: the launch's workspace (ops.khead_ws_floats floats)."""
+    nt = -(-int(B) // 32)
+    off = nt * 8 * 32 * 128 + nt * 32 * 128 // 2 + 2 * nt + 1
+    return int(ws[off:off + 1].view(torch.int32).item())
+
+
 def khead_train(p, pT, dp, w1, w1t, b1, w2, w2t, b2, h1T, dz1T, dz2T, logits, labels, idx, grad_scale, loss_part, ws,
                 drop=None, dh_scale=1.0, dp_scale=1.0, dp_mask=False):
     """The reference CNN's dense head on GPU (csrc/khead.hip): dense1 (K -> 128, ReLU, folded ``drop``),

@@ -26,7 +26,7 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
-from .. import ops
+from .. import native, ops
 from ..diagnostics import on as _diag_on
 
 
@@ -152,6 +152,8 @@ class DataParallelTrainer:
             # workgroups (each owning several slots) so that every rank's waiting workgroups fit on the chip
             # beside the peers' train kernels; with one rank per GPU every slot gets its own workgroup
             self.net.lenet_exch_blocks = shared_gpu_exch_blocks(self.world)
+            # likewise the reference CNN's persistent dense-head grid (csrc/khead.hip): its share of the CUs
+            native.require().khead_set_grid_cap(shared_gpu_cus(self.world))
 
     def _reduce(self, t: torch.Tensor, async_op: bool):
         if self.p2p is not None and t.numel() * 4 <= self.p2p_limit:
@@ -795,6 +797,17 @@ def _beat(step: int):
     from .watchdog import beat
 
     beat(step)
+
+
+def shared_gpu_cus(world: int) -> int:
+    """CUs of one rank's persistent kernels when ranks time-share a GPU (rehearsals), else 0 (no cap)."""
+    ndev = max(1, torch.cuda.device_count())
+    share = -(-world // ndev) if ndev < world else 1
+    if share == 1:
+        return 0
+    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    # three quarters of the chip split between the ranks: the rest stays free for their other kernels
+    return max(8, cus * 3 // 4 // share // 8 * 8)
 
 
 def shared_gpu_exch_blocks(world: int) -> int:

@@ -73,6 +73,10 @@ def test_khead_repeatable_across_launches(monkeypatch):
         assert torch.equal(s, outs[0][0])
         assert torch.equal(g, outs[0][1])
         assert torch.equal(dx, outs[0][2])
+    # no row tile's flag wait timed out (the bounded wait's sticky error word)
+    from distriflow_amd import ops
+
+    assert ops.khead_error(f.khead_ws, 333) == 0
 
 
 def test_khead_training_in_graph(monkeypatch):
