@@ -191,9 +191,13 @@ class DataParallelTrainer:
         self._works = []
 
     def check_comm(self):
-        """Raise if the one-shot all-reduce recorded a peer timeout (call outside the timed loop)."""
+        """Raise if the one-shot all-reduce recorded a peer timeout, or the reference CNN's dense head a row
+        tile's flag-wait timeout (csrc/khead.hip; call outside the timed loop)."""
         if self.p2p is not None:
             self.p2p.check()
+        ws = getattr(self.net, "khead_ws", None)
+        if ws is not None and self.net._bound_B and ops.khead_error(ws, self.net._bound_B) != 0:
+            raise RuntimeError("dense head: a row tile's flag wait timed out (its step's results are invalid)")
 
     @property
     def allreduce_path(self) -> str:
