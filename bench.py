@@ -167,6 +167,11 @@ def main():
                     help="sync = all-reduce data parallel (headline); async = device-resident bounded-staleness "
                          "parameter server on rank 0 (parallel/async_ps.py)")
     ap.add_argument("--max-staleness", type=int, default=4)
+    ap.add_argument("--settle-ms", type=float, default=40.0,
+                    help="before the W warm-up steps, run untimed training steps (whole K-step replays) for about this "
+                         "long: the GPU's clocks ramp up over the first ~15 ms of continuous load after idle "
+                         "(profiles/r6/lenet_clock_ramp_r6.txt), so without it a short timed run measures the ramp; "
+                         "0 disables; reported as \"settle\" in the JSON")
     ap.add_argument("--async-steps", type=int, default=None,
                     help="after the sync measurement, also time this many steps of the async parameter-server "
                          "engine and report the async speedup (default: --steps; 0 disables)")
@@ -211,7 +216,8 @@ def main():
         data, labels = synthetic_cifar10(50000, seed=0, device=dev)
     else:
         data, labels = synthetic_mnist(60000, seed=0, device=dev)
-    total = args.warmup + args.steps
+    SETTLE_MAX_STEPS = 1024  # cap of the settle phase's steps (the datasets below are sized for it)
+    total = args.warmup + args.steps + (SETTLE_MAX_STEPS if args.settle_ms > 0 else 0)
 
     def make_trainer(mode, net):
         if mode == "async":
@@ -231,9 +237,43 @@ def main():
             tr.bind_distri_dataset(ds, rank=rank, world=world, scale=1.0 / 255.0)
         return tr
 
+    settle_recs = []
+
+    def settle(tr, steps, multi):
+        """Untimed training steps (replays of the timed run's own multi-step graph) until about
+        ``--settle-ms`` of continuous device work: the clock ramp after idle is ~15 ms long
+        (``scripts/launch_overhead_probe.py --ramp``: LeNet-5 B = 4096 62.4 -> 57.1 us per step), so a
+        short timed run would measure the power manager's ramp, not the step.  Every rank runs the same
+        number of chunks (rank 0 decides after each one): the steps are complete training steps, with the
+        same collectives on every rank."""
+        if args.settle_ms <= 0 or dev.type != "cuda":
+            return
+        u = getattr(tr, "_multi_u", 0) if multi else 0
+        chunk = u if u > 1 else max(1, min(steps, 16))  # one multi-step replay, or up to 16 single steps
+        n, chunks = 0, 0
+        t0 = time.perf_counter()
+        while True:
+            if u > 1:
+                tr.run(chunk)
+            else:
+                for _ in range(chunk):
+                    tr.step()
+            n += chunk
+            chunks += 1
+            sync()
+            go = (time.perf_counter() - t0) * 1e3 < args.settle_ms and n + chunk <= SETTLE_MAX_STEPS
+            if world > 1:
+                f = torch.tensor([1 if go else 0], dtype=torch.int32, device=dev)
+                dist.broadcast(f, src=0)
+                go = bool(f.item())
+            if not go:
+                break
+        settle_recs.append({"steps": n, "replays": chunks, "ms": round((time.perf_counter() - t0) * 1e3, 1)})
+
     def timed(tr, steps):
-        """W untimed warm-up steps, then ``steps`` timed ones between barrier + device syncs; max over ranks.
-        The sync trainer replays its steps from multi-step hipGraphs (captured here, before timing)."""
+        """Settle (see :func:`settle`), W untimed warm-up steps, then ``steps`` timed ones between barrier +
+        device syncs; max over ranks.  The sync trainer replays its steps from multi-step hipGraphs (captured
+        here, before timing)."""
         multi = getattr(tr, "SUPPORTS_MULTISTEP", False) and diag_on("multistep")
         # ranks time-sharing one device (rehearsals) must yield the GPU at graph boundaries: a long unrolled
         # graph whose one-shot all-reduce spins on a descheduled peer's flag runs at the hardware
@@ -242,6 +282,8 @@ def main():
             multi = False
         if multi:
             tr.prepare_run(steps)
+        settle(tr, steps, multi)
+        if multi:
             tr.run(args.warmup)
         else:
             for _ in range(args.warmup):
@@ -292,9 +334,8 @@ def main():
             atr = make_trainer("async", anet)
             ael, _ = timed(atr, async_steps)
             aval = world * B * async_steps / ael
-            # the sync trainer timed again right after, the same way: the GPU's clocks ramp up over the first
-            # ~15 ms of load (profiles/r5/lenet_clock_ramp.txt), so the sync run before the async one is colder
-            # and the one after it warmer; the ratio is against their mean step time (the async run sits
+            # the sync trainer timed again right after, the same way (each run settles first, but the box's
+            # clocks still drift between runs); the ratio is against their mean step time (the async run sits
             # between them)
             sel2, _ = timed(trainer, async_steps)
             sync_ms = 0.5 * (elapsed / args.steps + sel2 / async_steps) * 1e3
@@ -317,6 +358,9 @@ def main():
             "backend": live_backend,
             "steps": args.steps,
             "warmup": args.warmup,
+            # untimed steps before the warm-up of each timed run (the clock ramp, see settle()); the timed
+            # region is exactly ``steps`` steps either way
+            "settle": {"target_ms": args.settle_ms, "runs": settle_recs} if settle_recs else None,
             "ms_per_step": round(ms, 4),
             "final_loss": round(loss, 6),
             "check": check,
