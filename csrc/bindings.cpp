@@ -2477,6 +2477,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("khead_wgrad", &khead_wgrad_py, "reference CNN dense head: weight gradients + loss stats (1 launch)");
   m.def("khead_set_grid_cap", [](int64_t cus) { dfa::khead_set_grid_cap((int)cus); },
         "persistent dense-head grid cap (CUs) for ranks time-sharing one GPU; 0 = the whole chip");
+  m.def("kcnn_set_stamps", [](c10::optional<torch::Tensor> buf) {
+    dfa::kcnn_set_stamps(buf.has_value() && buf->defined() ? buf->data_ptr() : nullptr);
+  }, "profiling aid: per-image phase clocks of the reference CNN's fused backward ([G][2][16] int64)");
   m.def("khead_set_stamps", [](c10::optional<torch::Tensor> buf) {
     dfa::khead_set_stamps(buf.has_value() && buf->defined() ? buf->data_ptr() : nullptr);
   }, "profiling aid: per-workgroup phase clocks of the khead launch into buf ([G][16] int64), None = off");

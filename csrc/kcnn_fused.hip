@@ -218,6 +218,21 @@ __global__ void __launch_bounds__(KT, 3) kcnn_fwd_kernel(KcnnArgs a) {
   }
 }
 
+unsigned long long* g_kcnn_stamps = nullptr;
+
+// per-phase clocks of the first two images of every workgroup (diagnostic; scripts/kcnnstamps.py)
+#define KC_STAMP(slot)                                                               \
+  do {                                                                               \
+    if (a.stamps) {                                                                  \
+      __builtin_amdgcn_sched_barrier(0);                                             \
+      unsigned long long t_;                                                         \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");   \
+      __builtin_amdgcn_sched_barrier(0);                                             \
+      const int im_ = (b - (int)blockIdx.x) / (int)gridDim.x;                        \
+      if (threadIdx.x == 0 && im_ < 2) a.stamps[(blockIdx.x * 2 + im_) * 16 + (slot)] = t_; \
+    }                                                                                \
+  } while (0)
+
 __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 x0[NP0];
   __shared__ __attribute__((aligned(16))) bf16 x1[NP1 * C];
@@ -225,11 +240,14 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 zc[8];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, G = lane >> 4, i = lane & 15;
   if (tid < 8) zc[tid] = (bf16)0.f;
-  // conv2 weight gradient: this wave's output channel half hn and input channel half hc, all 9 taps
+  // conv2 weight gradient: this wave's output channel half hn and input channel half hc, all 9 taps.  Its
+  // accumulators live in registers only from the conv1 recompute of an image to the end of that image's
+  // weight-gradient phase: stored into the workgroup's slab after it and reloaded (issued before the next
+  // image's conv1 recompute) -- the same fp32 sums in the same order, and 36 registers free in the data
+  // gradient phase, which holds its 72-register B operand (with them live there the dY2 reads of a tile
+  // were serialised, one LDS round trip per tap)
   const int hn = wid & 1, hc = wid >> 1;
-  f32x4 acc2[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) acc2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float* s2 = a.slab2 + (long long)blockIdx.x * C * S2;
   float db2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) db2[j] = 0.f;
@@ -239,6 +257,7 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
   X0Regs xr = load_x0(a, blockIdx.x);
   for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
     // ---- stage x0; expand dY2 from the pooled gradient and the codes (conv2 bias gradient on the way)
+    KC_STAMP(0);
     store_x0(a, xr, x0);
     xr = load_x0(a, b + gridDim.x);
     for (int e = tid; e < NPP * 4; e += KT) {
@@ -260,9 +279,23 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
         *reinterpret_cast<bf16x8*>(dy2 + xsr(py * H2 + 2 * pw + (p & 1), py, 8 * c8)) = ov;
       }
     }
+    KC_STAMP(1);
     __syncthreads();
+    KC_STAMP(2);
+    f32x4 acc2[9];
+    if (b == (int)blockIdx.x) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc2[t][r] = s2[(16 * hn + 4 * G + r) * S2 + t * C + 16 * hc + i];
+    }
     conv1_to_lds(a, x0, x1);
+    KC_STAMP(3);
     __syncthreads();
+    KC_STAMP(4);
 
     // ---- conv2 weight gradient: D[n][(tap, ci)] += dY2^T[n][p] X1[p + tap][ci] over 18 blocks of 32 output
     // pixels, block = 4 rows x 8 columns: k slot 8G + 4hf + r is pixel (oy0 + G, ox0 + 4hf + r), so the
@@ -291,6 +324,7 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
         }
       }
     }
+    KC_STAMP(5);
 
     // ---- conv2 data gradient x relu'(X1) over 4x4 pixel tiles of X1 (7 x 7 tiles cover 26 x 26), and the
     // conv1 weight gradient on MFMA from pairs of tiles: D1[ci][tap1] += g[ci][pixel] x0[pixel + tap1]
@@ -303,10 +337,21 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
       for (int t = 0; t < 9; ++t)
 #pragma unroll
         for (int h = 0; h < 2; ++h) bt[t][h] = ld8(a.w2t + (16 * h + i) * K2 + t * C + 8 * G);
-      const int ty1 = i / 3, tx1 = i - 3 * (i / 3);  // this lane's conv1 tap (column of the conv1 B operand)
+      // (after the B loads: vmcnt counts stores too, and the first MFMA waits for the B operand)
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s2[(16 * hn + 4 * G + r) * S2 + t * C + 16 * hc + i] = acc2[t][r];
+      KC_STAMP(6);
+      // this lane's conv1 tap (column of the conv1 B operand; lanes i >= 9 read tap 0 and drop it)
+      const int ty1 = i < 9 ? i / 3 : 0, tx1 = i < 9 ? i - 3 * (i / 3) : 0;
 #pragma unroll 1
       for (int T0 = wid; T0 < 49; T0 += 8) {
-        bf16 gv[2][2][4];  // [tile of the pair][h][r]
+        bf16x8 ag[2];  // conv1 A operand per channel half h: element 4u + r = the gradient of tile u, column r
+        // the relu' mask and conv1 B operand reads are unconditional, at clamped (valid) addresses, and selected
+        // afterwards: with the reads under their validity conditions (a short-circuit &&) the compiler built one
+        // exec-mask branch per read, each waiting for its read -- 24 serialised LDS round trips per pair, half
+        // of the kernel's time (scripts/kcnnstamps.py)
         int py[2], px0[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -315,58 +360,63 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
           const int iy = 4 * ty + (i >> 2), ix = 4 * tx + (i & 3);
           f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
           if (T < 49) {
+            // the tile's nine dY2 reads first, then the MFMAs (read, wait, MFMA per tap serialised the reads)
+            bf16x8 af[9];
 #pragma unroll
             for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
               for (int kx = 0; kx < 3; ++kx) {
                 const int sy = iy - ky, sx = ix - kx;
                 const bool ok = iy < H1 && ix < H1 && (unsigned)sy < (unsigned)H2 && (unsigned)sx < (unsigned)H2;
-                const bf16x8 af = ld8(ok ? dy2 + xsr(sy * H2 + sx, sy, 8 * G) : zc);
-                acc[0] = mfma16x16x32(af, bt[3 * ky + kx][0], acc[0]);
-                acc[1] = mfma16x16x32(af, bt[3 * ky + kx][1], acc[1]);
+                af[3 * ky + kx] = ld8(ok ? dy2 + xsr(sy * H2 + sx, sy, 8 * G) : zc);
               }
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+              acc[0] = mfma16x16x32(af[t], bt[t][0], acc[0]);
+              acc[1] = mfma16x16x32(af[t], bt[t][1], acc[1]);
+            }
           }
-          const int ry = 4 * ty + G;
-          py[u] = ry < H1 ? ry : H1 - 1;
+          const int ry = 4 * ty + G, cy = min(ry, H1 - 1);
+          py[u] = cy;
           px0[u] = 4 * tx;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int rx = 4 * tx + r;
+            const int rx = 4 * tx + r, cx = min(rx, H1 - 1);
             const bool valid = T < 49 && ry < H1 && rx < H1;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-              const bool live = valid && (float)x1[xsr(ry * H1 + rx, ry, 16 * h + i)] > 0.f;
-              gv[u][h][r] = live ? f2bf(acc[h][r]) : (bf16)0.f;
+              const float mv = (float)x1[xsr(cy * H1 + cx, cy, 16 * h + i)];
+              const bool live = valid & (mv > 0.f);
+              ag[h][4 * u + r] = live ? f2bf(acc[h][r]) : (bf16)0.f;
             }
           }
         }
         // conv1 B operand: B[8G + e][tap1 = i] = x0 at (pixel e) + tap1, 1 for the bias column
         bf16x8 bx;
+        {
+          // lanes i >= 9 read tap 0 too and mask it out with bit operations (a select let the compiler sink
+          // the read into an exec-mask branch of the i < 9 lanes)
+          const unsigned short keep = i < 9 ? 0xffffu : 0u, one = i == 9 ? 0x3f80u : 0u;  // bf16 1.0
+          const unsigned short* x0u = reinterpret_cast<const unsigned short*>(x0);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int u = e >> 2;
-          const int cx = min(px0[u] + (e & 3), H1 - 1);
-          bx[e] = i < 9 ? x0[(py[u] + ty1) * H0 + cx + tx1] : (i == 9 ? (bf16)1.f : (bf16)0.f);
+          for (int e = 0; e < 8; ++e) {
+            const int u = e >> 2;
+            const int cx = min(px0[u] + (e & 3), H1 - 1);
+            const unsigned short v = x0u[(py[u] + ty1) * H0 + cx + tx1];
+            bx[e] = __builtin_bit_cast(bf16, (unsigned short)((v & keep) | one));
+          }
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          bf16x8 ag;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) ag[e] = gv[e >> 2][h][e & 3];
-          acc1[h] = mfma16x16x32(ag, bx, acc1[h]);
-        }
+        for (int h = 0; h < 2; ++h) acc1[h] = mfma16x16x32(ag[h], bx, acc1[h]);
       }
     }
+    KC_STAMP(7);
     __syncthreads();  // LDS is rewritten for the next image
+    KC_STAMP(8);
   }
 
-  // ---- per-workgroup slabs
-  float* s2 = a.slab2 + (long long)blockIdx.x * C * S2;
+  // ---- per-workgroup slabs (conv2's weights: stored after every image's weight-gradient phase)
   float* s1 = a.slab1 + (long long)blockIdx.x * C * S1;
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) s2[(16 * hn + 4 * G + r) * S2 + t * C + 16 * hc + i] = acc2[t][r];
   // conv2 bias: threads sharing c8 (lane bits 0-1) -> xor over lane bits 2-5, then the 4 waves
   float* red = reinterpret_cast<float*>(x1);  // LDS reuse (after the final barrier)
 #pragma unroll
@@ -448,6 +498,7 @@ __global__ void __launch_bounds__(1024) kcnn_reduce_kernel(const float* __restri
 
 }  // namespace
 
+void kcnn_set_stamps(void* buf) { g_kcnn_stamps = reinterpret_cast<unsigned long long*>(buf); }
 int kcnn_blocks(int B) { return B < 512 ? B : 512; }
 size_t kcnn_slab_floats(int B) { return (size_t)kcnn_blocks(B) * C * (S2 + S1); }
 
@@ -467,7 +518,9 @@ hipError_t kcnn_bwd(const KcnnArgs& a, float* g_w1, float* g_b1, float* g_w2, fl
       !g_w1 || !g_b1 || !g_w2 || !g_b2)
     return hipErrorInvalidValue;
   const int nb = kcnn_blocks(a.B);
-  hipLaunchKernelGGL(kcnn_bwd_kernel, dim3(nb), dim3(KT), 0, st, a);
+  KcnnArgs ab = a;
+  ab.stamps = g_kcnn_stamps;
+  hipLaunchKernelGGL(kcnn_bwd_kernel, dim3(nb), dim3(KT), 0, st, ab);
   DFA_HIP_CHECK(hipGetLastError());
   const int outs = C * (S2 + S1);
   hipLaunchKernelGGL(kcnn_reduce_kernel, dim3(cdiv(outs, 64)), dim3(1024), 0, st, a.slab2, a.slab1, nb, g_w2, g_b2,

@@ -611,7 +611,9 @@ struct KcnnArgs {
   float* slab1;     // [blocks][32][10]
   int B, kpad1;
   DropSpec drop;
+  unsigned long long* stamps;  // profiling aid (kcnn_set_stamps): backward [G][2 images][16] phase clocks, or null
 };
+void kcnn_set_stamps(void* buf);
 int kcnn_blocks(int B);
 size_t kcnn_slab_floats(int B);
 hipError_t kcnn_fwd(const KcnnArgs& a, hipStream_t st);
