@@ -159,6 +159,72 @@ __device__ __forceinline__ void conv1_to_lds(const KcnnArgs& a, const bf16* x0, 
   }
 }
 
+// conv1 + bias + ReLU -> X1 (LDS) on MFMA: D[channel][pixel] = W1[channel][k] x0col[k][pixel] over 16-pixel
+// tiles, k = the 9 taps (zero-padded to 32), two 16-channel tiles per pixel tile.  A (the weights) stays in
+// registers; lane (G, i) supplies the taps 8G..8G+7 of pixel i as B; its D rows are channels 4G..4G+3 of
+// pixel i, so the epilogue (fp32 bias, ReLU, bf16) ends in one 8-byte store per channel tile.  ~3x fewer
+// instructions than the VALU FMA chains (the phase was VALU-bound); the products are exact in fp32 either
+// way, only the order of the fp32 sum of the 9 taps differs (forward and backward recompute use this same
+// code, so they agree bit for bit).
+__device__ __forceinline__ void conv1_mfma_to_lds(const KcnnArgs& a, const bf16* x0, bf16* x1) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
+  const unsigned short* x0u = reinterpret_cast<const unsigned short*>(x0);
+  bf16x8 wa[2];
+  float bias[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * G + e;
+      wa[h][e] = k < 9 ? a.w1[(16 * h + i) * a.kpad1 + k] : (bf16)0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[h][r] = a.b1[16 * h + 4 * G + r];
+  }
+  // this lane's taps k = 8G + e as x0 offsets (clamped to tap 8 past the ninth; masked below)
+  int toff[8];
+  unsigned short keep[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = min(8 * G + e, 8);
+    toff[e] = (k / 3) * H0 + (k - 3 * (k / 3));
+    keep[e] = 8 * G + e < 9 ? 0xffffu : 0u;
+  }
+  // two pixel tiles per iteration (t, t + 4): all 16 tap reads go out before the first MFMA
+  constexpr int NT = (NP1 + 15) / 16;  // 43
+  for (int t0 = wid; t0 < NT; t0 += 8) {
+    int pp[2], py[2];
+    bf16x8 bx[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = 16 * (t0 + 4 * u) + i, pc = min(p, NP1 - 1);
+      const int oy = pc / H1, ox = pc - oy * H1;
+      pp[u] = p;
+      py[u] = oy;
+      const int base = oy * H0 + ox;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        bx[u][e] = __builtin_bit_cast(bf16, (unsigned short)(x0u[base + toff[e]] & keep[e]));
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 d0 = mfma16x16x32(wa[0], bx[u], z);
+      const f32x4 d1 = mfma16x16x32(wa[1], bx[u], z);
+      if (pp[u] < NP1) {
+        bf16x4 o0, o1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          o0[r] = f2bf(fmaxf(d0[r] * 1.f + bias[0][r], 0.f));
+          o1[r] = f2bf(fmaxf(d1[r] * 1.f + bias[1][r], 0.f));
+        }
+        *reinterpret_cast<bf16x4*>(x1 + xsr(pp[u], py[u], 4 * G)) = o0;
+        *reinterpret_cast<bf16x4*>(x1 + xsr(pp[u], py[u], 16 + 4 * G)) = o1;
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(KT, 3) kcnn_fwd_kernel(KcnnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 x0[NP0];
   __shared__ __attribute__((aligned(16))) bf16 x1[NP1 * C];
@@ -178,7 +244,7 @@ __global__ void __launch_bounds__(KT, 3) kcnn_fwd_kernel(KcnnArgs a) {
     store_x0(a, xr, x0);
     xr = load_x0(a, b + gridDim.x);  // next image: in flight during this one
     __syncthreads();
-    conv1_to_lds<4>(a, x0, x1);
+    conv1_mfma_to_lds(a, x0, x1);
     __syncthreads();
     for (int t = wid; t < NPP / 4; t += 4) {
       const int q0 = 4 * t, ph = q0 / PW, pw0 = q0 - ph * PW;
@@ -292,7 +358,7 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc2[t][r] = s2[(16 * hn + 4 * G + r) * S2 + t * C + 16 * hc + i];
     }
-    conv1_to_lds(a, x0, x1);
+    conv1_mfma_to_lds(a, x0, x1);
     KC_STAMP(3);
     __syncthreads();
     KC_STAMP(4);
@@ -352,42 +418,54 @@ __global__ void __launch_bounds__(KT, 2) kcnn_bwd_kernel(KcnnArgs a) {
         // afterwards: with the reads under their validity conditions (a short-circuit &&) the compiler built one
         // exec-mask branch per read, each waiting for its read -- 24 serialised LDS round trips per pair, half
         // of the kernel's time (scripts/kcnnstamps.py)
-        int py[2], px0[2];
+        // both tiles of the pair unconditionally (the second clamped to tile 48 and dropped when past the
+        // last): their four MFMA accumulation chains interleave (a per-tile branch kept them apart)
+        int py[2], px0[2], Tt[2], iy[2], ix[2];
+        bool tl[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const int T = T0 + 4 * u;
-          const int ty = T / 7, tx = T - 7 * (T / 7);
-          const int iy = 4 * ty + (i >> 2), ix = 4 * tx + (i & 3);
-          f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-          if (T < 49) {
-            // the tile's nine dY2 reads first, then the MFMAs (read, wait, MFMA per tap serialised the reads)
-            bf16x8 af[9];
+          tl[u] = T0 + 4 * u < 49;
+          Tt[u] = min(T0 + 4 * u, 48);
+          const int ty = Tt[u] / 7, tx = Tt[u] - 7 * (Tt[u] / 7);
+          iy[u] = 4 * ty + (i >> 2);
+          ix[u] = 4 * tx + (i & 3);
+        }
+        f32x4 acc[2][2];
+        bf16x8 af[2][9];
 #pragma unroll
-            for (int ky = 0; ky < 3; ++ky)
+        for (int u = 0; u < 2; ++u) {
+          acc[u][0] = acc[u][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-              for (int kx = 0; kx < 3; ++kx) {
-                const int sy = iy - ky, sx = ix - kx;
-                const bool ok = iy < H1 && ix < H1 && (unsigned)sy < (unsigned)H2 && (unsigned)sx < (unsigned)H2;
-                af[3 * ky + kx] = ld8(ok ? dy2 + xsr(sy * H2 + sx, sy, 8 * G) : zc);
-              }
+          for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-            for (int t = 0; t < 9; ++t) {
-              acc[0] = mfma16x16x32(af[t], bt[t][0], acc[0]);
-              acc[1] = mfma16x16x32(af[t], bt[t][1], acc[1]);
+            for (int kx = 0; kx < 3; ++kx) {
+              const int sy = iy[u] - ky, sx = ix[u] - kx;
+              const bool ok = iy[u] < H1 && ix[u] < H1 && (unsigned)sy < (unsigned)H2 && (unsigned)sx < (unsigned)H2;
+              af[u][3 * ky + kx] = ld8(ok ? dy2 + xsr(sy * H2 + sx, sy, 8 * G) : zc);
             }
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            acc[u][0] = mfma16x16x32(af[u][t], bt[t][0], acc[u][0]);
+            acc[u][1] = mfma16x16x32(af[u][t], bt[t][1], acc[u][1]);
           }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int ty = Tt[u] / 7, tx = Tt[u] - 7 * (Tt[u] / 7);
           const int ry = 4 * ty + G, cy = min(ry, H1 - 1);
           py[u] = cy;
           px0[u] = 4 * tx;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int rx = 4 * tx + r, cx = min(rx, H1 - 1);
-            const bool valid = T < 49 && ry < H1 && rx < H1;
+            const bool valid = tl[u] && ry < H1 && rx < H1;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               const float mv = (float)x1[xsr(cy * H1 + cx, cy, 16 * h + i)];
               const bool live = valid & (mv > 0.f);
-              ag[h][4 * u + r] = live ? f2bf(acc[h][r]) : (bf16)0.f;
+              ag[h][4 * u + r] = live ? f2bf(acc[u][h][r]) : (bf16)0.f;
             }
           }
         }

@@ -1,7 +1,9 @@
 """The reference CNN's fused conv block (csrc/kcnn_fused.hip) against the per-layer kernels it replaces
 (conv1 image-resident kernel, conv2 igemm64 with the pooled epilogue, unpool + conv2 weight / data
-gradient + conv1 weight gradient): the forward (pooled map, codes, hence the loss and every dense-layer
-gradient) is equal bit for bit, the two conv layers' weight gradients agree to fp32 summation order."""
+gradient + conv1 weight gradient).  The fused block computes conv1 on MFMA (the per-layer kernel: VALU FMA
+chains), so the 9-tap fp32 sums differ in order: the pooled maps agree to bf16 rounding (a handful of
+elements one bf16 step apart, an argmax code flipped where two window values tie within it), the loss and
+every gradient to fp32 / bf16 summation order."""
 import pytest
 import torch
 
@@ -45,15 +47,14 @@ def test_kcnn_block_matches_per_layer_path(monkeypatch, B):
     sp = p.compute_gradients(x, y).clone()
     torch.cuda.synchronize()
     assert int(f.step_dev.item()) == 6 and int(p.step_dev.item()) == 6
-    assert torch.equal(f.exec_layers[0].out, p.exec_layers[1].out)  # pooled (+ dropout) map
-    assert torch.equal(f.exec_layers[0].code, p.exec_layers[1].code)
-    assert torch.equal(sf, sp)
+    of, op = f.exec_layers[0].out, p.exec_layers[1].out  # pooled (+ dropout) map
+    assert _rel(of, op) < 2e-3, _rel(of, op)
+    assert (of != op).float().mean().item() < 2e-3
+    assert (f.exec_layers[0].code != p.exec_layers[1].code).float().mean().item() < 1e-3
+    assert abs(float(sf[0]) - float(sp[0])) <= 1e-3 * abs(float(sp[0])) and abs(float(sf[1]) - float(sp[1])) <= 1
     for s in f.store.specs:
         gf, gp = f.store.gradient(s.name), p.store.gradient(s.name)
-        if s.name.startswith("conv2d"):
-            assert _rel(gf, gp) < 2e-3, (s.name, _rel(gf, gp))
-        else:
-            assert torch.equal(gf, gp), s.name
+        assert _rel(gf, gp) < 5e-3, (s.name, _rel(gf, gp))
 
 
 def test_kcnn_block_bf16_batch_input_and_training(monkeypatch):
@@ -70,7 +71,7 @@ def test_kcnn_block_bf16_batch_input_and_training(monkeypatch):
     sf = f.compute_gradients(xb, yb).clone()
     sp = p.compute_gradients(xb, yb).clone()
     torch.cuda.synchronize()
-    assert torch.equal(sf, sp)
+    assert abs(float(sf[0]) - float(sp[0])) <= 1e-3 * abs(float(sp[0]))
     tr = DataParallelTrainer(f, lr=0.05, graph="full")
     tr.bind_dataset(data, labels, 256, scale=1.0 / 255.0)
     tr.bind_index_stream(epoch_permutations(2048, 256, 30, dev, seed=0))
