@@ -6,9 +6,9 @@
 // run conv2 as short implicit GEMMs (K = 288) whose per-workgroup prologue/epilogue dominate.  Here a
 // workgroup keeps one image at a time entirely in LDS:
 //
-//   kcnn_fwd  (persistent, 768 workgroups: 3 per CU at 163 VGPRs, conv1 in two 4-channel passes)
+//   kcnn_fwd  (persistent, 768 workgroups: 3 per CU)
 //     x0 (uint8 dataset row through the batch index, or bf16)  -> LDS
-//     conv1 + bias + ReLU on the VALU (72 weights per thread)  -> X1 [676][32] bf16 in LDS (never in HBM)
+//     conv1 + bias + ReLU on MFMA (9 taps zero-padded to k = 32)  -> X1 [676][32] bf16 in LDS (never in HBM)
 //     conv2 on MFMA 16x16x32: one k-step per tap (32 channels), the 18 B fragments (9 taps x 2 channel
 //     halves) stay in registers, A fragments are 16-byte LDS reads of X1.  Output pixels are taken
 //     pool-window-major, so the four pixels of a 2x2 window are the four accumulator rows of one lane:
@@ -29,10 +29,10 @@
 //   kcnn_reduce  sums the slabs in a fixed order (deterministic), writes the four gradients and
 //     advances the dropout step counter (the last reader of the step's masks has run).
 //
-// Forward results equal the per-layer path bit for bit (same conv1 FMA order, same conv2 k order, the
-// conv output rounded to bf16 before the max exactly as it was stored); the weight gradients are the
-// same sums in a different fp32 order.  LDS in kcnn_bwd: 1.5 + 42.3 + 36 KB = 80 KB, two workgroups
-// per CU.
+// The forward matches the per-layer path to bf16 rounding: conv1's 9-tap fp32 sums run in the MFMA's order
+// (the per-layer kernel: a VALU FMA chain), conv2 has the same k order and the conv output is rounded to
+// bf16 before the max exactly as it was stored; the weight gradients are the same sums in a different fp32
+// order.  LDS in kcnn_bwd: 1.5 + 42.3 + 36 KB = 80 KB, two workgroups per CU.
 #include "common.h"
 #include "diag.h"
 #include "kernels.h"
@@ -119,43 +119,6 @@ __device__ __forceinline__ void store_x0(const KcnnArgs& a, const X0Regs& r, bf1
       if (a.idx) f *= a.scale;
     }
     if (e < NP0) x0[e] = f2bf(f);
-  }
-}
-
-// conv1 + bias + ReLU -> X1 (LDS).  Thread (ps = tid >> 2, g = tid & 3): channels 8g..8g+7 of pixels
-// ps, ps + 64, ...; the FMA chain is the per-layer kernel's (smallc.hip c1_fwd_kernel), so X1 is equal
-// bit for bit.  CPP: channels per pass (8, or 4 in two passes: half the weight registers -- 36 instead of
-// 72 -- for one more read of the 9 input pixels; the chains are the same)
-template <int CPP = 8>
-__device__ __forceinline__ void conv1_to_lds(const KcnnArgs& a, const bf16* x0, bf16* x1) {
-  const int g = threadIdx.x & 3, ps = threadIdx.x >> 2;
-#pragma unroll 1
-  for (int c0 = 8 * g; c0 < 8 * g + 8; c0 += CPP) {
-    float w[CPP][9], bias[CPP];
-#pragma unroll
-    for (int j = 0; j < CPP; ++j) {
-#pragma unroll
-      for (int k = 0; k < 9; ++k) w[j][k] = (float)a.w1[(c0 + j) * a.kpad1 + k];
-      bias[j] = a.b1[c0 + j];
-    }
-    for (int p = ps; p < NP1; p += 64) {
-      const int oy = p / H1, ox = p - oy * H1;
-      float xv[9];
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) xv[3 * ky + kx] = (float)x0[(oy + ky) * H0 + ox + kx];
-      typedef bf16 bfv __attribute__((ext_vector_type(CPP)));
-      bfv o;
-#pragma unroll
-      for (int j = 0; j < CPP; ++j) {
-        float acc = 0.f;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) acc = fmaf(xv[k], w[j][k], acc);
-        o[j] = f2bf(fmaxf(acc * 1.f + bias[j], 0.f));
-      }
-      *reinterpret_cast<bfv*>(x1 + xsr(p, oy, c0)) = o;
-    }
   }
 }
 
