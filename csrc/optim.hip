@@ -110,8 +110,16 @@ __device__ __forceinline__ void index_stream_body(const IndexStream& is) {
     return;
   }
   __shared__ long long next;
+  // thread 0 loads the cursor and, with it, the running / step statistics it updates at the end: one round
+  // trip for all of them (the statistics used to be read after the index copy, a third round trip on the
+  // launch's critical path)
+  float rs[3] = {0.f, 0.f, 0.f}, ss[2] = {0.f, 0.f};
   if (threadIdx.x == 0) {
     const long long c = *is.cursor;
+    if (is.run_stats != nullptr) {
+      rs[0] = is.run_stats[0], rs[1] = is.run_stats[1], rs[2] = is.run_stats[2];
+      ss[0] = is.step_stats[0], ss[1] = is.step_stats[1];
+    }
     next = (c + 1) % is.nsteps;
   }
   __syncthreads();
@@ -133,9 +141,9 @@ __device__ __forceinline__ void index_stream_body(const IndexStream& is) {
   if (threadIdx.x == 0) {
     *is.cursor = next;
     if (is.run_stats != nullptr) {  // this step's stats are final: every step kernel precedes this launch
-      is.run_stats[0] += is.step_stats[0];
-      is.run_stats[1] += is.step_stats[1];
-      is.run_stats[2] += 1.f;
+      is.run_stats[0] = rs[0] + ss[0];
+      is.run_stats[1] = rs[1] + ss[1];
+      is.run_stats[2] = rs[2] + 1.f;
     }
   }
 }
