@@ -446,11 +446,11 @@ __global__ void __launch_bounds__(KT) khead_train_kernel(KHeadArgs a) {
         // bounded: the owner runs concurrently by construction (persistent grid <= resident capacity), but a
         // wait that never ends -- e.g. ranks time-sharing a GPU whose other kernels hold the CUs -- must not
         // hang the device: past 2 s the tile is left (its results invalid) and the sticky error word, the
-        // workspace's word after the tag, is set (ops.khead_error reads it)
+        // workspace's word after the tag and the done counter, is set (ops.khead_error reads it)
         const unsigned long long t0 = wall_clock64();
         while (__hip_atomic_load(flags + rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag) {
           if (wall_clock64() - t0 > kKHeadWaitTicks) {
-            atomicOr(tagp + 1, 1u);
+            atomicOr(tagp + 2, 1u);  // (tagp + 1 is the done counter of the launch-tag hand-off)
             break;
           }
           __builtin_amdgcn_s_sleep(2);
@@ -697,7 +697,7 @@ hipError_t khead_wgrad(KHeadWgradArgs a, hipStream_t st) {
 size_t khead_ws_floats(int B, int K) {
   (void)K;
   const size_t nt = (size_t)cdiv(B, KR);
-  return nt * KCH * SLAB + nt * KR * N1 / 2 + 2 * nt + 2;
+  return nt * KCH * SLAB + nt * KR * N1 / 2 + 2 * nt + 3;  // ... tickets, flags, tag, done counter, error word
 }
 
 size_t khead_lds(int K) {

@@ -813,7 +813,7 @@ def khead_error(ws: torch.Tensor, B: int) -> int:
     """The dense-head launch's sticky error word (csrc/khead.hip): non-zero after a row tile's flag wait timed
     out (its results invalid).  ``ws``: the launch's workspace (ops.khead_ws_floats floats)."""
     nt = -(-int(B) // 32)
-    off = nt * 8 * 32 * 128 + nt * 32 * 128 // 2 + 2 * nt + 1
+    off = nt * 8 * 32 * 128 + nt * 32 * 128 // 2 + 2 * nt + 2  # (after the tag and the done counter)
     return int(ws[off:off + 1].view(torch.int32).item())
 
 
